@@ -1,0 +1,209 @@
+/*
+ * alvrl.h -- C ABI of the MI355X-native ALVRL hot path (libalvrl.so).
+ *
+ * This is the drop-in boundary: everything a Mitsuba 0.x 'vrl' integrator
+ * plugin (src/integrators/vrl/vrlIntegrator.cpp, exported through
+ * MTS_EXPORT_PLUGIN at :1127 and driven through the ProgressiveMonteCarlo-
+ * Integrator vtable, include/mitsuba/render/integrator.h:482-511) needs from
+ * the device.  Plain C types only: no torch, no HIP types in signatures
+ * (streams are passed as void* = hipStream_t, NULL = the context's stream).
+ * Errors are int status codes (ALVRL_OK = 0) plus alvrl_last_error(); no C++
+ * exception crosses this boundary (the reference throws from Log(EError),
+ * src/libcore/logger.cpp:147; the shim in INTEGRATION.md maps a non-zero
+ * status back to Log(EError)).
+ *
+ * Each entry point names the reference interface it replaces.
+ */
+#ifndef ALVRL_H
+#define ALVRL_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#if defined(__GNUC__)
+#define ALVRL_API __attribute__((visibility("default")))
+#else
+#define ALVRL_API
+#endif
+
+#define ALVRL_ABI_VERSION 1
+
+enum {
+    ALVRL_OK = 0,
+    ALVRL_ERR_INVALID = 1,   /* bad argument (reference: Log(EError, ...) on bad parameters) */
+    ALVRL_ERR_STATE = 2,     /* call order violated (e.g. gather before upload_vrls) */
+    ALVRL_ERR_HIP = 3,       /* HIP runtime failure */
+    ALVRL_ERR_NOMEM = 4,
+    ALVRL_ERR_NUMERIC = 5    /* an invariant of the clustering maths failed (reference: SLog(EError)) */
+};
+
+/* Record-flag bits of alvrl_gather_rec.flags */
+#define ALVRL_REC_HIT     1u   /* rRec.its.isValid()                          (vrlIntegrator.cpp:712) */
+#define ALVRL_REC_SMOOTH  2u   /* bsdf->getType() & BSDF::ESmooth             (vrlIntegrator.cpp:726-727) */
+#define ALVRL_REC_MEDIUM  4u   /* rRec.medium && !getSigmaS().isZero()         (vrlIntegrator.cpp:614, 795) */
+
+/* Integrator properties that shape the device maths.
+ * Replaces the Properties parsing in vrlIntegrator(const Properties&), vrlIntegrator.cpp:128-208. */
+typedef struct {
+    int device;             /* HIP device ordinal */
+    int vol_vol_samples;    /* "volVolSamples"  (default 2; 0 or >= 2), :148-151 */
+    int vol_surf_samples;   /* "volSurfSamples" (default 2; 0 or >= 2), :153-156 */
+    int short_vrls;         /* "shortVrls" (default true), :135 */
+    uint32_t seed;          /* sampler seed: replaces the SFMT /dev/urandom seeding (random.cpp:473-489) */
+} alvrl_config;
+
+/* Homogeneous medium + phase function of the (single) medium the VRLs live in.
+ * Replaces HomogeneousMedium(const Properties&) (src/medium/homogeneous.cpp:156-219),
+ * 'balance' strategy, and IsotropicPhaseFunction / HGPhaseFunction eval. */
+typedef struct {
+    float sigma_s[3];
+    float sigma_a[3];
+    float sampling_weight;  /* "mediumSamplingWeight"; -1 = auto (max albedo, >= 0.5) */
+    int phase_type;         /* 0 = isotropic (isotropic.cpp:76-78), 1 = HG (hg.cpp:107-110) */
+    float phase_g;
+} alvrl_medium_desc;
+
+/* One eye segment ("gather record"), 64 B.  What LiInternal knows at the point
+ * it calls getVRLContributions / getClusteredVrlContributions
+ * (vrlIntegrator.cpp:418-443): ray.o, ray.d, rRec.its.{p, shFrame.n}, the
+ * diffuse reflectance of its BSDF and the medium/hit flags. */
+typedef struct {
+    float o[3];        /* E  = ray.o */
+    float d[3];        /* ray.d */
+    float p[3];        /* Usurf = rRec.its.p */
+    float n[3];        /* rRec.its.shFrame.n */
+    float albedo[3];   /* SmoothDiffuse reflectance (diffuse.cpp:110-118) */
+    uint32_t flags;    /* ALVRL_REC_* */
+} alvrl_gather_rec;
+
+/* A wave-sized run of slice-bucketed records for the clustered gather:
+ * records [begin, begin+count) all use the representative list of 'slice'
+ * (UINT32_MAX = the fall-back list, vrlIntegrator.cpp:564-571). count <= 64. */
+typedef struct {
+    uint32_t slice;
+    uint32_t begin;
+    uint32_t count;
+    uint32_t pad;
+} alvrl_work_item;
+
+typedef struct alvrl_ctx alvrl_ctx;
+
+/* ---- lifecycle ------------------------------------------------------ */
+/* Replaces vrlIntegrator::vrlIntegrator(const Properties&) (:128-208) for the
+ * device state; returns ALVRL_OK and *out, or an error (see alvrl_last_error(NULL)). */
+ALVRL_API int alvrl_ctx_create(const alvrl_config *cfg, alvrl_ctx **out);
+/* Replaces the implicit destruction of m_vrls / m_ci (ref<> members, :1089-1090). */
+ALVRL_API void alvrl_ctx_destroy(alvrl_ctx *ctx);
+/* Last error of this context on the calling thread (ctx == NULL: global). */
+ALVRL_API const char *alvrl_last_error(const alvrl_ctx *ctx);
+ALVRL_API int alvrl_abi_version(void);
+
+/* ---- per-scene / per-pass state (set in preprocess/prepass; immutable
+ *      while gathers run, vrlIntegrator.cpp:237-356) -------------------- */
+/* Replaces scene->getMedia()[0] / vrl.m_medium lookups (:244-249, 607). */
+ALVRL_API int alvrl_set_medium(alvrl_ctx *ctx, const alvrl_medium_desc *m);
+/* Progressive pass index (integrator.cpp:396-433): keys the counter RNG. */
+ALVRL_API int alvrl_set_pass(alvrl_ctx *ctx, uint32_t pass);
+/* Replaces m_vrls = tracer->randomWalk(...) / new vrlVector(fs, medium) and
+ * registerResource(m_vrls) (:276-287, 353).  soa = 9 arrays of n floats:
+ * start xyz, end xyz, power rgb (VRL.h:89-96).  particle_count = vrlVector::
+ * getParticleCount() (VRL.h:164-166), the 1/particleCount normalisation.
+ * soa_on_device != 0: soa is a device pointer. */
+ALVRL_API int alvrl_upload_vrls(alvrl_ctx *ctx, const float *soa, uint32_t n,
+                                uint64_t particle_count, int soa_on_device);
+ALVRL_API uint32_t alvrl_num_vrls(const alvrl_ctx *ctx);
+
+/* Replaces m_ci->m_selectedVrls / m_clusterWeight / m_fallBackVrls /
+ * m_fallBackWeight (vrlClusterInfo, :17-115; written by buildClusters at :341-346).
+ * CSR on the host: slice s uses reps[slice_off[s] .. slice_off[s+1]). */
+ALVRL_API int alvrl_set_clusters(alvrl_ctx *ctx, uint32_t nslices, const uint32_t *slice_off,
+                                 const uint32_t *reps, const float *weights,
+                                 const uint32_t *fb_reps, const float *fb_weights, uint32_t n_fb);
+
+/* ---- hot path (a): per-record VRL gather ------------------------------ */
+/* Replaces getVRLContributions (:792-825) -> integrateVRL (:603-785) for every
+ * VRL.  d_recs / d_rec_ids / d_out_rgb are device pointers; d_rec_ids may be
+ * NULL (record id = index).  The record id keys the sampling uniforms.
+ * d_out_rgb[3*r..] = Li of record r (already * 1/particleCount). */
+ALVRL_API int alvrl_gather_brute(alvrl_ctx *ctx, const alvrl_gather_rec *d_recs,
+                                 const uint32_t *d_rec_ids, uint32_t nrec, float *d_out_rgb,
+                                 void *stream);
+/* Replaces getClusteredVrlContributions (:542-599): sum_k w_k * integrateVRL(rep_k)
+ * / particleCount over the record's slice list.  Records must be bucketed by
+ * slice and described by wave work items (alvrl_make_work_items). */
+ALVRL_API int alvrl_gather_clustered(alvrl_ctx *ctx, const alvrl_gather_rec *d_recs,
+                                     const uint32_t *d_rec_ids, const alvrl_work_item *d_items,
+                                     uint32_t nitems, float *d_out_rgb, void *stream);
+/* Host helper: build work items from a slice-sorted slice-of-record array
+ * (host memory).  Returns the number of items written (<= cap). */
+ALVRL_API uint32_t alvrl_make_work_items(const uint32_t *slice_of_rec_sorted, uint32_t nrec,
+                                         alvrl_work_item *items, uint32_t cap);
+
+/* ---- hot path (b) part 1: reduced transport matrix R ------------------ */
+/* Replaces Rbuilder::run (:1053-1067) -> getLiLuminanceVrlContributions
+ * (:527-539) with Rsamples = 1.  Writes (mean, var) float pairs to
+ * d_Rt[2*(v*ld + row0 + r) + {0,1}] for record r of d_recs and VRL v, i.e. R
+ * stored VRL-major with the representative rows contiguous. */
+ALVRL_API int alvrl_build_R(alvrl_ctx *ctx, const alvrl_gather_rec *d_recs,
+                            const uint32_t *d_rec_ids, uint32_t nrows, float *d_Rt, uint64_t ld,
+                            uint64_t row0, void *stream);
+
+/* ---- hot path (b) part 2: cluster refinement ------------------------- */
+/* One Clustering (Preprocessor.cpp:287-720): ctor (column weights, initial
+ * clusters, unclustered variances, :301-341), optional refine() (:380-489),
+ * sampleRepresentatives() (:354-378).  Host pointers. */
+typedef struct {
+    const uint32_t *rows;     /* local matrix rows = row ids into R (getLocalMatrix, :779-827) */
+    const double *locw;       /* locality weights, one per row (sum 1) */
+    uint32_t nrows;
+    float pixel_undersampling;/* m_sliceUndersampling[i] or m_globalPixelUndersampling */
+    float undersampling;      /* refine(): <= 0 adaptive (:402-489), > 0 fixed depth (:387-399) */
+    float depth_correction;   /* "depthCorrection" */
+    int do_refine;            /* 0: only sampleRepresentatives (localRefinement=false, :270-274) */
+    uint32_t stage_refine;    /* counter-RNG stream ids of the split / sampling draws */
+    uint32_t stage_sample;
+} alvrl_cluster_job;
+
+/* Replaces refinePerSlice -> refineSlice (Preprocessor.cpp:199-283) and the
+ * fall-back refinement in buildClusters (:175-186): runs every job on the
+ * device, one persistent workgroup per job, all jobs concurrently.
+ *   d_Rt, ld      : R as written by alvrl_build_R
+ *   init_vrls/off : the global clusters (Preprocessor::cluster, :838-898), host
+ * Outputs (host): per job the representatives and weights in CSR
+ * (out_off[njobs+1], capacity njobs * nvrl entries) and out_refined[j]
+ * (0 = refine() returned false, the caller substitutes the fall-back list). */
+ALVRL_API int alvrl_refine(alvrl_ctx *ctx, const float *d_Rt, uint64_t ld, uint32_t njobs,
+                           const alvrl_cluster_job *jobs, const uint32_t *init_vrls,
+                           const uint32_t *init_off, uint32_t ninit, uint32_t *out_off,
+                           uint32_t *out_reps, float *out_weights, int *out_refined,
+                           void *stream);
+/* Milliseconds the device spent in the last alvrl_refine call (HIP events). */
+ALVRL_API int alvrl_last_refine_ms(alvrl_ctx *ctx, float *ms);
+
+/* ---- statistics ------------------------------------------------------- */
+/* statsVrlsPreprocess / statsVrlsRender (:119-122, 593-596, 819-822): number
+ * of integrateVRL evaluations.  Synchronises the context's counters. */
+ALVRL_API int alvrl_get_stats(alvrl_ctx *ctx, uint64_t *preprocess, uint64_t *render);
+ALVRL_API int alvrl_reset_stats(alvrl_ctx *ctx);
+
+/* ---- host-pointer conveniences for the Mitsuba shim's renderBlock ----- */
+/* Same as alvrl_gather_brute / alvrl_gather_clustered with host arrays;
+ * slice_of_rec may be unsorted (UINT32_MAX = fall-back).  Blocking. */
+ALVRL_API int alvrl_gather_brute_host(alvrl_ctx *ctx, const alvrl_gather_rec *recs,
+                                      const uint32_t *rec_ids, uint32_t nrec, float *out_rgb);
+ALVRL_API int alvrl_gather_clustered_host(alvrl_ctx *ctx, const alvrl_gather_rec *recs,
+                                          const uint32_t *rec_ids, const uint32_t *slice_of_rec,
+                                          uint32_t nrec, float *out_rgb);
+
+/* ---- timing of the last kernel launched on the context (HIP events) --- */
+/* Milliseconds between the begin/end events recorded around the most recent
+ * gather / R-build launch, on the stream it ran on.  Synchronises. */
+ALVRL_API int alvrl_last_kernel_ms(alvrl_ctx *ctx, float *ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ALVRL_H */

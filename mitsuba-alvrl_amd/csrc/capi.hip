@@ -1,0 +1,495 @@
+// capi.hip -- implementation of the C ABI declared in include/alvrl.h.
+//
+// Owns the device state a vrlIntegrator instance holds between prepass and
+// render (vrlIntegrator.cpp:1088-1121: m_vrls, m_ci) and launches the kernels
+// of gather.hip / refine.hip.  Device state is immutable while gathers run, so
+// concurrent gathers from several host threads (the reference calls Li from
+// every LocalWorker, renderproc.cpp:52-86) only need their own streams.
+#include "../../include/alvrl.h"
+#include "vrl_device.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+namespace alvrl {
+hipError_t launch_prepare_vrls(const float* soa, uint32_t n, VrlPrep* out, hipStream_t s);
+hipError_t launch_gather_brute(const Rec* recs, const uint32_t* ids, uint32_t nrec,
+                               const VrlPrep* vp, uint32_t nvrl, const DevParams& P,
+                               float normalization, float* out, unsigned long long* counter,
+                               hipStream_t s);
+struct WorkItem { uint32_t slice, begin, count, pad; };
+hipError_t launch_gather_clustered(const Rec* recs, const uint32_t* ids, const WorkItem* items,
+                                   uint32_t nitems, const VrlPrep* vp, const uint32_t* slice_off,
+                                   const uint32_t* reps, const float* weights,
+                                   const uint32_t* fb_reps, const float* fb_w, uint32_t n_fb,
+                                   const DevParams& P, float inv_pc, float* out,
+                                   unsigned long long* counter, hipStream_t s);
+hipError_t launch_build_R(const Rec* recs, const uint32_t* ids, uint32_t nrows, const VrlPrep* vp,
+                          uint32_t nvrl, const DevParams& P, float normalization, float2* Rt,
+                          uint64_t ld, uint64_t row0, unsigned long long* counter, hipStream_t s);
+struct HostJob {
+    const uint32_t* rows;
+    const double* locw;
+    uint32_t nrows;
+    float pixel_under, undersampling, depth_correction;
+    int do_refine;
+    uint32_t stage_refine, stage_sample;
+};
+int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, uint32_t seed,
+                uint32_t pass, uint32_t njobs, const HostJob* jobs, const uint32_t* init_vrls,
+                const uint32_t* init_off, uint32_t ninit, uint32_t* out_off, uint32_t* out_reps,
+                float* out_w, int* out_refined, float* ms, std::string* err);
+}  // namespace alvrl
+
+using namespace alvrl;
+
+static_assert(sizeof(alvrl_gather_rec) == sizeof(Rec), "record layout");
+static_assert(sizeof(alvrl_work_item) == sizeof(WorkItem), "work item layout");
+
+struct alvrl_ctx {
+    alvrl_config cfg;
+    DevParams P;
+    bool medium_set = false;
+    hipStream_t stream = nullptr;
+    float* d_soa = nullptr;
+    VrlPrep* d_vrl = nullptr;
+    uint32_t nvrl = 0, cap_vrl = 0;
+    uint64_t particle_count = 0;
+    unsigned long long* d_counter = nullptr;   // [0] preprocess, [1] render
+    // clusters
+    uint32_t nslices = 0, n_fb = 0;
+    uint32_t* d_slice_off = nullptr;
+    uint32_t* d_reps = nullptr;
+    float* d_weights = nullptr;
+    uint32_t* d_fb_reps = nullptr;
+    float* d_fb_w = nullptr;
+    bool clusters_set = false;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    bool timed = false;
+    float refine_ms = 0.0f;
+    std::mutex mu;
+};
+
+static thread_local std::string g_err = "";
+
+static int fail(int code, const std::string& msg)
+{
+    g_err = msg;
+    return code;
+}
+
+#define HIPCHK(expr)                                                                  \
+    do {                                                                              \
+        hipError_t e_ = (expr);                                                       \
+        if (e_ != hipSuccess)                                                         \
+            return fail(ALVRL_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+static hipStream_t pick(alvrl_ctx* c, void* s) { return s ? (hipStream_t)s : c->stream; }
+
+extern "C" {
+
+ALVRL_API int alvrl_abi_version(void) { return ALVRL_ABI_VERSION; }
+
+ALVRL_API const char* alvrl_last_error(const alvrl_ctx*) { return g_err.c_str(); }
+
+ALVRL_API int alvrl_ctx_create(const alvrl_config* cfg, alvrl_ctx** out)
+{
+    if (!cfg || !out) return fail(ALVRL_ERR_INVALID, "alvrl_ctx_create: null argument");
+    // vrlIntegrator.cpp:148-156
+    if (cfg->vol_vol_samples != 0 && cfg->vol_vol_samples < 2)
+        return fail(ALVRL_ERR_INVALID, "Need at least 2 volVolSamples for variance estimate, but received: " +
+                                           std::to_string(cfg->vol_vol_samples));
+    if (cfg->vol_surf_samples != 0 && cfg->vol_surf_samples < 2)
+        return fail(ALVRL_ERR_INVALID, "Need at least 2 volSurfSamples for variance estimate, but received: " +
+                                           std::to_string(cfg->vol_surf_samples));
+    if (cfg->vol_vol_samples > 64 || cfg->vol_surf_samples > 64)
+        return fail(ALVRL_ERR_INVALID, "at most 64 volVol/volSurf samples are supported");
+    int ndev = 0;
+    HIPCHK(hipGetDeviceCount(&ndev));
+    if (cfg->device < 0 || cfg->device >= ndev)
+        return fail(ALVRL_ERR_INVALID, "alvrl_ctx_create: no HIP device " + std::to_string(cfg->device));
+    HIPCHK(hipSetDevice(cfg->device));
+    alvrl_ctx* c = new alvrl_ctx();
+    c->cfg = *cfg;
+    std::memset(&c->P, 0, sizeof(c->P));
+    c->P.nvv = cfg->vol_vol_samples;
+    c->P.nvs = cfg->vol_surf_samples;
+    c->P.short_vrls = cfg->short_vrls ? 1 : 0;
+    c->P.seed = cfg->seed;
+    c->P.pass = 0;
+    hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipMalloc(&c->d_counter, 2 * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMemset(c->d_counter, 0, 2 * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipEventCreate(&c->ev0);
+    if (e == hipSuccess) e = hipEventCreate(&c->ev1);
+    if (e != hipSuccess) {
+        alvrl_ctx_destroy(c);
+        return fail(ALVRL_ERR_HIP, std::string("alvrl_ctx_create: ") + hipGetErrorString(e));
+    }
+    *out = c;
+    return ALVRL_OK;
+}
+
+static void free_clusters(alvrl_ctx* c)
+{
+    hipFree(c->d_slice_off); hipFree(c->d_reps); hipFree(c->d_weights);
+    hipFree(c->d_fb_reps); hipFree(c->d_fb_w);
+    c->d_slice_off = nullptr; c->d_reps = nullptr; c->d_weights = nullptr;
+    c->d_fb_reps = nullptr; c->d_fb_w = nullptr;
+    c->clusters_set = false;
+}
+
+ALVRL_API void alvrl_ctx_destroy(alvrl_ctx* c)
+{
+    if (!c) return;
+    hipSetDevice(c->cfg.device);
+    if (c->stream) hipStreamSynchronize(c->stream);
+    hipFree(c->d_soa); hipFree(c->d_vrl); hipFree(c->d_counter);
+    free_clusters(c);
+    if (c->ev0) hipEventDestroy(c->ev0);
+    if (c->ev1) hipEventDestroy(c->ev1);
+    if (c->stream) hipStreamDestroy(c->stream);
+    delete c;
+}
+
+ALVRL_API int alvrl_set_medium(alvrl_ctx* c, const alvrl_medium_desc* m)
+{
+    if (!c || !m) return fail(ALVRL_ERR_INVALID, "alvrl_set_medium: null argument");
+    float w = m->sampling_weight;
+    float st[3];
+    for (int i = 0; i < 3; i++) st[i] = m->sigma_s[i] + m->sigma_a[i];
+    if (w == -1) {   // homogeneous.cpp:168-184
+        for (int i = 0; i < 3; i++) {
+            float albedo = m->sigma_s[i] / st[i];
+            if (albedo > w && st[i] != 0) w = albedo;
+        }
+        if (w > 0) w = std::max(w, 0.5f);
+    }
+    if (m->phase_type != 0 && m->phase_type != 1)
+        return fail(ALVRL_ERR_INVALID, "alvrl_set_medium: phase_type must be 0 (isotropic) or 1 (hg)");
+    for (int i = 0; i < 3; i++) { c->P.sigma_s[i] = m->sigma_s[i]; c->P.sigma_t[i] = st[i]; }
+    c->P.w = w;
+    c->P.phase_type = m->phase_type;
+    c->P.g = m->phase_g;
+    c->medium_set = true;
+    return ALVRL_OK;
+}
+
+ALVRL_API int alvrl_set_pass(alvrl_ctx* c, uint32_t pass)
+{
+    if (!c) return fail(ALVRL_ERR_INVALID, "alvrl_set_pass: null ctx");
+    c->P.pass = pass;
+    return ALVRL_OK;
+}
+
+ALVRL_API uint32_t alvrl_num_vrls(const alvrl_ctx* c) { return c ? c->nvrl : 0; }
+
+ALVRL_API int alvrl_upload_vrls(alvrl_ctx* c, const float* soa, uint32_t n, uint64_t pc, int on_dev)
+{
+    if (!c || (!soa && n)) return fail(ALVRL_ERR_INVALID, "alvrl_upload_vrls: null argument");
+    if (n > 0 && pc == 0) return fail(ALVRL_ERR_INVALID, "alvrl_upload_vrls: particle_count must be > 0");
+    HIPCHK(hipSetDevice(c->cfg.device));
+    if (n > c->cap_vrl) {
+        HIPCHK(hipStreamSynchronize(c->stream));
+        hipFree(c->d_soa); hipFree(c->d_vrl);
+        c->d_soa = nullptr; c->d_vrl = nullptr; c->cap_vrl = 0;
+        HIPCHK(hipMalloc(&c->d_soa, sizeof(float) * 9 * (size_t)n));
+        HIPCHK(hipMalloc(&c->d_vrl, sizeof(VrlPrep) * (size_t)n));
+        c->cap_vrl = n;
+    }
+    if (n) {
+        // SoA planes are compacted to stride n on the device.
+        HIPCHK(hipMemcpyAsync(c->d_soa, soa, sizeof(float) * 9 * (size_t)n,
+                              on_dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, c->stream));
+        HIPCHK(launch_prepare_vrls(c->d_soa, n, c->d_vrl, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+    }
+    c->nvrl = n;
+    c->particle_count = pc;
+    return ALVRL_OK;
+}
+
+ALVRL_API int alvrl_set_clusters(alvrl_ctx* c, uint32_t nslices, const uint32_t* slice_off,
+                                 const uint32_t* reps, const float* weights,
+                                 const uint32_t* fb_reps, const float* fb_w, uint32_t n_fb)
+{
+    if (!c || (!slice_off && nslices)) return fail(ALVRL_ERR_INVALID, "alvrl_set_clusters: null argument");
+    HIPCHK(hipSetDevice(c->cfg.device));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    const uint32_t nrep = nslices ? slice_off[nslices] : 0;
+    for (uint32_t i = 0; i < nrep; i++)
+        if (reps[i] >= c->nvrl) return fail(ALVRL_ERR_INVALID, "alvrl_set_clusters: representative out of range");
+    for (uint32_t i = 0; i < n_fb; i++)
+        if (fb_reps[i] >= c->nvrl) return fail(ALVRL_ERR_INVALID, "alvrl_set_clusters: fall-back representative out of range");
+    free_clusters(c);
+    HIPCHK(hipMalloc(&c->d_slice_off, sizeof(uint32_t) * (nslices + 1)));
+    HIPCHK(hipMalloc(&c->d_reps, sizeof(uint32_t) * std::max(nrep, 1u)));
+    HIPCHK(hipMalloc(&c->d_weights, sizeof(float) * std::max(nrep, 1u)));
+    HIPCHK(hipMalloc(&c->d_fb_reps, sizeof(uint32_t) * std::max(n_fb, 1u)));
+    HIPCHK(hipMalloc(&c->d_fb_w, sizeof(float) * std::max(n_fb, 1u)));
+    if (nslices) HIPCHK(hipMemcpy(c->d_slice_off, slice_off, sizeof(uint32_t) * (nslices + 1), hipMemcpyHostToDevice));
+    if (nrep) {
+        HIPCHK(hipMemcpy(c->d_reps, reps, sizeof(uint32_t) * nrep, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(c->d_weights, weights, sizeof(float) * nrep, hipMemcpyHostToDevice));
+    }
+    if (n_fb) {
+        HIPCHK(hipMemcpy(c->d_fb_reps, fb_reps, sizeof(uint32_t) * n_fb, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(c->d_fb_w, fb_w, sizeof(float) * n_fb, hipMemcpyHostToDevice));
+    }
+    c->nslices = nslices;
+    c->n_fb = n_fb;
+    c->clusters_set = true;
+    return ALVRL_OK;
+}
+
+static int check_ready(alvrl_ctx* c, const char* fn)
+{
+    if (!c) return fail(ALVRL_ERR_INVALID, std::string(fn) + ": null ctx");
+    if (!c->medium_set) return fail(ALVRL_ERR_STATE, std::string(fn) + ": alvrl_set_medium not called");
+    if (!c->d_vrl && c->nvrl) return fail(ALVRL_ERR_STATE, std::string(fn) + ": no VRLs uploaded");
+    if (c->particle_count == 0) return fail(ALVRL_ERR_STATE, std::string(fn) + ": alvrl_upload_vrls not called");
+    return ALVRL_OK;
+}
+
+ALVRL_API int alvrl_gather_brute(alvrl_ctx* c, const alvrl_gather_rec* d_recs, const uint32_t* d_ids,
+                                 uint32_t nrec, float* d_out, void* stream)
+{
+    int rc = check_ready(c, "alvrl_gather_brute");
+    if (rc) return rc;
+    if (nrec && (!d_recs || !d_out)) return fail(ALVRL_ERR_INVALID, "alvrl_gather_brute: null buffer");
+    HIPCHK(hipSetDevice(c->cfg.device));
+    hipStream_t s = pick(c, stream);
+    // Float normalization = 1.0 / m_vrls->getParticleCount()  (:805)
+    const float norm = (float)(1.0 / (double)c->particle_count);
+    HIPCHK(hipEventRecord(c->ev0, s));
+    HIPCHK(launch_gather_brute(reinterpret_cast<const Rec*>(d_recs), d_ids, nrec, c->d_vrl, c->nvrl,
+                               c->P, norm, d_out, c->d_counter + 1, s));
+    HIPCHK(hipEventRecord(c->ev1, s));
+    c->timed = true;
+    return ALVRL_OK;
+}
+
+ALVRL_API int alvrl_gather_clustered(alvrl_ctx* c, const alvrl_gather_rec* d_recs, const uint32_t* d_ids,
+                                     const alvrl_work_item* d_items, uint32_t nitems, float* d_out,
+                                     void* stream)
+{
+    int rc = check_ready(c, "alvrl_gather_clustered");
+    if (rc) return rc;
+    if (!c->clusters_set) return fail(ALVRL_ERR_STATE, "alvrl_gather_clustered: alvrl_set_clusters not called");
+    if (nitems && (!d_recs || !d_out || !d_items)) return fail(ALVRL_ERR_INVALID, "alvrl_gather_clustered: null buffer");
+    HIPCHK(hipSetDevice(c->cfg.device));
+    hipStream_t s = pick(c, stream);
+    const float inv_pc = 1.0f / (float)c->particle_count;   // Li /= getParticleCount() (:590)
+    HIPCHK(hipEventRecord(c->ev0, s));
+    HIPCHK(launch_gather_clustered(reinterpret_cast<const Rec*>(d_recs), d_ids,
+                                   reinterpret_cast<const WorkItem*>(d_items), nitems, c->d_vrl,
+                                   c->d_slice_off, c->d_reps, c->d_weights, c->d_fb_reps, c->d_fb_w,
+                                   c->n_fb, c->P, inv_pc, d_out, c->d_counter + 1, s));
+    HIPCHK(hipEventRecord(c->ev1, s));
+    c->timed = true;
+    return ALVRL_OK;
+}
+
+ALVRL_API uint32_t alvrl_make_work_items(const uint32_t* sl, uint32_t nrec, alvrl_work_item* items,
+                                         uint32_t cap)
+{
+    uint32_t n = 0, i = 0;
+    while (i < nrec) {
+        uint32_t j = i + 1;
+        while (j < nrec && j - i < 64 && sl[j] == sl[i]) j++;
+        if (n < cap) items[n] = alvrl_work_item{sl[i], i, j - i, 0u};
+        n++;
+        i = j;
+    }
+    return std::min(n, cap);
+}
+
+ALVRL_API int alvrl_build_R(alvrl_ctx* c, const alvrl_gather_rec* d_recs, const uint32_t* d_ids,
+                            uint32_t nrows, float* d_Rt, uint64_t ld, uint64_t row0, void* stream)
+{
+    int rc = check_ready(c, "alvrl_build_R");
+    if (rc) return rc;
+    if (nrows && (!d_recs || !d_Rt)) return fail(ALVRL_ERR_INVALID, "alvrl_build_R: null buffer");
+    if (row0 + nrows > ld) return fail(ALVRL_ERR_INVALID, "alvrl_build_R: rows exceed ld");
+    HIPCHK(hipSetDevice(c->cfg.device));
+    hipStream_t s = pick(c, stream);
+    const float norm = (float)(1.0 / (double)c->particle_count);
+    HIPCHK(hipEventRecord(c->ev0, s));
+    HIPCHK(launch_build_R(reinterpret_cast<const Rec*>(d_recs), d_ids, nrows, c->d_vrl, c->nvrl, c->P,
+                          norm, reinterpret_cast<float2*>(d_Rt), ld, row0, c->d_counter + 0, s));
+    HIPCHK(hipEventRecord(c->ev1, s));
+    c->timed = true;
+    return ALVRL_OK;
+}
+
+ALVRL_API int alvrl_refine(alvrl_ctx* c, const float* d_Rt, uint64_t ld, uint32_t njobs,
+                           const alvrl_cluster_job* jobs, const uint32_t* init_vrls,
+                           const uint32_t* init_off, uint32_t ninit, uint32_t* out_off,
+                           uint32_t* out_reps, float* out_weights, int* out_refined, void* stream)
+{
+    if (!c) return fail(ALVRL_ERR_INVALID, "alvrl_refine: null ctx");
+    if (njobs && (!d_Rt || !jobs || !init_off || !out_off || !out_reps || !out_weights || !out_refined))
+        return fail(ALVRL_ERR_INVALID, "alvrl_refine: null argument");
+    if (c->nvrl == 0) return fail(ALVRL_ERR_STATE, "alvrl_refine: no VRLs uploaded");
+    if (c->nvrl < 2) return fail(ALVRL_ERR_NUMERIC, "Need at least 2 VRLs to estimate variance");
+    std::vector<HostJob> hj(njobs);
+    for (uint32_t j = 0; j < njobs; j++) {
+        const alvrl_cluster_job& J = jobs[j];
+        if (!J.rows || !J.locw) return fail(ALVRL_ERR_INVALID, "alvrl_refine: job without rows");
+        // Clustering ctor checks (Preprocessor.cpp:307-313)
+        double n1 = 0.0;
+        for (uint32_t r = 0; r < J.nrows; r++) n1 += std::fabs(J.locw[r]);
+        if (std::fabs((float)n1 - 1) > 1e-3)
+            return fail(ALVRL_ERR_NUMERIC, "Incorrect normalization in localityWeights: " + std::to_string(n1));
+        if (J.pixel_undersampling <= 0 || J.pixel_undersampling > 1)
+            return fail(ALVRL_ERR_NUMERIC, "Invalid pixel undersampling: " + std::to_string(J.pixel_undersampling));
+        hj[j] = HostJob{J.rows, J.locw, J.nrows, J.pixel_undersampling, J.undersampling,
+                        J.depth_correction, J.do_refine, J.stage_refine, J.stage_sample};
+    }
+    HIPCHK(hipSetDevice(c->cfg.device));
+    std::string err;
+    float ms = 0.0f;
+    int rc = refine_jobs(pick(c, stream), d_Rt, ld, c->nvrl, c->P.seed, c->P.pass, njobs, hj.data(),
+                         init_vrls, init_off, ninit, out_off, out_reps, out_weights, out_refined,
+                         &ms, &err);
+    c->refine_ms = ms;
+    if (rc) return fail(rc, err);
+    return ALVRL_OK;
+}
+
+ALVRL_API int alvrl_last_refine_ms(alvrl_ctx* c, float* ms)
+{
+    if (!c || !ms) return fail(ALVRL_ERR_INVALID, "alvrl_last_refine_ms: null argument");
+    *ms = c->refine_ms;
+    return ALVRL_OK;
+}
+
+ALVRL_API int alvrl_get_stats(alvrl_ctx* c, uint64_t* pre, uint64_t* ren)
+{
+    if (!c) return fail(ALVRL_ERR_INVALID, "alvrl_get_stats: null ctx");
+    HIPCHK(hipSetDevice(c->cfg.device));
+    HIPCHK(hipDeviceSynchronize());
+    unsigned long long h[2];
+    HIPCHK(hipMemcpy(h, c->d_counter, sizeof(h), hipMemcpyDeviceToHost));
+    if (pre) *pre = h[0];
+    if (ren) *ren = h[1];
+    return ALVRL_OK;
+}
+
+ALVRL_API int alvrl_reset_stats(alvrl_ctx* c)
+{
+    if (!c) return fail(ALVRL_ERR_INVALID, "alvrl_reset_stats: null ctx");
+    HIPCHK(hipSetDevice(c->cfg.device));
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemset(c->d_counter, 0, 2 * sizeof(unsigned long long)));
+    return ALVRL_OK;
+}
+
+ALVRL_API int alvrl_last_kernel_ms(alvrl_ctx* c, float* ms)
+{
+    if (!c || !ms) return fail(ALVRL_ERR_INVALID, "alvrl_last_kernel_ms: null argument");
+    if (!c->timed) return fail(ALVRL_ERR_STATE, "alvrl_last_kernel_ms: nothing launched yet");
+    HIPCHK(hipSetDevice(c->cfg.device));
+    HIPCHK(hipEventSynchronize(c->ev1));
+    HIPCHK(hipEventElapsedTime(ms, c->ev0, c->ev1));
+    return ALVRL_OK;
+}
+
+ALVRL_API int alvrl_gather_brute_host(alvrl_ctx* c, const alvrl_gather_rec* recs, const uint32_t* ids,
+                                      uint32_t nrec, float* out)
+{
+    int rc = check_ready(c, "alvrl_gather_brute_host");
+    if (rc) return rc;
+    if (nrec == 0) return ALVRL_OK;
+    HIPCHK(hipSetDevice(c->cfg.device));
+    hipStream_t s;
+    HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    alvrl_gather_rec* dr = nullptr; uint32_t* di = nullptr; float* dout = nullptr;
+    hipError_t e = hipMallocAsync((void**)&dr, sizeof(alvrl_gather_rec) * nrec, s);
+    if (e == hipSuccess && ids) e = hipMallocAsync((void**)&di, sizeof(uint32_t) * nrec, s);
+    if (e == hipSuccess) e = hipMallocAsync((void**)&dout, sizeof(float) * 3 * nrec, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(dr, recs, sizeof(alvrl_gather_rec) * nrec, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess && ids) e = hipMemcpyAsync(di, ids, sizeof(uint32_t) * nrec, hipMemcpyHostToDevice, s);
+    int r2 = ALVRL_OK;
+    if (e == hipSuccess) {
+        const float norm = (float)(1.0 / (double)c->particle_count);
+        e = launch_gather_brute(reinterpret_cast<const Rec*>(dr), di, nrec, c->d_vrl, c->nvrl, c->P,
+                                norm, dout, c->d_counter + 1, s);
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(out, dout, sizeof(float) * 3 * nrec, hipMemcpyDeviceToHost, s);
+    if (dr) hipFreeAsync(dr, s);
+    if (di) hipFreeAsync(di, s);
+    if (dout) hipFreeAsync(dout, s);
+    hipError_t e2 = hipStreamSynchronize(s);
+    hipStreamDestroy(s);
+    if (e == hipSuccess) e = e2;
+    if (e != hipSuccess) r2 = fail(ALVRL_ERR_HIP, std::string("alvrl_gather_brute_host: ") + hipGetErrorString(e));
+    return r2;
+}
+
+ALVRL_API int alvrl_gather_clustered_host(alvrl_ctx* c, const alvrl_gather_rec* recs,
+                                          const uint32_t* ids, const uint32_t* slice_of_rec,
+                                          uint32_t nrec, float* out)
+{
+    int rc = check_ready(c, "alvrl_gather_clustered_host");
+    if (rc) return rc;
+    if (!c->clusters_set) return fail(ALVRL_ERR_STATE, "alvrl_gather_clustered_host: alvrl_set_clusters not called");
+    if (nrec == 0) return ALVRL_OK;
+    for (uint32_t i = 0; i < nrec; i++)
+        if (slice_of_rec[i] != 0xFFFFFFFFu && slice_of_rec[i] >= c->nslices)
+            return fail(ALVRL_ERR_INVALID, "alvrl_gather_clustered_host: slice out of range");
+    // bucket records by slice (stable), build wave work items
+    std::vector<uint32_t> perm(nrec);
+    for (uint32_t i = 0; i < nrec; i++) perm[i] = i;
+    std::stable_sort(perm.begin(), perm.end(), [&](uint32_t a, uint32_t b) {
+        return slice_of_rec[a] < slice_of_rec[b];
+    });
+    std::vector<alvrl_gather_rec> r2(nrec);
+    std::vector<uint32_t> id2(nrec), sl2(nrec);
+    for (uint32_t i = 0; i < nrec; i++) {
+        r2[i] = recs[perm[i]];
+        id2[i] = ids ? ids[perm[i]] : perm[i];
+        sl2[i] = slice_of_rec[perm[i]];
+    }
+    std::vector<alvrl_work_item> items(nrec);
+    uint32_t nit = alvrl_make_work_items(sl2.data(), nrec, items.data(), nrec);
+    HIPCHK(hipSetDevice(c->cfg.device));
+    hipStream_t s;
+    HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    alvrl_gather_rec* dr = nullptr; uint32_t* di = nullptr; float* dout = nullptr;
+    alvrl_work_item* dit = nullptr;
+    hipError_t e = hipMallocAsync((void**)&dr, sizeof(alvrl_gather_rec) * nrec, s);
+    if (e == hipSuccess) e = hipMallocAsync((void**)&di, sizeof(uint32_t) * nrec, s);
+    if (e == hipSuccess) e = hipMallocAsync((void**)&dout, sizeof(float) * 3 * nrec, s);
+    if (e == hipSuccess) e = hipMallocAsync((void**)&dit, sizeof(alvrl_work_item) * nit, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(dr, r2.data(), sizeof(alvrl_gather_rec) * nrec, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(di, id2.data(), sizeof(uint32_t) * nrec, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(dit, items.data(), sizeof(alvrl_work_item) * nit, hipMemcpyHostToDevice, s);
+    std::vector<float> o2(3 * (size_t)nrec);
+    if (e == hipSuccess) {
+        const float inv_pc = 1.0f / (float)c->particle_count;
+        e = launch_gather_clustered(reinterpret_cast<const Rec*>(dr), di,
+                                    reinterpret_cast<const WorkItem*>(dit), nit, c->d_vrl,
+                                    c->d_slice_off, c->d_reps, c->d_weights, c->d_fb_reps, c->d_fb_w,
+                                    c->n_fb, c->P, inv_pc, dout, c->d_counter + 1, s);
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(o2.data(), dout, sizeof(float) * 3 * nrec, hipMemcpyDeviceToHost, s);
+    if (dr) hipFreeAsync(dr, s);
+    if (di) hipFreeAsync(di, s);
+    if (dout) hipFreeAsync(dout, s);
+    if (dit) hipFreeAsync(dit, s);
+    hipError_t e2 = hipStreamSynchronize(s);
+    hipStreamDestroy(s);
+    if (e == hipSuccess) e = e2;
+    if (e != hipSuccess) return fail(ALVRL_ERR_HIP, std::string("alvrl_gather_clustered_host: ") + hipGetErrorString(e));
+    for (uint32_t i = 0; i < nrec; i++)
+        for (int ch = 0; ch < 3; ch++) out[3 * (size_t)perm[i] + ch] = o2[3 * (size_t)i + ch];
+    return ALVRL_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,232 @@
+// gather.hip -- gfx950 kernels of hot path (a) and the R build of (b).
+//
+//   k_prepare_vrls     VRL SoA (36 B/VRL, VRL.h:89-96) -> VrlPrep (80 B)
+//   k_gather_brute     getVRLContributions, vrlIntegrator.cpp:792-825
+//   k_gather_clustered getClusteredVrlContributions, vrlIntegrator.cpp:542-599
+//   k_build_R          Rbuilder::run -> getLiLuminanceVrlContributions,
+//                      vrlIntegrator.cpp:527-539, 1053-1067
+//
+// Mapping: a lane owns one eye segment (gather record); a wave walks the VRL
+// list in lock step so the VRL index is wave-uniform and VrlPrep arrives in
+// SGPRs through the scalar cache (64 pairs share every 80-B VRL fetch).  The
+// kernels are VALU/transcendental-bound; HBM traffic per pair is << 1 B.
+#include "vrl_device.hpp"
+
+namespace alvrl {
+
+__global__ void __launch_bounds__(256) k_prepare_vrls(const float* __restrict__ soa, uint32_t n,
+                                                      VrlPrep* __restrict__ out)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    VrlPrep p;
+    p.sx = soa[0 * (size_t)n + i]; p.sy = soa[1 * (size_t)n + i]; p.sz = soa[2 * (size_t)n + i];
+    p.ex = soa[3 * (size_t)n + i]; p.ey = soa[4 * (size_t)n + i]; p.ez = soa[5 * (size_t)n + i];
+    p.pr = soa[6 * (size_t)n + i]; p.pg = soa[7 * (size_t)n + i]; p.pb = soa[8 * (size_t)n + i];
+    const F3 v = f3(p.ex, p.ey, p.ez) - f3(p.sx, p.sy, p.sz);
+    p.vx = v.x; p.vy = v.y; p.vz = v.z;
+    const F3 d = nrm(v);
+    p.dx = d.x; p.dy = d.y; p.dz = d.z;
+    p.len = len(f3(p.sx, p.sy, p.sz) - f3(p.ex, p.ey, p.ez));
+    p.c = dot(v, v);
+    p.pad0 = p.pad1 = p.pad2 = 0.0f;
+    out[i] = p;
+}
+
+__device__ __forceinline__ Rec load_rec(const Rec* __restrict__ recs, uint32_t r, bool active)
+{
+    Rec x;
+    if (active) {
+        const float4* p = reinterpret_cast<const float4*>(recs + r);
+        const float4 a = p[0], b = p[1], c = p[2], d = p[3];
+        x.ox = a.x; x.oy = a.y; x.oz = a.z; x.dx = a.w;
+        x.dy = b.x; x.dz = b.y; x.px = b.z; x.py = b.w;
+        x.pz = c.x; x.nx = c.y; x.ny = c.z; x.nz = c.w;
+        x.ar = d.x; x.ag = d.y; x.ab = d.z; x.flags = __float_as_uint(d.w);
+    } else {
+        x.ox = x.oy = x.oz = 0.0f; x.dx = 0.0f; x.dy = 0.0f; x.dz = 1.0f;
+        x.px = x.py = 0.0f; x.pz = 1.0f; x.nx = x.ny = 0.0f; x.nz = -1.0f;
+        x.ar = x.ag = x.ab = 0.0f; x.flags = 0u;
+    }
+    return x;
+}
+
+__device__ __forceinline__ void count_pairs(unsigned long long* counter, bool lane_counts,
+                                            uint32_t per_lane)
+{
+    const unsigned long long m = __ballot(lane_counts);
+    if ((threadIdx.x & 63) == 0 && m)
+        atomicAdd(counter, (unsigned long long)__popcll(m) * per_lane);
+}
+
+template <int NVV, int NVS>
+__global__ void __launch_bounds__(256) k_gather_brute(const Rec* __restrict__ recs,
+                                                      const uint32_t* __restrict__ ids, uint32_t nrec,
+                                                      const VrlPrep* __restrict__ vp, uint32_t nvrl,
+                                                      DevParams P, float normalization,
+                                                      float* __restrict__ out,
+                                                      unsigned long long* counter)
+{
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool active = r < nrec;
+    const Rec rec = load_rec(recs, r, active);
+    const RecPre q = prepare_record(rec, P);
+    const uint32_t rid = active ? (ids ? ids[r] : r) : 0u;
+    float L0 = 0.0f, L1 = 0.0f, L2 = 0.0f;
+    if (q.medium) {
+        for (uint32_t v = 0; v < nvrl; ++v) {
+            const VrlPrep V = vp[v];
+            float c[3], m, s;
+            integrate_vrl<NVV, NVS, false>(P, q, V, rid, v, kDomGather, P.nvv, P.nvs, c, &m, &s);
+            // vrlContribution *= normalization; Li += vrlContribution (:810, 815)
+            L0 += c[0] * normalization; L1 += c[1] * normalization; L2 += c[2] * normalization;
+        }
+    }
+    count_pairs(counter, active && q.medium, nvrl);
+    if (active) {
+        out[3 * (size_t)r + 0] = L0; out[3 * (size_t)r + 1] = L1; out[3 * (size_t)r + 2] = L2;
+    }
+}
+
+struct WorkItem { uint32_t slice, begin, count, pad; };
+
+template <int NVV, int NVS>
+__global__ void __launch_bounds__(256) k_gather_clustered(
+    const Rec* __restrict__ recs, const uint32_t* __restrict__ ids,
+    const WorkItem* __restrict__ items, uint32_t nitems, const VrlPrep* __restrict__ vp,
+    const uint32_t* __restrict__ slice_off, const uint32_t* __restrict__ reps,
+    const float* __restrict__ weights, const uint32_t* __restrict__ fb_reps,
+    const float* __restrict__ fb_w, uint32_t n_fb, DevParams P, float inv_pc,
+    float* __restrict__ out, unsigned long long* counter)
+{
+    const uint32_t item = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+    if (item >= nitems) return;
+    const WorkItem it = items[item];
+    const uint32_t lane = threadIdx.x & 63;
+    const bool active = lane < it.count;
+    const uint32_t r = it.begin + lane;
+    const Rec rec = load_rec(recs, r, active);
+    const RecPre q = prepare_record(rec, P);
+    const uint32_t rid = active ? (ids ? ids[r] : r) : 0u;
+    const uint32_t* lr;
+    const float* lw;
+    uint32_t k;
+    if (it.slice == 0xFFFFFFFFu) { lr = fb_reps; lw = fb_w; k = n_fb; }
+    else { const uint32_t b = slice_off[it.slice]; lr = reps + b; lw = weights + b; k = slice_off[it.slice + 1] - b; }
+    float L0 = 0.0f, L1 = 0.0f, L2 = 0.0f;
+    if (q.medium) {
+        for (uint32_t i = 0; i < k; ++i) {
+            const uint32_t v = lr[i];
+            const float w = lw[i];
+            const VrlPrep V = vp[v];
+            float c[3], m, s;
+            integrate_vrl<NVV, NVS, false>(P, q, V, rid, v, kDomGather, P.nvv, P.nvs, c, &m, &s);
+            // Li += weights->at(i) * integrateVRL(...)  (:587-589)
+            L0 += c[0] * w; L1 += c[1] * w; L2 += c[2] * w;
+        }
+        // Li /= particleCount (:590)
+        L0 *= inv_pc; L1 *= inv_pc; L2 *= inv_pc;
+    }
+    count_pairs(counter, active && q.medium, k);
+    if (active) {
+        out[3 * (size_t)r + 0] = L0; out[3 * (size_t)r + 1] = L1; out[3 * (size_t)r + 2] = L2;
+    }
+}
+
+// R build: lane = representative row, the block's 4 waves interleave over a
+// VRL chunk.  Writes Rt[v][row0 + r] = (mean * norm, var * norm * norm).
+template <int NVV, int NVS>
+__global__ void __launch_bounds__(256) k_build_R(const Rec* __restrict__ recs,
+                                                 const uint32_t* __restrict__ ids, uint32_t nrows,
+                                                 const VrlPrep* __restrict__ vp, uint32_t nvrl,
+                                                 uint32_t chunk, DevParams P, float normalization,
+                                                 float2* __restrict__ Rt, uint64_t ld, uint64_t row0,
+                                                 unsigned long long* counter)
+{
+    const uint32_t r = blockIdx.x * 64 + (threadIdx.x & 63);
+    const uint32_t wave = threadIdx.x >> 6;
+    const bool active = r < nrows;
+    const Rec rec = load_rec(recs, r, active);
+    const RecPre q = prepare_record(rec, P);
+    const uint32_t rid = active ? (ids ? ids[r] : r) : 0u;
+    const uint32_t v0 = blockIdx.y * chunk;
+    const uint32_t v1 = min(nvrl, v0 + chunk);
+    uint32_t done = 0;
+    for (uint32_t v = v0 + wave; v < v1; v += 4) {
+        float mean = 0.0f, var = 0.0f;
+        if (q.medium) {
+            const VrlPrep V = vp[v];
+            float c[3];
+            integrate_vrl<NVV, NVS, true>(P, q, V, rid, v, kDomRbuild, P.nvv, P.nvs, c, &mean, &var);
+            mean = mean * normalization;
+            var = var * normalization * normalization;
+        }
+        if (active) Rt[(size_t)v * ld + row0 + r] = make_float2(mean, var);
+        ++done;
+    }
+    count_pairs(counter, active && q.medium, done);
+}
+
+// ---------------------------------------------------------------------------
+// host-side launchers (called from capi.cpp)
+// ---------------------------------------------------------------------------
+hipError_t launch_prepare_vrls(const float* soa, uint32_t n, VrlPrep* out, hipStream_t s)
+{
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_prepare_vrls, dim3((n + 255) / 256), dim3(256), 0, s, soa, n, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_gather_brute(const Rec* recs, const uint32_t* ids, uint32_t nrec,
+                               const VrlPrep* vp, uint32_t nvrl, const DevParams& P,
+                               float normalization, float* out, unsigned long long* counter,
+                               hipStream_t s)
+{
+    if (nrec == 0) return hipSuccess;
+    const dim3 grid((nrec + 255) / 256), block(256);
+    if (P.nvv == 2 && P.nvs == 2)
+        hipLaunchKernelGGL((k_gather_brute<2, 2>), grid, block, 0, s, recs, ids, nrec, vp, nvrl, P,
+                           normalization, out, counter);
+    else
+        hipLaunchKernelGGL((k_gather_brute<-1, -1>), grid, block, 0, s, recs, ids, nrec, vp, nvrl,
+                           P, normalization, out, counter);
+    return hipGetLastError();
+}
+
+hipError_t launch_gather_clustered(const Rec* recs, const uint32_t* ids, const WorkItem* items,
+                                   uint32_t nitems, const VrlPrep* vp, const uint32_t* slice_off,
+                                   const uint32_t* reps, const float* weights,
+                                   const uint32_t* fb_reps, const float* fb_w, uint32_t n_fb,
+                                   const DevParams& P, float inv_pc, float* out,
+                                   unsigned long long* counter, hipStream_t s)
+{
+    if (nitems == 0) return hipSuccess;
+    const dim3 grid((nitems + 3) / 4), block(256);
+    if (P.nvv == 2 && P.nvs == 2)
+        hipLaunchKernelGGL((k_gather_clustered<2, 2>), grid, block, 0, s, recs, ids, items, nitems,
+                           vp, slice_off, reps, weights, fb_reps, fb_w, n_fb, P, inv_pc, out,
+                           counter);
+    else
+        hipLaunchKernelGGL((k_gather_clustered<-1, -1>), grid, block, 0, s, recs, ids, items,
+                           nitems, vp, slice_off, reps, weights, fb_reps, fb_w, n_fb, P, inv_pc,
+                           out, counter);
+    return hipGetLastError();
+}
+
+hipError_t launch_build_R(const Rec* recs, const uint32_t* ids, uint32_t nrows, const VrlPrep* vp,
+                          uint32_t nvrl, const DevParams& P, float normalization, float2* Rt,
+                          uint64_t ld, uint64_t row0, unsigned long long* counter, hipStream_t s)
+{
+    if (nrows == 0 || nvrl == 0) return hipSuccess;
+    const uint32_t chunk = 256;
+    const dim3 grid((nrows + 63) / 64, (nvrl + chunk - 1) / chunk), block(256);
+    if (P.nvv == 2 && P.nvs == 2)
+        hipLaunchKernelGGL((k_build_R<2, 2>), grid, block, 0, s, recs, ids, nrows, vp, nvrl, chunk,
+                           P, normalization, Rt, ld, row0, counter);
+    else
+        hipLaunchKernelGGL((k_build_R<-1, -1>), grid, block, 0, s, recs, ids, nrows, vp, nvrl,
+                           chunk, P, normalization, Rt, ld, row0, counter);
+    return hipGetLastError();
+}
+
+}  // namespace alvrl

@@ -1,0 +1,428 @@
+// vrl_device.hpp -- gfx950 device maths of the ALVRL gather primitive.
+//
+// integrateVRL (src/integrators/vrl/vrlIntegrator.cpp:603-785) with its
+// samplers (:831-1032), HomogeneousMedium::eval / evalTransmittance
+// (src/medium/homogeneous.cpp:266-273, 354-396, 'balance' strategy), the
+// isotropic / HG phase eval (isotropic.cpp:76-78, hg.cpp:107-110) and
+// SmoothDiffuse::eval (diffuse.cpp:110-118), for one (eye segment, VRL) pair.
+//
+// Execution model: one lane = one eye segment; the VRL being integrated is
+// wave-uniform, so its prepared record (VrlPrep) is fetched with scalar loads
+// into SGPRs and every pair-independent quantity of the eye segment
+// (RecPre) is hoisted out of the VRL loop.  Quantities that the reference
+// recomputes per sample but that do not depend on the sample (the
+// segment-segment closest points, the asinh bounds of Novak's sampler, the
+// equi-angular frame of the vol->surf Kulla sampler) are computed once per
+// pair: identical values, fewer transcendentals.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace alvrl {
+
+constexpr float kEpsilon = 1e-4f;                       // constants.h:27-33
+constexpr float kInvFourPi = 0.07957747154594766788f;
+constexpr float kInvPi = 0.31830988618379067154f;
+
+constexpr uint32_t kDomGather = 1u;   // render gather draws
+constexpr uint32_t kDomRbuild = 2u;   // R-build draws
+
+// Prepared VRL: derived once per VRL set by k_prepare_vrls.  80 B, read with
+// s_load_dwordx16 + s_load_dwordx4.
+struct __attribute__((aligned(16))) VrlPrep {
+    float sx, sy, sz;       // m_start
+    float ex, ey, ez;       // m_end
+    float vx, vy, vz;       // m_end - m_start
+    float pr, pg, pb;       // m_power
+    float dx, dy, dz;       // normalize(m_end - m_start)
+    float len;              // distance(m_start, m_end)
+    float c;                // dot(v, v)
+    float pad0, pad1, pad2;
+};
+static_assert(sizeof(VrlPrep) == 80, "VrlPrep layout");
+
+struct DevParams {
+    float sigma_s[3];
+    float sigma_t[3];
+    float w;                // mediumSamplingWeight
+    float g;                // HG asymmetry
+    int phase_type;
+    int nvv, nvs;
+    int short_vrls;
+    uint32_t seed, pass;
+};
+
+// ---------------------------------------------------------------- RNG --
+struct U4 { uint32_t x, y, z, w; };
+
+__device__ __forceinline__ U4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                            uint32_t k0, uint32_t k1)
+{
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        if (r > 0) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
+        const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+        const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+    }
+    return U4{c0, c1, c2, c3};
+}
+
+// Random::nextFloat (src/libcore/random.cpp:630-639)
+__device__ __forceinline__ float u01(uint32_t b)
+{
+    return __uint_as_float((b >> 9) | 0x3f800000u) - 1.0f;
+}
+
+// ------------------------------------------------------------- vectors --
+struct F3 { float x, y, z; };
+__device__ __forceinline__ F3 f3(float x, float y, float z) { return F3{x, y, z}; }
+__device__ __forceinline__ F3 operator-(F3 a, F3 b) { return f3(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ F3 operator+(F3 a, F3 b) { return f3(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ F3 operator*(F3 a, float s) { return f3(a.x * s, a.y * s, a.z * s); }
+__device__ __forceinline__ F3 neg(F3 a) { return f3(-a.x, -a.y, -a.z); }
+__device__ __forceinline__ float dot(F3 a, F3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ float len2(F3 a) { return a.x * a.x + a.y * a.y + a.z * a.z; }
+__device__ __forceinline__ float len(F3 a) { return sqrtf(len2(a)); }
+__device__ __forceinline__ F3 nrm(F3 a) { const float r = 1.0f / len(a); return a * r; }
+__device__ __forceinline__ float fmax3(float a, float b, float c) { return fmaxf(fmaxf(a, b), c); }
+
+// --------------------------------------------------- per eye segment --
+struct Rec {
+    float ox, oy, oz, dx, dy, dz, px, py, pz, nx, ny, nz, ar, ag, ab;
+    uint32_t flags;
+};
+static_assert(sizeof(Rec) == 64, "Rec layout");
+
+struct RecPre {
+    F3 E, d, dN, P, n, B, dirAB;
+    float lenAB;      // distance(A, B) of the eye Kulla segment
+    float a;          // dot(u, u), u = P - E (getClosestPoints)
+    float cos_wi;     // Frame::cosTheta(its.wi)
+    float teus[3];    // transmittanceEUsurf (vrlIntegrator.cpp:711-719)
+    float alb[3];
+    bool medium, surf;
+};
+
+__device__ __forceinline__ void medium_tr(const DevParams& P, float d, float tr[3], float* pf)
+{
+    // HomogeneousMedium::eval (homogeneous.cpp:354-396): the pdf exponentials
+    // and the transmittance exponentials are the same values.
+    const float t0 = expf(P.sigma_t[0] * (-d));
+    const float t1 = expf(P.sigma_t[1] * (-d));
+    const float t2 = expf(P.sigma_t[2] * (-d));
+    float s = 0.0f;
+    s += t0; s += t1; s += t2;
+    s /= 3;
+    *pf = s * P.w + (1 - P.w);
+    const bool z = fmax3(t0, t1, t2) < 1e-20f;
+    tr[0] = z ? 0.0f : t0; tr[1] = z ? 0.0f : t1; tr[2] = z ? 0.0f : t2;
+}
+
+__device__ __forceinline__ void medium_tr_only(const DevParams& P, float d, float tr[3])
+{
+    const float t0 = expf(P.sigma_t[0] * (-d));
+    const float t1 = expf(P.sigma_t[1] * (-d));
+    const float t2 = expf(P.sigma_t[2] * (-d));
+    const bool z = fmax3(t0, t1, t2) < 1e-20f;
+    tr[0] = z ? 0.0f : t0; tr[1] = z ? 0.0f : t1; tr[2] = z ? 0.0f : t2;
+}
+
+__device__ __forceinline__ RecPre prepare_record(const Rec& r, const DevParams& P)
+{
+    RecPre q;
+    q.E = f3(r.ox, r.oy, r.oz);
+    q.d = f3(r.dx, r.dy, r.dz);
+    q.P = f3(r.px, r.py, r.pz);
+    q.n = f3(r.nx, r.ny, r.nz);
+    q.dN = nrm(q.d);
+    const float edist = len(q.P - q.E);               // sampleUVKulla :869
+    q.B = q.E + q.d * edist;                          // :871
+    q.dirAB = nrm(q.B - q.E);
+    q.lenAB = len(q.E - q.B);
+    const F3 u = q.P - q.E;
+    q.a = dot(u, u);
+    q.cos_wi = dot(neg(q.d), q.n);
+    q.alb[0] = r.ar; q.alb[1] = r.ag; q.alb[2] = r.ab;
+    q.medium = (r.flags & 4u) != 0;
+    q.teus[0] = q.teus[1] = q.teus[2] = 0.0f;
+    if ((r.flags & 1u) && len(q.P - q.E) != 0) medium_tr_only(P, len(q.P - q.E), q.teus);
+    q.surf = (q.teus[0] != 0 || q.teus[1] != 0 || q.teus[2] != 0) && (r.flags & 2u);
+    return q;
+}
+
+__device__ __forceinline__ float phase(const DevParams& P, F3 wi, F3 wo)
+{
+    if (P.phase_type == 0) return kInvFourPi;
+    const float g = P.g;
+    const float temp = 1.0f + g * g + 2.0f * g * dot(wi, wo);
+    return kInvFourPi * (1 - g * g) / (temp * sqrtf(temp));
+}
+
+__device__ __forceinline__ bool spec_valid(float a, float b, float c)
+{
+    return isfinite(a) && isfinite(b) && isfinite(c) && a >= 0.0f && b >= 0.0f && c >= 0.0f;
+}
+
+__device__ __forceinline__ float luminance(float r, float g, float b)
+{
+    return r * 0.212671f + g * 0.715160f + b * 0.072169f;
+}
+
+// Equi-angular (Kulla) frame of a segment A->B (dir, |A-B| given) w.r.t. D.
+struct KullaFrame { F3 I; float Dis, aa, ab; };
+
+__device__ __forceinline__ KullaFrame kulla_frame(F3 A, F3 dir, float lenAB, F3 D, F3 B)
+{
+    KullaFrame k;
+    const float dotPr = dot(dir, D - A);
+    k.I = A + dir * dotPr;
+    k.Dis = len(D - k.I);
+    const float dAI = len(A - k.I);
+    float aa = atanf(dAI / k.Dis);
+    float ab = atanf(len(k.I - B) / k.Dis);
+    if (dotPr > 0) {
+        aa = -aa;
+        if (dAI > lenAB) ab = -ab;
+    }
+    k.aa = aa; k.ab = ab;
+    return k;
+}
+
+// KullaSampling (vrlIntegrator.cpp:889-914) given its frame.
+__device__ __forceinline__ float kulla_sample(const KullaFrame& k, F3 dir, float u, F3* res)
+{
+    const float t = k.Dis * tanf(((1.0f - u) * k.aa) + (u * k.ab));
+    const float pdf = k.Dis / ((k.ab - k.aa) * (k.Dis * k.Dis + t * t));
+    *res = k.I + dir * t;
+    return pdf;
+}
+
+// Pair-constant part of sampleVtoDistance (:916-953) incl. getClosestPoints (:962-1032).
+struct NovakFrame { float sinT, h, A0, dA, denom, dVhS; bool parallel; };
+
+__device__ __forceinline__ NovakFrame novak_frame(const RecPre& q, const VrlPrep& v)
+{
+    NovakFrame f;
+    const F3 S = f3(v.sx, v.sy, v.sz), End = f3(v.ex, v.ey, v.ez);
+    const float cosT = dot(q.dN, f3(v.dx, v.dy, v.dz));
+    const float s2 = 1 - cosT * cosT;
+    f.sinT = sqrtf(s2 > 0.0f ? s2 : 0.0f);
+    f.parallel = f.sinT < kEpsilon;
+    f.h = f.A0 = f.dA = f.denom = f.dVhS = 0.0f;
+    if (!f.parallel) {
+        // getClosestPoints(E, its.p, start, end)
+        const F3 u = q.P - q.E;
+        const F3 vv = f3(v.vx, v.vy, v.vz);
+        const F3 w = q.E - S;
+        const float a = q.a, b = dot(u, vv), c = v.c, d = dot(u, w), e = dot(vv, w);
+        const float D = a * c - b * b;
+        float sN, sD = D, tN, tD = D;
+        if (D < kEpsilon * a * c) {
+            sN = 0.0f; sD = 1.0f; tN = e; tD = c;
+        } else {
+            sN = (b * e - c * d);
+            tN = (a * e - b * d);
+            if (sN < 0.0f) { sN = 0.0f; tN = e; tD = c; }
+            else if (sN > sD) { sN = sD; tN = e + b; tD = c; }
+        }
+        if (tN < 0.0f) {
+            tN = 0.0f;
+            if (-d < 0.0f) sN = 0.0f;
+            else if (-d > a) sN = sD;
+            else { sN = -d; sD = a; }
+        } else if (tN > tD) {
+            tN = tD;
+            if ((-d + b) < 0.0f) sN = 0.0f;
+            else if ((-d + b) > a) sN = sD;
+            else { sN = (-d + b); sD = a; }
+        }
+        const float sc = sN / sD, tc = tN / tD;
+        const F3 dP = (w + u * sc) - vv * tc;
+        const F3 Vh = S + vv * tc;
+        f.h = len(dP);
+        f.dVhS = len(Vh - S);
+        const float V0c = -1 * f.dVhS;
+        const float V1c = len(Vh - End);
+        const float A0 = asinhf((V0c / f.h) * f.sinT);
+        const float A1 = asinhf((V1c / f.h) * f.sinT);
+        f.A0 = A0;
+        f.dA = A1 - A0;
+        f.denom = f.dA / f.sinT;
+    }
+    return f;
+}
+
+// The vrl-dependent sample-0 independent data for vol->surf.
+struct PairPre {
+    NovakFrame nf;
+    KullaFrame ks;     // Kulla frame of the VRL segment w.r.t. Usurf
+};
+
+// One integrateVRL evaluation.  Returns RGB in c[]; *mean / *var receive the
+// luminance mean and variance-of-mean contributions (vrlIntegrator.cpp:693-703, 772-782).
+template <int NVV, int NVS, bool WANT_STATS>
+__device__ __forceinline__ void integrate_vrl(const DevParams& P, const RecPre& q, const VrlPrep& v,
+                                              uint32_t rec_id, uint32_t vrl_id, uint32_t domain,
+                                              int nvv_rt, int nvs_rt, float out[3], float* mean_out,
+                                              float* var_out)
+{
+    const int nVV = NVV >= 0 ? NVV : nvv_rt;
+    const int nVS = NVS >= 0 ? NVS : nvs_rt;
+    const F3 S = f3(v.sx, v.sy, v.sz), End = f3(v.ex, v.ey, v.ez);
+    const F3 SV = f3(v.dx, v.dy, v.dz);
+    float tot0 = 0.0f, tot1 = 0.0f, tot2 = 0.0f;
+    float mean = 0.0f, M2 = 0.0f, mean_acc = 0.0f, var_acc = 0.0f;
+    const uint32_t k0 = P.seed, k1 = P.pass;
+    const uint32_t c3 = domain << 24;
+
+    // draws 0..3: volVol samples 0,1 (V, U); draws 4..7: volSurf / further volVol
+    U4 rb = philox4x32_10(rec_id, vrl_id, 0u, c3, k0, k1);
+    uint32_t cur_blk = 0;
+    auto draw = [&](int k) -> float {
+        const uint32_t blk = (uint32_t)k >> 2;
+        if (blk != cur_blk) { rb = philox4x32_10(rec_id, vrl_id, blk, c3, k0, k1); cur_blk = blk; }
+        const uint32_t s = k & 3;
+        const uint32_t b = s == 0 ? rb.x : (s == 1 ? rb.y : (s == 2 ? rb.z : rb.w));
+        return u01(b);
+    };
+
+    const NovakFrame nf = novak_frame(q, v);
+    const float phV_const = kInvFourPi;
+
+    // ---------------- volume -> volume (:647-703) ----------------
+#pragma unroll
+    for (int sample = 0; sample < (NVV >= 0 ? NVV : 64); ++sample) {
+        if (NVV < 0 && sample >= nVV) break;
+        float lumv = 0.0f;
+        const float u0 = draw(2 * sample), u1 = draw(2 * sample + 1);
+        F3 V;
+        float pdfV;
+        if (nf.parallel) {
+            V = S + f3(v.vx, v.vy, v.vz) * u0;
+            pdfV = 1 / v.len;
+        } else {
+            float newV = nf.h * sinhf(nf.A0 + (u0 * nf.dA));
+            newV = newV / nf.sinT;
+            const float result = 1.0f / sqrtf(nf.h * nf.h + newV * newV * nf.sinT * nf.sinT);
+            newV += nf.dVhS;
+            V = S + SV * newV;
+            pdfV = result / nf.denom;
+        }
+        const KullaFrame ke = kulla_frame(q.E, q.dirAB, q.lenAB, V, q.B);
+        F3 U;
+        const float pdf = pdfV * kulla_sample(ke, q.dirAB, u1, &U);
+        const F3 UV = U - V;
+        const float l2 = len2(UV);
+        const float dUV = sqrtf(l2);
+        if (dUV != 0) {
+            const F3 VU = UV * (1.0f / dUV);
+            float tuv[3];
+            tuv[0] = P.sigma_t[0] != 0 ? expf(P.sigma_t[0] * (0.0f - dUV)) : 1.0f;
+            tuv[1] = P.sigma_t[1] != 0 ? expf(P.sigma_t[1] * (0.0f - dUV)) : 1.0f;
+            tuv[2] = P.sigma_t[2] != 0 ? expf(P.sigma_t[2] * (0.0f - dUV)) : 1.0f;
+            if (tuv[0] != 0 || tuv[1] != 0 || tuv[2] != 0) {
+                float teu[3], tsv[3], pf;
+                medium_tr_only(P, len(q.E - U), teu);
+                medium_tr(P, len(S - V), tsv, &pf);
+                const float rpdf = 1.0f / pdf;
+                const float rd2 = 1 / l2;
+                const float rpf = P.short_vrls ? 1.0f / pf : 1.0f;
+                const float phU = P.phase_type == 0 ? kInvFourPi : phase(P, neg(VU), neg(q.d));
+                const float phV = P.phase_type == 0 ? phV_const : phase(P, neg(SV), VU);
+                float c0 = v.pr, c1 = v.pg, c2 = v.pb;
+                c0 *= (P.sigma_s[0] * P.sigma_s[0]) * rpdf;
+                c1 *= (P.sigma_s[1] * P.sigma_s[1]) * rpdf;
+                c2 *= (P.sigma_s[2] * P.sigma_s[2]) * rpdf;
+                c0 *= rd2; c1 *= rd2; c2 *= rd2;
+                c0 *= tsv[0]; c1 *= tsv[1]; c2 *= tsv[2];
+                c0 *= tuv[0]; c1 *= tuv[1]; c2 *= tuv[2];
+                c0 *= teu[0]; c1 *= teu[1]; c2 *= teu[2];
+                c0 *= rpf; c1 *= rpf; c2 *= rpf;
+                c0 *= phU; c1 *= phU; c2 *= phU;
+                c0 *= phV; c1 *= phV; c2 *= phV;
+                if (spec_valid(c0, c1, c2)) {
+                    const float rn = 1.0f / (float)nVV;
+                    tot0 += c0 * rn; tot1 += c1 * rn; tot2 += c2 * rn;
+                    lumv = luminance(c0, c1, c2);
+                }
+            }
+        }
+        if (WANT_STATS) {
+            const float delta = lumv - mean;
+            mean += delta / (sample + 1);
+            M2 += delta * (lumv - mean);
+        }
+    }
+    if (WANT_STATS && nVV > 0) {
+        mean_acc += mean;
+        var_acc += M2 / ((nVV - 1) * nVV);
+    }
+
+    // ---------------- volume -> surface (:706-782) ----------------
+    if (nVS > 0) {
+        mean = 0.0f; M2 = 0.0f;
+        KullaFrame ks;
+        if (q.surf) ks = kulla_frame(S, SV, v.len, q.P, End);
+#pragma unroll
+        for (int sample = 0; sample < (NVS >= 0 ? NVS : 64); ++sample) {
+            if (NVS < 0 && sample >= nVS) break;
+            float lumv = 0.0f;
+            if (q.surf) {
+                const float u = draw(2 * nVV + sample);
+                F3 V;
+                const float pdf = kulla_sample(ks, SV, u, &V);
+                const F3 UV = q.P - V;
+                const float l2 = len2(UV);
+                const float dUV = sqrtf(l2);
+                if (dUV != 0) {
+                    const F3 VU = UV * (1.0f / dUV);
+                    float tuv[3], tsv[3], pf;
+                    tuv[0] = P.sigma_t[0] != 0 ? expf(P.sigma_t[0] * (0.0f - dUV)) : 1.0f;
+                    tuv[1] = P.sigma_t[1] != 0 ? expf(P.sigma_t[1] * (0.0f - dUV)) : 1.0f;
+                    tuv[2] = P.sigma_t[2] != 0 ? expf(P.sigma_t[2] * (0.0f - dUV)) : 1.0f;
+                    medium_tr(P, len(S - V), tsv, &pf);
+                    const float cos_wo = dot(neg(VU), q.n);
+                    const bool bz = (q.cos_wi <= 0 || cos_wo <= 0);
+                    const float fcos = kInvPi * cos_wo;
+                    const float f0 = bz ? 0.0f : q.alb[0] * fcos;
+                    const float f1 = bz ? 0.0f : q.alb[1] * fcos;
+                    const float f2 = bz ? 0.0f : q.alb[2] * fcos;
+                    const float phV = P.phase_type == 0 ? kInvFourPi : phase(P, neg(SV), VU);
+                    const float rpdf = 1.0f / pdf;
+                    const float rd2 = 1 / l2;
+                    const float rpf = P.short_vrls ? 1.0f / pf : 1.0f;
+                    float c0 = v.pr, c1 = v.pg, c2 = v.pb;
+                    c0 *= P.sigma_s[0] * rpdf; c1 *= P.sigma_s[1] * rpdf; c2 *= P.sigma_s[2] * rpdf;
+                    c0 *= rd2; c1 *= rd2; c2 *= rd2;
+                    c0 *= tsv[0]; c1 *= tsv[1]; c2 *= tsv[2];
+                    c0 *= tuv[0]; c1 *= tuv[1]; c2 *= tuv[2];
+                    c0 *= q.teus[0]; c1 *= q.teus[1]; c2 *= q.teus[2];
+                    c0 *= rpf; c1 *= rpf; c2 *= rpf;
+                    c0 *= phV; c1 *= phV; c2 *= phV;
+                    c0 *= f0; c1 *= f1; c2 *= f2;
+                    if (spec_valid(c0, c1, c2)) {
+                        const float rn = 1.0f / (float)nVS;
+                        tot0 += c0 * rn; tot1 += c1 * rn; tot2 += c2 * rn;
+                        lumv = luminance(c0, c1, c2);
+                    }
+                }
+            }
+            if (WANT_STATS) {
+                const float delta = lumv - mean;
+                mean += delta / (sample + 1);
+                M2 += delta * (lumv - mean);
+            }
+        }
+        if (WANT_STATS) {
+            mean_acc += mean;
+            var_acc += M2 / ((nVS - 1) * nVS);
+        }
+    }
+    out[0] = tot0; out[1] = tot1; out[2] = tot2;
+    if (WANT_STATS) { *mean_out = mean_acc; *var_out = var_acc; }
+}
+
+}  // namespace alvrl

@@ -1,0 +1,852 @@
+/*
+ * alvrl_oracle.c -- CPU restatement of the ALVRL gather path.
+ * TEST INFRASTRUCTURE ONLY (see alvrl_oracle.h for scope, citations and the
+ * "parity unpinned" status).  Compiled two ways by oracle/Makefile:
+ *   liboracle.so       strict IEEE (-O2 -ffp-contract=off), the parity checker
+ *   liboracle_fast.so  the reference's own flags (build/config-linux-gcc.py:7),
+ *                      used only as bench.py's timed CPU baseline.
+ */
+#include "alvrl_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#include <pthread.h>
+
+/* include/mitsuba/core/constants.h:27-33 (SINGLE_PRECISION) */
+#define EPSILON       1e-4f
+#define INV_FOURPI    0.07957747154594766788f
+#define INV_PI        0.31830988618379067154f
+#ifndef M_PI
+#define M_PI 3.14159265358979323846
+#endif
+
+/* ===================================================================== */
+/*  Counter RNG: Philox4x32-10 (Salmon et al., SC'11; Random123)           */
+/* ===================================================================== */
+static inline uint32_t mulhilo32(uint32_t a, uint32_t b, uint32_t *hi)
+{
+    uint64_t p = (uint64_t)a * (uint64_t)b;
+    *hi = (uint32_t)(p >> 32);
+    return (uint32_t)p;
+}
+
+void alvrl_o_philox4x32_10(const uint32_t ctr_in[4], const uint32_t key_in[2], uint32_t out[4])
+{
+    uint32_t c0 = ctr_in[0], c1 = ctr_in[1], c2 = ctr_in[2], c3 = ctr_in[3];
+    uint32_t k0 = key_in[0], k1 = key_in[1];
+    for (int r = 0; r < 10; r++) {
+        if (r > 0) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
+        uint32_t hi0, hi1;
+        uint32_t lo0 = mulhilo32(0xD2511F53u, c0, &hi0);
+        uint32_t lo1 = mulhilo32(0xCD9E8D57u, c2, &hi1);
+        uint32_t n0 = hi1 ^ c1 ^ k0, n1 = lo1, n2 = hi0 ^ c3 ^ k1, n3 = lo0;
+        c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+    }
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+/* Random::nextFloat, src/libcore/random.cpp:630-639 */
+float alvrl_o_u01(uint32_t bits)
+{
+    union { uint32_t u; float f; } x;
+    x.u = (bits >> 9) | 0x3f800000u;
+    return x.f - 1.0f;
+}
+
+/* Random-access draw k of the stream (dom, a, b, c). */
+static float draw(uint32_t seed, uint32_t pass, uint32_t dom, uint32_t a, uint32_t b,
+                  uint32_t c, uint32_t k)
+{
+    uint32_t ctr[4] = { a, b, k >> 2, (dom << 24) | (c & 0xFFFFFFu) };
+    uint32_t key[2] = { seed, pass };
+    uint32_t out[4];
+    alvrl_o_philox4x32_10(ctr, key, out);
+    return alvrl_o_u01(out[k & 3]);
+}
+
+/* Sequential sampler over one stream (Sampler::next1D / next2D). */
+typedef struct {
+    uint32_t seed, pass, dom, a, b, c, k;
+    uint32_t buf[4];
+    uint32_t buf_block;
+} seq_sampler;
+
+static void seq_init(seq_sampler *s, uint32_t seed, uint32_t pass, uint32_t dom,
+                     uint32_t a, uint32_t b, uint32_t c)
+{
+    s->seed = seed; s->pass = pass; s->dom = dom;
+    s->a = a; s->b = b; s->c = c; s->k = 0; s->buf_block = 0xFFFFFFFFu;
+}
+
+static float seq_next(seq_sampler *s)
+{
+    uint32_t blk = s->k >> 2;
+    if (blk != s->buf_block) {
+        uint32_t ctr[4] = { s->a, s->b, blk, (s->dom << 24) | (s->c & 0xFFFFFFu) };
+        uint32_t key[2] = { s->seed, s->pass };
+        alvrl_o_philox4x32_10(ctr, key, s->buf);
+        s->buf_block = blk;
+    }
+    float v = alvrl_o_u01(s->buf[s->k & 3]);
+    s->k++;
+    return v;
+}
+
+/* ===================================================================== */
+/*  Vector helpers (include/mitsuba/core/vector.h, point.h semantics)      */
+/* ===================================================================== */
+typedef struct { float x, y, z; } v3;
+
+static inline v3 mk(float x, float y, float z) { v3 r = { x, y, z }; return r; }
+static inline v3 sub(v3 a, v3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+static inline v3 add(v3 a, v3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+static inline v3 scl(v3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
+static inline v3 neg(v3 a) { return mk(-a.x, -a.y, -a.z); }
+static inline float dot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+static inline float len2(v3 a) { return a.x * a.x + a.y * a.y + a.z * a.z; }
+static inline float len(v3 a) { return sqrtf(len2(a)); }
+static inline float dist(v3 a, v3 b) { return len(sub(a, b)); }
+static inline float dist2(v3 a, v3 b) { return len2(sub(a, b)); }
+/* normalize(v) = v / v.length(), and operator/ multiplies by the reciprocal */
+static inline v3 nrm(v3 a) { float r = 1.0f / len(a); return scl(a, r); }
+static inline v3 cross(v3 a, v3 b)
+{
+    return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+static inline v3 ld3(const float *p) { return mk(p[0], p[1], p[2]); }
+
+/* math::fastexp on Linux/x86_64 (include/mitsuba/core/math.h:175-199) */
+static inline float fastexp(float v) { return (float)exp((double)v); }
+static inline float fastlog(float v) { return (float)log((double)v); }
+static inline float safe_sqrt(float v) { return sqrtf(v > 0.0f ? v : 0.0f); }
+
+/* Spectrum::isValid, include/mitsuba/core/spectrum.h:467-472 */
+static inline int spec_valid(const float s[3])
+{
+    for (int i = 0; i < 3; i++)
+        if (!isfinite(s[i]) || s[i] < 0.0f) return 0;
+    return 1;
+}
+/* Spectrum::getLuminance, spectrum.h:638-640 */
+static inline float lum(const float s[3])
+{
+    return s[0] * 0.212671f + s[1] * 0.715160f + s[2] * 0.072169f;
+}
+
+/* ===================================================================== */
+/*  Medium / phase / BSDF                                                  */
+/* ===================================================================== */
+void alvrl_o_medium_init(alvrl_o_medium *m, const float sigma_s[3], const float sigma_a[3],
+                         float w, int phase_type, float g)
+{
+    for (int i = 0; i < 3; i++) {
+        m->sigma_s[i] = sigma_s[i];
+        m->sigma_a[i] = sigma_a[i];
+        m->sigma_t[i] = sigma_s[i] + sigma_a[i];
+    }
+    /* homogeneous.cpp:168-184: highest albedo, clamped to >= 0.5 */
+    if (w == -1) {
+        for (int i = 0; i < 3; i++) {
+            float albedo = m->sigma_s[i] / m->sigma_t[i];
+            if (albedo > w && m->sigma_t[i] != 0) w = albedo;
+        }
+        if (w > 0) w = w > 0.5f ? w : 0.5f;
+    }
+    m->sampling_weight = w;
+    m->phase_type = phase_type;
+    m->phase_g = g;
+}
+
+/* HomogeneousMedium::eval, 'balance' strategy (homogeneous.cpp:354-396).
+ * Only the fields used by integrateVRL are produced. */
+static void medium_eval(const alvrl_o_medium *m, float distance, float tr[3], float *pdf_failure)
+{
+    float pf = 0.0f;
+    for (int i = 0; i < 3; i++) {
+        float temp = fastexp(-m->sigma_t[i] * distance);
+        pf += temp;
+    }
+    pf /= 3;
+    for (int i = 0; i < 3; i++) tr[i] = fastexp(m->sigma_t[i] * (-distance));
+    *pdf_failure = pf * m->sampling_weight + (1 - m->sampling_weight);
+    float mx = tr[0] > tr[1] ? tr[0] : tr[1];
+    mx = mx > tr[2] ? mx : tr[2];
+    if (mx < 1e-20f) tr[0] = tr[1] = tr[2] = 0.0f;
+}
+
+/* HomogeneousMedium::evalTransmittance (homogeneous.cpp:266-273) as used by
+ * Scene::evalTransmittance (scene.cpp:619-679) when no surface blocks the
+ * segment (convex container: every interior pair is mutually visible). */
+static void shadow_transmittance(const alvrl_o_medium *m, v3 p1, v3 p2, float tr[3])
+{
+    v3 d = sub(p2, p1);
+    float remaining = len(d);
+    float negLength = 0.0f - remaining;
+    for (int i = 0; i < 3; i++)
+        tr[i] = m->sigma_t[i] != 0 ? fastexp(m->sigma_t[i] * negLength) : 1.0f;
+}
+
+/* isotropic.cpp:76-78, hg.cpp:107-110 */
+static float phase_eval(const alvrl_o_medium *m, v3 wi, v3 wo)
+{
+    if (m->phase_type == 0) return INV_FOURPI;
+    float g = m->phase_g;
+    float temp = 1.0f + g * g + 2.0f * g * dot(wi, wo);
+    return INV_FOURPI * (1 - g * g) / (temp * sqrtf(temp));
+}
+
+/* ===================================================================== */
+/*  Samplers (vrlIntegrator.cpp:831-1032)                                  */
+/* ===================================================================== */
+/* getClosestPoints, vrlIntegrator.cpp:962-1032 */
+static float closest_points(v3 S1P0, v3 S1P1, v3 S2P0, v3 S2P1, v3 *S1h, v3 *S2h)
+{
+    v3 u = sub(S1P1, S1P0);
+    v3 v = sub(S2P1, S2P0);
+    v3 w = sub(S1P0, S2P0);
+    float a = dot(u, u);
+    float b = dot(u, v);
+    float c = dot(v, v);
+    float d = dot(u, w);
+    float e = dot(v, w);
+    float D = a * c - b * b;
+    float sc, sN, sD = D;
+    float tc, tN, tD = D;
+
+    if (D < EPSILON * len2(u) * len2(v)) {
+        sN = 0.0f; sD = 1.0f; tN = e; tD = c;
+    } else {
+        sN = (b * e - c * d);
+        tN = (a * e - b * d);
+        if (sN < 0.0f) { sN = 0.0f; tN = e; tD = c; }
+        else if (sN > sD) { sN = sD; tN = e + b; tD = c; }
+    }
+    if (tN < 0.0f) {
+        tN = 0.0f;
+        if (-d < 0.0f) sN = 0.0f;
+        else if (-d > a) sN = sD;
+        else { sN = -d; sD = a; }
+    } else if (tN > tD) {
+        tN = tD;
+        if ((-d + b) < 0.0f) sN = 0;
+        else if ((-d + b) > a) sN = sD;
+        else { sN = (-d + b); sD = a; }
+    }
+    sc = sN / sD;
+    tc = tN / tD;
+    v3 dP = sub(add(w, scl(u, sc)), scl(v, tc));
+    *S1h = add(S1P0, scl(sub(S1P1, S1P0), sc));
+    *S2h = add(S2P0, scl(sub(S2P1, S2P0), tc));
+    return len(dP);
+}
+
+/* KullaSampling, vrlIntegrator.cpp:889-914 (equi-angular sampling) */
+static float kulla(v3 A, v3 B, v3 D, v3 *result, float uniform)
+{
+    v3 dir = nrm(sub(B, A));
+    float dotPr = dot(dir, sub(D, A));
+    v3 I = add(A, scl(dir, dotPr));
+    float Dis = dist(D, I);
+    float angle_a = atanf(dist(A, I) / Dis);
+    float angle_b = atanf(dist(I, B) / Dis);
+    if (dotPr > 0) {
+        angle_a *= -1;
+        if (dist(A, I) > dist(A, B)) angle_b *= -1;
+    }
+    float t = Dis * tanf(((1.0f - uniform) * angle_a) + (uniform * angle_b));
+    float pdf = Dis / ((angle_b - angle_a) * (Dis * Dis + t * t));
+    *result = add(I, scl(dir, t));
+    return pdf;
+}
+
+static inline float Afun(float x, float h, float sinTheta) { return asinhf((x / h) * sinTheta); }
+
+/* sampleVtoDistance, vrlIntegrator.cpp:916-953 (Novak et al. 2012) */
+static float sample_v_to_distance(v3 E, v3 d, v3 hitp, v3 S, v3 End, v3 *V, float uniform)
+{
+    if (dist(S, End) == 0) { *V = S; return 1; }
+    float cosTheta = dot(nrm(d), nrm(sub(End, S)));
+    float sinTheta = safe_sqrt(1 - cosTheta * cosTheta);
+    if (sinTheta < EPSILON) {
+        *V = add(S, scl(sub(End, S), uniform));
+        return 1 / dist(End, S);
+    }
+    v3 Uh, Vh;
+    float h = closest_points(E, hitp, S, End, &Uh, &Vh);
+    float V0c = -1 * dist(Vh, S);
+    float V1c = dist(Vh, End);
+    float newV = h * sinhf(Afun(V0c, h, sinTheta)
+                           + (uniform * (Afun(V1c, h, sinTheta) - Afun(V0c, h, sinTheta))));
+    newV = newV / sinTheta;
+    float result = 1.0f / sqrtf(h * h + newV * newV * sinTheta * sinTheta);
+    float denom = (Afun(V1c, h, sinTheta) - Afun(V0c, h, sinTheta)) / sinTheta;
+    newV += dist(Vh, S);
+    *V = add(S, scl(nrm(sub(End, S)), newV));
+    return result / denom;
+}
+
+/* ===================================================================== */
+/*  integrateVRL, vrlIntegrator.cpp:603-785                                */
+/* ===================================================================== */
+void alvrl_o_integrate_vrl(const alvrl_o_params *P, const float *rec, uint32_t rec_id,
+                           const float *vs, uint32_t nvrl, uint32_t vrl_id,
+                           uint32_t domain, float out_rgb[3], float *contrib, float *variance)
+{
+    const alvrl_o_medium *m = &P->medium;
+    uint32_t flags;
+    memcpy(&flags, &rec[15], 4);
+    if (contrib) *contrib = 0;
+    if (variance) *variance = 0;
+    out_rgb[0] = out_rgb[1] = out_rgb[2] = 0.0f;
+    if (!(flags & ALVRL_O_FLAG_MEDIUM)) return;   /* :614-617 */
+
+    v3 E = ld3(rec + 0), dray = ld3(rec + 3), Usurf = ld3(rec + 6), nrmS = ld3(rec + 9);
+    v3 S = mk(vs[0 * nvrl + vrl_id], vs[1 * nvrl + vrl_id], vs[2 * nvrl + vrl_id]);
+    v3 End = mk(vs[3 * nvrl + vrl_id], vs[4 * nvrl + vrl_id], vs[5 * nvrl + vrl_id]);
+    float power[3] = { vs[6 * nvrl + vrl_id], vs[7 * nvrl + vrl_id], vs[8 * nvrl + vrl_id] };
+    v3 SV = nrm(sub(End, S));
+    v3 EU = dray;
+    const int nVV = P->vol_vol_samples, nVS = P->vol_surf_samples;
+    float total[3] = { 0, 0, 0 };
+
+    /* sampleUVKulla's eye segment end (:865-871); its.t is finite here */
+    float edist = dist(Usurf, E);
+    v3 A = E, B = add(E, scl(dray, edist));
+
+    /* ---- volume to volume (:647-703) ---- */
+    float mean = 0, M2 = 0;
+    for (int sample = 0; sample < nVV; sample++) {
+        float lumv = 0.0f;
+        float u0 = draw(P->seed, P->pass, domain, rec_id, vrl_id, 0, 2 * sample);
+        float u1 = draw(P->seed, P->pass, domain, rec_id, vrl_id, 0, 2 * sample + 1);
+        v3 V, U;
+        float pdf = sample_v_to_distance(E, dray, Usurf, S, End, &V, u0);
+        pdf *= kulla(A, B, V, &U, u1);
+        if (dist(U, V) == 0) goto vv_welford;
+        {
+            v3 VU = nrm(sub(U, V));
+            float tuv[3], teu[3], tsv[3], pf_eu, pf_sv;
+            shadow_transmittance(m, U, V, tuv);
+            if (tuv[0] == 0 && tuv[1] == 0 && tuv[2] == 0) goto vv_welford;
+            medium_eval(m, dist(E, U), teu, &pf_eu);
+            medium_eval(m, dist(S, V), tsv, &pf_sv);
+            float c[3];
+            float rpdf = 1.0f / pdf;
+            float rd2 = 1 / dist2(U, V);
+            float phU = phase_eval(m, neg(VU), neg(EU));
+            float phV = phase_eval(m, neg(SV), VU);
+            float rpf = 1.0f / pf_sv;
+            for (int i = 0; i < 3; i++) {
+                c[i] = 1.0f;
+                c[i] *= power[i];
+                c[i] *= (m->sigma_s[i] * m->sigma_s[i]) * rpdf;
+                c[i] *= rd2;
+                c[i] *= tsv[i];
+                c[i] *= tuv[i];
+                c[i] *= teu[i];
+                if (P->short_vrls) c[i] *= rpf;
+                c[i] *= phU;
+                c[i] *= phV;
+            }
+            if (spec_valid(c)) {
+                float rn = 1.0f / (float)nVV;
+                for (int i = 0; i < 3; i++) total[i] += c[i] * rn;
+                lumv = lum(c);
+            }
+        }
+    vv_welford: {
+            /* :693-699, evaluated online in the same order */
+            float delta = lumv - mean;
+            mean += delta / (sample + 1);
+            M2 += delta * (lumv - mean);
+        }
+    }
+    if (contrib && nVV > 0) *contrib += mean;
+    if (variance && nVV > 0) *variance += M2 / ((nVV - 1) * nVV);
+
+    /* ---- volume to surface (:706-782) ---- */
+    v3 U = Usurf;
+    float teus[3] = { 0, 0, 0 };
+    if (flags & ALVRL_O_FLAG_HIT) {
+        if (dist(Usurf, E) != 0) {
+            float pfd;
+            medium_eval(m, dist(Usurf, E), teus, &pfd);
+        }
+    }
+    mean = 0; M2 = 0;
+    int do_surf = (teus[0] != 0 || teus[1] != 0 || teus[2] != 0) && (flags & ALVRL_O_FLAG_SMOOTH);
+    for (int sample = 0; sample < nVS; sample++) {
+        float lumv = 0.0f;
+        if (do_surf) {
+            float u = draw(P->seed, P->pass, domain, rec_id, vrl_id, 0, 2 * nVV + sample);
+            v3 V;
+            float pdf = kulla(S, End, U, &V, u);
+            if (dist(U, V) != 0) {
+                v3 VU = nrm(sub(U, V));
+                float tuv[3], tsv[3], pf_sv;
+                shadow_transmittance(m, U, V, tuv);
+                medium_eval(m, dist(S, V), tsv, &pf_sv);
+                /* SmoothDiffuse::eval (diffuse.cpp:110-118), wi = its.wi, wo = toLocal(-VU) */
+                v3 mVU = neg(VU);
+                float cos_wi = dot(neg(dray), nrmS);
+                float cos_wo = dot(mVU, nrmS);
+                float f[3] = { 0, 0, 0 };
+                if (!(cos_wi <= 0 || cos_wo <= 0))
+                    for (int i = 0; i < 3; i++) f[i] = rec[12 + i] * (INV_PI * cos_wo);
+                float phV = phase_eval(m, neg(SV), VU);
+                float rpdf = 1.0f / pdf;
+                float rd2 = 1 / dist2(U, V);
+                float rpf = 1.0f / pf_sv;
+                float c[3];
+                for (int i = 0; i < 3; i++) {
+                    c[i] = 1.0f;
+                    c[i] *= power[i];
+                    c[i] *= m->sigma_s[i] * rpdf;
+                    c[i] *= rd2;
+                    c[i] *= tsv[i];
+                    c[i] *= tuv[i];
+                    c[i] *= teus[i];
+                    if (P->short_vrls) c[i] *= rpf;
+                    c[i] *= phV;
+                    c[i] *= f[i];
+                }
+                if (spec_valid(c)) {
+                    float rn = 1.0f / (float)nVS;
+                    for (int i = 0; i < 3; i++) total[i] += c[i] * rn;
+                    lumv = lum(c);
+                }
+            }
+        }
+        float delta = lumv - mean;
+        mean += delta / (sample + 1);
+        M2 += delta * (lumv - mean);
+    }
+    if (contrib && nVS > 0) *contrib += mean;
+    if (variance && nVS > 0) *variance += M2 / ((nVS - 1) * nVS);
+
+    out_rgb[0] = total[0]; out_rgb[1] = total[1]; out_rgb[2] = total[2];
+}
+
+/* ===================================================================== */
+/*  Gathers                                                                */
+/* ===================================================================== */
+typedef struct {
+    const alvrl_o_params *P;
+    const float *recs; uint32_t nrec; const uint32_t *rec_ids;
+    const float *vs; uint32_t nvrl; uint64_t pc; uint32_t domain;
+    float *out; float *R;
+    /* clustered */
+    const uint32_t *slice_of_rec, *slice_off, *reps, *fb_reps;
+    const float *weights, *fb_weights; uint32_t n_fb;
+    uint32_t r0, r1;
+    uint64_t count;
+} gjob;
+
+/* getVRLContributions, vrlIntegrator.cpp:792-825 */
+static void *brute_worker(void *arg)
+{
+    gjob *j = (gjob *)arg;
+    float normalization = (float)(1.0 / (double)j->pc);
+    for (uint32_t r = j->r0; r < j->r1; r++) {
+        const float *rec = j->recs + (size_t)r * ALVRL_O_REC_WORDS;
+        uint32_t flags;
+        memcpy(&flags, &rec[15], 4);
+        float Li[3] = { 0, 0, 0 };
+        uint32_t rid = j->rec_ids ? j->rec_ids[r] : r;
+        if (flags & ALVRL_O_FLAG_MEDIUM) {
+            for (uint32_t v = 0; v < j->nvrl; v++) {
+                float c[3], contribution, variance;
+                alvrl_o_integrate_vrl(j->P, rec, rid, j->vs, j->nvrl, v, j->domain, c,
+                                      &contribution, &variance);
+                for (int i = 0; i < 3; i++) c[i] *= normalization;
+                if (j->R) {
+                    float *e = j->R + 2 * ((size_t)r * j->nvrl + v);
+                    e[0] += contribution * normalization;
+                    e[1] += variance * normalization * normalization;
+                }
+                for (int i = 0; i < 3; i++) Li[i] += c[i];
+            }
+            j->count += j->nvrl;
+        }
+        for (int i = 0; i < 3; i++) j->out[3 * (size_t)r + i] = Li[i];
+    }
+    return NULL;
+}
+
+/* getClusteredVrlContributions, vrlIntegrator.cpp:542-599 */
+static void *clustered_worker(void *arg)
+{
+    gjob *j = (gjob *)arg;
+    for (uint32_t r = j->r0; r < j->r1; r++) {
+        const float *rec = j->recs + (size_t)r * ALVRL_O_REC_WORDS;
+        uint32_t flags;
+        memcpy(&flags, &rec[15], 4);
+        float Li[3] = { 0, 0, 0 };
+        uint32_t rid = j->rec_ids ? j->rec_ids[r] : r;
+        if (flags & ALVRL_O_FLAG_MEDIUM) {
+            uint32_t s = j->slice_of_rec[r];
+            const uint32_t *vr;
+            const float *w;
+            uint32_t k;
+            if (s == 0xFFFFFFFFu) { vr = j->fb_reps; w = j->fb_weights; k = j->n_fb; }
+            else {
+                vr = j->reps + j->slice_off[s];
+                w = j->weights + j->slice_off[s];
+                k = j->slice_off[s + 1] - j->slice_off[s];
+            }
+            for (uint32_t i = 0; i < k; i++) {
+                float c[3];
+                alvrl_o_integrate_vrl(j->P, rec, rid, j->vs, j->nvrl, vr[i], j->domain, c, NULL, NULL);
+                for (int ch = 0; ch < 3; ch++) Li[ch] += c[ch] * w[i];
+            }
+            float rp = 1.0f / (float)j->pc;   /* Li /= particleCount (spectrum.h:447-455) */
+            for (int ch = 0; ch < 3; ch++) Li[ch] *= rp;
+            j->count += k;
+        }
+        for (int ch = 0; ch < 3; ch++) j->out[3 * (size_t)r + ch] = Li[ch];
+    }
+    return NULL;
+}
+
+static uint64_t run_jobs(gjob *proto, void *(*fn)(void *), uint32_t nrec, int nthreads)
+{
+    if (nthreads < 1) nthreads = 1;
+    if ((uint32_t)nthreads > nrec && nrec > 0) nthreads = (int)nrec;
+    gjob *jobs = (gjob *)calloc((size_t)nthreads, sizeof(gjob));
+    pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
+    for (int t = 0; t < nthreads; t++) {
+        jobs[t] = *proto;
+        jobs[t].r0 = (uint32_t)(((uint64_t)t * nrec) / nthreads);
+        jobs[t].r1 = (uint32_t)(((uint64_t)(t + 1) * nrec) / nthreads);
+        jobs[t].count = 0;
+        if (nthreads > 1) pthread_create(&th[t], NULL, fn, &jobs[t]);
+        else fn(&jobs[t]);
+    }
+    uint64_t total = 0;
+    for (int t = 0; t < nthreads; t++) {
+        if (nthreads > 1) pthread_join(th[t], NULL);
+        total += jobs[t].count;
+    }
+    free(jobs);
+    free(th);
+    return total;
+}
+
+uint64_t alvrl_o_gather_brute(const alvrl_o_params *P, const float *recs, uint32_t nrec,
+                              const uint32_t *rec_ids, const float *vrl_soa, uint32_t nvrl,
+                              uint64_t particle_count, uint32_t domain,
+                              float *out_rgb, float *R_rows, int nthreads)
+{
+    gjob j;
+    memset(&j, 0, sizeof(j));
+    j.P = P; j.recs = recs; j.nrec = nrec; j.rec_ids = rec_ids; j.vs = vrl_soa; j.nvrl = nvrl;
+    j.pc = particle_count; j.domain = domain; j.out = out_rgb; j.R = R_rows;
+    if (R_rows) memset(R_rows, 0, sizeof(float) * 2 * (size_t)nrec * nvrl);
+    return run_jobs(&j, brute_worker, nrec, nthreads);
+}
+
+uint64_t alvrl_o_gather_clustered(const alvrl_o_params *P, const float *recs, uint32_t nrec,
+                                  const uint32_t *rec_ids, const uint32_t *slice_of_rec,
+                                  const float *vrl_soa, uint32_t nvrl, uint64_t particle_count,
+                                  const uint32_t *slice_off, const uint32_t *reps, const float *weights,
+                                  const uint32_t *fb_reps, const float *fb_weights, uint32_t n_fb,
+                                  float *out_rgb, int nthreads)
+{
+    gjob j;
+    memset(&j, 0, sizeof(j));
+    j.P = P; j.recs = recs; j.nrec = nrec; j.rec_ids = rec_ids; j.vs = vrl_soa; j.nvrl = nvrl;
+    j.pc = particle_count; j.domain = ALVRL_O_DOM_GATHER; j.out = out_rgb;
+    j.slice_of_rec = slice_of_rec; j.slice_off = slice_off; j.reps = reps; j.weights = weights;
+    j.fb_reps = fb_reps; j.fb_weights = fb_weights; j.n_fb = n_fb;
+    return run_jobs(&j, clustered_worker, nrec, nthreads);
+}
+
+/* ===================================================================== */
+/*  Smoke-box scene harness                                                */
+/* ===================================================================== */
+void alvrl_o_scene_default(alvrl_o_scene *s, int width, int height)
+{
+    /* BASELINE.md "homogeneous smoke box" */
+    memset(s, 0, sizeof(*s));
+    s->cam_origin[0] = 0; s->cam_origin[1] = 0; s->cam_origin[2] = -0.9f;
+    s->cam_target[0] = 0; s->cam_target[1] = 0; s->cam_target[2] = 1.0f;
+    s->cam_up[0] = 0; s->cam_up[1] = 1; s->cam_up[2] = 0;
+    s->fov_x_deg = 60.0f;
+    s->width = width; s->height = height;
+    for (int i = 0; i < 3; i++) {
+        s->box_min[i] = -1.0f; s->box_max[i] = 1.0f;
+        s->albedo[i] = 0.5f;
+        s->light_intensity[i] = 10.0f;
+    }
+    s->light_pos[0] = 0; s->light_pos[1] = 0.8f; s->light_pos[2] = 0;
+}
+
+/* Perspective pinhole with Mitsuba's conventions (perspective.cpp:126-155,
+ * 247-269; Transform::lookAt): camera-space x = 'left', y = up, z = forward,
+ * sample (0,0) = upper-left.  Evaluated analytically in float. */
+void alvrl_o_camera_ray(const alvrl_o_scene *s, float px, float py, float o[3], float d[3])
+{
+    v3 org = ld3(s->cam_origin), tgt = ld3(s->cam_target), up = ld3(s->cam_up);
+    v3 fwd = nrm(sub(tgt, org));
+    v3 left = nrm(cross(up, fwd));
+    v3 nup = cross(fwd, left);
+    float aspect = (float)s->width / (float)s->height;
+    float tanh_ = tanf(0.5f * s->fov_x_deg * (float)(M_PI / 180.0));
+    float sx = px * (1.0f / (float)s->width);
+    float sy = py * (1.0f / (float)s->height);
+    float xc = (1.0f - 2.0f * sx) * tanh_;
+    float yc = ((1.0f - 2.0f * sy) / aspect) * tanh_;
+    v3 dc = nrm(mk(xc, yc, 1.0f));
+    v3 dw = mk(left.x * dc.x + nup.x * dc.y + fwd.x * dc.z,
+               left.y * dc.x + nup.y * dc.y + fwd.y * dc.z,
+               left.z * dc.x + nup.z * dc.y + fwd.z * dc.z);
+    o[0] = org.x; o[1] = org.y; o[2] = org.z;
+    d[0] = dw.x; d[1] = dw.y; d[2] = dw.z;
+}
+
+/* Ray / inner-box-wall intersection from inside the box.  Returns t and the
+ * inward wall normal (the walls' BSDF is one-sided diffuse facing inward). */
+static float box_hit(const alvrl_o_scene *s, v3 o, v3 d, v3 *n)
+{
+    float best = INFINITY;
+    int axis = -1;
+    float oo[3] = { o.x, o.y, o.z }, dd[3] = { d.x, d.y, d.z };
+    for (int a = 0; a < 3; a++) {
+        float t;
+        if (dd[a] > 0) t = (s->box_max[a] - oo[a]) / dd[a];
+        else if (dd[a] < 0) t = (s->box_min[a] - oo[a]) / dd[a];
+        else continue;
+        if (t < best) { best = t; axis = a; }
+    }
+    float nn[3] = { 0, 0, 0 };
+    if (axis >= 0) nn[axis] = dd[axis] > 0 ? -1.0f : 1.0f;
+    *n = mk(nn[0], nn[1], nn[2]);
+    return best;
+}
+
+void alvrl_o_make_record(const alvrl_o_scene *s, int medium_scatters, int x, int y, float *rec)
+{
+    float o[3], d[3];
+    alvrl_o_camera_ray(s, (float)x + 0.5f, (float)y + 0.5f, o, d);
+    v3 O = ld3(o), D = ld3(d), n;
+    float t = box_hit(s, O, D, &n);
+    v3 p = add(O, scl(D, t));
+    uint32_t flags = 0;
+    if (isfinite(t)) flags |= ALVRL_O_FLAG_HIT | ALVRL_O_FLAG_SMOOTH;
+    if (medium_scatters) flags |= ALVRL_O_FLAG_MEDIUM;
+    rec[0] = O.x; rec[1] = O.y; rec[2] = O.z;
+    rec[3] = D.x; rec[4] = D.y; rec[5] = D.z;
+    rec[6] = p.x; rec[7] = p.y; rec[8] = p.z;
+    rec[9] = n.x; rec[10] = n.y; rec[11] = n.z;
+    rec[12] = s->albedo[0]; rec[13] = s->albedo[1]; rec[14] = s->albedo[2];
+    memcpy(&rec[15], &flags, 4);
+}
+
+void alvrl_o_make_records(const alvrl_o_scene *s, int medium_scatters, float *recs)
+{
+    for (int y = 0; y < s->height; y++)
+        for (int x = 0; x < s->width; x++)
+            alvrl_o_make_record(s, medium_scatters, x, y,
+                                recs + ((size_t)y * s->width + x) * ALVRL_O_REC_WORDS);
+}
+
+/* ===================================================================== */
+/*  VRL tracer (vrlTracer.h:13-230) in the smoke box                       */
+/* ===================================================================== */
+/* warp::squareToUniformSphere, src/libcore/warp.cpp:25-31 */
+static v3 uniform_sphere(float sx, float sy)
+{
+    float z = 1.0f - 2.0f * sy;
+    float r = safe_sqrt(1.0f - z * z);
+    float theta = (float)(2.0f * M_PI * sx);
+    float sp = sinf(theta), cp = cosf(theta);
+    return mk(r * cp, r * sp, z);
+}
+
+/* warp::squareToUniformDiskConcentric + squareToCosineHemisphere (warp.cpp:43-52, 81-102) */
+static v3 cosine_hemisphere(float sx, float sy)
+{
+    float r1 = 2.0f * sx - 1.0f;
+    float r2 = 2.0f * sy - 1.0f;
+    float phi, r;
+    if (r1 == 0 && r2 == 0) { r = phi = 0; }
+    else if (r1 * r1 > r2 * r2) { r = r1; phi = (float)((M_PI / 4.0f) * (r2 / r1)); }
+    else { r = r2; phi = (float)((M_PI / 2.0f) - (r1 / r2) * (M_PI / 4.0f)); }
+    float sp = sinf(phi), cp = cosf(phi);
+    float px = r * cp, py = r * sp;
+    float z = safe_sqrt(1.0f - px * px - py * py);
+    if (z == 0) z = 1e-10f;
+    return mk(px, py, z);
+}
+
+/* coordinateSystem, src/libcore/util.cpp:592-601 (Frame(n), frame.h:55-57) */
+static void frame_of(v3 a, v3 *b, v3 *c)
+{
+    if (fabsf(a.x) > fabsf(a.y)) {
+        float invLen = 1.0f / sqrtf(a.x * a.x + a.z * a.z);
+        *c = mk(a.z * invLen, 0.0f, -a.x * invLen);
+    } else {
+        float invLen = 1.0f / sqrtf(a.y * a.y + a.z * a.z);
+        *c = mk(0.0f, a.z * invLen, -a.y * invLen);
+    }
+    *b = cross(*c, a);
+}
+
+typedef struct {
+    float *soa; uint32_t cap, n;
+    v3 start; float power[3];
+    int sigma_s_zero;
+} vrl_sink;
+
+/* vrlVector::put filter (VRL.h:148-158) */
+static void vrl_put(vrl_sink *k, v3 end)
+{
+    if (k->sigma_s_zero) return;
+    if (k->power[0] == 0 && k->power[1] == 0 && k->power[2] == 0) return;
+    if (dist(k->start, end) == 0) return;
+    if (k->n >= k->cap) return;
+    uint32_t i = k->n++, c = k->cap;
+    k->soa[0 * c + i] = k->start.x; k->soa[1 * c + i] = k->start.y; k->soa[2 * c + i] = k->start.z;
+    k->soa[3 * c + i] = end.x; k->soa[4 * c + i] = end.y; k->soa[5 * c + i] = end.z;
+    k->soa[6 * c + i] = k->power[0]; k->soa[7 * c + i] = k->power[1]; k->soa[8 * c + i] = k->power[2];
+}
+
+/* vrlTracer::endCurrentVrl (vrlTracer.h:83-89) */
+static void end_current(vrl_sink *k, v3 p)
+{
+    if (dist(k->start, p) == 0) return;
+    vrl_put(k, p);
+}
+
+static void trace_particle(const alvrl_o_scene *s, const alvrl_o_medium *m, seq_sampler *smp,
+                           int short_vrls, int max_depth, int rr_depth, vrl_sink *k)
+{
+    /* sampleEmitterPosition (scene.cpp:958-974) + PointEmitter::samplePosition (point.cpp:81-89) */
+    (void)seq_next(smp); (void)seq_next(smp);
+    float power[3];
+    for (int i = 0; i < 3; i++) power[i] = s->light_intensity[i] * (float)(4 * M_PI);
+    /* PointEmitter::sampleDirection (point.cpp:99-106) */
+    float dx = seq_next(smp), dy = seq_next(smp);
+    v3 dir = uniform_sphere(dx, dy);
+    if (power[0] == 0 && power[1] == 0 && power[2] == 0) return;
+    /* handleEmission: m_vrls->nextParticle() is counted by the caller */
+    v3 o = ld3(s->light_pos);
+    k->start = o;
+    for (int i = 0; i < 3; i++) k->power[i] = power[i];
+
+    int depth = 1;
+    float thr[3] = { 1, 1, 1 };
+    float eta = 1.0f;
+    while (!(thr[0] == 0 && thr[1] == 0 && thr[2] == 0) && (depth <= max_depth || max_depth < 0)) {
+        v3 n;
+        float its_t = box_hit(s, o, dir, &n);
+        int its_valid = isfinite(its_t);
+        /* HomogeneousMedium::sampleDistance (homogeneous.cpp:275-352), balance */
+        float rnd = seq_next(smp), sampled;
+        float w = m->sampling_weight;
+        if (rnd < w) {
+            rnd /= w;
+            int ch = (int)(seq_next(smp) * 3);
+            if (ch > 2) ch = 2;
+            sampled = -fastlog(1 - rnd) / m->sigma_t[ch];
+        } else {
+            sampled = INFINITY;
+        }
+        float distSurf = its_t - 0.0f;
+        int success = 1;
+        v3 mp = o;
+        if (sampled < distSurf) {
+            float mt = sampled + 0.0f;
+            mp = add(o, scl(dir, mt));
+            if (mp.x == o.x && mp.y == o.y && mp.z == o.z) success = 0;
+        } else {
+            sampled = distSurf;
+            success = 0;
+        }
+        float pf = 0, ps = 0;
+        for (int i = 0; i < 3; i++) {
+            float tmp = fastexp(-m->sigma_t[i] * sampled);
+            pf += tmp;
+            ps += m->sigma_t[i] * tmp;
+        }
+        pf /= 3; ps /= 3;
+        float mtr[3];
+        for (int i = 0; i < 3; i++) mtr[i] = fastexp(m->sigma_t[i] * (-sampled));
+        ps = ps * w;
+        pf = w * pf + (1 - w);
+        {
+            float mx = mtr[0] > mtr[1] ? mtr[0] : mtr[1];
+            mx = mx > mtr[2] ? mx : mtr[2];
+            if (mx < 1e-20f) mtr[0] = mtr[1] = mtr[2] = 0;
+        }
+        if (success) {
+            /* medium interaction (vrlTracer.h:143-172) */
+            float rps = 1.0f / ps;
+            for (int i = 0; i < 3; i++) thr[i] *= mtr[i] * m->sigma_s[i] * rps;
+            float px_ = seq_next(smp), py_ = seq_next(smp);
+            v3 wo = uniform_sphere(px_, py_);   /* isotropic phase sample: weight 1 */
+            v3 endPoint = short_vrls ? mp : add(o, scl(dir, its_t));
+            end_current(k, endPoint);
+            k->start = mp;
+            for (int i = 0; i < 3; i++) k->power[i] = thr[i] * power[i];
+            o = mp; dir = wo;
+        } else if (its_valid) {
+            /* surface interaction (vrlTracer.h:173-213) */
+            float rpf = 1.0f / pf;
+            for (int i = 0; i < 3; i++) thr[i] *= mtr[i] * rpf;
+            v3 p = add(o, scl(dir, its_t));
+            v3 fs, ft;
+            frame_of(n, &fs, &ft);
+            v3 mwi = neg(dir);
+            float cos_wi = dot(mwi, n);       /* Frame::cosTheta(toLocal(-ray.d)) */
+            float bx = seq_next(smp), by = seq_next(smp);
+            float bw[3] = { 0, 0, 0 };
+            v3 wol = mk(0, 0, 0);
+            if (!(cos_wi <= 0)) {
+                wol = cosine_hemisphere(bx, by);
+                for (int i = 0; i < 3; i++) bw[i] = s->albedo[i];
+            }
+            if (bw[0] == 0 && bw[1] == 0 && bw[2] == 0) { end_current(k, p); break; }
+            v3 wo = add(add(scl(fs, wol.x), scl(ft, wol.y)), scl(n, wol.z));
+            float wiDotGeoN = dot(n, mwi), woDotGeoN = dot(n, wo);
+            if (wiDotGeoN * cos_wi <= 0 || woDotGeoN * wol.z <= 0) { end_current(k, p); break; }
+            for (int i = 0; i < 3; i++) thr[i] *= bw[i];
+            end_current(k, p);
+            k->start = p;
+            for (int i = 0; i < 3; i++) k->power[i] = thr[i] * power[i];
+            o = p; dir = wo;
+        } else {
+            break;
+        }
+        if (depth++ >= rr_depth) {
+            float mx = thr[0] > thr[1] ? thr[0] : thr[1];
+            mx = mx > thr[2] ? mx : thr[2];
+            float q = mx * eta * eta;
+            if (q > 0.95f) q = 0.95f;
+            if (seq_next(smp) >= q) break;
+            float rq = 1.0f / q;
+            for (int i = 0; i < 3; i++) thr[i] *= rq;
+        }
+    }
+}
+
+uint32_t alvrl_o_trace_vrls(const alvrl_o_scene *s, const alvrl_o_medium *m, uint32_t seed,
+                            uint32_t pass, uint32_t target, int short_vrls, int max_depth,
+                            int rr_depth, float *vrl_soa, uint32_t cap, uint64_t *particles)
+{
+    vrl_sink k;
+    memset(&k, 0, sizeof(k));
+    k.soa = vrl_soa; k.cap = cap; k.n = 0;
+    k.sigma_s_zero = (m->sigma_s[0] == 0 && m->sigma_s[1] == 0 && m->sigma_s[2] == 0);
+    uint64_t p = 0;
+    while (k.n < target && k.n < cap) {
+        seq_sampler smp;
+        seq_init(&smp, seed, pass, ALVRL_O_DOM_TRACER, (uint32_t)p, (uint32_t)(p >> 32), 0);
+        p++;   /* handleEmission -> nextParticle() (the point light always emits) */
+        trace_particle(s, m, &smp, short_vrls, max_depth, rr_depth, &k);
+        if (k.sigma_s_zero && p > 1000000) break;
+    }
+    if (particles) *particles = p;
+    return k.n;
+}

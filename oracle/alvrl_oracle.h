@@ -1,0 +1,136 @@
+/*
+ * alvrl_oracle.h -- CPU restatement of the ALVRL hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in the product (mitsuba-alvrl_amd/,
+ * libalvrl.so) may include, link or call this code.  It is imported only by
+ * tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg, and there
+ * only as the checker / the timed CPU baseline.
+ *
+ * What it restates (reference = neodyme06/mitsuba-ALVRL, paths relative to
+ * the reference root):
+ *   - integrateVRL + samplers   src/integrators/vrl/vrlIntegrator.cpp:603-1032
+ *   - brute / clustered gather  src/integrators/vrl/vrlIntegrator.cpp:542-599, 792-825
+ *   - R rows                    src/integrators/vrl/vrlIntegrator.cpp:527-539, 1038-1083
+ *   - homogeneous medium eval   src/medium/homogeneous.cpp:266-273, 354-396
+ *   - phase eval                src/phase/isotropic.cpp:76-78, src/phase/hg.cpp:107-110
+ *   - diffuse BSDF eval         src/bsdfs/diffuse.cpp:110-118
+ *   - shadow transmittance      src/librender/scene.cpp:619-679 (convex container)
+ *   - VRL tracer                src/integrators/vrl/vrlTracer.h:13-230
+ *   - LightSlice preprocessing  src/integrators/vrl/Preprocessor.cpp (whole file)
+ *
+ * Parity status: PARITY UNPINNED for the VRL / LightSlice maths.  The
+ * reference holds no golden vectors, known-answer tests or fixtures for this
+ * path and it cannot be compiled here (no Boost / Xerces /
+ * OpenEXR / SCons).  The only pinned component is the counter
+ * RNG (Philox4x32-10, checked against the Random123 published known-answer
+ * vectors in tests/test_oracle.py).
+ *
+ * Only intended semantic deviation from the reference: the SFMT sampler seeded
+ * from /dev/urandom (src/libcore/random.cpp:473-489) is replaced by a
+ * counter-based Philox4x32-10 stream, keyed so that results do not depend on
+ * thread count.  Uniform floats are built exactly like Random::nextFloat
+ * (src/libcore/random.cpp:630-639): 23 random mantissa bits in [1,2) minus 1.
+ */
+#ifndef ALVRL_ORACLE_H
+#define ALVRL_ORACLE_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- counter RNG domains (word 3 of the Philox counter, high byte) ---- */
+#define ALVRL_O_DOM_GATHER  1u   /* render gather (getClusteredVrlContributions / getVRLContributions) */
+#define ALVRL_O_DOM_RBUILD  2u   /* R rows (Rbuilder::run) */
+#define ALVRL_O_DOM_TRACER  3u   /* vrlTracer particles */
+#define ALVRL_O_DOM_REPS    4u   /* Slice::sampleRepresentativePixels */
+#define ALVRL_O_DOM_CLUSTER 5u   /* Clustering split / sampleRepresentatives */
+
+void alvrl_o_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
+float alvrl_o_u01(uint32_t bits);
+
+/* Homogeneous medium with the 'balance' strategy (homogeneous.cpp:156-184). */
+typedef struct {
+    float sigma_s[3];
+    float sigma_a[3];
+    float sigma_t[3];
+    float sampling_weight;   /* m_mediumSamplingWeight after the auto rule */
+    int   phase_type;        /* 0 = isotropic, 1 = Henyey-Greenstein */
+    float phase_g;
+} alvrl_o_medium;
+
+void alvrl_o_medium_init(alvrl_o_medium *m, const float sigma_s[3], const float sigma_a[3],
+                         float sampling_weight /* -1 = auto */, int phase_type, float g);
+
+typedef struct {
+    alvrl_o_medium medium;
+    int vol_vol_samples;     /* volVolSamples,  vrlIntegrator.cpp:148 */
+    int vol_surf_samples;    /* volSurfSamples, vrlIntegrator.cpp:153 */
+    int short_vrls;          /* shortVrls,      vrlIntegrator.cpp:135 */
+    uint32_t seed;
+    uint32_t pass;
+} alvrl_o_params;
+
+/* Gather record ("eye segment"): 16 x 32-bit words.
+ *   [0..2] E   eye ray origin           [3..5] d  eye ray direction
+ *   [6..8] p   its.p (surface hit)      [9..11] n shading normal
+ *   [12..14] diffuse reflectance        [15] flags (uint32)          */
+#define ALVRL_O_REC_WORDS 16
+#define ALVRL_O_FLAG_HIT     1u   /* rRec.its.isValid() */
+#define ALVRL_O_FLAG_SMOOTH  2u   /* bsdf->getType() & BSDF::ESmooth */
+#define ALVRL_O_FLAG_MEDIUM  4u   /* eye medium present and scattering */
+
+/* VRL set: SoA, 9 arrays of n floats: sx sy sz ex ey ez pr pg pb (VRL.h:89-96). */
+
+/* One integrateVRL(ray, rRec, vrl, nVV, nVS, &contrib, &variance) evaluation. */
+void alvrl_o_integrate_vrl(const alvrl_o_params *P, const float *rec, uint32_t rec_id,
+                           const float *vrl_soa, uint32_t nvrl, uint32_t vrl_id,
+                           uint32_t domain, float out_rgb[3], float *contrib, float *variance);
+
+/* Brute-force gather (getVRLContributions): out_rgb[3*nrec]; optional R rows
+ * R[r*nvrl + v] = (mean, var) as float pairs.  Returns # integrateVRL calls. */
+uint64_t alvrl_o_gather_brute(const alvrl_o_params *P, const float *recs, uint32_t nrec,
+                              const uint32_t *rec_ids, const float *vrl_soa, uint32_t nvrl,
+                              uint64_t particle_count, uint32_t domain,
+                              float *out_rgb, float *R_rows, int nthreads);
+
+/* Clustered gather (getClusteredVrlContributions).  slice_of_rec[r] indexes
+ * the CSR (slice_off / reps / weights); UINT32_MAX selects the fallback list. */
+uint64_t alvrl_o_gather_clustered(const alvrl_o_params *P, const float *recs, uint32_t nrec,
+                                  const uint32_t *rec_ids, const uint32_t *slice_of_rec,
+                                  const float *vrl_soa, uint32_t nvrl, uint64_t particle_count,
+                                  const uint32_t *slice_off, const uint32_t *reps, const float *weights,
+                                  const uint32_t *fb_reps, const float *fb_weights, uint32_t n_fb,
+                                  float *out_rgb, int nthreads);
+
+/* ---- smoke-box scene harness (stand-in for Mitsuba's Scene/Sensor/Shape) ---- */
+typedef struct {
+    float cam_origin[3], cam_target[3], cam_up[3];
+    float fov_x_deg;
+    int width, height;
+    float box_min[3], box_max[3];
+    float albedo[3];
+    float light_pos[3];
+    float light_intensity[3];
+} alvrl_o_scene;
+
+void alvrl_o_scene_default(alvrl_o_scene *s, int width, int height);
+/* Eye ray through pixel sample (px, py) (perspective.cpp:247-269 semantics). */
+void alvrl_o_camera_ray(const alvrl_o_scene *s, float px, float py, float o[3], float d[3]);
+/* Records for pixel centres, row-major (rec index = y*W + x). */
+void alvrl_o_make_records(const alvrl_o_scene *s, int medium_scatters, float *recs);
+/* Record of a single pixel centre. */
+void alvrl_o_make_record(const alvrl_o_scene *s, int medium_scatters, int x, int y, float *rec);
+
+/* vrlTracer::randomWalk restatement.  Writes up to max_vrls VRLs (SoA with
+ * capacity cap), returns # VRLs, *particles = particleCount. */
+uint32_t alvrl_o_trace_vrls(const alvrl_o_scene *s, const alvrl_o_medium *m, uint32_t seed,
+                            uint32_t pass, uint32_t target, int short_vrls, int max_depth,
+                            int rr_depth, float *vrl_soa, uint32_t cap, uint64_t *particles);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

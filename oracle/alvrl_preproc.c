@@ -1,0 +1,1116 @@
+/*
+ * alvrl_preproc.c -- CPU restatement of LightSlice preprocessing
+ * (src/integrators/vrl/Preprocessor.cpp).  TEST INFRASTRUCTURE ONLY.
+ *
+ * Third-party arithmetic the reference leans on (not vendored):
+ *  - boost::numeric::ublas vector ops: restated as sequential element loops
+ *    (inner_prod / norm_1 / norm_2 = plain in-order sums, norm_2 unscaled).
+ *  - boost::heap::priority_queue: a std::vector driven by std::push_heap /
+ *    std::pop_heap; restated with libstdc++'s __push_heap / __adjust_heap, and
+ *    its iteration order is the underlying vector order.
+ * Random draws come from Philox streams keyed by (stage, cluster range) so that
+ * refinement does not depend on thread count (the reference clones samplers
+ * per worker thread, Preprocessor.cpp:738, so it has no canonical stream).
+ */
+#include "alvrl_oracle.h"
+#include "alvrl_preproc.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#include <stdio.h>
+
+#define UINT32_T_MAX 0xffffffffu
+#ifndef M_PI
+#define M_PI 3.14159265358979323846
+#endif
+
+/* ---------------------------------------------------------------- RNG -- */
+typedef struct {
+    uint32_t seed, pass, dom, a, b, c, k, blk;
+    uint32_t buf[4];
+} smp_t;
+
+static void smp_init(smp_t *s, uint32_t seed, uint32_t pass, uint32_t dom, uint32_t a,
+                     uint32_t b, uint32_t c)
+{
+    s->seed = seed; s->pass = pass; s->dom = dom; s->a = a; s->b = b; s->c = c;
+    s->k = 0; s->blk = 0xFFFFFFFFu;
+}
+
+static float smp_next(smp_t *s)
+{
+    uint32_t blk = s->k >> 2;
+    if (blk != s->blk) {
+        uint32_t ctr[4] = { s->a, s->b, blk, (s->dom << 24) | (s->c & 0xFFFFFFu) };
+        uint32_t key[2] = { s->seed, s->pass };
+        alvrl_o_philox4x32_10(ctr, key, s->buf);
+        s->blk = blk;
+    }
+    float v = alvrl_o_u01(s->buf[s->k & 3]);
+    s->k++;
+    return v;
+}
+
+/* ---------------------------------------------------- matrix accessor -- */
+/* Local matrix M: rows are global row ids into Rt[v*ld + row] (mean,var). */
+typedef struct {
+    const float *Rt;
+    uint64_t ld;
+    const uint32_t *rows;
+    uint32_t nrows;
+    uint32_t nvrl;
+} mat_t;
+
+static inline float m_mean(const mat_t *M, uint32_t r, uint32_t v)
+{
+    return M->Rt[2 * ((uint64_t)v * M->ld + M->rows[r])];
+}
+static inline float m_var(const mat_t *M, uint32_t r, uint32_t v)
+{
+    return M->Rt[2 * ((uint64_t)v * M->ld + M->rows[r]) + 1];
+}
+
+/* ------------------------------------------- deterministic reductions -- */
+/* Every reduction over the ROWS of a local matrix (uBLAS inner_prod / norm_2,
+ * sequential in the reference source, re-associated by the reference's
+ * -funsafe-math-optimizations build) uses one fixed order that a 64-lane
+ * wavefront evaluates directly: lane l sums rows l, l+64, l+128, ... in
+ * ascending order, then lanes are combined by the halving tree
+ * p[l] += p[l+32] (l<32), p[l] += p[l+16] (l<16), ..., p[0] += p[1].
+ * The device refinement kernel (refine.hip) uses the identical order, which
+ * makes cluster indices bit-exact between the two. */
+#define WS_LANES 64
+static double wsum_d(const double *t, uint32_t R)
+{
+    double p[WS_LANES];
+    for (int l = 0; l < WS_LANES; l++) p[l] = 0.0;
+    for (uint32_t r = 0; r < R; r++) p[r % WS_LANES] = p[r % WS_LANES] + t[r];
+    for (int off = WS_LANES / 2; off >= 1; off >>= 1)
+        for (int l = 0; l < off; l++) p[l] = p[l] + p[l + off];
+    return p[0];
+}
+static float wsum_f(const float *t, uint32_t R)
+{
+    float p[WS_LANES];
+    for (int l = 0; l < WS_LANES; l++) p[l] = 0.0f;
+    for (uint32_t r = 0; r < R; r++) p[r % WS_LANES] = p[r % WS_LANES] + t[r];
+    for (int off = WS_LANES / 2; off >= 1; off >>= 1)
+        for (int l = 0; l < off; l++) p[l] = p[l] + p[l + off];
+    return p[0];
+}
+
+/* Deterministic standard normal from two uniforms (Box-Muller, the maths of
+ * warp::squareToStdNormal, warp.cpp:131-137), evaluated with +,-,*,/,sqrt
+ * only so that host and device agree bit for bit (libm / ocml cos and log
+ * differ in the last ulp).  Returns the x component, as Preprocessor.cpp:619. */
+static double det_log(double x)   /* x in (0, 1] */
+{
+    int e = 0;
+    while (x < 0.70710678118654752440) { x = x * 2.0; e--; }
+    /* log(x) = 2 atanh(z), z = (x-1)/(x+1), |z| <= 0.1716 */
+    double z = (x - 1.0) / (x + 1.0), z2 = z * z, term = z, sum = 0.0;
+    for (int k = 1; k <= 41; k += 2) { sum = sum + term / (double)k; term = term * z2; }
+    return 2.0 * sum + (double)e * 0.69314718055994530942;
+}
+static double det_cos(double phi)  /* phi in [0, 2pi) */
+{
+    const double PI_ = 3.14159265358979323846;
+    double x = phi;
+    if (x > PI_) x = 2.0 * PI_ - x;          /* cos symmetric: x in [0, pi] */
+    double sign = 1.0;
+    if (x > 0.5 * PI_) { x = PI_ - x; sign = -1.0; }   /* x in [0, pi/2] */
+    double x2 = x * x, term = 1.0, sum = 0.0;
+    for (int k = 0; k < 14; k++) { sum = sum + term; term = -term * x2 / (double)((2 * k + 1) * (2 * k + 2)); }
+    return sign * sum;
+}
+float alvrl_o_det_std_normal_x(float sx, float sy)
+{
+    double r = sqrt(-2.0 * det_log(1.0 - (double)sx));
+    double phi = 2.0 * 3.14159265358979323846 * (double)sy;
+    return (float)(det_cos(phi) * r);
+}
+
+/* --------------------------------------------------- heap (libstdc++) -- */
+typedef struct { float uvar, ivar; uint32_t begin, end; } cnode;
+
+static inline int cnode_less(const cnode *a, const cnode *b)
+{
+    /* ClusterNode::operator< (Preprocessor.cpp:292-293) */
+    return a->uvar + a->ivar < b->uvar + b->ivar;
+}
+
+static void c_push_heap_(cnode *first, long hole, long top, cnode value)
+{
+    long parent = (hole - 1) / 2;
+    while (hole > top && cnode_less(&first[parent], &value)) {
+        first[hole] = first[parent];
+        hole = parent;
+        parent = (hole - 1) / 2;
+    }
+    first[hole] = value;
+}
+static void c_adjust_heap(cnode *first, long hole, long len, cnode value)
+{
+    long top = hole, second = hole;
+    while (second < (len - 1) / 2) {
+        second = 2 * (second + 1);
+        if (cnode_less(&first[second], &first[second - 1])) second--;
+        first[hole] = first[second];
+        hole = second;
+    }
+    if ((len & 1) == 0 && second == (len - 2) / 2) {
+        second = 2 * (second + 1);
+        first[hole] = first[second - 1];
+        hole = second - 1;
+    }
+    c_push_heap_(first, hole, top, value);
+}
+
+typedef struct { cnode *v; long n, cap; } cheap;
+static void cheap_push(cheap *h, cnode x)
+{
+    if (h->n == h->cap) { h->cap = h->cap ? 2 * h->cap : 64; h->v = (cnode *)realloc(h->v, sizeof(cnode) * h->cap); }
+    h->v[h->n++] = x;
+    cnode val = h->v[h->n - 1];
+    c_push_heap_(h->v, h->n - 1, 0, val);
+}
+static cnode cheap_pop(cheap *h)
+{
+    cnode top = h->v[0];
+    if (h->n > 1) {
+        long last = h->n - 1;
+        cnode value = h->v[last];
+        h->v[last] = h->v[0];
+        c_adjust_heap(h->v, 0, last, value);
+    }
+    h->n--;
+    return top;
+}
+static void cheap_copy(cheap *dst, const cheap *src)
+{
+    if (dst->cap < src->n) { dst->cap = src->n > 64 ? src->n : 64; dst->v = (cnode *)realloc(dst->v, sizeof(cnode) * dst->cap); }
+    if (src->n) memcpy(dst->v, src->v, sizeof(cnode) * src->n);
+    dst->n = src->n;
+}
+
+/* singleton list with push_front: stored appended, iterated in reverse */
+typedef struct { uint32_t *v; long n, cap; } ulist;
+static void ulist_push_front(ulist *l, uint32_t x)
+{
+    if (l->n == l->cap) { l->cap = l->cap ? 2 * l->cap : 64; l->v = (uint32_t *)realloc(l->v, sizeof(uint32_t) * l->cap); }
+    l->v[l->n++] = x;
+}
+static void ulist_copy(ulist *dst, const ulist *src)
+{
+    if (dst->cap < src->n) { dst->cap = src->n > 64 ? src->n : 64; dst->v = (uint32_t *)realloc(dst->v, sizeof(uint32_t) * dst->cap); }
+    if (src->n) memcpy(dst->v, src->v, sizeof(uint32_t) * src->n);
+    dst->n = src->n;
+}
+
+/* ------------------------------------------------------ Clustering -- */
+typedef struct {
+    mat_t M;
+    const double *locw;
+    uint32_t *vrls;        /* m_vrls */
+    uint32_t nv;           /* size of m_vrls */
+    float *colw;           /* m_columnWeights, indexed by vrl id */
+    float tracingVar, unclIntVar, clUnderVar, clIntVar;
+    float pixelUndersampling, depthCorrection;
+    cheap pq; ulist singles;
+    float sh_clUnderVar, sh_clIntVar;
+    cheap sh_pq; ulist sh_singles;
+    uint32_t seed, pass, stage;
+    int err;
+    /* scratch */
+    double *sum, *Mv, *sumVars, *scr;
+    float *fa, *fb, *fc, *fd;
+} clustering_t;
+
+/* weightedSample, Preprocessor.cpp:1534-1580 */
+static size_t weighted_sample(const float *weights, smp_t *smp, float *prob, size_t begin,
+                              size_t end, const uint32_t *ind, int *err)
+{
+    if (begin >= end) { *err = 1; return begin; }
+    if (end == begin + 1) { if (prob) *prob = 1; return begin; }
+    float weightSum = 0.0f;
+    for (size_t i = begin; i < end; i++) weightSum += weights[ind ? ind[i] : i];
+    float probability;
+    size_t idx;
+    if (weightSum <= 0) {
+        int tries = 0;
+        do {
+            idx = (size_t)((float)begin + smp_next(smp) * (float)(end - begin));
+            if (++tries > 1000) { *err = 1; idx = begin; break; }   /* hang guard, as on the device */
+        } while (idx >= end);
+        probability = (float)(1.0 / (double)(end - begin));
+    } else {
+        float alpha = smp_next(smp) * weightSum;
+        float accum = 0.0f;
+        idx = begin;
+        for (size_t i = begin; i < end; i++) {
+            accum += weights[ind ? ind[i] : i];
+            if (accum >= alpha) { idx = i; break; }
+        }
+        probability = weights[ind ? ind[idx] : idx] / weightSum;
+    }
+    if (prob) *prob = probability;
+    return idx;
+}
+
+/* calculateColumnWeigths, Preprocessor.cpp:985-1008 */
+static int column_weights(const mat_t *M, const double *w, float *colw, double *tmp)
+{
+    for (uint32_t v = 0; v < M->nvrl; v++) {
+        for (uint32_t r = 0; r < M->nrows; r++) {
+            double mean = (double)m_mean(M, r, v);
+            double var = (double)m_var(M, r, v);
+            double x = mean * mean + var;
+            tmp[r] = w[r] * x;
+        }
+        double ip = wsum_d(tmp, M->nrows);
+        colw[v] = (float)sqrt(ip > 0.0 ? ip : 0.0);
+        if (!isfinite(colw[v])) return 1;
+    }
+    float acc = 0.0f;
+    for (uint32_t v = 0; v < M->nvrl; v++) acc += colw[v];
+    float averageWeight = acc / M->nvrl;
+    if (averageWeight == 0) averageWeight = 1.0;
+    for (uint32_t v = 0; v < M->nvrl; v++) colw[v] += averageWeight * 1e-2f;
+    return 0;
+}
+
+/* calculateUnclusteredVariance, Preprocessor.cpp:1022-1048 */
+static int unclustered_variance(const mat_t *M, const double *w, const uint32_t *vb,
+                                const uint32_t *ve, float *tracerVar, float *intVar)
+{
+    uint32_t R = M->nrows;
+    double *mean = (double *)calloc(R, sizeof(double));
+    double *M2 = (double *)calloc(R, sizeof(double));
+    double *sv = (double *)calloc(R, sizeof(double));
+    size_t n = 0;
+    for (const uint32_t *it = vb; it != ve; ++it) {
+        n++;
+        for (uint32_t r = 0; r < R; r++) {
+            sv[r] += (double)m_var(M, r, *it);
+            double x = (double)m_mean(M, r, *it);
+            double delta = x - mean[r];
+            mean[r] += delta / (double)n;
+            M2[r] += delta * (x - mean[r]);
+        }
+    }
+    int rc = 0;
+    if (n <= 1) rc = 1;
+    for (uint32_t r = 0; r < R; r++) sv[r] = w[r] * sv[r];
+    double ipv = wsum_d(sv, R);
+    *intVar = (float)ipv;
+    for (uint32_t r = 0; r < R; r++) M2[r] = w[r] * M2[r];
+    double ipm = wsum_d(M2, R);
+    *tracerVar = (float)(ipm - (double)*intVar);
+    free(mean); free(M2); free(sv);
+    return rc;
+}
+
+/* calculateClusterVariance, Preprocessor.cpp:1058-1120.  'vrls' is walked
+ * forward (step=+1) or backward (step=-1) over n entries. */
+static int cluster_variance(clustering_t *C, const uint32_t *first, long step, uint32_t n_items,
+                            float *inc_u, float *inc_i, float *res_u, float *res_i)
+{
+    const mat_t *M = &C->M;
+    uint32_t R = M->nrows;
+    double *sum = C->sum, *Mv = C->Mv, *sumVars = C->sumVars;
+    for (uint32_t r = 0; r < R; r++) { sum[r] = 0; Mv[r] = 0; sumVars[r] = 0; }
+    double weightSum = 0;
+    if (n_items == 0) return 1;
+    for (uint32_t n = 0; n < n_items; n++) {
+        uint32_t vrl = first[(long)n * step];
+        double weight = (double)C->colw[vrl];
+        if (!isfinite(weight) || weight <= 0) return 1;
+        double newWeightSum = weightSum + weight;
+        double a = (newWeightSum * newWeightSum) / (weightSum * weightSum);
+        double bcoef = (1.0 / weight + 1.0 / weightSum);
+        for (uint32_t r = 0; r < R; r++) {
+            double x = (double)m_mean(M, r, vrl);
+            double tmp = weight * sum[r] - weightSum * x;
+            if (n > 0) Mv[r] = a * Mv[r] + bcoef * (tmp * tmp);
+            sumVars[r] += (double)m_var(M, r, vrl) / weight;
+            sum[r] = sum[r] + x;
+        }
+        weightSum = newWeightSum;
+        if (inc_u) {
+            double *t = C->scr;
+            for (uint32_t r = 0; r < R; r++) t[r] = C->locw[r] * (sumVars[r] * weightSum);
+            double ipi = wsum_d(t, R);
+            if (n == 0) {
+                inc_u[n] = 0;
+            } else {
+                for (uint32_t r = 0; r < R; r++) t[r] = C->locw[r] * (Mv[r] / weightSum);
+                inc_u[n] = (float)wsum_d(t, R);
+            }
+            inc_i[n] = (float)ipi;
+        }
+    }
+    double *t = C->scr;
+    for (uint32_t r = 0; r < R; r++) t[r] = C->locw[r] * (Mv[r] / weightSum);
+    double ipu = wsum_d(t, R);
+    for (uint32_t r = 0; r < R; r++) t[r] = C->locw[r] * (sumVars[r] * weightSum);
+    double ipi = wsum_d(t, R);
+    *res_u = (float)ipu;
+    *res_i = (float)ipi;
+    if (!isfinite(*res_u) || *res_u < 0) return 1;
+    if (!isfinite(*res_i) || *res_i < 0) return 1;
+    return 0;
+}
+
+/* Clustering::addCluster, Preprocessor.cpp:549-579 */
+static void add_cluster(clustering_t *C, uint32_t begin, uint32_t end, float uvar, float ivar)
+{
+    if (end == begin) { C->err = 1; return; }
+    if (end == begin + 1) {
+        ulist_push_front(&C->singles, C->vrls[begin]);
+        if (uvar != 0) C->err = 1;
+        C->clIntVar += ivar;
+    } else {
+        cnode cn = { uvar, ivar, begin, end };
+        cheap_push(&C->pq, cn);
+        C->clUnderVar += uvar;
+        C->clIntVar += ivar;
+    }
+}
+
+static cnode pop_multi(clustering_t *C)
+{
+    cnode cn = cheap_pop(&C->pq);
+    C->clUnderVar -= cn.uvar;
+    C->clIntVar -= cn.ivar;
+    return cn;
+}
+
+static float norm2f(const float *v, uint32_t n, float *scr)
+{
+    for (uint32_t i = 0; i < n; i++) { float u = fabsf(v[i]); scr[i] = u * u; }
+    return sqrtf(wsum_f(scr, n));
+}
+
+typedef struct { float p; uint32_t v; } projpair;
+static int projpair_cmp(const void *a, const void *b)
+{
+    const projpair *x = (const projpair *)a, *y = (const projpair *)b;
+    if (x->p < y->p) return -1;
+    if (y->p < x->p) return 1;
+    return x->v < y->v ? -1 : (x->v > y->v ? 1 : 0);
+}
+
+/* Clustering::split, Preprocessor.cpp:590-684 */
+static int split(clustering_t *C, uint32_t begin, uint32_t end)
+{
+    uint32_t clusterSize = end - begin;
+    if (clusterSize < 2) return 0;
+    const mat_t *M = &C->M;
+    uint32_t R = M->nrows;
+    smp_t smp;
+    smp_init(&smp, C->seed, C->pass, ALVRL_O_DOM_CLUSTER, begin, end, C->stage);
+
+    uint32_t vrl1 = C->vrls[weighted_sample(C->colw, &smp, NULL, begin, end, C->vrls, &C->err)];
+    float weight1 = C->colw[vrl1];
+    C->colw[vrl1] = 0.0f;
+    uint32_t vrl2 = C->vrls[weighted_sample(C->colw, &smp, NULL, begin, end, C->vrls, &C->err)];
+    C->colw[vrl1] = weight1;
+
+    float *direction = C->fa, *c1 = C->fb, *c2 = C->fc;
+    for (uint32_t r = 0; r < R; r++) { c1[r] = m_mean(M, r, vrl1); c2[r] = m_mean(M, r, vrl2); }
+    float vrl1len = norm2f(c1, R, C->fd);
+    float vrl2len = norm2f(c2, R, C->fd);
+    for (uint32_t r = 0; r < R; r++) c2[r] = c2[r] - c1[r];   /* diff */
+    float diffLen = norm2f(c2, R, C->fd);
+    if (vrl1len != 0 && vrl2len != 0 && diffLen != 0) {
+        for (uint32_t r = 0; r < R; r++) direction[r] = c2[r] / diffLen;
+    } else {
+        float nd;
+        int guard = 0;
+        do {
+            for (uint32_t r = 0; r < R; r++) {
+                /* warp::squareToStdNormal(next2D()).x (warp.cpp:131-137) */
+                float sx = smp_next(&smp), sy = smp_next(&smp);
+                direction[r] = alvrl_o_det_std_normal_x(sx, sy);
+            }
+            nd = norm2f(direction, R, C->fd);
+            if (nd == 0 && ++guard > 64) { C->err = 1; nd = 1.0f; }   /* hang guard, as on the device */
+        } while (nd == 0);
+        for (uint32_t r = 0; r < R; r++) direction[r] = direction[r] / nd;
+    }
+
+    projpair *proj = (projpair *)malloc(sizeof(projpair) * clusterSize);
+    for (uint32_t j = begin; j < end; j++) {
+        uint32_t vrl = C->vrls[j];
+        for (uint32_t r = 0; r < R; r++) c1[r] = m_mean(M, r, vrl);
+        float nc = norm2f(c1, R, C->fd);
+        float projection;
+        if (nc == 0) {
+            projection = 0;
+        } else {
+            for (uint32_t r = 0; r < R; r++) C->fd[r] = direction[r] * (c1[r] / nc);
+            projection = wsum_f(C->fd, R);
+        }
+        proj[j - begin].p = projection;
+        proj[j - begin].v = vrl;
+    }
+    qsort(proj, clusterSize, sizeof(projpair), projpair_cmp);
+    for (uint32_t j = begin; j < end; j++) C->vrls[j] = proj[j - begin].v;
+    free(proj);
+
+    float *fsu = (float *)malloc(sizeof(float) * clusterSize * 4);
+    float *fsi = fsu + clusterSize, *feu = fsu + 2 * clusterSize, *fei = fsu + 3 * clusterSize;
+    float v1u, v1i, v2u, v2i;
+    if (cluster_variance(C, C->vrls + begin, 1, clusterSize, fsu, fsi, &v1u, &v1i)) C->err = 1;
+    if (cluster_variance(C, C->vrls + end - 1, -1, clusterSize, feu, fei, &v2u, &v2i)) C->err = 1;
+    float bestVariance = INFINITY;
+    uint32_t bestIndex = UINT32_T_MAX;
+    for (uint32_t i = 1; i < clusterSize; ++i) {
+        float thisVar = fsu[i - 1] + fsi[i - 1] + feu[clusterSize - 1 - i] + fei[clusterSize - 1 - i];
+        if (thisVar < bestVariance) { bestVariance = thisVar; bestIndex = i; }
+    }
+    if (bestIndex == UINT32_T_MAX) { C->err = 1; free(fsu); return 0; }
+    uint32_t splitIndex = begin + bestIndex;
+    add_cluster(C, begin, splitIndex, fsu[bestIndex - 1], fsi[bestIndex - 1]);
+    add_cluster(C, splitIndex, end, feu[clusterSize - 1 - bestIndex], fei[clusterSize - 1 - bestIndex]);
+    free(fsu);
+    return 1;
+}
+
+static uint32_t n_clusters(const clustering_t *C) { return (uint32_t)(C->singles.n + C->pq.n); }
+
+static float unclustered_var(const clustering_t *C) { return C->tracingVar + C->unclIntVar; }
+static float clustered_var(const clustering_t *C) { return C->tracingVar + C->clUnderVar + C->clIntVar; }
+static float convergence_constant(clustering_t *C)
+{
+    float c = ((float)C->M.nvrl * C->pixelUndersampling + (float)n_clusters(C)) * clustered_var(C);
+    if (!isfinite(c) || c <= 0) C->err = 1;
+    return c;
+}
+static float lower_bound(clustering_t *C)
+{
+    float c = ((float)C->M.nvrl * C->pixelUndersampling + (float)n_clusters(C)) * unclustered_var(C);
+    if (!isfinite(c) || c <= 0) C->err = 1;
+    return c;
+}
+
+static void snapshot(clustering_t *C)
+{
+    C->sh_clUnderVar = C->clUnderVar; C->sh_clIntVar = C->clIntVar;
+    cheap_copy(&C->sh_pq, &C->pq); ulist_copy(&C->sh_singles, &C->singles);
+}
+static void restore(clustering_t *C)
+{
+    C->clUnderVar = C->sh_clUnderVar; C->clIntVar = C->sh_clIntVar;
+    cheap_copy(&C->pq, &C->sh_pq); ulist_copy(&C->singles, &C->sh_singles);
+}
+
+/* Clustering ctor, Preprocessor.cpp:301-341 */
+static int clustering_init(clustering_t *C, const mat_t *M, const double *locw,
+                           const uint32_t *init_vrls, const uint32_t *init_off, uint32_t ninit,
+                           float pixelUndersampling, float depthCorrection,
+                           uint32_t seed, uint32_t pass, uint32_t stage)
+{
+    memset(C, 0, sizeof(*C));
+    C->M = *M; C->locw = locw;
+    C->pixelUndersampling = pixelUndersampling; C->depthCorrection = depthCorrection;
+    C->seed = seed; C->pass = pass; C->stage = stage;
+    double n1 = 0.0;
+    for (uint32_t r = 0; r < M->nrows; r++) n1 += fabs(locw[r]);
+    if (fabs((float)n1 - 1) > 1e-3) return 1;
+    if (pixelUndersampling <= 0 || pixelUndersampling > 1) return 1;
+    uint32_t R = M->nrows;
+    C->sum = (double *)calloc(R * 4 + 4, sizeof(double));
+    C->Mv = C->sum + R + 1; C->sumVars = C->Mv + R + 1; C->scr = C->sumVars + R + 1;
+    C->fa = (float *)calloc(R * 4 + 4, sizeof(float));
+    C->fb = C->fa + R + 1; C->fc = C->fb + R + 1; C->fd = C->fc + R + 1;
+    C->colw = (float *)malloc(sizeof(float) * (M->nvrl ? M->nvrl : 1));
+    if (column_weights(M, locw, C->colw, C->sum)) return 1;
+    C->nv = init_off[ninit];
+    C->vrls = (uint32_t *)malloc(sizeof(uint32_t) * (C->nv ? C->nv : 1));
+    memcpy(C->vrls, init_vrls, sizeof(uint32_t) * C->nv);
+    for (uint32_t i = 0; i < ninit; i++) {
+        uint32_t b = init_off[i], e = init_off[i + 1];
+        float u = 0, iv = 0;
+        if (b == e) { C->err = 1; continue; }
+        if (cluster_variance(C, C->vrls + b, 1, e - b, NULL, NULL, &u, &iv)) C->err = 1;
+        add_cluster(C, b, e, u, iv);
+    }
+    if (unclustered_variance(M, locw, C->vrls, C->vrls + C->nv, &C->tracingVar, &C->unclIntVar))
+        C->err = 1;
+    return C->err;
+}
+
+static void clustering_free(clustering_t *C)
+{
+    free(C->sum); free(C->fa); free(C->colw); free(C->vrls);
+    free(C->pq.v); free(C->singles.v); free(C->sh_pq.v); free(C->sh_singles.v);
+}
+
+/* refineFixedDepth, Preprocessor.cpp:387-399 */
+static int refine_fixed(clustering_t *C, float undersampling)
+{
+    uint32_t target = (uint32_t)(0.5 + (double)((float)C->M.nvrl / undersampling));
+    if (n_clusters(C) >= target || C->pq.n <= 0) return 1;
+    while (n_clusters(C) < target && C->pq.n > 0) {
+        cnode cn = pop_multi(C);
+        if (!split(C, cn.begin, cn.end)) C->err = 1;
+        if (C->err) return 0;
+    }
+    return 1;
+}
+
+/* refineAdaptively, Preprocessor.cpp:402-489 */
+static int refine_adaptive(clustering_t *C)
+{
+    float dc = C->depthCorrection;
+    if (C->pq.n <= 0) return 1;
+    if (unclustered_var(C) == 0) return 0;
+    float best = convergence_constant(C);
+    int nsplit = 0, bestN = 0;
+    snapshot(C);
+    while (C->pq.n > 0) {
+        cnode cn = pop_multi(C);
+        if (!split(C, cn.begin, cn.end)) C->err = 1;
+        nsplit++;
+        float curr = convergence_constant(C);
+        if (curr < best) {
+            if (dc == 1) snapshot(C);
+            best = curr;
+            bestN = nsplit;
+        }
+        if (lower_bound(C) >= best) break;
+        if (C->err) return 0;
+    }
+    restore(C);
+    if (dc != 1) {
+        int corrected = (int)(0.5 + dc * bestN);
+        for (int i = 0; i < corrected; i++) {
+            if (C->pq.n == 0) break;
+            cnode cn = pop_multi(C);
+            if (!split(C, cn.begin, cn.end)) C->err = 1;
+        }
+    }
+    return C->err ? 0 : 1;
+}
+
+static int refine(clustering_t *C, float undersampling)
+{
+    if (undersampling <= 0) return refine_adaptive(C);
+    return refine_fixed(C, undersampling);
+}
+
+/* Clustering::sampleRepresentatives, Preprocessor.cpp:354-378 */
+static uint32_t sample_reps(clustering_t *C, uint32_t stage, uint32_t *reps, float *w)
+{
+    uint32_t i = 0;
+    for (long k = C->singles.n - 1; k >= 0; k--) { reps[i] = C->singles.v[k]; w[i] = 1; i++; }
+    for (long k = 0; k < C->pq.n; k++) {
+        const cnode *cn = &C->pq.v[k];
+        smp_t smp;
+        smp_init(&smp, C->seed, C->pass, ALVRL_O_DOM_CLUSTER, cn->begin, cn->end, stage);
+        float prob = 1.0f;
+        size_t j = weighted_sample(C->colw, &smp, &prob, cn->begin, cn->end, C->vrls, &C->err);
+        reps[i] = C->vrls[j];
+        w[i] = 1.0f / prob;
+        i++;
+    }
+    return i;
+}
+
+int alvrl_o_cluster_refine(const float *Rt, uint64_t ld, const uint32_t *rows, uint32_t nrows,
+                           const double *locw, uint32_t nvrl,
+                           const uint32_t *init_vrls, const uint32_t *init_off, uint32_t ninit,
+                           float pixelUndersampling, float undersampling, float depthCorrection,
+                           int do_refine, uint32_t seed, uint32_t pass, uint32_t stage_refine,
+                           uint32_t stage_sample, uint32_t *reps, float *weights, uint32_t *nreps,
+                           int *refined)
+{
+    mat_t M = { Rt, ld, rows, nrows, nvrl };
+    clustering_t C;
+    int rc = clustering_init(&C, &M, locw, init_vrls, init_off, ninit, pixelUndersampling,
+                             depthCorrection, seed, pass, stage_refine);
+    if (rc) { clustering_free(&C); return -1; }
+    int ok = 1;
+    if (do_refine) ok = refine(&C, undersampling);
+    if (refined) *refined = ok;
+    if (ok) *nreps = sample_reps(&C, stage_sample, reps, weights);
+    else *nreps = 0;
+    int err = C.err;
+    clustering_free(&C);
+    return err ? -2 : 0;
+}
+
+/* ===================================================================== */
+/*  Preprocessor: slicing + representatives + localities + clusters         */
+/* ===================================================================== */
+typedef struct { float x, y, z; } p3;
+
+typedef struct {
+    uint32_t minInd, maxInd;
+    float distance;
+    unsigned char dim;
+    float split;
+    p3 posC, dirC;
+} snode;
+
+static inline int snode_less(const snode *a, const snode *b) { return a->distance < b->distance; }
+
+static void s_push_heap_(snode *first, long hole, long top, snode value)
+{
+    long parent = (hole - 1) / 2;
+    while (hole > top && snode_less(&first[parent], &value)) {
+        first[hole] = first[parent];
+        hole = parent;
+        parent = (hole - 1) / 2;
+    }
+    first[hole] = value;
+}
+static void s_adjust_heap(snode *first, long hole, long len, snode value)
+{
+    long top = hole, second = hole;
+    while (second < (len - 1) / 2) {
+        second = 2 * (second + 1);
+        if (snode_less(&first[second], &first[second - 1])) second--;
+        first[hole] = first[second];
+        hole = second;
+    }
+    if ((len & 1) == 0 && second == (len - 2) / 2) {
+        second = 2 * (second + 1);
+        first[hole] = first[second - 1];
+        hole = second - 1;
+    }
+    s_push_heap_(first, hole, top, value);
+}
+
+static float slice_distance(p3 p1, p3 d1, p3 p2, p3 d2)
+{
+    float dx = p1.x - p2.x, dy = p1.y - p2.y, dz = p1.z - p2.z;
+    float ex = d1.x - d2.x, ey = d1.y - d2.y, ez = d1.z - d2.z;
+    return sqrtf((dx * dx + dy * dy + dz * dz) + (ex * ex + ey * ey + ez * ez));
+}
+
+/* findSplitPoint, Preprocessor.cpp:1451-1487 */
+static void find_split_point(p3 mx, p3 mn, unsigned char *dim, float *split, float *extent)
+{
+    float dx = mx.x - mn.x, dy = mx.y - mn.y, dz = mx.z - mn.z;
+    if (dx == 0 && dy == 0 && dz == 0) { *extent = 0; *dim = 0; *split = NAN; return; }
+    if (dx > dy) {
+        if (dx > dz) { *dim = 0; *split = (float)(mn.x + 0.5 * dx); *extent = dx; }
+        else { *dim = 2; *split = (float)(mn.z + 0.5 * dz); *extent = dz; }
+    } else {
+        if (dy > dz) { *dim = 1; *split = (float)(mn.y + 0.5 * dy); *extent = dy; }
+        else { *dim = 2; *split = (float)(mn.z + 0.5 * dz); *extent = dz; }
+    }
+}
+
+static int make_snode(snode *sn, uint32_t minI, uint32_t maxI, const p3 *pos, const p3 *dir,
+                      const uint32_t *idx)
+{
+    sn->minInd = minI; sn->maxInd = maxI;
+    if (minI >= maxI) return 1;
+    if (minI + 1 == maxI) {
+        sn->distance = 0; sn->dim = 0; sn->split = NAN;
+        sn->posC.x = sn->posC.y = sn->posC.z = NAN;
+        sn->dirC = sn->posC;
+        return 0;
+    }
+    p3 mxp = { -INFINITY, -INFINITY, -INFINITY }, mnp = { INFINITY, INFINITY, INFINITY };
+    p3 mxd = mxp, mnd = mnp;
+    for (uint32_t i = minI; i < maxI; i++) {
+        p3 p = pos[idx[i]], d = dir[idx[i]];
+        if (p.x < mnp.x) { mnp.x = p.x; }
+        if (p.y < mnp.y) { mnp.y = p.y; }
+        if (p.z < mnp.z) { mnp.z = p.z; }
+        if (p.x > mxp.x) { mxp.x = p.x; }
+        if (p.y > mxp.y) { mxp.y = p.y; }
+        if (p.z > mxp.z) { mxp.z = p.z; }
+        if (d.x < mnd.x) { mnd.x = d.x; }
+        if (d.y < mnd.y) { mnd.y = d.y; }
+        if (d.z < mnd.z) { mnd.z = d.z; }
+        if (d.x > mxd.x) { mxd.x = d.x; }
+        if (d.y > mxd.y) { mxd.y = d.y; }
+        if (d.z > mxd.z) { mxd.z = d.z; }
+    }
+    sn->distance = slice_distance(mnp, mnd, mxp, mxd);
+    unsigned char dp, dd;
+    float sp, sd, ep, ed;
+    find_split_point(mxp, mnp, &dp, &sp, &ep);
+    find_split_point(mxd, mnd, &dd, &sd, &ed);
+    if (ep == 0 && ed == 0) return 1;
+    if (ep > ed) { sn->dim = dp; sn->split = sp; }
+    else { sn->dim = (unsigned char)(3 + dd); sn->split = sd; }
+    sn->posC.x = mnp.x + 0.5f * (mxp.x - mnp.x);
+    sn->posC.y = mnp.y + 0.5f * (mxp.y - mnp.y);
+    sn->posC.z = mnp.z + 0.5f * (mxp.z - mnp.z);
+    sn->dirC.x = mnd.x + 0.5f * (mxd.x - mnd.x);
+    sn->dirC.y = mnd.y + 0.5f * (mxd.y - mnd.y);
+    sn->dirC.z = mnd.z + 0.5f * (mxd.z - mnd.z);
+    return 0;
+}
+
+static inline int is_larger(p3 p, p3 d, int dim, float split)
+{
+    switch (dim) {
+    case 0: return p.x > split;
+    case 1: return p.y > split;
+    case 2: return p.z > split;
+    case 3: return d.x > split;
+    case 4: return d.y > split;
+    default: return d.z > split;
+    }
+}
+
+struct alvrl_o_prep {
+    alvrl_o_prep_params prm;
+    int W, H;
+    uint32_t nslices;
+    /* slice s: gather points idx[slice_lo[s] .. slice_hi[s]) (pixel ids, column-major) */
+    uint32_t *slice_lo, *slice_hi, *idx;
+    p3 *posC, *dirC;
+    uint32_t *reps_off, *reps_pix;   /* representative pixel ids (column-major id) */
+    float *slice_under;
+    float global_under;
+    /* localities: per slice list of (slice, distance) sorted like std::set<pair> */
+    uint32_t *loc_off, *loc_slice;
+    float *loc_dist;
+};
+
+alvrl_o_prep *alvrl_o_prep_create(const alvrl_o_prep_params *p)
+{
+    alvrl_o_prep *P = (alvrl_o_prep *)calloc(1, sizeof(alvrl_o_prep));
+    P->prm = *p;
+    P->global_under = -1;
+    return P;
+}
+
+void alvrl_o_prep_destroy(alvrl_o_prep *P)
+{
+    if (!P) return;
+    free(P->slice_lo); free(P->slice_hi); free(P->idx); free(P->posC); free(P->dirC);
+    free(P->reps_off); free(P->reps_pix); free(P->slice_under);
+    free(P->loc_off); free(P->loc_slice); free(P->loc_dist);
+    free(P);
+}
+
+/* buildSlices + getSlices + getSlicesPQ, Preprocessor.cpp:1130-1418.
+ * pixel_to_slice has W*H entries indexed y + H*x (vrlIntegrator.cpp:560). */
+int alvrl_o_prep_build_slices(alvrl_o_prep *P, const alvrl_o_scene *s, uint32_t *pixel_to_slice)
+{
+    int W = s->width, H = s->height;
+    uint32_t n = (uint32_t)W * (uint32_t)H;
+    P->W = W; P->H = H;
+    p3 *pos = (p3 *)malloc(sizeof(p3) * n), *dir = (p3 *)malloc(sizeof(p3) * n);
+    float bd[3] = { s->box_max[0] - s->box_min[0], s->box_max[1] - s->box_min[1],
+                    s->box_max[2] - s->box_min[2] };
+    float diag = sqrtf(bd[0] * bd[0] + bd[1] * bd[1] + bd[2] * bd[2]);
+    float directionScale = diag / 8 * P->prm.slice_curvature_factor;
+    int ngood = 0;
+    for (int i = 0; i < W; i++) {
+        for (int j = 0; j < H; j++) {
+            float rec[ALVRL_O_REC_WORDS];
+            alvrl_o_make_record(s, 1, i, j, rec);
+            uint32_t flags;
+            memcpy(&flags, &rec[15], 4);
+            uint32_t k = (uint32_t)i * H + j;
+            if (flags & ALVRL_O_FLAG_HIT) {
+                pos[k].x = rec[6]; pos[k].y = rec[7]; pos[k].z = rec[8];
+                dir[k].x = directionScale * rec[9];
+                dir[k].y = directionScale * rec[10];
+                dir[k].z = directionScale * rec[11];
+                ngood++;
+            } else {
+                pos[k].x = pos[k].y = pos[k].z = NAN;
+                dir[k] = pos[k];
+            }
+        }
+    }
+    uint32_t *idx = (uint32_t *)malloc(sizeof(uint32_t) * n);
+    for (uint32_t i = 0; i < n; i++) { idx[i] = i; pixel_to_slice[i] = UINT32_T_MAX; }
+#define FINITE3(q) (isfinite((q).x) && isfinite((q).y) && isfinite((q).z))
+    uint32_t first = 0;
+    while (first < n && !FINITE3(pos[first])) first++;
+    for (uint32_t i = first + 1; i < n; i++) {
+        if (!FINITE3(pos[i])) { idx[i] = idx[first]; idx[first] = i; first++; }
+    }
+    /* getSlicesPQ */
+    long cap = 2 * (long)P->prm.target_num_slices + 8, hn = 0;
+    snode *heap = (snode *)malloc(sizeof(snode) * cap);
+    int rc = 0;
+    if (first < n) {
+        snode sn;
+        rc |= make_snode(&sn, first, n, pos, dir, idx);
+        heap[hn++] = sn; s_push_heap_(heap, hn - 1, 0, sn);
+        while (hn < (long)P->prm.target_num_slices && heap[0].distance > 0 && !rc) {
+            snode top = heap[0];
+            if (hn > 1) { snode val = heap[hn - 1]; heap[hn - 1] = heap[0]; s_adjust_heap(heap, 0, hn - 1, val); }
+            hn--;
+            size_t lo = top.minInd, hi = top.maxInd - 1;
+            size_t i = lo - 1, j = hi + 1;
+            while (1) {
+                while (1) { i++; if (is_larger(pos[idx[i]], dir[idx[i]], top.dim, top.split) || i == hi) break; }
+                while (1) { j--; if (!is_larger(pos[idx[j]], dir[idx[j]], top.dim, top.split) || j == lo) break; }
+                if (i >= j) break;
+                uint32_t t = idx[i]; idx[i] = idx[j]; idx[j] = t;
+            }
+            snode a, b;
+            rc |= make_snode(&a, top.minInd, (uint32_t)(j + 1), pos, dir, idx);
+            rc |= make_snode(&b, (uint32_t)(j + 1), top.maxInd, pos, dir, idx);
+            if (hn + 2 > cap) { cap *= 2; heap = (snode *)realloc(heap, sizeof(snode) * cap); }
+            heap[hn++] = a; s_push_heap_(heap, hn - 1, 0, a);
+            heap[hn++] = b; s_push_heap_(heap, hn - 1, 0, b);
+        }
+    }
+    P->nslices = (uint32_t)hn;
+    P->slice_lo = (uint32_t *)malloc(sizeof(uint32_t) * (hn + 1));
+    P->slice_hi = (uint32_t *)malloc(sizeof(uint32_t) * (hn + 1));
+    P->posC = (p3 *)malloc(sizeof(p3) * (hn + 1));
+    P->dirC = (p3 *)malloc(sizeof(p3) * (hn + 1));
+    for (long k = 0; k < hn; k++) {
+        P->slice_lo[k] = heap[k].minInd; P->slice_hi[k] = heap[k].maxInd;
+        P->posC[k] = heap[k].posC; P->dirC[k] = heap[k].dirC;
+        for (uint32_t i = heap[k].minInd; i < heap[k].maxInd; i++) pixel_to_slice[idx[i]] = (uint32_t)k;
+    }
+    P->idx = idx;
+    free(heap); free(pos); free(dir);
+    (void)ngood;
+    return rc ? -1 : 0;
+}
+
+uint32_t alvrl_o_prep_num_slices(const alvrl_o_prep *P) { return P->nslices; }
+
+/* Slice::sampleRepresentativePixels (Preprocessor.cpp:66-121), sampleSliceMapping
+ * (:1502-1525) and buildLocalities (:1241-1293).  rep_pix receives pixel ids in
+ * the column-major numbering (id = x*H + y); rep_off has nslices+1 entries. */
+int alvrl_o_prep_sample_slice_mapping(alvrl_o_prep *P, float targetUnder, uint32_t *rep_off,
+                                      uint32_t *rep_pix, uint32_t cap, float *slice_under,
+                                      float *global_under)
+{
+    uint32_t ns = P->nslices;
+    free(P->reps_off); free(P->reps_pix); free(P->slice_under);
+    P->reps_off = (uint32_t *)malloc(sizeof(uint32_t) * (ns + 1));
+    P->reps_pix = (uint32_t *)malloc(sizeof(uint32_t) * (cap ? cap : 1));
+    P->slice_under = (float *)malloc(sizeof(float) * (ns + 1));
+    size_t totalPix = 0, totalRep = 0;
+    uint32_t outn = 0;
+    for (uint32_t s = 0; s < ns; s++) {
+        P->reps_off[s] = outn;
+        size_t np = P->slice_hi[s] - P->slice_lo[s];
+        const uint32_t *gp = P->idx + P->slice_lo[s];
+        size_t target = (size_t)(0.5 + (double)((float)np / targetUnder));
+        if (target < 2) target = np < 2 ? np : 2;
+        smp_t smp;
+        smp_init(&smp, P->prm.seed, P->prm.pass, ALVRL_O_DOM_REPS, s, 0, 0);
+        if (outn + (target < np ? target : np) > cap) return -1;
+        if (np <= target) {
+            for (size_t i = 0; i < np; i++) P->reps_pix[outn++] = gp[i];
+        } else if (np <= 2 * target) {
+            uint32_t *ind = (uint32_t *)malloc(sizeof(uint32_t) * np);
+            for (size_t i = 0; i < np; i++) ind[i] = (uint32_t)i;
+            for (size_t i = np - 1; i > 0; i--) {
+                size_t k = (size_t)((float)(i + 1) * smp_next(&smp));
+                uint32_t t = ind[i]; ind[i] = ind[k]; ind[k] = t;
+            }
+            for (size_t i = 0; i < target; i++) P->reps_pix[outn++] = gp[ind[i]];
+            free(ind);
+        } else {
+            uint32_t *ind = (uint32_t *)malloc(sizeof(uint32_t) * target);
+            size_t n = 0;
+            while (n < target) {
+                int unique;
+                do {
+                    ind[n] = (uint32_t)(smp_next(&smp) * (float)np);
+                    unique = 1;
+                    for (size_t i = 0; i < n; i++) if (ind[i] == ind[n]) { unique = 0; break; }
+                } while (!unique);
+                n++;
+            }
+            for (size_t i = 0; i < target; i++) P->reps_pix[outn++] = gp[ind[i]];
+            free(ind);
+        }
+        size_t nrep = outn - P->reps_off[s];
+        P->slice_under[s] = (float)nrep / (float)np;
+        totalRep += nrep; totalPix += np;
+    }
+    P->reps_off[ns] = outn;
+    /* buildLocalities */
+    free(P->loc_off); free(P->loc_slice); free(P->loc_dist);
+    uint32_t nc = P->prm.neighbour_count;
+    P->loc_off = (uint32_t *)calloc(ns + 1, sizeof(uint32_t));
+    uint32_t per = ns <= nc ? (ns ? ns - 1 : 0) : nc;
+    P->loc_slice = (uint32_t *)malloc(sizeof(uint32_t) * ((size_t)ns * per + 1));
+    P->loc_dist = (float *)malloc(sizeof(float) * ((size_t)ns * per + 1));
+    if (ns <= nc) {
+        for (uint32_t i = 0; i < ns; i++) {
+            P->loc_off[i] = i * per;
+            uint32_t c = 0;
+            for (uint32_t j = 0; j < ns; j++) if (i != j) {
+                P->loc_slice[i * per + c] = j;
+                P->loc_dist[i * per + c] = slice_distance(P->posC[i], P->dirC[i], P->posC[j], P->dirC[j]);
+                c++;
+            }
+        }
+    } else if (nc > 0) {
+        float *dist = (float *)malloc(sizeof(float) * nc);
+        uint32_t *ind = (uint32_t *)calloc(nc, sizeof(uint32_t));
+        uint32_t maxInd = 0;   /* not reset per slice (Preprocessor.cpp:1263) */
+        for (uint32_t i = 0; i < ns; i++) {
+            for (uint32_t j = 0; j < nc; j++) dist[j] = INFINITY;
+            for (uint32_t j = 0; j < ns; j++) {
+                if (i == j) continue;
+                float d = slice_distance(P->posC[i], P->dirC[i], P->posC[j], P->dirC[j]);
+                if (d < dist[maxInd]) {
+                    dist[maxInd] = d; ind[maxInd] = j;
+                    for (uint32_t k = 0; k < nc; k++) if (dist[k] > dist[maxInd]) maxInd = k;
+                }
+            }
+            /* std::set<pair<uint32,Float>> insertion: sort, drop duplicates */
+            P->loc_off[i] = i * per;
+            uint32_t c = 0;
+            for (uint32_t x = 0; x < nc; x++) {
+                uint32_t sl = ind[x]; float dd = dist[x];
+                uint32_t pos = c, dup = 0;
+                for (uint32_t q = 0; q < c; q++) {
+                    uint32_t qs = P->loc_slice[i * per + q]; float qd = P->loc_dist[i * per + q];
+                    if (qs == sl && qd == dd) { dup = 1; break; }
+                }
+                if (dup) continue;
+                while (pos > 0) {
+                    uint32_t qs = P->loc_slice[i * per + pos - 1]; float qd = P->loc_dist[i * per + pos - 1];
+                    if (qs < sl || (qs == sl && qd < dd)) break;
+                    P->loc_slice[i * per + pos] = qs; P->loc_dist[i * per + pos] = qd;
+                    pos--;
+                }
+                P->loc_slice[i * per + pos] = sl; P->loc_dist[i * per + pos] = dd;
+                c++;
+            }
+            if (c != per) return -3;
+        }
+        free(dist); free(ind);
+    }
+    P->loc_off[ns] = ns * per;
+    P->global_under = (float)totalRep / (float)totalPix;
+    memcpy(rep_off, P->reps_off, sizeof(uint32_t) * (ns + 1));
+    memcpy(rep_pix, P->reps_pix, sizeof(uint32_t) * outn);
+    if (slice_under) memcpy(slice_under, P->slice_under, sizeof(float) * ns);
+    if (global_under) *global_under = P->global_under;
+    return 0;
+}
+
+/* getLocalMatrix, Preprocessor.cpp:779-827: rows (global row ids) + weights. */
+static uint32_t local_matrix(const alvrl_o_prep *P, uint32_t i, uint32_t *rows, double *w)
+{
+    uint32_t n = 0;
+    uint32_t r0 = P->reps_off[i], r1 = P->reps_off[i + 1];
+    for (uint32_t r = r0; r < r1; r++) rows[n++] = r;
+    uint32_t ni = r1 - r0;
+    if (P->prm.neighbour_weight <= 0) {
+        for (uint32_t k = 0; k < ni; k++) w[k] = 1.0 / (double)ni;
+        return n;
+    }
+    uint32_t lo = P->loc_off[i], hi = P->loc_off[i + 1];
+    float *nw = (float *)malloc(sizeof(float) * (hi - lo + 1));
+    float summed = 0;
+    for (uint32_t q = lo; q < hi; q++) {
+        uint32_t sl = P->loc_slice[q];
+        for (uint32_t r = P->reps_off[sl]; r < P->reps_off[sl + 1]; r++) rows[n++] = r;
+        nw[q - lo] = (float)(1.0 / (double)P->loc_dist[q]);
+        summed += nw[q - lo];
+    }
+    float nwgt = P->prm.neighbour_weight;
+    float sliceWeight = summed * (1 - nwgt) / nwgt;
+    float normalization = 1 / (sliceWeight + summed);
+    uint32_t m = 0;
+    for (uint32_t k = 0; k < ni; k++) w[m++] = (double)(sliceWeight * normalization / (float)ni);
+    for (uint32_t q = lo; q < hi; q++) {
+        uint32_t sl = P->loc_slice[q];
+        uint32_t cnt = P->reps_off[sl + 1] - P->reps_off[sl];
+        for (uint32_t k = 0; k < cnt; k++) w[m++] = (double)(nw[q - lo] * normalization / (float)cnt);
+    }
+    free(nw);
+    return n;
+}
+
+uint32_t alvrl_o_prep_local_rows(const alvrl_o_prep *P, uint32_t slice, uint32_t *rows, double *w)
+{
+    return local_matrix(P, slice, rows, w);
+}
+
+/* cluster() (Preprocessor.cpp:838-898) with globalCluster=false, then
+ * buildClusters (:133-197) + refinePerSlice (:199-252) + refineSlice (:254-283).
+ * Rt is [nvrl][rows_total] (mean,var) pairs, rows in slice-major order.
+ * Outputs: per-slice CSR (slice_off[ns+1], reps, weights), fallback list. */
+int alvrl_o_prep_build_clusters(alvrl_o_prep *P, const float *Rt, uint32_t nvrl,
+                                uint32_t *slice_off, uint32_t *reps, float *weights, uint32_t cap,
+                                uint32_t *gc_reps, float *gc_w, uint32_t *n_gc,
+                                uint32_t *fb_reps, float *fb_w, uint32_t *n_fb)
+{
+    uint32_t ns = P->nslices;
+    uint32_t rows_total = P->reps_off[ns];
+    uint64_t ld = rows_total;
+    /* ---- global cluster (cluster()) on Rflat ---- */
+    uint32_t *all_rows = (uint32_t *)malloc(sizeof(uint32_t) * (rows_total + 1));
+    for (uint32_t r = 0; r < rows_total; r++) all_rows[r] = r;
+    uint32_t *init = (uint32_t *)malloc(sizeof(uint32_t) * (nvrl + 1));
+    uint32_t init_off[3] = { 0, 0, 0 }, ninit = 0;
+    uint32_t nz = 0;
+    for (uint32_t v = 0; v < nvrl; v++) {
+        float sum = 0;
+        for (uint32_t r = 0; r < rows_total; r++) sum += Rt[2 * ((uint64_t)v * ld + r)];
+        if (sum != 0) init[nz++] = v;
+    }
+    uint32_t nzero = 0;
+    if (P->prm.global_cluster) { free(all_rows); free(init); return -10; }   /* not restated */
+    if (nz) { init_off[1] = nz; ninit = 1; }
+    for (uint32_t v = 0; v < nvrl; v++) {
+        float sum = 0;
+        for (uint32_t r = 0; r < rows_total; r++) sum += Rt[2 * ((uint64_t)v * ld + r)];
+        if (sum == 0) init[nz + nzero++] = v;
+    }
+    if (nzero) { init_off[ninit + 1] = nz + nzero; ninit++; }
+    double *dw = (double *)malloc(sizeof(double) * (rows_total + 1));
+    for (uint32_t r = 0; r < rows_total; r++) dw[r] = 1.0 / (double)rows_total;
+    int rc = 0;
+    {
+        mat_t M = { Rt, ld, all_rows, rows_total, nvrl };
+        clustering_t C;
+        if (clustering_init(&C, &M, dw, init, init_off, ninit, P->global_under, 1.0f,
+                            P->prm.seed, P->prm.pass, ALVRL_O_STAGE_FALLBACK_REFINE)) rc = -2;
+        if (!rc) {
+            *n_gc = sample_reps(&C, ALVRL_O_STAGE_GLOBAL_SAMPLE, gc_reps, gc_w);
+            if (!refine(&C, P->prm.fallback_undersampling)) rc = -3;
+            *n_fb = sample_reps(&C, ALVRL_O_STAGE_FALLBACK_SAMPLE, fb_reps, fb_w);
+        }
+        if (C.err) rc = rc ? rc : -4;
+        clustering_free(&C);
+    }
+    if (rc) { free(all_rows); free(init); free(dw); return rc; }
+    /* ---- refinePerSlice ---- */
+    uint32_t *rows = all_rows;
+    double *w = dw;
+    uint32_t out = 0;
+    for (uint32_t s = 0; s < ns; s++) {
+        slice_off[s] = out;
+        uint32_t nr = local_matrix(P, s, rows, w);
+        uint32_t got = 0;
+        int refined = 0;
+        if (out + nvrl > cap) { rc = -5; break; }
+        int e = alvrl_o_cluster_refine(Rt, ld, rows, nr, w, nvrl, init, init_off, ninit,
+                                       P->slice_under[s], P->prm.local_undersampling,
+                                       P->prm.depth_correction, P->prm.local_refinement,
+                                       P->prm.seed, P->prm.pass, ALVRL_O_STAGE_SLICE_REFINE(s),
+                                       ALVRL_O_STAGE_SLICE_SAMPLE(s), reps + out, weights + out,
+                                       &got, &refined);
+        if (e) { rc = -6; break; }
+        if (!refined) {
+            memcpy(reps + out, fb_reps, sizeof(uint32_t) * *n_fb);
+            memcpy(weights + out, fb_w, sizeof(float) * *n_fb);
+            got = *n_fb;
+        }
+        out += got;
+    }
+    slice_off[ns] = out;
+    free(all_rows); free(init); free(dw);
+    return rc;
+}

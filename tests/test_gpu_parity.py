@@ -1,0 +1,268 @@
+"""Parity of the HIP hot path (libalvrl.so, through the C ABI) with the CPU
+restatement (oracle/), on identical inputs and identical counter-RNG streams.
+
+Tolerances (floating point, stated here):
+  * gather / R entries: the device uses ocml expf/atanf/tanf/sinhf/asinhf and
+    contracts a*b+c into FMA; the oracle uses glibc and no contraction.  Per
+    pixel |gpu - cpu| <= 2e-4 * |cpu| + 1e-6 * max|cpu|, and the image RMSE
+    (rms.cpp semantics: gamma 1, absolute, all pixels x RGB) <= 1e-5 * mean.
+  * refinement: cluster representatives and weights must be BIT-IDENTICAL
+    (integer/index work; the kernel is compiled without FMA contraction and
+    uses the oracle's reduction order).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+SEED_VRL = 0x5EED0001
+SEED_RNG = 0xA1B2C3D4
+REL_TOL = 2e-4
+ABS_TOL_FRAC = 1e-6
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def _ctx(medium=None, **kw):
+    import alvrl
+    ctx = alvrl.Context(device=0, seed=SEED_RNG, **kw)
+    ctx.set_medium(medium or alvrl.Medium())
+    return ctx
+
+
+def _scene_inputs(oracle, w, h, nvrl):
+    sc = oracle.scene(w, h)
+    m = oracle.medium()
+    vrls, pc = oracle.trace(sc, m, nvrl, seed=SEED_VRL)
+    recs = oracle.records(sc)
+    return sc, m, vrls, pc, recs
+
+
+def _assert_close(gpu, cpu, what):
+    gpu = np.asarray(gpu, np.float64)
+    cpu = np.asarray(cpu, np.float64)
+    assert gpu.shape == cpu.shape
+    assert np.isfinite(gpu).all(), f"{what}: non-finite device values"
+    scale = np.abs(cpu).max() if cpu.size else 0.0
+    err = np.abs(gpu - cpu)
+    bound = REL_TOL * np.abs(cpu) + ABS_TOL_FRAC * scale
+    rel = err / np.maximum(np.abs(cpu), 1e-30)
+    rmse = float(np.sqrt(np.mean((gpu - cpu) ** 2)))
+    print(f"[{what}] max_rel={rel.max():.3e} median_rel={np.median(rel):.3e} "
+          f"rmse={rmse:.3e} mean={np.abs(cpu).mean():.3e} viol={(err > bound).sum()}/{err.size}")
+    assert (err <= bound).all(), f"{what}: {(err > bound).sum()} entries outside tolerance"
+    assert rmse <= 1e-5 * max(np.abs(cpu).mean(), 1e-30), f"{what}: RMSE {rmse}"
+
+
+def test_gather_brute_small(oracle, gpu_ok):
+    """C1-shaped: 64x64 records x 1000 VRLs, every pixel."""
+    torch = _torch()
+    sc, m, vrls, pc, recs = _scene_inputs(oracle, 64, 64, 1000)
+    P = oracle.params(m, seed=SEED_RNG)
+    cpu, ccnt = oracle.gather_brute(P, recs, vrls, pc)
+    ctx = _ctx()
+    ctx.upload_vrls(vrls, pc)
+    d_recs = torch.from_numpy(recs).cuda()
+    d_out = torch.zeros((recs.shape[0], 3), dtype=torch.float32, device="cuda")
+    ctx.reset_stats()
+    ctx.gather_brute(d_recs, d_out)
+    torch.cuda.synchronize()
+    gpu = d_out.cpu().numpy()
+    _, ren = ctx.stats()
+    assert ren == ccnt == recs.shape[0] * vrls.shape[1]
+    _assert_close(gpu, cpu, "brute 64x64x1k")
+
+
+def test_gather_brute_c2_subset(oracle, gpu_ok):
+    """C2 shape (1024^2, 10k VRLs): a strided subset of pixels, ids = pixel ids."""
+    torch = _torch()
+    sc, m, vrls, pc, recs = _scene_inputs(oracle, 1024, 1024, 10000)
+    ids = np.arange(0, 1024 * 1024, 2053, dtype=np.uint32)
+    sub = recs[ids]
+    P = oracle.params(m, seed=SEED_RNG)
+    cpu, _ = oracle.gather_brute(P, sub, vrls, pc, rec_ids=ids)
+    ctx = _ctx()
+    ctx.upload_vrls(vrls, pc)
+    d_out = torch.zeros((len(ids), 3), dtype=torch.float32, device="cuda")
+    ctx.gather_brute(torch.from_numpy(sub).cuda(), d_out, d_ids=torch.from_numpy(ids.view(np.int32)).cuda())
+    torch.cuda.synchronize()
+    _assert_close(d_out.cpu().numpy(), cpu, "brute c2-subset")
+
+
+def test_gather_host_pointer_variant(oracle, gpu_ok):
+    sc, m, vrls, pc, recs = _scene_inputs(oracle, 32, 32, 500)
+    ctx = _ctx()
+    ctx.upload_vrls(vrls, pc)
+    a = ctx.gather_brute_host(recs)
+    P = oracle.params(m, seed=SEED_RNG)
+    cpu, _ = oracle.gather_brute(P, recs, vrls, pc)
+    _assert_close(a, cpu, "brute host-pointer")
+
+
+def test_gather_deterministic(oracle, gpu_ok):
+    torch = _torch()
+    sc, m, vrls, pc, recs = _scene_inputs(oracle, 64, 64, 2000)
+    ctx = _ctx()
+    ctx.upload_vrls(vrls, pc)
+    d_recs = torch.from_numpy(recs).cuda()
+    outs = []
+    for _ in range(2):
+        d = torch.zeros((recs.shape[0], 3), dtype=torch.float32, device="cuda")
+        ctx.gather_brute(d_recs, d)
+        torch.cuda.synchronize()
+        outs.append(d.cpu().numpy())
+    assert np.array_equal(outs[0].view(np.uint32), outs[1].view(np.uint32))
+
+
+def test_gather_nondefault_samples_and_hg(oracle, gpu_ok):
+    """Generic (runtime sample count) kernel path + HG phase + long VRL flag."""
+    import alvrl
+    torch = _torch()
+    sc = oracle.scene(32, 32)
+    m = oracle.medium(phase_type=1, g=0.4)
+    vrls, pc = oracle.trace(sc, oracle.medium(), 300, seed=SEED_VRL)
+    recs = oracle.records(sc)
+    P = oracle.params(m, nvv=3, nvs=4, short_vrls=0, seed=SEED_RNG)
+    cpu, _ = oracle.gather_brute(P, recs, vrls, pc)
+    ctx = _ctx(alvrl.Medium(phase_type=1, phase_g=0.4), vol_vol_samples=3, vol_surf_samples=4,
+               short_vrls=False)
+    ctx.upload_vrls(vrls, pc)
+    d = torch.zeros((recs.shape[0], 3), dtype=torch.float32, device="cuda")
+    ctx.gather_brute(torch.from_numpy(recs).cuda(), d)
+    torch.cuda.synchronize()
+    _assert_close(d.cpu().numpy(), cpu, "brute nvv3 nvs4 hg")
+
+
+def test_build_R_parity(oracle, gpu_ok):
+    """Rbuilder::run rows (mean, var) against the oracle's R rows."""
+    torch = _torch()
+    sc, m, vrls, pc, recs = _scene_inputs(oracle, 128, 128, 1500)
+    rows = np.arange(0, 128 * 128, 61, dtype=np.uint32)
+    sub = recs[rows]
+    P = oracle.params(m, seed=SEED_RNG)
+    _, Rcpu, cnt = oracle.gather_brute(P, sub, vrls, pc, rec_ids=rows, domain=2, want_R=True)
+    ctx = _ctx()
+    ctx.upload_vrls(vrls, pc)
+    nr, nv = len(rows), vrls.shape[1]
+    d_Rt = torch.zeros((nv, nr, 2), dtype=torch.float32, device="cuda")
+    ctx.reset_stats()
+    ctx.build_R(torch.from_numpy(sub).cuda(), d_Rt, ld=nr, d_ids=torch.from_numpy(rows.view(np.int32)).cuda())
+    torch.cuda.synchronize()
+    Rg = d_Rt.cpu().numpy().transpose(1, 0, 2)
+    pre, _ = ctx.stats()
+    assert pre == cnt
+    _assert_close(Rg[..., 0], Rcpu[..., 0], "R mean")
+    _assert_close(Rg[..., 1], Rcpu[..., 1], "R var")
+
+
+def _refine_case(oracle, w, h, nvrl, nslice_rows, undersampling, torch):
+    sc, m, vrls, pc, recs = _scene_inputs(oracle, w, h, nvrl)
+    rng = np.random.default_rng(7)
+    nrows = sum(nslice_rows)
+    rows_pix = rng.choice(w * h, size=nrows, replace=False).astype(np.uint32)
+    ctx = _ctx()
+    ctx.upload_vrls(vrls, pc)
+    d_Rt = torch.zeros((vrls.shape[1], nrows, 2), dtype=torch.float32, device="cuda")
+    ctx.build_R(torch.from_numpy(recs[rows_pix]).cuda(), d_Rt, ld=nrows,
+                d_ids=torch.from_numpy(rows_pix.view(np.int32)).cuda())
+    torch.cuda.synchronize()
+    Rt = d_Rt.cpu().numpy()
+    nv = vrls.shape[1]
+    colsum = Rt[:, :, 0].sum(axis=1)
+    nz = np.nonzero(colsum != 0)[0].astype(np.uint32)
+    z = np.nonzero(colsum == 0)[0].astype(np.uint32)
+    init = np.concatenate([nz, z])
+    init_off = [0] + ([len(nz)] if len(nz) else []) + ([nv] if len(z) else [])
+    init_off = np.array(init_off, np.uint32)
+    off = np.cumsum([0] + list(nslice_rows))
+    jobs = []
+    for s in range(len(nslice_rows)):
+        r = np.arange(off[s], off[s + 1], dtype=np.uint32)
+        jobs.append(dict(rows=r, locw=np.full(len(r), 1.0 / len(r)), pixel_undersampling=0.25,
+                         undersampling=undersampling, depth_correction=1.0, do_refine=True,
+                         stage_refine=3 + 2 * s, stage_sample=4 + 2 * s))
+    return ctx, d_Rt, Rt, jobs, init, init_off
+
+
+@pytest.mark.parametrize("undersampling", [-1.0, 10.0])
+def test_refine_bit_exact(oracle, gpu_ok, undersampling):
+    """Per-slice Clustering refine + sampleRepresentatives: device == oracle, bit for bit."""
+    torch = _torch()
+    ctx, d_Rt, Rt, jobs, init, init_off = _refine_case(oracle, 96, 96, 1200, [40, 23, 64, 70, 5],
+                                                       undersampling, torch)
+    off, reps, w, refined = ctx.refine(d_Rt, Rt.shape[1], jobs, init, init_off)
+    for s, j in enumerate(jobs):
+        cr, cw, cref = oracle.cluster_refine(Rt, j["rows"], j["locw"], init, init_off,
+                                             j["pixel_undersampling"], undersampling,
+                                             stage_refine=j["stage_refine"],
+                                             stage_sample=j["stage_sample"], seed=SEED_RNG)
+        gr, gw = reps[off[s]:off[s + 1]], w[off[s]:off[s + 1]]
+        print(f"slice {s}: {len(cr)} clusters (cpu) {len(gr)} (gpu) refined={cref}/{refined[s]}")
+        assert bool(refined[s]) == cref
+        assert np.array_equal(gr, cr)
+        assert np.array_equal(gw.view(np.uint32), cw.view(np.uint32))
+
+
+def test_refine_large_cluster_radix_path(oracle, gpu_ok):
+    """Cluster sizes above the LDS bitonic limit exercise the radix-sort path."""
+    torch = _torch()
+    ctx, d_Rt, Rt, jobs, init, init_off = _refine_case(oracle, 96, 96, 6000, [48], 200.0, torch)
+    off, reps, w, refined = ctx.refine(d_Rt, Rt.shape[1], jobs, init, init_off)
+    j = jobs[0]
+    cr, cw, cref = oracle.cluster_refine(Rt, j["rows"], j["locw"], init, init_off,
+                                         j["pixel_undersampling"], 200.0, stage_refine=3,
+                                         stage_sample=4, seed=SEED_RNG)
+    assert np.array_equal(reps, cr)
+    assert np.array_equal(w.view(np.uint32), cw.view(np.uint32))
+
+
+def test_gather_clustered_parity(oracle, gpu_ok):
+    torch = _torch()
+    import alvrl
+    sc, m, vrls, pc, recs = _scene_inputs(oracle, 64, 64, 800)
+    rng = np.random.default_rng(3)
+    ns = 7
+    slice_of = rng.integers(0, ns, size=recs.shape[0]).astype(np.uint32)
+    slice_of[::97] = 0xFFFFFFFF
+    sizes = rng.integers(1, 60, size=ns)
+    slice_off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint32)
+    reps = rng.integers(0, vrls.shape[1], size=slice_off[-1]).astype(np.uint32)
+    wts = rng.uniform(0.5, 20, size=slice_off[-1]).astype(np.float32)
+    fb = rng.choice(vrls.shape[1], 40, replace=False).astype(np.uint32)
+    fbw = rng.uniform(1, 5, size=40).astype(np.float32)
+    P = oracle.params(m, seed=SEED_RNG)
+    cpu, ccnt = oracle.gather_clustered(P, recs, slice_of, vrls, pc, slice_off, reps, wts, fb, fbw)
+    ctx = _ctx()
+    ctx.upload_vrls(vrls, pc)
+    ctx.set_clusters(slice_off, reps, wts, fb, fbw)
+    ctx.reset_stats()
+    gpu = ctx.gather_clustered_host(recs, slice_of)
+    _, ren = ctx.stats()
+    assert ren == ccnt
+    _assert_close(gpu, cpu, "clustered")
+
+
+def test_c2_full_frame_properties(gpu_ok):
+    """Full BASELINE configs[1] frame (1024^2 x 10k): size-independent checks."""
+    torch = _torch()
+    import alvrl
+    from oracle import Oracle
+    o = Oracle()
+    sc = o.scene(1024, 1024)
+    vrls, pc = o.trace(sc, o.medium(), 10000, seed=SEED_VRL)
+    recs = o.records(sc)
+    ctx = _ctx()
+    ctx.upload_vrls(vrls, pc)
+    d_recs = torch.from_numpy(recs).cuda()
+    d = torch.zeros((recs.shape[0], 3), dtype=torch.float32, device="cuda")
+    ctx.reset_stats()
+    ctx.gather_brute(d_recs, d)
+    torch.cuda.synchronize()
+    img = d.cpu().numpy()
+    assert np.isfinite(img).all() and (img >= 0).all()
+    _, ren = ctx.stats()
+    assert ren == recs.shape[0] * vrls.shape[1]
+    print(f"C2 frame: {ctx.last_kernel_ms():.1f} ms, mean {img.mean(0)}")
