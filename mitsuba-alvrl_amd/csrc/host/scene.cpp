@@ -1,0 +1,364 @@
+// scene.cpp -- smoke-box harness and the VRL tracer (see scene.hpp).
+// Compiled with g++ -ffp-contract=off: float semantics identical to the
+// oracle's restatement, so records and VRL sets agree bit for bit with it.
+#include "scene.hpp"
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+#include <string>
+
+namespace alvrl {
+namespace host {
+
+namespace {
+constexpr double kPi = 3.14159265358979323846;
+constexpr uint32_t kDomTracer = 3u;
+
+inline float fastexp(float v) { return (float)std::exp((double)v); }   // math.h:185-199
+inline float fastlog(float v) { return (float)std::log((double)v); }
+inline float safe_sqrt(float v) { return std::sqrt(v > 0.0f ? v : 0.0f); }
+}  // namespace
+
+float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+float length(V3 a) { return std::sqrt(a.x * a.x + a.y * a.y + a.z * a.z); }
+V3 normalize(V3 a) { const float r = 1.0f / length(a); return a * r; }
+V3 cross(V3 a, V3 b) { return v3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
+
+void MediumParams::resolve()
+{
+    for (int i = 0; i < 3; i++) sigma_t[i] = sigma_s[i] + sigma_a[i];
+    float w = sampling_weight;
+    if (w == -1) {
+        for (int i = 0; i < 3; i++) {
+            const float albedo = sigma_s[i] / sigma_t[i];
+            if (albedo > w && sigma_t[i] != 0) w = albedo;
+        }
+        if (w > 0) w = w > 0.5f ? w : 0.5f;
+    }
+    sampling_weight = w;
+}
+
+void SmokeBox::camera_ray(float px, float py, V3* o, V3* d) const
+{
+    const V3 fwd = normalize(cam_target - cam_origin);
+    const V3 left = normalize(cross(cam_up, fwd));
+    const V3 nup = cross(fwd, left);
+    const float aspect = (float)width / (float)height;
+    const float tanh_ = std::tan(0.5f * fov_x_deg * (float)(kPi / 180.0));
+    const float sx = px * (1.0f / (float)width);
+    const float sy = py * (1.0f / (float)height);
+    const float xc = (1.0f - 2.0f * sx) * tanh_;
+    const float yc = ((1.0f - 2.0f * sy) / aspect) * tanh_;
+    const V3 dc = normalize(v3(xc, yc, 1.0f));
+    *o = cam_origin;
+    *d = v3(left.x * dc.x + nup.x * dc.y + fwd.x * dc.z,
+            left.y * dc.x + nup.y * dc.y + fwd.y * dc.z,
+            left.z * dc.x + nup.z * dc.y + fwd.z * dc.z);
+}
+
+float SmokeBox::box_hit(V3 o, V3 d, V3* n) const
+{
+    float best = INFINITY;
+    int axis = -1;
+    const float oo[3] = {o.x, o.y, o.z}, dd[3] = {d.x, d.y, d.z};
+    for (int a = 0; a < 3; a++) {
+        float t;
+        if (dd[a] > 0) t = (box_max[a] - oo[a]) / dd[a];
+        else if (dd[a] < 0) t = (box_min[a] - oo[a]) / dd[a];
+        else continue;
+        if (t < best) { best = t; axis = a; }
+    }
+    float nn[3] = {0.0f, 0.0f, 0.0f};
+    if (axis >= 0) nn[axis] = dd[axis] > 0 ? -1.0f : 1.0f;
+    *n = v3(nn[0], nn[1], nn[2]);
+    return best;
+}
+
+void SmokeBox::make_record(int x, int y, bool medium_scatters, float rec[16]) const
+{
+    V3 O, D, n;
+    camera_ray((float)x + 0.5f, (float)y + 0.5f, &O, &D);   // renderBlock pixel centre, integrator.cpp:243-245
+    const float t = box_hit(O, D, &n);
+    const V3 p = O + D * t;
+    uint32_t flags = 0;
+    if (std::isfinite(t)) flags |= 1u | 2u;
+    if (medium_scatters) flags |= 4u;
+    rec[0] = O.x; rec[1] = O.y; rec[2] = O.z;
+    rec[3] = D.x; rec[4] = D.y; rec[5] = D.z;
+    rec[6] = p.x; rec[7] = p.y; rec[8] = p.z;
+    rec[9] = n.x; rec[10] = n.y; rec[11] = n.z;
+    rec[12] = albedo[0]; rec[13] = albedo[1]; rec[14] = albedo[2];
+    std::memcpy(&rec[15], &flags, 4);
+}
+
+float SmokeBox::scene_diagonal() const
+{
+    const float a = box_max[0] - box_min[0], b = box_max[1] - box_min[1], c = box_max[2] - box_min[2];
+    return std::sqrt(a * a + b * b + c * c);
+}
+
+// ---------------------------------------------------------------- tracer --
+namespace {
+
+void philox(const uint32_t ctr_in[4], const uint32_t key_in[2], uint32_t out[4])
+{
+    uint32_t c0 = ctr_in[0], c1 = ctr_in[1], c2 = ctr_in[2], c3 = ctr_in[3];
+    uint32_t k0 = key_in[0], k1 = key_in[1];
+    for (int r = 0; r < 10; r++) {
+        if (r > 0) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0, n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        c0 = n0; c1 = (uint32_t)p1; c2 = n2; c3 = (uint32_t)p0;
+    }
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+struct Stream {   // Sampler::next1D over the (dom, a, b, c) Philox stream
+    uint32_t seed, pass, dom, a, b, c, k = 0, blk = 0xFFFFFFFFu;
+    uint32_t buf[4];
+    float next()
+    {
+        const uint32_t bl = k >> 2;
+        if (bl != blk) {
+            const uint32_t ctr[4] = {a, b, bl, (dom << 24) | (c & 0xFFFFFFu)};
+            const uint32_t key[2] = {seed, pass};
+            philox(ctr, key, buf);
+            blk = bl;
+        }
+        union { uint32_t u; float f; } x;
+        x.u = (buf[k & 3] >> 9) | 0x3f800000u;   // Random::nextFloat, random.cpp:630-639
+        ++k;
+        return x.f - 1.0f;
+    }
+};
+
+V3 uniform_sphere(float sx, float sy)   // warp.cpp:25-31
+{
+    const float z = 1.0f - 2.0f * sy;
+    const float r = safe_sqrt(1.0f - z * z);
+    const float theta = (float)(2.0f * kPi * sx);
+    return v3(r * std::cos(theta), r * std::sin(theta), z);
+}
+
+V3 cosine_hemisphere(float sx, float sy)   // warp.cpp:43-52, 81-102
+{
+    const float r1 = 2.0f * sx - 1.0f, r2 = 2.0f * sy - 1.0f;
+    float phi, r;
+    if (r1 == 0 && r2 == 0) { r = phi = 0; }
+    else if (r1 * r1 > r2 * r2) { r = r1; phi = (float)((kPi / 4.0f) * (r2 / r1)); }
+    else { r = r2; phi = (float)((kPi / 2.0f) - (r1 / r2) * (kPi / 4.0f)); }
+    const float px = r * std::cos(phi), py = r * std::sin(phi);
+    float z = safe_sqrt(1.0f - px * px - py * py);
+    if (z == 0) z = 1e-10f;
+    return v3(px, py, z);
+}
+
+void frame_of(V3 a, V3* b, V3* c)   // coordinateSystem, util.cpp:592-601
+{
+    if (std::fabs(a.x) > std::fabs(a.y)) {
+        const float invLen = 1.0f / std::sqrt(a.x * a.x + a.z * a.z);
+        *c = v3(a.z * invLen, 0.0f, -a.x * invLen);
+    } else {
+        const float invLen = 1.0f / std::sqrt(a.y * a.y + a.z * a.z);
+        *c = v3(0.0f, a.z * invLen, -a.y * invLen);
+    }
+    *b = cross(*c, a);
+}
+
+struct Sink {   // vrlVector::put + the tracer's current VRL (vrlTracer.h:56-89, VRL.h:148-158)
+    std::vector<float> s[9];
+    V3 start;
+    float power[3];
+    bool sigma_s_zero;
+    void put(V3 end)
+    {
+        if (sigma_s_zero) return;
+        if (power[0] == 0 && power[1] == 0 && power[2] == 0) return;
+        if (length(start - end) == 0) return;
+        s[0].push_back(start.x); s[1].push_back(start.y); s[2].push_back(start.z);
+        s[3].push_back(end.x); s[4].push_back(end.y); s[5].push_back(end.z);
+        s[6].push_back(power[0]); s[7].push_back(power[1]); s[8].push_back(power[2]);
+    }
+    void end_current(V3 p)
+    {
+        if (length(start - p) == 0) return;
+        put(p);
+    }
+    uint32_t size() const { return (uint32_t)s[0].size(); }
+};
+
+void trace_particle(const SmokeBox& sc, Stream& smp, bool short_vrls, int max_depth, int rr_depth, Sink& k)
+{
+    const MediumParams& m = sc.medium;
+    (void)smp.next(); (void)smp.next();   // sampleEmitterPosition (scene.cpp:958-974)
+    float power[3];
+    for (int i = 0; i < 3; i++) power[i] = sc.light_intensity[i] * (float)(4 * kPi);
+    const float dx = smp.next(), dy = smp.next();   // sampleDirection (point.cpp:99-106)
+    V3 dir = uniform_sphere(dx, dy);
+    if (power[0] == 0 && power[1] == 0 && power[2] == 0) return;
+    V3 o = sc.light_pos;
+    k.start = o;
+    for (int i = 0; i < 3; i++) k.power[i] = power[i];
+    int depth = 1;
+    float thr[3] = {1.0f, 1.0f, 1.0f};
+    const float eta = 1.0f;
+    const float w = m.sampling_weight;
+    while (!(thr[0] == 0 && thr[1] == 0 && thr[2] == 0) && (depth <= max_depth || max_depth < 0)) {
+        V3 n;
+        const float its_t = sc.box_hit(o, dir, &n);
+        const bool its_valid = std::isfinite(its_t);
+        // HomogeneousMedium::sampleDistance (homogeneous.cpp:275-352), balance
+        float rnd = smp.next(), sampled;
+        if (rnd < w) {
+            rnd /= w;
+            int ch = (int)(smp.next() * 3);
+            if (ch > 2) ch = 2;
+            sampled = -fastlog(1 - rnd) / m.sigma_t[ch];
+        } else {
+            sampled = INFINITY;
+        }
+        const float distSurf = its_t - 0.0f;
+        bool success = true;
+        V3 mp = o;
+        if (sampled < distSurf) {
+            mp = o + dir * (sampled + 0.0f);
+            if (mp.x == o.x && mp.y == o.y && mp.z == o.z) success = false;
+        } else {
+            sampled = distSurf;
+            success = false;
+        }
+        float pf = 0, ps = 0;
+        for (int i = 0; i < 3; i++) {
+            const float tmp = fastexp(-m.sigma_t[i] * sampled);
+            pf += tmp;
+            ps += m.sigma_t[i] * tmp;
+        }
+        pf /= 3; ps /= 3;
+        float mtr[3];
+        for (int i = 0; i < 3; i++) mtr[i] = fastexp(m.sigma_t[i] * (-sampled));
+        ps = ps * w;
+        pf = w * pf + (1 - w);
+        {
+            float mx = mtr[0] > mtr[1] ? mtr[0] : mtr[1];
+            mx = mx > mtr[2] ? mx : mtr[2];
+            if (mx < 1e-20f) mtr[0] = mtr[1] = mtr[2] = 0;
+        }
+        if (success) {   // vrlTracer.h:143-172
+            const float rps = 1.0f / ps;
+            for (int i = 0; i < 3; i++) thr[i] *= mtr[i] * m.sigma_s[i] * rps;
+            const float px_ = smp.next(), py_ = smp.next();
+            const V3 wo = uniform_sphere(px_, py_);
+            const V3 endPoint = short_vrls ? mp : o + dir * its_t;
+            k.end_current(endPoint);
+            k.start = mp;
+            for (int i = 0; i < 3; i++) k.power[i] = thr[i] * power[i];
+            o = mp; dir = wo;
+        } else if (its_valid) {   // vrlTracer.h:173-213
+            const float rpf = 1.0f / pf;
+            for (int i = 0; i < 3; i++) thr[i] *= mtr[i] * rpf;
+            const V3 p = o + dir * its_t;
+            V3 fs, ft;
+            frame_of(n, &fs, &ft);
+            const V3 mwi = -dir;
+            const float cos_wi = dot(mwi, n);
+            const float bx = smp.next(), by = smp.next();
+            float bw[3] = {0, 0, 0};
+            V3 wol = v3(0, 0, 0);
+            if (!(cos_wi <= 0)) {
+                wol = cosine_hemisphere(bx, by);
+                for (int i = 0; i < 3; i++) bw[i] = sc.albedo[i];
+            }
+            if (bw[0] == 0 && bw[1] == 0 && bw[2] == 0) { k.end_current(p); break; }
+            const V3 wo = (fs * wol.x + ft * wol.y) + n * wol.z;
+            const float wiDotGeoN = dot(n, mwi), woDotGeoN = dot(n, wo);
+            if (wiDotGeoN * cos_wi <= 0 || woDotGeoN * wol.z <= 0) { k.end_current(p); break; }
+            for (int i = 0; i < 3; i++) thr[i] *= bw[i];
+            k.end_current(p);
+            k.start = p;
+            for (int i = 0; i < 3; i++) k.power[i] = thr[i] * power[i];
+            o = p; dir = wo;
+        } else {
+            break;
+        }
+        if (depth++ >= rr_depth) {
+            float mx = thr[0] > thr[1] ? thr[0] : thr[1];
+            mx = mx > thr[2] ? mx : thr[2];
+            float q = mx * eta * eta;
+            if (q > 0.95f) q = 0.95f;
+            if (smp.next() >= q) break;
+            const float rq = 1.0f / q;
+            for (int i = 0; i < 3; i++) thr[i] *= rq;
+        }
+    }
+}
+
+}  // namespace
+
+VrlSet trace_vrls(const SmokeBox& sc, uint32_t seed, uint32_t pass, uint32_t target, bool short_vrls,
+                  int max_depth, int rr_depth)
+{
+    Sink k;
+    const MediumParams& m = sc.medium;
+    k.sigma_s_zero = (m.sigma_s[0] == 0 && m.sigma_s[1] == 0 && m.sigma_s[2] == 0);
+    uint64_t p = 0;
+    while (k.size() < target) {   // vrlTracer::randomWalk, vrlTracer.h:29-39
+        Stream smp{seed, pass, kDomTracer, (uint32_t)p, (uint32_t)(p >> 32), 0u};
+        p++;   // handleEmission -> nextParticle (the point light always emits)
+        trace_particle(sc, smp, short_vrls, max_depth, rr_depth, k);
+        if (k.sigma_s_zero && p > 1000000) break;
+    }
+    VrlSet out;
+    out.n = k.size();
+    out.particle_count = p;
+    out.soa.resize(9 * (size_t)out.n);
+    for (int pl = 0; pl < 9; pl++)
+        std::memcpy(&out.soa[(size_t)pl * out.n], k.s[pl].data(), sizeof(float) * out.n);
+    return out;
+}
+
+bool read_vrl_file(const char* path, const MediumParams& m, VrlSet* out, std::string* err)
+{
+    std::ifstream f(path);
+    if (!f) { *err = std::string("cannot open VRL file ") + path; return false; }
+    Sink k;
+    k.sigma_s_zero = (m.sigma_s[0] == 0 && m.sigma_s[1] == 0 && m.sigma_s[2] == 0);
+    std::string line;
+    while (std::getline(f, line)) {
+        std::stringstream ss(line);
+        float v[9];
+        int got = 0;
+        while (got < 9 && (ss >> v[got])) got++;
+        if (got == 0) continue;
+        if (got != 9) break;   // the reference stops at the first unparsable line (VRL.h:121-126)
+        for (int i = 6; i < 9; i++)
+            if (!std::isfinite(v[i]) || v[i] < 0) { *err = "invalid parsed VRL power"; return false; }   // VRL.h:51-53
+        k.start = v3(v[0], v[1], v[2]);
+        k.power[0] = v[6]; k.power[1] = v[7]; k.power[2] = v[8];
+        k.put(v3(v[3], v[4], v[5]));
+    }
+    out->n = k.size();
+    out->particle_count = out->n;   // m_numParticles = size() (VRL.h:127)
+    out->soa.resize(9 * (size_t)out->n);
+    for (int pl = 0; pl < 9; pl++)
+        std::memcpy(&out->soa[(size_t)pl * out->n], k.s[pl].data(), sizeof(float) * out->n);
+    return true;
+}
+
+bool write_vrl_file(const char* path, const VrlSet& v, std::string* err)
+{
+    FILE* f = std::fopen(path, "w");
+    if (!f) { *err = std::string("cannot write VRL file ") + path; return false; }
+    for (uint32_t i = 0; i < v.n; i++) {
+        for (int pl = 0; pl < 9; pl++)
+            std::fprintf(f, pl ? " %.9g" : "%.9g", (double)v.soa[(size_t)pl * v.n + i]);
+        std::fputc('\n', f);
+    }
+    std::fclose(f);
+    return true;
+}
+
+}  // namespace host
+}  // namespace alvrl

@@ -1,0 +1,85 @@
+// scene.hpp -- standalone smoke-box scene: the minimal stand-in for the parts
+// of Mitsuba's Scene / Sensor / Shape / Emitter that the vrl integrator calls
+// (out of scope per SURVEY.md 2; restated only as far as the benchmark scene
+// needs them):
+//   perspective pinhole  src/sensors/perspective.cpp:126-155, 247-269
+//   ray / box walls      one-sided diffuse walls of an axis-aligned box, seen
+//                        from inside (no interior occluders => every interior
+//                        pair is mutually visible, scene.cpp:619-679)
+//   point light          src/emitters/point.cpp:81-106
+//   homogeneous fog      src/medium/homogeneous.cpp (balance strategy)
+#pragma once
+
+#include <cstdint>
+#include <vector>
+
+namespace alvrl {
+namespace host {
+
+struct V3 { float x, y, z; };
+
+inline V3 v3(float x, float y, float z) { return V3{x, y, z}; }
+inline V3 operator+(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
+inline V3 operator-(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
+inline V3 operator*(V3 a, float s) { return v3(a.x * s, a.y * s, a.z * s); }
+inline V3 operator-(V3 a) { return v3(-a.x, -a.y, -a.z); }
+float dot(V3 a, V3 b);
+float length(V3 a);
+V3 normalize(V3 a);
+V3 cross(V3 a, V3 b);
+
+struct MediumParams {
+    float sigma_s[3] = {0.8f, 0.6f, 0.4f};
+    float sigma_a[3] = {0.05f, 0.05f, 0.05f};
+    float sigma_t[3] = {0.85f, 0.65f, 0.45f};
+    float sampling_weight = -1.0f;   // resolved by resolve()
+    int phase_type = 0;              // 0 isotropic, 1 HG
+    float phase_g = 0.0f;
+    void resolve();                  // sigma_t and the auto sampling weight (homogeneous.cpp:168-184)
+};
+
+struct SmokeBox {
+    V3 cam_origin = v3(0.0f, 0.0f, -0.9f);
+    V3 cam_target = v3(0.0f, 0.0f, 1.0f);
+    V3 cam_up = v3(0.0f, 1.0f, 0.0f);
+    float fov_x_deg = 60.0f;
+    int width = 1024, height = 1024;
+    float box_min[3] = {-1.0f, -1.0f, -1.0f};
+    float box_max[3] = {1.0f, 1.0f, 1.0f};
+    float albedo[3] = {0.5f, 0.5f, 0.5f};
+    V3 light_pos = v3(0.0f, 0.8f, 0.0f);
+    float light_intensity[3] = {10.0f, 10.0f, 10.0f};
+    MediumParams medium;
+
+    // Sensor::sampleRay through pixel sample (px, py).
+    void camera_ray(float px, float py, V3* o, V3* d) const;
+    // First hit of a ray starting inside the box: t and inward normal.
+    float box_hit(V3 o, V3 d, V3* n) const;
+    // Gather record (alvrl_gather_rec layout) of pixel centre (x, y).
+    void make_record(int x, int y, bool medium_scatters, float rec[16]) const;
+    float scene_diagonal() const;   // distance(getAABB().min, getAABB().max)
+};
+
+// vrlVector: SoA planes (start xyz, end xyz, power rgb), VRL.h:105-194.
+struct VrlSet {
+    std::vector<float> soa;   // 9 * n, plane stride n
+    uint32_t n = 0;
+    uint64_t particle_count = 0;
+};
+
+// vrlTracer::randomWalk (vrlTracer.h:13-230) in the smoke box, with the
+// counter-based stream (seed, pass, particle index) instead of one sequential
+// sampler, so the VRL set does not depend on how particles are scheduled.
+VrlSet trace_vrls(const SmokeBox& s, uint32_t seed, uint32_t pass, uint32_t target, bool short_vrls,
+                  int max_depth, int rr_depth);
+
+// ASCII VRL file I/O: one VRL per line "sx sy sz ex ey ez r g b"
+// (VRL.h:43-54 reader, vrlVector(Stream*, Medium*) :120-128).  particleCount =
+// number of lines that pass the put-filter.  The writer separates fields with
+// spaces (the reference's serializeAscii, VRL.h:65-73, writes none and cannot
+// be read back).
+bool read_vrl_file(const char* path, const MediumParams& m, VrlSet* out, std::string* err);
+bool write_vrl_file(const char* path, const VrlSet& v, std::string* err);
+
+}  // namespace host
+}  // namespace alvrl

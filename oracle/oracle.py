@@ -161,7 +161,7 @@ class Oracle:
         ids = None if rec_ids is None else np.ascontiguousarray(rec_ids, np.uint32)
         cnt = self.lib.alvrl_o_gather_brute(C.byref(P), _p(recs), n, _p(ids, C.c_uint32), _p(vrls),
                                             nv, particle_count, domain, _p(out), _p(R),
-                                            nthreads or os.cpu_count() or 1)
+                                            nthreads or min(16, os.cpu_count() or 1))
         return (out, R, int(cnt)) if want_R else (out, int(cnt))
 
     def gather_clustered(self, P: Params, recs, slice_of_rec, vrls, particle_count, slice_off,
@@ -177,7 +177,7 @@ class Oracle:
         cnt = self.lib.alvrl_o_gather_clustered(
             C.byref(P), _p(recs), n, _p(ids, C.c_uint32), _p(a[0], C.c_uint32), _p(vrls), nv,
             particle_count, _p(a[1], C.c_uint32), _p(a[2], C.c_uint32), _p(a[3]),
-            _p(a[4], C.c_uint32), _p(a[5]), len(a[4]), _p(out), nthreads or os.cpu_count() or 1)
+            _p(a[4], C.c_uint32), _p(a[5]), len(a[4]), _p(out), nthreads or min(16, os.cpu_count() or 1))
         return out, int(cnt)
 
     # ---- LightSlice preprocessing ----
