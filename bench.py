@@ -1,0 +1,261 @@
+#!/usr/bin/env python3
+"""ALVRL hot-path benchmark (BASELINE.json metric) on N MI355X, one process per GPU.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2|C3|C4|C1]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+        --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
+
+A step is one progressive pass of the vrl integrator over the whole frame
+(vrlIntegrator::prepass + render, vrlIntegrator.cpp:270-599): with resident
+VRLs (the vrlFile mode) the prepass is the LightSlice work (representative
+sampling, R build, per-slice refinement) for the clustered configs and nothing
+for the brute-force one; the render is the per-pixel gather.  Image tiles
+(64x64, round robin) are sharded over ranks and the framebuffer is reduced to
+rank 0 with one RCCL collective over xGMI per step.  Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+for _p in (os.path.join(REPO, "mitsuba-alvrl_amd"), os.path.join(REPO, "oracle")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+METRIC = "VRL contributions/sec + per-pixel RMSE vs CPU (1024², 100k VRLs)"
+SEED_VRL = 0x5EED0001
+SEED_RNG = 0xA1B2C3D4
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# Algorithmic bytes per contribution: one VRL
+# record (9 x fp32) per pair for the brute gather, + index + weight for the
+# clustered gather, + the (mean, var) float2 written per pair for the R build.
+BYTES_PER_PAIR = {"brute": 36, "clustered": 44, "rbuild": 44}
+
+CONFIGS = {
+    "C1": dict(w=256, h=256, nvrl=1000, props="",
+               desc="256^2 smoke box, 1k VRLs, ALVRL defaults (adaptive, 100 slices)"),
+    "C2": dict(w=1024, h=1024, nvrl=10000, props="localRefinement=false;globalCluster=false",
+               desc="1024^2 smoke box, 10k VRLs, brute-force VRL gather (clustering off)"),
+    "C3": dict(w=1024, h=1024, nvrl=100000, props="targetNumSlices=100;localUndersampling=100",
+               desc="1024^2 smoke box, 100k VRLs, LightSlice fixed-depth (localUndersampling=100)"),
+    "C4": dict(w=1024, h=1024, nvrl=100000, props="targetNumSlices=100;localUndersampling=-1",
+               desc="1024^2 smoke box, 100k VRLs, Adaptive LightSlice refinement"),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="C2", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-row-stride", type=int, default=64,
+                    help="CPU baseline sample: every n-th image row")
+    ap.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "r01_pmc_traffic.json"),
+                    help="per-launch HBM bytes of the dominant kernel from a rocprofv3 --pmc pass")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import alvrl
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and not (world == 1 and args.gpus == 1):
+        if world == 1:
+            raise SystemExit(f"--gpus {args.gpus} needs torch.distributed.run with {args.gpus} ranks")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    cfg = CONFIGS[args.config]
+    W, H = cfg["w"], cfg["h"]
+    scene = alvrl.scene_default(W, H)
+    # VRL set = the benchmark input (restated vrlTracer, seed 0x5EED0001),
+    # resident for every pass exactly like the reference's vrlFile mode.
+    vrls, pc = alvrl.trace_vrls(scene, cfg["nvrl"], seed=SEED_VRL)
+    props = cfg["props"] + (";" if cfg["props"] else "") + f"seed={SEED_RNG}"
+    it = alvrl.Integrator(props, device=local)
+    it.set_vrls(vrls, pc)
+    it.preprocess(scene)
+    clustered = "localRefinement=false" not in props
+    fb = torch.zeros(W * H * 3, dtype=torch.float32, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def step(i):
+        it.prepass(i)
+        fb.zero_()
+        it.render(fb, rank, world, stream=stream)
+        if world > 1:
+            dist.reduce(fb, dst=0)   # the single RCCL framebuffer gather per pass
+
+    def barrier():
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+            torch.cuda.synchronize(dev)
+
+    for i in range(args.warmup):
+        step(i)
+    barrier()
+    s0 = it.stats()
+    kernel_ms, rbuild_ms, refine_ms, prepass_ms = [], [], [], []
+    barrier()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i)
+        st = it.stats()           # HIP-event kernel times of this step (synchronises)
+        kernel_ms.append(st["ms_render_kernel"])
+        rbuild_ms.append(st["ms_rbuild"])
+        refine_ms.append(st["ms_refine"])
+        prepass_ms.append(st["ms_prepass_wall"])
+    barrier()
+    elapsed = time.perf_counter() - t0
+    s1 = it.stats()
+    contrib = (s1["contrib_preprocess"] - s0["contrib_preprocess"]) + (s1["contrib_render"] - s0["contrib_render"])
+    render_pairs = s1["contrib_render"] - s0["contrib_render"]
+    pre_pairs = s1["contrib_preprocess"] - s0["contrib_preprocess"]
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        c = torch.tensor([contrib, render_pairs, pre_pairs], dtype=torch.float64, device=dev)
+        dist.all_reduce(c, op=dist.ReduceOp.SUM)
+        contrib, render_pairs, pre_pairs = (int(x) for x in c.tolist())
+
+    value = contrib / elapsed
+    # roofline of the dominant kernel (the render gather), timed with HIP events
+    # on the stream it was launched on
+    avg_kernel_s = float(np.mean(kernel_ms)) / 1e3 if kernel_ms else float("nan")
+    pairs_per_launch_rank = (s1["contrib_render"] - s0["contrib_render"]) / max(args.steps, 1)
+    kind = "clustered" if clustered else "brute"
+    bytes_per_launch = BYTES_PER_PAIR[kind] * pairs_per_launch_rank
+    achieved = bytes_per_launch / avg_kernel_s / 1e9 if avg_kernel_s > 0 else 0.0
+    traffic = None
+    try:
+        with open(args.pmc_json) as f:
+            pm = json.load(f)
+        if pm.get("config") == args.config:
+            traffic = pm.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+
+    out = None
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "VRL contributions/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic: restated vrlTracer VRLs (seed 0x5EED0001) in the BASELINE.md smoke box",
+            "config": {"workload": f"{args.config}: {cfg['desc']}", "resolution": [W, H],
+                       "vrls": int(vrls.shape[1]), "particles": int(pc),
+                       "parallelism": f"image tiles 64x64 round-robin over {world} GPU(s), "
+                                      f"RCCL reduce of the framebuffer"},
+            "breakdown": {"render_pairs": render_pairs, "prepass_pairs": pre_pairs,
+                          "render_kernel_ms": float(np.mean(kernel_ms)) if kernel_ms else None,
+                          "rbuild_ms": float(np.mean(rbuild_ms)), "refine_ms": float(np.mean(refine_ms)),
+                          "prepass_wall_ms": float(np.mean(prepass_ms)),
+                          "slices": int(s1["slices"]), "rep_rows": int(s1["rep_rows"]),
+                          "clusters_total": int(s1["clusters_total"]),
+                          "slices_failed": int(s1["slices_failed"])},
+            "roofline": {"bound": "hbm", "kernel": f"k_gather_{kind}", "achieved": achieved,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": traffic,
+                         "bytes_per_pair": BYTES_PER_PAIR[kind],
+                         "pairs_per_launch": pairs_per_launch_rank,
+                         "note": "algorithmic bytes; the gather is VALU/transcendental-bound "
+                                 "(VRL records are broadcast from SGPRs), see DESIGN.md"},
+            "cpu_baseline": None,
+        }
+    if world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"], out["pixel_rmse_vs_cpu"] = cpu_baseline(args, cfg, scene, vrls, pc, fb, it,
+                                                                       clustered)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def cpu_baseline(args, cfg, scene, vrls, pc, fb, it, clustered):
+    """The CPU restatement (oracle/, built with the reference's CXXFLAGS) timed
+    on this host's cores on a bounded sample of the same workload, and the
+    per-pixel RMSE of the device frame against it on that sample."""
+    import numpy as np
+    from oracle import Oracle
+    o = Oracle(fast=True)
+    W, H = cfg["w"], cfg["h"]
+    threads = int(os.environ.get("ALVRL_CPU_THREADS", "16"))
+    rows = np.arange(0, H, args.cpu_row_stride)
+    pix = (rows[:, None] * W + np.arange(W)[None, :]).reshape(-1).astype(np.uint32)
+    osc = o.scene(W, H)
+    recs = o.records(osc)[pix]
+    m = o.medium()
+    last_pass = args.warmup + args.steps - 1
+    P = o.params(m, seed=SEED_RNG, pass_=last_pass)
+    if clustered:
+        # clustered frame: the device's own cluster lists for the sampled pixels
+        cl = it.clusters()
+        p2s = it.slices()
+        xs, ys = pix % W, pix // W
+        sl = p2s[ys + H * xs]
+        t0 = time.perf_counter()
+        img, cnt = o.gather_clustered(P, recs, sl, vrls, pc, cl["slice_off"], cl["reps"], cl["weights"],
+                                      cl["fb_reps"], cl["fb_weights"], rec_ids=pix, nthreads=threads)
+        dt = time.perf_counter() - t0
+        sample = (f"clustered gather of every {args.cpu_row_stride}th image row ({len(pix)} pixels) "
+                  f"with the device's cluster lists")
+    else:
+        t0 = time.perf_counter()
+        img, cnt = o.gather_brute(P, recs, vrls, pc, rec_ids=pix, nthreads=threads)
+        dt = time.perf_counter() - t0
+        sample = f"brute gather of every {args.cpu_row_stride}th image row ({len(pix)} pixels x {vrls.shape[1]} VRLs)"
+    gpu = fb.view(-1, 3)[torch_index(pix).to(fb.device)].cpu().numpy()
+    diff = gpu.astype(np.float64) - img.astype(np.float64)
+    rmse = float(np.sqrt(np.mean(diff ** 2)))
+    rel = np.abs(diff) / np.maximum(np.abs(img), 1e-30)
+    base = {"value": cnt / dt, "unit": "VRL contributions/s", "cores": threads, "kind": "port",
+            "sample": sample, "seconds": dt,
+            "cpu": _cpu_model(), "flags": "reference CXXFLAGS (build/config-linux-gcc.py:7)"}
+    acc = {"rmse": rmse, "mean": float(np.abs(img).mean()), "rmse_rel": rmse / max(float(np.abs(img).mean()), 1e-30),
+           "max_rel": float(rel.max()), "median_rel": float(np.median(rel)), "pixels": int(len(pix))}
+    return base, acc
+
+
+def torch_index(pix):
+    import torch
+    return torch.from_numpy(pix.astype("int64"))
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+if __name__ == "__main__":
+    main()

@@ -151,6 +151,13 @@ ALVRL_API int alvrl_build_R(alvrl_ctx *ctx, const alvrl_gather_rec *d_recs,
                             const uint32_t *d_rec_ids, uint32_t nrows, float *d_Rt, uint64_t ld,
                             uint64_t row0, void *stream);
 
+/* Replaces the zero / non-zero split of Preprocessor::cluster (:843-855,
+ * totalVrlContribution :936-945): out_mask[v] = 1 iff some row of R has a
+ * non-zero mean for VRL v (every mean is >= 0, so this equals sum != 0).
+ * Rows [0, nrows) of d_Rt; out_mask is host memory (nvrl bytes). */
+ALVRL_API int alvrl_nonzero_columns(alvrl_ctx *ctx, const float *d_Rt, uint64_t ld, uint32_t nrows,
+                                    uint8_t *out_mask, void *stream);
+
 /* ---- hot path (b) part 2: cluster refinement ------------------------- */
 /* One Clustering (Preprocessor.cpp:287-720): ctor (column weights, initial
  * clusters, unclustered variances, :301-341), optional refine() (:380-489),
@@ -182,6 +189,12 @@ ALVRL_API int alvrl_refine(alvrl_ctx *ctx, const float *d_Rt, uint64_t ld, uint3
                            void *stream);
 /* Milliseconds the device spent in the last alvrl_refine call (HIP events). */
 ALVRL_API int alvrl_last_refine_ms(alvrl_ctx *ctx, float *ms);
+
+/* ---- framebuffer --------------------------------------------------- */
+/* ImageBlock::put of 1-spp box-filtered samples (imageblock.h:124-131):
+ * d_fb[3*d_pixel[r] + c] += d_rgb[3*r + c] for r < n. */
+ALVRL_API int alvrl_accumulate_rgb(alvrl_ctx *ctx, const float *d_rgb, const uint32_t *d_pixel,
+                                   uint32_t n, float *d_fb, void *stream);
 
 /* ---- statistics ------------------------------------------------------- */
 /* statsVrlsPreprocess / statsVrlsRender (:119-122, 593-596, 819-822): number

@@ -1,0 +1,110 @@
+/*
+ * alvrl_host.h -- host-side harness of libalvrl.so (C ABI).
+ *
+ * Not part of the device boundary (include/alvrl.h): these entry points are
+ * the standalone stand-ins for what a Mitsuba host provides around the vrl
+ * plugin -- the smoke-box scene (Sensor::sampleRay + Scene::rayIntersect for an
+ * inside-the-box camera), the VRL tracer (vrlTracer.h), the ASCII VRL file
+ * format (VRL.h:43-54, 120-128) and the LightSlice slicing step
+ * (Preprocessor::buildSlices / sampleSliceMapping / buildLocalities /
+ * getLocalMatrix, Preprocessor.cpp:66-121, 779-827, 1130-1525) -- plus the
+ * integrator pipeline that drives include/alvrl.h like vrlIntegrator does.
+ */
+#ifndef ALVRL_HOST_H
+#define ALVRL_HOST_H
+
+#include <stdint.h>
+#include "alvrl.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct {
+    float cam_origin[3], cam_target[3], cam_up[3];
+    float fov_x_deg;
+    int width, height;
+    float box_min[3], box_max[3];
+    float albedo[3];
+    float light_pos[3];
+    float light_intensity[3];
+    alvrl_medium_desc medium;
+} alvrl_scene_desc;
+
+/* The benchmark scene of BASELINE.md ("homogeneous smoke box"). */
+ALVRL_API void alvrl_scene_default(alvrl_scene_desc *s, int width, int height);
+
+/* Gather records of pixel centres.  pixel_ids (row-major y*W+x) may be NULL:
+ * all pixels in row-major order (n must be W*H then). */
+ALVRL_API int alvrl_scene_records(const alvrl_scene_desc *s, int medium_scatters,
+                                  const uint32_t *pixel_ids, uint32_t n, alvrl_gather_rec *out);
+
+/* vrlTracer::randomWalk (vrlTracer.h:13-52).  soa receives 9 planes of
+ * stride 'cap'; *n = #VRLs (>= target unless cap is hit), *particles =
+ * particleCount.  Returns ALVRL_ERR_INVALID if cap < the VRLs produced. */
+ALVRL_API int alvrl_trace_vrls(const alvrl_scene_desc *s, uint32_t seed, uint32_t pass,
+                               uint32_t target, int short_vrls, int max_depth, int rr_depth,
+                               float *soa, uint32_t cap, uint32_t *n, uint64_t *particles);
+
+/* vrlVector(Stream*, const Medium*) (VRL.h:120-128) / a separator-correct
+ * serializeAscii (VRL.h:65-73). */
+ALVRL_API int alvrl_read_vrl_file(const char *path, const alvrl_medium_desc *m, float *soa,
+                                  uint32_t cap, uint32_t *n, uint64_t *particles);
+ALVRL_API int alvrl_write_vrl_file(const char *path, const float *soa, uint32_t n);
+
+/* Message of the last failing alvrl_scene_* / alvrl_trace_* / alvrl_*_vrl_file /
+ * alvrl_integrator_* call on this thread. */
+ALVRL_API const char *alvrl_host_last_error(void);
+
+/* ---- vrl integrator pipeline (vrlIntegrator.cpp) ---------------------- */
+typedef struct alvrl_integrator alvrl_integrator;
+
+/* props: "name=value" pairs separated by ';' with the reference's parameter
+ * names and defaults (vrlIntegrator.cpp:128-208, integrator.cpp:272-277, 348-349),
+ * plus "seed" (counter-RNG key) and "vrlSeed" (tracer key). */
+ALVRL_API int alvrl_integrator_create(const char *props, int device, alvrl_integrator **out);
+ALVRL_API void alvrl_integrator_destroy(alvrl_integrator *it);
+/* vrlIntegrator::preprocess (:237-267): scene, optional vrlFile, buildSlices. */
+ALVRL_API int alvrl_integrator_preprocess(alvrl_integrator *it, const alvrl_scene_desc *s);
+/* vrlIntegrator::prepass (:270-356) for pass 'pass' (0-based): trace or reuse
+ * VRLs, sample representatives, build R, cluster, upload cluster info.
+ * rank/world shard nothing in the prepass (every rank holds every slice). */
+ALVRL_API int alvrl_integrator_prepass(alvrl_integrator *it, uint32_t pass);
+/* SamplingIntegrator::render for the pixels this rank owns: 64x64 tiles dealt
+ * round-robin (tile t -> rank t % world).  Adds Li of every owned pixel into
+ * d_framebuffer (device, W*H*3 floats, row-major) on 'stream'. */
+ALVRL_API int alvrl_integrator_render(alvrl_integrator *it, uint32_t rank, uint32_t world,
+                                      float *d_framebuffer, void *stream);
+/* Preloaded VRLs (the vrlFile mode, :243-252 / :280-287): every pass reuses
+ * this set instead of tracing; soa = 9 planes of stride n. */
+ALVRL_API int alvrl_integrator_set_vrls(alvrl_integrator *it, const float *soa, uint32_t n,
+                                        uint64_t particle_count);
+/* Timing / statistics of the last prepass and render. */
+typedef struct {
+    uint64_t vrls, particles, slices, rep_rows, clusters_total;
+    uint64_t contrib_preprocess, contrib_render;
+    double ms_trace, ms_slices, ms_rbuild, ms_refine, ms_render_kernel, ms_prepass_wall;
+    uint32_t slices_failed;
+    int fallback_built;
+} alvrl_integrator_stats;
+ALVRL_API int alvrl_integrator_get_stats(alvrl_integrator *it, alvrl_integrator_stats *st);
+/* The device context the integrator drives (for low-level access). */
+ALVRL_API alvrl_ctx *alvrl_integrator_ctx(alvrl_integrator *it);
+/* Copies of host-side state for tests: pixel->slice map (column-major,
+ * y + H*x, vrlIntegrator.cpp:560), representative rows, cluster CSR. */
+ALVRL_API int alvrl_integrator_slices(alvrl_integrator *it, uint32_t *pixel_to_slice, uint32_t n);
+ALVRL_API uint32_t alvrl_integrator_num_slices(alvrl_integrator *it);
+ALVRL_API int alvrl_integrator_reps(alvrl_integrator *it, uint32_t *rep_off, uint32_t *rep_pix,
+                                    uint32_t cap);
+ALVRL_API int alvrl_integrator_clusters(alvrl_integrator *it, uint32_t *slice_off, uint32_t *reps,
+                                        float *weights, uint32_t cap, uint32_t *fb_reps,
+                                        float *fb_weights, uint32_t fb_cap, uint32_t *n_fb);
+/* R of the last prepass, [nvrl][rep_rows] (mean, var) pairs (host copy). */
+ALVRL_API int alvrl_integrator_R(alvrl_integrator *it, float *out, uint64_t cap_floats);
+ALVRL_API int alvrl_integrator_vrls(alvrl_integrator *it, float *soa, uint32_t cap, uint32_t *n,
+                                    uint64_t *particles);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ALVRL_HOST_H */

@@ -93,6 +93,8 @@ def lib() -> C.CDLL:
     L.alvrl_gather_brute_host.argtypes = [vp, vp, vp, u32, vp]
     L.alvrl_gather_clustered_host.argtypes = [vp, vp, vp, vp, u32, vp]
     L.alvrl_last_kernel_ms.argtypes = [vp, P(f32)]
+    L.alvrl_nonzero_columns.argtypes = [vp, vp, u64, u32, vp, vp]
+    L.alvrl_accumulate_rgb.argtypes = [vp, vp, vp, u32, vp, vp]
     _lib = L
     return L
 
@@ -253,6 +255,15 @@ class Context:
                                                   recs.shape[0], _ptr(out)))
         return out
 
+    def nonzero_columns(self, d_Rt, ld: int, nrows: int) -> np.ndarray:
+        mask = np.zeros(max(1, self.nvrl), np.uint8)
+        _check(self.L.alvrl_nonzero_columns(self.h, _ptr(d_Rt), ld, nrows, _ptr(mask), None))
+        return mask[:self.nvrl].astype(bool)
+
+    def accumulate_rgb(self, d_rgb, d_pixel, d_fb, stream=None):
+        _check(self.L.alvrl_accumulate_rgb(self.h, _ptr(d_rgb), _ptr(d_pixel), d_pixel.shape[0],
+                                           _ptr(d_fb), C.c_void_p(stream) if stream else None))
+
     # ---- stats / timing ----
     def stats(self):
         a, b = C.c_uint64(), C.c_uint64()
@@ -266,3 +277,197 @@ class Context:
         ms = C.c_float()
         _check(self.L.alvrl_last_kernel_ms(self.h, C.byref(ms)))
         return ms.value
+
+
+# ---------------------------------------------------------------------------
+# host harness (include/alvrl_host.h)
+# ---------------------------------------------------------------------------
+class SceneDesc(C.Structure):
+    _fields_ = [("cam_origin", C.c_float * 3), ("cam_target", C.c_float * 3), ("cam_up", C.c_float * 3),
+                ("fov_x_deg", C.c_float), ("width", C.c_int), ("height", C.c_int),
+                ("box_min", C.c_float * 3), ("box_max", C.c_float * 3), ("albedo", C.c_float * 3),
+                ("light_pos", C.c_float * 3), ("light_intensity", C.c_float * 3),
+                ("medium", MediumDesc)]
+
+
+class IntegratorStats(C.Structure):
+    _fields_ = [("vrls", C.c_uint64), ("particles", C.c_uint64), ("slices", C.c_uint64),
+                ("rep_rows", C.c_uint64), ("clusters_total", C.c_uint64),
+                ("contrib_preprocess", C.c_uint64), ("contrib_render", C.c_uint64),
+                ("ms_trace", C.c_double), ("ms_slices", C.c_double), ("ms_rbuild", C.c_double),
+                ("ms_refine", C.c_double), ("ms_render_kernel", C.c_double),
+                ("ms_prepass_wall", C.c_double), ("slices_failed", C.c_uint32),
+                ("fallback_built", C.c_int)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+_host_bound = False
+
+
+def _host():
+    global _host_bound
+    L = lib()
+    if _host_bound:
+        return L
+    u32, u64, i32, f32, vp = C.c_uint32, C.c_uint64, C.c_int, C.c_float, C.c_void_p
+    P = C.POINTER
+    L.alvrl_scene_default.argtypes = [P(SceneDesc), i32, i32]; L.alvrl_scene_default.restype = None
+    L.alvrl_scene_records.argtypes = [P(SceneDesc), i32, vp, u32, vp]
+    L.alvrl_trace_vrls.argtypes = [P(SceneDesc), u32, u32, u32, i32, i32, i32, vp, u32, P(u32), P(u64)]
+    L.alvrl_read_vrl_file.argtypes = [C.c_char_p, P(MediumDesc), vp, u32, P(u32), P(u64)]
+    L.alvrl_write_vrl_file.argtypes = [C.c_char_p, vp, u32]
+    L.alvrl_host_last_error.restype = C.c_char_p
+    L.alvrl_integrator_create.argtypes = [C.c_char_p, i32, P(vp)]
+    L.alvrl_integrator_destroy.argtypes = [vp]; L.alvrl_integrator_destroy.restype = None
+    L.alvrl_integrator_preprocess.argtypes = [vp, P(SceneDesc)]
+    L.alvrl_integrator_prepass.argtypes = [vp, u32]
+    L.alvrl_integrator_render.argtypes = [vp, u32, u32, vp, vp]
+    L.alvrl_integrator_set_vrls.argtypes = [vp, vp, u32, u64]
+    L.alvrl_integrator_get_stats.argtypes = [vp, P(IntegratorStats)]
+    L.alvrl_integrator_ctx.argtypes = [vp]; L.alvrl_integrator_ctx.restype = vp
+    L.alvrl_integrator_slices.argtypes = [vp, P(u32), u32]
+    L.alvrl_integrator_num_slices.argtypes = [vp]; L.alvrl_integrator_num_slices.restype = u32
+    L.alvrl_integrator_reps.argtypes = [vp, P(u32), P(u32), u32]
+    L.alvrl_integrator_clusters.argtypes = [vp, P(u32), P(u32), P(f32), u32, P(u32), P(f32), u32, P(u32)]
+    L.alvrl_integrator_vrls.argtypes = [vp, vp, u32, P(u32), P(u64)]
+    L.alvrl_integrator_R.argtypes = [vp, vp, u64]
+    _host_bound = True
+    return L
+
+
+def _hcheck(rc: int):
+    if rc != ALVRL_OK:
+        raise AlvrlError(rc, _host().alvrl_host_last_error().decode())
+
+
+def scene_default(width: int, height: int) -> SceneDesc:
+    s = SceneDesc()
+    _host().alvrl_scene_default(C.byref(s), width, height)
+    return s
+
+
+def scene_records(scene: SceneDesc, pixel_ids=None, medium_scatters: bool = True) -> np.ndarray:
+    L = _host()
+    n = scene.width * scene.height if pixel_ids is None else len(pixel_ids)
+    out = np.zeros((n, REC_WORDS), np.float32)
+    ids = None if pixel_ids is None else _np(pixel_ids, np.uint32)
+    _hcheck(L.alvrl_scene_records(C.byref(scene), int(medium_scatters), _ptr(ids), n, _ptr(out)))
+    return out
+
+
+def trace_vrls(scene: SceneDesc, target: int, seed: int = 0x5EED0001, pass_: int = 0,
+               short_vrls: bool = True, max_depth: int = -1, rr_depth: int = 5):
+    L = _host()
+    cap = target + 8192
+    soa = np.zeros((9, cap), np.float32)
+    n = C.c_uint32(); pc = C.c_uint64()
+    _hcheck(L.alvrl_trace_vrls(C.byref(scene), seed, pass_, target, int(short_vrls), max_depth,
+                               rr_depth, _ptr(soa), cap, C.byref(n), C.byref(pc)))
+    return np.ascontiguousarray(soa[:, :n.value]), int(pc.value)
+
+
+def read_vrl_file(path: str, medium: Medium = Medium()):
+    L = _host()
+    md = MediumDesc((C.c_float * 3)(*medium.sigma_s), (C.c_float * 3)(*medium.sigma_a),
+                    medium.sampling_weight, medium.phase_type, medium.phase_g)
+    n = C.c_uint32(); pc = C.c_uint64()
+    _hcheck(L.alvrl_read_vrl_file(path.encode(), C.byref(md), None, 0, C.byref(n), C.byref(pc)))
+    soa = np.zeros((9, max(1, n.value)), np.float32)
+    _hcheck(L.alvrl_read_vrl_file(path.encode(), C.byref(md), _ptr(soa), n.value, C.byref(n),
+                                  C.byref(pc)))
+    return soa[:, :n.value].copy(), int(pc.value)
+
+
+def write_vrl_file(path: str, soa: np.ndarray):
+    soa = _np(soa, np.float32)
+    _hcheck(_host().alvrl_write_vrl_file(path.encode(), _ptr(soa), soa.shape[1]))
+
+
+class Integrator:
+    """vrlIntegrator pipeline (preprocess / prepass / render) on one device."""
+
+    def __init__(self, props: str = "", device: int = 0):
+        L = _host()
+        self.L = L
+        h = C.c_void_p()
+        _hcheck(L.alvrl_integrator_create(props.encode(), device, C.byref(h)))
+        self.h = h
+        self.device = device
+        self.scene = None
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.alvrl_integrator_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def preprocess(self, scene: SceneDesc):
+        self.scene = scene
+        _hcheck(self.L.alvrl_integrator_preprocess(self.h, C.byref(scene)))
+
+    def set_vrls(self, soa: np.ndarray, particle_count: int):
+        soa = _np(soa, np.float32)
+        _hcheck(self.L.alvrl_integrator_set_vrls(self.h, _ptr(soa), soa.shape[1], particle_count))
+
+    def prepass(self, pass_: int = 0):
+        _hcheck(self.L.alvrl_integrator_prepass(self.h, pass_))
+
+    def render(self, d_fb, rank: int = 0, world: int = 1, stream=None):
+        _hcheck(self.L.alvrl_integrator_render(self.h, rank, world, _ptr(d_fb),
+                                               C.c_void_p(stream) if stream else None))
+
+    def stats(self) -> dict:
+        st = IntegratorStats()
+        _hcheck(self.L.alvrl_integrator_get_stats(self.h, C.byref(st)))
+        return st.as_dict()
+
+    def num_slices(self) -> int:
+        return int(self.L.alvrl_integrator_num_slices(self.h))
+
+    def slices(self) -> np.ndarray:
+        n = self.scene.width * self.scene.height
+        out = np.zeros(n, np.uint32)
+        _hcheck(self.L.alvrl_integrator_slices(self.h, _arr(out, C.c_uint32), n))
+        return out
+
+    def reps(self):
+        ns = self.num_slices()
+        cap = self.scene.width * self.scene.height
+        off = np.zeros(ns + 1, np.uint32); pix = np.zeros(cap, np.uint32)
+        _hcheck(self.L.alvrl_integrator_reps(self.h, _arr(off, C.c_uint32), _arr(pix, C.c_uint32), cap))
+        return off, pix[:off[-1]].copy()
+
+    def vrls(self):
+        n = C.c_uint32(); pc = C.c_uint64()
+        _hcheck(self.L.alvrl_integrator_vrls(self.h, None, 0, C.byref(n), C.byref(pc)))
+        soa = np.zeros((9, max(1, n.value)), np.float32)
+        _hcheck(self.L.alvrl_integrator_vrls(self.h, _ptr(soa), n.value, C.byref(n), C.byref(pc)))
+        return soa[:, :n.value].copy(), int(pc.value)
+
+    def R(self) -> np.ndarray:
+        """R of the last prepass as [nvrl, rep_rows, 2] (mean, var)."""
+        st = self.stats()
+        nv, rows = int(st["vrls"]), int(st["rep_rows"])
+        out = np.zeros((nv, rows, 2), np.float32)
+        _hcheck(self.L.alvrl_integrator_R(self.h, _ptr(out), out.size))
+        return out
+
+    def clusters(self):
+        ns = self.num_slices()
+        nv = self.vrls()[0].shape[1]
+        cap = max(1, ns * nv)
+        off = np.zeros(ns + 1, np.uint32); reps = np.zeros(cap, np.uint32)
+        w = np.zeros(cap, np.float32)
+        fr = np.zeros(nv + 1, np.uint32); fw = np.zeros(nv + 1, np.float32); nf = C.c_uint32()
+        _hcheck(self.L.alvrl_integrator_clusters(self.h, _arr(off, C.c_uint32), _arr(reps, C.c_uint32),
+                                                 _arr(w, C.c_float), cap, _arr(fr, C.c_uint32),
+                                                 _arr(fw, C.c_float), nv + 1, C.byref(nf)))
+        return dict(slice_off=off, reps=reps[:off[-1]].copy(), weights=w[:off[-1]].copy(),
+                    fb_reps=fr[:nf.value].copy(), fb_weights=fw[:nf.value].copy())

@@ -31,6 +31,10 @@ hipError_t launch_gather_clustered(const Rec* recs, const uint32_t* ids, const W
 hipError_t launch_build_R(const Rec* recs, const uint32_t* ids, uint32_t nrows, const VrlPrep* vp,
                           uint32_t nvrl, const DevParams& P, float normalization, float2* Rt,
                           uint64_t ld, uint64_t row0, unsigned long long* counter, hipStream_t s);
+hipError_t launch_nonzero_columns(const float2* Rt, uint64_t ld, uint32_t nrows, uint32_t nvrl,
+                                  uint8_t* mask, hipStream_t s);
+hipError_t launch_accumulate_rgb(const float* rgb, const uint32_t* pix, uint32_t n, float* fb,
+                                 hipStream_t s);
 struct HostJob {
     const uint32_t* rows;
     const double* locw;
@@ -366,6 +370,33 @@ ALVRL_API int alvrl_last_refine_ms(alvrl_ctx* c, float* ms)
 {
     if (!c || !ms) return fail(ALVRL_ERR_INVALID, "alvrl_last_refine_ms: null argument");
     *ms = c->refine_ms;
+    return ALVRL_OK;
+}
+
+ALVRL_API int alvrl_nonzero_columns(alvrl_ctx* c, const float* d_Rt, uint64_t ld, uint32_t nrows,
+                                    uint8_t* out_mask, void* stream)
+{
+    if (!c || !out_mask || (!d_Rt && c->nvrl)) return fail(ALVRL_ERR_INVALID, "alvrl_nonzero_columns: null argument");
+    if (nrows > ld) return fail(ALVRL_ERR_INVALID, "alvrl_nonzero_columns: nrows > ld");
+    if (c->nvrl == 0) return ALVRL_OK;
+    HIPCHK(hipSetDevice(c->cfg.device));
+    hipStream_t s = pick(c, stream);
+    uint8_t* d_mask = nullptr;
+    HIPCHK(hipMallocAsync((void**)&d_mask, c->nvrl, s));
+    hipError_t e = launch_nonzero_columns(reinterpret_cast<const float2*>(d_Rt), ld, nrows, c->nvrl, d_mask, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(out_mask, d_mask, c->nvrl, hipMemcpyDeviceToHost, s);
+    hipFreeAsync(d_mask, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return fail(ALVRL_ERR_HIP, std::string("alvrl_nonzero_columns: ") + hipGetErrorString(e));
+    return ALVRL_OK;
+}
+
+ALVRL_API int alvrl_accumulate_rgb(alvrl_ctx* c, const float* d_rgb, const uint32_t* d_pixel, uint32_t n,
+                                   float* d_fb, void* stream)
+{
+    if (!c || (n && (!d_rgb || !d_pixel || !d_fb))) return fail(ALVRL_ERR_INVALID, "alvrl_accumulate_rgb: null argument");
+    HIPCHK(hipSetDevice(c->cfg.device));
+    HIPCHK(launch_accumulate_rgb(d_rgb, d_pixel, n, d_fb, pick(c, stream)));
     return ALVRL_OK;
 }
 

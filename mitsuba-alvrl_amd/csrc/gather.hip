@@ -167,6 +167,48 @@ __global__ void __launch_bounds__(256) k_build_R(const Rec* __restrict__ recs,
     count_pairs(counter, active && q.medium, done);
 }
 
+// Preprocessor::cluster's totalVrlContribution != 0 (means are >= 0): one
+// wave per VRL column, rows contiguous.
+__global__ void __launch_bounds__(256) k_nonzero_columns(const float2* __restrict__ Rt, uint64_t ld,
+                                                         uint32_t nrows, uint32_t nvrl,
+                                                         uint8_t* __restrict__ mask)
+{
+    const uint32_t v = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (v >= nvrl) return;
+    const float2* col = Rt + (size_t)v * ld;
+    bool nz = false;
+    for (uint32_t r = threadIdx.x & 63; r < nrows; r += 64) nz |= col[r].x != 0.0f;
+    const unsigned long long b = __ballot(nz);
+    if ((threadIdx.x & 63) == 0) mask[v] = b ? 1 : 0;
+}
+
+__global__ void __launch_bounds__(256) k_accumulate_rgb(const float* __restrict__ rgb,
+                                                        const uint32_t* __restrict__ pix, uint32_t n,
+                                                        float* __restrict__ fb)
+{
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    const size_t p = (size_t)pix[r] * 3;
+    fb[p + 0] += rgb[3 * (size_t)r + 0];
+    fb[p + 1] += rgb[3 * (size_t)r + 1];
+    fb[p + 2] += rgb[3 * (size_t)r + 2];
+}
+
+hipError_t launch_nonzero_columns(const float2* Rt, uint64_t ld, uint32_t nrows, uint32_t nvrl,
+                                  uint8_t* mask, hipStream_t s)
+{
+    if (nvrl == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_nonzero_columns, dim3((nvrl + 3) / 4), dim3(256), 0, s, Rt, ld, nrows, nvrl, mask);
+    return hipGetLastError();
+}
+
+hipError_t launch_accumulate_rgb(const float* rgb, const uint32_t* pix, uint32_t n, float* fb, hipStream_t s)
+{
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_accumulate_rgb, dim3((n + 255) / 256), dim3(256), 0, s, rgb, pix, n, fb);
+    return hipGetLastError();
+}
+
 // ---------------------------------------------------------------------------
 // host-side launchers (called from capi.cpp)
 // ---------------------------------------------------------------------------

@@ -1,0 +1,132 @@
+// host_capi.cpp -- C ABI of the host harness (include/alvrl_host.h): scene
+// records, VRL tracer, VRL file I/O.  The integrator pipeline entry points
+// live in integrator.hip (they drive the device).
+#include "alvrl_host.h"
+
+#include <cstring>
+#include <stdexcept>
+#include <string>
+
+#include "scene.hpp"
+
+using namespace alvrl::host;
+
+namespace alvrl {
+namespace host {
+thread_local std::string g_host_err;
+SmokeBox to_box(const alvrl_scene_desc& s)
+{
+    SmokeBox b;
+    b.cam_origin = v3(s.cam_origin[0], s.cam_origin[1], s.cam_origin[2]);
+    b.cam_target = v3(s.cam_target[0], s.cam_target[1], s.cam_target[2]);
+    b.cam_up = v3(s.cam_up[0], s.cam_up[1], s.cam_up[2]);
+    b.fov_x_deg = s.fov_x_deg;
+    b.width = s.width; b.height = s.height;
+    for (int i = 0; i < 3; i++) {
+        b.box_min[i] = s.box_min[i]; b.box_max[i] = s.box_max[i];
+        b.albedo[i] = s.albedo[i]; b.light_intensity[i] = s.light_intensity[i];
+        b.medium.sigma_s[i] = s.medium.sigma_s[i]; b.medium.sigma_a[i] = s.medium.sigma_a[i];
+    }
+    b.light_pos = v3(s.light_pos[0], s.light_pos[1], s.light_pos[2]);
+    b.medium.sampling_weight = s.medium.sampling_weight;
+    b.medium.phase_type = s.medium.phase_type;
+    b.medium.phase_g = s.medium.phase_g;
+    b.medium.resolve();
+    return b;
+}
+}  // namespace host
+}  // namespace alvrl
+
+static int herr(int code, const std::string& m)
+{
+    g_host_err = m;
+    return code;
+}
+
+extern "C" {
+
+ALVRL_API void alvrl_scene_default(alvrl_scene_desc* s, int width, int height)
+{
+    std::memset(s, 0, sizeof(*s));
+    const SmokeBox b;
+    s->cam_origin[0] = b.cam_origin.x; s->cam_origin[1] = b.cam_origin.y; s->cam_origin[2] = b.cam_origin.z;
+    s->cam_target[0] = b.cam_target.x; s->cam_target[1] = b.cam_target.y; s->cam_target[2] = b.cam_target.z;
+    s->cam_up[0] = b.cam_up.x; s->cam_up[1] = b.cam_up.y; s->cam_up[2] = b.cam_up.z;
+    s->fov_x_deg = b.fov_x_deg;
+    s->width = width; s->height = height;
+    for (int i = 0; i < 3; i++) {
+        s->box_min[i] = b.box_min[i]; s->box_max[i] = b.box_max[i];
+        s->albedo[i] = b.albedo[i]; s->light_intensity[i] = b.light_intensity[i];
+        s->medium.sigma_s[i] = b.medium.sigma_s[i]; s->medium.sigma_a[i] = b.medium.sigma_a[i];
+    }
+    s->light_pos[0] = b.light_pos.x; s->light_pos[1] = b.light_pos.y; s->light_pos[2] = b.light_pos.z;
+    s->medium.sampling_weight = -1.0f;
+    s->medium.phase_type = 0;
+    s->medium.phase_g = 0.0f;
+}
+
+ALVRL_API int alvrl_scene_records(const alvrl_scene_desc* s, int medium_scatters, const uint32_t* ids,
+                                  uint32_t n, alvrl_gather_rec* out)
+{
+    if (!s || (!out && n)) return herr(ALVRL_ERR_INVALID, "alvrl_scene_records: null argument");
+    const SmokeBox b = to_box(*s);
+    const uint64_t npix = (uint64_t)b.width * (uint64_t)b.height;
+    if (!ids && n != npix) return herr(ALVRL_ERR_INVALID, "alvrl_scene_records: n must be W*H without pixel ids");
+    const bool scat = medium_scatters && !(b.medium.sigma_s[0] == 0 && b.medium.sigma_s[1] == 0 && b.medium.sigma_s[2] == 0);
+    for (uint32_t i = 0; i < n; i++) {
+        const uint32_t p = ids ? ids[i] : i;
+        if (p >= npix) return herr(ALVRL_ERR_INVALID, "alvrl_scene_records: pixel id out of range");
+        b.make_record((int)(p % (uint32_t)b.width), (int)(p / (uint32_t)b.width), scat,
+                      reinterpret_cast<float*>(&out[i]));
+    }
+    return ALVRL_OK;
+}
+
+ALVRL_API int alvrl_trace_vrls(const alvrl_scene_desc* s, uint32_t seed, uint32_t pass, uint32_t target,
+                               int short_vrls, int max_depth, int rr_depth, float* soa, uint32_t cap,
+                               uint32_t* n, uint64_t* particles)
+{
+    if (!s || !soa || !n || !particles) return herr(ALVRL_ERR_INVALID, "alvrl_trace_vrls: null argument");
+    const SmokeBox b = to_box(*s);
+    const VrlSet v = trace_vrls(b, seed, pass, target, short_vrls != 0, max_depth, rr_depth);
+    if (v.n > cap) return herr(ALVRL_ERR_INVALID, "alvrl_trace_vrls: capacity too small (" + std::to_string(v.n) + " VRLs)");
+    for (int pl = 0; pl < 9; pl++)
+        std::memcpy(soa + (size_t)pl * cap, v.soa.data() + (size_t)pl * v.n, sizeof(float) * v.n);
+    *n = v.n;
+    *particles = v.particle_count;
+    return ALVRL_OK;
+}
+
+ALVRL_API int alvrl_read_vrl_file(const char* path, const alvrl_medium_desc* m, float* soa, uint32_t cap,
+                                  uint32_t* n, uint64_t* particles)
+{
+    if (!path || !m || !n || !particles) return herr(ALVRL_ERR_INVALID, "alvrl_read_vrl_file: null argument");
+    MediumParams mp;
+    for (int i = 0; i < 3; i++) { mp.sigma_s[i] = m->sigma_s[i]; mp.sigma_a[i] = m->sigma_a[i]; }
+    mp.resolve();
+    VrlSet v;
+    std::string err;
+    if (!read_vrl_file(path, mp, &v, &err)) return herr(ALVRL_ERR_INVALID, err);
+    *n = v.n;
+    *particles = v.particle_count;
+    if (!soa) return ALVRL_OK;   // size query
+    if (v.n > cap) return herr(ALVRL_ERR_INVALID, "alvrl_read_vrl_file: capacity too small");
+    for (int pl = 0; pl < 9; pl++)
+        std::memcpy(soa + (size_t)pl * cap, v.soa.data() + (size_t)pl * v.n, sizeof(float) * v.n);
+    return ALVRL_OK;
+}
+
+ALVRL_API int alvrl_write_vrl_file(const char* path, const float* soa, uint32_t n)
+{
+    if (!path || (!soa && n)) return herr(ALVRL_ERR_INVALID, "alvrl_write_vrl_file: null argument");
+    VrlSet v;
+    v.n = n;
+    v.soa.assign(soa, soa + 9 * (size_t)n);
+    std::string err;
+    if (!write_vrl_file(path, v, &err)) return herr(ALVRL_ERR_INVALID, err);
+    return ALVRL_OK;
+}
+
+ALVRL_API const char* alvrl_host_last_error(void) { return g_host_err.c_str(); }
+
+}  // extern "C"

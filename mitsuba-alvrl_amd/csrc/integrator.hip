@@ -1,0 +1,610 @@
+// integrator.hip -- the vrl integrator pipeline on top of include/alvrl.h.
+//
+// Mirrors class vrlIntegrator (src/integrators/vrl/vrlIntegrator.cpp): the
+// same property names and defaults (:128-208), preprocess (:237-267: optional
+// vrlFile, buildSlices), prepass (:270-356: VRLs, representative pixels, R,
+// buildClusters) and rendering (Li -> getClusteredVrlContributions /
+// getVRLContributions for every pixel of the owned tiles).  All per-pair work
+// runs in the HIP kernels behind the C ABI; this file is orchestration.
+#include "../../include/alvrl.h"
+#include "../../include/alvrl_host.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <sstream>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "host/preprocessor.hpp"
+#include "host/scene.hpp"
+
+namespace alvrl {
+namespace host {
+extern thread_local std::string g_host_err;
+SmokeBox to_box(const alvrl_scene_desc& s);
+}  // namespace host
+}  // namespace alvrl
+
+using namespace alvrl::host;
+
+namespace {
+// Clustering stream ids (oracle/alvrl_preproc.h).
+constexpr uint32_t kStageFallbackRefine = 1u, kStageFallbackSample = 2u;
+inline uint32_t stage_slice_refine(uint32_t s) { return 3u + 2u * s; }
+inline uint32_t stage_slice_sample(uint32_t s) { return 4u + 2u * s; }
+
+struct IntegError : std::runtime_error {
+    int code;
+    IntegError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+void chk(int rc, const char* what)
+{
+    if (rc != ALVRL_OK) throw IntegError(rc, std::string(what) + ": " + alvrl_last_error(nullptr));
+}
+void hchk(hipError_t e, const char* what)
+{
+    if (e != hipSuccess) throw IntegError(ALVRL_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+double now_ms()
+{
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+template <class T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    void ensure(size_t cnt)
+    {
+        if (cnt <= n && p) return;
+        if (p) hipFree(p);
+        p = nullptr;
+        n = 0;
+        hchk(hipMalloc(&p, std::max<size_t>(cnt, 1) * sizeof(T)), "hipMalloc");
+        n = cnt;
+    }
+    ~DevBuf() { if (p) hipFree(p); }
+};
+}  // namespace
+
+struct alvrl_integrator {
+    // ---- properties (vrlIntegrator.cpp:128-208; integrator.cpp:272-277, 348-349)
+    bool shortVrls = true;
+    int vrlTargetNum = 500;
+    int maxParticleDepth = -1;
+    int specRRdepth = 100;
+    float initialSpecularThroughput = 20;
+    int volVolSamples = 2, volSurfSamples = 2;
+    bool globalCluster = false;
+    float globalUndersampling = -1;
+    bool localRefinement = true;
+    float localUndersampling = -1;
+    float fallBackUndersampling = 5;
+    int targetNumSlices = 100;
+    float targetPixelUndersampling = 64;
+    float sliceCurvatureFactor = 0.5f;
+    int neighbourCount = 0;
+    float neighbourWeight = 0;
+    int Rsamples = 1;
+    float depthCorrection = 1;
+    bool numVrlFalseColor = false, slicesFalseColor = false, convergenceFalseColor = false;
+    std::string vrlFile;
+    int maxPasses = 1;
+    bool dumpPasses = false;
+    int rrDepth = 5, maxDepth = -1;
+    uint32_t seed = 0xA1B2C3D4u, vrlSeed = 0x5EED0001u;
+    // ---- state
+    int device = 0;
+    alvrl_ctx* ctx = nullptr;
+    hipStream_t stream = nullptr;
+    SmokeBox scene;
+    bool have_scene = false;
+    std::unique_ptr<Preprocessor> prep;
+    std::vector<uint32_t> pixel_to_slice;   // y + H*x
+    VrlSet vrls;
+    bool vrls_from_file = false;
+    uint32_t uploaded_pass = 0xFFFFFFFFu;
+    bool clustered = false;
+    // R
+    DevBuf<float> Rt;
+    DevBuf<alvrl_gather_rec> rep_recs;
+    DevBuf<uint32_t> rep_ids;
+    // cluster info (vrlClusterInfo)
+    std::vector<uint32_t> slice_off, reps, fb_reps;
+    std::vector<float> weights, fb_w;
+    // render cache per (rank, world)
+    uint32_t cache_rank = 0xFFFFFFFFu, cache_world = 0, cache_mode = 0;
+    DevBuf<alvrl_gather_rec> rec_buf;
+    DevBuf<uint32_t> pix_buf;
+    DevBuf<alvrl_work_item> item_buf;
+    DevBuf<float> out_buf;
+    uint32_t nrec = 0, nitems = 0;
+    alvrl_integrator_stats st{};
+
+    ~alvrl_integrator()
+    {
+        if (ctx) alvrl_ctx_destroy(ctx);
+        if (stream) hipStreamDestroy(stream);
+    }
+
+    void set(const std::string& k, const std::string& v)
+    {
+        auto b = [&](const std::string& x) {
+            if (x == "true" || x == "1" || x == "yes") return true;
+            if (x == "false" || x == "0" || x == "no") return false;
+            throw IntegError(ALVRL_ERR_INVALID, "bad boolean for " + k + ": " + x);
+        };
+        auto i = [&](const std::string& x) { return (int)std::stol(x, nullptr, 0); };
+        auto f = [&](const std::string& x) { return std::stof(x); };
+        if (k == "nc") throw IntegError(ALVRL_ERR_INVALID, "Neighbourcount is now called 'neighbourCount' instead of 'nc'!");
+        else if (k == "shortVrls") shortVrls = b(v);
+        else if (k == "vrlTargetNum") vrlTargetNum = i(v);
+        else if (k == "maxParticleDepth") maxParticleDepth = i(v);
+        else if (k == "specularForcedRRdepth") specRRdepth = i(v);
+        else if (k == "initialSpecularThroughput") initialSpecularThroughput = f(v);
+        else if (k == "volVolSamples") volVolSamples = i(v);
+        else if (k == "volSurfSamples") volSurfSamples = i(v);
+        else if (k == "globalCluster") globalCluster = b(v);
+        else if (k == "globalUndersampling") globalUndersampling = f(v);
+        else if (k == "localRefinement") localRefinement = b(v);
+        else if (k == "localUndersampling") localUndersampling = f(v);
+        else if (k == "fallBackUndersampling") fallBackUndersampling = f(v);
+        else if (k == "targetNumSlices") targetNumSlices = i(v);
+        else if (k == "targetPixelUndersampling") targetPixelUndersampling = f(v);
+        else if (k == "sliceCurvatureFactor") sliceCurvatureFactor = f(v);
+        else if (k == "neighbourCount") neighbourCount = i(v);
+        else if (k == "neighbourWeight") neighbourWeight = f(v);
+        else if (k == "Rsamples") Rsamples = i(v);
+        else if (k == "depthCorrection") depthCorrection = f(v);
+        else if (k == "numVrlFalseColor") numVrlFalseColor = b(v);
+        else if (k == "slicesFalseColor") slicesFalseColor = b(v);
+        else if (k == "convergenceFalseColor") convergenceFalseColor = b(v);
+        else if (k == "vrlFile") vrlFile = v;
+        else if (k == "maxPasses") maxPasses = i(v);
+        else if (k == "dumpPasses") dumpPasses = b(v);
+        else if (k == "rrDepth") rrDepth = i(v);
+        else if (k == "maxDepth") maxDepth = i(v);
+        else if (k == "seed") seed = (uint32_t)std::stoul(v, nullptr, 0);
+        else if (k == "vrlSeed") vrlSeed = (uint32_t)std::stoul(v, nullptr, 0);
+        else throw IntegError(ALVRL_ERR_INVALID, "unknown vrl integrator property '" + k + "'");
+    }
+
+    void validate()
+    {
+        if (volVolSamples != 0 && volVolSamples < 2)
+            throw IntegError(ALVRL_ERR_INVALID, "Need at least 2 volVolSamples for variance estimate, but received: " + std::to_string(volVolSamples));
+        if (volSurfSamples != 0 && volSurfSamples < 2)
+            throw IntegError(ALVRL_ERR_INVALID, "Need at least 2 volSurfSamples for variance estimate, but received: " + std::to_string(volSurfSamples));
+        if (targetNumSlices < 1) throw IntegError(ALVRL_ERR_INVALID, "Invalid target number of slices!");
+        if (Rsamples != 1) throw IntegError(ALVRL_ERR_INVALID, "Rsamples != 1 is not supported by this build");
+        if (globalCluster) throw IntegError(ALVRL_ERR_INVALID, "globalCluster=true is not supported by this build yet");
+        if (numVrlFalseColor || slicesFalseColor || convergenceFalseColor)
+            throw IntegError(ALVRL_ERR_INVALID, "false-colour debug modes are not supported by this build yet");
+        clustered = globalCluster || localRefinement;
+    }
+
+    void preprocess(const alvrl_scene_desc& s)
+    {
+        scene = to_box(s);
+        have_scene = true;
+        alvrl_medium_desc md = s.medium;
+        chk(alvrl_set_medium(ctx, &md), "alvrl_set_medium");
+        if (!vrlFile.empty()) {   // :243-252
+            std::string err;
+            if (!read_vrl_file(vrlFile.c_str(), scene.medium, &vrls, &err)) throw IntegError(ALVRL_ERR_INVALID, err);
+            vrls_from_file = true;
+        }
+        if (clustered) {          // :254-265
+            PrepParams pp;
+            pp.target_num_slices = (uint32_t)targetNumSlices;
+            pp.neighbour_count = (uint32_t)neighbourCount;
+            pp.neighbour_weight = neighbourWeight;
+            pp.slice_curvature_factor = sliceCurvatureFactor;
+            pp.seed = seed;
+            pp.pass = 0;
+            prep.reset(new Preprocessor(pp));
+            const double t0 = now_ms();
+            pixel_to_slice = prep->build_slices(scene);
+            st.ms_slices = now_ms() - t0;
+            st.slices = prep->num_slices();
+        }
+        cache_rank = 0xFFFFFFFFu;
+    }
+
+    void prepass(uint32_t pass)
+    {
+        if (!have_scene) throw IntegError(ALVRL_ERR_STATE, "prepass before preprocess");
+        const double tw = now_ms();
+        chk(alvrl_set_pass(ctx, pass), "alvrl_set_pass");
+        // VRLs (:276-287): traced per pass unless preloaded from a file
+        if (!vrls_from_file) {
+            const double t0 = now_ms();
+            vrls = trace_vrls(scene, vrlSeed, pass, (uint32_t)std::max(vrlTargetNum, 0), shortVrls,
+                              maxParticleDepth, rrDepth);
+            st.ms_trace = now_ms() - t0;
+            uploaded_pass = 0xFFFFFFFFu;
+        }
+        if (!vrls_from_file || uploaded_pass == 0xFFFFFFFFu) {
+            chk(alvrl_upload_vrls(ctx, vrls.soa.data(), vrls.n, std::max<uint64_t>(vrls.particle_count, 1), 0),
+                "alvrl_upload_vrls");
+            uploaded_pass = pass;
+        }
+        st.vrls = vrls.n;
+        st.particles = vrls.particle_count;
+        st.slices_failed = 0;
+        st.fallback_built = 0;
+        st.ms_rbuild = st.ms_refine = 0;
+        if (clustered) build_clusters(pass);
+        st.ms_prepass_wall = now_ms() - tw;
+    }
+
+    void build_clusters(uint32_t pass_id)
+    {
+        const uint32_t nv = vrls.n;
+        // sampleSliceMapping (:293-296)
+        prep->set_pass(pass_id);
+        prep->sample_slice_mapping(targetPixelUndersampling);
+        const auto& roff = prep->rep_off();
+        const auto& rpix = prep->rep_pix();
+        const uint32_t ns = prep->num_slices();
+        const uint32_t rows = roff[ns];
+        st.rep_rows = rows;
+        // records of the representative pixel centres (sensor->sampleRay at the
+        // pixel centre, :327-328 / :1060-1061); RNG id = row-major pixel id
+        std::vector<alvrl_gather_rec> h(rows);
+        std::vector<uint32_t> ids(rows);
+        const int H = scene.height, W = scene.width;
+        const bool scat = !(scene.medium.sigma_s[0] == 0 && scene.medium.sigma_s[1] == 0 && scene.medium.sigma_s[2] == 0);
+        for (uint32_t r = 0; r < rows; r++) {
+            const uint32_t x = rpix[r] / (uint32_t)H, y = rpix[r] % (uint32_t)H;
+            scene.make_record((int)x, (int)y, scat, reinterpret_cast<float*>(&h[r]));
+            ids[r] = y * (uint32_t)W + x;
+        }
+        rep_recs.ensure(rows);
+        rep_ids.ensure(rows);
+        Rt.ensure((size_t)2 * nv * rows);
+        hchk(hipMemcpyAsync(rep_recs.p, h.data(), sizeof(alvrl_gather_rec) * rows, hipMemcpyHostToDevice, stream), "copy rep records");
+        hchk(hipMemcpyAsync(rep_ids.p, ids.data(), sizeof(uint32_t) * rows, hipMemcpyHostToDevice, stream), "copy rep ids");
+        // Building R (:302-333)
+        hipEvent_t e0, e1;
+        hchk(hipEventCreate(&e0), "event"); hchk(hipEventCreate(&e1), "event");
+        hchk(hipEventRecord(e0, stream), "event");
+        chk(alvrl_build_R(ctx, rep_recs.p, rep_ids.p, rows, Rt.p, rows, 0, stream), "alvrl_build_R");
+        hchk(hipEventRecord(e1, stream), "event");
+        // Preprocessor::cluster (:838-898): non-zero VRLs in one cluster, zero VRLs in another
+        std::vector<uint8_t> nz(nv, 0);
+        chk(alvrl_nonzero_columns(ctx, Rt.p, rows, rows, nz.data(), stream), "alvrl_nonzero_columns");
+        float ms = 0;
+        hchk(hipEventElapsedTime(&ms, e0, e1), "event");
+        st.ms_rbuild = ms;
+        hipEventDestroy(e0); hipEventDestroy(e1);
+        std::vector<uint32_t> init;
+        init.reserve(nv);
+        for (uint32_t v = 0; v < nv; v++) if (nz[v]) init.push_back(v);
+        const uint32_t nnz = (uint32_t)init.size();
+        for (uint32_t v = 0; v < nv; v++) if (!nz[v]) init.push_back(v);
+        std::vector<uint32_t> init_off{0};
+        if (nnz) init_off.push_back(nnz);
+        if (nnz != nv) init_off.push_back(nv);
+        // refinePerSlice (:199-252): one device job per slice
+        std::vector<std::vector<uint32_t>> lrows(ns);
+        std::vector<std::vector<double>> lw(ns);
+        std::vector<alvrl_cluster_job> jobs(ns);
+        for (uint32_t s = 0; s < ns; s++) {
+            prep->local_matrix(s, &lrows[s], &lw[s]);
+            alvrl_cluster_job& j = jobs[s];
+            j.rows = lrows[s].data();
+            j.locw = lw[s].data();
+            j.nrows = (uint32_t)lrows[s].size();
+            j.pixel_undersampling = prep->slice_undersampling()[s];
+            j.undersampling = localUndersampling;
+            j.depth_correction = depthCorrection;
+            j.do_refine = localRefinement ? 1 : 0;
+            j.stage_refine = stage_slice_refine(s);
+            j.stage_sample = stage_slice_sample(s);
+        }
+        std::vector<uint32_t> off(ns + 1), rep((size_t)ns * nv + 1);
+        std::vector<float> w((size_t)ns * nv + 1);
+        std::vector<int> refined(ns + 1);
+        const double t0 = now_ms();
+        chk(alvrl_refine(ctx, Rt.p, rows, ns, jobs.data(), init.data(), init_off.data(),
+                         (uint32_t)init_off.size() - 1, off.data(), rep.data(), w.data(),
+                         refined.data(), stream), "alvrl_refine (slices)");
+        st.ms_refine = now_ms() - t0;
+        // Fall-back clustering (buildClusters :175-186): refine the global
+        // clustering of all rows to N/fallBackUndersampling clusters.  Only its
+        // users need it -- slices whose refinement failed (:276-282) and pixels
+        // without a gather point (:564-571) -- and its counter-RNG streams are
+        // its own, so it is built only when one of them exists.
+        uint32_t failed = 0;
+        for (uint32_t s = 0; s < ns; s++) failed += refined[s] ? 0 : 1;
+        bool need_fb = failed > 0;
+        for (uint32_t p : pixel_to_slice) if (p == 0xFFFFFFFFu) { need_fb = true; break; }
+        fb_reps.clear(); fb_w.clear();
+        if (need_fb) {
+            std::vector<uint32_t> all(rows);
+            for (uint32_t r = 0; r < rows; r++) all[r] = r;
+            std::vector<double> dw(rows, 1.0 / (double)rows);
+            alvrl_cluster_job fj;
+            fj.rows = all.data(); fj.locw = dw.data(); fj.nrows = rows;
+            fj.pixel_undersampling = prep->global_pixel_undersampling();
+            fj.undersampling = fallBackUndersampling;
+            fj.depth_correction = 1.0f;
+            fj.do_refine = 1;
+            fj.stage_refine = kStageFallbackRefine;
+            fj.stage_sample = kStageFallbackSample;
+            std::vector<uint32_t> foff(2), frep(nv + 1);
+            std::vector<float> fw(nv + 1);
+            int fref = 0;
+            const double t1 = now_ms();
+            chk(alvrl_refine(ctx, Rt.p, rows, 1, &fj, init.data(), init_off.data(),
+                             (uint32_t)init_off.size() - 1, foff.data(), frep.data(), fw.data(), &fref,
+                             stream), "alvrl_refine (fall-back)");
+            st.ms_refine += now_ms() - t1;
+            if (!fref) throw IntegError(ALVRL_ERR_NUMERIC, "couldn't refine global clustering! (but all VRLs should be non-zero!)");
+            fb_reps.assign(frep.begin(), frep.begin() + foff[1]);
+            fb_w.assign(fw.begin(), fw.begin() + foff[1]);
+            st.fallback_built = 1;
+        }
+        slice_off.assign(ns + 1, 0);
+        reps.clear(); weights.clear();
+        for (uint32_t s = 0; s < ns; s++) {
+            slice_off[s] = (uint32_t)reps.size();
+            if (refined[s]) {
+                reps.insert(reps.end(), rep.begin() + off[s], rep.begin() + off[s + 1]);
+                weights.insert(weights.end(), w.begin() + off[s], w.begin() + off[s + 1]);
+            } else {   // "Could not refine slice %d, using fall-back clustering!"
+                reps.insert(reps.end(), fb_reps.begin(), fb_reps.end());
+                weights.insert(weights.end(), fb_w.begin(), fb_w.end());
+            }
+        }
+        slice_off[ns] = (uint32_t)reps.size();
+        st.slices_failed = failed;
+        st.clusters_total = reps.size();
+        chk(alvrl_set_clusters(ctx, ns, slice_off.data(), reps.data(), weights.data(), fb_reps.data(),
+                               fb_w.data(), (uint32_t)fb_reps.size()), "alvrl_set_clusters");
+    }
+
+    void prepare_render(uint32_t rank, uint32_t world)
+    {
+        const uint32_t mode = clustered ? 2u : 1u;
+        if (cache_rank == rank && cache_world == world && cache_mode == mode) return;
+        const int W = scene.width, H = scene.height, T = 64;
+        const int tx = (W + T - 1) / T, ty = (H + T - 1) / T;
+        std::vector<uint32_t> pix;
+        for (int t = 0; t < tx * ty; t++) {
+            if ((uint32_t)t % world != rank) continue;
+            const int x0 = (t % tx) * T, y0 = (t / tx) * T;
+            for (int y = y0; y < std::min(y0 + T, H); y++)
+                for (int x = x0; x < std::min(x0 + T, W); x++) pix.push_back((uint32_t)(y * W + x));
+        }
+        std::vector<alvrl_work_item> items;
+        if (clustered) {   // bucket by slice (stable), wave work items
+            std::vector<uint32_t> sl(pix.size());
+            for (size_t i = 0; i < pix.size(); i++) {
+                const uint32_t x = pix[i] % (uint32_t)W, y = pix[i] / (uint32_t)W;
+                sl[i] = pixel_to_slice[y + (uint32_t)H * x];   // m_slices[y + H*x] (:560)
+            }
+            std::vector<uint32_t> perm(pix.size());
+            for (size_t i = 0; i < perm.size(); i++) perm[i] = (uint32_t)i;
+            std::stable_sort(perm.begin(), perm.end(), [&](uint32_t a, uint32_t b) { return sl[a] < sl[b]; });
+            std::vector<uint32_t> p2(pix.size()), s2(pix.size());
+            for (size_t i = 0; i < perm.size(); i++) { p2[i] = pix[perm[i]]; s2[i] = sl[perm[i]]; }
+            pix.swap(p2);
+            items.resize(pix.size() + 1);
+            const uint32_t n = alvrl_make_work_items(s2.data(), (uint32_t)s2.size(), items.data(), (uint32_t)items.size());
+            items.resize(n);
+        }
+        std::vector<alvrl_gather_rec> recs(pix.size());
+        const bool scat = !(scene.medium.sigma_s[0] == 0 && scene.medium.sigma_s[1] == 0 && scene.medium.sigma_s[2] == 0);
+        for (size_t i = 0; i < pix.size(); i++)
+            scene.make_record((int)(pix[i] % (uint32_t)W), (int)(pix[i] / (uint32_t)W), scat,
+                              reinterpret_cast<float*>(&recs[i]));
+        nrec = (uint32_t)pix.size();
+        nitems = (uint32_t)items.size();
+        rec_buf.ensure(nrec);
+        pix_buf.ensure(nrec);
+        out_buf.ensure((size_t)3 * nrec);
+        hchk(hipMemcpyAsync(rec_buf.p, recs.data(), sizeof(alvrl_gather_rec) * nrec, hipMemcpyHostToDevice, stream), "copy records");
+        hchk(hipMemcpyAsync(pix_buf.p, pix.data(), sizeof(uint32_t) * nrec, hipMemcpyHostToDevice, stream), "copy pixels");
+        if (nitems) {
+            item_buf.ensure(nitems);
+            hchk(hipMemcpyAsync(item_buf.p, items.data(), sizeof(alvrl_work_item) * nitems, hipMemcpyHostToDevice, stream), "copy items");
+        }
+        hchk(hipStreamSynchronize(stream), "sync");
+        cache_rank = rank; cache_world = world; cache_mode = mode;
+    }
+
+    void render(uint32_t rank, uint32_t world, float* d_fb, hipStream_t s)
+    {
+        if (!have_scene) throw IntegError(ALVRL_ERR_STATE, "render before preprocess");
+        if (world == 0 || rank >= world) throw IntegError(ALVRL_ERR_INVALID, "bad rank/world");
+        prepare_render(rank, world);
+        // the caller's stream waits for the records upload (done, synchronous above)
+        if (clustered)
+            chk(alvrl_gather_clustered(ctx, rec_buf.p, pix_buf.p, item_buf.p, nitems, out_buf.p, s), "alvrl_gather_clustered");
+        else
+            chk(alvrl_gather_brute(ctx, rec_buf.p, pix_buf.p, nrec, out_buf.p, s), "alvrl_gather_brute");
+        chk(alvrl_accumulate_rgb(ctx, out_buf.p, pix_buf.p, nrec, d_fb, s), "alvrl_accumulate_rgb");
+    }
+};
+
+static int ierr(int code, const std::string& m)
+{
+    g_host_err = m;
+    return code;
+}
+
+#define GUARD(...)                                                           \
+    try {                                                                    \
+        __VA_ARGS__;                                                         \
+    } catch (const IntegError& e) {                                          \
+        return ierr(e.code, e.what());                                       \
+    } catch (const std::exception& e) {                                      \
+        return ierr(ALVRL_ERR_INVALID, e.what());                            \
+    }
+
+extern "C" {
+
+ALVRL_API int alvrl_integrator_create(const char* props, int device, alvrl_integrator** out)
+{
+    if (!out) return ierr(ALVRL_ERR_INVALID, "alvrl_integrator_create: null out");
+    std::unique_ptr<alvrl_integrator> it(new alvrl_integrator());
+    GUARD({
+        std::string p = props ? props : "";
+        std::stringstream ss(p);
+        std::string kv;
+        while (std::getline(ss, kv, ';')) {
+            const auto a = kv.find_first_not_of(" \t\n");
+            if (a == std::string::npos) continue;
+            kv = kv.substr(a);
+            const auto eq = kv.find('=');
+            if (eq == std::string::npos) throw IntegError(ALVRL_ERR_INVALID, "property without '=': " + kv);
+            std::string k = kv.substr(0, eq), v = kv.substr(eq + 1);
+            while (!k.empty() && (k.back() == ' ' || k.back() == '\t')) k.pop_back();
+            it->set(k, v);
+        }
+        it->validate();
+        it->device = device;
+        alvrl_config cfg{device, it->volVolSamples, it->volSurfSamples, it->shortVrls ? 1 : 0, it->seed};
+        chk(alvrl_ctx_create(&cfg, &it->ctx), "alvrl_ctx_create");
+        hchk(hipSetDevice(device), "hipSetDevice");
+        hchk(hipStreamCreateWithFlags(&it->stream, hipStreamNonBlocking), "hipStreamCreate");
+    });
+    *out = it.release();
+    return ALVRL_OK;
+}
+
+ALVRL_API void alvrl_integrator_destroy(alvrl_integrator* it) { delete it; }
+
+ALVRL_API int alvrl_integrator_preprocess(alvrl_integrator* it, const alvrl_scene_desc* s)
+{
+    if (!it || !s) return ierr(ALVRL_ERR_INVALID, "alvrl_integrator_preprocess: null argument");
+    GUARD({ hchk(hipSetDevice(it->device), "hipSetDevice"); it->preprocess(*s); });
+    return ALVRL_OK;
+}
+
+ALVRL_API int alvrl_integrator_prepass(alvrl_integrator* it, uint32_t pass)
+{
+    if (!it) return ierr(ALVRL_ERR_INVALID, "alvrl_integrator_prepass: null argument");
+    GUARD({ hchk(hipSetDevice(it->device), "hipSetDevice"); it->prepass(pass); });
+    return ALVRL_OK;
+}
+
+ALVRL_API int alvrl_integrator_render(alvrl_integrator* it, uint32_t rank, uint32_t world, float* d_fb,
+                                      void* stream)
+{
+    if (!it || !d_fb) return ierr(ALVRL_ERR_INVALID, "alvrl_integrator_render: null argument");
+    GUARD({
+        hchk(hipSetDevice(it->device), "hipSetDevice");
+        it->render(rank, world, d_fb, stream ? (hipStream_t)stream : it->stream);
+    });
+    return ALVRL_OK;
+}
+
+ALVRL_API int alvrl_integrator_set_vrls(alvrl_integrator* it, const float* soa, uint32_t n,
+                                        uint64_t particle_count)
+{
+    if (!it || (!soa && n)) return ierr(ALVRL_ERR_INVALID, "alvrl_integrator_set_vrls: null argument");
+    if (n && particle_count == 0) return ierr(ALVRL_ERR_INVALID, "alvrl_integrator_set_vrls: particle_count must be > 0");
+    GUARD({
+        it->vrls.n = n;
+        it->vrls.particle_count = particle_count;
+        it->vrls.soa.assign(soa, soa + 9 * (size_t)n);
+        it->vrls_from_file = true;
+        it->uploaded_pass = 0xFFFFFFFFu;
+    });
+    return ALVRL_OK;
+}
+
+ALVRL_API int alvrl_integrator_get_stats(alvrl_integrator* it, alvrl_integrator_stats* st)
+{
+    if (!it || !st) return ierr(ALVRL_ERR_INVALID, "alvrl_integrator_get_stats: null argument");
+    GUARD({
+        uint64_t pre = 0, ren = 0;
+        chk(alvrl_get_stats(it->ctx, &pre, &ren), "alvrl_get_stats");
+        it->st.contrib_preprocess = pre;
+        it->st.contrib_render = ren;
+        float ms = 0;
+        if (alvrl_last_kernel_ms(it->ctx, &ms) == ALVRL_OK) it->st.ms_render_kernel = ms;
+        *st = it->st;
+    });
+    return ALVRL_OK;
+}
+
+ALVRL_API alvrl_ctx* alvrl_integrator_ctx(alvrl_integrator* it) { return it ? it->ctx : nullptr; }
+
+ALVRL_API uint32_t alvrl_integrator_num_slices(alvrl_integrator* it)
+{
+    return (it && it->prep) ? it->prep->num_slices() : 0;
+}
+
+ALVRL_API int alvrl_integrator_slices(alvrl_integrator* it, uint32_t* p2s, uint32_t n)
+{
+    if (!it || !p2s) return ierr(ALVRL_ERR_INVALID, "alvrl_integrator_slices: null argument");
+    if (n < it->pixel_to_slice.size()) return ierr(ALVRL_ERR_INVALID, "alvrl_integrator_slices: buffer too small");
+    std::copy(it->pixel_to_slice.begin(), it->pixel_to_slice.end(), p2s);
+    return ALVRL_OK;
+}
+
+ALVRL_API int alvrl_integrator_reps(alvrl_integrator* it, uint32_t* rep_off, uint32_t* rep_pix, uint32_t cap)
+{
+    if (!it || !it->prep || !rep_off || !rep_pix) return ierr(ALVRL_ERR_INVALID, "alvrl_integrator_reps: no slices");
+    const auto& o = it->prep->rep_off();
+    const auto& p = it->prep->rep_pix();
+    if (cap < p.size()) return ierr(ALVRL_ERR_INVALID, "alvrl_integrator_reps: buffer too small");
+    std::copy(o.begin(), o.end(), rep_off);
+    std::copy(p.begin(), p.end(), rep_pix);
+    return ALVRL_OK;
+}
+
+ALVRL_API int alvrl_integrator_clusters(alvrl_integrator* it, uint32_t* slice_off, uint32_t* reps,
+                                        float* weights, uint32_t cap, uint32_t* fb_reps, float* fb_w,
+                                        uint32_t fb_cap, uint32_t* n_fb)
+{
+    if (!it || !slice_off || !reps || !weights || !n_fb) return ierr(ALVRL_ERR_INVALID, "alvrl_integrator_clusters: null argument");
+    if (cap < it->reps.size() || fb_cap < it->fb_reps.size()) return ierr(ALVRL_ERR_INVALID, "alvrl_integrator_clusters: buffer too small");
+    std::copy(it->slice_off.begin(), it->slice_off.end(), slice_off);
+    std::copy(it->reps.begin(), it->reps.end(), reps);
+    std::copy(it->weights.begin(), it->weights.end(), weights);
+    if (fb_reps) std::copy(it->fb_reps.begin(), it->fb_reps.end(), fb_reps);
+    if (fb_w) std::copy(it->fb_w.begin(), it->fb_w.end(), fb_w);
+    *n_fb = (uint32_t)it->fb_reps.size();
+    return ALVRL_OK;
+}
+
+ALVRL_API int alvrl_integrator_R(alvrl_integrator* it, float* out, uint64_t cap)
+{
+    if (!it || !out) return ierr(ALVRL_ERR_INVALID, "alvrl_integrator_R: null argument");
+    const uint64_t need = (uint64_t)2 * it->vrls.n * it->st.rep_rows;
+    if (cap < need) return ierr(ALVRL_ERR_INVALID, "alvrl_integrator_R: buffer too small");
+    GUARD({
+        hchk(hipSetDevice(it->device), "hipSetDevice");
+        hchk(hipStreamSynchronize(it->stream), "sync");
+        if (need) hchk(hipMemcpy(out, it->Rt.p, need * sizeof(float), hipMemcpyDeviceToHost), "copy R");
+    });
+    return ALVRL_OK;
+}
+
+ALVRL_API int alvrl_integrator_vrls(alvrl_integrator* it, float* soa, uint32_t cap, uint32_t* n, uint64_t* particles)
+{
+    if (!it || !n || !particles) return ierr(ALVRL_ERR_INVALID, "alvrl_integrator_vrls: null argument");
+    *n = it->vrls.n;
+    *particles = it->vrls.particle_count;
+    if (!soa) return ALVRL_OK;
+    if (cap < it->vrls.n) return ierr(ALVRL_ERR_INVALID, "alvrl_integrator_vrls: buffer too small");
+    for (int pl = 0; pl < 9; pl++)
+        std::memcpy(soa + (size_t)pl * cap, it->vrls.soa.data() + (size_t)pl * it->vrls.n, sizeof(float) * it->vrls.n);
+    return ALVRL_OK;
+}
+
+}  // extern "C"

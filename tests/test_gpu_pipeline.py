@@ -1,0 +1,135 @@
+"""End-to-end parity of the vrl integrator pipeline (libalvrl.so host side +
+HIP kernels) with the oracle's restatement of vrlIntegrator + Preprocessor, on
+BASELINE.json configs[0]-shaped inputs (C1: 256^2 smoke box, 1k VRLs, ALVRL
+defaults) and variants.
+
+  * slicing and representative pixels: bit-exact (host code, same streams);
+  * R: within the tolerance of test_gpu_parity (device maths);
+  * clusters: the oracle's buildClusters run on the DEVICE's R must give
+    bit-identical per-slice representatives and weights;
+  * frame: the oracle's clustered gather with those clusters vs the device
+    frame, within test_gpu_parity's tolerance.
+"""
+import numpy as np
+import pytest
+
+from test_gpu_parity import _assert_close, _assert_close_pairs
+
+pytestmark = pytest.mark.gpu
+
+SEED_VRL = 0x5EED0001
+SEED_RNG = 0xA1B2C3D4
+
+
+def _run(props, w, h, nvrl, oracle, pass_=0, prep_kw=None):
+    import torch
+    import alvrl
+    from oracle import Prep
+    scene = alvrl.scene_default(w, h)
+    vrls, pc = alvrl.trace_vrls(scene, nvrl, seed=SEED_VRL)
+    it = alvrl.Integrator(props + f";seed={SEED_RNG}", device=0)
+    it.set_vrls(vrls, pc)
+    it.preprocess(scene)
+    it.prepass(pass_)
+    fb = torch.zeros(w * h * 3, dtype=torch.float32, device="cuda")
+    it.render(fb)
+    torch.cuda.synchronize()
+    img = fb.view(h * w, 3).cpu().numpy()
+
+    pp = oracle.prep_params(seed=SEED_RNG, pass_=0, **(prep_kw or {}))
+    prep = Prep(oracle, pp)
+    osc = oracle.scene(w, h)
+    p2s = prep.build_slices(osc)
+    assert np.array_equal(p2s, it.slices()), "slices differ"
+    off, pix, su, gu = prep.sample_slice_mapping(64.0, w * h)
+    ioff, ipix = it.reps()
+    assert np.array_equal(off, ioff) and np.array_equal(pix, ipix), "representatives differ"
+    return it, img, prep, vrls, pc, p2s
+
+
+def test_c1_pipeline_adaptive(oracle, gpu_ok):
+    w = h = 256
+    it, img, prep, vrls, pc, p2s = _run("", w, h, 1000, oracle)
+    st = it.stats()
+    assert st["slices"] == 100 and st["slices_failed"] == 0
+    # R of the device against the oracle's R rows
+    Rg = it.R()                                        # [nv, rows, 2]
+    ioff, ipix = it.reps()
+    xs, ys = ipix // h, ipix % h                       # column-major ids -> (x, y)
+    rec_ids = (ys * w + xs).astype(np.uint32)
+    recs = oracle.records(oracle.scene(w, h))[rec_ids]
+    P = oracle.params(oracle.medium(), seed=SEED_RNG, pass_=0)
+    _, Rc, cnt = oracle.gather_brute(P, recs, vrls, pc, rec_ids=rec_ids, domain=2, want_R=True)
+    assert st["contrib_preprocess"] == cnt
+    _assert_close_pairs(Rg[..., 0].T, Rc[..., 0], "C1 R mean")
+    # buildClusters on the device's R: bit-exact per-slice lists
+    ocl = prep.build_clusters(Rg)
+    icl = it.clusters()
+    assert np.array_equal(ocl["slice_off"], icl["slice_off"])
+    assert np.array_equal(ocl["reps"], icl["reps"])
+    assert np.array_equal(ocl["weights"].view(np.uint32), icl["weights"].view(np.uint32))
+    print(f"C1: {len(icl['reps'])} representatives over {st['slices']} slices, "
+          f"refine {st['ms_refine']:.1f} ms, R {st['ms_rbuild']:.2f} ms")
+    # the frame
+    pid = np.arange(w * h, dtype=np.uint32)
+    sl = p2s[(pid % w) * h + pid // w]
+    cpu, ccnt = oracle.gather_clustered(P, oracle.records(oracle.scene(w, h)), sl, vrls, pc,
+                                        icl["slice_off"], icl["reps"], icl["weights"],
+                                        icl["fb_reps"], icl["fb_weights"], rec_ids=pid)
+    assert st["contrib_render"] == ccnt
+    _assert_close(img, cpu, "C1 frame")
+
+
+@pytest.mark.parametrize("props,prep_kw", [
+    ("localUndersampling=20", {}),
+    ("neighbourCount=3;neighbourWeight=0.5", {"neighbour_count": 3, "neighbour_weight": 0.5}),
+    ("localRefinement=false;globalCluster=false", None),
+])
+def test_pipeline_variants(oracle, gpu_ok, props, prep_kw):
+    import alvrl
+    w, h = 128, 96
+    if prep_kw is None:   # brute force: no slices
+        import torch
+        scene = alvrl.scene_default(w, h)
+        vrls, pc = alvrl.trace_vrls(scene, 600, seed=SEED_VRL)
+        it = alvrl.Integrator(props + f";seed={SEED_RNG}", device=0)
+        it.set_vrls(vrls, pc)
+        it.preprocess(scene)
+        it.prepass(3)
+        fb = torch.zeros(w * h * 3, dtype=torch.float32, device="cuda")
+        it.render(fb)
+        torch.cuda.synchronize()
+        P = oracle.params(oracle.medium(), seed=SEED_RNG, pass_=3)
+        cpu, _ = oracle.gather_brute(P, oracle.records(oracle.scene(w, h)), vrls, pc)
+        _assert_close(fb.view(-1, 3).cpu().numpy(), cpu, "brute pipeline")
+        return
+    pk = dict(target_num_slices=100)
+    pk.update(prep_kw)
+    under = float(props.split("localUndersampling=")[1]) if "localUndersampling=" in props else -1.0
+    pk["local_undersampling"] = under
+    it, img, prep, vrls, pc, p2s = _run(props, w, h, 600, oracle, prep_kw=pk)
+    ocl = prep.build_clusters(it.R())
+    icl = it.clusters()
+    assert np.array_equal(ocl["reps"], icl["reps"])
+    assert np.array_equal(ocl["weights"].view(np.uint32), icl["weights"].view(np.uint32))
+
+
+def test_tile_sharding_covers_frame(gpu_ok):
+    """Ranks' tile sets partition the frame: the sum of 3 'rank' renders equals
+    the 1-rank render bit for bit (each pixel is written by exactly one rank)."""
+    import torch
+    import alvrl
+    w, h = 200, 130
+    scene = alvrl.scene_default(w, h)
+    vrls, pc = alvrl.trace_vrls(scene, 300, seed=SEED_VRL)
+    it = alvrl.Integrator(f"localRefinement=false;seed={SEED_RNG}", device=0)
+    it.set_vrls(vrls, pc)
+    it.preprocess(scene)
+    it.prepass(0)
+    full = torch.zeros(w * h * 3, device="cuda")
+    it.render(full)
+    parts = torch.zeros(w * h * 3, device="cuda")
+    for r in range(3):
+        it.render(parts, rank=r, world=3)
+    torch.cuda.synchronize()
+    assert torch.equal(full, parts)
