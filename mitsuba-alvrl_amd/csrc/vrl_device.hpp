@@ -110,9 +110,9 @@ __device__ __forceinline__ void medium_tr(const DevParams& P, float d, float tr[
 {
     // HomogeneousMedium::eval (homogeneous.cpp:354-396): the pdf exponentials
     // and the transmittance exponentials are the same values.
-    const float t0 = expf(P.sigma_t[0] * (-d));
-    const float t1 = expf(P.sigma_t[1] * (-d));
-    const float t2 = expf(P.sigma_t[2] * (-d));
+    const float t0 = __expf(P.sigma_t[0] * (-d));
+    const float t1 = __expf(P.sigma_t[1] * (-d));
+    const float t2 = __expf(P.sigma_t[2] * (-d));
     float s = 0.0f;
     s += t0; s += t1; s += t2;
     s /= 3;
@@ -123,9 +123,9 @@ __device__ __forceinline__ void medium_tr(const DevParams& P, float d, float tr[
 
 __device__ __forceinline__ void medium_tr_only(const DevParams& P, float d, float tr[3])
 {
-    const float t0 = expf(P.sigma_t[0] * (-d));
-    const float t1 = expf(P.sigma_t[1] * (-d));
-    const float t2 = expf(P.sigma_t[2] * (-d));
+    const float t0 = __expf(P.sigma_t[0] * (-d));
+    const float t1 = __expf(P.sigma_t[1] * (-d));
+    const float t2 = __expf(P.sigma_t[2] * (-d));
     const bool z = fmax3(t0, t1, t2) < 1e-20f;
     tr[0] = z ? 0.0f : t0; tr[1] = z ? 0.0f : t1; tr[2] = z ? 0.0f : t2;
 }
@@ -320,9 +320,9 @@ __device__ __forceinline__ void integrate_vrl(const DevParams& P, const RecPre& 
         if (dUV != 0) {
             const F3 VU = UV * (1.0f / dUV);
             float tuv[3];
-            tuv[0] = P.sigma_t[0] != 0 ? expf(P.sigma_t[0] * (0.0f - dUV)) : 1.0f;
-            tuv[1] = P.sigma_t[1] != 0 ? expf(P.sigma_t[1] * (0.0f - dUV)) : 1.0f;
-            tuv[2] = P.sigma_t[2] != 0 ? expf(P.sigma_t[2] * (0.0f - dUV)) : 1.0f;
+            tuv[0] = P.sigma_t[0] != 0 ? __expf(P.sigma_t[0] * (0.0f - dUV)) : 1.0f;
+            tuv[1] = P.sigma_t[1] != 0 ? __expf(P.sigma_t[1] * (0.0f - dUV)) : 1.0f;
+            tuv[2] = P.sigma_t[2] != 0 ? __expf(P.sigma_t[2] * (0.0f - dUV)) : 1.0f;
             if (tuv[0] != 0 || tuv[1] != 0 || tuv[2] != 0) {
                 float teu[3], tsv[3], pf;
                 medium_tr_only(P, len(q.E - U), teu);
@@ -380,9 +380,9 @@ __device__ __forceinline__ void integrate_vrl(const DevParams& P, const RecPre& 
                 if (dUV != 0) {
                     const F3 VU = UV * (1.0f / dUV);
                     float tuv[3], tsv[3], pf;
-                    tuv[0] = P.sigma_t[0] != 0 ? expf(P.sigma_t[0] * (0.0f - dUV)) : 1.0f;
-                    tuv[1] = P.sigma_t[1] != 0 ? expf(P.sigma_t[1] * (0.0f - dUV)) : 1.0f;
-                    tuv[2] = P.sigma_t[2] != 0 ? expf(P.sigma_t[2] * (0.0f - dUV)) : 1.0f;
+                    tuv[0] = P.sigma_t[0] != 0 ? __expf(P.sigma_t[0] * (0.0f - dUV)) : 1.0f;
+                    tuv[1] = P.sigma_t[1] != 0 ? __expf(P.sigma_t[1] * (0.0f - dUV)) : 1.0f;
+                    tuv[2] = P.sigma_t[2] != 0 ? __expf(P.sigma_t[2] * (0.0f - dUV)) : 1.0f;
                     medium_tr(P, len(S - V), tsv, &pf);
                     const float cos_wo = dot(neg(VU), q.n);
                     const bool bz = (q.cos_wi <= 0 || cos_wo <= 0);

@@ -13,7 +13,8 @@ Tolerances (floating point, stated here):
         median rel <= 1e-6, q99 <= 1e-4, q99.9 <= 2e-3, max <= 5e-2,
         RMSE (rms.cpp: gamma 1, absolute, all pixels x RGB) <= 2e-4 * mean.
     R entries are single pairs (no averaging over VRLs), so their tail is
-    heavier: median <= 1e-6, at most 0.5% of entries above 1e-3, and every
+    heavier: median <= 1e-6 (mean) / 1e-5 (variance: Welford's M2 is a
+    difference of nearby values), at most 0.5% of entries above 1e-3, and every
     VRL column sum (what clustering consumes first) within 1e-3.
   * refinement: cluster representatives and weights must be BIT-IDENTICAL
     (integer/index work; the kernel is compiled without FMA contraction and
@@ -70,11 +71,11 @@ def _assert_close(gpu, cpu, what, q50=1e-6, q99=1e-4, q999=2e-3, qmax=5e-2, rmse
     assert rmse <= rmse_rel * max(mean, 1e-30), f"{what}: RMSE {rmse}"
 
 
-def _assert_close_pairs(gpu, cpu, what):
+def _assert_close_pairs(gpu, cpu, what, q50=1e-6):
     gpu, cpu, err, rel = _rel(gpu, cpu)
     frac = float((rel > 1e-3).mean())
     print(f"[{what}] rel q50={np.median(rel):.2e} frac>1e-3={frac:.2e} max={rel.max():.2e}")
-    assert np.median(rel) <= 1e-6 and frac <= 5e-3, what
+    assert np.median(rel) <= q50 and frac <= 5e-3, what
     cs_g, cs_c = gpu.sum(axis=0), cpu.sum(axis=0)
     crel = np.abs(cs_g - cs_c) / np.maximum(np.abs(cs_c), 1e-30)
     assert ((cs_c == 0) == (cs_g == 0)).all(), f"{what}: zero-column pattern differs"
@@ -179,7 +180,7 @@ def test_build_R_parity(oracle, gpu_ok):
     pre, _ = ctx.stats()
     assert pre == cnt
     _assert_close_pairs(Rg[..., 0], Rcpu[..., 0], "R mean")
-    _assert_close_pairs(Rg[..., 1], Rcpu[..., 1], "R var")
+    _assert_close_pairs(Rg[..., 1], Rcpu[..., 1], "R var", q50=1e-5)   # M2: a difference, cancels
 
 
 def _refine_case(oracle, w, h, nvrl, nslice_rows, undersampling, torch):
