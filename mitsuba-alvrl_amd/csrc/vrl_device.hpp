@@ -89,6 +89,85 @@ __device__ __forceinline__ float len(F3 a) { return sqrtf(len2(a)); }
 __device__ __forceinline__ F3 nrm(F3 a) { const float r = 1.0f / len(a); return a * r; }
 __device__ __forceinline__ float fmax3(float a, float b, float c) { return fmaxf(fmaxf(a, b), c); }
 
+// Division as v_rcp_f32 (1 ulp) times the numerator: 2 VALU instead of the
+// 6 of the range-checked fdiv lowering.  Operands here are far from the
+// 2^+-126 limits where the two differ beyond rounding.
+__device__ __forceinline__ float rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ __forceinline__ float fdiv(float a, float b) { return a * __builtin_amdgcn_rcpf(b); }
+
+// ------------------------------------------------- hyperbolic functions --
+// ocml's asinhf / sinhf carry double-float intermediates and cost ~30% of the
+// gather (measured, DESIGN.md "gather instruction budget").  These use the
+// hardware log2 / exp2 with the cancellation-prone ranges handled explicitly;
+// max relative error vs. double asinh / sinh is a few ulp (tools/mathcheck.hip).
+constexpr float kLn2 = 0.69314718055994530942f;
+constexpr float kLog2e = 1.44269504088896340736f;
+constexpr float kLog2eLo = 1.925963033500e-8f;          // log2(e) - (float)log2(e)
+
+// asinh(x) = log1p(|x| + x^2 / (1 + sqrt(1 + x^2))), log1p by Goldberg's
+// correction log(u) * y / (u - 1), u = 1 + y; log(2|x|) beyond 2^12.
+__device__ __forceinline__ float asinh_fast(float x)
+{
+    const float ax = fabsf(x);
+    const float s = sqrtf(fmaf(ax, ax, 1.0f));
+    const float y = ax + fdiv(ax * ax, 1.0f + s);
+    const float u = 1.0f + y;
+    const float l = __builtin_amdgcn_logf(u) * kLn2;
+    const float small = (u == 1.0f) ? y : l * fdiv(y, u - 1.0f);
+    const float big = (__builtin_amdgcn_logf(ax) + 1.0f) * kLn2;
+    return copysignf(ax > 4096.0f ? big : small, x);
+}
+
+// sinh: odd Taylor polynomial below 1/4, else (e - 1/e) / 2 with exp through
+// exp2 of a two-term product x*log2(e) (keeps the argument rounding out).
+__device__ __forceinline__ float sinh_fast(float x)
+{
+    const float ax = fabsf(x);
+    const float x2 = ax * ax;
+    const float poly = fmaf(ax * x2, fmaf(x2, fmaf(x2, 1.0f / 5040.0f, 1.0f / 120.0f), 1.0f / 6.0f), ax);
+    const float ph = ax * kLog2e;
+    const float pl = fmaf(ax, kLog2e, -ph) + ax * kLog2eLo;
+    const float e = __builtin_amdgcn_exp2f(ph) * fmaf(pl, kLn2, 1.0f);
+    const float big = 0.5f * (e - rcp(e));
+    return copysignf(ax < 0.25f ? poly : big, x);
+}
+
+// ------------------------------------------------- circular functions --
+// The Kulla sampler only evaluates tan on (-pi/2, pi/2) and atan of finite
+// ratios; ocml's tanf carries a Payne-Hanek reduction for huge arguments,
+// evaluated branch-free.  Cody-Waite reduction by pi/2 in three parts and the
+// Cephes minimax polynomials (tanf / atanf, public domain) instead.
+__device__ __forceinline__ float tan_fast(float x)     // |x| < 3*pi/4
+{
+    const float j = rintf(x * 0.63661977236758134308f);
+    float r = fmaf(j, -1.5703125f, x);
+    r = fmaf(j, -4.837512969970703125e-4f, r);
+    r = fmaf(j, -7.54978995489188216e-8f, r);
+    const float z = r * r;
+    float p = fmaf(z, 9.38540185543e-3f, 3.11992232697e-3f);
+    p = fmaf(p, z, 2.44301354525e-2f);
+    p = fmaf(p, z, 5.34112807005e-2f);
+    p = fmaf(p, z, 1.33387994085e-1f);
+    p = fmaf(p, z, 3.33331568548e-1f);
+    const float t = fmaf(p * z, r, r);
+    return j != 0.0f ? -rcp(t) : t;
+}
+
+__device__ __forceinline__ float atan_fast(float x)
+{
+    const float ax = fabsf(x);
+    const bool hi = ax > 2.414213562373095f, mid = ax > 0.4142135623730950f;
+    const float num = hi ? -1.0f : (mid ? ax - 1.0f : ax);
+    const float den = hi ? ax : (mid ? ax + 1.0f : 1.0f);
+    const float t = fdiv(num, den);
+    const float y0 = hi ? 1.57079632679489661923f : (mid ? 0.78539816339744830962f : 0.0f);
+    const float z = t * t;
+    float p = fmaf(z, 8.05374449538e-2f, -1.38776856032e-1f);
+    p = fmaf(p, z, 1.99777106478e-1f);
+    p = fmaf(p, z, -3.33329491539e-1f);
+    return copysignf(y0 + fmaf(p * z, t, t), x);
+}
+
 // --------------------------------------------------- per eye segment --
 struct Rec {
     float ox, oy, oz, dx, dy, dz, px, py, pz, nx, ny, nz, ar, ag, ab;
@@ -115,7 +194,7 @@ __device__ __forceinline__ void medium_tr(const DevParams& P, float d, float tr[
     const float t2 = __expf(P.sigma_t[2] * (-d));
     float s = 0.0f;
     s += t0; s += t1; s += t2;
-    s /= 3;
+    s *= (1.0f / 3.0f);
     *pf = s * P.w + (1 - P.w);
     const bool z = fmax3(t0, t1, t2) < 1e-20f;
     tr[0] = z ? 0.0f : t0; tr[1] = z ? 0.0f : t1; tr[2] = z ? 0.0f : t2;
@@ -158,7 +237,7 @@ __device__ __forceinline__ float phase(const DevParams& P, F3 wi, F3 wo)
     if (P.phase_type == 0) return kInvFourPi;
     const float g = P.g;
     const float temp = 1.0f + g * g + 2.0f * g * dot(wi, wo);
-    return kInvFourPi * (1 - g * g) / (temp * sqrtf(temp));
+    return fdiv(kInvFourPi * (1 - g * g), temp * sqrtf(temp));
 }
 
 __device__ __forceinline__ bool spec_valid(float a, float b, float c)
@@ -181,8 +260,9 @@ __device__ __forceinline__ KullaFrame kulla_frame(F3 A, F3 dir, float lenAB, F3 
     k.I = A + dir * dotPr;
     k.Dis = len(D - k.I);
     const float dAI = len(A - k.I);
-    float aa = atanf(dAI / k.Dis);
-    float ab = atanf(len(k.I - B) / k.Dis);
+    const float rDis = rcp(k.Dis);
+    float aa = atan_fast(dAI * rDis);
+    float ab = atan_fast(len(k.I - B) * rDis);
     if (dotPr > 0) {
         aa = -aa;
         if (dAI > lenAB) ab = -ab;
@@ -194,14 +274,14 @@ __device__ __forceinline__ KullaFrame kulla_frame(F3 A, F3 dir, float lenAB, F3 
 // KullaSampling (vrlIntegrator.cpp:889-914) given its frame.
 __device__ __forceinline__ float kulla_sample(const KullaFrame& k, F3 dir, float u, F3* res)
 {
-    const float t = k.Dis * tanf(((1.0f - u) * k.aa) + (u * k.ab));
-    const float pdf = k.Dis / ((k.ab - k.aa) * (k.Dis * k.Dis + t * t));
+    const float t = k.Dis * tan_fast(((1.0f - u) * k.aa) + (u * k.ab));
+    const float pdf = fdiv(k.Dis, (k.ab - k.aa) * (k.Dis * k.Dis + t * t));
     *res = k.I + dir * t;
     return pdf;
 }
 
 // Pair-constant part of sampleVtoDistance (:916-953) incl. getClosestPoints (:962-1032).
-struct NovakFrame { float sinT, h, A0, dA, denom, dVhS; bool parallel; };
+struct NovakFrame { float sinT, rsinT, h, A0, dA, rdenom, dVhS; bool parallel; };
 
 __device__ __forceinline__ NovakFrame novak_frame(const RecPre& q, const VrlPrep& v)
 {
@@ -211,7 +291,7 @@ __device__ __forceinline__ NovakFrame novak_frame(const RecPre& q, const VrlPrep
     const float s2 = 1 - cosT * cosT;
     f.sinT = sqrtf(s2 > 0.0f ? s2 : 0.0f);
     f.parallel = f.sinT < kEpsilon;
-    f.h = f.A0 = f.dA = f.denom = f.dVhS = 0.0f;
+    f.h = f.A0 = f.dA = f.rdenom = f.rsinT = f.dVhS = 0.0f;
     if (!f.parallel) {
         // getClosestPoints(E, its.p, start, end)
         const F3 u = q.P - q.E;
@@ -239,18 +319,20 @@ __device__ __forceinline__ NovakFrame novak_frame(const RecPre& q, const VrlPrep
             else if ((-d + b) > a) sN = sD;
             else { sN = (-d + b); sD = a; }
         }
-        const float sc = sN / sD, tc = tN / tD;
+        const float sc = fdiv(sN, sD), tc = fdiv(tN, tD);
         const F3 dP = (w + u * sc) - vv * tc;
         const F3 Vh = S + vv * tc;
         f.h = len(dP);
         f.dVhS = len(Vh - S);
         const float V0c = -1 * f.dVhS;
         const float V1c = len(Vh - End);
-        const float A0 = asinhf((V0c / f.h) * f.sinT);
-        const float A1 = asinhf((V1c / f.h) * f.sinT);
+        const float rh = rcp(f.h);
+        const float A0 = asinh_fast((V0c * rh) * f.sinT);
+        const float A1 = asinh_fast((V1c * rh) * f.sinT);
         f.A0 = A0;
         f.dA = A1 - A0;
-        f.denom = f.dA / f.sinT;
+        f.rsinT = rcp(f.sinT);
+        f.rdenom = fdiv(f.sinT, f.dA);
     }
     return f;
 }
@@ -302,14 +384,14 @@ __device__ __forceinline__ void integrate_vrl(const DevParams& P, const RecPre& 
         float pdfV;
         if (nf.parallel) {
             V = S + f3(v.vx, v.vy, v.vz) * u0;
-            pdfV = 1 / v.len;
+            pdfV = rcp(v.len);
         } else {
-            float newV = nf.h * sinhf(nf.A0 + (u0 * nf.dA));
-            newV = newV / nf.sinT;
-            const float result = 1.0f / sqrtf(nf.h * nf.h + newV * newV * nf.sinT * nf.sinT);
+            float newV = nf.h * sinh_fast(nf.A0 + (u0 * nf.dA));
+            newV = newV * nf.rsinT;
+            const float result = __builtin_amdgcn_rsqf(nf.h * nf.h + newV * newV * nf.sinT * nf.sinT);
             newV += nf.dVhS;
             V = S + SV * newV;
-            pdfV = result / nf.denom;
+            pdfV = result * nf.rdenom;
         }
         const KullaFrame ke = kulla_frame(q.E, q.dirAB, q.lenAB, V, q.B);
         F3 U;
@@ -318,7 +400,7 @@ __device__ __forceinline__ void integrate_vrl(const DevParams& P, const RecPre& 
         const float l2 = len2(UV);
         const float dUV = sqrtf(l2);
         if (dUV != 0) {
-            const F3 VU = UV * (1.0f / dUV);
+            const F3 VU = UV * rcp(dUV);
             float tuv[3];
             tuv[0] = P.sigma_t[0] != 0 ? __expf(P.sigma_t[0] * (0.0f - dUV)) : 1.0f;
             tuv[1] = P.sigma_t[1] != 0 ? __expf(P.sigma_t[1] * (0.0f - dUV)) : 1.0f;
@@ -327,9 +409,9 @@ __device__ __forceinline__ void integrate_vrl(const DevParams& P, const RecPre& 
                 float teu[3], tsv[3], pf;
                 medium_tr_only(P, len(q.E - U), teu);
                 medium_tr(P, len(S - V), tsv, &pf);
-                const float rpdf = 1.0f / pdf;
-                const float rd2 = 1 / l2;
-                const float rpf = P.short_vrls ? 1.0f / pf : 1.0f;
+                const float rpdf = rcp(pdf);
+                const float rd2 = rcp(l2);
+                const float rpf = P.short_vrls ? rcp(pf) : 1.0f;
                 const float phU = P.phase_type == 0 ? kInvFourPi : phase(P, neg(VU), neg(q.d));
                 const float phV = P.phase_type == 0 ? phV_const : phase(P, neg(SV), VU);
                 float c0 = v.pr, c1 = v.pg, c2 = v.pb;
@@ -378,7 +460,7 @@ __device__ __forceinline__ void integrate_vrl(const DevParams& P, const RecPre& 
                 const float l2 = len2(UV);
                 const float dUV = sqrtf(l2);
                 if (dUV != 0) {
-                    const F3 VU = UV * (1.0f / dUV);
+                    const F3 VU = UV * rcp(dUV);
                     float tuv[3], tsv[3], pf;
                     tuv[0] = P.sigma_t[0] != 0 ? __expf(P.sigma_t[0] * (0.0f - dUV)) : 1.0f;
                     tuv[1] = P.sigma_t[1] != 0 ? __expf(P.sigma_t[1] * (0.0f - dUV)) : 1.0f;
@@ -391,9 +473,9 @@ __device__ __forceinline__ void integrate_vrl(const DevParams& P, const RecPre& 
                     const float f1 = bz ? 0.0f : q.alb[1] * fcos;
                     const float f2 = bz ? 0.0f : q.alb[2] * fcos;
                     const float phV = P.phase_type == 0 ? kInvFourPi : phase(P, neg(SV), VU);
-                    const float rpdf = 1.0f / pdf;
-                    const float rd2 = 1 / l2;
-                    const float rpf = P.short_vrls ? 1.0f / pf : 1.0f;
+                    const float rpdf = rcp(pdf);
+                    const float rd2 = rcp(l2);
+                    const float rpf = P.short_vrls ? rcp(pf) : 1.0f;
                     float c0 = v.pr, c1 = v.pg, c2 = v.pb;
                     c0 *= P.sigma_s[0] * rpdf; c1 *= P.sigma_s[1] * rpdf; c2 *= P.sigma_s[2] * rpdf;
                     c0 *= rd2; c1 *= rd2; c2 *= rd2;
