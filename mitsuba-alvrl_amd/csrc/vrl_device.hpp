@@ -118,20 +118,6 @@ __device__ __forceinline__ float asinh_fast(float x)
     return copysignf(ax > 4096.0f ? big : small, x);
 }
 
-// sinh: odd Taylor polynomial below 1/4, else (e - 1/e) / 2 with exp through
-// exp2 of a two-term product x*log2(e) (keeps the argument rounding out).
-__device__ __forceinline__ float sinh_fast(float x)
-{
-    const float ax = fabsf(x);
-    const float x2 = ax * ax;
-    const float poly = fmaf(ax * x2, fmaf(x2, fmaf(x2, 1.0f / 5040.0f, 1.0f / 120.0f), 1.0f / 6.0f), ax);
-    const float ph = ax * kLog2e;
-    const float pl = fmaf(ax, kLog2e, -ph) + ax * kLog2eLo;
-    const float e = __builtin_amdgcn_exp2f(ph) * fmaf(pl, kLn2, 1.0f);
-    const float big = 0.5f * (e - rcp(e));
-    return copysignf(ax < 0.25f ? poly : big, x);
-}
-
 // ------------------------------------------------- circular functions --
 // The Kulla sampler only evaluates tan on (-pi/2, pi/2) and atan of finite
 // ratios; ocml's tanf carries a Payne-Hanek reduction for huge arguments,
@@ -250,20 +236,24 @@ __device__ __forceinline__ float luminance(float r, float g, float b)
     return r * 0.212671f + g * 0.715160f + b * 0.072169f;
 }
 
-// Equi-angular (Kulla) frame of a segment A->B (dir, |A-B| given) w.r.t. D.
-struct KullaFrame { F3 I; float Dis, aa, ab; };
+// Equi-angular (Kulla) frame of a segment A->B w.r.t. a point D
+// (KullaSampling, vrlIntegrator.cpp:889-914).  I = A + dotPr * dir is the foot
+// of D on the segment's line, DI = D - I.  The reference's distance(A, I) and
+// distance(I, B) are |dotPr| and |lenAB - dotPr| (I, A, B are collinear).
+struct KullaFrame { F3 DI; float Dis, dotPr, aa, ab; };
 
-__device__ __forceinline__ KullaFrame kulla_frame(F3 A, F3 dir, float lenAB, F3 D, F3 B)
+__device__ __forceinline__ KullaFrame kulla_frame(F3 A, F3 dir, float lenAB, F3 D)
 {
     KullaFrame k;
-    const float dotPr = dot(dir, D - A);
-    k.I = A + dir * dotPr;
-    k.Dis = len(D - k.I);
-    const float dAI = len(A - k.I);
+    const F3 w = D - A;
+    k.dotPr = dot(dir, w);
+    k.DI = w - dir * k.dotPr;
+    k.Dis = len(k.DI);
     const float rDis = rcp(k.Dis);
+    const float dAI = fabsf(k.dotPr);
     float aa = atan_fast(dAI * rDis);
-    float ab = atan_fast(len(k.I - B) * rDis);
-    if (dotPr > 0) {
+    float ab = atan_fast(fabsf(lenAB - k.dotPr) * rDis);
+    if (k.dotPr > 0) {
         aa = -aa;
         if (dAI > lenAB) ab = -ab;
     }
@@ -271,17 +261,30 @@ __device__ __forceinline__ KullaFrame kulla_frame(F3 A, F3 dir, float lenAB, F3 
     return k;
 }
 
-// KullaSampling (vrlIntegrator.cpp:889-914) given its frame.
-__device__ __forceinline__ float kulla_sample(const KullaFrame& k, F3 dir, float u, F3* res)
+// The sampled offset t along the segment from I (result = I + t * dir).
+__device__ __forceinline__ float kulla_t(const KullaFrame& k, float u)
 {
-    const float t = k.Dis * tan_fast(((1.0f - u) * k.aa) + (u * k.ab));
-    const float pdf = fdiv(k.Dis, (k.ab - k.aa) * (k.Dis * k.Dis + t * t));
-    *res = k.I + dir * t;
-    return pdf;
+    return k.Dis * tan_fast(((1.0f - u) * k.aa) + (u * k.ab));
+}
+
+// sinh and cosh of x together (cosh for Novak's pdf, see below).
+__device__ __forceinline__ void sinhcosh_fast(float x, float* sh, float* ch)
+{
+    const float ax = fabsf(x);
+    const float x2 = ax * ax;
+    const float ps = fmaf(ax * x2, fmaf(x2, fmaf(x2, 1.0f / 5040.0f, 1.0f / 120.0f), 1.0f / 6.0f), ax);
+    const float pc = fmaf(x2, fmaf(x2, fmaf(x2, 1.0f / 720.0f, 1.0f / 24.0f), 0.5f), 1.0f);
+    const float ph = ax * kLog2e;
+    const float pl = fmaf(ax, kLog2e, -ph) + ax * kLog2eLo;
+    const float e = __builtin_amdgcn_exp2f(ph) * fmaf(pl, kLn2, 1.0f);
+    const float re = rcp(e);
+    const bool small = ax < 0.25f;
+    *sh = copysignf(small ? ps : 0.5f * (e - re), x);
+    *ch = small ? pc : 0.5f * (e + re);
 }
 
 // Pair-constant part of sampleVtoDistance (:916-953) incl. getClosestPoints (:962-1032).
-struct NovakFrame { float sinT, rsinT, h, A0, dA, rdenom, dVhS; bool parallel; };
+struct NovakFrame { float sinT, rsinT, h, rh, A0, dA, rdenom, dVhS; bool parallel, zero; };
 
 __device__ __forceinline__ NovakFrame novak_frame(const RecPre& q, const VrlPrep& v)
 {
@@ -289,10 +292,11 @@ __device__ __forceinline__ NovakFrame novak_frame(const RecPre& q, const VrlPrep
     const F3 S = f3(v.sx, v.sy, v.sz), End = f3(v.ex, v.ey, v.ez);
     const float cosT = dot(q.dN, f3(v.dx, v.dy, v.dz));
     const float s2 = 1 - cosT * cosT;
+    f.zero = v.len == 0.0f;                          // :920-924
     f.sinT = sqrtf(s2 > 0.0f ? s2 : 0.0f);
     f.parallel = f.sinT < kEpsilon;
-    f.h = f.A0 = f.dA = f.rdenom = f.rsinT = f.dVhS = 0.0f;
-    if (!f.parallel) {
+    f.h = f.rh = f.A0 = f.dA = f.rdenom = f.rsinT = f.dVhS = 0.0f;
+    if (!f.parallel && !f.zero) {
         // getClosestPoints(E, its.p, start, end)
         const F3 u = q.P - q.E;
         const F3 vv = f3(v.vx, v.vy, v.vz);
@@ -326,9 +330,9 @@ __device__ __forceinline__ NovakFrame novak_frame(const RecPre& q, const VrlPrep
         f.dVhS = len(Vh - S);
         const float V0c = -1 * f.dVhS;
         const float V1c = len(Vh - End);
-        const float rh = rcp(f.h);
-        const float A0 = asinh_fast((V0c * rh) * f.sinT);
-        const float A1 = asinh_fast((V1c * rh) * f.sinT);
+        f.rh = rcp(f.h);
+        const float A0 = asinh_fast((V0c * f.rh) * f.sinT);
+        const float A1 = asinh_fast((V1c * f.rh) * f.sinT);
         f.A0 = A0;
         f.dA = A1 - A0;
         f.rsinT = rcp(f.sinT);
@@ -337,14 +341,23 @@ __device__ __forceinline__ NovakFrame novak_frame(const RecPre& q, const VrlPrep
     return f;
 }
 
-// The vrl-dependent sample-0 independent data for vol->surf.
-struct PairPre {
-    NovakFrame nf;
-    KullaFrame ks;     // Kulla frame of the VRL segment w.r.t. Usurf
-};
-
-// One integrateVRL evaluation.  Returns RGB in c[]; *mean / *var receive the
-// luminance mean and variance-of-mean contributions (vrlIntegrator.cpp:693-703, 772-782).
+// One integrateVRL evaluation (vrlIntegrator.cpp:603-785).  Returns RGB in
+// out[]; *mean_out / *var_out receive the luminance mean and variance-of-mean
+// contributions (:693-703, :772-782).
+//
+// Evaluated in reduced form; every identity below is exact in real
+// arithmetic, so only float rounding separates it from the reference's
+// sequence of point constructions:
+//  * V = S + SV * newV, so distance(S, V) = |newV| (Novak) or u * len
+//    (parallel); the vol->surf V = I + t * SV gives |dotPr + t|;
+//  * U = I + t * dirAB with I = E + dotPr * dirAB, so distance(E, U) =
+//    |dotPr + t|; U - V = t * dir - DI with DI perpendicular to dir, so
+//    distanceSquared(U, V) = Dis^2 + t^2;
+//  * Kulla's pdf is Dis / ((ab - aa)(Dis^2 + t^2)), so pdf^-1 * dist^-2 =
+//    (ab - aa) / Dis (the equi-angular cancellation);
+//  * Novak's 1 / sqrt(h^2 + (newV sinT)^2) with newV sinT = h sinh(x) is
+//    1 / (h cosh(x)).
+// Directions (VU) are formed only for the HG phase function / the BSDF cosine.
 template <int NVV, int NVS, bool WANT_STATS>
 __device__ __forceinline__ void integrate_vrl(const DevParams& P, const RecPre& q, const VrlPrep& v,
                                               uint32_t rec_id, uint32_t vrl_id, uint32_t domain,
@@ -353,7 +366,7 @@ __device__ __forceinline__ void integrate_vrl(const DevParams& P, const RecPre& 
 {
     const int nVV = NVV >= 0 ? NVV : nvv_rt;
     const int nVS = NVS >= 0 ? NVS : nvs_rt;
-    const F3 S = f3(v.sx, v.sy, v.sz), End = f3(v.ex, v.ey, v.ez);
+    const F3 S = f3(v.sx, v.sy, v.sz);
     const F3 SV = f3(v.dx, v.dy, v.dz);
     float tot0 = 0.0f, tot1 = 0.0f, tot2 = 0.0f;
     float mean = 0.0f, M2 = 0.0f, mean_acc = 0.0f, var_acc = 0.0f;
@@ -372,7 +385,8 @@ __device__ __forceinline__ void integrate_vrl(const DevParams& P, const RecPre& 
     };
 
     const NovakFrame nf = novak_frame(q, v);
-    const float phV_const = kInvFourPi;
+    const bool hg = P.phase_type != 0;
+    const float ss0 = P.sigma_s[0], ss1 = P.sigma_s[1], ss2 = P.sigma_s[2];
 
     // ---------------- volume -> volume (:647-703) ----------------
 #pragma unroll
@@ -381,50 +395,48 @@ __device__ __forceinline__ void integrate_vrl(const DevParams& P, const RecPre& 
         float lumv = 0.0f;
         const float u0 = draw(2 * sample), u1 = draw(2 * sample + 1);
         F3 V;
-        float pdfV;
-        if (nf.parallel) {
+        float pdfV, dSV;
+        if (nf.zero) {                              // sampleVtoDistance :920-924
+            V = S; pdfV = 1.0f; dSV = 0.0f;
+        } else if (nf.parallel) {                   // :929-933
             V = S + f3(v.vx, v.vy, v.vz) * u0;
             pdfV = rcp(v.len);
-        } else {
-            float newV = nf.h * sinh_fast(nf.A0 + (u0 * nf.dA));
-            newV = newV * nf.rsinT;
-            const float result = __builtin_amdgcn_rsqf(nf.h * nf.h + newV * newV * nf.sinT * nf.sinT);
-            newV += nf.dVhS;
+            dSV = u0 * v.len;
+        } else {                                    // :935-952
+            float sh, ch;
+            sinhcosh_fast(nf.A0 + (u0 * nf.dA), &sh, &ch);
+            const float newV = fmaf(nf.h * sh, nf.rsinT, nf.dVhS);
             V = S + SV * newV;
-            pdfV = result * nf.rdenom;
+            pdfV = (nf.rh * rcp(ch)) * nf.rdenom;
+            dSV = fabsf(newV);
         }
-        const KullaFrame ke = kulla_frame(q.E, q.dirAB, q.lenAB, V, q.B);
-        F3 U;
-        const float pdf = pdfV * kulla_sample(ke, q.dirAB, u1, &U);
-        const F3 UV = U - V;
-        const float l2 = len2(UV);
-        const float dUV = sqrtf(l2);
-        if (dUV != 0) {
-            const F3 VU = UV * rcp(dUV);
+        const KullaFrame ke = kulla_frame(q.E, q.dirAB, q.lenAB, V);
+        const float t = kulla_t(ke, u1);
+        const float l2 = fmaf(ke.Dis, ke.Dis, t * t);
+        if (l2 != 0) {
+            const float dUV = sqrtf(l2);
             float tuv[3];
             tuv[0] = P.sigma_t[0] != 0 ? __expf(P.sigma_t[0] * (0.0f - dUV)) : 1.0f;
             tuv[1] = P.sigma_t[1] != 0 ? __expf(P.sigma_t[1] * (0.0f - dUV)) : 1.0f;
             tuv[2] = P.sigma_t[2] != 0 ? __expf(P.sigma_t[2] * (0.0f - dUV)) : 1.0f;
             if (tuv[0] != 0 || tuv[1] != 0 || tuv[2] != 0) {
                 float teu[3], tsv[3], pf;
-                medium_tr_only(P, len(q.E - U), teu);
-                medium_tr(P, len(S - V), tsv, &pf);
-                const float rpdf = rcp(pdf);
-                const float rd2 = rcp(l2);
+                medium_tr_only(P, fabsf(ke.dotPr + t), teu);
+                medium_tr(P, dSV, tsv, &pf);
+                // 1 / samplingPDF / distanceSquared(U, V)
+                const float g = (ke.ab - ke.aa) * rcp(ke.Dis * pdfV);
                 const float rpf = P.short_vrls ? rcp(pf) : 1.0f;
-                const float phU = P.phase_type == 0 ? kInvFourPi : phase(P, neg(VU), neg(q.d));
-                const float phV = P.phase_type == 0 ? phV_const : phase(P, neg(SV), VU);
-                float c0 = v.pr, c1 = v.pg, c2 = v.pb;
-                c0 *= (P.sigma_s[0] * P.sigma_s[0]) * rpdf;
-                c1 *= (P.sigma_s[1] * P.sigma_s[1]) * rpdf;
-                c2 *= (P.sigma_s[2] * P.sigma_s[2]) * rpdf;
-                c0 *= rd2; c1 *= rd2; c2 *= rd2;
-                c0 *= tsv[0]; c1 *= tsv[1]; c2 *= tsv[2];
-                c0 *= tuv[0]; c1 *= tuv[1]; c2 *= tuv[2];
-                c0 *= teu[0]; c1 *= teu[1]; c2 *= teu[2];
-                c0 *= rpf; c1 *= rpf; c2 *= rpf;
-                c0 *= phU; c1 *= phU; c2 *= phU;
-                c0 *= phV; c1 *= phV; c2 *= phV;
+                float ph = kInvFourPi * kInvFourPi;
+                if (hg) {
+                    const F3 VU = (q.dirAB * t - ke.DI) * rcp(dUV);
+                    ph = phase(P, neg(VU), neg(q.d)) * phase(P, neg(SV), VU);
+                }
+                const float gg = g * rpf * ph;
+                float c0 = v.pr * (ss0 * ss0), c1 = v.pg * (ss1 * ss1), c2 = v.pb * (ss2 * ss2);
+                c0 *= tsv[0] * tuv[0] * teu[0];
+                c1 *= tsv[1] * tuv[1] * teu[1];
+                c2 *= tsv[2] * tuv[2] * teu[2];
+                c0 *= gg; c1 *= gg; c2 *= gg;
                 if (spec_valid(c0, c1, c2)) {
                     const float rn = 1.0f / (float)nVV;
                     tot0 += c0 * rn; tot1 += c1 * rn; tot2 += c2 * rn;
@@ -447,44 +459,44 @@ __device__ __forceinline__ void integrate_vrl(const DevParams& P, const RecPre& 
     if (nVS > 0) {
         mean = 0.0f; M2 = 0.0f;
         KullaFrame ks;
-        if (q.surf) ks = kulla_frame(S, SV, v.len, q.P, End);
+        float gs = 0.0f, sn = 0.0f, dn = 0.0f, base0 = 0.0f, base1 = 0.0f, base2 = 0.0f;
+        if (q.surf) {
+            ks = kulla_frame(S, SV, v.len, q.P);    // sampleV -> KullaSampling(S, End, Usurf)
+            gs = (ks.ab - ks.aa) * rcp(ks.Dis);     // 1 / samplingPDF / distanceSquared(U, V)
+            sn = dot(SV, q.n);                      // cos_wo = (t sn - dn) / dUV
+            dn = dot(ks.DI, q.n);
+            base0 = v.pr * ss0 * q.teus[0];
+            base1 = v.pg * ss1 * q.teus[1];
+            base2 = v.pb * ss2 * q.teus[2];
+        }
 #pragma unroll
         for (int sample = 0; sample < (NVS >= 0 ? NVS : 64); ++sample) {
             if (NVS < 0 && sample >= nVS) break;
             float lumv = 0.0f;
             if (q.surf) {
                 const float u = draw(2 * nVV + sample);
-                F3 V;
-                const float pdf = kulla_sample(ks, SV, u, &V);
-                const F3 UV = q.P - V;
-                const float l2 = len2(UV);
-                const float dUV = sqrtf(l2);
-                if (dUV != 0) {
-                    const F3 VU = UV * rcp(dUV);
+                const float t = kulla_t(ks, u);
+                const float l2 = fmaf(ks.Dis, ks.Dis, t * t);
+                if (l2 != 0) {
+                    const float dUV = sqrtf(l2);
+                    const float rdUV = rcp(dUV);
                     float tuv[3], tsv[3], pf;
                     tuv[0] = P.sigma_t[0] != 0 ? __expf(P.sigma_t[0] * (0.0f - dUV)) : 1.0f;
                     tuv[1] = P.sigma_t[1] != 0 ? __expf(P.sigma_t[1] * (0.0f - dUV)) : 1.0f;
                     tuv[2] = P.sigma_t[2] != 0 ? __expf(P.sigma_t[2] * (0.0f - dUV)) : 1.0f;
-                    medium_tr(P, len(S - V), tsv, &pf);
-                    const float cos_wo = dot(neg(VU), q.n);
+                    medium_tr(P, fabsf(ks.dotPr + t), tsv, &pf);
+                    const float cos_wo = fmaf(t, sn, -dn) * rdUV;
                     const bool bz = (q.cos_wi <= 0 || cos_wo <= 0);
-                    const float fcos = kInvPi * cos_wo;
-                    const float f0 = bz ? 0.0f : q.alb[0] * fcos;
-                    const float f1 = bz ? 0.0f : q.alb[1] * fcos;
-                    const float f2 = bz ? 0.0f : q.alb[2] * fcos;
-                    const float phV = P.phase_type == 0 ? kInvFourPi : phase(P, neg(SV), VU);
-                    const float rpdf = rcp(pdf);
-                    const float rd2 = rcp(l2);
+                    const float fcos = bz ? 0.0f : kInvPi * cos_wo;
+                    float phV = kInvFourPi;
+                    if (hg) phV = phase(P, neg(SV), (ks.DI - SV * t) * rdUV);
                     const float rpf = P.short_vrls ? rcp(pf) : 1.0f;
-                    float c0 = v.pr, c1 = v.pg, c2 = v.pb;
-                    c0 *= P.sigma_s[0] * rpdf; c1 *= P.sigma_s[1] * rpdf; c2 *= P.sigma_s[2] * rpdf;
-                    c0 *= rd2; c1 *= rd2; c2 *= rd2;
-                    c0 *= tsv[0]; c1 *= tsv[1]; c2 *= tsv[2];
-                    c0 *= tuv[0]; c1 *= tuv[1]; c2 *= tuv[2];
-                    c0 *= q.teus[0]; c1 *= q.teus[1]; c2 *= q.teus[2];
-                    c0 *= rpf; c1 *= rpf; c2 *= rpf;
-                    c0 *= phV; c1 *= phV; c2 *= phV;
-                    c0 *= f0; c1 *= f1; c2 *= f2;
+                    const float gg = gs * rpf * phV * fcos;
+                    float c0 = base0 * q.alb[0], c1 = base1 * q.alb[1], c2 = base2 * q.alb[2];
+                    c0 *= tsv[0] * tuv[0];
+                    c1 *= tsv[1] * tuv[1];
+                    c2 *= tsv[2] * tuv[2];
+                    c0 *= gg; c1 *= gg; c2 *= gg;
                     if (spec_valid(c0, c1, c2)) {
                         const float rn = 1.0f / (float)nVS;
                         tot0 += c0 * rn; tot1 += c1 * rn; tot2 += c2 * rn;

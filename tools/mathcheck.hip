@@ -11,7 +11,7 @@
 
 using namespace alvrl;
 
-enum { F_ASINH, F_SINH, F_OCML_ASINH, F_OCML_SINH, F_TAN, F_OCML_TAN, F_ATAN, F_OCML_ATAN, F_N };
+enum { F_ASINH, F_SINH, F_COSH, F_OCML_ASINH, F_OCML_SINH, F_TAN, F_OCML_TAN, F_ATAN, F_OCML_ATAN, F_N };
 
 __global__ void k_eval(const float* x, float* y, int n, int f)
 {
@@ -21,7 +21,8 @@ __global__ void k_eval(const float* x, float* y, int n, int f)
     float r = 0;
     switch (f) {
     case F_ASINH: r = asinh_fast(v); break;
-    case F_SINH: r = sinh_fast(v); break;
+    case F_SINH: { float c; sinhcosh_fast(v, &r, &c); } break;
+    case F_COSH: { float sh; sinhcosh_fast(v, &sh, &r); } break;
     case F_OCML_ASINH: r = asinhf(v); break;
     case F_OCML_SINH: r = sinhf(v); break;
     case F_TAN: r = tan_fast(v); break;
@@ -50,7 +51,7 @@ int main()
     float *dx, *dy;
     (void)hipMalloc(&dx, 4 * n); (void)hipMalloc(&dy, 4 * n);
     (void)hipMemcpy(dx, xs.data(), 4 * n, hipMemcpyHostToDevice);
-    const char* names[F_N] = {"asinh_fast", "sinh_fast", "ocml asinhf", "ocml sinhf", "tan_fast", "ocml tanf", "atan_fast", "ocml atanf"};
+    const char* names[F_N] = {"asinh_fast", "sinhcosh.sh", "sinhcosh.ch", "ocml asinhf", "ocml sinhf", "tan_fast", "ocml tanf", "atan_fast", "ocml atanf"};
     std::vector<float> ys(n);
     for (int f = 0; f < F_N; f++) {
         hipLaunchKernelGGL(k_eval, dim3((n + 255) / 256), dim3(256), 0, 0, dx, dy, n, f);
@@ -61,12 +62,12 @@ int main()
             for (int i = 0; i < n; i++) {
                 const double a = std::fabs((double)xs[i]);
                 if (a < bands[b] || a >= bands[b + 1]) continue;
-                const bool s = (f == F_SINH || f == F_OCML_SINH);
+                const bool s = (f == F_SINH || f == F_OCML_SINH), ch = (f == F_COSH);
                 const bool tn = (f == F_TAN || f == F_OCML_TAN), at = (f == F_ATAN || f == F_OCML_ATAN);
-                if (s && a > 88) continue;                          // overflow range
+                if ((s || ch) && a > 88) continue;                          // overflow range
                 if (tn && a >= 1.5707963267948966) continue;        // sampler domain
                 const double xd = xs[i];
-                const double t = s ? std::sinh(xd) : tn ? std::tan(xd) : at ? std::atan(xd) : std::asinh(xd);
+                const double t = ch ? std::cosh(xd) : s ? std::sinh(xd) : tn ? std::tan(xd) : at ? std::atan(xd) : std::asinh(xd);
                 const double err = std::fabs((double)ys[i] - t) / std::fabs(t);
                 const double ulp = std::ldexp(1.0, std::ilogb((float)t) - 23);
                 const double eu = std::fabs((double)ys[i] - t) / ulp;
