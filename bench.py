@@ -61,6 +61,20 @@ def parse():
     return ap.parse_args()
 
 
+def aggregate_over_ranks(elapsed, counts, world, device):
+    """The contract's whole-job numbers: the MAX of the ranks' timed-region
+    wall times and the SUM of their work counts (exact in float64 below 2^53)."""
+    if world == 1:
+        return elapsed, [int(c) for c in counts]
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    c = torch.tensor([float(x) for x in counts], dtype=torch.float64, device=device)
+    dist.all_reduce(c, op=dist.ReduceOp.SUM)
+    return float(t.item()), [int(x) for x in c.tolist()]
+
+
 def main():
     args = parse()
     import numpy as np
@@ -126,13 +140,8 @@ def main():
     contrib = (s1["contrib_preprocess"] - s0["contrib_preprocess"]) + (s1["contrib_render"] - s0["contrib_render"])
     render_pairs = s1["contrib_render"] - s0["contrib_render"]
     pre_pairs = s1["contrib_preprocess"] - s0["contrib_preprocess"]
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        c = torch.tensor([contrib, render_pairs, pre_pairs], dtype=torch.float64, device=dev)
-        dist.all_reduce(c, op=dist.ReduceOp.SUM)
-        contrib, render_pairs, pre_pairs = (int(x) for x in c.tolist())
+    elapsed, (contrib, render_pairs, pre_pairs) = aggregate_over_ranks(
+        elapsed, [contrib, render_pairs, pre_pairs], world, dev)
 
     value = contrib / elapsed
     # roofline of the dominant kernel (the render gather), timed with HIP events

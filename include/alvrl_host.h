@@ -39,6 +39,15 @@ ALVRL_API void alvrl_scene_default(alvrl_scene_desc *s, int width, int height);
 ALVRL_API int alvrl_scene_records(const alvrl_scene_desc *s, int medium_scatters,
                                   const uint32_t *pixel_ids, uint32_t n, alvrl_gather_rec *out);
 
+/* Multi-GPU image partition of alvrl_integrator_render: 64x64 tiles in
+ * row-major tile order, tile t owned by rank t % world (the
+ * reference's analogue is the block scheduler handing 32x32 blocks to workers,
+ * blockedrenderprocess.cpp).  Writes the owned pixel ids (row-major y*W+x,
+ * tile by tile, rows within a tile) to out if out != NULL and cap suffices;
+ * *n = count.  ALVRL_ERR_INVALID for world == 0, rank >= world or cap < count. */
+ALVRL_API int alvrl_tile_pixels(int width, int height, uint32_t rank, uint32_t world,
+                                uint32_t *out, uint32_t cap, uint32_t *n);
+
 /* vrlTracer::randomWalk (vrlTracer.h:13-52).  soa receives 9 planes of
  * stride 'cap'; *n = #VRLs (>= target unless cap is hit), *particles =
  * particleCount.  Returns ALVRL_ERR_INVALID if cap < the VRLs produced. */

@@ -318,6 +318,7 @@ def _host():
     L.alvrl_trace_vrls.argtypes = [P(SceneDesc), u32, u32, u32, i32, i32, i32, vp, u32, P(u32), P(u64)]
     L.alvrl_read_vrl_file.argtypes = [C.c_char_p, P(MediumDesc), vp, u32, P(u32), P(u64)]
     L.alvrl_write_vrl_file.argtypes = [C.c_char_p, vp, u32]
+    L.alvrl_tile_pixels.argtypes = [i32, i32, u32, u32, vp, u32, P(u32)]
     L.alvrl_host_last_error.restype = C.c_char_p
     L.alvrl_integrator_create.argtypes = [C.c_char_p, i32, P(vp)]
     L.alvrl_integrator_destroy.argtypes = [vp]; L.alvrl_integrator_destroy.restype = None
@@ -366,6 +367,17 @@ def trace_vrls(scene: SceneDesc, target: int, seed: int = 0x5EED0001, pass_: int
     _hcheck(L.alvrl_trace_vrls(C.byref(scene), seed, pass_, target, int(short_vrls), max_depth,
                                rr_depth, _ptr(soa), cap, C.byref(n), C.byref(pc)))
     return np.ascontiguousarray(soa[:, :n.value]), int(pc.value)
+
+
+def tile_pixels(width: int, height: int, rank: int = 0, world: int = 1) -> np.ndarray:
+    """Pixel ids (row-major) rendered by `rank` of `world` (64x64 tiles,
+    round-robin): the partition alvrl_integrator_render uses."""
+    L = _host()
+    n = C.c_uint32()
+    _hcheck(L.alvrl_tile_pixels(width, height, rank, world, None, 0, C.byref(n)))
+    out = np.zeros(max(1, n.value), np.uint32)
+    _hcheck(L.alvrl_tile_pixels(width, height, rank, world, _ptr(out), n.value, C.byref(n)))
+    return out[:n.value].copy()
 
 
 def read_vrl_file(path: str, medium: Medium = Medium()):

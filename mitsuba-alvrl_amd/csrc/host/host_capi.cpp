@@ -82,6 +82,29 @@ ALVRL_API int alvrl_scene_records(const alvrl_scene_desc* s, int medium_scatters
     return ALVRL_OK;
 }
 
+ALVRL_API int alvrl_tile_pixels(int width, int height, uint32_t rank, uint32_t world, uint32_t* out,
+                                uint32_t cap, uint32_t* n)
+{
+    if (!n || width < 0 || height < 0) return herr(ALVRL_ERR_INVALID, "alvrl_tile_pixels: bad argument");
+    if (world == 0 || rank >= world) return herr(ALVRL_ERR_INVALID, "alvrl_tile_pixels: bad rank/world");
+    const int T = 64;
+    const int tx = (width + T - 1) / T, ty = (height + T - 1) / T;
+    uint32_t k = 0;
+    for (int t = 0; t < tx * ty; t++) {
+        if ((uint32_t)t % world != rank) continue;
+        const int x0 = (t % tx) * T, y0 = (t / tx) * T;
+        const int x1 = x0 + T < width ? x0 + T : width, y1 = y0 + T < height ? y0 + T : height;
+        for (int y = y0; y < y1; y++)
+            for (int x = x0; x < x1; x++) {
+                if (out && k < cap) out[k] = (uint32_t)(y * width + x);
+                k++;
+            }
+    }
+    *n = k;
+    if (out && k > cap) return herr(ALVRL_ERR_INVALID, "alvrl_tile_pixels: capacity too small");
+    return ALVRL_OK;
+}
+
 ALVRL_API int alvrl_trace_vrls(const alvrl_scene_desc* s, uint32_t seed, uint32_t pass, uint32_t target,
                                int short_vrls, int max_depth, int rr_depth, float* soa, uint32_t cap,
                                uint32_t* n, uint64_t* particles)

@@ -49,6 +49,10 @@ void chk(int rc, const char* what)
 {
     if (rc != ALVRL_OK) throw IntegError(rc, std::string(what) + ": " + alvrl_last_error(nullptr));
 }
+void chk_host(int rc)
+{
+    if (rc != ALVRL_OK) throw IntegError(rc, alvrl_host_last_error());
+}
 void hchk(hipError_t e, const char* what)
 {
     if (e != hipSuccess) throw IntegError(ALVRL_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
@@ -378,15 +382,11 @@ struct alvrl_integrator {
     {
         const uint32_t mode = clustered ? 2u : 1u;
         if (cache_rank == rank && cache_world == world && cache_mode == mode) return;
-        const int W = scene.width, H = scene.height, T = 64;
-        const int tx = (W + T - 1) / T, ty = (H + T - 1) / T;
-        std::vector<uint32_t> pix;
-        for (int t = 0; t < tx * ty; t++) {
-            if ((uint32_t)t % world != rank) continue;
-            const int x0 = (t % tx) * T, y0 = (t / tx) * T;
-            for (int y = y0; y < std::min(y0 + T, H); y++)
-                for (int x = x0; x < std::min(x0 + T, W); x++) pix.push_back((uint32_t)(y * W + x));
-        }
+        const int W = scene.width, H = scene.height;
+        uint32_t npix = 0;
+        chk_host(alvrl_tile_pixels(W, H, rank, world, nullptr, 0, &npix));
+        std::vector<uint32_t> pix(npix);
+        chk_host(alvrl_tile_pixels(W, H, rank, world, pix.data(), npix, &npix));
         std::vector<alvrl_work_item> items;
         if (clustered) {   // bucket by slice (stable), wave work items
             std::vector<uint32_t> sl(pix.size());

@@ -286,6 +286,42 @@ static float sample_v_to_distance(v3 E, v3 d, v3 hitp, v3 S, v3 End, v3 *V, floa
     return result / denom;
 }
 
+/* Exported single-function entry points: per-function known-answer fixtures
+ * (tests/golden/make_golden.py).  Points are float[3]. */
+static v3 v3p(const float *p) { v3 r = {p[0], p[1], p[2]}; return r; }
+static void v3s(v3 a, float *p) { p[0] = a.x; p[1] = a.y; p[2] = a.z; }
+
+float alvrl_o_closest_points(const float s1p0[3], const float s1p1[3], const float s2p0[3],
+                             const float s2p1[3], float s1h[3], float s2h[3])
+{
+    v3 a, b;
+    float h = closest_points(v3p(s1p0), v3p(s1p1), v3p(s2p0), v3p(s2p1), &a, &b);
+    v3s(a, s1h); v3s(b, s2h);
+    return h;
+}
+
+float alvrl_o_kulla(const float A[3], const float B[3], const float D[3], float uniform, float res[3])
+{
+    v3 r;
+    float pdf = kulla(v3p(A), v3p(B), v3p(D), &r, uniform);
+    v3s(r, res);
+    return pdf;
+}
+
+float alvrl_o_sample_v_to_distance(const float E[3], const float d[3], const float hitp[3],
+                                   const float S[3], const float End[3], float uniform, float V[3])
+{
+    v3 r;
+    float pdf = sample_v_to_distance(v3p(E), v3p(d), v3p(hitp), v3p(S), v3p(End), &r, uniform);
+    v3s(r, V);
+    return pdf;
+}
+
+void alvrl_o_medium_eval(const alvrl_o_medium *m, float distance, float tr[3], float *pdf_failure)
+{
+    medium_eval(m, distance, tr, pdf_failure);
+}
+
 /* ===================================================================== */
 /*  integrateVRL, vrlIntegrator.cpp:603-785                                */
 /* ===================================================================== */

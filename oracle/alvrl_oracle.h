@@ -51,6 +51,13 @@ extern "C" {
 void alvrl_o_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
 float alvrl_o_u01(uint32_t bits);
 
+/* single functions of the gather (known-answer fixtures) */
+float alvrl_o_closest_points(const float s1p0[3], const float s1p1[3], const float s2p0[3],
+                             const float s2p1[3], float s1h[3], float s2h[3]);
+float alvrl_o_kulla(const float A[3], const float B[3], const float D[3], float uniform, float res[3]);
+float alvrl_o_sample_v_to_distance(const float E[3], const float d[3], const float hitp[3],
+                                   const float S[3], const float End[3], float uniform, float V[3]);
+
 /* Homogeneous medium with the 'balance' strategy (homogeneous.cpp:156-184). */
 typedef struct {
     float sigma_s[3];
@@ -63,6 +70,8 @@ typedef struct {
 
 void alvrl_o_medium_init(alvrl_o_medium *m, const float sigma_s[3], const float sigma_a[3],
                          float sampling_weight /* -1 = auto */, int phase_type, float g);
+/* HomogeneousMedium::eval, 'balance' strategy: transmittance + pdfFailure */
+void alvrl_o_medium_eval(const alvrl_o_medium *m, float distance, float tr[3], float *pdf_failure);
 
 typedef struct {
     alvrl_o_medium medium;

@@ -70,6 +70,13 @@ class Oracle:
         L.alvrl_o_philox4x32_10.argtypes = [P(u32), P(u32), P(u32)]
         L.alvrl_o_u01.argtypes = [u32]; L.alvrl_o_u01.restype = f32
         L.alvrl_o_medium_init.argtypes = [P(Medium), P(f32), P(f32), f32, i32, f32]
+        L.alvrl_o_medium_eval.argtypes = [P(Medium), f32, P(f32), P(f32)]
+        L.alvrl_o_closest_points.argtypes = [P(f32)] * 6
+        L.alvrl_o_closest_points.restype = f32
+        L.alvrl_o_kulla.argtypes = [P(f32), P(f32), P(f32), f32, P(f32)]
+        L.alvrl_o_kulla.restype = f32
+        L.alvrl_o_sample_v_to_distance.argtypes = [P(f32)] * 5 + [f32, P(f32)]
+        L.alvrl_o_sample_v_to_distance.restype = f32
         L.alvrl_o_integrate_vrl.argtypes = [P(Params), P(f32), u32, P(f32), u32, u32, u32,
                                             P(f32), P(f32), P(f32)]
         L.alvrl_o_gather_brute.argtypes = [P(Params), P(f32), u32, P(u32), P(f32), u32, u64, u32,
@@ -105,6 +112,30 @@ class Oracle:
         c = (C.c_uint32 * 4)(*ctr); k = (C.c_uint32 * 2)(*key); o = (C.c_uint32 * 4)()
         self.lib.alvrl_o_philox4x32_10(c, k, o)
         return list(o)
+
+    # ---- single functions (known-answer fixtures) ----
+    def closest_points(self, s1p0, s1p1, s2p0, s2p1):
+        f3 = C.c_float * 3
+        a, b = f3(), f3()
+        h = self.lib.alvrl_o_closest_points(f3(*s1p0), f3(*s1p1), f3(*s2p0), f3(*s2p1), a, b)
+        return h, list(a), list(b)
+
+    def kulla(self, A, B, D, u):
+        f3 = C.c_float * 3
+        r = f3()
+        pdf = self.lib.alvrl_o_kulla(f3(*A), f3(*B), f3(*D), u, r)
+        return pdf, list(r)
+
+    def sample_v_to_distance(self, E, d, hitp, S, End, u):
+        f3 = C.c_float * 3
+        r = f3()
+        pdf = self.lib.alvrl_o_sample_v_to_distance(f3(*E), f3(*d), f3(*hitp), f3(*S), f3(*End), u, r)
+        return pdf, list(r)
+
+    def medium_eval(self, medium: Medium, distance: float):
+        tr = (C.c_float * 3)(); pf = C.c_float()
+        self.lib.alvrl_o_medium_eval(C.byref(medium), distance, tr, C.byref(pf))
+        return list(tr), pf.value
 
     # ---- scene / medium ----
     def scene(self, width: int, height: int) -> Scene:

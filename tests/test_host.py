@@ -55,6 +55,16 @@ def test_vrl_file_roundtrip(alvrl):
             alvrl.read_vrl_file(p)
 
 
+def test_golden_vrl_file_reader(alvrl):
+    """The host reader of the reference ASCII format (VRL.h:43-54, :105-158)
+    returns the committed fixture's VRLs exactly, particleCount = #VRLs."""
+    path = os.path.join(os.path.dirname(__file__), "golden", "vrls_c1.txt")
+    rows = np.array([list(map(float, l.split())) for l in open(path) if l.strip()], np.float32).T
+    soa, pc = alvrl.read_vrl_file(path)
+    assert pc == rows.shape[1] == soa.shape[1]
+    assert np.array_equal(soa.view(np.uint32), np.ascontiguousarray(rows).view(np.uint32))
+
+
 def test_integrator_properties_validation(alvrl):
     with pytest.raises(alvrl.AlvrlError, match="neighbourCount"):
         alvrl.Integrator("nc=3")

@@ -160,17 +160,52 @@ def test_slicing_partitions_pixels(oracle):
         assert su[s] == pytest.approx(len(reps) / counts[s])
 
 
-@pytest.mark.skipif(not os.path.exists(os.path.join(GOLDEN, "c1_small.npz")),
-                    reason="golden fixtures not generated")
-def test_golden_fixtures(oracle):
+def _make_golden():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("make_golden", os.path.join(GOLDEN, "make_golden.py"))
+    mg = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mg)
+    return mg
+
+
+def _bits_equal(a, b):
+    a = np.asarray(a); b = np.asarray(b)
+    if a.dtype.kind == "f":
+        return a.shape == b.shape and np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    return np.array_equal(a, b)
+
+
+def test_golden_kats(oracle):
+    """Per-function known answers (getClosestPoints, KullaSampling,
+    sampleVtoDistance, HomogeneousMedium::eval): the oracle reproduces the
+    committed values bit for bit, and the hand-built cases hit their
+    closed forms."""
+    g = np.load(os.path.join(GOLDEN, "kats.npz"))
+    k = _make_golden().kats(oracle)
+    for name in g.files:
+        assert _bits_equal(k[name], g[name]), name
+    # closed forms of the constructed cases
+    cp = g["closest_out"]
+    assert cp[0, 0] == pytest.approx(1.0) and cp[1, 0] == pytest.approx(0.0, abs=1e-7)
+    assert g["kulla_out"][0, 0] == pytest.approx(2 / np.pi, rel=1e-6)           # symmetric, Dis = 1
+    sv = g["svd_out"]
+    assert sv[0, 0] == 1.0 and np.array_equal(sv[0, 1:], g["svd_in"][0, 9:12])  # zero-length VRL
+    assert sv[1, 0] == pytest.approx(1 / 0.7, rel=1e-6)                         # parallel: uniform
+    me = g["medium_out"]
+    assert np.array_equal(me[0, 0], [1, 1, 1, 1])                               # d = 0
+    assert (me[:, -1, :3] == 0).all()                                           # < 1e-20 -> 0
+
+
+def test_golden_c1_small(oracle):
+    """48x32 smoke box with the committed VRL file: frame, R rows, slicing,
+    representatives, clusters and clustered frame reproduce bit for bit."""
+    mg = _make_golden()
     g = np.load(os.path.join(GOLDEN, "c1_small.npz"))
-    w, h = int(g["width"]), int(g["height"])
-    sc = oracle.scene(w, h)
-    m = oracle.medium()
-    vrls, pc = oracle.trace(sc, m, int(g["nvrl_target"]))
-    assert pc == int(g["particle_count"])
-    assert np.array_equal(vrls, g["vrls"])
-    recs = oracle.records(sc)
-    assert np.array_equal(recs, g["records"])
-    img, _ = oracle.gather_brute(oracle.params(m), recs, vrls, pc)
-    assert np.array_equal(img.view(np.uint32), g["image_brute"].view(np.uint32))
+    vrls = mg.read_vrl_ascii(os.path.join(GOLDEN, "vrls_c1.txt"))
+    assert vrls.shape == (9, mg.NVRL)
+    cur = mg.c1_small(oracle, vrls)
+    for name in g.files:
+        assert _bits_equal(cur[name], g[name]), name
+    assert (g["brute"] > 0).all() and len(g["cl_reps"]) > mg.NSLICES
+
+
