@@ -25,6 +25,8 @@
 // indices and weights are bit-identical to the CPU restatement.
 #include "vrl_device.hpp"
 
+#include <cstdio>
+#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -32,8 +34,10 @@ namespace alvrl {
 
 constexpr int kThreads = 512;
 constexpr int kWaves = kThreads / 64;
-constexpr int kChunk = 64;
-constexpr int kBitonicMax = 4096;
+constexpr int kCH = 16;                                     // columns per variance chunk (per direction)
+constexpr int kGT = kThreads / 2;                           // threads per variance direction
+constexpr uint32_t kPoolBytes = 144 * 1024;                 // dynamic LDS: sort keys / variance chunks
+constexpr int kBitonicMax = 16384;                          // 8-byte keys sorted in the pool
 constexpr uint32_t kDomCluster = 5u;
 
 struct CNode { float uvar, ivar; uint32_t begin, end; };
@@ -42,6 +46,8 @@ struct JobDev {
     const uint32_t* rows;
     const double* locw;
     uint32_t nrows;
+    uint32_t row0;            // rows[r] == row0 + r for every r when contig
+    int contig;
     float pixel_under, undersampling, depth_correction;
     int do_refine;
     uint32_t stage_refine, stage_sample;
@@ -56,8 +62,8 @@ struct JobDev {
     unsigned long long* keys0;
     unsigned long long* keys1;
     float* fsu; float* fsi; float* feu; float* fei;
-    double* st;        // 3 * nrows: sum, M, sumVars
-    double* bufM;      // kChunk * nrows
+    double* st;        // 2 x 3 * nrows: sum, M, sumVars per variance direction
+    double* bufM;      // 2 x kCH * (nrows | 1): per-row terms when they do not fit in LDS
     double* bufV;
     // outputs
     uint32_t* out_reps;
@@ -75,9 +81,44 @@ struct Common {
     const uint32_t* init_off;
     uint32_t ninit;
     uint32_t seed, pass;
+    unsigned long long* prof;   // per-phase cycle totals (ALVRL_REFINE_PROFILE=1), or null
+};
+
+// Phase timer of lane 0 (s_memtime deltas summed over jobs).
+enum { PF_COLW, PF_INIT, PF_UNCL, PF_WSAMP, PF_DIR, PF_PROJ, PF_SORT, PF_CVF, PF_CVR, PF_ARGMIN,
+       PF_CTRL, PF_REPS, PF_V_COEF, PF_V_REC, PF_V_RED, PF_P_STAGE, PF_P_COMP, PF_NSPLIT, PF_SPLITCOLS, PF_N };
+static const char* kPfNames[PF_N] = {"column weights", "initial clusters", "unclustered var",
+                                     "split: centres", "split: direction", "split: projections",
+                                     "split: sort", "split: variance fwd", "split: variance rev",
+                                     "split: argmin+add", "heap/snapshot/ctrl", "representatives",
+                                     " var: coefficients", " var: recurrence", " var: column sums",
+                                     " proj: staging", " proj: compute",
+                                     "#splits", "#split columns"};
+struct Prof {
+    unsigned long long* p;
+    long long t;
+    __device__ void mark(int id)
+    {
+        if (p && threadIdx.x == 0) {
+            const long long now = clock64();
+            atomicAdd(&p[id], (unsigned long long)(now - t));
+            t = now;
+        }
+    }
+    __device__ void count(int id, unsigned long long v) { if (p && threadIdx.x == 0) atomicAdd(&p[id], v); }
+};
+
+// Per-column coefficients of the variance recurrence, read as broadcasts.
+struct Coef { double w, Wo, a, bb, rw, Wn, rWn, pad; };
+struct VarGroup {
+    Coef cf[kCH];
+    uint32_t cv[kCH];
+    double Wcur;
+    float res_u, res_i;
 };
 
 struct Ctl {
+    VarGroup vg[2];
     float tracingVar, unclIntVar, clUnderVar, clIntVar;
     float sh_clUnderVar, sh_clIntVar;
     int heap_n, sh_heap_n, singles_n, sh_singles_n;
@@ -86,16 +127,9 @@ struct Ctl {
     int degenerate;
     float diffLen, nd;
     int go, do_snap, stop, refined;
-    double Wcur;
-    float res_u, res_i;
     float avg;
-    // chunk coefficients
-    double W[kChunk + 1];
-    double w[kChunk];
-    double a[kChunk];
-    double bb[kChunk];
-    uint32_t cv[kChunk];
     // reductions
+    float nrm3[3];
     float best_v[kWaves];
     uint32_t best_i[kWaves];
     uint32_t cnt[kWaves];
@@ -103,27 +137,6 @@ struct Ctl {
 };
 
 // ------------------------------------------------------------ helpers --
-__device__ __forceinline__ double wave_tree_d(double p)
-{
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        const double o = __shfl_down(p, off, 64);
-        if (lane < off) p = p + o;
-    }
-    return p;
-}
-__device__ __forceinline__ float wave_tree_f(float p)
-{
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        const float o = __shfl_down(p, off, 64);
-        if (lane < off) p = p + o;
-    }
-    return p;
-}
-
 __device__ __forceinline__ float Rmean(const Common& cm, uint32_t row, uint32_t v)
 {
     return cm.Rt[(size_t)v * cm.ld + row].x;
@@ -188,6 +201,34 @@ __device__ uint32_t weighted_sample(const float* w, Smp& smp, float* prob, uint3
         probability = w[ind[idx]] / weightSum;
     }
     if (prob) *prob = probability;
+    return idx;
+}
+
+// weightedSample over weights already gathered contiguously (wv[i] = w[ind[begin + i]],
+// i < m); returns the local index.  Same float operations in the same order.
+__device__ uint32_t weighted_sample_gathered(const float* wv, uint32_t m, Smp& smp, int* err)
+{
+    if (m == 0) { *err = 1; return 0; }
+    if (m == 1) return 0;
+    float weightSum = 0.0f;
+#pragma unroll 16
+    for (uint32_t i = 0; i < m; i++) weightSum += wv[i];
+    uint32_t idx;
+    if (weightSum <= 0) {
+        int tries = 0;
+        do {
+            idx = (uint32_t)((float)0u + smp.next() * (float)m);
+            if (++tries > 1000) { *err = 1; idx = 0; break; }
+        } while (idx >= m);
+    } else {
+        const float alpha = smp.next() * weightSum;
+        float accum = 0.0f;
+        idx = 0;
+        for (uint32_t i = 0; i < m; i++) {
+            accum += wv[i];
+            if (accum >= alpha) { idx = i; break; }
+        }
+    }
     return idx;
 }
 
@@ -327,92 +368,202 @@ __device__ void restore(const JobDev& J, Ctl& C)
 }
 
 // ------------------------------------------------ variance recurrence --
-// calculateClusterVariance over vrls[first + n*step], n in [0, m).  With
-// fu/fi: the incremental (prefix) variances are written.  Result in C.res_*.
-__device__ void cluster_variance(const JobDev& J, const Common& cm, Ctl& C, const uint32_t* order,
-                                 long step, uint32_t m, float* fu, float* fi)
+__device__ __forceinline__ uint32_t row_of(const JobDev& J, uint32_t r) { return J.contig ? J.row0 + r : J.rows[r]; }
+
+__device__ __forceinline__ double readlane_d(double v, uint32_t l)
+{
+    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, (int)l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), (int)l);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+// calculateClusterVariance (:1058-1120), one or two passes at once: pass g
+// (g = 0 forward from base[0], g = 1 backward from base[m-1]) runs on threads
+// [g*kGT, (g+1)*kGT).  Per chunk of <= kCH columns:
+//  * the first wave of the pass fetches the columns and weights (one lane
+//    each), forms the running weight total in the reference's sequential
+//    order through v_readlane (no memory round trip), and the per-column
+//    coefficients (one lane each);
+//  * one thread per row prefetches the chunk's (mean, var) entries into
+//    registers and runs the recurrence, writing the per-row prefix terms
+//    locw*(M/W) and locw*(V*W) to LDS;
+//  * one lane per column sums its terms over the rows in row order.
+// With fu == nullptr only the final variances are formed (initial clusters).
+template <bool TLDS>
+__device__ void variance_passes_t(const JobDev& J, const Common& cm, Ctl& C, const uint32_t* base,
+                                  uint32_t m, int npass, float* fu0, float* fi0, float* fu1, float* fi1,
+                                  unsigned char* pool, uint32_t ch, Prof* pf)
+{
+    long long t0 = pf ? (long long)clock64() : 0, t1 = 0, tc = 0, trc = 0, trd = 0;
+    const uint32_t R = J.nrows;
+    const uint32_t Rp = R | 1u;
+    const int tid = threadIdx.x;
+    const int g = tid / kGT, lt = tid - g * kGT;
+    const bool active = g < npass;
+    float* fu = g == 0 ? fu0 : fu1;
+    float* fi = g == 0 ? fi0 : fi1;
+    VarGroup& V = C.vg[g];
+    double* st = J.st + (size_t)g * 3 * R;
+    double* TU = TLDS ? reinterpret_cast<double*>(pool) + (size_t)g * 2 * kCH * Rp : J.bufM + (size_t)g * kCH * Rp;
+    double* TI = TLDS ? TU + (size_t)kCH * Rp : J.bufV + (size_t)g * kCH * Rp;
+    // (vrl, weight) of every column of the cluster, gathered in parallel once
+    unsigned long long* cw = J.keys1;
+    for (uint32_t i = tid; i < m; i += kThreads) {
+        const uint32_t vrl = base[i];
+        cw[i] = ((unsigned long long)__float_as_uint(J.colw[vrl]) << 32) | vrl;
+    }
+    if (active) {
+        for (uint32_t r = lt; r < R; r += kGT) { st[r] = 0.0; st[R + r] = 0.0; st[2 * R + r] = 0.0; }
+        if (lt == 0) V.Wcur = 0.0;
+    }
+    __syncthreads();
+    for (uint32_t c0 = 0; c0 < m; c0 += ch) {
+        const uint32_t cn = min(ch, m - c0);
+        if (active && lt < 64) {
+            const uint32_t lane = (uint32_t)lt;
+            uint32_t vrl = 0;
+            double w = 1.0;
+            if (lane < cn) {
+                const uint32_t i = c0 + lane;
+                const unsigned long long k = cw[g == 0 ? i : m - 1 - i];
+                vrl = (uint32_t)k;
+                w = (double)__uint_as_float((uint32_t)(k >> 32));
+                if (!isfinite(w) || w <= 0) C.err = 1;
+            }
+            double W = V.Wcur, Wo = 0.0, Wn = 0.0;
+            for (uint32_t c = 0; c < cn; c++) {
+                const double wc = readlane_d(w, c);
+                if (lane == c) Wo = W;
+                W = W + wc;
+                if (lane == c) Wn = W;
+            }
+            if (lane < cn) {
+                Coef k;
+                k.w = w; k.Wo = Wo; k.Wn = Wn;
+                k.a = (Wn * Wn) / (Wo * Wo);
+                k.rw = 1.0 / w;
+                k.bb = (k.rw + 1.0 / Wo);
+                k.rWn = 1.0 / Wn;
+                k.pad = 0.0;
+                V.cf[lane] = k;
+                V.cv[lane] = vrl;
+            }
+            if (lane == 0) V.Wcur = W;
+        }
+        __syncthreads();
+        if (pf) { t1 = clock64(); tc += t1 - t0; t0 = t1; }
+        if (active) {
+            for (uint32_t r = lt; r < R; r += kGT) {
+                const size_t row = row_of(J, r);
+                uint32_t cvv[kCH];
+#pragma unroll
+                for (int c = 0; c < kCH; c++) cvv[c] = V.cv[(uint32_t)c < cn ? c : 0];
+                float2 e[kCH];
+#pragma unroll
+                for (int c = 0; c < kCH; c++) e[c] = cm.Rt[(size_t)cvv[c] * cm.ld + row];
+                const double lw = J.locw[r];
+                double sum = st[r], M = st[R + r], Vs = st[2 * R + r];
+#pragma unroll
+                for (int c = 0; c < kCH; c++) {
+                    if ((uint32_t)c < cn) {
+                        const Coef k = V.cf[c];
+                        const double x = (double)e[c].x;
+                        const double tmp = k.w * sum - k.Wo * x;
+                        if (c0 + c > 0) M = k.a * M + k.bb * (tmp * tmp);
+                        Vs = Vs + (double)e[c].y * k.rw;
+                        sum = sum + x;
+                        if (fu) {
+                            TU[(size_t)c * Rp + r] = lw * (M * k.rWn);
+                            TI[(size_t)c * Rp + r] = lw * (Vs * k.Wn);
+                        }
+                    }
+                }
+                st[r] = sum; st[R + r] = M; st[2 * R + r] = Vs;
+            }
+        }
+        __syncthreads();
+        if (pf) { t1 = clock64(); trc += t1 - t0; t0 = t1; }
+        if (active && fu && lt < (int)cn) {
+            const uint32_t c = (uint32_t)lt, n = c0 + c;
+            const double* tu = TU + (size_t)c * Rp;
+            const double* ti = TI + (size_t)c * Rp;
+            double pu = 0.0, pi = 0.0;
+#pragma unroll 16
+            for (uint32_t r = 0; r < R; r++) { pi = pi + ti[r]; pu = pu + tu[r]; }
+            fi[n] = (float)pi;
+            fu[n] = n == 0 ? 0.0f : (float)pu;
+        }
+        if (pf) { t1 = clock64(); trd += t1 - t0; t0 = t1; }
+        // the next chunk's coefficient phase runs on the wave that just did
+        // the column sums, and the next recurrence waits at the barrier
+    }
+    __syncthreads();
+    if (active && lt == 0) {
+        if (fu) {
+            V.res_u = fu[m - 1]; V.res_i = fi[m - 1];
+        } else {
+            const double W = V.Wcur, rW = 1.0 / W;
+            double pu = 0.0, pi = 0.0;
+            for (uint32_t r = 0; r < R; r++) pu = pu + J.locw[r] * (st[R + r] * rW);
+            for (uint32_t r = 0; r < R; r++) pi = pi + J.locw[r] * (st[2 * R + r] * W);
+            V.res_u = (float)pu; V.res_i = (float)pi;
+        }
+        if (!isfinite(V.res_u) || V.res_u < 0) C.err = 1;
+        if (!isfinite(V.res_i) || V.res_i < 0) C.err = 1;
+    }
+    __syncthreads();
+    if (pf) { pf->count(PF_V_COEF, tc); pf->count(PF_V_REC, trc); pf->count(PF_V_RED, trd); }
+}
+
+__device__ void variance_passes(const JobDev& J, const Common& cm, Ctl& C, const uint32_t* base, uint32_t m,
+                                int npass, float* fu0, float* fi0, float* fu1, float* fi1, unsigned char* pool,
+                                Prof* pf = nullptr)
+{
+    const uint32_t Rp = J.nrows | 1u;
+    if (pf && (!pf->p || threadIdx.x != 0)) pf = nullptr;
+    if ((size_t)2 * 2 * kCH * Rp * sizeof(double) <= kPoolBytes)
+        variance_passes_t<true>(J, cm, C, base, m, npass, fu0, fi0, fu1, fi1, pool, (uint32_t)kCH, pf);
+    else
+        variance_passes_t<false>(J, cm, C, base, m, npass, fu0, fi0, fu1, fi1, pool, (uint32_t)kCH, pf);
+}
+
+__device__ __forceinline__ unsigned char* pool_end(void* pool) { return reinterpret_cast<unsigned char*>(pool) + kPoolBytes; }
+
+// Stages the (mean, var) entries of ncols columns (ids[c], c < ncols) into
+// LDS as S[r * ncols + c] (MEANS: floats of the means only): coalesced row
+// runs of one column per group of consecutive threads.
+template <bool MEANS>
+__device__ void stage_tile(const JobDev& J, const Common& cm, const uint32_t* ids, uint32_t ncols, void* S)
 {
     const uint32_t R = J.nrows;
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    for (uint32_t r = tid; r < R; r += kThreads) { J.st[r] = 0.0; J.st[R + r] = 0.0; J.st[2 * R + r] = 0.0; }
-    if (tid == 0) C.Wcur = 0.0;
-    __syncthreads();
-    for (uint32_t c0 = 0; c0 < m; c0 += kChunk) {
-        const uint32_t cn = min((uint32_t)kChunk, m - c0);
-        if (tid == 0) {
-            double W = C.Wcur;
-            C.W[0] = W;
-            for (uint32_t c = 0; c < cn; c++) {
-                const uint32_t vrl = order[(long)(c0 + c) * step];
-                const double weight = (double)J.colw[vrl];
-                if (!isfinite(weight) || weight <= 0) C.err = 1;
-                C.cv[c] = vrl;
-                C.w[c] = weight;
-                W = W + weight;
-                C.W[c + 1] = W;
-            }
-            C.Wcur = W;
+    const uint32_t total = ncols * R;
+    const int tid = threadIdx.x;
+    uint32_t c = (uint32_t)tid / R, r = (uint32_t)tid - c * R;
+    const uint32_t dc = (uint32_t)kThreads / R, dr = (uint32_t)kThreads - dc * R;
+    constexpr int B = 8;                       // loads in flight per thread
+    for (uint32_t e0 = (uint32_t)tid; e0 < total; e0 += B * kThreads) {
+        uint32_t cc[B], rr[B];
+        float2 v[B];
+#pragma unroll
+        for (int b = 0; b < B; b++) {
+            cc[b] = c; rr[b] = r;
+            r += dr; c += dc;
+            if (r >= R) { r -= R; c++; }
         }
-        __syncthreads();
-        if (tid < (int)cn) {
-            const double nW = C.W[tid + 1], oW = C.W[tid];
-            C.a[tid] = (nW * nW) / (oW * oW);
-            C.bb[tid] = (1.0 / C.w[tid] + 1.0 / oW);
+#pragma unroll
+        for (int b = 0; b < B; b++) {
+            const bool ok = e0 + (uint32_t)b * kThreads < total;
+            v[b] = cm.Rt[(size_t)ids[ok ? cc[b] : 0] * cm.ld + row_of(J, ok ? rr[b] : 0)];
         }
-        __syncthreads();
-        for (uint32_t r = tid; r < R; r += kThreads) {
-            const uint32_t row = J.rows[r];
-            double sum = J.st[r], M = J.st[R + r], V = J.st[2 * R + r];
-            for (uint32_t c = 0; c < cn; c++) {
-                const float2 mv = Rmv(cm, row, C.cv[c]);
-                const double x = (double)mv.x;
-                const double tmp = C.w[c] * sum - C.W[c] * x;
-                if (c0 + c > 0) M = C.a[c] * M + C.bb[c] * (tmp * tmp);
-                V = V + (double)mv.y / C.w[c];
-                sum = sum + x;
-                if (fu) { J.bufM[(size_t)c * R + r] = M; J.bufV[(size_t)c * R + r] = V; }
+#pragma unroll
+        for (int b = 0; b < B; b++) {
+            if (e0 + (uint32_t)b * kThreads < total) {
+                if (MEANS) reinterpret_cast<float*>(S)[(size_t)rr[b] * ncols + cc[b]] = v[b].x;
+                else reinterpret_cast<float2*>(S)[(size_t)rr[b] * ncols + cc[b]] = v[b];
             }
-            J.st[r] = sum; J.st[R + r] = M; J.st[2 * R + r] = V;
-        }
-        __syncthreads();
-        if (fu) {
-            for (uint32_t c = wave; c < cn; c += kWaves) {
-                const double Wn = C.W[c + 1];
-                double pi = 0.0, pu = 0.0;
-                for (uint32_t r = lane; r < R; r += 64) {
-                    pi = pi + J.locw[r] * (J.bufV[(size_t)c * R + r] * Wn);
-                    pu = pu + J.locw[r] * (J.bufM[(size_t)c * R + r] / Wn);
-                }
-                pi = wave_tree_d(pi);
-                pu = wave_tree_d(pu);
-                if (lane == 0) {
-                    const uint32_t n = c0 + c;
-                    fi[n] = (float)pi;
-                    fu[n] = n == 0 ? 0.0f : (float)pu;
-                }
-            }
-            __syncthreads();
         }
     }
-    if (fu) {
-        if (tid == 0) { C.res_u = fu[m - 1]; C.res_i = fi[m - 1]; }
-    } else if (wave == 0) {
-        const double W = C.Wcur;
-        double pu = 0.0, pi = 0.0;
-        for (uint32_t r = lane; r < R; r += 64) {
-            pu = pu + J.locw[r] * (J.st[R + r] / W);
-            pi = pi + J.locw[r] * (J.st[2 * R + r] * W);
-        }
-        pu = wave_tree_d(pu);
-        pi = wave_tree_d(pi);
-        if (lane == 0) { C.res_u = (float)pu; C.res_i = (float)pi; }
-    }
-    __syncthreads();
-    if (tid == 0) {
-        if (!isfinite(C.res_u) || C.res_u < 0) C.err = 1;
-        if (!isfinite(C.res_i) || C.res_i < 0) C.err = 1;
-    }
-    __syncthreads();
 }
 
 // ------------------------------------------------------------- sort --
@@ -509,43 +660,50 @@ __device__ unsigned long long* sort_keys(const JobDev& J, Ctl& C, uint32_t m, un
 // ------------------------------------------------------------ split --
 // Clustering::split (:590-684), collective.
 __device__ void split(const JobDev& J, const Common& cm, Ctl& C, uint32_t begin, uint32_t end,
-                      unsigned long long* lds)
+                      unsigned long long* lds, Prof& pf)
 {
+    pf.mark(PF_CTRL);
+    pf.count(PF_NSPLIT, 1);
+    pf.count(PF_SPLITCOLS, end - begin);
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const uint32_t m = end - begin;
     const uint32_t R = J.nrows;
+    // the two centres (:597-602): weights gathered in parallel into contiguous
+    // LDS (or scratch for large clusters), scanned by one lane
+    float* wv = (size_t)m * 4 <= kPoolBytes ? reinterpret_cast<float*>(lds) : J.fei;
+    for (uint32_t i = tid; i < m; i += kThreads) wv[i] = J.colw[J.vrls[begin + i]];
+    __syncthreads();
     if (tid == 0) {
         Smp smp;
         smp.init(cm.seed, cm.pass, begin, end, J.stage_refine);
-        const uint32_t vrl1 = J.vrls[weighted_sample(J.colw, smp, nullptr, begin, end, J.vrls, &C.err)];
-        const float weight1 = J.colw[vrl1];
-        J.colw[vrl1] = 0.0f;
-        const uint32_t vrl2 = J.vrls[weighted_sample(J.colw, smp, nullptr, begin, end, J.vrls, &C.err)];
-        J.colw[vrl1] = weight1;
-        C.vrl1 = vrl1; C.vrl2 = vrl2; C.draw_k = smp.k;
+        const uint32_t i1 = weighted_sample_gathered(wv, m, smp, &C.err);
+        wv[i1] = 0.0f;                     // colw[vrl1] = 0 for the second draw
+        const uint32_t i2 = weighted_sample_gathered(wv, m, smp, &C.err);
+        C.vrl1 = J.vrls[begin + i1]; C.vrl2 = J.vrls[begin + i2]; C.draw_k = smp.k;
     }
     __syncthreads();
+    pf.mark(PF_WSAMP);
     const uint32_t vrl1 = C.vrl1, vrl2 = C.vrl2;
-    if (wave == 0) {
-        float p1 = 0.0f, p2 = 0.0f, pd = 0.0f;
-        for (uint32_t r = lane; r < R; r += 64) {
-            const float a = Rmean(cm, J.rows[r], vrl1), b = Rmean(cm, J.rows[r], vrl2);
-            const float d = b - a;
-            const float ua = fabsf(a), ub = fabsf(b), ud = fabsf(d);
-            p1 = p1 + ua * ua; p2 = p2 + ub * ub; pd = pd + ud * ud;
+    // |c1|, |c2|, |c2 - c1| (:607-616): three lanes, rows in order
+    if (tid < 3) {
+        float p = 0.0f;
+        for (uint32_t r = 0; r < R; r++) {
+            const float a = Rmean(cm, row_of(J, r), vrl1), b = Rmean(cm, row_of(J, r), vrl2);
+            const float u = fabsf(tid == 0 ? a : (tid == 1 ? b : b - a));
+            p = p + u * u;
         }
-        p1 = wave_tree_f(p1); p2 = wave_tree_f(p2); pd = wave_tree_f(pd);
-        if (lane == 0) {
-            const float l1 = sqrtf(p1), l2 = sqrtf(p2), ld_ = sqrtf(pd);
-            C.diffLen = ld_;
-            C.degenerate = !(l1 != 0 && l2 != 0 && ld_ != 0);
-        }
+        C.nrm3[tid] = sqrtf(p);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        C.diffLen = C.nrm3[2];
+        C.degenerate = !(C.nrm3[0] != 0 && C.nrm3[1] != 0 && C.nrm3[2] != 0);
     }
     __syncthreads();
     if (!C.degenerate) {
         const float dl = C.diffLen;
         for (uint32_t r = tid; r < R; r += kThreads) {
-            const float a = Rmean(cm, J.rows[r], vrl1), b = Rmean(cm, J.rows[r], vrl2);
+            const float a = Rmean(cm, row_of(J, r), vrl1), b = Rmean(cm, row_of(J, r), vrl2);
             J.dir[r] = (b - a) / dl;
         }
         __syncthreads();
@@ -558,11 +716,10 @@ __device__ void split(const JobDev& J, const Common& cm, Ctl& C, uint32_t begin,
                 J.dir[r] = det_std_normal_x(sx, sy);
             }
             __syncthreads();
-            if (wave == 0) {
+            if (tid == 0) {
                 float p = 0.0f;
-                for (uint32_t r = lane; r < R; r += 64) { const float u = fabsf(J.dir[r]); p = p + u * u; }
-                p = wave_tree_f(p);
-                if (lane == 0) C.nd = sqrtf(p);
+                for (uint32_t r = 0; r < R; r++) { const float u = fabsf(J.dir[r]); p = p + u * u; }
+                C.nd = sqrtf(p);
             }
             __syncthreads();
             if (C.nd != 0) break;
@@ -577,31 +734,57 @@ __device__ void split(const JobDev& J, const Common& cm, Ctl& C, uint32_t begin,
         for (uint32_t r = tid; r < R; r += kThreads) J.dir[r] = J.dir[r] / nd;
         __syncthreads();
     }
-    // projections (:625-640), one wave per column
-    for (uint32_t j = wave; j < m; j += kWaves) {
-        const uint32_t vrl = J.vrls[begin + j];
-        float pn = 0.0f;
-        for (uint32_t r = lane; r < R; r += 64) {
-            const float a = fabsf(Rmean(cm, J.rows[r], vrl));
-            pn = pn + a * a;
+    pf.mark(PF_DIR);
+    // projections (:625-640): one lane per column, rows in order, over
+    // column tiles staged in LDS (or straight from global for tall matrices)
+    const uint32_t tcols = min((uint32_t)kThreads, (uint32_t)(kPoolBytes / (R * 4u) - 1u) & ~63u);
+    if (tcols >= 64) {
+        float* S = reinterpret_cast<float*>(lds);
+        float* sdir = reinterpret_cast<float*>(pool_end(lds)) - R;    // R floats at the top of the pool
+        for (uint32_t r = tid; r < R; r += kThreads) sdir[r] = J.dir[r];
+        for (uint32_t t0 = 0; t0 < m; t0 += tcols) {
+            const uint32_t tn = min(tcols, m - t0);
+            stage_tile<true>(J, cm, J.vrls + begin + t0, tn, S);
+            __syncthreads();
+            pf.mark(PF_P_STAGE);
+            if ((uint32_t)tid < tn) {
+                const uint32_t j = t0 + tid;
+                float pn = 0.0f;
+#pragma unroll 8
+                for (uint32_t r = 0; r < R; r++) { const float a = fabsf(S[(size_t)r * tn + tid]); pn = pn + a * a; }
+                const float nc = sqrtf(pn);
+                float proj = 0.0f;
+                if (nc != 0) {
+#pragma unroll 8
+                    for (uint32_t r = 0; r < R; r++) proj = proj + sdir[r] * (S[(size_t)r * tn + tid] / nc);
+                }
+                J.keys0[j] = proj_key(proj, J.vrls[begin + j]);
+            }
+            __syncthreads();
+            pf.mark(PF_P_COMP);
         }
-        pn = wave_tree_f(pn);
-        const float nc = sqrtf(__shfl(pn, 0, 64));
-        float proj = 0.0f;
-        if (nc != 0) {
-            float pp = 0.0f;
-            for (uint32_t r = lane; r < R; r += 64) pp = pp + J.dir[r] * (Rmean(cm, J.rows[r], vrl) / nc);
-            pp = wave_tree_f(pp);
-            proj = pp;
+    } else {
+        for (uint32_t j = tid; j < m; j += kThreads) {
+            const uint32_t vrl = J.vrls[begin + j];
+            const float2* col = cm.Rt + (size_t)vrl * cm.ld;
+            float pn = 0.0f;
+            for (uint32_t r = 0; r < R; r++) { const float a = fabsf(col[row_of(J, r)].x); pn = pn + a * a; }
+            const float nc = sqrtf(pn);
+            float proj = 0.0f;
+            if (nc != 0)
+                for (uint32_t r = 0; r < R; r++) proj = proj + J.dir[r] * (col[row_of(J, r)].x / nc);
+            J.keys0[j] = proj_key(proj, vrl);
         }
-        if (lane == 0) J.keys0[j] = proj_key(proj, vrl);
+        __syncthreads();
     }
-    __syncthreads();
+    pf.mark(PF_PROJ);
     const unsigned long long* sorted = sort_keys(J, C, m, lds);
     for (uint32_t i = tid; i < m; i += kThreads) J.vrls[begin + i] = (uint32_t)sorted[i];
     __syncthreads();
-    cluster_variance(J, cm, C, J.vrls + begin, 1, m, J.fsu, J.fsi);
-    cluster_variance(J, cm, C, J.vrls + end - 1, -1, m, J.feu, J.fei);
+    pf.mark(PF_SORT);
+    variance_passes(J, cm, C, J.vrls + begin, m, 2, J.fsu, J.fsi, J.feu, J.fei,
+                    reinterpret_cast<unsigned char*>(lds), &pf);
+    pf.mark(PF_CVF);
     // argmin over split position (:664-675)
     float bv = INFINITY;
     uint32_t bi = 0xFFFFFFFFu;
@@ -631,6 +814,7 @@ __device__ void split(const JobDev& J, const Common& cm, Ctl& C, uint32_t begin,
         }
     }
     __syncthreads();
+    pf.mark(PF_ARGMIN);
 }
 
 // ---------------------------------------------------------- kernel --
@@ -638,31 +822,44 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
 {
     const JobDev J = jobs[blockIdx.x];
     __shared__ Ctl C;
-    __shared__ unsigned long long lds[kBitonicMax];
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    __shared__ __attribute__((aligned(16))) unsigned char pool[kPoolBytes];
+    unsigned long long* lds = reinterpret_cast<unsigned long long*>(pool);
+    const int tid = threadIdx.x;
     const uint32_t N = cm.nvrl, R = J.nrows;
     const uint32_t nv = cm.init_off[cm.ninit];
+    Prof pf{cm.prof, (long long)clock64()};
     if (tid == 0) {
         C.tracingVar = C.unclIntVar = C.clUnderVar = C.clIntVar = 0.0f;
         C.heap_n = C.singles_n = C.sh_heap_n = C.sh_singles_n = 0;
         C.err = 0; C.refined = 1;
     }
     __syncthreads();
-    for (uint32_t i = tid; i < nv; i += kThreads) J.vrls[i] = cm.init_vrls[i];
     // calculateColumnWeigths (:985-1008)
-    for (uint32_t v = wave; v < N; v += kWaves) {
-        double p = 0.0;
-        for (uint32_t r = lane; r < R; r += 64) {
-            const float2 mv = Rmv(cm, J.rows[r], v);
-            const double mean = (double)mv.x, var = (double)mv.y;
-            const double x = mean * mean + var;
-            p = p + J.locw[r] * x;
-        }
-        p = wave_tree_d(p);
-        if (lane == 0) {
-            const float cw = (float)sqrt(p > 0.0 ? p : 0.0);
-            J.colw[v] = cw;
-            if (!isfinite(cw)) C.err = 1;
+    // one lane per column, rows in order, over column tiles staged in LDS
+    // (the identity column list is the J.vrls scratch before it is filled)
+    for (uint32_t v = tid; v < N; v += kThreads) J.vrls[v] = v;
+    __syncthreads();
+    {
+        const uint32_t tcols = min((uint32_t)kThreads, (uint32_t)(kPoolBytes / (R * 8u)) & ~63u);
+        const uint32_t step_c = tcols >= 64 ? tcols : (uint32_t)kThreads;
+        for (uint32_t t0 = 0; t0 < N; t0 += step_c) {
+            const uint32_t tn = min(step_c, N - t0);
+            if (tcols >= 64) { stage_tile<false>(J, cm, J.vrls + t0, tn, lds); __syncthreads(); }
+            if ((uint32_t)tid < tn) {
+                const uint32_t v = t0 + tid;
+                const float2* S = reinterpret_cast<const float2*>(lds);
+                double p = 0.0;
+                for (uint32_t r = 0; r < R; r++) {
+                    const float2 mv = tcols >= 64 ? S[(size_t)r * tn + tid] : cm.Rt[(size_t)v * cm.ld + row_of(J, r)];
+                    const double mean = (double)mv.x, var = (double)mv.y;
+                    const double x = mean * mean + var;
+                    p = p + J.locw[r] * x;
+                }
+                const float cw = (float)sqrt(p > 0.0 ? p : 0.0);
+                J.colw[v] = cw;
+                if (!isfinite(cw)) C.err = 1;
+            }
+            __syncthreads();
         }
     }
     __syncthreads();
@@ -679,44 +876,63 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
         for (uint32_t v = tid; v < N; v += kThreads) J.colw[v] += add;
     }
     __syncthreads();
+    pf.mark(PF_COLW);
+    for (uint32_t i = tid; i < nv; i += kThreads) J.vrls[i] = cm.init_vrls[i];
+    __syncthreads();
     // initial clusters
-    for (uint32_t i = 0; i < cm.ninit; i++) {
-        const uint32_t b = cm.init_off[i], e = cm.init_off[i + 1];
-        if (b == e) { if (tid == 0) C.err = 1; __syncthreads(); continue; }
-        cluster_variance(J, cm, C, J.vrls + b, 1, e - b, nullptr, nullptr);
-        if (tid == 0) add_cluster(J, C, b, e, C.res_u, C.res_i);
+    for (uint32_t i = 0; i < cm.ninit; i += 2) {
+        const uint32_t b0 = cm.init_off[i], e0 = cm.init_off[i + 1];
+        const bool two = i + 1 < cm.ninit;
+        const uint32_t b1 = two ? cm.init_off[i + 1] : 0, e1 = two ? cm.init_off[i + 2] : 0;
+        if (b0 == e0 || (two && b1 == e1)) { if (tid == 0) C.err = 1; __syncthreads(); continue; }
+        variance_passes(J, cm, C, J.vrls + b0, e0 - b0, 1, nullptr, nullptr, nullptr, nullptr, pool);
+        if (tid == 0) add_cluster(J, C, b0, e0, C.vg[0].res_u, C.vg[0].res_i);
         __syncthreads();
+        if (two) {
+            variance_passes(J, cm, C, J.vrls + b1, e1 - b1, 1, nullptr, nullptr, nullptr, nullptr, pool);
+            if (tid == 0) add_cluster(J, C, b1, e1, C.vg[0].res_u, C.vg[0].res_i);
+            __syncthreads();
+        }
     }
+    pf.mark(PF_INIT);
     // calculateUnclusteredVariance (:1022-1048): per-row Welford in m_vrls order
     for (uint32_t r = tid; r < R; r += kThreads) {
-        const uint32_t row = J.rows[r];
+        const size_t row = row_of(J, r);
         double mean = 0.0, M2 = 0.0, sv = 0.0;
-        for (uint32_t n = 0; n < nv; n++) {
-            const float2 mv = Rmv(cm, row, J.vrls[n]);
-            sv = sv + (double)mv.y;
-            const double x = (double)mv.x;
-            const double delta = x - mean;
-            mean = mean + delta / (double)(n + 1);
-            M2 = M2 + delta * (x - mean);
+        for (uint32_t n0 = 0; n0 < nv; n0 += kCH) {
+            uint32_t ids[kCH];
+#pragma unroll
+            for (int k = 0; k < kCH; k++) ids[k] = J.vrls[n0 + k < nv ? n0 + k : 0];
+            float2 e[kCH];
+#pragma unroll
+            for (int k = 0; k < kCH; k++) e[k] = cm.Rt[(size_t)ids[k] * cm.ld + row];
+#pragma unroll
+            for (int k = 0; k < kCH; k++) {
+                if (n0 + k < nv) {
+                    const double rn = 1.0 / (double)(n0 + k + 1);
+                    sv = sv + (double)e[k].y;
+                    const double x = (double)e[k].x;
+                    const double delta = x - mean;
+                    mean = mean + delta * rn;
+                    M2 = M2 + delta * (x - mean);
+                }
+            }
         }
         J.st[r] = sv; J.st[R + r] = M2;
     }
     __syncthreads();
-    if (wave == 0) {
+    if (tid == 0) {
         double pv = 0.0, pm = 0.0;
-        for (uint32_t r = lane; r < R; r += 64) {
-            pv = pv + J.locw[r] * J.st[r];
-            pm = pm + J.locw[r] * J.st[R + r];
-        }
-        pv = wave_tree_d(pv);
-        pm = wave_tree_d(pm);
-        if (lane == 0) {
+        for (uint32_t r = 0; r < R; r++) pv = pv + J.locw[r] * J.st[r];
+        for (uint32_t r = 0; r < R; r++) pm = pm + J.locw[r] * J.st[R + r];
+        {
             if (nv <= 1) C.err = 1;
             C.unclIntVar = (float)pv;
             C.tracingVar = (float)(pm - (double)C.unclIntVar);
         }
     }
     __syncthreads();
+    pf.mark(PF_UNCL);
 
     // refine (:380-489)
     if (J.do_refine && !C.err) {
@@ -730,7 +946,7 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
                 }
                 __syncthreads();
                 if (!C.go) break;
-                split(J, cm, C, C.b, C.e, lds);
+                split(J, cm, C, C.b, C.e, lds, pf);
             }
         } else {
             // refineAdaptively (:402-489)
@@ -755,7 +971,7 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
                     }
                     __syncthreads();
                     if (!C.go) break;
-                    split(J, cm, C, C.b, C.e, lds);
+                    split(J, cm, C, C.b, C.e, lds, pf);
                     if (tid == 0) {
                         nsplit++;
                         const float curr = conv_const(C, N, J.pixel_under);
@@ -781,31 +997,43 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
                         }
                         __syncthreads();
                         if (!C.go) break;
-                        split(J, cm, C, C.b, C.e, lds);
+                        split(J, cm, C, C.b, C.e, lds, pf);
                     }
                 }
             }
         }
     }
     __syncthreads();
+    pf.mark(PF_CTRL);
     // sampleRepresentatives (:354-378)
-    if (tid == 0) {
-        const int refined = C.err ? 0 : C.refined;
-        uint32_t i = 0;
-        if (refined) {
-            for (int k = C.singles_n - 1; k >= 0; k--) { J.out_reps[i] = J.singles[k]; J.out_w[i] = 1; i++; }
-            for (int k = 0; k < C.heap_n; k++) {
-                const CNode cn = J.heap[k];
-                Smp smp;
-                smp.init(cm.seed, cm.pass, cn.begin, cn.end, J.stage_sample);
-                float prob = 1.0f;
-                const uint32_t j = weighted_sample(J.colw, smp, &prob, cn.begin, cn.end, J.vrls, &C.err);
-                J.out_reps[i] = J.vrls[j];
-                J.out_w[i] = 1.0f / prob;
-                i++;
-            }
+    // singletons first (std::list push_front order), then one weighted pick
+    // per multi-cluster in heap order; every cluster has its own stream, so
+    // the picks run one cluster per lane
+    const int refined = C.err ? 0 : C.refined;
+    const int ns = C.singles_n, nh = C.heap_n;
+    __syncthreads();                       // every wave has read C.err before any pick sets it
+    if (refined) {
+        for (int k = tid; k < ns; k += kThreads) {
+            J.out_reps[ns - 1 - k] = J.singles[k];
+            J.out_w[ns - 1 - k] = 1.0f;
         }
-        *J.out_n = i;
+        for (int k = tid; k < nh; k += kThreads) {
+            const CNode cn = J.heap[k];
+            Smp smp;
+            smp.init(cm.seed, cm.pass, cn.begin, cn.end, J.stage_sample);
+            float prob = 1.0f;
+            int e = 0;
+            const uint32_t j = weighted_sample(J.colw, smp, &prob, cn.begin, cn.end, J.vrls, &e);
+            if (e) atomicOr(&C.err, 1);
+            J.out_reps[ns + k] = J.vrls[j];
+            J.out_w[ns + k] = 1.0f / prob;
+        }
+    }
+    __syncthreads();
+    __syncthreads();
+    pf.mark(PF_REPS);
+    if (tid == 0) {
+        *J.out_n = refined ? (uint32_t)(ns + nh) : 0u;
         *J.out_refined = refined;
         *J.out_err = C.err;
     }
@@ -855,7 +1083,7 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
     auto job_bytes = [&](uint32_t R) {
         return align_up(N * 4) * 2 + align_up(N * sizeof(CNode)) * 2 + align_up(N * 4) * 2 +
                align_up((size_t)R * 4) + align_up(N * 8) * 2 + align_up(N * 4) * 4 +
-               align_up((size_t)3 * R * 8) + align_up((size_t)kChunk * R * 8) * 2 +
+               align_up((size_t)6 * R * 8) + align_up((size_t)2 * kCH * (R | 1u) * 8) * 2 +
                align_up(N * 4) * 2 + align_up(16);
     };
     size_t total = align_up(rows_total * 4) + align_up(rows_total * 8) + align_up((size_t)nv * 4) +
@@ -884,6 +1112,10 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
         char* p = arena + job_off[j];
         const uint32_t R = H.nrows;
         J.rows = d_rows + row_off[j]; J.locw = d_locw + row_off[j]; J.nrows = R;
+        J.row0 = H.rows[0];
+        J.contig = 1;
+        for (uint32_t r = 0; r < R; r++)
+            if (H.rows[r] != H.rows[0] + r) { J.contig = 0; break; }
         J.pixel_under = H.pixel_under; J.undersampling = H.undersampling;
         J.depth_correction = H.depth_correction; J.do_refine = H.do_refine;
         J.stage_refine = H.stage_refine; J.stage_sample = H.stage_sample;
@@ -900,9 +1132,9 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
         J.fsi = (float*)p; p += align_up(N * 4);
         J.feu = (float*)p; p += align_up(N * 4);
         J.fei = (float*)p; p += align_up(N * 4);
-        J.st = (double*)p; p += align_up((size_t)3 * R * 8);
-        J.bufM = (double*)p; p += align_up((size_t)kChunk * R * 8);
-        J.bufV = (double*)p; p += align_up((size_t)kChunk * R * 8);
+        J.st = (double*)p; p += align_up((size_t)6 * R * 8);
+        J.bufM = (double*)p; p += align_up((size_t)2 * kCH * (R | 1u) * 8);
+        J.bufV = (double*)p; p += align_up((size_t)2 * kCH * (R | 1u) * 8);
         J.out_reps = (uint32_t*)p; p += align_up(N * 4);
         J.out_w = (float*)p; p += align_up(N * 4);
         J.out_n = (uint32_t*)p;
@@ -913,6 +1145,10 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
     cm.Rt = reinterpret_cast<const float2*>(d_Rt); cm.ld = ld; cm.nvrl = nvrl;
     cm.init_vrls = d_init; cm.init_off = d_init_off; cm.ninit = ninit;
     cm.seed = seed; cm.pass = pass;
+    cm.prof = nullptr;
+    const char* pe = std::getenv("ALVRL_REFINE_PROFILE");
+    if (pe && pe[0] == '1' && hipMalloc(&cm.prof, PF_N * 8) == hipSuccess)
+        (void)hipMemsetAsync(cm.prof, 0, PF_N * 8, s);
     hipEvent_t e0 = nullptr, e1 = nullptr;
     e = hipEventCreate(&e0);
     if (e == hipSuccess) e = hipEventCreate(&e1);
@@ -932,6 +1168,18 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
     for (uint32_t j = 0; j < njobs && e == hipSuccess; j++)
         e = hipMemcpyAsync(&meta[3 * (size_t)j], h_jobs[j].out_n, 12, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (cm.prof) {
+        unsigned long long h[PF_N];
+        if (hipMemcpy(h, cm.prof, sizeof(h), hipMemcpyDeviceToHost) == hipSuccess) {
+            unsigned long long tot = 0;
+            for (int i = 0; i < PF_NSPLIT; i++) tot += h[i];
+            std::fprintf(stderr, "[refine profile] %u jobs, lane-0 cycles summed over jobs:\n", njobs);
+            for (int i = 0; i < PF_N; i++)
+                std::fprintf(stderr, "  %-22s %16llu%s\n", kPfNames[i], h[i],
+                             i < PF_NSPLIT ? (std::string("  ") + std::to_string(100.0 * h[i] / (tot ? tot : 1)).substr(0, 5) + "%").c_str() : "");
+        }
+        hipFree(cm.prof);
+    }
     int rc = 0;
     if (e == hipSuccess) {
         uint32_t off = 0;

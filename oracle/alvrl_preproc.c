@@ -72,32 +72,23 @@ static inline float m_var(const mat_t *M, uint32_t r, uint32_t v)
 }
 
 /* ------------------------------------------- deterministic reductions -- */
-/* Every reduction over the ROWS of a local matrix (uBLAS inner_prod / norm_2,
- * sequential in the reference source, re-associated by the reference's
- * -funsafe-math-optimizations build) uses one fixed order that a 64-lane
- * wavefront evaluates directly: lane l sums rows l, l+64, l+128, ... in
- * ascending order, then lanes are combined by the halving tree
- * p[l] += p[l+32] (l<32), p[l] += p[l+16] (l<16), ..., p[0] += p[1].
- * The device refinement kernel (refine.hip) uses the identical order, which
- * makes cluster indices bit-exact between the two. */
-#define WS_LANES 64
+/* Every reduction over the ROWS of a local matrix (uBLAS inner_prod /
+ * norm_2) is the plain in-order sum of the reference source, row 0 first.
+ * (The reference's -funsafe-math-optimizations build may re-associate it, so
+ * it has no canonical rounding; this is the source-level order.)  The device
+ * refinement kernel (refine.hip) evaluates the identical sums, one lane per
+ * column, which makes cluster indices bit-exact between the two. */
 static double wsum_d(const double *t, uint32_t R)
 {
-    double p[WS_LANES];
-    for (int l = 0; l < WS_LANES; l++) p[l] = 0.0;
-    for (uint32_t r = 0; r < R; r++) p[r % WS_LANES] = p[r % WS_LANES] + t[r];
-    for (int off = WS_LANES / 2; off >= 1; off >>= 1)
-        for (int l = 0; l < off; l++) p[l] = p[l] + p[l + off];
-    return p[0];
+    double p = 0.0;
+    for (uint32_t r = 0; r < R; r++) p = p + t[r];
+    return p;
 }
 static float wsum_f(const float *t, uint32_t R)
 {
-    float p[WS_LANES];
-    for (int l = 0; l < WS_LANES; l++) p[l] = 0.0f;
-    for (uint32_t r = 0; r < R; r++) p[r % WS_LANES] = p[r % WS_LANES] + t[r];
-    for (int off = WS_LANES / 2; off >= 1; off >>= 1)
-        for (int l = 0; l < off; l++) p[l] = p[l] + p[l + off];
-    return p[0];
+    float p = 0.0f;
+    for (uint32_t r = 0; r < R; r++) p = p + t[r];
+    return p;
 }
 
 /* Deterministic standard normal from two uniforms (Box-Muller, the maths of
@@ -291,11 +282,12 @@ static int unclustered_variance(const mat_t *M, const double *w, const uint32_t 
     size_t n = 0;
     for (const uint32_t *it = vb; it != ve; ++it) {
         n++;
+        double rn = 1.0 / (double)n;            /* -freciprocal-math form, see cluster_variance */
         for (uint32_t r = 0; r < R; r++) {
             sv[r] += (double)m_var(M, r, *it);
             double x = (double)m_mean(M, r, *it);
             double delta = x - mean[r];
-            mean[r] += delta / (double)n;
+            mean[r] += delta * rn;
             M2[r] += delta * (x - mean[r]);
         }
     }
@@ -312,7 +304,11 @@ static int unclustered_variance(const mat_t *M, const double *w, const uint32_t 
 }
 
 /* calculateClusterVariance, Preprocessor.cpp:1058-1120.  'vrls' is walked
- * forward (step=+1) or backward (step=-1) over n entries. */
+ * forward (step=+1) or backward (step=-1) over n entries.  The row-vector
+ * divisions by the loop-invariant scalars weight and weightSum (:1093,
+ * :1100-1106) are taken in their -freciprocal-math form (the reference is
+ * built with -funsafe-math-optimizations, build/config-linux-gcc.py:7):
+ * one reciprocal per column, a multiply per row. */
 static int cluster_variance(clustering_t *C, const uint32_t *first, long step, uint32_t n_items,
                             float *inc_u, float *inc_i, float *res_u, float *res_i)
 {
@@ -328,30 +324,33 @@ static int cluster_variance(clustering_t *C, const uint32_t *first, long step, u
         if (!isfinite(weight) || weight <= 0) return 1;
         double newWeightSum = weightSum + weight;
         double a = (newWeightSum * newWeightSum) / (weightSum * weightSum);
-        double bcoef = (1.0 / weight + 1.0 / weightSum);
+        double rweight = 1.0 / weight;
+        double bcoef = (rweight + 1.0 / weightSum);
         for (uint32_t r = 0; r < R; r++) {
             double x = (double)m_mean(M, r, vrl);
             double tmp = weight * sum[r] - weightSum * x;
             if (n > 0) Mv[r] = a * Mv[r] + bcoef * (tmp * tmp);
-            sumVars[r] += (double)m_var(M, r, vrl) / weight;
+            sumVars[r] += (double)m_var(M, r, vrl) * rweight;
             sum[r] = sum[r] + x;
         }
         weightSum = newWeightSum;
         if (inc_u) {
+            double rws = 1.0 / weightSum;
             double *t = C->scr;
             for (uint32_t r = 0; r < R; r++) t[r] = C->locw[r] * (sumVars[r] * weightSum);
             double ipi = wsum_d(t, R);
             if (n == 0) {
                 inc_u[n] = 0;
             } else {
-                for (uint32_t r = 0; r < R; r++) t[r] = C->locw[r] * (Mv[r] / weightSum);
+                for (uint32_t r = 0; r < R; r++) t[r] = C->locw[r] * (Mv[r] * rws);
                 inc_u[n] = (float)wsum_d(t, R);
             }
             inc_i[n] = (float)ipi;
         }
     }
+    double rws = 1.0 / weightSum;
     double *t = C->scr;
-    for (uint32_t r = 0; r < R; r++) t[r] = C->locw[r] * (Mv[r] / weightSum);
+    for (uint32_t r = 0; r < R; r++) t[r] = C->locw[r] * (Mv[r] * rws);
     double ipu = wsum_d(t, R);
     for (uint32_t r = 0; r < R; r++) t[r] = C->locw[r] * (sumVars[r] * weightSum);
     double ipi = wsum_d(t, R);
