@@ -52,7 +52,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", default="C2", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default="C4", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-row-stride", type=int, default=64,
                     help="CPU baseline sample: every n-th image row")
@@ -198,6 +198,10 @@ def main():
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"], out["pixel_rmse_vs_cpu"] = cpu_baseline(args, cfg, scene, vrls, pc, fb, it,
                                                                        clustered)
+        if clustered:
+            out["cpu_baseline"] = cpu_baseline_prepass(args, cfg, vrls, pc, it, out["cpu_baseline"],
+                                                       pre_pairs / max(args.steps, 1),
+                                                       render_pairs / max(args.steps, 1))
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
@@ -248,6 +252,56 @@ def cpu_baseline(args, cfg, scene, vrls, pc, fb, it, clustered):
     acc = {"rmse": rmse, "mean": float(np.abs(img).mean()), "rmse_rel": rmse / max(float(np.abs(img).mean()), 1e-30),
            "max_rel": float(rel.max()), "median_rel": float(np.median(rel)), "pixels": int(len(pix))}
     return base, acc
+
+
+def cpu_baseline_prepass(args, cfg, vrls, pc, it, render_base, pre_pairs_step, render_pairs_step):
+    """Clustered configs: one CPU step = R build + refinement + clustered render.
+    Bounded samples: the R rows of one slice's representatives (16 threads),
+    that slice's refinement (one thread: the reference refines whole slices
+    per worker thread, Preprocessor.cpp:722-773), and the clustered gather
+    sample of cpu_baseline().  The step time is extrapolated from them
+    (R rows x columns, ceil(slices / threads) refinements, render pairs) and
+    value = the step's contributions / that time."""
+    import numpy as np
+    from oracle import Oracle
+    o = Oracle(fast=True)
+    W, H = cfg["w"], cfg["h"]
+    threads = int(os.environ.get("ALVRL_CPU_THREADS", "16"))
+    off, pix = it.reps()
+    ns = len(off) - 1
+    s0 = int(np.argsort(np.diff(off))[ns // 2])            # a median-size slice
+    rp = pix[off[s0]:off[s0 + 1]]
+    rec_ids = ((rp % H) * W + rp // H).astype(np.uint32)   # column-major ids -> row-major
+    recs = o.records(o.scene(W, H))[rec_ids]
+    last_pass = args.warmup + args.steps - 1
+    P = o.params(o.medium(), seed=SEED_RNG, pass_=last_pass)
+    t0 = time.perf_counter()
+    _, Rs, cnt = o.gather_brute(P, recs, vrls, pc, rec_ids=rec_ids, domain=2, want_R=True, nthreads=threads)
+    t_r = time.perf_counter() - t0
+    Rt = np.ascontiguousarray(Rs.transpose(1, 0, 2))
+    nrow = Rt.shape[1]
+    nz = Rt[:, :, 0].sum(axis=1) != 0
+    init = np.concatenate([np.nonzero(nz)[0], np.nonzero(~nz)[0]]).astype(np.uint32)
+    init_off = np.array([0, int(nz.sum()), len(init)] if (~nz).any() and nz.any() else [0, len(init)], np.uint32)
+    npix = int((it.slices() == s0).sum())
+    under = (-1.0 if "localUndersampling=-1" in cfg["props"]
+             else float(cfg["props"].split("localUndersampling=")[1].split(";")[0]))
+    t0 = time.perf_counter()
+    reps, w, refined = o.cluster_refine(Rt, np.arange(nrow, dtype=np.uint32), np.full(nrow, 1.0 / nrow),
+                                        init, init_off, float(np.float32(nrow) / np.float32(npix)), under,
+                                        seed=SEED_RNG, pass_=last_pass)
+    t_ref = time.perf_counter() - t0
+    r_rate = cnt / t_r
+    render_rate = render_base["value"]
+    t_step = pre_pairs_step / r_rate + int(np.ceil(ns / threads)) * t_ref + render_pairs_step / render_rate
+    return {"value": (pre_pairs_step + render_pairs_step) / t_step, "unit": "VRL contributions/s",
+            "cores": threads, "kind": "port",
+            "sample": (f"R rows of slice {s0} ({nrow} representatives x {vrls.shape[1]} VRLs, {t_r:.2f} s), "
+                       f"its adaptive refinement ({len(reps)} clusters, {t_ref:.2f} s, one thread), and "
+                       f"{render_base['sample']}; step extrapolated: {ns} slices over {threads} threads"),
+            "seconds": t_r + t_ref + render_base["seconds"], "step_seconds_estimate": t_step,
+            "cpu": render_base["cpu"], "flags": render_base["flags"],
+            "rates": {"rbuild": r_rate, "render": render_rate, "refine_s_per_slice": t_ref}}
 
 
 def torch_index(pix):
