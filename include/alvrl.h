@@ -172,6 +172,12 @@ typedef struct {
     int do_refine;            /* 0: only sampleRepresentatives (localRefinement=false, :270-274) */
     uint32_t stage_refine;    /* counter-RNG stream ids of the split / sampling draws */
     uint32_t stage_sample;
+    /* Optional R layout per row (NULL: entry (v, r) is d_Rt[rows[r] + v * ld]).
+     * Otherwise entry (v, r) is the float2 at index row_off[r] + v * row_stride[r]
+     * -- e.g. R stored as one [vrl][row] block per slice, which keeps a slice's
+     * local matrix contiguous (rows is then ignored and may be NULL). */
+    const uint64_t *row_off;
+    const uint32_t *row_stride;
 } alvrl_cluster_job;
 
 /* Replaces refinePerSlice -> refineSlice (Preprocessor.cpp:199-283) and the

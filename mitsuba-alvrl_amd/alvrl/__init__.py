@@ -55,7 +55,8 @@ class ClusterJob(C.Structure):
     _fields_ = [("rows", C.POINTER(C.c_uint32)), ("locw", C.POINTER(C.c_double)),
                 ("nrows", C.c_uint32), ("pixel_undersampling", C.c_float),
                 ("undersampling", C.c_float), ("depth_correction", C.c_float),
-                ("do_refine", C.c_int), ("stage_refine", C.c_uint32), ("stage_sample", C.c_uint32)]
+                ("do_refine", C.c_int), ("stage_refine", C.c_uint32), ("stage_sample", C.c_uint32),
+                ("row_off", C.POINTER(C.c_uint64)), ("row_stride", C.POINTER(C.c_uint32))]
 
 
 _lib: Optional[C.CDLL] = None

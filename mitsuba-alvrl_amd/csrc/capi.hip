@@ -42,6 +42,8 @@ struct HostJob {
     float pixel_under, undersampling, depth_correction;
     int do_refine;
     uint32_t stage_refine, stage_sample;
+    const uint64_t* row_off;
+    const uint32_t* row_stride;
 };
 int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, uint32_t seed,
                 uint32_t pass, uint32_t njobs, const HostJob* jobs, const uint32_t* init_vrls,
@@ -344,7 +346,8 @@ ALVRL_API int alvrl_refine(alvrl_ctx* c, const float* d_Rt, uint64_t ld, uint32_
     std::vector<HostJob> hj(njobs);
     for (uint32_t j = 0; j < njobs; j++) {
         const alvrl_cluster_job& J = jobs[j];
-        if (!J.rows || !J.locw) return fail(ALVRL_ERR_INVALID, "alvrl_refine: job without rows");
+        if ((!J.rows && !J.row_off) || !J.locw || (J.row_off && !J.row_stride))
+            return fail(ALVRL_ERR_INVALID, "alvrl_refine: job without rows");
         // Clustering ctor checks (Preprocessor.cpp:307-313)
         double n1 = 0.0;
         for (uint32_t r = 0; r < J.nrows; r++) n1 += std::fabs(J.locw[r]);
@@ -353,7 +356,8 @@ ALVRL_API int alvrl_refine(alvrl_ctx* c, const float* d_Rt, uint64_t ld, uint32_
         if (J.pixel_undersampling <= 0 || J.pixel_undersampling > 1)
             return fail(ALVRL_ERR_NUMERIC, "Invalid pixel undersampling: " + std::to_string(J.pixel_undersampling));
         hj[j] = HostJob{J.rows, J.locw, J.nrows, J.pixel_undersampling, J.undersampling,
-                        J.depth_correction, J.do_refine, J.stage_refine, J.stage_sample};
+                        J.depth_correction, J.do_refine, J.stage_refine, J.stage_sample,
+                        J.row_off, J.row_stride};
     }
     HIPCHK(hipSetDevice(c->cfg.device));
     std::string err;

@@ -119,7 +119,9 @@ struct alvrl_integrator {
     uint32_t uploaded_pass = 0xFFFFFFFFu;
     bool clustered = false;
     // R
-    DevBuf<float> Rt;
+    DevBuf<float> Rt;                       // R in per-slice [vrl][row] blocks
+    std::vector<uint64_t> row_base;         // float2 index of (vrl 0, global row g)
+    std::vector<uint32_t> row_stride;       // rows of g's slice
     DevBuf<alvrl_gather_rec> rep_recs;
     DevBuf<uint32_t> rep_ids;
     // cluster info (vrlClusterInfo)
@@ -278,15 +280,37 @@ struct alvrl_integrator {
         Rt.ensure((size_t)2 * nv * rows);
         hchk(hipMemcpyAsync(rep_recs.p, h.data(), sizeof(alvrl_gather_rec) * rows, hipMemcpyHostToDevice, stream), "copy rep records");
         hchk(hipMemcpyAsync(rep_ids.p, ids.data(), sizeof(uint32_t) * rows, hipMemcpyHostToDevice, stream), "copy rep ids");
-        // Building R (:302-333)
+        // Building R (:302-333).  R is stored as one [vrl][row] block per slice
+        // (the reference's R[slice][rep][vrl], transposed): a slice's local
+        // matrix is then one contiguous run -- consecutive VRL columns 8 * R_s
+        // bytes apart instead of 8 * rows -- which the refinement streams.
+        // Global row g of slice s lives at float2 index
+        //   nv * rep_off[s] + (g - rep_off[s]) + v * R_s.
+        row_base.resize(rows); row_stride.resize(rows);
+        for (uint32_t s2 = 0; s2 < ns; s2++)
+            for (uint32_t g = roff[s2]; g < roff[s2 + 1]; g++) {
+                row_base[g] = (uint64_t)nv * roff[s2] + (g - roff[s2]);
+                row_stride[g] = roff[s2 + 1] - roff[s2];
+            }
         hipEvent_t e0, e1;
         hchk(hipEventCreate(&e0), "event"); hchk(hipEventCreate(&e1), "event");
         hchk(hipEventRecord(e0, stream), "event");
-        chk(alvrl_build_R(ctx, rep_recs.p, rep_ids.p, rows, Rt.p, rows, 0, stream), "alvrl_build_R");
+        for (uint32_t s2 = 0; s2 < ns; s2++) {
+            const uint32_t n = roff[s2 + 1] - roff[s2];
+            if (!n) continue;
+            chk(alvrl_build_R(ctx, rep_recs.p + roff[s2], rep_ids.p + roff[s2], n,
+                              Rt.p + (size_t)2 * nv * roff[s2], n, 0, stream), "alvrl_build_R");
+        }
         hchk(hipEventRecord(e1, stream), "event");
         // Preprocessor::cluster (:838-898): non-zero VRLs in one cluster, zero VRLs in another
-        std::vector<uint8_t> nz(nv, 0);
-        chk(alvrl_nonzero_columns(ctx, Rt.p, rows, rows, nz.data(), stream), "alvrl_nonzero_columns");
+        std::vector<uint8_t> nz(nv, 0), nzs(nv);
+        for (uint32_t s2 = 0; s2 < ns; s2++) {
+            const uint32_t n = roff[s2 + 1] - roff[s2];
+            if (!n) continue;
+            chk(alvrl_nonzero_columns(ctx, Rt.p + (size_t)2 * nv * roff[s2], n, n, nzs.data(), stream),
+                "alvrl_nonzero_columns");
+            for (uint32_t v = 0; v < nv; v++) nz[v] |= nzs[v];
+        }
         float ms = 0;
         hchk(hipEventElapsedTime(&ms, e0, e1), "event");
         st.ms_rbuild = ms;
@@ -302,11 +326,16 @@ struct alvrl_integrator {
         // refinePerSlice (:199-252): one device job per slice
         std::vector<std::vector<uint32_t>> lrows(ns);
         std::vector<std::vector<double>> lw(ns);
+        std::vector<std::vector<uint64_t>> loff(ns);
+        std::vector<std::vector<uint32_t>> lstr(ns);
         std::vector<alvrl_cluster_job> jobs(ns);
         for (uint32_t s = 0; s < ns; s++) {
             prep->local_matrix(s, &lrows[s], &lw[s]);
+            for (uint32_t g : lrows[s]) { loff[s].push_back(row_base[g]); lstr[s].push_back(row_stride[g]); }
             alvrl_cluster_job& j = jobs[s];
             j.rows = lrows[s].data();
+            j.row_off = loff[s].data();
+            j.row_stride = lstr[s].data();
             j.locw = lw[s].data();
             j.nrows = (uint32_t)lrows[s].size();
             j.pixel_undersampling = prep->slice_undersampling()[s];
@@ -340,6 +369,7 @@ struct alvrl_integrator {
             std::vector<double> dw(rows, 1.0 / (double)rows);
             alvrl_cluster_job fj;
             fj.rows = all.data(); fj.locw = dw.data(); fj.nrows = rows;
+            fj.row_off = row_base.data(); fj.row_stride = row_stride.data();
             fj.pixel_undersampling = prep->global_pixel_undersampling();
             fj.undersampling = fallBackUndersampling;
             fj.depth_correction = 1.0f;
@@ -590,7 +620,15 @@ ALVRL_API int alvrl_integrator_R(alvrl_integrator* it, float* out, uint64_t cap)
     GUARD({
         hchk(hipSetDevice(it->device), "hipSetDevice");
         hchk(hipStreamSynchronize(it->stream), "sync");
-        if (need) hchk(hipMemcpy(out, it->Rt.p, need * sizeof(float), hipMemcpyDeviceToHost), "copy R");
+        // per-slice [vrl][row] blocks -> one [vrl][rep_rows] matrix
+        const auto& ro = it->prep->rep_off();
+        const uint64_t nv = it->vrls.n, rows = it->st.rep_rows;
+        for (size_t s = 0; need && s + 1 < ro.size(); s++) {
+            const uint64_t n = ro[s + 1] - ro[s];
+            if (!n) continue;
+            hchk(hipMemcpy2D(out + 2 * ro[s], rows * 8, it->Rt.p + 2 * nv * ro[s], n * 8, n * 8, nv,
+                             hipMemcpyDeviceToHost), "copy R");
+        }
     });
     return ALVRL_OK;
 }

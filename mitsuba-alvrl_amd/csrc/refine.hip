@@ -25,6 +25,7 @@
 // indices and weights are bit-identical to the CPU restatement.
 #include "vrl_device.hpp"
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <string>
@@ -34,7 +35,7 @@ namespace alvrl {
 
 constexpr int kThreads = 512;
 constexpr int kWaves = kThreads / 64;
-constexpr int kCH = 16;                                     // columns per variance chunk (per direction)
+constexpr int kCH = 8;                                      // columns per variance chunk (per direction)
 constexpr int kGT = kThreads / 2;                           // threads per variance direction
 constexpr uint32_t kPoolBytes = 144 * 1024;                 // dynamic LDS: sort keys / variance chunks
 constexpr int kBitonicMax = 16384;                          // 8-byte keys sorted in the pool
@@ -43,11 +44,15 @@ constexpr uint32_t kDomCluster = 5u;
 struct CNode { float uvar, ivar; uint32_t begin, end; };
 
 struct JobDev {
-    const uint32_t* rows;
+    // entry (vrl v, local row r) of R is Rt[roff[r] + v * rstride[r]] (float2
+    // units); contig: roff[r] == off0 + r and rstride[r] == stride0 for all r
+    const unsigned long long* roff;
+    const uint32_t* rstride;
+    unsigned long long off0;
+    uint32_t stride0;
+    int contig;
     const double* locw;
     uint32_t nrows;
-    uint32_t row0;            // rows[r] == row0 + r for every r when contig
-    int contig;
     float pixel_under, undersampling, depth_correction;
     int do_refine;
     uint32_t stage_refine, stage_sample;
@@ -86,13 +91,17 @@ struct Common {
 
 // Phase timer of lane 0 (s_memtime deltas summed over jobs).
 enum { PF_COLW, PF_INIT, PF_UNCL, PF_WSAMP, PF_DIR, PF_PROJ, PF_SORT, PF_CVF, PF_CVR, PF_ARGMIN,
-       PF_CTRL, PF_REPS, PF_V_COEF, PF_V_REC, PF_V_RED, PF_P_STAGE, PF_P_COMP, PF_NSPLIT, PF_SPLITCOLS, PF_N };
+       PF_CTRL, PF_REPS, PF_V_COEF, PF_V_REC, PF_V_RED, PF_P_STAGE, PF_P_COMP, PF_V_OWN, PF_V_CW,
+       PF_V_ISSUE, PF_V_DATA,
+       PF_NSPLIT, PF_SPLITCOLS, PF_N };
 static const char* kPfNames[PF_N] = {"column weights", "initial clusters", "unclustered var",
                                      "split: centres", "split: direction", "split: projections",
                                      "split: sort", "split: variance fwd", "split: variance rev",
                                      "split: argmin+add", "heap/snapshot/ctrl", "representatives",
                                      " var: coefficients", " var: recurrence", " var: column sums",
                                      " proj: staging", " proj: compute",
+                                     "  rec: row wave 0 busy", "  rec: coef wave busy",
+                                     "   row wave: prefetch issue", "   row wave: wait for data",
                                      "#splits", "#split columns"};
 struct Prof {
     unsigned long long* p;
@@ -109,10 +118,10 @@ struct Prof {
 };
 
 // Per-column coefficients of the variance recurrence, read as broadcasts.
-struct Coef { double w, Wo, a, bb, rw, Wn, rWn, pad; };
+struct Coef { double w, Wo, a, bb, rw, Wn, rWn; uint32_t vrl, pad; };
 struct VarGroup {
-    Coef cf[kCH];
-    uint32_t cv[kCH];
+    Coef cf[4][kCH];         // coefficients of chunk k in cf[k % 4]
+    float res_fu[2 * kCH], res_fi[2 * kCH];   // column sums of the last chunk pair, written out by wave 3
     double Wcur;
     float res_u, res_i;
 };
@@ -137,13 +146,29 @@ struct Ctl {
 };
 
 // ------------------------------------------------------------ helpers --
-__device__ __forceinline__ float Rmean(const Common& cm, uint32_t row, uint32_t v)
+// Global-address-space view of a pointer: loads through it are global_load
+// (vmcnt only).  Through a generic pointer they are flat loads, which also
+// count in lgkmcnt -- every LDS wait and every barrier would then wait for
+// the prefetches in flight.
+template <typename T>
+__device__ __forceinline__ const __attribute__((address_space(1))) T* gp(const T* p)
 {
-    return cm.Rt[(size_t)v * cm.ld + row].x;
+    return (const __attribute__((address_space(1))) T*)p;
 }
-__device__ __forceinline__ float2 Rmv(const Common& cm, uint32_t row, uint32_t v)
+__device__ __forceinline__ float2 ldg2(const float2* base, size_t i)
 {
-    return cm.Rt[(size_t)v * cm.ld + row];
+    const unsigned long long u = gp(reinterpret_cast<const unsigned long long*>(base))[i];
+    return make_float2(__uint_as_float((uint32_t)u), __uint_as_float((uint32_t)(u >> 32)));
+}
+
+struct RowRef { size_t base, stride; };
+__device__ __forceinline__ RowRef row_ref(const JobDev& J, uint32_t r)
+{
+    return J.contig ? RowRef{(size_t)(J.off0 + r), (size_t)J.stride0} : RowRef{(size_t)J.roff[r], (size_t)J.rstride[r]};
+}
+__device__ __forceinline__ float Rmean(const Common& cm, RowRef rr, uint32_t v)
+{
+    return ldg2(cm.Rt, rr.base + (size_t)v * rr.stride).x;
 }
 
 // Sequential stream of one (stage, cluster range) (see oracle smp_t).
@@ -204,16 +229,31 @@ __device__ uint32_t weighted_sample(const float* w, Smp& smp, float* prob, uint3
     return idx;
 }
 
-// weightedSample over weights already gathered contiguously (wv[i] = w[ind[begin + i]],
-// i < m); returns the local index.  Same float operations in the same order.
-__device__ uint32_t weighted_sample_gathered(const float* wv, uint32_t m, Smp& smp, int* err)
+// The same weightedSample, executed by one whole wave: the weights stream in
+// 64 at a time (one coalesced load per block, the next block in flight) and
+// the float running sums walk them in order through v_readlane, so the
+// sequential chain costs one add per weight instead of a memory round trip.
+// Every lane returns the same index.  The weight at index `zero_at` counts
+// as 0 (the second centre of split(), drawn with colw[vrl1] = 0).
+__device__ __noinline__ uint32_t weighted_sample_wave(const float* wv, uint32_t m, Smp& smp, int* err,
+                                                      uint32_t zero_at)
 {
+    const uint32_t lane = threadIdx.x & 63;
     if (m == 0) { *err = 1; return 0; }
     if (m == 1) return 0;
+    const uint32_t nb = (m + 63) / 64;
     float weightSum = 0.0f;
-#pragma unroll 16
-    for (uint32_t i = 0; i < m; i++) weightSum += wv[i];
-    uint32_t idx;
+    float cur = wv[min(lane, m - 1)];
+    for (uint32_t b = 0; b < nb; b++) {
+        const float nxt = b + 1 < nb ? wv[min((b + 1) * 64 + lane, m - 1)] : 0.0f;
+        const uint32_t n = min(64u, m - b * 64);
+        for (uint32_t j = 0; j < n; j++) {
+            const float x = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cur), (int)j));
+            weightSum += b * 64 + j == zero_at ? 0.0f : x;
+        }
+        cur = nxt;
+    }
+    uint32_t idx = 0;
     if (weightSum <= 0) {
         int tries = 0;
         do {
@@ -223,10 +263,17 @@ __device__ uint32_t weighted_sample_gathered(const float* wv, uint32_t m, Smp& s
     } else {
         const float alpha = smp.next() * weightSum;
         float accum = 0.0f;
-        idx = 0;
-        for (uint32_t i = 0; i < m; i++) {
-            accum += wv[i];
-            if (accum >= alpha) { idx = i; break; }
+        cur = wv[min(lane, m - 1)];
+        bool found = false;
+        for (uint32_t b = 0; b < nb && !found; b++) {
+            const float nxt = b + 1 < nb ? wv[min((b + 1) * 64 + lane, m - 1)] : 0.0f;
+            const uint32_t n = min(64u, m - b * 64);
+            for (uint32_t j = 0; j < n; j++) {
+                const float x = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cur), (int)j));
+                accum += b * 64 + j == zero_at ? 0.0f : x;
+                if (accum >= alpha) { idx = b * 64 + j; found = true; break; }
+            }
+            cur = nxt;
         }
     }
     return idx;
@@ -368,7 +415,6 @@ __device__ void restore(const JobDev& J, Ctl& C)
 }
 
 // ------------------------------------------------ variance recurrence --
-__device__ __forceinline__ uint32_t row_of(const JobDev& J, uint32_t r) { return J.contig ? J.row0 + r : J.rows[r]; }
 
 __device__ __forceinline__ double readlane_d(double v, uint32_t l)
 {
@@ -378,105 +424,237 @@ __device__ __forceinline__ double readlane_d(double v, uint32_t l)
     return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 
-// calculateClusterVariance (:1058-1120), one or two passes at once: pass g
-// (g = 0 forward from base[0], g = 1 backward from base[m-1]) runs on threads
-// [g*kGT, (g+1)*kGT).  Per chunk of <= kCH columns:
-//  * the first wave of the pass fetches the columns and weights (one lane
-//    each), forms the running weight total in the reference's sequential
-//    order through v_readlane (no memory round trip), and the per-column
-//    coefficients (one lane each);
-//  * one thread per row prefetches the chunk's (mean, var) entries into
-//    registers and runs the recurrence, writing the per-row prefix terms
-//    locw*(M/W) and locw*(V*W) to LDS;
-//  * one lane per column sums its terms over the rows in row order.
-// With fu == nullptr only the final variances are formed (initial clusters).
-template <bool TLDS>
-__device__ void variance_passes_t(const JobDev& J, const Common& cm, Ctl& C, const uint32_t* base,
-                                  uint32_t m, int npass, float* fu0, float* fi0, float* fu1, float* fi1,
-                                  unsigned char* pool, uint32_t ch, Prof* pf)
+// Lane l receives lane l+off's value (used only where l < off): permlane
+// swaps for the cross-row steps, DPP row shifts inside a 16-lane row -- VALU
+// only, no LDS round trip.
+template <int OFF>
+__device__ __forceinline__ uint32_t from_lane_plus(uint32_t v)
 {
-    long long t0 = pf ? (long long)clock64() : 0, t1 = 0, tc = 0, trc = 0, trd = 0;
+    if constexpr (OFF == 32) return __builtin_amdgcn_permlane32_swap(v, v, false, false)[1];
+    else if constexpr (OFF == 16) return __builtin_amdgcn_permlane16_swap(v, v, false, false)[1];
+    else return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x100 + OFF, 0xF, 0xF, false);
+}
+template <int OFF>
+__device__ __forceinline__ double from_lane_plus_d(double v)
+{
+    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    const uint32_t lo = from_lane_plus<OFF>((uint32_t)u), hi = from_lane_plus<OFF>((uint32_t)(u >> 32));
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+template <int OFF>
+__device__ __forceinline__ float from_lane_plus_f(float v) { return __uint_as_float(from_lane_plus<OFF>(__float_as_uint(v))); }
+
+// The row-reduction order shared with the oracle (wsum_d / wsum_f): lane l
+// holds the in-order sum of rows l, l+64, ...; the halving tree p[l] +=
+// p[l+off], off = 32..1, leaves the total in lane 0 (lanes >= off compute
+// values nothing reads).  N independent sums are combined level by level.
+template <int N>
+__device__ __forceinline__ void tree_dn(double* p)
+{
+#define ALVRL_TREE_LEVEL(OFF) { double o[N]; _Pragma("unroll") for (int q = 0; q < N; q++) o[q] = from_lane_plus_d<OFF>(p[q]); \
+                                _Pragma("unroll") for (int q = 0; q < N; q++) p[q] = p[q] + o[q]; }
+    ALVRL_TREE_LEVEL(32) ALVRL_TREE_LEVEL(16) ALVRL_TREE_LEVEL(8) ALVRL_TREE_LEVEL(4) ALVRL_TREE_LEVEL(2) ALVRL_TREE_LEVEL(1)
+#undef ALVRL_TREE_LEVEL
+}
+template <int N>
+__device__ __forceinline__ void tree_fn(float* p)
+{
+#define ALVRL_TREE_LEVEL(OFF) { float o[N]; _Pragma("unroll") for (int q = 0; q < N; q++) o[q] = from_lane_plus_f<OFF>(p[q]); \
+                                _Pragma("unroll") for (int q = 0; q < N; q++) p[q] = p[q] + o[q]; }
+    ALVRL_TREE_LEVEL(32) ALVRL_TREE_LEVEL(16) ALVRL_TREE_LEVEL(8) ALVRL_TREE_LEVEL(4) ALVRL_TREE_LEVEL(2) ALVRL_TREE_LEVEL(1)
+#undef ALVRL_TREE_LEVEL
+}
+__device__ __forceinline__ double tree_d(double p) { tree_dn<1>(&p); return p; }
+__device__ __forceinline__ float tree_f(float p) { tree_fn<1>(&p); return p; }
+
+// Per-column coefficients of the recurrence for one chunk (one lane each),
+// the running weight total in the reference's sequential order via
+// v_readlane.  Runs on one full wave; kw = this lane's (weight bits << 32 |
+// vrl) of the chunk (lanes >= cn ignored).
+__device__ __forceinline__ void chunk_coefs(VarGroup& V, Ctl& C, unsigned long long kw, uint32_t cn, Coef* out)
+{
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t vrl = (uint32_t)kw;
+    const double w = lane < cn ? (double)__uint_as_float((uint32_t)(kw >> 32)) : 1.0;
+    if (lane < cn && (!isfinite(w) || w <= 0)) C.err = 1;
+    double W = V.Wcur, Wo = 0.0, Wn = 0.0;
+    for (uint32_t c = 0; c < cn; c++) {
+        const double wc = readlane_d(w, c);
+        if (lane == c) Wo = W;
+        W = W + wc;
+        if (lane == c) Wn = W;
+    }
+    if (lane < cn) {
+        Coef k;
+        k.w = w; k.Wo = Wo; k.Wn = Wn;
+        k.a = (Wn * Wn) / (Wo * Wo);
+        k.rw = 1.0 / w;
+        k.bb = (k.rw + 1.0 / Wo);
+        k.rWn = 1.0 / Wn;
+        k.vrl = vrl; k.pad = 0;
+        out[lane] = k;
+    }
+    if (lane == 0) V.Wcur = W;
+}
+
+// calculateClusterVariance (:1058-1120), one or two passes at once: pass g
+// (g = 0 forward over base[0..m), g = 1 backward) runs on the 4 waves
+// [4g, 4g+4).  Rows are split in 64-row blocks, block b on wave b mod 4 of
+// the pass (lane = row mod 64).  Chunks of kCH columns are software
+// pipelined:
+//  phase 1 (every chunk)  wave 3 forms the coefficients of chunk k+3 (ring of
+//           4; its (vrl, weight) was loaded a chunk earlier) and writes the
+//           last pair's column sums out; the row waves issue the entries of
+//           chunk k+2 (register ring of 3, ids from the LDS coefficients) and
+//           run the recurrence of chunk k, writing each row's prefix terms
+//           locw*(M/W) and locw*(V*W) to T[k & 1][c][block][lane];
+//  phase 2 (every 2nd chunk)  the pass's 4 waves reduce the pair's columns
+//           in the shared row order (in-order over the blocks per lane, then
+//           the lane tree), all of a wave's sums interleaved.
+// No global store and no dependent global load sits on the row waves'
+// critical path.  With FU == false only the final variances are formed.
+template <bool TLDS, bool FU>
+__device__ __noinline__ void variance_passes_t(const JobDev& J, const Common& cm, Ctl& C, const uint32_t* base,
+                                               uint32_t m, int npass, float* fu0, float* fi0, float* fu1, float* fi1,
+                                               unsigned char* pool, Prof* pf)
+{
     const uint32_t R = J.nrows;
-    const uint32_t Rp = R | 1u;
+    const uint32_t NB = (R + 63) / 64;
     const int tid = threadIdx.x;
-    const int g = tid / kGT, lt = tid - g * kGT;
+    const int g = tid / kGT, lt = tid - g * kGT, w = lt >> 6;
+    const uint32_t lane = (uint32_t)(tid & 63);
     const bool active = g < npass;
     float* fu = g == 0 ? fu0 : fu1;
     float* fi = g == 0 ? fi0 : fi1;
     VarGroup& V = C.vg[g];
     double* st = J.st + (size_t)g * 3 * R;
-    double* TU = TLDS ? reinterpret_cast<double*>(pool) + (size_t)g * 2 * kCH * Rp : J.bufM + (size_t)g * kCH * Rp;
-    double* TI = TLDS ? TU + (size_t)kCH * Rp : J.bufV + (size_t)g * kCH * Rp;
-    // (vrl, weight) of every column of the cluster, gathered in parallel once
+    const size_t tsz = (size_t)kCH * NB * 64;          // one chunk's terms
+    double2* T = TLDS ? reinterpret_cast<double2*>(pool) + (size_t)g * 2 * tsz
+                      : reinterpret_cast<double2*>(J.bufM) + (size_t)g * 2 * tsz;
     unsigned long long* cw = J.keys1;
-    for (uint32_t i = tid; i < m; i += kThreads) {
-        const uint32_t vrl = base[i];
-        cw[i] = ((unsigned long long)__float_as_uint(J.colw[vrl]) << 32) | vrl;
+    long long t0 = pf ? (long long)clock64() : 0, t1 = 0, tc = 0, trc = 0, trd = 0;
+    const uint32_t nch = (m + kCH - 1) / kCH;
+    auto cn_of = [&](uint32_t k) { return min((uint32_t)kCH, m - k * kCH); };
+    auto kw_of = [&](uint32_t k) -> unsigned long long {   // this lane's (weight, vrl) of chunk k
+        if (k >= nch) return 0ull;
+        const uint32_t i = k * kCH + min(lane, cn_of(k) - 1);
+        return gp(cw)[g == 0 ? i : m - 1 - i];
+    };
+
+    // (vrl, weight) of every column of the cluster, gathered in parallel once
+    {
+        constexpr int B = 8;
+        for (uint32_t i0 = (uint32_t)tid; i0 < m; i0 += B * kThreads) {
+            uint32_t v[B];
+#pragma unroll
+            for (int b = 0; b < B; b++) v[b] = gp(base)[min(i0 + (uint32_t)b * kThreads, m - 1)];
+            float wv[B];
+#pragma unroll
+            for (int b = 0; b < B; b++) wv[b] = gp(J.colw)[v[b]];
+#pragma unroll
+            for (int b = 0; b < B; b++)
+                if (i0 + (uint32_t)b * kThreads < m)
+                    cw[i0 + (uint32_t)b * kThreads] = ((unsigned long long)__float_as_uint(wv[b]) << 32) | v[b];
+        }
     }
-    if (active) {
-        for (uint32_t r = lt; r < R; r += kGT) { st[r] = 0.0; st[R + r] = 0.0; st[2 * R + r] = 0.0; }
-        if (lt == 0) V.Wcur = 0.0;
+    if (active && lt == 0) V.Wcur = 0.0;
+    __syncthreads();
+    unsigned long long kw_next = 0;                 // wave 3: (weight, vrl) of the next coefficient chunk
+    if (active && w == 3) {
+        for (uint32_t k = 0; k < 3 && k < nch; k++) chunk_coefs(V, C, kw_of(k), cn_of(k), V.cf[k]);
+        kw_next = kw_of(3);
     }
     __syncthreads();
-    for (uint32_t c0 = 0; c0 < m; c0 += ch) {
-        const uint32_t cn = min(ch, m - c0);
-        if (active && lt < 64) {
-            const uint32_t lane = (uint32_t)lt;
-            uint32_t vrl = 0;
-            double w = 1.0;
-            if (lane < cn) {
-                const uint32_t i = c0 + lane;
-                const unsigned long long k = cw[g == 0 ? i : m - 1 - i];
-                vrl = (uint32_t)k;
-                w = (double)__uint_as_float((uint32_t)(k >> 32));
-                if (!isfinite(w) || w <= 0) C.err = 1;
-            }
-            double W = V.Wcur, Wo = 0.0, Wn = 0.0;
-            for (uint32_t c = 0; c < cn; c++) {
-                const double wc = readlane_d(w, c);
-                if (lane == c) Wo = W;
-                W = W + wc;
-                if (lane == c) Wn = W;
-            }
-            if (lane < cn) {
-                Coef k;
-                k.w = w; k.Wo = Wo; k.Wn = Wn;
-                k.a = (Wn * Wn) / (Wo * Wo);
-                k.rw = 1.0 / w;
-                k.bb = (k.rw + 1.0 / Wo);
-                k.rWn = 1.0 / Wn;
-                k.pad = 0.0;
-                V.cf[lane] = k;
-                V.cv[lane] = vrl;
-            }
-            if (lane == 0) V.Wcur = W;
-        }
-        __syncthreads();
-        if (pf) { t1 = clock64(); tc += t1 - t0; t0 = t1; }
-        if (active) {
-            for (uint32_t r = lt; r < R; r += kGT) {
-                const size_t row = row_of(J, r);
-                uint32_t cvv[kCH];
+
+    // the first block of this wave lives in registers across chunks
+    const uint32_t b0 = (uint32_t)w;
+    const bool own = active && b0 < NB && b0 * 64 + lane < R;
+    const uint32_t r0 = b0 * 64 + lane;
+    const RowRef rr0 = own ? row_ref(J, r0) : RowRef{0, 0};
+    const double lw0 = own ? J.locw[r0] : 0.0;
+    double sum0 = 0.0, M0 = 0.0, V0 = 0.0;
+    float2 bufA[kCH], bufB[kCH], bufC[kCH];
+    auto load_chunk = [&](uint32_t k, float2* dst) {    // ids from the LDS coefficients of chunk k
+        const Coef* cf = V.cf[k % 4];
+        const uint32_t cn = cn_of(k);
 #pragma unroll
-                for (int c = 0; c < kCH; c++) cvv[c] = V.cv[(uint32_t)c < cn ? c : 0];
+#ifdef ALVRL_EXP_NOLOAD
+        for (int c = 0; c < kCH; c++) dst[c] = make_float2((float)cf[(uint32_t)c < cn ? c : 0].vrl * 1e-7f + rr0.base * 1e-9f, 0.25f);
+#else
+        for (int c = 0; c < kCH; c++) dst[c] = ldg2(cm.Rt, rr0.base + (size_t)cf[(uint32_t)c < cn ? c : 0].vrl * rr0.stride);
+#endif
+    };
+    if (own) { load_chunk(0, bufA); if (nch > 1) load_chunk(1, bufB); }
+    if (active && NB > 4)
+        for (uint32_t b = b0 + 4; b < NB; b += 4)
+            if (b * 64 + lane < R) { const uint32_t r = b * 64 + lane; st[r] = 0.0; st[R + r] = 0.0; st[2 * R + r] = 0.0; }
+    if (pf) { t1 = clock64(); tc += t1 - t0; t0 = t1; }
+
+    constexpr int NQ = kCH / 4;                      // columns per wave per chunk in phase 2
+    // phase 1 of chunk k: entries in cur, chunk k+2's into pre
+    auto step = [&](uint32_t k, float2* cur, float2* pre) {
+        const uint32_t c0 = k * kCH, cn = cn_of(k);
+        const Coef* cf = V.cf[k % 4];
+        double2* Tk = T + (size_t)(k & 1) * tsz;
+        if (FU && active && w == 3 && k >= 2 && (k & 1) == 0 && lane < 2u * kCH) {
+            // the pair (k-2, k-1) was reduced after chunk k-1: write it out
+            const uint32_t j = lane / kCH, c = lane % kCH, kk = k - 2 + j;
+            if (c < cn_of(kk)) { const uint32_t n = kk * kCH + c; fu[n] = V.res_fu[lane]; fi[n] = V.res_fi[lane]; }
+        }
+        if (active && w == 3 && k + 3 < nch) {
+            chunk_coefs(V, C, kw_next, cn_of(k + 3), V.cf[(k + 3) % 4]);
+            kw_next = kw_of(k + 4);
+        }
+        if (own) {
+            if (k + 2 < nch) load_chunk(k + 2, pre);      // in flight during the next two chunks
+            if (cn == (uint32_t)kCH && k > 0) {            // full chunk, no first column: no guards
+                Coef qn = cf[0];
+#pragma unroll
+                for (int c = 0; c < kCH; c++) {
+                    const Coef q = qn;
+                    if (c + 1 < kCH) qn = cf[c + 1];
+                    const double x = (double)cur[c].x;
+                    const double tmp = q.w * sum0 - q.Wo * x;
+                    M0 = q.a * M0 + q.bb * (tmp * tmp);
+                    V0 = V0 + (double)cur[c].y * q.rw;
+                    sum0 = sum0 + x;
+                    if (FU) Tk[((size_t)c * NB + b0) * 64 + lane] = make_double2(lw0 * (M0 * q.rWn), lw0 * (V0 * q.Wn));
+                }
+            } else {
+#pragma unroll
+                for (int c = 0; c < kCH; c++) {
+                    if ((uint32_t)c < cn) {
+                        const Coef q = cf[c];
+                        const double x = (double)cur[c].x;
+                        const double tmp = q.w * sum0 - q.Wo * x;
+                        if (c0 + c > 0) M0 = q.a * M0 + q.bb * (tmp * tmp);
+                        V0 = V0 + (double)cur[c].y * q.rw;
+                        sum0 = sum0 + x;
+                        if (FU) Tk[((size_t)c * NB + b0) * 64 + lane] = make_double2(lw0 * (M0 * q.rWn), lw0 * (V0 * q.Wn));
+                    }
+                }
+            }
+        }
+        if (active && NB > 4) {
+            for (uint32_t b = b0 + 4; b < NB; b += 4) {
+                if (b * 64 + lane >= R) continue;
+                const uint32_t r = b * 64 + lane;
+                const RowRef rr = row_ref(J, r);
+                const double lw = J.locw[r];
                 float2 e[kCH];
 #pragma unroll
-                for (int c = 0; c < kCH; c++) e[c] = cm.Rt[(size_t)cvv[c] * cm.ld + row];
-                const double lw = J.locw[r];
+                for (int c = 0; c < kCH; c++) e[c] = ldg2(cm.Rt, rr.base + (size_t)cf[(uint32_t)c < cn ? c : 0].vrl * rr.stride);
                 double sum = st[r], M = st[R + r], Vs = st[2 * R + r];
 #pragma unroll
                 for (int c = 0; c < kCH; c++) {
                     if ((uint32_t)c < cn) {
-                        const Coef k = V.cf[c];
+                        const Coef q = cf[c];
                         const double x = (double)e[c].x;
-                        const double tmp = k.w * sum - k.Wo * x;
-                        if (c0 + c > 0) M = k.a * M + k.bb * (tmp * tmp);
-                        Vs = Vs + (double)e[c].y * k.rw;
+                        const double tmp = q.w * sum - q.Wo * x;
+                        if (c0 + c > 0) M = q.a * M + q.bb * (tmp * tmp);
+                        Vs = Vs + (double)e[c].y * q.rw;
                         sum = sum + x;
-                        if (fu) {
-                            TU[(size_t)c * Rp + r] = lw * (M * k.rWn);
-                            TI[(size_t)c * Rp + r] = lw * (Vs * k.Wn);
-                        }
+                        if (FU) Tk[((size_t)c * NB + b) * 64 + lane] = make_double2(lw * (M * q.rWn), lw * (Vs * q.Wn));
                     }
                 }
                 st[r] = sum; st[R + r] = M; st[2 * R + r] = Vs;
@@ -484,33 +662,83 @@ __device__ void variance_passes_t(const JobDev& J, const Common& cm, Ctl& C, con
         }
         __syncthreads();
         if (pf) { t1 = clock64(); trc += t1 - t0; t0 = t1; }
-        if (active && fu && lt < (int)cn) {
-            const uint32_t c = (uint32_t)lt, n = c0 + c;
-            const double* tu = TU + (size_t)c * Rp;
-            const double* ti = TI + (size_t)c * Rp;
-            double pu = 0.0, pi = 0.0;
-#pragma unroll 16
-            for (uint32_t r = 0; r < R; r++) { pi = pi + ti[r]; pu = pu + tu[r]; }
-            fi[n] = (float)pi;
-            fu[n] = n == 0 ? 0.0f : (float)pu;
+    };
+    // phase 2: reduce chunks kf .. kf+nk-1 (nk <= 2) into the staging sums
+    auto reduce = [&](uint32_t kf, uint32_t nk) {
+        if (active) {
+            double pz[4 * NQ];                       // [pu of 2*NQ columns, pi of 2*NQ columns]
+#pragma unroll
+            for (int j = 0; j < 2; j++) {
+#pragma unroll
+                for (int q = 0; q < NQ; q++) {
+                    const uint32_t c = (uint32_t)w + 4u * q;
+                    double pu = 0.0, pi = 0.0;
+                    if ((uint32_t)j < nk && c < cn_of(kf + j)) {
+                        const double2* Tk = T + (size_t)((kf + j) & 1) * tsz;
+                        for (uint32_t b = 0; b < NB; b++) {
+                            if (b * 64 + lane < R) {
+                                const double2 t = Tk[((size_t)c * NB + b) * 64 + lane];
+                                pu = pu + t.x; pi = pi + t.y;
+                            }
+                        }
+                    }
+                    pz[j * NQ + q] = pu;
+                    pz[2 * NQ + j * NQ + q] = pi;
+                }
+            }
+            tree_dn<4 * NQ>(pz);
+            if (lane == 0) {
+#pragma unroll
+                for (int j = 0; j < 2; j++) {
+#pragma unroll
+                    for (int q = 0; q < NQ; q++) {
+                        const uint32_t c = (uint32_t)w + 4u * q;
+                        if ((uint32_t)j < nk && c < cn_of(kf + j)) {
+                            const uint32_t slot = (uint32_t)j * kCH + c;
+                            V.res_fi[slot] = (float)pz[2 * NQ + j * NQ + q];
+                            V.res_fu[slot] = (kf + j) * kCH + c == 0 ? 0.0f : (float)pz[j * NQ + q];
+                        }
+                    }
+                }
+            }
         }
+        __syncthreads();
         if (pf) { t1 = clock64(); trd += t1 - t0; t0 = t1; }
-        // the next chunk's coefficient phase runs on the wave that just did
-        // the column sums, and the next recurrence waits at the barrier
+    };
+    static_assert(kCH % 4 == 0, "phase 2: 4 waves x kCH/4 columns per chunk");
+    auto after = [&](uint32_t k) { if (FU && (k & 1)) reduce(k - 1, 2); };
+    for (uint32_t k = 0; k < nch; k += 3) {
+        step(k, bufA, bufC); after(k);
+        if (k + 1 < nch) { step(k + 1, bufB, bufA); after(k + 1); }
+        if (k + 2 < nch) { step(k + 2, bufC, bufB); after(k + 2); }
     }
+    if (FU && (nch & 1)) reduce(nch - 1, 1);
+    // the last pair's sums, the final variances
+    if (FU && active && w == 3 && nch > 0 && lane < 2u * kCH) {
+        const uint32_t kf = (nch & 1) ? nch - 1 : nch - 2;
+        const uint32_t j = lane / kCH, c = lane % kCH, kk = kf + j;
+        if (kk < nch && c < cn_of(kk)) { const uint32_t n = kk * kCH + c; fu[n] = V.res_fu[lane]; fi[n] = V.res_fi[lane]; }
+    }
+    if (own) { st[r0] = sum0; st[R + r0] = M0; st[2 * R + r0] = V0; }
     __syncthreads();
-    if (active && lt == 0) {
-        if (fu) {
-            V.res_u = fu[m - 1]; V.res_i = fi[m - 1];
+    if (active && w == 0) {
+        if (FU) {
+            if (lane == 0) { V.res_u = fu[m - 1]; V.res_i = fi[m - 1]; }
         } else {
-            const double W = V.Wcur, rW = 1.0 / W;
+            const double Wt = V.Wcur, rW = 1.0 / Wt;
             double pu = 0.0, pi = 0.0;
-            for (uint32_t r = 0; r < R; r++) pu = pu + J.locw[r] * (st[R + r] * rW);
-            for (uint32_t r = 0; r < R; r++) pi = pi + J.locw[r] * (st[2 * R + r] * W);
-            V.res_u = (float)pu; V.res_i = (float)pi;
+            for (uint32_t r = lane; r < R; r += 64) {
+                pu = pu + J.locw[r] * (st[R + r] * rW);
+                pi = pi + J.locw[r] * (st[2 * R + r] * Wt);
+            }
+            pu = tree_d(pu);
+            pi = tree_d(pi);
+            if (lane == 0) { V.res_u = (float)pu; V.res_i = (float)pi; }
         }
-        if (!isfinite(V.res_u) || V.res_u < 0) C.err = 1;
-        if (!isfinite(V.res_i) || V.res_i < 0) C.err = 1;
+        if (lane == 0) {
+            if (!isfinite(V.res_u) || V.res_u < 0) C.err = 1;
+            if (!isfinite(V.res_i) || V.res_i < 0) C.err = 1;
+        }
     }
     __syncthreads();
     if (pf) { pf->count(PF_V_COEF, tc); pf->count(PF_V_REC, trc); pf->count(PF_V_RED, trd); }
@@ -520,51 +748,24 @@ __device__ void variance_passes(const JobDev& J, const Common& cm, Ctl& C, const
                                 int npass, float* fu0, float* fi0, float* fu1, float* fi1, unsigned char* pool,
                                 Prof* pf = nullptr)
 {
-    const uint32_t Rp = J.nrows | 1u;
+    const uint32_t NB = (J.nrows + 63) / 64;
     if (pf && (!pf->p || threadIdx.x != 0)) pf = nullptr;
-    if ((size_t)2 * 2 * kCH * Rp * sizeof(double) <= kPoolBytes)
-        variance_passes_t<true>(J, cm, C, base, m, npass, fu0, fi0, fu1, fi1, pool, (uint32_t)kCH, pf);
-    else
-        variance_passes_t<false>(J, cm, C, base, m, npass, fu0, fi0, fu1, fi1, pool, (uint32_t)kCH, pf);
+    const bool lds = (size_t)2 * 2 * kCH * NB * 64 * sizeof(double2) <= kPoolBytes;
+    if (fu0) {
+        if (lds) variance_passes_t<true, true>(J, cm, C, base, m, npass, fu0, fi0, fu1, fi1, pool, pf);
+        else variance_passes_t<false, true>(J, cm, C, base, m, npass, fu0, fi0, fu1, fi1, pool, pf);
+    } else {
+        if (lds) variance_passes_t<true, false>(J, cm, C, base, m, npass, fu0, fi0, fu1, fi1, pool, pf);
+        else variance_passes_t<false, false>(J, cm, C, base, m, npass, fu0, fi0, fu1, fi1, pool, pf);
+    }
 }
 
 __device__ __forceinline__ unsigned char* pool_end(void* pool) { return reinterpret_cast<unsigned char*>(pool) + kPoolBytes; }
 
-// Stages the (mean, var) entries of ncols columns (ids[c], c < ncols) into
-// LDS as S[r * ncols + c] (MEANS: floats of the means only): coalesced row
-// runs of one column per group of consecutive threads.
-template <bool MEANS>
-__device__ void stage_tile(const JobDev& J, const Common& cm, const uint32_t* ids, uint32_t ncols, void* S)
-{
-    const uint32_t R = J.nrows;
-    const uint32_t total = ncols * R;
-    const int tid = threadIdx.x;
-    uint32_t c = (uint32_t)tid / R, r = (uint32_t)tid - c * R;
-    const uint32_t dc = (uint32_t)kThreads / R, dr = (uint32_t)kThreads - dc * R;
-    constexpr int B = 8;                       // loads in flight per thread
-    for (uint32_t e0 = (uint32_t)tid; e0 < total; e0 += B * kThreads) {
-        uint32_t cc[B], rr[B];
-        float2 v[B];
-#pragma unroll
-        for (int b = 0; b < B; b++) {
-            cc[b] = c; rr[b] = r;
-            r += dr; c += dc;
-            if (r >= R) { r -= R; c++; }
-        }
-#pragma unroll
-        for (int b = 0; b < B; b++) {
-            const bool ok = e0 + (uint32_t)b * kThreads < total;
-            v[b] = cm.Rt[(size_t)ids[ok ? cc[b] : 0] * cm.ld + row_of(J, ok ? rr[b] : 0)];
-        }
-#pragma unroll
-        for (int b = 0; b < B; b++) {
-            if (e0 + (uint32_t)b * kThreads < total) {
-                if (MEANS) reinterpret_cast<float*>(S)[(size_t)rr[b] * ncols + cc[b]] = v[b].x;
-                else reinterpret_cast<float2*>(S)[(size_t)rr[b] * ncols + cc[b]] = v[b];
-            }
-        }
-    }
-}
+// Column reductions over the rows, one wave per column, kCB columns per wave
+// at a time (their loads in flight together), rows in the shared order.
+constexpr int kCB = 8;
+constexpr int kRB = 4;                 // row blocks kept in registers (R <= 256)
 
 // ------------------------------------------------------------- sort --
 __device__ __forceinline__ unsigned long long proj_key(float p, uint32_t vrl)
@@ -576,7 +777,7 @@ __device__ __forceinline__ unsigned long long proj_key(float p, uint32_t vrl)
 }
 
 // Sorts J.keys0[0..m); returns the buffer holding the result.
-__device__ unsigned long long* sort_keys(const JobDev& J, Ctl& C, uint32_t m, unsigned long long* lds)
+__device__ __noinline__ unsigned long long* sort_keys(const JobDev& J, Ctl& C, uint32_t m, unsigned long long* lds)
 {
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     if (m <= (uint32_t)kBitonicMax) {
@@ -657,6 +858,103 @@ __device__ unsigned long long* sort_keys(const JobDev& J, Ctl& C, uint32_t m, un
     return src;
 }
 
+// Projections of split() (:625-640): one wave per column, kCB columns per
+// batch, rows in the shared order (norm, then the normalised dot product with
+// the split direction).  For R <= 64*kRB the batch's entries stay in
+// registers for both sums and the next batch's loads are in flight while
+// the current one is reduced (ping-pong buffers, no copies).
+__device__ __noinline__ void split_projections(const JobDev& J, const Common& cm, uint32_t begin, uint32_t m)
+{
+    const uint32_t R = J.nrows;
+    const int wave = threadIdx.x >> 6;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t stride = kWaves * kCB;
+    if (R <= 64u * kRB) {
+        float d[kRB];
+        RowRef row[kRB];
+#pragma unroll
+        for (int rb = 0; rb < kRB; rb++) {
+            const uint32_t r = lane + 64u * rb;
+            d[rb] = r < R ? J.dir[r] : 0.0f;
+            row[rb] = row_ref(J, r < R ? r : 0);
+        }
+        uint32_t vA[kCB], vB[kCB];
+        float xA[kRB][kCB], xB[kRB][kCB];
+        auto load = [&](uint32_t j0, uint32_t* v, float (*x)[kCB]) {
+#pragma unroll
+            for (int q = 0; q < kCB; q++) v[q] = gp(J.vrls)[begin + min(j0 + (uint32_t)q, m - 1)];
+#pragma unroll
+            for (int rb = 0; rb < kRB; rb++)
+#pragma unroll
+                for (int q = 0; q < kCB; q++) x[rb][q] = ldg2(cm.Rt, row[rb].base + (size_t)v[q] * row[rb].stride).x;
+        };
+        auto reduce = [&](uint32_t j0, const uint32_t* v, float (*x)[kCB]) {
+            float pn[kCB], pp[kCB];
+#pragma unroll
+            for (int q = 0; q < kCB; q++) { pn[q] = 0.0f; pp[q] = 0.0f; }
+#pragma unroll
+            for (int rb = 0; rb < kRB; rb++)
+                if (lane + 64u * rb < R) {
+#pragma unroll
+                    for (int q = 0; q < kCB; q++) { const float a = fabsf(x[rb][q]); pn[q] = pn[q] + a * a; }
+                }
+            tree_fn<kCB>(pn);
+            float nc[kCB];
+#pragma unroll
+            for (int q = 0; q < kCB; q++) nc[q] = sqrtf(__shfl(pn[q], 0, 64));
+#pragma unroll
+            for (int rb = 0; rb < kRB; rb++)
+                if (lane + 64u * rb < R) {
+#pragma unroll
+                    for (int q = 0; q < kCB; q++) pp[q] = pp[q] + d[rb] * (x[rb][q] / nc[q]);
+                }
+            tree_fn<kCB>(pp);
+            if (lane == 0) {
+#pragma unroll
+                for (int q = 0; q < kCB; q++)
+                    if (j0 + q < m) J.keys0[j0 + q] = proj_key(nc[q] != 0 ? pp[q] : 0.0f, v[q]);
+            }
+        };
+        uint32_t j0 = (uint32_t)wave * kCB;
+        if (j0 < m) load(j0, vA, xA);
+        for (; j0 < m; j0 += 2 * stride) {
+            if (j0 + stride < m) load(j0 + stride, vB, xB);
+            reduce(j0, vA, xA);
+            if (j0 + stride >= m) break;
+            if (j0 + 2 * stride < m) load(j0 + 2 * stride, vA, xA);
+            reduce(j0 + stride, vB, xB);
+        }
+    } else {                                // tall local matrices: two passes from memory
+        for (uint32_t j0 = (uint32_t)wave * kCB; j0 < m; j0 += stride) {
+            uint32_t vr[kCB];
+#pragma unroll
+            for (int q = 0; q < kCB; q++) vr[q] = J.vrls[begin + min(j0 + (uint32_t)q, m - 1)];
+            float pn[kCB], pp[kCB];
+#pragma unroll
+            for (int q = 0; q < kCB; q++) { pn[q] = 0.0f; pp[q] = 0.0f; }
+            for (uint32_t r = lane; r < R; r += 64) {
+                const RowRef rw = row_ref(J, r);
+#pragma unroll
+                for (int q = 0; q < kCB; q++) { const float a = fabsf(ldg2(cm.Rt, rw.base + (size_t)vr[q] * rw.stride).x); pn[q] = pn[q] + a * a; }
+            }
+            float nc[kCB];
+#pragma unroll
+            for (int q = 0; q < kCB; q++) nc[q] = sqrtf(__shfl(tree_f(pn[q]), 0, 64));
+            for (uint32_t r = lane; r < R; r += 64) {
+                const RowRef rw = row_ref(J, r);
+                const float dd = J.dir[r];
+#pragma unroll
+                for (int q = 0; q < kCB; q++) pp[q] = pp[q] + dd * (ldg2(cm.Rt, rw.base + (size_t)vr[q] * rw.stride).x / nc[q]);
+            }
+#pragma unroll
+            for (int q = 0; q < kCB; q++) {
+                const float pr = tree_f(pp[q]);
+                if (lane == 0 && j0 + q < m) J.keys0[j0 + q] = proj_key(nc[q] != 0 ? pr : 0.0f, vr[q]);
+            }
+        }
+    }
+}
+
 // ------------------------------------------------------------ split --
 // Clustering::split (:590-684), collective.
 __device__ void split(const JobDev& J, const Common& cm, Ctl& C, uint32_t begin, uint32_t end,
@@ -671,28 +969,47 @@ __device__ void split(const JobDev& J, const Common& cm, Ctl& C, uint32_t begin,
     // the two centres (:597-602): weights gathered in parallel into contiguous
     // LDS (or scratch for large clusters), scanned by one lane
     float* wv = (size_t)m * 4 <= kPoolBytes ? reinterpret_cast<float*>(lds) : J.fei;
-    for (uint32_t i = tid; i < m; i += kThreads) wv[i] = J.colw[J.vrls[begin + i]];
+    {
+        constexpr int B = 8;
+        for (uint32_t i0 = (uint32_t)tid; i0 < m; i0 += B * kThreads) {
+            uint32_t v[B];
+#pragma unroll
+            for (int b = 0; b < B; b++) v[b] = gp(J.vrls)[begin + min(i0 + (uint32_t)b * kThreads, m - 1)];
+            float x[B];
+#pragma unroll
+            for (int b = 0; b < B; b++) x[b] = gp(J.colw)[v[b]];
+#pragma unroll
+            for (int b = 0; b < B; b++)
+                if (i0 + (uint32_t)b * kThreads < m) wv[i0 + (uint32_t)b * kThreads] = x[b];
+        }
+    }
     __syncthreads();
-    if (tid == 0) {
+    if (wave == 0) {
         Smp smp;
         smp.init(cm.seed, cm.pass, begin, end, J.stage_refine);
-        const uint32_t i1 = weighted_sample_gathered(wv, m, smp, &C.err);
-        wv[i1] = 0.0f;                     // colw[vrl1] = 0 for the second draw
-        const uint32_t i2 = weighted_sample_gathered(wv, m, smp, &C.err);
-        C.vrl1 = J.vrls[begin + i1]; C.vrl2 = J.vrls[begin + i2]; C.draw_k = smp.k;
+        int e = 0;
+        const uint32_t i1 = weighted_sample_wave(wv, m, smp, &e, 0xFFFFFFFFu);
+        const uint32_t i2 = weighted_sample_wave(wv, m, smp, &e, i1);   // colw[vrl1] = 0
+        if (lane == 0) {
+            if (e) C.err = 1;
+            C.vrl1 = J.vrls[begin + i1]; C.vrl2 = J.vrls[begin + i2]; C.draw_k = smp.k;
+        }
     }
     __syncthreads();
     pf.mark(PF_WSAMP);
     const uint32_t vrl1 = C.vrl1, vrl2 = C.vrl2;
-    // |c1|, |c2|, |c2 - c1| (:607-616): three lanes, rows in order
-    if (tid < 3) {
-        float p = 0.0f;
-        for (uint32_t r = 0; r < R; r++) {
-            const float a = Rmean(cm, row_of(J, r), vrl1), b = Rmean(cm, row_of(J, r), vrl2);
-            const float u = fabsf(tid == 0 ? a : (tid == 1 ? b : b - a));
-            p = p + u * u;
+    // |c1|, |c2|, |c2 - c1| (:607-616), rows in the shared order
+    if (wave == 0) {
+        float p1 = 0.0f, p2 = 0.0f, pd = 0.0f;
+        for (uint32_t r = lane; r < R; r += 64) {
+            const RowRef rr = row_ref(J, r);
+            const float a = Rmean(cm, rr, vrl1), b = Rmean(cm, rr, vrl2);
+            const float d = b - a;
+            const float ua = fabsf(a), ub = fabsf(b), ud = fabsf(d);
+            p1 = p1 + ua * ua; p2 = p2 + ub * ub; pd = pd + ud * ud;
         }
-        C.nrm3[tid] = sqrtf(p);
+        p1 = tree_f(p1); p2 = tree_f(p2); pd = tree_f(pd);
+        if (lane == 0) { C.nrm3[0] = sqrtf(p1); C.nrm3[1] = sqrtf(p2); C.nrm3[2] = sqrtf(pd); }
     }
     __syncthreads();
     if (tid == 0) {
@@ -703,7 +1020,8 @@ __device__ void split(const JobDev& J, const Common& cm, Ctl& C, uint32_t begin,
     if (!C.degenerate) {
         const float dl = C.diffLen;
         for (uint32_t r = tid; r < R; r += kThreads) {
-            const float a = Rmean(cm, row_of(J, r), vrl1), b = Rmean(cm, row_of(J, r), vrl2);
+            const RowRef rr = row_ref(J, r);
+            const float a = Rmean(cm, rr, vrl1), b = Rmean(cm, rr, vrl2);
             J.dir[r] = (b - a) / dl;
         }
         __syncthreads();
@@ -716,10 +1034,11 @@ __device__ void split(const JobDev& J, const Common& cm, Ctl& C, uint32_t begin,
                 J.dir[r] = det_std_normal_x(sx, sy);
             }
             __syncthreads();
-            if (tid == 0) {
+            if (wave == 0) {
                 float p = 0.0f;
-                for (uint32_t r = 0; r < R; r++) { const float u = fabsf(J.dir[r]); p = p + u * u; }
-                C.nd = sqrtf(p);
+                for (uint32_t r = lane; r < R; r += 64) { const float u = fabsf(J.dir[r]); p = p + u * u; }
+                p = tree_f(p);
+                if (lane == 0) C.nd = sqrtf(p);
             }
             __syncthreads();
             if (C.nd != 0) break;
@@ -735,48 +1054,8 @@ __device__ void split(const JobDev& J, const Common& cm, Ctl& C, uint32_t begin,
         __syncthreads();
     }
     pf.mark(PF_DIR);
-    // projections (:625-640): one lane per column, rows in order, over
-    // column tiles staged in LDS (or straight from global for tall matrices)
-    const uint32_t tcols = min((uint32_t)kThreads, (uint32_t)(kPoolBytes / (R * 4u) - 1u) & ~63u);
-    if (tcols >= 64) {
-        float* S = reinterpret_cast<float*>(lds);
-        float* sdir = reinterpret_cast<float*>(pool_end(lds)) - R;    // R floats at the top of the pool
-        for (uint32_t r = tid; r < R; r += kThreads) sdir[r] = J.dir[r];
-        for (uint32_t t0 = 0; t0 < m; t0 += tcols) {
-            const uint32_t tn = min(tcols, m - t0);
-            stage_tile<true>(J, cm, J.vrls + begin + t0, tn, S);
-            __syncthreads();
-            pf.mark(PF_P_STAGE);
-            if ((uint32_t)tid < tn) {
-                const uint32_t j = t0 + tid;
-                float pn = 0.0f;
-#pragma unroll 8
-                for (uint32_t r = 0; r < R; r++) { const float a = fabsf(S[(size_t)r * tn + tid]); pn = pn + a * a; }
-                const float nc = sqrtf(pn);
-                float proj = 0.0f;
-                if (nc != 0) {
-#pragma unroll 8
-                    for (uint32_t r = 0; r < R; r++) proj = proj + sdir[r] * (S[(size_t)r * tn + tid] / nc);
-                }
-                J.keys0[j] = proj_key(proj, J.vrls[begin + j]);
-            }
-            __syncthreads();
-            pf.mark(PF_P_COMP);
-        }
-    } else {
-        for (uint32_t j = tid; j < m; j += kThreads) {
-            const uint32_t vrl = J.vrls[begin + j];
-            const float2* col = cm.Rt + (size_t)vrl * cm.ld;
-            float pn = 0.0f;
-            for (uint32_t r = 0; r < R; r++) { const float a = fabsf(col[row_of(J, r)].x); pn = pn + a * a; }
-            const float nc = sqrtf(pn);
-            float proj = 0.0f;
-            if (nc != 0)
-                for (uint32_t r = 0; r < R; r++) proj = proj + J.dir[r] * (col[row_of(J, r)].x / nc);
-            J.keys0[j] = proj_key(proj, vrl);
-        }
-        __syncthreads();
-    }
+    split_projections(J, cm, begin, m);
+    __syncthreads();
     pf.mark(PF_PROJ);
     const unsigned long long* sorted = sort_keys(J, C, m, lds);
     for (uint32_t i = tid; i < m; i += kThreads) J.vrls[begin + i] = (uint32_t)sorted[i];
@@ -824,7 +1103,8 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
     __shared__ Ctl C;
     __shared__ __attribute__((aligned(16))) unsigned char pool[kPoolBytes];
     unsigned long long* lds = reinterpret_cast<unsigned long long*>(pool);
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, wave = tid >> 6;
+    const uint32_t lane = (uint32_t)(tid & 63);
     const uint32_t N = cm.nvrl, R = J.nrows;
     const uint32_t nv = cm.init_off[cm.ninit];
     Prof pf{cm.prof, (long long)clock64()};
@@ -835,31 +1115,33 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
     }
     __syncthreads();
     // calculateColumnWeigths (:985-1008)
-    // one lane per column, rows in order, over column tiles staged in LDS
-    // (the identity column list is the J.vrls scratch before it is filled)
-    for (uint32_t v = tid; v < N; v += kThreads) J.vrls[v] = v;
-    __syncthreads();
-    {
-        const uint32_t tcols = min((uint32_t)kThreads, (uint32_t)(kPoolBytes / (R * 8u)) & ~63u);
-        const uint32_t step_c = tcols >= 64 ? tcols : (uint32_t)kThreads;
-        for (uint32_t t0 = 0; t0 < N; t0 += step_c) {
-            const uint32_t tn = min(step_c, N - t0);
-            if (tcols >= 64) { stage_tile<false>(J, cm, J.vrls + t0, tn, lds); __syncthreads(); }
-            if ((uint32_t)tid < tn) {
-                const uint32_t v = t0 + tid;
-                const float2* S = reinterpret_cast<const float2*>(lds);
-                double p = 0.0;
-                for (uint32_t r = 0; r < R; r++) {
-                    const float2 mv = tcols >= 64 ? S[(size_t)r * tn + tid] : cm.Rt[(size_t)v * cm.ld + row_of(J, r)];
-                    const double mean = (double)mv.x, var = (double)mv.y;
-                    const double x = mean * mean + var;
-                    p = p + J.locw[r] * x;
-                }
-                const float cw = (float)sqrt(p > 0.0 ? p : 0.0);
-                J.colw[v] = cw;
+    // calculateColumnWeigths: one wave per column, kCB columns in flight,
+    // rows in the shared order
+    for (uint32_t v0 = (uint32_t)wave * kCB; v0 < N; v0 += kWaves * kCB) {
+        double p[kCB];
+#pragma unroll
+        for (int q = 0; q < kCB; q++) p[q] = 0.0;
+        for (uint32_t r = lane; r < R; r += 64) {
+            const RowRef rr = row_ref(J, r);
+            const double lw = J.locw[r];
+            float2 mv[kCB];
+#pragma unroll
+            for (int q = 0; q < kCB; q++) mv[q] = ldg2(cm.Rt, rr.base + (size_t)min(v0 + (uint32_t)q, N - 1) * rr.stride);
+#pragma unroll
+            for (int q = 0; q < kCB; q++) {
+                const double mean = (double)mv[q].x, var = (double)mv[q].y;
+                const double x = mean * mean + var;
+                p[q] = p[q] + lw * x;
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < kCB; q++) {
+            const double t = tree_d(p[q]);
+            if (lane == 0 && v0 + q < N) {
+                const float cw = (float)sqrt(t > 0.0 ? t : 0.0);
+                J.colw[v0 + q] = cw;
                 if (!isfinite(cw)) C.err = 1;
             }
-            __syncthreads();
         }
     }
     __syncthreads();
@@ -897,7 +1179,7 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
     pf.mark(PF_INIT);
     // calculateUnclusteredVariance (:1022-1048): per-row Welford in m_vrls order
     for (uint32_t r = tid; r < R; r += kThreads) {
-        const size_t row = row_of(J, r);
+        const RowRef rr = row_ref(J, r);
         double mean = 0.0, M2 = 0.0, sv = 0.0;
         for (uint32_t n0 = 0; n0 < nv; n0 += kCH) {
             uint32_t ids[kCH];
@@ -905,7 +1187,7 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
             for (int k = 0; k < kCH; k++) ids[k] = J.vrls[n0 + k < nv ? n0 + k : 0];
             float2 e[kCH];
 #pragma unroll
-            for (int k = 0; k < kCH; k++) e[k] = cm.Rt[(size_t)ids[k] * cm.ld + row];
+            for (int k = 0; k < kCH; k++) e[k] = ldg2(cm.Rt, rr.base + (size_t)ids[k] * rr.stride);
 #pragma unroll
             for (int k = 0; k < kCH; k++) {
                 if (n0 + k < nv) {
@@ -921,11 +1203,15 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
         J.st[r] = sv; J.st[R + r] = M2;
     }
     __syncthreads();
-    if (tid == 0) {
+    if (wave == 0) {
         double pv = 0.0, pm = 0.0;
-        for (uint32_t r = 0; r < R; r++) pv = pv + J.locw[r] * J.st[r];
-        for (uint32_t r = 0; r < R; r++) pm = pm + J.locw[r] * J.st[R + r];
-        {
+        for (uint32_t r = lane; r < R; r += 64) {
+            pv = pv + J.locw[r] * J.st[r];
+            pm = pm + J.locw[r] * J.st[R + r];
+        }
+        pv = tree_d(pv);
+        pm = tree_d(pm);
+        if (lane == 0) {
             if (nv <= 1) C.err = 1;
             C.unclIntVar = (float)pv;
             C.tracingVar = (float)(pm - (double)C.unclIntVar);
@@ -1049,6 +1335,8 @@ struct HostJob {
     float pixel_under, undersampling, depth_correction;
     int do_refine;
     uint32_t stage_refine, stage_sample;
+    const uint64_t* row_off;      // optional per-row layout, see alvrl_cluster_job
+    const uint32_t* row_stride;
 };
 
 // Runs every clustering job on the device (one workgroup each) and copies the
@@ -1083,39 +1371,52 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
     auto job_bytes = [&](uint32_t R) {
         return align_up(N * 4) * 2 + align_up(N * sizeof(CNode)) * 2 + align_up(N * 4) * 2 +
                align_up((size_t)R * 4) + align_up(N * 8) * 2 + align_up(N * 4) * 4 +
-               align_up((size_t)6 * R * 8) + align_up((size_t)2 * kCH * (R | 1u) * 8) * 2 +
+               align_up((size_t)6 * R * 8) + align_up((size_t)2 * 2 * kCH * ((R + 63) / 64) * 64 * 16) +
                align_up(N * 4) * 2 + align_up(16);
     };
-    size_t total = align_up(rows_total * 4) + align_up(rows_total * 8) + align_up((size_t)nv * 4) +
+    size_t total = align_up(rows_total * 8) + align_up(rows_total * 4) + align_up(rows_total * 8) + align_up((size_t)nv * 4) +
                    align_up((size_t)(ninit + 1) * 4) + align_up((size_t)njobs * sizeof(JobDev));
     for (uint32_t j = 0; j < njobs; j++) { job_off[j] = total; total += job_bytes(jobs[j].nrows); }
     char* arena = nullptr;
     hipError_t e = hipMalloc(&arena, total);
     if (e != hipSuccess) { *err = std::string("alvrl_refine: hipMalloc: ") + hipGetErrorString(e); return 4; }
     size_t o = 0;
-    uint32_t* d_rows = (uint32_t*)(arena + o); o += align_up(rows_total * 4);
+    unsigned long long* d_roff = (unsigned long long*)(arena + o); o += align_up(rows_total * 8);
+    uint32_t* d_rstride = (uint32_t*)(arena + o); o += align_up(rows_total * 4);
     double* d_locw = (double*)(arena + o); o += align_up(rows_total * 8);
     uint32_t* d_init = (uint32_t*)(arena + o); o += align_up((size_t)nv * 4);
     uint32_t* d_init_off = (uint32_t*)(arena + o); o += align_up((size_t)(ninit + 1) * 4);
     JobDev* d_jobs = (JobDev*)(arena + o);
-    std::vector<uint32_t> h_rows(rows_total);
+    std::vector<unsigned long long> h_roff(rows_total);
+    std::vector<uint32_t> h_rstride(rows_total);
     std::vector<double> h_locw(rows_total);
     std::vector<JobDev> h_jobs(njobs);
     for (uint32_t j = 0; j < njobs; j++) {
         const HostJob& H = jobs[j];
         for (uint32_t r = 0; r < H.nrows; r++) {
-            if (H.rows[r] >= ld) { hipFree(arena); *err = "alvrl_refine: row id out of range"; return 1; }
-            h_rows[row_off[j] + r] = H.rows[r];
+            if (H.row_off) {
+                if (H.row_stride[r] == 0) { hipFree(arena); *err = "alvrl_refine: zero row stride"; return 1; }
+                h_roff[row_off[j] + r] = H.row_off[r];
+                h_rstride[row_off[j] + r] = H.row_stride[r];
+            } else {
+                if (H.rows[r] >= ld) { hipFree(arena); *err = "alvrl_refine: row id out of range"; return 1; }
+                if (ld > 0xFFFFFFFFull) { hipFree(arena); *err = "alvrl_refine: ld too large"; return 1; }
+                h_roff[row_off[j] + r] = H.rows[r];
+                h_rstride[row_off[j] + r] = (uint32_t)ld;
+            }
             h_locw[row_off[j] + r] = H.locw[r];
         }
         JobDev& J = h_jobs[j];
         char* p = arena + job_off[j];
         const uint32_t R = H.nrows;
-        J.rows = d_rows + row_off[j]; J.locw = d_locw + row_off[j]; J.nrows = R;
-        J.row0 = H.rows[0];
+        J.roff = d_roff + row_off[j]; J.rstride = d_rstride + row_off[j];
+        J.locw = d_locw + row_off[j]; J.nrows = R;
+        const unsigned long long* ho = &h_roff[row_off[j]];
+        const uint32_t* hs = &h_rstride[row_off[j]];
+        J.off0 = ho[0]; J.stride0 = hs[0];
         J.contig = 1;
         for (uint32_t r = 0; r < R; r++)
-            if (H.rows[r] != H.rows[0] + r) { J.contig = 0; break; }
+            if (ho[r] != ho[0] + r || hs[r] != hs[0]) { J.contig = 0; break; }
         J.pixel_under = H.pixel_under; J.undersampling = H.undersampling;
         J.depth_correction = H.depth_correction; J.do_refine = H.do_refine;
         J.stage_refine = H.stage_refine; J.stage_sample = H.stage_sample;
@@ -1133,8 +1434,8 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
         J.feu = (float*)p; p += align_up(N * 4);
         J.fei = (float*)p; p += align_up(N * 4);
         J.st = (double*)p; p += align_up((size_t)6 * R * 8);
-        J.bufM = (double*)p; p += align_up((size_t)2 * kCH * (R | 1u) * 8);
-        J.bufV = (double*)p; p += align_up((size_t)2 * kCH * (R | 1u) * 8);
+        J.bufM = (double*)p; p += align_up((size_t)2 * 2 * kCH * ((R + 63) / 64) * 64 * 16);   // T, 2 passes x 2 chunks
+        J.bufV = nullptr;
         J.out_reps = (uint32_t*)p; p += align_up(N * 4);
         J.out_w = (float*)p; p += align_up(N * 4);
         J.out_n = (uint32_t*)p;
@@ -1152,15 +1453,22 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
     hipEvent_t e0 = nullptr, e1 = nullptr;
     e = hipEventCreate(&e0);
     if (e == hipSuccess) e = hipEventCreate(&e1);
-    if (e == hipSuccess) e = hipMemcpyAsync(d_rows, h_rows.data(), rows_total * 4, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(d_roff, h_roff.data(), rows_total * 8, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(d_rstride, h_rstride.data(), rows_total * 4, hipMemcpyHostToDevice, s);
     if (e == hipSuccess) e = hipMemcpyAsync(d_locw, h_locw.data(), rows_total * 8, hipMemcpyHostToDevice, s);
     if (e == hipSuccess) e = hipMemcpyAsync(d_init, init_vrls, (size_t)nv * 4, hipMemcpyHostToDevice, s);
     if (e == hipSuccess) e = hipMemcpyAsync(d_init_off, init_off, (size_t)(ninit + 1) * 4, hipMemcpyHostToDevice, s);
     if (e == hipSuccess) e = hipMemcpyAsync(d_jobs, h_jobs.data(), njobs * sizeof(JobDev), hipMemcpyHostToDevice, s);
     if (e == hipSuccess) e = hipEventRecord(e0, s);
     if (e == hipSuccess) {
-        hipLaunchKernelGGL(k_refine, dim3(njobs), dim3(kThreads), 0, s, d_jobs, cm);
-        e = hipGetLastError();
+        // ALVRL_REFINE_BATCH=n (developer knob): launch the jobs n at a time,
+        // to separate per-CU cost from contention between concurrent jobs
+        const char* bs = std::getenv("ALVRL_REFINE_BATCH");
+        const uint32_t batch = bs ? (uint32_t)std::max(1, std::atoi(bs)) : njobs;
+        for (uint32_t j0 = 0; j0 < njobs && e == hipSuccess; j0 += batch) {
+            hipLaunchKernelGGL(k_refine, dim3(std::min(batch, njobs - j0)), dim3(kThreads), 0, s, d_jobs + j0, cm);
+            e = hipGetLastError();
+        }
     }
     if (e == hipSuccess) e = hipEventRecord(e1, s);
     // gather results

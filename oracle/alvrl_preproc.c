@@ -72,23 +72,33 @@ static inline float m_var(const mat_t *M, uint32_t r, uint32_t v)
 }
 
 /* ------------------------------------------- deterministic reductions -- */
-/* Every reduction over the ROWS of a local matrix (uBLAS inner_prod /
- * norm_2) is the plain in-order sum of the reference source, row 0 first.
- * (The reference's -funsafe-math-optimizations build may re-associate it, so
- * it has no canonical rounding; this is the source-level order.)  The device
- * refinement kernel (refine.hip) evaluates the identical sums, one lane per
- * column, which makes cluster indices bit-exact between the two. */
+/* Every reduction over the ROWS of a local matrix (uBLAS inner_prod / norm_2,
+ * an in-order loop in the reference source that its -funsafe-math-optimizations
+ * build is free to re-associate, so the reference has no canonical rounding
+ * here) uses one fixed order that a 64-lane wavefront evaluates directly:
+ * lane l sums rows l, l+64, l+128, ... in ascending order starting from 0,
+ * then lanes are combined by the halving tree p[l] += p[l+32] (l<32),
+ * p[l] += p[l+16] (l<16), ..., p[0] += p[1].  The device refinement kernel
+ * (refine.hip) uses the identical order, which makes cluster indices
+ * bit-exact between the two. */
+#define WS_LANES 64
 static double wsum_d(const double *t, uint32_t R)
 {
-    double p = 0.0;
-    for (uint32_t r = 0; r < R; r++) p = p + t[r];
-    return p;
+    double p[WS_LANES];
+    for (int l = 0; l < WS_LANES; l++) p[l] = 0.0;
+    for (uint32_t r = 0; r < R; r++) p[r % WS_LANES] = p[r % WS_LANES] + t[r];
+    for (int off = WS_LANES / 2; off >= 1; off >>= 1)
+        for (int l = 0; l < off; l++) p[l] = p[l] + p[l + off];
+    return p[0];
 }
 static float wsum_f(const float *t, uint32_t R)
 {
-    float p = 0.0f;
-    for (uint32_t r = 0; r < R; r++) p = p + t[r];
-    return p;
+    float p[WS_LANES];
+    for (int l = 0; l < WS_LANES; l++) p[l] = 0.0f;
+    for (uint32_t r = 0; r < R; r++) p[r % WS_LANES] = p[r % WS_LANES] + t[r];
+    for (int off = WS_LANES / 2; off >= 1; off >>= 1)
+        for (int l = 0; l < off; l++) p[l] = p[l] + p[l + off];
+    return p[0];
 }
 
 /* Deterministic standard normal from two uniforms (Box-Muller, the maths of
