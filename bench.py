@@ -9,9 +9,21 @@ A step is one progressive pass of the vrl integrator over the whole frame
 (vrlIntegrator::prepass + render, vrlIntegrator.cpp:270-599): with resident
 VRLs (the vrlFile mode) the prepass is the LightSlice work (representative
 sampling, R build, per-slice refinement) for the clustered configs and nothing
-for the brute-force one; the render is the per-pixel gather.  Image tiles
-(64x64, round robin) are sharded over ranks and the framebuffer is reduced to
-rank 0 with one RCCL collective over xGMI per step.  Rank 0 prints one JSON line.
+for the brute-force one; the render is the per-pixel gather.  Rank 0 prints one JSON line.
+
+Multi-GPU (--shard):
+  passes (default)  progressive passes are independent units: at step i rank r
+                    runs pass i*N + r over the whole frame (its own
+                    representatives, R and clusters) and one RCCL reduce over
+                    xGMI sums the N passes' framebuffers into rank 0 -- the
+                    progressive accumulation (integrator.cpp:396-433) spread
+                    over GPUs.  Per-GPU work is fixed: "scaling": "weak".
+  slices            one pass per step, sharded inside the pass:
+                    rank r builds R for and refines slices s % N == r, the
+                    non-zero mask is OR-reduced and the cluster lists are
+                    all-gathered over RCCL (alvrl_integrator_prepass_dist),
+                    64x64 image tiles are dealt round robin, and the
+                    framebuffer is reduced to rank 0: "scaling": "strong".
 """
 from __future__ import annotations
 
@@ -53,6 +65,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="C4", choices=sorted(CONFIGS))
+    ap.add_argument("--shard", default="passes", choices=["passes", "slices"],
+                    help="multi-GPU decomposition (see the module docstring)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-row-stride", type=int, default=64,
                     help="CPU baseline sample: every n-th image row")
@@ -107,12 +121,19 @@ def main():
     fb = torch.zeros(W * H * 3, dtype=torch.float32, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
 
+    by_slices = args.shard == "slices"
+    exchange = alvrl.Exchange(device=dev) if (world > 1 and by_slices) else None
+
     def step(i):
-        it.prepass(i)
         fb.zero_()
-        it.render(fb, rank, world, stream=stream)
+        if by_slices:   # one pass, LightSlice work and tiles sharded over ranks
+            it.prepass(i, rank, world, exchange)
+            it.render(fb, rank, world, stream=stream)
+        else:           # pass i*N + rank, whole frame
+            it.prepass(i * world + rank)
+            it.render(fb, 0, 1, stream=stream)
         if world > 1:
-            dist.reduce(fb, dst=0)   # the single RCCL framebuffer gather per pass
+            dist.reduce(fb, dst=0)   # the single RCCL framebuffer reduce per step
 
     def barrier():
         torch.cuda.synchronize(dev)
@@ -171,21 +192,25 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": "strong" if by_slices else "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic: restated vrlTracer VRLs (seed 0x5EED0001) in the BASELINE.md smoke box",
             "config": {"workload": f"{args.config}: {cfg['desc']}", "resolution": [W, H],
                        "vrls": int(vrls.shape[1]), "particles": int(pc),
-                       "parallelism": f"image tiles 64x64 round-robin over {world} GPU(s), "
-                                      f"RCCL reduce of the framebuffer"},
+                       "parallelism": (f"one pass per step: slices and 64x64 image tiles round-robin over "
+                                       f"{world} GPU(s), RCCL mask OR + cluster all-gather + framebuffer reduce"
+                                       if by_slices else
+                                       f"{world} progressive pass(es) per step, one per GPU, "
+                                       f"RCCL reduce of the framebuffer")},
             "breakdown": {"render_pairs": render_pairs, "prepass_pairs": pre_pairs,
                           "render_kernel_ms": float(np.mean(kernel_ms)) if kernel_ms else None,
                           "rbuild_ms": float(np.mean(rbuild_ms)), "refine_ms": float(np.mean(refine_ms)),
                           "prepass_wall_ms": float(np.mean(prepass_ms)),
                           "slices": int(s1["slices"]), "rep_rows": int(s1["rep_rows"]),
                           "clusters_total": int(s1["clusters_total"]),
-                          "slices_failed": int(s1["slices_failed"])},
+                          "slices_failed": int(s1["slices_failed"]),
+                          "exchange_ms": float(s1["ms_exchange"])},
             "roofline": {"bound": "hbm", "kernel": f"k_gather_{kind}", "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic,

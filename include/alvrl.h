@@ -37,7 +37,8 @@ enum {
     ALVRL_ERR_STATE = 2,     /* call order violated (e.g. gather before upload_vrls) */
     ALVRL_ERR_HIP = 3,       /* HIP runtime failure */
     ALVRL_ERR_NOMEM = 4,
-    ALVRL_ERR_NUMERIC = 5    /* an invariant of the clustering maths failed (reference: SLog(EError)) */
+    ALVRL_ERR_NUMERIC = 5,   /* an invariant of the clustering maths failed (reference: SLog(EError)) */
+    ALVRL_ERR_COMM = 6       /* the caller's collective (alvrl_exchange) failed */
 };
 
 /* Record-flag bits of alvrl_gather_rec.flags */
@@ -157,6 +158,16 @@ ALVRL_API int alvrl_build_R(alvrl_ctx *ctx, const alvrl_gather_rec *d_recs,
  * Rows [0, nrows) of d_Rt; out_mask is host memory (nvrl bytes). */
 ALVRL_API int alvrl_nonzero_columns(alvrl_ctx *ctx, const float *d_Rt, uint64_t ld, uint32_t nrows,
                                     uint8_t *out_mask, void *stream);
+
+/* alvrl_build_R for rows scattered over per-slice blocks, in one launch:
+ * row r's pair for VRL v goes to float2 index d_row_off[r] + v * d_row_stride[r]
+ * (device arrays).  If d_nonzero (device, nvrl bytes) is given, every VRL
+ * with a non-zero mean in these rows sets d_nonzero[v] = 1 (never clears it),
+ * which is alvrl_nonzero_columns fused into the build. */
+ALVRL_API int alvrl_build_R_blocks(alvrl_ctx *ctx, const alvrl_gather_rec *d_recs,
+                                   const uint32_t *d_rec_ids, uint32_t nrows, float *d_Rt,
+                                   const uint64_t *d_row_off, const uint32_t *d_row_stride,
+                                   uint8_t *d_nonzero, void *stream);
 
 /* ---- hot path (b) part 2: cluster refinement ------------------------- */
 /* One Clustering (Preprocessor.cpp:287-720): ctor (column weights, initial

@@ -77,7 +77,8 @@ ALVRL_API void alvrl_integrator_destroy(alvrl_integrator *it);
 ALVRL_API int alvrl_integrator_preprocess(alvrl_integrator *it, const alvrl_scene_desc *s);
 /* vrlIntegrator::prepass (:270-356) for pass 'pass' (0-based): trace or reuse
  * VRLs, sample representatives, build R, cluster, upload cluster info.
- * rank/world shard nothing in the prepass (every rank holds every slice). */
+ * Every slice on this GPU (see alvrl_integrator_prepass_dist for the
+ * slice-sharded form). */
 ALVRL_API int alvrl_integrator_prepass(alvrl_integrator *it, uint32_t pass);
 /* SamplingIntegrator::render for the pixels this rank owns: 64x64 tiles dealt
  * round-robin (tile t -> rank t % world).  Adds Li of every owned pixel into
@@ -88,6 +89,49 @@ ALVRL_API int alvrl_integrator_render(alvrl_integrator *it, uint32_t rank, uint3
  * this set instead of tracing; soa = 9 planes of stride n. */
 ALVRL_API int alvrl_integrator_set_vrls(alvrl_integrator *it, const float *soa, uint32_t n,
                                         uint64_t particle_count);
+/* ---- multi-GPU prepass ------------------------------------
+ * The one collective the slice-sharded prepass needs, supplied by the
+ * caller's communicator (RCCL through torch.distributed, MPI, ...): every
+ * rank passes the same 'bytes' and receives world * bytes in rank order.
+ * Returns 0 on success; anything else aborts the prepass with ALVRL_ERR_COMM. */
+typedef struct {
+    void *user;
+    int (*allgather)(void *user, const void *send, uint64_t bytes, void *recv);
+} alvrl_exchange;
+
+/* vrlIntegrator::prepass with the LightSlice work sharded by slice: rank r
+ * builds R for, and refines, the slices s with s % world == r (plus the rows
+ * of their neighbour slices when neighbourCount > 0), the non-zero VRL mask
+ * of Preprocessor::cluster (:843-855) is OR-reduced over ranks, and the
+ * per-slice cluster lists are all-gathered so every rank can render any
+ * tile.  Results are identical to alvrl_integrator_prepass on one GPU.  The
+ * fall-back clustering (needed only if a slice fails to refine or a pixel
+ * has no slice) is computed by every rank over all rows.  world == 1 (ex
+ * may be NULL) is alvrl_integrator_prepass. */
+ALVRL_API int alvrl_integrator_prepass_dist(alvrl_integrator *it, uint32_t pass, uint32_t rank,
+                                            uint32_t world, const alvrl_exchange *ex);
+
+/* Building blocks of the exchange, exported for hosts that orchestrate the
+ * prepass themselves and for the CPU tests.
+ * Variable-size all-gather: counts[r] = bytes of rank r; with recv != NULL
+ * (cap bytes) rank r's data lands at recv + sum(counts[<r]).  Call with
+ * recv == NULL first to learn the counts. */
+ALVRL_API int alvrl_exchange_allgatherv(const alvrl_exchange *ex, uint32_t world, const void *send,
+                                        uint64_t bytes, void *recv, uint64_t cap, uint64_t *counts);
+/* Element-wise OR of n bytes over ranks, in place. */
+ALVRL_API int alvrl_exchange_or(const alvrl_exchange *ex, uint32_t world, uint8_t *buf, uint64_t n);
+/* Merge per-slice cluster lists: this rank holds n_local slices (ids
+ * local_slice[], refined flags, CSR local_off/local_reps/local_w); the
+ * output is the CSR over all nslices slices (a slice no rank reports gets
+ * refined = 0 and no clusters).  *total = clusters of all slices; returns
+ * ALVRL_ERR_INVALID if cap is smaller (call again with a larger buffer). */
+ALVRL_API int alvrl_exchange_clusters(const alvrl_exchange *ex, uint32_t world, uint32_t nslices,
+                                      uint32_t n_local, const uint32_t *local_slice,
+                                      const int *local_refined, const uint32_t *local_off,
+                                      const uint32_t *local_reps, const float *local_w,
+                                      int *refined, uint32_t *slice_off, uint32_t *reps,
+                                      float *weights, uint64_t cap, uint64_t *total);
+
 /* Timing / statistics of the last prepass and render. */
 typedef struct {
     uint64_t vrls, particles, slices, rep_rows, clusters_total;
@@ -95,6 +139,10 @@ typedef struct {
     double ms_trace, ms_slices, ms_rbuild, ms_refine, ms_render_kernel, ms_prepass_wall;
     uint32_t slices_failed;
     int fallback_built;
+    /* slices this rank refined and R rows it built (all of them at world 1),
+     * and the host time spent in the exchange of the last prepass */
+    uint64_t slices_local, rows_built;
+    double ms_exchange;
 } alvrl_integrator_stats;
 ALVRL_API int alvrl_integrator_get_stats(alvrl_integrator *it, alvrl_integrator_stats *st);
 /* The device context the integrator drives (for low-level access). */

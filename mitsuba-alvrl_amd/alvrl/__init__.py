@@ -298,10 +298,107 @@ class IntegratorStats(C.Structure):
                 ("ms_trace", C.c_double), ("ms_slices", C.c_double), ("ms_rbuild", C.c_double),
                 ("ms_refine", C.c_double), ("ms_render_kernel", C.c_double),
                 ("ms_prepass_wall", C.c_double), ("slices_failed", C.c_uint32),
-                ("fallback_built", C.c_int)]
+                ("fallback_built", C.c_int), ("slices_local", C.c_uint64), ("rows_built", C.c_uint64),
+                ("ms_exchange", C.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p)
+
+
+class ExchangeDesc(C.Structure):
+    _fields_ = [("user", C.c_void_p), ("allgather", ALLGATHER_FN)]
+
+
+class Exchange:
+    """alvrl_exchange over a torch.distributed process group.
+
+    The library asks for one collective: a fixed-size all-gather of bytes.  With
+    the "nccl" backend (RCCL on ROCm) the bytes travel as a device tensor over
+    xGMI; with gloo (CPU tests) as a host tensor.  A failing collective is kept
+    in `error` and reported to the library as a non-zero status, which aborts the
+    prepass with ALVRL_ERR_COMM."""
+
+    def __init__(self, group=None, device=None):
+        import torch
+        import torch.distributed as dist
+        self.group = group
+        self.world = dist.get_world_size(group)
+        if device is None:
+            device = (torch.device("cuda", torch.cuda.current_device())
+                      if dist.get_backend(group) == "nccl" else torch.device("cpu"))
+        self.device = device
+        self.error = None
+        self.calls = 0
+
+        def allgather(user, send, nbytes, recv):
+            try:
+                n = int(nbytes)
+                src = np.frombuffer((C.c_uint8 * n).from_address(send), np.uint8).copy()
+                t = torch.from_numpy(src).to(self.device)
+                out = torch.empty(n * self.world, dtype=torch.uint8, device=self.device)
+                dist.all_gather_into_tensor(out, t, group=self.group)
+                host = out.cpu().numpy()
+                C.memmove(recv, host.ctypes.data, host.nbytes)
+                self.calls += 1
+                return 0
+            except Exception as e:   # reported to the library as ALVRL_ERR_COMM
+                self.error = e
+                return 1
+
+        self._fn = ALLGATHER_FN(allgather)   # keep the thunk alive
+        self.desc = ExchangeDesc(None, self._fn)
+
+    def _check(self, rc: int):
+        if rc != ALVRL_OK:
+            raise AlvrlError(rc, _host().alvrl_host_last_error().decode()
+                             + (f" ({self.error!r})" if self.error else ""))
+
+    def allgatherv(self, data: np.ndarray) -> list:
+        """Variable-size all-gather of a uint8 array: one array per rank."""
+        L = _host()
+        data = _np(data, np.uint8)
+        counts = np.zeros(self.world, np.uint64)
+        self._check(L.alvrl_exchange_allgatherv(C.byref(self.desc), self.world, _ptr(data), data.size,
+                                                None, 0, _arr(counts, C.c_uint64)))
+        out = np.zeros(max(1, int(counts.sum())), np.uint8)
+        self._check(L.alvrl_exchange_allgatherv(C.byref(self.desc), self.world, _ptr(data), data.size,
+                                                _ptr(out), out.size, _arr(counts, C.c_uint64)))
+        ends = np.cumsum(counts.astype(np.int64))
+        return [out[e - int(c):e].copy() for e, c in zip(ends, counts)]
+
+    def or_(self, mask: np.ndarray) -> np.ndarray:
+        m = _np(mask, np.uint8).copy()
+        self._check(_host().alvrl_exchange_or(C.byref(self.desc), self.world, _ptr(m), m.size))
+        return m
+
+    def clusters(self, nslices: int, local: dict):
+        """Merge {slice: (refined, reps, weights)} of every rank into the CSR
+        over all slices: (refined[nslices], slice_off, reps, weights)."""
+        L = _host()
+        ids = np.array(sorted(local), np.uint32)
+        ref = np.array([int(bool(local[s][0])) for s in ids], np.int32)
+        off = np.zeros(len(ids) + 1, np.uint32)
+        for k, s in enumerate(ids):
+            off[k + 1] = off[k] + len(local[s][1])
+        reps = np.concatenate([np.asarray(local[s][1], np.uint32) for s in ids] or [np.zeros(0, np.uint32)])
+        w = np.concatenate([np.asarray(local[s][2], np.float32) for s in ids] or [np.zeros(0, np.float32)])
+        refined = np.zeros(max(1, nslices), np.int32)
+        soff = np.zeros(nslices + 1, np.uint32)
+        total = C.c_uint64()
+        cap = 0
+        while True:
+            out_r = np.zeros(max(1, cap), np.uint32); out_w = np.zeros(max(1, cap), np.float32)
+            rc = L.alvrl_exchange_clusters(C.byref(self.desc), self.world, nslices, len(ids), _ptr(ids),
+                                           _ptr(ref), _ptr(off), _ptr(reps), _ptr(w), _ptr(refined),
+                                           _ptr(soff), _ptr(out_r), _ptr(out_w), cap, C.byref(total))
+            if rc == ALVRL_OK:
+                return refined[:nslices], soff, out_r[:total.value], out_w[:total.value]
+            if total.value <= cap:
+                self._check(rc)
+            cap = int(total.value)
 
 
 _host_bound = False
@@ -335,6 +432,11 @@ def _host():
     L.alvrl_integrator_clusters.argtypes = [vp, P(u32), P(u32), P(f32), u32, P(u32), P(f32), u32, P(u32)]
     L.alvrl_integrator_vrls.argtypes = [vp, vp, u32, P(u32), P(u64)]
     L.alvrl_integrator_R.argtypes = [vp, vp, u64]
+    L.alvrl_integrator_prepass_dist.argtypes = [vp, u32, u32, u32, P(ExchangeDesc)]
+    L.alvrl_exchange_allgatherv.argtypes = [P(ExchangeDesc), u32, vp, u64, vp, u64, P(u64)]
+    L.alvrl_exchange_or.argtypes = [P(ExchangeDesc), u32, vp, u64]
+    L.alvrl_exchange_clusters.argtypes = [P(ExchangeDesc), u32, u32, u32, vp, vp, vp, vp, vp, vp, vp, vp, vp,
+                                          u64, P(u64)]
     _host_bound = True
     return L
 
@@ -429,8 +531,17 @@ class Integrator:
         soa = _np(soa, np.float32)
         _hcheck(self.L.alvrl_integrator_set_vrls(self.h, _ptr(soa), soa.shape[1], particle_count))
 
-    def prepass(self, pass_: int = 0):
-        _hcheck(self.L.alvrl_integrator_prepass(self.h, pass_))
+    def prepass(self, pass_: int = 0, rank: int = 0, world: int = 1, exchange: "Exchange" = None):
+        """vrlIntegrator::prepass; with world > 1 the LightSlice work is sharded
+        by slice over the ranks of `exchange` (alvrl_integrator_prepass_dist)."""
+        if world == 1:
+            _hcheck(self.L.alvrl_integrator_prepass(self.h, pass_))
+            return
+        if exchange is None:
+            raise ValueError("a sharded prepass needs an Exchange")
+        rc = self.L.alvrl_integrator_prepass_dist(self.h, pass_, rank, world, C.byref(exchange.desc))
+        if rc != ALVRL_OK:
+            exchange._check(rc)
 
     def render(self, d_fb, rank: int = 0, world: int = 1, stream=None):
         _hcheck(self.L.alvrl_integrator_render(self.h, rank, world, _ptr(d_fb),

@@ -31,6 +31,10 @@ hipError_t launch_gather_clustered(const Rec* recs, const uint32_t* ids, const W
 hipError_t launch_build_R(const Rec* recs, const uint32_t* ids, uint32_t nrows, const VrlPrep* vp,
                           uint32_t nvrl, const DevParams& P, float normalization, float2* Rt,
                           uint64_t ld, uint64_t row0, unsigned long long* counter, hipStream_t s);
+hipError_t launch_build_R_blocks(const Rec* recs, const uint32_t* ids, uint32_t nrows, const VrlPrep* vp,
+                                 uint32_t nvrl, const DevParams& P, float normalization, float2* Rt,
+                                 const uint64_t* roff, const uint32_t* rstride, uint8_t* nonzero,
+                                 unsigned long long* counter, hipStream_t s);
 hipError_t launch_nonzero_columns(const float2* Rt, uint64_t ld, uint32_t nrows, uint32_t nvrl,
                                   uint8_t* mask, hipStream_t s);
 hipError_t launch_accumulate_rgb(const float* rgb, const uint32_t* pix, uint32_t n, float* fb,
@@ -328,6 +332,26 @@ ALVRL_API int alvrl_build_R(alvrl_ctx* c, const alvrl_gather_rec* d_recs, const 
     HIPCHK(hipEventRecord(c->ev0, s));
     HIPCHK(launch_build_R(reinterpret_cast<const Rec*>(d_recs), d_ids, nrows, c->d_vrl, c->nvrl, c->P,
                           norm, reinterpret_cast<float2*>(d_Rt), ld, row0, c->d_counter + 0, s));
+    HIPCHK(hipEventRecord(c->ev1, s));
+    c->timed = true;
+    return ALVRL_OK;
+}
+
+ALVRL_API int alvrl_build_R_blocks(alvrl_ctx* c, const alvrl_gather_rec* d_recs, const uint32_t* d_ids,
+                                   uint32_t nrows, float* d_Rt, const uint64_t* d_row_off,
+                                   const uint32_t* d_row_stride, uint8_t* d_nonzero, void* stream)
+{
+    int rc = check_ready(c, "alvrl_build_R_blocks");
+    if (rc) return rc;
+    if (nrows && (!d_recs || !d_Rt || !d_row_off || !d_row_stride))
+        return fail(ALVRL_ERR_INVALID, "alvrl_build_R_blocks: null buffer");
+    HIPCHK(hipSetDevice(c->cfg.device));
+    hipStream_t s = pick(c, stream);
+    const float norm = (float)(1.0 / (double)c->particle_count);
+    HIPCHK(hipEventRecord(c->ev0, s));
+    HIPCHK(launch_build_R_blocks(reinterpret_cast<const Rec*>(d_recs), d_ids, nrows, c->d_vrl, c->nvrl, c->P,
+                                 norm, reinterpret_cast<float2*>(d_Rt), d_row_off, d_row_stride, d_nonzero,
+                                 c->d_counter + 0, s));
     HIPCHK(hipEventRecord(c->ev1, s));
     c->timed = true;
     return ALVRL_OK;

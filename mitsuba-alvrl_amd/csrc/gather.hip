@@ -167,6 +167,49 @@ __global__ void __launch_bounds__(256) k_build_R(const Rec* __restrict__ recs,
     count_pairs(counter, active && q.medium, done);
 }
 
+// The same over per-slice blocks: row r of the launch lives at float2 index
+// roff[r] + v * rstride[r].  Lanes of a wave are consecutive rows of one
+// block except across slice boundaries, so the stores stay coalesced.  The
+// non-zero column test of Preprocessor::cluster rides along: one ballot per
+// (wave, VRL), one byte store when a mean is non-zero.
+template <int NVV, int NVS>
+__global__ void __launch_bounds__(256) k_build_R_blocks(const Rec* __restrict__ recs,
+                                                        const uint32_t* __restrict__ ids, uint32_t nrows,
+                                                        const VrlPrep* __restrict__ vp, uint32_t nvrl,
+                                                        uint32_t chunk, DevParams P, float normalization,
+                                                        float2* __restrict__ Rt,
+                                                        const uint64_t* __restrict__ roff,
+                                                        const uint32_t* __restrict__ rstride,
+                                                        uint8_t* __restrict__ nonzero,
+                                                        unsigned long long* counter)
+{
+    const uint32_t r = blockIdx.x * 64 + (threadIdx.x & 63);
+    const uint32_t wave = threadIdx.x >> 6;
+    const bool active = r < nrows;
+    const Rec rec = load_rec(recs, r, active);
+    const RecPre q = prepare_record(rec, P);
+    const uint32_t rid = active ? (ids ? ids[r] : r) : 0u;
+    const uint64_t base = active ? roff[r] : 0;
+    const uint64_t stride = active ? rstride[r] : 0;
+    const uint32_t v0 = blockIdx.y * chunk;
+    const uint32_t v1 = min(nvrl, v0 + chunk);
+    uint32_t done = 0;
+    for (uint32_t v = v0 + wave; v < v1; v += 4) {
+        float mean = 0.0f, var = 0.0f;
+        if (q.medium) {
+            const VrlPrep V = vp[v];
+            float c[3];
+            integrate_vrl<NVV, NVS, true>(P, q, V, rid, v, kDomRbuild, P.nvv, P.nvs, c, &mean, &var);
+            mean = mean * normalization;
+            var = var * normalization * normalization;
+        }
+        if (active) Rt[base + (uint64_t)v * stride] = make_float2(mean, var);
+        if (nonzero && __ballot(active && mean != 0.0f) && (threadIdx.x & 63) == 0) nonzero[v] = 1;
+        ++done;
+    }
+    count_pairs(counter, active && q.medium, done);
+}
+
 // Preprocessor::cluster's totalVrlContribution != 0 (means are >= 0): one
 // wave per VRL column, rows contiguous.
 __global__ void __launch_bounds__(256) k_nonzero_columns(const float2* __restrict__ Rt, uint64_t ld,
@@ -268,6 +311,23 @@ hipError_t launch_build_R(const Rec* recs, const uint32_t* ids, uint32_t nrows, 
     else
         hipLaunchKernelGGL((k_build_R<-1, -1>), grid, block, 0, s, recs, ids, nrows, vp, nvrl,
                            chunk, P, normalization, Rt, ld, row0, counter);
+    return hipGetLastError();
+}
+
+hipError_t launch_build_R_blocks(const Rec* recs, const uint32_t* ids, uint32_t nrows, const VrlPrep* vp,
+                                 uint32_t nvrl, const DevParams& P, float normalization, float2* Rt,
+                                 const uint64_t* roff, const uint32_t* rstride, uint8_t* nonzero,
+                                 unsigned long long* counter, hipStream_t s)
+{
+    if (nrows == 0 || nvrl == 0) return hipSuccess;
+    const uint32_t chunk = 256;
+    const dim3 grid((nrows + 63) / 64, (nvrl + chunk - 1) / chunk), block(256);
+    if (P.nvv == 2 && P.nvs == 2)
+        hipLaunchKernelGGL((k_build_R_blocks<2, 2>), grid, block, 0, s, recs, ids, nrows, vp, nvrl, chunk,
+                           P, normalization, Rt, roff, rstride, nonzero, counter);
+    else
+        hipLaunchKernelGGL((k_build_R_blocks<-1, -1>), grid, block, 0, s, recs, ids, nrows, vp, nvrl,
+                           chunk, P, normalization, Rt, roff, rstride, nonzero, counter);
     return hipGetLastError();
 }
 

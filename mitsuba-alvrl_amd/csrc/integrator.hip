@@ -22,6 +22,7 @@
 #include <string>
 #include <vector>
 
+#include "host/exchange.hpp"
 #include "host/preprocessor.hpp"
 #include "host/scene.hpp"
 
@@ -120,10 +121,14 @@ struct alvrl_integrator {
     bool clustered = false;
     // R
     DevBuf<float> Rt;                       // R in per-slice [vrl][row] blocks
-    std::vector<uint64_t> row_base;         // float2 index of (vrl 0, global row g)
+    std::vector<uint64_t> row_base;         // float2 index of (vrl 0, global row g); UINT64_MAX if not built
     std::vector<uint32_t> row_stride;       // rows of g's slice
     DevBuf<alvrl_gather_rec> rep_recs;
     DevBuf<uint32_t> rep_ids;
+    DevBuf<uint64_t> rb_off;                // per built row: float2 index of (vrl 0, row)
+    DevBuf<uint32_t> rb_stride;
+    DevBuf<uint8_t> nz_dev;
+    uint32_t rows_built = 0;                // rows of R held (all of them at world 1)
     // cluster info (vrlClusterInfo)
     std::vector<uint32_t> slice_off, reps, fb_reps;
     std::vector<float> weights, fb_w;
@@ -226,8 +231,10 @@ struct alvrl_integrator {
         cache_rank = 0xFFFFFFFFu;
     }
 
-    void prepass(uint32_t pass)
+    void prepass(uint32_t pass, uint32_t rank = 0, uint32_t world = 1, const alvrl_exchange* ex = nullptr)
     {
+        if (world == 0 || rank >= world) throw IntegError(ALVRL_ERR_INVALID, "bad rank/world");
+        if (world > 1 && (!ex || !ex->allgather)) throw IntegError(ALVRL_ERR_INVALID, "world > 1 needs an alvrl_exchange");
         if (!have_scene) throw IntegError(ALVRL_ERR_STATE, "prepass before preprocess");
         const double tw = now_ms();
         chk(alvrl_set_pass(ctx, pass), "alvrl_set_pass");
@@ -248,73 +255,117 @@ struct alvrl_integrator {
         st.particles = vrls.particle_count;
         st.slices_failed = 0;
         st.fallback_built = 0;
-        st.ms_rbuild = st.ms_refine = 0;
-        if (clustered) build_clusters(pass);
+        st.ms_rbuild = st.ms_refine = st.ms_exchange = 0;
+        st.slices_local = 0;
+        st.rows_built = 0;
+        if (clustered) build_clusters(pass, rank, world, ex);
         st.ms_prepass_wall = now_ms() - tw;
     }
 
-    void build_clusters(uint32_t pass_id)
+    // Building R (:302-333) for the rows of the slices flagged in 'need'.  R is
+    // stored as one [vrl][row] block per slice (the reference's
+    // R[slice][rep][vrl], transposed): a slice's local matrix is then one
+    // contiguous run -- consecutive VRL columns 8 * R_s bytes apart instead of
+    // 8 * rows -- which the refinement streams.  Blocks are packed in slice
+    // order, so with every slice built global row g of slice s lives at
+    // float2 index nv * rep_off[s] + (g - rep_off[s]) + v * R_s.  One launch
+    // builds every block and ORs the non-zero VRL mask of Preprocessor::cluster
+    // (:843-855) into 'nz'.
+    void build_R(const std::vector<char>& need, std::vector<uint8_t>* nz)
+    {
+        const uint32_t nv = vrls.n;
+        const auto& roff = prep->rep_off();
+        const auto& rpix = prep->rep_pix();
+        const uint32_t ns = prep->num_slices();
+        const uint32_t rows = roff[ns];
+        const int H = scene.height, W = scene.width;
+        const bool scat = !(scene.medium.sigma_s[0] == 0 && scene.medium.sigma_s[1] == 0 && scene.medium.sigma_s[2] == 0);
+        row_base.assign(rows, UINT64_MAX);
+        row_stride.assign(rows, 0);
+        // records of the representative pixel centres (sensor->sampleRay at
+        // the pixel centre, :327-328 / :1060-1061); RNG id = row-major pixel id
+        std::vector<alvrl_gather_rec> h;
+        std::vector<uint32_t> ids, bstr;
+        std::vector<uint64_t> boff;
+        uint64_t acc = 0;
+        for (uint32_t s2 = 0; s2 < ns; s2++) {
+            if (!need[s2]) continue;
+            const uint32_t n = roff[s2 + 1] - roff[s2];
+            for (uint32_t g = roff[s2]; g < roff[s2 + 1]; g++) {
+                row_base[g] = (uint64_t)nv * acc + (g - roff[s2]);
+                row_stride[g] = n;
+                const uint32_t x = rpix[g] / (uint32_t)H, y = rpix[g] % (uint32_t)H;
+                h.emplace_back();
+                scene.make_record((int)x, (int)y, scat, reinterpret_cast<float*>(&h.back()));
+                ids.push_back(y * (uint32_t)W + x);
+                boff.push_back(row_base[g]);
+                bstr.push_back(n);
+            }
+            acc += n;
+        }
+        const uint32_t nb = (uint32_t)h.size();
+        rows_built = nb;
+        rep_recs.ensure(nb);
+        rep_ids.ensure(nb);
+        rb_off.ensure(nb);
+        rb_stride.ensure(nb);
+        nz_dev.ensure(nv);
+        Rt.ensure((size_t)2 * nv * acc);
+        if (nb) {
+            hchk(hipMemcpyAsync(rep_recs.p, h.data(), sizeof(alvrl_gather_rec) * nb, hipMemcpyHostToDevice, stream), "copy rep records");
+            hchk(hipMemcpyAsync(rep_ids.p, ids.data(), sizeof(uint32_t) * nb, hipMemcpyHostToDevice, stream), "copy rep ids");
+            hchk(hipMemcpyAsync(rb_off.p, boff.data(), sizeof(uint64_t) * nb, hipMemcpyHostToDevice, stream), "copy row offsets");
+            hchk(hipMemcpyAsync(rb_stride.p, bstr.data(), sizeof(uint32_t) * nb, hipMemcpyHostToDevice, stream), "copy row strides");
+        }
+        hchk(hipMemsetAsync(nz_dev.p, 0, nv, stream), "clear mask");
+        hipEvent_t e0, e1;
+        hchk(hipEventCreate(&e0), "event"); hchk(hipEventCreate(&e1), "event");
+        hchk(hipEventRecord(e0, stream), "event");
+        chk(alvrl_build_R_blocks(ctx, rep_recs.p, rep_ids.p, nb, Rt.p, rb_off.p, rb_stride.p, nz_dev.p, stream),
+            "alvrl_build_R_blocks");
+        hchk(hipEventRecord(e1, stream), "event");
+        nz->assign(nv, 0);
+        if (nv) hchk(hipMemcpyAsync(nz->data(), nz_dev.p, nv, hipMemcpyDeviceToHost, stream), "copy mask");
+        hchk(hipStreamSynchronize(stream), "sync");
+        float ms = 0;
+        hchk(hipEventElapsedTime(&ms, e0, e1), "event");
+        st.ms_rbuild += ms;
+        hipEventDestroy(e0); hipEventDestroy(e1);
+    }
+
+    // buildClusters (:293-346).  With world > 1 the slices are dealt round
+    // robin (s % world == rank): this rank builds R for its slices and their
+    // neighbours' rows, refines its slices, and the exchange makes the mask
+    // and the cluster lists global.
+    void build_clusters(uint32_t pass_id, uint32_t rank, uint32_t world, const alvrl_exchange* ex)
     {
         const uint32_t nv = vrls.n;
         // sampleSliceMapping (:293-296)
         prep->set_pass(pass_id);
         prep->sample_slice_mapping(targetPixelUndersampling);
         const auto& roff = prep->rep_off();
-        const auto& rpix = prep->rep_pix();
         const uint32_t ns = prep->num_slices();
         const uint32_t rows = roff[ns];
         st.rep_rows = rows;
-        // records of the representative pixel centres (sensor->sampleRay at the
-        // pixel centre, :327-328 / :1060-1061); RNG id = row-major pixel id
-        std::vector<alvrl_gather_rec> h(rows);
-        std::vector<uint32_t> ids(rows);
-        const int H = scene.height, W = scene.width;
-        const bool scat = !(scene.medium.sigma_s[0] == 0 && scene.medium.sigma_s[1] == 0 && scene.medium.sigma_s[2] == 0);
-        for (uint32_t r = 0; r < rows; r++) {
-            const uint32_t x = rpix[r] / (uint32_t)H, y = rpix[r] % (uint32_t)H;
-            scene.make_record((int)x, (int)y, scat, reinterpret_cast<float*>(&h[r]));
-            ids[r] = y * (uint32_t)W + x;
+        // local matrices of this rank's slices (getLocalMatrix, :779-827)
+        std::vector<uint32_t> mine;
+        for (uint32_t s = rank; s < ns; s += world) mine.push_back(s);
+        const uint32_t nm = (uint32_t)mine.size();
+        std::vector<std::vector<uint32_t>> lrows(nm);
+        std::vector<std::vector<double>> lw(nm);
+        std::vector<char> need(ns, 0);
+        for (uint32_t k = 0; k < nm; k++) {
+            prep->local_matrix(mine[k], &lrows[k], &lw[k]);
+            need[mine[k]] = 1;
+            for (uint32_t g : lrows[k])
+                need[(uint32_t)(std::upper_bound(roff.begin(), roff.end(), g) - roff.begin()) - 1] = 1;
         }
-        rep_recs.ensure(rows);
-        rep_ids.ensure(rows);
-        Rt.ensure((size_t)2 * nv * rows);
-        hchk(hipMemcpyAsync(rep_recs.p, h.data(), sizeof(alvrl_gather_rec) * rows, hipMemcpyHostToDevice, stream), "copy rep records");
-        hchk(hipMemcpyAsync(rep_ids.p, ids.data(), sizeof(uint32_t) * rows, hipMemcpyHostToDevice, stream), "copy rep ids");
-        // Building R (:302-333).  R is stored as one [vrl][row] block per slice
-        // (the reference's R[slice][rep][vrl], transposed): a slice's local
-        // matrix is then one contiguous run -- consecutive VRL columns 8 * R_s
-        // bytes apart instead of 8 * rows -- which the refinement streams.
-        // Global row g of slice s lives at float2 index
-        //   nv * rep_off[s] + (g - rep_off[s]) + v * R_s.
-        row_base.resize(rows); row_stride.resize(rows);
-        for (uint32_t s2 = 0; s2 < ns; s2++)
-            for (uint32_t g = roff[s2]; g < roff[s2 + 1]; g++) {
-                row_base[g] = (uint64_t)nv * roff[s2] + (g - roff[s2]);
-                row_stride[g] = roff[s2 + 1] - roff[s2];
-            }
-        hipEvent_t e0, e1;
-        hchk(hipEventCreate(&e0), "event"); hchk(hipEventCreate(&e1), "event");
-        hchk(hipEventRecord(e0, stream), "event");
-        for (uint32_t s2 = 0; s2 < ns; s2++) {
-            const uint32_t n = roff[s2 + 1] - roff[s2];
-            if (!n) continue;
-            chk(alvrl_build_R(ctx, rep_recs.p + roff[s2], rep_ids.p + roff[s2], n,
-                              Rt.p + (size_t)2 * nv * roff[s2], n, 0, stream), "alvrl_build_R");
-        }
-        hchk(hipEventRecord(e1, stream), "event");
+        std::vector<uint8_t> nz;
+        build_R(need, &nz);
         // Preprocessor::cluster (:838-898): non-zero VRLs in one cluster, zero VRLs in another
-        std::vector<uint8_t> nz(nv, 0), nzs(nv);
-        for (uint32_t s2 = 0; s2 < ns; s2++) {
-            const uint32_t n = roff[s2 + 1] - roff[s2];
-            if (!n) continue;
-            chk(alvrl_nonzero_columns(ctx, Rt.p + (size_t)2 * nv * roff[s2], n, n, nzs.data(), stream),
-                "alvrl_nonzero_columns");
-            for (uint32_t v = 0; v < nv; v++) nz[v] |= nzs[v];
-        }
-        float ms = 0;
-        hchk(hipEventElapsedTime(&ms, e0, e1), "event");
-        st.ms_rbuild = ms;
-        hipEventDestroy(e0); hipEventDestroy(e1);
+        double tx = now_ms();
+        if (world > 1) or_reduce(*ex, world, nz.data(), nv);
+        st.ms_exchange += now_ms() - tx;
         std::vector<uint32_t> init;
         init.reserve(nv);
         for (uint32_t v = 0; v < nv; v++) if (nz[v]) init.push_back(v);
@@ -324,20 +375,18 @@ struct alvrl_integrator {
         if (nnz) init_off.push_back(nnz);
         if (nnz != nv) init_off.push_back(nv);
         // refinePerSlice (:199-252): one device job per slice
-        std::vector<std::vector<uint32_t>> lrows(ns);
-        std::vector<std::vector<double>> lw(ns);
-        std::vector<std::vector<uint64_t>> loff(ns);
-        std::vector<std::vector<uint32_t>> lstr(ns);
-        std::vector<alvrl_cluster_job> jobs(ns);
-        for (uint32_t s = 0; s < ns; s++) {
-            prep->local_matrix(s, &lrows[s], &lw[s]);
-            for (uint32_t g : lrows[s]) { loff[s].push_back(row_base[g]); lstr[s].push_back(row_stride[g]); }
-            alvrl_cluster_job& j = jobs[s];
-            j.rows = lrows[s].data();
-            j.row_off = loff[s].data();
-            j.row_stride = lstr[s].data();
-            j.locw = lw[s].data();
-            j.nrows = (uint32_t)lrows[s].size();
+        std::vector<std::vector<uint64_t>> loff(nm);
+        std::vector<std::vector<uint32_t>> lstr(nm);
+        std::vector<alvrl_cluster_job> jobs(nm);
+        for (uint32_t k = 0; k < nm; k++) {
+            const uint32_t s = mine[k];
+            for (uint32_t g : lrows[k]) { loff[k].push_back(row_base[g]); lstr[k].push_back(row_stride[g]); }
+            alvrl_cluster_job& j = jobs[k];
+            j.rows = lrows[k].data();
+            j.row_off = loff[k].data();
+            j.row_stride = lstr[k].data();
+            j.locw = lw[k].data();
+            j.nrows = (uint32_t)lrows[k].size();
             j.pixel_undersampling = prep->slice_undersampling()[s];
             j.undersampling = localUndersampling;
             j.depth_correction = depthCorrection;
@@ -345,25 +394,44 @@ struct alvrl_integrator {
             j.stage_refine = stage_slice_refine(s);
             j.stage_sample = stage_slice_sample(s);
         }
-        std::vector<uint32_t> off(ns + 1), rep((size_t)ns * nv + 1);
-        std::vector<float> w((size_t)ns * nv + 1);
-        std::vector<int> refined(ns + 1);
+        std::vector<uint32_t> off(nm + 1), rep((size_t)nm * nv + 1);
+        std::vector<float> w((size_t)nm * nv + 1);
+        std::vector<int> refined(nm + 1);
         const double t0 = now_ms();
-        chk(alvrl_refine(ctx, Rt.p, rows, ns, jobs.data(), init.data(), init_off.data(),
-                         (uint32_t)init_off.size() - 1, off.data(), rep.data(), w.data(),
-                         refined.data(), stream), "alvrl_refine (slices)");
+        if (nm)
+            chk(alvrl_refine(ctx, Rt.p, rows, nm, jobs.data(), init.data(), init_off.data(),
+                             (uint32_t)init_off.size() - 1, off.data(), rep.data(), w.data(),
+                             refined.data(), stream), "alvrl_refine (slices)");
         st.ms_refine = now_ms() - t0;
+        st.slices_local = nm;
+        // every rank gets every slice's list
+        SliceClusters m;
+        if (world > 1) {
+            tx = now_ms();
+            m = merge_clusters(*ex, world, ns, nm, mine.data(), refined.data(), off.data(), rep.data(), w.data());
+            st.ms_exchange += now_ms() - tx;
+        } else {
+            m.refined.assign(refined.begin(), refined.begin() + ns);
+            m.off.assign(off.begin(), off.begin() + ns + 1);
+            m.reps.assign(rep.begin(), rep.begin() + off[ns]);
+            m.w.assign(w.begin(), w.begin() + off[ns]);
+        }
         // Fall-back clustering (buildClusters :175-186): refine the global
         // clustering of all rows to N/fallBackUndersampling clusters.  Only its
         // users need it -- slices whose refinement failed (:276-282) and pixels
         // without a gather point (:564-571) -- and its counter-RNG streams are
-        // its own, so it is built only when one of them exists.
+        // its own, so it is built only when one of them exists.  Every rank
+        // computes it from all rows (R of the missing slices built here).
         uint32_t failed = 0;
-        for (uint32_t s = 0; s < ns; s++) failed += refined[s] ? 0 : 1;
+        for (uint32_t s = 0; s < ns; s++) failed += m.refined[s] ? 0 : 1;
         bool need_fb = failed > 0;
         for (uint32_t p : pixel_to_slice) if (p == 0xFFFFFFFFu) { need_fb = true; break; }
         fb_reps.clear(); fb_w.clear();
         if (need_fb) {
+            if (rows_built != rows) {
+                std::vector<uint8_t> unused;
+                build_R(std::vector<char>(ns, 1), &unused);
+            }
             std::vector<uint32_t> all(rows);
             for (uint32_t r = 0; r < rows; r++) all[r] = r;
             std::vector<double> dw(rows, 1.0 / (double)rows);
@@ -393,9 +461,9 @@ struct alvrl_integrator {
         reps.clear(); weights.clear();
         for (uint32_t s = 0; s < ns; s++) {
             slice_off[s] = (uint32_t)reps.size();
-            if (refined[s]) {
-                reps.insert(reps.end(), rep.begin() + off[s], rep.begin() + off[s + 1]);
-                weights.insert(weights.end(), w.begin() + off[s], w.begin() + off[s + 1]);
+            if (m.refined[s]) {
+                reps.insert(reps.end(), m.reps.begin() + m.off[s], m.reps.begin() + m.off[s + 1]);
+                weights.insert(weights.end(), m.w.begin() + m.off[s], m.w.begin() + m.off[s + 1]);
             } else {   // "Could not refine slice %d, using fall-back clustering!"
                 reps.insert(reps.end(), fb_reps.begin(), fb_reps.end());
                 weights.insert(weights.end(), fb_w.begin(), fb_w.end());
@@ -404,6 +472,7 @@ struct alvrl_integrator {
         slice_off[ns] = (uint32_t)reps.size();
         st.slices_failed = failed;
         st.clusters_total = reps.size();
+        st.rows_built = rows_built;
         chk(alvrl_set_clusters(ctx, ns, slice_off.data(), reps.data(), weights.data(), fb_reps.data(),
                                fb_w.data(), (uint32_t)fb_reps.size()), "alvrl_set_clusters");
     }
@@ -479,6 +548,8 @@ static int ierr(int code, const std::string& m)
         __VA_ARGS__;                                                         \
     } catch (const IntegError& e) {                                          \
         return ierr(e.code, e.what());                                       \
+    } catch (const CommError& e) {                                           \
+        return ierr(e.code, e.what());                                       \
     } catch (const std::exception& e) {                                      \
         return ierr(ALVRL_ERR_INVALID, e.what());                            \
     }
@@ -527,6 +598,14 @@ ALVRL_API int alvrl_integrator_prepass(alvrl_integrator* it, uint32_t pass)
 {
     if (!it) return ierr(ALVRL_ERR_INVALID, "alvrl_integrator_prepass: null argument");
     GUARD({ hchk(hipSetDevice(it->device), "hipSetDevice"); it->prepass(pass); });
+    return ALVRL_OK;
+}
+
+ALVRL_API int alvrl_integrator_prepass_dist(alvrl_integrator* it, uint32_t pass, uint32_t rank,
+                                            uint32_t world, const alvrl_exchange* ex)
+{
+    if (!it) return ierr(ALVRL_ERR_INVALID, "alvrl_integrator_prepass_dist: null argument");
+    GUARD({ hchk(hipSetDevice(it->device), "hipSetDevice"); it->prepass(pass, rank, world, ex); });
     return ALVRL_OK;
 }
 
@@ -617,6 +696,8 @@ ALVRL_API int alvrl_integrator_R(alvrl_integrator* it, float* out, uint64_t cap)
     if (!it || !out) return ierr(ALVRL_ERR_INVALID, "alvrl_integrator_R: null argument");
     const uint64_t need = (uint64_t)2 * it->vrls.n * it->st.rep_rows;
     if (cap < need) return ierr(ALVRL_ERR_INVALID, "alvrl_integrator_R: buffer too small");
+    if (it->rows_built != it->st.rep_rows)
+        return ierr(ALVRL_ERR_STATE, "alvrl_integrator_R: this rank holds R of its own slices only");
     GUARD({
         hchk(hipSetDevice(it->device), "hipSetDevice");
         hchk(hipStreamSynchronize(it->stream), "sync");

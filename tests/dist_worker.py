@@ -21,6 +21,51 @@ import bench                # noqa: E402
 from oracle import Oracle   # noqa: E402
 
 
+def _slice_lists(s, nv=50):
+    """Deterministic stand-in for slice s's refined cluster list (ragged,
+    some empty, every fifth slice failed)."""
+    rng = np.random.default_rng(1000 + s)
+    k = int(rng.integers(0, 12)) if s % 7 else 0
+    return (s % 5 != 3, rng.choice(nv, k, replace=False).astype(np.uint32),
+            rng.random(k, dtype=np.float32))
+
+
+def check_exchange(rank, world):
+    """alvrl_exchange's building blocks (the collectives of the slice-sharded
+    prepass, alvrl_integrator_prepass_dist) over gloo."""
+    ex = alvrl.Exchange()
+    ok = {}
+    # variable-size all-gather, rank 0 contributing nothing
+    mine = np.arange(3 * rank, dtype=np.uint8) + rank
+    got = ex.allgatherv(mine)
+    ok["allgatherv"] = all(np.array_equal(g, np.arange(3 * r, dtype=np.uint8) + r) for r, g in enumerate(got))
+    # OR of the ranks' non-zero masks
+    nv = 77
+    mask = np.zeros(nv, np.uint8)
+    mask[rank::world + 1] = 1
+    ref = np.zeros(nv, np.uint8)
+    for r in range(world):
+        ref[r::world + 1] = 1
+    ok["or"] = bool(np.array_equal(ex.or_(mask), ref))
+    # cluster lists of slices dealt round robin, merged into the global CSR
+    ns = 23
+    local = {s: _slice_lists(s) for s in range(rank, ns, world)}
+    refined, off, reps, w = ex.clusters(ns, local)
+    good = len(off) == ns + 1 and off[0] == 0
+    for s in range(ns):
+        r_ok, rr, ww = _slice_lists(s)
+        good &= bool(refined[s]) == r_ok
+        good &= np.array_equal(reps[off[s]:off[s + 1]], rr) and np.array_equal(ww, w[off[s]:off[s + 1]])
+    ok["clusters"] = bool(good)
+    # a slice reported twice is rejected
+    try:
+        ex.clusters(ns, {0: _slice_lists(0)})
+        ok["duplicate_rejected"] = world == 1
+    except alvrl.AlvrlError as e:
+        ok["duplicate_rejected"] = e.code == 6
+    return ok
+
+
 def main():
     out_path = sys.argv[1]
     dist.init_process_group("gloo")
@@ -40,6 +85,7 @@ def main():
     elapsed, counts = bench.aggregate_over_ranks(1.0 + rank, [cnt, 1], world, torch.device("cpu"))
     sizes = torch.tensor([len(pix)], dtype=torch.int64)
     dist.all_reduce(sizes)
+    exchange = check_exchange(rank, world)
     if rank == 0:
         full, fcnt = o.gather_brute(P, recs, vrls, pc, nthreads=2)
         verdict = {
@@ -48,6 +94,7 @@ def main():
             "pixels_total": int(sizes.item()),
             "elapsed_max": elapsed,
             "count_sum": counts[0], "count_full": int(fcnt), "ranks": counts[1],
+            "exchange": exchange,
         }
         with open(out_path, "w") as f:
             json.dump(verdict, f)

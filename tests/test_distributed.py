@@ -3,7 +3,9 @@ launches bench.py (torch.distributed.run, 127.0.0.1 rendezvous).  Each rank
 renders its 64x64 tiles (alvrl_tile_pixels) with the oracle; the framebuffer
 reduce to rank 0 must equal the single-process frame bit for bit (every pixel
 is owned by exactly one rank), and bench.aggregate_over_ranks must give the
-max of the ranks' times and the sum of their counts."""
+max of the ranks' times and the sum of their counts.  The same run checks the
+collectives of the slice-sharded prepass (alvrl.Exchange over gloo:
+variable-size all-gather, mask OR, cluster-list merge)."""
 import json
 import os
 import socket
@@ -37,3 +39,4 @@ def test_tile_sharding_gloo(tmp_path, world):
     assert v["pixels_total"] == 150 * 70
     assert v["elapsed_max"] == float(world) and v["ranks"] == world
     assert v["count_sum"] == v["count_full"]
+    assert v["exchange"] == {"allgatherv": True, "or": True, "clusters": True, "duplicate_rejected": True}

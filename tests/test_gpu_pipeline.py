@@ -186,3 +186,38 @@ def test_golden_c1_small_device(oracle, gpu_ok):
         img = fb.view(-1, 3).cpu().numpy()
         rel = abs(img.mean() - g["clustered"].mean()) / g["clustered"].mean()
         assert rel < 2e-2, rel
+
+
+def test_sharded_prepass(gpu_ok, tmp_path):
+    """The slice-sharded prepass (alvrl_integrator_prepass_dist):
+    2 gloo ranks on the one GPU, see tests/gpu_dist_worker.py.  Cluster lists
+    and the frame are identical to the one-GPU prepass bit for bit; without
+    neighbours every slice and R row is built exactly once over the ranks."""
+    import json
+    import os
+    import socket
+    import subprocess
+    import sys
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    out = tmp_path / "verdict.json"
+    here = os.path.dirname(os.path.abspath(__file__))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.join(here, "gpu_dist_worker.py"), str(out)]
+    r = subprocess.run(cmd, env=dict(os.environ, OMP_NUM_THREADS="4"), capture_output=True, text=True,
+                       timeout=900)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    v = json.loads(out.read_text())
+    print(v)
+    assert v["world"] == 2
+    for name in ("adaptive", "neighbours", "fixed"):
+        c = v[name]
+        assert c["clusters_identical_all_ranks"] and c["frame_bit_exact"], name
+        assert c["slices_sum"] == c["slices"], name
+        if name != "neighbours":
+            assert c["pairs_sum"] == c["pairs_one"] and c["rows_sum"] == c["rows"], name
+        else:
+            assert c["rows_sum"] >= c["rows"], name
