@@ -145,7 +145,7 @@ def main():
         step(i)
     barrier()
     s0 = it.stats()
-    kernel_ms, rbuild_ms, refine_ms, prepass_ms = [], [], [], []
+    kernel_ms, rbuild_ms, refine_ms, prepass_ms, refine_kms, refine_ent = [], [], [], [], [], []
     barrier()
     t0 = time.perf_counter()
     for i in range(args.steps):
@@ -155,6 +155,8 @@ def main():
         rbuild_ms.append(st["ms_rbuild"])
         refine_ms.append(st["ms_refine"])
         prepass_ms.append(st["ms_prepass_wall"])
+        refine_kms.append(st["ms_refine_kernel"])
+        refine_ent.append(st["refine_entries"])
     barrier()
     elapsed = time.perf_counter() - t0
     s1 = it.stats()
@@ -165,21 +167,42 @@ def main():
         elapsed, [contrib, render_pairs, pre_pairs], world, dev)
 
     value = contrib / elapsed
-    # roofline of the dominant kernel (the render gather), timed with HIP events
-    # on the stream it was launched on
-    avg_kernel_s = float(np.mean(kernel_ms)) / 1e3 if kernel_ms else float("nan")
-    pairs_per_launch_rank = (s1["contrib_render"] - s0["contrib_render"]) / max(args.steps, 1)
+    # Rooflines (this rank's launches, HIP events on the stream each kernel ran
+    # on).  Algorithmic bytes per launch (DESIGN.md "Roofline"): the gathers
+    # and the R build count BYTES_PER_PAIR per VRL contribution; the
+    # refinement counts 8 B per R entry it must read (alvrl_last_refine_entries).
+    nst = max(args.steps, 1)
     kind = "clustered" if clustered else "brute"
-    bytes_per_launch = BYTES_PER_PAIR[kind] * pairs_per_launch_rank
-    achieved = bytes_per_launch / avg_kernel_s / 1e9 if avg_kernel_s > 0 else 0.0
-    traffic = None
+    pmc = {}
     try:
         with open(args.pmc_json) as f:
             pm = json.load(f)
-        if pm.get("config") == args.config:
-            traffic = pm.get("hbm_bytes_per_launch")
+        for rec in (pm if isinstance(pm, list) else [pm]):
+            if rec.get("config") == args.config:
+                pmc[rec.get("kernel_key", "render")] = rec.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass
+
+    def roof(name, key, bytes_per_launch, ms, note):
+        s_ = ms / 1e3
+        ach = bytes_per_launch / s_ / 1e9 if s_ > 0 else 0.0
+        return {"bound": "hbm", "kernel": name, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": ach / HBM_PEAK_GBS, "traffic": pmc.get(key), "bytes_per_launch": bytes_per_launch,
+                "launch_ms": ms, "note": note}
+
+    pairs_per_launch_rank = (s1["contrib_render"] - s0["contrib_render"]) / nst
+    rooflines = {"render": roof(f"k_gather_{kind}", "render", BYTES_PER_PAIR[kind] * pairs_per_launch_rank,
+                               float(np.mean(kernel_ms)) if kernel_ms else 0.0,
+                               "the gather is VALU/transcendental-bound (VRL records are broadcast from "
+                               "SGPRs), see DESIGN.md")}
+    if clustered:
+        rooflines["refine"] = roof("k_refine", "refine", 8.0 * float(np.mean(refine_ent)),
+                                   float(np.mean(refine_kms)),
+                                   "latency-bound: one workgroup per slice, f64 recurrences, see DESIGN.md")
+        rooflines["rbuild"] = roof("k_build_R_blocks", "rbuild",
+                                   BYTES_PER_PAIR["rbuild"] * (s1["contrib_preprocess"] - s0["contrib_preprocess"]) / nst,
+                                   float(np.mean(rbuild_ms)), "VALU-bound like the gather")
+    dominant = max(rooflines, key=lambda k: rooflines[k]["launch_ms"])
 
     out = None
     if rank == 0:
@@ -206,18 +229,15 @@ def main():
             "breakdown": {"render_pairs": render_pairs, "prepass_pairs": pre_pairs,
                           "render_kernel_ms": float(np.mean(kernel_ms)) if kernel_ms else None,
                           "rbuild_ms": float(np.mean(rbuild_ms)), "refine_ms": float(np.mean(refine_ms)),
+                          "refine_kernel_ms": float(np.mean(refine_kms)),
+                          "refine_entries": float(np.mean(refine_ent)),
                           "prepass_wall_ms": float(np.mean(prepass_ms)),
                           "slices": int(s1["slices"]), "rep_rows": int(s1["rep_rows"]),
                           "clusters_total": int(s1["clusters_total"]),
                           "slices_failed": int(s1["slices_failed"]),
                           "exchange_ms": float(s1["ms_exchange"])},
-            "roofline": {"bound": "hbm", "kernel": f"k_gather_{kind}", "achieved": achieved,
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": traffic,
-                         "bytes_per_pair": BYTES_PER_PAIR[kind],
-                         "pairs_per_launch": pairs_per_launch_rank,
-                         "note": "algorithmic bytes; the gather is VALU/transcendental-bound "
-                                 "(VRL records are broadcast from SGPRs), see DESIGN.md"},
+            "roofline": rooflines[dominant],
+            "rooflines": rooflines,
             "cpu_baseline": None,
         }
     if world == 1 and not args.no_cpu_baseline:

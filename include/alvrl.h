@@ -206,6 +206,12 @@ ALVRL_API int alvrl_refine(alvrl_ctx *ctx, const float *d_Rt, uint64_t ld, uint3
                            void *stream);
 /* Milliseconds the device spent in the last alvrl_refine call (HIP events). */
 ALVRL_API int alvrl_last_refine_ms(alvrl_ctx *ctx, float *ms);
+/* R entries (float2, 8 B each) the last alvrl_refine had to read, summed over
+ * its jobs: nrows * (3 * nvrl + the columns of every cluster it split) --
+ * column weights, initial cluster variances and the unclustered variance read
+ * the whole local matrix once, a split reads its cluster's columns once.  The
+ * algorithmic bytes of the refinement's roofline. */
+ALVRL_API int alvrl_last_refine_entries(alvrl_ctx *ctx, uint64_t *entries);
 
 /* ---- framebuffer --------------------------------------------------- */
 /* ImageBlock::put of 1-spp box-filtered samples (imageblock.h:124-131):

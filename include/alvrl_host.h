@@ -143,6 +143,10 @@ typedef struct {
      * and the host time spent in the exchange of the last prepass */
     uint64_t slices_local, rows_built;
     double ms_exchange;
+    /* device time of the last prepass's refinement and R-build kernels (HIP
+     * events) and the R entries its refinement read (alvrl_last_refine_entries) */
+    double ms_refine_kernel;
+    uint64_t refine_entries;
 } alvrl_integrator_stats;
 ALVRL_API int alvrl_integrator_get_stats(alvrl_integrator *it, alvrl_integrator_stats *st);
 /* The device context the integrator drives (for low-level access). */

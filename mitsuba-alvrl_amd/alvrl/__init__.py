@@ -89,6 +89,7 @@ def lib() -> C.CDLL:
     L.alvrl_refine.argtypes = [vp, vp, u64, u32, P(ClusterJob), P(u32), P(u32), u32, P(u32),
                                P(u32), P(f32), P(i32), vp]
     L.alvrl_last_refine_ms.argtypes = [vp, P(f32)]
+    L.alvrl_last_refine_entries.argtypes = [vp, P(u64)]
     L.alvrl_get_stats.argtypes = [vp, P(u64), P(u64)]
     L.alvrl_reset_stats.argtypes = [vp]
     L.alvrl_gather_brute_host.argtypes = [vp, vp, vp, u32, vp]
@@ -238,6 +239,11 @@ class Context:
         _check(self.L.alvrl_last_refine_ms(self.h, C.byref(ms)))
         return ms.value
 
+    def last_refine_entries(self) -> int:
+        n = C.c_uint64()
+        _check(self.L.alvrl_last_refine_entries(self.h, C.byref(n)))
+        return int(n.value)
+
     # ---- host-pointer conveniences ----
     def gather_brute_host(self, recs: np.ndarray, ids=None) -> np.ndarray:
         recs = _np(recs, np.float32)
@@ -299,7 +305,8 @@ class IntegratorStats(C.Structure):
                 ("ms_refine", C.c_double), ("ms_render_kernel", C.c_double),
                 ("ms_prepass_wall", C.c_double), ("slices_failed", C.c_uint32),
                 ("fallback_built", C.c_int), ("slices_local", C.c_uint64), ("rows_built", C.c_uint64),
-                ("ms_exchange", C.c_double)]
+                ("ms_exchange", C.c_double), ("ms_refine_kernel", C.c_double),
+                ("refine_entries", C.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

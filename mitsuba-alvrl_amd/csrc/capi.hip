@@ -52,7 +52,7 @@ struct HostJob {
 int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, uint32_t seed,
                 uint32_t pass, uint32_t njobs, const HostJob* jobs, const uint32_t* init_vrls,
                 const uint32_t* init_off, uint32_t ninit, uint32_t* out_off, uint32_t* out_reps,
-                float* out_w, int* out_refined, float* ms, std::string* err);
+                float* out_w, int* out_refined, float* ms, unsigned long long* entries, std::string* err);
 }  // namespace alvrl
 
 using namespace alvrl;
@@ -81,6 +81,7 @@ struct alvrl_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
     float refine_ms = 0.0f;
+    unsigned long long refine_entries = 0;
     std::mutex mu;
 };
 
@@ -388,7 +389,7 @@ ALVRL_API int alvrl_refine(alvrl_ctx* c, const float* d_Rt, uint64_t ld, uint32_
     float ms = 0.0f;
     int rc = refine_jobs(pick(c, stream), d_Rt, ld, c->nvrl, c->P.seed, c->P.pass, njobs, hj.data(),
                          init_vrls, init_off, ninit, out_off, out_reps, out_weights, out_refined,
-                         &ms, &err);
+                         &ms, &c->refine_entries, &err);
     c->refine_ms = ms;
     if (rc) return fail(rc, err);
     return ALVRL_OK;
@@ -398,6 +399,13 @@ ALVRL_API int alvrl_last_refine_ms(alvrl_ctx* c, float* ms)
 {
     if (!c || !ms) return fail(ALVRL_ERR_INVALID, "alvrl_last_refine_ms: null argument");
     *ms = c->refine_ms;
+    return ALVRL_OK;
+}
+
+ALVRL_API int alvrl_last_refine_entries(alvrl_ctx* c, uint64_t* entries)
+{
+    if (!c || !entries) return fail(ALVRL_ERR_INVALID, "alvrl_last_refine_entries: null argument");
+    *entries = c->refine_entries;
     return ALVRL_OK;
 }
 

@@ -255,7 +255,8 @@ struct alvrl_integrator {
         st.particles = vrls.particle_count;
         st.slices_failed = 0;
         st.fallback_built = 0;
-        st.ms_rbuild = st.ms_refine = st.ms_exchange = 0;
+        st.ms_rbuild = st.ms_refine = st.ms_exchange = st.ms_refine_kernel = 0;
+        st.refine_entries = 0;
         st.slices_local = 0;
         st.rows_built = 0;
         if (clustered) build_clusters(pass, rank, world, ex);
@@ -404,6 +405,14 @@ struct alvrl_integrator {
                              refined.data(), stream), "alvrl_refine (slices)");
         st.ms_refine = now_ms() - t0;
         st.slices_local = nm;
+        if (nm) {
+            float kms = 0.0f;
+            uint64_t ent = 0;
+            chk(alvrl_last_refine_ms(ctx, &kms), "alvrl_last_refine_ms");
+            chk(alvrl_last_refine_entries(ctx, &ent), "alvrl_last_refine_entries");
+            st.ms_refine_kernel = kms;
+            st.refine_entries = ent;
+        }
         // every rank gets every slice's list
         SliceClusters m;
         if (world > 1) {
@@ -452,6 +461,14 @@ struct alvrl_integrator {
                              (uint32_t)init_off.size() - 1, foff.data(), frep.data(), fw.data(), &fref,
                              stream), "alvrl_refine (fall-back)");
             st.ms_refine += now_ms() - t1;
+            {
+                float kms = 0.0f;
+                uint64_t ent = 0;
+                chk(alvrl_last_refine_ms(ctx, &kms), "alvrl_last_refine_ms");
+                chk(alvrl_last_refine_entries(ctx, &ent), "alvrl_last_refine_entries");
+                st.ms_refine_kernel += kms;
+                st.refine_entries += ent;
+            }
             if (!fref) throw IntegError(ALVRL_ERR_NUMERIC, "couldn't refine global clustering! (but all VRLs should be non-zero!)");
             fb_reps.assign(frep.begin(), frep.begin() + foff[1]);
             fb_w.assign(fw.begin(), fw.begin() + foff[1]);

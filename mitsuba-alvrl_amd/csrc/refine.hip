@@ -87,6 +87,7 @@ struct Common {
     uint32_t ninit;
     uint32_t seed, pass;
     unsigned long long* prof;   // per-phase cycle totals (ALVRL_REFINE_PROFILE=1), or null
+    unsigned long long* entries;   // R entries the clustering has to read (roofline bytes / 8)
 };
 
 // Phase timer of lane 0 (s_memtime deltas summed over jobs).
@@ -1108,6 +1109,7 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
     const uint32_t N = cm.nvrl, R = J.nrows;
     const uint32_t nv = cm.init_off[cm.ninit];
     Prof pf{cm.prof, (long long)clock64()};
+    unsigned long long split_cols = 0;   // thread 0: columns of the clusters split
     if (tid == 0) {
         C.tracingVar = C.unclIntVar = C.clUnderVar = C.clIntVar = 0.0f;
         C.heap_n = C.singles_n = C.sh_heap_n = C.sh_singles_n = 0;
@@ -1228,7 +1230,7 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
             while (true) {
                 if (tid == 0) {
                     C.go = (n_clusters(C) < target && C.heap_n > 0 && !C.err);
-                    if (C.go) { const CNode cn = pop_multi(J, C); C.b = cn.begin; C.e = cn.end; }
+                    if (C.go) { const CNode cn = pop_multi(J, C); C.b = cn.begin; C.e = cn.end; split_cols += cn.end - cn.begin; }
                 }
                 __syncthreads();
                 if (!C.go) break;
@@ -1253,7 +1255,7 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
                 while (true) {
                     if (tid == 0) {
                         C.go = C.heap_n > 0 && !C.err;
-                        if (C.go) { const CNode cn = pop_multi(J, C); C.b = cn.begin; C.e = cn.end; }
+                        if (C.go) { const CNode cn = pop_multi(J, C); C.b = cn.begin; C.e = cn.end; split_cols += cn.end - cn.begin; }
                     }
                     __syncthreads();
                     if (!C.go) break;
@@ -1279,7 +1281,7 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
                     for (int i = 0; i < corrected; i++) {
                         if (tid == 0) {
                             C.go = C.heap_n > 0 && !C.err;
-                            if (C.go) { const CNode cn = pop_multi(J, C); C.b = cn.begin; C.e = cn.end; }
+                            if (C.go) { const CNode cn = pop_multi(J, C); C.b = cn.begin; C.e = cn.end; split_cols += cn.end - cn.begin; }
                         }
                         __syncthreads();
                         if (!C.go) break;
@@ -1322,6 +1324,36 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
         *J.out_n = refined ? (uint32_t)(ns + nh) : 0u;
         *J.out_refined = refined;
         *J.out_err = C.err;
+        // column weights, initial clusters and unclustered variance read every
+        // entry once; a split reads its cluster's columns (at least) once
+        if (cm.entries) atomicAdd(cm.entries, (3ull * N + split_cols) * R);
+    }
+}
+
+// Packs the jobs' representative lists back to back (job order) so the host
+// fetches every result with three copies: meta[3j..3j+2] = (n, refined, err).
+__global__ void __launch_bounds__(256) k_pack_results(const JobDev* __restrict__ jobs, uint32_t njobs,
+                                                      uint32_t nvrl, uint32_t* __restrict__ meta,
+                                                      uint32_t* __restrict__ reps, float* __restrict__ w)
+{
+    const uint32_t j = blockIdx.x;
+    __shared__ unsigned long long off;
+    if (threadIdx.x == 0) {
+        unsigned long long o = 0;
+        for (uint32_t i = 0; i < j; i++) o += min(*jobs[i].out_n, nvrl);
+        off = o;
+    }
+    __syncthreads();
+    const JobDev& J = jobs[j];
+    const uint32_t n = min(*J.out_n, nvrl);
+    for (uint32_t k = threadIdx.x; k < n; k += 256) {
+        reps[off + k] = J.out_reps[k];
+        w[off + k] = J.out_w[k];
+    }
+    if (threadIdx.x == 0) {
+        meta[3 * j] = *J.out_n;
+        meta[3 * j + 1] = (uint32_t)*J.out_refined;
+        meta[3 * j + 2] = (uint32_t)*J.out_err;
     }
 }
 
@@ -1344,9 +1376,10 @@ struct HostJob {
 int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, uint32_t seed,
                 uint32_t pass, uint32_t njobs, const HostJob* jobs, const uint32_t* init_vrls,
                 const uint32_t* init_off, uint32_t ninit, uint32_t* out_off, uint32_t* out_reps,
-                float* out_w, int* out_refined, float* ms, std::string* err)
+                float* out_w, int* out_refined, float* ms, unsigned long long* entries, std::string* err)
 {
     if (ms) *ms = 0.0f;
+    if (entries) *entries = 0;
     out_off[0] = 0;
     if (njobs == 0) return 0;
     const uint32_t nv = init_off[ninit];
@@ -1375,7 +1408,8 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
                align_up(N * 4) * 2 + align_up(16);
     };
     size_t total = align_up(rows_total * 8) + align_up(rows_total * 4) + align_up(rows_total * 8) + align_up((size_t)nv * 4) +
-                   align_up((size_t)(ninit + 1) * 4) + align_up((size_t)njobs * sizeof(JobDev));
+                   align_up((size_t)(ninit + 1) * 4) + align_up((size_t)njobs * sizeof(JobDev)) +
+                   align_up((size_t)njobs * 12) + 2 * align_up((size_t)njobs * N * 4) + align_up(8);
     for (uint32_t j = 0; j < njobs; j++) { job_off[j] = total; total += job_bytes(jobs[j].nrows); }
     char* arena = nullptr;
     hipError_t e = hipMalloc(&arena, total);
@@ -1386,7 +1420,11 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
     double* d_locw = (double*)(arena + o); o += align_up(rows_total * 8);
     uint32_t* d_init = (uint32_t*)(arena + o); o += align_up((size_t)nv * 4);
     uint32_t* d_init_off = (uint32_t*)(arena + o); o += align_up((size_t)(ninit + 1) * 4);
-    JobDev* d_jobs = (JobDev*)(arena + o);
+    JobDev* d_jobs = (JobDev*)(arena + o); o += align_up((size_t)njobs * sizeof(JobDev));
+    uint32_t* d_meta = (uint32_t*)(arena + o); o += align_up((size_t)njobs * 12);
+    uint32_t* d_preps = (uint32_t*)(arena + o); o += align_up((size_t)njobs * N * 4);
+    float* d_pw = (float*)(arena + o); o += align_up((size_t)njobs * N * 4);
+    unsigned long long* d_entries = (unsigned long long*)(arena + o);
     std::vector<unsigned long long> h_roff(rows_total);
     std::vector<uint32_t> h_rstride(rows_total);
     std::vector<double> h_locw(rows_total);
@@ -1447,6 +1485,7 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
     cm.init_vrls = d_init; cm.init_off = d_init_off; cm.ninit = ninit;
     cm.seed = seed; cm.pass = pass;
     cm.prof = nullptr;
+    cm.entries = d_entries;
     const char* pe = std::getenv("ALVRL_REFINE_PROFILE");
     if (pe && pe[0] == '1' && hipMalloc(&cm.prof, PF_N * 8) == hipSuccess)
         (void)hipMemsetAsync(cm.prof, 0, PF_N * 8, s);
@@ -1459,6 +1498,7 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
     if (e == hipSuccess) e = hipMemcpyAsync(d_init, init_vrls, (size_t)nv * 4, hipMemcpyHostToDevice, s);
     if (e == hipSuccess) e = hipMemcpyAsync(d_init_off, init_off, (size_t)(ninit + 1) * 4, hipMemcpyHostToDevice, s);
     if (e == hipSuccess) e = hipMemcpyAsync(d_jobs, h_jobs.data(), njobs * sizeof(JobDev), hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipMemsetAsync(d_entries, 0, 8, s);
     if (e == hipSuccess) e = hipEventRecord(e0, s);
     if (e == hipSuccess) {
         // ALVRL_REFINE_BATCH=n (developer knob): launch the jobs n at a time,
@@ -1471,11 +1511,17 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
         }
     }
     if (e == hipSuccess) e = hipEventRecord(e1, s);
-    // gather results
+    // gather results: packed on the device, three copies
     std::vector<uint32_t> meta(3 * (size_t)njobs);
-    for (uint32_t j = 0; j < njobs && e == hipSuccess; j++)
-        e = hipMemcpyAsync(&meta[3 * (size_t)j], h_jobs[j].out_n, 12, hipMemcpyDeviceToHost, s);
+    unsigned long long h_entries = 0;
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_pack_results, dim3(njobs), dim3(256), 0, s, d_jobs, njobs, nvrl, d_meta, d_preps, d_pw);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(meta.data(), d_meta, (size_t)njobs * 12, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(&h_entries, d_entries, 8, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (entries) *entries = h_entries;
     if (cm.prof) {
         unsigned long long h[PF_N];
         if (hipMemcpy(h, cm.prof, sizeof(h), hipMemcpyDeviceToHost) == hipSuccess) {
@@ -1498,13 +1544,12 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
             if (jerr) { rc = 5; *err = "alvrl_refine: clustering invariant violated in job " + std::to_string(j); }
             if (n > nvrl) { rc = 5; *err = "alvrl_refine: corrupt representative count"; break; }
             out_refined[j] = refined;
-            if (n) {
-                e = hipMemcpyAsync(out_reps + off, h_jobs[j].out_reps, (size_t)n * 4, hipMemcpyDeviceToHost, s);
-                if (e == hipSuccess) e = hipMemcpyAsync(out_w + off, h_jobs[j].out_w, (size_t)n * 4, hipMemcpyDeviceToHost, s);
-                if (e != hipSuccess) break;
-            }
             off += n;
             out_off[j + 1] = off;
+        }
+        if (off) {
+            e = hipMemcpyAsync(out_reps, d_preps, (size_t)off * 4, hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess) e = hipMemcpyAsync(out_w, d_pw, (size_t)off * 4, hipMemcpyDeviceToHost, s);
         }
         if (e == hipSuccess) e = hipStreamSynchronize(s);
         if (e == hipSuccess && ms) e = hipEventElapsedTime(ms, e0, e1);
