@@ -204,6 +204,17 @@ ALVRL_API int alvrl_refine(alvrl_ctx *ctx, const float *d_Rt, uint64_t ld, uint3
                            const uint32_t *init_off, uint32_t ninit, uint32_t *out_off,
                            uint32_t *out_reps, float *out_weights, int *out_refined,
                            void *stream);
+/* clusterRefinement (Preprocessor.cpp:899-912, the globalCluster option):
+ * one Clustering ctor + refine(job->undersampling), then getVrlsPerCluster
+ * (:526-543) -- singletons in list order, then the heap's clusters.  The
+ * initial clusters may list a subset of the VRLs (the non-zero ones).
+ * out_vrls: init_off[ninit] ids; out_off: *n_clusters + 1 offsets (capacity
+ * init_off[ninit] + 1).  job->do_refine and depth_correction are ignored. */
+ALVRL_API int alvrl_refine_members(alvrl_ctx *ctx, const float *d_Rt, uint64_t ld,
+                                   const alvrl_cluster_job *job, const uint32_t *init_vrls,
+                                   const uint32_t *init_off, uint32_t ninit, uint32_t *out_vrls,
+                                   uint32_t *out_off, uint32_t *n_clusters, int *out_refined,
+                                   void *stream);
 /* Milliseconds the device spent in the last alvrl_refine call (HIP events). */
 ALVRL_API int alvrl_last_refine_ms(alvrl_ctx *ctx, float *ms);
 /* R entries (float2, 8 B each) the last alvrl_refine had to read, summed over

@@ -90,6 +90,8 @@ def lib() -> C.CDLL:
                                P(u32), P(f32), P(i32), vp]
     L.alvrl_last_refine_ms.argtypes = [vp, P(f32)]
     L.alvrl_last_refine_entries.argtypes = [vp, P(u64)]
+    L.alvrl_refine_members.argtypes = [vp, vp, u64, P(ClusterJob), P(u32), P(u32), u32, P(u32), P(u32),
+                                       P(u32), P(i32), vp]
     L.alvrl_get_stats.argtypes = [vp, P(u64), P(u64)]
     L.alvrl_reset_stats.argtypes = [vp]
     L.alvrl_gather_brute_host.argtypes = [vp, vp, vp, u32, vp]
@@ -234,6 +236,23 @@ class Context:
                                    _arr(refined, C.c_int), C.c_void_p(stream) if stream else None))
         return off, reps[:off[-1]].copy(), w[:off[-1]].copy(), refined[:nj].astype(bool)
 
+    def refine_members(self, d_Rt, ld: int, job: dict, init_vrls, init_off, stream=None):
+        """clusterRefinement + getVrlsPerCluster (alvrl_refine_members):
+        (member ids, cluster offsets, refined)."""
+        rows = _np(job["rows"], np.uint32); lw = _np(job["locw"], np.float64)
+        cj = ClusterJob(_arr(rows, C.c_uint32), _arr(lw, C.c_double), len(rows),
+                        job["pixel_undersampling"], job["undersampling"], 1.0, 1,
+                        job.get("stage_refine", 0xFFFFFFFE), job.get("stage_refine", 0xFFFFFFFE))
+        iv = _np(init_vrls, np.uint32); io = _np(init_off, np.uint32)
+        nv = int(io[-1])
+        mem = np.zeros(max(1, nv), np.uint32); off = np.zeros(nv + 2, np.uint32)
+        nc = C.c_uint32(); ok = C.c_int()
+        _check(self.L.alvrl_refine_members(self.h, _ptr(d_Rt), ld, C.byref(cj), _arr(iv, C.c_uint32),
+                                           _arr(io, C.c_uint32), len(io) - 1, _arr(mem, C.c_uint32),
+                                           _arr(off, C.c_uint32), C.byref(nc), C.byref(ok),
+                                           C.c_void_p(stream) if stream else None))
+        return mem[:nv].copy(), off[:nc.value + 1].copy(), bool(ok.value)
+
     def last_refine_ms(self) -> float:
         ms = C.c_float()
         _check(self.L.alvrl_last_refine_ms(self.h, C.byref(ms)))
@@ -306,7 +325,7 @@ class IntegratorStats(C.Structure):
                 ("ms_prepass_wall", C.c_double), ("slices_failed", C.c_uint32),
                 ("fallback_built", C.c_int), ("slices_local", C.c_uint64), ("rows_built", C.c_uint64),
                 ("ms_exchange", C.c_double), ("ms_refine_kernel", C.c_double),
-                ("refine_entries", C.c_uint64)]
+                ("refine_entries", C.c_uint64), ("global_clusters", C.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -48,6 +48,9 @@ struct HostJob {
     uint32_t stage_refine, stage_sample;
     const uint64_t* row_off;
     const uint32_t* row_stride;
+    uint32_t* members;
+    uint32_t* moff;
+    uint32_t* nclusters;
 };
 int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, uint32_t seed,
                 uint32_t pass, uint32_t njobs, const HostJob* jobs, const uint32_t* init_vrls,
@@ -382,7 +385,7 @@ ALVRL_API int alvrl_refine(alvrl_ctx* c, const float* d_Rt, uint64_t ld, uint32_
             return fail(ALVRL_ERR_NUMERIC, "Invalid pixel undersampling: " + std::to_string(J.pixel_undersampling));
         hj[j] = HostJob{J.rows, J.locw, J.nrows, J.pixel_undersampling, J.undersampling,
                         J.depth_correction, J.do_refine, J.stage_refine, J.stage_sample,
-                        J.row_off, J.row_stride};
+                        J.row_off, J.row_stride, nullptr, nullptr, nullptr};
     }
     HIPCHK(hipSetDevice(c->cfg.device));
     std::string err;
@@ -392,6 +395,43 @@ ALVRL_API int alvrl_refine(alvrl_ctx* c, const float* d_Rt, uint64_t ld, uint32_
                          &ms, &c->refine_entries, &err);
     c->refine_ms = ms;
     if (rc) return fail(rc, err);
+    return ALVRL_OK;
+}
+
+ALVRL_API int alvrl_refine_members(alvrl_ctx* c, const float* d_Rt, uint64_t ld, const alvrl_cluster_job* job,
+                                   const uint32_t* init_vrls, const uint32_t* init_off, uint32_t ninit,
+                                   uint32_t* out_vrls, uint32_t* out_off, uint32_t* n_clusters,
+                                   int* out_refined, void* stream)
+{
+    if (!c) return fail(ALVRL_ERR_INVALID, "alvrl_refine_members: null ctx");
+    if (!d_Rt || !job || !init_off || !out_vrls || !out_off || !n_clusters || !out_refined)
+        return fail(ALVRL_ERR_INVALID, "alvrl_refine_members: null argument");
+    if (c->nvrl == 0) return fail(ALVRL_ERR_STATE, "alvrl_refine_members: no VRLs uploaded");
+    if (c->nvrl < 2) return fail(ALVRL_ERR_NUMERIC, "Need at least 2 VRLs to estimate variance");
+    const alvrl_cluster_job& J = *job;
+    if ((!J.rows && !J.row_off) || !J.locw || (J.row_off && !J.row_stride))
+        return fail(ALVRL_ERR_INVALID, "alvrl_refine_members: job without rows");
+    double n1 = 0.0;
+    for (uint32_t r = 0; r < J.nrows; r++) n1 += std::fabs(J.locw[r]);
+    if (std::fabs((float)n1 - 1) > 1e-3)
+        return fail(ALVRL_ERR_NUMERIC, "Incorrect normalization in localityWeights: " + std::to_string(n1));
+    if (J.pixel_undersampling <= 0 || J.pixel_undersampling > 1)
+        return fail(ALVRL_ERR_NUMERIC, "Invalid pixel undersampling: " + std::to_string(J.pixel_undersampling));
+    HostJob hj{J.rows, J.locw, J.nrows, J.pixel_undersampling, J.undersampling, 1.0f, 1,
+               J.stage_refine, J.stage_sample, J.row_off, J.row_stride, out_vrls, out_off, n_clusters};
+    const uint32_t nv = init_off[ninit];
+    std::vector<uint32_t> off(2), reps(c->nvrl + 1);
+    std::vector<float> w(c->nvrl + 1);
+    HIPCHK(hipSetDevice(c->cfg.device));
+    std::string err;
+    float ms = 0.0f;
+    *n_clusters = 0;
+    int rc = refine_jobs(pick(c, stream), d_Rt, ld, c->nvrl, c->P.seed, c->P.pass, 1, &hj, init_vrls,
+                         init_off, ninit, off.data(), reps.data(), w.data(), out_refined, &ms,
+                         &c->refine_entries, &err);
+    c->refine_ms = ms;
+    if (rc) return fail(rc, err);
+    (void)nv;
     return ALVRL_OK;
 }
 

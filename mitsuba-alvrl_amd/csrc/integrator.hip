@@ -37,7 +37,7 @@ using namespace alvrl::host;
 
 namespace {
 // Clustering stream ids (oracle/alvrl_preproc.h).
-constexpr uint32_t kStageFallbackRefine = 1u, kStageFallbackSample = 2u;
+constexpr uint32_t kStageFallbackRefine = 1u, kStageFallbackSample = 2u, kStageGlobalRefine = 0xFFFFFFFEu;
 inline uint32_t stage_slice_refine(uint32_t s) { return 3u + 2u * s; }
 inline uint32_t stage_slice_sample(uint32_t s) { return 4u + 2u * s; }
 
@@ -197,7 +197,6 @@ struct alvrl_integrator {
             throw IntegError(ALVRL_ERR_INVALID, "Need at least 2 volSurfSamples for variance estimate, but received: " + std::to_string(volSurfSamples));
         if (targetNumSlices < 1) throw IntegError(ALVRL_ERR_INVALID, "Invalid target number of slices!");
         if (Rsamples != 1) throw IntegError(ALVRL_ERR_INVALID, "Rsamples != 1 is not supported by this build");
-        if (globalCluster) throw IntegError(ALVRL_ERR_INVALID, "globalCluster=true is not supported by this build yet");
         if (numVrlFalseColor || slicesFalseColor || convergenceFalseColor)
             throw IntegError(ALVRL_ERR_INVALID, "false-colour debug modes are not supported by this build yet");
         clustered = globalCluster || localRefinement;
@@ -257,6 +256,7 @@ struct alvrl_integrator {
         st.fallback_built = 0;
         st.ms_rbuild = st.ms_refine = st.ms_exchange = st.ms_refine_kernel = 0;
         st.refine_entries = 0;
+        st.global_clusters = 0;
         st.slices_local = 0;
         st.rows_built = 0;
         if (clustered) build_clusters(pass, rank, world, ex);
@@ -375,6 +375,48 @@ struct alvrl_integrator {
         std::vector<uint32_t> init_off{0};
         if (nnz) init_off.push_back(nnz);
         if (nnz != nv) init_off.push_back(nv);
+        if (globalCluster && nnz) {
+            // clusterRefinement (Preprocessor.cpp:899-912): the non-zero VRLs
+            // refined as one cluster over all rows with globalUndersampling;
+            // its clusters (getVrlsPerCluster) plus the zero cluster become
+            // every slice's initial clusters.  Needs every row of R.
+            if (rows_built != rows) {
+                std::vector<uint8_t> unused;
+                build_R(std::vector<char>(ns, 1), &unused);
+            }
+            std::vector<uint32_t> all(rows);
+            for (uint32_t r = 0; r < rows; r++) all[r] = r;
+            std::vector<double> dw(rows, 1.0 / (double)rows);
+            alvrl_cluster_job gj{};
+            gj.rows = all.data(); gj.locw = dw.data(); gj.nrows = rows;
+            gj.row_off = row_base.data(); gj.row_stride = row_stride.data();
+            gj.pixel_undersampling = prep->global_pixel_undersampling();
+            gj.undersampling = globalUndersampling;
+            gj.depth_correction = 1.0f;
+            gj.do_refine = 1;
+            gj.stage_refine = gj.stage_sample = kStageGlobalRefine;
+            const uint32_t one[2] = {0, nnz};
+            std::vector<uint32_t> mem(nnz + 1), moff(nnz + 2);
+            uint32_t nc = 0;
+            int ok = 0;
+            const double tg = now_ms();
+            chk(alvrl_refine_members(ctx, Rt.p, rows, &gj, init.data(), one, 1, mem.data(), moff.data(), &nc,
+                                     &ok, stream), "alvrl_refine_members (global cluster)");
+            st.ms_refine += now_ms() - tg;
+            {
+                float kms = 0.0f;
+                uint64_t ent = 0;
+                chk(alvrl_last_refine_ms(ctx, &kms), "alvrl_last_refine_ms");
+                chk(alvrl_last_refine_entries(ctx, &ent), "alvrl_last_refine_entries");
+                st.ms_refine_kernel += kms;
+                st.refine_entries += ent;
+            }
+            if (!ok) throw IntegError(ALVRL_ERR_NUMERIC, "Couldn't refine global clustering!");
+            std::copy(mem.begin(), mem.begin() + nnz, init.begin());
+            init_off.assign(moff.begin(), moff.begin() + nc + 1);
+            if (nnz != nv) init_off.push_back(nv);
+            st.global_clusters = nc;
+        }
         // refinePerSlice (:199-252): one device job per slice
         std::vector<std::vector<uint64_t>> loff(nm);
         std::vector<std::vector<uint32_t>> lstr(nm);
@@ -398,7 +440,7 @@ struct alvrl_integrator {
         std::vector<uint32_t> off(nm + 1), rep((size_t)nm * nv + 1);
         std::vector<float> w((size_t)nm * nv + 1);
         std::vector<int> refined(nm + 1);
-        const double t0 = now_ms();
+        const double t0 = now_ms() - st.ms_refine;
         if (nm)
             chk(alvrl_refine(ctx, Rt.p, rows, nm, jobs.data(), init.data(), init_off.data(),
                              (uint32_t)init_off.size() - 1, off.data(), rep.data(), w.data(),
@@ -410,8 +452,8 @@ struct alvrl_integrator {
             uint64_t ent = 0;
             chk(alvrl_last_refine_ms(ctx, &kms), "alvrl_last_refine_ms");
             chk(alvrl_last_refine_entries(ctx, &ent), "alvrl_last_refine_entries");
-            st.ms_refine_kernel = kms;
-            st.refine_entries = ent;
+            st.ms_refine_kernel += kms;
+            st.refine_entries += ent;
         }
         // every rank gets every slice's list
         SliceClusters m;

@@ -76,6 +76,10 @@ struct JobDev {
     uint32_t* out_n;
     int* out_refined;
     int* out_err;
+    // getVrlsPerCluster (optional): member ids, cluster offsets, cluster count
+    uint32_t* out_members;
+    uint32_t* out_moff;
+    uint32_t* out_nclusters;
 };
 
 struct Common {
@@ -1318,6 +1322,26 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
         }
     }
     __syncthreads();
+    if (J.out_members) {
+        // getVrlsPerCluster (:526-543): singletons in list order (newest
+        // first), then the heap's clusters in its vector order
+        for (int k = tid; k < ns; k += kThreads) {
+            J.out_members[k] = J.singles[ns - 1 - k];
+            J.out_moff[k + 1] = (uint32_t)(k + 1);
+        }
+        if (tid == 0) {
+            J.out_moff[0] = 0;
+            uint32_t at = (uint32_t)ns;
+            for (int k = 0; k < nh; k++) { at += J.heap[k].end - J.heap[k].begin; J.out_moff[ns + k + 1] = at; }
+            *J.out_nclusters = (uint32_t)(ns + nh);
+        }
+        __syncthreads();
+        for (int k = 0; k < nh; k++) {
+            const CNode cn = J.heap[k];
+            const uint32_t at = J.out_moff[ns + k];
+            for (uint32_t j = cn.begin + (uint32_t)tid; j < cn.end; j += kThreads) J.out_members[at + (j - cn.begin)] = J.vrls[j];
+        }
+    }
     __syncthreads();
     pf.mark(PF_REPS);
     if (tid == 0) {
@@ -1369,6 +1393,9 @@ struct HostJob {
     uint32_t stage_refine, stage_sample;
     const uint64_t* row_off;      // optional per-row layout, see alvrl_cluster_job
     const uint32_t* row_stride;
+    uint32_t* members;            // optional getVrlsPerCluster outputs (host): ids,
+    uint32_t* moff;               //   offsets (clusters + 1) and the cluster count
+    uint32_t* nclusters;
 };
 
 // Runs every clustering job on the device (one workgroup each) and copies the
@@ -1382,14 +1409,16 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
     if (entries) *entries = 0;
     out_off[0] = 0;
     if (njobs == 0) return 0;
+    // the initial clusters partition the VRLs they list (every VRL for the
+    // per-slice jobs; the non-zero ones for clusterRefinement, :899-912)
     const uint32_t nv = init_off[ninit];
-    if (nv != nvrl) { *err = "alvrl_refine: initial clusters must cover every VRL exactly once"; return 1; }
+    if (nv > nvrl) { *err = "alvrl_refine: initial clusters list more VRLs than there are"; return 1; }
     for (uint32_t i = 0; i < ninit; i++)
         if (init_off[i + 1] < init_off[i]) { *err = "alvrl_refine: init_off not monotone"; return 1; }
     {
         std::vector<unsigned char> seen(nvrl, 0);
         for (uint32_t i = 0; i < nv; i++) {
-            if (init_vrls[i] >= nvrl || seen[init_vrls[i]]) { *err = "alvrl_refine: initial clusters are not a partition of the VRLs"; return 1; }
+            if (init_vrls[i] >= nvrl || seen[init_vrls[i]]) { *err = "alvrl_refine: initial clusters are not disjoint"; return 1; }
             seen[init_vrls[i]] = 1;
         }
     }
@@ -1401,16 +1430,17 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
         row_off[j] = rows_total;
         rows_total += jobs[j].nrows;
     }
-    auto job_bytes = [&](uint32_t R) {
+    auto job_bytes = [&](const HostJob& H) {
+        const uint32_t R = H.nrows;
         return align_up(N * 4) * 2 + align_up(N * sizeof(CNode)) * 2 + align_up(N * 4) * 2 +
                align_up((size_t)R * 4) + align_up(N * 8) * 2 + align_up(N * 4) * 4 +
                align_up((size_t)6 * R * 8) + align_up((size_t)2 * 2 * kCH * ((R + 63) / 64) * 64 * 16) +
-               align_up(N * 4) * 2 + align_up(16);
+               align_up(N * 4) * 2 + align_up(16) + (H.members ? align_up(N * 4) + align_up((N + 1) * 4) + align_up(4) : 0);
     };
     size_t total = align_up(rows_total * 8) + align_up(rows_total * 4) + align_up(rows_total * 8) + align_up((size_t)nv * 4) +
                    align_up((size_t)(ninit + 1) * 4) + align_up((size_t)njobs * sizeof(JobDev)) +
                    align_up((size_t)njobs * 12) + 2 * align_up((size_t)njobs * N * 4) + align_up(8);
-    for (uint32_t j = 0; j < njobs; j++) { job_off[j] = total; total += job_bytes(jobs[j].nrows); }
+    for (uint32_t j = 0; j < njobs; j++) { job_off[j] = total; total += job_bytes(jobs[j]); }
     char* arena = nullptr;
     hipError_t e = hipMalloc(&arena, total);
     if (e != hipSuccess) { *err = std::string("alvrl_refine: hipMalloc: ") + hipGetErrorString(e); return 4; }
@@ -1479,6 +1509,13 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
         J.out_n = (uint32_t*)p;
         J.out_refined = (int*)(p + 4);
         J.out_err = (int*)(p + 8);
+        p += align_up(16);
+        J.out_members = J.out_moff = J.out_nclusters = nullptr;
+        if (H.members) {
+            J.out_members = (uint32_t*)p; p += align_up(N * 4);
+            J.out_moff = (uint32_t*)p; p += align_up((N + 1) * 4);
+            J.out_nclusters = (uint32_t*)p;
+        }
     }
     Common cm;
     cm.Rt = reinterpret_cast<const float2*>(d_Rt); cm.ld = ld; cm.nvrl = nvrl;
@@ -1552,6 +1589,16 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
             if (e == hipSuccess) e = hipMemcpyAsync(out_w, d_pw, (size_t)off * 4, hipMemcpyDeviceToHost, s);
         }
         if (e == hipSuccess) e = hipStreamSynchronize(s);
+        for (uint32_t j = 0; j < njobs && e == hipSuccess; j++) {
+            if (!jobs[j].members) continue;
+            uint32_t nc = 0;
+            e = hipMemcpy(&nc, h_jobs[j].out_nclusters, 4, hipMemcpyDeviceToHost);
+            if (e != hipSuccess) break;
+            if (nc > nv) { rc = 5; *err = "alvrl_refine: corrupt cluster count"; break; }
+            *jobs[j].nclusters = nc;
+            e = hipMemcpy(jobs[j].moff, h_jobs[j].out_moff, (size_t)(nc + 1) * 4, hipMemcpyDeviceToHost);
+            if (e == hipSuccess && nv) e = hipMemcpy(jobs[j].members, h_jobs[j].out_members, (size_t)nv * 4, hipMemcpyDeviceToHost);
+        }
         if (e == hipSuccess && ms) e = hipEventElapsedTime(ms, e0, e1);
     }
     if (e != hipSuccess) { rc = 3; *err = std::string("alvrl_refine: ") + hipGetErrorString(e); }

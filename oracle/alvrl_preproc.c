@@ -628,6 +628,43 @@ static uint32_t sample_reps(clustering_t *C, uint32_t stage, uint32_t *reps, flo
     return i;
 }
 
+/* Clustering::getVrlsPerCluster, Preprocessor.cpp:526-543: singletons in
+ * std::list order (push_front, so newest first), then the heap's clusters in
+ * its underlying vector order.  out_vrls gets C->nv ids, out_off the
+ * (clusters + 1) offsets; returns the cluster count. */
+static uint32_t vrls_per_cluster(const clustering_t *C, uint32_t *out_vrls, uint32_t *out_off)
+{
+    uint32_t c = 0, at = 0;
+    out_off[0] = 0;
+    for (long k = C->singles.n - 1; k >= 0; k--) { out_vrls[at++] = C->singles.v[k]; out_off[++c] = at; }
+    for (long k = 0; k < C->pq.n; k++) {
+        const cnode *cn = &C->pq.v[k];
+        for (uint32_t j = cn->begin; j < cn->end; j++) out_vrls[at++] = C->vrls[j];
+        out_off[++c] = at;
+    }
+    return c;
+}
+
+int alvrl_o_cluster_members(const float *Rt, uint64_t ld, const uint32_t *rows, uint32_t nrows,
+                            const double *locw, uint32_t nvrl,
+                            const uint32_t *init_vrls, const uint32_t *init_off, uint32_t ninit,
+                            float pixelUndersampling, float undersampling, uint32_t seed, uint32_t pass,
+                            uint32_t stage_refine, uint32_t *out_vrls, uint32_t *out_off,
+                            uint32_t *nclusters, int *refined)
+{
+    mat_t M = { Rt, ld, rows, nrows, nvrl };
+    clustering_t C;
+    int rc = clustering_init(&C, &M, locw, init_vrls, init_off, ninit, pixelUndersampling, 1.0f,
+                             seed, pass, stage_refine);
+    if (rc) { clustering_free(&C); return -1; }
+    int ok = refine(&C, undersampling);
+    if (refined) *refined = ok;
+    *nclusters = vrls_per_cluster(&C, out_vrls, out_off);
+    int err = C.err;
+    clustering_free(&C);
+    return err ? -2 : 0;
+}
+
 int alvrl_o_cluster_refine(const float *Rt, uint64_t ld, const uint32_t *rows, uint32_t nrows,
                            const double *locw, uint32_t nvrl,
                            const uint32_t *init_vrls, const uint32_t *init_off, uint32_t ninit,
@@ -1046,8 +1083,10 @@ uint32_t alvrl_o_prep_local_rows(const alvrl_o_prep *P, uint32_t slice, uint32_t
     return local_matrix(P, slice, rows, w);
 }
 
-/* cluster() (Preprocessor.cpp:838-898) with globalCluster=false, then
- * buildClusters (:133-197) + refinePerSlice (:199-252) + refineSlice (:254-283).
+/* cluster() (Preprocessor.cpp:838-898; with globalCluster, clusterRefinement
+ * :899-912 refines the non-zero VRLs over all rows and its clusters become
+ * the initial clusters), then buildClusters (:133-197) + refinePerSlice
+ * (:199-252) + refineSlice (:254-283).
  * Rt is [nvrl][rows_total] (mean,var) pairs, rows in slice-major order.
  * Outputs: per-slice CSR (slice_off[ns+1], reps, weights), fallback list. */
 int alvrl_o_prep_build_clusters(alvrl_o_prep *P, const float *Rt, uint32_t nvrl,
@@ -1062,7 +1101,7 @@ int alvrl_o_prep_build_clusters(alvrl_o_prep *P, const float *Rt, uint32_t nvrl,
     uint32_t *all_rows = (uint32_t *)malloc(sizeof(uint32_t) * (rows_total + 1));
     for (uint32_t r = 0; r < rows_total; r++) all_rows[r] = r;
     uint32_t *init = (uint32_t *)malloc(sizeof(uint32_t) * (nvrl + 1));
-    uint32_t init_off[3] = { 0, 0, 0 }, ninit = 0;
+    uint32_t *init_off = (uint32_t *)calloc(nvrl + 2, sizeof(uint32_t)), ninit = 0;
     uint32_t nz = 0;
     for (uint32_t v = 0; v < nvrl; v++) {
         float sum = 0;
@@ -1070,18 +1109,33 @@ int alvrl_o_prep_build_clusters(alvrl_o_prep *P, const float *Rt, uint32_t nvrl,
         if (sum != 0) init[nz++] = v;
     }
     uint32_t nzero = 0;
-    if (P->prm.global_cluster) { free(all_rows); free(init); return -10; }   /* not restated */
-    if (nz) { init_off[1] = nz; ninit = 1; }
+    double *dw = (double *)malloc(sizeof(double) * (rows_total + 1));
+    for (uint32_t r = 0; r < rows_total; r++) dw[r] = 1.0 / (double)rows_total;
+    int rc = 0;
+    if (nz && P->prm.global_cluster) {
+        /* clusterRefinement (:899-912): all non-zero VRLs in one cluster over
+         * Rflat, refined with globalUndersampling; getVrlsPerCluster */
+        uint32_t one[2] = { 0, nz }, nc = 0;
+        uint32_t *members = (uint32_t *)malloc(sizeof(uint32_t) * (nz + 1));
+        int ok = 0;
+        if (alvrl_o_cluster_members(Rt, ld, all_rows, rows_total, dw, nvrl, init, one, 1,
+                                    P->global_under, P->prm.global_undersampling, P->prm.seed,
+                                    P->prm.pass, ALVRL_O_STAGE_GLOBAL_REFINE, members, init_off,
+                                    &nc, &ok) || !ok)
+            rc = -7;   /* "Couldn't refine global clustering!" */
+        memcpy(init, members, sizeof(uint32_t) * nz);
+        free(members);
+        ninit = nc;
+    } else if (nz) {
+        init_off[1] = nz; ninit = 1;
+    }
     for (uint32_t v = 0; v < nvrl; v++) {
         float sum = 0;
         for (uint32_t r = 0; r < rows_total; r++) sum += Rt[2 * ((uint64_t)v * ld + r)];
         if (sum == 0) init[nz + nzero++] = v;
     }
     if (nzero) { init_off[ninit + 1] = nz + nzero; ninit++; }
-    double *dw = (double *)malloc(sizeof(double) * (rows_total + 1));
-    for (uint32_t r = 0; r < rows_total; r++) dw[r] = 1.0 / (double)rows_total;
-    int rc = 0;
-    {
+    if (!rc) {
         mat_t M = { Rt, ld, all_rows, rows_total, nvrl };
         clustering_t C;
         if (clustering_init(&C, &M, dw, init, init_off, ninit, P->global_under, 1.0f,
@@ -1094,7 +1148,7 @@ int alvrl_o_prep_build_clusters(alvrl_o_prep *P, const float *Rt, uint32_t nvrl,
         if (C.err) rc = rc ? rc : -4;
         clustering_free(&C);
     }
-    if (rc) { free(all_rows); free(init); free(dw); return rc; }
+    if (rc) { free(all_rows); free(init); free(init_off); free(dw); return rc; }
     /* ---- refinePerSlice ---- */
     uint32_t *rows = all_rows;
     double *w = dw;
@@ -1120,6 +1174,6 @@ int alvrl_o_prep_build_clusters(alvrl_o_prep *P, const float *Rt, uint32_t nvrl,
         out += got;
     }
     slice_off[ns] = out;
-    free(all_rows); free(init); free(dw);
+    free(all_rows); free(init); free(init_off); free(dw);
     return rc;
 }

@@ -18,6 +18,7 @@ extern "C" {
 #define ALVRL_O_STAGE_FALLBACK_SAMPLE  2u
 #define ALVRL_O_STAGE_SLICE_REFINE(s)  (3u + 2u * (uint32_t)(s))
 #define ALVRL_O_STAGE_SLICE_SAMPLE(s)  (4u + 2u * (uint32_t)(s))
+#define ALVRL_O_STAGE_GLOBAL_REFINE    0xFFFFFFFEu   /* clusterRefinement (globalCluster) */
 
 /* Preprocessor ctor arguments (Preprocessor.cpp:20-39, vrlIntegrator.cpp:158-197). */
 typedef struct {
@@ -57,6 +58,15 @@ int alvrl_o_cluster_refine(const float *Rt, uint64_t ld, const uint32_t *rows, u
                            int do_refine, uint32_t seed, uint32_t pass, uint32_t stage_refine,
                            uint32_t stage_sample, uint32_t *reps, float *weights, uint32_t *nreps,
                            int *refined);
+
+/* ctor + refine(undersampling) + getVrlsPerCluster (Preprocessor.cpp:526-543):
+ * out_vrls (init_off[ninit] ids) and out_off (clusters + 1), depthCorrection 1. */
+int alvrl_o_cluster_members(const float *Rt, uint64_t ld, const uint32_t *rows, uint32_t nrows,
+                            const double *locw, uint32_t nvrl,
+                            const uint32_t *init_vrls, const uint32_t *init_off, uint32_t ninit,
+                            float pixel_undersampling, float undersampling, uint32_t seed, uint32_t pass,
+                            uint32_t stage_refine, uint32_t *out_vrls, uint32_t *out_off,
+                            uint32_t *nclusters, int *refined);
 
 #ifdef __cplusplus
 }

@@ -103,6 +103,9 @@ class Oracle:
         L.alvrl_o_prep_local_rows.restype = u32
         L.alvrl_o_prep_build_clusters.argtypes = [C.c_void_p, P(f32), u32, P(u32), P(u32), P(f32),
                                                   u32, P(u32), P(f32), P(u32), P(u32), P(f32), P(u32)]
+        L.alvrl_o_cluster_members.argtypes = [P(f32), u64, P(u32), u32, P(C.c_double), u32, P(u32),
+                                              P(u32), u32, f32, f32, u32, u32, u32, P(u32), P(u32),
+                                              P(u32), P(C.c_int)]
         L.alvrl_o_cluster_refine.argtypes = [P(f32), u64, P(u32), u32, P(C.c_double), u32, P(u32),
                                              P(u32), u32, f32, f32, f32, i32, u32, u32, u32, u32,
                                              P(u32), P(f32), P(u32), P(i32)]
@@ -241,6 +244,27 @@ class Oracle:
         if rc != 0:
             raise RuntimeError(f"oracle cluster_refine failed rc={rc}")
         return reps[:nr.value].copy(), w[:nr.value].copy(), bool(refined.value)
+
+    def cluster_members(self, Rt, rows, locw, init_vrls, init_off, pixel_undersampling,
+                        undersampling, seed=0xA1B2C3D4, pass_=0, stage_refine=0xFFFFFFFE):
+        """ctor + refine + getVrlsPerCluster (Preprocessor.cpp:526-543):
+        (vrls, offsets, refined)."""
+        Rt = np.ascontiguousarray(Rt, np.float32)
+        nv, ld = Rt.shape[0], Rt.shape[1]
+        rows = np.ascontiguousarray(rows, np.uint32)
+        locw = np.ascontiguousarray(locw, np.float64)
+        iv = np.ascontiguousarray(init_vrls, np.uint32)
+        io = np.ascontiguousarray(init_off, np.uint32)
+        out = np.zeros(len(iv) + 1, np.uint32); off = np.zeros(len(iv) + 2, np.uint32)
+        nc = C.c_uint32(); refined = C.c_int()
+        rc = self.lib.alvrl_o_cluster_members(
+            _p(Rt), ld, _p(rows, C.c_uint32), len(rows), _p(locw, C.c_double), nv,
+            _p(iv, C.c_uint32), _p(io, C.c_uint32), len(io) - 1, pixel_undersampling,
+            undersampling, seed, pass_, stage_refine, _p(out, C.c_uint32), _p(off, C.c_uint32),
+            C.byref(nc), C.byref(refined))
+        if rc != 0:
+            raise RuntimeError(f"oracle cluster_members failed rc={rc}")
+        return out[:len(iv)].copy(), off[:nc.value + 1].copy(), bool(refined.value)
 
 
 class Prep:

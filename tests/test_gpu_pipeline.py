@@ -84,6 +84,8 @@ def test_c1_pipeline_adaptive(oracle, gpu_ok):
     ("localUndersampling=20", {}),
     ("neighbourCount=3;neighbourWeight=0.5", {"neighbour_count": 3, "neighbour_weight": 0.5}),
     ("localRefinement=false;globalCluster=false", None),
+    ("globalCluster=true;globalUndersampling=20", {"global_cluster": True, "global_undersampling": 20.0}),
+    ("globalCluster=true;targetNumSlices=40", {"global_cluster": True, "target_num_slices": 40}),
 ])
 def test_pipeline_variants(oracle, gpu_ok, props, prep_kw):
     import alvrl
@@ -110,6 +112,8 @@ def test_pipeline_variants(oracle, gpu_ok, props, prep_kw):
     it, img, prep, vrls, pc, p2s = _run(props, w, h, 600, oracle, prep_kw=pk)
     ocl = prep.build_clusters(it.R())
     icl = it.clusters()
+    if pk.get("global_cluster"):
+        assert it.stats()["global_clusters"] > 1
     assert np.array_equal(ocl["reps"], icl["reps"])
     assert np.array_equal(ocl["weights"].view(np.uint32), icl["weights"].view(np.uint32))
 
@@ -213,11 +217,44 @@ def test_sharded_prepass(gpu_ok, tmp_path):
     v = json.loads(out.read_text())
     print(v)
     assert v["world"] == 2
-    for name in ("adaptive", "neighbours", "fixed"):
+    for name in ("adaptive", "neighbours", "fixed", "global"):
         c = v[name]
         assert c["clusters_identical_all_ranks"] and c["frame_bit_exact"], name
         assert c["slices_sum"] == c["slices"], name
-        if name != "neighbours":
-            assert c["pairs_sum"] == c["pairs_one"] and c["rows_sum"] == c["rows"], name
-        else:
+        if name == "neighbours":
             assert c["rows_sum"] >= c["rows"], name
+        elif name == "global":     # the global refinement needs every row on every rank
+            assert c["rows_sum"] == 2 * c["rows"], name
+        else:
+            assert c["pairs_sum"] == c["pairs_one"] and c["rows_sum"] == c["rows"], name
+
+
+@pytest.mark.parametrize("gu", [15.0, -1.0])
+def test_refine_members(oracle, gpu_ok, gu):
+    """alvrl_refine_members (clusterRefinement + getVrlsPerCluster) against the
+    oracle on the same R: identical member order and cluster offsets."""
+    import torch
+    import alvrl
+    w, h = 96, 64
+    scene = alvrl.scene_default(w, h)
+    vrls, pc = alvrl.trace_vrls(scene, 500, seed=SEED_VRL)
+    rows = np.arange(0, w * h, 37, dtype=np.uint32)
+    recs = alvrl.scene_records(scene, rows)
+    ctx = alvrl.Context(device=0, seed=SEED_RNG)
+    ctx.set_medium(alvrl.Medium())
+    ctx.upload_vrls(vrls, pc)
+    nv = vrls.shape[1]
+    d_Rt = torch.zeros((nv, len(rows), 2), dtype=torch.float32, device="cuda")
+    ctx.build_R(torch.from_numpy(recs).cuda(), d_Rt, ld=len(rows),
+                d_ids=torch.from_numpy(rows.view(np.int32)).cuda())
+    torch.cuda.synchronize()
+    Rt = d_Rt.cpu().numpy()
+    nz = np.nonzero((Rt[..., 0] != 0).any(axis=1))[0].astype(np.uint32)
+    lrows = np.arange(len(rows), dtype=np.uint32)
+    locw = np.full(len(rows), 1.0 / len(rows))
+    job = dict(rows=lrows, locw=locw, pixel_undersampling=0.25, undersampling=gu)
+    mem, off, ok = ctx.refine_members(d_Rt, len(rows), job, nz, [0, len(nz)])
+    omem, ooff, ook = oracle.cluster_members(Rt, lrows, locw, nz, [0, len(nz)], 0.25, gu)
+    assert ok and ook
+    print(f"global clusters: {len(off) - 1} (device) {len(ooff) - 1} (oracle)")
+    assert np.array_equal(off, ooff) and np.array_equal(mem, omem)

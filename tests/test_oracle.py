@@ -209,3 +209,43 @@ def test_golden_c1_small(oracle):
     assert (g["brute"] > 0).all() and len(g["cl_reps"]) > mg.NSLICES
 
 
+
+
+@pytest.mark.parametrize("gu", [10.0, -1.0])
+def test_oracle_global_cluster(oracle, gu):
+    """globalCluster=true (clusterRefinement, Preprocessor.cpp:899-912): the
+    refinement of the non-zero VRLs over all rows gives a partition of them
+    (getVrlsPerCluster, :526-543) -- round(N / globalUndersampling) clusters
+    in fixed-depth mode -- and the per-slice refinement starting from those
+    clusters completes."""
+    from oracle import Prep
+    mg = _make_golden()
+    vrls = mg.read_vrl_ascii(os.path.join(GOLDEN, "vrls_c1.txt"))
+    pc = vrls.shape[1]
+    W, H = mg.W, mg.H
+    sc = oracle.scene(W, H)
+    recs = oracle.records(sc)
+    P = oracle.params(oracle.medium(), seed=0xA1B2C3D4)
+    kw = dict(seed=0xA1B2C3D4, pass_=0, target_num_slices=mg.NSLICES)
+    prep = Prep(oracle, oracle.prep_params(global_cluster=True, global_undersampling=gu, **kw))
+    prep.build_slices(sc)
+    off, pix, su, g_under = prep.sample_slice_mapping(64.0, W * H)
+    rep_ids = ((pix % H) * W + pix // H).astype(np.uint32)
+    _, R, _ = oracle.gather_brute(P, recs[rep_ids], vrls, pc, rec_ids=rep_ids, domain=2, want_R=True)
+    Rt = np.ascontiguousarray(R.transpose(1, 0, 2))          # [vrl][row]
+    nz = np.nonzero(Rt[..., 0].sum(axis=1, dtype=np.float32) != 0)[0].astype(np.uint32)
+    rows = np.arange(Rt.shape[1], dtype=np.uint32)
+    mem, moff, ok = oracle.cluster_members(Rt, rows, np.full(len(rows), 1.0 / len(rows)), nz,
+                                           [0, len(nz)], float(g_under), gu)
+    assert ok and moff[0] == 0 and moff[-1] == len(nz)
+    assert np.array_equal(np.sort(mem), np.sort(nz))
+    assert (np.diff(moff) > 0).all()
+    if gu > 0:
+        assert len(moff) - 1 == int(0.5 + pc / gu)
+    cl = prep.build_clusters(Rt)
+    assert cl["slice_off"][-1] == len(cl["reps"]) > mg.NSLICES
+    base = Prep(oracle, oracle.prep_params(**kw))
+    base.build_slices(sc)
+    base.sample_slice_mapping(64.0, W * H)
+    cl0 = base.build_clusters(Rt)
+    assert not np.array_equal(cl0["reps"], cl["reps"])
