@@ -138,12 +138,32 @@ ALVRL_API int alvrl_gather_brute(alvrl_ctx *ctx, const alvrl_gather_rec *d_recs,
 ALVRL_API int alvrl_gather_clustered(alvrl_ctx *ctx, const alvrl_gather_rec *d_recs,
                                      const uint32_t *d_rec_ids, const alvrl_work_item *d_items,
                                      uint32_t nitems, float *d_out_rgb, void *stream);
+/* The false-colour debug images of LiInternal (vrlIntegrator.cpp:199-201,
+ * 545-599, 794-806) for primary rays, instead of a gather:
+ *   ALVRL_FALSE_COLOR_NUM_VRLS ("numVrlFalseColor"): |slice list| / N with
+ *     d_items (clustered, :574-575), 1 without (brute, :800-801), where the
+ *     record's medium scatters, else 0;
+ *   ALVRL_FALSE_COLOR_SLICES ("slicesFalseColor", clustered only, :576-583):
+ *     the slice's hash colour, grey 0.5 for the fall-back list.
+ * n = work items (d_items != NULL) or records.  The render counter grows by
+ * the list sizes as the reference's stats do (:593-596). */
+#define ALVRL_FALSE_COLOR_NUM_VRLS 1
+#define ALVRL_FALSE_COLOR_SLICES 2
+ALVRL_API int alvrl_gather_false_color(alvrl_ctx *ctx, int mode, const alvrl_gather_rec *d_recs,
+                                       const alvrl_work_item *d_items, uint32_t n, float *d_out_rgb,
+                                       void *stream);
 /* Host helper: build work items from a slice-sorted slice-of-record array
  * (host memory).  Returns the number of items written (<= cap). */
 ALVRL_API uint32_t alvrl_make_work_items(const uint32_t *slice_of_rec_sorted, uint32_t nrec,
                                          alvrl_work_item *items, uint32_t cap);
 
 /* ---- hot path (b) part 1: reduced transport matrix R ------------------ */
+/* "Rsamples" (vrlIntegrator.cpp:194, default 1): gather samples per R entry.
+ * getLiLuminanceVrlContributions runs LiInternal with samples = Rsamples and
+ * the entries accumulate, so they are SUMS over the samples (:427-443,
+ * :812-813).  Sample i draws from stream (R domain, i). */
+ALVRL_API int alvrl_set_rsamples(alvrl_ctx *ctx, int rsamples);
+
 /* Replaces Rbuilder::run (:1053-1067) -> getLiLuminanceVrlContributions
  * (:527-539) with Rsamples = 1.  Writes (mean, var) float pairs to
  * d_Rt[2*(v*ld + row0 + r) + {0,1}] for record r of d_recs and VRL v, i.e. R

@@ -90,6 +90,8 @@ def lib() -> C.CDLL:
                                P(u32), P(f32), P(i32), vp]
     L.alvrl_last_refine_ms.argtypes = [vp, P(f32)]
     L.alvrl_last_refine_entries.argtypes = [vp, P(u64)]
+    L.alvrl_set_rsamples.argtypes = [vp, i32]
+    L.alvrl_build_R_blocks.argtypes = [vp, vp, vp, u32, vp, vp, vp, vp, vp]
     L.alvrl_refine_members.argtypes = [vp, vp, u64, P(ClusterJob), P(u32), P(u32), u32, P(u32), P(u32),
                                        P(u32), P(i32), vp]
     L.alvrl_get_stats.argtypes = [vp, P(u64), P(u64)]
@@ -211,6 +213,18 @@ class Context:
         n = d_recs.shape[0]
         _check(self.L.alvrl_build_R(self.h, _ptr(d_recs), _ptr(d_ids), n, _ptr(d_Rt), ld, row0,
                                     C.c_void_p(stream) if stream else None))
+
+    def set_rsamples(self, n: int):
+        _check(self.L.alvrl_set_rsamples(self.h, n))
+
+    def build_R_blocks(self, d_recs, d_Rt, d_row_off, d_row_stride, d_nonzero=None, d_ids=None,
+                       stream=None):
+        """Rows scattered over per-slice blocks: row r's pair for VRL v at float2
+        index row_off[r] + v * row_stride[r] (alvrl_build_R_blocks)."""
+        n = int(d_recs.shape[0])
+        _check(self.L.alvrl_build_R_blocks(self.h, _ptr(d_recs), _ptr(d_ids), n, _ptr(d_Rt),
+                                           _ptr(d_row_off), _ptr(d_row_stride), _ptr(d_nonzero),
+                                           C.c_void_p(stream) if stream else None))
 
     def refine(self, d_Rt, ld: int, jobs: list, init_vrls, init_off, stream=None):
         """jobs: list of dicts(rows, locw, pixel_undersampling, undersampling,

@@ -35,6 +35,9 @@ hipError_t launch_build_R_blocks(const Rec* recs, const uint32_t* ids, uint32_t 
                                  uint32_t nvrl, const DevParams& P, float normalization, float2* Rt,
                                  const uint64_t* roff, const uint32_t* rstride, uint8_t* nonzero,
                                  unsigned long long* counter, hipStream_t s);
+hipError_t launch_false_color(const Rec* recs, const WorkItem* items, uint32_t n, int mode,
+                              const uint32_t* slice_off, uint32_t n_fb, uint32_t nvrl, float* out,
+                              unsigned long long* counter, hipStream_t s);
 hipError_t launch_nonzero_columns(const float2* Rt, uint64_t ld, uint32_t nrows, uint32_t nvrl,
                                   uint8_t* mask, hipStream_t s);
 hipError_t launch_accumulate_rgb(const float* rgb, const uint32_t* pix, uint32_t n, float* fb,
@@ -309,6 +312,25 @@ ALVRL_API int alvrl_gather_clustered(alvrl_ctx* c, const alvrl_gather_rec* d_rec
     return ALVRL_OK;
 }
 
+ALVRL_API int alvrl_gather_false_color(alvrl_ctx* c, int mode, const alvrl_gather_rec* d_recs,
+                                       const alvrl_work_item* d_items, uint32_t n, float* d_out_rgb,
+                                       void* stream)
+{
+    int rc = check_ready(c, "alvrl_gather_false_color");
+    if (rc) return rc;
+    if (mode != ALVRL_FALSE_COLOR_NUM_VRLS && mode != ALVRL_FALSE_COLOR_SLICES)
+        return fail(ALVRL_ERR_INVALID, "alvrl_gather_false_color: bad mode");
+    if (mode == ALVRL_FALSE_COLOR_SLICES && !d_items)
+        return fail(ALVRL_ERR_INVALID, "requested slices false color image without clustering!");
+    if (d_items && !c->clusters_set) return fail(ALVRL_ERR_STATE, "alvrl_gather_false_color: no clusters set");
+    if (n && (!d_recs || !d_out_rgb)) return fail(ALVRL_ERR_INVALID, "alvrl_gather_false_color: null buffer");
+    HIPCHK(hipSetDevice(c->cfg.device));
+    hipStream_t s = pick(c, stream);
+    HIPCHK(launch_false_color(reinterpret_cast<const Rec*>(d_recs), reinterpret_cast<const WorkItem*>(d_items), n,
+                              mode, c->d_slice_off, c->n_fb, c->nvrl, d_out_rgb, c->d_counter + 1, s));
+    return ALVRL_OK;
+}
+
 ALVRL_API uint32_t alvrl_make_work_items(const uint32_t* sl, uint32_t nrec, alvrl_work_item* items,
                                          uint32_t cap)
 {
@@ -338,6 +360,15 @@ ALVRL_API int alvrl_build_R(alvrl_ctx* c, const alvrl_gather_rec* d_recs, const 
                           norm, reinterpret_cast<float2*>(d_Rt), ld, row0, c->d_counter + 0, s));
     HIPCHK(hipEventRecord(c->ev1, s));
     c->timed = true;
+    return ALVRL_OK;
+}
+
+ALVRL_API int alvrl_set_rsamples(alvrl_ctx* c, int rsamples)
+{
+    if (!c) return fail(ALVRL_ERR_INVALID, "alvrl_set_rsamples: null ctx");
+    if (rsamples < 1 || rsamples > 0xFFFFFF) return fail(ALVRL_ERR_INVALID, "Rsamples must be in [1, 2^24)");
+    std::lock_guard<std::mutex> g(c->mu);
+    c->P.rsamples = rsamples;
     return ALVRL_OK;
 }
 

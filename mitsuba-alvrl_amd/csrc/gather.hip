@@ -133,6 +133,60 @@ __global__ void __launch_bounds__(256) k_gather_clustered(
     }
 }
 
+// The debug images of LiInternal for a primary ray (weight 1): numVrlFalseColor
+// gives |list| / N (clustered, :574-575) or 1 (brute, :800-801) where the
+// medium scatters, 0 elsewhere; slicesFalseColor (clustered only) colours the
+// slice with the integer hash of :578-583 (grey for the fall-back list), also
+// outside the medium (:546).  The stats counter gets the list size, as there.
+// items == nullptr: one record per lane (brute).
+__global__ void __launch_bounds__(256) k_false_color(const Rec* __restrict__ recs,
+                                                     const WorkItem* __restrict__ items, uint32_t n,
+                                                     int mode, const uint32_t* __restrict__ slice_off,
+                                                     uint32_t n_fb, uint32_t nvrl, float* __restrict__ out,
+                                                     unsigned long long* counter)
+{
+    uint32_t r, k, slice = 0xFFFFFFFFu;
+    bool active;
+    if (items) {
+        const uint32_t item = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+        if (item >= n) return;
+        const WorkItem it = items[item];
+        const uint32_t lane = threadIdx.x & 63;
+        active = lane < it.count;
+        r = it.begin + lane;
+        slice = it.slice;
+        k = slice == 0xFFFFFFFFu ? n_fb : slice_off[slice + 1] - slice_off[slice];
+    } else {
+        r = blockIdx.x * blockDim.x + threadIdx.x;
+        active = r < n;
+        k = nvrl;
+    }
+    const bool medium = active && (__float_as_uint(reinterpret_cast<const float4*>(recs + (active ? r : 0))[3].w) & 4u);
+    float c0 = 0.0f, c1 = 0.0f, c2 = 0.0f;
+    if (mode == 1) {
+        if (medium) c0 = c1 = c2 = items ? (float)k / (float)nvrl : 1.0f;
+    } else if (slice == 0xFFFFFFFFu) {
+        c0 = c1 = c2 = 0.5f;
+    } else {
+        const uint32_t s = slice;
+        c0 = (float)((double)((s + s * s) % 43u) / 43.0);
+        c1 = (float)((double)((7u * s + 2u * s * s + 7u) % 41u) / 41.0);
+        c2 = (float)((double)((23u * s + 5u * s * s + s * s * s + 17u) % 53u) / 53.0);
+    }
+    count_pairs(counter, mode == 1 ? medium : active, k);
+    if (active) { out[3 * (size_t)r + 0] = c0; out[3 * (size_t)r + 1] = c1; out[3 * (size_t)r + 2] = c2; }
+}
+
+hipError_t launch_false_color(const Rec* recs, const WorkItem* items, uint32_t n, int mode,
+                              const uint32_t* slice_off, uint32_t n_fb, uint32_t nvrl, float* out,
+                              unsigned long long* counter, hipStream_t s)
+{
+    if (n == 0) return hipSuccess;
+    const dim3 grid(items ? (n + 3) / 4 : (n + 255) / 256), block(256);
+    hipLaunchKernelGGL(k_false_color, grid, block, 0, s, recs, items, n, mode, slice_off, n_fb, nvrl, out, counter);
+    return hipGetLastError();
+}
+
 // R build: lane = representative row, the block's 4 waves interleave over a
 // VRL chunk.  Writes Rt[v][row0 + r] = (mean * norm, var * norm * norm).
 template <int NVV, int NVS>
@@ -151,20 +205,32 @@ __global__ void __launch_bounds__(256) k_build_R(const Rec* __restrict__ recs,
     const uint32_t rid = active ? (ids ? ids[r] : r) : 0u;
     const uint32_t v0 = blockIdx.y * chunk;
     const uint32_t v1 = min(nvrl, v0 + chunk);
+    const int nsamp = P.rsamples > 1 ? P.rsamples : 1;
     uint32_t done = 0;
     for (uint32_t v = v0 + wave; v < v1; v += 4) {
         float mean = 0.0f, var = 0.0f;
         if (q.medium) {
             const VrlPrep V = vp[v];
             float c[3];
-            integrate_vrl<NVV, NVS, true>(P, q, V, rid, v, kDomRbuild, P.nvv, P.nvs, c, &mean, &var);
-            mean = mean * normalization;
-            var = var * normalization * normalization;
+            if (nsamp == 1) {
+                integrate_vrl<NVV, NVS, true>(P, q, V, rid, v, kDomRbuild, P.nvv, P.nvs, c, &mean, &var);
+                mean = mean * normalization;
+                var = var * normalization * normalization;
+            } else {
+                // LiInternal's samples loop: entries are sums over the samples (:812-813)
+                for (int si = 0; si < nsamp; si++) {
+                    float m, s2;
+                    integrate_vrl<NVV, NVS, true>(P, q, V, rid, v, kDomRbuild, P.nvv, P.nvs, c, &m, &s2,
+                                                  (uint32_t)si);
+                    mean += m * normalization;
+                    var += s2 * normalization * normalization;
+                }
+            }
         }
         if (active) Rt[(size_t)v * ld + row0 + r] = make_float2(mean, var);
         ++done;
     }
-    count_pairs(counter, active && q.medium, done);
+    count_pairs(counter, active && q.medium, done * (uint32_t)nsamp);
 }
 
 // The same over per-slice blocks: row r of the launch lives at float2 index
@@ -193,21 +259,33 @@ __global__ void __launch_bounds__(256) k_build_R_blocks(const Rec* __restrict__ 
     const uint64_t stride = active ? rstride[r] : 0;
     const uint32_t v0 = blockIdx.y * chunk;
     const uint32_t v1 = min(nvrl, v0 + chunk);
+    const int nsamp = P.rsamples > 1 ? P.rsamples : 1;
     uint32_t done = 0;
     for (uint32_t v = v0 + wave; v < v1; v += 4) {
         float mean = 0.0f, var = 0.0f;
         if (q.medium) {
             const VrlPrep V = vp[v];
             float c[3];
-            integrate_vrl<NVV, NVS, true>(P, q, V, rid, v, kDomRbuild, P.nvv, P.nvs, c, &mean, &var);
-            mean = mean * normalization;
-            var = var * normalization * normalization;
+            if (nsamp == 1) {
+                integrate_vrl<NVV, NVS, true>(P, q, V, rid, v, kDomRbuild, P.nvv, P.nvs, c, &mean, &var);
+                mean = mean * normalization;
+                var = var * normalization * normalization;
+            } else {
+                // LiInternal's samples loop: entries are sums over the samples (:812-813)
+                for (int si = 0; si < nsamp; si++) {
+                    float m, s2;
+                    integrate_vrl<NVV, NVS, true>(P, q, V, rid, v, kDomRbuild, P.nvv, P.nvs, c, &m, &s2,
+                                                  (uint32_t)si);
+                    mean += m * normalization;
+                    var += s2 * normalization * normalization;
+                }
+            }
         }
         if (active) Rt[base + (uint64_t)v * stride] = make_float2(mean, var);
         if (nonzero && __ballot(active && mean != 0.0f) && (threadIdx.x & 63) == 0) nonzero[v] = 1;
         ++done;
     }
-    count_pairs(counter, active && q.medium, done);
+    count_pairs(counter, active && q.medium, done * (uint32_t)nsamp);
 }
 
 // Preprocessor::cluster's totalVrlContribution != 0 (means are >= 0): one

@@ -196,9 +196,7 @@ struct alvrl_integrator {
         if (volSurfSamples != 0 && volSurfSamples < 2)
             throw IntegError(ALVRL_ERR_INVALID, "Need at least 2 volSurfSamples for variance estimate, but received: " + std::to_string(volSurfSamples));
         if (targetNumSlices < 1) throw IntegError(ALVRL_ERR_INVALID, "Invalid target number of slices!");
-        if (Rsamples != 1) throw IntegError(ALVRL_ERR_INVALID, "Rsamples != 1 is not supported by this build");
-        if (numVrlFalseColor || slicesFalseColor || convergenceFalseColor)
-            throw IntegError(ALVRL_ERR_INVALID, "false-colour debug modes are not supported by this build yet");
+        if (Rsamples < 1) throw IntegError(ALVRL_ERR_INVALID, "Rsamples must be >= 1");
         clustered = globalCluster || localRefinement;
     }
 
@@ -588,7 +586,17 @@ struct alvrl_integrator {
         if (world == 0 || rank >= world) throw IntegError(ALVRL_ERR_INVALID, "bad rank/world");
         prepare_render(rank, world);
         // the caller's stream waits for the records upload (done, synchronous above)
-        if (clustered)
+        // false colour (LiInternal, :427-443, 545-599, 794-806): numVrlFalseColor
+        // wins over slicesFalseColor; convergenceFalseColor only rewrites the
+        // result after a specular (delta-BSDF) chain (:514-521), which the
+        // smoke box's diffuse walls never start, so it leaves the image as is
+        if (numVrlFalseColor || slicesFalseColor) {
+            if (!clustered && !numVrlFalseColor)
+                throw IntegError(ALVRL_ERR_INVALID, "requested slices false color image without clustering!");
+            const int mode = numVrlFalseColor ? ALVRL_FALSE_COLOR_NUM_VRLS : ALVRL_FALSE_COLOR_SLICES;
+            chk(alvrl_gather_false_color(ctx, mode, rec_buf.p, clustered ? item_buf.p : nullptr,
+                                         clustered ? nitems : nrec, out_buf.p, s), "alvrl_gather_false_color");
+        } else if (clustered)
             chk(alvrl_gather_clustered(ctx, rec_buf.p, pix_buf.p, item_buf.p, nitems, out_buf.p, s), "alvrl_gather_clustered");
         else
             chk(alvrl_gather_brute(ctx, rec_buf.p, pix_buf.p, nrec, out_buf.p, s), "alvrl_gather_brute");
@@ -637,6 +645,7 @@ ALVRL_API int alvrl_integrator_create(const char* props, int device, alvrl_integ
         it->device = device;
         alvrl_config cfg{device, it->volVolSamples, it->volSurfSamples, it->shortVrls ? 1 : 0, it->seed};
         chk(alvrl_ctx_create(&cfg, &it->ctx), "alvrl_ctx_create");
+        chk(alvrl_set_rsamples(it->ctx, it->Rsamples), "alvrl_set_rsamples");
         hchk(hipSetDevice(device), "hipSetDevice");
         hchk(hipStreamCreateWithFlags(&it->stream, hipStreamNonBlocking), "hipStreamCreate");
     });

@@ -51,6 +51,7 @@ struct DevParams {
     int nvv, nvs;
     int short_vrls;
     uint32_t seed, pass;
+    int rsamples;           // Rsamples (vrlIntegrator.cpp:194): samples per R entry (0 = 1)
 };
 
 // ---------------------------------------------------------------- RNG --
@@ -362,7 +363,7 @@ template <int NVV, int NVS, bool WANT_STATS>
 __device__ __forceinline__ void integrate_vrl(const DevParams& P, const RecPre& q, const VrlPrep& v,
                                               uint32_t rec_id, uint32_t vrl_id, uint32_t domain,
                                               int nvv_rt, int nvs_rt, float out[3], float* mean_out,
-                                              float* var_out)
+                                              float* var_out, uint32_t rsub = 0u)
 {
     const int nVV = NVV >= 0 ? NVV : nvv_rt;
     const int nVS = NVS >= 0 ? NVS : nvs_rt;
@@ -371,7 +372,7 @@ __device__ __forceinline__ void integrate_vrl(const DevParams& P, const RecPre& 
     float tot0 = 0.0f, tot1 = 0.0f, tot2 = 0.0f;
     float mean = 0.0f, M2 = 0.0f, mean_acc = 0.0f, var_acc = 0.0f;
     const uint32_t k0 = P.seed, k1 = P.pass;
-    const uint32_t c3 = domain << 24;
+    const uint32_t c3 = (domain << 24) | (rsub & 0xFFFFFFu);   // rsub: R sample index
 
     // draws 0..3: volVol samples 0,1 (V, U); draws 4..7: volSurf / further volVol
     U4 rb = philox4x32_10(rec_id, vrl_id, 0u, c3, k0, k1);

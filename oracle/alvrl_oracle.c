@@ -325,9 +325,11 @@ void alvrl_o_medium_eval(const alvrl_o_medium *m, float distance, float tr[3], f
 /* ===================================================================== */
 /*  integrateVRL, vrlIntegrator.cpp:603-785                                */
 /* ===================================================================== */
-void alvrl_o_integrate_vrl(const alvrl_o_params *P, const float *rec, uint32_t rec_id,
-                           const float *vs, uint32_t nvrl, uint32_t vrl_id,
-                           uint32_t domain, float out_rgb[3], float *contrib, float *variance)
+/* 'rsub' is the low 24 bits of the stream word: the sample index of an R
+ * entry with Rsamples > 1 (LiInternal's samples loop, vrlIntegrator.cpp:427-443). */
+static void integrate_vrl_s(const alvrl_o_params *P, const float *rec, uint32_t rec_id,
+                            const float *vs, uint32_t nvrl, uint32_t vrl_id, uint32_t domain,
+                            uint32_t rsub, float out_rgb[3], float *contrib, float *variance)
 {
     const alvrl_o_medium *m = &P->medium;
     uint32_t flags;
@@ -354,8 +356,8 @@ void alvrl_o_integrate_vrl(const alvrl_o_params *P, const float *rec, uint32_t r
     float mean = 0, M2 = 0;
     for (int sample = 0; sample < nVV; sample++) {
         float lumv = 0.0f;
-        float u0 = draw(P->seed, P->pass, domain, rec_id, vrl_id, 0, 2 * sample);
-        float u1 = draw(P->seed, P->pass, domain, rec_id, vrl_id, 0, 2 * sample + 1);
+        float u0 = draw(P->seed, P->pass, domain, rec_id, vrl_id, rsub, 2 * sample);
+        float u1 = draw(P->seed, P->pass, domain, rec_id, vrl_id, rsub, 2 * sample + 1);
         v3 V, U;
         float pdf = sample_v_to_distance(E, dray, Usurf, S, End, &V, u0);
         pdf *= kulla(A, B, V, &U, u1);
@@ -415,7 +417,7 @@ void alvrl_o_integrate_vrl(const alvrl_o_params *P, const float *rec, uint32_t r
     for (int sample = 0; sample < nVS; sample++) {
         float lumv = 0.0f;
         if (do_surf) {
-            float u = draw(P->seed, P->pass, domain, rec_id, vrl_id, 0, 2 * nVV + sample);
+            float u = draw(P->seed, P->pass, domain, rec_id, vrl_id, rsub, 2 * nVV + sample);
             v3 V;
             float pdf = kulla(S, End, U, &V, u);
             if (dist(U, V) != 0) {
@@ -467,6 +469,13 @@ void alvrl_o_integrate_vrl(const alvrl_o_params *P, const float *rec, uint32_t r
 /* ===================================================================== */
 /*  Gathers                                                                */
 /* ===================================================================== */
+void alvrl_o_integrate_vrl(const alvrl_o_params *P, const float *rec, uint32_t rec_id,
+                           const float *vs, uint32_t nvrl, uint32_t vrl_id,
+                           uint32_t domain, float out_rgb[3], float *contrib, float *variance)
+{
+    integrate_vrl_s(P, rec, rec_id, vs, nvrl, vrl_id, domain, 0u, out_rgb, contrib, variance);
+}
+
 typedef struct {
     const alvrl_o_params *P;
     const float *recs; uint32_t nrec; const uint32_t *rec_ids;
@@ -490,20 +499,27 @@ static void *brute_worker(void *arg)
         memcpy(&flags, &rec[15], 4);
         float Li[3] = { 0, 0, 0 };
         uint32_t rid = j->rec_ids ? j->rec_ids[r] : r;
+        /* R rows: LiInternal with samples = Rsamples; the entries are sums
+         * over the samples (:812-813), the radiance their mean (:445) */
+        const uint32_t ns = (j->R && j->P->r_samples > 1) ? (uint32_t)j->P->r_samples : 1u;
         if (flags & ALVRL_O_FLAG_MEDIUM) {
-            for (uint32_t v = 0; v < j->nvrl; v++) {
-                float c[3], contribution, variance;
-                alvrl_o_integrate_vrl(j->P, rec, rid, j->vs, j->nvrl, v, j->domain, c,
-                                      &contribution, &variance);
-                for (int i = 0; i < 3; i++) c[i] *= normalization;
-                if (j->R) {
-                    float *e = j->R + 2 * ((size_t)r * j->nvrl + v);
-                    e[0] += contribution * normalization;
-                    e[1] += variance * normalization * normalization;
+            for (uint32_t s = 0; s < ns; s++) {
+                for (uint32_t v = 0; v < j->nvrl; v++) {
+                    float c[3], contribution, variance;
+                    integrate_vrl_s(j->P, rec, rid, j->vs, j->nvrl, v, j->domain, s, c,
+                                    &contribution, &variance);
+                    for (int i = 0; i < 3; i++) c[i] *= normalization;
+                    if (j->R) {
+                        float *e = j->R + 2 * ((size_t)r * j->nvrl + v);
+                        e[0] += contribution * normalization;
+                        e[1] += variance * normalization * normalization;
+                    }
+                    for (int i = 0; i < 3; i++) Li[i] += c[i];
                 }
-                for (int i = 0; i < 3; i++) Li[i] += c[i];
+                j->count += j->nvrl;
             }
-            j->count += j->nvrl;
+            if (ns > 1)
+                for (int i = 0; i < 3; i++) Li[i] /= (float)ns;
         }
         for (int i = 0; i < 3; i++) j->out[3 * (size_t)r + i] = Li[i];
     }

@@ -80,6 +80,7 @@ typedef struct {
     int short_vrls;          /* shortVrls,      vrlIntegrator.cpp:135 */
     uint32_t seed;
     uint32_t pass;
+    int r_samples;           /* Rsamples (vrlIntegrator.cpp:194): samples per R entry, 0/1 = one */
 } alvrl_o_params;
 
 /* Gather record ("eye segment"): 16 x 32-bit words.

@@ -35,7 +35,8 @@ class Medium(C.Structure):
 
 class Params(C.Structure):
     _fields_ = [("medium", Medium), ("vol_vol_samples", C.c_int), ("vol_surf_samples", C.c_int),
-                ("short_vrls", C.c_int), ("seed", C.c_uint32), ("pass_", C.c_uint32)]
+                ("short_vrls", C.c_int), ("seed", C.c_uint32), ("pass_", C.c_uint32),
+                ("r_samples", C.c_int)]
 
 
 class Scene(C.Structure):
@@ -153,8 +154,9 @@ class Oracle:
         self.lib.alvrl_o_medium_init(C.byref(m), ss, sa, weight, phase_type, g)
         return m
 
-    def params(self, medium: Medium, nvv=2, nvs=2, short_vrls=1, seed=0xA1B2C3D4, pass_=0) -> Params:
-        return Params(medium, nvv, nvs, short_vrls, seed, pass_)
+    def params(self, medium: Medium, nvv=2, nvs=2, short_vrls=1, seed=0xA1B2C3D4, pass_=0,
+               r_samples=1) -> Params:
+        return Params(medium, nvv, nvs, short_vrls, seed, pass_, r_samples)
 
     def records(self, scene: Scene, medium_scatters: bool = True) -> np.ndarray:
         out = np.zeros((scene.width * scene.height, REC_WORDS), np.float32)

@@ -186,6 +186,47 @@ def test_build_R_parity(oracle, gpu_ok):
     _assert_close_pairs(Rg[..., 1], Rcpu[..., 1], "R var", q50=1e-5)   # M2: a difference, cancels
 
 
+def test_build_R_rsamples(oracle, gpu_ok):
+    """Rsamples = 3 (vrlIntegrator.cpp:194): R entries are sums over three
+    independent samples (LiInternal's samples loop, :427-443 / :812-813);
+    blocked build (alvrl_build_R_blocks) with its fused non-zero mask."""
+    torch = _torch()
+    sc, m, vrls, pc, recs = _scene_inputs(oracle, 96, 96, 700)
+    rows = np.arange(0, 96 * 96, 97, dtype=np.uint32)
+    sub = recs[rows]
+    P = oracle.params(m, seed=SEED_RNG, r_samples=3)
+    _, Rcpu, cnt = oracle.gather_brute(P, sub, vrls, pc, rec_ids=rows, domain=2, want_R=True)
+    P1 = oracle.params(m, seed=SEED_RNG)
+    _, R1, _ = oracle.gather_brute(P1, sub, vrls, pc, rec_ids=rows, domain=2, want_R=True)
+    assert not np.array_equal(Rcpu, R1)
+    ctx = _ctx()
+    ctx.upload_vrls(vrls, pc)
+    ctx.set_rsamples(3)
+    nr, nv = len(rows), vrls.shape[1]
+    d_Rt = torch.zeros((nv, nr, 2), dtype=torch.float32, device="cuda")
+    ctx.reset_stats()
+    ctx.build_R(torch.from_numpy(sub).cuda(), d_Rt, ld=nr, d_ids=torch.from_numpy(rows.view(np.int32)).cuda())
+    # the same rows through the blocked build: two blocks of different strides
+    h = nr // 2
+    boff = np.concatenate([np.arange(h), nv * h + np.arange(nr - h)]).astype(np.uint64)
+    bstr = np.concatenate([np.full(h, h), np.full(nr - h, nr - h)]).astype(np.uint32)
+    d_B = torch.zeros(nv * nr * 2, dtype=torch.float32, device="cuda")
+    d_nz = torch.zeros(nv, dtype=torch.uint8, device="cuda")
+    ctx.build_R_blocks(torch.from_numpy(sub).cuda(), d_B, torch.from_numpy(boff.view(np.int64)).cuda(),
+                       torch.from_numpy(bstr.view(np.int32)).cuda(), d_nz,
+                       d_ids=torch.from_numpy(rows.view(np.int32)).cuda())
+    torch.cuda.synchronize()
+    Rg = d_Rt.cpu().numpy().transpose(1, 0, 2)
+    pre, _ = ctx.stats()
+    assert pre == 2 * cnt
+    _assert_close_pairs(Rg[..., 0], Rcpu[..., 0], "R mean (Rsamples=3)")
+    _assert_close_pairs(Rg[..., 1], Rcpu[..., 1], "R var (Rsamples=3)", q50=1e-5)
+    B = d_B.cpu().numpy().reshape(-1, 2)
+    Bt = np.concatenate([B[:nv * h].reshape(nv, h, 2), B[nv * h:].reshape(nv, nr - h, 2)], axis=1)
+    assert np.array_equal(Bt.view(np.uint32), d_Rt.cpu().numpy().view(np.uint32))
+    assert np.array_equal(d_nz.cpu().numpy().astype(bool), (Rg[..., 0] != 0).any(axis=0))
+
+
 def _degenerate_inputs(oracle):
     """Eye rays exactly along +z (so sinTheta is exactly 0 against z-aligned
     VRLs on both sides), VRLs parallel to them (sampleVtoDistance's uniform

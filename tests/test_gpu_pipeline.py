@@ -86,6 +86,7 @@ def test_c1_pipeline_adaptive(oracle, gpu_ok):
     ("localRefinement=false;globalCluster=false", None),
     ("globalCluster=true;globalUndersampling=20", {"global_cluster": True, "global_undersampling": 20.0}),
     ("globalCluster=true;targetNumSlices=40", {"global_cluster": True, "target_num_slices": 40}),
+    ("Rsamples=2", {}),
 ])
 def test_pipeline_variants(oracle, gpu_ok, props, prep_kw):
     import alvrl
@@ -258,3 +259,50 @@ def test_refine_members(oracle, gpu_ok, gu):
     assert ok and ook
     print(f"global clusters: {len(off) - 1} (device) {len(ooff) - 1} (oracle)")
     assert np.array_equal(off, ooff) and np.array_equal(mem, omem)
+
+
+def test_false_color_modes(gpu_ok):
+    """numVrlFalseColor / slicesFalseColor (vrlIntegrator.cpp:545-599, 794-806)
+    against their closed forms from the integrator's own slice map and
+    cluster lists; slicesFalseColor without clustering is an error, and
+    convergenceFalseColor leaves a diffuse-only frame unchanged (:514-521)."""
+    import torch
+    import alvrl
+    w, h = 128, 96
+    scene = alvrl.scene_default(w, h)
+    vrls, pc = alvrl.trace_vrls(scene, 400, seed=SEED_VRL)
+    nv = vrls.shape[1]
+
+    def frame(props):
+        it = alvrl.Integrator(props + f";seed={SEED_RNG}", device=0)
+        it.set_vrls(vrls, pc)
+        it.preprocess(scene)
+        it.prepass(0)
+        fb = torch.zeros(w * h * 3, dtype=torch.float32, device="cuda")
+        it.render(fb)
+        torch.cuda.synchronize()
+        return it, fb.view(h, w, 3).cpu().numpy()
+
+    it, img = frame("targetNumSlices=20;numVrlFalseColor=true")
+    cl, p2s = it.clusters(), it.slices()
+    sizes = np.diff(cl["slice_off"]).astype(np.float32)
+    ys, xs = np.mgrid[0:h, 0:w]
+    sl = p2s[ys + h * xs]                                        # m_slices[y + H*x]
+    k = np.where(sl == 0xFFFFFFFF, np.float32(len(cl["fb_reps"])), sizes[np.minimum(sl, len(sizes) - 1)])
+    assert np.array_equal(img[..., 0], (k / np.float32(nv)).astype(np.float32))
+    assert it.stats()["contrib_render"] == int(k.sum())
+
+    it, img = frame("targetNumSlices=20;slicesFalseColor=true")
+    s = sl.astype(np.uint32)
+    col = np.stack([((s + s * s) % 43) / 43.0, ((7 * s + 2 * s * s + 7) % 41) / 41.0,
+                    ((23 * s + 5 * s * s + s * s * s + 17) % 53) / 53.0], axis=-1).astype(np.float32)
+    col[sl == 0xFFFFFFFF] = 0.5
+    assert np.array_equal(img, col)
+
+    _, img = frame("localRefinement=false;numVrlFalseColor=true")
+    assert (img == 1.0).all()
+    with pytest.raises(alvrl.AlvrlError):
+        frame("localRefinement=false;slicesFalseColor=true")
+    _, a = frame("targetNumSlices=20;convergenceFalseColor=true")
+    _, b = frame("targetNumSlices=20")
+    assert np.array_equal(a, b)
