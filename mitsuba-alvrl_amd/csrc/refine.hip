@@ -26,7 +26,10 @@
 #include "vrl_device.hpp"
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
+#include <cstring>
+#include <thread>
 #include <cstdlib>
 #include <string>
 #include <vector>
@@ -42,6 +45,34 @@ constexpr int kBitonicMax = 16384;                          // 8-byte keys sorte
 constexpr uint32_t kDomCluster = 5u;
 
 struct CNode { float uvar, ivar; uint32_t begin, end; };
+
+// Speculative splits (team mode).  A split's result is a function of its
+// cluster alone (its draws are keyed by the cluster range, the sort is a
+// total order), and the live clusters are disjoint ranges of vrls.  Helper
+// workgroups therefore split clusters near the top of the heap ahead of the
+// leader into range-indexed side buffers; the leader, which runs the
+// reference's control flow unchanged, commits a finished result when it pops
+// that cluster (or claims a queued one, or splits an unqueued one itself).
+struct SplitRes { uint32_t idx; int err; float fsu, fsi, feu, fei; };
+struct SplitWs {                      // a workgroup's private split scratch
+    float* dir;
+    double* st;
+    double* bufM;
+    unsigned long long* keys0;
+    unsigned long long* keys1;
+    float* fsu; float* fsi; float* feu; float* fei;
+};
+struct Team {
+    uint32_t helpers;                 // workgroups besides the leader (0 = off)
+    uint32_t* spec;                   // [N] sorted ranges of speculative splits, by position
+    unsigned long long* state;        // [N] by cluster begin: (end << 3) | kSt*
+    SplitRes* res;                    // [N] by cluster begin
+    unsigned long long* queue;        // [kQueue] (begin << 32) | end
+    uint32_t* ctl;                    // head, tail, stop
+    const SplitWs* ws;                // [helpers]
+};
+enum : uint32_t { kStNone = 0, kStQueued = 1, kStRunning = 2, kStDone = 3, kStLeader = 4 };
+constexpr uint32_t kQueue = 1024;
 
 struct JobDev {
     // entry (vrl v, local row r) of R is Rt[roff[r] + v * rstride[r]] (float2
@@ -80,6 +111,7 @@ struct JobDev {
     uint32_t* out_members;
     uint32_t* out_moff;
     uint32_t* out_nclusters;
+    Team team;
 };
 
 struct Common {
@@ -92,7 +124,25 @@ struct Common {
     uint32_t seed, pass;
     unsigned long long* prof;   // per-phase cycle totals (ALVRL_REFINE_PROFILE=1), or null
     unsigned long long* entries;   // R entries the clustering has to read (roofline bytes / 8)
+    uint32_t njobs;                // leaders = blocks [0, njobs); helpers follow, team by team
+    uint32_t team;                 // workgroups per job (1 = no speculation)
+    uint32_t spec_min;             // smallest cluster worth a speculative split
+    unsigned long long spin_ticks; // bound of every team wait (100 MHz ticks)
+    unsigned long long* tstat;     // team counters (ALVRL_REFINE_TEAM_STATS=1), or null
+    unsigned long long* trace;     // host-mapped per-block (phase << 32 | value), ALVRL_REFINE_TRACE=1
 };
+__device__ __forceinline__ void trace(const Common& cm, uint32_t phase, uint32_t value)
+{
+    if (cm.trace && threadIdx.x == 0 && blockIdx.x < 256)
+        __hip_atomic_store(&cm.trace[blockIdx.x], ((unsigned long long)phase << 32) | value, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// team counters
+enum { TS_ENQ, TS_HSTART, TS_HDONE, TS_COMMIT, TS_STEAL, TS_WAIT_TMO, TS_OWN, TS_IDLE_EXIT, TS_LSIDE, TS_N };
+__device__ __forceinline__ void tcount(const Common& cm, int k)
+{
+    if (cm.tstat) atomicAdd(&cm.tstat[k], 1ull);
+}
 
 // Phase timer of lane 0 (s_memtime deltas summed over jobs).
 enum { PF_COLW, PF_INIT, PF_UNCL, PF_WSAMP, PF_DIR, PF_PROJ, PF_SORT, PF_CVF, PF_CVR, PF_ARGMIN,
@@ -141,6 +191,9 @@ struct Ctl {
     int degenerate;
     float diffLen, nd;
     int go, do_snap, stop, refined;
+    int tmode, side;
+    uint32_t yb, ye;
+    unsigned long long t0;
     float avg;
     // reductions
     float nrm3[3];
@@ -962,8 +1015,10 @@ __device__ __noinline__ void split_projections(const JobDev& J, const Common& cm
 
 // ------------------------------------------------------------ split --
 // Clustering::split (:590-684), collective.
+// commit: push the two children (the leader); otherwise write the result to
+// *res (a helper working on J with its own scratch and vrls = team.spec)
 __device__ void split(const JobDev& J, const Common& cm, Ctl& C, uint32_t begin, uint32_t end,
-                      unsigned long long* lds, Prof& pf)
+                      unsigned long long* lds, Prof& pf, bool commit = true, SplitRes* res = nullptr)
 {
     pf.mark(PF_CTRL);
     pf.count(PF_NSPLIT, 1);
@@ -1089,7 +1144,14 @@ __device__ void split(const JobDev& J, const Common& cm, Ctl& C, uint32_t begin,
         uint32_t idx = 0xFFFFFFFFu;
         for (int w = 0; w < kWaves; w++)
             if (C.best_v[w] < v || (C.best_v[w] == v && C.best_i[w] < idx)) { v = C.best_v[w]; idx = C.best_i[w]; }
-        if (idx == 0xFFFFFFFFu) {
+        if (!commit) {
+            SplitRes r{idx, C.err | (idx == 0xFFFFFFFFu ? 1 : 0), 0.0f, 0.0f, 0.0f, 0.0f};
+            if (idx != 0xFFFFFFFFu) {
+                r.fsu = J.fsu[idx - 1]; r.fsi = J.fsi[idx - 1];
+                r.feu = J.feu[m - 1 - idx]; r.fei = J.fei[m - 1 - idx];
+            }
+            *res = r;
+        } else if (idx == 0xFFFFFFFFu) {
             C.err = 1;
         } else {
             const uint32_t s = begin + idx;
@@ -1101,13 +1163,266 @@ __device__ void split(const JobDev& J, const Common& cm, Ctl& C, uint32_t begin,
     pf.mark(PF_ARGMIN);
 }
 
+// ------------------------------------------------------- team mode --
+__device__ __forceinline__ unsigned long long ld_acq(unsigned long long* p)
+{
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ld_acq(uint32_t* p)
+{
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_rel(unsigned long long* p, unsigned long long v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_rel(uint32_t* p, uint32_t v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T>
+__device__ __forceinline__ bool cas_acq_rel(T* p, T expect, T v)
+{
+    return __hip_atomic_compare_exchange_strong(p, &expect, v, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+}
+// Polling uses relaxed agent-scope loads (coherent across XCDs without
+// invalidating the L2 on every iteration); one acquire fence follows success.
+__device__ __forceinline__ unsigned long long ld_rlx(unsigned long long* p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ld_rlx(uint32_t* p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void fence_acq() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent"); }
+// constant 100 MHz clock.  No wait is unbounded: a leader that has waited
+// kSpinTicks (~60 s) for a helper splits the cluster itself (the helper's late
+// result lands in side buffers nobody commits), an idle helper gives up after
+// the same time without a task.
+__device__ __forceinline__ unsigned long long wall() { return __builtin_amdgcn_s_memrealtime(); }
+constexpr unsigned long long kSpinTicks = 6000000000ull;   // default of Common::spin_ticks
+
+// Thread 0 of the leader: queue the multi-clusters near the top of the heap
+// that are not queued yet.
+__device__ void enqueue_candidates(const JobDev& J, const Common& cm, Ctl& C)
+{
+    const Team& T = J.team;
+    const int K = min(C.heap_n, (int)(2 * T.helpers + 2));
+    uint32_t tail = T.ctl[1];
+    const uint32_t head = ld_acq(&T.ctl[0]);
+    bool pushed = false;
+    for (int k = 0; k < K; k++) {
+        const CNode cn = J.heap[k];
+        if (cn.end - cn.begin < cm.spec_min) continue;
+        if (tail - head >= kQueue) break;
+        unsigned long long* st = &T.state[cn.begin];
+        const unsigned long long sv = __hip_atomic_load(st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((uint32_t)(sv >> 3) == cn.end && (sv & 7) != kStNone) continue;
+        st_rel(st, ((unsigned long long)cn.end << 3) | kStQueued);
+        __hip_atomic_store(&T.queue[tail % kQueue], ((unsigned long long)cn.begin << 32) | cn.end,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        tail++;
+        pushed = true;
+        tcount(cm, TS_ENQ);
+    }
+    if (pushed) st_rel(&T.ctl[1], tail);
+}
+
+__device__ void stop_team(const JobDev& J, const Common& cm)
+{
+    if (J.team.helpers && threadIdx.x == 0) st_rel(&J.team.ctl[2], 1u);
+    trace(cm, 6, 0);
+}
+
+__device__ __forceinline__ JobDev J_spec(const JobDev& J)
+{
+    JobDev Jw = J;
+    Jw.vrls = J.team.spec;
+    return Jw;
+}
+
+// Thread 0: take the oldest queued task.  1 = claimed (*b, *e), 0 = queue
+// empty, 2 = lost a race (try again).
+__device__ int try_claim(const Team& T, uint32_t* b, uint32_t* e)
+{
+    const uint32_t h = ld_rlx(&T.ctl[0]), t = ld_rlx(&T.ctl[1]);
+    if (h >= t) return 0;
+    fence_acq();
+    const unsigned long long task = __hip_atomic_load(&T.queue[h % kQueue], __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT);
+    if (!cas_acq_rel(&T.ctl[0], h, h + 1)) return 2;
+    *b = (uint32_t)(task >> 32); *e = (uint32_t)task;
+    const unsigned long long want = ((unsigned long long)*e << 3) | kStQueued;
+    return cas_acq_rel(&T.state[*b], want, ((unsigned long long)*e << 3) | kStRunning) ? 1 : 2;
+}
+
+// Split [b, e) speculatively with Jw's scratch (Jw.vrls = team.spec) and
+// publish the result (MI355X_MICROARCH.md, valid producer form: every storing
+// wave drains, barrier, lane 0 releases at agent scope and drains the
+// write-back, then the relaxed agent flag store).  C.err is the caller's.
+__device__ void spec_split(const JobDev& J0, const JobDev& Jw, const Common& cm, Ctl& C,
+                           unsigned long long* lds, uint32_t b, uint32_t e)
+{
+    const Team& T = J0.team;
+    const int tid = threadIdx.x;
+    fence_acq();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (uint32_t i = b + (uint32_t)tid; i < e; i += kThreads) T.spec[i] = J0.vrls[i];
+    __syncthreads();
+    const int err_saved = C.err;
+    __syncthreads();
+    if (tid == 0) C.err = 0;
+    __syncthreads();
+    Prof off{nullptr, 0};
+    split(Jw, cm, C, b, e, lds, off, false, &T.res[b]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+        C.err = err_saved;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(&T.state[b], ((unsigned long long)e << 3) | kStDone, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+}
+
+// The leader's split of [b, e): claim a queued task, wait for a running one
+// and commit its result, or split here.  While a helper still runs [b, e)
+// the leader splits other queued clusters speculatively.  spec = false:
+// plain split.
+__device__ void split_team(const JobDev& J, const Common& cm, Ctl& C, uint32_t b, uint32_t e,
+                           unsigned long long* lds, Prof& pf, bool spec)
+{
+    const Team& T = J.team;
+    if (!T.helpers || !spec) { split(J, cm, C, b, e, lds, pf); return; }
+    const int tid = threadIdx.x;
+    if (tid == 0) {
+        trace(cm, 3, b);
+        enqueue_candidates(J, cm, C);
+        unsigned long long* st = &T.state[b];
+        const unsigned long long key = (unsigned long long)e << 3;
+        unsigned long long sv = ld_acq(st);
+        int mode = 0;
+        if ((uint32_t)(sv >> 3) == e && (sv & 7) != kStNone && (sv & 7) != kStLeader) {
+            if ((sv & 7) == kStQueued && cas_acq_rel(st, sv, key | kStLeader)) {
+                mode = 0;
+                tcount(cm, TS_STEAL);
+            } else {
+                mode = 3;   // running on a helper: wait below, splitting other tasks meanwhile
+                C.t0 = wall();
+                trace(cm, 4, b);
+            }
+        } else {
+            st_rel(st, key | kStLeader);
+            tcount(cm, TS_OWN);
+        }
+        C.tmode = mode;
+    }
+    __syncthreads();
+    while (true) {
+        const int tm = C.tmode;
+        __syncthreads();   // every thread has read tmode before thread 0 rewrites it
+        if (tm != 3) break;
+        if (tid == 0) {
+            const unsigned long long sv = ld_rlx(&T.state[b]);
+            C.side = 0;
+            if ((sv & 7) == kStDone) {
+                fence_acq();
+                C.tmode = 1;
+                tcount(cm, TS_COMMIT);
+            } else if (wall() - C.t0 > cm.spin_ticks) {
+                C.tmode = 0;   // give up on the helper: split here
+                tcount(cm, TS_WAIT_TMO);
+            } else {
+                uint32_t yb = 0, ye = 0;
+                const int got = try_claim(T, &yb, &ye);
+                if (got == 1) { C.side = 1; C.yb = yb; C.ye = ye; tcount(cm, TS_LSIDE); }
+                else if (got == 0) __builtin_amdgcn_s_sleep(8);
+            }
+        }
+        __syncthreads();
+        if (C.side) spec_split(J, J_spec(J), cm, C, lds, C.yb, C.ye);
+        __syncthreads();
+    }
+    const int mode = C.tmode;
+    if (mode == 0) {
+        split(J, cm, C, b, e, lds, pf);
+    } else if (mode == 1) {
+        fence_acq();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        for (uint32_t i = b + (uint32_t)tid; i < e; i += kThreads) J.vrls[i] = T.spec[i];
+        __syncthreads();
+        if (tid == 0) {
+            const SplitRes r = T.res[b];
+            if (r.err || r.idx == 0xFFFFFFFFu) {
+                C.err = 1;
+            } else {
+                const uint32_t m = e - b, s2 = b + r.idx;
+                add_cluster(J, C, b, s2, r.fsu, r.fsi);
+                add_cluster(J, C, s2, e, r.feu, r.fei);
+                (void)m;
+            }
+        }
+        __syncthreads();
+    }
+    if (tid == 0) { enqueue_candidates(J, cm, C); trace(cm, 5, b); }
+    __syncthreads();
+}
+
+// A helper workgroup: split queued clusters of job J until the leader stops.
+__device__ __noinline__ void helper_loop(const JobDev& J0, uint32_t hid, const Common& cm, Ctl& C,
+                                         unsigned long long* lds)
+{
+    const Team& T = J0.team;
+    JobDev J = J0;
+    const SplitWs& w = T.ws[hid];
+    J.vrls = T.spec;
+    J.dir = w.dir; J.st = w.st; J.bufM = w.bufM; J.keys0 = w.keys0; J.keys1 = w.keys1;
+    J.fsu = w.fsu; J.fsi = w.fsi; J.feu = w.feu; J.fei = w.fei;
+    const int tid = threadIdx.x;
+    if (tid == 0) C.err = 0;
+    trace(cm, 10, 0);
+    while (true) {
+        if (tid == 0) {
+            const unsigned long long t_idle = wall();
+            int got = 0;
+            uint32_t b = 0, e = 0;
+            while (true) {
+                if (ld_rlx(&T.ctl[2])) { got = -1; break; }
+                const int c = try_claim(T, &b, &e);
+                if (c == 1) { got = 1; tcount(cm, TS_HSTART); break; }
+                if (c == 2) continue;
+                if (wall() - t_idle > cm.spin_ticks) { got = -1; tcount(cm, TS_IDLE_EXIT); break; }
+                __builtin_amdgcn_s_sleep(32);
+            }
+            C.go = got; C.b = b; C.e = e;
+        }
+        __syncthreads();
+        if (C.go < 0) break;
+        trace(cm, 11, C.b);
+        spec_split(J0, J, cm, C, lds, C.b, C.e);
+        if (tid == 0) tcount(cm, TS_HDONE);
+        trace(cm, 12, C.b);
+    }
+}
+
 // ---------------------------------------------------------- kernel --
 __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ jobs, Common cm)
 {
-    const JobDev J = jobs[blockIdx.x];
     __shared__ Ctl C;
     __shared__ __attribute__((aligned(16))) unsigned char pool[kPoolBytes];
     unsigned long long* lds = reinterpret_cast<unsigned long long*>(pool);
+    if (blockIdx.x >= cm.njobs) {   // a helper of job (blockIdx.x - njobs) / (team - 1)
+        const uint32_t h = blockIdx.x - cm.njobs, per = cm.team - 1;
+        helper_loop(jobs[h / per], h % per, cm, C, lds);
+        trace(cm, 13, 0);
+        return;
+    }
+    const JobDev J = jobs[blockIdx.x];
+    trace(cm, 1, 0);
     const int tid = threadIdx.x, wave = tid >> 6;
     const uint32_t lane = (uint32_t)(tid & 63);
     const uint32_t N = cm.nvrl, R = J.nrows;
@@ -1238,7 +1553,7 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
                 }
                 __syncthreads();
                 if (!C.go) break;
-                split(J, cm, C, C.b, C.e, lds, pf);
+                split_team(J, cm, C, C.b, C.e, lds, pf, true);
             }
         } else {
             // refineAdaptively (:402-489)
@@ -1263,7 +1578,7 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
                     }
                     __syncthreads();
                     if (!C.go) break;
-                    split(J, cm, C, C.b, C.e, lds, pf);
+                    split_team(J, cm, C, C.b, C.e, lds, pf, true);
                     if (tid == 0) {
                         nsplit++;
                         const float curr = conv_const(C, N, J.pixel_under);
@@ -1279,6 +1594,7 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
                     if (C.do_snap) snapshot(J, C);
                     if (C.stop) break;
                 }
+                stop_team(J, cm);
                 restore(J, C);
                 if (dc != 1) {
                     const int corrected = (int)(0.5 + dc * bestN);
@@ -1289,12 +1605,13 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
                         }
                         __syncthreads();
                         if (!C.go) break;
-                        split(J, cm, C, C.b, C.e, lds, pf);
+                        split_team(J, cm, C, C.b, C.e, lds, pf, false);
                     }
                 }
             }
         }
     }
+    stop_team(J, cm);
     __syncthreads();
     pf.mark(PF_CTRL);
     // sampleRepresentatives (:354-378)
@@ -1517,8 +1834,87 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
             J.out_nclusters = (uint32_t*)p;
         }
     }
+    // Team size: every workgroup of a team must be resident at once (helpers
+    // and leader wait on each other), so teams are launched cooperatively and
+    // sized from the occupancy: teams of G workgroups for njobs jobs fit when
+    // njobs * G <= resident blocks.  ALVRL_REFINE_TEAM=n caps G (1 = off).
+    const char* bs_env = std::getenv("ALVRL_REFINE_BATCH");
+    uint32_t G = 1;
+    {
+        int ncu = 0, nb = 0, coop = 0, dev = 0;
+        const char* te = std::getenv("ALVRL_REFINE_TEAM");
+        const uint32_t cap = te ? (uint32_t)std::max(1, std::atoi(te)) : 8u;
+        if (!bs_env && hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+            hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, dev) == hipSuccess && coop &&
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_refine, kThreads, 0) == hipSuccess && nb > 0)
+            G = std::min<uint32_t>(cap, (uint32_t)(nb * ncu) / njobs);
+        if (G < 2) G = 1;
+    }
+    char* tarena = nullptr;
+    size_t tbytes = 0;
+    if (G > 1) {
+        auto helper_bytes = [&](uint32_t R) {
+            return align_up((size_t)R * 4) + align_up((size_t)6 * R * 8) +
+                   align_up((size_t)2 * 2 * kCH * ((R + 63) / 64) * 64 * 16) + 2 * align_up(N * 8) + 4 * align_up(N * 4);
+        };
+        const size_t team_fixed = align_up(N * 4) + align_up(N * 8) + align_up(N * sizeof(SplitRes)) +
+                                  align_up((size_t)kQueue * 8) + align_up(16) + align_up((size_t)(G - 1) * sizeof(SplitWs));
+        for (uint32_t j = 0; j < njobs; j++) tbytes += team_fixed + (size_t)(G - 1) * helper_bytes(jobs[j].nrows);
+        if (hipMalloc(&tarena, tbytes) != hipSuccess) { (void)hipGetLastError(); tarena = nullptr; G = 1; }
+    }
+    std::vector<SplitWs> h_ws(G > 1 ? (size_t)njobs * (G - 1) : 0);
+    {
+        size_t to = 0;
+        for (uint32_t j = 0; j < njobs; j++) {
+            Team& T = h_jobs[j].team;
+            T = Team{0u, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+            if (G < 2) continue;
+            const uint32_t R = jobs[j].nrows;
+            char* q = tarena + to;
+            T.helpers = G - 1;
+            T.spec = (uint32_t*)q; q += align_up(N * 4);
+            T.state = (unsigned long long*)q; q += align_up(N * 8);
+            T.res = (SplitRes*)q; q += align_up(N * sizeof(SplitRes));
+            T.queue = (unsigned long long*)q; q += align_up((size_t)kQueue * 8);
+            T.ctl = (uint32_t*)q; q += align_up(16);
+            T.ws = (const SplitWs*)q; q += align_up((size_t)(G - 1) * sizeof(SplitWs));
+            for (uint32_t h = 0; h + 1 < G; h++) {
+                SplitWs& w = h_ws[(size_t)j * (G - 1) + h];
+                w.dir = (float*)q; q += align_up((size_t)R * 4);
+                w.st = (double*)q; q += align_up((size_t)6 * R * 8);
+                w.bufM = (double*)q; q += align_up((size_t)2 * 2 * kCH * ((R + 63) / 64) * 64 * 16);
+                w.keys0 = (unsigned long long*)q; q += align_up(N * 8);
+                w.keys1 = (unsigned long long*)q; q += align_up(N * 8);
+                w.fsu = (float*)q; q += align_up(N * 4);
+                w.fsi = (float*)q; q += align_up(N * 4);
+                w.feu = (float*)q; q += align_up(N * 4);
+                w.fei = (float*)q; q += align_up(N * 4);
+            }
+            to = (size_t)(q - tarena);
+        }
+    }
     Common cm;
     cm.Rt = reinterpret_cast<const float2*>(d_Rt); cm.ld = ld; cm.nvrl = nvrl;
+    cm.njobs = njobs; cm.team = G;
+    {
+        const char* sp = std::getenv("ALVRL_REFINE_SPIN_MS");
+        cm.spin_ticks = sp ? (unsigned long long)std::max(1, std::atoi(sp)) * 100000ull : kSpinTicks;
+    }
+    cm.tstat = nullptr;
+    cm.trace = nullptr;
+    const char* tre = std::getenv("ALVRL_REFINE_TRACE");
+    if (tre && tre[0] == '1' && hipHostMalloc(&cm.trace, 256 * 8, hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess)
+        std::memset(cm.trace, 0, 256 * 8);
+    else
+        cm.trace = nullptr;
+    const char* tse = std::getenv("ALVRL_REFINE_TEAM_STATS");
+    if (G > 1 && tse && tse[0] == '1' && hipMalloc(&cm.tstat, TS_N * 8) == hipSuccess)
+        (void)hipMemsetAsync(cm.tstat, 0, TS_N * 8, s);
+    {
+        const char* sm = std::getenv("ALVRL_SPEC_MIN");
+        cm.spec_min = sm ? (uint32_t)std::max(2, std::atoi(sm)) : 16u;
+    }
     cm.init_vrls = d_init; cm.init_off = d_init_off; cm.ninit = ninit;
     cm.seed = seed; cm.pass = pass;
     cm.prof = nullptr;
@@ -1536,11 +1932,19 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
     if (e == hipSuccess) e = hipMemcpyAsync(d_init_off, init_off, (size_t)(ninit + 1) * 4, hipMemcpyHostToDevice, s);
     if (e == hipSuccess) e = hipMemcpyAsync(d_jobs, h_jobs.data(), njobs * sizeof(JobDev), hipMemcpyHostToDevice, s);
     if (e == hipSuccess) e = hipMemsetAsync(d_entries, 0, 8, s);
+    if (e == hipSuccess && tarena) e = hipMemsetAsync(tarena, 0, tbytes, s);
+    for (uint32_t j = 0; j < njobs && e == hipSuccess && G > 1; j++)
+        e = hipMemcpyAsync(const_cast<SplitWs*>(h_jobs[j].team.ws), &h_ws[(size_t)j * (G - 1)],
+                           (size_t)(G - 1) * sizeof(SplitWs), hipMemcpyHostToDevice, s);
     if (e == hipSuccess) e = hipEventRecord(e0, s);
-    if (e == hipSuccess) {
+    if (e == hipSuccess && G > 1) {
+        const JobDev* jp = d_jobs;
+        void* args[] = {(void*)&jp, (void*)&cm};
+        e = hipLaunchCooperativeKernel((const void*)k_refine, dim3(njobs * G), dim3(kThreads), args, 0, s);
+    } else if (e == hipSuccess) {
         // ALVRL_REFINE_BATCH=n (developer knob): launch the jobs n at a time,
         // to separate per-CU cost from contention between concurrent jobs
-        const char* bs = std::getenv("ALVRL_REFINE_BATCH");
+        const char* bs = bs_env;
         const uint32_t batch = bs ? (uint32_t)std::max(1, std::atoi(bs)) : njobs;
         for (uint32_t j0 = 0; j0 < njobs && e == hipSuccess; j0 += batch) {
             hipLaunchKernelGGL(k_refine, dim3(std::min(batch, njobs - j0)), dim3(kThreads), 0, s, d_jobs + j0, cm);
@@ -1548,6 +1952,26 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
         }
     }
     if (e == hipSuccess) e = hipEventRecord(e1, s);
+    if (cm.trace && e == hipSuccess) {
+        // print every block's (phase, value) whenever it changes, until the kernel ends
+        const uint32_t nblk = std::min<uint32_t>(256, njobs * G);
+        std::vector<unsigned long long> last(nblk, ~0ull);
+        const auto t0 = std::chrono::steady_clock::now();
+        while (hipEventQuery(e1) == hipErrorNotReady) {
+            std::string line;
+            for (uint32_t b = 0; b < nblk; b++) {
+                const unsigned long long v = __atomic_load_n(&cm.trace[b], __ATOMIC_RELAXED);
+                if (v != last[b]) {
+                    last[b] = v;
+                    line += " b" + std::to_string(b) + "=" + std::to_string(v >> 32) + ":" + std::to_string((uint32_t)v);
+                }
+            }
+            if (!line.empty())
+                std::fprintf(stderr, "[trace %.2f s]%s\n",
+                             std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(), line.c_str());
+            std::this_thread::sleep_for(std::chrono::milliseconds(200));
+        }
+    }
     // gather results: packed on the device, three copies
     std::vector<uint32_t> meta(3 * (size_t)njobs);
     unsigned long long h_entries = 0;
@@ -1559,6 +1983,15 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
     if (e == hipSuccess) e = hipMemcpyAsync(&h_entries, d_entries, 8, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (entries) *entries = h_entries;
+    if (cm.tstat) {
+        unsigned long long h[TS_N];
+        if (hipMemcpy(h, cm.tstat, sizeof(h), hipMemcpyDeviceToHost) == hipSuccess)
+            std::fprintf(stderr, "[refine team] G=%u jobs=%u enqueued %llu helper start %llu done %llu | leader "
+                         "commit %llu steal %llu wait-timeout %llu own %llu side %llu | helper idle exits %llu\n",
+                         G, njobs, h[TS_ENQ], h[TS_HSTART], h[TS_HDONE], h[TS_COMMIT], h[TS_STEAL],
+                         h[TS_WAIT_TMO], h[TS_OWN], h[TS_LSIDE], h[TS_IDLE_EXIT]);
+        hipFree(cm.tstat);
+    }
     if (cm.prof) {
         unsigned long long h[PF_N];
         if (hipMemcpy(h, cm.prof, sizeof(h), hipMemcpyDeviceToHost) == hipSuccess) {
@@ -1603,6 +2036,8 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
     }
     if (e != hipSuccess) { rc = 3; *err = std::string("alvrl_refine: ") + hipGetErrorString(e); }
     hipFree(arena);
+    if (tarena) hipFree(tarena);
+    if (cm.trace) hipHostFree(cm.trace);
     if (e0) hipEventDestroy(e0);
     if (e1) hipEventDestroy(e1);
     return rc;
