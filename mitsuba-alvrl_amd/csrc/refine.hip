@@ -130,6 +130,9 @@ struct Common {
     unsigned long long spin_ticks; // bound of every team wait (100 MHz ticks)
     unsigned long long* tstat;     // team counters (ALVRL_REFINE_TEAM_STATS=1), or null
     unsigned long long* trace;     // host-mapped per-block (phase << 32 | value), ALVRL_REFINE_TRACE=1
+    uint32_t spec_width;           // heap entries examined per enqueue (0 = 2 * helpers + 2)
+    uint32_t nroam;                // roaming helpers (after the teams): serve every job's queue
+    const SplitWs* roam_ws;        // [nroam] their scratch, sized for the largest job
 };
 __device__ __forceinline__ void trace(const Common& cm, uint32_t phase, uint32_t value)
 {
@@ -192,7 +195,7 @@ struct Ctl {
     float diffLen, nd;
     int go, do_snap, stop, refined;
     int tmode, side;
-    uint32_t yb, ye;
+    uint32_t yb, ye, j;
     unsigned long long t0;
     float avg;
     // reductions
@@ -1209,7 +1212,7 @@ constexpr unsigned long long kSpinTicks = 6000000000ull;   // default of Common:
 __device__ void enqueue_candidates(const JobDev& J, const Common& cm, Ctl& C)
 {
     const Team& T = J.team;
-    const int K = min(C.heap_n, (int)(2 * T.helpers + 2));
+    const int K = min(C.heap_n, (int)(cm.spec_width ? cm.spec_width : 2 * T.helpers + 2));
     uint32_t tail = T.ctl[1];
     const uint32_t head = ld_acq(&T.ctl[0]);
     bool pushed = false;
@@ -1409,12 +1412,62 @@ __device__ __noinline__ void helper_loop(const JobDev& J0, uint32_t hid, const C
     }
 }
 
+// A roaming helper: takes queued clusters from any job's queue (starting
+// from the job it last served), splits them with its own scratch.
+__device__ __noinline__ void roam_loop(const JobDev* jobs, uint32_t rid, const Common& cm, Ctl& C,
+                                       unsigned long long* lds)
+{
+    const SplitWs& w = cm.roam_ws[rid];
+    const uint32_t njobs = cm.njobs;
+    const int tid = threadIdx.x;
+    uint32_t j = (rid * 37u) % njobs;
+    if (tid == 0) C.err = 0;
+    while (true) {
+        if (tid == 0) {
+            const unsigned long long t_idle = wall();
+            int got = 0;
+            uint32_t b = 0, e = 0, jj = j;
+            while (true) {
+                uint32_t live = 0;
+                for (uint32_t k = 0; k < njobs && !got; k++) {
+                    jj = j + k < njobs ? j + k : j + k - njobs;
+                    const Team& T = jobs[jj].team;
+                    if (ld_rlx(&T.ctl[2])) continue;
+                    live++;
+                    int c;
+                    do { c = try_claim(T, &b, &e); } while (c == 2);
+                    if (c == 1) got = 1;
+                }
+                if (got) { tcount(cm, TS_HSTART); break; }
+                if (!live || wall() - t_idle > cm.spin_ticks) { got = -1; break; }
+                __builtin_amdgcn_s_sleep(32);
+            }
+            C.go = got; C.b = b; C.e = e; C.j = jj;
+        }
+        __syncthreads();
+        if (C.go < 0) break;
+        j = C.j;
+        const JobDev& J0 = jobs[j];
+        JobDev Jw = J0;
+        Jw.vrls = J0.team.spec;
+        Jw.dir = w.dir; Jw.st = w.st; Jw.bufM = w.bufM; Jw.keys0 = w.keys0; Jw.keys1 = w.keys1;
+        Jw.fsu = w.fsu; Jw.fsi = w.fsi; Jw.feu = w.feu; Jw.fei = w.fei;
+        spec_split(J0, Jw, cm, C, lds, C.b, C.e);
+        if (tid == 0) tcount(cm, TS_HDONE);
+    }
+}
+
 // ---------------------------------------------------------- kernel --
 __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ jobs, Common cm)
 {
     __shared__ Ctl C;
     __shared__ __attribute__((aligned(16))) unsigned char pool[kPoolBytes];
     unsigned long long* lds = reinterpret_cast<unsigned long long*>(pool);
+    if (blockIdx.x >= cm.njobs * cm.team) {   // a roaming helper
+        roam_loop(jobs, blockIdx.x - cm.njobs * cm.team, cm, C, lds);
+        trace(cm, 14, 0);
+        return;
+    }
     if (blockIdx.x >= cm.njobs) {   // a helper of job (blockIdx.x - njobs) / (team - 1)
         const uint32_t h = blockIdx.x - cm.njobs, per = cm.team - 1;
         helper_loop(jobs[h / per], h % per, cm, C, lds);
@@ -1839,7 +1892,7 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
     // sized from the occupancy: teams of G workgroups for njobs jobs fit when
     // njobs * G <= resident blocks.  ALVRL_REFINE_TEAM=n caps G (1 = off).
     const char* bs_env = std::getenv("ALVRL_REFINE_BATCH");
-    uint32_t G = 1;
+    uint32_t G = 1, nroam = 0;
     {
         int ncu = 0, nb = 0, coop = 0, dev = 0;
         const char* te = std::getenv("ALVRL_REFINE_TEAM");
@@ -1850,10 +1903,17 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
             hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_refine, kThreads, 0) == hipSuccess && nb > 0)
             G = std::min<uint32_t>(cap, (uint32_t)(nb * ncu) / njobs);
         if (G < 2) G = 1;
+        // the CUs the teams leave free get roaming helpers (ALVRL_REFINE_ROAM=0: none)
+        const char* re = std::getenv("ALVRL_REFINE_ROAM");
+        if (cap > 1 && nb > 0 && (!re || std::atoi(re) != 0) && (uint32_t)(nb * ncu) > njobs * G)
+            nroam = std::min<uint32_t>((uint32_t)(nb * ncu) - njobs * G, 1024u);
     }
+    const bool team_on = G > 1 || nroam > 0;
     char* tarena = nullptr;
     size_t tbytes = 0;
-    if (G > 1) {
+    uint32_t Rmax = 0;
+    for (uint32_t j = 0; j < njobs; j++) Rmax = std::max(Rmax, jobs[j].nrows);
+    if (team_on) {
         auto helper_bytes = [&](uint32_t R) {
             return align_up((size_t)R * 4) + align_up((size_t)6 * R * 8) +
                    align_up((size_t)2 * 2 * kCH * ((R + 63) / 64) * 64 * 16) + 2 * align_up(N * 8) + 4 * align_up(N * 4);
@@ -1861,18 +1921,20 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
         const size_t team_fixed = align_up(N * 4) + align_up(N * 8) + align_up(N * sizeof(SplitRes)) +
                                   align_up((size_t)kQueue * 8) + align_up(16) + align_up((size_t)(G - 1) * sizeof(SplitWs));
         for (uint32_t j = 0; j < njobs; j++) tbytes += team_fixed + (size_t)(G - 1) * helper_bytes(jobs[j].nrows);
-        if (hipMalloc(&tarena, tbytes) != hipSuccess) { (void)hipGetLastError(); tarena = nullptr; G = 1; }
+        tbytes += align_up((size_t)nroam * sizeof(SplitWs)) + (size_t)nroam * helper_bytes(Rmax);
+        if (hipMalloc(&tarena, tbytes) != hipSuccess) { (void)hipGetLastError(); tarena = nullptr; G = 1; nroam = 0; }
     }
-    std::vector<SplitWs> h_ws(G > 1 ? (size_t)njobs * (G - 1) : 0);
+    std::vector<SplitWs> h_ws(G > 1 ? (size_t)njobs * (G - 1) : 0), h_rws(nroam);
+    SplitWs* d_rws = nullptr;
     {
         size_t to = 0;
         for (uint32_t j = 0; j < njobs; j++) {
             Team& T = h_jobs[j].team;
             T = Team{0u, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
-            if (G < 2) continue;
+            if (!tarena) continue;
             const uint32_t R = jobs[j].nrows;
             char* q = tarena + to;
-            T.helpers = G - 1;
+            T.helpers = (G - 1) + (nroam + njobs - 1) / njobs;
             T.spec = (uint32_t*)q; q += align_up(N * 4);
             T.state = (unsigned long long*)q; q += align_up(N * 8);
             T.res = (SplitRes*)q; q += align_up(N * sizeof(SplitRes));
@@ -1893,10 +1955,31 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
             }
             to = (size_t)(q - tarena);
         }
+        if (tarena && nroam) {
+            auto carve = [&](size_t n) { char* q = tarena + to; to += align_up(n); return q; };
+            d_rws = (SplitWs*)carve((size_t)nroam * sizeof(SplitWs));
+            for (uint32_t r = 0; r < nroam; r++) {
+                SplitWs& w = h_rws[r];
+                w.dir = (float*)carve((size_t)Rmax * 4);
+                w.st = (double*)carve((size_t)6 * Rmax * 8);
+                w.bufM = (double*)carve((size_t)2 * 2 * kCH * ((Rmax + 63) / 64) * 64 * 16);
+                w.keys0 = (unsigned long long*)carve(N * 8);
+                w.keys1 = (unsigned long long*)carve(N * 8);
+                w.fsu = (float*)carve(N * 4);
+                w.fsi = (float*)carve(N * 4);
+                w.feu = (float*)carve(N * 4);
+                w.fei = (float*)carve(N * 4);
+            }
+        }
     }
     Common cm;
     cm.Rt = reinterpret_cast<const float2*>(d_Rt); cm.ld = ld; cm.nvrl = nvrl;
     cm.njobs = njobs; cm.team = G;
+    cm.nroam = nroam; cm.roam_ws = d_rws;
+    {
+        const char* sw = std::getenv("ALVRL_SPEC_WIDTH");
+        cm.spec_width = sw ? (uint32_t)std::max(1, std::atoi(sw)) : 12u;   // profiles/r01/team: 6 -> 727 ms, 16 -> 713 ms
+    }
     {
         const char* sp = std::getenv("ALVRL_REFINE_SPIN_MS");
         cm.spin_ticks = sp ? (unsigned long long)std::max(1, std::atoi(sp)) * 100000ull : kSpinTicks;
@@ -1909,7 +1992,7 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
     else
         cm.trace = nullptr;
     const char* tse = std::getenv("ALVRL_REFINE_TEAM_STATS");
-    if (G > 1 && tse && tse[0] == '1' && hipMalloc(&cm.tstat, TS_N * 8) == hipSuccess)
+    if (team_on && tse && tse[0] == '1' && hipMalloc(&cm.tstat, TS_N * 8) == hipSuccess)
         (void)hipMemsetAsync(cm.tstat, 0, TS_N * 8, s);
     {
         const char* sm = std::getenv("ALVRL_SPEC_MIN");
@@ -1936,11 +2019,21 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
     for (uint32_t j = 0; j < njobs && e == hipSuccess && G > 1; j++)
         e = hipMemcpyAsync(const_cast<SplitWs*>(h_jobs[j].team.ws), &h_ws[(size_t)j * (G - 1)],
                            (size_t)(G - 1) * sizeof(SplitWs), hipMemcpyHostToDevice, s);
+    if (e == hipSuccess && nroam)
+        e = hipMemcpyAsync(d_rws, h_rws.data(), (size_t)nroam * sizeof(SplitWs), hipMemcpyHostToDevice, s);
     if (e == hipSuccess) e = hipEventRecord(e0, s);
-    if (e == hipSuccess && G > 1) {
+    if (e == hipSuccess && team_on && tarena) {
         const JobDev* jp = d_jobs;
         void* args[] = {(void*)&jp, (void*)&cm};
-        e = hipLaunchCooperativeKernel((const void*)k_refine, dim3(njobs * G), dim3(kThreads), args, 0, s);
+        e = hipLaunchCooperativeKernel((const void*)k_refine, dim3(njobs * G + nroam), dim3(kThreads), args, 0, s);
+        if (e == hipErrorCooperativeLaunchTooLarge) {
+            // residency smaller than the occupancy query said: leaders alone
+            // (they claim their own queued clusters, results are unchanged)
+            (void)hipGetLastError();
+            cm.team = 1; cm.nroam = 0;
+            hipLaunchKernelGGL(k_refine, dim3(njobs), dim3(kThreads), 0, s, d_jobs, cm);
+            e = hipGetLastError();
+        }
     } else if (e == hipSuccess) {
         // ALVRL_REFINE_BATCH=n (developer knob): launch the jobs n at a time,
         // to separate per-CU cost from contention between concurrent jobs
@@ -1954,7 +2047,7 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
     if (e == hipSuccess) e = hipEventRecord(e1, s);
     if (cm.trace && e == hipSuccess) {
         // print every block's (phase, value) whenever it changes, until the kernel ends
-        const uint32_t nblk = std::min<uint32_t>(256, njobs * G);
+        const uint32_t nblk = std::min<uint32_t>(256, njobs * G + nroam);
         std::vector<unsigned long long> last(nblk, ~0ull);
         const auto t0 = std::chrono::steady_clock::now();
         while (hipEventQuery(e1) == hipErrorNotReady) {
@@ -1986,9 +2079,9 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
     if (cm.tstat) {
         unsigned long long h[TS_N];
         if (hipMemcpy(h, cm.tstat, sizeof(h), hipMemcpyDeviceToHost) == hipSuccess)
-            std::fprintf(stderr, "[refine team] G=%u jobs=%u enqueued %llu helper start %llu done %llu | leader "
+            std::fprintf(stderr, "[refine team] G=%u roam=%u jobs=%u enqueued %llu helper start %llu done %llu | leader "
                          "commit %llu steal %llu wait-timeout %llu own %llu side %llu | helper idle exits %llu\n",
-                         G, njobs, h[TS_ENQ], h[TS_HSTART], h[TS_HDONE], h[TS_COMMIT], h[TS_STEAL],
+                         G, nroam, njobs, h[TS_ENQ], h[TS_HSTART], h[TS_HDONE], h[TS_COMMIT], h[TS_STEAL],
                          h[TS_WAIT_TMO], h[TS_OWN], h[TS_LSIDE], h[TS_IDLE_EXIT]);
         hipFree(cm.tstat);
     }
