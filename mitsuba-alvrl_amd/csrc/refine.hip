@@ -260,58 +260,57 @@ __device__ __forceinline__ float draw_at(uint32_t seed, uint32_t pass, uint32_t 
 }
 
 // weightedSample (Preprocessor.cpp:1534-1580), single lane.
-__device__ uint32_t weighted_sample(const float* w, Smp& smp, float* prob, uint32_t begin,
-                                    uint32_t end, const uint32_t* ind, int* err)
+// weightedSample (Preprocessor.cpp:1534-1580) by one whole wave, in the
+// blocked summation order of the oracle (alvrl_preproc.c weighted_sample):
+// a block of 64 weights per step, Hillis-Steele within rows of 16 (DPP
+// row_shr 1/2/4/8), row bases b1 = t0, b2 = b1 + t1, b3 = b2 + t2, block
+// bases S_{b+1} = S_b + total_b, and the pick is the first index whose
+// prefix S_b + P[l] reaches alpha (a ballot).  Weights come from wv[i], or
+// colw[ids[i]] when wv is null; index zero_at weighs 0 (the second centre of
+// split(), drawn with colw[vrl1] = 0).  Every lane returns the same index;
+// *prob = w / weightSum as in the reference.
+template <int K>
+__device__ __forceinline__ float row_shr_masked(float x, uint32_t lane)
 {
-    if (begin >= end) { *err = 1; return begin; }
-    if (end == begin + 1) { if (prob) *prob = 1; return begin; }
-    float weightSum = 0.0f;
-    for (uint32_t i = begin; i < end; i++) weightSum += w[ind[i]];
-    float probability;
-    uint32_t idx;
-    if (weightSum <= 0) {
-        int tries = 0;
-        do {
-            idx = (uint32_t)((float)begin + smp.next() * (float)(end - begin));
-            if (++tries > 1000) { *err = 1; idx = begin; break; }
-        } while (idx >= end);
-        probability = (float)(1.0 / (double)(end - begin));
-    } else {
-        const float alpha = smp.next() * weightSum;
-        float accum = 0.0f;
-        idx = begin;
-        for (uint32_t i = begin; i < end; i++) {
-            accum += w[ind[i]];
-            if (accum >= alpha) { idx = i; break; }
-        }
-        probability = w[ind[idx]] / weightSum;
-    }
-    if (prob) *prob = probability;
-    return idx;
+    const float v = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x110 + K, 0xF, 0xF, false));
+    return (lane & 15u) >= (uint32_t)K ? v : 0.0f;
 }
-
-// The same weightedSample, executed by one whole wave: the weights stream in
-// 64 at a time (one coalesced load per block, the next block in flight) and
-// the float running sums walk them in order through v_readlane, so the
-// sequential chain costs one add per weight instead of a memory round trip.
-// Every lane returns the same index.  The weight at index `zero_at` counts
-// as 0 (the second centre of split(), drawn with colw[vrl1] = 0).
-__device__ __noinline__ uint32_t weighted_sample_wave(const float* wv, uint32_t m, Smp& smp, int* err,
-                                                      uint32_t zero_at)
+__device__ __forceinline__ float ws_block_wave(float x, uint32_t lane, float* tot)
+{
+    x = x + row_shr_masked<1>(x, lane);
+    x = x + row_shr_masked<2>(x, lane);
+    x = x + row_shr_masked<4>(x, lane);
+    x = x + row_shr_masked<8>(x, lane);
+    const float t0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 15));
+    const float t1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 31));
+    const float t2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 47));
+    const float t3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 63));
+    const float b1 = t0, b2 = b1 + t1, b3 = b2 + t2;
+    *tot = b3 + t3;
+    const uint32_t r = lane >> 4;
+    const float base = r == 0 ? 0.0f : (r == 1 ? b1 : (r == 2 ? b2 : b3));
+    return base + x;
+}
+__device__ __noinline__ uint32_t weighted_sample_wave(const float* wv, const float* colw, const uint32_t* ids,
+                                                      uint32_t m, Smp& smp, int* err, uint32_t zero_at,
+                                                      float* prob)
 {
     const uint32_t lane = threadIdx.x & 63;
     if (m == 0) { *err = 1; return 0; }
-    if (m == 1) return 0;
+    if (m == 1) { if (prob) *prob = 1.0f; return 0; }
+    auto ld = [&](uint32_t i) -> float {
+        const uint32_t c = min(i, m - 1);
+        const float x = wv ? wv[c] : gp(colw)[gp(ids)[c]];
+        return (i >= m || i == zero_at) ? 0.0f : x;
+    };
     const uint32_t nb = (m + 63) / 64;
     float weightSum = 0.0f;
-    float cur = wv[min(lane, m - 1)];
+    float cur = ld(lane);
     for (uint32_t b = 0; b < nb; b++) {
-        const float nxt = b + 1 < nb ? wv[min((b + 1) * 64 + lane, m - 1)] : 0.0f;
-        const uint32_t n = min(64u, m - b * 64);
-        for (uint32_t j = 0; j < n; j++) {
-            const float x = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cur), (int)j));
-            weightSum += b * 64 + j == zero_at ? 0.0f : x;
-        }
+        const float nxt = b + 1 < nb ? ld((b + 1) * 64 + lane) : 0.0f;
+        float tot;
+        (void)ws_block_wave(cur, lane, &tot);
+        weightSum = weightSum + tot;
         cur = nxt;
     }
     uint32_t idx = 0;
@@ -321,20 +320,23 @@ __device__ __noinline__ uint32_t weighted_sample_wave(const float* wv, uint32_t 
             idx = (uint32_t)((float)0u + smp.next() * (float)m);
             if (++tries > 1000) { *err = 1; idx = 0; break; }
         } while (idx >= m);
+        if (prob) *prob = (float)(1.0 / (double)m);
     } else {
         const float alpha = smp.next() * weightSum;
-        float accum = 0.0f;
-        cur = wv[min(lane, m - 1)];
-        bool found = false;
-        for (uint32_t b = 0; b < nb && !found; b++) {
-            const float nxt = b + 1 < nb ? wv[min((b + 1) * 64 + lane, m - 1)] : 0.0f;
-            const uint32_t n = min(64u, m - b * 64);
-            for (uint32_t j = 0; j < n; j++) {
-                const float x = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cur), (int)j));
-                accum += b * 64 + j == zero_at ? 0.0f : x;
-                if (accum >= alpha) { idx = b * 64 + j; found = true; break; }
-            }
+        float S = 0.0f;
+        cur = ld(lane);
+        for (uint32_t b = 0; b < nb; b++) {
+            const float nxt = b + 1 < nb ? ld((b + 1) * 64 + lane) : 0.0f;
+            float tot;
+            const float P = ws_block_wave(cur, lane, &tot);
+            const unsigned long long hit = __ballot(b * 64 + lane < m && S + P >= alpha);
+            if (hit) { idx = b * 64 + (uint32_t)__ffsll((long long)hit) - 1; break; }
+            S = S + tot;
             cur = nxt;
+        }
+        if (prob) {
+            const float wi = idx == zero_at ? 0.0f : (wv ? wv[idx] : colw[ids[idx]]);
+            *prob = wi / weightSum;
         }
     }
     return idx;
@@ -1051,8 +1053,8 @@ __device__ void split(const JobDev& J, const Common& cm, Ctl& C, uint32_t begin,
         Smp smp;
         smp.init(cm.seed, cm.pass, begin, end, J.stage_refine);
         int e = 0;
-        const uint32_t i1 = weighted_sample_wave(wv, m, smp, &e, 0xFFFFFFFFu);
-        const uint32_t i2 = weighted_sample_wave(wv, m, smp, &e, i1);   // colw[vrl1] = 0
+        const uint32_t i1 = weighted_sample_wave(wv, nullptr, nullptr, m, smp, &e, 0xFFFFFFFFu, nullptr);
+        const uint32_t i2 = weighted_sample_wave(wv, nullptr, nullptr, m, smp, &e, i1, nullptr);   // colw[vrl1] = 0
         if (lane == 0) {
             if (e) C.err = 1;
             C.vrl1 = J.vrls[begin + i1]; C.vrl2 = J.vrls[begin + i2]; C.draw_k = smp.k;
@@ -1679,16 +1681,19 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
             J.out_reps[ns - 1 - k] = J.singles[k];
             J.out_w[ns - 1 - k] = 1.0f;
         }
-        for (int k = tid; k < nh; k += kThreads) {
+        for (int k = wave; k < nh; k += kWaves) {   // one wave per multi-cluster
             const CNode cn = J.heap[k];
             Smp smp;
             smp.init(cm.seed, cm.pass, cn.begin, cn.end, J.stage_sample);
             float prob = 1.0f;
             int e = 0;
-            const uint32_t j = weighted_sample(J.colw, smp, &prob, cn.begin, cn.end, J.vrls, &e);
-            if (e) atomicOr(&C.err, 1);
-            J.out_reps[ns + k] = J.vrls[j];
-            J.out_w[ns + k] = 1.0f / prob;
+            const uint32_t j = weighted_sample_wave(nullptr, J.colw, J.vrls + cn.begin, cn.end - cn.begin, smp,
+                                                    &e, 0xFFFFFFFFu, &prob);
+            if ((threadIdx.x & 63) == 0) {
+                if (e) atomicOr(&C.err, 1);
+                J.out_reps[ns + k] = J.vrls[cn.begin + j];
+                J.out_w[ns + k] = 1.0f / prob;
+            }
         }
     }
     __syncthreads();

@@ -228,14 +228,54 @@ typedef struct {
     float *fa, *fb, *fc, *fd;
 } clustering_t;
 
-/* weightedSample, Preprocessor.cpp:1534-1580 */
+/* weightedSample, Preprocessor.cpp:1534-1580.  The running float sums of the
+ * reference (weightSum += w, accum += w, in index order) are taken in one
+ * fixed blocked order that a 64-lane wavefront evaluates directly -- the
+ * reference's -funsafe-math-optimizations build (build/config-linux-gcc.py:7)
+ * may reassociate them, so it has no canonical rounding here either:
+ *   block b = indices [64b, 64b + 64) (missing ones weigh 0);
+ *   within each row of 16: Hillis-Steele inclusive scan, y[l] += y[l - k]
+ *     for k = 1, 2, 4, 8 (lanes with l % 16 >= k, simultaneous);
+ *   row bases b0 = 0, b1 = t0, b2 = b1 + t1, b3 = b2 + t2 (t_r = row total);
+ *   block prefix P[l] = b_row + y[l], block total = b3 + t3;
+ *   block bases S_0 = 0, S_{b+1} = S_b + total_b; prefix(64b + l) = S_b + P[l].
+ * weightSum = S_nb; the pick is the first index whose prefix >= alpha. */
+static float ws_block(const float x[64], float P[64])
+{
+    float y[64], t[64];
+    memcpy(y, x, sizeof(y));
+    for (int k = 1; k <= 8; k <<= 1) {
+        memcpy(t, y, sizeof(t));
+        for (int l = 0; l < 64; l++)
+            if (l % 16 >= k) y[l] = t[l] + t[l - k];
+    }
+    const float b1 = y[15], b2 = b1 + y[31], b3 = b2 + y[47];
+    const float base[4] = { 0.0f, b1, b2, b3 };
+    for (int l = 0; l < 64; l++) P[l] = base[l / 16] + y[l];
+    return b3 + y[63];
+}
+
+static void ws_load(const float *weights, const uint32_t *ind, size_t begin, size_t end, size_t b,
+                    float x[64])
+{
+    for (int l = 0; l < 64; l++) {
+        size_t i = begin + 64 * b + (size_t)l;
+        x[l] = i < end ? weights[ind ? ind[i] : i] : 0.0f;
+    }
+}
+
 static size_t weighted_sample(const float *weights, smp_t *smp, float *prob, size_t begin,
                               size_t end, const uint32_t *ind, int *err)
 {
     if (begin >= end) { *err = 1; return begin; }
     if (end == begin + 1) { if (prob) *prob = 1; return begin; }
+    const size_t nb = (end - begin + 63) / 64;
+    float x[64], P[64];
     float weightSum = 0.0f;
-    for (size_t i = begin; i < end; i++) weightSum += weights[ind ? ind[i] : i];
+    for (size_t b = 0; b < nb; b++) {
+        ws_load(weights, ind, begin, end, b, x);
+        weightSum = weightSum + ws_block(x, P);
+    }
     float probability;
     size_t idx;
     if (weightSum <= 0) {
@@ -247,11 +287,15 @@ static size_t weighted_sample(const float *weights, smp_t *smp, float *prob, siz
         probability = (float)(1.0 / (double)(end - begin));
     } else {
         float alpha = smp_next(smp) * weightSum;
-        float accum = 0.0f;
+        float S = 0.0f;
         idx = begin;
-        for (size_t i = begin; i < end; i++) {
-            accum += weights[ind ? ind[i] : i];
-            if (accum >= alpha) { idx = i; break; }
+        int found = 0;
+        for (size_t b = 0; b < nb && !found; b++) {
+            ws_load(weights, ind, begin, end, b, x);
+            const float tot = ws_block(x, P);
+            for (int l = 0; l < 64 && begin + 64 * b + (size_t)l < end; l++)
+                if (S + P[l] >= alpha) { idx = begin + 64 * b + (size_t)l; found = 1; break; }
+            S = S + tot;
         }
         probability = weights[ind ? ind[idx] : idx] / weightSum;
     }
