@@ -259,7 +259,6 @@ __device__ __forceinline__ float draw_at(uint32_t seed, uint32_t pass, uint32_t 
     return u01(s == 0 ? r.x : (s == 1 ? r.y : (s == 2 ? r.z : r.w)));
 }
 
-// weightedSample (Preprocessor.cpp:1534-1580), single lane.
 // weightedSample (Preprocessor.cpp:1534-1580) by one whole wave, in the
 // blocked summation order of the oracle (alvrl_preproc.c weighted_sample):
 // a block of 64 weights per step, Hillis-Steele within rows of 16 (DPP
