@@ -198,7 +198,7 @@ def main():
     if clustered:
         rooflines["refine"] = roof("k_refine", "refine", 8.0 * float(np.mean(refine_ent)),
                                    float(np.mean(refine_kms)),
-                                   "latency-bound: one workgroup per slice, f64 recurrences, see DESIGN.md")
+                                   "latency-bound f64 recurrences (speculative split teams), see DESIGN.md")
         rooflines["rbuild"] = roof("k_build_R_blocks", "rbuild",
                                    BYTES_PER_PAIR["rbuild"] * (s1["contrib_preprocess"] - s0["contrib_preprocess"]) / nst,
                                    float(np.mean(rbuild_ms)), "VALU-bound like the gather")

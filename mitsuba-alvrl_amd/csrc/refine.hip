@@ -1891,19 +1891,18 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
             J.out_nclusters = (uint32_t*)p;
         }
     }
-    // Team size: every workgroup of a team must be resident at once (helpers
-    // and leader wait on each other), so teams are launched cooperatively and
-    // sized from the occupancy: teams of G workgroups for njobs jobs fit when
-    // njobs * G <= resident blocks.  ALVRL_REFINE_TEAM=n caps G (1 = off).
+    // Team size from the occupancy: teams of G workgroups for njobs jobs are
+    // resident together when njobs * G <= resident blocks; the rest of the
+    // resident capacity gets roaming helpers.  ALVRL_REFINE_TEAM=n caps G
+    // (1 = no speculation).
     const char* bs_env = std::getenv("ALVRL_REFINE_BATCH");
     uint32_t G = 1, nroam = 0;
     {
-        int ncu = 0, nb = 0, coop = 0, dev = 0;
+        int ncu = 0, nb = 0, dev = 0;
         const char* te = std::getenv("ALVRL_REFINE_TEAM");
         const uint32_t cap = te ? (uint32_t)std::max(1, std::atoi(te)) : 8u;
         if (!bs_env && hipGetDevice(&dev) == hipSuccess &&
             hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-            hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, dev) == hipSuccess && coop &&
             hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_refine, kThreads, 0) == hipSuccess && nb > 0)
             G = std::min<uint32_t>(cap, (uint32_t)(nb * ncu) / njobs);
         if (G < 2) G = 1;
@@ -2027,17 +2026,12 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
         e = hipMemcpyAsync(d_rws, h_rws.data(), (size_t)nroam * sizeof(SplitWs), hipMemcpyHostToDevice, s);
     if (e == hipSuccess) e = hipEventRecord(e0, s);
     if (e == hipSuccess && team_on && tarena) {
-        const JobDev* jp = d_jobs;
-        void* args[] = {(void*)&jp, (void*)&cm};
-        e = hipLaunchCooperativeKernel((const void*)k_refine, dim3(njobs * G + nroam), dim3(kThreads), args, 0, s);
-        if (e == hipErrorCooperativeLaunchTooLarge) {
-            // residency smaller than the occupancy query said: leaders alone
-            // (they claim their own queued clusters, results are unchanged)
-            (void)hipGetLastError();
-            cm.team = 1; cm.nroam = 0;
-            hipLaunchKernelGGL(k_refine, dim3(njobs), dim3(kThreads), 0, s, d_jobs, cm);
-            e = hipGetLastError();
-        }
+        // sized to the resident capacity, but correct without co-residency:
+        // no workgroup ever waits for one that has not started (a leader waits
+        // only on a cluster a running helper has claimed, helpers only poll),
+        // so a late helper finds its job stopped and leaves
+        hipLaunchKernelGGL(k_refine, dim3(njobs * G + nroam), dim3(kThreads), 0, s, d_jobs, cm);
+        e = hipGetLastError();
     } else if (e == hipSuccess) {
         // ALVRL_REFINE_BATCH=n (developer knob): launch the jobs n at a time,
         // to separate per-CU cost from contention between concurrent jobs
