@@ -129,9 +129,11 @@ struct Common {
     uint32_t spec_min;             // smallest cluster worth a speculative split
     unsigned long long spin_ticks; // bound of every team wait (100 MHz ticks)
     unsigned long long* tstat;     // team counters (ALVRL_REFINE_TEAM_STATS=1), or null
+    unsigned long long* jtime;     // with tstat: per job, wall ticks at start / end of refine / end
     unsigned long long* trace;     // host-mapped per-block (phase << 32 | value), ALVRL_REFINE_TRACE=1
     uint32_t spec_width;           // heap entries examined per enqueue (0 = 2 * helpers + 2)
     uint32_t nroam;                // roaming helpers (after the teams): serve every job's queue
+    int roam_on;                   // finished leaders and helpers roam too (scratch sized for Rmax)
     const SplitWs* roam_ws;        // [nroam] their scratch, sized for the largest job
 };
 __device__ __forceinline__ void trace(const Common& cm, uint32_t phase, uint32_t value)
@@ -1415,13 +1417,12 @@ __device__ __noinline__ void helper_loop(const JobDev& J0, uint32_t hid, const C
 
 // A roaming helper: takes queued clusters from any job's queue (starting
 // from the job it last served), splits them with its own scratch.
-__device__ __noinline__ void roam_loop(const JobDev* jobs, uint32_t rid, const Common& cm, Ctl& C,
-                                       unsigned long long* lds)
+__device__ __noinline__ void roam_loop(const JobDev* jobs, const SplitWs& w, uint32_t start, const Common& cm,
+                                       Ctl& C, unsigned long long* lds)
 {
-    const SplitWs& w = cm.roam_ws[rid];
     const uint32_t njobs = cm.njobs;
     const int tid = threadIdx.x;
-    uint32_t j = (rid * 37u) % njobs;
+    uint32_t j = start % njobs;
     if (tid == 0) C.err = 0;
     while (true) {
         if (tid == 0) {
@@ -1465,18 +1466,22 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
     __shared__ __attribute__((aligned(16))) unsigned char pool[kPoolBytes];
     unsigned long long* lds = reinterpret_cast<unsigned long long*>(pool);
     if (blockIdx.x >= cm.njobs * cm.team) {   // a roaming helper
-        roam_loop(jobs, blockIdx.x - cm.njobs * cm.team, cm, C, lds);
+        const uint32_t rid = blockIdx.x - cm.njobs * cm.team;
+        roam_loop(jobs, cm.roam_ws[rid], rid * 37u, cm, C, lds);
         trace(cm, 14, 0);
         return;
     }
     if (blockIdx.x >= cm.njobs) {   // a helper of job (blockIdx.x - njobs) / (team - 1)
         const uint32_t h = blockIdx.x - cm.njobs, per = cm.team - 1;
         helper_loop(jobs[h / per], h % per, cm, C, lds);
+        // its job is done: help the others until every job is
+        if (cm.roam_on) roam_loop(jobs, jobs[h / per].team.ws[h % per], h / per + 1, cm, C, lds);
         trace(cm, 13, 0);
         return;
     }
     const JobDev J = jobs[blockIdx.x];
     trace(cm, 1, 0);
+    if (cm.jtime && threadIdx.x == 0) cm.jtime[3 * blockIdx.x] = wall();
     const int tid = threadIdx.x, wave = tid >> 6;
     const uint32_t lane = (uint32_t)(tid & 63);
     const uint32_t N = cm.nvrl, R = J.nrows;
@@ -1666,6 +1671,7 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
         }
     }
     stop_team(J, cm);
+    if (cm.jtime && threadIdx.x == 0) cm.jtime[3 * blockIdx.x + 1] = wall();
     __syncthreads();
     pf.mark(PF_CTRL);
     // sampleRepresentatives (:354-378)
@@ -1725,6 +1731,13 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
         // column weights, initial clusters and unclustered variance read every
         // entry once; a split reads its cluster's columns (at least) once
         if (cm.entries) atomicAdd(cm.entries, (3ull * N + split_cols) * R);
+    }
+    if (cm.jtime && tid == 0) cm.jtime[3 * blockIdx.x + 2] = wall();
+    if (cm.roam_on) {
+        // this job is done: its leader helps the others with its own scratch
+        __syncthreads();
+        const SplitWs w{J.dir, J.st, J.bufM, J.keys0, J.keys1, J.fsu, J.fsi, J.feu, J.fei};
+        roam_loop(jobs, w, blockIdx.x + 1, cm, C, lds);
     }
 }
 
@@ -1804,8 +1817,34 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
         row_off[j] = rows_total;
         rows_total += jobs[j].nrows;
     }
+    // Team size from the occupancy: teams of G workgroups for njobs jobs are
+    // resident together when njobs * G <= resident blocks; the rest of the
+    // resident capacity gets roaming helpers.  ALVRL_REFINE_TEAM=n caps G
+    // (1 = no speculation).
+    const char* bs_env = std::getenv("ALVRL_REFINE_BATCH");
+    uint32_t G = 1, nroam = 0;
+    {
+        int ncu = 0, nb = 0, dev = 0;
+        const char* te = std::getenv("ALVRL_REFINE_TEAM");
+        const uint32_t cap = te ? (uint32_t)std::max(1, std::atoi(te)) : 8u;
+        if (!bs_env && hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_refine, kThreads, 0) == hipSuccess && nb > 0)
+            G = std::min<uint32_t>(cap, (uint32_t)(nb * ncu) / njobs);
+        if (G < 2) G = 1;
+        // the CUs the teams leave free get roaming helpers (ALVRL_REFINE_ROAM=0: none)
+        const char* re = std::getenv("ALVRL_REFINE_ROAM");
+        if (cap > 1 && nb > 0 && (!re || std::atoi(re) != 0) && (uint32_t)(nb * ncu) > njobs * G)
+            nroam = std::min<uint32_t>((uint32_t)(nb * ncu) - njobs * G, 1024u);
+    }
+    const bool team_on = G > 1 || nroam > 0;
+    // finished leaders and helpers roam too: their split scratch is sized for
+    // the largest job
+    const bool roam_on = team_on && !(std::getenv("ALVRL_REFINE_ROAM") && std::atoi(std::getenv("ALVRL_REFINE_ROAM")) == 0);
+    uint32_t Rmax = 0;
+    for (uint32_t j = 0; j < njobs; j++) Rmax = std::max(Rmax, jobs[j].nrows);
     auto job_bytes = [&](const HostJob& H) {
-        const uint32_t R = H.nrows;
+        const uint32_t R = roam_on ? Rmax : H.nrows;
         return align_up(N * 4) * 2 + align_up(N * sizeof(CNode)) * 2 + align_up(N * 4) * 2 +
                align_up((size_t)R * 4) + align_up(N * 8) * 2 + align_up(N * 4) * 4 +
                align_up((size_t)6 * R * 8) + align_up((size_t)2 * 2 * kCH * ((R + 63) / 64) * 64 * 16) +
@@ -1850,7 +1889,7 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
         }
         JobDev& J = h_jobs[j];
         char* p = arena + job_off[j];
-        const uint32_t R = H.nrows;
+        const uint32_t R = H.nrows, Rw = roam_on ? Rmax : R;
         J.roff = d_roff + row_off[j]; J.rstride = d_rstride + row_off[j];
         J.locw = d_locw + row_off[j]; J.nrows = R;
         const unsigned long long* ho = &h_roff[row_off[j]];
@@ -1868,15 +1907,15 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
         J.sh_heap = (CNode*)p; p += align_up(N * sizeof(CNode));
         J.singles = (uint32_t*)p; p += align_up(N * 4);
         J.sh_singles = (uint32_t*)p; p += align_up(N * 4);
-        J.dir = (float*)p; p += align_up((size_t)R * 4);
+        J.dir = (float*)p; p += align_up((size_t)Rw * 4);
         J.keys0 = (unsigned long long*)p; p += align_up(N * 8);
         J.keys1 = (unsigned long long*)p; p += align_up(N * 8);
         J.fsu = (float*)p; p += align_up(N * 4);
         J.fsi = (float*)p; p += align_up(N * 4);
         J.feu = (float*)p; p += align_up(N * 4);
         J.fei = (float*)p; p += align_up(N * 4);
-        J.st = (double*)p; p += align_up((size_t)6 * R * 8);
-        J.bufM = (double*)p; p += align_up((size_t)2 * 2 * kCH * ((R + 63) / 64) * 64 * 16);   // T, 2 passes x 2 chunks
+        J.st = (double*)p; p += align_up((size_t)6 * Rw * 8);
+        J.bufM = (double*)p; p += align_up((size_t)2 * 2 * kCH * ((Rw + 63) / 64) * 64 * 16);   // T, 2 passes x 2 chunks
         J.bufV = nullptr;
         J.out_reps = (uint32_t*)p; p += align_up(N * 4);
         J.out_w = (float*)p; p += align_up(N * 4);
@@ -1891,31 +1930,8 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
             J.out_nclusters = (uint32_t*)p;
         }
     }
-    // Team size from the occupancy: teams of G workgroups for njobs jobs are
-    // resident together when njobs * G <= resident blocks; the rest of the
-    // resident capacity gets roaming helpers.  ALVRL_REFINE_TEAM=n caps G
-    // (1 = no speculation).
-    const char* bs_env = std::getenv("ALVRL_REFINE_BATCH");
-    uint32_t G = 1, nroam = 0;
-    {
-        int ncu = 0, nb = 0, dev = 0;
-        const char* te = std::getenv("ALVRL_REFINE_TEAM");
-        const uint32_t cap = te ? (uint32_t)std::max(1, std::atoi(te)) : 8u;
-        if (!bs_env && hipGetDevice(&dev) == hipSuccess &&
-            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_refine, kThreads, 0) == hipSuccess && nb > 0)
-            G = std::min<uint32_t>(cap, (uint32_t)(nb * ncu) / njobs);
-        if (G < 2) G = 1;
-        // the CUs the teams leave free get roaming helpers (ALVRL_REFINE_ROAM=0: none)
-        const char* re = std::getenv("ALVRL_REFINE_ROAM");
-        if (cap > 1 && nb > 0 && (!re || std::atoi(re) != 0) && (uint32_t)(nb * ncu) > njobs * G)
-            nroam = std::min<uint32_t>((uint32_t)(nb * ncu) - njobs * G, 1024u);
-    }
-    const bool team_on = G > 1 || nroam > 0;
     char* tarena = nullptr;
     size_t tbytes = 0;
-    uint32_t Rmax = 0;
-    for (uint32_t j = 0; j < njobs; j++) Rmax = std::max(Rmax, jobs[j].nrows);
     if (team_on) {
         auto helper_bytes = [&](uint32_t R) {
             return align_up((size_t)R * 4) + align_up((size_t)6 * R * 8) +
@@ -1923,7 +1939,7 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
         };
         const size_t team_fixed = align_up(N * 4) + align_up(N * 8) + align_up(N * sizeof(SplitRes)) +
                                   align_up((size_t)kQueue * 8) + align_up(16) + align_up((size_t)(G - 1) * sizeof(SplitWs));
-        for (uint32_t j = 0; j < njobs; j++) tbytes += team_fixed + (size_t)(G - 1) * helper_bytes(jobs[j].nrows);
+        for (uint32_t j = 0; j < njobs; j++) tbytes += team_fixed + (size_t)(G - 1) * helper_bytes(roam_on ? Rmax : jobs[j].nrows);
         tbytes += align_up((size_t)nroam * sizeof(SplitWs)) + (size_t)nroam * helper_bytes(Rmax);
         if (hipMalloc(&tarena, tbytes) != hipSuccess) { (void)hipGetLastError(); tarena = nullptr; G = 1; nroam = 0; }
     }
@@ -1935,7 +1951,7 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
             Team& T = h_jobs[j].team;
             T = Team{0u, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
             if (!tarena) continue;
-            const uint32_t R = jobs[j].nrows;
+            const uint32_t R = roam_on ? Rmax : jobs[j].nrows;
             char* q = tarena + to;
             T.helpers = (G - 1) + (nroam + njobs - 1) / njobs;
             T.spec = (uint32_t*)q; q += align_up(N * 4);
@@ -1979,6 +1995,7 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
     cm.Rt = reinterpret_cast<const float2*>(d_Rt); cm.ld = ld; cm.nvrl = nvrl;
     cm.njobs = njobs; cm.team = G;
     cm.nroam = nroam; cm.roam_ws = d_rws;
+    cm.roam_on = roam_on && tarena ? 1 : 0;
     {
         const char* sw = std::getenv("ALVRL_SPEC_WIDTH");
         cm.spec_width = sw ? (uint32_t)std::max(1, std::atoi(sw)) : 12u;   // profiles/r01/team: 6 -> 727 ms, 16 -> 713 ms
@@ -1995,8 +2012,11 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
     else
         cm.trace = nullptr;
     const char* tse = std::getenv("ALVRL_REFINE_TEAM_STATS");
-    if (team_on && tse && tse[0] == '1' && hipMalloc(&cm.tstat, TS_N * 8) == hipSuccess)
+    cm.jtime = nullptr;
+    if (team_on && tse && tse[0] == '1' && hipMalloc(&cm.tstat, TS_N * 8) == hipSuccess) {
         (void)hipMemsetAsync(cm.tstat, 0, TS_N * 8, s);
+        if (hipMalloc(&cm.jtime, (size_t)njobs * 3 * 8) != hipSuccess) cm.jtime = nullptr;
+    }
     {
         const char* sm = std::getenv("ALVRL_SPEC_MIN");
         cm.spec_min = sm ? (uint32_t)std::max(2, std::atoi(sm)) : 16u;
@@ -2082,6 +2102,25 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
                          G, nroam, njobs, h[TS_ENQ], h[TS_HSTART], h[TS_HDONE], h[TS_COMMIT], h[TS_STEAL],
                          h[TS_WAIT_TMO], h[TS_OWN], h[TS_LSIDE], h[TS_IDLE_EXIT]);
         hipFree(cm.tstat);
+        if (cm.jtime) {
+            std::vector<unsigned long long> jt((size_t)njobs * 3);
+            if (hipMemcpy(jt.data(), cm.jtime, jt.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
+                unsigned long long t0 = ~0ull;
+                for (uint32_t j = 0; j < njobs; j++) t0 = std::min(t0, jt[3 * j]);
+                std::vector<double> fin(njobs), dur(njobs);
+                for (uint32_t j = 0; j < njobs; j++) {
+                    fin[j] = (jt[3 * j + 2] - t0) * 1e-5;          // ms (100 MHz ticks)
+                    dur[j] = (jt[3 * j + 1] - jt[3 * j]) * 1e-5;
+                }
+                std::vector<double> f2 = fin;
+                std::sort(f2.begin(), f2.end());
+                const uint32_t jmax = (uint32_t)(std::max_element(fin.begin(), fin.end()) - fin.begin());
+                std::fprintf(stderr, "[refine team] job end ms: min %.1f p10 %.1f median %.1f p90 %.1f max %.1f "
+                             "(job %u, %u rows, refine %.1f ms)\n", f2.front(), f2[njobs / 10], f2[njobs / 2],
+                             f2[(njobs * 9) / 10], f2.back(), jmax, jobs[jmax].nrows, dur[jmax]);
+            }
+            hipFree(cm.jtime);
+        }
     }
     if (cm.prof) {
         unsigned long long h[PF_N];
