@@ -306,3 +306,52 @@ def test_false_color_modes(gpu_ok):
     _, a = frame("targetNumSlices=20;convergenceFalseColor=true")
     _, b = frame("targetNumSlices=20")
     assert np.array_equal(a, b)
+
+
+def test_team_mode_settings(gpu_ok):
+    """Speculative split teams (refine.hip team mode) under every knob: team
+    size, roaming helpers, speculation width and threshold, and a 1 ms bound
+    on every wait (leaders give up on running helpers and split themselves,
+    idle helpers leave).  The cluster lists must equal those of one workgroup
+    per slice bit for bit in every case."""
+    import os
+    import torch
+    import alvrl
+    w, h = 256, 192
+    scene = alvrl.scene_default(w, h)
+    vrls, pc = alvrl.trace_vrls(scene, 3000, seed=SEED_VRL)
+    keys = ("ALVRL_REFINE_TEAM", "ALVRL_REFINE_ROAM", "ALVRL_SPEC_WIDTH", "ALVRL_SPEC_MIN",
+            "ALVRL_REFINE_SPIN_MS")
+    saved = {k: os.environ.get(k) for k in keys}
+
+    def run(props, **env):
+        for k in keys:
+            os.environ.pop(k, None)
+        os.environ.update({k: str(v) for k, v in env.items()})
+        it = alvrl.Integrator(props + f";seed={SEED_RNG}", device=0)
+        it.set_vrls(vrls, pc)
+        it.preprocess(scene)
+        it.prepass(1)
+        cl = it.clusters()
+        it.close()
+        return cl
+
+    settings = [dict(ALVRL_REFINE_TEAM=2), dict(ALVRL_REFINE_TEAM=4, ALVRL_REFINE_ROAM=0),
+                dict(ALVRL_REFINE_TEAM=8), dict(ALVRL_SPEC_WIDTH=1, ALVRL_SPEC_MIN=2),
+                dict(ALVRL_SPEC_WIDTH=32, ALVRL_SPEC_MIN=2), dict(ALVRL_REFINE_SPIN_MS=1),
+                dict(ALVRL_REFINE_TEAM=3, ALVRL_REFINE_SPIN_MS=1, ALVRL_SPEC_MIN=2), {}]
+    try:
+        for props in ("targetNumSlices=40", "targetNumSlices=30;localUndersampling=10",
+                      "targetNumSlices=25;depthCorrection=0.8"):
+            ref = run(props, ALVRL_REFINE_TEAM=1)
+            for st in settings:
+                cl = run(props, **st)
+                for k in ref:
+                    assert np.array_equal(ref[k].view(np.uint32), cl[k].view(np.uint32)), (props, st, k)
+        torch.cuda.synchronize()
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
