@@ -56,6 +56,11 @@ CONFIGS = {
                desc="1024^2 smoke box, 100k VRLs, LightSlice fixed-depth (localUndersampling=100)"),
     "C4": dict(w=1024, h=1024, nvrl=100000, props="targetNumSlices=100;localUndersampling=-1",
                desc="1024^2 smoke box, 100k VRLs, Adaptive LightSlice refinement"),
+    # R is 65,536 rows x 1M VRLs x 8 B = 524 GB: only the slice-sharded pass fits
+    # (524/N GB per GPU), so C5 needs --shard slices on >= 4 GPUs
+    "C5": dict(w=2048, h=2048, nvrl=1000000, props="targetNumSlices=100;localUndersampling=-1",
+               desc="2048^2 smoke box, 1M VRLs, Adaptive LightSlice, slices and tiles over the GPUs",
+               min_world=4, shard="slices"),
 }
 
 
@@ -102,6 +107,10 @@ def main():
     if world != args.gpus and not (world == 1 and args.gpus == 1):
         if world == 1:
             raise SystemExit(f"--gpus {args.gpus} needs torch.distributed.run with {args.gpus} ranks")
+    cfg0 = CONFIGS[args.config]
+    if world < cfg0.get("min_world", 1) or (cfg0.get("shard") and args.shard != cfg0["shard"]):
+        raise SystemExit(f"{args.config} needs --shard {cfg0.get('shard', args.shard)} on >= "
+                         f"{cfg0.get('min_world', 1)} GPUs (R does not fit one GPU)")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
