@@ -133,6 +133,7 @@ struct Common {
     unsigned long long* trace;     // host-mapped per-block (phase << 32 | value), ALVRL_REFINE_TRACE=1
     uint32_t spec_width;           // heap entries examined per enqueue (0 = 2 * helpers + 2)
     uint32_t nroam;                // roaming helpers (after the teams): serve every job's queue
+    int var_v3;                    // split variances on variance_split_v3 (ALVRL_VAR_V3=0: the older engine)
     int roam_on;                   // finished leaders and helpers roam too (scratch sized for Rmax)
     const SplitWs* roam_ws;        // [nroam] their scratch, sized for the largest job
 };
@@ -176,6 +177,12 @@ struct Prof {
     }
     __device__ void count(int id, unsigned long long v) { if (p && threadIdx.x == 0) atomicAdd(&p[id], v); }
 };
+// split-size histogram after the phase totals: per log2(columns) bucket
+// (count, split cycles, variance cycles, cycles before the projections)
+constexpr int kPfBuckets = 18;
+constexpr int kPfWaveBusy = PF_N + 4 * kPfBuckets;   // per-wave busy cycles in the variance passes (+ 8 wall)
+constexpr int kPfTotal = kPfWaveBusy + 3 * kWaves;
+__device__ __forceinline__ int pf_bucket(uint32_t m) { return min(kPfBuckets - 1, 31 - (int)__builtin_clz(max(m, 1u))); }
 
 // Per-column coefficients of the variance recurrence, read as broadcasts.
 struct Coef { double w, Wo, a, bb, rw, Wn, rWn; uint32_t vrl, pad; };
@@ -217,6 +224,11 @@ template <typename T>
 __device__ __forceinline__ const __attribute__((address_space(1))) T* gp(const T* p)
 {
     return (const __attribute__((address_space(1))) T*)p;
+}
+template <typename T>
+__device__ __forceinline__ __attribute__((address_space(1))) T* gpw(T* p)
+{
+    return (__attribute__((address_space(1))) T*)p;
 }
 __device__ __forceinline__ float2 ldg2(const float2* base, size_t i)
 {
@@ -656,7 +668,10 @@ __device__ __noinline__ void variance_passes_t(const JobDev& J, const Common& cm
 
     constexpr int NQ = kCH / 4;                      // columns per wave per chunk in phase 2
     // phase 1 of chunk k: entries in cur, chunk k+2's into pre
+    const bool wprof = cm.prof != nullptr;
+    long long wbusy = 0, wred = 0, wwall0 = wprof ? (long long)clock64() : 0;
     auto step = [&](uint32_t k, float2* cur, float2* pre) {
+        const long long ws0 = wprof ? (long long)clock64() : 0;
         const uint32_t c0 = k * kCH, cn = cn_of(k);
         const Coef* cf = V.cf[k % 4];
         double2* Tk = T + (size_t)(k & 1) * tsz;
@@ -724,11 +739,13 @@ __device__ __noinline__ void variance_passes_t(const JobDev& J, const Common& cm
                 st[r] = sum; st[R + r] = M; st[2 * R + r] = Vs;
             }
         }
+        if (wprof) wbusy += (long long)clock64() - ws0;
         __syncthreads();
         if (pf) { t1 = clock64(); trc += t1 - t0; t0 = t1; }
     };
     // phase 2: reduce chunks kf .. kf+nk-1 (nk <= 2) into the staging sums
     auto reduce = [&](uint32_t kf, uint32_t nk) {
+        const long long ws0 = wprof ? (long long)clock64() : 0;
         if (active) {
             double pz[4 * NQ];                       // [pu of 2*NQ columns, pi of 2*NQ columns]
 #pragma unroll
@@ -766,6 +783,7 @@ __device__ __noinline__ void variance_passes_t(const JobDev& J, const Common& cm
                 }
             }
         }
+        if (wprof) wred += (long long)clock64() - ws0;
         __syncthreads();
         if (pf) { t1 = clock64(); trd += t1 - t0; t0 = t1; }
     };
@@ -777,6 +795,11 @@ __device__ __noinline__ void variance_passes_t(const JobDev& J, const Common& cm
         if (k + 2 < nch) { step(k + 2, bufC, bufB); after(k + 2); }
     }
     if (FU && (nch & 1)) reduce(nch - 1, 1);
+    if (wprof && lane == 0 && m >= 4096) {
+        atomicAdd(&cm.prof[kPfWaveBusy + tid / 64], (unsigned long long)wbusy);
+        atomicAdd(&cm.prof[kPfWaveBusy + kWaves + tid / 64], (unsigned long long)((long long)clock64() - wwall0));
+        atomicAdd(&cm.prof[kPfWaveBusy + 2 * kWaves + tid / 64], (unsigned long long)wred);
+    }
     // the last pair's sums, the final variances
     if (FU && active && w == 3 && nch > 0 && lane < 2u * kCH) {
         const uint32_t kf = (nch & 1) ? nch - 1 : nch - 2;
@@ -808,6 +831,369 @@ __device__ __noinline__ void variance_passes_t(const JobDev& J, const Common& cm
     if (pf) { pf->count(PF_V_COEF, tc); pf->count(PF_V_REC, trc); pf->count(PF_V_RED, trd); }
 }
 
+
+// ---------------------------------------------- split variance engine --
+// The two calculateClusterVariance passes of a split (forward over base[0..m)
+// and backward, with per-prefix outputs), for local matrices of <= 3 row
+// blocks.  Same arithmetic, same operation order and the same row-reduction
+// order as variance_passes_t; what changes is the schedule:
+//  * each pass has 3 row waves (block b, lane = row mod 64) and one
+//    coefficient wave (pass 0: wave 3, pass 1: wave 4, so that the f64 work
+//    spreads over the four SIMDs);
+//  * one barrier per chunk: during chunk k the row waves run the recurrence
+//    of chunk k (T[k & 1]) and issue the entries of chunk k+2, while the
+//    coefficient wave reduces chunk k-1 (T[(k-1) & 1]) and forms the
+//    coefficients of chunk k+3;
+//  * coefficients are stored per chunk as SoA (two columns of one
+//    coefficient per ds_read_b128);
+//  * the 16 row sums of a chunk (pu, pi of 8 columns) are reduced with a
+//    transposed halving tree: at every level the pairs p[l] + p[l+off] of
+//    the shared tree are formed for two sums at once, the second in the lanes
+//    the tree leaves idle (permlane32/16 swaps, DPP row rotations), so the
+//    additions and their operand order are exactly those of tree_dn.
+// Coefficients of 64 consecutive columns (8 chunks) of one pass, SoA so a row
+// wave reads two columns' worth of one coefficient with one ds_read_b128.
+constexpr int kCB64 = 64;
+struct CoefBlock { double w[kCB64], Wo[kCB64], a[kCB64], bb[kCB64], rw[kCB64], Wn[kCB64], rWn[kCB64]; uint32_t vrl[kCB64]; };
+constexpr uint32_t kSplitTBytes = 2u * 2u * kCH * 3u * 64u * sizeof(double2);     // [pass][k & 1][c][block][lane]
+constexpr uint32_t kSplitStageBytes = 2u * 2u * 2u * kCB64 * sizeof(float);      // [pass][block & 1][u|i][64]
+constexpr uint32_t kSplitPoolBytes = kSplitTBytes + 2u * 2u * sizeof(CoefBlock) + kSplitStageBytes;
+static_assert(kSplitPoolBytes <= kPoolBytes, "split variance engine: pool");
+
+__device__ __forceinline__ double dbl_of(uint32_t hi, uint32_t lo)
+{
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+__device__ __forceinline__ uint32_t lo_of(double d) { return (uint32_t)(unsigned long long)__double_as_longlong(d); }
+__device__ __forceinline__ uint32_t hi_of(double d) { return (uint32_t)((unsigned long long)__double_as_longlong(d) >> 32); }
+// lanes 0-31: A[l] + A[l+32]; lanes 32-63: B[l-32] + B[l]
+__device__ __forceinline__ double swap32_add(double A, double B)
+{
+    const auto lo = __builtin_amdgcn_permlane32_swap(lo_of(A), lo_of(B), false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap(hi_of(A), hi_of(B), false, false);
+    return dbl_of(hi[0], lo[0]) + dbl_of(hi[1], lo[1]);
+}
+// per 32 lanes: row 0: A[l] + A[l+16]; row 1: B[l-16] + B[l]
+__device__ __forceinline__ double swap16_add(double A, double B)
+{
+    const auto lo = __builtin_amdgcn_permlane16_swap(lo_of(A), lo_of(B), false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap(hi_of(A), hi_of(B), false, false);
+    return dbl_of(hi[0], lo[0]) + dbl_of(hi[1], lo[1]);
+}
+// per 16 lanes: lanes 0-7: P[l] + P[l+8]; lanes 8-15: Q[l-8] + Q[l]
+__device__ __forceinline__ double pair8_add(double P, double Q, uint32_t lane)
+{
+    const bool lo = (lane & 8) == 0;
+    const double X = lo ? P : Q, Y = lo ? Q : P;
+    const uint32_t zl = (uint32_t)__builtin_amdgcn_mov_dpp((int)lo_of(Y), 0x128, 0xF, 0xF, false);   // row_ror:8
+    const uint32_t zh = (uint32_t)__builtin_amdgcn_mov_dpp((int)hi_of(Y), 0x128, 0xF, 0xF, false);
+    return X + dbl_of(zh, zl);
+}
+// per 8 lanes: lanes 0-3: P[l] + P[l+4]; lanes 4-7: Q[l-4] + Q[l]
+__device__ __forceinline__ double pair4_add(double P, double Q, uint32_t lane)
+{
+    const bool lo = (lane & 4) == 0;
+    const double X = lo ? P : Q, Y = lo ? Q : P;
+    const uint32_t al = (uint32_t)__builtin_amdgcn_mov_dpp((int)lo_of(Y), 0x104, 0xF, 0xF, false);   // row_shl:4
+    const uint32_t ah = (uint32_t)__builtin_amdgcn_mov_dpp((int)hi_of(Y), 0x104, 0xF, 0xF, false);
+    const uint32_t bl = (uint32_t)__builtin_amdgcn_mov_dpp((int)lo_of(Y), 0x114, 0xF, 0xF, false);   // row_shr:4
+    const uint32_t bh = (uint32_t)__builtin_amdgcn_mov_dpp((int)hi_of(Y), 0x114, 0xF, 0xF, false);
+    return X + (lo ? dbl_of(ah, al) : dbl_of(bh, bl));
+}
+// v[2c + h] (c < 8: column, h: 0 = pu, 1 = pi) -> the shared-order total of
+// value (c, h) in lane 32h + 16(c & 1) + 8((c >> 1) & 1) + 4(c >> 2)
+__device__ __forceinline__ double tree16_transposed(const double* v, uint32_t lane)
+{
+    double u[8], x[4], y[2];
+#pragma unroll
+    for (int i = 0; i < 8; i++) u[i] = swap32_add(v[2 * i], v[2 * i + 1]);
+#pragma unroll
+    for (int i = 0; i < 4; i++) x[i] = swap16_add(u[2 * i], u[2 * i + 1]);
+#pragma unroll
+    for (int i = 0; i < 2; i++) y[i] = pair8_add(x[2 * i], x[2 * i + 1], lane);
+    double z = pair4_add(y[0], y[1], lane);
+    z = z + from_lane_plus_d<2>(z);
+    z = z + from_lane_plus_d<1>(z);
+    return z;
+}
+
+// The coefficient wave's share of chunk_coefs for 8 columns of a 64-column
+// block: the running total W in the reference's order (v_readlane), the
+// column's lane (8j + c) keeping W before (Wo) and after (Wn) its weight.
+__device__ __forceinline__ void coef_chain8(double& W, double w, uint32_t j, uint32_t ncol, double& Wo, double& Wn)
+{
+    const uint32_t lane = threadIdx.x & 63;
+#pragma unroll
+    for (uint32_t c = 0; c < (uint32_t)kCH; c++) {
+        if (8 * j + c < ncol) {
+            const double wc = readlane_d(w, 8 * j + c);
+            if (lane == 8 * j + c) Wo = W;
+            W = W + wc;
+            if (lane == 8 * j + c) Wn = W;
+        }
+    }
+}
+// chunk_coefs' divisions for the block's columns, one lane each
+__device__ __forceinline__ void coef_block_finish(Ctl& C, double w, double Wo, double Wn, uint32_t vrl, uint32_t ncol,
+                                                  CoefBlock* out)
+{
+    const uint32_t lane = threadIdx.x & 63;
+    if (lane < ncol) {
+        if (!isfinite(w) || w <= 0) C.err = 1;
+        out->w[lane] = w; out->Wo[lane] = Wo; out->Wn[lane] = Wn;
+        out->a[lane] = (Wn * Wn) / (Wo * Wo);
+        const double rw = 1.0 / w;
+        out->rw[lane] = rw;
+        out->bb[lane] = (rw + 1.0 / Wo);
+        out->rWn[lane] = 1.0 / Wn;
+        (void)vrl;
+    }
+}
+
+__device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm, Ctl& C, const uint32_t* base,
+                                               uint32_t m, float* fu0, float* fi0, float* fu1, float* fi1,
+                                               unsigned char* pool)
+{
+    const uint32_t R = J.nrows;
+    const uint32_t NB = (R + 63) / 64;                 // <= 3
+    const int tid = threadIdx.x, wv = tid >> 6;
+    const uint32_t lane = (uint32_t)(tid & 63);
+    const int g = wv < 4 ? 0 : 1;
+    const bool coefw = wv == (g == 0 ? 3 : 4);
+    const uint32_t b0 = g == 0 ? (uint32_t)wv : (uint32_t)(wv - 5);      // row block (row waves)
+    float* fu = g == 0 ? fu0 : fu1;
+    float* fi = g == 0 ? fi0 : fi1;
+    VarGroup& V = C.vg[g];
+    constexpr size_t tsz = (size_t)kCH * 3 * 64;       // one chunk's terms
+    double2* T = reinterpret_cast<double2*>(pool) + (size_t)g * 2 * tsz;
+    CoefBlock* ring = reinterpret_cast<CoefBlock*>(pool + kSplitTBytes) + g * 2;
+    // prefix results of the last two 64-column blocks, stored out once per
+    // block: a global store in every chunk would make the next chunk's LDS
+    // reads wait for it (vmcnt(0) for the store's registers)
+    float* stg = reinterpret_cast<float*>(pool + kSplitTBytes + 4 * sizeof(CoefBlock)) + g * 2 * 2 * kCB64;
+    unsigned long long* cw = J.keys1;
+    const uint32_t nch = (m + kCH - 1) / kCH;
+    const uint32_t nblk = (m + kCB64 - 1) / kCB64;
+    auto cn_of = [&](uint32_t k) { return min((uint32_t)kCH, m - k * kCH); };
+    auto ncol_of = [&](uint32_t b) { return min((uint32_t)kCB64, m - b * kCB64); };
+    const bool wprof = cm.prof != nullptr;
+    long long wbusy = 0, wred = 0, wwall0 = wprof ? (long long)clock64() : 0;
+
+    // (vrl, weight) of every column of the cluster, gathered in parallel once
+    {
+        constexpr int B = 8;
+        for (uint32_t i0 = (uint32_t)tid; i0 < m; i0 += B * kThreads) {
+            uint32_t v[B];
+#pragma unroll
+            for (int b = 0; b < B; b++) v[b] = gp(base)[min(i0 + (uint32_t)b * kThreads, m - 1)];
+            float wt[B];
+#pragma unroll
+            for (int b = 0; b < B; b++) wt[b] = gp(J.colw)[v[b]];
+#pragma unroll
+            for (int b = 0; b < B; b++)
+                if (i0 + (uint32_t)b * kThreads < m)
+                    cw[i0 + (uint32_t)b * kThreads] = ((unsigned long long)__float_as_uint(wt[b]) << 32) | v[b];
+        }
+    }
+    __syncthreads();
+    // coefficient wave state: this lane's column of the block being formed
+    const auto cwp = gp(cw);
+    auto kw_of_blk = [&](uint32_t b) -> unsigned long long {
+        if (b >= nblk) return 0ull;
+        const uint32_t i = b * kCB64 + min(lane, ncol_of(b) - 1);
+        return cwp[g == 0 ? i : m - 1 - i];
+    };
+    double W = 0.0, cWo = 0.0, cWn = 0.0, cw_w = 1.0;
+    uint32_t cw_v = 0;
+    unsigned long long kwN = 0;
+    auto take = [&](unsigned long long kw, uint32_t b) {   // start forming block b
+        cw_v = (uint32_t)kw;
+        cw_w = lane < ncol_of(b) ? (double)__uint_as_float((uint32_t)(kw >> 32)) : 1.0;
+        cWo = 0.0; cWn = 0.0;
+        if (lane < ncol_of(b)) ring[b & 1].vrl[lane] = cw_v;
+    };
+    if (coefw) {
+        take(kw_of_blk(0), 0);
+        for (uint32_t j = 0; j < 8; j++) coef_chain8(W, cw_w, j, ncol_of(0), cWo, cWn);
+        coef_block_finish(C, cw_w, cWo, cWn, cw_v, ncol_of(0), &ring[0]);
+        kwN = kw_of_blk(1);
+    }
+    __syncthreads();
+
+    const bool roww = !coefw && b0 < NB;
+    // every lane of a row wave runs the recurrence (rows past R on row R-1's
+    // data: their terms are never reduced), so no load or store is predicated
+    const uint32_t r0 = min(b0 * 64 + lane, R - 1);
+    const RowRef rr0 = roww ? row_ref(J, r0) : RowRef{0, 0};
+    const double lw0 = roww ? J.locw[r0] : 0.0;
+
+    // coefficient wave: the 16 row sums of chunk kk, written out by their lanes
+    auto reduce = [&](uint32_t kk) {
+        const uint32_t cn = cn_of(kk);
+        const double2* Tk = T + (size_t)(kk & 1) * tsz;
+        double v[2 * kCH];
+#pragma unroll
+        for (int h4 = 0; h4 < 2; h4++) {            // 12 LDS reads in flight at a time (lgkmcnt holds 15)
+            double2 t[4][3];
+#pragma unroll
+            for (int c = 0; c < 4; c++)
+#pragma unroll
+                for (int b = 0; b < 3; b++) t[c][b] = Tk[((size_t)(4 * h4 + c) * 3 + b) * 64 + lane];
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                double pu = 0.0, pi = 0.0;
+                if ((uint32_t)(4 * h4 + c) < cn) {
+#pragma unroll
+                    for (int b = 0; b < 3; b++) {
+                        if ((uint32_t)b < NB && (uint32_t)b * 64 + lane < R) { pu = pu + t[c][b].x; pi = pi + t[c][b].y; }
+                    }
+                }
+                v[2 * (4 * h4 + c)] = pu; v[2 * (4 * h4 + c) + 1] = pi;
+            }
+        }
+        const double z = tree16_transposed(v, lane);
+        if ((lane & 3) == 0) {
+            const uint32_t h = lane >> 5, c = 4 * ((lane >> 2) & 1) + 2 * ((lane >> 3) & 1) + ((lane >> 4) & 1);
+            if (c < cn) {
+                const uint32_t n = kk * kCH + c;
+                const float f = h == 0 ? (n == 0 ? 0.0f : (float)z) : (float)z;
+                stg[(((kk / 8) & 1) * 2 + h) * kCB64 + (kk % 8) * kCH + c] = f;
+                if (n == m - 1) {
+                    if (h == 0) V.res_u = f; else V.res_i = f;
+                    if (!isfinite(f) || f < 0) C.err = 1;
+                }
+            }
+        }
+    };
+
+    auto flush = [&](uint32_t b) {                     // block b's prefix results, one column per lane
+        const uint32_t col = b * kCB64 + lane;
+        if (col < m) {                                 // global, not flat: a flat store would make
+            gpw(fu)[col] = stg[((b & 1) * 2 + 0) * kCB64 + lane];   // every LDS wait a vmcnt(0)
+            gpw(fi)[col] = stg[((b & 1) * 2 + 1) * kCB64 + lane];
+        }
+    };
+    if (coefw) {
+        // chunk k = 8B + j: reduce chunk k-1; form block B+1's coefficients
+        // (8 columns of the running total per chunk, the divisions at j = 7).
+        // Block B+2's (weight, vrl) is loaded at j = 0 and taken 8 chunks
+        // later (one block per outer iteration: no register copy of a load
+        // in flight, which would wait for it at once)
+        for (uint32_t B = 0; B * 8 < nch; B++) {
+            const uint32_t nb = B + 1;
+            if (nb < nblk) take(kwN, nb);
+            kwN = kw_of_blk(nb + 1);
+#pragma unroll 1
+            for (uint32_t j = 0; j < 8; j++) {
+                const uint32_t k = B * 8 + j;
+                if (k >= nch) break;
+                const long long ws0 = wprof ? (long long)clock64() : 0;
+#ifndef ALVRL_EXP_NORED
+                if (k >= 1) reduce(k - 1);
+#endif
+                if (j == 0 && B >= 1) flush(B - 1);
+                if (nb < nblk) {
+                    coef_chain8(W, cw_w, j, ncol_of(nb), cWo, cWn);
+                    if (j == 7 || k == nch - 1) coef_block_finish(C, cw_w, cWo, cWn, cw_v, ncol_of(nb), &ring[nb & 1]);
+                }
+                if (wprof) wred += (long long)clock64() - ws0;
+                __syncthreads();
+            }
+        }
+        reduce(nch - 1);
+        flush((nch - 1) / 8);
+    } else if (roww) {
+        double sum0 = 0.0, M0 = 0.0, V0 = 0.0;
+        float2 bufA[kCH], bufB[kCH], bufC[kCH];
+        // a register copy: cm is reached through a generic pointer, and a flat
+        // reload after every barrier would wait for every load in flight
+        const float2* const Rt = cm.Rt + rr0.base;
+        const size_t rstride = rr0.stride;
+        auto load_chunk = [&](uint32_t k, float2* dst) {    // ids from the LDS ring
+            const uint32_t* ids = &ring[(k / 8) & 1].vrl[(k % 8) * kCH];
+            const uint32_t cn = cn_of(k);
+#pragma unroll
+#ifdef ALVRL_EXP_NOLOAD
+            for (int c = 0; c < kCH; c++) dst[c] = make_float2((float)ids[(uint32_t)c < cn ? c : 0] * 1e-7f + (float)lane * 1e-9f, 0.25f);
+#else
+            for (int c = 0; c < kCH; c++) dst[c] = ldg2(Rt, (size_t)ids[(uint32_t)c < cn ? c : 0] * rstride);
+#endif
+        };
+        load_chunk(0, bufA);
+        load_chunk(min(1u, nch - 1), bufB);
+        // chunk k: issue the entries of chunk k+2 (clamped: the last chunk is
+        // re-read, so the wait for chunk k is always "all but the 16 youngest"),
+        // run the recurrence of chunk k into T[k & 1]
+        auto step = [&](uint32_t k, float2* cur, float2* pre) {
+            const long long ws0 = wprof ? (long long)clock64() : 0;
+            const uint32_t c0 = k * kCH, cn = cn_of(k);
+            const CoefBlock& q = ring[(k / 8) & 1];
+            const uint32_t o = (k % 8) * kCH;
+            double2* Tk = T + (size_t)(k & 1) * tsz + (size_t)b0 * 64 + lane;
+            load_chunk(min(k + 2, nch - 1), pre);
+            if (cn == (uint32_t)kCH && k > 0) {            // full chunk, no first column: no guards
+                double2 w2[4], o2[4], a2[4], bb2[4], rw2[4], n2[4], rn2[4];
+#pragma unroll
+                for (int p = 0; p < 4; p++) {
+                    w2[p] = *reinterpret_cast<const double2*>(&q.w[o + 2 * p]);
+                    o2[p] = *reinterpret_cast<const double2*>(&q.Wo[o + 2 * p]);
+                    a2[p] = *reinterpret_cast<const double2*>(&q.a[o + 2 * p]);
+                    bb2[p] = *reinterpret_cast<const double2*>(&q.bb[o + 2 * p]);
+                    rw2[p] = *reinterpret_cast<const double2*>(&q.rw[o + 2 * p]);
+                    n2[p] = *reinterpret_cast<const double2*>(&q.Wn[o + 2 * p]);
+                    rn2[p] = *reinterpret_cast<const double2*>(&q.rWn[o + 2 * p]);
+                }
+#pragma unroll
+                for (int p = 0; p < 4; p++) {
+                    {
+                        const double x = (double)cur[2 * p].x;
+                        const double tmp = w2[p].x * sum0 - o2[p].x * x;
+                        M0 = a2[p].x * M0 + bb2[p].x * (tmp * tmp);
+                        V0 = V0 + (double)cur[2 * p].y * rw2[p].x;
+                        sum0 = sum0 + x;
+                        Tk[(size_t)(2 * p) * 3 * 64] = make_double2(lw0 * (M0 * rn2[p].x), lw0 * (V0 * n2[p].x));
+                    }
+                    {
+                        const double x = (double)cur[2 * p + 1].x;
+                        const double tmp = w2[p].y * sum0 - o2[p].y * x;
+                        M0 = a2[p].y * M0 + bb2[p].y * (tmp * tmp);
+                        V0 = V0 + (double)cur[2 * p + 1].y * rw2[p].y;
+                        sum0 = sum0 + x;
+                        Tk[(size_t)(2 * p + 1) * 3 * 64] = make_double2(lw0 * (M0 * rn2[p].y), lw0 * (V0 * n2[p].y));
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int c = 0; c < kCH; c++) {
+                    if ((uint32_t)c < cn) {
+                        const double x = (double)cur[c].x;
+                        const double tmp = q.w[o + c] * sum0 - q.Wo[o + c] * x;
+                        if (c0 + c > 0) M0 = q.a[o + c] * M0 + q.bb[o + c] * (tmp * tmp);
+                        V0 = V0 + (double)cur[c].y * q.rw[o + c];
+                        sum0 = sum0 + x;
+                        Tk[(size_t)c * 3 * 64] = make_double2(lw0 * (M0 * q.rWn[o + c]), lw0 * (V0 * q.Wn[o + c]));
+                    }
+                }
+            }
+            if (wprof) wbusy += (long long)clock64() - ws0;
+            __syncthreads();
+        };
+        for (uint32_t k = 0; k < nch; k += 3) {
+            step(k, bufA, bufC);
+            if (k + 1 < nch) step(k + 1, bufB, bufA);
+            if (k + 2 < nch) step(k + 2, bufC, bufB);
+        }
+    } else {
+        for (uint32_t k = 0; k < nch; k++) __syncthreads();
+    }
+    if (wprof && lane == 0 && m >= 4096) {
+        atomicAdd(&cm.prof[kPfWaveBusy + wv], (unsigned long long)wbusy);
+        atomicAdd(&cm.prof[kPfWaveBusy + kWaves + wv], (unsigned long long)((long long)clock64() - wwall0));
+        atomicAdd(&cm.prof[kPfWaveBusy + 2 * kWaves + wv], (unsigned long long)wred);
+    }
+    __syncthreads();
+}
+
 __device__ void variance_passes(const JobDev& J, const Common& cm, Ctl& C, const uint32_t* base, uint32_t m,
                                 int npass, float* fu0, float* fi0, float* fu1, float* fi1, unsigned char* pool,
                                 Prof* pf = nullptr)
@@ -815,6 +1201,10 @@ __device__ void variance_passes(const JobDev& J, const Common& cm, Ctl& C, const
     const uint32_t NB = (J.nrows + 63) / 64;
     if (pf && (!pf->p || threadIdx.x != 0)) pf = nullptr;
     const bool lds = (size_t)2 * 2 * kCH * NB * 64 * sizeof(double2) <= kPoolBytes;
+    if (fu0 && npass == 2 && NB <= 3 && cm.var_v3) {
+        variance_split_v3(J, cm, C, base, m, fu0, fi0, fu1, fi1, pool);
+        return;
+    }
     if (fu0) {
         if (lds) variance_passes_t<true, true>(J, cm, C, base, m, npass, fu0, fi0, fu1, fi1, pool, pf);
         else variance_passes_t<false, true>(J, cm, C, base, m, npass, fu0, fi0, fu1, fi1, pool, pf);
@@ -1029,6 +1419,8 @@ __device__ void split(const JobDev& J, const Common& cm, Ctl& C, uint32_t begin,
     pf.mark(PF_CTRL);
     pf.count(PF_NSPLIT, 1);
     pf.count(PF_SPLITCOLS, end - begin);
+    const long long hb0 = pf.t;
+    long long hbv = 0, hbp = 0;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const uint32_t m = end - begin;
     const uint32_t R = J.nrows;
@@ -1120,6 +1512,7 @@ __device__ void split(const JobDev& J, const Common& cm, Ctl& C, uint32_t begin,
         __syncthreads();
     }
     pf.mark(PF_DIR);
+    hbp = pf.t - hb0;
     split_projections(J, cm, begin, m);
     __syncthreads();
     pf.mark(PF_PROJ);
@@ -1127,8 +1520,10 @@ __device__ void split(const JobDev& J, const Common& cm, Ctl& C, uint32_t begin,
     for (uint32_t i = tid; i < m; i += kThreads) J.vrls[begin + i] = (uint32_t)sorted[i];
     __syncthreads();
     pf.mark(PF_SORT);
+    const long long hv0 = pf.p && tid == 0 ? (long long)clock64() : 0;
     variance_passes(J, cm, C, J.vrls + begin, m, 2, J.fsu, J.fsi, J.feu, J.fei,
                     reinterpret_cast<unsigned char*>(lds), &pf);
+    if (pf.p && tid == 0) hbv = (long long)clock64() - hv0;
     pf.mark(PF_CVF);
     // argmin over split position (:664-675)
     float bv = INFINITY;
@@ -1167,6 +1562,13 @@ __device__ void split(const JobDev& J, const Common& cm, Ctl& C, uint32_t begin,
     }
     __syncthreads();
     pf.mark(PF_ARGMIN);
+    if (pf.p && tid == 0) {
+        const int b = pf_bucket(m);
+        atomicAdd(&pf.p[PF_N + 4 * b], 1ull);
+        atomicAdd(&pf.p[PF_N + 4 * b + 1], (unsigned long long)(pf.t - hb0));
+        atomicAdd(&pf.p[PF_N + 4 * b + 2], (unsigned long long)hbv);
+        atomicAdd(&pf.p[PF_N + 4 * b + 3], (unsigned long long)hbp);
+    }
 }
 
 // ------------------------------------------------------- team mode --
@@ -2025,9 +2427,13 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
     cm.seed = seed; cm.pass = pass;
     cm.prof = nullptr;
     cm.entries = d_entries;
+    {
+        const char* vv = std::getenv("ALVRL_VAR_V3");
+        cm.var_v3 = !(vv && vv[0] == '0');
+    }
     const char* pe = std::getenv("ALVRL_REFINE_PROFILE");
-    if (pe && pe[0] == '1' && hipMalloc(&cm.prof, PF_N * 8) == hipSuccess)
-        (void)hipMemsetAsync(cm.prof, 0, PF_N * 8, s);
+    if (pe && pe[0] == '1' && hipMalloc(&cm.prof, kPfTotal * 8) == hipSuccess)
+        (void)hipMemsetAsync(cm.prof, 0, kPfTotal * 8, s);
     hipEvent_t e0 = nullptr, e1 = nullptr;
     e = hipEventCreate(&e0);
     if (e == hipSuccess) e = hipEventCreate(&e1);
@@ -2123,7 +2529,7 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
         }
     }
     if (cm.prof) {
-        unsigned long long h[PF_N];
+        unsigned long long h[kPfTotal];
         if (hipMemcpy(h, cm.prof, sizeof(h), hipMemcpyDeviceToHost) == hipSuccess) {
             unsigned long long tot = 0;
             for (int i = 0; i < PF_NSPLIT; i++) tot += h[i];
@@ -2131,6 +2537,21 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
             for (int i = 0; i < PF_N; i++)
                 std::fprintf(stderr, "  %-22s %16llu%s\n", kPfNames[i], h[i],
                              i < PF_NSPLIT ? (std::string("  ") + std::to_string(100.0 * h[i] / (tot ? tot : 1)).substr(0, 5) + "%").c_str() : "");
+            for (int w = 0; w < kWaves; w++)
+                std::fprintf(stderr, "  variance wave %d (clusters >= 4096 columns): step busy %llu, reduce busy %llu of %llu cycles (%.1f%%)\n", w,
+                             h[kPfWaveBusy + w], h[kPfWaveBusy + 2 * kWaves + w], h[kPfWaveBusy + kWaves + w],
+                             100.0 * h[kPfWaveBusy + w] / (h[kPfWaveBusy + kWaves + w] ? h[kPfWaveBusy + kWaves + w] : 1));
+            std::fprintf(stderr, "  split columns   #splits   cycles/split   variance/split   pre-proj/split   cycles/column   %%cycles\n");
+            unsigned long long stot = 0;
+            for (int b = 0; b < kPfBuckets; b++) stot += h[PF_N + 4 * b + 1];
+            for (int b = 0; b < kPfBuckets; b++) {
+                const unsigned long long n = h[PF_N + 4 * b];
+                if (!n) continue;
+                const double cs = (double)h[PF_N + 4 * b + 1] / n;
+                std::fprintf(stderr, "  [%6u,%6u) %9llu %14.0f %16.0f %16.0f %15.1f %8.2f\n", 1u << b, 2u << b, n, cs,
+                             (double)h[PF_N + 4 * b + 2] / n, (double)h[PF_N + 4 * b + 3] / n, cs / (1.5 * (1u << b)),
+                             100.0 * h[PF_N + 4 * b + 1] / (stot ? stot : 1));
+            }
         }
         hipFree(cm.prof);
     }

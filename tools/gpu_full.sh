@@ -9,7 +9,7 @@ T=${1:-run}
 cd "$R" && mkdir -p gpurun_out
 export TMPDIR=/tmp
 step() { echo "== $(date +%T) $*" >> gpurun_out/steps_$T.log; }
-step pytest && timeout -k 10 600 python -m pytest tests -m gpu -x -q -s > gpurun_out/pytest_$T.log 2>&1 \
+step pytest && timeout -k 10 600 python -u -m pytest tests -m gpu -x -v -s --timeout 120 --timeout-method thread > gpurun_out/pytest_$T.log 2>&1 \
  && step bench && timeout -k 10 600 python bench.py > gpurun_out/bench_$T.json 2> gpurun_out/bench_$T.err \
  && step rocprof && (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_$T" -o run --output-format csv -- python3 "$R/bench.py" --no-cpu-baseline > "$R/gpurun_out/prof_$T.log" 2>&1) \
  && step pmc && "$R/tools/pmc_traffic.sh" C4 \
