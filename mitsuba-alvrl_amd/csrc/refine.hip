@@ -230,6 +230,16 @@ __device__ __forceinline__ __attribute__((address_space(1))) T* gpw(T* p)
 {
     return (__attribute__((address_space(1))) T*)p;
 }
+// LDS views of pointers that noinline functions receive as generic ones:
+// through a generic pointer every access is a flat op, and a flat op makes
+// the next LDS wait also wait for every global load in flight (vmcnt(0)).
+typedef __attribute__((address_space(3))) unsigned long long lds_u64;
+typedef __attribute__((address_space(3))) float lds_f32;
+template <typename T>
+__device__ __forceinline__ __attribute__((address_space(3))) T* lp(T* p)
+{
+    return (__attribute__((address_space(3))) T*)p;
+}
 __device__ __forceinline__ float2 ldg2(const float2* base, size_t i)
 {
     const unsigned long long u = gp(reinterpret_cast<const unsigned long long*>(base))[i];
@@ -306,14 +316,14 @@ __device__ __forceinline__ float ws_block_wave(float x, uint32_t lane, float* to
 }
 __device__ __noinline__ uint32_t weighted_sample_wave(const float* wv, const float* colw, const uint32_t* ids,
                                                       uint32_t m, Smp& smp, int* err, uint32_t zero_at,
-                                                      float* prob)
+                                                      float* prob, bool wv_lds = false)
 {
     const uint32_t lane = threadIdx.x & 63;
     if (m == 0) { *err = 1; return 0; }
     if (m == 1) { if (prob) *prob = 1.0f; return 0; }
     auto ld = [&](uint32_t i) -> float {
         const uint32_t c = min(i, m - 1);
-        const float x = wv ? wv[c] : gp(colw)[gp(ids)[c]];
+        const float x = wv ? (wv_lds ? lp(wv)[c] : gp(wv)[c]) : gp(colw)[gp(ids)[c]];
         return (i >= m || i == zero_at) ? 0.0f : x;
     };
     const uint32_t nb = (m + 63) / 64;
@@ -348,7 +358,7 @@ __device__ __noinline__ uint32_t weighted_sample_wave(const float* wv, const flo
             cur = nxt;
         }
         if (prob) {
-            const float wi = idx == zero_at ? 0.0f : (wv ? wv[idx] : colw[ids[idx]]);
+            const float wi = idx == zero_at ? 0.0f : (wv ? (wv_lds ? lp(wv)[idx] : gp(wv)[idx]) : gp(colw)[gp(ids)[idx]]);
             *prob = wi / weightSum;
         }
     }
@@ -1231,13 +1241,16 @@ __device__ __forceinline__ unsigned long long proj_key(float p, uint32_t vrl)
 }
 
 // Sorts J.keys0[0..m); returns the buffer holding the result.
-__device__ __noinline__ unsigned long long* sort_keys(const JobDev& J, Ctl& C, uint32_t m, unsigned long long* lds)
+__device__ __noinline__ unsigned long long* sort_keys(const JobDev& J, Ctl& C, uint32_t m, unsigned long long* lds_g)
 {
+    lds_u64* const lds = lp(lds_g);
+    auto* const k0 = gpw(J.keys0);
+    auto* const Cn = lp(&C.cnt[0]);
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     if (m <= (uint32_t)kBitonicMax) {
         uint32_t n2 = 1;
         while (n2 < m) n2 <<= 1;
-        for (uint32_t i = tid; i < n2; i += kThreads) lds[i] = i < m ? J.keys0[i] : ~0ull;
+        for (uint32_t i = tid; i < n2; i += kThreads) lds[i] = i < m ? k0[i] : ~0ull;
         __syncthreads();
         for (uint32_t k = 2; k <= n2; k <<= 1) {
             for (uint32_t j = k >> 1; j > 0; j >>= 1) {
@@ -1252,7 +1265,7 @@ __device__ __noinline__ unsigned long long* sort_keys(const JobDev& J, Ctl& C, u
                 __syncthreads();
             }
         }
-        for (uint32_t i = tid; i < m; i += kThreads) J.keys0[i] = lds[i];
+        for (uint32_t i = tid; i < m; i += kThreads) k0[i] = lds[i];
         __syncthreads();
         return J.keys0;
     }
@@ -1262,7 +1275,7 @@ __device__ __noinline__ unsigned long long* sort_keys(const JobDev& J, Ctl& C, u
     {
         uint32_t lo_o = 0, hi_o = 0, lo_a = 0xFFFFFFFFu, hi_a = 0xFFFFFFFFu;
         for (uint32_t i = tid; i < m; i += kThreads) {
-            const unsigned long long k = J.keys0[i];
+            const unsigned long long k = k0[i];
             lo_o |= (uint32_t)k; hi_o |= (uint32_t)(k >> 32);
             lo_a &= (uint32_t)k; hi_a &= (uint32_t)(k >> 32);
         }
@@ -1272,8 +1285,8 @@ __device__ __noinline__ unsigned long long* sort_keys(const JobDev& J, Ctl& C, u
     __syncthreads();
     const unsigned long long vary = (((unsigned long long)(C.hi_or ^ C.hi_and)) << 32) |
                                     (unsigned long long)(C.lo_or ^ C.lo_and);
-    unsigned long long* src = J.keys0;
-    unsigned long long* dst = J.keys1;
+    auto* src = gpw(J.keys0);
+    auto* dst = gpw(J.keys1);
     for (int bit = 0; bit < 64; bit++) {
         if (!((vary >> bit) & 1ull)) continue;
         // total zeros
@@ -1294,11 +1307,11 @@ __device__ __noinline__ unsigned long long* sort_keys(const JobDev& J, Ctl& C, u
             const unsigned long long bz = __ballot(zero), bo = __ballot(one);
             const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
             const uint32_t rz = __popcll(bz & lt), ro = __popcll(bo & lt);
-            if (lane == 0) C.cnt[wave] = (uint32_t)__popcll(bz) | ((uint32_t)__popcll(bo) << 16);
+            if (lane == 0) Cn[wave] = (uint32_t)__popcll(bz) | ((uint32_t)__popcll(bo) << 16);
             __syncthreads();
             uint32_t pz = 0, po = 0, tz = 0, to = 0;
             for (int w = 0; w < kWaves; w++) {
-                const uint32_t cz = C.cnt[w] & 0xFFFFu, co = C.cnt[w] >> 16;
+                const uint32_t cz = Cn[w] & 0xFFFFu, co = Cn[w] >> 16;
                 if (w < wave) { pz += cz; po += co; }
                 tz += cz; to += co;
             }
@@ -1307,9 +1320,9 @@ __device__ __noinline__ unsigned long long* sort_keys(const JobDev& J, Ctl& C, u
             zbase += tz; obase += to;
             __syncthreads();
         }
-        unsigned long long* t = src; src = dst; dst = t;
+        auto* t = src; src = dst; dst = t;
     }
-    return src;
+    return (unsigned long long*)src;
 }
 
 // Projections of split() (:625-640): one wave per column, kCB columns per
@@ -1323,24 +1336,28 @@ __device__ __noinline__ void split_projections(const JobDev& J, const Common& cm
     const int wave = threadIdx.x >> 6;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t stride = kWaves * kCB;
+    const float2* const Rt = cm.Rt;                  // register copy (cm is behind a generic pointer)
+    auto* const k0 = gpw(J.keys0);
+    const auto* const vrls = gp(J.vrls);
+    const auto* const dir = gp(J.dir);
     if (R <= 64u * kRB) {
         float d[kRB];
         RowRef row[kRB];
 #pragma unroll
         for (int rb = 0; rb < kRB; rb++) {
             const uint32_t r = lane + 64u * rb;
-            d[rb] = r < R ? J.dir[r] : 0.0f;
+            d[rb] = r < R ? dir[r] : 0.0f;
             row[rb] = row_ref(J, r < R ? r : 0);
         }
         uint32_t vA[kCB], vB[kCB];
         float xA[kRB][kCB], xB[kRB][kCB];
         auto load = [&](uint32_t j0, uint32_t* v, float (*x)[kCB]) {
 #pragma unroll
-            for (int q = 0; q < kCB; q++) v[q] = gp(J.vrls)[begin + min(j0 + (uint32_t)q, m - 1)];
+            for (int q = 0; q < kCB; q++) v[q] = vrls[begin + min(j0 + (uint32_t)q, m - 1)];
 #pragma unroll
             for (int rb = 0; rb < kRB; rb++)
 #pragma unroll
-                for (int q = 0; q < kCB; q++) x[rb][q] = ldg2(cm.Rt, row[rb].base + (size_t)v[q] * row[rb].stride).x;
+                for (int q = 0; q < kCB; q++) x[rb][q] = ldg2(Rt, row[rb].base + (size_t)v[q] * row[rb].stride).x;
         };
         auto reduce = [&](uint32_t j0, const uint32_t* v, float (*x)[kCB]) {
             float pn[kCB], pp[kCB];
@@ -1366,7 +1383,7 @@ __device__ __noinline__ void split_projections(const JobDev& J, const Common& cm
             if (lane == 0) {
 #pragma unroll
                 for (int q = 0; q < kCB; q++)
-                    if (j0 + q < m) J.keys0[j0 + q] = proj_key(nc[q] != 0 ? pp[q] : 0.0f, v[q]);
+                    if (j0 + q < m) k0[j0 + q] = proj_key(nc[q] != 0 ? pp[q] : 0.0f, v[q]);
             }
         };
         uint32_t j0 = (uint32_t)wave * kCB;
@@ -1382,28 +1399,28 @@ __device__ __noinline__ void split_projections(const JobDev& J, const Common& cm
         for (uint32_t j0 = (uint32_t)wave * kCB; j0 < m; j0 += stride) {
             uint32_t vr[kCB];
 #pragma unroll
-            for (int q = 0; q < kCB; q++) vr[q] = J.vrls[begin + min(j0 + (uint32_t)q, m - 1)];
+            for (int q = 0; q < kCB; q++) vr[q] = vrls[begin + min(j0 + (uint32_t)q, m - 1)];
             float pn[kCB], pp[kCB];
 #pragma unroll
             for (int q = 0; q < kCB; q++) { pn[q] = 0.0f; pp[q] = 0.0f; }
             for (uint32_t r = lane; r < R; r += 64) {
                 const RowRef rw = row_ref(J, r);
 #pragma unroll
-                for (int q = 0; q < kCB; q++) { const float a = fabsf(ldg2(cm.Rt, rw.base + (size_t)vr[q] * rw.stride).x); pn[q] = pn[q] + a * a; }
+                for (int q = 0; q < kCB; q++) { const float a = fabsf(ldg2(Rt, rw.base + (size_t)vr[q] * rw.stride).x); pn[q] = pn[q] + a * a; }
             }
             float nc[kCB];
 #pragma unroll
             for (int q = 0; q < kCB; q++) nc[q] = sqrtf(__shfl(tree_f(pn[q]), 0, 64));
             for (uint32_t r = lane; r < R; r += 64) {
                 const RowRef rw = row_ref(J, r);
-                const float dd = J.dir[r];
+                const float dd = dir[r];
 #pragma unroll
-                for (int q = 0; q < kCB; q++) pp[q] = pp[q] + dd * (ldg2(cm.Rt, rw.base + (size_t)vr[q] * rw.stride).x / nc[q]);
+                for (int q = 0; q < kCB; q++) pp[q] = pp[q] + dd * (ldg2(Rt, rw.base + (size_t)vr[q] * rw.stride).x / nc[q]);
             }
 #pragma unroll
             for (int q = 0; q < kCB; q++) {
                 const float pr = tree_f(pp[q]);
-                if (lane == 0 && j0 + q < m) J.keys0[j0 + q] = proj_key(nc[q] != 0 ? pr : 0.0f, vr[q]);
+                if (lane == 0 && j0 + q < m) k0[j0 + q] = proj_key(nc[q] != 0 ? pr : 0.0f, vr[q]);
             }
         }
     }
@@ -1424,91 +1441,120 @@ __device__ void split(const JobDev& J, const Common& cm, Ctl& C, uint32_t begin,
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const uint32_t m = end - begin;
     const uint32_t R = J.nrows;
+    // register copies of the job's fields and of cm: both sit behind generic
+    // pointers, so every field read after a barrier would be a flat reload,
+    // and a flat op makes the next LDS wait wait for all loads in flight
+    const auto* const vrlsR = gp(J.vrls);
+    auto* const vrlsW = gpw(J.vrls);
+    const auto* const colwR = gp(J.colw);
+    auto* const dirW = gpw(J.dir);
+    float* const feiP = J.fei;
+    const auto* const fsuR = gp(J.fsu);
+    const auto* const fsiR = gp(J.fsi);
+    const auto* const feuR = gp(J.feu);
+    const auto* const feiR = gp(J.fei);
+    const uint32_t stage = J.stage_refine;
+    const uint32_t seed = cm.seed, pass = cm.pass;
+    const float2* const Rt = cm.Rt;
+    const int contig = J.contig;
+    const unsigned long long off0 = J.off0;
+    const uint32_t stride0 = J.stride0;
+    const auto* const roffR = gp(J.roff);
+    const auto* const rstrR = gp(J.rstride);
+    auto rowref = [&](uint32_t r) {
+        return contig ? RowRef{(size_t)(off0 + r), (size_t)stride0} : RowRef{(size_t)roffR[r], (size_t)rstrR[r]};
+    };
+    auto rmean = [&](RowRef rr, uint32_t v) { return ldg2(Rt, rr.base + (size_t)v * rr.stride).x; };
+    auto& Cs = *lp(&C);
     // the two centres (:597-602): weights gathered in parallel into contiguous
     // LDS (or scratch for large clusters), scanned by one lane
-    float* wv = (size_t)m * 4 <= kPoolBytes ? reinterpret_cast<float*>(lds) : J.fei;
+    const bool wv_lds = (size_t)m * 4 <= kPoolBytes;
+    float* wv = wv_lds ? reinterpret_cast<float*>(lds) : feiP;
     {
         constexpr int B = 8;
         for (uint32_t i0 = (uint32_t)tid; i0 < m; i0 += B * kThreads) {
             uint32_t v[B];
 #pragma unroll
-            for (int b = 0; b < B; b++) v[b] = gp(J.vrls)[begin + min(i0 + (uint32_t)b * kThreads, m - 1)];
+            for (int b = 0; b < B; b++) v[b] = vrlsR[begin + min(i0 + (uint32_t)b * kThreads, m - 1)];
             float x[B];
 #pragma unroll
-            for (int b = 0; b < B; b++) x[b] = gp(J.colw)[v[b]];
+            for (int b = 0; b < B; b++) x[b] = colwR[v[b]];
 #pragma unroll
             for (int b = 0; b < B; b++)
-                if (i0 + (uint32_t)b * kThreads < m) wv[i0 + (uint32_t)b * kThreads] = x[b];
+                if (i0 + (uint32_t)b * kThreads < m) {
+                    if (wv_lds) lp(wv)[i0 + (uint32_t)b * kThreads] = x[b];
+                    else gpw(wv)[i0 + (uint32_t)b * kThreads] = x[b];
+                }
         }
     }
     __syncthreads();
     if (wave == 0) {
         Smp smp;
-        smp.init(cm.seed, cm.pass, begin, end, J.stage_refine);
+        smp.init(seed, pass, begin, end, stage);
         int e = 0;
-        const uint32_t i1 = weighted_sample_wave(wv, nullptr, nullptr, m, smp, &e, 0xFFFFFFFFu, nullptr);
-        const uint32_t i2 = weighted_sample_wave(wv, nullptr, nullptr, m, smp, &e, i1, nullptr);   // colw[vrl1] = 0
+        const uint32_t i1 = weighted_sample_wave(wv, nullptr, nullptr, m, smp, &e, 0xFFFFFFFFu, nullptr, wv_lds);
+        const uint32_t i2 = weighted_sample_wave(wv, nullptr, nullptr, m, smp, &e, i1, nullptr, wv_lds);   // colw[vrl1] = 0
         if (lane == 0) {
-            if (e) C.err = 1;
-            C.vrl1 = J.vrls[begin + i1]; C.vrl2 = J.vrls[begin + i2]; C.draw_k = smp.k;
+            if (e) Cs.err = 1;
+            Cs.vrl1 = vrlsR[begin + i1]; Cs.vrl2 = vrlsR[begin + i2]; Cs.draw_k = smp.k;
         }
     }
     __syncthreads();
     pf.mark(PF_WSAMP);
-    const uint32_t vrl1 = C.vrl1, vrl2 = C.vrl2;
+    const uint32_t vrl1 = Cs.vrl1, vrl2 = Cs.vrl2;
     // |c1|, |c2|, |c2 - c1| (:607-616), rows in the shared order
     if (wave == 0) {
         float p1 = 0.0f, p2 = 0.0f, pd = 0.0f;
         for (uint32_t r = lane; r < R; r += 64) {
-            const RowRef rr = row_ref(J, r);
-            const float a = Rmean(cm, rr, vrl1), b = Rmean(cm, rr, vrl2);
+            const RowRef rr = rowref(r);
+            const float a = rmean(rr, vrl1), b = rmean(rr, vrl2);
             const float d = b - a;
             const float ua = fabsf(a), ub = fabsf(b), ud = fabsf(d);
             p1 = p1 + ua * ua; p2 = p2 + ub * ub; pd = pd + ud * ud;
         }
         p1 = tree_f(p1); p2 = tree_f(p2); pd = tree_f(pd);
-        if (lane == 0) { C.nrm3[0] = sqrtf(p1); C.nrm3[1] = sqrtf(p2); C.nrm3[2] = sqrtf(pd); }
+        if (lane == 0) { Cs.nrm3[0] = sqrtf(p1); Cs.nrm3[1] = sqrtf(p2); Cs.nrm3[2] = sqrtf(pd); }
     }
     __syncthreads();
     if (tid == 0) {
-        C.diffLen = C.nrm3[2];
-        C.degenerate = !(C.nrm3[0] != 0 && C.nrm3[1] != 0 && C.nrm3[2] != 0);
+        Cs.diffLen = Cs.nrm3[2];
+        Cs.degenerate = !(Cs.nrm3[0] != 0 && Cs.nrm3[1] != 0 && Cs.nrm3[2] != 0);
     }
     __syncthreads();
-    if (!C.degenerate) {
-        const float dl = C.diffLen;
+    if (!Cs.degenerate) {
+        const float dl = Cs.diffLen;
         for (uint32_t r = tid; r < R; r += kThreads) {
-            const RowRef rr = row_ref(J, r);
-            const float a = Rmean(cm, rr, vrl1), b = Rmean(cm, rr, vrl2);
-            J.dir[r] = (b - a) / dl;
+            const RowRef rr = rowref(r);
+            const float a = rmean(rr, vrl1), b = rmean(rr, vrl2);
+            dirW[r] = (b - a) / dl;
         }
         __syncthreads();
     } else {
-        uint32_t k = C.draw_k;
+        uint32_t k = Cs.draw_k;
         while (true) {
             for (uint32_t r = tid; r < R; r += kThreads) {
-                const float sx = draw_at(cm.seed, cm.pass, begin, end, J.stage_refine, k + 2 * r);
-                const float sy = draw_at(cm.seed, cm.pass, begin, end, J.stage_refine, k + 2 * r + 1);
-                J.dir[r] = det_std_normal_x(sx, sy);
+                const float sx = draw_at(seed, pass, begin, end, stage, k + 2 * r);
+                const float sy = draw_at(seed, pass, begin, end, stage, k + 2 * r + 1);
+                dirW[r] = det_std_normal_x(sx, sy);
             }
             __syncthreads();
             if (wave == 0) {
                 float p = 0.0f;
-                for (uint32_t r = lane; r < R; r += 64) { const float u = fabsf(J.dir[r]); p = p + u * u; }
+                for (uint32_t r = lane; r < R; r += 64) { const float u = fabsf(dirW[r]); p = p + u * u; }
                 p = tree_f(p);
-                if (lane == 0) C.nd = sqrtf(p);
+                if (lane == 0) Cs.nd = sqrtf(p);
             }
             __syncthreads();
-            if (C.nd != 0) break;
+            if (Cs.nd != 0) break;
             k += 2 * R;
-            if (k > C.draw_k + 64u * 2u * R) {   // hang guard (p ~ 2^-23 per retry)
-                if (tid == 0) C.err = 1;
+            if (k > Cs.draw_k + 64u * 2u * R) {   // hang guard (p ~ 2^-23 per retry)
+                if (tid == 0) Cs.err = 1;
                 __syncthreads();
                 break;
             }
         }
-        const float nd = C.nd != 0 ? C.nd : 1.0f;
-        for (uint32_t r = tid; r < R; r += kThreads) J.dir[r] = J.dir[r] / nd;
+        const float nd = Cs.nd != 0 ? Cs.nd : 1.0f;
+        for (uint32_t r = tid; r < R; r += kThreads) dirW[r] = dirW[r] / nd;
         __syncthreads();
     }
     pf.mark(PF_DIR);
@@ -1517,7 +1563,7 @@ __device__ void split(const JobDev& J, const Common& cm, Ctl& C, uint32_t begin,
     __syncthreads();
     pf.mark(PF_PROJ);
     const unsigned long long* sorted = sort_keys(J, C, m, lds);
-    for (uint32_t i = tid; i < m; i += kThreads) J.vrls[begin + i] = (uint32_t)sorted[i];
+    for (uint32_t i = tid; i < m; i += kThreads) vrlsW[begin + i] = (uint32_t)gp(sorted)[i];
     __syncthreads();
     pf.mark(PF_SORT);
     const long long hv0 = pf.p && tid == 0 ? (long long)clock64() : 0;
@@ -1529,7 +1575,7 @@ __device__ void split(const JobDev& J, const Common& cm, Ctl& C, uint32_t begin,
     float bv = INFINITY;
     uint32_t bi = 0xFFFFFFFFu;
     for (uint32_t i = 1 + tid; i < m; i += kThreads) {
-        const float v = J.fsu[i - 1] + J.fsi[i - 1] + J.feu[m - 1 - i] + J.fei[m - 1 - i];
+        const float v = fsuR[i - 1] + fsiR[i - 1] + feuR[m - 1 - i] + feiR[m - 1 - i];
         if (v < bv) { bv = v; bi = i; }
     }
 #pragma unroll
@@ -1538,26 +1584,26 @@ __device__ void split(const JobDev& J, const Common& cm, Ctl& C, uint32_t begin,
         const uint32_t oi = __shfl_down(bi, off, 64);
         if (lane < off && (ov < bv || (ov == bv && oi < bi))) { bv = ov; bi = oi; }
     }
-    if (lane == 0) { C.best_v[wave] = bv; C.best_i[wave] = bi; }
+    if (lane == 0) { Cs.best_v[wave] = bv; Cs.best_i[wave] = bi; }
     __syncthreads();
     if (tid == 0) {
         float v = INFINITY;
         uint32_t idx = 0xFFFFFFFFu;
         for (int w = 0; w < kWaves; w++)
-            if (C.best_v[w] < v || (C.best_v[w] == v && C.best_i[w] < idx)) { v = C.best_v[w]; idx = C.best_i[w]; }
+            if (Cs.best_v[w] < v || (Cs.best_v[w] == v && Cs.best_i[w] < idx)) { v = Cs.best_v[w]; idx = Cs.best_i[w]; }
         if (!commit) {
-            SplitRes r{idx, C.err | (idx == 0xFFFFFFFFu ? 1 : 0), 0.0f, 0.0f, 0.0f, 0.0f};
+            SplitRes r{idx, Cs.err | (idx == 0xFFFFFFFFu ? 1 : 0), 0.0f, 0.0f, 0.0f, 0.0f};
             if (idx != 0xFFFFFFFFu) {
-                r.fsu = J.fsu[idx - 1]; r.fsi = J.fsi[idx - 1];
-                r.feu = J.feu[m - 1 - idx]; r.fei = J.fei[m - 1 - idx];
+                r.fsu = fsuR[idx - 1]; r.fsi = fsiR[idx - 1];
+                r.feu = feuR[m - 1 - idx]; r.fei = feiR[m - 1 - idx];
             }
             *res = r;
         } else if (idx == 0xFFFFFFFFu) {
-            C.err = 1;
+            Cs.err = 1;
         } else {
             const uint32_t s = begin + idx;
-            add_cluster(J, C, begin, s, J.fsu[idx - 1], J.fsi[idx - 1]);
-            add_cluster(J, C, s, end, J.feu[m - 1 - idx], J.fei[m - 1 - idx]);
+            add_cluster(J, C, begin, s, fsuR[idx - 1], fsiR[idx - 1]);
+            add_cluster(J, C, s, end, feuR[m - 1 - idx], feiR[m - 1 - idx]);
         }
     }
     __syncthreads();
