@@ -1241,41 +1241,45 @@ __device__ __forceinline__ unsigned long long proj_key(float p, uint32_t vrl)
 }
 
 // Sorts J.keys0[0..m); returns the buffer holding the result.
-__device__ __noinline__ unsigned long long* sort_keys(const JobDev& J, Ctl& C, uint32_t m, unsigned long long* lds_g)
+typedef __attribute__((address_space(1))) unsigned long long glb_u64;
+
+// Bitonic sort of n <= kBitonicMax keys in LDS: in[0..n) -> out[0..n)
+__device__ __forceinline__ void bitonic_lds(lds_u64* lds, const glb_u64* in, glb_u64* out, uint32_t n)
 {
-    lds_u64* const lds = lp(lds_g);
-    auto* const k0 = gpw(J.keys0);
-    auto* const Cn = lp(&C.cnt[0]);
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    if (m <= (uint32_t)kBitonicMax) {
-        uint32_t n2 = 1;
-        while (n2 < m) n2 <<= 1;
-        for (uint32_t i = tid; i < n2; i += kThreads) lds[i] = i < m ? k0[i] : ~0ull;
-        __syncthreads();
-        for (uint32_t k = 2; k <= n2; k <<= 1) {
-            for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-                for (uint32_t i = tid; i < n2; i += kThreads) {
-                    const uint32_t ixj = i ^ j;
-                    if (ixj > i) {
-                        const unsigned long long a = lds[i], b = lds[ixj];
-                        const bool up = (i & k) == 0;
-                        if ((a > b) == up) { lds[i] = b; lds[ixj] = a; }
-                    }
+    const int tid = threadIdx.x;
+    uint32_t n2 = 1;
+    while (n2 < n) n2 <<= 1;
+    for (uint32_t i = tid; i < n2; i += kThreads) lds[i] = i < n ? in[i] : ~0ull;
+    __syncthreads();
+    for (uint32_t k = 2; k <= n2; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = tid; i < n2; i += kThreads) {
+                const uint32_t ixj = i ^ j;
+                if (ixj > i) {
+                    const unsigned long long a = lds[i], b = lds[ixj];
+                    const bool up = (i & k) == 0;
+                    if ((a > b) == up) { lds[i] = b; lds[ixj] = a; }
                 }
-                __syncthreads();
             }
+            __syncthreads();
         }
-        for (uint32_t i = tid; i < m; i += kThreads) k0[i] = lds[i];
-        __syncthreads();
-        return J.keys0;
     }
-    // varying bits
+    for (uint32_t i = tid; i < n; i += kThreads) out[i] = lds[i];
+    __syncthreads();
+}
+
+// 1-bit LSD radix over the bits that vary, n keys in src (dst: scratch of
+// the same size); returns the array that holds the sorted keys
+__device__ glb_u64* radix_sort(Ctl& C, glb_u64* src, glb_u64* dst, uint32_t n)
+{
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    auto* const Cn = lp(&C.cnt[0]);
     if (tid == 0) { C.lo_or = 0; C.hi_or = 0; C.lo_and = 0xFFFFFFFFu; C.hi_and = 0xFFFFFFFFu; }
     __syncthreads();
     {
         uint32_t lo_o = 0, hi_o = 0, lo_a = 0xFFFFFFFFu, hi_a = 0xFFFFFFFFu;
-        for (uint32_t i = tid; i < m; i += kThreads) {
-            const unsigned long long k = k0[i];
+        for (uint32_t i = tid; i < n; i += kThreads) {
+            const unsigned long long k = src[i];
             lo_o |= (uint32_t)k; hi_o |= (uint32_t)(k >> 32);
             lo_a &= (uint32_t)k; hi_a &= (uint32_t)(k >> 32);
         }
@@ -1285,22 +1289,19 @@ __device__ __noinline__ unsigned long long* sort_keys(const JobDev& J, Ctl& C, u
     __syncthreads();
     const unsigned long long vary = (((unsigned long long)(C.hi_or ^ C.hi_and)) << 32) |
                                     (unsigned long long)(C.lo_or ^ C.lo_and);
-    auto* src = gpw(J.keys0);
-    auto* dst = gpw(J.keys1);
     for (int bit = 0; bit < 64; bit++) {
         if (!((vary >> bit) & 1ull)) continue;
-        // total zeros
         if (tid == 0) C.zeros = 0;
         __syncthreads();
         uint32_t z = 0;
-        for (uint32_t i = tid; i < m; i += kThreads) z += ((src[i] >> bit) & 1ull) ? 0u : 1u;
+        for (uint32_t i = tid; i < n; i += kThreads) z += ((src[i] >> bit) & 1ull) ? 0u : 1u;
         atomicAdd(&C.zeros, z);
         __syncthreads();
         const uint32_t zeros = C.zeros;
         uint32_t zbase = 0, obase = zeros;
-        for (uint32_t t0 = 0; t0 < m; t0 += kThreads) {
+        for (uint32_t t0 = 0; t0 < n; t0 += kThreads) {
             const uint32_t i = t0 + tid;
-            const bool valid = i < m;
+            const bool valid = i < n;
             const unsigned long long k = valid ? src[i] : 0ull;
             const bool one = valid && ((k >> bit) & 1ull);
             const bool zero = valid && !one;
@@ -1322,7 +1323,89 @@ __device__ __noinline__ unsigned long long* sort_keys(const JobDev& J, Ctl& C, u
         }
         auto* t = src; src = dst; dst = t;
     }
-    return (unsigned long long*)src;
+    return src;
+}
+
+// The projection sort of split() (:641-648): sorts keys0[0..m) in place
+// (keys are unique, so every correct sort gives the same order).  Up to
+// kBitonicMax keys: one bitonic sort in LDS.  Larger clusters: a bucket pass
+// on the projection value (monotone: bucket = floor((p - pmin) * NB /
+// (pmax - pmin)), non-finite values at the ends) scatters the keys into
+// buckets of ~4k, each then sorted in LDS (a bucket above kBitonicMax, e.g.
+// many equal projections, takes the radix sort).
+constexpr uint32_t kSortBuckets = 1024;
+constexpr uint32_t kSortCtlBytes = 2 * kSortBuckets * 4;                 // counts, cursors
+constexpr uint32_t kBucketSortMax = (kPoolBytes - kSortCtlBytes) / 8 >= (uint32_t)kBitonicMax ? (uint32_t)kBitonicMax : 8192u;
+__device__ __forceinline__ float key_proj(uint32_t u)
+{
+    return __uint_as_float((u & 0x80000000u) ? (u & 0x7FFFFFFFu) : ~u);
+}
+__device__ __noinline__ unsigned long long* sort_keys(const JobDev& J, Ctl& C, uint32_t m, unsigned long long* lds_g)
+{
+    const int tid = threadIdx.x;
+    auto* const k0 = gpw(J.keys0);
+    auto* const k1 = gpw(J.keys1);
+    if (m <= (uint32_t)kBitonicMax) {
+        bitonic_lds(lp(lds_g), k0, k0, m);
+        return J.keys0;
+    }
+    auto* const cnt = lp(reinterpret_cast<uint32_t*>(lds_g));
+    auto* const cur = cnt + kSortBuckets;
+    auto lds_inc = [](__attribute__((address_space(3))) uint32_t* p) {
+        return __hip_atomic_fetch_add(p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+    lds_u64* const lds = lp(lds_g) + kSortCtlBytes / 8;
+    const uint32_t NB = min(kSortBuckets, (m + 4095) / 4096);
+    // finite range of the projections, as key words (monotone in p)
+    if (tid == 0) { C.lo_and = 0xFFFFFFFFu; C.hi_or = 0; }
+    for (uint32_t b = tid; b < NB; b += kThreads) cnt[b] = 0;
+    __syncthreads();
+    {
+        uint32_t lo = 0xFFFFFFFFu, hi = 0;
+        for (uint32_t i = tid; i < m; i += kThreads) {
+            const uint32_t u = (uint32_t)(k0[i] >> 32);
+            if (isfinite(key_proj(u))) { lo = min(lo, u); hi = max(hi, u); }
+        }
+        atomicMin(&C.lo_and, lo); atomicMax(&C.hi_or, hi);
+    }
+    __syncthreads();
+    const uint32_t ulo = C.lo_and, uhi = C.hi_or;
+    const bool any = ulo <= uhi;
+    const float plo = any ? key_proj(ulo) : 0.0f, phi = any ? key_proj(uhi) : 0.0f;
+    const float scale = phi > plo ? (float)NB / (phi - plo) : 0.0f;
+    auto bucket = [&](uint32_t u) -> uint32_t {
+        if (!any || u < ulo) return 0u;
+        if (u > uhi) return NB - 1;
+        const float x = (key_proj(u) - plo) * scale;
+        return min(NB - 1, (uint32_t)max(0.0f, x));
+    };
+    for (uint32_t i = tid; i < m; i += kThreads) lds_inc(&cnt[bucket((uint32_t)(k0[i] >> 32))]);
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t o = 0;
+        for (uint32_t b = 0; b < NB; b++) { cur[b] = o; o += cnt[b]; }
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < m; i += kThreads) {
+        const unsigned long long k = k0[i];
+        k1[lds_inc(&cur[bucket((uint32_t)(k >> 32))])] = k;
+    }
+    __syncthreads();
+    // cur[b] is now the end of bucket b
+    for (uint32_t b = 0; b < NB; b++) {
+        const uint32_t e = cur[b], n = cnt[b], o = e - n;
+        if (n == 0) continue;
+        if (n <= kBucketSortMax) {
+            bitonic_lds(lds, k1 + o, k0 + o, n);
+        } else {
+            glb_u64* r = radix_sort(C, k1 + o, k0 + o, n);
+            if (r != k0 + o) {
+                for (uint32_t i = tid; i < n; i += kThreads) k0[o + i] = r[i];
+                __syncthreads();
+            }
+        }
+    }
+    return J.keys0;
 }
 
 // Projections of split() (:625-640): one wave per column, kCB columns per
