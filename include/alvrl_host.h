@@ -166,6 +166,51 @@ ALVRL_API int alvrl_integrator_R(alvrl_integrator *it, float *out, uint64_t cap_
 ALVRL_API int alvrl_integrator_vrls(alvrl_integrator *it, float *soa, uint32_t cap, uint32_t *n,
                                     uint64_t *particles);
 
+/* ---- on-disk formats -------------------------------
+ * vrlClusterInfo stream (vrlIntegrator.cpp:29-101, the resource the
+ * reference ships to remote render workers): ULong counts, UInt ids, Float
+ * weights, little-endian.  pixel_to_slice is m_slices (y + H*x); per-slice
+ * lists as CSR (slice_off has nslices + 1 entries); the global-cluster and
+ * fall-back lists.  The reader fixes the reference's slip at :56-59 (the
+ * fall-back ids go to the id list, not the weights). */
+typedef struct alvrl_cluster_info alvrl_cluster_info;
+ALVRL_API int alvrl_cluster_info_write(const char *path, uint32_t npix, const uint32_t *pixel_to_slice,
+                                       uint32_t nslices, const uint32_t *slice_off, const uint32_t *reps,
+                                       const float *weights, uint32_t n_global, const uint32_t *global_reps,
+                                       const float *global_w, uint32_t n_fb, const uint32_t *fb_reps,
+                                       const float *fb_w);
+ALVRL_API int alvrl_cluster_info_read(const char *path, alvrl_cluster_info **out);
+ALVRL_API void alvrl_cluster_info_free(alvrl_cluster_info *ci);
+ALVRL_API int alvrl_cluster_info_sizes(const alvrl_cluster_info *ci, uint32_t *npix, uint32_t *nslices,
+                                       uint32_t *nreps, uint32_t *n_global, uint32_t *n_fb);
+/* any output may be NULL; sizes from alvrl_cluster_info_sizes */
+ALVRL_API int alvrl_cluster_info_get(const alvrl_cluster_info *ci, uint32_t *pixel_to_slice,
+                                     uint32_t *slice_off, uint32_t *reps, float *weights,
+                                     uint32_t *global_reps, float *global_w, uint32_t *fb_reps, float *fb_w);
+/* The integrator's cluster info after prepass, to a file; and the reverse:
+ * install a saved one for pass 'pass' (VRLs traced or reused as prepass
+ * would, no R build or refinement), as a remote worker renders with the
+ * m_ci it receives.  The file's pixel count must match the scene. */
+ALVRL_API int alvrl_integrator_save_cluster_info(alvrl_integrator *it, const char *path);
+ALVRL_API int alvrl_integrator_load_cluster_info(alvrl_integrator *it, const char *path, uint32_t pass);
+
+/* Single-part scanline OpenEXR, no compression, channels B/G/R, FLOAT
+ * (half = 0) or HALF (half = 1) -- the hdrfilm output of a pass; rgb is
+ * row-major W*H*3.  The reader takes files of this layout (rgb == NULL:
+ * size query). */
+ALVRL_API int alvrl_write_exr(const char *path, const float *rgb, int width, int height, int half);
+ALVRL_API int alvrl_read_exr(const char *path, float *rgb, uint64_t cap_floats, int *width, int *height);
+/* mtsutil rms (src/utils/rms.cpp:36-110): gamma, robust fraction dropped at
+ * both ends of the sorted deviations, relative = deviations / reference
+ * (zero-reference entries masked). */
+ALVRL_API int alvrl_image_rms(const float *sample, const float *reference, uint64_t n, double gamma,
+                              double robust_fraction, int relative, double *out);
+/* dumpPass file name (integrator.cpp:361-378) with the vrl integrator's
+ * passFileSuffix (vrlIntegrator.cpp:357-364) and hdrfilm's ".exr". */
+ALVRL_API int alvrl_pass_file_name(char *out, uint64_t cap, const char *dest, int pass, double prepass_cpu,
+                                   double prepass_wall, double render_cpu, double render_wall,
+                                   double vrls_preprocess, double vrls_render);
+
 #ifdef __cplusplus
 }
 #endif

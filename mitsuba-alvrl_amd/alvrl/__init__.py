@@ -477,6 +477,17 @@ def _host():
     L.alvrl_exchange_or.argtypes = [P(ExchangeDesc), u32, vp, u64]
     L.alvrl_exchange_clusters.argtypes = [P(ExchangeDesc), u32, u32, u32, vp, vp, vp, vp, vp, vp, vp, vp, vp,
                                           u64, P(u64)]
+    L.alvrl_cluster_info_write.argtypes = [C.c_char_p, u32, vp, u32, vp, vp, vp, u32, vp, vp, u32, vp, vp]
+    L.alvrl_cluster_info_read.argtypes = [C.c_char_p, P(vp)]
+    L.alvrl_cluster_info_free.argtypes = [vp]; L.alvrl_cluster_info_free.restype = None
+    L.alvrl_cluster_info_sizes.argtypes = [vp, P(u32), P(u32), P(u32), P(u32), P(u32)]
+    L.alvrl_cluster_info_get.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.alvrl_integrator_save_cluster_info.argtypes = [vp, C.c_char_p]
+    L.alvrl_integrator_load_cluster_info.argtypes = [vp, C.c_char_p, u32]
+    L.alvrl_write_exr.argtypes = [C.c_char_p, vp, i32, i32, i32]
+    L.alvrl_read_exr.argtypes = [C.c_char_p, vp, u64, P(i32), P(i32)]
+    L.alvrl_image_rms.argtypes = [vp, vp, u64, C.c_double, C.c_double, i32, P(C.c_double)]
+    L.alvrl_pass_file_name.argtypes = [C.c_char_p, u64, C.c_char_p, i32] + [C.c_double] * 6
     _host_bound = True
     return L
 
@@ -540,6 +551,75 @@ def write_vrl_file(path: str, soa: np.ndarray):
     _hcheck(_host().alvrl_write_vrl_file(path.encode(), _ptr(soa), soa.shape[1]))
 
 
+def write_cluster_info(path: str, info: dict):
+    """vrlClusterInfo stream (vrlIntegrator.cpp:66-101).  info: slices
+    (m_slices, y + H*x), slice_off / reps / weights (CSR), optional
+    global_reps / global_weights and fb_reps / fb_weights."""
+    u = lambda k: _np(info.get(k, np.zeros(0)), np.uint32)
+    f = lambda k: _np(info.get(k, np.zeros(0)), np.float32)
+    sl, so, rp, w = u("slices"), u("slice_off"), u("reps"), f("weights")
+    gr, gw, fr, fw = u("global_reps"), f("global_weights"), u("fb_reps"), f("fb_weights")
+    _hcheck(_host().alvrl_cluster_info_write(path.encode(), len(sl), _ptr(sl), max(0, len(so) - 1), _ptr(so),
+                                             _ptr(rp), _ptr(w), len(gr), _ptr(gr), _ptr(gw), len(fr),
+                                             _ptr(fr), _ptr(fw)))
+
+
+def read_cluster_info(path: str) -> dict:
+    """vrlClusterInfo(Stream*, InstanceManager*) (:29-64, fall-back ids fixed)."""
+    L = _host()
+    h = C.c_void_p()
+    _hcheck(L.alvrl_cluster_info_read(path.encode(), C.byref(h)))
+    try:
+        n = [C.c_uint32() for _ in range(5)]
+        _hcheck(L.alvrl_cluster_info_sizes(h, *[C.byref(x) for x in n]))
+        npix, ns, nr, ng, nfb = (x.value for x in n)
+        out = {"slices": np.zeros(npix, np.uint32), "slice_off": np.zeros(ns + 1, np.uint32),
+               "reps": np.zeros(nr, np.uint32), "weights": np.zeros(nr, np.float32),
+               "global_reps": np.zeros(ng, np.uint32), "global_weights": np.zeros(ng, np.float32),
+               "fb_reps": np.zeros(nfb, np.uint32), "fb_weights": np.zeros(nfb, np.float32)}
+        keys = ("slices", "slice_off", "reps", "weights", "global_reps", "global_weights", "fb_reps", "fb_weights")
+        _hcheck(L.alvrl_cluster_info_get(h, *[_ptr(out[k]) if out[k].size else None for k in keys]))
+        return out
+    finally:
+        L.alvrl_cluster_info_free(h)
+
+
+def write_exr(path: str, rgb: np.ndarray, half: bool = False):
+    """Uncompressed scanline OpenEXR, rgb of shape (H, W, 3)."""
+    rgb = _np(rgb, np.float32)
+    _hcheck(_host().alvrl_write_exr(path.encode(), _ptr(rgb), rgb.shape[1], rgb.shape[0], int(half)))
+
+
+def read_exr(path: str) -> np.ndarray:
+    L = _host()
+    w, h = C.c_int(), C.c_int()
+    _hcheck(L.alvrl_read_exr(path.encode(), None, 0, C.byref(w), C.byref(h)))
+    out = np.zeros((h.value, w.value, 3), np.float32)
+    _hcheck(L.alvrl_read_exr(path.encode(), _ptr(out), out.size, C.byref(w), C.byref(h)))
+    return out
+
+
+def image_rms(sample, reference, gamma: float = 1.0, robust_fraction: float = 0.0,
+              relative: bool = False) -> float:
+    """mtsutil rms (src/utils/rms.cpp)."""
+    a, b = _np(sample, np.float32).ravel(), _np(reference, np.float32).ravel()
+    if a.size != b.size:
+        raise ValueError("images differ in size")
+    r = C.c_double()
+    _hcheck(_host().alvrl_image_rms(_ptr(a), _ptr(b), a.size, gamma, robust_fraction, int(relative),
+                                    C.byref(r)))
+    return r.value
+
+
+def pass_file_name(dest: str, pass_: int, prepass_cpu: float, prepass_wall: float, render_cpu: float,
+                   render_wall: float, vrls_preprocess: float, vrls_render: float) -> str:
+    """dumpPass file name (integrator.cpp:361-378 + passFileSuffix)."""
+    buf = C.create_string_buffer(len(dest) + 256)
+    _hcheck(_host().alvrl_pass_file_name(buf, len(buf), dest.encode(), pass_, prepass_cpu, prepass_wall,
+                                         render_cpu, render_wall, vrls_preprocess, vrls_render))
+    return buf.value.decode()
+
+
 class Integrator:
     """vrlIntegrator pipeline (preprocess / prepass / render) on one device."""
 
@@ -586,6 +666,15 @@ class Integrator:
     def render(self, d_fb, rank: int = 0, world: int = 1, stream=None):
         _hcheck(self.L.alvrl_integrator_render(self.h, rank, world, _ptr(d_fb),
                                                C.c_void_p(stream) if stream else None))
+
+    def save_cluster_info(self, path: str):
+        """The vrlClusterInfo of the last prepass, to a file (vrlIntegrator.cpp:66-101)."""
+        _hcheck(self.L.alvrl_integrator_save_cluster_info(self.h, path.encode()))
+
+    def load_cluster_info(self, path: str, pass_: int = 0):
+        """Install a saved vrlClusterInfo for `pass_` instead of running the
+        prepass's R build and refinement (a remote worker's wakeup)."""
+        _hcheck(self.L.alvrl_integrator_load_cluster_info(self.h, path.encode(), pass_))
 
     def stats(self) -> dict:
         st = IntegratorStats()

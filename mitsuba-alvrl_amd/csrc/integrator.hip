@@ -234,6 +234,21 @@ struct alvrl_integrator {
         if (world > 1 && (!ex || !ex->allgather)) throw IntegError(ALVRL_ERR_INVALID, "world > 1 needs an alvrl_exchange");
         if (!have_scene) throw IntegError(ALVRL_ERR_STATE, "prepass before preprocess");
         const double tw = now_ms();
+        pass_vrls(pass);
+        st.slices_failed = 0;
+        st.fallback_built = 0;
+        st.ms_rbuild = st.ms_refine = st.ms_exchange = st.ms_refine_kernel = 0;
+        st.refine_entries = 0;
+        st.global_clusters = 0;
+        st.slices_local = 0;
+        st.rows_built = 0;
+        if (clustered) build_clusters(pass, rank, world, ex);
+        st.ms_prepass_wall = now_ms() - tw;
+    }
+
+    // the pass's VRLs on the device (:276-287): traced per pass unless preloaded
+    void pass_vrls(uint32_t pass)
+    {
         chk(alvrl_set_pass(ctx, pass), "alvrl_set_pass");
         // VRLs (:276-287): traced per pass unless preloaded from a file
         if (!vrls_from_file) {
@@ -250,15 +265,48 @@ struct alvrl_integrator {
         }
         st.vrls = vrls.n;
         st.particles = vrls.particle_count;
-        st.slices_failed = 0;
-        st.fallback_built = 0;
-        st.ms_rbuild = st.ms_refine = st.ms_exchange = st.ms_refine_kernel = 0;
-        st.refine_entries = 0;
-        st.global_clusters = 0;
-        st.slices_local = 0;
-        st.rows_built = 0;
-        if (clustered) build_clusters(pass, rank, world, ex);
-        st.ms_prepass_wall = now_ms() - tw;
+    }
+
+    // vrlClusterInfo out / in (vrlIntegrator.cpp:29-101): the state a remote
+    // worker receives instead of running the prepass (:353-354)
+    void save_cluster_info(const char* path) const
+    {
+        if (!clustered || slice_off.empty())
+            throw IntegError(ALVRL_ERR_STATE, "no cluster info: run a clustered prepass first");
+        chk_host(alvrl_cluster_info_write(path, (uint32_t)pixel_to_slice.size(), pixel_to_slice.data(),
+                                          (uint32_t)slice_off.size() - 1, slice_off.data(), reps.data(),
+                                          weights.data(), 0, nullptr, nullptr, (uint32_t)fb_reps.size(),
+                                          fb_reps.data(), fb_w.data()));
+    }
+
+    void load_cluster_info(const char* path, uint32_t pass)
+    {
+        if (!have_scene) throw IntegError(ALVRL_ERR_STATE, "load_cluster_info before preprocess");
+        alvrl_cluster_info* ci = nullptr;
+        chk_host(alvrl_cluster_info_read(path, &ci));
+        std::unique_ptr<alvrl_cluster_info, void (*)(alvrl_cluster_info*)> guard(ci, alvrl_cluster_info_free);
+        uint32_t npix = 0, ns = 0, nr = 0, ng = 0, nfb = 0;
+        chk_host(alvrl_cluster_info_sizes(ci, &npix, &ns, &nr, &ng, &nfb));
+        if (npix != (uint32_t)scene.width * (uint32_t)scene.height)
+            throw IntegError(ALVRL_ERR_INVALID, "cluster info: pixel count does not match the scene");
+        std::vector<uint32_t> p2s(npix), so(ns + 1), rp(nr), fr(nfb);
+        std::vector<float> w(nr), fw(nfb);
+        chk_host(alvrl_cluster_info_get(ci, p2s.data(), so.data(), rp.data(), w.data(), nullptr, nullptr,
+                                        fr.data(), fw.data()));
+        for (uint32_t s : p2s)
+            if (s != 0xFFFFFFFFu && s >= ns) throw IntegError(ALVRL_ERR_INVALID, "cluster info: slice id out of range");
+        pass_vrls(pass);
+        for (uint32_t v : rp)
+            if (v >= vrls.n) throw IntegError(ALVRL_ERR_INVALID, "cluster info: VRL id out of range");
+        for (uint32_t v : fr)
+            if (v >= vrls.n) throw IntegError(ALVRL_ERR_INVALID, "cluster info: VRL id out of range");
+        chk(alvrl_set_clusters(ctx, ns, so.data(), rp.data(), w.data(), fr.data(), fw.data(), nfb), "alvrl_set_clusters");
+        pixel_to_slice.swap(p2s);
+        slice_off.swap(so); reps.swap(rp); weights.swap(w); fb_reps.swap(fr); fb_w.swap(fw);
+        clustered = true;
+        cache_rank = 0xFFFFFFFFu;
+        st.slices = ns;
+        st.clusters_total = reps.size();
     }
 
     // Building R (:302-333) for the rows of the slices flagged in 'need'.  R is
@@ -719,6 +767,20 @@ ALVRL_API int alvrl_integrator_get_stats(alvrl_integrator* it, alvrl_integrator_
 }
 
 ALVRL_API alvrl_ctx* alvrl_integrator_ctx(alvrl_integrator* it) { return it ? it->ctx : nullptr; }
+
+ALVRL_API int alvrl_integrator_save_cluster_info(alvrl_integrator* it, const char* path)
+{
+    if (!it || !path) return ierr(ALVRL_ERR_INVALID, "alvrl_integrator_save_cluster_info: null argument");
+    GUARD({ it->save_cluster_info(path); });
+    return ALVRL_OK;
+}
+
+ALVRL_API int alvrl_integrator_load_cluster_info(alvrl_integrator* it, const char* path, uint32_t pass)
+{
+    if (!it || !path) return ierr(ALVRL_ERR_INVALID, "alvrl_integrator_load_cluster_info: null argument");
+    GUARD({ hchk(hipSetDevice(it->device), "hipSetDevice"); it->load_cluster_info(path, pass); });
+    return ALVRL_OK;
+}
 
 ALVRL_API uint32_t alvrl_integrator_num_slices(alvrl_integrator* it)
 {

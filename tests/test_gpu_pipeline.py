@@ -355,3 +355,39 @@ def test_team_mode_settings(gpu_ok):
                 os.environ.pop(k, None)
             else:
                 os.environ[k] = v
+
+
+def test_cluster_info_checkpoint(gpu_ok, tmp_path):
+    """vrlClusterInfo out of one integrator and into another (the resource the
+    reference ships to remote workers, vrlIntegrator.cpp:29-101, :353-354):
+    the second renders the same frame bit for bit without R build or
+    refinement; the frame goes through the EXR writer unchanged."""
+    import torch
+    import alvrl
+    w, h = 48, 32
+    scene = alvrl.scene_default(w, h)
+    vrls, pc = alvrl.trace_vrls(scene, 600, seed=SEED_VRL)
+    frames = []
+    for load in (False, True):
+        it = alvrl.Integrator(f"targetNumSlices=12;seed={SEED_RNG}", device=0)
+        it.set_vrls(vrls, pc)
+        it.preprocess(scene)
+        if load:
+            it.load_cluster_info(str(tmp_path / "ci.bin"), 0)
+            assert it.stats()["refine_entries"] == 0
+        else:
+            it.prepass(0)
+            it.save_cluster_info(str(tmp_path / "ci.bin"))
+        fb = torch.zeros(w * h * 3, dtype=torch.float32, device="cuda")
+        it.render(fb)
+        torch.cuda.synchronize()
+        frames.append(fb.cpu().numpy())
+        it.close()
+    assert frames[0].any()
+    assert np.array_equal(frames[0].view(np.uint32), frames[1].view(np.uint32))
+    ci = alvrl.read_cluster_info(str(tmp_path / "ci.bin"))
+    assert len(ci["slices"]) == w * h and len(ci["slice_off"]) == 13
+    p = str(tmp_path / alvrl.pass_file_name("smoke", 0, 0, 0, 0, 0, 0, 0).split("/")[-1])
+    alvrl.write_exr(p, frames[0].reshape(h, w, 3))
+    assert np.array_equal(alvrl.read_exr(p).ravel(), frames[0])
+    assert alvrl.image_rms(frames[1], frames[0]) == 0.0
