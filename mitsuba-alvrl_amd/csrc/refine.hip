@@ -960,8 +960,12 @@ __device__ __forceinline__ void coef_block_finish(Ctl& C, double w, double Wo, d
     }
 }
 
+// FU == false: only the final variances of npass passes (no prefix terms, no
+// reduction per chunk): the rows' final states go to J.st and one wave per
+// pass forms the two sums, as variance_passes_t does.
+template <bool FU>
 __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm, Ctl& C, const uint32_t* base,
-                                               uint32_t m, float* fu0, float* fi0, float* fu1, float* fi1,
+                                               uint32_t m, int npass, float* fu0, float* fi0, float* fu1, float* fi1,
                                                unsigned char* pool)
 {
     const uint32_t R = J.nrows;
@@ -969,7 +973,8 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
     const int tid = threadIdx.x, wv = tid >> 6;
     const uint32_t lane = (uint32_t)(tid & 63);
     const int g = wv < 4 ? 0 : 1;
-    const bool coefw = wv == (g == 0 ? 3 : 4);
+    const bool active = g < npass;
+    const bool coefw = active && wv == (g == 0 ? 3 : 4);
     const uint32_t b0 = g == 0 ? (uint32_t)wv : (uint32_t)(wv - 5);      // row block (row waves)
     float* fu = g == 0 ? fu0 : fu1;
     float* fi = g == 0 ? fi0 : fi1;
@@ -1030,7 +1035,7 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
     }
     __syncthreads();
 
-    const bool roww = !coefw && b0 < NB;
+    const bool roww = active && !coefw && b0 < NB;
     // every lane of a row wave runs the recurrence (rows past R on row R-1's
     // data: their terms are never reduced), so no load or store is predicated
     const uint32_t r0 = min(b0 * 64 + lane, R - 1);
@@ -1099,9 +1104,9 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
                 if (k >= nch) break;
                 const long long ws0 = wprof ? (long long)clock64() : 0;
 #ifndef ALVRL_EXP_NORED
-                if (k >= 1) reduce(k - 1);
+                if (FU && k >= 1) reduce(k - 1);
 #endif
-                if (j == 0 && B >= 1) flush(B - 1);
+                if (FU && j == 0 && B >= 1) flush(B - 1);
                 if (nb < nblk) {
                     coef_chain8(W, cw_w, j, ncol_of(nb), cWo, cWn);
                     if (j == 7 || k == nch - 1) coef_block_finish(C, cw_w, cWo, cWn, cw_v, ncol_of(nb), &ring[nb & 1]);
@@ -1110,8 +1115,12 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
                 __syncthreads();
             }
         }
-        reduce(nch - 1);
-        flush((nch - 1) / 8);
+        if (FU) {
+            reduce(nch - 1);
+            flush((nch - 1) / 8);
+        } else if (lane == 0) {
+            V.Wcur = W;
+        }
     } else if (roww) {
         double sum0 = 0.0, M0 = 0.0, V0 = 0.0;
         float2 bufA[kCH], bufB[kCH], bufC[kCH];
@@ -1161,7 +1170,7 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
                         M0 = a2[p].x * M0 + bb2[p].x * (tmp * tmp);
                         V0 = V0 + (double)cur[2 * p].y * rw2[p].x;
                         sum0 = sum0 + x;
-                        Tk[(size_t)(2 * p) * 3 * 64] = make_double2(lw0 * (M0 * rn2[p].x), lw0 * (V0 * n2[p].x));
+                        if (FU) Tk[(size_t)(2 * p) * 3 * 64] = make_double2(lw0 * (M0 * rn2[p].x), lw0 * (V0 * n2[p].x));
                     }
                     {
                         const double x = (double)cur[2 * p + 1].x;
@@ -1169,7 +1178,7 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
                         M0 = a2[p].y * M0 + bb2[p].y * (tmp * tmp);
                         V0 = V0 + (double)cur[2 * p + 1].y * rw2[p].y;
                         sum0 = sum0 + x;
-                        Tk[(size_t)(2 * p + 1) * 3 * 64] = make_double2(lw0 * (M0 * rn2[p].y), lw0 * (V0 * n2[p].y));
+                        if (FU) Tk[(size_t)(2 * p + 1) * 3 * 64] = make_double2(lw0 * (M0 * rn2[p].y), lw0 * (V0 * n2[p].y));
                     }
                 }
             } else {
@@ -1181,7 +1190,7 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
                         if (c0 + c > 0) M0 = q.a[o + c] * M0 + q.bb[o + c] * (tmp * tmp);
                         V0 = V0 + (double)cur[c].y * q.rw[o + c];
                         sum0 = sum0 + x;
-                        Tk[(size_t)c * 3 * 64] = make_double2(lw0 * (M0 * q.rWn[o + c]), lw0 * (V0 * q.Wn[o + c]));
+                        if (FU) Tk[(size_t)c * 3 * 64] = make_double2(lw0 * (M0 * q.rWn[o + c]), lw0 * (V0 * q.Wn[o + c]));
                     }
                 }
             }
@@ -1193,6 +1202,11 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
             if (k + 1 < nch) step(k + 1, bufB, bufA);
             if (k + 2 < nch) step(k + 2, bufC, bufB);
         }
+        if (!FU && b0 * 64 + lane < R) {
+            double* st = J.st + (size_t)g * 3 * R;
+            gpw(st)[R + b0 * 64 + lane] = M0;
+            gpw(st)[2 * R + b0 * 64 + lane] = V0;
+        }
     } else {
         for (uint32_t k = 0; k < nch; k++) __syncthreads();
     }
@@ -1200,6 +1214,24 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
         atomicAdd(&cm.prof[kPfWaveBusy + wv], (unsigned long long)wbusy);
         atomicAdd(&cm.prof[kPfWaveBusy + kWaves + wv], (unsigned long long)((long long)clock64() - wwall0));
         atomicAdd(&cm.prof[kPfWaveBusy + 2 * kWaves + wv], (unsigned long long)wred);
+    }
+    __syncthreads();
+    if (!FU && active && wv == (g == 0 ? 0 : 5)) {
+        // the pass's final variances from the rows' states (variance_passes_t, FU == false)
+        const double* st = J.st + (size_t)g * 3 * R;
+        const double Wt = V.Wcur, rW = 1.0 / Wt;
+        double pu = 0.0, pi = 0.0;
+        for (uint32_t r = lane; r < R; r += 64) {
+            pu = pu + J.locw[r] * (gp(st)[R + r] * rW);
+            pi = pi + J.locw[r] * (gp(st)[2 * R + r] * Wt);
+        }
+        pu = tree_d(pu);
+        pi = tree_d(pi);
+        if (lane == 0) {
+            V.res_u = (float)pu; V.res_i = (float)pi;
+            if (!isfinite(V.res_u) || V.res_u < 0) C.err = 1;
+            if (!isfinite(V.res_i) || V.res_i < 0) C.err = 1;
+        }
     }
     __syncthreads();
 }
@@ -1212,7 +1244,11 @@ __device__ void variance_passes(const JobDev& J, const Common& cm, Ctl& C, const
     if (pf && (!pf->p || threadIdx.x != 0)) pf = nullptr;
     const bool lds = (size_t)2 * 2 * kCH * NB * 64 * sizeof(double2) <= kPoolBytes;
     if (fu0 && npass == 2 && NB <= 3 && cm.var_v3) {
-        variance_split_v3(J, cm, C, base, m, fu0, fi0, fu1, fi1, pool);
+        variance_split_v3<true>(J, cm, C, base, m, 2, fu0, fi0, fu1, fi1, pool);
+        return;
+    }
+    if (!fu0 && NB <= 3 && cm.var_v3) {
+        variance_split_v3<false>(J, cm, C, base, m, npass, nullptr, nullptr, nullptr, nullptr, pool);
         return;
     }
     if (fu0) {
@@ -1990,6 +2026,191 @@ __device__ __noinline__ void roam_loop(const JobDev* jobs, const SplitWs& w, uin
     }
 }
 
+// calculateColumnWeigths (:985-1008) with the +1% of the mean (:1002-1007).
+// Out of line: inlined into k_refine its loops ran on spilled registers
+// (scratch reloads, each a vmcnt(0) wait).
+__device__ __noinline__ void column_weights(const JobDev& J, const Common& cm, Ctl& C)
+{
+    const int tid = threadIdx.x, wave = tid >> 6;
+    const uint32_t lane = (uint32_t)(tid & 63);
+    const uint32_t N = cm.nvrl, R = J.nrows;
+    // calculateColumnWeigths (:985-1008): one wave per 16 columns, rows in the
+    // shared order (lane l sums rows l, l+64, l+128 from 0, then the halving
+    // tree, here transposed: the 16 column sums in one tree16_transposed)
+    if (R <= 64u * 3u) {
+        const uint32_t NBr = (R + 63) / 64;
+        const float2* const Rt = cm.Rt;
+        auto* const colw = gpw(J.colw);
+        constexpr int Q = 16;
+        RowRef rr[3];
+        double lw[3];
+#pragma unroll
+        for (int b = 0; b < 3; b++) {
+            const uint32_t r = (uint32_t)b * 64 + lane;
+            rr[b] = row_ref(J, min(r, R - 1));
+            lw[b] = r < R ? gp(J.locw)[r] : 0.0;
+        }
+        for (uint32_t v0 = (uint32_t)wave * Q; v0 < N; v0 += kWaves * Q) {
+            float2 x[3][Q];
+#pragma unroll
+            for (int b = 0; b < 3; b++)
+#pragma unroll
+                for (int q = 0; q < Q; q++)
+                    x[b][q] = (uint32_t)b < NBr ? ldg2(Rt, rr[b].base + (size_t)min(v0 + (uint32_t)q, N - 1) * rr[b].stride)
+                                                : make_float2(0.0f, 0.0f);
+            double v[Q];
+#pragma unroll
+            for (int q = 0; q < Q; q++) {
+                double p = 0.0;
+#pragma unroll
+                for (int b = 0; b < 3; b++) {
+                    if ((uint32_t)b * 64 + lane < R) {
+                        const double mean = (double)x[b][q].x, var = (double)x[b][q].y;
+                        const double xx = mean * mean + var;
+                        p = p + lw[b] * xx;
+                    }
+                }
+                v[q] = p;
+            }
+            const double t = tree16_transposed(v, lane);
+            if ((lane & 3) == 0) {
+                const uint32_t j = ((lane >> 5) & 1) | (((lane >> 4) & 1) << 1) | (((lane >> 3) & 1) << 2) | (((lane >> 2) & 1) << 3);
+                if (v0 + j < N) {
+                    const float cw = (float)sqrt(t > 0.0 ? t : 0.0);
+                    colw[v0 + j] = cw;
+                    if (!isfinite(cw)) C.err = 1;
+                }
+            }
+        }
+    } else {
+        for (uint32_t v0 = (uint32_t)wave * kCB; v0 < N; v0 += kWaves * kCB) {
+            double p[kCB];
+#pragma unroll
+            for (int q = 0; q < kCB; q++) p[q] = 0.0;
+            for (uint32_t r = lane; r < R; r += 64) {
+                const RowRef rr = row_ref(J, r);
+                const double lw = J.locw[r];
+                float2 mv[kCB];
+#pragma unroll
+                for (int q = 0; q < kCB; q++) mv[q] = ldg2(cm.Rt, rr.base + (size_t)min(v0 + (uint32_t)q, N - 1) * rr.stride);
+#pragma unroll
+                for (int q = 0; q < kCB; q++) {
+                    const double mean = (double)mv[q].x, var = (double)mv[q].y;
+                    const double x = mean * mean + var;
+                    p[q] = p[q] + lw * x;
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < kCB; q++) {
+                const double t = tree_d(p[q]);
+                if (lane == 0 && v0 + q < N) {
+                    const float cw = (float)sqrt(t > 0.0 ? t : 0.0);
+                    J.colw[v0 + q] = cw;
+                    if (!isfinite(cw)) C.err = 1;
+                }
+            }
+        }
+    }
+    __syncthreads();
+    if (wave == 0) {
+        // the running float sum in index order (one add after the other, as
+        // the reference's loop), 64 weights per load, broadcast by v_readlane
+        const auto* cwp = gp(J.colw);
+        float acc = 0.0f;
+        float x = lane < N ? cwp[lane] : 0.0f;
+        for (uint32_t b = 0; b < N; b += 64) {
+            const float nx = b + 64 + lane < N ? cwp[b + 64 + lane] : 0.0f;
+            const uint32_t cnt = min(64u, N - b);
+            for (uint32_t c = 0; c < cnt; c++) acc += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), c));
+            x = nx;
+        }
+        if (lane == 0) {
+            float avg = acc / N;
+            if (avg == 0) avg = 1.0f;
+            C.avg = avg;
+        }
+    }
+    __syncthreads();
+    {
+        const float add = C.avg * 1e-2f;
+        for (uint32_t v = tid; v < N; v += kThreads) J.colw[v] += add;
+    }
+    __syncthreads();
+}
+
+// calculateUnclusteredVariance (:1022-1048), out of line for the same reason
+__device__ __noinline__ void unclustered_variance(const JobDev& J, const Common& cm, Ctl& C, uint32_t nv)
+{
+    const int tid = threadIdx.x, wave = tid >> 6;
+    const uint32_t lane = (uint32_t)(tid & 63);
+    const uint32_t R = J.nrows;
+    // calculateUnclusteredVariance (:1022-1048): per-row Welford in m_vrls
+    // order, one lane per row; column ids 64 at a time (one per lane, the
+    // next block's in flight) broadcast by v_readlane, 1/(n+1) formed once
+    // per lane for the block, entries 16 columns ahead
+    {
+        const uint32_t NBr = (R + 63) / 64;
+        const auto* vr = gp(J.vrls);
+        constexpr int G = 16;
+        for (uint32_t rb = (uint32_t)wave; rb < NBr; rb += kWaves) {
+            const uint32_t r = rb * 64 + lane;
+            const RowRef rr = row_ref(J, min(r, R - 1));
+            const float2* const Rt = cm.Rt + rr.base;
+            const size_t rs = rr.stride;
+            double mean = 0.0, M2 = 0.0, sv = 0.0;
+            uint32_t vid = lane < nv ? vr[lane] : 0u;
+            float2 eA[G], eB[G];
+            auto load = [&](uint32_t vids, uint32_t g, uint32_t cnt, float2* e) {
+#pragma unroll
+                for (int k = 0; k < G; k++) {
+                    const uint32_t c = g + (uint32_t)k < cnt ? g + (uint32_t)k : 0u;
+                    e[k] = ldg2(Rt, (size_t)(uint32_t)__builtin_amdgcn_readlane((int)vids, (int)c) * rs);
+                }
+            };
+            for (uint32_t b = 0; b < nv; b += 64) {
+                const uint32_t nvid = b + 64 + lane < nv ? vr[b + 64 + lane] : 0u;
+                const uint32_t cnt = min(64u, nv - b);
+                const double rnl = 1.0 / (double)(b + lane + 1);
+                load(vid, 0, cnt, eA);
+                for (uint32_t g = 0; g < cnt; g += G) {
+                    if (g + G < cnt) load(vid, g + G, cnt, eB);
+#pragma unroll
+                    for (int k = 0; k < G; k++) {
+                        if (g + (uint32_t)k < cnt) {
+                            const double rn = readlane_d(rnl, g + (uint32_t)k);
+                            sv = sv + (double)eA[k].y;
+                            const double x = (double)eA[k].x;
+                            const double delta = x - mean;
+                            mean = mean + delta * rn;
+                            M2 = M2 + delta * (x - mean);
+                        }
+                    }
+#pragma unroll
+                    for (int k = 0; k < G; k++) eA[k] = eB[k];
+                }
+                vid = nvid;
+            }
+            if (r < R) { gpw(J.st)[r] = sv; gpw(J.st)[R + r] = M2; }
+        }
+    }
+    __syncthreads();
+    if (wave == 0) {
+        double pv = 0.0, pm = 0.0;
+        for (uint32_t r = lane; r < R; r += 64) {
+            pv = pv + J.locw[r] * J.st[r];
+            pm = pm + J.locw[r] * J.st[R + r];
+        }
+        pv = tree_d(pv);
+        pm = tree_d(pm);
+        if (lane == 0) {
+            if (nv <= 1) C.err = 1;
+            C.unclIntVar = (float)pv;
+            C.tracingVar = (float)(pm - (double)C.unclIntVar);
+        }
+    }
+    __syncthreads();
+}
+
 // ---------------------------------------------------------- kernel --
 __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ jobs, Common cm)
 {
@@ -2025,50 +2246,7 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
         C.err = 0; C.refined = 1;
     }
     __syncthreads();
-    // calculateColumnWeigths (:985-1008)
-    // calculateColumnWeigths: one wave per column, kCB columns in flight,
-    // rows in the shared order
-    for (uint32_t v0 = (uint32_t)wave * kCB; v0 < N; v0 += kWaves * kCB) {
-        double p[kCB];
-#pragma unroll
-        for (int q = 0; q < kCB; q++) p[q] = 0.0;
-        for (uint32_t r = lane; r < R; r += 64) {
-            const RowRef rr = row_ref(J, r);
-            const double lw = J.locw[r];
-            float2 mv[kCB];
-#pragma unroll
-            for (int q = 0; q < kCB; q++) mv[q] = ldg2(cm.Rt, rr.base + (size_t)min(v0 + (uint32_t)q, N - 1) * rr.stride);
-#pragma unroll
-            for (int q = 0; q < kCB; q++) {
-                const double mean = (double)mv[q].x, var = (double)mv[q].y;
-                const double x = mean * mean + var;
-                p[q] = p[q] + lw * x;
-            }
-        }
-#pragma unroll
-        for (int q = 0; q < kCB; q++) {
-            const double t = tree_d(p[q]);
-            if (lane == 0 && v0 + q < N) {
-                const float cw = (float)sqrt(t > 0.0 ? t : 0.0);
-                J.colw[v0 + q] = cw;
-                if (!isfinite(cw)) C.err = 1;
-            }
-        }
-    }
-    __syncthreads();
-    if (tid == 0) {
-        float acc = 0.0f;
-        for (uint32_t v = 0; v < N; v++) acc += J.colw[v];
-        float avg = acc / N;
-        if (avg == 0) avg = 1.0f;
-        C.avg = avg;
-    }
-    __syncthreads();
-    {
-        const float add = C.avg * 1e-2f;
-        for (uint32_t v = tid; v < N; v += kThreads) J.colw[v] += add;
-    }
-    __syncthreads();
+    column_weights(J, cm, C);
     pf.mark(PF_COLW);
     for (uint32_t i = tid; i < nv; i += kThreads) J.vrls[i] = cm.init_vrls[i];
     __syncthreads();
@@ -2088,47 +2266,7 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
         }
     }
     pf.mark(PF_INIT);
-    // calculateUnclusteredVariance (:1022-1048): per-row Welford in m_vrls order
-    for (uint32_t r = tid; r < R; r += kThreads) {
-        const RowRef rr = row_ref(J, r);
-        double mean = 0.0, M2 = 0.0, sv = 0.0;
-        for (uint32_t n0 = 0; n0 < nv; n0 += kCH) {
-            uint32_t ids[kCH];
-#pragma unroll
-            for (int k = 0; k < kCH; k++) ids[k] = J.vrls[n0 + k < nv ? n0 + k : 0];
-            float2 e[kCH];
-#pragma unroll
-            for (int k = 0; k < kCH; k++) e[k] = ldg2(cm.Rt, rr.base + (size_t)ids[k] * rr.stride);
-#pragma unroll
-            for (int k = 0; k < kCH; k++) {
-                if (n0 + k < nv) {
-                    const double rn = 1.0 / (double)(n0 + k + 1);
-                    sv = sv + (double)e[k].y;
-                    const double x = (double)e[k].x;
-                    const double delta = x - mean;
-                    mean = mean + delta * rn;
-                    M2 = M2 + delta * (x - mean);
-                }
-            }
-        }
-        J.st[r] = sv; J.st[R + r] = M2;
-    }
-    __syncthreads();
-    if (wave == 0) {
-        double pv = 0.0, pm = 0.0;
-        for (uint32_t r = lane; r < R; r += 64) {
-            pv = pv + J.locw[r] * J.st[r];
-            pm = pm + J.locw[r] * J.st[R + r];
-        }
-        pv = tree_d(pv);
-        pm = tree_d(pm);
-        if (lane == 0) {
-            if (nv <= 1) C.err = 1;
-            C.unclIntVar = (float)pv;
-            C.tracingVar = (float)(pm - (double)C.unclIntVar);
-        }
-    }
-    __syncthreads();
+    unclustered_variance(J, cm, C, nv);
     pf.mark(PF_UNCL);
 
     // refine (:380-489)
