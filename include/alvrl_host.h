@@ -54,6 +54,12 @@ ALVRL_API int alvrl_tile_pixels(int width, int height, uint32_t rank, uint32_t w
 ALVRL_API int alvrl_trace_vrls(const alvrl_scene_desc *s, uint32_t seed, uint32_t pass,
                                uint32_t target, int short_vrls, int max_depth, int rr_depth,
                                float *soa, uint32_t cap, uint32_t *n, uint64_t *particles);
+/* The same walk on the current HIP device (csrc/tracer.hip, SURVEY 8(f) row
+ * 2): one lane per particle, bit-identical VRL set and particle count.
+ * soa == NULL: size query (*n, *particles). */
+ALVRL_API int alvrl_trace_vrls_gpu(const alvrl_scene_desc *s, uint32_t seed, uint32_t pass,
+                                   uint32_t target, int short_vrls, int max_depth, int rr_depth,
+                                   float *soa, uint32_t cap, uint32_t *n, uint64_t *particles);
 
 /* vrlVector(Stream*, const Medium*) (VRL.h:120-128) / a separator-correct
  * serializeAscii (VRL.h:65-73). */

@@ -454,6 +454,7 @@ def _host():
     L.alvrl_scene_default.argtypes = [P(SceneDesc), i32, i32]; L.alvrl_scene_default.restype = None
     L.alvrl_scene_records.argtypes = [P(SceneDesc), i32, vp, u32, vp]
     L.alvrl_trace_vrls.argtypes = [P(SceneDesc), u32, u32, u32, i32, i32, i32, vp, u32, P(u32), P(u64)]
+    L.alvrl_trace_vrls_gpu.argtypes = [P(SceneDesc), u32, u32, u32, i32, i32, i32, vp, u32, P(u32), P(u64)]
     L.alvrl_read_vrl_file.argtypes = [C.c_char_p, P(MediumDesc), vp, u32, P(u32), P(u64)]
     L.alvrl_write_vrl_file.argtypes = [C.c_char_p, vp, u32]
     L.alvrl_tile_pixels.argtypes = [i32, i32, u32, u32, vp, u32, P(u32)]
@@ -520,6 +521,20 @@ def trace_vrls(scene: SceneDesc, target: int, seed: int = 0x5EED0001, pass_: int
     n = C.c_uint32(); pc = C.c_uint64()
     _hcheck(L.alvrl_trace_vrls(C.byref(scene), seed, pass_, target, int(short_vrls), max_depth,
                                rr_depth, _ptr(soa), cap, C.byref(n), C.byref(pc)))
+    return np.ascontiguousarray(soa[:, :n.value]), int(pc.value)
+
+
+def trace_vrls_gpu(scene: SceneDesc, target: int, seed: int = 0x5EED0001, pass_: int = 0,
+                   short_vrls: bool = True, max_depth: int = -1, rr_depth: int = 5):
+    """vrlTracer::randomWalk on the current HIP device (same result as trace_vrls)."""
+    L = _host()
+    n = C.c_uint32(); pc = C.c_uint64()
+    _hcheck(L.alvrl_trace_vrls_gpu(C.byref(scene), seed, pass_, target, int(short_vrls), max_depth, rr_depth,
+                                   None, 0, C.byref(n), C.byref(pc)))
+    cap = max(1, n.value)
+    soa = np.zeros((9, cap), np.float32)
+    _hcheck(L.alvrl_trace_vrls_gpu(C.byref(scene), seed, pass_, target, int(short_vrls), max_depth, rr_depth,
+                                   _ptr(soa), cap, C.byref(n), C.byref(pc)))
     return np.ascontiguousarray(soa[:, :n.value]), int(pc.value)
 
 

@@ -140,7 +140,8 @@ V3 uniform_sphere(float sx, float sy)   // warp.cpp:25-31
     const float z = 1.0f - 2.0f * sy;
     const float r = safe_sqrt(1.0f - z * z);
     const float theta = (float)(2.0f * kPi * sx);
-    return v3(r * std::cos(theta), r * std::sin(theta), z);
+    // sin/cos in double, rounded once (the oracle and tracer.hip do the same)
+    return v3(r * (float)std::cos((double)theta), r * (float)std::sin((double)theta), z);
 }
 
 V3 cosine_hemisphere(float sx, float sy)   // warp.cpp:43-52, 81-102
@@ -150,7 +151,7 @@ V3 cosine_hemisphere(float sx, float sy)   // warp.cpp:43-52, 81-102
     if (r1 == 0 && r2 == 0) { r = phi = 0; }
     else if (r1 * r1 > r2 * r2) { r = r1; phi = (float)((kPi / 4.0f) * (r2 / r1)); }
     else { r = r2; phi = (float)((kPi / 2.0f) - (r1 / r2) * (kPi / 4.0f)); }
-    const float px = r * std::cos(phi), py = r * std::sin(phi);
+    const float px = r * (float)std::cos((double)phi), py = r * (float)std::sin((double)phi);
     float z = safe_sqrt(1.0f - px * px - py * py);
     if (z == 0) z = 1e-10f;
     return v3(px, py, z);

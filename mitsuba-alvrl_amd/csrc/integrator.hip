@@ -107,11 +107,13 @@ struct alvrl_integrator {
     bool dumpPasses = false;
     int rrDepth = 5, maxDepth = -1;
     uint32_t seed = 0xA1B2C3D4u, vrlSeed = 0x5EED0001u;
+    bool gpuTracer = false;   // trace the pass's VRLs on the device (csrc/tracer.hip)
     // ---- state
     int device = 0;
     alvrl_ctx* ctx = nullptr;
     hipStream_t stream = nullptr;
     SmokeBox scene;
+    alvrl_scene_desc scene_desc{};
     bool have_scene = false;
     std::unique_ptr<Preprocessor> prep;
     std::vector<uint32_t> pixel_to_slice;   // y + H*x
@@ -158,6 +160,7 @@ struct alvrl_integrator {
         auto f = [&](const std::string& x) { return std::stof(x); };
         if (k == "nc") throw IntegError(ALVRL_ERR_INVALID, "Neighbourcount is now called 'neighbourCount' instead of 'nc'!");
         else if (k == "shortVrls") shortVrls = b(v);
+        else if (k == "gpuTracer") gpuTracer = b(v);
         else if (k == "vrlTargetNum") vrlTargetNum = i(v);
         else if (k == "maxParticleDepth") maxParticleDepth = i(v);
         else if (k == "specularForcedRRdepth") specRRdepth = i(v);
@@ -203,6 +206,7 @@ struct alvrl_integrator {
     void preprocess(const alvrl_scene_desc& s)
     {
         scene = to_box(s);
+        scene_desc = s;
         have_scene = true;
         alvrl_medium_desc md = s.medium;
         chk(alvrl_set_medium(ctx, &md), "alvrl_set_medium");
@@ -253,8 +257,22 @@ struct alvrl_integrator {
         // VRLs (:276-287): traced per pass unless preloaded from a file
         if (!vrls_from_file) {
             const double t0 = now_ms();
-            vrls = trace_vrls(scene, vrlSeed, pass, (uint32_t)std::max(vrlTargetNum, 0), shortVrls,
-                              maxParticleDepth, rrDepth);
+            if (gpuTracer) {
+                const uint32_t target = (uint32_t)std::max(vrlTargetNum, 0);
+                uint32_t n = 0;
+                uint64_t pc = 0;
+                chk_host(alvrl_trace_vrls_gpu(&scene_desc, vrlSeed, pass, target, shortVrls ? 1 : 0, maxParticleDepth,
+                                              rrDepth, nullptr, 0, &n, &pc));
+                vrls.n = n;
+                vrls.particle_count = pc;
+                vrls.soa.assign(9 * (size_t)n, 0.0f);
+                if (n)
+                    chk_host(alvrl_trace_vrls_gpu(&scene_desc, vrlSeed, pass, target, shortVrls ? 1 : 0,
+                                                  maxParticleDepth, rrDepth, vrls.soa.data(), n, &n, &pc));
+            } else {
+                vrls = trace_vrls(scene, vrlSeed, pass, (uint32_t)std::max(vrlTargetNum, 0), shortVrls,
+                                  maxParticleDepth, rrDepth);
+            }
             st.ms_trace = now_ms() - t0;
             uploaded_pass = 0xFFFFFFFFu;
         }

@@ -1,0 +1,385 @@
+// tracer.hip -- vrlTracer::randomWalk (vrlTracer.h:13-230) on the GPU,
+// SURVEY.md 8(f) row 2.  One lane per particle: particle p draws from its own
+// counter-based stream (seed, pass, p), exactly as the host tracer
+// (csrc/host/scene.cpp trace_particle) and the oracle do, so the VRL set is
+// the host's bit for bit.  Built with -ffp-contract=off and IEEE division /
+// square root like the host; sin, cos, exp and log are evaluated in double
+// and rounded once, as on the host.
+//
+// Two passes per batch of particles: count each particle's VRLs, then (after
+// a prefix sum on the host picks the particles the sequential loop would have
+// traced -- it stops after the particle that brings the set to the target)
+// write them at their final positions in the SoA planes.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "alvrl_host.h"
+#include "host/scene.hpp"
+
+namespace alvrl {
+namespace host {
+extern thread_local std::string g_host_err;
+SmokeBox to_box(const alvrl_scene_desc& s);   // host_capi.cpp
+}
+}  // namespace alvrl
+
+namespace {
+
+constexpr double kPi = 3.14159265358979323846;
+constexpr uint32_t kDomTracer = 3u;
+
+struct TScene {
+    float light_pos[3], power[3];
+    float box_min[3], box_max[3], albedo[3];
+    float sigma_s[3], sigma_t[3], w;
+    int sigma_s_zero;
+};
+
+struct F3 { float x, y, z; };
+__device__ __forceinline__ F3 f3(float x, float y, float z) { return F3{x, y, z}; }
+__device__ __forceinline__ F3 add(F3 a, F3 b) { return f3(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ F3 sub(F3 a, F3 b) { return f3(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ F3 mul(F3 a, float s) { return f3(a.x * s, a.y * s, a.z * s); }
+__device__ __forceinline__ float dot(F3 a, F3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ float len(F3 a) { return sqrtf(a.x * a.x + a.y * a.y + a.z * a.z); }
+__device__ __forceinline__ F3 cross(F3 a, F3 b)
+{
+    return f3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+__device__ __forceinline__ float safe_sqrt(float v) { return sqrtf(v > 0.0f ? v : 0.0f); }
+__device__ __forceinline__ float fastexp(float v) { return (float)exp((double)v); }   // math.h:185-199
+__device__ __forceinline__ float fastlog(float v) { return (float)log((double)v); }
+
+// Random123 Philox4x32-10 and Random::nextFloat (random.cpp:630-639), as the host
+struct Stream {
+    uint32_t seed, pass, a, b, k, blk;
+    uint32_t buf[4];
+    __device__ float next()
+    {
+        const uint32_t bl = k >> 2;
+        if (bl != blk) {
+            uint32_t c0 = a, c1 = b, c2 = bl, c3 = (kDomTracer << 24);
+            uint32_t k0 = seed, k1 = pass;
+            for (int r = 0; r < 10; r++) {
+                if (r > 0) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
+                const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+                const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0, n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+                c0 = n0; c1 = (uint32_t)p1; c2 = n2; c3 = (uint32_t)p0;
+            }
+            buf[0] = c0; buf[1] = c1; buf[2] = c2; buf[3] = c3;
+            blk = bl;
+        }
+        const uint32_t u = (buf[k & 3] >> 9) | 0x3f800000u;
+        ++k;
+        return __uint_as_float(u) - 1.0f;
+    }
+};
+
+__device__ F3 uniform_sphere(float sx, float sy)   // warp.cpp:25-31
+{
+    const float z = 1.0f - 2.0f * sy;
+    const float r = safe_sqrt(1.0f - z * z);
+    const float theta = (float)(2.0f * kPi * sx);
+    return f3(r * (float)cos((double)theta), r * (float)sin((double)theta), z);
+}
+
+__device__ F3 cosine_hemisphere(float sx, float sy)   // warp.cpp:43-52, 81-102
+{
+    const float r1 = 2.0f * sx - 1.0f, r2 = 2.0f * sy - 1.0f;
+    float phi, r;
+    if (r1 == 0 && r2 == 0) { r = phi = 0; }
+    else if (r1 * r1 > r2 * r2) { r = r1; phi = (float)((kPi / 4.0f) * (r2 / r1)); }
+    else { r = r2; phi = (float)((kPi / 2.0f) - (r1 / r2) * (kPi / 4.0f)); }
+    const float px = r * (float)cos((double)phi), py = r * (float)sin((double)phi);
+    float z = safe_sqrt(1.0f - px * px - py * py);
+    if (z == 0) z = 1e-10f;
+    return f3(px, py, z);
+}
+
+__device__ void frame_of(F3 a, F3* b, F3* c)   // coordinateSystem, util.cpp:592-601
+{
+    if (fabsf(a.x) > fabsf(a.y)) {
+        const float invLen = 1.0f / sqrtf(a.x * a.x + a.z * a.z);
+        *c = f3(a.z * invLen, 0.0f, -a.x * invLen);
+    } else {
+        const float invLen = 1.0f / sqrtf(a.y * a.y + a.z * a.z);
+        *c = f3(0.0f, a.z * invLen, -a.y * invLen);
+    }
+    *b = cross(*c, a);
+}
+
+__device__ float box_hit(const TScene& sc, F3 o, F3 d, F3* n)   // first wall hit from inside
+{
+    float best = INFINITY;
+    int axis = -1;
+    const float oo[3] = {o.x, o.y, o.z}, dd[3] = {d.x, d.y, d.z};
+    for (int a = 0; a < 3; a++) {
+        float t;
+        if (dd[a] > 0) t = (sc.box_max[a] - oo[a]) / dd[a];
+        else if (dd[a] < 0) t = (sc.box_min[a] - oo[a]) / dd[a];
+        else continue;
+        if (t < best) { best = t; axis = a; }
+    }
+    float nn[3] = {0.0f, 0.0f, 0.0f};
+    if (axis >= 0) nn[axis] = dd[axis] > 0 ? -1.0f : 1.0f;
+    *n = f3(nn[0], nn[1], nn[2]);
+    return best;
+}
+
+// vrlVector::put + the current VRL (vrlTracer.h:56-89, VRL.h:148-158); counts,
+// or writes into the SoA planes at 'pos' when soa != nullptr
+struct Sink {
+    F3 start;
+    float power[3];
+    int sigma_s_zero;
+    uint32_t n;
+    float* soa;
+    uint64_t pos, stride;
+    __device__ void put(F3 end)
+    {
+        if (sigma_s_zero) return;
+        if (power[0] == 0 && power[1] == 0 && power[2] == 0) return;
+        if (len(sub(start, end)) == 0) return;
+        if (soa) {
+            const uint64_t i = pos + n;
+            const float v[9] = {start.x, start.y, start.z, end.x, end.y, end.z, power[0], power[1], power[2]};
+#pragma unroll
+            for (int pl = 0; pl < 9; pl++) soa[(uint64_t)pl * stride + i] = v[pl];
+        }
+        n++;
+    }
+    __device__ void end_current(F3 p)
+    {
+        if (len(sub(start, p)) == 0) return;
+        put(p);
+    }
+};
+
+__device__ void trace_particle(const TScene& sc, Stream& smp, bool short_vrls, int max_depth, int rr_depth, Sink& k)
+{
+    (void)smp.next(); (void)smp.next();   // sampleEmitterPosition (scene.cpp:958-974)
+    const float dx = smp.next(), dy = smp.next();   // sampleDirection (point.cpp:99-106)
+    F3 dir = uniform_sphere(dx, dy);
+    if (sc.power[0] == 0 && sc.power[1] == 0 && sc.power[2] == 0) return;
+    F3 o = f3(sc.light_pos[0], sc.light_pos[1], sc.light_pos[2]);
+    k.start = o;
+    for (int i = 0; i < 3; i++) k.power[i] = sc.power[i];
+    int depth = 1;
+    float thr[3] = {1.0f, 1.0f, 1.0f};
+    const float eta = 1.0f;
+    const float w = sc.w;
+    while (!(thr[0] == 0 && thr[1] == 0 && thr[2] == 0) && (depth <= max_depth || max_depth < 0)) {
+        F3 n;
+        const float its_t = box_hit(sc, o, dir, &n);
+        const bool its_valid = isfinite(its_t);
+        // HomogeneousMedium::sampleDistance (homogeneous.cpp:275-352), balance
+        float rnd = smp.next(), sampled;
+        if (rnd < w) {
+            rnd /= w;
+            int ch = (int)(smp.next() * 3);
+            if (ch > 2) ch = 2;
+            sampled = -fastlog(1 - rnd) / sc.sigma_t[ch];
+        } else {
+            sampled = INFINITY;
+        }
+        const float distSurf = its_t - 0.0f;
+        bool success = true;
+        F3 mp = o;
+        if (sampled < distSurf) {
+            mp = add(o, mul(dir, sampled + 0.0f));
+            if (mp.x == o.x && mp.y == o.y && mp.z == o.z) success = false;
+        } else {
+            sampled = distSurf;
+            success = false;
+        }
+        float pf = 0, ps = 0;
+        for (int i = 0; i < 3; i++) {
+            const float tmp = fastexp(-sc.sigma_t[i] * sampled);
+            pf += tmp;
+            ps += sc.sigma_t[i] * tmp;
+        }
+        pf /= 3; ps /= 3;
+        float mtr[3];
+        for (int i = 0; i < 3; i++) mtr[i] = fastexp(sc.sigma_t[i] * (-sampled));
+        ps = ps * w;
+        pf = w * pf + (1 - w);
+        {
+            float mx = mtr[0] > mtr[1] ? mtr[0] : mtr[1];
+            mx = mx > mtr[2] ? mx : mtr[2];
+            if (mx < 1e-20f) mtr[0] = mtr[1] = mtr[2] = 0;
+        }
+        if (success) {   // vrlTracer.h:143-172
+            const float rps = 1.0f / ps;
+            for (int i = 0; i < 3; i++) thr[i] *= mtr[i] * sc.sigma_s[i] * rps;
+            const float px_ = smp.next(), py_ = smp.next();
+            const F3 wo = uniform_sphere(px_, py_);
+            const F3 endPoint = short_vrls ? mp : add(o, mul(dir, its_t));
+            k.end_current(endPoint);
+            k.start = mp;
+            for (int i = 0; i < 3; i++) k.power[i] = thr[i] * sc.power[i];
+            o = mp; dir = wo;
+        } else if (its_valid) {   // vrlTracer.h:173-213
+            const float rpf = 1.0f / pf;
+            for (int i = 0; i < 3; i++) thr[i] *= mtr[i] * rpf;
+            const F3 p = add(o, mul(dir, its_t));
+            F3 fs, ft;
+            frame_of(n, &fs, &ft);
+            const F3 mwi = f3(-dir.x, -dir.y, -dir.z);
+            const float cos_wi = dot(mwi, n);
+            const float bx = smp.next(), by = smp.next();
+            float bw[3] = {0, 0, 0};
+            F3 wol = f3(0, 0, 0);
+            if (!(cos_wi <= 0)) {
+                wol = cosine_hemisphere(bx, by);
+                for (int i = 0; i < 3; i++) bw[i] = sc.albedo[i];
+            }
+            if (bw[0] == 0 && bw[1] == 0 && bw[2] == 0) { k.end_current(p); break; }
+            const F3 wo = add(add(mul(fs, wol.x), mul(ft, wol.y)), mul(n, wol.z));
+            const float wiDotGeoN = dot(n, mwi), woDotGeoN = dot(n, wo);
+            if (wiDotGeoN * cos_wi <= 0 || woDotGeoN * wol.z <= 0) { k.end_current(p); break; }
+            for (int i = 0; i < 3; i++) thr[i] *= bw[i];
+            k.end_current(p);
+            k.start = p;
+            for (int i = 0; i < 3; i++) k.power[i] = thr[i] * sc.power[i];
+            o = p; dir = wo;
+        } else {
+            break;
+        }
+        if (depth++ >= rr_depth) {
+            float mx = thr[0] > thr[1] ? thr[0] : thr[1];
+            mx = mx > thr[2] ? mx : thr[2];
+            float q = mx * eta * eta;
+            if (q > 0.95f) q = 0.95f;
+            if (smp.next() >= q) break;
+            const float rq = 1.0f / q;
+            for (int i = 0; i < 3; i++) thr[i] *= rq;
+        }
+    }
+}
+
+struct TArgs {
+    uint32_t seed, pass;
+    int short_vrls, max_depth, rr_depth;
+};
+
+__global__ void __launch_bounds__(256) k_trace_count(TScene sc, TArgs a, uint64_t p0, uint32_t P, uint32_t* counts)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P) return;
+    const uint64_t p = p0 + i;
+    Stream smp{a.seed, a.pass, (uint32_t)p, (uint32_t)(p >> 32), 0u, 0xFFFFFFFFu, {0, 0, 0, 0}};
+    Sink k{};
+    k.sigma_s_zero = sc.sigma_s_zero;
+    k.soa = nullptr;
+    trace_particle(sc, smp, a.short_vrls != 0, a.max_depth, a.rr_depth, k);
+    counts[i] = k.n;
+}
+
+__global__ void __launch_bounds__(256) k_trace_write(TScene sc, TArgs a, uint64_t p0, uint32_t P,
+                                                     const uint64_t* offs, float* soa, uint64_t stride)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P) return;
+    const uint64_t p = p0 + i;
+    Stream smp{a.seed, a.pass, (uint32_t)p, (uint32_t)(p >> 32), 0u, 0xFFFFFFFFu, {0, 0, 0, 0}};
+    Sink k{};
+    k.sigma_s_zero = sc.sigma_s_zero;
+    k.soa = soa;
+    k.pos = offs[i];
+    k.stride = stride;
+    trace_particle(sc, smp, a.short_vrls != 0, a.max_depth, a.rr_depth, k);
+}
+
+int terr(int code, const std::string& m)
+{
+    alvrl::host::g_host_err = m;
+    return code;
+}
+
+template <typename T>
+struct DMem {
+    T* p = nullptr;
+    ~DMem() { if (p) (void)hipFree(p); }
+    hipError_t alloc(size_t n) { return hipMalloc(&p, std::max<size_t>(n, 1) * sizeof(T)); }
+};
+
+}  // namespace
+
+extern "C" {
+
+// The GPU form of alvrl_trace_vrls (same arguments and results); runs on the
+// current HIP device.
+ALVRL_API int alvrl_trace_vrls_gpu(const alvrl_scene_desc* s, uint32_t seed, uint32_t pass, uint32_t target,
+                                   int short_vrls, int max_depth, int rr_depth, float* soa, uint32_t cap,
+                                   uint32_t* n, uint64_t* particles)
+{
+    if (!s || !n || !particles) return terr(ALVRL_ERR_INVALID, "alvrl_trace_vrls_gpu: null argument");
+    // the scene as the host tracer resolves it (to_box + MediumParams::resolve)
+    const alvrl::host::SmokeBox box = alvrl::host::to_box(*s);
+    TScene sc;
+    sc.light_pos[0] = box.light_pos.x; sc.light_pos[1] = box.light_pos.y; sc.light_pos[2] = box.light_pos.z;
+    for (int i = 0; i < 3; i++) {
+        sc.power[i] = box.light_intensity[i] * (float)(4 * kPi);
+        sc.box_min[i] = box.box_min[i]; sc.box_max[i] = box.box_max[i];
+        sc.albedo[i] = box.albedo[i];
+        sc.sigma_s[i] = box.medium.sigma_s[i];
+        sc.sigma_t[i] = box.medium.sigma_t[i];
+    }
+    sc.w = box.medium.sampling_weight;
+    sc.sigma_s_zero = (sc.sigma_s[0] == 0 && sc.sigma_s[1] == 0 && sc.sigma_s[2] == 0) ? 1 : 0;
+    const TArgs a{seed, pass, short_vrls, max_depth, rr_depth};
+    *n = 0;
+    if (target == 0) { *particles = 0; return ALVRL_OK; }
+    if (sc.sigma_s_zero) { *particles = 1000001; return ALVRL_OK; }   // the host loop's bound
+    if (sc.power[0] == 0 && sc.power[1] == 0 && sc.power[2] == 0)
+        return terr(ALVRL_ERR_INVALID, "alvrl_trace_vrls_gpu: the light emits nothing (the VRL target is unreachable)");
+    // count pass, batch by batch, until the running total reaches the target
+    const uint32_t P = std::min<uint32_t>(1u << 20, std::max<uint32_t>(4096u, target));
+    DMem<uint32_t> d_cnt;
+    if (d_cnt.alloc(P) != hipSuccess) return terr(ALVRL_ERR_NOMEM, "alvrl_trace_vrls_gpu: device memory");
+    std::vector<uint32_t> counts;
+    uint64_t total = 0, used = 0;
+    for (uint64_t p0 = 0; used == 0; p0 += P) {
+        if (p0 > (1ull << 32)) return terr(ALVRL_ERR_INVALID, "alvrl_trace_vrls_gpu: target not reached");
+        hipLaunchKernelGGL(k_trace_count, dim3((P + 255) / 256), dim3(256), 0, 0, sc, a, p0, P, d_cnt.p);
+        if (hipGetLastError() != hipSuccess) return terr(ALVRL_ERR_HIP, "alvrl_trace_vrls_gpu: launch");
+        const size_t base = counts.size();
+        counts.resize(base + P);
+        if (hipMemcpy(counts.data() + base, d_cnt.p, P * 4, hipMemcpyDeviceToHost) != hipSuccess)
+            return terr(ALVRL_ERR_HIP, "alvrl_trace_vrls_gpu: copy");
+        for (uint32_t i = 0; i < P; i++) {
+            total += counts[base + i];
+            if (total >= target) { used = base + i + 1; break; }
+        }
+    }
+    *particles = used;
+    *n = (uint32_t)total;
+    if (!soa) return ALVRL_OK;   // size query
+    if (total > cap) return terr(ALVRL_ERR_INVALID, "alvrl_trace_vrls_gpu: capacity too small");
+    // write pass: every particle's VRLs at its exclusive prefix offset
+    std::vector<uint64_t> offs(used);
+    uint64_t o = 0;
+    for (uint64_t i = 0; i < used; i++) { offs[i] = o; o += counts[i]; }
+    DMem<uint64_t> d_off;
+    DMem<float> d_soa;
+    if (d_off.alloc(used) != hipSuccess || d_soa.alloc(9 * total) != hipSuccess)
+        return terr(ALVRL_ERR_NOMEM, "alvrl_trace_vrls_gpu: device memory");
+    if (hipMemcpy(d_off.p, offs.data(), used * 8, hipMemcpyHostToDevice) != hipSuccess)
+        return terr(ALVRL_ERR_HIP, "alvrl_trace_vrls_gpu: copy");
+    for (uint64_t p0 = 0; p0 < used; p0 += P) {
+        const uint32_t np = (uint32_t)std::min<uint64_t>(P, used - p0);
+        hipLaunchKernelGGL(k_trace_write, dim3((np + 255) / 256), dim3(256), 0, 0, sc, a, p0, np, d_off.p + p0,
+                           d_soa.p, total);
+        if (hipGetLastError() != hipSuccess) return terr(ALVRL_ERR_HIP, "alvrl_trace_vrls_gpu: launch");
+    }
+    if (hipMemcpy2D(soa, (size_t)cap * 4, d_soa.p, total * 4, total * 4, 9, hipMemcpyDeviceToHost) != hipSuccess)
+        return terr(ALVRL_ERR_HIP, "alvrl_trace_vrls_gpu: copy");
+    return ALVRL_OK;
+}
+
+}  // extern "C"

@@ -712,7 +712,9 @@ static v3 uniform_sphere(float sx, float sy)
     float z = 1.0f - 2.0f * sy;
     float r = safe_sqrt(1.0f - z * z);
     float theta = (float)(2.0f * M_PI * sx);
-    float sp = sinf(theta), cp = cosf(theta);
+    /* sin/cos evaluated in double and rounded once: the correctly rounded float
+       value, reproducible on the device (tracer.hip) -- libm's sinf/cosf are not */
+    float sp = (float)sin((double)theta), cp = (float)cos((double)theta);
     return mk(r * cp, r * sp, z);
 }
 
@@ -725,7 +727,7 @@ static v3 cosine_hemisphere(float sx, float sy)
     if (r1 == 0 && r2 == 0) { r = phi = 0; }
     else if (r1 * r1 > r2 * r2) { r = r1; phi = (float)((M_PI / 4.0f) * (r2 / r1)); }
     else { r = r2; phi = (float)((M_PI / 2.0f) - (r1 / r2) * (M_PI / 4.0f)); }
-    float sp = sinf(phi), cp = cosf(phi);
+    float sp = (float)sin((double)phi), cp = (float)cos((double)phi);
     float px = r * cp, py = r * sp;
     float z = safe_sqrt(1.0f - px * px - py * py);
     if (z == 0) z = 1e-10f;

@@ -391,3 +391,48 @@ def test_cluster_info_checkpoint(gpu_ok, tmp_path):
     alvrl.write_exr(p, frames[0].reshape(h, w, 3))
     assert np.array_equal(alvrl.read_exr(p).ravel(), frames[0])
     assert alvrl.image_rms(frames[1], frames[0]) == 0.0
+
+
+@pytest.mark.parametrize("target,short,max_depth,rr_depth,pass_", [
+    (700, True, -1, 5, 0), (300, False, -1, 5, 0), (500, True, 3, 5, 2), (400, True, -1, 1, 1),
+    (100003, True, -1, 5, 0)])
+def test_gpu_tracer_matches_host(oracle, gpu_ok, target, short, max_depth, rr_depth, pass_):
+    """vrlTracer::randomWalk on the device (csrc/tracer.hip, SURVEY 8(f) row 2)
+    gives the host tracer's VRL set and particle count bit for bit (the host
+    tracer is itself bit-exact with the oracle, tests/test_host.py)."""
+    import alvrl
+    s = alvrl.scene_default(16, 16)
+    host, hpc = alvrl.trace_vrls(s, target, seed=SEED_VRL, pass_=pass_, short_vrls=short,
+                                 max_depth=max_depth, rr_depth=rr_depth)
+    dev, dpc = alvrl.trace_vrls_gpu(s, target, seed=SEED_VRL, pass_=pass_, short_vrls=short,
+                                    max_depth=max_depth, rr_depth=rr_depth)
+    assert dpc == hpc and dev.shape == host.shape
+    assert np.array_equal(dev.view(np.uint32), host.view(np.uint32))
+    if target <= 1000:
+        ref, rpc = oracle.trace(oracle.scene(16, 16), oracle.medium(), target, seed=SEED_VRL, pass_=pass_,
+                                short_vrls=short, max_depth=max_depth, rr_depth=rr_depth)
+        assert rpc == dpc and np.array_equal(ref.view(np.uint32), dev.view(np.uint32))
+
+
+def test_integrator_gpu_tracer(gpu_ok):
+    """prepass with gpuTracer=true traces on the device; the pass (VRLs,
+    clusters, frame) is the host-traced one bit for bit."""
+    import torch
+    import alvrl
+    w, h = 32, 24
+    scene = alvrl.scene_default(w, h)
+    out = []
+    for gt in ("false", "true"):
+        it = alvrl.Integrator(f"targetNumSlices=8;vrlTargetNum=800;gpuTracer={gt};seed={SEED_RNG}", device=0)
+        it.preprocess(scene)
+        it.prepass(1)
+        fb = torch.zeros(w * h * 3, dtype=torch.float32, device="cuda")
+        it.render(fb)
+        torch.cuda.synchronize()
+        out.append((it.vrls(), it.clusters(), fb.cpu().numpy()))
+        it.close()
+    (v0, p0), c0, f0 = out[0]
+    (v1, p1), c1, f1 = out[1]
+    assert p0 == p1 and np.array_equal(v0.view(np.uint32), v1.view(np.uint32))
+    assert np.array_equal(c0["reps"], c1["reps"])
+    assert np.array_equal(f0.view(np.uint32), f1.view(np.uint32))
