@@ -13,5 +13,6 @@ step pytest && timeout -k 10 600 python -u -m pytest tests -m gpu -x -v -s --tim
  && step bench && timeout -k 10 600 python bench.py > gpurun_out/bench_$T.json 2> gpurun_out/bench_$T.err \
  && step rocprof && (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_$T" -o run --output-format csv -- python3 "$R/bench.py" --no-cpu-baseline > "$R/gpurun_out/prof_$T.log" 2>&1) \
  && step pmc && "$R/tools/pmc_traffic.sh" C4 \
+&& step tracer && timeout -k 10 120 python tools/tracer_bench.py > gpurun_out/tracer_$T.log 2>&1 \
  && step done
 echo "exit=$?"
