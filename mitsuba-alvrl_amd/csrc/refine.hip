@@ -40,7 +40,7 @@ constexpr int kThreads = 512;
 constexpr int kWaves = kThreads / 64;
 constexpr int kCH = 8;                                      // columns per variance chunk (per direction)
 constexpr int kGT = kThreads / 2;                           // threads per variance direction
-constexpr uint32_t kPoolBytes = 144 * 1024;                 // dynamic LDS: sort keys / variance chunks
+constexpr uint32_t kPoolBytes = 152 * 1024;                 // dynamic LDS: sort keys / variance chunks
 constexpr int kBitonicMax = 16384;                          // 8-byte keys sorted in the pool
 constexpr uint32_t kDomCluster = 5u;
 
@@ -865,7 +865,7 @@ __device__ __noinline__ void variance_passes_t(const JobDev& J, const Common& cm
 // wave reads two columns' worth of one coefficient with one ds_read_b128.
 constexpr int kCB64 = 64;
 struct CoefBlock { double w[kCB64], Wo[kCB64], a[kCB64], bb[kCB64], rw[kCB64], Wn[kCB64], rWn[kCB64]; uint32_t vrl[kCB64]; };
-constexpr uint32_t kSplitTBytes = 2u * 2u * kCH * 3u * 64u * sizeof(double2);     // [pass][k & 1][c][block][lane]
+constexpr uint32_t kSplitTBytes = 2u * 2u * kCH * 4u * 64u * sizeof(double2);     // [pass][k & 1][c][block][lane]
 constexpr uint32_t kSplitStageBytes = 2u * 2u * 2u * kCB64 * sizeof(float);      // [pass][block & 1][u|i][64]
 constexpr uint32_t kSplitPoolBytes = kSplitTBytes + 2u * 2u * sizeof(CoefBlock) + kSplitStageBytes;
 static_assert(kSplitPoolBytes <= kPoolBytes, "split variance engine: pool");
@@ -969,7 +969,7 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
                                                unsigned char* pool)
 {
     const uint32_t R = J.nrows;
-    const uint32_t NB = (R + 63) / 64;                 // <= 3
+    const uint32_t NB = (R + 63) / 64;                 // <= 4 (block 3 on the coefficient wave)
     const int tid = threadIdx.x, wv = tid >> 6;
     const uint32_t lane = (uint32_t)(tid & 63);
     const int g = wv < 4 ? 0 : 1;
@@ -979,7 +979,7 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
     float* fu = g == 0 ? fu0 : fu1;
     float* fi = g == 0 ? fi0 : fi1;
     VarGroup& V = C.vg[g];
-    constexpr size_t tsz = (size_t)kCH * 3 * 64;       // one chunk's terms
+    constexpr size_t tsz = (size_t)kCH * 4 * 64;       // one chunk's terms
     double2* T = reinterpret_cast<double2*>(pool) + (size_t)g * 2 * tsz;
     CoefBlock* ring = reinterpret_cast<CoefBlock*>(pool + kSplitTBytes) + g * 2;
     // prefix results of the last two 64-column blocks, stored out once per
@@ -1048,22 +1048,22 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
         const double2* Tk = T + (size_t)(kk & 1) * tsz;
         double v[2 * kCH];
 #pragma unroll
-        for (int h4 = 0; h4 < 2; h4++) {            // 12 LDS reads in flight at a time (lgkmcnt holds 15)
-            double2 t[4][3];
+        for (int h2 = 0; h2 < 4; h2++) {            // 8 LDS reads in flight at a time (lgkmcnt holds 15)
+            double2 t[2][4];
 #pragma unroll
-            for (int c = 0; c < 4; c++)
+            for (int c = 0; c < 2; c++)
 #pragma unroll
-                for (int b = 0; b < 3; b++) t[c][b] = Tk[((size_t)(4 * h4 + c) * 3 + b) * 64 + lane];
+                for (int b = 0; b < 4; b++) t[c][b] = Tk[((size_t)(2 * h2 + c) * 4 + b) * 64 + lane];
 #pragma unroll
-            for (int c = 0; c < 4; c++) {
+            for (int c = 0; c < 2; c++) {
                 double pu = 0.0, pi = 0.0;
-                if ((uint32_t)(4 * h4 + c) < cn) {
+                if ((uint32_t)(2 * h2 + c) < cn) {
 #pragma unroll
-                    for (int b = 0; b < 3; b++) {
+                    for (int b = 0; b < 4; b++) {
                         if ((uint32_t)b < NB && (uint32_t)b * 64 + lane < R) { pu = pu + t[c][b].x; pi = pi + t[c][b].y; }
                     }
                 }
-                v[2 * (4 * h4 + c)] = pu; v[2 * (4 * h4 + c) + 1] = pi;
+                v[2 * (2 * h2 + c)] = pu; v[2 * (2 * h2 + c) + 1] = pi;
             }
         }
         const double z = tree16_transposed(v, lane);
@@ -1088,38 +1088,126 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
             gpw(fi)[col] = stg[((b & 1) * 2 + 1) * kCB64 + lane];
         }
     };
+    // the recurrence of chunk k for one 64-row block (lane = row), terms into T[k & 1]
+    auto rec = [&](uint32_t k, const float2* cur, uint32_t blk, double lw, double& sum0, double& M0, double& V0) {
+        const uint32_t c0 = k * kCH, cn = cn_of(k);
+        const CoefBlock& q = ring[(k / 8) & 1];
+        const uint32_t o = (k % 8) * kCH;
+        double2* Tk = T + (size_t)(k & 1) * tsz + (size_t)blk * 64 + lane;
+        if (cn == (uint32_t)kCH && k > 0) {            // full chunk, no first column: no guards
+            double2 w2[4], o2[4], a2[4], bb2[4], rw2[4], n2[4], rn2[4];
+#pragma unroll
+            for (int p = 0; p < 4; p++) {
+                w2[p] = *reinterpret_cast<const double2*>(&q.w[o + 2 * p]);
+                o2[p] = *reinterpret_cast<const double2*>(&q.Wo[o + 2 * p]);
+                a2[p] = *reinterpret_cast<const double2*>(&q.a[o + 2 * p]);
+                bb2[p] = *reinterpret_cast<const double2*>(&q.bb[o + 2 * p]);
+                rw2[p] = *reinterpret_cast<const double2*>(&q.rw[o + 2 * p]);
+                n2[p] = *reinterpret_cast<const double2*>(&q.Wn[o + 2 * p]);
+                rn2[p] = *reinterpret_cast<const double2*>(&q.rWn[o + 2 * p]);
+            }
+#pragma unroll
+            for (int p = 0; p < 4; p++) {
+                {
+                    const double x = (double)cur[2 * p].x;
+                    const double tmp = w2[p].x * sum0 - o2[p].x * x;
+                    M0 = a2[p].x * M0 + bb2[p].x * (tmp * tmp);
+                    V0 = V0 + (double)cur[2 * p].y * rw2[p].x;
+                    sum0 = sum0 + x;
+                    if (FU) Tk[(size_t)(2 * p) * 4 * 64] = make_double2(lw * (M0 * rn2[p].x), lw * (V0 * n2[p].x));
+                }
+                {
+                    const double x = (double)cur[2 * p + 1].x;
+                    const double tmp = w2[p].y * sum0 - o2[p].y * x;
+                    M0 = a2[p].y * M0 + bb2[p].y * (tmp * tmp);
+                    V0 = V0 + (double)cur[2 * p + 1].y * rw2[p].y;
+                    sum0 = sum0 + x;
+                    if (FU) Tk[(size_t)(2 * p + 1) * 4 * 64] = make_double2(lw * (M0 * rn2[p].y), lw * (V0 * n2[p].y));
+                }
+            }
+        } else {
+#pragma unroll
+            for (int c = 0; c < kCH; c++) {
+                if ((uint32_t)c < cn) {
+                    const double x = (double)cur[c].x;
+                    const double tmp = q.w[o + c] * sum0 - q.Wo[o + c] * x;
+                    if (c0 + c > 0) M0 = q.a[o + c] * M0 + q.bb[o + c] * (tmp * tmp);
+                    V0 = V0 + (double)cur[c].y * q.rw[o + c];
+                    sum0 = sum0 + x;
+                    if (FU) Tk[(size_t)c * 4 * 64] = make_double2(lw * (M0 * q.rWn[o + c]), lw * (V0 * q.Wn[o + c]));
+                }
+            }
+        }
+    };
+    // entries of chunk k for a row block (ids from the LDS ring)
+    auto load_rows = [&](const float2* Rt, size_t rstride, uint32_t k, float2* dst) {
+        const uint32_t* ids = &ring[(k / 8) & 1].vrl[(k % 8) * kCH];
+        const uint32_t cn = cn_of(k);
+#ifdef ALVRL_EXP_NOLOAD
+#pragma unroll
+        for (int c = 0; c < kCH; c++) dst[c] = make_float2((float)ids[(uint32_t)c < cn ? c : 0] * 1e-7f + (float)lane * 1e-9f, 0.25f);
+#else
+#pragma unroll
+        for (int c = 0; c < kCH; c++) dst[c] = ldg2(Rt, (size_t)ids[(uint32_t)c < cn ? c : 0] * rstride);
+#endif
+    };
+
     if (coefw) {
         // chunk k = 8B + j: reduce chunk k-1; form block B+1's coefficients
-        // (8 columns of the running total per chunk, the divisions at j = 7).
-        // Block B+2's (weight, vrl) is loaded at j = 0 and taken 8 chunks
-        // later (one block per outer iteration: no register copy of a load
-        // in flight, which would wait for it at once)
+        // (8 columns of the running total per chunk, the divisions at j = 7);
+        // with 4 row blocks this wave also runs block 3's recurrence (its
+        // entries one chunk ahead, ping-pong buffers).  Block B+2's (weight,
+        // vrl) is loaded at j = 0 and taken 8 chunks later (one block per
+        // outer iteration: no register copy of a load in flight)
+        const bool own3 = NB == 4;
+        const uint32_t r3 = min(3u * 64u + lane, R - 1);
+        const RowRef rr3 = own3 ? row_ref(J, r3) : RowRef{0, 0};
+        const double lw3 = own3 ? J.locw[r3] : 0.0;
+        const float2* const Rt3 = cm.Rt + rr3.base;
+        const size_t rs3 = rr3.stride;
+        double sum3 = 0.0, M3 = 0.0, V3 = 0.0;
+        float2 cA[kCH], cB[kCH];
+        if (own3) load_rows(Rt3, rs3, 0, cA);
+        auto stepc = [&](uint32_t B, uint32_t j, uint32_t nb, float2* cur, float2* nxt) {
+            const uint32_t k = B * 8 + j;
+            const long long ws0 = wprof ? (long long)clock64() : 0;
+#ifndef ALVRL_EXP_NORED
+            if (FU && k >= 1) reduce(k - 1);
+#endif
+            if (FU && j == 0 && B >= 1) flush(B - 1);
+            if (nb < nblk) {
+                coef_chain8(W, cw_w, j, ncol_of(nb), cWo, cWn);
+                if (j == 7 || k == nch - 1) coef_block_finish(C, cw_w, cWo, cWn, cw_v, ncol_of(nb), &ring[nb & 1]);
+            }
+            if (own3) {
+                load_rows(Rt3, rs3, min(k + 1, nch - 1), nxt);
+                rec(k, cur, 3, lw3, sum3, M3, V3);
+            }
+            if (wprof) wred += (long long)clock64() - ws0;
+            __syncthreads();
+        };
         for (uint32_t B = 0; B * 8 < nch; B++) {
             const uint32_t nb = B + 1;
             if (nb < nblk) take(kwN, nb);
             kwN = kw_of_blk(nb + 1);
 #pragma unroll 1
-            for (uint32_t j = 0; j < 8; j++) {
-                const uint32_t k = B * 8 + j;
-                if (k >= nch) break;
-                const long long ws0 = wprof ? (long long)clock64() : 0;
-#ifndef ALVRL_EXP_NORED
-                if (FU && k >= 1) reduce(k - 1);
-#endif
-                if (FU && j == 0 && B >= 1) flush(B - 1);
-                if (nb < nblk) {
-                    coef_chain8(W, cw_w, j, ncol_of(nb), cWo, cWn);
-                    if (j == 7 || k == nch - 1) coef_block_finish(C, cw_w, cWo, cWn, cw_v, ncol_of(nb), &ring[nb & 1]);
-                }
-                if (wprof) wred += (long long)clock64() - ws0;
-                __syncthreads();
+            for (uint32_t j = 0; j < 8; j += 2) {
+                if (B * 8 + j >= nch) break;
+                stepc(B, j, nb, cA, cB);
+                if (B * 8 + j + 1 >= nch) break;
+                stepc(B, j + 1, nb, cB, cA);
             }
         }
         if (FU) {
             reduce(nch - 1);
             flush((nch - 1) / 8);
-        } else if (lane == 0) {
-            V.Wcur = W;
+        } else {
+            if (lane == 0) V.Wcur = W;
+            if (own3 && 3u * 64u + lane < R) {
+                double* st = J.st + (size_t)g * 3 * R;
+                gpw(st)[R + 3u * 64u + lane] = M3;
+                gpw(st)[2 * R + 3u * 64u + lane] = V3;
+            }
         }
     } else if (roww) {
         double sum0 = 0.0, M0 = 0.0, V0 = 0.0;
@@ -1128,16 +1216,7 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
         // reload after every barrier would wait for every load in flight
         const float2* const Rt = cm.Rt + rr0.base;
         const size_t rstride = rr0.stride;
-        auto load_chunk = [&](uint32_t k, float2* dst) {    // ids from the LDS ring
-            const uint32_t* ids = &ring[(k / 8) & 1].vrl[(k % 8) * kCH];
-            const uint32_t cn = cn_of(k);
-#pragma unroll
-#ifdef ALVRL_EXP_NOLOAD
-            for (int c = 0; c < kCH; c++) dst[c] = make_float2((float)ids[(uint32_t)c < cn ? c : 0] * 1e-7f + (float)lane * 1e-9f, 0.25f);
-#else
-            for (int c = 0; c < kCH; c++) dst[c] = ldg2(Rt, (size_t)ids[(uint32_t)c < cn ? c : 0] * rstride);
-#endif
-        };
+        auto load_chunk = [&](uint32_t k, float2* dst) { load_rows(Rt, rstride, k, dst); };
         load_chunk(0, bufA);
         load_chunk(min(1u, nch - 1), bufB);
         // chunk k: issue the entries of chunk k+2 (clamped: the last chunk is
@@ -1145,55 +1224,8 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
         // run the recurrence of chunk k into T[k & 1]
         auto step = [&](uint32_t k, float2* cur, float2* pre) {
             const long long ws0 = wprof ? (long long)clock64() : 0;
-            const uint32_t c0 = k * kCH, cn = cn_of(k);
-            const CoefBlock& q = ring[(k / 8) & 1];
-            const uint32_t o = (k % 8) * kCH;
-            double2* Tk = T + (size_t)(k & 1) * tsz + (size_t)b0 * 64 + lane;
             load_chunk(min(k + 2, nch - 1), pre);
-            if (cn == (uint32_t)kCH && k > 0) {            // full chunk, no first column: no guards
-                double2 w2[4], o2[4], a2[4], bb2[4], rw2[4], n2[4], rn2[4];
-#pragma unroll
-                for (int p = 0; p < 4; p++) {
-                    w2[p] = *reinterpret_cast<const double2*>(&q.w[o + 2 * p]);
-                    o2[p] = *reinterpret_cast<const double2*>(&q.Wo[o + 2 * p]);
-                    a2[p] = *reinterpret_cast<const double2*>(&q.a[o + 2 * p]);
-                    bb2[p] = *reinterpret_cast<const double2*>(&q.bb[o + 2 * p]);
-                    rw2[p] = *reinterpret_cast<const double2*>(&q.rw[o + 2 * p]);
-                    n2[p] = *reinterpret_cast<const double2*>(&q.Wn[o + 2 * p]);
-                    rn2[p] = *reinterpret_cast<const double2*>(&q.rWn[o + 2 * p]);
-                }
-#pragma unroll
-                for (int p = 0; p < 4; p++) {
-                    {
-                        const double x = (double)cur[2 * p].x;
-                        const double tmp = w2[p].x * sum0 - o2[p].x * x;
-                        M0 = a2[p].x * M0 + bb2[p].x * (tmp * tmp);
-                        V0 = V0 + (double)cur[2 * p].y * rw2[p].x;
-                        sum0 = sum0 + x;
-                        if (FU) Tk[(size_t)(2 * p) * 3 * 64] = make_double2(lw0 * (M0 * rn2[p].x), lw0 * (V0 * n2[p].x));
-                    }
-                    {
-                        const double x = (double)cur[2 * p + 1].x;
-                        const double tmp = w2[p].y * sum0 - o2[p].y * x;
-                        M0 = a2[p].y * M0 + bb2[p].y * (tmp * tmp);
-                        V0 = V0 + (double)cur[2 * p + 1].y * rw2[p].y;
-                        sum0 = sum0 + x;
-                        if (FU) Tk[(size_t)(2 * p + 1) * 3 * 64] = make_double2(lw0 * (M0 * rn2[p].y), lw0 * (V0 * n2[p].y));
-                    }
-                }
-            } else {
-#pragma unroll
-                for (int c = 0; c < kCH; c++) {
-                    if ((uint32_t)c < cn) {
-                        const double x = (double)cur[c].x;
-                        const double tmp = q.w[o + c] * sum0 - q.Wo[o + c] * x;
-                        if (c0 + c > 0) M0 = q.a[o + c] * M0 + q.bb[o + c] * (tmp * tmp);
-                        V0 = V0 + (double)cur[c].y * q.rw[o + c];
-                        sum0 = sum0 + x;
-                        if (FU) Tk[(size_t)c * 3 * 64] = make_double2(lw0 * (M0 * q.rWn[o + c]), lw0 * (V0 * q.Wn[o + c]));
-                    }
-                }
-            }
+            rec(k, cur, b0, lw0, sum0, M0, V0);
             if (wprof) wbusy += (long long)clock64() - ws0;
             __syncthreads();
         };
@@ -1243,11 +1275,11 @@ __device__ void variance_passes(const JobDev& J, const Common& cm, Ctl& C, const
     const uint32_t NB = (J.nrows + 63) / 64;
     if (pf && (!pf->p || threadIdx.x != 0)) pf = nullptr;
     const bool lds = (size_t)2 * 2 * kCH * NB * 64 * sizeof(double2) <= kPoolBytes;
-    if (fu0 && npass == 2 && NB <= 3 && cm.var_v3) {
+    if (fu0 && npass == 2 && NB <= 4 && cm.var_v3) {
         variance_split_v3<true>(J, cm, C, base, m, 2, fu0, fi0, fu1, fi1, pool);
         return;
     }
-    if (!fu0 && NB <= 3 && cm.var_v3) {
+    if (!fu0 && NB <= 4 && cm.var_v3) {
         variance_split_v3<false>(J, cm, C, base, m, npass, nullptr, nullptr, nullptr, nullptr, pool);
         return;
     }

@@ -390,3 +390,22 @@ def test_c2_full_frame_properties(gpu_ok):
     _, ren = ctx.stats()
     assert ren == recs.shape[0] * vrls.shape[1]
     print(f"C2 frame: {ctx.last_kernel_ms():.1f} ms, mean {img.mean(0)}")
+
+
+def test_refine_bit_exact_row_blocks(oracle, gpu_ok):
+    """Local matrices of 3, 4 and 5 row blocks (up to 192 rows, 193-256 and
+    beyond: the split variance engine's row-block layouts and the older
+    engine above 256 rows): device == oracle, bit for bit."""
+    torch = _torch()
+    sizes = [129, 192, 193, 214, 256, 260]
+    ctx, d_Rt, Rt, jobs, init, init_off = _refine_case(oracle, 64, 64, 700, sizes, -1.0, torch)
+    off, reps, w, refined = ctx.refine(d_Rt, Rt.shape[1], jobs, init, init_off)
+    for s, j in enumerate(jobs):
+        cr, cw, cref = oracle.cluster_refine(Rt, j["rows"], j["locw"], init, init_off,
+                                             j["pixel_undersampling"], -1.0,
+                                             stage_refine=j["stage_refine"],
+                                             stage_sample=j["stage_sample"], seed=SEED_RNG)
+        gr, gw = reps[off[s]:off[s + 1]], w[off[s]:off[s + 1]]
+        assert bool(refined[s]) == cref, sizes[s]
+        assert np.array_equal(gr, cr), sizes[s]
+        assert np.array_equal(gw.view(np.uint32), cw.view(np.uint32)), sizes[s]
