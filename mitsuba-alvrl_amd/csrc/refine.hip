@@ -193,6 +193,7 @@ struct VarGroup {
     float res_u, res_i;
 };
 
+constexpr int kHeapLog = 96;
 struct Ctl {
     VarGroup vg[2];
     float tracingVar, unclIntVar, clUnderVar, clIntVar;
@@ -213,6 +214,9 @@ struct Ctl {
     uint32_t best_i[kWaves];
     uint32_t cnt[kWaves];
     uint32_t zeros, lo_or, hi_or, lo_and, hi_and;
+    // heap writes since the last snapshot (lane 0)
+    uint32_t hlog[kHeapLog];
+    int hlog_n, hlog_full;
 };
 
 // ------------------------------------------------------------ helpers --
@@ -399,32 +403,62 @@ __device__ __forceinline__ bool cless(const CNode& a, const CNode& b)
 {
     return a.uvar + a.ivar < b.uvar + b.ivar;
 }
-__device__ void push_heap_(CNode* first, long hole, long top, CNode value)
+// The heap lives in global memory and is worked by lane 0.  Typed global
+// accesses (not flat: a flat op makes the next LDS wait drain every load in
+// flight), and every write is logged so a snapshot copies only what changed.
+typedef uint32_t hnode_v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) hnode_v* hnode_p;
+__device__ __forceinline__ hnode_p hnodes(CNode* p) { return (hnode_p)p; }
+__device__ __forceinline__ CNode hld(hnode_p H, long i)
 {
+    const hnode_v v = H[i];
+    return CNode{__uint_as_float(v.x), __uint_as_float(v.y), v.z, v.w};
+}
+__device__ __forceinline__ void hst(hnode_p H, long i, const CNode& c)
+{
+    H[i] = hnode_v{__float_as_uint(c.uvar), __float_as_uint(c.ivar), c.begin, c.end};
+}
+__device__ __forceinline__ void heap_log(Ctl& C, long i)
+{
+    if (C.hlog_n < kHeapLog) C.hlog[C.hlog_n++] = (uint32_t)i;
+    else C.hlog_full = 1;
+}
+__device__ void push_heap_(CNode* first_g, long hole, long top, CNode value, Ctl& C)
+{
+    const hnode_p first = hnodes(first_g);
     long parent = (hole - 1) / 2;
-    while (hole > top && cless(first[parent], value)) {
-        first[hole] = first[parent];
+    while (hole > top) {
+        const CNode pn = hld(first, parent);
+        if (!cless(pn, value)) break;
+        hst(first, hole, pn);
+        heap_log(C, hole);
         hole = parent;
         parent = (hole - 1) / 2;
     }
-    first[hole] = value;
+    hst(first, hole, value);
+    heap_log(C, hole);
 }
-__device__ void adjust_heap(CNode* first, long hole, long len, CNode value)
+__device__ void adjust_heap(CNode* first_g, long hole, long len, CNode value, Ctl& C)
 {
+    const hnode_p first = hnodes(first_g);
     const long top = hole;
     long second = hole;
     while (second < (len - 1) / 2) {
         second = 2 * (second + 1);
-        if (cless(first[second], first[second - 1])) second--;
-        first[hole] = first[second];
+        const CNode r = hld(first, second), l = hld(first, second - 1);
+        const bool left = cless(r, l);
+        if (left) second--;
+        hst(first, hole, left ? l : r);
+        heap_log(C, hole);
         hole = second;
     }
     if ((len & 1) == 0 && second == (len - 2) / 2) {
         second = 2 * (second + 1);
-        first[hole] = first[second - 1];
+        hst(first, hole, hld(first, second - 1));
+        heap_log(C, hole);
         hole = second - 1;
     }
-    push_heap_(first, hole, top, value);
+    push_heap_(first_g, hole, top, value, C);
 }
 
 // lane-0-only Clustering::addCluster (:549-579)
@@ -432,25 +466,28 @@ __device__ void add_cluster(const JobDev& J, Ctl& C, uint32_t begin, uint32_t en
 {
     if (end == begin) { C.err = 1; return; }
     if (end == begin + 1) {
-        J.singles[C.singles_n++] = J.vrls[begin];
+        gpw(J.singles)[C.singles_n++] = gp(J.vrls)[begin];
         if (uvar != 0) C.err = 1;
         C.clIntVar += ivar;
     } else {
         CNode cn{uvar, ivar, begin, end};
-        J.heap[C.heap_n++] = cn;
-        push_heap_(J.heap, C.heap_n - 1, 0, cn);
+        hst(hnodes(J.heap), C.heap_n++, cn);
+        heap_log(C, C.heap_n - 1);
+        push_heap_(J.heap, C.heap_n - 1, 0, cn, C);
         C.clUnderVar += uvar;
         C.clIntVar += ivar;
     }
 }
 __device__ CNode pop_multi(const JobDev& J, Ctl& C)
 {
-    const CNode top = J.heap[0];
+    const hnode_p H = hnodes(J.heap);
+    const CNode top = hld(H, 0);
     if (C.heap_n > 1) {
         const long last = C.heap_n - 1;
-        const CNode value = J.heap[last];
-        J.heap[last] = J.heap[0];
-        adjust_heap(J.heap, 0, last, value);
+        const CNode value = hld(H, last);
+        hst(H, last, top);
+        heap_log(C, last);
+        adjust_heap(J.heap, 0, last, value, C);
     }
     C.heap_n--;
     C.clUnderVar -= top.uvar;
@@ -475,27 +512,55 @@ __device__ float lower_bound(Ctl& C, uint32_t nvrl, float pu)
 }
 
 // collective snapshot / restore (:686-699)
+// Between two snapshots the singles only grow and the heap changes where the
+// log says; a snapshot copies those (or everything after a restore or a log
+// overflow).  The snapshot's content is the same as a full copy.
 __device__ void snapshot(const JobDev& J, Ctl& C)
 {
     const int nh = C.heap_n, ns = C.singles_n;
-    for (int i = threadIdx.x; i < nh; i += kThreads) J.sh_heap[i] = J.heap[i];
-    for (int i = threadIdx.x; i < ns; i += kThreads) J.sh_singles[i] = J.singles[i];
+    const hnode_p H = hnodes(J.heap);
+    const hnode_p SH = hnodes(J.sh_heap);
+    if (C.hlog_full) {
+        for (int i = threadIdx.x; i < nh; i += kThreads) SH[i] = H[i];
+        for (int i = threadIdx.x; i < ns; i += kThreads) gpw(J.sh_singles)[i] = gp(J.singles)[i];
+    } else {
+        const int nl = C.hlog_n;
+        for (int t = threadIdx.x; t < nl; t += kThreads) {
+            const uint32_t i = C.hlog[t];
+            if ((int)i < nh) SH[i] = H[i];
+        }
+        for (int i = C.sh_singles_n + threadIdx.x; i < ns; i += kThreads) gpw(J.sh_singles)[i] = gp(J.singles)[i];
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
         C.sh_clUnderVar = C.clUnderVar; C.sh_clIntVar = C.clIntVar;
         C.sh_heap_n = nh; C.sh_singles_n = ns;
+        C.hlog_n = 0; C.hlog_full = 0;
     }
     __syncthreads();
 }
 __device__ void restore(const JobDev& J, Ctl& C)
 {
+    // The singles below the snapshot's count never change (appends only), and
+    // the heap differs from the snapshot only where the log says.
     const int nh = C.sh_heap_n, ns = C.sh_singles_n;
-    for (int i = threadIdx.x; i < nh; i += kThreads) J.heap[i] = J.sh_heap[i];
-    for (int i = threadIdx.x; i < ns; i += kThreads) J.singles[i] = J.sh_singles[i];
+    const hnode_p H = hnodes(J.heap);
+    const hnode_p SH = hnodes(J.sh_heap);
+    if (C.hlog_full) {
+        for (int i = threadIdx.x; i < nh; i += kThreads) H[i] = SH[i];
+        for (int i = threadIdx.x; i < ns; i += kThreads) gpw(J.singles)[i] = gp(J.sh_singles)[i];
+    } else {
+        const int nl = C.hlog_n;
+        for (int t = threadIdx.x; t < nl; t += kThreads) {
+            const uint32_t i = C.hlog[t];
+            if ((int)i < nh) H[i] = SH[i];
+        }
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
         C.clUnderVar = C.sh_clUnderVar; C.clIntVar = C.sh_clIntVar;
         C.heap_n = nh; C.singles_n = ns;
+        C.hlog_n = 0; C.hlog_full = 0;
     }
     __syncthreads();
 }
@@ -1811,28 +1876,42 @@ constexpr unsigned long long kSpinTicks = 6000000000ull;   // default of Common:
 
 // Thread 0 of the leader: queue the multi-clusters near the top of the heap
 // that are not queued yet.
+// The leader's queueing of the clusters near the top of the heap, on wave 0:
+// lane k examines heap entry k (one round trip for all of them instead of a
+// dependent chain on lane 0); the first 'room' eligible entries in heap order
+// are queued, as the sequential loop would.
 __device__ void enqueue_candidates(const JobDev& J, const Common& cm, Ctl& C)
 {
     const Team& T = J.team;
-    const int K = min(C.heap_n, (int)(cm.spec_width ? cm.spec_width : 2 * T.helpers + 2));
-    uint32_t tail = T.ctl[1];
+    const uint32_t lane = threadIdx.x & 63;
+    const int K = min(min(C.heap_n, (int)(cm.spec_width ? cm.spec_width : 2 * T.helpers + 2)), 64);
+    const uint32_t tail = T.ctl[1];
     const uint32_t head = ld_acq(&T.ctl[0]);
-    bool pushed = false;
-    for (int k = 0; k < K; k++) {
-        const CNode cn = J.heap[k];
-        if (cn.end - cn.begin < cm.spec_min) continue;
-        if (tail - head >= kQueue) break;
-        unsigned long long* st = &T.state[cn.begin];
-        const unsigned long long sv = __hip_atomic_load(st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if ((uint32_t)(sv >> 3) == cn.end && (sv & 7) != kStNone) continue;
-        st_rel(st, ((unsigned long long)cn.end << 3) | kStQueued);
-        __hip_atomic_store(&T.queue[tail % kQueue], ((unsigned long long)cn.begin << 32) | cn.end,
+    bool elig = false;
+    CNode cn{0.0f, 0.0f, 0u, 0u};
+    if ((int)lane < K) {
+        cn = hld(hnodes(J.heap), lane);
+        if (cn.end - cn.begin >= cm.spec_min) {
+            const unsigned long long sv = __hip_atomic_load(&T.state[cn.begin], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            elig = !((uint32_t)(sv >> 3) == cn.end && (sv & 7) != kStNone);
+        }
+    }
+    const unsigned long long bal = __ballot(elig);
+    const uint32_t used = tail - head;
+    const uint32_t room = used >= kQueue ? 0u : kQueue - used;
+    const unsigned long long lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    const uint32_t rank = (uint32_t)__popcll(bal & lt);
+    if (elig && rank < room) {
+        st_rel(&T.state[cn.begin], ((unsigned long long)cn.end << 3) | kStQueued);
+        __hip_atomic_store(&T.queue[(tail + rank) % kQueue], ((unsigned long long)cn.begin << 32) | cn.end,
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        tail++;
-        pushed = true;
         tcount(cm, TS_ENQ);
     }
-    if (pushed) st_rel(&T.ctl[1], tail);
+    const uint32_t npush = min((uint32_t)__popcll(bal), room);
+    if (npush) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        if (lane == 0) st_rel(&T.ctl[1], tail + npush);
+    }
 }
 
 __device__ void stop_team(const JobDev& J, const Common& cm)
@@ -1904,9 +1983,9 @@ __device__ void split_team(const JobDev& J, const Common& cm, Ctl& C, uint32_t b
     const Team& T = J.team;
     if (!T.helpers || !spec) { split(J, cm, C, b, e, lds, pf); return; }
     const int tid = threadIdx.x;
+    if (tid < 64) enqueue_candidates(J, cm, C);
     if (tid == 0) {
         trace(cm, 3, b);
-        enqueue_candidates(J, cm, C);
         unsigned long long* st = &T.state[b];
         const unsigned long long key = (unsigned long long)e << 3;
         unsigned long long sv = ld_acq(st);
@@ -1973,7 +2052,8 @@ __device__ void split_team(const JobDev& J, const Common& cm, Ctl& C, uint32_t b
         }
         __syncthreads();
     }
-    if (tid == 0) { enqueue_candidates(J, cm, C); trace(cm, 5, b); }
+    if (tid < 64) enqueue_candidates(J, cm, C);
+    if (tid == 0) trace(cm, 5, b);
     __syncthreads();
 }
 
@@ -2276,6 +2356,7 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
         C.tracingVar = C.unclIntVar = C.clUnderVar = C.clIntVar = 0.0f;
         C.heap_n = C.singles_n = C.sh_heap_n = C.sh_singles_n = 0;
         C.err = 0; C.refined = 1;
+        C.hlog_n = 0; C.hlog_full = 1;
     }
     __syncthreads();
     column_weights(J, cm, C);
