@@ -153,7 +153,7 @@ __device__ __forceinline__ void tcount(const Common& cm, int k)
 // Phase timer of lane 0 (s_memtime deltas summed over jobs).
 enum { PF_COLW, PF_INIT, PF_UNCL, PF_WSAMP, PF_DIR, PF_PROJ, PF_SORT, PF_CVF, PF_CVR, PF_ARGMIN,
        PF_CTRL, PF_REPS, PF_V_COEF, PF_V_REC, PF_V_RED, PF_P_STAGE, PF_P_COMP, PF_V_OWN, PF_V_CW,
-       PF_V_ISSUE, PF_V_DATA,
+       PF_V_ISSUE, PF_V_DATA, PF_T_HEAP, PF_T_ENQ, PF_T_WAIT, PF_T_SIDE, PF_T_COMMIT,
        PF_NSPLIT, PF_SPLITCOLS, PF_N };
 static const char* kPfNames[PF_N] = {"column weights", "initial clusters", "unclustered var",
                                      "split: centres", "split: direction", "split: projections",
@@ -163,6 +163,8 @@ static const char* kPfNames[PF_N] = {"column weights", "initial clusters", "uncl
                                      " proj: staging", " proj: compute",
                                      "  rec: row wave 0 busy", "  rec: coef wave busy",
                                      "   row wave: prefetch issue", "   row wave: wait for data",
+                                     "ctrl: heap pop/snapshot", "ctrl: enqueue", "ctrl: wait for helper",
+                                     "ctrl: side splits", "ctrl: commit",
                                      "#splits", "#split columns"};
 struct Prof {
     unsigned long long* p;
@@ -1867,6 +1869,27 @@ __device__ __forceinline__ uint32_t ld_rlx(uint32_t* p)
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ void fence_acq() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent"); }
+// Task bookkeeping (queue slots, tail, head, per-cluster state words) carries
+// no payload of its own: relaxed agent-scope atomics, ordered where it
+// matters by draining them (s_waitcnt vmcnt(0)) before the next one.  The
+// only payload is the vrls a helper copies, released once per split by the
+// leader (split_team) and acquired by the helper (spec_split).  An
+// agent-scope release is an L2 write-back (MI355X_MICROARCH.md, fence table).
+__device__ __forceinline__ void st_rlx(unsigned long long* p, unsigned long long v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_rlx(uint32_t* p, uint32_t v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T>
+__device__ __forceinline__ bool cas_rlx(T* p, T expect, T v)
+{
+    return __hip_atomic_compare_exchange_strong(p, &expect, v, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void drain_vmem() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 // constant 100 MHz clock.  No wait is unbounded: a leader that has waited
 // kSpinTicks (~60 s) for a helper splits the cluster itself (the helper's late
 // result lands in side buffers nobody commits), an idle helper gives up after
@@ -1879,14 +1902,15 @@ constexpr unsigned long long kSpinTicks = 6000000000ull;   // default of Common:
 // The leader's queueing of the clusters near the top of the heap, on wave 0:
 // lane k examines heap entry k (one round trip for all of them instead of a
 // dependent chain on lane 0); the first 'room' eligible entries in heap order
-// are queued, as the sequential loop would.
+// are queued, as the sequential loop would.  The vrls of every cluster in the
+// heap were released when its parent's split ended (split_team).
 __device__ void enqueue_candidates(const JobDev& J, const Common& cm, Ctl& C)
 {
     const Team& T = J.team;
     const uint32_t lane = threadIdx.x & 63;
     const int K = min(min(C.heap_n, (int)(cm.spec_width ? cm.spec_width : 2 * T.helpers + 2)), 64);
     const uint32_t tail = T.ctl[1];
-    const uint32_t head = ld_acq(&T.ctl[0]);
+    const uint32_t head = ld_rlx(&T.ctl[0]);
     bool elig = false;
     CNode cn{0.0f, 0.0f, 0u, 0u};
     if ((int)lane < K) {
@@ -1902,15 +1926,14 @@ __device__ void enqueue_candidates(const JobDev& J, const Common& cm, Ctl& C)
     const unsigned long long lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     const uint32_t rank = (uint32_t)__popcll(bal & lt);
     if (elig && rank < room) {
-        st_rel(&T.state[cn.begin], ((unsigned long long)cn.end << 3) | kStQueued);
-        __hip_atomic_store(&T.queue[(tail + rank) % kQueue], ((unsigned long long)cn.begin << 32) | cn.end,
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        st_rlx(&T.state[cn.begin], ((unsigned long long)cn.end << 3) | kStQueued);
+        st_rlx(&T.queue[(tail + rank) % kQueue], ((unsigned long long)cn.begin << 32) | cn.end);
         tcount(cm, TS_ENQ);
     }
     const uint32_t npush = min((uint32_t)__popcll(bal), room);
     if (npush) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        if (lane == 0) st_rel(&T.ctl[1], tail + npush);
+        drain_vmem();   // slots and states land before the tail that publishes them
+        if (lane == 0) st_rlx(&T.ctl[1], tail + npush);
     }
 }
 
@@ -1933,13 +1956,11 @@ __device__ int try_claim(const Team& T, uint32_t* b, uint32_t* e)
 {
     const uint32_t h = ld_rlx(&T.ctl[0]), t = ld_rlx(&T.ctl[1]);
     if (h >= t) return 0;
-    fence_acq();
-    const unsigned long long task = __hip_atomic_load(&T.queue[h % kQueue], __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_AGENT);
-    if (!cas_acq_rel(&T.ctl[0], h, h + 1)) return 2;
+    const unsigned long long task = ld_rlx(&T.queue[h % kQueue]);
+    if (!cas_rlx(&T.ctl[0], h, h + 1)) return 2;
     *b = (uint32_t)(task >> 32); *e = (uint32_t)task;
     const unsigned long long want = ((unsigned long long)*e << 3) | kStQueued;
-    return cas_acq_rel(&T.state[*b], want, ((unsigned long long)*e << 3) | kStRunning) ? 1 : 2;
+    return cas_rlx(&T.state[*b], want, ((unsigned long long)*e << 3) | kStRunning) ? 1 : 2;   // spec_split acquires
 }
 
 // Split [b, e) speculatively with Jw's scratch (Jw.vrls = team.spec) and
@@ -1988,10 +2009,10 @@ __device__ void split_team(const JobDev& J, const Common& cm, Ctl& C, uint32_t b
         trace(cm, 3, b);
         unsigned long long* st = &T.state[b];
         const unsigned long long key = (unsigned long long)e << 3;
-        unsigned long long sv = ld_acq(st);
+        unsigned long long sv = ld_rlx(st);
         int mode = 0;
         if ((uint32_t)(sv >> 3) == e && (sv & 7) != kStNone && (sv & 7) != kStLeader) {
-            if ((sv & 7) == kStQueued && cas_acq_rel(st, sv, key | kStLeader)) {
+            if ((sv & 7) == kStQueued && cas_rlx(st, sv, key | kStLeader)) {
                 mode = 0;
                 tcount(cm, TS_STEAL);
             } else {
@@ -2000,12 +2021,13 @@ __device__ void split_team(const JobDev& J, const Common& cm, Ctl& C, uint32_t b
                 trace(cm, 4, b);
             }
         } else {
-            st_rel(st, key | kStLeader);
+            st_rlx(st, key | kStLeader);
             tcount(cm, TS_OWN);
         }
         C.tmode = mode;
     }
     __syncthreads();
+    pf.mark(PF_T_ENQ);
     while (true) {
         const int tm = C.tmode;
         __syncthreads();   // every thread has read tmode before thread 0 rewrites it
@@ -2028,8 +2050,10 @@ __device__ void split_team(const JobDev& J, const Common& cm, Ctl& C, uint32_t b
             }
         }
         __syncthreads();
+        pf.mark(PF_T_WAIT);
         if (C.side) spec_split(J, J_spec(J), cm, C, lds, C.yb, C.ye);
         __syncthreads();
+        pf.mark(PF_T_SIDE);
     }
     const int mode = C.tmode;
     if (mode == 0) {
@@ -2051,10 +2075,19 @@ __device__ void split_team(const JobDev& J, const Common& cm, Ctl& C, uint32_t b
             }
         }
         __syncthreads();
+        pf.mark(PF_T_COMMIT);
     }
-    if (tid < 64) enqueue_candidates(J, cm, C);
+    // release this split's vrls (every wave drained, barrier, one write-back)
+    // before its children can be queued
+    drain_vmem();
+    __syncthreads();
+    if (tid < 64) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        enqueue_candidates(J, cm, C);
+    }
     if (tid == 0) trace(cm, 5, b);
     __syncthreads();
+    pf.mark(PF_T_ENQ);
 }
 
 // A helper workgroup: split queued clusters of job J until the leader stops.
@@ -2381,6 +2414,11 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
     pf.mark(PF_INIT);
     unclustered_variance(J, cm, C, nv);
     pf.mark(PF_UNCL);
+    // release the initial clusters' vrls to the helpers (see split_team)
+    drain_vmem();
+    __syncthreads();
+    if (tid == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __syncthreads();
 
     // refine (:380-489)
     if (J.do_refine && !C.err) {
@@ -2419,6 +2457,7 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
                     }
                     __syncthreads();
                     if (!C.go) break;
+                    pf.mark(PF_T_HEAP);
                     split_team(J, cm, C, C.b, C.e, lds, pf, true);
                     if (tid == 0) {
                         nsplit++;
