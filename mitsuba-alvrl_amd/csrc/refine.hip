@@ -72,6 +72,13 @@ struct Team {
     const SplitWs* ws;                // [helpers]
 };
 enum : uint32_t { kStNone = 0, kStQueued = 1, kStRunning = 2, kStDone = 3, kStLeader = 4 };
+// A cluster born from a committed speculative split has its vrls in team.spec
+// already (the parent's output, which the leader copied to vrls): bit 63 of
+// its state word and bit 31 of its queue entry's end say so, and its helper
+// splits team.spec in place instead of copying vrls, which the leader then
+// need not release.
+constexpr unsigned long long kStSpecBit = 1ull << 63;
+constexpr uint32_t kQSpecBit = 1u << 31;
 constexpr uint32_t kQueue = 1024;
 
 struct JobDev {
@@ -127,6 +134,7 @@ struct Common {
     uint32_t njobs;                // leaders = blocks [0, njobs); helpers follow, team by team
     uint32_t team;                 // workgroups per job (1 = no speculation)
     uint32_t spec_min;             // smallest cluster worth a speculative split
+    uint32_t side_k;               // a waiting leader takes a side task of <= awaited columns * side_k / 16
     unsigned long long spin_ticks; // bound of every team wait (100 MHz ticks)
     unsigned long long* tstat;     // team counters (ALVRL_REFINE_TEAM_STATS=1), or null
     unsigned long long* jtime;     // with tstat: per job, wall ticks at start / end of refine / end
@@ -1912,12 +1920,15 @@ __device__ void enqueue_candidates(const JobDev& J, const Common& cm, Ctl& C)
     const uint32_t tail = T.ctl[1];
     const uint32_t head = ld_rlx(&T.ctl[0]);
     bool elig = false;
+    unsigned long long spec = 0;
     CNode cn{0.0f, 0.0f, 0u, 0u};
     if ((int)lane < K) {
         cn = hld(hnodes(J.heap), lane);
         if (cn.end - cn.begin >= cm.spec_min) {
-            const unsigned long long sv = __hip_atomic_load(&T.state[cn.begin], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            elig = !((uint32_t)(sv >> 3) == cn.end && (sv & 7) != kStNone);
+            const unsigned long long sv = ld_rlx(&T.state[cn.begin]);
+            const bool mine = (uint32_t)(sv >> 3) == cn.end;
+            elig = !(mine && (sv & 7) != kStNone);
+            spec = mine ? (sv & kStSpecBit) : 0ull;
         }
     }
     const unsigned long long bal = __ballot(elig);
@@ -1926,8 +1937,8 @@ __device__ void enqueue_candidates(const JobDev& J, const Common& cm, Ctl& C)
     const unsigned long long lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     const uint32_t rank = (uint32_t)__popcll(bal & lt);
     if (elig && rank < room) {
-        st_rlx(&T.state[cn.begin], ((unsigned long long)cn.end << 3) | kStQueued);
-        st_rlx(&T.queue[(tail + rank) % kQueue], ((unsigned long long)cn.begin << 32) | cn.end);
+        st_rlx(&T.state[cn.begin], ((unsigned long long)cn.end << 3) | kStQueued | spec);
+        st_rlx(&T.queue[(tail + rank) % kQueue], ((unsigned long long)cn.begin << 32) | cn.end | (spec ? kQSpecBit : 0u));
         tcount(cm, TS_ENQ);
     }
     const uint32_t npush = min((uint32_t)__popcll(bal), room);
@@ -1952,18 +1963,20 @@ __device__ __forceinline__ JobDev J_spec(const JobDev& J)
 
 // Thread 0: take the oldest queued task.  1 = claimed (*b, *e), 0 = queue
 // empty, 2 = lost a race (try again).
-__device__ int try_claim(const Team& T, uint32_t* b, uint32_t* e)
+__device__ int try_claim(const Team& T, uint32_t* b, uint32_t* e, uint64_t max_cols = ~0ull)
 {
     const uint32_t h = ld_rlx(&T.ctl[0]), t = ld_rlx(&T.ctl[1]);
     if (h >= t) return 0;
     const unsigned long long task = ld_rlx(&T.queue[h % kQueue]);
+    if (((uint32_t)task & ~kQSpecBit) - (uint32_t)(task >> 32) > max_cols) return 0;
     if (!cas_rlx(&T.ctl[0], h, h + 1)) return 2;
-    *b = (uint32_t)(task >> 32); *e = (uint32_t)task;
-    const unsigned long long want = ((unsigned long long)*e << 3) | kStQueued;
-    return cas_rlx(&T.state[*b], want, ((unsigned long long)*e << 3) | kStRunning) ? 1 : 2;   // spec_split acquires
+    *b = (uint32_t)(task >> 32); *e = (uint32_t)task;   // end with kQSpecBit
+    const unsigned long long key = ((unsigned long long)(*e & ~kQSpecBit) << 3) | ((*e & kQSpecBit) ? kStSpecBit : 0ull);
+    return cas_rlx(&T.state[*b], key | kStQueued, key | kStRunning) ? 1 : 2;   // spec_split acquires
 }
 
-// Split [b, e) speculatively with Jw's scratch (Jw.vrls = team.spec) and
+// Split [b, e) speculatively with Jw's scratch (Jw.vrls = team.spec; e may
+// carry kQSpecBit: the input is there already) and
 // publish the result (MI355X_MICROARCH.md, valid producer form: every storing
 // wave drains, barrier, lane 0 releases at agent scope and drains the
 // write-back, then the relaxed agent flag store).  C.err is the caller's.
@@ -1972,9 +1985,12 @@ __device__ void spec_split(const JobDev& J0, const JobDev& Jw, const Common& cm,
 {
     const Team& T = J0.team;
     const int tid = threadIdx.x;
+    const bool in_spec = (e & kQSpecBit) != 0;
+    e &= ~kQSpecBit;
     fence_acq();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    for (uint32_t i = b + (uint32_t)tid; i < e; i += kThreads) T.spec[i] = J0.vrls[i];
+    if (!in_spec)
+        for (uint32_t i = b + (uint32_t)tid; i < e; i += kThreads) T.spec[i] = J0.vrls[i];
     __syncthreads();
     const int err_saved = C.err;
     __syncthreads();
@@ -2044,7 +2060,7 @@ __device__ void split_team(const JobDev& J, const Common& cm, Ctl& C, uint32_t b
                 tcount(cm, TS_WAIT_TMO);
             } else {
                 uint32_t yb = 0, ye = 0;
-                const int got = try_claim(T, &yb, &ye);
+                const int got = try_claim(T, &yb, &ye, (uint64_t)(e - b) * cm.side_k / 16);
                 if (got == 1) { C.side = 1; C.yb = yb; C.ye = ye; tcount(cm, TS_LSIDE); }
                 else if (got == 0) __builtin_amdgcn_s_sleep(8);
             }
@@ -2071,18 +2087,22 @@ __device__ void split_team(const JobDev& J, const Common& cm, Ctl& C, uint32_t b
                 const uint32_t m = e - b, s2 = b + r.idx;
                 add_cluster(J, C, b, s2, r.fsu, r.fsi);
                 add_cluster(J, C, s2, e, r.feu, r.fei);
+                // the children's input is this result, in team.spec
+                st_rlx(&T.state[b], ((unsigned long long)s2 << 3) | kStNone | kStSpecBit);
+                st_rlx(&T.state[s2], ((unsigned long long)e << 3) | kStNone | kStSpecBit);
                 (void)m;
             }
         }
         __syncthreads();
         pf.mark(PF_T_COMMIT);
     }
-    // release this split's vrls (every wave drained, barrier, one write-back)
-    // before its children can be queued
+    // an own split releases its vrls (every wave drained, barrier, one
+    // write-back) before its children can be queued; a committed one's
+    // children read team.spec
     drain_vmem();
     __syncthreads();
     if (tid < 64) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        if (mode == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         enqueue_candidates(J, cm, C);
     }
     if (tid == 0) trace(cm, 5, b);
@@ -2841,6 +2861,8 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
     {
         const char* sm = std::getenv("ALVRL_SPEC_MIN");
         cm.spec_min = sm ? (uint32_t)std::max(2, std::atoi(sm)) : 16u;
+        const char* sk = std::getenv("ALVRL_LEADER_SIDE");
+        cm.side_k = sk ? (uint32_t)std::max(0, std::atoi(sk)) : 1u << 24;
     }
     cm.init_vrls = d_init; cm.init_off = d_init_off; cm.ninit = ninit;
     cm.seed = seed; cm.pass = pass;
