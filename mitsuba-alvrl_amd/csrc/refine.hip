@@ -134,7 +134,8 @@ struct Common {
     uint32_t njobs;                // leaders = blocks [0, njobs); helpers follow, team by team
     uint32_t team;                 // workgroups per job (1 = no speculation)
     uint32_t spec_min;             // smallest cluster worth a speculative split
-    uint32_t side_k;               // a waiting leader takes a side task of <= awaited columns * side_k / 16
+    uint32_t side_k;
+    int enq_start;                 // also queue candidates right after the pop (before the split)               // a waiting leader takes a side task of <= awaited columns * side_k / 16
     unsigned long long spin_ticks; // bound of every team wait (100 MHz ticks)
     unsigned long long* tstat;     // team counters (ALVRL_REFINE_TEAM_STATS=1), or null
     unsigned long long* jtime;     // with tstat: per job, wall ticks at start / end of refine / end
@@ -488,20 +489,84 @@ __device__ void add_cluster(const JobDev& J, Ctl& C, uint32_t begin, uint32_t en
         C.clIntVar += ivar;
     }
 }
-__device__ CNode pop_multi(const JobDev& J, Ctl& C)
+// std::pop_heap (Clustering's heap pop, via pop_multi's move of the top to
+// the end and __adjust_heap + __push_heap), on wave 0.  The sift-down path is
+// found five levels per round trip: lane t loads node t of the 62-node
+// subtree below the current hole, each lane decides whether it is the child
+// __adjust_heap would descend to (the right one unless right < left; the left
+// one when it is the only child), and the path is read off the ballot.  The
+// moved last element then climbs that path while the node above it is less
+// (__push_heap), which only needs the path's original values: lane i holds
+// path node i.  Final array = std::pop_heap's; the slots written are logged.
+__device__ CNode pop_wave(const JobDev& J, Ctl& C)
 {
+    const int lane = (int)(threadIdx.x & 63);
     const hnode_p H = hnodes(J.heap);
+    const long n = __builtin_amdgcn_readfirstlane(C.heap_n);
     const CNode top = hld(H, 0);
-    if (C.heap_n > 1) {
-        const long last = C.heap_n - 1;
-        const CNode value = hld(H, last);
-        hst(H, last, top);
-        heap_log(C, last);
-        adjust_heap(J.heap, 0, last, value, C);
+    if (n > 1) {
+        const long len = n - 1;
+        const CNode value = hld(H, len);
+        const float vkey = value.uvar + value.ivar;
+        long h = 0;                        // current path node (uniform)
+        int L = 0;                         // path length: p_0 = 0 .. p_L
+        long pidx = 0;                     // lane i: index of path node i
+        hnode_v pv = {0u, 0u, 0u, 0u};     // lane i: its original value
+        const int k = 31 - __builtin_clz((uint32_t)lane + 2);
+        const long j = (long)lane + 2 - (1l << k);
+        bool more = true;
+        while (more) {
+            const long idx = ((h + 1) << k) - 1 + j;
+            const bool ex = lane < 62 && idx < len;
+            hnode_v v = {0u, 0u, 0u, 0u};
+            if (ex) v = H[idx];
+            const float key = __uint_as_float(v.x) + __uint_as_float(v.y);
+            const float skey = __shfl_xor(key, 1);
+            const int sex = __shfl_xor((int)ex, 1);
+            // left (even j): taken unless the right exists and !(right < left)
+            const bool chosen = (j & 1) ? (ex && !(key < skey)) : (ex && (!sex || skey < key));
+            const unsigned long long mask = __ballot(chosen);
+            long jp = 0;
+            for (int kk = 1; kk <= 5; kk++) {
+                const int lc = (1 << kk) - 2 + 2 * (int)jp;
+                const unsigned long long two = (mask >> lc) & 3ull;
+                if (!two) { more = false; break; }
+                const int c = (two & 1ull) ? lc : lc + 1;
+                jp = 2 * jp + (c - lc);
+                const long ic = ((h + 1) << kk) - 1 + jp;
+                hnode_v vc;
+                vc.x = __builtin_amdgcn_readlane(v.x, c);
+                vc.y = __builtin_amdgcn_readlane(v.y, c);
+                vc.z = __builtin_amdgcn_readlane(v.z, c);
+                vc.w = __builtin_amdgcn_readlane(v.w, c);
+                L++;
+                if (lane == L) { pidx = ic; pv = vc; }
+                if (kk == 5) h = ic;
+            }
+        }
+        // __push_heap from p_L: climbs while the node above is less
+        const bool stay = lane >= 1 && lane <= L && !((__uint_as_float(pv.x) + __uint_as_float(pv.y)) < vkey);
+        const unsigned long long nf = __ballot(stay);
+        const int fin = nf ? 63 - __builtin_clzll(nf) : 0;
+        hnode_v up;
+        up.x = __shfl_down(pv.x, 1); up.y = __shfl_down(pv.y, 1);
+        up.z = __shfl_down(pv.z, 1); up.w = __shfl_down(pv.w, 1);
+        if (lane < fin) H[pidx] = up;
+        if (lane == fin) hst(H, pidx, value);
+        if (lane == 0) hst(H, len, top);
+        const int base = C.hlog_n, w = fin + 2;
+        if (base + w <= kHeapLog) {
+            if (lane <= fin) C.hlog[base + lane] = (uint32_t)pidx;
+            if (lane == 0) { C.hlog[base + fin + 1] = (uint32_t)len; C.hlog_n = base + w; }
+        } else if (lane == 0) {
+            C.hlog_full = 1;
+        }
     }
-    C.heap_n--;
-    C.clUnderVar -= top.uvar;
-    C.clIntVar -= top.ivar;
+    if (lane == 0) {
+        C.heap_n = (int)n - 1;
+        C.clUnderVar -= top.uvar;
+        C.clIntVar -= top.ivar;
+    }
     return top;
 }
 
@@ -2020,7 +2085,7 @@ __device__ void split_team(const JobDev& J, const Common& cm, Ctl& C, uint32_t b
     const Team& T = J.team;
     if (!T.helpers || !spec) { split(J, cm, C, b, e, lds, pf); return; }
     const int tid = threadIdx.x;
-    if (tid < 64) enqueue_candidates(J, cm, C);
+    if (tid < 64 && cm.enq_start) enqueue_candidates(J, cm, C);
     if (tid == 0) {
         trace(cm, 3, b);
         unsigned long long* st = &T.state[b];
@@ -2446,9 +2511,13 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
             // refineFixedDepth (:387-399)
             const uint32_t target = (uint32_t)(0.5 + (double)((float)N / J.undersampling));
             while (true) {
-                if (tid == 0) {
-                    C.go = (n_clusters(C) < target && C.heap_n > 0 && !C.err);
-                    if (C.go) { const CNode cn = pop_multi(J, C); C.b = cn.begin; C.e = cn.end; split_cols += cn.end - cn.begin; }
+                if (tid < 64) {   // wave 0 decides (every lane reads C itself) and pops (pop_wave)
+                    const bool go = (n_clusters(C) < target && C.heap_n > 0 && !C.err);
+                    if (tid == 0) C.go = go;
+                    if (go) {
+                        const CNode cn = pop_wave(J, C);
+                        if (tid == 0) { C.b = cn.begin; C.e = cn.end; split_cols += cn.end - cn.begin; }
+                    }
                 }
                 __syncthreads();
                 if (!C.go) break;
@@ -2471,9 +2540,13 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
                 if (tid == 0) { best = conv_const(C, N, J.pixel_under); nsplit = 0; bestN = 0; }
                 snapshot(J, C);
                 while (true) {
-                    if (tid == 0) {
-                        C.go = C.heap_n > 0 && !C.err;
-                        if (C.go) { const CNode cn = pop_multi(J, C); C.b = cn.begin; C.e = cn.end; split_cols += cn.end - cn.begin; }
+                    if (tid < 64) {   // wave 0 decides (every lane reads C itself) and pops (pop_wave)
+                        const bool go = C.heap_n > 0 && !C.err;
+                        if (tid == 0) C.go = go;
+                        if (go) {
+                            const CNode cn = pop_wave(J, C);
+                            if (tid == 0) { C.b = cn.begin; C.e = cn.end; split_cols += cn.end - cn.begin; }
+                        }
                     }
                     __syncthreads();
                     if (!C.go) break;
@@ -2499,9 +2572,13 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
                 if (dc != 1) {
                     const int corrected = (int)(0.5 + dc * bestN);
                     for (int i = 0; i < corrected; i++) {
-                        if (tid == 0) {
-                            C.go = C.heap_n > 0 && !C.err;
-                            if (C.go) { const CNode cn = pop_multi(J, C); C.b = cn.begin; C.e = cn.end; split_cols += cn.end - cn.begin; }
+                        if (tid < 64) {   // wave 0 decides (every lane reads C itself) and pops (pop_wave)
+                            const bool go = C.heap_n > 0 && !C.err;
+                            if (tid == 0) C.go = go;
+                            if (go) {
+                                const CNode cn = pop_wave(J, C);
+                                if (tid == 0) { C.b = cn.begin; C.e = cn.end; split_cols += cn.end - cn.begin; }
+                            }
                         }
                         __syncthreads();
                         if (!C.go) break;
@@ -2839,7 +2916,7 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
     cm.roam_on = roam_on && tarena ? 1 : 0;
     {
         const char* sw = std::getenv("ALVRL_SPEC_WIDTH");
-        cm.spec_width = sw ? (uint32_t)std::max(1, std::atoi(sw)) : 12u;   // profiles/r01/team: 6 -> 727 ms, 16 -> 713 ms
+        cm.spec_width = sw ? (uint32_t)std::max(1, std::atoi(sw)) : 16u;   // sweeps: 12 -> 424 ms, 16 -> 420 ms (C4 refine)
     }
     {
         const char* sp = std::getenv("ALVRL_REFINE_SPIN_MS");
@@ -2863,6 +2940,8 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
         cm.spec_min = sm ? (uint32_t)std::max(2, std::atoi(sm)) : 16u;
         const char* sk = std::getenv("ALVRL_LEADER_SIDE");
         cm.side_k = sk ? (uint32_t)std::max(0, std::atoi(sk)) : 1u << 24;
+        const char* es = std::getenv("ALVRL_ENQ_START");
+        cm.enq_start = es ? std::atoi(es) : 1;
     }
     cm.init_vrls = d_init; cm.init_off = d_init_off; cm.ninit = ninit;
     cm.seed = seed; cm.pass = pass;
