@@ -2020,6 +2020,29 @@ __device__ void stop_team(const JobDev& J, const Common& cm)
     trace(cm, 6, 0);
 }
 
+// Block copy of vrls[b, e) between the job's array and the side buffer:
+// typed global accesses, eight loads in flight per thread before their
+// stores (a one-element loop waits out a cross-XCD load per element).
+__device__ void copy_range(uint32_t* dst, const uint32_t* src, uint32_t b, uint32_t e)
+{
+    const auto d = gpw(dst);
+    const auto sp = gp(src);
+    constexpr uint32_t U = 8;
+    for (uint32_t i0 = b + threadIdx.x; i0 < e; i0 += U * kThreads) {
+        uint32_t v[U];
+#pragma unroll
+        for (uint32_t k = 0; k < U; k++) {
+            const uint32_t i = i0 + k * kThreads;
+            v[k] = i < e ? sp[i] : 0u;
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < U; k++) {
+            const uint32_t i = i0 + k * kThreads;
+            if (i < e) d[i] = v[k];
+        }
+    }
+}
+
 __device__ __forceinline__ JobDev J_spec(const JobDev& J)
 {
     JobDev Jw = J;
@@ -2056,7 +2079,7 @@ __device__ void spec_split(const JobDev& J0, const JobDev& Jw, const Common& cm,
     fence_acq();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (!in_spec)
-        for (uint32_t i = b + (uint32_t)tid; i < e; i += kThreads) T.spec[i] = J0.vrls[i];
+        copy_range(T.spec, J0.vrls, b, e);
     __syncthreads();
     const int err_saved = C.err;
     __syncthreads();
@@ -2143,7 +2166,7 @@ __device__ void split_team(const JobDev& J, const Common& cm, Ctl& C, uint32_t b
     } else if (mode == 1) {
         fence_acq();
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        for (uint32_t i = b + (uint32_t)tid; i < e; i += kThreads) J.vrls[i] = T.spec[i];
+        copy_range(J.vrls, T.spec, b, e);
         __syncthreads();
         if (tid == 0) {
             const SplitRes r = T.res[b];
