@@ -2941,7 +2941,7 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
     cm.roam_on = roam_on && tarena ? 1 : 0;
     {
         const char* sw = std::getenv("ALVRL_SPEC_WIDTH");
-        cm.spec_width = sw ? (uint32_t)std::max(1, std::atoi(sw)) : 16u;   // sweeps: 12 -> 424 ms, 16 -> 420 ms (C4 refine)
+        cm.spec_width = sw ? (uint32_t)std::max(1, std::atoi(sw)) : 24u;   // C4 refine sweeps (tools/env_sweep.sh), min 2: width 20 403 ms, 24 403, 28 405
     }
     {
         const char* sp = std::getenv("ALVRL_REFINE_SPIN_MS");
@@ -2962,7 +2962,7 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
     }
     {
         const char* sm = std::getenv("ALVRL_SPEC_MIN");
-        cm.spec_min = sm ? (uint32_t)std::max(2, std::atoi(sm)) : 16u;
+        cm.spec_min = sm ? (uint32_t)std::max(2, std::atoi(sm)) : 2u;   // width 16: min 32 447 ms, 16 422, 8 413, 4 409, 2 407
         const char* sk = std::getenv("ALVRL_LEADER_SIDE");
         cm.side_k = sk ? (uint32_t)std::max(0, std::atoi(sk)) : 1u << 24;
         const char* es = std::getenv("ALVRL_ENQ_START");
