@@ -2941,7 +2941,7 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
     cm.roam_on = roam_on && tarena ? 1 : 0;
     {
         const char* sw = std::getenv("ALVRL_SPEC_WIDTH");
-        cm.spec_width = sw ? (uint32_t)std::max(1, std::atoi(sw)) : 24u;   // C4 refine sweeps (tools/env_sweep.sh), min 2: width 20 403 ms, 24 403, 28 405
+        cm.spec_width = sw ? (uint32_t)std::max(1, std::atoi(sw)) : 32u;   // C4 refine sweeps (tools/env_sweep.sh), min 2: width 24 401 ms; 32 398 (no queueing after the pop)
     }
     {
         const char* sp = std::getenv("ALVRL_REFINE_SPIN_MS");
@@ -2966,7 +2966,7 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
         const char* sk = std::getenv("ALVRL_LEADER_SIDE");
         cm.side_k = sk ? (uint32_t)std::max(0, std::atoi(sk)) : 1u << 24;
         const char* es = std::getenv("ALVRL_ENQ_START");
-        cm.enq_start = es ? std::atoi(es) : 1;
+        cm.enq_start = es ? std::atoi(es) : 0;   // queueing after the commit only: 398 vs 401 ms at width 32
     }
     // ALVRL_ROAM_ORDER=1: roaming helpers scan the jobs with the most rows
     // first.  Measured slower (C4 refine 436 vs 420 ms: the roamers crowd the
