@@ -193,10 +193,17 @@ def main():
         pass
 
     def roof(name, key, bytes_per_launch, ms, note):
+        # achieved / frac: ALGORITHMIC bytes per launch (the contract's
+        # definition); traffic: measured HBM bytes per launch
+        # (rocprofv3 PMC, FETCH_SIZE x2 + WRITE_SIZE), and hbm_achieved /
+        # hbm_frac the rate those bytes moved at in the same launch time
         s_ = ms / 1e3
         ach = bytes_per_launch / s_ / 1e9 if s_ > 0 else 0.0
+        tr = pmc.get(key)
+        hbm = tr / s_ / 1e9 if (tr is not None and s_ > 0) else None
         return {"bound": "hbm", "kernel": name, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": ach / HBM_PEAK_GBS, "traffic": pmc.get(key), "bytes_per_launch": bytes_per_launch,
+                "frac": ach / HBM_PEAK_GBS, "traffic": tr, "bytes_per_launch": bytes_per_launch,
+                "hbm_achieved": hbm, "hbm_frac": hbm / HBM_PEAK_GBS if hbm is not None else None,
                 "launch_ms": ms, "note": note}
 
     pairs_per_launch_rank = (s1["contrib_render"] - s0["contrib_render"]) / nst
@@ -332,19 +339,32 @@ def cpu_baseline_prepass(args, cfg, vrls, pc, it, render_base, pre_pairs_step, r
     t0 = time.perf_counter()
     _, Rs, cnt = o.gather_brute(P, recs, vrls, pc, rec_ids=rec_ids, domain=2, want_R=True, nthreads=threads)
     t_r = time.perf_counter() - t0
-    Rt = np.ascontiguousarray(Rs.transpose(1, 0, 2))
-    nrow = Rt.shape[1]
-    nz = Rt[:, :, 0].sum(axis=1) != 0
-    init = np.concatenate([np.nonzero(nz)[0], np.nonzero(~nz)[0]]).astype(np.uint32)
-    init_off = np.array([0, int(nz.sum()), len(init)] if (~nz).any() and nz.any() else [0, len(init)], np.uint32)
-    npix = int((it.slices() == s0).sum())
-    under = (-1.0 if "localUndersampling=-1" in cfg["props"]
-             else float(cfg["props"].split("localUndersampling=")[1].split(";")[0]))
+    # the refinement sample is the device's own job for slice s0 (its R rows,
+    # locality weights, pixel undersampling and initial clusters), so the
+    # oracle's clusters must equal the device's bit for bit (C4 scale: 100k
+    # columns, team mode with speculation and roaming helpers)
+    job = it.slice_job(s0)
+    nrow = job["R"].shape[1]
+    kv = dict(x.split("=", 1) for x in cfg["props"].split(";") if "=" in x)
+    under = float(kv.get("localUndersampling", -1.0))
+    dcorr = float(kv.get("depthCorrection", 1.0))
     t0 = time.perf_counter()
-    reps, w, refined = o.cluster_refine(Rt, np.arange(nrow, dtype=np.uint32), np.full(nrow, 1.0 / nrow),
-                                        init, init_off, float(np.float32(nrow) / np.float32(npix)), under,
-                                        seed=SEED_RNG, pass_=last_pass)
+    reps, w, refined = o.cluster_refine(job["R"], np.arange(nrow, dtype=np.uint32), job["locw"],
+                                        job["init_vrls"], job["init_off"], job["pixel_undersampling"], under,
+                                        depth_correction=dcorr, seed=SEED_RNG, pass_=last_pass, stage_refine=3 + 2 * s0,
+                                        stage_sample=4 + 2 * s0)
     t_ref = time.perf_counter() - t0
+    # the timed run is the reference-flags build (reassociating float maths);
+    # the bit-exact check runs the strict build of the same restatement
+    reps, w, refined = Oracle().cluster_refine(job["R"], np.arange(nrow, dtype=np.uint32), job["locw"],
+                                               job["init_vrls"], job["init_off"], job["pixel_undersampling"],
+                                               under, depth_correction=dcorr, seed=SEED_RNG, pass_=last_pass,
+                                               stage_refine=3 + 2 * s0, stage_sample=4 + 2 * s0)
+    cl = it.clusters()
+    dev_reps = cl["reps"][cl["slice_off"][s0]:cl["slice_off"][s0 + 1]]
+    dev_w = cl["weights"][cl["slice_off"][s0]:cl["slice_off"][s0 + 1]]
+    identical = bool(refined and np.array_equal(reps, dev_reps)
+                     and np.array_equal(w.view(np.uint32), dev_w.view(np.uint32)))
     r_rate = cnt / t_r
     render_rate = render_base["value"]
     t_step = pre_pairs_step / r_rate + int(np.ceil(ns / threads)) * t_ref + render_pairs_step / render_rate
@@ -355,7 +375,9 @@ def cpu_baseline_prepass(args, cfg, vrls, pc, it, render_base, pre_pairs_step, r
                        f"{render_base['sample']}; step extrapolated: {ns} slices over {threads} threads"),
             "seconds": t_r + t_ref + render_base["seconds"], "step_seconds_estimate": t_step,
             "cpu": render_base["cpu"], "flags": render_base["flags"],
-            "rates": {"rbuild": r_rate, "render": render_rate, "refine_s_per_slice": t_ref}}
+            "rates": {"rbuild": r_rate, "render": render_rate, "refine_s_per_slice": t_ref},
+            "refine_parity": {"slice": s0, "rows": nrow, "clusters_oracle": int(len(reps)),
+                              "clusters_device": int(len(dev_reps)), "identical": identical}}
 
 
 def torch_index(pix):

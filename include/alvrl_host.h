@@ -171,6 +171,16 @@ ALVRL_API int alvrl_integrator_clusters(alvrl_integrator *it, uint32_t *slice_of
 ALVRL_API int alvrl_integrator_R(alvrl_integrator *it, float *out, uint64_t cap_floats);
 ALVRL_API int alvrl_integrator_vrls(alvrl_integrator *it, float *soa, uint32_t cap, uint32_t *n,
                                     uint64_t *particles);
+/* The clustering job of slice s in the last prepass, as refineSlice hands it
+ * to a Clustering (Preprocessor.cpp:254-283; getLocalMatrix :779-827;
+ * initial clusters of cluster() :838-898): the local matrix [nvrl][nrows]
+ * (mean, var) pairs (R may be null), locality weights, the slice's pixel
+ * undersampling and the initial clusters (init_vrls: nvrl ids, init_off:
+ * ninit + 1 offsets).  Null output buffers are skipped; *nrows and *ninit
+ * are always set.  For checking the device refinement of one slice. */
+ALVRL_API int alvrl_integrator_slice_job(alvrl_integrator *it, uint32_t s, float *R, double *locw,
+                                         uint32_t cap_rows, uint32_t *nrows, float *pixel_under,
+                                         uint32_t *init_vrls, uint32_t *init_off, uint32_t *ninit);
 
 /* ---- on-disk formats -------------------------------
  * vrlClusterInfo stream (vrlIntegrator.cpp:29-101, the resource the

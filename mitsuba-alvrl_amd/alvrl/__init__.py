@@ -473,6 +473,7 @@ def _host():
     L.alvrl_integrator_clusters.argtypes = [vp, P(u32), P(u32), P(f32), u32, P(u32), P(f32), u32, P(u32)]
     L.alvrl_integrator_vrls.argtypes = [vp, vp, u32, P(u32), P(u64)]
     L.alvrl_integrator_R.argtypes = [vp, vp, u64]
+    L.alvrl_integrator_slice_job.argtypes = [vp, u32, vp, vp, u32, P(u32), P(f32), vp, vp, P(u32)]
     L.alvrl_integrator_prepass_dist.argtypes = [vp, u32, u32, u32, P(ExchangeDesc)]
     L.alvrl_exchange_allgatherv.argtypes = [P(ExchangeDesc), u32, vp, u64, vp, u64, P(u64)]
     L.alvrl_exchange_or.argtypes = [P(ExchangeDesc), u32, vp, u64]
@@ -726,6 +727,22 @@ class Integrator:
         out = np.zeros((nv, rows, 2), np.float32)
         _hcheck(self.L.alvrl_integrator_R(self.h, _ptr(out), out.size))
         return out
+
+    def slice_job(self, s: int, with_R: bool = True) -> dict:
+        """Slice s's clustering job of the last prepass (refineSlice's
+        inputs, Preprocessor.cpp:254-283): R [nvrl, nrows, 2], rows' locality
+        weights, pixel undersampling, initial clusters."""
+        nr = C.c_uint32(); ni = C.c_uint32(); pu = C.c_float()
+        _hcheck(self.L.alvrl_integrator_slice_job(self.h, s, None, None, 0, C.byref(nr), C.byref(pu), None, None,
+                                                  C.byref(ni)))
+        nv = int(self.stats()["vrls"])
+        R = np.zeros((nv, nr.value, 2), np.float32) if with_R else None
+        locw = np.zeros(max(1, nr.value), np.float64)
+        iv = np.zeros(max(1, nv), np.uint32); io = np.zeros(ni.value + 1, np.uint32)
+        _hcheck(self.L.alvrl_integrator_slice_job(self.h, s, _ptr(R) if with_R else None, _ptr(locw), nr.value,
+                                                  C.byref(nr), C.byref(pu), _ptr(iv), _ptr(io), C.byref(ni)))
+        return dict(R=R, locw=locw[:nr.value].copy(), pixel_undersampling=pu.value, init_vrls=iv[:nv].copy(),
+                    init_off=io)
 
     def clusters(self):
         ns = self.num_slices()

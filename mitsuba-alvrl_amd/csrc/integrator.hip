@@ -131,6 +131,11 @@ struct alvrl_integrator {
     DevBuf<uint32_t> rb_stride;
     DevBuf<uint8_t> nz_dev;
     uint32_t rows_built = 0;                // rows of R held (all of them at world 1)
+    // the last prepass's clustering inputs (alvrl_integrator_slice_job):
+    // initial clusters, and per local slice its rows and locality weights
+    std::vector<uint32_t> job_init, job_init_off, job_slices;
+    std::vector<std::vector<uint32_t>> job_rows;
+    std::vector<std::vector<double>> job_locw;
     // cluster info (vrlClusterInfo)
     std::vector<uint32_t> slice_off, reps, fb_reps;
     std::vector<float> weights, fb_w;
@@ -501,6 +506,7 @@ struct alvrl_integrator {
             j.stage_refine = stage_slice_refine(s);
             j.stage_sample = stage_slice_sample(s);
         }
+        job_init = init; job_init_off = init_off; job_slices = mine; job_rows = lrows; job_locw = lw;
         std::vector<uint32_t> off(nm + 1), rep((size_t)nm * nv + 1);
         std::vector<float> w((size_t)nm * nv + 1);
         std::vector<int> refined(nm + 1);
@@ -857,6 +863,43 @@ ALVRL_API int alvrl_integrator_R(alvrl_integrator* it, float* out, uint64_t cap)
             if (!n) continue;
             hchk(hipMemcpy2D(out + 2 * ro[s], rows * 8, it->Rt.p + 2 * nv * ro[s], n * 8, n * 8, nv,
                              hipMemcpyDeviceToHost), "copy R");
+        }
+    });
+    return ALVRL_OK;
+}
+
+ALVRL_API int alvrl_integrator_slice_job(alvrl_integrator* it, uint32_t s, float* R, double* locw, uint32_t cap_rows,
+                                         uint32_t* nrows, float* pixel_under, uint32_t* init_vrls,
+                                         uint32_t* init_off, uint32_t* ninit)
+{
+    if (!it || !nrows || !ninit) return ierr(ALVRL_ERR_INVALID, "alvrl_integrator_slice_job: null argument");
+    const auto k = std::find(it->job_slices.begin(), it->job_slices.end(), s) - it->job_slices.begin();
+    if (k == (long)it->job_slices.size())
+        return ierr(ALVRL_ERR_STATE, "alvrl_integrator_slice_job: slice not refined on this rank in the last prepass");
+    const auto& rows = it->job_rows[k];
+    const uint32_t n = (uint32_t)rows.size();
+    *nrows = n;
+    *ninit = (uint32_t)it->job_init_off.size() - 1;
+    if (pixel_under) *pixel_under = it->prep->slice_undersampling()[s];
+    if (init_vrls) std::copy(it->job_init.begin(), it->job_init.end(), init_vrls);
+    if (init_off) std::copy(it->job_init_off.begin(), it->job_init_off.end(), init_off);
+    if (locw) std::copy(it->job_locw[k].begin(), it->job_locw[k].end(), locw);
+    if (!R) return ALVRL_OK;
+    if (cap_rows < n) return ierr(ALVRL_ERR_INVALID, "alvrl_integrator_slice_job: buffer too small");
+    GUARD({
+        hchk(hipSetDevice(it->device), "hipSetDevice");
+        hchk(hipStreamSynchronize(it->stream), "sync");
+        const uint64_t nv = it->vrls.n;
+        // rows that are one contiguous run of a slice block: one 2-D copy
+        uint32_t r = 0;
+        while (r < n) {
+            const uint32_t g = rows[r];
+            const uint64_t b = it->row_base[g], st = it->row_stride[g];
+            uint32_t q = r + 1;
+            while (q < n && it->row_stride[rows[q]] == st && it->row_base[rows[q]] == b + (q - r)) q++;
+            hchk(hipMemcpy2D(R + 2 * (uint64_t)r, (uint64_t)n * 8, it->Rt.p + 2 * b, st * 8, (uint64_t)(q - r) * 8,
+                             nv, hipMemcpyDeviceToHost), "copy slice R");
+            r = q;
         }
     });
     return ALVRL_OK;

@@ -136,7 +136,8 @@ struct Common {
     uint32_t spec_min;             // smallest cluster worth a speculative split
     uint32_t side_k;
     int enq_start;                 // also queue candidates right after the pop (before the split)               // a waiting leader takes a side task of <= awaited columns * side_k / 16
-    unsigned long long spin_ticks; // bound of every team wait (100 MHz ticks)
+    unsigned long long spin_ticks; // bound of an idle helper's wait for a task (100 MHz ticks)
+    unsigned long long wait_ticks; // bound of a leader's wait for a running helper (100 MHz ticks)
     unsigned long long* tstat;     // team counters (ALVRL_REFINE_TEAM_STATS=1), or null
     unsigned long long* jtime;     // with tstat: per job, wall ticks at start / end of refine / end
     unsigned long long* trace;     // host-mapped per-block (phase << 32 | value), ALVRL_REFINE_TRACE=1
@@ -217,6 +218,7 @@ struct Ctl {
     float diffLen, nd;
     int go, do_snap, stop, refined;
     int tmode, side;
+    int team_off;          // the job's team was retired after a timed-out wait (split_team)
     uint32_t yb, ye, j;
     unsigned long long t0;
     float avg;
@@ -1965,9 +1967,11 @@ __device__ __forceinline__ bool cas_rlx(T* p, T expect, T v)
 }
 __device__ __forceinline__ void drain_vmem() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 // constant 100 MHz clock.  No wait is unbounded: a leader that has waited
-// kSpinTicks (~60 s) for a helper splits the cluster itself (the helper's late
-// result lands in side buffers nobody commits), an idle helper gives up after
-// the same time without a task.
+// Common::wait_ticks (default kSpinTicks, ~60 s) for a helper retires its
+// job's team (split_team: stop flag, and every later split of the job is the
+// leader's own, so nothing the late helper writes to team.spec / team.res /
+// team.state is read again), an idle helper gives up after spin_ticks
+// without a task.
 __device__ __forceinline__ unsigned long long wall() { return __builtin_amdgcn_s_memrealtime(); }
 constexpr unsigned long long kSpinTicks = 6000000000ull;   // default of Common::spin_ticks
 
@@ -2107,7 +2111,7 @@ __device__ void split_team(const JobDev& J, const Common& cm, Ctl& C, uint32_t b
                            unsigned long long* lds, Prof& pf, bool spec)
 {
     const Team& T = J.team;
-    if (!T.helpers || !spec) { split(J, cm, C, b, e, lds, pf); return; }
+    if (!T.helpers || !spec || C.team_off) { split(J, cm, C, b, e, lds, pf); return; }
     const int tid = threadIdx.x;
     if (tid < 64 && cm.enq_start) enqueue_candidates(J, cm, C);
     if (tid == 0) {
@@ -2140,12 +2144,16 @@ __device__ void split_team(const JobDev& J, const Common& cm, Ctl& C, uint32_t b
         if (tid == 0) {
             const unsigned long long sv = ld_rlx(&T.state[b]);
             C.side = 0;
-            if ((sv & 7) == kStDone) {
+            if ((sv & 7) == kStDone && (uint32_t)(sv >> 3) == e) {
                 fence_acq();
                 C.tmode = 1;
                 tcount(cm, TS_COMMIT);
-            } else if (wall() - C.t0 > cm.spin_ticks) {
-                C.tmode = 0;   // give up on the helper: split here
+            } else if (wall() - C.t0 > cm.wait_ticks) {
+                // give up on the helper: it still owns team.spec[b, e),
+                // team.res[b] and state[b], so the team is retired and the
+                // leader splits this and every later cluster of the job itself
+                C.tmode = 0;
+                C.team_off = 1;
                 tcount(cm, TS_WAIT_TMO);
             } else {
                 uint32_t yb = 0, ye = 0;
@@ -2161,6 +2169,11 @@ __device__ void split_team(const JobDev& J, const Common& cm, Ctl& C, uint32_t b
         pf.mark(PF_T_SIDE);
     }
     const int mode = C.tmode;
+    if (C.team_off) {   // set by thread 0 before the loop's last barrier
+        stop_team(J, cm);
+        split(J, cm, C, b, e, lds, pf);
+        return;
+    }
     if (mode == 0) {
         split(J, cm, C, b, e, lds, pf);
     } else if (mode == 1) {
@@ -2489,7 +2502,6 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
     trace(cm, 1, 0);
     if (cm.jtime && threadIdx.x == 0) cm.jtime[3 * blockIdx.x] = wall();
     const int tid = threadIdx.x, wave = tid >> 6;
-    const uint32_t lane = (uint32_t)(tid & 63);
     const uint32_t N = cm.nvrl, R = J.nrows;
     const uint32_t nv = cm.init_off[cm.ninit];
     Prof pf{cm.prof, (long long)clock64()};
@@ -2497,7 +2509,7 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
     if (tid == 0) {
         C.tracingVar = C.unclIntVar = C.clUnderVar = C.clIntVar = 0.0f;
         C.heap_n = C.singles_n = C.sh_heap_n = C.sh_singles_n = 0;
-        C.err = 0; C.refined = 1;
+        C.err = 0; C.refined = 1; C.team_off = 0;
         C.hlog_n = 0; C.hlog_full = 1;
     }
     __syncthreads();
@@ -2946,6 +2958,10 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
     {
         const char* sp = std::getenv("ALVRL_REFINE_SPIN_MS");
         cm.spin_ticks = sp ? (unsigned long long)std::max(1, std::atoi(sp)) * 100000ull : kSpinTicks;
+        // ALVRL_LEADER_WAIT_TICKS (test knob, may be 0): bound of a leader's
+        // wait for a running helper; by default the same as an idle helper's
+        const char* wt = std::getenv("ALVRL_LEADER_WAIT_TICKS");
+        cm.wait_ticks = wt ? std::strtoull(wt, nullptr, 10) : cm.spin_ticks;
     }
     cm.tstat = nullptr;
     cm.trace = nullptr;

@@ -226,7 +226,16 @@ typedef struct {
     /* scratch */
     double *sum, *Mv, *sumVars, *scr;
     float *fa, *fb, *fc, *fd;
+    uint16_t *gen;         /* diagnostic: split-tree depth of the cluster starting at [begin] */
+    uint16_t cur_gen;
 } clustering_t;
+
+/* Diagnostic pop trace (test infrastructure): when set, every cluster the
+ * refinement pops is recorded as (begin, end, depth in the split tree). */
+static uint32_t *g_pop_trace;
+static uint32_t g_pop_cap, g_pop_n;
+void alvrl_o_set_pop_trace(uint32_t *buf, uint32_t cap) { g_pop_trace = buf; g_pop_cap = cap; g_pop_n = 0; }
+uint32_t alvrl_o_pop_trace_n(void) { return g_pop_n; }
 
 /* weightedSample, Preprocessor.cpp:1534-1580.  The running float sums of the
  * reference (weightSum += w, accum += w, in index order) are taken in one
@@ -419,6 +428,7 @@ static int cluster_variance(clustering_t *C, const uint32_t *first, long step, u
 static void add_cluster(clustering_t *C, uint32_t begin, uint32_t end, float uvar, float ivar)
 {
     if (end == begin) { C->err = 1; return; }
+    if (C->gen) C->gen[begin] = (uint16_t)(C->cur_gen + 1);
     if (end == begin + 1) {
         ulist_push_front(&C->singles, C->vrls[begin]);
         if (uvar != 0) C->err = 1;
@@ -434,6 +444,11 @@ static void add_cluster(clustering_t *C, uint32_t begin, uint32_t end, float uva
 static cnode pop_multi(clustering_t *C)
 {
     cnode cn = cheap_pop(&C->pq);
+    C->cur_gen = C->gen ? C->gen[cn.begin] : 0;
+    if (g_pop_trace && g_pop_n < g_pop_cap) {
+        g_pop_trace[3 * g_pop_n] = cn.begin; g_pop_trace[3 * g_pop_n + 1] = cn.end;
+        g_pop_trace[3 * g_pop_n + 2] = C->cur_gen; g_pop_n++;
+    }
     C->clUnderVar -= cn.uvar;
     C->clIntVar -= cn.ivar;
     return cn;
@@ -583,6 +598,8 @@ static int clustering_init(clustering_t *C, const mat_t *M, const double *locw,
     C->nv = init_off[ninit];
     C->vrls = (uint32_t *)malloc(sizeof(uint32_t) * (C->nv ? C->nv : 1));
     memcpy(C->vrls, init_vrls, sizeof(uint32_t) * C->nv);
+    if (g_pop_trace) C->gen = (uint16_t *)calloc(C->nv ? C->nv : 1, sizeof(uint16_t));
+    C->cur_gen = (uint16_t)-1;
     for (uint32_t i = 0; i < ninit; i++) {
         uint32_t b = init_off[i], e = init_off[i + 1];
         float u = 0, iv = 0;
@@ -597,7 +614,7 @@ static int clustering_init(clustering_t *C, const mat_t *M, const double *locw,
 
 static void clustering_free(clustering_t *C)
 {
-    free(C->sum); free(C->fa); free(C->colw); free(C->vrls);
+    free(C->sum); free(C->fa); free(C->colw); free(C->vrls); free(C->gen);
     free(C->pq.v); free(C->singles.v); free(C->sh_pq.v); free(C->sh_singles.v);
 }
 

@@ -308,6 +308,13 @@ def test_false_color_modes(gpu_ok):
     assert np.array_equal(a, b)
 
 
+# every environment knob of the refine kernel's team mode (refine.hip host
+# side): saved, cleared and restored by the team tests so no value leaks in
+TEAM_ENV_KEYS = ("ALVRL_REFINE_TEAM", "ALVRL_REFINE_ROAM", "ALVRL_SPEC_WIDTH", "ALVRL_SPEC_MIN",
+                 "ALVRL_REFINE_SPIN_MS", "ALVRL_ENQ_START", "ALVRL_LEADER_SIDE",
+                 "ALVRL_LEADER_WAIT_TICKS", "ALVRL_REFINE_TEAM_STATS", "ALVRL_ROAM_ORDER")
+
+
 def test_team_mode_settings(gpu_ok):
     """Speculative split teams (refine.hip team mode) under every knob: team
     size, roaming helpers, speculation width and threshold, and a 1 ms bound
@@ -320,8 +327,7 @@ def test_team_mode_settings(gpu_ok):
     w, h = 256, 192
     scene = alvrl.scene_default(w, h)
     vrls, pc = alvrl.trace_vrls(scene, 3000, seed=SEED_VRL)
-    keys = ("ALVRL_REFINE_TEAM", "ALVRL_REFINE_ROAM", "ALVRL_SPEC_WIDTH", "ALVRL_SPEC_MIN",
-            "ALVRL_REFINE_SPIN_MS")
+    keys = TEAM_ENV_KEYS
     saved = {k: os.environ.get(k) for k in keys}
 
     def run(props, **env):
@@ -339,7 +345,9 @@ def test_team_mode_settings(gpu_ok):
     settings = [dict(ALVRL_REFINE_TEAM=2), dict(ALVRL_REFINE_TEAM=4, ALVRL_REFINE_ROAM=0),
                 dict(ALVRL_REFINE_TEAM=8), dict(ALVRL_SPEC_WIDTH=1, ALVRL_SPEC_MIN=2),
                 dict(ALVRL_SPEC_WIDTH=32, ALVRL_SPEC_MIN=2), dict(ALVRL_REFINE_SPIN_MS=1),
-                dict(ALVRL_REFINE_TEAM=3, ALVRL_REFINE_SPIN_MS=1, ALVRL_SPEC_MIN=2), {}]
+                dict(ALVRL_REFINE_TEAM=3, ALVRL_REFINE_SPIN_MS=1, ALVRL_SPEC_MIN=2),
+                dict(ALVRL_ENQ_START=1), dict(ALVRL_LEADER_SIDE=0, ALVRL_REFINE_SPIN_MS=1),
+                dict(ALVRL_LEADER_WAIT_TICKS=0), {}]
     try:
         for props in ("targetNumSlices=40", "targetNumSlices=30;localUndersampling=10",
                       "targetNumSlices=25;depthCorrection=0.8"):
@@ -355,6 +363,94 @@ def test_team_mode_settings(gpu_ok):
                 os.environ.pop(k, None)
             else:
                 os.environ[k] = v
+
+
+def test_team_wait_timeout(gpu_ok, capfd):
+    """A leader that gives up waiting on a running helper (refine.hip
+    split_team, wait bound 0 ticks here) retires its job's team and splits
+    that cluster and every later one itself; the helper's late result in
+    team.spec / team.res / state is never committed.  Large clusters (few
+    slices, 20k VRLs) keep helpers mid-split when their leader pops the
+    cluster.  The cluster lists equal one workgroup per slice bit for bit,
+    and the team counters show that timeouts happened."""
+    import os
+    import re
+    import alvrl
+    w, h = 256, 192
+    scene = alvrl.scene_default(w, h)
+    vrls, pc = alvrl.trace_vrls(scene, 20000, seed=SEED_VRL)
+    saved = {k: os.environ.get(k) for k in TEAM_ENV_KEYS}
+
+    def run(props, **env):
+        for k in TEAM_ENV_KEYS:
+            os.environ.pop(k, None)
+        os.environ.update({k: str(v) for k, v in env.items()})
+        it = alvrl.Integrator(props + f";seed={SEED_RNG}", device=0)
+        it.set_vrls(vrls, pc)
+        it.preprocess(scene)
+        it.prepass(1)
+        cl = it.clusters()
+        it.close()
+        return cl
+
+    timeouts = 0
+    try:
+        for props in ("targetNumSlices=6", "targetNumSlices=4;localUndersampling=4"):
+            ref = run(props, ALVRL_REFINE_TEAM=1)
+            capfd.readouterr()
+            for st in (dict(ALVRL_LEADER_WAIT_TICKS=0), dict(ALVRL_LEADER_WAIT_TICKS=0, ALVRL_REFINE_TEAM=8),
+                       dict(ALVRL_LEADER_WAIT_TICKS=2000, ALVRL_REFINE_ROAM=0)):
+                cl = run(props, ALVRL_REFINE_TEAM_STATS=1, **st)
+                err = capfd.readouterr().err
+                m = re.search(r"wait-timeout (\d+)", err)
+                assert m, err
+                timeouts += int(m.group(1))
+                for k in ref:
+                    assert np.array_equal(ref[k].view(np.uint32), cl[k].view(np.uint32)), (props, st, k)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    assert timeouts > 0
+
+
+@pytest.mark.parametrize("props", ["targetNumSlices=100;localUndersampling=-1",
+                                   "targetNumSlices=100;localUndersampling=100"])
+def test_refine_c4_scale(oracle, gpu_ok, props):
+    """Refinement at the benchmark's own scale (C4 / C3: 1024^2, 100k VRLs,
+    100 slices, team mode with speculation and roaming helpers as by
+    default): the oracle's Clustering (Preprocessor.cpp:254-283, strict
+    build) on the device's job for three slices -- the most rows, the most
+    clusters and a median one -- gives the device's cluster lists bit for
+    bit (representatives and weights)."""
+    import alvrl
+    W = H = 1024
+    scene = alvrl.scene_default(W, H)
+    vrls, pc = alvrl.trace_vrls(scene, 100000, seed=SEED_VRL)
+    it = alvrl.Integrator(props + f";seed={SEED_RNG}", device=0)
+    it.set_vrls(vrls, pc)
+    it.preprocess(scene)
+    it.prepass(2)
+    cl = it.clusters()
+    off, _ = it.reps()
+    nrows, ncl = np.diff(off), np.diff(cl["slice_off"])
+    kv = dict(x.split("=", 1) for x in props.split(";"))
+    under = float(kv["localUndersampling"])
+    picks = sorted({int(np.argmax(nrows)), int(np.argmax(ncl)), int(np.argsort(ncl)[len(ncl) // 2])})
+    for s in picks:
+        job = it.slice_job(s)
+        n = job["R"].shape[1]
+        reps, w, refined = oracle.cluster_refine(job["R"], np.arange(n, dtype=np.uint32), job["locw"],
+                                                 job["init_vrls"], job["init_off"], job["pixel_undersampling"],
+                                                 under, seed=SEED_RNG, pass_=2, stage_refine=3 + 2 * s,
+                                                 stage_sample=4 + 2 * s)
+        assert refined
+        b, e = cl["slice_off"][s], cl["slice_off"][s + 1]
+        assert np.array_equal(reps, cl["reps"][b:e]), (s, n, len(reps), e - b)
+        assert np.array_equal(w.view(np.uint32), cl["weights"][b:e].view(np.uint32)), s
+    it.close()
 
 
 def test_cluster_info_checkpoint(gpu_ok, tmp_path):
