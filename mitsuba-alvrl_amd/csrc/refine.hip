@@ -170,10 +170,13 @@ static const char* kPfNames[PF_N] = {"column weights", "initial clusters", "uncl
                                      "split: centres", "split: direction", "split: projections",
                                      "split: sort", "split: variance fwd", "split: variance rev",
                                      "split: argmin+add", "heap/snapshot/ctrl", "representatives",
-                                     " var: coefficients", " var: recurrence", " var: column sums",
-                                     " proj: staging", " proj: compute",
-                                     "  rec: row wave 0 busy", "  rec: coef wave busy",
-                                     "   row wave: prefetch issue", "   row wave: wait for data",
+                                     // the split engine's coefficient waves (m >= 4096; the
+                                     // > 256-row engine adds its own phases to the first three)
+                                     " coef wave <=192 rows: chain", " coef wave <=192 rows: (block 3)",
+                                     " coef wave <=192 rows: reduce", " coef wave <=192 rows: flush",
+                                     " proj: compute",
+                                     " coef wave 193-256 rows: chain", " coef wave 193-256 rows: block 3",
+                                     " coef wave 193-256 rows: (reduce)", " coef wave 193-256 rows: (flush)",
                                      "ctrl: heap pop/snapshot", "ctrl: enqueue", "ctrl: wait for helper",
                                      "ctrl: side splits", "ctrl: commit",
                                      "#splits", "#split columns"};
@@ -194,7 +197,7 @@ struct Prof {
 // (count, split cycles, variance cycles, cycles before the projections)
 constexpr int kPfBuckets = 18;
 constexpr int kPfWaveBusy = PF_N + 4 * kPfBuckets;   // per-wave busy cycles in the variance passes (+ 8 wall)
-constexpr int kPfTotal = kPfWaveBusy + 3 * kWaves;
+constexpr int kPfTotal = kPfWaveBusy + 6 * kWaves;   // [NB < 4 | NB == 4][busy, wall, reduce][wave]
 __device__ __forceinline__ int pf_bucket(uint32_t m) { return min(kPfBuckets - 1, 31 - (int)__builtin_clz(max(m, 1u))); }
 
 // Per-column coefficients of the variance recurrence, read as broadcasts.
@@ -900,27 +903,29 @@ __device__ __noinline__ void variance_passes_t(const JobDev& J, const Common& cm
     auto reduce = [&](uint32_t kf, uint32_t nk) {
         const long long ws0 = wprof ? (long long)clock64() : 0;
         if (active) {
+            // per 64-row block the halving tree (rows past R as +0.0), the
+            // block totals added in block order (oracle wsum_blk)
             double pz[4 * NQ];                       // [pu of 2*NQ columns, pi of 2*NQ columns]
+            for (uint32_t b = 0; b < NB; b++) {
+                double tz[4 * NQ];
 #pragma unroll
-            for (int j = 0; j < 2; j++) {
+                for (int j = 0; j < 2; j++) {
 #pragma unroll
-                for (int q = 0; q < NQ; q++) {
-                    const uint32_t c = (uint32_t)w + 4u * q;
-                    double pu = 0.0, pi = 0.0;
-                    if ((uint32_t)j < nk && c < cn_of(kf + j)) {
-                        const double2* Tk = T + (size_t)((kf + j) & 1) * tsz;
-                        for (uint32_t b = 0; b < NB; b++) {
-                            if (b * 64 + lane < R) {
-                                const double2 t = Tk[((size_t)c * NB + b) * 64 + lane];
-                                pu = pu + t.x; pi = pi + t.y;
-                            }
+                    for (int q = 0; q < NQ; q++) {
+                        const uint32_t c = (uint32_t)w + 4u * q;
+                        double pu = 0.0, pi = 0.0;
+                        if ((uint32_t)j < nk && c < cn_of(kf + j) && b * 64 + lane < R) {
+                            const double2 t = (T + (size_t)((kf + j) & 1) * tsz)[((size_t)c * NB + b) * 64 + lane];
+                            pu = t.x; pi = t.y;
                         }
+                        tz[j * NQ + q] = pu;
+                        tz[2 * NQ + j * NQ + q] = pi;
                     }
-                    pz[j * NQ + q] = pu;
-                    pz[2 * NQ + j * NQ + q] = pi;
                 }
+                tree_dn<4 * NQ>(tz);
+#pragma unroll
+                for (int i = 0; i < 4 * NQ; i++) pz[i] = b == 0 ? tz[i] : pz[i] + tz[i];
             }
-            tree_dn<4 * NQ>(pz);
             if (lane == 0) {
 #pragma unroll
                 for (int j = 0; j < 2; j++) {
@@ -1076,13 +1081,31 @@ __device__ __forceinline__ double tree16_transposed(const double* v, uint32_t la
 __device__ __forceinline__ void coef_chain8(double& W, double w, uint32_t j, uint32_t ncol, double& Wo, double& Wn)
 {
     const uint32_t lane = threadIdx.x & 63;
+    const uint32_t c0 = 8 * j;
+    if (c0 >= ncol) return;                            // wave-uniform
+    // the 8 weights to SGPRs first (independent of W), then the dependent
+    // chain of adds; the column's lane keeps W before / after by selects
+    double wc[kCH];
 #pragma unroll
-    for (uint32_t c = 0; c < (uint32_t)kCH; c++) {
-        if (8 * j + c < ncol) {
-            const double wc = readlane_d(w, 8 * j + c);
-            if (lane == 8 * j + c) Wo = W;
-            W = W + wc;
-            if (lane == 8 * j + c) Wn = W;
+    for (int c = 0; c < kCH; c++) wc[c] = readlane_d(w, c0 + (uint32_t)c);
+    if (ncol - c0 >= (uint32_t)kCH) {
+#pragma unroll
+        for (int c = 0; c < kCH; c++) {
+            const bool me = lane == c0 + (uint32_t)c;
+            Wo = me ? W : Wo;
+            W = W + wc[c];
+            Wn = me ? W : Wn;
+        }
+    } else {
+        const uint32_t n = ncol - c0;
+#pragma unroll
+        for (int c = 0; c < kCH; c++) {
+            if ((uint32_t)c < n) {
+                const bool me = lane == c0 + (uint32_t)c;
+                Wo = me ? W : Wo;
+                W = W + wc[c];
+                Wn = me ? W : Wn;
+            }
         }
     }
 }
@@ -1122,8 +1145,9 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
     float* fu = g == 0 ? fu0 : fu1;
     float* fi = g == 0 ? fi0 : fi1;
     VarGroup& V = C.vg[g];
-    constexpr size_t tsz = (size_t)kCH * 4 * 64;       // one chunk's terms
-    double2* T = reinterpret_cast<double2*>(pool) + (size_t)g * 2 * tsz;
+    // per chunk and row block the 16 block totals (pu, pi of 8 columns) of
+    // the rows' prefix terms, [k & 1][block][2c + h]
+    double* Q = reinterpret_cast<double*>(pool) + (size_t)g * 2 * 4 * 16;
     CoefBlock* ring = reinterpret_cast<CoefBlock*>(pool + kSplitTBytes) + g * 2;
     // prefix results of the last two 64-column blocks, stored out once per
     // block: a global store in every chunk would make the next chunk's LDS
@@ -1185,41 +1209,23 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
     const RowRef rr0 = roww ? row_ref(J, r0) : RowRef{0, 0};
     const double lw0 = roww ? J.locw[r0] : 0.0;
 
-    // coefficient wave: the 16 row sums of chunk kk, written out by their lanes
+    // coefficient wave: the 16 row sums of chunk kk, the row blocks' tree
+    // totals added in block order (wsum_blk), one sum per lane 0-15
     auto reduce = [&](uint32_t kk) {
         const uint32_t cn = cn_of(kk);
-        const double2* Tk = T + (size_t)(kk & 1) * tsz;
-        double v[2 * kCH];
+        const double* Qk = Q + (size_t)(kk & 1) * 4 * 16;
+        const uint32_t sl = lane & 15, c = sl >> 1, h = sl & 1;
+        double acc = Qk[sl];
 #pragma unroll
-        for (int h2 = 0; h2 < 4; h2++) {            // 8 LDS reads in flight at a time (lgkmcnt holds 15)
-            double2 t[2][4];
-#pragma unroll
-            for (int c = 0; c < 2; c++)
-#pragma unroll
-                for (int b = 0; b < 4; b++) t[c][b] = Tk[((size_t)(2 * h2 + c) * 4 + b) * 64 + lane];
-#pragma unroll
-            for (int c = 0; c < 2; c++) {
-                double pu = 0.0, pi = 0.0;
-                if ((uint32_t)(2 * h2 + c) < cn) {
-#pragma unroll
-                    for (int b = 0; b < 4; b++) {
-                        if ((uint32_t)b < NB && (uint32_t)b * 64 + lane < R) { pu = pu + t[c][b].x; pi = pi + t[c][b].y; }
-                    }
-                }
-                v[2 * (2 * h2 + c)] = pu; v[2 * (2 * h2 + c) + 1] = pi;
-            }
-        }
-        const double z = tree16_transposed(v, lane);
-        if ((lane & 3) == 0) {
-            const uint32_t h = lane >> 5, c = 4 * ((lane >> 2) & 1) + 2 * ((lane >> 3) & 1) + ((lane >> 4) & 1);
-            if (c < cn) {
-                const uint32_t n = kk * kCH + c;
-                const float f = h == 0 ? (n == 0 ? 0.0f : (float)z) : (float)z;
-                stg[(((kk / 8) & 1) * 2 + h) * kCB64 + (kk % 8) * kCH + c] = f;
-                if (n == m - 1) {
-                    if (h == 0) V.res_u = f; else V.res_i = f;
-                    if (!isfinite(f) || f < 0) C.err = 1;
-                }
+        for (uint32_t b = 1; b < 4; b++)
+            if (b < NB) acc = acc + Qk[b * 16 + sl];
+        if (lane < 16 && c < cn) {
+            const uint32_t n = kk * kCH + c;
+            const float f = h == 0 ? (n == 0 ? 0.0f : (float)acc) : (float)acc;
+            stg[(((kk / 8) & 1) * 2 + h) * kCB64 + (kk % 8) * kCH + c] = f;
+            if (n == m - 1) {
+                if (h == 0) V.res_u = f; else V.res_i = f;
+                if (!isfinite(f) || f < 0) C.err = 1;
             }
         }
     };
@@ -1232,11 +1238,12 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
         }
     };
     // the recurrence of chunk k for one 64-row block (lane = row), terms into T[k & 1]
-    auto rec = [&](uint32_t k, const float2* cur, uint32_t blk, double lw, double& sum0, double& M0, double& V0) {
+    auto rec = [&](uint32_t k, const float2* cur, uint32_t blk, double lw, double& sum0, double& M0, double& V0,
+                   bool valid) {
         const uint32_t c0 = k * kCH, cn = cn_of(k);
         const CoefBlock& q = ring[(k / 8) & 1];
         const uint32_t o = (k % 8) * kCH;
-        double2* Tk = T + (size_t)(k & 1) * tsz + (size_t)blk * 64 + lane;
+        double tv[2 * kCH];                            // this row's prefix terms (pu, pi) per column
         if (cn == (uint32_t)kCH && k > 0) {            // full chunk, no first column: no guards
             double2 w2[4], o2[4], a2[4], bb2[4], rw2[4], n2[4], rn2[4];
 #pragma unroll
@@ -1257,7 +1264,7 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
                     M0 = a2[p].x * M0 + bb2[p].x * (tmp * tmp);
                     V0 = V0 + (double)cur[2 * p].y * rw2[p].x;
                     sum0 = sum0 + x;
-                    if (FU) Tk[(size_t)(2 * p) * 4 * 64] = make_double2(lw * (M0 * rn2[p].x), lw * (V0 * n2[p].x));
+                    if (FU) { tv[4 * p] = lw * (M0 * rn2[p].x); tv[4 * p + 1] = lw * (V0 * n2[p].x); }
                 }
                 {
                     const double x = (double)cur[2 * p + 1].x;
@@ -1265,7 +1272,7 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
                     M0 = a2[p].y * M0 + bb2[p].y * (tmp * tmp);
                     V0 = V0 + (double)cur[2 * p + 1].y * rw2[p].y;
                     sum0 = sum0 + x;
-                    if (FU) Tk[(size_t)(2 * p + 1) * 4 * 64] = make_double2(lw * (M0 * rn2[p].y), lw * (V0 * n2[p].y));
+                    if (FU) { tv[4 * p + 2] = lw * (M0 * rn2[p].y); tv[4 * p + 3] = lw * (V0 * n2[p].y); }
                 }
             }
         } else {
@@ -1277,8 +1284,20 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
                     if (c0 + c > 0) M0 = q.a[o + c] * M0 + q.bb[o + c] * (tmp * tmp);
                     V0 = V0 + (double)cur[c].y * q.rw[o + c];
                     sum0 = sum0 + x;
-                    if (FU) Tk[(size_t)c * 4 * 64] = make_double2(lw * (M0 * q.rWn[o + c]), lw * (V0 * q.Wn[o + c]));
+                    if (FU) { tv[2 * c] = lw * (M0 * q.rWn[o + c]); tv[2 * c + 1] = lw * (V0 * q.Wn[o + c]); }
+                } else if (FU) {
+                    tv[2 * c] = 0.0; tv[2 * c + 1] = 0.0;
                 }
+            }
+        }
+        if (FU) {
+            // the block's halving tree (rows past R enter as +0.0), totals to Q[k & 1][blk]
+#pragma unroll
+            for (int i = 0; i < 2 * kCH; i++) tv[i] = valid ? tv[i] : 0.0;
+            const double z = tree16_transposed(tv, lane);
+            if ((lane & 3) == 0) {
+                const uint32_t h = lane >> 5, c = 4 * ((lane >> 2) & 1) + 2 * ((lane >> 3) & 1) + ((lane >> 4) & 1);
+                Q[((size_t)(k & 1) * 4 + blk) * 16 + 2 * c + h] = z;
             }
         }
     };
@@ -1311,22 +1330,30 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
         double sum3 = 0.0, M3 = 0.0, V3 = 0.0;
         float2 cA[kCH], cB[kCH];
         if (own3) load_rows(Rt3, rs3, 0, cA);
+        long long sp[4] = {0, 0, 0, 0};                // sub-phases (profile): reduce, flush, chain, rec 3
         auto stepc = [&](uint32_t B, uint32_t j, uint32_t nb, float2* cur, float2* nxt) {
             const uint32_t k = B * 8 + j;
             const long long ws0 = wprof ? (long long)clock64() : 0;
 #ifndef ALVRL_EXP_NORED
-            if (FU && k >= 1) reduce(k - 1);
+            if (FU && !own3 && k >= 1) reduce(k - 1);
 #endif
-            if (FU && j == 0 && B >= 1) flush(B - 1);
+            const long long ws1 = wprof ? (long long)clock64() : 0;
+            if (FU && !own3 && j == 0 && B >= 1) flush(B - 1);
+            const long long ws2 = wprof ? (long long)clock64() : 0;
             if (nb < nblk) {
                 coef_chain8(W, cw_w, j, ncol_of(nb), cWo, cWn);
                 if (j == 7 || k == nch - 1) coef_block_finish(C, cw_w, cWo, cWn, cw_v, ncol_of(nb), &ring[nb & 1]);
             }
+            const long long ws3 = wprof ? (long long)clock64() : 0;
             if (own3) {
                 load_rows(Rt3, rs3, min(k + 1, nch - 1), nxt);
-                rec(k, cur, 3, lw3, sum3, M3, V3);
+                rec(k, cur, 3, lw3, sum3, M3, V3, 3u * 64u + lane < R);
             }
-            if (wprof) wred += (long long)clock64() - ws0;
+            if (wprof) {
+                const long long ws4 = (long long)clock64();
+                wred += ws4 - ws0;
+                sp[0] += ws1 - ws0; sp[1] += ws2 - ws1; sp[2] += ws3 - ws2; sp[3] += ws4 - ws3;
+            }
             __syncthreads();
         };
         for (uint32_t B = 0; B * 8 < nch; B++) {
@@ -1341,9 +1368,18 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
                 stepc(B, j + 1, nb, cB, cA);
             }
         }
+        if (wprof && lane == 0 && m >= 4096) {
+            const bool n4 = NB == 4;
+            atomicAdd(&cm.prof[n4 ? PF_V_ISSUE : PF_V_RED], (unsigned long long)sp[0]);
+            atomicAdd(&cm.prof[n4 ? PF_V_DATA : PF_P_STAGE], (unsigned long long)sp[1]);
+            atomicAdd(&cm.prof[n4 ? PF_V_OWN : PF_V_COEF], (unsigned long long)sp[2]);
+            atomicAdd(&cm.prof[n4 ? PF_V_CW : PF_V_REC], (unsigned long long)sp[3]);
+        }
         if (FU) {
-            reduce(nch - 1);
-            flush((nch - 1) / 8);
+            if (!own3) {
+                reduce(nch - 1);
+                flush((nch - 1) / 8);
+            }
         } else {
             if (lane == 0) V.Wcur = W;
             if (own3 && 3u * 64u + lane < R) {
@@ -1365,10 +1401,17 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
         // chunk k: issue the entries of chunk k+2 (clamped: the last chunk is
         // re-read, so the wait for chunk k is always "all but the 16 youngest"),
         // run the recurrence of chunk k into T[k & 1]
+        // with 4 row blocks the coefficient wave also runs block 3, and the
+        // row wave of block 0 takes the chunk reductions and block flushes
+        const bool red = FU && NB == 4 && b0 == 0;
         auto step = [&](uint32_t k, float2* cur, float2* pre) {
             const long long ws0 = wprof ? (long long)clock64() : 0;
             load_chunk(min(k + 2, nch - 1), pre);
-            rec(k, cur, b0, lw0, sum0, M0, V0);
+            if (red) {
+                if (k >= 1) reduce(k - 1);
+                if ((k & 7) == 0 && k >= 8) flush(k / 8 - 1);
+            }
+            rec(k, cur, b0, lw0, sum0, M0, V0, b0 * 64 + lane < R);
             if (wprof) wbusy += (long long)clock64() - ws0;
             __syncthreads();
         };
@@ -1376,6 +1419,10 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
             step(k, bufA, bufC);
             if (k + 1 < nch) step(k + 1, bufB, bufA);
             if (k + 2 < nch) step(k + 2, bufC, bufB);
+        }
+        if (red) {
+            reduce(nch - 1);
+            flush((nch - 1) / 8);
         }
         if (!FU && b0 * 64 + lane < R) {
             double* st = J.st + (size_t)g * 3 * R;
@@ -1386,9 +1433,10 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
         for (uint32_t k = 0; k < nch; k++) __syncthreads();
     }
     if (wprof && lane == 0 && m >= 4096) {
-        atomicAdd(&cm.prof[kPfWaveBusy + wv], (unsigned long long)wbusy);
-        atomicAdd(&cm.prof[kPfWaveBusy + kWaves + wv], (unsigned long long)((long long)clock64() - wwall0));
-        atomicAdd(&cm.prof[kPfWaveBusy + 2 * kWaves + wv], (unsigned long long)wred);
+        const int pb = kPfWaveBusy + (NB == 4 ? 3 * kWaves : 0);
+        atomicAdd(&cm.prof[pb + wv], (unsigned long long)wbusy);
+        atomicAdd(&cm.prof[pb + kWaves + wv], (unsigned long long)((long long)clock64() - wwall0));
+        atomicAdd(&cm.prof[pb + 2 * kWaves + wv], (unsigned long long)wred);
     }
     __syncthreads();
     if (!FU && active && wv == (g == 0 ? 0 : 5)) {
@@ -3116,10 +3164,14 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
             for (int i = 0; i < PF_N; i++)
                 std::fprintf(stderr, "  %-22s %16llu%s\n", kPfNames[i], h[i],
                              i < PF_NSPLIT ? (std::string("  ") + std::to_string(100.0 * h[i] / (tot ? tot : 1)).substr(0, 5) + "%").c_str() : "");
-            for (int w = 0; w < kWaves; w++)
-                std::fprintf(stderr, "  variance wave %d (clusters >= 4096 columns): step busy %llu, reduce busy %llu of %llu cycles (%.1f%%)\n", w,
-                             h[kPfWaveBusy + w], h[kPfWaveBusy + 2 * kWaves + w], h[kPfWaveBusy + kWaves + w],
-                             100.0 * h[kPfWaveBusy + w] / (h[kPfWaveBusy + kWaves + w] ? h[kPfWaveBusy + kWaves + w] : 1));
+            for (int c = 0; c < 2; c++)
+                for (int w = 0; w < kWaves; w++) {
+                    const unsigned long long* hb = h + kPfWaveBusy + 3 * kWaves * c;
+                    const double wall = (double)(hb[kWaves + w] ? hb[kWaves + w] : 1);
+                    std::fprintf(stderr, "  variance wave %d (clusters >= 4096 columns, %s rows): step busy %llu (%.1f%%), "
+                                 "reduce busy %llu (%.1f%%) of %llu cycles\n", w, c ? "193-256" : "<= 192",
+                                 hb[w], 100.0 * hb[w] / wall, hb[2 * kWaves + w], 100.0 * hb[2 * kWaves + w] / wall, hb[kWaves + w]);
+                }
             std::fprintf(stderr, "  split columns   #splits   cycles/split   variance/split   pre-proj/split   cycles/column   %%cycles\n");
             unsigned long long stot = 0;
             for (int b = 0; b < kPfBuckets; b++) stot += h[PF_N + 4 * b + 1];

@@ -91,6 +91,27 @@ static double wsum_d(const double *t, uint32_t R)
         for (int l = 0; l < off; l++) p[l] = p[l] + p[l + off];
     return p[0];
 }
+/* The per-prefix row sums of a split's two calculateClusterVariance passes
+ * (inc_u / inc_i below) use a second fixed order, the one the device's split
+ * engine forms without moving the per-row terms between waves: each 64-row
+ * block is reduced by the halving tree on its own (rows past R enter as +0.0),
+ * and the block totals are added in ascending block order.  Like wsum_d this
+ * is a re-association of the reference's in-order inner_prod (:1107-1117). */
+static double wsum_blk(const double *t, uint32_t R)
+{
+    double acc = 0.0;
+    for (uint32_t b = 0; b * WS_LANES < R; b++) {
+        double p[WS_LANES];
+        for (int l = 0; l < WS_LANES; l++) {
+            uint32_t r = b * WS_LANES + (uint32_t)l;
+            p[l] = r < R ? t[r] : 0.0;
+        }
+        for (int off = WS_LANES / 2; off >= 1; off >>= 1)
+            for (int l = 0; l < off; l++) p[l] = p[l] + p[l + off];
+        acc = b == 0 ? p[0] : acc + p[0];
+    }
+    return acc;
+}
 static float wsum_f(const float *t, uint32_t R)
 {
     float p[WS_LANES];
@@ -401,22 +422,24 @@ static int cluster_variance(clustering_t *C, const uint32_t *first, long step, u
             double rws = 1.0 / weightSum;
             double *t = C->scr;
             for (uint32_t r = 0; r < R; r++) t[r] = C->locw[r] * (sumVars[r] * weightSum);
-            double ipi = wsum_d(t, R);
+            double ipi = wsum_blk(t, R);
             if (n == 0) {
                 inc_u[n] = 0;
             } else {
                 for (uint32_t r = 0; r < R; r++) t[r] = C->locw[r] * (Mv[r] * rws);
-                inc_u[n] = (float)wsum_d(t, R);
+                inc_u[n] = (float)wsum_blk(t, R);
             }
             inc_i[n] = (float)ipi;
         }
     }
+    /* with per-prefix outputs the totals are the last prefix's (same order) */
+    double (*wsum)(const double *, uint32_t) = inc_u ? wsum_blk : wsum_d;
     double rws = 1.0 / weightSum;
     double *t = C->scr;
     for (uint32_t r = 0; r < R; r++) t[r] = C->locw[r] * (Mv[r] * rws);
-    double ipu = wsum_d(t, R);
+    double ipu = wsum(t, R);
     for (uint32_t r = 0; r < R; r++) t[r] = C->locw[r] * (sumVars[r] * weightSum);
-    double ipi = wsum_d(t, R);
+    double ipi = wsum(t, R);
     *res_u = (float)ipu;
     *res_i = (float)ipi;
     if (!isfinite(*res_u) || *res_u < 0) return 1;
