@@ -2350,25 +2350,25 @@ __device__ __noinline__ void column_weights(const JobDev& J, const Common& cm, C
     const uint32_t lane = (uint32_t)(tid & 63);
     const uint32_t N = cm.nvrl, R = J.nrows;
     // calculateColumnWeigths (:985-1008): one wave per 16 columns, rows in the
-    // shared order (lane l sums rows l, l+64, l+128 from 0, then the halving
+    // shared order (lane l sums rows l, l+64, l+128, l+192 from 0, then the halving
     // tree, here transposed: the 16 column sums in one tree16_transposed)
-    if (R <= 64u * 3u) {
-        const uint32_t NBr = (R + 63) / 64;
+    if (R <= 64u * 4u) {
+        const uint32_t NBr = (uint32_t)__builtin_amdgcn_readfirstlane((int)((R + 63) / 64));   // uniform: scalar branches
         const float2* const Rt = cm.Rt;
         auto* const colw = gpw(J.colw);
         constexpr int Q = 16;
-        RowRef rr[3];
-        double lw[3];
+        RowRef rr[4];
+        double lw[4];
 #pragma unroll
-        for (int b = 0; b < 3; b++) {
+        for (int b = 0; b < 4; b++) {
             const uint32_t r = (uint32_t)b * 64 + lane;
             rr[b] = row_ref(J, min(r, R - 1));
             lw[b] = r < R ? gp(J.locw)[r] : 0.0;
         }
         for (uint32_t v0 = (uint32_t)wave * Q; v0 < N; v0 += kWaves * Q) {
-            float2 x[3][Q];
+            float2 x[4][Q];
 #pragma unroll
-            for (int b = 0; b < 3; b++)
+            for (int b = 0; b < 4; b++)
 #pragma unroll
                 for (int q = 0; q < Q; q++)
                     x[b][q] = (uint32_t)b < NBr ? ldg2(Rt, rr[b].base + (size_t)min(v0 + (uint32_t)q, N - 1) * rr[b].stride)
@@ -2378,11 +2378,12 @@ __device__ __noinline__ void column_weights(const JobDev& J, const Common& cm, C
             for (int q = 0; q < Q; q++) {
                 double p = 0.0;
 #pragma unroll
-                for (int b = 0; b < 3; b++) {
-                    if ((uint32_t)b * 64 + lane < R) {
+                for (int b = 0; b < 4; b++) {
+                    if ((uint32_t)b < NBr) {                   // wave-uniform
                         const double mean = (double)x[b][q].x, var = (double)x[b][q].y;
                         const double xx = mean * mean + var;
-                        p = p + lw[b] * xx;
+                        const double pn = p + lw[b] * xx;
+                        p = (uint32_t)b * 64 + lane < R ? pn : p;   // a select, not a branch
                     }
                 }
                 v[q] = p;
