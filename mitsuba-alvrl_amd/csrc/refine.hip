@@ -147,6 +147,8 @@ struct Common {
     int roam_on;                   // finished leaders and helpers roam too (scratch sized for Rmax)
     const SplitWs* roam_ws;        // [nroam] their scratch, sized for the largest job
     const uint32_t* roam_order;    // null: roam from the last job served; else scan jobs in this order
+    int team_setup;                // a job's first helper takes half the column weights and the
+                                   // unclustered variance off the leader (ALVRL_TEAM_SETUP=0: off)
 };
 __device__ __forceinline__ void trace(const Common& cm, uint32_t phase, uint32_t value)
 {
@@ -2260,6 +2262,85 @@ __device__ void split_team(const JobDev& J, const Common& cm, Ctl& C, uint32_t b
     pf.mark(PF_T_ENQ);
 }
 
+// Setup tasks of a job's first helper (Team::ctl words 4-9, zeroed per
+// launch): task 0 = the column weights of [N/2, N), task 1 = the unclustered
+// variance.  Either side claims a free task with a CAS (state 0 -> 1); the
+// one that ran it publishes the outputs and sets state 2 (producer form of
+// spec_split: drained stores, barrier, one agent-scope release, relaxed
+// flag).  The leader waits only for a task a running helper has claimed, so
+// nothing depends on the helper being resident.  Results are those of the
+// leader alone: the same per-column and per-row arithmetic in the same order.
+enum : uint32_t { kSuColw = 4, kSuUncl = 5, kSuIntVar = 6, kSuTrVar = 7, kSuUnclErr = 8, kSuColwErr = 9 };
+__device__ bool su_claim(const Team& T, uint32_t task, Ctl& C)
+{
+    if (threadIdx.x == 0) C.go = cas_rlx(&T.ctl[task], 0u, 1u) ? 1 : 0;
+    __syncthreads();
+    const bool got = C.go != 0;
+    __syncthreads();
+    return got;
+}
+__device__ void su_publish(const Team& T, uint32_t task)
+{
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        st_rlx(&T.ctl[task], 2u);
+    }
+    __syncthreads();
+}
+// the leader's wait for a task a helper has claimed: that helper is running
+// and depends on nobody, so the wait ends; it is not bounded by the wait
+// knobs (the helper writes colw, which the leader must not finish under it),
+// only by a 60 s guard (false: the job fails)
+__device__ bool su_wait(const Team& T, uint32_t task, const Common& cm, Ctl& C)
+{
+    if (threadIdx.x == 0) {
+        const unsigned long long t0 = wall();
+        int ok = 1;
+        while (ld_rlx(&T.ctl[task]) != 2u) {
+            if (wall() - t0 > kSpinTicks) { ok = 0; break; }
+            __builtin_amdgcn_s_sleep(8);
+        }
+        C.go = ok;
+    }
+    __syncthreads();
+    fence_acq();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const bool ok = C.go != 0;
+    __syncthreads();
+    return ok;
+}
+__device__ void colw_raw(const JobDev& J, const Common& cm, Ctl& C, uint32_t vb, uint32_t ve);
+__device__ void unclustered_variance(const JobDev& J, const Common& cm, Ctl& C, const uint32_t* vrls_in, uint32_t nv);
+// the helper's side (Jw: its own scratch, colw shared with the leader)
+__device__ void setup_tasks(const JobDev& J0, const JobDev& Jw, const Common& cm, Ctl& C, bool)
+{
+    const Team& T = J0.team;
+    const uint32_t N = cm.nvrl;
+    if (su_claim(T, kSuColw, C)) {
+        if (threadIdx.x == 0) C.err = 0;
+        __syncthreads();
+        colw_raw(Jw, cm, C, N / 2, N);
+        if (threadIdx.x == 0) st_rlx(&T.ctl[kSuColwErr], (uint32_t)C.err);
+        su_publish(T, kSuColw);
+    }
+    if (su_claim(T, kSuUncl, C)) {
+        if (threadIdx.x == 0) C.err = 0;
+        __syncthreads();
+        unclustered_variance(Jw, cm, C, cm.init_vrls, cm.init_off[cm.ninit]);
+        if (threadIdx.x == 0) {
+            st_rlx(&T.ctl[kSuIntVar], __float_as_uint(C.unclIntVar));
+            st_rlx(&T.ctl[kSuTrVar], __float_as_uint(C.tracingVar));
+            st_rlx(&T.ctl[kSuUnclErr], (uint32_t)C.err);
+        }
+        su_publish(T, kSuUncl);
+    }
+    if (threadIdx.x == 0) C.err = 0;
+    __syncthreads();
+}
+
 // A helper workgroup: split queued clusters of job J until the leader stops.
 __device__ __noinline__ void helper_loop(const JobDev& J0, uint32_t hid, const Common& cm, Ctl& C,
                                          unsigned long long* lds)
@@ -2273,6 +2354,7 @@ __device__ __noinline__ void helper_loop(const JobDev& J0, uint32_t hid, const C
     const int tid = threadIdx.x;
     if (tid == 0) C.err = 0;
     trace(cm, 10, 0);
+    if (hid == 0 && cm.team_setup) setup_tasks(J0, J, cm, C, false);
     while (true) {
         if (tid == 0) {
             const unsigned long long t_idle = wall();
@@ -2344,11 +2426,13 @@ __device__ __noinline__ void roam_loop(const JobDev* jobs, const SplitWs& w, uin
 // calculateColumnWeigths (:985-1008) with the +1% of the mean (:1002-1007).
 // Out of line: inlined into k_refine its loops ran on spilled registers
 // (scratch reloads, each a vmcnt(0) wait).
-__device__ __noinline__ void column_weights(const JobDev& J, const Common& cm, Ctl& C)
+// calculateColumnWeigths' per-column weights of columns [vb, ve) (the part
+// a job's helper can take; colw_finish adds the average afterwards)
+__device__ __noinline__ void colw_raw(const JobDev& J, const Common& cm, Ctl& C, uint32_t vb, uint32_t ve)
 {
     const int tid = threadIdx.x, wave = tid >> 6;
     const uint32_t lane = (uint32_t)(tid & 63);
-    const uint32_t N = cm.nvrl, R = J.nrows;
+    const uint32_t R = J.nrows;
     // calculateColumnWeigths (:985-1008): one wave per 16 columns, rows in the
     // shared order (lane l sums rows l, l+64, l+128, l+192 from 0, then the halving
     // tree, here transposed: the 16 column sums in one tree16_transposed)
@@ -2365,13 +2449,13 @@ __device__ __noinline__ void column_weights(const JobDev& J, const Common& cm, C
             rr[b] = row_ref(J, min(r, R - 1));
             lw[b] = r < R ? gp(J.locw)[r] : 0.0;
         }
-        for (uint32_t v0 = (uint32_t)wave * Q; v0 < N; v0 += kWaves * Q) {
+        for (uint32_t v0 = vb + (uint32_t)wave * Q; v0 < ve; v0 += kWaves * Q) {
             float2 x[4][Q];
 #pragma unroll
             for (int b = 0; b < 4; b++)
 #pragma unroll
                 for (int q = 0; q < Q; q++)
-                    x[b][q] = (uint32_t)b < NBr ? ldg2(Rt, rr[b].base + (size_t)min(v0 + (uint32_t)q, N - 1) * rr[b].stride)
+                    x[b][q] = (uint32_t)b < NBr ? ldg2(Rt, rr[b].base + (size_t)min(v0 + (uint32_t)q, ve - 1) * rr[b].stride)
                                                 : make_float2(0.0f, 0.0f);
             double v[Q];
 #pragma unroll
@@ -2391,7 +2475,7 @@ __device__ __noinline__ void column_weights(const JobDev& J, const Common& cm, C
             const double t = tree16_transposed(v, lane);
             if ((lane & 3) == 0) {
                 const uint32_t j = ((lane >> 5) & 1) | (((lane >> 4) & 1) << 1) | (((lane >> 3) & 1) << 2) | (((lane >> 2) & 1) << 3);
-                if (v0 + j < N) {
+                if (v0 + j < ve) {
                     const float cw = (float)sqrt(t > 0.0 ? t : 0.0);
                     colw[v0 + j] = cw;
                     if (!isfinite(cw)) C.err = 1;
@@ -2399,7 +2483,7 @@ __device__ __noinline__ void column_weights(const JobDev& J, const Common& cm, C
             }
         }
     } else {
-        for (uint32_t v0 = (uint32_t)wave * kCB; v0 < N; v0 += kWaves * kCB) {
+        for (uint32_t v0 = vb + (uint32_t)wave * kCB; v0 < ve; v0 += kWaves * kCB) {
             double p[kCB];
 #pragma unroll
             for (int q = 0; q < kCB; q++) p[q] = 0.0;
@@ -2408,7 +2492,7 @@ __device__ __noinline__ void column_weights(const JobDev& J, const Common& cm, C
                 const double lw = J.locw[r];
                 float2 mv[kCB];
 #pragma unroll
-                for (int q = 0; q < kCB; q++) mv[q] = ldg2(cm.Rt, rr.base + (size_t)min(v0 + (uint32_t)q, N - 1) * rr.stride);
+                for (int q = 0; q < kCB; q++) mv[q] = ldg2(cm.Rt, rr.base + (size_t)min(v0 + (uint32_t)q, ve - 1) * rr.stride);
 #pragma unroll
                 for (int q = 0; q < kCB; q++) {
                     const double mean = (double)mv[q].x, var = (double)mv[q].y;
@@ -2419,7 +2503,7 @@ __device__ __noinline__ void column_weights(const JobDev& J, const Common& cm, C
 #pragma unroll
             for (int q = 0; q < kCB; q++) {
                 const double t = tree_d(p[q]);
-                if (lane == 0 && v0 + q < N) {
+                if (lane == 0 && v0 + q < ve) {
                     const float cw = (float)sqrt(t > 0.0 ? t : 0.0);
                     J.colw[v0 + q] = cw;
                     if (!isfinite(cw)) C.err = 1;
@@ -2428,6 +2512,15 @@ __device__ __noinline__ void column_weights(const JobDev& J, const Common& cm, C
         }
     }
     __syncthreads();
+}
+
+// the average of all column weights (running float sum in index order) and
+// its 1 % added to every weight (:1002-1007)
+__device__ __noinline__ void colw_finish(const JobDev& J, const Common& cm, Ctl& C)
+{
+    const int tid = threadIdx.x, wave = tid >> 6;
+    const uint32_t lane = (uint32_t)(tid & 63);
+    const uint32_t N = cm.nvrl;
     if (wave == 0) {
         // the running float sum in index order (one add after the other, as
         // the reference's loop), 64 weights per load, broadcast by v_readlane
@@ -2455,7 +2548,8 @@ __device__ __noinline__ void column_weights(const JobDev& J, const Common& cm, C
 }
 
 // calculateUnclusteredVariance (:1022-1048), out of line for the same reason
-__device__ __noinline__ void unclustered_variance(const JobDev& J, const Common& cm, Ctl& C, uint32_t nv)
+__device__ __noinline__ void unclustered_variance(const JobDev& J, const Common& cm, Ctl& C, const uint32_t* vrls_in,
+                                                  uint32_t nv)
 {
     const int tid = threadIdx.x, wave = tid >> 6;
     const uint32_t lane = (uint32_t)(tid & 63);
@@ -2466,7 +2560,7 @@ __device__ __noinline__ void unclustered_variance(const JobDev& J, const Common&
     // per lane for the block, entries 16 columns ahead
     {
         const uint32_t NBr = (R + 63) / 64;
-        const auto* vr = gp(J.vrls);
+        const auto* vr = gp(vrls_in);
         constexpr int G = 16;
         for (uint32_t rb = (uint32_t)wave; rb < NBr; rb += kWaves) {
             const uint32_t r = rb * 64 + lane;
@@ -2562,7 +2656,23 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
         C.hlog_n = 0; C.hlog_full = 1;
     }
     __syncthreads();
-    column_weights(J, cm, C);
+    const bool tsu = cm.team_setup && cm.team > 1 && J.team.helpers != 0;
+    if (tsu) {
+        // the first half here, the second on the job's helper unless it
+        // has not claimed it yet
+        colw_raw(J, cm, C, 0, N / 2);
+        if (su_claim(J.team, kSuColw, C)) {
+            colw_raw(J, cm, C, N / 2, N);
+        } else if (!su_wait(J.team, kSuColw, cm, C)) {
+            if (tid == 0) C.err = 1;
+        } else if (tid == 0 && ld_rlx(&J.team.ctl[kSuColwErr])) {
+            C.err = 1;
+        }
+        __syncthreads();
+    } else {
+        colw_raw(J, cm, C, 0, N);
+    }
+    colw_finish(J, cm, C);
     pf.mark(PF_COLW);
     for (uint32_t i = tid; i < nv; i += kThreads) J.vrls[i] = cm.init_vrls[i];
     __syncthreads();
@@ -2582,7 +2692,17 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
         }
     }
     pf.mark(PF_INIT);
-    unclustered_variance(J, cm, C, nv);
+    if (tsu && !su_claim(J.team, kSuUncl, C)) {
+        const bool ok = su_wait(J.team, kSuUncl, cm, C);
+        if (tid == 0) {
+            if (!ok || ld_rlx(&J.team.ctl[kSuUnclErr])) C.err = 1;
+            C.unclIntVar = __uint_as_float(ld_rlx(&J.team.ctl[kSuIntVar]));
+            C.tracingVar = __uint_as_float(ld_rlx(&J.team.ctl[kSuTrVar]));
+        }
+        __syncthreads();
+    } else {
+        unclustered_variance(J, cm, C, cm.init_vrls, nv);
+    }
     pf.mark(PF_UNCL);
     // release the initial clusters' vrls to the helpers (see split_team)
     drain_vmem();
@@ -3032,6 +3152,8 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
         cm.side_k = sk ? (uint32_t)std::max(0, std::atoi(sk)) : 1u << 24;
         const char* es = std::getenv("ALVRL_ENQ_START");
         cm.enq_start = es ? std::atoi(es) : 0;   // queueing after the commit only: 398 vs 401 ms at width 32
+        const char* tsu = std::getenv("ALVRL_TEAM_SETUP");
+        cm.team_setup = tsu ? std::atoi(tsu) : 1;
     }
     // ALVRL_ROAM_ORDER=1: roaming helpers scan the jobs with the most rows
     // first.  Measured slower (C4 refine 436 vs 420 ms: the roamers crowd the
