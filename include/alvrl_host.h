@@ -29,6 +29,17 @@ typedef struct {
     float light_pos[3];
     float light_intensity[3];
     alvrl_medium_desc medium;
+    /* Optional occluders inside the box: n_occluders triangles, 9 floats
+     * each (p0, p1, p2; counter-clockwise seen from the lit side: the face
+     * normal is normalize(cross(p1 - p0, p2 - p0)), skdtree.h:367-396), with
+     * a one-sided diffuse BSDF of reflectance occluder_albedo.  They are hit
+     * by eye rays and particles and block the gather's U-V and surface-V
+     * connections (Scene::evalTransmittance, scene.cpp:619-679).  The array
+     * is read during the call that receives the descriptor (and copied by
+     * alvrl_integrator_preprocess). */
+    const float *occluders;
+    uint32_t n_occluders;
+    float occluder_albedo[3];
 } alvrl_scene_desc;
 
 /* The benchmark scene of BASELINE.md ("homogeneous smoke box"). */
@@ -39,6 +50,13 @@ ALVRL_API void alvrl_scene_default(alvrl_scene_desc *s, int width, int height);
 ALVRL_API int alvrl_scene_records(const alvrl_scene_desc *s, int medium_scatters,
                                   const uint32_t *pixel_ids, uint32_t n, alvrl_gather_rec *out);
 
+/* The same records on the current HIP device (Sensor::sampleRay +
+ * Scene::rayIntersect through the occluder BVH: the GPU eye-ray first hit),
+ * bit-identical to alvrl_scene_records.  d_pixel_ids: device array (NULL:
+ * pixels 0..n-1); d_out: n device records, written on 'stream' (NULL: the
+ * null stream); returns after they are written. */
+ALVRL_API int alvrl_scene_records_gpu(const alvrl_scene_desc *s, int medium_scatters, const uint32_t *d_pixel_ids,
+                                      uint32_t n, alvrl_gather_rec *d_out, void *stream);
 /* Multi-GPU image partition of alvrl_integrator_render: 64x64 tiles in
  * row-major tile order, tile t owned by rank t % world (the
  * reference's analogue is the block scheduler handing 32x32 blocks to workers,

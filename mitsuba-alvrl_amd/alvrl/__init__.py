@@ -79,6 +79,7 @@ def lib() -> C.CDLL:
     L.alvrl_ctx_destroy.argtypes = [vp]; L.alvrl_ctx_destroy.restype = None
     L.alvrl_set_medium.argtypes = [vp, P(MediumDesc)]
     L.alvrl_set_pass.argtypes = [vp, u32]
+    L.alvrl_set_occluders.argtypes = [vp, vp, u32]
     L.alvrl_upload_vrls.argtypes = [vp, vp, u32, u64, i32]
     L.alvrl_num_vrls.argtypes = [vp]; L.alvrl_num_vrls.restype = u32
     L.alvrl_set_clusters.argtypes = [vp, u32, P(u32), P(u32), P(f32), P(u32), P(f32), u32]
@@ -169,6 +170,11 @@ class Context:
 
     def set_pass(self, p: int):
         _check(self.L.alvrl_set_pass(self.h, p))
+
+    def set_occluders(self, tris):
+        """Occluder triangles ((n, 9) float32) blocking the gathers' connections."""
+        arr = np.ascontiguousarray(np.asarray(tris, np.float32).reshape(-1, 9))
+        _check(self.L.alvrl_set_occluders(self.h, _ptr(arr) if len(arr) else None, len(arr)))
 
     def upload_vrls(self, soa, particle_count: int):
         """soa: (9, n) float32 numpy array or CUDA tensor (start xyz, end xyz, power rgb)."""
@@ -327,7 +333,8 @@ class SceneDesc(C.Structure):
                 ("fov_x_deg", C.c_float), ("width", C.c_int), ("height", C.c_int),
                 ("box_min", C.c_float * 3), ("box_max", C.c_float * 3), ("albedo", C.c_float * 3),
                 ("light_pos", C.c_float * 3), ("light_intensity", C.c_float * 3),
-                ("medium", MediumDesc)]
+                ("medium", MediumDesc), ("occluders", C.POINTER(C.c_float)), ("n_occluders", C.c_uint32),
+                ("occluder_albedo", C.c_float * 3)]
 
 
 class IntegratorStats(C.Structure):
@@ -455,6 +462,7 @@ def _host():
     L.alvrl_scene_records.argtypes = [P(SceneDesc), i32, vp, u32, vp]
     L.alvrl_trace_vrls.argtypes = [P(SceneDesc), u32, u32, u32, i32, i32, i32, vp, u32, P(u32), P(u64)]
     L.alvrl_trace_vrls_gpu.argtypes = [P(SceneDesc), u32, u32, u32, i32, i32, i32, vp, u32, P(u32), P(u64)]
+    L.alvrl_scene_records_gpu.argtypes = [P(SceneDesc), i32, vp, u32, vp, vp]
     L.alvrl_read_vrl_file.argtypes = [C.c_char_p, P(MediumDesc), vp, u32, P(u32), P(u64)]
     L.alvrl_write_vrl_file.argtypes = [C.c_char_p, vp, u32]
     L.alvrl_tile_pixels.argtypes = [i32, i32, u32, u32, vp, u32, P(u32)]
@@ -505,6 +513,33 @@ def scene_default(width: int, height: int) -> SceneDesc:
     return s
 
 
+def scene_set_occluders(scene: SceneDesc, tris, albedo=(0.5, 0.5, 0.5)) -> SceneDesc:
+    """Occluder triangles inside the box (alvrl_scene_desc.occluders): an
+    (n, 9) float array of (p0, p1, p2), face normal cross(p1 - p0, p2 - p0).
+    The array is kept alive on the descriptor."""
+    arr = np.ascontiguousarray(np.asarray(tris, np.float32).reshape(-1, 9))
+    scene._occ_keep = arr
+    scene.occluders = arr.ctypes.data_as(C.POINTER(C.c_float)) if len(arr) else None
+    scene.n_occluders = len(arr)
+    for i in range(3):
+        scene.occluder_albedo[i] = float(albedo[i])
+    return scene
+
+
+def box_mesh(lo, hi) -> np.ndarray:
+    """12 triangles of an axis-aligned box [lo, hi] with outward face normals."""
+    lo = np.asarray(lo, np.float32)
+    hi = np.asarray(hi, np.float32)
+    c = np.array([[lo[0] if i & 1 == 0 else hi[0], lo[1] if i & 2 == 0 else hi[1],
+                   lo[2] if i & 4 == 0 else hi[2]] for i in range(8)], np.float32)
+    quads = [(0, 2, 6, 4), (1, 5, 7, 3), (0, 4, 5, 1), (2, 3, 7, 6), (0, 1, 3, 2), (4, 6, 7, 5)]
+    tris = []
+    for a, b, cc, d in quads:   # outward: x-, x+, y-, y+, z-, z+
+        tris.append(np.concatenate([c[a], c[cc], c[b]]))
+        tris.append(np.concatenate([c[a], c[d], c[cc]]))
+    return np.asarray(tris, np.float32)
+
+
 def scene_records(scene: SceneDesc, pixel_ids=None, medium_scatters: bool = True) -> np.ndarray:
     L = _host()
     n = scene.width * scene.height if pixel_ids is None else len(pixel_ids)
@@ -523,6 +558,21 @@ def trace_vrls(scene: SceneDesc, target: int, seed: int = 0x5EED0001, pass_: int
     _hcheck(L.alvrl_trace_vrls(C.byref(scene), seed, pass_, target, int(short_vrls), max_depth,
                                rr_depth, _ptr(soa), cap, C.byref(n), C.byref(pc)))
     return np.ascontiguousarray(soa[:, :n.value]), int(pc.value)
+
+
+def scene_records_gpu(scene: SceneDesc, pixel_ids=None, medium_scatters: bool = True, device: int = 0):
+    """alvrl_scene_records_gpu: the records on the HIP device (a CUDA tensor)."""
+    import torch
+    L = _host()
+    dev = torch.device("cuda", device)
+    n = scene.width * scene.height if pixel_ids is None else len(pixel_ids)
+    out = torch.empty((n, REC_WORDS), dtype=torch.float32, device=dev)
+    ids = None if pixel_ids is None else torch.as_tensor(np.asarray(pixel_ids, np.uint32).astype(np.int32)).to(dev)
+    with torch.cuda.device(dev):
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        _hcheck(L.alvrl_scene_records_gpu(C.byref(scene), int(medium_scatters),
+                                          None if ids is None else ids.data_ptr(), n, out.data_ptr(), stream))
+    return out
 
 
 def trace_vrls_gpu(scene: SceneDesc, target: int, seed: int = 0x5EED0001, pass_: int = 0,

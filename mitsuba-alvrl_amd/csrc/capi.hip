@@ -88,8 +88,19 @@ struct alvrl_ctx {
     bool timed = false;
     float refine_ms = 0.0f;
     unsigned long long refine_entries = 0;
+    // occluder BVH (alvrl_set_occluders); P.occ views it
+    BvhNode* d_bvh_nodes = nullptr;
+    float* d_bvh_tris = nullptr;
+    uint32_t* d_bvh_ids = nullptr;
     std::mutex mu;
 };
+
+static void free_occluders(alvrl_ctx* c)
+{
+    hipFree(c->d_bvh_nodes); hipFree(c->d_bvh_tris); hipFree(c->d_bvh_ids);
+    c->d_bvh_nodes = nullptr; c->d_bvh_tris = nullptr; c->d_bvh_ids = nullptr;
+    c->P.occ = bvh::View{nullptr, nullptr, nullptr, 0u};
+}
 
 static thread_local std::string g_err = "";
 
@@ -168,6 +179,7 @@ ALVRL_API void alvrl_ctx_destroy(alvrl_ctx* c)
     if (c->stream) hipStreamSynchronize(c->stream);
     hipFree(c->d_soa); hipFree(c->d_vrl); hipFree(c->d_counter);
     free_clusters(c);
+    free_occluders(c);
     if (c->ev0) hipEventDestroy(c->ev0);
     if (c->ev1) hipEventDestroy(c->ev1);
     if (c->stream) hipStreamDestroy(c->stream);
@@ -194,6 +206,26 @@ ALVRL_API int alvrl_set_medium(alvrl_ctx* c, const alvrl_medium_desc* m)
     c->P.phase_type = m->phase_type;
     c->P.g = m->phase_g;
     c->medium_set = true;
+    return ALVRL_OK;
+}
+
+ALVRL_API int alvrl_set_occluders(alvrl_ctx* c, const float* tris, uint32_t ntri)
+{
+    if (!c || (!tris && ntri)) return fail(ALVRL_ERR_INVALID, "alvrl_set_occluders: null argument");
+    HIPCHK(hipSetDevice(c->cfg.device));
+    HIPCHK(hipStreamSynchronize(c->stream));   // no gather still reads the old BVH
+    free_occluders(c);
+    if (ntri == 0) return ALVRL_OK;
+    for (size_t i = 0; i < 9 * (size_t)ntri; i++)
+        if (!std::isfinite(tris[i])) return fail(ALVRL_ERR_INVALID, "alvrl_set_occluders: non-finite vertex");
+    const BvhHost b = build_bvh(tris, ntri);
+    HIPCHK(hipMalloc(&c->d_bvh_nodes, b.nodes.size() * sizeof(BvhNode)));
+    HIPCHK(hipMalloc(&c->d_bvh_tris, b.tris.size() * 4));
+    HIPCHK(hipMalloc(&c->d_bvh_ids, b.ids.size() * 4));
+    HIPCHK(hipMemcpy(c->d_bvh_nodes, b.nodes.data(), b.nodes.size() * sizeof(BvhNode), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->d_bvh_tris, b.tris.data(), b.tris.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->d_bvh_ids, b.ids.data(), b.ids.size() * 4, hipMemcpyHostToDevice));
+    c->P.occ = bvh::View{c->d_bvh_nodes, c->d_bvh_tris, c->d_bvh_ids, ntri};
     return ALVRL_OK;
 }
 

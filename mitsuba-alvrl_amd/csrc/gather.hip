@@ -59,7 +59,7 @@ __device__ __forceinline__ void count_pairs(unsigned long long* counter, bool la
         atomicAdd(counter, (unsigned long long)__popcll(m) * per_lane);
 }
 
-template <int NVV, int NVS>
+template <int NVV, int NVS, bool VIS = false>
 __global__ void __launch_bounds__(256) k_gather_brute(const Rec* __restrict__ recs,
                                                       const uint32_t* __restrict__ ids, uint32_t nrec,
                                                       const VrlPrep* __restrict__ vp, uint32_t nvrl,
@@ -77,7 +77,7 @@ __global__ void __launch_bounds__(256) k_gather_brute(const Rec* __restrict__ re
         for (uint32_t v = 0; v < nvrl; ++v) {
             const VrlPrep V = vp[v];
             float c[3], m, s;
-            integrate_vrl<NVV, NVS, false>(P, q, V, rid, v, kDomGather, P.nvv, P.nvs, c, &m, &s);
+            integrate_vrl<NVV, NVS, false, VIS>(P, q, V, rid, v, kDomGather, P.nvv, P.nvs, c, &m, &s);
             // vrlContribution *= normalization; Li += vrlContribution (:810, 815)
             L0 += c[0] * normalization; L1 += c[1] * normalization; L2 += c[2] * normalization;
         }
@@ -90,7 +90,7 @@ __global__ void __launch_bounds__(256) k_gather_brute(const Rec* __restrict__ re
 
 struct WorkItem { uint32_t slice, begin, count, pad; };
 
-template <int NVV, int NVS>
+template <int NVV, int NVS, bool VIS = false>
 __global__ void __launch_bounds__(256) k_gather_clustered(
     const Rec* __restrict__ recs, const uint32_t* __restrict__ ids,
     const WorkItem* __restrict__ items, uint32_t nitems, const VrlPrep* __restrict__ vp,
@@ -120,7 +120,7 @@ __global__ void __launch_bounds__(256) k_gather_clustered(
             const float w = lw[i];
             const VrlPrep V = vp[v];
             float c[3], m, s;
-            integrate_vrl<NVV, NVS, false>(P, q, V, rid, v, kDomGather, P.nvv, P.nvs, c, &m, &s);
+            integrate_vrl<NVV, NVS, false, VIS>(P, q, V, rid, v, kDomGather, P.nvv, P.nvs, c, &m, &s);
             // Li += weights->at(i) * integrateVRL(...)  (:587-589)
             L0 += c[0] * w; L1 += c[1] * w; L2 += c[2] * w;
         }
@@ -189,7 +189,7 @@ hipError_t launch_false_color(const Rec* recs, const WorkItem* items, uint32_t n
 
 // R build: lane = representative row, the block's 4 waves interleave over a
 // VRL chunk.  Writes Rt[v][row0 + r] = (mean * norm, var * norm * norm).
-template <int NVV, int NVS>
+template <int NVV, int NVS, bool VIS = false>
 __global__ void __launch_bounds__(256) k_build_R(const Rec* __restrict__ recs,
                                                  const uint32_t* __restrict__ ids, uint32_t nrows,
                                                  const VrlPrep* __restrict__ vp, uint32_t nvrl,
@@ -213,14 +213,14 @@ __global__ void __launch_bounds__(256) k_build_R(const Rec* __restrict__ recs,
             const VrlPrep V = vp[v];
             float c[3];
             if (nsamp == 1) {
-                integrate_vrl<NVV, NVS, true>(P, q, V, rid, v, kDomRbuild, P.nvv, P.nvs, c, &mean, &var);
+                integrate_vrl<NVV, NVS, true, VIS>(P, q, V, rid, v, kDomRbuild, P.nvv, P.nvs, c, &mean, &var);
                 mean = mean * normalization;
                 var = var * normalization * normalization;
             } else {
                 // LiInternal's samples loop: entries are sums over the samples (:812-813)
                 for (int si = 0; si < nsamp; si++) {
                     float m, s2;
-                    integrate_vrl<NVV, NVS, true>(P, q, V, rid, v, kDomRbuild, P.nvv, P.nvs, c, &m, &s2,
+                    integrate_vrl<NVV, NVS, true, VIS>(P, q, V, rid, v, kDomRbuild, P.nvv, P.nvs, c, &m, &s2,
                                                   (uint32_t)si);
                     mean += m * normalization;
                     var += s2 * normalization * normalization;
@@ -238,7 +238,7 @@ __global__ void __launch_bounds__(256) k_build_R(const Rec* __restrict__ recs,
 // block except across slice boundaries, so the stores stay coalesced.  The
 // non-zero column test of Preprocessor::cluster rides along: one ballot per
 // (wave, VRL), one byte store when a mean is non-zero.
-template <int NVV, int NVS>
+template <int NVV, int NVS, bool VIS = false>
 __global__ void __launch_bounds__(256) k_build_R_blocks(const Rec* __restrict__ recs,
                                                         const uint32_t* __restrict__ ids, uint32_t nrows,
                                                         const VrlPrep* __restrict__ vp, uint32_t nvrl,
@@ -267,14 +267,14 @@ __global__ void __launch_bounds__(256) k_build_R_blocks(const Rec* __restrict__ 
             const VrlPrep V = vp[v];
             float c[3];
             if (nsamp == 1) {
-                integrate_vrl<NVV, NVS, true>(P, q, V, rid, v, kDomRbuild, P.nvv, P.nvs, c, &mean, &var);
+                integrate_vrl<NVV, NVS, true, VIS>(P, q, V, rid, v, kDomRbuild, P.nvv, P.nvs, c, &mean, &var);
                 mean = mean * normalization;
                 var = var * normalization * normalization;
             } else {
                 // LiInternal's samples loop: entries are sums over the samples (:812-813)
                 for (int si = 0; si < nsamp; si++) {
                     float m, s2;
-                    integrate_vrl<NVV, NVS, true>(P, q, V, rid, v, kDomRbuild, P.nvv, P.nvs, c, &m, &s2,
+                    integrate_vrl<NVV, NVS, true, VIS>(P, q, V, rid, v, kDomRbuild, P.nvv, P.nvs, c, &m, &s2,
                                                   (uint32_t)si);
                     mean += m * normalization;
                     var += s2 * normalization * normalization;
@@ -347,7 +347,9 @@ hipError_t launch_gather_brute(const Rec* recs, const uint32_t* ids, uint32_t nr
 {
     if (nrec == 0) return hipSuccess;
     const dim3 grid((nrec + 255) / 256), block(256);
-    if (P.nvv == 2 && P.nvs == 2)
+    if (P.occ.ntri)   // occluders: shadow tests (generic sample counts only)
+        hipLaunchKernelGGL((k_gather_brute<-1, -1, true>), grid, block, 0, s, recs, ids, nrec, vp, nvrl, P, normalization, out, counter);
+    else if (P.nvv == 2 && P.nvs == 2)
         hipLaunchKernelGGL((k_gather_brute<2, 2>), grid, block, 0, s, recs, ids, nrec, vp, nvrl, P,
                            normalization, out, counter);
     else
@@ -365,7 +367,9 @@ hipError_t launch_gather_clustered(const Rec* recs, const uint32_t* ids, const W
 {
     if (nitems == 0) return hipSuccess;
     const dim3 grid((nitems + 3) / 4), block(256);
-    if (P.nvv == 2 && P.nvs == 2)
+    if (P.occ.ntri)   // occluders: shadow tests (generic sample counts only)
+        hipLaunchKernelGGL((k_gather_clustered<-1, -1, true>), grid, block, 0, s, recs, ids, items, nitems, vp, slice_off, reps, weights, fb_reps, fb_w, n_fb, P, inv_pc, out, counter);
+    else if (P.nvv == 2 && P.nvs == 2)
         hipLaunchKernelGGL((k_gather_clustered<2, 2>), grid, block, 0, s, recs, ids, items, nitems,
                            vp, slice_off, reps, weights, fb_reps, fb_w, n_fb, P, inv_pc, out,
                            counter);
@@ -383,7 +387,9 @@ hipError_t launch_build_R(const Rec* recs, const uint32_t* ids, uint32_t nrows, 
     if (nrows == 0 || nvrl == 0) return hipSuccess;
     const uint32_t chunk = 256;
     const dim3 grid((nrows + 63) / 64, (nvrl + chunk - 1) / chunk), block(256);
-    if (P.nvv == 2 && P.nvs == 2)
+    if (P.occ.ntri)   // occluders: shadow tests (generic sample counts only)
+        hipLaunchKernelGGL((k_build_R<-1, -1, true>), grid, block, 0, s, recs, ids, nrows, vp, nvrl, chunk, P, normalization, Rt, ld, row0, counter);
+    else if (P.nvv == 2 && P.nvs == 2)
         hipLaunchKernelGGL((k_build_R<2, 2>), grid, block, 0, s, recs, ids, nrows, vp, nvrl, chunk,
                            P, normalization, Rt, ld, row0, counter);
     else
@@ -400,7 +406,9 @@ hipError_t launch_build_R_blocks(const Rec* recs, const uint32_t* ids, uint32_t 
     if (nrows == 0 || nvrl == 0) return hipSuccess;
     const uint32_t chunk = 256;
     const dim3 grid((nrows + 63) / 64, (nvrl + chunk - 1) / chunk), block(256);
-    if (P.nvv == 2 && P.nvs == 2)
+    if (P.occ.ntri)   // occluders: shadow tests (generic sample counts only)
+        hipLaunchKernelGGL((k_build_R_blocks<-1, -1, true>), grid, block, 0, s, recs, ids, nrows, vp, nvrl, chunk, P, normalization, Rt, roff, rstride, nonzero, counter);
+    else if (P.nvv == 2 && P.nvs == 2)
         hipLaunchKernelGGL((k_build_R_blocks<2, 2>), grid, block, 0, s, recs, ids, nrows, vp, nvrl, chunk,
                            P, normalization, Rt, roff, rstride, nonzero, counter);
     else

@@ -32,6 +32,8 @@ SmokeBox to_box(const alvrl_scene_desc& s)
     b.medium.phase_type = s.medium.phase_type;
     b.medium.phase_g = s.medium.phase_g;
     b.medium.resolve();
+    if (s.occluders && s.n_occluders) b.occ.assign(s.occluders, s.occluders + 9 * (size_t)s.n_occluders);
+    for (int i = 0; i < 3; i++) b.occ_albedo[i] = s.occluder_albedo[i];
     return b;
 }
 }  // namespace host
@@ -63,6 +65,9 @@ ALVRL_API void alvrl_scene_default(alvrl_scene_desc* s, int width, int height)
     s->medium.sampling_weight = -1.0f;
     s->medium.phase_type = 0;
     s->medium.phase_g = 0.0f;
+    s->occluders = nullptr;
+    s->n_occluders = 0;
+    for (int i = 0; i < 3; i++) s->occluder_albedo[i] = b.occ_albedo[i];
 }
 
 ALVRL_API int alvrl_scene_records(const alvrl_scene_desc* s, int medium_scatters, const uint32_t* ids,

@@ -41,7 +41,7 @@ void MediumParams::resolve()
     sampling_weight = w;
 }
 
-void SmokeBox::camera_ray(float px, float py, V3* o, V3* d) const
+void SmokeBox::camera_ray(float px, float py, V3* o, V3* d, float* mint) const
 {
     const V3 fwd = normalize(cam_target - cam_origin);
     const V3 left = normalize(cross(cam_up, fwd));
@@ -53,6 +53,7 @@ void SmokeBox::camera_ray(float px, float py, V3* o, V3* d) const
     const float xc = (1.0f - 2.0f * sx) * tanh_;
     const float yc = ((1.0f - 2.0f * sy) / aspect) * tanh_;
     const V3 dc = normalize(v3(xc, yc, 1.0f));
+    if (mint) *mint = 1e-2f * (1.0f / dc.z);
     *o = cam_origin;
     *d = v3(left.x * dc.x + nup.x * dc.y + fwd.x * dc.z,
             left.y * dc.x + nup.y * dc.y + fwd.y * dc.z,
@@ -77,20 +78,88 @@ float SmokeBox::box_hit(V3 o, V3 d, V3* n) const
     return best;
 }
 
+bool tri_intersect(const float* tri, V3 o, V3 d, float* u, float* v, float* t)
+{
+    const V3 p0 = v3(tri[0], tri[1], tri[2]), p1 = v3(tri[3], tri[4], tri[5]), p2 = v3(tri[6], tri[7], tri[8]);
+    const V3 edge1 = p1 - p0, edge2 = p2 - p0;
+    const V3 pvec = cross(d, edge2);
+    const float det = dot(edge1, pvec);
+    if (det == 0) return false;
+    const float inv_det = 1.0f / det;
+    const V3 tvec = o - p0;
+    *u = dot(tvec, pvec) * inv_det;
+    if (*u < 0.0f || *u > 1.0f) return false;
+    const V3 qvec = cross(tvec, edge1);
+    *v = dot(d, qvec) * inv_det;
+    if (*v >= 0.0f && *u + *v <= 1.0f) {   // inverted comparison (catches NaNs)
+        *t = dot(edge2, qvec) * inv_det;
+        return true;
+    }
+    return false;
+}
+
+float SmokeBox::first_hit(V3 o, V3 d, float mint, V3* n, V3* p, int* tri) const
+{
+    float best = box_hit(o, d, n);
+    int bi = -1;
+    float bu = 0.0f, bv = 0.0f;
+    const uint32_t nt = n_occ();
+    for (uint32_t i = 0; i < nt; i++) {   // shape kd-tree leaf test, t in [mint, maxt] (skdtree.h:248-262)
+        float u, v, t;
+        if (!tri_intersect(&occ[9 * (size_t)i], o, d, &u, &v, &t)) continue;
+        if (t < mint || !(t < best)) continue;
+        best = t; bi = (int)i; bu = u; bv = v;
+    }
+    *tri = bi;
+    if (bi < 0) {
+        *p = o + d * best;
+        return best;
+    }
+    // fillIntersectionRecord (skdtree.h:350-396): barycentric position, face normal
+    const float* q = &occ[9 * (size_t)bi];
+    const V3 p0 = v3(q[0], q[1], q[2]), p1 = v3(q[3], q[4], q[5]), p2 = v3(q[6], q[7], q[8]);
+    const float b0 = 1 - bu - bv;
+    *p = (p0 * b0 + p1 * bu) + p2 * bv;
+    V3 fn = cross(p1 - p0, p2 - p0);
+    const float len = length(fn);
+    if (!(fn.x == 0 && fn.y == 0 && fn.z == 0)) fn = fn * (1.0f / len);
+    *n = fn;
+    return best;
+}
+
+bool SmokeBox::visible(V3 p1, bool p1_surface, V3 p2, bool p2_surface) const
+{
+    const uint32_t nt = n_occ();
+    if (nt == 0) return true;
+    V3 d = p2 - p1;
+    const float remaining = length(d);
+    if (!(remaining > 0)) return true;   // the loop of scene.cpp:634 does not run
+    d = d * (1.0f / remaining);
+    const float mint = p1_surface ? 1e-4f : 0.0f;                     // Epsilon
+    const float maxt = remaining * (p2_surface ? (1 - 1e-3f) : 1.0f);   // ShadowEpsilon
+    for (uint32_t i = 0; i < nt; i++) {
+        float u, v, t;
+        if (tri_intersect(&occ[9 * (size_t)i], p1, d, &u, &v, &t) && !(t < mint || t > maxt)) return false;
+    }
+    return true;
+}
+
 void SmokeBox::make_record(int x, int y, bool medium_scatters, float rec[16]) const
 {
-    V3 O, D, n;
-    camera_ray((float)x + 0.5f, (float)y + 0.5f, &O, &D);   // renderBlock pixel centre, integrator.cpp:243-245
-    const float t = box_hit(O, D, &n);
-    const V3 p = O + D * t;
+    V3 O, D, n, p;
+    float mint;
+    camera_ray((float)x + 0.5f, (float)y + 0.5f, &O, &D, &mint);   // renderBlock pixel centre, integrator.cpp:243-245
+    int tri;
+    const float t = first_hit(O, D, mint, &n, &p, &tri);
     uint32_t flags = 0;
     if (std::isfinite(t)) flags |= 1u | 2u;
     if (medium_scatters) flags |= 4u;
+    const float* a = tri >= 0 ? occ_albedo : albedo;
     rec[0] = O.x; rec[1] = O.y; rec[2] = O.z;
     rec[3] = D.x; rec[4] = D.y; rec[5] = D.z;
     rec[6] = p.x; rec[7] = p.y; rec[8] = p.z;
     rec[9] = n.x; rec[10] = n.y; rec[11] = n.z;
-    rec[12] = albedo[0]; rec[13] = albedo[1]; rec[14] = albedo[2];
+    rec[12] = a[0]; rec[13] = a[1]; rec[14] = a[2];
     std::memcpy(&rec[15], &flags, 4);
 }
 
@@ -207,9 +276,11 @@ void trace_particle(const SmokeBox& sc, Stream& smp, bool short_vrls, int max_de
     float thr[3] = {1.0f, 1.0f, 1.0f};
     const float eta = 1.0f;
     const float w = m.sampling_weight;
+    float mint = 1e-4f;   // Ray() default mint (Epsilon), then 0 after a medium and Epsilon after a surface
     while (!(thr[0] == 0 && thr[1] == 0 && thr[2] == 0) && (depth <= max_depth || max_depth < 0)) {
-        V3 n;
-        const float its_t = sc.box_hit(o, dir, &n);
+        V3 n, hp;
+        int tri;
+        const float its_t = sc.first_hit(o, dir, mint, &n, &hp, &tri);
         const bool its_valid = std::isfinite(its_t);
         // HomogeneousMedium::sampleDistance (homogeneous.cpp:275-352), balance
         float rnd = smp.next(), sampled;
@@ -252,15 +323,16 @@ void trace_particle(const SmokeBox& sc, Stream& smp, bool short_vrls, int max_de
             for (int i = 0; i < 3; i++) thr[i] *= mtr[i] * m.sigma_s[i] * rps;
             const float px_ = smp.next(), py_ = smp.next();
             const V3 wo = uniform_sphere(px_, py_);
-            const V3 endPoint = short_vrls ? mp : o + dir * its_t;
+            const V3 endPoint = short_vrls ? mp : hp;
             k.end_current(endPoint);
             k.start = mp;
             for (int i = 0; i < 3; i++) k.power[i] = thr[i] * power[i];
-            o = mp; dir = wo;
+            o = mp; dir = wo; mint = 0.0f;
         } else if (its_valid) {   // vrlTracer.h:173-213
             const float rpf = 1.0f / pf;
             for (int i = 0; i < 3; i++) thr[i] *= mtr[i] * rpf;
-            const V3 p = o + dir * its_t;
+            const V3 p = hp;
+            const float* alb = tri >= 0 ? sc.occ_albedo : sc.albedo;
             V3 fs, ft;
             frame_of(n, &fs, &ft);
             const V3 mwi = -dir;
@@ -270,7 +342,7 @@ void trace_particle(const SmokeBox& sc, Stream& smp, bool short_vrls, int max_de
             V3 wol = v3(0, 0, 0);
             if (!(cos_wi <= 0)) {
                 wol = cosine_hemisphere(bx, by);
-                for (int i = 0; i < 3; i++) bw[i] = sc.albedo[i];
+                for (int i = 0; i < 3; i++) bw[i] = alb[i];
             }
             if (bw[0] == 0 && bw[1] == 0 && bw[2] == 0) { k.end_current(p); break; }
             const V3 wo = (fs * wol.x + ft * wol.y) + n * wol.z;
@@ -280,7 +352,7 @@ void trace_particle(const SmokeBox& sc, Stream& smp, bool short_vrls, int max_de
             k.end_current(p);
             k.start = p;
             for (int i = 0; i < 3; i++) k.power[i] = thr[i] * power[i];
-            o = p; dir = wo;
+            o = p; dir = wo; mint = 1e-4f;
         } else {
             break;
         }

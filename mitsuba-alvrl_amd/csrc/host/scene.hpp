@@ -4,8 +4,13 @@
 // needs them):
 //   perspective pinhole  src/sensors/perspective.cpp:126-155, 247-269
 //   ray / box walls      one-sided diffuse walls of an axis-aligned box, seen
-//                        from inside (no interior occluders => every interior
-//                        pair is mutually visible, scene.cpp:619-679)
+//                        from inside
+//   occluders            optional triangles inside the box (a TriMesh with a
+//                        one-sided diffuse BSDF): TriangleT::rayIntersect
+//                        (include/mitsuba/core/triangle.h:109-145), the hit
+//                        record of skdtree.h:350-396, and the visibility
+//                        part of Scene::evalTransmittance (scene.cpp:619-679);
+//                        without them every interior pair is mutually visible
 //   point light          src/emitters/point.cpp:81-106
 //   homogeneous fog      src/medium/homogeneous.cpp (balance strategy)
 #pragma once
@@ -51,15 +56,30 @@ struct SmokeBox {
     V3 light_pos = v3(0.0f, 0.8f, 0.0f);
     float light_intensity[3] = {10.0f, 10.0f, 10.0f};
     MediumParams medium;
+    std::vector<float> occ;           // occluder triangles, 9 floats each (p0, p1, p2)
+    float occ_albedo[3] = {0.5f, 0.5f, 0.5f};
 
-    // Sensor::sampleRay through pixel sample (px, py).
-    void camera_ray(float px, float py, V3* o, V3* d) const;
+    // Sensor::sampleRay through pixel sample (px, py); *mint = nearClip / d.z
+    // in camera space (perspective.cpp:247-263, nearClip 1e-2).
+    void camera_ray(float px, float py, V3* o, V3* d, float* mint = nullptr) const;
     // First hit of a ray starting inside the box: t and inward normal.
     float box_hit(V3 o, V3 d, V3* n) const;
+    // Scene::rayIntersect over the walls and the occluders, t >= mint; the
+    // walls win ties, then the lowest triangle index.  *tri = -1 for a wall;
+    // *p = its.p (ray(t) for a wall, barycentric for a triangle).
+    float first_hit(V3 o, V3 d, float mint, V3* n, V3* p, int* tri) const;
+    // The occluder part of Scene::evalTransmittance(p1, p1OnSurface, p2,
+    // p2OnSurface): false if a triangle lies on the segment (the walls
+    // cannot: both points are inside the box).
+    bool visible(V3 p1, bool p1_surface, V3 p2, bool p2_surface) const;
+    uint32_t n_occ() const { return (uint32_t)(occ.size() / 9); }
     // Gather record (alvrl_gather_rec layout) of pixel centre (x, y).
     void make_record(int x, int y, bool medium_scatters, float rec[16]) const;
     float scene_diagonal() const;   // distance(getAABB().min, getAABB().max)
 };
+
+// TriangleT::rayIntersect (triangle.h:109-145): t of the hit, or false.
+bool tri_intersect(const float* tri, V3 o, V3 d, float* u, float* v, float* t);
 
 // vrlVector: SoA planes (start xyz, end xyz, power rgb), VRL.h:105-194.
 struct VrlSet {

@@ -212,9 +212,12 @@ struct alvrl_integrator {
     {
         scene = to_box(s);
         scene_desc = s;
+        scene_desc.occluders = scene.occ.empty() ? nullptr : scene.occ.data();   // the owned copy
+        scene_desc.n_occluders = scene.n_occ();
         have_scene = true;
         alvrl_medium_desc md = s.medium;
         chk(alvrl_set_medium(ctx, &md), "alvrl_set_medium");
+        chk(alvrl_set_occluders(ctx, scene_desc.occluders, scene_desc.n_occluders), "alvrl_set_occluders");
         if (!vrlFile.empty()) {   // :243-252
             std::string err;
             if (!read_vrl_file(vrlFile.c_str(), scene.medium, &vrls, &err)) throw IntegError(ALVRL_ERR_INVALID, err);
@@ -353,8 +356,8 @@ struct alvrl_integrator {
         row_base.assign(rows, UINT64_MAX);
         row_stride.assign(rows, 0);
         // records of the representative pixel centres (sensor->sampleRay at
-        // the pixel centre, :327-328 / :1060-1061); RNG id = row-major pixel id
-        std::vector<alvrl_gather_rec> h;
+        // the pixel centre, :327-328 / :1060-1061), formed on the device from
+        // the row-major pixel ids (the RNG ids too)
         std::vector<uint32_t> ids, bstr;
         std::vector<uint64_t> boff;
         uint64_t acc = 0;
@@ -365,15 +368,13 @@ struct alvrl_integrator {
                 row_base[g] = (uint64_t)nv * acc + (g - roff[s2]);
                 row_stride[g] = n;
                 const uint32_t x = rpix[g] / (uint32_t)H, y = rpix[g] % (uint32_t)H;
-                h.emplace_back();
-                scene.make_record((int)x, (int)y, scat, reinterpret_cast<float*>(&h.back()));
                 ids.push_back(y * (uint32_t)W + x);
                 boff.push_back(row_base[g]);
                 bstr.push_back(n);
             }
             acc += n;
         }
-        const uint32_t nb = (uint32_t)h.size();
+        const uint32_t nb = (uint32_t)ids.size();
         rows_built = nb;
         rep_recs.ensure(nb);
         rep_ids.ensure(nb);
@@ -382,8 +383,8 @@ struct alvrl_integrator {
         nz_dev.ensure(nv);
         Rt.ensure((size_t)2 * nv * acc);
         if (nb) {
-            hchk(hipMemcpyAsync(rep_recs.p, h.data(), sizeof(alvrl_gather_rec) * nb, hipMemcpyHostToDevice, stream), "copy rep records");
             hchk(hipMemcpyAsync(rep_ids.p, ids.data(), sizeof(uint32_t) * nb, hipMemcpyHostToDevice, stream), "copy rep ids");
+            chk_host(alvrl_scene_records_gpu(&scene_desc, scat ? 1 : 0, rep_ids.p, nb, rep_recs.p, stream));
             hchk(hipMemcpyAsync(rb_off.p, boff.data(), sizeof(uint64_t) * nb, hipMemcpyHostToDevice, stream), "copy row offsets");
             hchk(hipMemcpyAsync(rb_stride.p, bstr.data(), sizeof(uint32_t) * nb, hipMemcpyHostToDevice, stream), "copy row strides");
         }
@@ -632,18 +633,15 @@ struct alvrl_integrator {
             const uint32_t n = alvrl_make_work_items(s2.data(), (uint32_t)s2.size(), items.data(), (uint32_t)items.size());
             items.resize(n);
         }
-        std::vector<alvrl_gather_rec> recs(pix.size());
         const bool scat = !(scene.medium.sigma_s[0] == 0 && scene.medium.sigma_s[1] == 0 && scene.medium.sigma_s[2] == 0);
-        for (size_t i = 0; i < pix.size(); i++)
-            scene.make_record((int)(pix[i] % (uint32_t)W), (int)(pix[i] / (uint32_t)W), scat,
-                              reinterpret_cast<float*>(&recs[i]));
         nrec = (uint32_t)pix.size();
         nitems = (uint32_t)items.size();
         rec_buf.ensure(nrec);
         pix_buf.ensure(nrec);
         out_buf.ensure((size_t)3 * nrec);
-        hchk(hipMemcpyAsync(rec_buf.p, recs.data(), sizeof(alvrl_gather_rec) * nrec, hipMemcpyHostToDevice, stream), "copy records");
         hchk(hipMemcpyAsync(pix_buf.p, pix.data(), sizeof(uint32_t) * nrec, hipMemcpyHostToDevice, stream), "copy pixels");
+        // the eye-ray first hits of the owned pixels, on the device
+        chk_host(alvrl_scene_records_gpu(&scene_desc, scat ? 1 : 0, pix_buf.p, nrec, rec_buf.p, stream));
         if (nitems) {
             item_buf.ensure(nitems);
             hchk(hipMemcpyAsync(item_buf.p, items.data(), sizeof(alvrl_work_item) * nitems, hipMemcpyHostToDevice, stream), "copy items");

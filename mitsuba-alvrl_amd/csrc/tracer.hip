@@ -19,6 +19,8 @@
 #include <vector>
 
 #include "alvrl_host.h"
+#include "bvh_device.hpp"
+#include "host/bvh.hpp"
 #include "host/scene.hpp"
 
 namespace alvrl {
@@ -38,6 +40,8 @@ struct TScene {
     float box_min[3], box_max[3], albedo[3];
     float sigma_s[3], sigma_t[3], w;
     int sigma_s_zero;
+    alvrl::bvh::View bv;          // occluders (ntri == 0: none)
+    float occ_albedo[3];
 };
 
 struct F3 { float x, y, z; };
@@ -131,6 +135,31 @@ __device__ float box_hit(const TScene& sc, F3 o, F3 d, F3* n)   // first wall hi
     return best;
 }
 
+// Scene::rayIntersect over the walls and the occluders (host SmokeBox::first_hit):
+// t, normal, its.p (ray(t) on a wall, barycentric on a triangle), occluder or not
+__device__ float first_hit(const TScene& sc, F3 o, F3 d, float mint, F3* n, F3* p, bool* occ)
+{
+    float best = box_hit(sc, o, d, n);
+    int id = -1, slot = -1;
+    float bu = 0.0f, bv = 0.0f;
+    alvrl::bvh::closest(sc.bv, alvrl::bvh::mk(o.x, o.y, o.z), alvrl::bvh::mk(d.x, d.y, d.z), mint, &best, &id, &slot,
+                        &bu, &bv);
+    *occ = id >= 0;
+    if (id < 0) {
+        *p = add(o, mul(d, best));
+        return best;
+    }
+    const float* q = sc.bv.tris + 9 * (size_t)slot;
+    const F3 p0 = f3(q[0], q[1], q[2]), p1 = f3(q[3], q[4], q[5]), p2 = f3(q[6], q[7], q[8]);
+    const float b0 = 1 - bu - bv;
+    *p = add(add(mul(p0, b0), mul(p1, bu)), mul(p2, bv));
+    F3 fn = cross(sub(p1, p0), sub(p2, p0));
+    const float l = len(fn);
+    if (!(fn.x == 0 && fn.y == 0 && fn.z == 0)) fn = mul(fn, 1.0f / l);
+    *n = fn;
+    return best;
+}
+
 // vrlVector::put + the current VRL (vrlTracer.h:56-89, VRL.h:148-158); counts,
 // or writes into the SoA planes at 'pos' when soa != nullptr
 struct Sink {
@@ -173,9 +202,11 @@ __device__ void trace_particle(const TScene& sc, Stream& smp, bool short_vrls, i
     float thr[3] = {1.0f, 1.0f, 1.0f};
     const float eta = 1.0f;
     const float w = sc.w;
+    float mint = 1e-4f;   // Ray() default mint (Epsilon), then 0 after a medium and Epsilon after a surface
     while (!(thr[0] == 0 && thr[1] == 0 && thr[2] == 0) && (depth <= max_depth || max_depth < 0)) {
-        F3 n;
-        const float its_t = box_hit(sc, o, dir, &n);
+        F3 n, hp;
+        bool hit_occ;
+        const float its_t = first_hit(sc, o, dir, mint, &n, &hp, &hit_occ);
         const bool its_valid = isfinite(its_t);
         // HomogeneousMedium::sampleDistance (homogeneous.cpp:275-352), balance
         float rnd = smp.next(), sampled;
@@ -218,15 +249,16 @@ __device__ void trace_particle(const TScene& sc, Stream& smp, bool short_vrls, i
             for (int i = 0; i < 3; i++) thr[i] *= mtr[i] * sc.sigma_s[i] * rps;
             const float px_ = smp.next(), py_ = smp.next();
             const F3 wo = uniform_sphere(px_, py_);
-            const F3 endPoint = short_vrls ? mp : add(o, mul(dir, its_t));
+            const F3 endPoint = short_vrls ? mp : hp;
             k.end_current(endPoint);
             k.start = mp;
             for (int i = 0; i < 3; i++) k.power[i] = thr[i] * sc.power[i];
-            o = mp; dir = wo;
+            o = mp; dir = wo; mint = 0.0f;
         } else if (its_valid) {   // vrlTracer.h:173-213
             const float rpf = 1.0f / pf;
             for (int i = 0; i < 3; i++) thr[i] *= mtr[i] * rpf;
-            const F3 p = add(o, mul(dir, its_t));
+            const F3 p = hp;
+            const float* alb = hit_occ ? sc.occ_albedo : sc.albedo;
             F3 fs, ft;
             frame_of(n, &fs, &ft);
             const F3 mwi = f3(-dir.x, -dir.y, -dir.z);
@@ -236,7 +268,7 @@ __device__ void trace_particle(const TScene& sc, Stream& smp, bool short_vrls, i
             F3 wol = f3(0, 0, 0);
             if (!(cos_wi <= 0)) {
                 wol = cosine_hemisphere(bx, by);
-                for (int i = 0; i < 3; i++) bw[i] = sc.albedo[i];
+                for (int i = 0; i < 3; i++) bw[i] = alb[i];
             }
             if (bw[0] == 0 && bw[1] == 0 && bw[2] == 0) { k.end_current(p); break; }
             const F3 wo = add(add(mul(fs, wol.x), mul(ft, wol.y)), mul(n, wol.z));
@@ -246,7 +278,7 @@ __device__ void trace_particle(const TScene& sc, Stream& smp, bool short_vrls, i
             k.end_current(p);
             k.start = p;
             for (int i = 0; i < 3; i++) k.power[i] = thr[i] * sc.power[i];
-            o = p; dir = wo;
+            o = p; dir = wo; mint = 1e-4f;
         } else {
             break;
         }
@@ -308,9 +340,133 @@ struct DMem {
     hipError_t alloc(size_t n) { return hipMalloc(&p, std::max<size_t>(n, 1) * sizeof(T)); }
 };
 
+// The scene's occluder BVH on the device (built on the host, host/bvh.cpp).
+struct DevBvh {
+    DMem<alvrl::BvhNode> nodes;
+    DMem<float> tris;
+    DMem<uint32_t> ids;
+    alvrl::bvh::View view{nullptr, nullptr, nullptr, 0u};
+    hipError_t upload(const std::vector<float>& occ)
+    {
+        const uint32_t nt = (uint32_t)(occ.size() / 9);
+        if (nt == 0) return hipSuccess;
+        const alvrl::BvhHost b = alvrl::build_bvh(occ.data(), nt);
+        hipError_t e = nodes.alloc(b.nodes.size());
+        if (e == hipSuccess) e = tris.alloc(b.tris.size());
+        if (e == hipSuccess) e = ids.alloc(b.ids.size());
+        if (e == hipSuccess) e = hipMemcpy(nodes.p, b.nodes.data(), b.nodes.size() * sizeof(alvrl::BvhNode), hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemcpy(tris.p, b.tris.data(), b.tris.size() * 4, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemcpy(ids.p, b.ids.data(), b.ids.size() * 4, hipMemcpyHostToDevice);
+        if (e == hipSuccess) view = alvrl::bvh::View{nodes.p, tris.p, ids.p, nt};
+        return e;
+    }
+};
+
+// The camera of SmokeBox::camera_ray with its per-scene terms formed on the
+// host (the same float operations, so the same values).
+struct TCam {
+    float o[3], fwd[3], left[3], nup[3];
+    float tanh_, aspect, inv_w, inv_h;
+    uint32_t width;
+    int scat;
+};
+
+// Sensor::sampleRay at the pixel centre + Scene::rayIntersect (host
+// SmokeBox::make_record, bit for bit): the GPU eye-ray first hit of SURVEY
+// 8(f) row 1.  pix == nullptr: pixel i.
+__global__ void __launch_bounds__(256) k_eye_records(TCam c, TScene sc, const uint32_t* __restrict__ pix,
+                                                     uint32_t n, float* __restrict__ out)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t id = pix ? pix[i] : i;
+    const float px = (float)(id % c.width) + 0.5f, py = (float)(id / c.width) + 0.5f;
+    const float sx = px * c.inv_w, sy = py * c.inv_h;
+    const float xc = (1.0f - 2.0f * sx) * c.tanh_;
+    const float yc = ((1.0f - 2.0f * sy) / c.aspect) * c.tanh_;
+    F3 dc = f3(xc, yc, 1.0f);
+    dc = mul(dc, 1.0f / len(dc));
+    const float mint = 1e-2f * (1.0f / dc.z);
+    const F3 O = f3(c.o[0], c.o[1], c.o[2]);
+    const F3 D = f3(c.left[0] * dc.x + c.nup[0] * dc.y + c.fwd[0] * dc.z,
+                    c.left[1] * dc.x + c.nup[1] * dc.y + c.fwd[1] * dc.z,
+                    c.left[2] * dc.x + c.nup[2] * dc.y + c.fwd[2] * dc.z);
+    F3 nn, p;
+    bool occ;
+    const float t = first_hit(sc, O, D, mint, &nn, &p, &occ);
+    uint32_t flags = 0;
+    if (isfinite(t)) flags |= 1u | 2u;
+    if (c.scat) flags |= 4u;
+    const float* a = occ ? sc.occ_albedo : sc.albedo;
+    float* r = out + 16 * (size_t)i;
+    const float v[15] = {O.x, O.y, O.z, D.x, D.y, D.z, p.x, p.y, p.z, nn.x, nn.y, nn.z, a[0], a[1], a[2]};
+#pragma unroll
+    for (int k = 0; k < 15; k++) r[k] = v[k];
+    r[15] = __uint_as_float(flags);
+}
+
+TScene make_tscene(const alvrl::host::SmokeBox& box)
+{
+    TScene sc;
+    sc.light_pos[0] = box.light_pos.x; sc.light_pos[1] = box.light_pos.y; sc.light_pos[2] = box.light_pos.z;
+    for (int i = 0; i < 3; i++) {
+        sc.power[i] = box.light_intensity[i] * (float)(4 * kPi);
+        sc.box_min[i] = box.box_min[i]; sc.box_max[i] = box.box_max[i];
+        sc.albedo[i] = box.albedo[i];
+        sc.sigma_s[i] = box.medium.sigma_s[i];
+        sc.sigma_t[i] = box.medium.sigma_t[i];
+        sc.occ_albedo[i] = box.occ_albedo[i];
+    }
+    sc.w = box.medium.sampling_weight;
+    sc.sigma_s_zero = (sc.sigma_s[0] == 0 && sc.sigma_s[1] == 0 && sc.sigma_s[2] == 0) ? 1 : 0;
+    sc.bv = alvrl::bvh::View{nullptr, nullptr, nullptr, 0u};
+    return sc;
+}
+
 }  // namespace
 
 extern "C" {
+
+// Gather records of pixel centres on the current HIP device (the host
+// alvrl_scene_records, bit for bit).  d_pixel_ids (device, row-major y*W+x)
+// may be NULL: pixels 0..n-1.  d_out: n device records.  Stream-ordered on
+// 'stream' (the occluder BVH is built and uploaded synchronously first).
+ALVRL_API int alvrl_scene_records_gpu(const alvrl_scene_desc* s, int medium_scatters, const uint32_t* d_pixel_ids,
+                                      uint32_t n, alvrl_gather_rec* d_out, void* stream)
+{
+    if (!s || (!d_out && n)) return terr(ALVRL_ERR_INVALID, "alvrl_scene_records_gpu: null argument");
+    const alvrl::host::SmokeBox box = alvrl::host::to_box(*s);
+    const uint64_t npix = (uint64_t)box.width * (uint64_t)box.height;
+    if (!d_pixel_ids && n > npix) return terr(ALVRL_ERR_INVALID, "alvrl_scene_records_gpu: n > W*H without pixel ids");
+    if (n == 0) return ALVRL_OK;
+    TScene sc = make_tscene(box);
+    DevBvh bv;
+    if (bv.upload(box.occ) != hipSuccess) return terr(ALVRL_ERR_HIP, "alvrl_scene_records_gpu: BVH upload");
+    sc.bv = bv.view;
+    TCam c;
+    {
+        using namespace alvrl::host;
+        const V3 fwd = normalize(box.cam_target - box.cam_origin);
+        const V3 left = normalize(cross(box.cam_up, fwd));
+        const V3 nup = cross(fwd, left);
+        const float vv[4][3] = {{box.cam_origin.x, box.cam_origin.y, box.cam_origin.z}, {fwd.x, fwd.y, fwd.z},
+                                {left.x, left.y, left.z}, {nup.x, nup.y, nup.z}};
+        for (int k = 0; k < 3; k++) { c.o[k] = vv[0][k]; c.fwd[k] = vv[1][k]; c.left[k] = vv[2][k]; c.nup[k] = vv[3][k]; }
+        c.aspect = (float)box.width / (float)box.height;
+        c.tanh_ = std::tan(0.5f * box.fov_x_deg * (float)(kPi / 180.0));
+        c.inv_w = 1.0f / (float)box.width;
+        c.inv_h = 1.0f / (float)box.height;
+        c.width = (uint32_t)box.width;
+        c.scat = medium_scatters && !sc.sigma_s_zero ? 1 : 0;
+    }
+    hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL(k_eye_records, dim3((n + 255) / 256), dim3(256), 0, st, c, sc, d_pixel_ids, n,
+                       reinterpret_cast<float*>(d_out));
+    if (hipGetLastError() != hipSuccess) return terr(ALVRL_ERR_HIP, "alvrl_scene_records_gpu: launch");
+    // the BVH buffers are freed on return: wait for the kernel that reads them
+    if (hipStreamSynchronize(st) != hipSuccess) return terr(ALVRL_ERR_HIP, "alvrl_scene_records_gpu: sync");
+    return ALVRL_OK;
+}
 
 // The GPU form of alvrl_trace_vrls (same arguments and results); runs on the
 // current HIP device.
@@ -321,17 +477,10 @@ ALVRL_API int alvrl_trace_vrls_gpu(const alvrl_scene_desc* s, uint32_t seed, uin
     if (!s || !n || !particles) return terr(ALVRL_ERR_INVALID, "alvrl_trace_vrls_gpu: null argument");
     // the scene as the host tracer resolves it (to_box + MediumParams::resolve)
     const alvrl::host::SmokeBox box = alvrl::host::to_box(*s);
-    TScene sc;
-    sc.light_pos[0] = box.light_pos.x; sc.light_pos[1] = box.light_pos.y; sc.light_pos[2] = box.light_pos.z;
-    for (int i = 0; i < 3; i++) {
-        sc.power[i] = box.light_intensity[i] * (float)(4 * kPi);
-        sc.box_min[i] = box.box_min[i]; sc.box_max[i] = box.box_max[i];
-        sc.albedo[i] = box.albedo[i];
-        sc.sigma_s[i] = box.medium.sigma_s[i];
-        sc.sigma_t[i] = box.medium.sigma_t[i];
-    }
-    sc.w = box.medium.sampling_weight;
-    sc.sigma_s_zero = (sc.sigma_s[0] == 0 && sc.sigma_s[1] == 0 && sc.sigma_s[2] == 0) ? 1 : 0;
+    TScene sc = make_tscene(box);
+    DevBvh bvh;
+    if (bvh.upload(box.occ) != hipSuccess) return terr(ALVRL_ERR_HIP, "alvrl_trace_vrls_gpu: BVH upload");
+    sc.bv = bvh.view;
     const TArgs a{seed, pass, short_vrls, max_depth, rr_depth};
     *n = 0;
     if (target == 0) { *particles = 0; return ALVRL_OK; }

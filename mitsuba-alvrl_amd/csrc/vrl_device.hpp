@@ -19,6 +19,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "bvh_device.hpp"
+
 namespace alvrl {
 
 constexpr float kEpsilon = 1e-4f;                       // constants.h:27-33
@@ -52,6 +54,7 @@ struct DevParams {
     int short_vrls;
     uint32_t seed, pass;
     int rsamples;           // Rsamples (vrlIntegrator.cpp:194): samples per R entry (0 = 1)
+    bvh::View occ;          // occluders blocking U-V and surface-V (ntri == 0: convex container)
 };
 
 // ---------------------------------------------------------------- RNG --
@@ -359,7 +362,19 @@ __device__ __forceinline__ NovakFrame novak_frame(const RecPre& q, const VrlPrep
 //  * Novak's 1 / sqrt(h^2 + (newV sinT)^2) with newV sinT = h sinh(x) is
 //    1 / (h cosh(x)).
 // Directions (VU) are formed only for the HG phase function / the BSDF cosine.
-template <int NVV, int NVS, bool WANT_STATS>
+// VIS: occluders present (Scene::evalTransmittance's occluder test,
+// scene.cpp:619-679: from U (a medium point, mint 0) or the surface point
+// (mint Epsilon) to V, the whole segment).
+__device__ __forceinline__ bool blocked(const DevParams& P, F3 p1, bool p1_surface, F3 p2)
+{
+    const F3 d = p2 - p1;
+    const float rem = len(d);
+    if (!(rem > 0.0f)) return false;
+    const F3 dn = d * (1.0f / rem);
+    return bvh::occluded(P.occ, bvh::mk(p1.x, p1.y, p1.z), bvh::mk(dn.x, dn.y, dn.z), p1_surface ? 1e-4f : 0.0f, rem);
+}
+
+template <int NVV, int NVS, bool WANT_STATS, bool VIS = false>
 __device__ __forceinline__ void integrate_vrl(const DevParams& P, const RecPre& q, const VrlPrep& v,
                                               uint32_t rec_id, uint32_t vrl_id, uint32_t domain,
                                               int nvv_rt, int nvs_rt, float out[3], float* mean_out,
@@ -414,7 +429,7 @@ __device__ __forceinline__ void integrate_vrl(const DevParams& P, const RecPre& 
         const KullaFrame ke = kulla_frame(q.E, q.dirAB, q.lenAB, V);
         const float t = kulla_t(ke, u1);
         const float l2 = fmaf(ke.Dis, ke.Dis, t * t);
-        if (l2 != 0) {
+        if (l2 != 0 && !(VIS && blocked(P, q.E + q.dirAB * (ke.dotPr + t), false, V))) {
             const float dUV = sqrtf(l2);
             float tuv[3];
             tuv[0] = P.sigma_t[0] != 0 ? __expf(P.sigma_t[0] * (0.0f - dUV)) : 1.0f;
@@ -478,7 +493,7 @@ __device__ __forceinline__ void integrate_vrl(const DevParams& P, const RecPre& 
                 const float u = draw(2 * nVV + sample);
                 const float t = kulla_t(ks, u);
                 const float l2 = fmaf(ks.Dis, ks.Dis, t * t);
-                if (l2 != 0) {
+                if (l2 != 0 && !(VIS && blocked(P, q.P, true, S + SV * (ks.dotPr + t)))) {
                     const float dUV = sqrtf(l2);
                     const float rdUV = rcp(dUV);
                     float tuv[3], tsv[3], pf;

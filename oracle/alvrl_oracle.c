@@ -178,13 +178,53 @@ static void medium_eval(const alvrl_o_medium *m, float distance, float tr[3], fl
 /* HomogeneousMedium::evalTransmittance (homogeneous.cpp:266-273) as used by
  * Scene::evalTransmittance (scene.cpp:619-679) when no surface blocks the
  * segment (convex container: every interior pair is mutually visible). */
-static void shadow_transmittance(const alvrl_o_medium *m, v3 p1, v3 p2, float tr[3])
+/* TriangleT::rayIntersect, include/mitsuba/core/triangle.h:109-145 */
+static int tri_intersect(const float *tri, v3 o, v3 d, float *u, float *v, float *t)
 {
+    v3 p0 = mk(tri[0], tri[1], tri[2]), p1 = mk(tri[3], tri[4], tri[5]), p2 = mk(tri[6], tri[7], tri[8]);
+    v3 edge1 = sub(p1, p0), edge2 = sub(p2, p0);
+    v3 pvec = cross(d, edge2);
+    float det = dot(edge1, pvec);
+    if (det == 0) return 0;
+    float inv_det = 1.0f / det;
+    v3 tvec = sub(o, p0);
+    *u = dot(tvec, pvec) * inv_det;
+    if (*u < 0.0f || *u > 1.0f) return 0;
+    v3 qvec = cross(tvec, edge1);
+    *v = dot(d, qvec) * inv_det;
+    if (*v >= 0.0f && *u + *v <= 1.0f) { *t = dot(edge2, qvec) * inv_det; return 1; }
+    return 0;
+}
+
+/* The occluder part of Scene::evalTransmittance(p1, p1OnSurface, p2, false)
+ * (scene.cpp:619-679): the segment's ray has mint = Epsilon (1e-4) from a
+ * surface, 0 from a medium point; any triangle hit in [mint, remaining]
+ * blocks.  The box walls cannot (both points are inside). */
+static int segment_visible(const float *occ, uint32_t nocc, v3 p1, int p1_surface, v3 p2)
+{
+    if (!nocc) return 1;
+    v3 d = sub(p2, p1);
+    float remaining = len(d);
+    if (!(remaining > 0)) return 1;
+    d = scl(d, 1.0f / remaining);
+    float mint = p1_surface ? 1e-4f : 0.0f;
+    float maxt = remaining * 1.0f;
+    for (uint32_t i = 0; i < nocc; i++) {
+        float u, v, t;
+        if (tri_intersect(occ + 9 * (size_t)i, p1, d, &u, &v, &t) && !(t < mint || t > maxt)) return 0;
+    }
+    return 1;
+}
+
+static void shadow_transmittance(const alvrl_o_params *P, v3 p1, int p1_surface, v3 p2, float tr[3])
+{
+    const alvrl_o_medium *m = &P->medium;
     v3 d = sub(p2, p1);
     float remaining = len(d);
     float negLength = 0.0f - remaining;
     for (int i = 0; i < 3; i++)
         tr[i] = m->sigma_t[i] != 0 ? fastexp(m->sigma_t[i] * negLength) : 1.0f;
+    if (!segment_visible(P->occ, P->nocc, p1, p1_surface, p2)) tr[0] = tr[1] = tr[2] = 0.0f;
 }
 
 /* isotropic.cpp:76-78, hg.cpp:107-110 */
@@ -365,7 +405,7 @@ static void integrate_vrl_s(const alvrl_o_params *P, const float *rec, uint32_t 
         {
             v3 VU = nrm(sub(U, V));
             float tuv[3], teu[3], tsv[3], pf_eu, pf_sv;
-            shadow_transmittance(m, U, V, tuv);
+            shadow_transmittance(P, U, 0, V, tuv);
             if (tuv[0] == 0 && tuv[1] == 0 && tuv[2] == 0) goto vv_welford;
             medium_eval(m, dist(E, U), teu, &pf_eu);
             medium_eval(m, dist(S, V), tsv, &pf_sv);
@@ -423,7 +463,7 @@ static void integrate_vrl_s(const alvrl_o_params *P, const float *rec, uint32_t 
             if (dist(U, V) != 0) {
                 v3 VU = nrm(sub(U, V));
                 float tuv[3], tsv[3], pf_sv;
-                shadow_transmittance(m, U, V, tuv);
+                shadow_transmittance(P, U, 1, V, tuv);
                 medium_eval(m, dist(S, V), tsv, &pf_sv);
                 /* SmoothDiffuse::eval (diffuse.cpp:110-118), wi = its.wi, wo = toLocal(-VU) */
                 v3 mVU = neg(VU);
@@ -657,6 +697,19 @@ void alvrl_o_camera_ray(const alvrl_o_scene *s, float px, float py, float o[3], 
     d[0] = dw.x; d[1] = dw.y; d[2] = dw.z;
 }
 
+/* ray.mint of sampleRay (perspective.cpp:258-260): nearClip (1e-2) / d.z in camera space */
+static float camera_mint(const alvrl_o_scene *s, float px, float py)
+{
+    float aspect = (float)s->width / (float)s->height;
+    float tanh_ = tanf(0.5f * s->fov_x_deg * (float)(M_PI / 180.0));
+    float sx = px * (1.0f / (float)s->width);
+    float sy = py * (1.0f / (float)s->height);
+    float xc = (1.0f - 2.0f * sx) * tanh_;
+    float yc = ((1.0f - 2.0f * sy) / aspect) * tanh_;
+    v3 dc = nrm(mk(xc, yc, 1.0f));
+    return 1e-2f * (1.0f / dc.z);
+}
+
 /* Ray / inner-box-wall intersection from inside the box.  Returns t and the
  * inward wall normal (the walls' BSDF is one-sided diffuse facing inward). */
 static float box_hit(const alvrl_o_scene *s, v3 o, v3 d, v3 *n)
@@ -677,13 +730,52 @@ static float box_hit(const alvrl_o_scene *s, v3 o, v3 d, v3 *n)
     return best;
 }
 
+/* Scene::rayIntersect over the walls and the occluders (shape kd-tree leaf
+ * test t in [mint, maxt], skdtree.h:248-262; hit record skdtree.h:350-396:
+ * barycentric position, face normal).  Ties: the walls, then the lowest
+ * triangle index (the reference's kd-tree order is unspecified there). */
+static float first_hit(const alvrl_o_scene *s, v3 o, v3 d, float mint, v3 *n, v3 *p, int *tri)
+{
+    float best = box_hit(s, o, d, n);
+    int bi = -1;
+    float bu = 0.0f, bv = 0.0f;
+    for (uint32_t i = 0; i < s->nocc; i++) {
+        float u, v, t;
+        if (!tri_intersect(s->occ + 9 * (size_t)i, o, d, &u, &v, &t)) continue;
+        if (t < mint || !(t < best)) continue;
+        best = t; bi = (int)i; bu = u; bv = v;
+    }
+    *tri = bi;
+    if (bi < 0) { *p = add(o, scl(d, best)); return best; }
+    const float *q = s->occ + 9 * (size_t)bi;
+    v3 p0 = mk(q[0], q[1], q[2]), p1 = mk(q[3], q[4], q[5]), p2 = mk(q[6], q[7], q[8]);
+    float b0 = 1 - bu - bv;
+    *p = add(add(scl(p0, b0), scl(p1, bu)), scl(p2, bv));
+    v3 fn = cross(sub(p1, p0), sub(p2, p0));
+    float l = len(fn);
+    if (!(fn.x == 0 && fn.y == 0 && fn.z == 0)) fn = scl(fn, 1.0f / l);
+    *n = fn;
+    return best;
+}
+
+float alvrl_o_first_hit(const alvrl_o_scene *s, const float o[3], const float d[3], float mint,
+                        float n[3], float p[3], int *tri)
+{
+    v3 nn, pp;
+    float t = first_hit(s, ld3(o), ld3(d), mint, &nn, &pp, tri);
+    n[0] = nn.x; n[1] = nn.y; n[2] = nn.z;
+    p[0] = pp.x; p[1] = pp.y; p[2] = pp.z;
+    return t;
+}
+
 void alvrl_o_make_record(const alvrl_o_scene *s, int medium_scatters, int x, int y, float *rec)
 {
     float o[3], d[3];
     alvrl_o_camera_ray(s, (float)x + 0.5f, (float)y + 0.5f, o, d);
-    v3 O = ld3(o), D = ld3(d), n;
-    float t = box_hit(s, O, D, &n);
-    v3 p = add(O, scl(D, t));
+    v3 O = ld3(o), D = ld3(d), n, p;
+    int tri;
+    float t = first_hit(s, O, D, camera_mint(s, (float)x + 0.5f, (float)y + 0.5f), &n, &p, &tri);
+    const float *alb = tri >= 0 ? s->occ_albedo : s->albedo;
     uint32_t flags = 0;
     if (isfinite(t)) flags |= ALVRL_O_FLAG_HIT | ALVRL_O_FLAG_SMOOTH;
     if (medium_scatters) flags |= ALVRL_O_FLAG_MEDIUM;
@@ -691,7 +783,7 @@ void alvrl_o_make_record(const alvrl_o_scene *s, int medium_scatters, int x, int
     rec[3] = D.x; rec[4] = D.y; rec[5] = D.z;
     rec[6] = p.x; rec[7] = p.y; rec[8] = p.z;
     rec[9] = n.x; rec[10] = n.y; rec[11] = n.z;
-    rec[12] = s->albedo[0]; rec[13] = s->albedo[1]; rec[14] = s->albedo[2];
+    rec[12] = alb[0]; rec[13] = alb[1]; rec[14] = alb[2];
     memcpy(&rec[15], &flags, 4);
 }
 
@@ -792,9 +884,11 @@ static void trace_particle(const alvrl_o_scene *s, const alvrl_o_medium *m, seq_
     int depth = 1;
     float thr[3] = { 1, 1, 1 };
     float eta = 1.0f;
+    float mint = 1e-4f;   /* Ray() default (Epsilon); 0 after a medium, Epsilon after a surface */
     while (!(thr[0] == 0 && thr[1] == 0 && thr[2] == 0) && (depth <= max_depth || max_depth < 0)) {
-        v3 n;
-        float its_t = box_hit(s, o, dir, &n);
+        v3 n, hp;
+        int tri;
+        float its_t = first_hit(s, o, dir, mint, &n, &hp, &tri);
         int its_valid = isfinite(its_t);
         /* HomogeneousMedium::sampleDistance (homogeneous.cpp:275-352), balance */
         float rnd = seq_next(smp), sampled;
@@ -840,16 +934,17 @@ static void trace_particle(const alvrl_o_scene *s, const alvrl_o_medium *m, seq_
             for (int i = 0; i < 3; i++) thr[i] *= mtr[i] * m->sigma_s[i] * rps;
             float px_ = seq_next(smp), py_ = seq_next(smp);
             v3 wo = uniform_sphere(px_, py_);   /* isotropic phase sample: weight 1 */
-            v3 endPoint = short_vrls ? mp : add(o, scl(dir, its_t));
+            v3 endPoint = short_vrls ? mp : hp;
             end_current(k, endPoint);
             k->start = mp;
             for (int i = 0; i < 3; i++) k->power[i] = thr[i] * power[i];
-            o = mp; dir = wo;
+            o = mp; dir = wo; mint = 0.0f;
         } else if (its_valid) {
             /* surface interaction (vrlTracer.h:173-213) */
             float rpf = 1.0f / pf;
             for (int i = 0; i < 3; i++) thr[i] *= mtr[i] * rpf;
-            v3 p = add(o, scl(dir, its_t));
+            v3 p = hp;
+            const float *alb = tri >= 0 ? s->occ_albedo : s->albedo;
             v3 fs, ft;
             frame_of(n, &fs, &ft);
             v3 mwi = neg(dir);
@@ -859,7 +954,7 @@ static void trace_particle(const alvrl_o_scene *s, const alvrl_o_medium *m, seq_
             v3 wol = mk(0, 0, 0);
             if (!(cos_wi <= 0)) {
                 wol = cosine_hemisphere(bx, by);
-                for (int i = 0; i < 3; i++) bw[i] = s->albedo[i];
+                for (int i = 0; i < 3; i++) bw[i] = alb[i];
             }
             if (bw[0] == 0 && bw[1] == 0 && bw[2] == 0) { end_current(k, p); break; }
             v3 wo = add(add(scl(fs, wol.x), scl(ft, wol.y)), scl(n, wol.z));
@@ -869,7 +964,7 @@ static void trace_particle(const alvrl_o_scene *s, const alvrl_o_medium *m, seq_
             end_current(k, p);
             k->start = p;
             for (int i = 0; i < 3; i++) k->power[i] = thr[i] * power[i];
-            o = p; dir = wo;
+            o = p; dir = wo; mint = 1e-4f;
         } else {
             break;
         }

@@ -81,6 +81,8 @@ typedef struct {
     uint32_t seed;
     uint32_t pass;
     int r_samples;           /* Rsamples (vrlIntegrator.cpp:194): samples per R entry, 0/1 = one */
+    const float *occ;        /* occluder triangles (9 floats each) blocking U-V / surface-V, or NULL */
+    uint32_t nocc;
 } alvrl_o_params;
 
 /* Gather record ("eye segment"): 16 x 32-bit words.
@@ -124,7 +126,15 @@ typedef struct {
     float albedo[3];
     float light_pos[3];
     float light_intensity[3];
+    const float *occ;        /* occluder triangles inside the box (9 floats: p0 p1 p2), or NULL */
+    uint32_t nocc;
+    float occ_albedo[3];     /* their one-sided diffuse reflectance */
 } alvrl_o_scene;
+/* Scene::rayIntersect over walls + occluders (t >= mint; walls win ties, then
+ * the lowest triangle index): t (INFINITY: none), normal, its.p, triangle (-1
+ * = wall). */
+float alvrl_o_first_hit(const alvrl_o_scene *s, const float o[3], const float d[3], float mint,
+                        float n[3], float p[3], int *tri);
 
 void alvrl_o_scene_default(alvrl_o_scene *s, int width, int height);
 /* Eye ray through pixel sample (px, py) (perspective.cpp:247-269 semantics). */

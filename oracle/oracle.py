@@ -36,14 +36,29 @@ class Medium(C.Structure):
 class Params(C.Structure):
     _fields_ = [("medium", Medium), ("vol_vol_samples", C.c_int), ("vol_surf_samples", C.c_int),
                 ("short_vrls", C.c_int), ("seed", C.c_uint32), ("pass_", C.c_uint32),
-                ("r_samples", C.c_int)]
+                ("r_samples", C.c_int), ("occ", C.POINTER(C.c_float)), ("nocc", C.c_uint32)]
 
 
 class Scene(C.Structure):
     _fields_ = [("cam_origin", C.c_float * 3), ("cam_target", C.c_float * 3), ("cam_up", C.c_float * 3),
                 ("fov_x_deg", C.c_float), ("width", C.c_int), ("height", C.c_int),
                 ("box_min", C.c_float * 3), ("box_max", C.c_float * 3), ("albedo", C.c_float * 3),
-                ("light_pos", C.c_float * 3), ("light_intensity", C.c_float * 3)]
+                ("light_pos", C.c_float * 3), ("light_intensity", C.c_float * 3),
+                ("occ", C.POINTER(C.c_float)), ("nocc", C.c_uint32), ("occ_albedo", C.c_float * 3)]
+
+
+def set_occluders(obj, tris, albedo=None):
+    """Occluder triangles ((n, 9) float32) on a Scene (hit by eye rays and
+    particles, occ_albedo) or a Params (blocking the gather's connections).
+    The array is kept alive on the object."""
+    arr = np.ascontiguousarray(np.asarray(tris, np.float32).reshape(-1, 9))
+    obj._occ_keep = arr
+    obj.occ = arr.ctypes.data_as(C.POINTER(C.c_float)) if len(arr) else None
+    obj.nocc = len(arr)
+    if albedo is not None:
+        for i in range(3):
+            obj.occ_albedo[i] = float(albedo[i])
+    return obj
 
 
 class PrepParams(C.Structure):

@@ -74,7 +74,7 @@ def _assert_close(gpu, cpu, what, q50=1e-6, q99=1e-4, q999=2e-3, qmax=5e-2, rmse
     assert rmse <= rmse_rel * max(mean, 1e-30), f"{what}: RMSE {rmse}"
 
 
-def _assert_close_pairs(gpu, cpu, what, q50=1e-6):
+def _assert_close_pairs(gpu, cpu, what, q50=1e-6, csum=1e-3):
     gpu, cpu, err, rel = _rel(gpu, cpu)
     frac = float((rel > 1e-3).mean())
     print(f"[{what}] rel q50={np.median(rel):.2e} frac>1e-3={frac:.2e} max={rel.max():.2e}")
@@ -82,7 +82,7 @@ def _assert_close_pairs(gpu, cpu, what, q50=1e-6):
     cs_g, cs_c = gpu.sum(axis=0), cpu.sum(axis=0)
     crel = np.abs(cs_g - cs_c) / np.maximum(np.abs(cs_c), 1e-30)
     assert ((cs_c == 0) == (cs_g == 0)).all(), f"{what}: zero-column pattern differs"
-    assert crel.max() <= 1e-3, f"{what}: column sums max rel {crel.max()}"
+    assert crel.max() <= csum, f"{what}: column sums max rel {crel.max()}"
 
 
 def test_gather_brute_small(oracle, gpu_ok):
