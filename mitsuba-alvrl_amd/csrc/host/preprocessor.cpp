@@ -138,7 +138,7 @@ inline bool finite3(V3 p) { return std::isfinite(p.x) && std::isfinite(p.y) && s
 
 }  // namespace
 
-std::vector<uint32_t> Preprocessor::build_slices(const SmokeBox& s)
+std::vector<uint32_t> Preprocessor::build_slices(const SmokeBox& s, const float* recs)
 {
     const int W = s.width, H = s.height;
     m_W = W; m_H = H;
@@ -148,8 +148,10 @@ std::vector<uint32_t> Preprocessor::build_slices(const SmokeBox& s)
     const float nan = std::numeric_limits<float>::quiet_NaN();
     for (int i = 0; i < W; i++) {          // pixel order: x outer, y inner (:1140-1141)
         for (int j = 0; j < H; j++) {
-            float rec[16];
-            s.make_record(i, j, true, rec);
+            float own[16];
+            const float* rec = own;
+            if (recs) rec = recs + 16 * ((size_t)j * W + i);
+            else s.make_record(i, j, true, own);
             uint32_t flags;
             std::memcpy(&flags, &rec[15], 4);
             const uint32_t k = (uint32_t)i * H + j;

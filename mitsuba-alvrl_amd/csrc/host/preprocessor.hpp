@@ -27,7 +27,9 @@ public:
 
     // buildSlices (Preprocessor.cpp:1130-1193) + getSlices / getSlicesPQ
     // (:1200-1418).  Returns the pixel -> slice map indexed y + H*x.
-    std::vector<uint32_t> build_slices(const SmokeBox& s);
+    // recs: the W*H gather records in row-major pixel order (the GPU eye-ray
+    // first hits, alvrl_scene_records_gpu), or null to form them here
+    std::vector<uint32_t> build_slices(const SmokeBox& s, const float* recs = nullptr);
     // sampleSliceMapping (:1502-1525): representative pixels per slice (pixel
     // ids in the column-major numbering x*H + y), m_sliceUndersampling,
     // buildLocalities (:1241-1293) and m_globalPixelUndersampling.

@@ -233,7 +233,16 @@ struct alvrl_integrator {
             pp.pass = 0;
             prep.reset(new Preprocessor(pp));
             const double t0 = now_ms();
-            pixel_to_slice = prep->build_slices(scene);
+            // the eye-ray first hit of every pixel on the device (Preprocessor.cpp:1140-1170)
+            const uint32_t npix = (uint32_t)scene.width * (uint32_t)scene.height;
+            DevBuf<alvrl_gather_rec> d_all;
+            d_all.ensure(npix);
+            std::vector<alvrl_gather_rec> h_all(npix);
+            if (npix) {
+                chk_host(alvrl_scene_records_gpu(&scene_desc, 1, nullptr, npix, d_all.p, stream));
+                hchk(hipMemcpy(h_all.data(), d_all.p, sizeof(alvrl_gather_rec) * npix, hipMemcpyDeviceToHost), "copy records");
+            }
+            pixel_to_slice = prep->build_slices(scene, reinterpret_cast<const float*>(h_all.data()));
             st.ms_slices = now_ms() - t0;
             st.slices = prep->num_slices();
         }
