@@ -57,6 +57,24 @@ ALVRL_API int alvrl_scene_records(const alvrl_scene_desc *s, int medium_scatters
  * null stream); returns after they are written. */
 ALVRL_API int alvrl_scene_records_gpu(const alvrl_scene_desc *s, int medium_scatters, const uint32_t *d_pixel_ids,
                                       uint32_t n, alvrl_gather_rec *d_out, void *stream);
+/* ---- reference integrator: volpath with onlyVRLpaths --------------------
+ * VolumetricPathTracer::Li (src/integrators/path/volpath.cpp:110-457) on the
+ * current HIP device: the path-traced ground truth of exactly the light
+ * transport the VRLs represent (eye -> volume or diffuse surface -> volume
+ * -> light path), for statistical checks of the VRL method (SURVEY 8(f)
+ * row 4).  Pixel centres, isotropic phase; counter-RNG stream (seed, pass,
+ * pixel id, sample).  d_out_rgb: 3 floats per pixel, the mean over spp. */
+typedef struct {
+    int max_depth;        /* maxDepth (-1: unbounded) */
+    int rr_depth;         /* rrDepth (5) */
+    int only_vrl_paths;   /* onlyVRLpaths (1) */
+    int vrl_vol_to_vol;   /* vrlVolToVol (1) */
+    int vrl_vol_to_surf;  /* vrlVolToSurf (1) */
+} alvrl_volpath_params;
+ALVRL_API void alvrl_volpath_default(alvrl_volpath_params *p);
+ALVRL_API int alvrl_volpath_render(const alvrl_scene_desc *s, const alvrl_volpath_params *p, uint32_t seed,
+                                   uint32_t pass, uint32_t spp, const uint32_t *d_pixel_ids, uint32_t n,
+                                   float *d_out_rgb, void *stream);
 /* Multi-GPU image partition of alvrl_integrator_render: 64x64 tiles in
  * row-major tile order, tile t owned by rank t % world (the
  * reference's analogue is the block scheduler handing 32x32 blocks to workers,

@@ -463,6 +463,8 @@ def _host():
     L.alvrl_trace_vrls.argtypes = [P(SceneDesc), u32, u32, u32, i32, i32, i32, vp, u32, P(u32), P(u64)]
     L.alvrl_trace_vrls_gpu.argtypes = [P(SceneDesc), u32, u32, u32, i32, i32, i32, vp, u32, P(u32), P(u64)]
     L.alvrl_scene_records_gpu.argtypes = [P(SceneDesc), i32, vp, u32, vp, vp]
+    L.alvrl_volpath_default.argtypes = [P(VolpathParams)]; L.alvrl_volpath_default.restype = None
+    L.alvrl_volpath_render.argtypes = [P(SceneDesc), P(VolpathParams), u32, u32, u32, vp, u32, vp, vp]
     L.alvrl_read_vrl_file.argtypes = [C.c_char_p, P(MediumDesc), vp, u32, P(u32), P(u64)]
     L.alvrl_write_vrl_file.argtypes = [C.c_char_p, vp, u32]
     L.alvrl_tile_pixels.argtypes = [i32, i32, u32, u32, vp, u32, P(u32)]
@@ -572,6 +574,33 @@ def scene_records_gpu(scene: SceneDesc, pixel_ids=None, medium_scatters: bool = 
         stream = torch.cuda.current_stream(dev).cuda_stream
         _hcheck(L.alvrl_scene_records_gpu(C.byref(scene), int(medium_scatters),
                                           None if ids is None else ids.data_ptr(), n, out.data_ptr(), stream))
+    return out
+
+
+class VolpathParams(C.Structure):
+    _fields_ = [("max_depth", C.c_int), ("rr_depth", C.c_int), ("only_vrl_paths", C.c_int),
+                ("vrl_vol_to_vol", C.c_int), ("vrl_vol_to_surf", C.c_int)]
+
+
+def volpath_render(scene: SceneDesc, spp: int, seed: int = 0xA1B2C3D4, pass_: int = 0, pixel_ids=None,
+                   device: int = 0, **params):
+    """alvrl_volpath_render: the volpath onlyVRLpaths reference image (a CUDA
+    tensor (n, 3), means over spp); params: max_depth, rr_depth,
+    only_vrl_paths, vrl_vol_to_vol, vrl_vol_to_surf."""
+    import torch
+    L = _host()
+    vp = VolpathParams()
+    L.alvrl_volpath_default(C.byref(vp))
+    for k, v in params.items():
+        setattr(vp, k, int(v))
+    dev = torch.device("cuda", device)
+    n = scene.width * scene.height if pixel_ids is None else len(pixel_ids)
+    out = torch.empty((n, 3), dtype=torch.float32, device=dev)
+    ids = None if pixel_ids is None else torch.as_tensor(np.asarray(pixel_ids, np.uint32).astype(np.int32)).to(dev)
+    with torch.cuda.device(dev):
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        _hcheck(L.alvrl_volpath_render(C.byref(scene), C.byref(vp), seed, pass_, spp,
+                                       None if ids is None else ids.data_ptr(), n, out.data_ptr(), stream))
     return out
 
 

@@ -405,6 +405,238 @@ __global__ void __launch_bounds__(256) k_eye_records(TCam c, TScene sc, const ui
     r[15] = __uint_as_float(flags);
 }
 
+// ----------------------------------------------------- volpath reference --
+// VolumetricPathTracer::Li_original with onlyVRLpaths (src/integrators/path/
+// volpath.cpp:120-457): the path-traced ground truth of the light transport
+// VRLs represent, for the statistical parity of the VRL
+// method.  One lane per pixel, its samples in order; draws from the counter
+// stream (seed, pass, dom 6, pixel, sample) in the reference's order:
+// sampleDistance (1-2), medium NEE (2, when requested), phase sample (2),
+// surface NEE (2, when requested), BSDF sample (2), Russian roulette (1).
+// Isotropic phase, point light (EDiscrete: every MIS weight is 1), diffuse
+// walls and occluders, strictNormals off, no emitter is hit by a ray.
+constexpr uint32_t kDomVolpath = 6u;
+
+struct VStream {
+    uint32_t seed, pass, a, b, k, blk;
+    uint32_t buf[4];
+    __device__ float next()
+    {
+        const uint32_t bl = k >> 2;
+        if (bl != blk) {
+            uint32_t c0 = a, c1 = b, c2 = bl, c3 = (kDomVolpath << 24);
+            uint32_t k0 = seed, k1 = pass;
+            for (int r = 0; r < 10; r++) {
+                if (r > 0) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
+                const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+                const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0, n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+                c0 = n0; c1 = (uint32_t)p1; c2 = n2; c3 = (uint32_t)p0;
+            }
+            buf[0] = c0; buf[1] = c1; buf[2] = c2; buf[3] = c3;
+            blk = bl;
+        }
+        const uint32_t u = (buf[k & 3] >> 9) | 0x3f800000u;
+        ++k;
+        return __uint_as_float(u) - 1.0f;
+    }
+};
+
+struct VParams {
+    int max_depth, rr_depth, only_vrl, vol_to_vol, vol_to_surf;
+    float intensity[3];
+};
+
+// evalTransmittance(p1, p1OnSurface, light, false) (scene.cpp:619-679):
+// medium transmittance over the whole segment, 0 behind an occluder
+__device__ void attenuation(const TScene& sc, F3 p1, bool p1_surface, F3 p2, float tr[3])
+{
+    const F3 d0 = sub(p2, p1);
+    const float remaining = len(d0);
+    const float negLength = 0.0f - remaining;
+    for (int i = 0; i < 3; i++) tr[i] = sc.sigma_t[i] != 0 ? fastexp(sc.sigma_t[i] * negLength) : 1.0f;
+    if (sc.bv.ntri && remaining > 0) {
+        const F3 d = mul(d0, 1.0f / remaining);
+        if (alvrl::bvh::occluded(sc.bv, alvrl::bvh::mk(p1.x, p1.y, p1.z), alvrl::bvh::mk(d.x, d.y, d.z),
+                                 p1_surface ? 1e-4f : 0.0f, remaining))
+            tr[0] = tr[1] = tr[2] = 0.0f;
+    }
+}
+
+// Scene::sampleAttenuatedEmitterDirect + PointEmitter::sampleDirect
+// (scene.cpp:854-898, point.cpp:131-147): value and unit direction to the light
+__device__ void light_direct(const TScene& sc, const VParams& vp, F3 ref, bool on_surface, float val[3], F3* dir)
+{
+    const F3 L = f3(sc.light_pos[0], sc.light_pos[1], sc.light_pos[2]);
+    F3 d = sub(L, ref);
+    const float dist = len(d);
+    const float invDist = 1.0f / dist;
+    d = mul(d, invDist);
+    *dir = d;
+    float tr[3];
+    attenuation(sc, ref, on_surface, L, tr);
+    for (int i = 0; i < 3; i++) {
+        val[i] = vp.intensity[i] * (invDist * invDist);
+        val[i] *= tr[i] * 1.0f;   // / emPdf (one emitter)
+    }
+}
+
+__device__ void volpath_li(const TScene& sc, const VParams& vp, VStream& smp, F3 o, F3 dir, float mint, float Li[3])
+{
+    Li[0] = Li[1] = Li[2] = 0.0f;
+    bool first_ok = false, second_ok = false, prev_diffuse = false, prev_volume = false;
+    F3 n, hp;
+    bool hit_occ;
+    float its_t = first_hit(sc, o, dir, mint, &n, &hp, &hit_occ);
+    float thr[3] = {1.0f, 1.0f, 1.0f};
+    const float eta = 1.0f;
+    const float w = sc.w;
+    int depth = 1;
+    bool indirect = true;   // rRec.type keeps EIndirect*Radiance (ERadiance / ERadianceNoEmission)
+    while (depth <= vp.max_depth || vp.max_depth < 0) {
+        if (vp.only_vrl && depth > 2 && !(first_ok && second_ok)) break;   // :144-145
+        // HomogeneousMedium::sampleDistance over Ray(ray, 0, its.t)
+        float rnd = smp.next(), sampled;
+        if (rnd < w) {
+            rnd /= w;
+            int ch = (int)(smp.next() * 3);
+            if (ch > 2) ch = 2;
+            sampled = -fastlog(1 - rnd) / sc.sigma_t[ch];
+        } else {
+            sampled = INFINITY;
+        }
+        const float distSurf = its_t - 0.0f;
+        bool success = true;
+        F3 mp = o;
+        if (sampled < distSurf) {
+            mp = add(o, mul(dir, sampled + 0.0f));
+            if (mp.x == o.x && mp.y == o.y && mp.z == o.z) success = false;
+        } else {
+            sampled = distSurf;
+            success = false;
+        }
+        float pf = 0, ps = 0;
+        for (int i = 0; i < 3; i++) {
+            const float tmp = fastexp(-sc.sigma_t[i] * sampled);
+            pf += tmp;
+            ps += sc.sigma_t[i] * tmp;
+        }
+        pf /= 3; ps /= 3;
+        float mtr[3];
+        for (int i = 0; i < 3; i++) mtr[i] = fastexp(sc.sigma_t[i] * (-sampled));
+        ps = ps * w;
+        pf = w * pf + (1 - w);
+        {
+            float mx = mtr[0] > mtr[1] ? mtr[0] : mtr[1];
+            mx = mx > mtr[2] ? mx : mtr[2];
+            if (mx < 1e-20f) mtr[0] = mtr[1] = mtr[2] = 0;
+        }
+        if (success) {   // :150-267
+            if (depth == 1 && vp.vol_to_vol) first_ok = true;
+            if (depth == 2) second_ok = true;
+            if (depth >= vp.max_depth && vp.max_depth != -1) break;
+            const float rps = 1.0f / ps;
+            for (int i = 0; i < 3; i++) thr[i] *= (sc.sigma_s[i] * mtr[i]) * rps;
+            // luminaire sampling; the reference's "(!rRec.depth==2 || ...)" is
+            // "((!depth) == 2 || ...)", i.e. the bracket alone (:183-190)
+            const bool nee = !vp.only_vrl ||
+                             (depth != 1 && (prev_volume || prev_diffuse) && (!prev_diffuse || vp.vol_to_surf) &&
+                              (!prev_volume || vp.vol_to_vol));
+            if (nee) {
+                (void)smp.next(); (void)smp.next();   // rRec.nextSample2D() (unused by a point light)
+                float val[3];
+                F3 ld;
+                light_direct(sc, vp, mp, false, val, &ld);
+                if (!(val[0] == 0 && val[1] == 0 && val[2] == 0)) {
+                    const float phaseVal = 0.079577471545947667884f;   // IsotropicPhaseFunction::eval, 1/(4 pi)
+                    for (int i = 0; i < 3; i++) Li[i] += ((thr[i] * val[i]) * phaseVal) * 1.0f;
+                }
+            }
+            // phase sampling (isotropic: weight 1)
+            const float px_ = smp.next(), py_ = smp.next();
+            const F3 wo = uniform_sphere(px_, py_);
+            o = mp; dir = wo;
+            its_t = first_hit(sc, o, dir, 0.0f, &n, &hp, &hit_occ);
+            if (!indirect) break;
+            prev_volume = true;
+            prev_diffuse = false;
+        } else {   // :268-435
+            const float rpf = 1.0f / pf;
+            for (int i = 0; i < 3; i++) thr[i] *= mtr[i] * rpf;
+            if (!isfinite(its_t)) break;
+            if (depth >= vp.max_depth && vp.max_depth != -1) break;
+            const float* alb = hit_occ ? sc.occ_albedo : sc.albedo;
+            const F3 p = hp;
+            const float cos_wi = dot(f3(-dir.x, -dir.y, -dir.z), n);
+            if (!vp.only_vrl || (first_ok && second_ok)) {   // :319-350 (ESmooth diffuse)
+                (void)smp.next(); (void)smp.next();
+                float val[3];
+                F3 ld;
+                light_direct(sc, vp, p, true, val, &ld);
+                if (!(val[0] == 0 && val[1] == 0 && val[2] == 0)) {
+                    const float cos_wo = dot(ld, n);
+                    if (!(cos_wi <= 0 || cos_wo <= 0)) {
+                        const float k = 0.31830988618379067154f * cos_wo;   // INV_PI * cosTheta(wo)
+                        for (int i = 0; i < 3; i++) Li[i] += ((thr[i] * val[i]) * (alb[i] * k)) * 1.0f;
+                    }
+                }
+            }
+            // BSDF sampling (diffuse.cpp:140-150)
+            const float bx = smp.next(), by = smp.next();
+            if (cos_wi <= 0) break;   // bsdfWeight.isZero()
+            const F3 wol = cosine_hemisphere(bx, by);
+            F3 fs, ft;
+            frame_of(n, &fs, &ft);
+            const F3 wo = add(add(mul(fs, wol.x), mul(ft, wol.y)), mul(n, wol.z));
+            if (depth == 1 && vp.vol_to_surf) first_ok = true;   // :377-382 (inside the medium, smooth)
+            prev_volume = false;
+            prev_diffuse = true;
+            for (int i = 0; i < 3; i++) thr[i] *= alb[i];
+            o = p; dir = wo;
+            its_t = first_hit(sc, o, dir, 1e-4f, &n, &hp, &hit_occ);
+            if (!indirect) break;
+        }
+        if (depth++ >= vp.rr_depth) {   // :437-446
+            float mx = thr[0] > thr[1] ? thr[0] : thr[1];
+            mx = mx > thr[2] ? mx : thr[2];
+            float q = mx * eta * eta;
+            if (q > 0.95f) q = 0.95f;
+            if (smp.next() >= q) break;
+            const float rq = 1.0f / q;
+            for (int i = 0; i < 3; i++) thr[i] *= rq;
+        }
+    }
+    if (vp.only_vrl && !(first_ok && second_ok)) Li[0] = Li[1] = Li[2] = 0.0f;   // :453-455
+}
+
+__global__ void __launch_bounds__(256) k_volpath(TCam c, TScene sc, VParams vp, uint32_t seed, uint32_t pass,
+                                                 uint32_t spp, const uint32_t* __restrict__ pix, uint32_t n,
+                                                 float* __restrict__ out)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t id = pix ? pix[i] : i;
+    const float px = (float)(id % c.width) + 0.5f, py = (float)(id / c.width) + 0.5f;
+    const float sx = px * c.inv_w, sy = py * c.inv_h;
+    const float xc = (1.0f - 2.0f * sx) * c.tanh_;
+    const float yc = ((1.0f - 2.0f * sy) / c.aspect) * c.tanh_;
+    F3 dc = f3(xc, yc, 1.0f);
+    dc = mul(dc, 1.0f / len(dc));
+    const float mint = 1e-2f * (1.0f / dc.z);
+    const F3 O = f3(c.o[0], c.o[1], c.o[2]);
+    const F3 D = f3(c.left[0] * dc.x + c.nup[0] * dc.y + c.fwd[0] * dc.z,
+                    c.left[1] * dc.x + c.nup[1] * dc.y + c.fwd[1] * dc.z,
+                    c.left[2] * dc.x + c.nup[2] * dc.y + c.fwd[2] * dc.z);
+    float acc[3] = {0.0f, 0.0f, 0.0f};
+    for (uint32_t s = 0; s < spp; s++) {
+        VStream smp{seed, pass, id, s, 0u, 0xFFFFFFFFu, {0, 0, 0, 0}};
+        float li[3];
+        volpath_li(sc, vp, smp, O, D, mint, li);
+        for (int k = 0; k < 3; k++) acc[k] += li[k];
+    }
+    const float r = 1.0f / (float)spp;
+    for (int k = 0; k < 3; k++) out[3 * (size_t)i + k] = acc[k] * r;
+}
+
 TScene make_tscene(const alvrl::host::SmokeBox& box)
 {
     TScene sc;
@@ -423,9 +655,67 @@ TScene make_tscene(const alvrl::host::SmokeBox& box)
     return sc;
 }
 
+TCam make_tcam(const alvrl::host::SmokeBox& box, int scat)
+{
+    using namespace alvrl::host;
+    TCam c;
+    const V3 fwd = normalize(box.cam_target - box.cam_origin);
+    const V3 left = normalize(cross(box.cam_up, fwd));
+    const V3 nup = cross(fwd, left);
+    const float vv[4][3] = {{box.cam_origin.x, box.cam_origin.y, box.cam_origin.z}, {fwd.x, fwd.y, fwd.z},
+                            {left.x, left.y, left.z}, {nup.x, nup.y, nup.z}};
+    for (int k = 0; k < 3; k++) { c.o[k] = vv[0][k]; c.fwd[k] = vv[1][k]; c.left[k] = vv[2][k]; c.nup[k] = vv[3][k]; }
+    c.aspect = (float)box.width / (float)box.height;
+    c.tanh_ = std::tan(0.5f * box.fov_x_deg * (float)(kPi / 180.0));
+    c.inv_w = 1.0f / (float)box.width;
+    c.inv_h = 1.0f / (float)box.height;
+    c.width = (uint32_t)box.width;
+    c.scat = scat;
+    return c;
+}
+
 }  // namespace
 
 extern "C" {
+
+ALVRL_API void alvrl_volpath_default(alvrl_volpath_params* p)
+{
+    if (!p) return;
+    p->max_depth = -1;       // MonteCarloIntegrator maxDepth
+    p->rr_depth = 5;         // rrDepth
+    p->only_vrl_paths = 1;   // volpath.cpp:79-81
+    p->vrl_vol_to_vol = 1;
+    p->vrl_vol_to_surf = 1;
+}
+
+ALVRL_API int alvrl_volpath_render(const alvrl_scene_desc* s, const alvrl_volpath_params* p, uint32_t seed,
+                                   uint32_t pass, uint32_t spp, const uint32_t* d_pixel_ids, uint32_t n,
+                                   float* d_out_rgb, void* stream)
+{
+    if (!s || !p || (!d_out_rgb && n)) return terr(ALVRL_ERR_INVALID, "alvrl_volpath_render: null argument");
+    if (spp == 0) return terr(ALVRL_ERR_INVALID, "alvrl_volpath_render: spp must be > 0");
+    if (s->medium.phase_type != 0)
+        return terr(ALVRL_ERR_INVALID, "alvrl_volpath_render: only the isotropic phase function is supported");
+    const alvrl::host::SmokeBox box = alvrl::host::to_box(*s);
+    const uint64_t npix = (uint64_t)box.width * (uint64_t)box.height;
+    if (!d_pixel_ids && n > npix) return terr(ALVRL_ERR_INVALID, "alvrl_volpath_render: n > W*H without pixel ids");
+    if (n == 0) return ALVRL_OK;
+    TScene sc = make_tscene(box);
+    DevBvh bv;
+    if (bv.upload(box.occ) != hipSuccess) return terr(ALVRL_ERR_HIP, "alvrl_volpath_render: BVH upload");
+    sc.bv = bv.view;
+    const TCam c = make_tcam(box, 1);
+    VParams vp;
+    vp.max_depth = p->max_depth; vp.rr_depth = p->rr_depth; vp.only_vrl = p->only_vrl_paths ? 1 : 0;
+    vp.vol_to_vol = p->vrl_vol_to_vol ? 1 : 0; vp.vol_to_surf = p->vrl_vol_to_surf ? 1 : 0;
+    for (int i = 0; i < 3; i++) vp.intensity[i] = box.light_intensity[i];
+    hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL(k_volpath, dim3((n + 255) / 256), dim3(256), 0, st, c, sc, vp, seed, pass, spp, d_pixel_ids, n,
+                       d_out_rgb);
+    if (hipGetLastError() != hipSuccess) return terr(ALVRL_ERR_HIP, "alvrl_volpath_render: launch");
+    if (hipStreamSynchronize(st) != hipSuccess) return terr(ALVRL_ERR_HIP, "alvrl_volpath_render: sync");
+    return ALVRL_OK;
+}
 
 // Gather records of pixel centres on the current HIP device (the host
 // alvrl_scene_records, bit for bit).  d_pixel_ids (device, row-major y*W+x)
@@ -443,22 +733,7 @@ ALVRL_API int alvrl_scene_records_gpu(const alvrl_scene_desc* s, int medium_scat
     DevBvh bv;
     if (bv.upload(box.occ) != hipSuccess) return terr(ALVRL_ERR_HIP, "alvrl_scene_records_gpu: BVH upload");
     sc.bv = bv.view;
-    TCam c;
-    {
-        using namespace alvrl::host;
-        const V3 fwd = normalize(box.cam_target - box.cam_origin);
-        const V3 left = normalize(cross(box.cam_up, fwd));
-        const V3 nup = cross(fwd, left);
-        const float vv[4][3] = {{box.cam_origin.x, box.cam_origin.y, box.cam_origin.z}, {fwd.x, fwd.y, fwd.z},
-                                {left.x, left.y, left.z}, {nup.x, nup.y, nup.z}};
-        for (int k = 0; k < 3; k++) { c.o[k] = vv[0][k]; c.fwd[k] = vv[1][k]; c.left[k] = vv[2][k]; c.nup[k] = vv[3][k]; }
-        c.aspect = (float)box.width / (float)box.height;
-        c.tanh_ = std::tan(0.5f * box.fov_x_deg * (float)(kPi / 180.0));
-        c.inv_w = 1.0f / (float)box.width;
-        c.inv_h = 1.0f / (float)box.height;
-        c.width = (uint32_t)box.width;
-        c.scat = medium_scatters && !sc.sigma_s_zero ? 1 : 0;
-    }
+    const TCam c = make_tcam(box, medium_scatters && !sc.sigma_s_zero ? 1 : 0);
     hipStream_t st = (hipStream_t)stream;
     hipLaunchKernelGGL(k_eye_records, dim3((n + 255) / 256), dim3(256), 0, st, c, sc, d_pixel_ids, n,
                        reinterpret_cast<float*>(d_out));

@@ -999,3 +999,175 @@ uint32_t alvrl_o_trace_vrls(const alvrl_o_scene *s, const alvrl_o_medium *m, uin
     if (particles) *particles = p;
     return k.n;
 }
+
+
+/* ===================================================================== */
+/*  volpath with onlyVRLpaths (src/integrators/path/volpath.cpp:110-457)   */
+/* ===================================================================== */
+#define ALVRL_O_DOM_VOLPATH 6u
+
+/* Scene::sampleAttenuatedEmitterDirect + PointEmitter::sampleDirect
+ * (scene.cpp:854-898, point.cpp:131-147), one emitter (emPdf = 1) */
+static void vp_light_direct(const alvrl_o_scene *s, const alvrl_o_medium *m, v3 ref, int on_surface,
+                            float val[3], v3 *dir)
+{
+    v3 L = ld3(s->light_pos);
+    v3 d = sub(L, ref);
+    float dist = len(d);
+    float invDist = 1.0f / dist;
+    d = scl(d, invDist);
+    *dir = d;
+    /* evalTransmittance(ref, on_surface, light, false): medium + occluders */
+    v3 d0 = sub(L, ref);
+    float remaining = len(d0);
+    float negLength = 0.0f - remaining;
+    float tr[3];
+    for (int i = 0; i < 3; i++) tr[i] = m->sigma_t[i] != 0 ? fastexp(m->sigma_t[i] * negLength) : 1.0f;
+    if (!segment_visible(s->occ, s->nocc, ref, on_surface, L)) tr[0] = tr[1] = tr[2] = 0.0f;
+    for (int i = 0; i < 3; i++) {
+        val[i] = s->light_intensity[i] * (invDist * invDist);
+        val[i] *= tr[i] * 1.0f;
+    }
+}
+
+static void vp_li(const alvrl_o_scene *s, const alvrl_o_medium *m, const alvrl_o_volpath_params *vp,
+                  seq_sampler *smp, v3 o, v3 dir, float mint, float Li[3])
+{
+    Li[0] = Li[1] = Li[2] = 0.0f;
+    int first_ok = 0, second_ok = 0, prev_diffuse = 0, prev_volume = 0;
+    v3 n, hp;
+    int tri;
+    float its_t = first_hit(s, o, dir, mint, &n, &hp, &tri);
+    float thr[3] = { 1, 1, 1 };
+    float eta = 1.0f, w = m->sampling_weight;
+    int depth = 1;
+    while (depth <= vp->max_depth || vp->max_depth < 0) {
+        if (vp->only_vrl_paths && depth > 2 && !(first_ok && second_ok)) break;   /* :144-145 */
+        float rnd = seq_next(smp), sampled;
+        if (rnd < w) {
+            rnd /= w;
+            int ch = (int)(seq_next(smp) * 3);
+            if (ch > 2) ch = 2;
+            sampled = -fastlog(1 - rnd) / m->sigma_t[ch];
+        } else {
+            sampled = INFINITY;
+        }
+        float distSurf = its_t - 0.0f;
+        int success = 1;
+        v3 mp = o;
+        if (sampled < distSurf) {
+            mp = add(o, scl(dir, sampled + 0.0f));
+            if (mp.x == o.x && mp.y == o.y && mp.z == o.z) success = 0;
+        } else {
+            sampled = distSurf;
+            success = 0;
+        }
+        float pf = 0, ps = 0;
+        for (int i = 0; i < 3; i++) {
+            float tmp = fastexp(-m->sigma_t[i] * sampled);
+            pf += tmp;
+            ps += m->sigma_t[i] * tmp;
+        }
+        pf /= 3; ps /= 3;
+        float mtr[3];
+        for (int i = 0; i < 3; i++) mtr[i] = fastexp(m->sigma_t[i] * (-sampled));
+        ps = ps * w;
+        pf = w * pf + (1 - w);
+        {
+            float mx = mtr[0] > mtr[1] ? mtr[0] : mtr[1];
+            mx = mx > mtr[2] ? mx : mtr[2];
+            if (mx < 1e-20f) mtr[0] = mtr[1] = mtr[2] = 0;
+        }
+        if (success) {   /* :150-267 */
+            if (depth == 1 && vp->vrl_vol_to_vol) first_ok = 1;
+            if (depth == 2) second_ok = 1;
+            if (depth >= vp->max_depth && vp->max_depth != -1) break;
+            float rps = 1.0f / ps;
+            for (int i = 0; i < 3; i++) thr[i] *= (m->sigma_s[i] * mtr[i]) * rps;
+            /* "(!rRec.depth==2 || (...))" parses as "((!depth) == 2 || (...))" (:183-190) */
+            int nee = !vp->only_vrl_paths ||
+                      (depth != 1 && (prev_volume || prev_diffuse) && (!prev_diffuse || vp->vrl_vol_to_surf) &&
+                       (!prev_volume || vp->vrl_vol_to_vol));
+            if (nee) {
+                (void)seq_next(smp); (void)seq_next(smp);
+                float val[3];
+                v3 ld;
+                vp_light_direct(s, m, mp, 0, val, &ld);
+                if (!(val[0] == 0 && val[1] == 0 && val[2] == 0))
+                    for (int i = 0; i < 3; i++) Li[i] += ((thr[i] * val[i]) * INV_FOURPI) * 1.0f;
+            }
+            float px_ = seq_next(smp), py_ = seq_next(smp);
+            v3 wo = uniform_sphere(px_, py_);
+            o = mp; dir = wo;
+            its_t = first_hit(s, o, dir, 0.0f, &n, &hp, &tri);
+            prev_volume = 1;
+            prev_diffuse = 0;
+        } else {   /* :268-435 */
+            float rpf = 1.0f / pf;
+            for (int i = 0; i < 3; i++) thr[i] *= mtr[i] * rpf;
+            if (!isfinite(its_t)) break;
+            if (depth >= vp->max_depth && vp->max_depth != -1) break;
+            const float *alb = tri >= 0 ? s->occ_albedo : s->albedo;
+            v3 p = hp;
+            float cos_wi = dot(neg(dir), n);
+            if (!vp->only_vrl_paths || (first_ok && second_ok)) {   /* :319-350 */
+                (void)seq_next(smp); (void)seq_next(smp);
+                float val[3];
+                v3 ld;
+                vp_light_direct(s, m, p, 1, val, &ld);
+                if (!(val[0] == 0 && val[1] == 0 && val[2] == 0)) {
+                    float cos_wo = dot(ld, n);
+                    if (!(cos_wi <= 0 || cos_wo <= 0)) {
+                        float k = INV_PI * cos_wo;
+                        for (int i = 0; i < 3; i++) Li[i] += ((thr[i] * val[i]) * (alb[i] * k)) * 1.0f;
+                    }
+                }
+            }
+            float bx = seq_next(smp), by = seq_next(smp);   /* diffuse.cpp:140-150 */
+            if (cos_wi <= 0) break;
+            v3 wol = cosine_hemisphere(bx, by);
+            v3 fs, ft;
+            frame_of(n, &fs, &ft);
+            v3 wo = add(add(scl(fs, wol.x), scl(ft, wol.y)), scl(n, wol.z));
+            if (depth == 1 && vp->vrl_vol_to_surf) first_ok = 1;   /* :377-382 */
+            prev_volume = 0;
+            prev_diffuse = 1;
+            for (int i = 0; i < 3; i++) thr[i] *= alb[i];
+            o = p; dir = wo;
+            its_t = first_hit(s, o, dir, 1e-4f, &n, &hp, &tri);
+        }
+        if (depth++ >= vp->rr_depth) {   /* :437-446 */
+            float mx = thr[0] > thr[1] ? thr[0] : thr[1];
+            mx = mx > thr[2] ? mx : thr[2];
+            float q = mx * eta * eta;
+            if (q > 0.95f) q = 0.95f;
+            if (seq_next(smp) >= q) break;
+            float rq = 1.0f / q;
+            for (int i = 0; i < 3; i++) thr[i] *= rq;
+        }
+    }
+    if (vp->only_vrl_paths && !(first_ok && second_ok)) Li[0] = Li[1] = Li[2] = 0.0f;   /* :453-455 */
+}
+
+void alvrl_o_volpath(const alvrl_o_scene *s, const alvrl_o_medium *m, const alvrl_o_volpath_params *vp,
+                     uint32_t seed, uint32_t pass, uint32_t spp, const uint32_t *pixel_ids, uint32_t n,
+                     float *out_rgb)
+{
+    for (uint32_t i = 0; i < n; i++) {
+        uint32_t id = pixel_ids ? pixel_ids[i] : i;
+        float px = (float)(id % (uint32_t)s->width) + 0.5f, py = (float)(id / (uint32_t)s->width) + 0.5f;
+        float o[3], d[3];
+        alvrl_o_camera_ray(s, px, py, o, d);
+        float mint = camera_mint(s, px, py);
+        float acc[3] = { 0, 0, 0 };
+        for (uint32_t k = 0; k < spp; k++) {
+            seq_sampler smp;
+            seq_init(&smp, seed, pass, ALVRL_O_DOM_VOLPATH, id, k, 0);
+            float li[3];
+            vp_li(s, m, vp, &smp, ld3(o), ld3(d), mint, li);
+            for (int c = 0; c < 3; c++) acc[c] += li[c];
+        }
+        float r = 1.0f / (float)spp;
+        for (int c = 0; c < 3; c++) out_rgb[3 * (size_t)i + c] = acc[c] * r;
+    }
+}

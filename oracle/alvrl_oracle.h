@@ -150,6 +150,15 @@ uint32_t alvrl_o_trace_vrls(const alvrl_o_scene *s, const alvrl_o_medium *m, uin
                             uint32_t pass, uint32_t target, int short_vrls, int max_depth,
                             int rr_depth, float *vrl_soa, uint32_t cap, uint64_t *particles);
 
+/* volpath with onlyVRLpaths (src/integrators/path/volpath.cpp:110-457) at
+ * pixel centres: the mean of spp samples per pixel; counter stream (seed,
+ * pass, dom 6, pixel id, sample index).  Isotropic phase only. */
+typedef struct {
+    int max_depth, rr_depth, only_vrl_paths, vrl_vol_to_vol, vrl_vol_to_surf;
+} alvrl_o_volpath_params;
+void alvrl_o_volpath(const alvrl_o_scene *s, const alvrl_o_medium *m, const alvrl_o_volpath_params *vp,
+                     uint32_t seed, uint32_t pass, uint32_t spp, const uint32_t *pixel_ids, uint32_t n,
+                     float *out_rgb);
 #ifdef __cplusplus
 }
 #endif

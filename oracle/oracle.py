@@ -183,6 +183,20 @@ class Oracle:
         self.lib.alvrl_o_make_record(C.byref(scene), int(medium_scatters), x, y, _p(out))
         return out
 
+    def volpath(self, scene: Scene, medium: Medium, spp: int, seed=0xA1B2C3D4, pass_=0, pixel_ids=None,
+                max_depth=-1, rr_depth=5, only_vrl_paths=True, vol_to_vol=True, vol_to_surf=True):
+        """volpath onlyVRLpaths reference (alvrl_o_volpath): (n, 3) means over spp."""
+        class VP(C.Structure):
+            _fields_ = [("max_depth", C.c_int), ("rr_depth", C.c_int), ("only_vrl_paths", C.c_int),
+                        ("vrl_vol_to_vol", C.c_int), ("vrl_vol_to_surf", C.c_int)]
+        vp = VP(max_depth, rr_depth, int(only_vrl_paths), int(vol_to_vol), int(vol_to_surf))
+        n = scene.width * scene.height if pixel_ids is None else len(pixel_ids)
+        ids = None if pixel_ids is None else np.ascontiguousarray(pixel_ids, np.uint32)
+        out = np.zeros((n, 3), np.float32)
+        self.lib.alvrl_o_volpath(C.byref(scene), C.byref(medium), C.byref(vp), seed, pass_, spp,
+                                 _p(ids, C.c_uint32), n, _p(out))
+        return out
+
     def trace(self, scene: Scene, medium: Medium, target: int, seed=0x5EED0001, pass_=0,
               short_vrls=True, max_depth=-1, rr_depth=5):
         cap = target + 4096
