@@ -157,10 +157,15 @@ __device__ __forceinline__ void trace(const Common& cm, uint32_t phase, uint32_t
                            __HIP_MEMORY_SCOPE_SYSTEM);
 }
 // team counters
-enum { TS_ENQ, TS_HSTART, TS_HDONE, TS_COMMIT, TS_STEAL, TS_WAIT_TMO, TS_OWN, TS_IDLE_EXIT, TS_LSIDE, TS_N };
+enum { TS_ENQ, TS_HSTART, TS_HDONE, TS_COMMIT, TS_STEAL, TS_WAIT_TMO, TS_OWN, TS_IDLE_EXIT, TS_LSIDE,
+       TS_HIDLE, TS_RIDLE, TS_HBUSY, TS_RBUSY, TS_N };   // *IDLE/*BUSY: wall ticks (100 MHz) summed
 __device__ __forceinline__ void tcount(const Common& cm, int k)
 {
     if (cm.tstat) atomicAdd(&cm.tstat[k], 1ull);
+}
+__device__ __forceinline__ void tadd(const Common& cm, int k, unsigned long long v)
+{
+    if (cm.tstat) atomicAdd(&cm.tstat[k], v);
 }
 
 // Phase timer of lane 0 (s_memtime deltas summed over jobs).
@@ -2368,13 +2373,15 @@ __device__ __noinline__ void helper_loop(const JobDev& J0, uint32_t hid, const C
                 if (wall() - t_idle > cm.spin_ticks) { got = -1; tcount(cm, TS_IDLE_EXIT); break; }
                 __builtin_amdgcn_s_sleep(32);
             }
+            tadd(cm, TS_HIDLE, wall() - t_idle);
             C.go = got; C.b = b; C.e = e;
         }
         __syncthreads();
         if (C.go < 0) break;
         trace(cm, 11, C.b);
+        const unsigned long long t_busy = wall();
         spec_split(J0, J, cm, C, lds, C.b, C.e);
-        if (tid == 0) tcount(cm, TS_HDONE);
+        if (tid == 0) { tcount(cm, TS_HDONE); tadd(cm, TS_HBUSY, wall() - t_busy); }
         trace(cm, 12, C.b);
     }
 }
@@ -2408,6 +2415,7 @@ __device__ __noinline__ void roam_loop(const JobDev* jobs, const SplitWs& w, uin
                 if (!live || wall() - t_idle > cm.spin_ticks) { got = -1; break; }
                 __builtin_amdgcn_s_sleep(32);
             }
+            tadd(cm, TS_RIDLE, wall() - t_idle);
             C.go = got; C.b = b; C.e = e; C.j = jj;
         }
         __syncthreads();
@@ -2418,8 +2426,9 @@ __device__ __noinline__ void roam_loop(const JobDev* jobs, const SplitWs& w, uin
         Jw.vrls = J0.team.spec;
         Jw.dir = w.dir; Jw.st = w.st; Jw.bufM = w.bufM; Jw.keys0 = w.keys0; Jw.keys1 = w.keys1;
         Jw.fsu = w.fsu; Jw.fsi = w.fsi; Jw.feu = w.feu; Jw.fei = w.fei;
+        const unsigned long long t_busy = wall();
         spec_split(J0, Jw, cm, C, lds, C.b, C.e);
-        if (tid == 0) tcount(cm, TS_HDONE);
+        if (tid == 0) { tcount(cm, TS_HDONE); tadd(cm, TS_RBUSY, wall() - t_busy); }
     }
 }
 
@@ -3257,6 +3266,9 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
                          "commit %llu steal %llu wait-timeout %llu own %llu side %llu | helper idle exits %llu\n",
                          G, nroam, njobs, h[TS_ENQ], h[TS_HSTART], h[TS_HDONE], h[TS_COMMIT], h[TS_STEAL],
                          h[TS_WAIT_TMO], h[TS_OWN], h[TS_LSIDE], h[TS_IDLE_EXIT]);
+            std::fprintf(stderr, "[refine team] wall ms summed: team helpers idle %.0f busy %.0f | roamers (incl. "
+                         "finished helpers) idle %.0f busy %.0f\n", h[TS_HIDLE] * 1e-5, h[TS_HBUSY] * 1e-5,
+                         h[TS_RIDLE] * 1e-5, h[TS_RBUSY] * 1e-5);
         hipFree(cm.tstat);
         if (cm.jtime) {
             std::vector<unsigned long long> jt((size_t)njobs * 3);
