@@ -147,6 +147,8 @@ struct Common {
     int roam_on;                   // finished leaders and helpers roam too (scratch sized for Rmax)
     const SplitWs* roam_ws;        // [nroam] their scratch, sized for the largest job
     const uint32_t* roam_order;    // null: roam from the last job served; else scan jobs in this order
+    int early_spec;                // queue the first initial cluster for a helper's split before the
+                                   // leader computes the initial clusters' variances (ALVRL_EARLY_SPEC=0: off)
     int team_setup;                // a job's first helper takes half the column weights and the
                                    // unclustered variance off the leader (ALVRL_TEAM_SETUP=0: off)
 };
@@ -2073,6 +2075,24 @@ __device__ void enqueue_candidates(const JobDev& J, const Common& cm, Ctl& C)
     }
 }
 
+// Thread 0 of the leader: queue [b, e) ahead of the heap (the first initial
+// cluster, the root of the refinement, while the leader is still computing
+// the initial clusters' variances).  Its vrls and the column weights were
+// released by the caller.  Popped later, the cluster is stolen back, waited
+// for or committed exactly like a cluster enqueue_candidates queued.
+__device__ void enqueue_early(const JobDev& J, const Common& cm, uint32_t b, uint32_t e)
+{
+    const Team& T = J.team;
+    if (e <= b || e - b < cm.spec_min) return;
+    const uint32_t tail = T.ctl[1];
+    if (tail - ld_rlx(&T.ctl[0]) >= kQueue) return;
+    st_rlx(&T.state[b], ((unsigned long long)e << 3) | kStQueued);
+    st_rlx(&T.queue[tail % kQueue], ((unsigned long long)b << 32) | e);
+    tcount(cm, TS_ENQ);
+    drain_vmem();   // slot and state land before the tail that publishes them
+    st_rlx(&T.ctl[1], tail + 1);
+}
+
 __device__ void stop_team(const JobDev& J, const Common& cm)
 {
     if (J.team.helpers && threadIdx.x == 0) st_rel(&J.team.ctl[2], 1u);
@@ -2685,6 +2705,17 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
     pf.mark(PF_COLW);
     for (uint32_t i = tid; i < nv; i += kThreads) J.vrls[i] = cm.init_vrls[i];
     __syncthreads();
+    if (cm.early_spec && cm.team > 1 && J.team.helpers != 0 && J.do_refine && cm.ninit > 0 && !C.err) {
+        // the root's split starts on a helper now (its vrls and colw released
+        // first: every wave drained, barrier, one agent-scope release)
+        drain_vmem();
+        __syncthreads();
+        if (tid == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            enqueue_early(J, cm, cm.init_off[0], cm.init_off[1]);
+        }
+        __syncthreads();
+    }
     // initial clusters
     for (uint32_t i = 0; i < cm.ninit; i += 2) {
         const uint32_t b0 = cm.init_off[i], e0 = cm.init_off[i + 1];
@@ -3163,6 +3194,8 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
         cm.enq_start = es ? std::atoi(es) : 0;   // queueing after the commit only: 398 vs 401 ms at width 32
         const char* tsu = std::getenv("ALVRL_TEAM_SETUP");
         cm.team_setup = tsu ? std::atoi(tsu) : 1;
+        const char* esp = std::getenv("ALVRL_EARLY_SPEC");
+        cm.early_spec = esp ? std::atoi(esp) : 1;
     }
     // ALVRL_ROAM_ORDER=1: roaming helpers scan the jobs with the most rows
     // first.  Measured slower (C4 refine 436 vs 420 ms: the roamers crowd the
