@@ -189,24 +189,31 @@ static const char* kPfNames[PF_N] = {"column weights", "initial clusters", "uncl
                                      "ctrl: heap pop/snapshot", "ctrl: enqueue", "ctrl: wait for helper",
                                      "ctrl: side splits", "ctrl: commit",
                                      "#splits", "#split columns"};
+constexpr int kPfSmall = 2;   // split-phase table of small splits: m < 64, 64 <= m < 256
 struct Prof {
     unsigned long long* p;
     long long t;
-    __device__ void mark(int id)
-    {
-        if (p && threadIdx.x == 0) {
-            const long long now = clock64();
-            atomicAdd(&p[id], (unsigned long long)(now - t));
-            t = now;
-        }
-    }
+    int sm = -1;                 // small-split class of the split in progress (-1: none)
+    __device__ void mark(int id);
     __device__ void count(int id, unsigned long long v) { if (p && threadIdx.x == 0) atomicAdd(&p[id], v); }
 };
 // split-size histogram after the phase totals: per log2(columns) bucket
 // (count, split cycles, variance cycles, cycles before the projections)
 constexpr int kPfBuckets = 18;
 constexpr int kPfWaveBusy = PF_N + 4 * kPfBuckets;   // per-wave busy cycles in the variance passes (+ 8 wall)
-constexpr int kPfTotal = kPfWaveBusy + 6 * kWaves;   // [NB < 4 | NB == 4][busy, wall, reduce][wave]
+constexpr int kPfSmallAt = kPfWaveBusy + 6 * kWaves;   // [NB < 4 | NB == 4][busy, wall, reduce][wave]
+constexpr int kPfSmallPh = PF_ARGMIN - PF_WSAMP + 1;
+constexpr int kPfTotal = kPfSmallAt + kPfSmall * kPfSmallPh;
+__device__ void Prof::mark(int id)
+{
+    if (p && threadIdx.x == 0) {
+        const long long now = clock64();
+        atomicAdd(&p[id], (unsigned long long)(now - t));
+        if (sm >= 0 && id >= PF_WSAMP && id <= PF_ARGMIN)
+            atomicAdd(&p[kPfSmallAt + sm * kPfSmallPh + (id - PF_WSAMP)], (unsigned long long)(now - t));
+        t = now;
+    }
+}
 __device__ __forceinline__ int pf_bucket(uint32_t m) { return min(kPfBuckets - 1, 31 - (int)__builtin_clz(max(m, 1u))); }
 
 // Per-column coefficients of the variance recurrence, read as broadcasts.
@@ -1429,7 +1436,7 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
             if (k + 1 < nch) step(k + 1, bufB, bufA);
             if (k + 2 < nch) step(k + 2, bufC, bufB);
         }
-        if (red) {
+            if (red) {
             reduce(nch - 1);
             flush((nch - 1) / 8);
         }
@@ -1787,6 +1794,7 @@ __device__ void split(const JobDev& J, const Common& cm, Ctl& C, uint32_t begin,
     pf.mark(PF_CTRL);
     pf.count(PF_NSPLIT, 1);
     pf.count(PF_SPLITCOLS, end - begin);
+    pf.sm = end - begin < 64 ? 0 : end - begin < 256 ? 1 : -1;
     const long long hb0 = pf.t;
     long long hbv = 0, hbp = 0;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -1959,6 +1967,7 @@ __device__ void split(const JobDev& J, const Common& cm, Ctl& C, uint32_t begin,
     }
     __syncthreads();
     pf.mark(PF_ARGMIN);
+    pf.sm = -1;
     if (pf.p && tid == 0) {
         const int b = pf_bucket(m);
         atomicAdd(&pf.p[PF_N + 4 * b], 1ull);
@@ -2155,8 +2164,12 @@ __device__ void spec_split(const JobDev& J0, const JobDev& Jw, const Common& cm,
     const int tid = threadIdx.x;
     const bool in_spec = (e & kQSpecBit) != 0;
     e &= ~kQSpecBit;
-    fence_acq();
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // one agent acquire for the CU (its L1), complete before the barrier
+    if (tid < 64) {
+        fence_acq();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
     if (!in_spec)
         copy_range(T.spec, J0.vrls, b, e);
     __syncthreads();
@@ -2220,7 +2233,8 @@ __device__ void split_team(const JobDev& J, const Common& cm, Ctl& C, uint32_t b
             const unsigned long long sv = ld_rlx(&T.state[b]);
             C.side = 0;
             if ((sv & 7) == kStDone && (uint32_t)(sv >> 3) == e) {
-                fence_acq();
+                fence_acq();   // the CU's one acquire, complete before the loop's barriers
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 C.tmode = 1;
                 tcount(cm, TS_COMMIT);
             } else if (wall() - C.t0 > cm.wait_ticks) {
@@ -2252,8 +2266,6 @@ __device__ void split_team(const JobDev& J, const Common& cm, Ctl& C, uint32_t b
     if (mode == 0) {
         split(J, cm, C, b, e, lds, pf);
     } else if (mode == 1) {
-        fence_acq();
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         copy_range(J.vrls, T.spec, b, e);
         __syncthreads();
         if (tid == 0) {
@@ -2328,11 +2340,11 @@ __device__ bool su_wait(const Team& T, uint32_t task, const Common& cm, Ctl& C)
             if (wall() - t0 > kSpinTicks) { ok = 0; break; }
             __builtin_amdgcn_s_sleep(8);
         }
+        fence_acq();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         C.go = ok;
     }
     __syncthreads();
-    fence_acq();
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const bool ok = C.go != 0;
     __syncthreads();
     return ok;
@@ -3340,6 +3352,15 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
                                  "reduce busy %llu (%.1f%%) of %llu cycles\n", w, c ? "193-256" : "<= 192",
                                  hb[w], 100.0 * hb[w] / wall, hb[2 * kWaves + w], 100.0 * hb[2 * kWaves + w] / wall, hb[kWaves + w]);
                 }
+            for (int c = 0; c < kPfSmall; c++) {
+                unsigned long long n = 0;
+                for (int b = 0; b < kPfBuckets; b++)
+                    if (c == 0 ? (1u << b) < 64u : ((1u << b) >= 64u && (1u << b) < 256u)) n += h[PF_N + 4 * b];
+                std::fprintf(stderr, "  splits of %s columns, cycles per split:", c ? "64-255" : "< 64");
+                for (int i = 0; i < kPfSmallPh; i++)
+                    std::fprintf(stderr, " %s %.0f", kPfNames[PF_WSAMP + i] + 7, (double)h[kPfSmallAt + c * kPfSmallPh + i] / (n ? n : 1));
+                std::fprintf(stderr, "\n");
+            }
             std::fprintf(stderr, "  split columns   #splits   cycles/split   variance/split   pre-proj/split   cycles/column   %%cycles\n");
             unsigned long long stot = 0;
             for (int b = 0; b < kPfBuckets; b++) stot += h[PF_N + 4 * b + 1];
