@@ -144,6 +144,7 @@ struct Common {
     uint32_t spec_width;           // heap entries examined per enqueue (0 = 2 * helpers + 2)
     uint32_t nroam;                // roaming helpers (after the teams): serve every job's queue
     int var_v3;                    // split variances on variance_split_v3 (ALVRL_VAR_V3=0: the older engine)
+    int var_small;                 // splits of <= kSmallMax columns on variance_split_small (ALVRL_VAR_SMALL=0: off)
     int roam_on;                   // finished leaders and helpers roam too (scratch sized for Rmax)
     const SplitWs* roam_ws;        // [nroam] their scratch, sized for the largest job
     const uint32_t* roam_order;    // null: roam from the last job served; else scan jobs in this order
@@ -160,7 +161,7 @@ __device__ __forceinline__ void trace(const Common& cm, uint32_t phase, uint32_t
 }
 // team counters
 enum { TS_ENQ, TS_HSTART, TS_HDONE, TS_COMMIT, TS_STEAL, TS_WAIT_TMO, TS_OWN, TS_IDLE_EXIT, TS_LSIDE,
-       TS_HIDLE, TS_RIDLE, TS_HBUSY, TS_RBUSY, TS_N };   // *IDLE/*BUSY: wall ticks (100 MHz) summed
+       TS_HIDLE, TS_RIDLE, TS_HBUSY, TS_RBUSY, TS_ACQ, TS_REL, TS_N };   // *IDLE/*BUSY: wall ticks (100 MHz) summed
 __device__ __forceinline__ void tcount(const Common& cm, int k)
 {
     if (cm.tstat) atomicAdd(&cm.tstat[k], 1ull);
@@ -173,7 +174,7 @@ __device__ __forceinline__ void tadd(const Common& cm, int k, unsigned long long
 // Phase timer of lane 0 (s_memtime deltas summed over jobs).
 enum { PF_COLW, PF_INIT, PF_UNCL, PF_WSAMP, PF_DIR, PF_PROJ, PF_SORT, PF_CVF, PF_CVR, PF_ARGMIN,
        PF_CTRL, PF_REPS, PF_V_COEF, PF_V_REC, PF_V_RED, PF_P_STAGE, PF_P_COMP, PF_V_OWN, PF_V_CW,
-       PF_V_ISSUE, PF_V_DATA, PF_T_HEAP, PF_T_ENQ, PF_T_WAIT, PF_T_SIDE, PF_T_COMMIT,
+       PF_V_ISSUE, PF_V_DATA, PF_T_HEAP, PF_T_ENQ, PF_T_WAIT, PF_T_SIDE, PF_T_COMMIT, PF_T_SNAP, PF_T_STATE,
        PF_NSPLIT, PF_SPLITCOLS, PF_N };
 static const char* kPfNames[PF_N] = {"column weights", "initial clusters", "unclustered var",
                                      "split: centres", "split: direction", "split: projections",
@@ -187,7 +188,7 @@ static const char* kPfNames[PF_N] = {"column weights", "initial clusters", "uncl
                                      " coef wave 193-256 rows: chain", " coef wave 193-256 rows: block 3",
                                      " coef wave 193-256 rows: (reduce)", " coef wave 193-256 rows: (flush)",
                                      "ctrl: heap pop/snapshot", "ctrl: enqueue", "ctrl: wait for helper",
-                                     "ctrl: side splits", "ctrl: commit",
+                                     "ctrl: side splits", "ctrl: commit", "ctrl: snapshot", "ctrl: state check",
                                      "#splits", "#split columns"};
 constexpr int kPfSmall = 2;   // split-phase table of small splits: m < 64, 64 <= m < 256
 struct Prof {
@@ -1475,6 +1476,137 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
     __syncthreads();
 }
 
+// The two passes of a small split (m <= kSmallMax columns, R <= 256 rows) in
+// one step, without the chunk pipeline of variance_split_v3: waves 0-3 run
+// the forward pass over row blocks 0-3, waves 4-7 the reverse one.  Wave 0
+// (4) forms its pass's coefficients for all m columns (the running weight
+// total in column order, one lane per column), every row wave then runs the
+// recurrence over all m columns (its entries 8 columns ahead) and reduces
+// each column's two prefix terms over its 64 rows with the halving tree
+// (tree16_transposed); the block totals are added in ascending block order
+// (wsum_blk).  The same IEEE operations in the same order as the oracle's
+// cluster_variance and variance_split_v3, so the prefixes are bit-identical.
+// Outputs stay in LDS: out[0..3][c] = fsu, fsi, feu, fei (prefix c of the
+// forward / reverse pass; the forward u of prefix 0 is 0).
+constexpr uint32_t kSmallMax = 256;
+constexpr uint32_t kSmallCoefBytes = 2u * 7u * kSmallMax * 8u;
+constexpr uint32_t kSmallVrlBytes = 2u * kSmallMax * 4u;
+constexpr uint32_t kSmallQBytes = 2u * kSmallMax * 2u * 4u * 8u;
+constexpr uint32_t kSmallOutOff = kSmallCoefBytes + kSmallVrlBytes + kSmallQBytes;
+static_assert(kSmallOutOff + 4u * kSmallMax * 4u <= kPoolBytes, "small split engine exceeds the LDS pool");
+__device__ __forceinline__ const float* small_out(const unsigned char* pool) { return reinterpret_cast<const float*>(pool + kSmallOutOff); }
+__device__ __noinline__ void variance_split_small(const JobDev& J, const Common& cm, Ctl& C, const uint32_t* base,
+                                                  uint32_t m, unsigned char* pool)
+{
+    const uint32_t R = J.nrows, NB = (R + 63) / 64;
+    const int tid = threadIdx.x, wv = tid >> 6;
+    const uint32_t lane = (uint32_t)(tid & 63);
+    const int g = wv >> 2;                              // 0: forward, 1: reverse
+    const uint32_t blk = (uint32_t)(wv & 3);
+    auto* const coef = lp(reinterpret_cast<double*>(pool));                          // [g][7][kSmallMax]
+    auto* const vr = lp(reinterpret_cast<uint32_t*>(pool + kSmallCoefBytes));        // [g][kSmallMax]
+    auto* const Q = lp(reinterpret_cast<double*>(pool + kSmallCoefBytes + kSmallVrlBytes));   // [g][c][h][blk]
+    auto* const out = lp(reinterpret_cast<float*>(pool + kSmallOutOff));             // [g * 2 + h][c]
+    auto* const cg = coef + (size_t)g * 7 * kSmallMax;
+    auto* const vg = vr + (size_t)g * kSmallMax;
+    if (blk == 0) {
+        // chunk_coefs (:1075-1085): W before / after each column's weight
+        double W = 0.0;
+        for (uint32_t c0 = 0; c0 < m; c0 += 64) {
+            const uint32_t c = c0 + lane;
+            const bool has = c < m;
+            const uint32_t i = has ? c : m - 1;
+            const uint32_t v = gp(base)[g == 0 ? i : m - 1 - i];
+            const double w = (double)gp(J.colw)[v];
+            const uint32_t n = min(64u, m - c0);
+            double Wo = 0.0, Wn = 0.0;
+            for (uint32_t k = 0; k < n; k++) {
+                const double wk = readlane_d(w, k);
+                const bool me = lane == k;
+                Wo = me ? W : Wo;
+                W = W + wk;
+                Wn = me ? W : Wn;
+            }
+            if (has) {
+                if (!isfinite(w) || w <= 0) C.err = 1;
+                const double rw = 1.0 / w;
+                cg[c] = w;
+                cg[kSmallMax + c] = Wo;
+                cg[2 * kSmallMax + c] = (Wn * Wn) / (Wo * Wo);
+                cg[3 * kSmallMax + c] = (rw + 1.0 / Wo);
+                cg[4 * kSmallMax + c] = rw;
+                cg[5 * kSmallMax + c] = Wn;
+                cg[6 * kSmallMax + c] = 1.0 / Wn;
+                vg[c] = v;
+            }
+        }
+    }
+    __syncthreads();
+    if (blk < NB) {
+        const bool valid = blk * 64 + lane < R;
+        const uint32_t r = min(blk * 64 + lane, R - 1);
+        const RowRef rr = row_ref(J, r);
+        const double lw = J.locw[r];
+        const float2* const Rt = cm.Rt + rr.base;
+        const size_t rs = rr.stride;
+        double sum = 0.0, M = 0.0, V = 0.0;
+        float2 bufA[kCH], bufB[kCH];
+        auto load = [&](uint32_t c0, float2* d) {
+#pragma unroll
+            for (int q = 0; q < kCH; q++) d[q] = ldg2(Rt, (size_t)vg[min(c0 + (uint32_t)q, m - 1)] * rs);
+        };
+        auto chunk = [&](uint32_t c0, const float2* cur) {
+            double tv[2 * kCH];
+#pragma unroll
+            for (int q = 0; q < kCH; q++) {
+                const uint32_t c = c0 + (uint32_t)q;
+                if (c < m) {
+                    const double x = (double)cur[q].x;
+                    const double tmp = cg[c] * sum - cg[kSmallMax + c] * x;
+                    if (c > 0) M = cg[2 * kSmallMax + c] * M + cg[3 * kSmallMax + c] * (tmp * tmp);
+                    V = V + (double)cur[q].y * cg[4 * kSmallMax + c];
+                    sum = sum + x;
+                    tv[2 * q] = lw * (M * cg[6 * kSmallMax + c]);
+                    tv[2 * q + 1] = lw * (V * cg[5 * kSmallMax + c]);
+                } else {
+                    tv[2 * q] = 0.0; tv[2 * q + 1] = 0.0;
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < 2 * kCH; i++) tv[i] = valid ? tv[i] : 0.0;
+            const double z = tree16_transposed(tv, lane);
+            if ((lane & 3) == 0) {
+                const uint32_t h = lane >> 5, c = 4 * ((lane >> 2) & 1) + 2 * ((lane >> 3) & 1) + ((lane >> 4) & 1);
+                if (c0 + c < m) Q[(((size_t)g * kSmallMax + c0 + c) * 2 + h) * 4 + blk] = z;
+            }
+        };
+        load(0, bufA);
+        for (uint32_t c0 = 0; c0 < m; c0 += 2 * kCH) {
+            if (c0 + kCH < m) load(c0 + kCH, bufB);
+            chunk(c0, bufA);
+            if (c0 + kCH >= m) break;
+            if (c0 + 2 * kCH < m) load(c0 + 2 * kCH, bufA);
+            chunk(c0 + kCH, bufB);
+        }
+    }
+    __syncthreads();
+    // block totals in ascending block order (wsum_blk), as floats
+    VarGroup* const vgrp = C.vg;
+    for (uint32_t t = (uint32_t)tid; t < 4 * m; t += kThreads) {
+        const uint32_t gh = t / m, c = t - gh * m, gg = gh >> 1, h = gh & 1;
+        const auto* q = Q + (((size_t)gg * kSmallMax + c) * 2 + h) * 4;
+        double acc = q[0];
+        for (uint32_t b = 1; b < NB; b++) acc = acc + q[b];
+        const float f = (h == 0 && c == 0) ? 0.0f : (float)acc;
+        out[gh * kSmallMax + c] = f;
+        if (c == m - 1) {
+            if (h == 0) vgrp[gg].res_u = f; else vgrp[gg].res_i = f;
+            if (!isfinite(f) || f < 0) C.err = 1;
+        }
+    }
+    __syncthreads();
+}
+
 __device__ void variance_passes(const JobDev& J, const Common& cm, Ctl& C, const uint32_t* base, uint32_t m,
                                 int npass, float* fu0, float* fi0, float* fu1, float* fi1, unsigned char* pool,
                                 Prof* pf = nullptr)
@@ -1926,15 +2058,25 @@ __device__ void split(const JobDev& J, const Common& cm, Ctl& C, uint32_t begin,
     __syncthreads();
     pf.mark(PF_SORT);
     const long long hv0 = pf.p && tid == 0 ? (long long)clock64() : 0;
-    variance_passes(J, cm, C, J.vrls + begin, m, 2, J.fsu, J.fsi, J.feu, J.fei,
-                    reinterpret_cast<unsigned char*>(lds), &pf);
+    const bool small = cm.var_small && m <= kSmallMax && R <= 256;
+    unsigned char* const pool = reinterpret_cast<unsigned char*>(lds);
+    if (small)
+        variance_split_small(J, cm, C, J.vrls + begin, m, pool);
+    else
+        variance_passes(J, cm, C, J.vrls + begin, m, 2, J.fsu, J.fsi, J.feu, J.fei, pool, &pf);
     if (pf.p && tid == 0) hbv = (long long)clock64() - hv0;
     pf.mark(PF_CVF);
+    // the prefix variances: fsu/fsi of the forward pass, feu/fei of the reverse
+    const auto* const so = lp(small_out(pool));
+    auto pref = [&](int k, uint32_t i) -> float {
+        if (small) return so[k * kSmallMax + i];
+        return k == 0 ? fsuR[i] : k == 1 ? fsiR[i] : k == 2 ? feuR[i] : feiR[i];
+    };
     // argmin over split position (:664-675)
     float bv = INFINITY;
     uint32_t bi = 0xFFFFFFFFu;
     for (uint32_t i = 1 + tid; i < m; i += kThreads) {
-        const float v = fsuR[i - 1] + fsiR[i - 1] + feuR[m - 1 - i] + feiR[m - 1 - i];
+        const float v = pref(0, i - 1) + pref(1, i - 1) + pref(2, m - 1 - i) + pref(3, m - 1 - i);
         if (v < bv) { bv = v; bi = i; }
     }
 #pragma unroll
@@ -1953,16 +2095,16 @@ __device__ void split(const JobDev& J, const Common& cm, Ctl& C, uint32_t begin,
         if (!commit) {
             SplitRes r{idx, Cs.err | (idx == 0xFFFFFFFFu ? 1 : 0), 0.0f, 0.0f, 0.0f, 0.0f};
             if (idx != 0xFFFFFFFFu) {
-                r.fsu = fsuR[idx - 1]; r.fsi = fsiR[idx - 1];
-                r.feu = feuR[m - 1 - idx]; r.fei = feiR[m - 1 - idx];
+                r.fsu = pref(0, idx - 1); r.fsi = pref(1, idx - 1);
+                r.feu = pref(2, m - 1 - idx); r.fei = pref(3, m - 1 - idx);
             }
             *res = r;
         } else if (idx == 0xFFFFFFFFu) {
             Cs.err = 1;
         } else {
             const uint32_t s = begin + idx;
-            add_cluster(J, C, begin, s, fsuR[idx - 1], fsiR[idx - 1]);
-            add_cluster(J, C, s, end, feuR[m - 1 - idx], feiR[m - 1 - idx]);
+            add_cluster(J, C, begin, s, pref(0, idx - 1), pref(1, idx - 1));
+            add_cluster(J, C, s, end, pref(2, m - 1 - idx), pref(3, m - 1 - idx));
         }
     }
     __syncthreads();
@@ -2166,8 +2308,10 @@ __device__ void spec_split(const JobDev& J0, const JobDev& Jw, const Common& cm,
     e &= ~kQSpecBit;
     // one agent acquire for the CU (its L1), complete before the barrier
     if (tid < 64) {
+        const unsigned long long ta = wall();
         fence_acq();
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (tid == 0) tadd(cm, TS_ACQ, wall() - ta);
     }
     __syncthreads();
     if (!in_spec)
@@ -2183,8 +2327,10 @@ __device__ void spec_split(const JobDev& J0, const JobDev& Jw, const Common& cm,
     __syncthreads();
     if (tid == 0) {
         C.err = err_saved;
+        const unsigned long long tr = wall();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        tadd(cm, TS_REL, wall() - tr);
         __hip_atomic_store(&T.state[b], ((unsigned long long)e << 3) | kStDone, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -2224,7 +2370,7 @@ __device__ void split_team(const JobDev& J, const Common& cm, Ctl& C, uint32_t b
         C.tmode = mode;
     }
     __syncthreads();
-    pf.mark(PF_T_ENQ);
+    pf.mark(PF_T_STATE);
     while (true) {
         const int tm = C.tmode;
         __syncthreads();   // every thread has read tmode before thread 0 rewrites it
@@ -2821,7 +2967,9 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
                         C.stop = lower_bound(C, N, J.pixel_under) >= best;
                     }
                     __syncthreads();
+                    pf.mark(PF_T_HEAP);
                     if (C.do_snap) snapshot(J, C);
+                    pf.mark(PF_T_SNAP);
                     if (C.stop) break;
                 }
                 stop_team(J, cm);
@@ -3232,6 +3380,8 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
     {
         const char* vv = std::getenv("ALVRL_VAR_V3");
         cm.var_v3 = !(vv && vv[0] == '0');
+        const char* vs = std::getenv("ALVRL_VAR_SMALL");
+        cm.var_small = !(vs && vs[0] == '0');
     }
     const char* pe = std::getenv("ALVRL_REFINE_PROFILE");
     if (pe && pe[0] == '1' && hipMalloc(&cm.prof, kPfTotal * 8) == hipSuccess)
@@ -3306,7 +3456,7 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
     if (entries) *entries = h_entries;
     if (cm.tstat) {
         unsigned long long h[TS_N];
-        if (hipMemcpy(h, cm.tstat, sizeof(h), hipMemcpyDeviceToHost) == hipSuccess)
+        if (hipMemcpy(h, cm.tstat, sizeof(h), hipMemcpyDeviceToHost) == hipSuccess) {
             std::fprintf(stderr, "[refine team] G=%u roam=%u jobs=%u enqueued %llu helper start %llu done %llu | leader "
                          "commit %llu steal %llu wait-timeout %llu own %llu side %llu | helper idle exits %llu\n",
                          G, nroam, njobs, h[TS_ENQ], h[TS_HSTART], h[TS_HDONE], h[TS_COMMIT], h[TS_STEAL],
@@ -3314,6 +3464,10 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
             std::fprintf(stderr, "[refine team] wall ms summed: team helpers idle %.0f busy %.0f | roamers (incl. "
                          "finished helpers) idle %.0f busy %.0f\n", h[TS_HIDLE] * 1e-5, h[TS_HBUSY] * 1e-5,
                          h[TS_RIDLE] * 1e-5, h[TS_RBUSY] * 1e-5);
+            std::fprintf(stderr, "[refine team] speculative splits' hand-offs, wall ms summed: acquire %.1f, release %.1f "
+                         "(%.2f / %.2f us each)\n", h[TS_ACQ] * 1e-5, h[TS_REL] * 1e-5,
+                         h[TS_HSTART] ? h[TS_ACQ] * 1e-2 / h[TS_HSTART] : 0.0, h[TS_HSTART] ? h[TS_REL] * 1e-2 / h[TS_HSTART] : 0.0);
+        }
         hipFree(cm.tstat);
         if (cm.jtime) {
             std::vector<unsigned long long> jt((size_t)njobs * 3);
