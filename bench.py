@@ -75,7 +75,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-row-stride", type=int, default=64,
                     help="CPU baseline sample: every n-th image row")
-    ap.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "r01_pmc_traffic.json"),
+    ap.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "r02_pmc_traffic.json"),
                     help="per-launch HBM bytes of the dominant kernel from a rocprofv3 --pmc pass")
     return ap.parse_args()
 

@@ -5,8 +5,9 @@
 
 FETCH_SIZE / WRITE_SIZE are kB per dispatch.  MI355X_MICROARCH.md (HBM): on
 gfx950 FETCH_SIZE reports half the bytes of 16-B-per-lane coalesced streaming
-reads, so the read bytes are doubled; the refinement's 8-B-per-lane loads are
-an access width the guide leaves uncalibrated (stated in the record).  The
+reads, so the read bytes are doubled; tools/pmc_calib.hip confirms the same
+factor for the refinement's 8-B-per-lane loads (1 GiB read: 536.9 MB
+reported) and shows that an agent-scope atomic counts 64 B of WRITE_SIZE.  The
 bench reads the "hbm_bytes_per_launch" of the record whose config and
 kernel_key match."""
 import csv
@@ -52,9 +53,8 @@ def main():
             "config": cfg, "kernel_key": key, "launches": len(fetch[key]),
             "source": "rocprofv3 --kernel-trace --pmc FETCH_SIZE / WRITE_SIZE, separate passes",
             "FETCH_SIZE_bytes": fb, "WRITE_SIZE_bytes": wb,
-            "correction": "FETCH_SIZE x2 (gfx950 tallies 128-B requests at 64 B, MI355X_MICROARCH.md HBM)"
-                          + ("; k_refine loads 8 B per lane, a width the guide leaves uncalibrated"
-                             if key == "refine" else ""),
+            "correction": "FETCH_SIZE x2 (gfx950 tallies 128-B requests at 64 B, MI355X_MICROARCH.md HBM;"
+                          " the same factor for 8-B-per-lane loads, tools/pmc_calib.hip)",
             "hbm_bytes_per_launch": 2.0 * fb + wb,
         })
     with open(dst, "w") as f:
