@@ -58,7 +58,8 @@ struct HostJob {
 int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, uint32_t seed,
                 uint32_t pass, uint32_t njobs, const HostJob* jobs, const uint32_t* init_vrls,
                 const uint32_t* init_off, uint32_t ninit, uint32_t* out_off, uint32_t* out_reps,
-                float* out_w, int* out_refined, float* ms, unsigned long long* entries, std::string* err);
+                float* out_w, int* out_refined, float* ms, unsigned long long* entries, std::string* err,
+                RefineArenas* cache);
 }  // namespace alvrl
 
 using namespace alvrl;
@@ -83,6 +84,7 @@ struct alvrl_ctx {
     float* d_weights = nullptr;
     uint32_t* d_fb_reps = nullptr;
     float* d_fb_w = nullptr;
+    uint32_t cap_slices = 0, cap_rep = 0, cap_fb = 0;   // grow-only: a prepass re-sets them every pass
     bool clusters_set = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
@@ -92,6 +94,7 @@ struct alvrl_ctx {
     BvhNode* d_bvh_nodes = nullptr;
     float* d_bvh_tris = nullptr;
     uint32_t* d_bvh_ids = nullptr;
+    RefineArenas refine_arenas;   // alvrl_refine's device scratch, reused across passes
     std::mutex mu;
 };
 
@@ -169,6 +172,7 @@ static void free_clusters(alvrl_ctx* c)
     hipFree(c->d_fb_reps); hipFree(c->d_fb_w);
     c->d_slice_off = nullptr; c->d_reps = nullptr; c->d_weights = nullptr;
     c->d_fb_reps = nullptr; c->d_fb_w = nullptr;
+    c->cap_slices = c->cap_rep = c->cap_fb = 0;
     c->clusters_set = false;
 }
 
@@ -180,6 +184,7 @@ ALVRL_API void alvrl_ctx_destroy(alvrl_ctx* c)
     hipFree(c->d_soa); hipFree(c->d_vrl); hipFree(c->d_counter);
     free_clusters(c);
     free_occluders(c);
+    c->refine_arenas.release();
     if (c->ev0) hipEventDestroy(c->ev0);
     if (c->ev1) hipEventDestroy(c->ev1);
     if (c->stream) hipStreamDestroy(c->stream);
@@ -275,21 +280,36 @@ ALVRL_API int alvrl_set_clusters(alvrl_ctx* c, uint32_t nslices, const uint32_t*
         if (reps[i] >= c->nvrl) return fail(ALVRL_ERR_INVALID, "alvrl_set_clusters: representative out of range");
     for (uint32_t i = 0; i < n_fb; i++)
         if (fb_reps[i] >= c->nvrl) return fail(ALVRL_ERR_INVALID, "alvrl_set_clusters: fall-back representative out of range");
-    free_clusters(c);
-    HIPCHK(hipMalloc(&c->d_slice_off, sizeof(uint32_t) * (nslices + 1)));
-    HIPCHK(hipMalloc(&c->d_reps, sizeof(uint32_t) * std::max(nrep, 1u)));
-    HIPCHK(hipMalloc(&c->d_weights, sizeof(float) * std::max(nrep, 1u)));
-    HIPCHK(hipMalloc(&c->d_fb_reps, sizeof(uint32_t) * std::max(n_fb, 1u)));
-    HIPCHK(hipMalloc(&c->d_fb_w, sizeof(float) * std::max(n_fb, 1u)));
-    if (nslices) HIPCHK(hipMemcpy(c->d_slice_off, slice_off, sizeof(uint32_t) * (nslices + 1), hipMemcpyHostToDevice));
+    c->clusters_set = false;
+    if (nslices + 1 > c->cap_slices) {
+        hipFree(c->d_slice_off); c->d_slice_off = nullptr; c->cap_slices = 0;
+        HIPCHK(hipMalloc(&c->d_slice_off, sizeof(uint32_t) * (nslices + 1)));
+        c->cap_slices = nslices + 1;
+    }
+    if (std::max(nrep, 1u) > c->cap_rep) {
+        hipFree(c->d_reps); hipFree(c->d_weights); c->d_reps = nullptr; c->d_weights = nullptr; c->cap_rep = 0;
+        const uint32_t cap = std::max(nrep, 1u) + std::max(nrep, 1u) / 4;
+        HIPCHK(hipMalloc(&c->d_reps, sizeof(uint32_t) * cap));
+        HIPCHK(hipMalloc(&c->d_weights, sizeof(float) * cap));
+        c->cap_rep = cap;
+    }
+    if (std::max(n_fb, 1u) > c->cap_fb) {
+        hipFree(c->d_fb_reps); hipFree(c->d_fb_w); c->d_fb_reps = nullptr; c->d_fb_w = nullptr; c->cap_fb = 0;
+        HIPCHK(hipMalloc(&c->d_fb_reps, sizeof(uint32_t) * std::max(n_fb, 1u)));
+        HIPCHK(hipMalloc(&c->d_fb_w, sizeof(float) * std::max(n_fb, 1u)));
+        c->cap_fb = std::max(n_fb, 1u);
+    }
+    if (nslices)
+        HIPCHK(hipMemcpyAsync(c->d_slice_off, slice_off, sizeof(uint32_t) * (nslices + 1), hipMemcpyHostToDevice, c->stream));
     if (nrep) {
-        HIPCHK(hipMemcpy(c->d_reps, reps, sizeof(uint32_t) * nrep, hipMemcpyHostToDevice));
-        HIPCHK(hipMemcpy(c->d_weights, weights, sizeof(float) * nrep, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpyAsync(c->d_reps, reps, sizeof(uint32_t) * nrep, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipMemcpyAsync(c->d_weights, weights, sizeof(float) * nrep, hipMemcpyHostToDevice, c->stream));
     }
     if (n_fb) {
-        HIPCHK(hipMemcpy(c->d_fb_reps, fb_reps, sizeof(uint32_t) * n_fb, hipMemcpyHostToDevice));
-        HIPCHK(hipMemcpy(c->d_fb_w, fb_w, sizeof(float) * n_fb, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpyAsync(c->d_fb_reps, fb_reps, sizeof(uint32_t) * n_fb, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipMemcpyAsync(c->d_fb_w, fb_w, sizeof(float) * n_fb, hipMemcpyHostToDevice, c->stream));
     }
+    HIPCHK(hipStreamSynchronize(c->stream));   // the host buffers are the caller's
     c->nslices = nslices;
     c->n_fb = n_fb;
     c->clusters_set = true;
@@ -453,9 +473,10 @@ ALVRL_API int alvrl_refine(alvrl_ctx* c, const float* d_Rt, uint64_t ld, uint32_
     HIPCHK(hipSetDevice(c->cfg.device));
     std::string err;
     float ms = 0.0f;
+    std::lock_guard<std::mutex> g(c->mu);   // the context's refine scratch
     int rc = refine_jobs(pick(c, stream), d_Rt, ld, c->nvrl, c->P.seed, c->P.pass, njobs, hj.data(),
                          init_vrls, init_off, ninit, out_off, out_reps, out_weights, out_refined,
-                         &ms, &c->refine_entries, &err);
+                         &ms, &c->refine_entries, &err, &c->refine_arenas);
     c->refine_ms = ms;
     if (rc) return fail(rc, err);
     return ALVRL_OK;
@@ -489,9 +510,10 @@ ALVRL_API int alvrl_refine_members(alvrl_ctx* c, const float* d_Rt, uint64_t ld,
     std::string err;
     float ms = 0.0f;
     *n_clusters = 0;
+    std::lock_guard<std::mutex> g(c->mu);   // the context's refine scratch
     int rc = refine_jobs(pick(c, stream), d_Rt, ld, c->nvrl, c->P.seed, c->P.pass, 1, &hj, init_vrls,
                          init_off, ninit, off.data(), reps.data(), w.data(), out_refined, &ms,
-                         &c->refine_entries, &err);
+                         &c->refine_entries, &err, &c->refine_arenas);
     c->refine_ms = ms;
     if (rc) return fail(rc, err);
     (void)nv;

@@ -138,6 +138,8 @@ struct alvrl_integrator {
     std::vector<std::vector<double>> job_locw;
     // cluster info (vrlClusterInfo)
     std::vector<uint32_t> slice_off, reps, fb_reps;
+    std::vector<uint32_t> rep_buf;          // alvrl_refine's output buffers, reused across passes
+    std::vector<float> w_buf;
     std::vector<float> weights, fb_w;
     // render cache per (rank, world)
     uint32_t cache_rank = 0xFFFFFFFFu, cache_world = 0, cache_mode = 0;
@@ -517,8 +519,13 @@ struct alvrl_integrator {
             j.stage_sample = stage_slice_sample(s);
         }
         job_init = init; job_init_off = init_off; job_slices = mine; job_rows = lrows; job_locw = lw;
-        std::vector<uint32_t> off(nm + 1), rep((size_t)nm * nv + 1);
-        std::vector<float> w((size_t)nm * nv + 1);
+        // output lists sized for every VRL in every job: kept between passes
+        // (value-initialising 2 x 40 MB per pass cost milliseconds)
+        std::vector<uint32_t> off(nm + 1);
+        if (rep_buf.size() < (size_t)nm * nv + 1) rep_buf.resize((size_t)nm * nv + 1);
+        if (w_buf.size() < (size_t)nm * nv + 1) w_buf.resize((size_t)nm * nv + 1);
+        std::vector<uint32_t>& rep = rep_buf;
+        std::vector<float>& w = w_buf;
         std::vector<int> refined(nm + 1);
         const double t0 = now_ms() - st.ms_refine;
         if (nm)

@@ -3110,11 +3110,40 @@ struct HostJob {
 
 // Runs every clustering job on the device (one workgroup each) and copies the
 // representatives back.  Returns 0 or an ALVRL_ERR_* code with *err set.
+// Device scratch of refine_jobs kept by the caller between calls (grow-only):
+// a ~1 GB hipMalloc / hipFree pair per prepass costs milliseconds of host time
+// on the critical path (hipFree also waits for the device).
+void RefineArenas::release()
+{
+    if (arena) (void)hipFree(arena);
+    if (tarena) (void)hipFree(tarena);
+    arena = tarena = nullptr;
+    arena_cap = tarena_cap = 0;
+}
+static hipError_t arena_get(char** buf, size_t* cap, size_t bytes, bool cached)
+{
+    if (cached && *buf && *cap >= bytes) return hipSuccess;
+    if (*buf) { (void)hipFree(*buf); *buf = nullptr; *cap = 0; }
+    const size_t want = cached ? bytes + bytes / 4 : bytes;   // slack for the next pass's sizes
+    hipError_t e = hipMalloc(buf, want);
+    if (e != hipSuccess && want != bytes) { (void)hipGetLastError(); e = hipMalloc(buf, bytes); if (e == hipSuccess) *cap = bytes; }
+    else if (e == hipSuccess) *cap = want;
+    if (e != hipSuccess) *buf = nullptr;
+    return e;
+}
+
 int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, uint32_t seed,
                 uint32_t pass, uint32_t njobs, const HostJob* jobs, const uint32_t* init_vrls,
                 const uint32_t* init_off, uint32_t ninit, uint32_t* out_off, uint32_t* out_reps,
-                float* out_w, int* out_refined, float* ms, unsigned long long* entries, std::string* err)
+                float* out_w, int* out_refined, float* ms, unsigned long long* entries, std::string* err,
+                RefineArenas* cache)
 {
+    RefineArenas local;
+    RefineArenas& ar = cache ? *cache : local;
+    struct Finally {
+        RefineArenas* l;
+        ~Finally() { if (l) l->release(); }
+    } fin{cache ? nullptr : &local};
     if (ms) *ms = 0.0f;
     if (entries) *entries = 0;
     out_off[0] = 0;
@@ -3177,9 +3206,9 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
                    align_up((size_t)(ninit + 1) * 4) + align_up((size_t)njobs * sizeof(JobDev)) +
                    align_up((size_t)njobs * 12) + 2 * align_up((size_t)njobs * N * 4) + align_up(8);
     for (uint32_t j = 0; j < njobs; j++) { job_off[j] = total; total += job_bytes(jobs[j]); }
-    char* arena = nullptr;
-    hipError_t e = hipMalloc(&arena, total);
+    hipError_t e = arena_get(&ar.arena, &ar.arena_cap, total, cache != nullptr);
     if (e != hipSuccess) { *err = std::string("alvrl_refine: hipMalloc: ") + hipGetErrorString(e); return 4; }
+    char* const arena = ar.arena;
     size_t o = 0;
     unsigned long long* d_roff = (unsigned long long*)(arena + o); o += align_up(rows_total * 8);
     uint32_t* d_rstride = (uint32_t*)(arena + o); o += align_up(rows_total * 4);
@@ -3199,12 +3228,12 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
         const HostJob& H = jobs[j];
         for (uint32_t r = 0; r < H.nrows; r++) {
             if (H.row_off) {
-                if (H.row_stride[r] == 0) { hipFree(arena); *err = "alvrl_refine: zero row stride"; return 1; }
+                if (H.row_stride[r] == 0) { *err = "alvrl_refine: zero row stride"; return 1; }
                 h_roff[row_off[j] + r] = H.row_off[r];
                 h_rstride[row_off[j] + r] = H.row_stride[r];
             } else {
-                if (H.rows[r] >= ld) { hipFree(arena); *err = "alvrl_refine: row id out of range"; return 1; }
-                if (ld > 0xFFFFFFFFull) { hipFree(arena); *err = "alvrl_refine: ld too large"; return 1; }
+                if (H.rows[r] >= ld) { *err = "alvrl_refine: row id out of range"; return 1; }
+                if (ld > 0xFFFFFFFFull) { *err = "alvrl_refine: ld too large"; return 1; }
                 h_roff[row_off[j] + r] = H.rows[r];
                 h_rstride[row_off[j] + r] = (uint32_t)ld;
             }
@@ -3265,7 +3294,10 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
         for (uint32_t j = 0; j < njobs; j++) tbytes += team_fixed + (size_t)(G - 1) * helper_bytes(roam_on ? Rmax : jobs[j].nrows);
         tbytes += align_up((size_t)nroam * sizeof(SplitWs)) + (size_t)nroam * helper_bytes(Rmax);
         tbytes += align_up((size_t)njobs * 4);   // roam order
-        if (hipMalloc(&tarena, tbytes) != hipSuccess) { (void)hipGetLastError(); tarena = nullptr; G = 1; nroam = 0; }
+        if (arena_get(&ar.tarena, &ar.tarena_cap, tbytes, cache != nullptr) != hipSuccess) {
+            (void)hipGetLastError(); G = 1; nroam = 0;
+        }
+        tarena = ar.tarena;
     }
     std::vector<SplitWs> h_ws(G > 1 ? (size_t)njobs * (G - 1) : 0), h_rws(nroam);
     SplitWs* d_rws = nullptr;
@@ -3560,8 +3592,7 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
         if (e == hipSuccess && ms) e = hipEventElapsedTime(ms, e0, e1);
     }
     if (e != hipSuccess) { rc = 3; *err = std::string("alvrl_refine: ") + hipGetErrorString(e); }
-    hipFree(arena);
-    if (tarena) hipFree(tarena);
+
     if (cm.trace) hipHostFree(cm.trace);
     if (e0) hipEventDestroy(e0);
     if (e1) hipEventDestroy(e1);

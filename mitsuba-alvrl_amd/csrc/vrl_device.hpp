@@ -535,4 +535,12 @@ __device__ __forceinline__ void integrate_vrl(const DevParams& P, const RecPre& 
     if (WANT_STATS) { *mean_out = mean_acc; *var_out = var_acc; }
 }
 
+// refine_jobs' device scratch, kept by a context between calls (refine.hip)
+struct RefineArenas {
+    char* arena = nullptr;
+    char* tarena = nullptr;
+    size_t arena_cap = 0, tarena_cap = 0;
+    void release();
+};
+
 }  // namespace alvrl
