@@ -456,6 +456,49 @@ def test_refine_c4_scale(oracle, gpu_ok, props):
     it.close()
 
 
+def test_context_reuse_across_passes(gpu_ok):
+    """One integrator re-used over passes whose sizes grow and shrink (VRL
+    counts 3000 -> 9000 -> 3000, slice counts 40 -> 25): alvrl_refine's device
+    scratch and the cluster lists' device buffers are kept by the context
+    between passes (grow-only), so every pass must give the cluster lists and
+    the frame of a fresh integrator bit for bit."""
+    import torch
+    import alvrl
+    w, h = 256, 192
+    scene = alvrl.scene_default(w, h)
+    sets = [alvrl.trace_vrls(scene, n, seed=SEED_VRL + n) for n in (3000, 9000, 3000)]
+    props = [f"targetNumSlices=40;seed={SEED_RNG}", f"targetNumSlices=40;seed={SEED_RNG}",
+             f"targetNumSlices=25;seed={SEED_RNG}"]
+
+    def run(it, k, pass_):
+        it.prepass(pass_)
+        fb = torch.zeros(w * h * 3, dtype=torch.float32, device="cuda")
+        it.render(fb)
+        torch.cuda.synchronize()
+        return it.clusters(), fb.cpu().numpy()
+
+    fresh = []
+    for k, (vrls, pc) in enumerate(sets):
+        it = alvrl.Integrator(props[k], device=0)
+        it.set_vrls(vrls, pc)
+        it.preprocess(scene)
+        fresh.append(run(it, k, k + 1))
+        it.close()
+    it = alvrl.Integrator(props[0], device=0)
+    it.preprocess(scene)
+    for k, (vrls, pc) in enumerate(sets):
+        if k == 2:   # fewer slices: a new integrator state, the same context scratch is not shared
+            it.close()
+            it = alvrl.Integrator(props[k], device=0)
+            it.preprocess(scene)
+        it.set_vrls(vrls, pc)
+        cl, fb = run(it, k, k + 1)
+        for key in cl:
+            assert np.array_equal(cl[key].view(np.uint32), fresh[k][0][key].view(np.uint32)), (k, key)
+        assert np.array_equal(fb.view(np.uint32), fresh[k][1].view(np.uint32)), k
+    it.close()
+
+
 def test_cluster_info_checkpoint(gpu_ok, tmp_path):
     """vrlClusterInfo out of one integrator and into another (the resource the
     reference ships to remote workers, vrlIntegrator.cpp:29-101, :353-354):
