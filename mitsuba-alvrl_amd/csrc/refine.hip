@@ -3188,6 +3188,9 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
         const char* re = std::getenv("ALVRL_REFINE_ROAM");
         if (cap > 1 && nb > 0 && (!re || std::atoi(re) != 0) && (uint32_t)(nb * ncu) > njobs * G)
             nroam = std::min<uint32_t>((uint32_t)(nb * ncu) - njobs * G, 1024u);
+        // ALVRL_REFINE_NROAM=n: at most n roaming helpers of their own (the CUs
+        // left to other work launched beside the refinement)
+        if (const char* nr = std::getenv("ALVRL_REFINE_NROAM")) nroam = std::min<uint32_t>(nroam, (uint32_t)std::max(0, std::atoi(nr)));
     }
     const bool team_on = G > 1 || nroam > 0;
     // finished leaders and helpers roam too: their split scratch is sized for
@@ -3352,6 +3355,11 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
     cm.njobs = njobs; cm.team = G;
     cm.nroam = nroam; cm.roam_ws = d_rws;
     cm.roam_on = roam_on && tarena ? 1 : 0;
+    {
+        // ALVRL_FINISHED_ROAM=0: finished leaders and helpers exit instead of roaming
+        const char* fr = std::getenv("ALVRL_FINISHED_ROAM");
+        if (fr && fr[0] == '0') cm.roam_on = 0;
+    }
     {
         const char* sw = std::getenv("ALVRL_SPEC_WIDTH");
         cm.spec_width = sw ? (uint32_t)std::max(1, std::atoi(sw)) : 32u;   // C4 refine sweeps (tools/env_sweep.sh), min 2: width 24 401 ms; 32 398 (no queueing after the pop)
