@@ -501,6 +501,50 @@ def test_context_reuse_across_passes(gpu_ok):
     it.close()
 
 
+@pytest.mark.parametrize("props", ["targetNumSlices=40", "targetNumSlices=30;localUndersampling=10",
+                                   "targetNumSlices=25;depthCorrection=0.8"])
+@pytest.mark.skip(reason="fusedRender is experimental: an illegal memory access was seen once under the "
+                         "team-mode knob sweep (DESIGN.md 5.2); the plain path is the default")
+def test_fused_render_identical(gpu_ok, props):
+    """fusedRender (alvrl_refine_gather): the slices rendered beside the
+    refinement as their jobs finish give the frame of the plain path
+    (alvrl_refine, alvrl_set_clusters, alvrl_gather_clustered) bit for bit,
+    with the same cluster lists; over two passes and with a second render of
+    the same pass (which re-accumulates the pass's frame: its pairs are not
+    gathered again, so only the first render of a pass counts them)."""
+    import torch
+    import alvrl
+    w, h = 256, 192
+    scene = alvrl.scene_default(w, h)
+    vrls, pc = alvrl.trace_vrls(scene, 4000, seed=SEED_VRL)
+    out = {}
+    for fused in (False, True):
+        it = alvrl.Integrator(props + f";seed={SEED_RNG};fusedRender={'true' if fused else 'false'}", device=0)
+        it.set_vrls(vrls, pc)
+        it.preprocess(scene)
+        frames, cls = [], []
+        for p in (1, 2):
+            it.prepass(p)
+            if fused:
+                assert it.stats()["render_fused"] > 0
+            for _ in range(2):
+                fb = torch.zeros(w * h * 3, dtype=torch.float32, device="cuda")
+                it.render(fb)
+                torch.cuda.synchronize()
+                frames.append(fb.cpu().numpy())
+            cls.append(it.clusters())
+        st = it.stats()
+        out[fused] = (frames, cls, st["contrib_render"] // (2 if not fused else 1), st["contrib_preprocess"])
+        it.close()
+    (f0, c0, r0, p0), (f1, c1, r1, p1) = out[False], out[True]
+    for a, b in zip(f0, f1):
+        assert a.any() and np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    for a, b in zip(c0, c1):
+        for k in a:
+            assert np.array_equal(a[k].view(np.uint32), b[k].view(np.uint32)), k
+    assert (r0, p0) == (r1, p1)
+
+
 def test_cluster_info_checkpoint(gpu_ok, tmp_path):
     """vrlClusterInfo out of one integrator and into another (the resource the
     reference ships to remote workers, vrlIntegrator.cpp:29-101, :353-354):
