@@ -66,7 +66,7 @@ hipError_t launch_gather_ready(const Rec* recs, const uint32_t* ids, const WorkI
                                const SliceList* lists, uint32_t* ready, uint32_t* cursor,
                                const uint32_t* resident, uint32_t nresident, const DevParams& P,
                                float inv_pc, float* out, unsigned long long* counter,
-                               unsigned long long spin_ticks, uint32_t nblocks, hipStream_t s);
+                               unsigned long long spin_ticks, uint32_t nblocks, uint32_t nvrl, hipStream_t s);
 }  // namespace alvrl
 
 using namespace alvrl;
@@ -481,13 +481,14 @@ struct GatherArgs {
     unsigned long long* counter;
     unsigned long long spin_ticks;
     uint32_t nblocks;
+    uint32_t nvrl;
 };
 hipError_t launch_ready_gather(void* user, const SliceList* lists, uint32_t* ready, uint32_t* cursor,
                                const uint32_t* resident, uint32_t nresident, hipStream_t s)
 {
     const GatherArgs& a = *static_cast<const GatherArgs*>(user);
     return launch_gather_ready(a.recs, a.ids, a.items, a.slice_item_off, a.nslices, a.vp, lists, ready, cursor,
-                               resident, nresident, a.P, a.inv_pc, a.out, a.counter, a.spin_ticks, a.nblocks, s);
+                               resident, nresident, a.P, a.inv_pc, a.out, a.counter, a.spin_ticks, a.nblocks, a.nvrl, s);
 }
 }  // namespace
 
@@ -513,7 +514,7 @@ ALVRL_API int alvrl_refine_gather(alvrl_ctx* c, const float* d_Rt, uint64_t ld, 
     GatherArgs a{reinterpret_cast<const Rec*>(d_recs), d_rec_ids, reinterpret_cast<const WorkItem*>(d_items),
                  d_slice_item_off, njobs, c->d_vrl, c->P, 1.0f / (float)c->particle_count, d_out_rgb,
                  c->d_counter + 1, sp ? (unsigned long long)std::max(1, std::atoi(sp)) * 100000ull : 6000000000ull,
-                 (uint32_t)std::max(1, ncu) * 8u};
+                 (uint32_t)std::max(1, ncu) * 8u, c->nvrl};
     std::vector<uint32_t> claimed(njobs, 0), item_off(njobs + 1, 0);
     ReadyGather rg{launch_ready_gather, &a, c->stream2, 0, claimed.data()};
     rc = refine_impl(c, d_Rt, ld, njobs, jobs, init_vrls, init_off, ninit, out_off, out_reps, out_weights,

@@ -134,24 +134,37 @@ __device__ __forceinline__ void gather_item(const Rec* __restrict__ recs, const 
     const RecPre q = prepare_record(rec, P);
     const uint32_t rid = active ? (ids ? ids[r] : r) : 0u;
     float L0 = 0.0f, L1 = 0.0f, L2 = 0.0f;
-    if (q.medium) {
-        uint32_t vr = 0u, vw = 0u;
-        for (uint32_t i = 0; i < k; ++i) {
-            uint32_t v;
-            float w;
-            if (VL) {
+    if constexpr (VL) {
+        // the list is loaded by every lane of the wave and broadcast with
+        // v_readlane, so the walk runs on the whole wave (a lane outside the
+        // medium would leave its slot of the 64-entry block unloaded and the
+        // broadcast would read a stale register); lanes outside the medium
+        // compute nothing
+        const bool med = q.medium;
+        if (__ballot(med) != 0ull) {
+            uint32_t vr = 0u, vw = 0u;
+            for (uint32_t i = 0; i < k; ++i) {
                 if ((i & 63u) == 0u) {
                     const uint32_t j = min(i + lane, k - 1);
                     vr = __hip_atomic_load(lr + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     vw = __hip_atomic_load(reinterpret_cast<const uint32_t*>(lw) + j, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
                 }
-                v = (uint32_t)__builtin_amdgcn_readlane((int)vr, (int)(i & 63u));
-                w = __int_as_float(__builtin_amdgcn_readlane((int)vw, (int)(i & 63u)));
-            } else {
-                v = lr[i];
-                w = lw[i];
+                const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)vr, (int)(i & 63u));
+                const float w = __int_as_float(__builtin_amdgcn_readlane((int)vw, (int)(i & 63u)));
+                if (med) {
+                    const VrlPrep V = vp[v];
+                    float c[3], m, s;
+                    integrate_vrl<NVV, NVS, false, VIS>(P, q, V, rid, v, kDomGather, P.nvv, P.nvs, c, &m, &s);
+                    L0 += c[0] * w; L1 += c[1] * w; L2 += c[2] * w;
+                }
             }
+            L0 *= inv_pc; L1 *= inv_pc; L2 *= inv_pc;
+        }
+    } else if (q.medium) {
+        for (uint32_t i = 0; i < k; ++i) {
+            const uint32_t v = lr[i];
+            const float w = lw[i];
             const VrlPrep V = vp[v];
             float c[3], m, s;
             integrate_vrl<NVV, NVS, false, VIS>(P, q, V, rid, v, kDomGather, P.nvv, P.nvs, c, &m, &s);
@@ -187,7 +200,7 @@ __global__ void __launch_bounds__(256) k_gather_ready(
     const uint32_t* __restrict__ slice_item_off, uint32_t nslices, const VrlPrep* __restrict__ vp,
     const SliceList* __restrict__ lists, uint32_t* ready, uint32_t* cursor, const uint32_t* resident,
     uint32_t nresident, DevParams P, float inv_pc, float* __restrict__ out, unsigned long long* counter,
-    unsigned long long spin_ticks)
+    unsigned long long spin_ticks, uint32_t nvrl)
 {
     // a workgroup dispatched before every k_refine workgroup is resident gives
     // its CU back at once (the refinement's teams assume co-residency)
@@ -241,6 +254,16 @@ __global__ void __launch_bounds__(256) k_gather_ready(
         const WorkItem it = items[slice_item_off[sp] + item];
         const SliceList L = lists[sp];
         const uint32_t k = __builtin_amdgcn_readfirstlane(__hip_atomic_load(L.n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        // a published list is checked before any VRL record is read through
+        // it (k entries, every index < nvrl): a bad one flags the slice
+        // (ready bit 2) for the host to report instead of faulting here
+        bool bad = k > nvrl;
+        for (uint32_t i = lane; !bad && i < k; i += 64)
+            bad = __hip_atomic_load(L.reps + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= nvrl;
+        if (__ballot(bad) != 0ull) {
+            if (lane == 0) atomicOr(&ready[sp], 4u);
+            continue;
+        }
         gather_item<NVV, NVS, VIS, true>(recs, ids, it, L.reps, L.w, k, vp, P, inv_pc, out, counter);
     }
 }
@@ -497,19 +520,19 @@ hipError_t launch_gather_ready(const Rec* recs, const uint32_t* ids, const WorkI
                                const SliceList* lists, uint32_t* ready, uint32_t* cursor,
                                const uint32_t* resident, uint32_t nresident, const DevParams& P,
                                float inv_pc, float* out, unsigned long long* counter,
-                               unsigned long long spin_ticks, uint32_t nblocks, hipStream_t s)
+                               unsigned long long spin_ticks, uint32_t nblocks, uint32_t nvrl, hipStream_t s)
 {
     if (nslices == 0 || nblocks == 0) return hipSuccess;
     const dim3 grid(nblocks), block(256);
     if (P.occ.ntri)
         hipLaunchKernelGGL((k_gather_ready<-1, -1, true>), grid, block, 0, s, recs, ids, items, slice_item_off, nslices,
-                           vp, lists, ready, cursor, resident, nresident, P, inv_pc, out, counter, spin_ticks);
+                           vp, lists, ready, cursor, resident, nresident, P, inv_pc, out, counter, spin_ticks, nvrl);
     else if (P.nvv == 2 && P.nvs == 2)
         hipLaunchKernelGGL((k_gather_ready<2, 2>), grid, block, 0, s, recs, ids, items, slice_item_off, nslices,
-                           vp, lists, ready, cursor, resident, nresident, P, inv_pc, out, counter, spin_ticks);
+                           vp, lists, ready, cursor, resident, nresident, P, inv_pc, out, counter, spin_ticks, nvrl);
     else
         hipLaunchKernelGGL((k_gather_ready<-1, -1>), grid, block, 0, s, recs, ids, items, slice_item_off, nslices,
-                           vp, lists, ready, cursor, resident, nresident, P, inv_pc, out, counter, spin_ticks);
+                           vp, lists, ready, cursor, resident, nresident, P, inv_pc, out, counter, spin_ticks, nvrl);
     return hipGetLastError();
 }
 

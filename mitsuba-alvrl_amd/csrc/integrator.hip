@@ -150,7 +150,7 @@ struct alvrl_integrator {
     uint32_t nrec = 0, nitems = 0;
     // slices rendered beside the refinement (alvrl_refine_gather): the work
     // items per slice of the full frame, and which slices this pass rendered
-    bool fusedRender = false;   // experimental: an illegal access seen once under the team-mode knob sweep
+    bool fusedRender = false;   // experimental: bit-identical frames, but slower than the plain path at C4
     std::vector<alvrl_work_item> items_h;
     std::vector<uint32_t> item_off_h;     // slice s: items [item_off_h[s], item_off_h[s + 1])
     DevBuf<uint32_t> item_off_buf;
@@ -541,8 +541,10 @@ struct alvrl_integrator {
         const double t0 = now_ms() - st.ms_refine;
         // render every slice beside the refinement when this pass's frame is
         // the whole frame on this GPU (alvrl_refine_gather)
-        const bool fuse = fusedRender && world == 1 && nm == ns && ns > 0 && !numVrlFalseColor && !slicesFalseColor &&
-                          !(std::getenv("ALVRL_FUSED_RENDER") && std::getenv("ALVRL_FUSED_RENDER")[0] == '0');
+        // ALVRL_FUSED_RENDER=0/1 overrides the property (developer knob)
+        const char* fre = std::getenv("ALVRL_FUSED_RENDER");
+        const bool fuse = (fre && fre[0] ? fre[0] == '1' : fusedRender) && world == 1 && nm == ns && ns > 0 &&
+                          !numVrlFalseColor && !slicesFalseColor;
         fused_valid = false;
         st.render_fused = 0;
         if (nm && fuse) {

@@ -3069,7 +3069,8 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
         if (tid == 0) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            st_rlx(&cm.ready[blockIdx.x], 1u | (refined ? 2u : 0u));
+            // C.err as it stands after the picks: a failed pick unpublishes the list
+            st_rlx(&cm.ready[blockIdx.x], 1u | (refined && !C.err ? 2u : 0u));
         }
     }
     if (cm.roam_on) {
@@ -3422,7 +3423,9 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
             if (hipHostGetDevicePointer(&dp, ar.h_resident, 0) == hipSuccess) cm.resident = (uint32_t*)dp;
         }
     }
-    const bool fuse_go = fused && cm.resident;
+    // ALVRL_FUSED_NOGATHER=1 (diagnostic): k_refine as in fused mode, no gather launched
+    const char* fng = std::getenv("ALVRL_FUSED_NOGATHER");
+    const bool fuse_go = fused && cm.resident && !(fng && fng[0] == '1');
     const char* tre = std::getenv("ALVRL_REFINE_TRACE");
     if (tre && tre[0] == '1' && hipHostMalloc(&cm.trace, 256 * 8, hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess)
         std::memset(cm.trace, 0, 256 * 8);
@@ -3514,7 +3517,16 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
         // so a late helper finds its job stopped and leaves
         hipLaunchKernelGGL(k_refine, dim3(njobs * G + nroam), dim3(kThreads), 0, s, d_jobs, cm);
         e = hipGetLastError();
-        if (fuse_go && e == hipSuccess) {
+        const char* fser = std::getenv("ALVRL_FUSED_SERIAL");   // diagnostic: the gather after k_refine
+        if (fuse_go && e == hipSuccess && fser && fser[0] == '1') {
+            hipEvent_t er = nullptr;
+            e = hipEventCreateWithFlags(&er, hipEventDisableTiming);
+            if (e == hipSuccess) e = hipEventRecord(er, s);
+            if (e == hipSuccess) e = hipStreamWaitEvent(rg->stream, er, 0);
+            if (e == hipSuccess) e = rg->launch(rg->user, d_lists, d_ready, d_cursor, cm.resident, 0u, rg->stream);
+            if (e == hipSuccess) rg->launched = 1;
+            if (er) hipEventDestroy(er);
+        } else if (fuse_go && e == hipSuccess) {
             // wait (bounded) until every workgroup of k_refine has started
             const uint32_t want = njobs * G + nroam;
             const auto tw = std::chrono::steady_clock::now();
@@ -3681,6 +3693,11 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
         hipError_t eg = hipStreamSynchronize(rg->stream);
         if (eg == hipSuccess && rg->claimed) eg = hipMemcpy(rg->claimed, d_cursor, (size_t)njobs * 4, hipMemcpyDeviceToHost);
         if (eg != hipSuccess && !rc) { rc = 4; *err = std::string("alvrl_refine_gather: ") + hipGetErrorString(eg); }
+        // ready bit 2: the gather found a published list it could not use
+        std::vector<uint32_t> rdy(njobs);
+        if (eg == hipSuccess) eg = hipMemcpy(rdy.data(), d_ready, (size_t)njobs * 4, hipMemcpyDeviceToHost);
+        for (uint32_t j = 0; j < njobs && eg == hipSuccess && !rc; j++)
+            if (rdy[j] & 4u) { rc = 5; *err = "alvrl_refine_gather: slice " + std::to_string(j) + " published an invalid list"; }
     }
     if (eprep) hipEventDestroy(eprep);
     if (e0) hipEventDestroy(e0);

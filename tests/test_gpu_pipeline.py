@@ -10,6 +10,7 @@ defaults) and variants.
   * frame: the oracle's clustered gather with those clusters vs the device
     frame, within test_gpu_parity's tolerance.
 """
+import os
 import numpy as np
 import pytest
 
@@ -503,8 +504,9 @@ def test_context_reuse_across_passes(gpu_ok):
 
 @pytest.mark.parametrize("props", ["targetNumSlices=40", "targetNumSlices=30;localUndersampling=10",
                                    "targetNumSlices=25;depthCorrection=0.8"])
-@pytest.mark.skip(reason="fusedRender is experimental: an illegal memory access was seen once under the "
-                         "team-mode knob sweep (DESIGN.md 5.2); the plain path is the default")
+@pytest.mark.skipif(os.environ.get("ALVRL_TEST_FUSED") != "1",
+                    reason="fusedRender is experimental and off by default (slower than the plain path at C4, "
+                           "DESIGN.md 5.2); ALVRL_TEST_FUSED=1 runs it")
 def test_fused_render_identical(gpu_ok, props):
     """fusedRender (alvrl_refine_gather): the slices rendered beside the
     refinement as their jobs finish give the frame of the plain path
@@ -537,8 +539,10 @@ def test_fused_render_identical(gpu_ok, props):
         out[fused] = (frames, cls, st["contrib_render"] // (2 if not fused else 1), st["contrib_preprocess"])
         it.close()
     (f0, c0, r0, p0), (f1, c1, r1, p1) = out[False], out[True]
-    for a, b in zip(f0, f1):
-        assert a.any() and np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    for n, (a, b) in enumerate(zip(f0, f1)):
+        assert a.any(), n
+        bad = np.nonzero(a.view(np.uint32) != b.view(np.uint32))[0]
+        assert bad.size == 0, (n, bad.size, bad[:4].tolist(), a[bad[:4]].tolist(), b[bad[:4]].tolist())
     for a, b in zip(c0, c1):
         for k in a:
             assert np.array_equal(a[k].view(np.uint32), b[k].view(np.uint32)), k
