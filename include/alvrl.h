@@ -245,7 +245,9 @@ ALVRL_API int alvrl_refine(alvrl_ctx *ctx, const float *d_Rt, uint64_t ld, uint3
  * rendered here; the caller renders the rest -- always those of slices whose
  * refinement failed (the fall-back list is the caller's) and of slice
  * 0xFFFFFFFF, and all of them (out_items_done 0) when the device cannot run
- * the two kernels together. */
+ * the two kernels together.  A published list with more than N entries or an
+ * index >= N is not read: the call returns ALVRL_ERR_NUMERIC.  Experimental:
+ * bit-identical to the plain path, but slower at C4. */
 ALVRL_API int alvrl_refine_gather(alvrl_ctx *ctx, const float *d_Rt, uint64_t ld, uint32_t njobs,
                                   const alvrl_cluster_job *jobs, const uint32_t *init_vrls,
                                   const uint32_t *init_off, uint32_t ninit, uint32_t *out_off,
