@@ -6,7 +6,8 @@
  * MTS_EXPORT_PLUGIN at :1127 and driven through the ProgressiveMonteCarlo-
  * Integrator vtable, include/mitsuba/render/integrator.h:482-511) needs from
  * the device.  Plain C types only: no torch, no HIP types in signatures
- * (streams are passed as void* = hipStream_t, NULL = the context's stream).
+ * (streams are passed as void* = hipStream_t, NULL = the context's stream,
+ * ordered after the work already queued on the null stream).
  * Errors are int status codes (ALVRL_OK = 0) plus alvrl_last_error(); no C++
  * exception crosses this boundary (the reference throws from Log(EError),
  * src/libcore/logger.cpp:147; the shim in INTEGRATION.md maps a non-zero

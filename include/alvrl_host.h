@@ -124,7 +124,9 @@ ALVRL_API int alvrl_integrator_preprocess(alvrl_integrator *it, const alvrl_scen
 ALVRL_API int alvrl_integrator_prepass(alvrl_integrator *it, uint32_t pass);
 /* SamplingIntegrator::render for the pixels this rank owns: 64x64 tiles dealt
  * round-robin (tile t -> rank t % world).  Adds Li of every owned pixel into
- * d_framebuffer (device, W*H*3 floats, row-major) on 'stream'. */
+ * d_framebuffer (device, W*H*3 floats, row-major) on 'stream' (NULL: the
+ * integrator's stream, ordered after the work already queued on the null
+ * stream, e.g. the caller's zero fill of d_framebuffer). */
 ALVRL_API int alvrl_integrator_render(alvrl_integrator *it, uint32_t rank, uint32_t world,
                                       float *d_framebuffer, void *stream);
 /* Preloaded VRLs (the vrlFile mode, :243-252 / :280-287): every pass reuses

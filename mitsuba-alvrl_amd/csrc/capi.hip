@@ -128,7 +128,19 @@ static int fail(int code, const std::string& msg)
             return fail(ALVRL_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
     } while (0)
 
-static hipStream_t pick(alvrl_ctx* c, void* s) { return s ? (hipStream_t)s : c->stream; }
+// NULL stream argument: the context's (non-blocking) stream, ordered after
+// the work already queued on the null stream -- a caller's zero fill or copy
+// of the buffers it passes, which the non-blocking stream would otherwise race
+static hipStream_t pick(alvrl_ctx* c, void* s)
+{
+    if (s) return (hipStream_t)s;
+    hipEvent_t ev = nullptr;
+    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess) {
+        if (hipEventRecord(ev, nullptr) == hipSuccess) (void)hipStreamWaitEvent(c->stream, ev, 0);
+        (void)hipEventDestroy(ev);
+    }
+    return c->stream;
+}
 
 extern "C" {
 

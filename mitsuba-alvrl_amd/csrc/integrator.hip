@@ -836,7 +836,19 @@ ALVRL_API int alvrl_integrator_render(alvrl_integrator* it, uint32_t rank, uint3
     if (!it || !d_fb) return ierr(ALVRL_ERR_INVALID, "alvrl_integrator_render: null argument");
     GUARD({
         hchk(hipSetDevice(it->device), "hipSetDevice");
-        it->render(rank, world, d_fb, stream ? (hipStream_t)stream : it->stream);
+        hipStream_t s = stream ? (hipStream_t)stream : it->stream;
+        if (!stream) {
+            // the integrator's own stream is non-blocking: order it after the
+            // caller's work on the null stream (e.g. the frame's zero fill),
+            // which it would otherwise race
+            hipEvent_t ev = nullptr;
+            hchk(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
+            hipError_t e = hipEventRecord(ev, nullptr);
+            if (e == hipSuccess) e = hipStreamWaitEvent(s, ev, 0);
+            (void)hipEventDestroy(ev);
+            hchk(e, "order after the null stream");
+        }
+        it->render(rank, world, d_fb, s);
     });
     return ALVRL_OK;
 }

@@ -3409,8 +3409,9 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
     if (fused) {
         cm.roam_on = 0;
         // ALVRL_ROAM_IDLE_US: idle bound of a roaming helper while the gather waits for CUs
+        // (20 ms: shorter bounds let the roamers leave before any work is queued)
         const char* ri = std::getenv("ALVRL_ROAM_IDLE_US");
-        cm.roam_idle = (unsigned long long)(ri ? std::max(1, std::atoi(ri)) : 200) * 100ull;
+        cm.roam_idle = (unsigned long long)(ri ? std::max(1, std::atoi(ri)) : 20000) * 100ull;
         // started workgroups, counted where the host can see them: the gather is
         // launched once every k_refine workgroup is resident
         if (!ar.h_resident && hipHostMalloc(&ar.h_resident, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
