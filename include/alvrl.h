@@ -232,30 +232,6 @@ ALVRL_API int alvrl_refine(alvrl_ctx *ctx, const float *d_Rt, uint64_t ld, uint3
                            const uint32_t *init_off, uint32_t ninit, uint32_t *out_off,
                            uint32_t *out_reps, float *out_weights, int *out_refined,
                            void *stream);
-/* alvrl_refine plus the clustered gather of the slices' pixels, overlapped
- * (an MI355X-native fusion of prepass and renderBlock, vrlIntegrator.cpp:
- * 270-356 then :542-599 for every pixel; the reference runs them one after
- * the other).  Job j must be slice j (njobs == number of slices).  While the
- * refinement runs, every job that finishes publishes its representative list
- * and a second kernel renders that slice's work items (d_items sorted by
- * slice, slice s's items at [d_slice_item_off[s], d_slice_item_off[s + 1]))
- * on the CUs the finished jobs leave, with the list as published, which is
- * the list alvrl_refine returns for it: every value written to d_out_rgb is
- * what alvrl_gather_clustered writes after alvrl_set_clusters of these lists.
- * out_items_done[s] (host): slice s's first out_items_done[s] work items were
- * rendered here; the caller renders the rest -- always those of slices whose
- * refinement failed (the fall-back list is the caller's) and of slice
- * 0xFFFFFFFF, and all of them (out_items_done 0) when the device cannot run
- * the two kernels together.  A published list with more than N entries or an
- * index >= N is not read: the call returns ALVRL_ERR_NUMERIC.  Experimental:
- * bit-identical to the plain path, but slower at C4. */
-ALVRL_API int alvrl_refine_gather(alvrl_ctx *ctx, const float *d_Rt, uint64_t ld, uint32_t njobs,
-                                  const alvrl_cluster_job *jobs, const uint32_t *init_vrls,
-                                  const uint32_t *init_off, uint32_t ninit, uint32_t *out_off,
-                                  uint32_t *out_reps, float *out_weights, int *out_refined,
-                                  const alvrl_gather_rec *d_recs, const uint32_t *d_rec_ids,
-                                  const alvrl_work_item *d_items, const uint32_t *d_slice_item_off,
-                                  float *d_out_rgb, uint32_t *out_items_done, void *stream);
 /* clusterRefinement (Preprocessor.cpp:899-912, the globalCluster option):
  * one Clustering ctor + refine(job->undersampling), then getVrlsPerCluster
  * (:526-543) -- singletons in list order, then the heap's clusters.  The

@@ -192,9 +192,6 @@ typedef struct {
     double ms_refine_kernel;
     uint64_t refine_entries;
     uint64_t global_clusters;   /* clusters of the globalCluster refinement (0 if off) */
-    /* slices the last prepass rendered beside its refinement (fusedRender,
-     * alvrl_refine_gather); their render time is inside ms_refine_kernel */
-    uint64_t render_fused;
 } alvrl_integrator_stats;
 ALVRL_API int alvrl_integrator_get_stats(alvrl_integrator *it, alvrl_integrator_stats *st);
 /* The device context the integrator drives (for low-level access). */

@@ -346,8 +346,7 @@ class IntegratorStats(C.Structure):
                 ("ms_prepass_wall", C.c_double), ("slices_failed", C.c_uint32),
                 ("fallback_built", C.c_int), ("slices_local", C.c_uint64), ("rows_built", C.c_uint64),
                 ("ms_exchange", C.c_double), ("ms_refine_kernel", C.c_double),
-                ("refine_entries", C.c_uint64), ("global_clusters", C.c_uint64),
-                ("render_fused", C.c_uint64)]
+                ("refine_entries", C.c_uint64), ("global_clusters", C.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -60,13 +60,7 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
                 uint32_t pass, uint32_t njobs, const HostJob* jobs, const uint32_t* init_vrls,
                 const uint32_t* init_off, uint32_t ninit, uint32_t* out_off, uint32_t* out_reps,
                 float* out_w, int* out_refined, float* ms, unsigned long long* entries, std::string* err,
-                RefineArenas* cache, ReadyGather* rg);
-hipError_t launch_gather_ready(const Rec* recs, const uint32_t* ids, const WorkItem* items,
-                               const uint32_t* slice_item_off, uint32_t nslices, const VrlPrep* vp,
-                               const SliceList* lists, uint32_t* ready, uint32_t* cursor,
-                               const uint32_t* resident, uint32_t nresident, const DevParams& P,
-                               float inv_pc, float* out, unsigned long long* counter,
-                               unsigned long long spin_ticks, uint32_t nblocks, uint32_t nvrl, hipStream_t s);
+                RefineArenas* cache);
 }  // namespace alvrl
 
 using namespace alvrl;
@@ -102,7 +96,6 @@ struct alvrl_ctx {
     float* d_bvh_tris = nullptr;
     uint32_t* d_bvh_ids = nullptr;
     RefineArenas refine_arenas;   // alvrl_refine's device scratch, reused across passes
-    hipStream_t stream2 = nullptr;   // alvrl_refine_gather's gather, beside the refinement
     std::mutex mu;
 };
 
@@ -205,7 +198,6 @@ ALVRL_API void alvrl_ctx_destroy(alvrl_ctx* c)
     free_clusters(c);
     free_occluders(c);
     c->refine_arenas.release();
-    if (c->stream2) hipStreamDestroy(c->stream2);
     if (c->ev0) hipEventDestroy(c->ev0);
     if (c->ev1) hipEventDestroy(c->ev1);
     if (c->stream) hipStreamDestroy(c->stream);
@@ -465,86 +457,10 @@ ALVRL_API int alvrl_build_R_blocks(alvrl_ctx* c, const alvrl_gather_rec* d_recs,
     return ALVRL_OK;
 }
 
-static int refine_impl(alvrl_ctx* c, const float* d_Rt, uint64_t ld, uint32_t njobs,
-                       const alvrl_cluster_job* jobs, const uint32_t* init_vrls,
-                       const uint32_t* init_off, uint32_t ninit, uint32_t* out_off,
-                       uint32_t* out_reps, float* out_weights, int* out_refined, void* stream, ReadyGather* rg);
-
 ALVRL_API int alvrl_refine(alvrl_ctx* c, const float* d_Rt, uint64_t ld, uint32_t njobs,
                            const alvrl_cluster_job* jobs, const uint32_t* init_vrls,
                            const uint32_t* init_off, uint32_t ninit, uint32_t* out_off,
                            uint32_t* out_reps, float* out_weights, int* out_refined, void* stream)
-{
-    return refine_impl(c, d_Rt, ld, njobs, jobs, init_vrls, init_off, ninit, out_off, out_reps, out_weights,
-                       out_refined, stream, nullptr);
-}
-
-namespace {
-struct GatherArgs {
-    const Rec* recs;
-    const uint32_t* ids;
-    const WorkItem* items;
-    const uint32_t* slice_item_off;
-    uint32_t nslices;
-    const VrlPrep* vp;
-    DevParams P;
-    float inv_pc;
-    float* out;
-    unsigned long long* counter;
-    unsigned long long spin_ticks;
-    uint32_t nblocks;
-    uint32_t nvrl;
-};
-hipError_t launch_ready_gather(void* user, const SliceList* lists, uint32_t* ready, uint32_t* cursor,
-                               const uint32_t* resident, uint32_t nresident, hipStream_t s)
-{
-    const GatherArgs& a = *static_cast<const GatherArgs*>(user);
-    return launch_gather_ready(a.recs, a.ids, a.items, a.slice_item_off, a.nslices, a.vp, lists, ready, cursor,
-                               resident, nresident, a.P, a.inv_pc, a.out, a.counter, a.spin_ticks, a.nblocks, a.nvrl, s);
-}
-}  // namespace
-
-ALVRL_API int alvrl_refine_gather(alvrl_ctx* c, const float* d_Rt, uint64_t ld, uint32_t njobs,
-                                  const alvrl_cluster_job* jobs, const uint32_t* init_vrls,
-                                  const uint32_t* init_off, uint32_t ninit, uint32_t* out_off,
-                                  uint32_t* out_reps, float* out_weights, int* out_refined,
-                                  const alvrl_gather_rec* d_recs, const uint32_t* d_rec_ids,
-                                  const alvrl_work_item* d_items, const uint32_t* d_slice_item_off,
-                                  float* d_out_rgb, uint32_t* out_items_done, void* stream)
-{
-    int rc = check_ready(c, "alvrl_refine_gather");
-    if (rc) return rc;
-    if (njobs && (!d_recs || !d_items || !d_slice_item_off || !d_out_rgb || !out_items_done))
-        return fail(ALVRL_ERR_INVALID, "alvrl_refine_gather: null buffer");
-    for (uint32_t j = 0; j < njobs; j++) out_items_done[j] = 0;
-    HIPCHK(hipSetDevice(c->cfg.device));
-    if (!c->stream2) HIPCHK(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
-    int dev = 0, ncu = 0;
-    HIPCHK(hipGetDevice(&dev));
-    HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-    const char* sp = std::getenv("ALVRL_GATHER_SPIN_MS");
-    GatherArgs a{reinterpret_cast<const Rec*>(d_recs), d_rec_ids, reinterpret_cast<const WorkItem*>(d_items),
-                 d_slice_item_off, njobs, c->d_vrl, c->P, 1.0f / (float)c->particle_count, d_out_rgb,
-                 c->d_counter + 1, sp ? (unsigned long long)std::max(1, std::atoi(sp)) * 100000ull : 6000000000ull,
-                 (uint32_t)std::max(1, ncu) * 8u, c->nvrl};
-    std::vector<uint32_t> claimed(njobs, 0), item_off(njobs + 1, 0);
-    ReadyGather rg{launch_ready_gather, &a, c->stream2, 0, claimed.data()};
-    rc = refine_impl(c, d_Rt, ld, njobs, jobs, init_vrls, init_off, ninit, out_off, out_reps, out_weights,
-                     out_refined, stream, &rg);
-    if (rc) return rc;
-    c->timed = false;   // the last gather timing (alvrl_last_kernel_ms) does not cover this one
-    if (rg.launched && njobs) {
-        HIPCHK(hipMemcpy(item_off.data(), d_slice_item_off, (size_t)(njobs + 1) * 4, hipMemcpyDeviceToHost));
-        for (uint32_t j = 0; j < njobs; j++)
-            out_items_done[j] = std::min(claimed[j], item_off[j + 1] - item_off[j]);
-    }
-    return ALVRL_OK;
-}
-
-static int refine_impl(alvrl_ctx* c, const float* d_Rt, uint64_t ld, uint32_t njobs,
-                       const alvrl_cluster_job* jobs, const uint32_t* init_vrls,
-                       const uint32_t* init_off, uint32_t ninit, uint32_t* out_off,
-                       uint32_t* out_reps, float* out_weights, int* out_refined, void* stream, ReadyGather* rg)
 {
     if (!c) return fail(ALVRL_ERR_INVALID, "alvrl_refine: null ctx");
     if (njobs && (!d_Rt || !jobs || !init_off || !out_off || !out_reps || !out_weights || !out_refined))
@@ -573,7 +489,7 @@ static int refine_impl(alvrl_ctx* c, const float* d_Rt, uint64_t ld, uint32_t nj
     std::lock_guard<std::mutex> g(c->mu);   // the context's refine scratch
     int rc = refine_jobs(pick(c, stream), d_Rt, ld, c->nvrl, c->P.seed, c->P.pass, njobs, hj.data(),
                          init_vrls, init_off, ninit, out_off, out_reps, out_weights, out_refined,
-                         &ms, &c->refine_entries, &err, &c->refine_arenas, rg);
+                         &ms, &c->refine_entries, &err, &c->refine_arenas);
     c->refine_ms = ms;
     if (rc) return fail(rc, err);
     return ALVRL_OK;
@@ -610,7 +526,7 @@ ALVRL_API int alvrl_refine_members(alvrl_ctx* c, const float* d_Rt, uint64_t ld,
     std::lock_guard<std::mutex> g(c->mu);   // the context's refine scratch
     int rc = refine_jobs(pick(c, stream), d_Rt, ld, c->nvrl, c->P.seed, c->P.pass, 1, &hj, init_vrls,
                          init_off, ninit, off.data(), reps.data(), w.data(), out_refined, &ms,
-                         &c->refine_entries, &err, &c->refine_arenas, nullptr);
+                         &c->refine_entries, &err, &c->refine_arenas);
     c->refine_ms = ms;
     if (rc) return fail(rc, err);
     (void)nv;

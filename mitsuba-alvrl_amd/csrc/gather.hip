@@ -90,7 +90,7 @@ __global__ void __launch_bounds__(256) k_gather_brute(const Rec* __restrict__ re
 
 struct WorkItem { uint32_t slice, begin, count, pad; };
 
-template <int NVV, int NVS, bool VIS, bool VL = false>
+template <int NVV, int NVS, bool VIS>
 __device__ __forceinline__ void gather_item(const Rec* __restrict__ recs, const uint32_t* __restrict__ ids,
                                             const WorkItem& it, const uint32_t* lr, const float* lw, uint32_t k,
                                             const VrlPrep* __restrict__ vp, const DevParams& P, float inv_pc,
@@ -118,10 +118,7 @@ __global__ void __launch_bounds__(256) k_gather_clustered(
 
 // One work item (<= 64 pixels of one slice, a lane each) over a
 // representative list: Li = sum_i w_i * integrateVRL(rep_i) / particleCount.
-// VL: the list was written during this launch by another CU (k_gather_ready):
-// it is read with vector loads, 64 entries at a time, and broadcast by
-// v_readlane -- never through the scalar cache, which no acquire refreshes.
-template <int NVV, int NVS, bool VIS, bool VL>
+template <int NVV, int NVS, bool VIS>
 __device__ __forceinline__ void gather_item(const Rec* __restrict__ recs, const uint32_t* __restrict__ ids,
                                             const WorkItem& it, const uint32_t* lr, const float* lw, uint32_t k,
                                             const VrlPrep* __restrict__ vp, const DevParams& P, float inv_pc,
@@ -134,34 +131,7 @@ __device__ __forceinline__ void gather_item(const Rec* __restrict__ recs, const 
     const RecPre q = prepare_record(rec, P);
     const uint32_t rid = active ? (ids ? ids[r] : r) : 0u;
     float L0 = 0.0f, L1 = 0.0f, L2 = 0.0f;
-    if constexpr (VL) {
-        // the list is loaded by every lane of the wave and broadcast with
-        // v_readlane, so the walk runs on the whole wave (a lane outside the
-        // medium would leave its slot of the 64-entry block unloaded and the
-        // broadcast would read a stale register); lanes outside the medium
-        // compute nothing
-        const bool med = q.medium;
-        if (__ballot(med) != 0ull) {
-            uint32_t vr = 0u, vw = 0u;
-            for (uint32_t i = 0; i < k; ++i) {
-                if ((i & 63u) == 0u) {
-                    const uint32_t j = min(i + lane, k - 1);
-                    vr = __hip_atomic_load(lr + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    vw = __hip_atomic_load(reinterpret_cast<const uint32_t*>(lw) + j, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-                }
-                const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)vr, (int)(i & 63u));
-                const float w = __int_as_float(__builtin_amdgcn_readlane((int)vw, (int)(i & 63u)));
-                if (med) {
-                    const VrlPrep V = vp[v];
-                    float c[3], m, s;
-                    integrate_vrl<NVV, NVS, false, VIS>(P, q, V, rid, v, kDomGather, P.nvv, P.nvs, c, &m, &s);
-                    L0 += c[0] * w; L1 += c[1] * w; L2 += c[2] * w;
-                }
-            }
-            L0 *= inv_pc; L1 *= inv_pc; L2 *= inv_pc;
-        }
-    } else if (q.medium) {
+    if (q.medium) {
         for (uint32_t i = 0; i < k; ++i) {
             const uint32_t v = lr[i];
             const float w = lw[i];
@@ -177,94 +147,6 @@ __device__ __forceinline__ void gather_item(const Rec* __restrict__ recs, const 
     count_pairs(counter, active && q.medium, k);
     if (active) {
         out[3 * (size_t)r + 0] = L0; out[3 * (size_t)r + 1] = L1; out[3 * (size_t)r + 2] = L2;
-    }
-}
-
-// Slices rendered while the refinement still runs (alvrl_refine_gather): a
-// persistent kernel launched beside k_refine on a second stream.  Its
-// workgroups start on the CUs that finished refinement jobs leave; a wave
-// takes the next work item of any slice whose job has published its
-// representative list (k_refine: every storing wave drained, barrier, one
-// agent-scope release, then the relaxed flag ready[s] = 1 | refined << 1),
-// after one agent-scope acquire per slice it switches to, and renders it with
-// the list as published (the same list, in the same order, as the packed
-// cluster lists the standard gather reads: identical sums).  Slices whose
-// refinement failed are left to the caller (their fall-back list is built on
-// the host afterwards).  Every wait is bounded (spin_ticks of the 100 MHz
-// clock since the wave's last item); a wave exits once every slice is
-// published and taken, and only between items, so cursor[s] (capped at the
-// slice's item count) is the number of slice s's items rendered here.
-template <int NVV, int NVS, bool VIS = false>
-__global__ void __launch_bounds__(256) k_gather_ready(
-    const Rec* __restrict__ recs, const uint32_t* __restrict__ ids, const WorkItem* __restrict__ items,
-    const uint32_t* __restrict__ slice_item_off, uint32_t nslices, const VrlPrep* __restrict__ vp,
-    const SliceList* __restrict__ lists, uint32_t* ready, uint32_t* cursor, const uint32_t* resident,
-    uint32_t nresident, DevParams P, float inv_pc, float* __restrict__ out, unsigned long long* counter,
-    unsigned long long spin_ticks, uint32_t nvrl)
-{
-    // a workgroup dispatched before every k_refine workgroup is resident gives
-    // its CU back at once (the refinement's teams assume co-residency)
-    if (__hip_atomic_load(resident, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < nresident) return;
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    uint32_t acquired = 0xFFFFFFFFu;   // the slice this wave last acquired
-    while (true) {
-        int pick = -1;
-        uint32_t item = 0;
-        bool pending = false;
-        for (uint32_t base = 0; base < nslices && pick < 0; base += 64) {
-            const uint32_t s = base + lane;
-            uint32_t st = 1u, cur = 0u, cnt = 0u;
-            if (s < nslices) {
-                st = __hip_atomic_load(&ready[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                cur = __hip_atomic_load(&cursor[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                cnt = slice_item_off[s + 1] - slice_item_off[s];
-            }
-            const bool open = s < nslices && (st == 0u || ((st & 2u) && cur < cnt));
-            const bool avail = s < nslices && (st & 2u) && cur < cnt;
-            pending = pending || __ballot(open) != 0ull;
-            unsigned long long av = __ballot(avail);
-            while (av) {
-                // spread the waves over the open slices: start at wave id mod 64
-                const uint32_t rot = wid & 63u;
-                const unsigned long long hi = rot ? (av >> rot) : av;
-                const uint32_t l = hi ? rot + (uint32_t)__builtin_ctzll(hi) : (uint32_t)__builtin_ctzll(av);
-                const uint32_t sp = base + l;
-                uint32_t got = 0u;
-                if (lane == 0) got = atomicAdd(&cursor[sp], 1u);
-                got = __builtin_amdgcn_readfirstlane(got);
-                if (got < slice_item_off[sp + 1] - slice_item_off[sp]) { pick = (int)sp; item = got; break; }
-                av &= ~(1ull << l);
-            }
-        }
-        if (pick < 0) {
-            if (!pending) break;                                   // everything published and taken
-            if (__builtin_amdgcn_s_memrealtime() - t0 > spin_ticks) break;   // bounded wait
-            __builtin_amdgcn_s_sleep(32);
-            continue;
-        }
-        const uint32_t sp = (uint32_t)pick;
-        t0 = __builtin_amdgcn_s_memrealtime();   // the wait bound counts from the last item
-        if (sp != acquired) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            acquired = sp;
-        }
-        const WorkItem it = items[slice_item_off[sp] + item];
-        const SliceList L = lists[sp];
-        const uint32_t k = __builtin_amdgcn_readfirstlane(__hip_atomic_load(L.n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        // a published list is checked before any VRL record is read through
-        // it (k entries, every index < nvrl): a bad one flags the slice
-        // (ready bit 2) for the host to report instead of faulting here
-        bool bad = k > nvrl;
-        for (uint32_t i = lane; !bad && i < k; i += 64)
-            bad = __hip_atomic_load(L.reps + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= nvrl;
-        if (__ballot(bad) != 0ull) {
-            if (lane == 0) atomicOr(&ready[sp], 4u);
-            continue;
-        }
-        gather_item<NVV, NVS, VIS, true>(recs, ids, it, L.reps, L.w, k, vp, P, inv_pc, out, counter);
     }
 }
 
@@ -512,27 +394,6 @@ hipError_t launch_gather_clustered(const Rec* recs, const uint32_t* ids, const W
         hipLaunchKernelGGL((k_gather_clustered<-1, -1>), grid, block, 0, s, recs, ids, items,
                            nitems, vp, slice_off, reps, weights, fb_reps, fb_w, n_fb, P, inv_pc,
                            out, counter);
-    return hipGetLastError();
-}
-
-hipError_t launch_gather_ready(const Rec* recs, const uint32_t* ids, const WorkItem* items,
-                               const uint32_t* slice_item_off, uint32_t nslices, const VrlPrep* vp,
-                               const SliceList* lists, uint32_t* ready, uint32_t* cursor,
-                               const uint32_t* resident, uint32_t nresident, const DevParams& P,
-                               float inv_pc, float* out, unsigned long long* counter,
-                               unsigned long long spin_ticks, uint32_t nblocks, uint32_t nvrl, hipStream_t s)
-{
-    if (nslices == 0 || nblocks == 0) return hipSuccess;
-    const dim3 grid(nblocks), block(256);
-    if (P.occ.ntri)
-        hipLaunchKernelGGL((k_gather_ready<-1, -1, true>), grid, block, 0, s, recs, ids, items, slice_item_off, nslices,
-                           vp, lists, ready, cursor, resident, nresident, P, inv_pc, out, counter, spin_ticks, nvrl);
-    else if (P.nvv == 2 && P.nvs == 2)
-        hipLaunchKernelGGL((k_gather_ready<2, 2>), grid, block, 0, s, recs, ids, items, slice_item_off, nslices,
-                           vp, lists, ready, cursor, resident, nresident, P, inv_pc, out, counter, spin_ticks, nvrl);
-    else
-        hipLaunchKernelGGL((k_gather_ready<-1, -1>), grid, block, 0, s, recs, ids, items, slice_item_off, nslices,
-                           vp, lists, ready, cursor, resident, nresident, P, inv_pc, out, counter, spin_ticks, nvrl);
     return hipGetLastError();
 }
 

@@ -148,16 +148,6 @@ struct alvrl_integrator {
     DevBuf<alvrl_work_item> item_buf;
     DevBuf<float> out_buf;
     uint32_t nrec = 0, nitems = 0;
-    // slices rendered beside the refinement (alvrl_refine_gather): the work
-    // items per slice of the full frame, and which slices this pass rendered
-    bool fusedRender = false;   // experimental: bit-identical frames, but slower than the plain path at C4
-    std::vector<alvrl_work_item> items_h;
-    std::vector<uint32_t> item_off_h;     // slice s: items [item_off_h[s], item_off_h[s + 1])
-    DevBuf<uint32_t> item_off_buf;
-    DevBuf<alvrl_work_item> left_buf;
-    std::vector<uint32_t> slice_done;     // per slice: its first slice_done[s] items are in out_buf
-    bool fused_valid = false;             // out_buf holds this pass's frame for the rendered slices
-    bool left_done = false;               // ... and for the rest
     alvrl_integrator_stats st{};
 
     ~alvrl_integrator()
@@ -178,7 +168,6 @@ struct alvrl_integrator {
         if (k == "nc") throw IntegError(ALVRL_ERR_INVALID, "Neighbourcount is now called 'neighbourCount' instead of 'nc'!");
         else if (k == "shortVrls") shortVrls = b(v);
         else if (k == "gpuTracer") gpuTracer = b(v);
-        else if (k == "fusedRender") fusedRender = b(v);
         else if (k == "vrlTargetNum") vrlTargetNum = i(v);
         else if (k == "maxParticleDepth") maxParticleDepth = i(v);
         else if (k == "specularForcedRRdepth") specRRdepth = i(v);
@@ -539,28 +528,7 @@ struct alvrl_integrator {
         std::vector<float>& w = w_buf;
         std::vector<int> refined(nm + 1);
         const double t0 = now_ms() - st.ms_refine;
-        // render every slice beside the refinement when this pass's frame is
-        // the whole frame on this GPU (alvrl_refine_gather)
-        // ALVRL_FUSED_RENDER=0/1 overrides the property (developer knob)
-        const char* fre = std::getenv("ALVRL_FUSED_RENDER");
-        const bool fuse = (fre && fre[0] ? fre[0] == '1' : fusedRender) && world == 1 && nm == ns && ns > 0 &&
-                          !numVrlFalseColor && !slicesFalseColor;
-        fused_valid = false;
-        st.render_fused = 0;
-        if (nm && fuse) {
-            clustered = true;
-            prepare_render(0, 1);
-            slice_done.assign(ns, 0);
-            chk(alvrl_refine_gather(ctx, Rt.p, rows, nm, jobs.data(), init.data(), init_off.data(),
-                                    (uint32_t)init_off.size() - 1, off.data(), rep.data(), w.data(),
-                                    refined.data(), rec_buf.p, pix_buf.p, item_buf.p, item_off_buf.p, out_buf.p,
-                                    slice_done.data(), stream), "alvrl_refine_gather (slices)");
-            uint32_t nr = 0;
-            for (uint32_t x : slice_done) nr += x ? 1 : 0;
-            fused_valid = nr > 0;
-            left_done = false;
-            st.render_fused = nr;
-        } else if (nm)
+        if (nm)
             chk(alvrl_refine(ctx, Rt.p, rows, nm, jobs.data(), init.data(), init_off.data(),
                              (uint32_t)init_off.size() - 1, off.data(), rep.data(), w.data(),
                              refined.data(), stream), "alvrl_refine (slices)");
@@ -659,7 +627,6 @@ struct alvrl_integrator {
     {
         const uint32_t mode = clustered ? 2u : 1u;
         if (cache_rank == rank && cache_world == world && cache_mode == mode) return;
-        fused_valid = false;
         const int W = scene.width, H = scene.height;
         uint32_t npix = 0;
         chk_host(alvrl_tile_pixels(W, H, rank, world, nullptr, 0, &npix));
@@ -695,22 +662,6 @@ struct alvrl_integrator {
             item_buf.ensure(nitems);
             hchk(hipMemcpyAsync(item_buf.p, items.data(), sizeof(alvrl_work_item) * nitems, hipMemcpyHostToDevice, stream), "copy items");
         }
-        if (clustered && world == 1) {
-            // the items are sorted by slice (0xFFFFFFFF, no gather point, last)
-            const uint32_t ns = prep ? prep->num_slices() : 0;
-            item_off_h.assign(ns + 1, 0);
-            uint32_t i = 0;
-            for (uint32_t sl = 0; sl <= ns; sl++) {
-                while (i < nitems && items[i].slice < sl) i++;
-                item_off_h[sl] = i;
-            }
-            item_off_buf.ensure(ns + 1);
-            hchk(hipMemcpyAsync(item_off_buf.p, item_off_h.data(), sizeof(uint32_t) * (ns + 1), hipMemcpyHostToDevice, stream), "copy item offsets");
-            items_h = items;
-        } else {
-            item_off_h.clear();
-            items_h.clear();
-        }
         hchk(hipStreamSynchronize(stream), "sync");
         cache_rank = rank; cache_world = world; cache_mode = mode;
     }
@@ -731,24 +682,6 @@ struct alvrl_integrator {
             const int mode = numVrlFalseColor ? ALVRL_FALSE_COLOR_NUM_VRLS : ALVRL_FALSE_COLOR_SLICES;
             chk(alvrl_gather_false_color(ctx, mode, rec_buf.p, clustered ? item_buf.p : nullptr,
                                          clustered ? nitems : nrec, out_buf.p, s), "alvrl_gather_false_color");
-        } else if (clustered && fused_valid) {
-            // the slices rendered beside this pass's refinement are in out_buf;
-            // the rest (failed slices, pixels without a gather point) here
-            if (!left_done) {
-                std::vector<alvrl_work_item> left;
-                const uint32_t ns = (uint32_t)slice_done.size();
-                for (uint32_t sl = 0; sl < ns; sl++)
-                    for (uint32_t i = item_off_h[sl] + slice_done[sl]; i < item_off_h[sl + 1]; i++) left.push_back(items_h[i]);
-                for (uint32_t i = item_off_h[ns]; i < (uint32_t)items_h.size(); i++) left.push_back(items_h[i]);
-                if (!left.empty()) {
-                    left_buf.ensure(left.size());
-                    hchk(hipMemcpyAsync(left_buf.p, left.data(), sizeof(alvrl_work_item) * left.size(), hipMemcpyHostToDevice, s), "copy items");
-                    chk(alvrl_gather_clustered(ctx, rec_buf.p, pix_buf.p, left_buf.p, (uint32_t)left.size(), out_buf.p, s),
-                        "alvrl_gather_clustered");
-                    hchk(hipStreamSynchronize(s), "sync");   // left goes out of scope
-                }
-                left_done = true;
-            }
         } else if (clustered)
             chk(alvrl_gather_clustered(ctx, rec_buf.p, pix_buf.p, item_buf.p, nitems, out_buf.p, s), "alvrl_gather_clustered");
         else
@@ -878,7 +811,6 @@ ALVRL_API int alvrl_integrator_get_stats(alvrl_integrator* it, alvrl_integrator_
         it->st.contrib_render = ren;
         float ms = 0;
         if (alvrl_last_kernel_ms(it->ctx, &ms) == ALVRL_OK) it->st.ms_render_kernel = ms;
-        else if (it->st.render_fused) it->st.ms_render_kernel = 0.0;   // rendered inside the refinement's time
         *st = it->st;
     });
     return ALVRL_OK;

@@ -134,10 +134,9 @@ struct Common {
     uint32_t njobs;                // leaders = blocks [0, njobs); helpers follow, team by team
     uint32_t team;                 // workgroups per job (1 = no speculation)
     uint32_t spec_min;             // smallest cluster worth a speculative split
-    uint32_t side_k;
-    int enq_start;                 // also queue candidates right after the pop (before the split)               // a waiting leader takes a side task of <= awaited columns * side_k / 16
+    uint32_t side_k;               // a waiting leader takes a side task of <= awaited columns * side_k / 16
+    int enq_start;                 // also queue candidates right after the pop (before the split)
     unsigned long long spin_ticks; // bound of an idle helper's wait for a task (100 MHz ticks)
-    unsigned long long roam_idle;  // alvrl_refine_gather: a roamer idle this long leaves its CU to the gather
     unsigned long long wait_ticks; // bound of a leader's wait for a running helper (100 MHz ticks)
     unsigned long long* tstat;     // team counters (ALVRL_REFINE_TEAM_STATS=1), or null
     unsigned long long* jtime;     // with tstat: per job, wall ticks at start / end of refine / end
@@ -151,8 +150,6 @@ struct Common {
     const uint32_t* roam_order;    // null: roam from the last job served; else scan jobs in this order
     int early_spec;                // queue the first initial cluster for a helper's split before the
                                    // leader computes the initial clusters' variances (ALVRL_EARLY_SPEC=0: off)
-    uint32_t* ready;               // alvrl_refine_gather: per job, 1 | refined << 1 once its lists are out
-    uint32_t* resident;            // alvrl_refine_gather: workgroups started
     int team_setup;                // a job's first helper takes half the column weights and the
                                    // unclustered variance off the leader (ALVRL_TEAM_SETUP=0: off)
 };
@@ -2593,7 +2590,7 @@ __device__ __noinline__ void roam_loop(const JobDev* jobs, const SplitWs& w, uin
                     if (c == 1) got = 1;
                 }
                 if (got) { tcount(cm, TS_HSTART); break; }
-                if (!live || wall() - t_idle > (cm.roam_idle ? cm.roam_idle : cm.spin_ticks)) { got = -1; break; }
+                if (!live || wall() - t_idle > cm.spin_ticks) { got = -1; break; }
                 __builtin_amdgcn_s_sleep(32);
             }
             tadd(cm, TS_RIDLE, wall() - t_idle);
@@ -2817,8 +2814,6 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
     __shared__ Ctl C;
     __shared__ __attribute__((aligned(16))) unsigned char pool[kPoolBytes];
     unsigned long long* lds = reinterpret_cast<unsigned long long*>(pool);
-    if (cm.resident && threadIdx.x == 0)
-        __hip_atomic_fetch_add(cm.resident, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     if (blockIdx.x >= cm.njobs * cm.team) {   // a roaming helper
         const uint32_t rid = blockIdx.x - cm.njobs * cm.team;
         roam_loop(jobs, cm.roam_ws[rid], rid * 37u, cm, C, lds);
@@ -3061,18 +3056,6 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
         if (cm.entries) atomicAdd(cm.entries, (3ull * N + split_cols) * R);
     }
     if (cm.jtime && tid == 0) cm.jtime[3 * blockIdx.x + 2] = wall();
-    if (cm.ready) {
-        // publish the job's lists to k_gather_ready (producer form: every
-        // storing wave drained, barrier, one agent-scope release, then the flag)
-        drain_vmem();
-        __syncthreads();
-        if (tid == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            // C.err as it stands after the picks: a failed pick unpublishes the list
-            st_rlx(&cm.ready[blockIdx.x], 1u | (refined && !C.err ? 2u : 0u));
-        }
-    }
     if (cm.roam_on) {
         // this job is done: its leader helps the others with its own scratch
         __syncthreads();
@@ -3134,8 +3117,6 @@ void RefineArenas::release()
 {
     if (arena) (void)hipFree(arena);
     if (tarena) (void)hipFree(tarena);
-    if (h_resident) (void)hipHostFree(h_resident);
-    h_resident = nullptr;
     arena = tarena = nullptr;
     arena_cap = tarena_cap = 0;
 }
@@ -3155,9 +3136,8 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
                 uint32_t pass, uint32_t njobs, const HostJob* jobs, const uint32_t* init_vrls,
                 const uint32_t* init_off, uint32_t ninit, uint32_t* out_off, uint32_t* out_reps,
                 float* out_w, int* out_refined, float* ms, unsigned long long* entries, std::string* err,
-                RefineArenas* cache, ReadyGather* rg)
+                RefineArenas* cache)
 {
-    if (rg) rg->launched = 0;
     RefineArenas local;
     RefineArenas& ar = cache ? *cache : local;
     struct Finally {
@@ -3227,8 +3207,7 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
     };
     size_t total = align_up(rows_total * 8) + align_up(rows_total * 4) + align_up(rows_total * 8) + align_up((size_t)nv * 4) +
                    align_up((size_t)(ninit + 1) * 4) + align_up((size_t)njobs * sizeof(JobDev)) +
-                   align_up((size_t)njobs * 12) + 2 * align_up((size_t)njobs * N * 4) + align_up(8) +
-                   2 * align_up((size_t)njobs * 4) + align_up(16) + align_up((size_t)njobs * sizeof(SliceList));
+                   align_up((size_t)njobs * 12) + 2 * align_up((size_t)njobs * N * 4) + align_up(8);
     for (uint32_t j = 0; j < njobs; j++) { job_off[j] = total; total += job_bytes(jobs[j]); }
     hipError_t e = arena_get(&ar.arena, &ar.arena_cap, total, cache != nullptr);
     if (e != hipSuccess) { *err = std::string("alvrl_refine: hipMalloc: ") + hipGetErrorString(e); return 4; }
@@ -3243,10 +3222,6 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
     uint32_t* d_meta = (uint32_t*)(arena + o); o += align_up((size_t)njobs * 12);
     uint32_t* d_preps = (uint32_t*)(arena + o); o += align_up((size_t)njobs * N * 4);
     float* d_pw = (float*)(arena + o); o += align_up((size_t)njobs * N * 4);
-    uint32_t* d_ready = (uint32_t*)(arena + o); o += align_up((size_t)njobs * 4);
-    uint32_t* d_cursor = (uint32_t*)(arena + o); o += align_up((size_t)njobs * 4);
-    uint32_t* d_resident = (uint32_t*)(arena + o); o += align_up(16);
-    SliceList* d_lists = (SliceList*)(arena + o); o += align_up((size_t)njobs * sizeof(SliceList));
     unsigned long long* d_entries = (unsigned long long*)(arena + o);
     std::vector<unsigned long long> h_roff(rows_total);
     std::vector<uint32_t> h_rstride(rows_total);
@@ -3399,34 +3374,6 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
     }
     cm.tstat = nullptr;
     cm.trace = nullptr;
-    // slices rendered beside the refinement: one launch with every team
-    // co-resident (team mode); finished leaders and helpers exit instead of
-    // roaming so their CUs take the gather's workgroups
-    const bool fused = rg && rg->launch && team_on && tarena && !bs_env;
-    cm.ready = fused ? d_ready : nullptr;
-    cm.resident = nullptr;
-    cm.roam_idle = 0;
-    if (fused) {
-        cm.roam_on = 0;
-        // ALVRL_ROAM_IDLE_US: idle bound of a roaming helper while the gather waits for CUs
-        // (20 ms: shorter bounds let the roamers leave before any work is queued)
-        const char* ri = std::getenv("ALVRL_ROAM_IDLE_US");
-        cm.roam_idle = (unsigned long long)(ri ? std::max(1, std::atoi(ri)) : 20000) * 100ull;
-        // started workgroups, counted where the host can see them: the gather is
-        // launched once every k_refine workgroup is resident
-        if (!ar.h_resident && hipHostMalloc(&ar.h_resident, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
-            (void)hipGetLastError();
-            ar.h_resident = nullptr;
-        }
-        if (ar.h_resident) {
-            __atomic_store_n(ar.h_resident, 0u, __ATOMIC_SEQ_CST);
-            void* dp = nullptr;
-            if (hipHostGetDevicePointer(&dp, ar.h_resident, 0) == hipSuccess) cm.resident = (uint32_t*)dp;
-        }
-    }
-    // ALVRL_FUSED_NOGATHER=1 (diagnostic): k_refine as in fused mode, no gather launched
-    const char* fng = std::getenv("ALVRL_FUSED_NOGATHER");
-    const bool fuse_go = fused && cm.resident && !(fng && fng[0] == '1');
     const char* tre = std::getenv("ALVRL_REFINE_TRACE");
     if (tre && tre[0] == '1' && hipHostMalloc(&cm.trace, 256 * 8, hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess)
         std::memset(cm.trace, 0, 256 * 8);
@@ -3497,19 +3444,6 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
         e = hipMemcpyAsync(d_rws, h_rws.data(), (size_t)nroam * sizeof(SplitWs), hipMemcpyHostToDevice, s);
     if (e == hipSuccess && cm.roam_order)
         e = hipMemcpyAsync(const_cast<uint32_t*>(cm.roam_order), h_order.data(), (size_t)njobs * 4, hipMemcpyHostToDevice, s);
-    hipEvent_t eprep = nullptr;
-    if (fused && e == hipSuccess) {
-        std::vector<SliceList> h_lists(njobs);
-        for (uint32_t j = 0; j < njobs; j++) h_lists[j] = SliceList{h_jobs[j].out_reps, h_jobs[j].out_w, h_jobs[j].out_n};
-        e = hipMemsetAsync(d_ready, 0, (size_t)njobs * 4, s);
-        if (e == hipSuccess) e = hipMemsetAsync(d_cursor, 0, (size_t)njobs * 4, s);
-        if (e == hipSuccess) e = hipMemsetAsync(d_resident, 0, 16, s);
-        if (e == hipSuccess) e = hipMemcpyAsync(d_lists, h_lists.data(), (size_t)njobs * sizeof(SliceList), hipMemcpyHostToDevice, s);
-        if (e == hipSuccess) e = hipEventCreateWithFlags(&eprep, hipEventDisableTiming);
-        if (e == hipSuccess) e = hipEventRecord(eprep, s);
-        if (e == hipSuccess) e = hipStreamWaitEvent(rg->stream, eprep, 0);
-        if (e == hipSuccess) e = hipStreamSynchronize(s);   // h_lists goes out of scope
-    }
     if (e == hipSuccess) e = hipEventRecord(e0, s);
     if (e == hipSuccess && team_on && tarena) {
         // sized to the resident capacity, but correct without co-residency:
@@ -3518,25 +3452,6 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
         // so a late helper finds its job stopped and leaves
         hipLaunchKernelGGL(k_refine, dim3(njobs * G + nroam), dim3(kThreads), 0, s, d_jobs, cm);
         e = hipGetLastError();
-        const char* fser = std::getenv("ALVRL_FUSED_SERIAL");   // diagnostic: the gather after k_refine
-        if (fuse_go && e == hipSuccess && fser && fser[0] == '1') {
-            hipEvent_t er = nullptr;
-            e = hipEventCreateWithFlags(&er, hipEventDisableTiming);
-            if (e == hipSuccess) e = hipEventRecord(er, s);
-            if (e == hipSuccess) e = hipStreamWaitEvent(rg->stream, er, 0);
-            if (e == hipSuccess) e = rg->launch(rg->user, d_lists, d_ready, d_cursor, cm.resident, 0u, rg->stream);
-            if (e == hipSuccess) rg->launched = 1;
-            if (er) hipEventDestroy(er);
-        } else if (fuse_go && e == hipSuccess) {
-            // wait (bounded) until every workgroup of k_refine has started
-            const uint32_t want = njobs * G + nroam;
-            const auto tw = std::chrono::steady_clock::now();
-            while (__atomic_load_n(ar.h_resident, __ATOMIC_ACQUIRE) < want &&
-                   std::chrono::steady_clock::now() - tw < std::chrono::milliseconds(200))
-                std::this_thread::yield();
-            e = rg->launch(rg->user, d_lists, d_ready, d_cursor, cm.resident, want, rg->stream);
-            if (e == hipSuccess) rg->launched = 1;
-        }
     } else if (e == hipSuccess) {
         // ALVRL_REFINE_BATCH=n (developer knob): launch the jobs n at a time,
         // to separate per-CU cost from contention between concurrent jobs
@@ -3687,20 +3602,6 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
     if (e != hipSuccess) { rc = 3; *err = std::string("alvrl_refine: ") + hipGetErrorString(e); }
 
     if (cm.trace) hipHostFree(cm.trace);
-    if (rg && rg->launched) {
-        // the gather reads the jobs' lists in this arena: done before it is
-        // reused; a taken item is always rendered (a wave leaves only between
-        // items), so the cursors say what is left for the caller
-        hipError_t eg = hipStreamSynchronize(rg->stream);
-        if (eg == hipSuccess && rg->claimed) eg = hipMemcpy(rg->claimed, d_cursor, (size_t)njobs * 4, hipMemcpyDeviceToHost);
-        if (eg != hipSuccess && !rc) { rc = 4; *err = std::string("alvrl_refine_gather: ") + hipGetErrorString(eg); }
-        // ready bit 2: the gather found a published list it could not use
-        std::vector<uint32_t> rdy(njobs);
-        if (eg == hipSuccess) eg = hipMemcpy(rdy.data(), d_ready, (size_t)njobs * 4, hipMemcpyDeviceToHost);
-        for (uint32_t j = 0; j < njobs && eg == hipSuccess && !rc; j++)
-            if (rdy[j] & 4u) { rc = 5; *err = "alvrl_refine_gather: slice " + std::to_string(j) + " published an invalid list"; }
-    }
-    if (eprep) hipEventDestroy(eprep);
     if (e0) hipEventDestroy(e0);
     if (e1) hipEventDestroy(e1);
     return rc;

@@ -544,22 +544,7 @@ struct RefineArenas {
     char* arena = nullptr;
     char* tarena = nullptr;
     size_t arena_cap = 0, tarena_cap = 0;
-    uint32_t* h_resident = nullptr;   // host-mapped count of started k_refine workgroups
     void release();
-};
-
-// alvrl_refine_gather: slices rendered beside the refinement (gather.hip
-// k_gather_ready).  SliceList: a job's published representative list.
-struct SliceList { const uint32_t* reps; const float* w; const uint32_t* n; };
-struct ReadyGather {
-    // launches k_gather_ready on `stream` (called by refine_jobs right after
-    // k_refine is launched; the stream already waits for the lists' setup)
-    hipError_t (*launch)(void* user, const SliceList* lists, uint32_t* ready, uint32_t* cursor,
-                         const uint32_t* resident, uint32_t nresident, hipStream_t stream);
-    void* user;
-    hipStream_t stream;
-    int launched;       // out: 1 when the kernel ran beside the refinement
-    uint32_t* claimed;  // out (host, per job): work items the kernel took, all of them rendered
 };
 
 }  // namespace alvrl

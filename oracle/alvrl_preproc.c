@@ -19,6 +19,8 @@
 #include <stdlib.h>
 #include <string.h>
 #include <stdio.h>
+#include <pthread.h>
+#include <unistd.h>
 
 #define UINT32_T_MAX 0xffffffffu
 #ifndef M_PI
@@ -231,6 +233,22 @@ static void ulist_copy(ulist *dst, const ulist *src)
 }
 
 /* ------------------------------------------------------ Clustering -- */
+/* per-thread scratch of a split: row vectors (R + 1 entries each) */
+typedef struct {
+    double *sum, *Mv, *sumVars, *scr;
+    float *fa, *fb, *fc, *fd;
+} scratch_t;
+
+static void scratch_alloc(scratch_t *S, uint32_t R)
+{
+    S->sum = (double *)calloc((size_t)R * 4 + 4, sizeof(double));
+    S->Mv = S->sum + R + 1; S->sumVars = S->Mv + R + 1; S->scr = S->sumVars + R + 1;
+    S->fa = (float *)calloc((size_t)R * 4 + 4, sizeof(float));
+    S->fb = S->fa + R + 1; S->fc = S->fb + R + 1; S->fd = S->fc + R + 1;
+}
+static void scratch_free(scratch_t *S) { free(S->sum); free(S->fa); S->sum = NULL; S->fa = NULL; }
+
+struct spec_pool;
 typedef struct {
     mat_t M;
     const double *locw;
@@ -244,9 +262,9 @@ typedef struct {
     cheap sh_pq; ulist sh_singles;
     uint32_t seed, pass, stage;
     int err;
-    /* scratch */
-    double *sum, *Mv, *sumVars, *scr;
-    float *fa, *fb, *fc, *fd;
+    scratch_t S;           /* the refining thread's scratch */
+    int par;               /* threads for the inner loops of big splits on the refining thread */
+    struct spec_pool *spec;   /* speculative split workers, or NULL (sequential) */
     uint16_t *gen;         /* diagnostic: split-tree depth of the cluster starting at [begin] */
     uint16_t cur_gen;
 } clustering_t;
@@ -285,17 +303,22 @@ static float ws_block(const float x[64], float P[64])
     return b3 + y[63];
 }
 
-static void ws_load(const float *weights, const uint32_t *ind, size_t begin, size_t end, size_t b,
-                    float x[64])
+/* excl: an index whose weight counts as 0 (split's second draw, which the
+ * reference takes with the first pick's weight temporarily zeroed,
+ * Preprocessor.cpp:597-602; ~0u = none) */
+static void ws_load(const float *weights, const uint32_t *ind, size_t ind_base, size_t begin, size_t end,
+                    size_t b, uint32_t excl, float x[64])
 {
     for (int l = 0; l < 64; l++) {
         size_t i = begin + 64 * b + (size_t)l;
-        x[l] = i < end ? weights[ind ? ind[i] : i] : 0.0f;
+        size_t id = i < end ? (ind ? ind[i - ind_base] : i) : 0;
+        x[l] = i < end && id != excl ? weights[id] : 0.0f;
     }
 }
 
+/* ind: the index array, ind[i - ind_base] for i in [begin, end) */
 static size_t weighted_sample(const float *weights, smp_t *smp, float *prob, size_t begin,
-                              size_t end, const uint32_t *ind, int *err)
+                              size_t end, const uint32_t *ind, size_t ind_base, uint32_t excl, int *err)
 {
     if (begin >= end) { *err = 1; return begin; }
     if (end == begin + 1) { if (prob) *prob = 1; return begin; }
@@ -303,7 +326,7 @@ static size_t weighted_sample(const float *weights, smp_t *smp, float *prob, siz
     float x[64], P[64];
     float weightSum = 0.0f;
     for (size_t b = 0; b < nb; b++) {
-        ws_load(weights, ind, begin, end, b, x);
+        ws_load(weights, ind, ind_base, begin, end, b, excl, x);
         weightSum = weightSum + ws_block(x, P);
     }
     float probability;
@@ -321,13 +344,13 @@ static size_t weighted_sample(const float *weights, smp_t *smp, float *prob, siz
         idx = begin;
         int found = 0;
         for (size_t b = 0; b < nb && !found; b++) {
-            ws_load(weights, ind, begin, end, b, x);
+            ws_load(weights, ind, ind_base, begin, end, b, excl, x);
             const float tot = ws_block(x, P);
             for (int l = 0; l < 64 && begin + 64 * b + (size_t)l < end; l++)
                 if (S + P[l] >= alpha) { idx = begin + 64 * b + (size_t)l; found = 1; break; }
             S = S + tot;
         }
-        probability = weights[ind ? ind[idx] : idx] / weightSum;
+        probability = weights[ind ? ind[idx - ind_base] : idx] / weightSum;
     }
     if (prob) *prob = probability;
     return idx;
@@ -393,12 +416,12 @@ static int unclustered_variance(const mat_t *M, const double *w, const uint32_t 
  * :1100-1106) are taken in their -freciprocal-math form (the reference is
  * built with -funsafe-math-optimizations, build/config-linux-gcc.py:7):
  * one reciprocal per column, a multiply per row. */
-static int cluster_variance(clustering_t *C, const uint32_t *first, long step, uint32_t n_items,
-                            float *inc_u, float *inc_i, float *res_u, float *res_i)
+static int cluster_variance(const clustering_t *C, const scratch_t *S, const uint32_t *first, long step,
+                            uint32_t n_items, float *inc_u, float *inc_i, float *res_u, float *res_i)
 {
     const mat_t *M = &C->M;
     uint32_t R = M->nrows;
-    double *sum = C->sum, *Mv = C->Mv, *sumVars = C->sumVars;
+    double *sum = S->sum, *Mv = S->Mv, *sumVars = S->sumVars;
     for (uint32_t r = 0; r < R; r++) { sum[r] = 0; Mv[r] = 0; sumVars[r] = 0; }
     double weightSum = 0;
     if (n_items == 0) return 1;
@@ -420,7 +443,7 @@ static int cluster_variance(clustering_t *C, const uint32_t *first, long step, u
         weightSum = newWeightSum;
         if (inc_u) {
             double rws = 1.0 / weightSum;
-            double *t = C->scr;
+            double *t = S->scr;
             for (uint32_t r = 0; r < R; r++) t[r] = C->locw[r] * (sumVars[r] * weightSum);
             double ipi = wsum_blk(t, R);
             if (n == 0) {
@@ -435,7 +458,7 @@ static int cluster_variance(clustering_t *C, const uint32_t *first, long step, u
     /* with per-prefix outputs the totals are the last prefix's (same order) */
     double (*wsum)(const double *, uint32_t) = inc_u ? wsum_blk : wsum_d;
     double rws = 1.0 / weightSum;
-    double *t = C->scr;
+    double *t = S->scr;
     for (uint32_t r = 0; r < R; r++) t[r] = C->locw[r] * (Mv[r] * rws);
     double ipu = wsum(t, R);
     for (uint32_t r = 0; r < R; r++) t[r] = C->locw[r] * (sumVars[r] * weightSum);
@@ -492,28 +515,103 @@ static int projpair_cmp(const void *a, const void *b)
     return x->v < y->v ? -1 : (x->v > y->v ? 1 : 0);
 }
 
-/* Clustering::split, Preprocessor.cpp:590-684 */
-static int split(clustering_t *C, uint32_t begin, uint32_t end)
+/* Inner loops of a big split on several threads (test-infrastructure speed-up
+ * for the C5-sized checks, see the speculative splits below): the
+ * projections of disjoint column chunks, and the forward and reverse variance
+ * passes side by side.  Every value is computed by the same code in the same
+ * order as sequentially. */
+typedef struct {
+    const mat_t *M;
+    const float *direction;
+    const uint32_t *v;
+    projpair *proj;
+    uint32_t j0, j1;
+} proj_job;
+
+static void project_range(const proj_job *x, float *c1, float *fd)
 {
+    const mat_t *M = x->M;
+    const uint32_t R = M->nrows;
+    for (uint32_t j = x->j0; j < x->j1; j++) {
+        uint32_t vrl = x->v[j];
+        for (uint32_t r = 0; r < R; r++) c1[r] = m_mean(M, r, vrl);
+        float nc = norm2f(c1, R, fd);
+        float projection;
+        if (nc == 0) {
+            projection = 0;
+        } else {
+            for (uint32_t r = 0; r < R; r++) fd[r] = x->direction[r] * (c1[r] / nc);
+            projection = wsum_f(fd, R);
+        }
+        x->proj[j].p = projection;
+        x->proj[j].v = vrl;
+    }
+}
+
+static void *proj_thread(void *arg)
+{
+    const proj_job *x = (const proj_job *)arg;
+    float *buf = (float *)malloc(sizeof(float) * 2 * ((size_t)x->M->nrows + 1));
+    project_range(x, buf, buf + x->M->nrows + 1);
+    free(buf);
+    return NULL;
+}
+
+typedef struct {
+    const clustering_t *C;
+    scratch_t S;
+    const uint32_t *first;
+    long step;
+    uint32_t n;
+    float *inc_u, *inc_i;
+    float ru, ri;
+    int rc;
+} var_job;
+
+static int cluster_variance(const clustering_t *C, const scratch_t *S, const uint32_t *first, long step,
+                            uint32_t n_items, float *inc_u, float *inc_i, float *res_u, float *res_i);
+static void *var_thread(void *arg)
+{
+    var_job *x = (var_job *)arg;
+    x->rc = cluster_variance(x->C, &x->S, x->first, x->step, x->n, x->inc_u, x->inc_i, &x->ru, &x->ri);
+    return NULL;
+}
+
+/* The outcome of one split: the two children (begin, split point, end) with
+ * their variances.  ok = 0: no split point (the caller's error). */
+typedef struct {
+    int ok, err;
+    uint32_t split;
+    float u1, i1, u2, i2;
+} split_res;
+
+/* Clustering::split, Preprocessor.cpp:590-684, without its side effects on
+ * the clustering state: v = the cluster's ids (positions [begin, end), v[0]
+ * is position begin) are sorted in place; the children's variances come back
+ * in *out.  Reads only C's immutable inputs (matrix, column weights, locality
+ * weights, stream keys), so speculative splits run it on worker threads. */
+static void split_compute(const clustering_t *C, const scratch_t *S, uint32_t begin, uint32_t end,
+                          uint32_t *v, split_res *out)
+{
+    memset(out, 0, sizeof(*out));
     uint32_t clusterSize = end - begin;
-    if (clusterSize < 2) return 0;
+    if (clusterSize < 2) return;
     const mat_t *M = &C->M;
     uint32_t R = M->nrows;
+    int err = 0;
     smp_t smp;
     smp_init(&smp, C->seed, C->pass, ALVRL_O_DOM_CLUSTER, begin, end, C->stage);
 
-    uint32_t vrl1 = C->vrls[weighted_sample(C->colw, &smp, NULL, begin, end, C->vrls, &C->err)];
-    float weight1 = C->colw[vrl1];
-    C->colw[vrl1] = 0.0f;
-    uint32_t vrl2 = C->vrls[weighted_sample(C->colw, &smp, NULL, begin, end, C->vrls, &C->err)];
-    C->colw[vrl1] = weight1;
+    /* the second centre is drawn with the first one's weight zeroed (:597-602) */
+    uint32_t vrl1 = v[weighted_sample(C->colw, &smp, NULL, begin, end, v, begin, ~0u, &err) - begin];
+    uint32_t vrl2 = v[weighted_sample(C->colw, &smp, NULL, begin, end, v, begin, vrl1, &err) - begin];
 
-    float *direction = C->fa, *c1 = C->fb, *c2 = C->fc;
+    float *direction = S->fa, *c1 = S->fb, *c2 = S->fc, *fd = S->fd;
     for (uint32_t r = 0; r < R; r++) { c1[r] = m_mean(M, r, vrl1); c2[r] = m_mean(M, r, vrl2); }
-    float vrl1len = norm2f(c1, R, C->fd);
-    float vrl2len = norm2f(c2, R, C->fd);
+    float vrl1len = norm2f(c1, R, fd);
+    float vrl2len = norm2f(c2, R, fd);
     for (uint32_t r = 0; r < R; r++) c2[r] = c2[r] - c1[r];   /* diff */
-    float diffLen = norm2f(c2, R, C->fd);
+    float diffLen = norm2f(c2, R, fd);
     if (vrl1len != 0 && vrl2len != 0 && diffLen != 0) {
         for (uint32_t r = 0; r < R; r++) direction[r] = c2[r] / diffLen;
     } else {
@@ -525,48 +623,101 @@ static int split(clustering_t *C, uint32_t begin, uint32_t end)
                 float sx = smp_next(&smp), sy = smp_next(&smp);
                 direction[r] = alvrl_o_det_std_normal_x(sx, sy);
             }
-            nd = norm2f(direction, R, C->fd);
-            if (nd == 0 && ++guard > 64) { C->err = 1; nd = 1.0f; }   /* hang guard, as on the device */
+            nd = norm2f(direction, R, fd);
+            if (nd == 0 && ++guard > 64) { err = 1; nd = 1.0f; }   /* hang guard, as on the device */
         } while (nd == 0);
         for (uint32_t r = 0; r < R; r++) direction[r] = direction[r] / nd;
     }
 
     projpair *proj = (projpair *)malloc(sizeof(projpair) * clusterSize);
-    for (uint32_t j = begin; j < end; j++) {
-        uint32_t vrl = C->vrls[j];
-        for (uint32_t r = 0; r < R; r++) c1[r] = m_mean(M, r, vrl);
-        float nc = norm2f(c1, R, C->fd);
-        float projection;
-        if (nc == 0) {
-            projection = 0;
-        } else {
-            for (uint32_t r = 0; r < R; r++) C->fd[r] = direction[r] * (c1[r] / nc);
-            projection = wsum_f(C->fd, R);
+    const int par = clusterSize >= (1u << 14) ? C->par : 0;
+    if (par > 1) {
+        pthread_t th[64];
+        int spawned[64];
+        proj_job pj[64];
+        const int nt = par < 64 ? par : 64;
+        const uint32_t chunk = (clusterSize + (uint32_t)nt - 1) / (uint32_t)nt;
+        for (int t = 0; t < nt; t++) {
+            uint32_t j0 = (uint32_t)t * chunk, j1 = j0 + chunk;
+            if (j0 > clusterSize) j0 = clusterSize;
+            if (j1 > clusterSize) j1 = clusterSize;
+            proj_job x = { M, direction, v, proj, j0, j1 };
+            pj[t] = x;
+            spawned[t] = t > 0 && pthread_create(&th[t], NULL, proj_thread, &pj[t]) == 0;
         }
-        proj[j - begin].p = projection;
-        proj[j - begin].v = vrl;
+        proj_thread(&pj[0]);
+        for (int t = 1; t < nt; t++) {
+            if (spawned[t]) pthread_join(th[t], NULL);
+            else proj_thread(&pj[t]);
+        }
+    } else {
+        proj_job x = { M, direction, v, proj, 0, clusterSize };
+        project_range(&x, c1, fd);
     }
     qsort(proj, clusterSize, sizeof(projpair), projpair_cmp);
-    for (uint32_t j = begin; j < end; j++) C->vrls[j] = proj[j - begin].v;
+    for (uint32_t j = 0; j < clusterSize; j++) v[j] = proj[j].v;
     free(proj);
 
     float *fsu = (float *)malloc(sizeof(float) * clusterSize * 4);
     float *fsi = fsu + clusterSize, *feu = fsu + 2 * clusterSize, *fei = fsu + 3 * clusterSize;
     float v1u, v1i, v2u, v2i;
-    if (cluster_variance(C, C->vrls + begin, 1, clusterSize, fsu, fsi, &v1u, &v1i)) C->err = 1;
-    if (cluster_variance(C, C->vrls + end - 1, -1, clusterSize, feu, fei, &v2u, &v2i)) C->err = 1;
+    if (par > 1) {   /* the two directions on two threads, each with its own scratch */
+        var_job vj = { C, { 0 }, v + clusterSize - 1, -1, clusterSize, feu, fei, 0, 0, 0 };
+        scratch_alloc(&vj.S, R);
+        pthread_t th;
+        const int spawned = pthread_create(&th, NULL, var_thread, &vj) == 0;
+        if (cluster_variance(C, S, v, 1, clusterSize, fsu, fsi, &v1u, &v1i)) err = 1;
+        if (spawned) pthread_join(th, NULL);
+        else var_thread(&vj);
+        v2u = vj.ru; v2i = vj.ri;
+        if (vj.rc) err = 1;
+        scratch_free(&vj.S);
+    } else {
+        if (cluster_variance(C, S, v, 1, clusterSize, fsu, fsi, &v1u, &v1i)) err = 1;
+        if (cluster_variance(C, S, v + clusterSize - 1, -1, clusterSize, feu, fei, &v2u, &v2i)) err = 1;
+    }
     float bestVariance = INFINITY;
     uint32_t bestIndex = UINT32_T_MAX;
     for (uint32_t i = 1; i < clusterSize; ++i) {
         float thisVar = fsu[i - 1] + fsi[i - 1] + feu[clusterSize - 1 - i] + fei[clusterSize - 1 - i];
         if (thisVar < bestVariance) { bestVariance = thisVar; bestIndex = i; }
     }
-    if (bestIndex == UINT32_T_MAX) { C->err = 1; free(fsu); return 0; }
-    uint32_t splitIndex = begin + bestIndex;
-    add_cluster(C, begin, splitIndex, fsu[bestIndex - 1], fsi[bestIndex - 1]);
-    add_cluster(C, splitIndex, end, feu[clusterSize - 1 - bestIndex], fei[clusterSize - 1 - bestIndex]);
+    out->err = err;
+    if (bestIndex != UINT32_T_MAX) {
+        out->ok = 1;
+        out->split = begin + bestIndex;
+        out->u1 = fsu[bestIndex - 1]; out->i1 = fsi[bestIndex - 1];
+        out->u2 = feu[clusterSize - 1 - bestIndex]; out->i2 = fei[clusterSize - 1 - bestIndex];
+    } else {
+        out->err = 1;
+    }
     free(fsu);
+}
+
+/* the split's effect on the clustering (:680-683): the two children */
+static int split_apply(clustering_t *C, uint32_t begin, uint32_t end, const split_res *r)
+{
+    if (r->err) C->err = 1;
+    if (!r->ok) return 0;
+    add_cluster(C, begin, r->split, r->u1, r->i1);
+    add_cluster(C, r->split, end, r->u2, r->i2);
     return 1;
+}
+
+static int spec_take(clustering_t *C, uint32_t begin, uint32_t end, split_res *r);
+static void spec_offer(clustering_t *C);
+
+/* Clustering::split (:590-684) of the popped cluster [begin, end): its
+ * speculative result when a worker has it (identical: the split depends only
+ * on the cluster's ids and its stream), else computed here. */
+static int split(clustering_t *C, uint32_t begin, uint32_t end)
+{
+    split_res r;
+    if (!(C->spec && spec_take(C, begin, end, &r)))
+        split_compute(C, &C->S, begin, end, C->vrls + begin, &r);
+    int ok = split_apply(C, begin, end, &r);
+    if (C->spec) spec_offer(C);
+    return ok;
 }
 
 static uint32_t n_clusters(const clustering_t *C) { return (uint32_t)(C->singles.n + C->pq.n); }
@@ -597,6 +748,163 @@ static void restore(clustering_t *C)
     cheap_copy(&C->pq, &C->sh_pq); ulist_copy(&C->singles, &C->sh_singles);
 }
 
+/* ------------------------------------------------ speculative splits -- */
+/* Test-infrastructure speed-up, not part of the restatement: a split's result
+ * depends only on its cluster's ids and its stream (keyed by the cluster's
+ * range), and live clusters are disjoint ranges of vrls, so worker threads
+ * may split the clusters near the top of the heap ahead of the sequential
+ * loop, each on a private copy of the range.  The loop commits a finished
+ * result when it pops that cluster and computes anything else itself, so the
+ * outcome is the sequential one bit for bit (the same idea as the device's
+ * team mode, refine.hip).  Used while no restore() can intervene: it stops
+ * before refineAdaptively's restore, and is off for small jobs.
+ *   ALVRL_ORACLE_THREADS   workers (default min(16, online CPUs), 0 = off)
+ *   ALVRL_ORACLE_SPEC_MIN  job size (rows x VRLs) from which it is used
+ *                          (default 2^24; tests set 0 to exercise it) */
+typedef struct {
+    uint32_t begin, end;
+    int state;                 /* 0 queued, 1 running, 2 done */
+    uint32_t *buf;             /* the sorted ids, when done */
+    split_res res;
+} spec_entry;
+
+struct spec_pool {
+    pthread_mutex_t mu;
+    pthread_cond_t cv_work, cv_done;
+    pthread_t *th;
+    int nth, stop;
+    const clustering_t *C;
+    spec_entry *e;
+    long n, cap;
+    uint64_t task_min;         /* rows x cluster size below which a split is not offered */
+    long width;                /* heap entries examined per offer */
+};
+
+static void *spec_worker(void *arg)
+{
+    struct spec_pool *P = (struct spec_pool *)arg;
+    const clustering_t *C = P->C;
+    scratch_t S;
+    scratch_alloc(&S, C->M.nrows);
+    pthread_mutex_lock(&P->mu);
+    while (!P->stop) {
+        long k = 0;
+        while (k < P->n && P->e[k].state != 0) k++;
+        if (k == P->n) { pthread_cond_wait(&P->cv_work, &P->mu); continue; }
+        spec_entry *x = &P->e[k];
+        x->state = 1;
+        const uint32_t b = x->begin, e = x->end;
+        pthread_mutex_unlock(&P->mu);
+        uint32_t *buf = (uint32_t *)malloc(sizeof(uint32_t) * (e - b));
+        memcpy(buf, C->vrls + b, sizeof(uint32_t) * (e - b));
+        split_res r;
+        split_compute(C, &S, b, e, buf, &r);
+        pthread_mutex_lock(&P->mu);
+        for (k = 0; k < P->n; k++)      /* entries move when others are removed */
+            if (P->e[k].begin == b && P->e[k].end == e) break;
+        P->e[k].buf = buf;
+        P->e[k].res = r;
+        P->e[k].state = 2;
+        pthread_cond_broadcast(&P->cv_done);
+    }
+    pthread_mutex_unlock(&P->mu);
+    scratch_free(&S);
+    return NULL;
+}
+
+static void spec_remove(struct spec_pool *P, long k)
+{
+    P->e[k] = P->e[P->n - 1];
+    P->n--;
+}
+
+static void spec_start(clustering_t *C)
+{
+    const char *t = getenv("ALVRL_ORACLE_THREADS");
+    const char *m = getenv("ALVRL_ORACLE_SPEC_MIN");
+    long nth = t ? atol(t) : sysconf(_SC_NPROCESSORS_ONLN);
+    if (!t && nth > 16) nth = 16;
+    const uint64_t job_min = m ? (uint64_t)atoll(m) : (1ull << 24);
+    if (nth < 1 || (uint64_t)C->M.nrows * C->nv < job_min) return;
+    struct spec_pool *P = (struct spec_pool *)calloc(1, sizeof(*P));
+    pthread_mutex_init(&P->mu, NULL);
+    pthread_cond_init(&P->cv_work, NULL);
+    pthread_cond_init(&P->cv_done, NULL);
+    P->C = C;
+    P->task_min = m ? 0 : (1u << 16);
+    P->width = 2 * nth + 8;
+    P->th = (pthread_t *)calloc((size_t)nth, sizeof(pthread_t));
+    for (long i = 0; i < nth; i++)
+        if (pthread_create(&P->th[P->nth], NULL, spec_worker, P) == 0) P->nth++;
+    C->spec = P;
+    C->par = P->nth;
+}
+
+/* join the workers and drop every pending result */
+static void spec_stop(clustering_t *C)
+{
+    struct spec_pool *P = C->spec;
+    if (!P) return;
+    pthread_mutex_lock(&P->mu);
+    P->stop = 1;
+    pthread_cond_broadcast(&P->cv_work);
+    pthread_mutex_unlock(&P->mu);
+    for (int i = 0; i < P->nth; i++) pthread_join(P->th[i], NULL);
+    for (long k = 0; k < P->n; k++) free(P->e[k].buf);
+    free(P->e); free(P->th);
+    pthread_mutex_destroy(&P->mu);
+    pthread_cond_destroy(&P->cv_work);
+    pthread_cond_destroy(&P->cv_done);
+    free(P);
+    C->spec = NULL;
+    C->par = 0;
+}
+
+/* the popped cluster [begin, end): 1 = a worker's result, committed here */
+static int spec_take(clustering_t *C, uint32_t begin, uint32_t end, split_res *r)
+{
+    struct spec_pool *P = C->spec;
+    pthread_mutex_lock(&P->mu);
+    for (;;) {
+        long k = 0;
+        while (k < P->n && !(P->e[k].begin == begin && P->e[k].end == end)) k++;
+        if (k == P->n) { pthread_mutex_unlock(&P->mu); return 0; }
+        if (P->e[k].state == 0) { spec_remove(P, k); pthread_mutex_unlock(&P->mu); return 0; }
+        if (P->e[k].state == 1) { pthread_cond_wait(&P->cv_done, &P->mu); continue; }
+        memcpy(C->vrls + begin, P->e[k].buf, sizeof(uint32_t) * (end - begin));
+        *r = P->e[k].res;
+        free(P->e[k].buf);
+        spec_remove(P, k);
+        pthread_mutex_unlock(&P->mu);
+        return 1;
+    }
+}
+
+/* queue the multi-clusters near the top of the heap not queued yet */
+static void spec_offer(clustering_t *C)
+{
+    struct spec_pool *P = C->spec;
+    const uint64_t R = C->M.nrows;
+    int added = 0;
+    pthread_mutex_lock(&P->mu);
+    for (long i = 0; i < C->pq.n && i < P->width; i++) {
+        const cnode *cn = &C->pq.v[i];
+        if (cn->end - cn->begin < 2 || (uint64_t)(cn->end - cn->begin) * R < P->task_min) continue;
+        long k = 0;
+        while (k < P->n && !(P->e[k].begin == cn->begin && P->e[k].end == cn->end)) k++;
+        if (k < P->n) continue;
+        if (P->n == P->cap) {
+            P->cap = P->cap ? 2 * P->cap : 64;
+            P->e = (spec_entry *)realloc(P->e, sizeof(spec_entry) * P->cap);
+        }
+        spec_entry x = { cn->begin, cn->end, 0, NULL, { 0, 0, 0, 0, 0, 0, 0 } };
+        P->e[P->n++] = x;
+        added = 1;
+    }
+    if (added) pthread_cond_broadcast(&P->cv_work);
+    pthread_mutex_unlock(&P->mu);
+}
+
 /* Clustering ctor, Preprocessor.cpp:301-341 */
 static int clustering_init(clustering_t *C, const mat_t *M, const double *locw,
                            const uint32_t *init_vrls, const uint32_t *init_off, uint32_t ninit,
@@ -612,12 +920,9 @@ static int clustering_init(clustering_t *C, const mat_t *M, const double *locw,
     if (fabs((float)n1 - 1) > 1e-3) return 1;
     if (pixelUndersampling <= 0 || pixelUndersampling > 1) return 1;
     uint32_t R = M->nrows;
-    C->sum = (double *)calloc(R * 4 + 4, sizeof(double));
-    C->Mv = C->sum + R + 1; C->sumVars = C->Mv + R + 1; C->scr = C->sumVars + R + 1;
-    C->fa = (float *)calloc(R * 4 + 4, sizeof(float));
-    C->fb = C->fa + R + 1; C->fc = C->fb + R + 1; C->fd = C->fc + R + 1;
+    scratch_alloc(&C->S, R);
     C->colw = (float *)malloc(sizeof(float) * (M->nvrl ? M->nvrl : 1));
-    if (column_weights(M, locw, C->colw, C->sum)) return 1;
+    if (column_weights(M, locw, C->colw, C->S.sum)) return 1;
     C->nv = init_off[ninit];
     C->vrls = (uint32_t *)malloc(sizeof(uint32_t) * (C->nv ? C->nv : 1));
     memcpy(C->vrls, init_vrls, sizeof(uint32_t) * C->nv);
@@ -627,7 +932,7 @@ static int clustering_init(clustering_t *C, const mat_t *M, const double *locw,
         uint32_t b = init_off[i], e = init_off[i + 1];
         float u = 0, iv = 0;
         if (b == e) { C->err = 1; continue; }
-        if (cluster_variance(C, C->vrls + b, 1, e - b, NULL, NULL, &u, &iv)) C->err = 1;
+        if (cluster_variance(C, &C->S, C->vrls + b, 1, e - b, NULL, NULL, &u, &iv)) C->err = 1;
         add_cluster(C, b, e, u, iv);
     }
     if (unclustered_variance(M, locw, C->vrls, C->vrls + C->nv, &C->tracingVar, &C->unclIntVar))
@@ -637,7 +942,7 @@ static int clustering_init(clustering_t *C, const mat_t *M, const double *locw,
 
 static void clustering_free(clustering_t *C)
 {
-    free(C->sum); free(C->fa); free(C->colw); free(C->vrls); free(C->gen);
+    scratch_free(&C->S); free(C->colw); free(C->vrls); free(C->gen);
     free(C->pq.v); free(C->singles.v); free(C->sh_pq.v); free(C->sh_singles.v);
 }
 
@@ -676,8 +981,13 @@ static int refine_adaptive(clustering_t *C)
         if (lower_bound(C) >= best) break;
         if (C->err) return 0;
     }
+    spec_stop(C);      /* before restore(): the replay below is sequential */
     restore(C);
     if (dc != 1) {
+        /* the replay pops the restored clusters; their ids are what the
+         * discarded splits left, so only results computed from here on count */
+        spec_start(C);
+        if (C->spec) spec_offer(C);
         int corrected = (int)(0.5 + dc * bestN);
         for (int i = 0; i < corrected; i++) {
             if (C->pq.n == 0) break;
@@ -690,8 +1000,11 @@ static int refine_adaptive(clustering_t *C)
 
 static int refine(clustering_t *C, float undersampling)
 {
-    if (undersampling <= 0) return refine_adaptive(C);
-    return refine_fixed(C, undersampling);
+    spec_start(C);
+    if (C->spec) spec_offer(C);
+    int ok = undersampling <= 0 ? refine_adaptive(C) : refine_fixed(C, undersampling);
+    spec_stop(C);
+    return ok;
 }
 
 /* Clustering::sampleRepresentatives, Preprocessor.cpp:354-378 */
@@ -704,7 +1017,7 @@ static uint32_t sample_reps(clustering_t *C, uint32_t stage, uint32_t *reps, flo
         smp_t smp;
         smp_init(&smp, C->seed, C->pass, ALVRL_O_DOM_CLUSTER, cn->begin, cn->end, stage);
         float prob = 1.0f;
-        size_t j = weighted_sample(C->colw, &smp, &prob, cn->begin, cn->end, C->vrls, &C->err);
+        size_t j = weighted_sample(C->colw, &smp, &prob, cn->begin, cn->end, C->vrls, 0, ~0u, &C->err);
         reps[i] = C->vrls[j];
         w[i] = 1.0f / prob;
         i++;

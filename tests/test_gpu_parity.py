@@ -409,3 +409,54 @@ def test_refine_bit_exact_row_blocks(oracle, gpu_ok):
         assert bool(refined[s]) == cref, sizes[s]
         assert np.array_equal(gr, cr), sizes[s]
         assert np.array_equal(gw.view(np.uint32), cw.view(np.uint32)), sizes[s]
+
+
+@pytest.mark.parametrize("undersampling", [-1.0, 20.0])
+def test_refine_bit_exact_c5_rows(oracle, gpu_ok, undersampling):
+    """Local matrices of C5's size (2048^2 / 100 slices: ~655 representative
+    rows, 11 row blocks) and around it -- 320, 512, 655 and 700 rows -- on
+    the >256-row variance engine: device == oracle, bit for bit."""
+    torch = _torch()
+    sizes = [320, 512, 655, 700]
+    ctx, d_Rt, Rt, jobs, init, init_off = _refine_case(oracle, 64, 64, 900, sizes, undersampling, torch)
+    off, reps, w, refined = ctx.refine(d_Rt, Rt.shape[1], jobs, init, init_off)
+    for s, j in enumerate(jobs):
+        cr, cw, cref = oracle.cluster_refine(Rt, j["rows"], j["locw"], init, init_off,
+                                             j["pixel_undersampling"], undersampling,
+                                             stage_refine=j["stage_refine"],
+                                             stage_sample=j["stage_sample"], seed=SEED_RNG)
+        gr, gw = reps[off[s]:off[s + 1]], w[off[s]:off[s + 1]]
+        print(f"{sizes[s]} rows: {len(cr)} clusters")
+        assert bool(refined[s]) == cref, sizes[s]
+        assert np.array_equal(gr, cr), sizes[s]
+        assert np.array_equal(gw.view(np.uint32), cw.view(np.uint32)), sizes[s]
+
+
+@pytest.mark.parametrize("depth_correction", [0.8, 1.3])
+def test_refine_depth_correction(oracle, gpu_ok, depth_correction):
+    """refineAdaptively with depthCorrection != 1 (Preprocessor.cpp:456-469:
+    after the convergence stop the snapshot is restored and the splits are
+    replayed with the replayable sampler, src/libbidir/rsampler.cpp:68-91, up
+    to the corrected cluster count): device == oracle, bit for bit, on
+    slices of 1-5 row blocks."""
+    torch = _torch()
+    ctx, d_Rt, Rt, jobs, init, init_off = _refine_case(oracle, 96, 96, 1500, [40, 64, 150, 230, 300], -1.0,
+                                                       torch)
+    for j in jobs:
+        j["depth_correction"] = depth_correction
+    off, reps, w, refined = ctx.refine(d_Rt, Rt.shape[1], jobs, init, init_off)
+    for s, j in enumerate(jobs):
+        cr, cw, cref = oracle.cluster_refine(Rt, j["rows"], j["locw"], init, init_off,
+                                             j["pixel_undersampling"], -1.0,
+                                             depth_correction=depth_correction,
+                                             stage_refine=j["stage_refine"],
+                                             stage_sample=j["stage_sample"], seed=SEED_RNG)
+        c1, _, _ = oracle.cluster_refine(Rt, j["rows"], j["locw"], init, init_off,
+                                         j["pixel_undersampling"], -1.0, stage_refine=j["stage_refine"],
+                                         stage_sample=j["stage_sample"], seed=SEED_RNG)
+        gr, gw = reps[off[s]:off[s + 1]], w[off[s]:off[s + 1]]
+        print(f"slice {s} ({len(j['rows'])} rows): {len(cr)} clusters at depthCorrection "
+              f"{depth_correction}, {len(c1)} at 1")
+        assert bool(refined[s]) == cref
+        assert np.array_equal(gr, cr), s
+        assert np.array_equal(gw.view(np.uint32), cw.view(np.uint32)), s

@@ -88,6 +88,10 @@ def test_c1_pipeline_adaptive(oracle, gpu_ok):
     ("globalCluster=true;globalUndersampling=20", {"global_cluster": True, "global_undersampling": 20.0}),
     ("globalCluster=true;targetNumSlices=40", {"global_cluster": True, "target_num_slices": 40}),
     ("Rsamples=2", {}),
+    # depthCorrection (Preprocessor.cpp:456-469): the adaptive refinement
+    # replays its splits past the best snapshot with the scaled bound
+    ("depthCorrection=0.8", {"depth_correction": 0.8}),
+    ("depthCorrection=1.3;targetNumSlices=60", {"depth_correction": 1.3, "target_num_slices": 60}),
 ])
 def test_pipeline_variants(oracle, gpu_ok, props, prep_kw):
     import alvrl
@@ -425,12 +429,18 @@ def test_team_wait_timeout(gpu_ok, capfd):
 @pytest.mark.parametrize("props", ["targetNumSlices=100;localUndersampling=-1",
                                    "targetNumSlices=100;localUndersampling=100"])
 def test_refine_c4_scale(oracle, gpu_ok, props):
-    """Refinement at the benchmark's own scale (C4 / C3: 1024^2, 100k VRLs,
-    100 slices, team mode with speculation and roaming helpers as by
-    default): the oracle's Clustering (Preprocessor.cpp:254-283, strict
-    build) on the device's job for three slices -- the most rows, the most
-    clusters and a median one -- gives the device's cluster lists bit for
-    bit (representatives and weights)."""
+    """The benchmark's own configs (C4 / C3: 1024^2, 100k VRLs, 100 slices,
+    team mode with speculation and roaming helpers as by default).
+
+      * refinement: the oracle's Clustering (Preprocessor.cpp:254-283, strict
+        build) on the device's job for three slices -- the most rows, the
+        most clusters and a median one -- gives the device's cluster lists
+        bit for bit (representatives and weights);
+      * frame: every 64th image row of the device's full-frame render
+        (getClusteredVrlContributions, vrlIntegrator.cpp:542-599, through
+        alvrl_integrator_render) against the oracle's clustered gather with
+        the device's cluster lists, on test_gpu_parity's tolerance."""
+    import torch
     import alvrl
     W = H = 1024
     scene = alvrl.scene_default(W, H)
@@ -439,7 +449,20 @@ def test_refine_c4_scale(oracle, gpu_ok, props):
     it.set_vrls(vrls, pc)
     it.preprocess(scene)
     it.prepass(2)
+    fb = torch.zeros(W * H * 3, dtype=torch.float32, device="cuda")
+    it.render(fb)
+    torch.cuda.synchronize()
+    img = fb.view(H * W, 3).cpu().numpy()
     cl = it.clusters()
+    p2s = it.slices()
+    pid = (np.arange(0, H, 64, dtype=np.uint32)[:, None] * W + np.arange(W, dtype=np.uint32)[None, :]).ravel()
+    sl = p2s[(pid % W) * H + pid // W]                 # m_slices[y + H*x]
+    recs = oracle.records(oracle.scene(W, H))[pid]
+    P = oracle.params(oracle.medium(), seed=SEED_RNG, pass_=2)
+    cpu, _ = oracle.gather_clustered(P, recs, sl, vrls, pc, cl["slice_off"], cl["reps"], cl["weights"],
+                                     cl["fb_reps"], cl["fb_weights"], rec_ids=pid)
+    assert (sl != 0xFFFFFFFF).all() and img.any()
+    _assert_close(img[pid], cpu, f"{props} frame, every 64th row")
     off, _ = it.reps()
     nrows, ncl = np.diff(off), np.diff(cl["slice_off"])
     kv = dict(x.split("=", 1) for x in props.split(";"))
@@ -500,53 +523,6 @@ def test_context_reuse_across_passes(gpu_ok):
             assert np.array_equal(cl[key].view(np.uint32), fresh[k][0][key].view(np.uint32)), (k, key)
         assert np.array_equal(fb.view(np.uint32), fresh[k][1].view(np.uint32)), k
     it.close()
-
-
-@pytest.mark.parametrize("props", ["targetNumSlices=40", "targetNumSlices=30;localUndersampling=10",
-                                   "targetNumSlices=25;depthCorrection=0.8"])
-@pytest.mark.skipif(os.environ.get("ALVRL_TEST_FUSED") != "1",
-                    reason="fusedRender is experimental and off by default (slower than the plain path at C4, "
-                           "DESIGN.md 5.2); ALVRL_TEST_FUSED=1 runs it")
-def test_fused_render_identical(gpu_ok, props):
-    """fusedRender (alvrl_refine_gather): the slices rendered beside the
-    refinement as their jobs finish give the frame of the plain path
-    (alvrl_refine, alvrl_set_clusters, alvrl_gather_clustered) bit for bit,
-    with the same cluster lists; over two passes and with a second render of
-    the same pass (which re-accumulates the pass's frame: its pairs are not
-    gathered again, so only the first render of a pass counts them)."""
-    import torch
-    import alvrl
-    w, h = 256, 192
-    scene = alvrl.scene_default(w, h)
-    vrls, pc = alvrl.trace_vrls(scene, 4000, seed=SEED_VRL)
-    out = {}
-    for fused in (False, True):
-        it = alvrl.Integrator(props + f";seed={SEED_RNG};fusedRender={'true' if fused else 'false'}", device=0)
-        it.set_vrls(vrls, pc)
-        it.preprocess(scene)
-        frames, cls = [], []
-        for p in (1, 2):
-            it.prepass(p)
-            if fused:
-                assert it.stats()["render_fused"] > 0
-            for _ in range(2):
-                fb = torch.zeros(w * h * 3, dtype=torch.float32, device="cuda")
-                it.render(fb)
-                torch.cuda.synchronize()
-                frames.append(fb.cpu().numpy())
-            cls.append(it.clusters())
-        st = it.stats()
-        out[fused] = (frames, cls, st["contrib_render"] // (2 if not fused else 1), st["contrib_preprocess"])
-        it.close()
-    (f0, c0, r0, p0), (f1, c1, r1, p1) = out[False], out[True]
-    for n, (a, b) in enumerate(zip(f0, f1)):
-        assert a.any(), n
-        bad = np.nonzero(a.view(np.uint32) != b.view(np.uint32))[0]
-        assert bad.size == 0, (n, bad.size, bad[:4].tolist(), a[bad[:4]].tolist(), b[bad[:4]].tolist())
-    for a, b in zip(c0, c1):
-        for k in a:
-            assert np.array_equal(a[k].view(np.uint32), b[k].view(np.uint32)), k
-    assert (r0, p0) == (r1, p1)
 
 
 def test_cluster_info_checkpoint(gpu_ok, tmp_path):

@@ -249,3 +249,35 @@ def test_oracle_global_cluster(oracle, gu):
     base.sample_slice_mapping(64.0, W * H)
     cl0 = base.build_clusters(Rt)
     assert not np.array_equal(cl0["reps"], cl["reps"])
+
+
+@pytest.mark.parametrize("undersampling,dc", [(-1.0, 1.0), (15.0, 1.0), (-1.0, 0.8), (-1.0, 1.3)])
+def test_oracle_speculative_splits_identical(oracle, monkeypatch, undersampling, dc):
+    """The oracle's speculative split workers and its threaded big-split loops
+    (alvrl_preproc.c spec_pool / proj_thread / var_thread, the speed-up that
+    makes C5-sized checks feasible) give the sequential restatement's
+    clusters and weights bit for bit, in adaptive, fixed-depth and
+    depthCorrection replay modes."""
+    W = 128
+    sc = oracle.scene(W, W)
+    m = oracle.medium()
+    vrls, pc = oracle.trace(sc, m, 4000, seed=0x5EED0001)
+    rng = np.random.default_rng(3)
+    rows = np.sort(rng.choice(W * W, 70, replace=False)).astype(np.uint32)
+    _, R, _ = oracle.gather_brute(oracle.params(m), oracle.records(sc)[rows], vrls, pc, rec_ids=rows,
+                                  domain=2, want_R=True)
+    Rt = np.ascontiguousarray(R.transpose(1, 0, 2))
+    nzm = (Rt[..., 0] != 0).any(axis=1)
+    init = np.concatenate([np.nonzero(nzm)[0], np.nonzero(~nzm)[0]]).astype(np.uint32)
+    off = [0, int(nzm.sum())] + ([len(init)] if (~nzm).any() else [])
+    lr = np.arange(len(rows), dtype=np.uint32)
+    lw = np.full(len(rows), 1.0 / len(rows))
+    out = []
+    for env in ({"ALVRL_ORACLE_THREADS": "0"}, {"ALVRL_ORACLE_THREADS": "4", "ALVRL_ORACLE_SPEC_MIN": "0"}):
+        monkeypatch.delenv("ALVRL_ORACLE_SPEC_MIN", raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        out.append(oracle.cluster_refine(Rt, lr, lw, init, off, 0.3, undersampling, depth_correction=dc))
+    (a, aw, ar), (b, bw, br) = out
+    assert ar == br and len(a) > 10
+    assert np.array_equal(a, b) and np.array_equal(aw.view(np.uint32), bw.view(np.uint32))

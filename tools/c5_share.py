@@ -1,0 +1,76 @@
+"""C5 rank-0 share on one GPU (tests/c5_share.py): timings, and with
+--oracle the strict oracle's refinement of the smallest local slice compared
+bit for bit with the device's lists (a heartbeat line every 20 s while the
+oracle runs, so a long check is not taken for a hang).
+
+  python tools/c5_share.py [--oracle] [--json out.json] [--props "..."]
+"""
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+for p in (ROOT, os.path.join(ROOT, "tests"), os.path.join(ROOT, "mitsuba-alvrl_amd"), os.path.join(ROOT, "oracle")):
+    sys.path.insert(0, p)
+
+import numpy as np   # noqa: E402
+
+import c5_share      # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--oracle", action="store_true")
+    ap.add_argument("--props", default="")
+    ap.add_argument("--json", default="")
+    ap.add_argument("--vrls", type=int, default=c5_share.C5_VRLS)
+    a = ap.parse_args()
+    it, info, mine = c5_share.run_share(a.props, nvrl=a.vrls, log=lambda s: print(s, flush=True))
+    cl = it.clusters()
+    ncl = np.diff(cl["slice_off"])
+    info["clusters_local"] = [int(ncl[s]) for s in mine]
+    print("clusters per local slice:", info["clusters_local"], flush=True)
+    if a.oracle:
+        from oracle import Oracle
+        o = Oracle()
+        k = int(np.argmin(info["rows_local"]))
+        s = mine[k]
+        t0 = time.time()
+        job = it.slice_job(s)
+        n = job["R"].shape[1]
+        print(f"slice {s}: {n} rows x {job['R'].shape[0]} VRLs copied in {time.time() - t0:.1f} s", flush=True)
+        res = {}
+
+        def work():
+            res["out"] = o.cluster_refine(job["R"], np.arange(n, dtype=np.uint32), job["locw"], job["init_vrls"],
+                                          job["init_off"], job["pixel_undersampling"], -1.0,
+                                          seed=c5_share.SEED_RNG, pass_=0, stage_refine=3 + 2 * s,
+                                          stage_sample=4 + 2 * s)
+
+        th = threading.Thread(target=work)
+        t1 = time.time()
+        th.start()
+        while th.is_alive():
+            th.join(20)
+            if th.is_alive():
+                print(f"  oracle refining slice {s}: {time.time() - t1:.0f} s", flush=True)
+        reps, w, refined = res["out"]
+        b, e = cl["slice_off"][s], cl["slice_off"][s + 1]
+        same = bool(refined and np.array_equal(reps, cl["reps"][b:e]) and
+                    np.array_equal(w.view(np.uint32), cl["weights"][b:e].view(np.uint32)))
+        info["oracle"] = dict(slice=s, rows=n, clusters_oracle=len(reps), clusters_device=int(e - b),
+                              identical=same, oracle_s=time.time() - t1)
+        print(f"oracle slice {s}: {len(reps)} clusters (device {e - b}), identical: {same}, "
+              f"{time.time() - t1:.1f} s", flush=True)
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump(info, f, indent=1)
+    it.close()
+
+
+if __name__ == "__main__":
+    main()
