@@ -12,18 +12,19 @@ sampling, R build, per-slice refinement) for the clustered configs and nothing
 for the brute-force one; the render is the per-pixel gather.  Rank 0 prints one JSON line.
 
 Multi-GPU (--shard):
-  passes (default)  progressive passes are independent units: at step i rank r
+  slices (default)  one pass per step, sharded inside the pass (BASELINE.json
+                    north_star): rank r builds R for and refines
+                    slices s % N == r, the non-zero mask is OR-reduced and the
+                    cluster lists are all-gathered over RCCL
+                    (alvrl_integrator_prepass_dist), 64x64 image tiles are
+                    dealt round robin, and one RCCL reduce brings the
+                    framebuffer to rank 0: "scaling": "strong".
+  passes            progressive passes are independent units: at step i rank r
                     runs pass i*N + r over the whole frame (its own
                     representatives, R and clusters) and one RCCL reduce over
                     xGMI sums the N passes' framebuffers into rank 0 -- the
                     progressive accumulation (integrator.cpp:396-433) spread
                     over GPUs.  Per-GPU work is fixed: "scaling": "weak".
-  slices            one pass per step, sharded inside the pass:
-                    rank r builds R for and refines slices s % N == r, the
-                    non-zero mask is OR-reduced and the cluster lists are
-                    all-gathered over RCCL (alvrl_integrator_prepass_dist),
-                    64x64 image tiles are dealt round robin, and the
-                    framebuffer is reduced to rank 0: "scaling": "strong".
 """
 from __future__ import annotations
 
@@ -70,7 +71,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="C4", choices=sorted(CONFIGS))
-    ap.add_argument("--shard", default="passes", choices=["passes", "slices"],
+    ap.add_argument("--shard", default="slices", choices=["passes", "slices"],
                     help="multi-GPU decomposition (see the module docstring)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-row-stride", type=int, default=64,
@@ -278,7 +279,7 @@ def cpu_baseline(args, cfg, scene, vrls, pc, fb, it, clustered):
     from oracle import Oracle
     o = Oracle(fast=True)
     W, H = cfg["w"], cfg["h"]
-    threads = int(os.environ.get("ALVRL_CPU_THREADS", "16"))
+    threads = cpu_threads()
     rows = np.arange(0, H, args.cpu_row_stride)
     pix = (rows[:, None] * W + np.arange(W)[None, :]).reshape(-1).astype(np.uint32)
     osc = o.scene(W, H)
@@ -308,7 +309,7 @@ def cpu_baseline(args, cfg, scene, vrls, pc, fb, it, clustered):
     rmse = float(np.sqrt(np.mean(diff ** 2)))
     rel = np.abs(diff) / np.maximum(np.abs(img), 1e-30)
     base = {"value": cnt / dt, "unit": "VRL contributions/s", "cores": threads, "kind": "port",
-            "sample": sample, "seconds": dt,
+            "sample": sample, "seconds": dt, "host_cpus": _host_cpus(),
             "cpu": _cpu_model(), "flags": "reference CXXFLAGS (build/config-linux-gcc.py:7)"}
     acc = {"rmse": rmse, "mean": float(np.abs(img).mean()), "rmse_rel": rmse / max(float(np.abs(img).mean()), 1e-30),
            "max_rel": float(rel.max()), "median_rel": float(np.median(rel)), "pixels": int(len(pix))}
@@ -317,21 +318,25 @@ def cpu_baseline(args, cfg, scene, vrls, pc, fb, it, clustered):
 
 def cpu_baseline_prepass(args, cfg, vrls, pc, it, render_base, pre_pairs_step, render_pairs_step):
     """Clustered configs: one CPU step = R build + refinement + clustered render.
-    Bounded samples: the R rows of one slice's representatives (16 threads),
-    that slice's refinement (one thread: the reference refines whole slices
-    per worker thread, Preprocessor.cpp:722-773), and the clustered gather
-    sample of cpu_baseline().  The step time is extrapolated from them
-    (R rows x columns, ceil(slices / threads) refinements, render pairs) and
-    value = the step's contributions / that time."""
+    Bounded samples: the R rows of one slice's representatives (all threads),
+    the refinement of the median-size and of the largest slice (one thread
+    each: the reference refines whole slices per worker thread,
+    Preprocessor.cpp:722-773), and the clustered gather sample of
+    cpu_baseline().  The step time is extrapolated from them: R rows x
+    columns at the measured rate, ceil(slices / threads) rounds of
+    refinement of which the last waits for the largest slice, and the render
+    pairs at the measured rate; value = the step's contributions / that time."""
     import numpy as np
     from oracle import Oracle
     o = Oracle(fast=True)
     W, H = cfg["w"], cfg["h"]
-    threads = int(os.environ.get("ALVRL_CPU_THREADS", "16"))
+    threads = cpu_threads()
     off, pix = it.reps()
     ns = len(off) - 1
-    s0 = int(np.argsort(np.diff(off))[ns // 2])            # a median-size slice
-    rp = pix[off[s0]:off[s0 + 1]]
+    nrows = np.diff(off)
+    s_med = int(np.argsort(nrows, kind="stable")[ns // 2])      # a median-size slice
+    s_max = int(np.argmax(nrows))                                # the largest slice
+    rp = pix[off[s_med]:off[s_med + 1]]
     rec_ids = ((rp % H) * W + rp // H).astype(np.uint32)   # column-major ids -> row-major
     recs = o.records(o.scene(W, H))[rec_ids]
     last_pass = args.warmup + args.steps - 1
@@ -339,45 +344,77 @@ def cpu_baseline_prepass(args, cfg, vrls, pc, it, render_base, pre_pairs_step, r
     t0 = time.perf_counter()
     _, Rs, cnt = o.gather_brute(P, recs, vrls, pc, rec_ids=rec_ids, domain=2, want_R=True, nthreads=threads)
     t_r = time.perf_counter() - t0
-    # the refinement sample is the device's own job for slice s0 (its R rows,
-    # locality weights, pixel undersampling and initial clusters), so the
-    # oracle's clusters must equal the device's bit for bit (C4 scale: 100k
-    # columns, team mode with speculation and roaming helpers)
-    job = it.slice_job(s0)
-    nrow = job["R"].shape[1]
     kv = dict(x.split("=", 1) for x in cfg["props"].split(";") if "=" in x)
     under = float(kv.get("localUndersampling", -1.0))
     dcorr = float(kv.get("depthCorrection", 1.0))
-    t0 = time.perf_counter()
-    reps, w, refined = o.cluster_refine(job["R"], np.arange(nrow, dtype=np.uint32), job["locw"],
-                                        job["init_vrls"], job["init_off"], job["pixel_undersampling"], under,
-                                        depth_correction=dcorr, seed=SEED_RNG, pass_=last_pass, stage_refine=3 + 2 * s0,
-                                        stage_sample=4 + 2 * s0)
-    t_ref = time.perf_counter() - t0
-    # the timed run is the reference-flags build (reassociating float maths);
-    # the bit-exact check runs the strict build of the same restatement
-    reps, w, refined = Oracle().cluster_refine(job["R"], np.arange(nrow, dtype=np.uint32), job["locw"],
-                                               job["init_vrls"], job["init_off"], job["pixel_undersampling"],
-                                               under, depth_correction=dcorr, seed=SEED_RNG, pass_=last_pass,
-                                               stage_refine=3 + 2 * s0, stage_sample=4 + 2 * s0)
     cl = it.clusters()
-    dev_reps = cl["reps"][cl["slice_off"][s0]:cl["slice_off"][s0 + 1]]
-    dev_w = cl["weights"][cl["slice_off"][s0]:cl["slice_off"][s0 + 1]]
-    identical = bool(refined and np.array_equal(reps, dev_reps)
-                     and np.array_equal(w.view(np.uint32), dev_w.view(np.uint32)))
+    t_ref, parity = {}, []
+    for s0 in dict.fromkeys((s_med, s_max)):
+        # the refinement sample is the device's own job for slice s0 (its R
+        # rows, locality weights, pixel undersampling and initial clusters)
+        job = it.slice_job(s0)
+        nrow = job["R"].shape[1]
+        args_ = (job["R"], np.arange(nrow, dtype=np.uint32), job["locw"], job["init_vrls"], job["init_off"],
+                 job["pixel_undersampling"], under)
+        kw = dict(depth_correction=dcorr, seed=SEED_RNG, pass_=last_pass, stage_refine=3 + 2 * s0,
+                  stage_sample=4 + 2 * s0)
+        os.environ["ALVRL_ORACLE_THREADS"] = "0"    # timed: sequential, one slice per thread as the reference
+        t0 = time.perf_counter()
+        reps, w, refined = o.cluster_refine(*args_, **kw)
+        t_ref[s0] = time.perf_counter() - t0
+        os.environ.pop("ALVRL_ORACLE_THREADS", None)
+        # the timed run is the reference-flags build (reassociating float
+        # maths); the bit-exact check runs the strict build of the same restatement
+        reps, w, refined = Oracle().cluster_refine(*args_, **kw)
+        dev_reps = cl["reps"][cl["slice_off"][s0]:cl["slice_off"][s0 + 1]]
+        dev_w = cl["weights"][cl["slice_off"][s0]:cl["slice_off"][s0 + 1]]
+        identical = bool(refined and np.array_equal(reps, dev_reps)
+                         and np.array_equal(w.view(np.uint32), dev_w.view(np.uint32)))
+        parity.append({"slice": s0, "rows": int(nrow), "clusters_oracle": int(len(reps)),
+                       "clusters_device": int(len(dev_reps)), "identical": identical,
+                       "refine_s": t_ref[s0]})
     r_rate = cnt / t_r
     render_rate = render_base["value"]
-    t_step = pre_pairs_step / r_rate + int(np.ceil(ns / threads)) * t_ref + render_pairs_step / render_rate
+    rounds = int(np.ceil(ns / threads))
+    t_refine = (rounds - 1) * t_ref[s_med] + t_ref[s_max]
+    t_step = pre_pairs_step / r_rate + t_refine + render_pairs_step / render_rate
     return {"value": (pre_pairs_step + render_pairs_step) / t_step, "unit": "VRL contributions/s",
             "cores": threads, "kind": "port",
-            "sample": (f"R rows of slice {s0} ({nrow} representatives x {vrls.shape[1]} VRLs, {t_r:.2f} s), "
-                       f"its adaptive refinement ({len(reps)} clusters, {t_ref:.2f} s, one thread), and "
-                       f"{render_base['sample']}; step extrapolated: {ns} slices over {threads} threads"),
-            "seconds": t_r + t_ref + render_base["seconds"], "step_seconds_estimate": t_step,
-            "cpu": render_base["cpu"], "flags": render_base["flags"],
-            "rates": {"rbuild": r_rate, "render": render_rate, "refine_s_per_slice": t_ref},
-            "refine_parity": {"slice": s0, "rows": nrow, "clusters_oracle": int(len(reps)),
-                              "clusters_device": int(len(dev_reps)), "identical": identical}}
+            "sample": (f"R rows of slice {s_med} ({nrows[s_med]} representatives x {vrls.shape[1]} VRLs, "
+                       f"{t_r:.2f} s on {threads} threads), the adaptive refinement of slices {s_med} "
+                       f"({t_ref[s_med]:.2f} s) and {s_max} (the largest, {nrows[s_max]} rows, "
+                       f"{t_ref[s_max]:.2f} s), one thread each, and {render_base['sample']}; step "
+                       f"extrapolated: {ns} slices over {threads} threads ({rounds} rounds)"),
+            "seconds": t_r + sum(t_ref.values()) + render_base["seconds"], "step_seconds_estimate": t_step,
+            "host_cpus": render_base["host_cpus"], "cpu": render_base["cpu"], "flags": render_base["flags"],
+            "rates": {"rbuild": r_rate, "render": render_rate, "refine_s_median_slice": t_ref[s_med],
+                      "refine_s_largest_slice": t_ref[s_max]},
+            "refine_parity": parity}
+
+
+def cpu_threads():
+    """The host cores this process may use: its CPU affinity, capped by a
+    cgroup CPU quota when one is set (a GPU box shares its host), or
+    ALVRL_CPU_THREADS."""
+    env = os.environ.get("ALVRL_CPU_THREADS")
+    if env:
+        return max(1, int(env))
+    n = _host_cpus()["affinity"]
+    q = _host_cpus()["cgroup_quota"]
+    return max(1, min(n, int(q)) if q else n)
+
+
+def _host_cpus():
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            a, b = f.read().split()[:2]
+            if a != "max":
+                quota = float(a) / float(b)
+    except (OSError, ValueError):
+        pass
+    return {"affinity": aff, "cgroup_quota": quota, "os_cpu_count": os.cpu_count()}
 
 
 def torch_index(pix):

@@ -120,19 +120,29 @@ ALVRL_API int alvrl_set_occluders(alvrl_ctx *ctx, const float *tris, uint32_t nt
  * registerResource(m_vrls) (:276-287, 353).  soa = 9 arrays of n floats:
  * start xyz, end xyz, power rgb (VRL.h:89-96).  particle_count = vrlVector::
  * getParticleCount() (VRL.h:164-166), the 1/particleCount normalisation.
- * soa_on_device != 0: soa is a device pointer. */
+ * soa_on_device != 0: soa is a device pointer.  Waits for every launch on the
+ * device first (the records are overwritten in place). */
 ALVRL_API int alvrl_upload_vrls(alvrl_ctx *ctx, const float *soa, uint32_t n,
                                 uint64_t particle_count, int soa_on_device);
 ALVRL_API uint32_t alvrl_num_vrls(const alvrl_ctx *ctx);
 
 /* Replaces m_ci->m_selectedVrls / m_clusterWeight / m_fallBackVrls /
  * m_fallBackWeight (vrlClusterInfo, :17-115; written by buildClusters at :341-346).
- * CSR on the host: slice s uses reps[slice_off[s] .. slice_off[s+1]). */
+ * CSR on the host: slice s uses reps[slice_off[s] .. slice_off[s+1]).  The
+ * device lists are overwritten in place: the call first waits for every
+ * launch on the device (hipDeviceSynchronize), so a gather still reading the
+ * previous lists on any stream -- the caller's included -- finishes first. */
 ALVRL_API int alvrl_set_clusters(alvrl_ctx *ctx, uint32_t nslices, const uint32_t *slice_off,
                                  const uint32_t *reps, const float *weights,
                                  const uint32_t *fb_reps, const float *fb_weights, uint32_t n_fb);
 
 /* ---- hot path (a): per-record VRL gather ------------------------------ */
+/* Threading (renderBlock runs on every LocalWorker at once, renderproc.cpp:
+ * 52-86): the gathers may be called concurrently from any number of host
+ * threads on one context.  Each calling thread gets its own HIP stream (the
+ * NULL-stream and host-pointer variants use it), its own grow-only device
+ * scratch for the host-pointer variants (no allocation per call) and its own
+ * timing events: alvrl_last_kernel_ms reports the calling thread's last launch. */
 /* Replaces getVRLContributions (:792-825) -> integrateVRL (:603-785) for every
  * VRL.  d_recs / d_rec_ids / d_out_rgb are device pointers; d_rec_ids may be
  * NULL (record id = index).  The record id keys the sampling uniforms.

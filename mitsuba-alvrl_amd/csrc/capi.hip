@@ -12,8 +12,11 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
+#include <unordered_map>
 #include <vector>
 
 namespace alvrl {
@@ -68,6 +71,52 @@ using namespace alvrl;
 static_assert(sizeof(alvrl_gather_rec) == sizeof(Rec), "record layout");
 static_assert(sizeof(alvrl_work_item) == sizeof(WorkItem), "work item layout");
 
+// Per calling thread of one context: the stream and grow-only device scratch
+// of the host-pointer gathers, and the HIP events that time the thread's last
+// launch.  Mitsuba calls renderBlock from every LocalWorker at once
+// (renderproc.cpp:52-86), each block a separate call: one stream per thread
+// keeps the calls concurrent, and nothing is allocated or freed per call.
+struct ThreadSlot {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    bool timed = false;
+    char* scratch = nullptr;
+    size_t cap = 0;
+    hipError_t init(int dev)
+    {
+        device = dev;
+        hipError_t e = hipStreamCreateWithFlags(&stream, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipEventCreate(&ev0);
+        if (e == hipSuccess) e = hipEventCreate(&ev1);
+        return e;
+    }
+    // scratch of at least n bytes; a grown buffer replaces the old one after
+    // this thread's earlier calls (the only users of it) have finished
+    hipError_t need(size_t n)
+    {
+        if (n <= cap) return hipSuccess;
+        hipError_t e = hipStreamSynchronize(stream);
+        if (e != hipSuccess) return e;
+        if (scratch) (void)hipFree(scratch);
+        scratch = nullptr;
+        cap = 0;
+        const size_t want = n + n / 2;
+        e = hipMalloc(&scratch, want);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    ~ThreadSlot()
+    {
+        (void)hipSetDevice(device);
+        if (stream) (void)hipStreamSynchronize(stream);
+        if (scratch) (void)hipFree(scratch);
+        if (ev0) (void)hipEventDestroy(ev0);
+        if (ev1) (void)hipEventDestroy(ev1);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+};
+
 struct alvrl_ctx {
     alvrl_config cfg;
     DevParams P;
@@ -87,8 +136,6 @@ struct alvrl_ctx {
     float* d_fb_w = nullptr;
     uint32_t cap_slices = 0, cap_rep = 0, cap_fb = 0;   // grow-only: a prepass re-sets them every pass
     bool clusters_set = false;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    bool timed = false;
     float refine_ms = 0.0f;
     unsigned long long refine_entries = 0;
     // occluder BVH (alvrl_set_occluders); P.occ views it
@@ -97,7 +144,32 @@ struct alvrl_ctx {
     uint32_t* d_bvh_ids = nullptr;
     RefineArenas refine_arenas;   // alvrl_refine's device scratch, reused across passes
     std::mutex mu;
+    std::mutex slots_mu;
+    std::unordered_map<std::thread::id, std::unique_ptr<ThreadSlot>> slots;
 };
+
+// the calling thread's slot (created on first use)
+static ThreadSlot* slot_of(alvrl_ctx* c, hipError_t* e)
+{
+    std::lock_guard<std::mutex> g(c->slots_mu);
+    auto& p = c->slots[std::this_thread::get_id()];
+    *e = hipSuccess;
+    if (!p) {
+        std::unique_ptr<ThreadSlot> t(new ThreadSlot());
+        *e = t->init(c->cfg.device);
+        if (*e != hipSuccess) return nullptr;
+        p = std::move(t);
+    }
+    return p.get();
+}
+
+#define SLOT(c, t)                                                                              \
+    ThreadSlot* t = nullptr;                                                                    \
+    do {                                                                                        \
+        hipError_t es_;                                                                         \
+        t = slot_of(c, &es_);                                                                   \
+        if (!t) return fail(ALVRL_ERR_HIP, std::string("per-thread stream: ") + hipGetErrorString(es_)); \
+    } while (0)
 
 static void free_occluders(alvrl_ctx* c)
 {
@@ -121,18 +193,22 @@ static int fail(int code, const std::string& msg)
             return fail(ALVRL_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
     } while (0)
 
-// NULL stream argument: the context's (non-blocking) stream, ordered after
-// the work already queued on the null stream -- a caller's zero fill or copy
-// of the buffers it passes, which the non-blocking stream would otherwise race
+// NULL stream argument: the calling thread's (non-blocking) stream of this
+// context, ordered after the work already queued on the null stream -- a
+// caller's zero fill or copy of the buffers it passes, which the non-blocking
+// stream would otherwise race
 static hipStream_t pick(alvrl_ctx* c, void* s)
 {
     if (s) return (hipStream_t)s;
+    hipError_t e;
+    ThreadSlot* t = slot_of(c, &e);
+    hipStream_t st = t ? t->stream : c->stream;
     hipEvent_t ev = nullptr;
     if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess) {
-        if (hipEventRecord(ev, nullptr) == hipSuccess) (void)hipStreamWaitEvent(c->stream, ev, 0);
+        if (hipEventRecord(ev, nullptr) == hipSuccess) (void)hipStreamWaitEvent(st, ev, 0);
         (void)hipEventDestroy(ev);
     }
-    return c->stream;
+    return st;
 }
 
 extern "C" {
@@ -169,8 +245,6 @@ ALVRL_API int alvrl_ctx_create(const alvrl_config* cfg, alvrl_ctx** out)
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipMalloc(&c->d_counter, 2 * sizeof(unsigned long long));
     if (e == hipSuccess) e = hipMemset(c->d_counter, 0, 2 * sizeof(unsigned long long));
-    if (e == hipSuccess) e = hipEventCreate(&c->ev0);
-    if (e == hipSuccess) e = hipEventCreate(&c->ev1);
     if (e != hipSuccess) {
         alvrl_ctx_destroy(c);
         return fail(ALVRL_ERR_HIP, std::string("alvrl_ctx_create: ") + hipGetErrorString(e));
@@ -198,8 +272,7 @@ ALVRL_API void alvrl_ctx_destroy(alvrl_ctx* c)
     free_clusters(c);
     free_occluders(c);
     c->refine_arenas.release();
-    if (c->ev0) hipEventDestroy(c->ev0);
-    if (c->ev1) hipEventDestroy(c->ev1);
+    c->slots.clear();
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
 }
@@ -231,7 +304,7 @@ ALVRL_API int alvrl_set_occluders(alvrl_ctx* c, const float* tris, uint32_t ntri
 {
     if (!c || (!tris && ntri)) return fail(ALVRL_ERR_INVALID, "alvrl_set_occluders: null argument");
     HIPCHK(hipSetDevice(c->cfg.device));
-    HIPCHK(hipStreamSynchronize(c->stream));   // no gather still reads the old BVH
+    HIPCHK(hipDeviceSynchronize());   // no gather on any stream still reads the old BVH
     free_occluders(c);
     if (ntri == 0) return ALVRL_OK;
     for (size_t i = 0; i < 9 * (size_t)ntri; i++)
@@ -261,8 +334,10 @@ ALVRL_API int alvrl_upload_vrls(alvrl_ctx* c, const float* soa, uint32_t n, uint
     if (!c || (!soa && n)) return fail(ALVRL_ERR_INVALID, "alvrl_upload_vrls: null argument");
     if (n > 0 && pc == 0) return fail(ALVRL_ERR_INVALID, "alvrl_upload_vrls: particle_count must be > 0");
     HIPCHK(hipSetDevice(c->cfg.device));
+    // the records are overwritten in place: no launch on any stream (the
+    // caller's included) may still read the previous pass's
+    HIPCHK(hipDeviceSynchronize());
     if (n > c->cap_vrl) {
-        HIPCHK(hipStreamSynchronize(c->stream));
         hipFree(c->d_soa); hipFree(c->d_vrl);
         c->d_soa = nullptr; c->d_vrl = nullptr; c->cap_vrl = 0;
         HIPCHK(hipMalloc(&c->d_soa, sizeof(float) * 9 * (size_t)n));
@@ -287,7 +362,10 @@ ALVRL_API int alvrl_set_clusters(alvrl_ctx* c, uint32_t nslices, const uint32_t*
 {
     if (!c || (!slice_off && nslices)) return fail(ALVRL_ERR_INVALID, "alvrl_set_clusters: null argument");
     HIPCHK(hipSetDevice(c->cfg.device));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    // the lists' device buffers are reused: every gather or false-colour
+    // launch still reading them -- on any stream, the caller's included --
+    // finishes first (the contract in alvrl.h)
+    HIPCHK(hipDeviceSynchronize());
     const uint32_t nrep = nslices ? slice_off[nslices] : 0;
     for (uint32_t i = 0; i < nrep; i++)
         if (reps[i] >= c->nvrl) return fail(ALVRL_ERR_INVALID, "alvrl_set_clusters: representative out of range");
@@ -348,11 +426,12 @@ ALVRL_API int alvrl_gather_brute(alvrl_ctx* c, const alvrl_gather_rec* d_recs, c
     hipStream_t s = pick(c, stream);
     // Float normalization = 1.0 / m_vrls->getParticleCount()  (:805)
     const float norm = (float)(1.0 / (double)c->particle_count);
-    HIPCHK(hipEventRecord(c->ev0, s));
+    SLOT(c, ts);
+    HIPCHK(hipEventRecord(ts->ev0, s));
     HIPCHK(launch_gather_brute(reinterpret_cast<const Rec*>(d_recs), d_ids, nrec, c->d_vrl, c->nvrl,
                                c->P, norm, d_out, c->d_counter + 1, s));
-    HIPCHK(hipEventRecord(c->ev1, s));
-    c->timed = true;
+    HIPCHK(hipEventRecord(ts->ev1, s));
+    ts->timed = true;
     return ALVRL_OK;
 }
 
@@ -367,13 +446,14 @@ ALVRL_API int alvrl_gather_clustered(alvrl_ctx* c, const alvrl_gather_rec* d_rec
     HIPCHK(hipSetDevice(c->cfg.device));
     hipStream_t s = pick(c, stream);
     const float inv_pc = 1.0f / (float)c->particle_count;   // Li /= getParticleCount() (:590)
-    HIPCHK(hipEventRecord(c->ev0, s));
+    SLOT(c, ts);
+    HIPCHK(hipEventRecord(ts->ev0, s));
     HIPCHK(launch_gather_clustered(reinterpret_cast<const Rec*>(d_recs), d_ids,
                                    reinterpret_cast<const WorkItem*>(d_items), nitems, c->d_vrl,
                                    c->d_slice_off, c->d_reps, c->d_weights, c->d_fb_reps, c->d_fb_w,
                                    c->n_fb, c->P, inv_pc, d_out, c->d_counter + 1, s));
-    HIPCHK(hipEventRecord(c->ev1, s));
-    c->timed = true;
+    HIPCHK(hipEventRecord(ts->ev1, s));
+    ts->timed = true;
     return ALVRL_OK;
 }
 
@@ -420,11 +500,12 @@ ALVRL_API int alvrl_build_R(alvrl_ctx* c, const alvrl_gather_rec* d_recs, const 
     HIPCHK(hipSetDevice(c->cfg.device));
     hipStream_t s = pick(c, stream);
     const float norm = (float)(1.0 / (double)c->particle_count);
-    HIPCHK(hipEventRecord(c->ev0, s));
+    SLOT(c, ts);
+    HIPCHK(hipEventRecord(ts->ev0, s));
     HIPCHK(launch_build_R(reinterpret_cast<const Rec*>(d_recs), d_ids, nrows, c->d_vrl, c->nvrl, c->P,
                           norm, reinterpret_cast<float2*>(d_Rt), ld, row0, c->d_counter + 0, s));
-    HIPCHK(hipEventRecord(c->ev1, s));
-    c->timed = true;
+    HIPCHK(hipEventRecord(ts->ev1, s));
+    ts->timed = true;
     return ALVRL_OK;
 }
 
@@ -448,12 +529,13 @@ ALVRL_API int alvrl_build_R_blocks(alvrl_ctx* c, const alvrl_gather_rec* d_recs,
     HIPCHK(hipSetDevice(c->cfg.device));
     hipStream_t s = pick(c, stream);
     const float norm = (float)(1.0 / (double)c->particle_count);
-    HIPCHK(hipEventRecord(c->ev0, s));
+    SLOT(c, ts);
+    HIPCHK(hipEventRecord(ts->ev0, s));
     HIPCHK(launch_build_R_blocks(reinterpret_cast<const Rec*>(d_recs), d_ids, nrows, c->d_vrl, c->nvrl, c->P,
                                  norm, reinterpret_cast<float2*>(d_Rt), d_row_off, d_row_stride, d_nonzero,
                                  c->d_counter + 0, s));
-    HIPCHK(hipEventRecord(c->ev1, s));
-    c->timed = true;
+    HIPCHK(hipEventRecord(ts->ev1, s));
+    ts->timed = true;
     return ALVRL_OK;
 }
 
@@ -554,12 +636,20 @@ ALVRL_API int alvrl_nonzero_columns(alvrl_ctx* c, const float* d_Rt, uint64_t ld
     if (nrows > ld) return fail(ALVRL_ERR_INVALID, "alvrl_nonzero_columns: nrows > ld");
     if (c->nvrl == 0) return ALVRL_OK;
     HIPCHK(hipSetDevice(c->cfg.device));
-    hipStream_t s = pick(c, stream);
-    uint8_t* d_mask = nullptr;
-    HIPCHK(hipMallocAsync((void**)&d_mask, c->nvrl, s));
+    SLOT(c, ts);
+    HIPCHK(ts->need(c->nvrl));   // the thread's scratch: free, its earlier calls synchronised
+    hipStream_t s = stream ? (hipStream_t)stream : ts->stream;
+    if (!stream) {   // after the caller's work on the null stream
+        hipEvent_t ev = nullptr;
+        HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        hipError_t ew = hipEventRecord(ev, nullptr);
+        if (ew == hipSuccess) ew = hipStreamWaitEvent(s, ev, 0);
+        (void)hipEventDestroy(ev);
+        HIPCHK(ew);
+    }
+    uint8_t* d_mask = reinterpret_cast<uint8_t*>(ts->scratch);
     hipError_t e = launch_nonzero_columns(reinterpret_cast<const float2*>(d_Rt), ld, nrows, c->nvrl, d_mask, s);
     if (e == hipSuccess) e = hipMemcpyAsync(out_mask, d_mask, c->nvrl, hipMemcpyDeviceToHost, s);
-    hipFreeAsync(d_mask, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) return fail(ALVRL_ERR_HIP, std::string("alvrl_nonzero_columns: ") + hipGetErrorString(e));
     return ALVRL_OK;
@@ -598,11 +688,20 @@ ALVRL_API int alvrl_reset_stats(alvrl_ctx* c)
 ALVRL_API int alvrl_last_kernel_ms(alvrl_ctx* c, float* ms)
 {
     if (!c || !ms) return fail(ALVRL_ERR_INVALID, "alvrl_last_kernel_ms: null argument");
-    if (!c->timed) return fail(ALVRL_ERR_STATE, "alvrl_last_kernel_ms: nothing launched yet");
     HIPCHK(hipSetDevice(c->cfg.device));
-    HIPCHK(hipEventSynchronize(c->ev1));
-    HIPCHK(hipEventElapsedTime(ms, c->ev0, c->ev1));
+    SLOT(c, ts);
+    if (!ts->timed) return fail(ALVRL_ERR_STATE, "alvrl_last_kernel_ms: nothing launched yet on this thread");
+    HIPCHK(hipEventSynchronize(ts->ev1));
+    HIPCHK(hipEventElapsedTime(ms, ts->ev0, ts->ev1));
     return ALVRL_OK;
+}
+
+// carve the slot's scratch into 256-byte aligned pieces
+static size_t carve(size_t* at, size_t bytes)
+{
+    const size_t o = *at;
+    *at += (bytes + 255) & ~(size_t)255;
+    return o;
 }
 
 ALVRL_API int alvrl_gather_brute_host(alvrl_ctx* c, const alvrl_gather_rec* recs, const uint32_t* ids,
@@ -611,30 +710,33 @@ ALVRL_API int alvrl_gather_brute_host(alvrl_ctx* c, const alvrl_gather_rec* recs
     int rc = check_ready(c, "alvrl_gather_brute_host");
     if (rc) return rc;
     if (nrec == 0) return ALVRL_OK;
+    if (!recs || !out) return fail(ALVRL_ERR_INVALID, "alvrl_gather_brute_host: null buffer");
     HIPCHK(hipSetDevice(c->cfg.device));
-    hipStream_t s;
-    HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-    alvrl_gather_rec* dr = nullptr; uint32_t* di = nullptr; float* dout = nullptr;
-    hipError_t e = hipMallocAsync((void**)&dr, sizeof(alvrl_gather_rec) * nrec, s);
-    if (e == hipSuccess && ids) e = hipMallocAsync((void**)&di, sizeof(uint32_t) * nrec, s);
-    if (e == hipSuccess) e = hipMallocAsync((void**)&dout, sizeof(float) * 3 * nrec, s);
-    if (e == hipSuccess) e = hipMemcpyAsync(dr, recs, sizeof(alvrl_gather_rec) * nrec, hipMemcpyHostToDevice, s);
+    SLOT(c, ts);
+    size_t at = 0;
+    const size_t o_r = carve(&at, sizeof(alvrl_gather_rec) * nrec);
+    const size_t o_i = carve(&at, ids ? sizeof(uint32_t) * nrec : 0);
+    const size_t o_o = carve(&at, sizeof(float) * 3 * nrec);
+    HIPCHK(ts->need(at));
+    hipStream_t s = ts->stream;
+    auto* dr = reinterpret_cast<alvrl_gather_rec*>(ts->scratch + o_r);
+    uint32_t* di = ids ? reinterpret_cast<uint32_t*>(ts->scratch + o_i) : nullptr;
+    float* dout = reinterpret_cast<float*>(ts->scratch + o_o);
+    hipError_t e = hipMemcpyAsync(dr, recs, sizeof(alvrl_gather_rec) * nrec, hipMemcpyHostToDevice, s);
     if (e == hipSuccess && ids) e = hipMemcpyAsync(di, ids, sizeof(uint32_t) * nrec, hipMemcpyHostToDevice, s);
-    int r2 = ALVRL_OK;
+    if (e == hipSuccess) e = hipEventRecord(ts->ev0, s);
     if (e == hipSuccess) {
         const float norm = (float)(1.0 / (double)c->particle_count);
         e = launch_gather_brute(reinterpret_cast<const Rec*>(dr), di, nrec, c->d_vrl, c->nvrl, c->P,
                                 norm, dout, c->d_counter + 1, s);
     }
+    if (e == hipSuccess) e = hipEventRecord(ts->ev1, s);
+    if (e == hipSuccess) ts->timed = true;
     if (e == hipSuccess) e = hipMemcpyAsync(out, dout, sizeof(float) * 3 * nrec, hipMemcpyDeviceToHost, s);
-    if (dr) hipFreeAsync(dr, s);
-    if (di) hipFreeAsync(di, s);
-    if (dout) hipFreeAsync(dout, s);
     hipError_t e2 = hipStreamSynchronize(s);
-    hipStreamDestroy(s);
     if (e == hipSuccess) e = e2;
-    if (e != hipSuccess) r2 = fail(ALVRL_ERR_HIP, std::string("alvrl_gather_brute_host: ") + hipGetErrorString(e));
-    return r2;
+    if (e != hipSuccess) return fail(ALVRL_ERR_HIP, std::string("alvrl_gather_brute_host: ") + hipGetErrorString(e));
+    return ALVRL_OK;
 }
 
 ALVRL_API int alvrl_gather_clustered_host(alvrl_ctx* c, const alvrl_gather_rec* recs,
@@ -645,6 +747,7 @@ ALVRL_API int alvrl_gather_clustered_host(alvrl_ctx* c, const alvrl_gather_rec* 
     if (rc) return rc;
     if (!c->clusters_set) return fail(ALVRL_ERR_STATE, "alvrl_gather_clustered_host: alvrl_set_clusters not called");
     if (nrec == 0) return ALVRL_OK;
+    if (!recs || !out || !slice_of_rec) return fail(ALVRL_ERR_INVALID, "alvrl_gather_clustered_host: null buffer");
     for (uint32_t i = 0; i < nrec; i++)
         if (slice_of_rec[i] != 0xFFFFFFFFu && slice_of_rec[i] >= c->nslices)
             return fail(ALVRL_ERR_INVALID, "alvrl_gather_clustered_host: slice out of range");
@@ -662,20 +765,25 @@ ALVRL_API int alvrl_gather_clustered_host(alvrl_ctx* c, const alvrl_gather_rec* 
         sl2[i] = slice_of_rec[perm[i]];
     }
     std::vector<alvrl_work_item> items(nrec);
-    uint32_t nit = alvrl_make_work_items(sl2.data(), nrec, items.data(), nrec);
+    const uint32_t nit = alvrl_make_work_items(sl2.data(), nrec, items.data(), nrec);
     HIPCHK(hipSetDevice(c->cfg.device));
-    hipStream_t s;
-    HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-    alvrl_gather_rec* dr = nullptr; uint32_t* di = nullptr; float* dout = nullptr;
-    alvrl_work_item* dit = nullptr;
-    hipError_t e = hipMallocAsync((void**)&dr, sizeof(alvrl_gather_rec) * nrec, s);
-    if (e == hipSuccess) e = hipMallocAsync((void**)&di, sizeof(uint32_t) * nrec, s);
-    if (e == hipSuccess) e = hipMallocAsync((void**)&dout, sizeof(float) * 3 * nrec, s);
-    if (e == hipSuccess) e = hipMallocAsync((void**)&dit, sizeof(alvrl_work_item) * nit, s);
-    if (e == hipSuccess) e = hipMemcpyAsync(dr, r2.data(), sizeof(alvrl_gather_rec) * nrec, hipMemcpyHostToDevice, s);
+    SLOT(c, ts);
+    size_t at = 0;
+    const size_t o_r = carve(&at, sizeof(alvrl_gather_rec) * nrec);
+    const size_t o_i = carve(&at, sizeof(uint32_t) * nrec);
+    const size_t o_o = carve(&at, sizeof(float) * 3 * nrec);
+    const size_t o_t = carve(&at, sizeof(alvrl_work_item) * nit);
+    HIPCHK(ts->need(at));
+    hipStream_t s = ts->stream;
+    auto* dr = reinterpret_cast<alvrl_gather_rec*>(ts->scratch + o_r);
+    auto* di = reinterpret_cast<uint32_t*>(ts->scratch + o_i);
+    auto* dout = reinterpret_cast<float*>(ts->scratch + o_o);
+    auto* dit = reinterpret_cast<alvrl_work_item*>(ts->scratch + o_t);
+    hipError_t e = hipMemcpyAsync(dr, r2.data(), sizeof(alvrl_gather_rec) * nrec, hipMemcpyHostToDevice, s);
     if (e == hipSuccess) e = hipMemcpyAsync(di, id2.data(), sizeof(uint32_t) * nrec, hipMemcpyHostToDevice, s);
     if (e == hipSuccess) e = hipMemcpyAsync(dit, items.data(), sizeof(alvrl_work_item) * nit, hipMemcpyHostToDevice, s);
     std::vector<float> o2(3 * (size_t)nrec);
+    if (e == hipSuccess) e = hipEventRecord(ts->ev0, s);
     if (e == hipSuccess) {
         const float inv_pc = 1.0f / (float)c->particle_count;
         e = launch_gather_clustered(reinterpret_cast<const Rec*>(dr), di,
@@ -683,13 +791,10 @@ ALVRL_API int alvrl_gather_clustered_host(alvrl_ctx* c, const alvrl_gather_rec* 
                                     c->d_slice_off, c->d_reps, c->d_weights, c->d_fb_reps, c->d_fb_w,
                                     c->n_fb, c->P, inv_pc, dout, c->d_counter + 1, s);
     }
+    if (e == hipSuccess) e = hipEventRecord(ts->ev1, s);
+    if (e == hipSuccess) ts->timed = true;
     if (e == hipSuccess) e = hipMemcpyAsync(o2.data(), dout, sizeof(float) * 3 * nrec, hipMemcpyDeviceToHost, s);
-    if (dr) hipFreeAsync(dr, s);
-    if (di) hipFreeAsync(di, s);
-    if (dout) hipFreeAsync(dout, s);
-    if (dit) hipFreeAsync(dit, s);
     hipError_t e2 = hipStreamSynchronize(s);
-    hipStreamDestroy(s);
     if (e == hipSuccess) e = e2;
     if (e != hipSuccess) return fail(ALVRL_ERR_HIP, std::string("alvrl_gather_clustered_host: ") + hipGetErrorString(e));
     for (uint32_t i = 0; i < nrec; i++)
