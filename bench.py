@@ -78,6 +78,8 @@ def parse():
                     help="CPU baseline sample: every n-th image row")
     ap.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "r02_pmc_traffic.json"),
                     help="per-launch HBM bytes of the dominant kernel from a rocprofv3 --pmc pass")
+    ap.add_argument("--valu-json", default=os.path.join(REPO, "profiles", "r03", "pmc_valu_{cfg}.json"),
+                    help="per-kernel VALU counters (tools/pmc_valu.sh + tools/pmc_valu.py)")
     return ap.parse_args()
 
 
@@ -193,6 +195,13 @@ def main():
     except (OSError, ValueError):
         pass
 
+    valu = {}
+    try:
+        with open(args.valu_json.format(cfg=args.config)) as f:
+            valu = json.load(f)
+    except (OSError, ValueError):
+        pass
+
     def roof(name, key, bytes_per_launch, ms, note):
         # achieved / frac: ALGORITHMIC bytes per launch (the contract's
         # definition); traffic: measured HBM bytes per launch
@@ -202,10 +211,19 @@ def main():
         ach = bytes_per_launch / s_ / 1e9 if s_ > 0 else 0.0
         tr = pmc.get(key)
         hbm = tr / s_ / 1e9 if (tr is not None and s_ > 0) else None
-        return {"bound": "hbm", "kernel": name, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": ach / HBM_PEAK_GBS, "traffic": tr, "bytes_per_launch": bytes_per_launch,
-                "hbm_achieved": hbm, "hbm_frac": hbm / HBM_PEAK_GBS if hbm is not None else None,
-                "launch_ms": ms, "note": note}
+        out = {"bound": "hbm", "kernel": name, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+               "frac": ach / HBM_PEAK_GBS, "traffic": tr, "bytes_per_launch": bytes_per_launch,
+               "hbm_achieved": hbm, "hbm_frac": hbm / HBM_PEAK_GBS if hbm is not None else None,
+               "launch_ms": ms, "note": note}
+        v = valu.get(key)
+        if v:
+            # VALU issue roofline (rocprofv3 pass of the same config, tools/pmc_valu.py):
+            # fraction of one wave-instruction per SIMD per 2 cycles, VALU
+            # instructions per VRL pair and the pair rate that issue peak allows
+            out["valu"] = {k: v.get(k) for k in ("valu_issue_frac", "insts_per_pair", "pair_rate",
+                                                 "pair_rate_at_valu_peak", "clock_ghz", "ms")}
+            out["valu"]["source"] = os.path.relpath(args.valu_json.format(cfg=args.config), REPO)
+        return out
 
     pairs_per_launch_rank = (s1["contrib_render"] - s0["contrib_render"]) / nst
     rooflines = {"render": roof(f"k_gather_{kind}", "render", BYTES_PER_PAIR[kind] * pairs_per_launch_rank,

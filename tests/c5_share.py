@@ -99,7 +99,7 @@ def run_share(props: str = "", nvrl: int = C5_VRLS, width: int = C5_W, height: i
                 refine_entries=st["refine_entries"], contrib_preprocess=st["contrib_preprocess"],
                 slices_failed=st["slices_failed"], s_preprocess=t1 - t0, s_prepass=t2 - t1,
                 exchange_calls=[c[0] for c in ex.calls])
-    log(f"C5 rank-0 share: {info['slices_local']} of {ns} slices, rows {rows.min()}..{rows.max()} "
+    log(f"{width}^2 x {nvrl} VRLs, rank 0 of {world}: {info['slices_local']} of {ns} slices, rows {rows.min()}..{rows.max()} "
         f"(sum {rows.sum()}), R {info['R_bytes'] / 1e9:.1f} GB, R build {info['ms_rbuild']:.0f} ms, "
         f"refine {info['ms_refine_kernel']:.0f} ms ({info['refine_entries'] / 1e9:.1f}e9 entries), "
         f"preprocess {info['s_preprocess']:.1f} s, prepass {info['s_prepass']:.1f} s")

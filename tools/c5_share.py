@@ -4,6 +4,7 @@ bit for bit with the device's lists (a heartbeat line every 20 s while the
 oracle runs, so a long check is not taken for a hang).
 
   python tools/c5_share.py [--oracle] [--json out.json] [--props "..."]
+  python tools/c5_share.py --res 1024 --vrls 100000 --world 8   # C4's rank-0 share at N = 8
 """
 import argparse
 import json
@@ -28,8 +29,15 @@ def main():
     ap.add_argument("--props", default="")
     ap.add_argument("--json", default="")
     ap.add_argument("--vrls", type=int, default=c5_share.C5_VRLS)
+    ap.add_argument("--res", type=int, default=c5_share.C5_W, help="image width = height")
+    ap.add_argument("--world", type=int, default=c5_share.C5_WORLD)
+    ap.add_argument("--passes", type=int, default=1, help="prepasses run (timings of the last)")
     a = ap.parse_args()
-    it, info, mine = c5_share.run_share(a.props, nvrl=a.vrls, log=lambda s: print(s, flush=True))
+    for p in range(a.passes):
+        it, info, mine = c5_share.run_share(a.props, nvrl=a.vrls, width=a.res, height=a.res, world=a.world,
+                                            pass_=p, log=lambda s: print(s, flush=True))
+        if p + 1 < a.passes:
+            it.close()
     cl = it.clusters()
     ncl = np.diff(cl["slice_off"])
     info["clusters_local"] = [int(ncl[s]) for s in mine]
