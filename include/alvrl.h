@@ -30,7 +30,7 @@ extern "C" {
 #define ALVRL_API
 #endif
 
-#define ALVRL_ABI_VERSION 1
+#define ALVRL_ABI_VERSION 2
 
 enum {
     ALVRL_OK = 0,
@@ -46,6 +46,9 @@ enum {
 #define ALVRL_REC_HIT     1u   /* rRec.its.isValid()                          (vrlIntegrator.cpp:712) */
 #define ALVRL_REC_SMOOTH  2u   /* bsdf->getType() & BSDF::ESmooth             (vrlIntegrator.cpp:726-727) */
 #define ALVRL_REC_MEDIUM  4u   /* rRec.medium && !getSigmaS().isZero()         (vrlIntegrator.cpp:614, 795) */
+#define ALVRL_REC_DELTA   8u   /* its BSDF has a delta component: the eye path continues (:449-511) */
+#define ALVRL_REC_ACCUM  16u   /* R build: add to the row's entries (a deeper segment of the row's
+                                  eye path; vrlContributions accumulate over the recursion, :812-813) */
 
 /* Integrator properties that shape the device maths.
  * Replaces the Properties parsing in vrlIntegrator(const Properties&), vrlIntegrator.cpp:128-208. */
@@ -68,10 +71,13 @@ typedef struct {
     float phase_g;
 } alvrl_medium_desc;
 
-/* One eye segment ("gather record"), 64 B.  What LiInternal knows at the point
+/* One eye segment ("gather record"), 80 B.  What LiInternal knows at the point
  * it calls getVRLContributions / getClusteredVrlContributions
  * (vrlIntegrator.cpp:418-443): ray.o, ray.d, rRec.its.{p, shFrame.n}, the
- * diffuse reflectance of its BSDF and the medium/hit flags. */
+ * diffuse reflectance of its BSDF and the medium/hit flags, and -- for the
+ * segments of a specular chain (LiInternal's recursion through delta BSDFs,
+ * :445-511) -- the path weight the recursion passes down and the segment's
+ * depth along the eye path. */
 typedef struct {
     float o[3];        /* E  = ray.o */
     float d[3];        /* ray.d */
@@ -79,6 +85,11 @@ typedef struct {
     float n[3];        /* rRec.its.shFrame.n */
     float albedo[3];   /* SmoothDiffuse reflectance (diffuse.cpp:110-118) */
     uint32_t flags;    /* ALVRL_REC_* */
+    float weight[3];   /* LiInternal's 'weight' (:503-510): the gathered radiance and the
+                          R entries' luminance samples are multiplied by it; (1, 1, 1) for a
+                          camera ray */
+    uint32_t depth;    /* eye-path vertex the segment starts at (0: the camera ray); keys the
+                          segment's own sample streams (< 256) */
 } alvrl_gather_rec;
 
 /* A wave-sized run of slice-bucketed records for the clustered gather:

@@ -21,7 +21,7 @@ PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REPO = os.path.dirname(PKG_DIR)
 LIB_PATH = os.environ.get("ALVRL_LIB") or os.path.join(PKG_DIR, "libalvrl.so")   # ALVRL_LIB: developer variant builds
 
-REC_WORDS = 16
+REC_WORDS = 20
 REC_HIT, REC_SMOOTH, REC_MEDIUM = 1, 2, 4
 UINT32_MAX = 0xFFFFFFFF
 

@@ -512,7 +512,7 @@ ALVRL_API int alvrl_build_R(alvrl_ctx* c, const alvrl_gather_rec* d_recs, const 
 ALVRL_API int alvrl_set_rsamples(alvrl_ctx* c, int rsamples)
 {
     if (!c) return fail(ALVRL_ERR_INVALID, "alvrl_set_rsamples: null ctx");
-    if (rsamples < 1 || rsamples > 0xFFFFFF) return fail(ALVRL_ERR_INVALID, "Rsamples must be in [1, 2^24)");
+    if (rsamples < 1 || rsamples > 0xFFFF) return fail(ALVRL_ERR_INVALID, "Rsamples must be in [1, 2^16)");
     std::lock_guard<std::mutex> g(c->mu);
     c->P.rsamples = rsamples;
     return ALVRL_OK;

@@ -38,15 +38,17 @@ __device__ __forceinline__ Rec load_rec(const Rec* __restrict__ recs, uint32_t r
     Rec x;
     if (active) {
         const float4* p = reinterpret_cast<const float4*>(recs + r);
-        const float4 a = p[0], b = p[1], c = p[2], d = p[3];
+        const float4 a = p[0], b = p[1], c = p[2], d = p[3], e = p[4];
         x.ox = a.x; x.oy = a.y; x.oz = a.z; x.dx = a.w;
         x.dy = b.x; x.dz = b.y; x.px = b.z; x.py = b.w;
         x.pz = c.x; x.nx = c.y; x.ny = c.z; x.nz = c.w;
         x.ar = d.x; x.ag = d.y; x.ab = d.z; x.flags = __float_as_uint(d.w);
+        x.wr = e.x; x.wg = e.y; x.wb = e.z; x.depth = __float_as_uint(e.w);
     } else {
         x.ox = x.oy = x.oz = 0.0f; x.dx = 0.0f; x.dy = 0.0f; x.dz = 1.0f;
         x.px = x.py = 0.0f; x.pz = 1.0f; x.nx = x.ny = 0.0f; x.nz = -1.0f;
         x.ar = x.ag = x.ab = 0.0f; x.flags = 0u;
+        x.wr = x.wg = x.wb = 1.0f; x.depth = 0u;
     }
     return x;
 }
@@ -81,6 +83,8 @@ __global__ void __launch_bounds__(256) k_gather_brute(const Rec* __restrict__ re
             // vrlContribution *= normalization; Li += vrlContribution (:810, 815)
             L0 += c[0] * normalization; L1 += c[1] * normalization; L2 += c[2] * normalization;
         }
+        // the segment's path weight (integrateVRL's 'weight', :668 / :743)
+        if (!q.unit) { L0 *= q.w[0]; L1 *= q.w[1]; L2 *= q.w[2]; }
     }
     count_pairs(counter, active && q.medium, nvrl);
     if (active) {
@@ -141,8 +145,9 @@ __device__ __forceinline__ void gather_item(const Rec* __restrict__ recs, const 
             // Li += weights->at(i) * integrateVRL(...)  (:587-589)
             L0 += c[0] * w; L1 += c[1] * w; L2 += c[2] * w;
         }
-        // Li /= particleCount (:590)
+        // Li /= particleCount (:590); return Li * weight (:598)
         L0 *= inv_pc; L1 *= inv_pc; L2 *= inv_pc;
+        if (!q.unit) { L0 *= q.w[0]; L1 *= q.w[1]; L2 *= q.w[2]; }
     }
     count_pairs(counter, active && q.medium, k);
     if (active) {
@@ -244,7 +249,11 @@ __global__ void __launch_bounds__(256) k_build_R(const Rec* __restrict__ recs,
                 }
             }
         }
-        if (active) Rt[(size_t)v * ld + row0 + r] = make_float2(mean, var);
+        if (active) {
+            float2* e = &Rt[(size_t)v * ld + row0 + r];
+            if (rec.flags & kRecAccum) { const float2 o = *e; *e = make_float2(o.x + mean, o.y + var); }
+            else *e = make_float2(mean, var);
+        }
         ++done;
     }
     count_pairs(counter, active && q.medium, done * (uint32_t)nsamp);
@@ -298,7 +307,11 @@ __global__ void __launch_bounds__(256) k_build_R_blocks(const Rec* __restrict__ 
                 }
             }
         }
-        if (active) Rt[base + (uint64_t)v * stride] = make_float2(mean, var);
+        if (active) {
+            float2* e = &Rt[base + (uint64_t)v * stride];
+            if (rec.flags & kRecAccum) { const float2 o = *e; *e = make_float2(o.x + mean, o.y + var); }
+            else *e = make_float2(mean, var);
+        }
         if (nonzero && __ballot(active && mean != 0.0f) && (threadIdx.x & 63) == 0) nonzero[v] = 1;
         ++done;
     }

@@ -148,9 +148,9 @@ std::vector<uint32_t> Preprocessor::build_slices(const SmokeBox& s, const float*
     const float nan = std::numeric_limits<float>::quiet_NaN();
     for (int i = 0; i < W; i++) {          // pixel order: x outer, y inner (:1140-1141)
         for (int j = 0; j < H; j++) {
-            float own[16];
+            float own[kRecWords];
             const float* rec = own;
-            if (recs) rec = recs + 16 * ((size_t)j * W + i);
+            if (recs) rec = recs + kRecWords * ((size_t)j * W + i);
             else s.make_record(i, j, true, own);
             uint32_t flags;
             std::memcpy(&flags, &rec[15], 4);

@@ -144,7 +144,7 @@ bool SmokeBox::visible(V3 p1, bool p1_surface, V3 p2, bool p2_surface) const
     return true;
 }
 
-void SmokeBox::make_record(int x, int y, bool medium_scatters, float rec[16]) const
+void SmokeBox::make_record(int x, int y, bool medium_scatters, float rec[kRecWords]) const
 {
     V3 O, D, n, p;
     float mint;
@@ -161,6 +161,9 @@ void SmokeBox::make_record(int x, int y, bool medium_scatters, float rec[16]) co
     rec[9] = n.x; rec[10] = n.y; rec[11] = n.z;
     rec[12] = a[0]; rec[13] = a[1]; rec[14] = a[2];
     std::memcpy(&rec[15], &flags, 4);
+    rec[16] = rec[17] = rec[18] = 1.0f;   // the camera ray: path weight 1, depth 0
+    const uint32_t depth = 0;
+    std::memcpy(&rec[19], &depth, 4);
 }
 
 float SmokeBox::scene_diagonal() const

@@ -24,6 +24,10 @@ namespace host {
 
 struct V3 { float x, y, z; };
 
+// words of a gather record (alvrl_gather_rec): o, d, p, n, albedo, flags,
+// path weight (3), eye-path depth
+constexpr int kRecWords = 20;
+
 inline V3 v3(float x, float y, float z) { return V3{x, y, z}; }
 inline V3 operator+(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
 inline V3 operator-(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
@@ -74,7 +78,7 @@ struct SmokeBox {
     bool visible(V3 p1, bool p1_surface, V3 p2, bool p2_surface) const;
     uint32_t n_occ() const { return (uint32_t)(occ.size() / 9); }
     // Gather record (alvrl_gather_rec layout) of pixel centre (x, y).
-    void make_record(int x, int y, bool medium_scatters, float rec[16]) const;
+    void make_record(int x, int y, bool medium_scatters, float rec[kRecWords]) const;
     float scene_diagonal() const;   // distance(getAABB().min, getAABB().max)
 };
 

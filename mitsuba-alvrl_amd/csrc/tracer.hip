@@ -398,11 +398,13 @@ __global__ void __launch_bounds__(256) k_eye_records(TCam c, TScene sc, const ui
     if (isfinite(t)) flags |= 1u | 2u;
     if (c.scat) flags |= 4u;
     const float* a = occ ? sc.occ_albedo : sc.albedo;
-    float* r = out + 16 * (size_t)i;
+    float* r = out + 20 * (size_t)i;   // alvrl_gather_rec: 20 words
     const float v[15] = {O.x, O.y, O.z, D.x, D.y, D.z, p.x, p.y, p.z, nn.x, nn.y, nn.z, a[0], a[1], a[2]};
 #pragma unroll
     for (int k = 0; k < 15; k++) r[k] = v[k];
     r[15] = __uint_as_float(flags);
+    r[16] = 1.0f; r[17] = 1.0f; r[18] = 1.0f;   // a camera ray: path weight 1, depth 0
+    r[19] = __uint_as_float(0u);
 }
 
 // ----------------------------------------------------- volpath reference --

@@ -166,8 +166,11 @@ __device__ __forceinline__ float atan_fast(float x)
 struct Rec {
     float ox, oy, oz, dx, dy, dz, px, py, pz, nx, ny, nz, ar, ag, ab;
     uint32_t flags;
+    float wr, wg, wb;   // path weight of the segment (LiInternal's 'weight', vrlIntegrator.cpp:503-510)
+    uint32_t depth;     // eye-path vertex of the segment's start (0: camera ray): keys its streams
 };
-static_assert(sizeof(Rec) == 64, "Rec layout");
+static_assert(sizeof(Rec) == 80, "Rec layout");
+constexpr uint32_t kRecAccum = 16u;   // ALVRL_REC_ACCUM: the R build adds to the row's entries
 
 struct RecPre {
     F3 E, d, dN, P, n, B, dirAB;
@@ -176,7 +179,9 @@ struct RecPre {
     float cos_wi;     // Frame::cosTheta(its.wi)
     float teus[3];    // transmittanceEUsurf (vrlIntegrator.cpp:711-719)
     float alb[3];
-    bool medium, surf;
+    float w[3];       // the segment's path weight
+    uint32_t depth;
+    bool medium, surf, unit;   // unit: weight (1, 1, 1)
 };
 
 __device__ __forceinline__ void medium_tr(const DevParams& P, float d, float tr[3], float* pf)
@@ -219,6 +224,9 @@ __device__ __forceinline__ RecPre prepare_record(const Rec& r, const DevParams& 
     q.a = dot(u, u);
     q.cos_wi = dot(neg(q.d), q.n);
     q.alb[0] = r.ar; q.alb[1] = r.ag; q.alb[2] = r.ab;
+    q.w[0] = r.wr; q.w[1] = r.wg; q.w[2] = r.wb;
+    q.unit = r.wr == 1.0f && r.wg == 1.0f && r.wb == 1.0f;
+    q.depth = r.depth;
     q.medium = (r.flags & 4u) != 0;
     q.teus[0] = q.teus[1] = q.teus[2] = 0.0f;
     if ((r.flags & 1u) && len(q.P - q.E) != 0) medium_tr_only(P, len(q.P - q.E), q.teus);
@@ -391,7 +399,8 @@ __device__ __forceinline__ void integrate_vrl(const DevParams& P, const RecPre& 
     float tot0 = 0.0f, tot1 = 0.0f, tot2 = 0.0f;
     float mean = 0.0f, M2 = 0.0f, mean_acc = 0.0f, var_acc = 0.0f;
     const uint32_t k0 = P.seed, k1 = P.pass;
-    const uint32_t c3 = (domain << 24) | (rsub & 0xFFFFFFu);   // rsub: R sample index
+    // stream word: domain, the segment's eye-path depth, the R sample index
+    const uint32_t c3 = (domain << 24) | ((q.depth & 0xFFu) << 16) | (rsub & 0xFFFFu);
 
     // draws 0..3: volVol samples 0,1 (V, U); draws 4..7: volSurf / further volVol
     U4 rb = philox4x32_10(rec_id, vrl_id, 0u, c3, k0, k1);
@@ -457,6 +466,7 @@ __device__ __forceinline__ void integrate_vrl(const DevParams& P, const RecPre& 
                 c1 *= tsv[1] * tuv[1] * teu[1];
                 c2 *= tsv[2] * tuv[2] * teu[2];
                 c0 *= gg; c1 *= gg; c2 *= gg;
+                if (WANT_STATS && !q.unit) { c0 *= q.w[0]; c1 *= q.w[1]; c2 *= q.w[2]; }
                 if (spec_valid(c0, c1, c2)) {
                     const float rn = 1.0f / (float)nVV;
                     tot0 += c0 * rn; tot1 += c1 * rn; tot2 += c2 * rn;
@@ -517,6 +527,7 @@ __device__ __forceinline__ void integrate_vrl(const DevParams& P, const RecPre& 
                     c1 *= tsv[1] * tuv[1];
                     c2 *= tsv[2] * tuv[2];
                     c0 *= gg; c1 *= gg; c2 *= gg;
+                    if (WANT_STATS && !q.unit) { c0 *= q.w[0]; c1 *= q.w[1]; c2 *= q.w[2]; }
                     if (spec_valid(c0, c1, c2)) {
                         const float rn = 1.0f / (float)nVS;
                         tot0 += c0 * rn; tot1 += c1 * rn; tot2 += c2 * rn;

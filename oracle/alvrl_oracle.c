@@ -365,15 +365,23 @@ void alvrl_o_medium_eval(const alvrl_o_medium *m, float distance, float tr[3], f
 /* ===================================================================== */
 /*  integrateVRL, vrlIntegrator.cpp:603-785                                */
 /* ===================================================================== */
-/* 'rsub' is the low 24 bits of the stream word: the sample index of an R
- * entry with Rsamples > 1 (LiInternal's samples loop, vrlIntegrator.cpp:427-443). */
-static void integrate_vrl_s(const alvrl_o_params *P, const float *rec, uint32_t rec_id,
+/* 'rsub' is the low 16 bits of the stream word: the sample index of an R
+ * entry with Rsamples > 1 (LiInternal's samples loop, vrlIntegrator.cpp:427-443);
+ * bits 16-23 carry the record's eye-path depth.  use_weight: integrateVRL's
+ * 'weight' argument (:605) is the record's path weight, the first factor of
+ * every sample's contribution (:668, :743), as getVRLContributions passes it
+ * (:808); getClusteredVrlContributions calls with the default 1 and
+ * multiplies its sum instead (:598). */
+static void integrate_vrl_w(const alvrl_o_params *P, const float *rec, uint32_t rec_id,
                             const float *vs, uint32_t nvrl, uint32_t vrl_id, uint32_t domain,
-                            uint32_t rsub, float out_rgb[3], float *contrib, float *variance)
+                            uint32_t rsub, int use_weight, float out_rgb[3], float *contrib, float *variance)
 {
     const alvrl_o_medium *m = &P->medium;
-    uint32_t flags;
+    uint32_t flags, depth;
     memcpy(&flags, &rec[15], 4);
+    memcpy(&depth, &rec[19], 4);
+    rsub = ((depth & 0xFFu) << 16) | (rsub & 0xFFFFu);
+    const float wt[3] = { use_weight ? rec[16] : 1.0f, use_weight ? rec[17] : 1.0f, use_weight ? rec[18] : 1.0f };
     if (contrib) *contrib = 0;
     if (variance) *variance = 0;
     out_rgb[0] = out_rgb[1] = out_rgb[2] = 0.0f;
@@ -416,7 +424,7 @@ static void integrate_vrl_s(const alvrl_o_params *P, const float *rec, uint32_t 
             float phV = phase_eval(m, neg(SV), VU);
             float rpf = 1.0f / pf_sv;
             for (int i = 0; i < 3; i++) {
-                c[i] = 1.0f;
+                c[i] = wt[i];
                 c[i] *= power[i];
                 c[i] *= (m->sigma_s[i] * m->sigma_s[i]) * rpdf;
                 c[i] *= rd2;
@@ -478,7 +486,7 @@ static void integrate_vrl_s(const alvrl_o_params *P, const float *rec, uint32_t 
                 float rpf = 1.0f / pf_sv;
                 float c[3];
                 for (int i = 0; i < 3; i++) {
-                    c[i] = 1.0f;
+                    c[i] = wt[i];
                     c[i] *= power[i];
                     c[i] *= m->sigma_s[i] * rpdf;
                     c[i] *= rd2;
@@ -513,7 +521,7 @@ void alvrl_o_integrate_vrl(const alvrl_o_params *P, const float *rec, uint32_t r
                            const float *vs, uint32_t nvrl, uint32_t vrl_id,
                            uint32_t domain, float out_rgb[3], float *contrib, float *variance)
 {
-    integrate_vrl_s(P, rec, rec_id, vs, nvrl, vrl_id, domain, 0u, out_rgb, contrib, variance);
+    integrate_vrl_w(P, rec, rec_id, vs, nvrl, vrl_id, domain, 0u, 0, out_rgb, contrib, variance);
 }
 
 typedef struct {
@@ -546,7 +554,7 @@ static void *brute_worker(void *arg)
             for (uint32_t s = 0; s < ns; s++) {
                 for (uint32_t v = 0; v < j->nvrl; v++) {
                     float c[3], contribution, variance;
-                    integrate_vrl_s(j->P, rec, rid, j->vs, j->nvrl, v, j->domain, s, c,
+                    integrate_vrl_w(j->P, rec, rid, j->vs, j->nvrl, v, j->domain, s, 1, c,
                                     &contribution, &variance);
                     for (int i = 0; i < 3; i++) c[i] *= normalization;
                     if (j->R) {
@@ -594,6 +602,7 @@ static void *clustered_worker(void *arg)
             }
             float rp = 1.0f / (float)j->pc;   /* Li /= particleCount (spectrum.h:447-455) */
             for (int ch = 0; ch < 3; ch++) Li[ch] *= rp;
+            for (int ch = 0; ch < 3; ch++) Li[ch] = Li[ch] * rec[16 + ch];   /* return Li * weight (:598) */
             j->count += k;
         }
         for (int ch = 0; ch < 3; ch++) j->out[3 * (size_t)r + ch] = Li[ch];
@@ -785,6 +794,9 @@ void alvrl_o_make_record(const alvrl_o_scene *s, int medium_scatters, int x, int
     rec[9] = n.x; rec[10] = n.y; rec[11] = n.z;
     rec[12] = alb[0]; rec[13] = alb[1]; rec[14] = alb[2];
     memcpy(&rec[15], &flags, 4);
+    rec[16] = rec[17] = rec[18] = 1.0f;   /* the camera ray: weight 1, depth 0 */
+    uint32_t depth = 0;
+    memcpy(&rec[19], &depth, 4);
 }
 
 void alvrl_o_make_records(const alvrl_o_scene *s, int medium_scatters, float *recs)

@@ -85,14 +85,17 @@ typedef struct {
     uint32_t nocc;
 } alvrl_o_params;
 
-/* Gather record ("eye segment"): 16 x 32-bit words.
+/* Gather record ("eye segment"): 20 x 32-bit words.
  *   [0..2] E   eye ray origin           [3..5] d  eye ray direction
  *   [6..8] p   its.p (surface hit)      [9..11] n shading normal
- *   [12..14] diffuse reflectance        [15] flags (uint32)          */
-#define ALVRL_O_REC_WORDS 16
+ *   [12..14] diffuse reflectance        [15] flags (uint32)
+ *   [16..18] path weight (LiInternal's 'weight', vrlIntegrator.cpp:503-510)
+ *   [19] eye-path depth of the segment's start (uint32, 0 = camera ray)   */
+#define ALVRL_O_REC_WORDS 20
 #define ALVRL_O_FLAG_HIT     1u   /* rRec.its.isValid() */
 #define ALVRL_O_FLAG_SMOOTH  2u   /* bsdf->getType() & BSDF::ESmooth */
 #define ALVRL_O_FLAG_MEDIUM  4u   /* eye medium present and scattering */
+#define ALVRL_O_FLAG_DELTA   8u   /* bsdf->getType() & BSDF::EDelta: the eye path continues */
 
 /* VRL set: SoA, 9 arrays of n floats: sx sy sz ex ey ez pr pg pb (VRL.h:89-96). */
 

@@ -14,7 +14,7 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-REC_WORDS = 16
+REC_WORDS = 20
 FLAG_HIT, FLAG_SMOOTH, FLAG_MEDIUM = 1, 2, 4
 DOM_GATHER, DOM_RBUILD, DOM_TRACER, DOM_REPS, DOM_CLUSTER = 1, 2, 3, 4, 5
 UINT32_MAX = 0xFFFFFFFF

@@ -24,14 +24,14 @@ def test_library_exports_every_declared_symbol():
     assert len(names) >= 20
     missing = [n for n in names if not hasattr(L, n)]
     assert not missing, f"declared but not exported: {missing}"
-    assert L.alvrl_abi_version() == 1
+    assert L.alvrl_abi_version() == 2
 
 
 def test_struct_layouts():
     import alvrl
     assert C.sizeof(alvrl.Config) == 20
     assert C.sizeof(alvrl.MediumDesc) == 36
-    assert alvrl.REC_WORDS * 4 == 64
+    assert alvrl.REC_WORDS * 4 == 80
 
 
 def test_work_items_split_runs():
