@@ -123,10 +123,12 @@ ALVRL_API int alvrl_set_pass(alvrl_ctx *ctx, uint32_t pass);
 /* Occluder triangles (9 floats each: p0 p1 p2) for the visibility part of
  * Scene::evalTransmittance (scene.cpp:619-679) in every gather and R build:
  * a U-V (vol->vol) or surface-V (vol->surf) connection crossing one
- * contributes 0.  Replaces the scene's ShapeKDTree (skdtree.h) for these
- * queries with a BVH built here and kept on the device.  ntri == 0: the
- * convex container (no tests).  Not while gathers run. */
-ALVRL_API int alvrl_set_occluders(alvrl_ctx *ctx, const float *tris, uint32_t ntri);
+ * contributes 0, unless its material (NULL: none is) is ALVRL_MAT_NULL
+ * (alvrl_host.h): a null-BSDF surface lets the connection pass (:636-637).
+ * Replaces the scene's ShapeKDTree (skdtree.h) for these queries with a BVH
+ * built here and kept on the device.  ntri == 0: the convex container (no
+ * tests).  Waits for every launch on the device first. */
+ALVRL_API int alvrl_set_occluders(alvrl_ctx *ctx, const float *tris, uint32_t ntri, const uint32_t *material);
 /* Replaces m_vrls = tracer->randomWalk(...) / new vrlVector(fs, medium) and
  * registerResource(m_vrls) (:276-287, 353).  soa = 9 arrays of n floats:
  * start xyz, end xyz, power rgb (VRL.h:89-96).  particle_count = vrlVector::

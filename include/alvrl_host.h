@@ -40,7 +40,22 @@ typedef struct {
     const float *occluders;
     uint32_t n_occluders;
     float occluder_albedo[3];
+    /* Per-occluder BSDF (NULL: every triangle diffuse), ALVRL_MAT_*:
+     *   DIFFUSE  one-sided diffuse of reflectance occluder_albedo (diffuse.cpp);
+     *   MIRROR   one-sided smooth conductor, material "none" (Fresnel 1) and
+     *            specular reflectance occluder_specular (conductor.cpp:254-268):
+     *            a delta BSDF, so eye paths continue past it (LiInternal's
+     *            specular chains, vrlIntegrator.cpp:445-511);
+     *   NULL     index-matched interface (null.cpp:38-76): light passes through
+     *            unchanged; transparent to Scene::evalTransmittance
+     *            (scene.cpp:633-676), skipped by buildSlices (Preprocessor.cpp:
+     *            1157-1169), it cuts VRLs (vrlTracer.h:173-213). */
+    const uint32_t *occluder_material;
+    float occluder_specular[3];
 } alvrl_scene_desc;
+#define ALVRL_MAT_DIFFUSE 0u
+#define ALVRL_MAT_MIRROR 1u
+#define ALVRL_MAT_NULL 2u
 
 /* The benchmark scene of BASELINE.md ("homogeneous smoke box"). */
 ALVRL_API void alvrl_scene_default(alvrl_scene_desc *s, int width, int height);
@@ -57,6 +72,23 @@ ALVRL_API int alvrl_scene_records(const alvrl_scene_desc *s, int medium_scatters
  * null stream); returns after they are written. */
 ALVRL_API int alvrl_scene_records_gpu(const alvrl_scene_desc *s, int medium_scatters, const uint32_t *d_pixel_ids,
                                       uint32_t n, alvrl_gather_rec *d_out, void *stream);
+/* LiInternal's eye path of pixel (x, y) (vrlIntegrator.cpp:398-524): the
+ * record of the first hit, then, while the hit surface has a delta BSDF
+ * (mirror, null) and the segment's transmittance is non-zero, the specular
+ * chain's next hit (bsdf->sample(bRec, Point2(0.5)), :470-476) with Russian
+ * roulette on throughputWithEtaSq = init_throughput * ... (:480-492; maxRR
+ * 0.98 from depth spec_rr_depth on), drawing from the (seed, pass, pixel,
+ * depth) eye stream.  Record k carries depth k and the path weight
+ * prod transmittance * bsdfWeight / rrProb (:505).  The gather adds every
+ * record's weighted contribution to its pixel.  *n = records (<= cap, at
+ * most 256); ALVRL_ERR_INVALID if cap is too small. */
+ALVRL_API int alvrl_scene_chain(const alvrl_scene_desc *s, int medium_scatters, uint32_t seed, uint32_t pass,
+                                int spec_rr_depth, float init_throughput, int x, int y, alvrl_gather_rec *out,
+                                uint32_t cap, uint32_t *n);
+/* The slicing record of pixel (x, y) (buildSlices, Preprocessor.cpp:1140-1170):
+ * the first hit that is not a null surface; HIT flag, position and normal. */
+ALVRL_API int alvrl_scene_slice_record(const alvrl_scene_desc *s, int x, int y, alvrl_gather_rec *out);
+
 /* ---- reference integrator: volpath with onlyVRLpaths --------------------
  * VolumetricPathTracer::Li (src/integrators/path/volpath.cpp:110-457) on the
  * current HIP device: the path-traced ground truth of exactly the light

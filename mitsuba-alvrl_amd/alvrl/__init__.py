@@ -22,6 +22,7 @@ REPO = os.path.dirname(PKG_DIR)
 LIB_PATH = os.environ.get("ALVRL_LIB") or os.path.join(PKG_DIR, "libalvrl.so")   # ALVRL_LIB: developer variant builds
 
 REC_WORDS = 20
+REC_HIT, REC_SMOOTH, REC_MEDIUM, REC_DELTA, REC_ACCUM = 1, 2, 4, 8, 16   # alvrl_gather_rec.flags
 REC_HIT, REC_SMOOTH, REC_MEDIUM = 1, 2, 4
 UINT32_MAX = 0xFFFFFFFF
 
@@ -171,10 +172,13 @@ class Context:
     def set_pass(self, p: int):
         _check(self.L.alvrl_set_pass(self.h, p))
 
-    def set_occluders(self, tris):
-        """Occluder triangles ((n, 9) float32) blocking the gathers' connections."""
+    def set_occluders(self, tris, material=None):
+        """Occluder triangles ((n, 9) float32) blocking the gathers' connections;
+        material: None or one MAT_* per triangle (MAT_NULL ones let them pass)."""
         arr = np.ascontiguousarray(np.asarray(tris, np.float32).reshape(-1, 9))
-        _check(self.L.alvrl_set_occluders(self.h, _ptr(arr) if len(arr) else None, len(arr)))
+        mat = None if material is None else np.ascontiguousarray(
+            np.broadcast_to(np.asarray(material, np.uint32), (len(arr),)))
+        _check(self.L.alvrl_set_occluders(self.h, _ptr(arr) if len(arr) else None, len(arr), _ptr(mat)))
 
     def upload_vrls(self, soa, particle_count: int):
         """soa: (9, n) float32 numpy array or CUDA tensor (start xyz, end xyz, power rgb)."""
@@ -334,7 +338,11 @@ class SceneDesc(C.Structure):
                 ("box_min", C.c_float * 3), ("box_max", C.c_float * 3), ("albedo", C.c_float * 3),
                 ("light_pos", C.c_float * 3), ("light_intensity", C.c_float * 3),
                 ("medium", MediumDesc), ("occluders", C.POINTER(C.c_float)), ("n_occluders", C.c_uint32),
-                ("occluder_albedo", C.c_float * 3)]
+                ("occluder_albedo", C.c_float * 3), ("occluder_material", C.POINTER(C.c_uint32)),
+                ("occluder_specular", C.c_float * 3)]
+
+
+MAT_DIFFUSE, MAT_MIRROR, MAT_NULL = 0, 1, 2
 
 
 class IntegratorStats(C.Structure):
@@ -460,6 +468,8 @@ def _host():
     P = C.POINTER
     L.alvrl_scene_default.argtypes = [P(SceneDesc), i32, i32]; L.alvrl_scene_default.restype = None
     L.alvrl_scene_records.argtypes = [P(SceneDesc), i32, vp, u32, vp]
+    L.alvrl_scene_chain.argtypes = [P(SceneDesc), i32, u32, u32, i32, f32, i32, i32, vp, u32, P(u32)]
+    L.alvrl_scene_slice_record.argtypes = [P(SceneDesc), i32, i32, vp]
     L.alvrl_trace_vrls.argtypes = [P(SceneDesc), u32, u32, u32, i32, i32, i32, vp, u32, P(u32), P(u64)]
     L.alvrl_trace_vrls_gpu.argtypes = [P(SceneDesc), u32, u32, u32, i32, i32, i32, vp, u32, P(u32), P(u64)]
     L.alvrl_scene_records_gpu.argtypes = [P(SceneDesc), i32, vp, u32, vp, vp]
@@ -515,16 +525,25 @@ def scene_default(width: int, height: int) -> SceneDesc:
     return s
 
 
-def scene_set_occluders(scene: SceneDesc, tris, albedo=(0.5, 0.5, 0.5)) -> SceneDesc:
+def scene_set_occluders(scene: SceneDesc, tris, albedo=(0.5, 0.5, 0.5), material=None,
+                        specular=(1.0, 1.0, 1.0)) -> SceneDesc:
     """Occluder triangles inside the box (alvrl_scene_desc.occluders): an
-    (n, 9) float array of (p0, p1, p2), face normal cross(p1 - p0, p2 - p0).
-    The array is kept alive on the descriptor."""
+    (n, 9) float array of (p0, p1, p2), face normal cross(p1 - p0, p2 - p0);
+    material: None (all diffuse) or one MAT_* per triangle; specular: the
+    mirrors' reflectance.  The arrays are kept alive on the descriptor."""
     arr = np.ascontiguousarray(np.asarray(tris, np.float32).reshape(-1, 9))
     scene._occ_keep = arr
     scene.occluders = arr.ctypes.data_as(C.POINTER(C.c_float)) if len(arr) else None
     scene.n_occluders = len(arr)
     for i in range(3):
         scene.occluder_albedo[i] = float(albedo[i])
+        scene.occluder_specular[i] = float(specular[i])
+    if material is None:
+        scene.occluder_material = None
+    else:
+        mat = np.ascontiguousarray(np.broadcast_to(np.asarray(material, np.uint32), (len(arr),)))
+        scene._mat_keep = mat
+        scene.occluder_material = mat.ctypes.data_as(C.POINTER(C.c_uint32))
     return scene
 
 
@@ -548,6 +567,24 @@ def scene_records(scene: SceneDesc, pixel_ids=None, medium_scatters: bool = True
     out = np.zeros((n, REC_WORDS), np.float32)
     ids = None if pixel_ids is None else _np(pixel_ids, np.uint32)
     _hcheck(L.alvrl_scene_records(C.byref(scene), int(medium_scatters), _ptr(ids), n, _ptr(out)))
+    return out
+
+
+def scene_chain(scene: SceneDesc, x: int, y: int, medium_scatters: bool = True, seed: int = 0xA1B2C3D4,
+                pass_: int = 0, spec_rr_depth: int = 100, init_throughput: float = 20.0) -> np.ndarray:
+    """alvrl_scene_chain: LiInternal's eye path of pixel (x, y), (k, REC_WORDS)."""
+    L = _host()
+    out = np.zeros((256, REC_WORDS), np.float32)
+    n = C.c_uint32()
+    _hcheck(L.alvrl_scene_chain(C.byref(scene), int(medium_scatters), seed, pass_, spec_rr_depth,
+                                float(init_throughput), x, y, _ptr(out), 256, C.byref(n)))
+    return out[:n.value].copy()
+
+
+def scene_slice_record(scene: SceneDesc, x: int, y: int) -> np.ndarray:
+    L = _host()
+    out = np.zeros(REC_WORDS, np.float32)
+    _hcheck(L.alvrl_scene_slice_record(C.byref(scene), x, y, _ptr(out)))
     return out
 
 

@@ -80,6 +80,7 @@ __device__ __forceinline__ V inv_dir(V d)
 }
 
 constexpr int kStack = 48;
+static_assert(kBvhMaxDepth + 2 <= (uint32_t)kStack, "BVH depth cap vs traversal stack");
 
 // Closest triangle hit with t in [mint, *best] that beats *best (strictly, or
 // equal with a lower index than *best_id when *best_id >= 0).  Updates best,
@@ -101,12 +102,12 @@ __device__ inline void closest(const View& b, V o, V d, float mint, float* best,
                 float u, v, t;
                 if (!tri_intersect(b.tris + 9 * (size_t)k, o, d, &u, &v, &t)) continue;
                 if (t < mint) continue;
-                const int id = (int)b.ids[k];
+                const int id = (int)(b.ids[k] & ~kBvhPassBit);
                 if (t < *best || (t == *best && *best_id >= 0 && id < *best_id)) {
                     *best = t; *best_id = id; *slot = (int)k; *bu = u; *bv = v;
                 }
             }
-        } else if (sp + 2 <= kStack) {
+        } else {   // the build caps the depth (kBvhMaxDepth), so the stack never overflows
             float t0, t1;
             const bool h0 = slab(b.nodes[nd.a], o, inv, mint, *best, &t0);
             const bool h1 = slab(b.nodes[nd.a + 1], o, inv, mint, *best, &t1);
@@ -138,10 +139,11 @@ __device__ inline bool occluded(const View& b, V o, V d, float mint, float maxt)
         if (!slab(nd, o, inv, mint, maxt, &tn)) continue;
         if (nd.n > 0) {
             for (uint32_t k = nd.a; k < nd.a + nd.n; k++) {
+                if (b.ids[k] & kBvhPassBit) continue;   // a null-BSDF surface lets the segment pass
                 float u, v, t;
                 if (tri_intersect(b.tris + 9 * (size_t)k, o, d, &u, &v, &t) && !(t < mint || t > maxt)) return true;
             }
-        } else if (sp + 2 <= kStack) {
+        } else {
             stack[sp++] = nd.a + 1;
             stack[sp++] = nd.a;
         }

@@ -300,7 +300,7 @@ ALVRL_API int alvrl_set_medium(alvrl_ctx* c, const alvrl_medium_desc* m)
     return ALVRL_OK;
 }
 
-ALVRL_API int alvrl_set_occluders(alvrl_ctx* c, const float* tris, uint32_t ntri)
+ALVRL_API int alvrl_set_occluders(alvrl_ctx* c, const float* tris, uint32_t ntri, const uint32_t* material)
 {
     if (!c || (!tris && ntri)) return fail(ALVRL_ERR_INVALID, "alvrl_set_occluders: null argument");
     HIPCHK(hipSetDevice(c->cfg.device));
@@ -309,7 +309,12 @@ ALVRL_API int alvrl_set_occluders(alvrl_ctx* c, const float* tris, uint32_t ntri
     if (ntri == 0) return ALVRL_OK;
     for (size_t i = 0; i < 9 * (size_t)ntri; i++)
         if (!std::isfinite(tris[i])) return fail(ALVRL_ERR_INVALID, "alvrl_set_occluders: non-finite vertex");
-    const BvhHost b = build_bvh(tris, ntri);
+    BvhHost b;
+    try {
+        b = build_bvh(tris, ntri, material);
+    } catch (const std::exception& ex) {
+        return fail(ALVRL_ERR_INVALID, std::string("alvrl_set_occluders: ") + ex.what());
+    }
     HIPCHK(hipMalloc(&c->d_bvh_nodes, b.nodes.size() * sizeof(BvhNode)));
     HIPCHK(hipMalloc(&c->d_bvh_tris, b.tris.size() * 4));
     HIPCHK(hipMalloc(&c->d_bvh_ids, b.ids.size() * 4));

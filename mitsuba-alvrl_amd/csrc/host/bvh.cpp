@@ -3,10 +3,11 @@
 
 #include <algorithm>
 #include <cmath>
+#include <stdexcept>
 
 namespace alvrl {
 
-BvhHost build_bvh(const float* tri, uint32_t ntri)
+BvhHost build_bvh(const float* tri, uint32_t ntri, const uint32_t* material)
 {
     BvhHost b;
     if (ntri == 0) return b;
@@ -17,12 +18,13 @@ BvhHost build_bvh(const float* tri, uint32_t ntri)
         for (int a = 0; a < 3; a++)
             cen[3 * (size_t)i + a] = (tri[9 * (size_t)i + a] + tri[9 * (size_t)i + 3 + a] + tri[9 * (size_t)i + 6 + a]) * (1.0f / 3.0f);
     }
-    struct Task { uint32_t node, begin, end; };
+    struct Task { uint32_t node, begin, end, depth; };
     b.nodes.push_back(BvhNode{});
-    std::vector<Task> stack{{0u, 0u, ntri}};
+    std::vector<Task> stack{{0u, 0u, ntri, 0u}};
     while (!stack.empty()) {
         const Task t = stack.back();
         stack.pop_back();
+        if (t.depth > kBvhMaxDepth) throw std::length_error("occluder BVH deeper than the traversal stack");
         float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
         float clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
         for (uint32_t k = t.begin; k < t.end; k++) {
@@ -50,7 +52,7 @@ BvhHost build_bvh(const float* tri, uint32_t ntri)
             nd.a = (uint32_t)b.ids.size();
             nd.n = cnt;
             for (uint32_t k = t.begin; k < t.end; k++) {
-                b.ids.push_back(idx[k]);
+                b.ids.push_back(idx[k] | (material && material[idx[k]] == 2u ? kBvhPassBit : 0u));
                 b.tris.insert(b.tris.end(), tri + 9 * (size_t)idx[k], tri + 9 * (size_t)idx[k] + 9);
             }
             continue;
@@ -68,8 +70,8 @@ BvhHost build_bvh(const float* tri, uint32_t ntri)
         b.nodes.push_back(BvhNode{});
         b.nodes[t.node].a = left;   // (nd may dangle after the push_backs)
         b.nodes[t.node].n = 0;
-        stack.push_back(Task{left + 1, mid, t.end});
-        stack.push_back(Task{left, t.begin, mid});
+        stack.push_back(Task{left + 1, mid, t.end, t.depth + 1});
+        stack.push_back(Task{left, t.begin, mid, t.depth + 1});
     }
     return b;
 }

@@ -28,11 +28,18 @@ static_assert(sizeof(BvhNode) == 32, "BvhNode layout");
 struct BvhHost {
     std::vector<BvhNode> nodes;     // root = nodes[0]
     std::vector<float> tris;        // 9 floats per triangle, leaf order
-    std::vector<uint32_t> ids;      // original triangle index per leaf slot
+    std::vector<uint32_t> ids;      // original triangle index per leaf slot (| kBvhPassBit)
 };
 
+// ids bit 31: a null-BSDF triangle, which the occlusion test passes
+// (Scene::evalTransmittance, scene.cpp:636-637) but closest hits see
+constexpr uint32_t kBvhPassBit = 0x80000000u;
+constexpr uint32_t kBvhMaxDepth = 40;   // the traversal stacks hold 48 nodes
+
 // Median split on the widest centroid axis (ties by triangle index), leaves
-// of at most 4 triangles; deterministic.
-BvhHost build_bvh(const float* tri, uint32_t ntri);
+// of at most 4 triangles; deterministic.  material: per triangle (2 = null:
+// kBvhPassBit), or null.  Throws std::length_error if the tree would be
+// deeper than kBvhMaxDepth (the device traversal could not hold it).
+BvhHost build_bvh(const float* tri, uint32_t ntri, const uint32_t* material = nullptr);
 
 }  // namespace alvrl

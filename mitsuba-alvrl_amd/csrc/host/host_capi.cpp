@@ -14,6 +14,16 @@ using namespace alvrl::host;
 namespace alvrl {
 namespace host {
 thread_local std::string g_host_err;
+// what is wrong with a scene descriptor, or nullptr
+const char* scene_problem(const alvrl_scene_desc& s)
+{
+    if (s.width <= 0 || s.height <= 0) return "alvrl_scene_desc: width and height must be > 0";
+    if (s.n_occluders && !s.occluders) return "alvrl_scene_desc: n_occluders > 0 without occluders";
+    if (s.occluders && s.occluder_material)
+        for (uint32_t i = 0; i < s.n_occluders; i++)
+            if (s.occluder_material[i] > ALVRL_MAT_NULL) return "alvrl_scene_desc: unknown occluder material";
+    return nullptr;
+}
 SmokeBox to_box(const alvrl_scene_desc& s)
 {
     SmokeBox b;
@@ -34,6 +44,9 @@ SmokeBox to_box(const alvrl_scene_desc& s)
     b.medium.resolve();
     if (s.occluders && s.n_occluders) b.occ.assign(s.occluders, s.occluders + 9 * (size_t)s.n_occluders);
     for (int i = 0; i < 3; i++) b.occ_albedo[i] = s.occluder_albedo[i];
+    if (s.occluders && s.n_occluders && s.occluder_material)
+        b.occ_mat.assign(s.occluder_material, s.occluder_material + s.n_occluders);
+    for (int i = 0; i < 3; i++) b.occ_spec[i] = s.occluder_specular[i];
     return b;
 }
 }  // namespace host
@@ -68,12 +81,15 @@ ALVRL_API void alvrl_scene_default(alvrl_scene_desc* s, int width, int height)
     s->occluders = nullptr;
     s->n_occluders = 0;
     for (int i = 0; i < 3; i++) s->occluder_albedo[i] = b.occ_albedo[i];
+    s->occluder_material = nullptr;
+    for (int i = 0; i < 3; i++) s->occluder_specular[i] = b.occ_spec[i];
 }
 
 ALVRL_API int alvrl_scene_records(const alvrl_scene_desc* s, int medium_scatters, const uint32_t* ids,
                                   uint32_t n, alvrl_gather_rec* out)
 {
     if (!s || (!out && n)) return herr(ALVRL_ERR_INVALID, "alvrl_scene_records: null argument");
+    if (const char* m = scene_problem(*s)) return herr(ALVRL_ERR_INVALID, m);
     const SmokeBox b = to_box(*s);
     const uint64_t npix = (uint64_t)b.width * (uint64_t)b.height;
     if (!ids && n != npix) return herr(ALVRL_ERR_INVALID, "alvrl_scene_records: n must be W*H without pixel ids");
@@ -84,6 +100,34 @@ ALVRL_API int alvrl_scene_records(const alvrl_scene_desc* s, int medium_scatters
         b.make_record((int)(p % (uint32_t)b.width), (int)(p / (uint32_t)b.width), scat,
                       reinterpret_cast<float*>(&out[i]));
     }
+    return ALVRL_OK;
+}
+
+ALVRL_API int alvrl_scene_chain(const alvrl_scene_desc* s, int medium_scatters, uint32_t seed, uint32_t pass,
+                                int spec_rr_depth, float init_throughput, int x, int y, alvrl_gather_rec* out,
+                                uint32_t cap, uint32_t* n)
+{
+    if (!s || !n || (!out && cap)) return herr(ALVRL_ERR_INVALID, "alvrl_scene_chain: null argument");
+    if (const char* m = scene_problem(*s)) return herr(ALVRL_ERR_INVALID, m);
+    const SmokeBox b = to_box(*s);
+    if (x < 0 || y < 0 || x >= b.width || y >= b.height) return herr(ALVRL_ERR_INVALID, "alvrl_scene_chain: pixel out of range");
+    const bool scat = medium_scatters && !(b.medium.sigma_s[0] == 0 && b.medium.sigma_s[1] == 0 && b.medium.sigma_s[2] == 0);
+    std::vector<float> recs;
+    b.make_chain(x, y, scat, seed, pass, spec_rr_depth, init_throughput, &recs);
+    const uint32_t k = (uint32_t)(recs.size() / kRecWords);
+    *n = k;
+    if (k > cap) return herr(ALVRL_ERR_INVALID, "alvrl_scene_chain: capacity too small");
+    if (k) std::memcpy(out, recs.data(), sizeof(float) * recs.size());
+    return ALVRL_OK;
+}
+
+ALVRL_API int alvrl_scene_slice_record(const alvrl_scene_desc* s, int x, int y, alvrl_gather_rec* out)
+{
+    if (!s || !out) return herr(ALVRL_ERR_INVALID, "alvrl_scene_slice_record: null argument");
+    if (const char* m = scene_problem(*s)) return herr(ALVRL_ERR_INVALID, m);
+    const SmokeBox b = to_box(*s);
+    if (x < 0 || y < 0 || x >= b.width || y >= b.height) return herr(ALVRL_ERR_INVALID, "alvrl_scene_slice_record: pixel out of range");
+    b.make_slice_record(x, y, reinterpret_cast<float*>(out));
     return ALVRL_OK;
 }
 
@@ -115,6 +159,7 @@ ALVRL_API int alvrl_trace_vrls(const alvrl_scene_desc* s, uint32_t seed, uint32_
                                uint32_t* n, uint64_t* particles)
 {
     if (!s || !soa || !n || !particles) return herr(ALVRL_ERR_INVALID, "alvrl_trace_vrls: null argument");
+    if (const char* m = scene_problem(*s)) return herr(ALVRL_ERR_INVALID, m);
     const SmokeBox b = to_box(*s);
     const VrlSet v = trace_vrls(b, seed, pass, target, short_vrls != 0, max_depth, rr_depth);
     if (v.n > cap) return herr(ALVRL_ERR_INVALID, "alvrl_trace_vrls: capacity too small (" + std::to_string(v.n) + " VRLs)");

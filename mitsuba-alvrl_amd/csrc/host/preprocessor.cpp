@@ -151,7 +151,7 @@ std::vector<uint32_t> Preprocessor::build_slices(const SmokeBox& s, const float*
             float own[kRecWords];
             const float* rec = own;
             if (recs) rec = recs + kRecWords * ((size_t)j * W + i);
-            else s.make_record(i, j, true, own);
+            else s.make_slice_record(i, j, own);
             uint32_t flags;
             std::memcpy(&flags, &rec[15], 4);
             const uint32_t k = (uint32_t)i * H + j;

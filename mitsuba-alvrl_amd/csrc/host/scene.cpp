@@ -16,6 +16,7 @@ namespace host {
 namespace {
 constexpr double kPi = 3.14159265358979323846;
 constexpr uint32_t kDomTracer = 3u;
+constexpr uint32_t kDomEye = 7u;   // Russian roulette of the eye paths' specular chains
 
 inline float fastexp(float v) { return (float)std::exp((double)v); }   // math.h:185-199
 inline float fastlog(float v) { return (float)std::log((double)v); }
@@ -138,6 +139,7 @@ bool SmokeBox::visible(V3 p1, bool p1_surface, V3 p2, bool p2_surface) const
     const float mint = p1_surface ? 1e-4f : 0.0f;                     // Epsilon
     const float maxt = remaining * (p2_surface ? (1 - 1e-3f) : 1.0f);   // ShadowEpsilon
     for (uint32_t i = 0; i < nt; i++) {
+        if (mat((int)i) == 2u) continue;   // ENull: passes (scene.cpp:636-637)
         float u, v, t;
         if (tri_intersect(&occ[9 * (size_t)i], p1, d, &u, &v, &t) && !(t < mint || t > maxt)) return false;
     }
@@ -151,10 +153,12 @@ void SmokeBox::make_record(int x, int y, bool medium_scatters, float rec[kRecWor
     camera_ray((float)x + 0.5f, (float)y + 0.5f, &O, &D, &mint);   // renderBlock pixel centre, integrator.cpp:243-245
     int tri;
     const float t = first_hit(O, D, mint, &n, &p, &tri);
+    const uint32_t m = mat(tri);
     uint32_t flags = 0;
-    if (std::isfinite(t)) flags |= 1u | 2u;
+    if (std::isfinite(t)) flags |= 1u | (m == 0u ? 2u : 8u);   // ESmooth (diffuse) or EDelta
     if (medium_scatters) flags |= 4u;
-    const float* a = tri >= 0 ? occ_albedo : albedo;
+    static const float kZero[3] = {0.0f, 0.0f, 0.0f};
+    const float* a = m != 0u ? kZero : (tri >= 0 ? occ_albedo : albedo);
     rec[0] = O.x; rec[1] = O.y; rec[2] = O.z;
     rec[3] = D.x; rec[4] = D.y; rec[5] = D.z;
     rec[6] = p.x; rec[7] = p.y; rec[8] = p.z;
@@ -164,6 +168,33 @@ void SmokeBox::make_record(int x, int y, bool medium_scatters, float rec[kRecWor
     rec[16] = rec[17] = rec[18] = 1.0f;   // the camera ray: path weight 1, depth 0
     const uint32_t depth = 0;
     std::memcpy(&rec[19], &depth, 4);
+}
+
+void SmokeBox::make_slice_record(int x, int y, float rec[kRecWords]) const
+{
+    V3 O, D, n, p;
+    float mint;
+    camera_ray((float)x + 0.5f, (float)y + 0.5f, &O, &D, &mint);
+    int tri;
+    float t = first_hit(O, D, mint, &n, &p, &tri);
+    uint32_t flags = 0;
+    V3 gp = p, gn = n;
+    if (std::isfinite(t)) {
+        flags = 1u;
+        while (true) {   // Preprocessor.cpp:1157-1169
+            gp = p; gn = n;
+            if (mat(tri) != 2u) break;
+            t = first_hit(O, D, t + 1e-4f, &n, &p, &tri);   // Ray(ray, its.t + Epsilon, ray.maxt)
+            if (!std::isfinite(t)) break;
+        }
+    }
+    for (int k = 0; k < kRecWords; k++) rec[k] = 0.0f;
+    rec[0] = O.x; rec[1] = O.y; rec[2] = O.z;
+    rec[3] = D.x; rec[4] = D.y; rec[5] = D.z;
+    rec[6] = gp.x; rec[7] = gp.y; rec[8] = gp.z;
+    rec[9] = gn.x; rec[10] = gn.y; rec[11] = gn.z;
+    std::memcpy(&rec[15], &flags, 4);
+    rec[16] = rec[17] = rec[18] = 1.0f;
 }
 
 float SmokeBox::scene_diagonal() const
@@ -340,12 +371,23 @@ void trace_particle(const SmokeBox& sc, Stream& smp, bool short_vrls, int max_de
             frame_of(n, &fs, &ft);
             const V3 mwi = -dir;
             const float cos_wi = dot(mwi, n);
-            const float bx = smp.next(), by = smp.next();
+            const float bx = smp.next(), by = smp.next();   // bsdf->sample(bRec, next2D())
             float bw[3] = {0, 0, 0};
             V3 wol = v3(0, 0, 0);
-            if (!(cos_wi <= 0)) {
-                wol = cosine_hemisphere(bx, by);
-                for (int i = 0; i < 3; i++) bw[i] = alb[i];
+            const uint32_t mt = sc.mat(tri);
+            if (mt == 0u) {          // SmoothDiffuse::sample (diffuse.cpp:120-133)
+                if (!(cos_wi <= 0)) {
+                    wol = cosine_hemisphere(bx, by);
+                    for (int i = 0; i < 3; i++) bw[i] = alb[i];
+                }
+            } else if (mt == 1u) {   // SmoothConductor::sample (conductor.cpp:254-268), material none
+                if (!(cos_wi <= 0)) {
+                    wol = v3(-dot(mwi, fs), -dot(mwi, ft), cos_wi);   // reflect(wi)
+                    for (int i = 0; i < 3; i++) bw[i] = sc.occ_spec[i];
+                }
+            } else {                 // Null::sample (null.cpp:53-63): wo = -wi
+                wol = v3(-dot(mwi, fs), -dot(mwi, ft), -cos_wi);
+                bw[0] = bw[1] = bw[2] = 1.0f;
             }
             if (bw[0] == 0 && bw[1] == 0 && bw[2] == 0) { k.end_current(p); break; }
             const V3 wo = (fs * wol.x + ft * wol.y) + n * wol.z;
@@ -372,6 +414,80 @@ void trace_particle(const SmokeBox& sc, Stream& smp, bool short_vrls, int max_de
 }
 
 }  // namespace
+
+void SmokeBox::make_chain(int x, int y, bool medium_scatters, uint32_t seed, uint32_t pass, int spec_rr_depth,
+                          float init_throughput, std::vector<float>* out) const
+{
+    V3 O, D;
+    float mint;
+    camera_ray((float)x + 0.5f, (float)y + 0.5f, &O, &D, &mint);   // the pixel centre (integrator.cpp:243-245)
+    const uint32_t pixel = (uint32_t)y * (uint32_t)width + (uint32_t)x;
+    float weight[3] = {1.0f, 1.0f, 1.0f};
+    float thr[3] = {init_throughput, init_throughput, init_throughput};   // throughputWithEtaSq (:381)
+    int depth = 1;                                                        // rRec.depth of the sensor ray
+    for (uint32_t k = 0; k < 256; k++) {
+        V3 n, p;
+        int tri;
+        const float t = first_hit(O, D, mint, &n, &p, &tri);
+        if (!std::isfinite(t)) break;                                     // :414-419
+        const uint32_t m = mat(tri);
+        uint32_t flags = 1u | (m == 0u ? 2u : 8u) | (medium_scatters ? 4u : 0u);
+        const float* a = tri >= 0 ? occ_albedo : albedo;
+        const size_t o = out->size();
+        out->resize(o + kRecWords);
+        float* rec = out->data() + o;
+        rec[0] = O.x; rec[1] = O.y; rec[2] = O.z;
+        rec[3] = D.x; rec[4] = D.y; rec[5] = D.z;
+        rec[6] = p.x; rec[7] = p.y; rec[8] = p.z;
+        rec[9] = n.x; rec[10] = n.y; rec[11] = n.z;
+        for (int i = 0; i < 3; i++) rec[12 + i] = m == 0u ? a[i] : 0.0f;
+        std::memcpy(&rec[15], &flags, 4);
+        for (int i = 0; i < 3; i++) rec[16 + i] = weight[i];
+        std::memcpy(&rec[19], &k, 4);
+        if (m == 0u) break;                                               // no delta component (:449-450)
+        // transmittance of the segment, rRec.medium->eval(Ray(ray, 0, its.t)) (:452-458)
+        float tr[3];
+        for (int i = 0; i < 3; i++) tr[i] = fastexp(medium.sigma_t[i] * (-t));
+        {
+            float mx = tr[0] > tr[1] ? tr[0] : tr[1];
+            mx = mx > tr[2] ? mx : tr[2];
+            if (mx < 1e-20f) tr[0] = tr[1] = tr[2] = 0;
+        }
+        if (tr[0] == 0 && tr[1] == 0 && tr[2] == 0) break;               // :459-460
+        // the delta component, bsdf->sample(bRec, Point2(0.5f)) (:470-475)
+        V3 fs, ft;
+        frame_of(n, &fs, &ft);
+        const V3 mwi = -D;
+        const float cos_wi = dot(mwi, n);
+        float bw[3];
+        V3 wol;
+        if (m == 1u) {   // conductor.cpp:254-268
+            if (cos_wi <= 0) break;
+            wol = v3(-dot(mwi, fs), -dot(mwi, ft), cos_wi);
+            for (int i = 0; i < 3; i++) bw[i] = occ_spec[i];
+        } else {         // null.cpp:53-63
+            wol = v3(-dot(mwi, fs), -dot(mwi, ft), -cos_wi);
+            bw[0] = bw[1] = bw[2] = 1.0f;
+        }
+        // Russian roulette (:477-492): eta = 1 for both BSDFs
+        float thr2[3];
+        for (int i = 0; i < 3; i++) thr2[i] = ((thr[i] * tr[i]) * bw[i]) * 1.0f;
+        const float maxRR = depth >= spec_rr_depth ? 0.98f : 1.0f;
+        float mx = thr2[0] > thr2[1] ? thr2[0] : thr2[1];
+        mx = mx > thr2[2] ? mx : thr2[2];
+        const float rrProb = maxRR < mx ? maxRR : mx;
+        Stream smp{seed, pass, kDomEye, pixel, k, 0u};
+        if (rrProb <= 0 || (rrProb < 1 && smp.next() > rrProb)) break;
+        for (int i = 0; i < 3; i++) {
+            thr[i] = thr2[i] / rrProb;
+            weight[i] = ((weight[i] * tr[i]) * bw[i]) / rrProb;             // weight * transmittance * bsdfWeight / rrProb (:503-510)
+        }
+        O = p;
+        D = (fs * wol.x + ft * wol.y) + n * wol.z;                            // its.toWorld(bRec.wo)
+        mint = 1e-4f;                                                         // RayDifferential(its.p, wo): mint = Epsilon
+        depth++;
+    }
+}
 
 VrlSet trace_vrls(const SmokeBox& sc, uint32_t seed, uint32_t pass, uint32_t target, bool short_vrls,
                   int max_depth, int rr_depth)

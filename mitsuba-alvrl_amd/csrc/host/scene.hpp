@@ -62,6 +62,15 @@ struct SmokeBox {
     MediumParams medium;
     std::vector<float> occ;           // occluder triangles, 9 floats each (p0, p1, p2)
     float occ_albedo[3] = {0.5f, 0.5f, 0.5f};
+    std::vector<uint32_t> occ_mat;    // per triangle ALVRL_MAT_* (empty: all diffuse)
+    float occ_spec[3] = {1.0f, 1.0f, 1.0f};
+    // the BSDF of a hit: 0 diffuse (walls: tri < 0), 1 mirror, 2 null
+    uint32_t mat(int tri) const { return (tri < 0 || occ_mat.empty()) ? 0u : occ_mat[(size_t)tri]; }
+    bool has_delta() const
+    {
+        for (uint32_t m : occ_mat) if (m != 0u) return true;
+        return false;
+    }
 
     // Sensor::sampleRay through pixel sample (px, py); *mint = nearClip / d.z
     // in camera space (perspective.cpp:247-263, nearClip 1e-2).
@@ -74,8 +83,20 @@ struct SmokeBox {
     float first_hit(V3 o, V3 d, float mint, V3* n, V3* p, int* tri) const;
     // The occluder part of Scene::evalTransmittance(p1, p1OnSurface, p2,
     // p2OnSurface): false if a triangle lies on the segment (the walls
-    // cannot: both points are inside the box).
+    // cannot: both points are inside the box); null triangles let it pass.
     bool visible(V3 p1, bool p1_surface, V3 p2, bool p2_surface) const;
+    // The eye path of pixel centre (x, y) through delta BSDFs: LiInternal's
+    // recursion (vrlIntegrator.cpp:386-524) as gather records, one per
+    // segment, each with the weight the recursion passes down (:503-510) and
+    // its depth; Russian roulette from initialSpecularThroughput, maxRR 0.98
+    // past specularForcedRRdepth (:475-492), its uniform from the stream
+    // (seed, pass, dom 7, pixel, depth).  Appends kRecWords floats per record.
+    void make_chain(int x, int y, bool medium_scatters, uint32_t seed, uint32_t pass, int spec_rr_depth,
+                    float init_throughput, std::vector<float>* out) const;
+    // buildSlices' gather point of pixel (x, y) (Preprocessor.cpp:1144-1170):
+    // the camera ray's first hit, continued through null surfaces; a record
+    // with the hit flag, position and normal of that point.
+    void make_slice_record(int x, int y, float rec[kRecWords]) const;
     uint32_t n_occ() const { return (uint32_t)(occ.size() / 9); }
     // Gather record (alvrl_gather_rec layout) of pixel centre (x, y).
     void make_record(int x, int y, bool medium_scatters, float rec[kRecWords]) const;

@@ -20,6 +20,7 @@
 #include <sstream>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "host/exchange.hpp"
@@ -142,7 +143,16 @@ struct alvrl_integrator {
     std::vector<float> w_buf;
     std::vector<float> weights, fb_w;
     // render cache per (rank, world)
-    uint32_t cache_rank = 0xFFFFFFFFu, cache_world = 0, cache_mode = 0;
+    uint32_t cache_rank = 0xFFFFFFFFu, cache_world = 0, cache_mode = 0, cache_pass = 0xFFFFFFFFu;
+    uint32_t cur_pass = 0;
+    // the eye paths' delta-BSDF chains (scene.has_delta()): records of depth
+    // d >= 1 follow the primary records, level by level
+    bool chains = false;
+    DevBuf<alvrl_gather_rec> ch_recs;
+    DevBuf<uint32_t> ch_ids, ch_stride;
+    DevBuf<uint64_t> ch_off;
+    std::vector<uint32_t> level_rec;        // render: first record of each depth level (+ end)
+    std::vector<uint32_t> level_item;       // render: first work item of each level (+ end)
     DevBuf<alvrl_gather_rec> rec_buf;
     DevBuf<uint32_t> pix_buf;
     DevBuf<alvrl_work_item> item_buf;
@@ -219,7 +229,12 @@ struct alvrl_integrator {
         have_scene = true;
         alvrl_medium_desc md = s.medium;
         chk(alvrl_set_medium(ctx, &md), "alvrl_set_medium");
-        chk(alvrl_set_occluders(ctx, scene_desc.occluders, scene_desc.n_occluders), "alvrl_set_occluders");
+        scene_desc.occluder_material = scene.occ_mat.empty() ? nullptr : scene.occ_mat.data();
+        chains = scene.has_delta();
+        if (chains && convergenceFalseColor)
+            throw IntegError(ALVRL_ERR_INVALID, "convergenceFalseColor is not supported with delta-BSDF occluders");
+        chk(alvrl_set_occluders(ctx, scene_desc.occluders, scene_desc.n_occluders, scene_desc.occluder_material),
+            "alvrl_set_occluders");
         if (!vrlFile.empty()) {   // :243-252
             std::string err;
             if (!read_vrl_file(vrlFile.c_str(), scene.medium, &vrls, &err)) throw IntegError(ALVRL_ERR_INVALID, err);
@@ -237,14 +252,16 @@ struct alvrl_integrator {
             const double t0 = now_ms();
             // the eye-ray first hit of every pixel on the device (Preprocessor.cpp:1140-1170)
             const uint32_t npix = (uint32_t)scene.width * (uint32_t)scene.height;
-            DevBuf<alvrl_gather_rec> d_all;
-            d_all.ensure(npix);
-            std::vector<alvrl_gather_rec> h_all(npix);
-            if (npix) {
+            std::vector<alvrl_gather_rec> h_all;
+            if (npix && !chains) {
+                DevBuf<alvrl_gather_rec> d_all;
+                d_all.ensure(npix);
+                h_all.resize(npix);
                 chk_host(alvrl_scene_records_gpu(&scene_desc, 1, nullptr, npix, d_all.p, stream));
                 hchk(hipMemcpy(h_all.data(), d_all.p, sizeof(alvrl_gather_rec) * npix, hipMemcpyDeviceToHost), "copy records");
             }
-            pixel_to_slice = prep->build_slices(scene, reinterpret_cast<const float*>(h_all.data()));
+            // with null surfaces the slicing ray passes them (:1157-1169): host records
+            pixel_to_slice = prep->build_slices(scene, h_all.empty() ? nullptr : reinterpret_cast<const float*>(h_all.data()));
             st.ms_slices = now_ms() - t0;
             st.slices = prep->num_slices();
         }
@@ -273,6 +290,7 @@ struct alvrl_integrator {
     void pass_vrls(uint32_t pass)
     {
         chk(alvrl_set_pass(ctx, pass), "alvrl_set_pass");
+        cur_pass = pass;
         // VRLs (:276-287): traced per pass unless preloaded from a file
         if (!vrls_from_file) {
             const double t0 = now_ms();
@@ -346,6 +364,66 @@ struct alvrl_integrator {
         st.clusters_total = reps.size();
     }
 
+    // LiInternal's specular chains (:445-511) of the given row-major pixels,
+    // traced on the host (SmokeBox::make_chain, the occluders are few):
+    // recs[d - 1] = the records of depth d >= 1 (their path weights
+    // transmittance * bsdfWeight / rrProb multiplied along the chain), src =
+    // the index into ids of each; prim[i] = the primary record of ids[i]
+    // (the device's eye-ray kernel knows no materials).  The Russian roulette
+    // draws from the pass's (seed, pass, pixel, depth) stream.
+    struct Chains {
+        std::vector<std::vector<alvrl_gather_rec>> recs;
+        std::vector<std::vector<uint32_t>> src;
+    };
+    Chains expand_chains(const std::vector<uint32_t>& ids, bool scat, bool accum,
+                         std::vector<alvrl_gather_rec>* prim) const
+    {
+        prim->resize(ids.size());
+        const uint32_t n = (uint32_t)ids.size();
+        const uint32_t W = (uint32_t)scene.width;
+        unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+        if (n < 4096) nt = 1;
+        std::vector<Chains> part(nt);
+        auto work = [&](unsigned t) {
+            std::vector<float> buf;
+            Chains& c = part[t];
+            const uint32_t b = (uint32_t)((uint64_t)n * t / nt), e = (uint32_t)((uint64_t)n * (t + 1) / nt);
+            for (uint32_t i = b; i < e; i++) {
+                scene.make_record((int)(ids[i] % W), (int)(ids[i] / W), scat, reinterpret_cast<float*>(&(*prim)[i]));
+                buf.clear();
+                scene.make_chain((int)(ids[i] % W), (int)(ids[i] / W), scat, seed, cur_pass, specRRdepth,
+                                 initialSpecularThroughput, &buf);
+                const size_t k = buf.size() / kRecWords;
+                for (size_t d = 1; d < k; d++) {
+                    if (c.recs.size() < d) { c.recs.resize(d); c.src.resize(d); }
+                    alvrl_gather_rec r;
+                    std::memcpy(&r, &buf[d * kRecWords], sizeof(r));
+                    if (accum) r.flags |= ALVRL_REC_ACCUM;
+                    c.recs[d - 1].push_back(r);
+                    c.src[d - 1].push_back(i);
+                }
+            }
+        };
+        if (nt == 1) work(0);
+        else {
+            std::vector<std::thread> th;
+            for (unsigned t = 0; t < nt; t++) th.emplace_back(work, t);
+            for (auto& x : th) x.join();
+        }
+        Chains out;
+        for (unsigned t = 0; t < nt; t++) {
+            if (out.recs.size() < part[t].recs.size()) {
+                out.recs.resize(part[t].recs.size());
+                out.src.resize(part[t].recs.size());
+            }
+            for (size_t d = 0; d < part[t].recs.size(); d++) {
+                out.recs[d].insert(out.recs[d].end(), part[t].recs[d].begin(), part[t].recs[d].end());
+                out.src[d].insert(out.src[d].end(), part[t].src[d].begin(), part[t].src[d].end());
+            }
+        }
+        return out;
+    }
+
     // Building R (:302-333) for the rows of the slices flagged in 'need'.  R is
     // stored as one [vrl][row] block per slice (the reference's
     // R[slice][rep][vrl], transposed): a slice's local matrix is then one
@@ -395,9 +473,40 @@ struct alvrl_integrator {
         Rt.ensure((size_t)2 * nv * acc);
         if (nb) {
             hchk(hipMemcpyAsync(rep_ids.p, ids.data(), sizeof(uint32_t) * nb, hipMemcpyHostToDevice, stream), "copy rep ids");
-            chk_host(alvrl_scene_records_gpu(&scene_desc, scat ? 1 : 0, rep_ids.p, nb, rep_recs.p, stream));
+            if (!chains) chk_host(alvrl_scene_records_gpu(&scene_desc, scat ? 1 : 0, rep_ids.p, nb, rep_recs.p, stream));
             hchk(hipMemcpyAsync(rb_off.p, boff.data(), sizeof(uint64_t) * nb, hipMemcpyHostToDevice, stream), "copy row offsets");
             hchk(hipMemcpyAsync(rb_stride.p, bstr.data(), sizeof(uint32_t) * nb, hipMemcpyHostToDevice, stream), "copy row strides");
+        }
+        // getLiLuminanceVrlContributions follows the row's delta-BSDF chain
+        // (:527-539 -> LiInternal :445-511) and the contributions of every
+        // level add into the row (:812-813): one launch per depth level, its
+        // records flagged ALVRL_REC_ACCUM (a row has at most one record per level)
+        Chains ch;
+        std::vector<uint32_t> lv_off{0};
+        if (chains && nb) {
+            std::vector<alvrl_gather_rec> prim;
+            ch = expand_chains(ids, scat, true, &prim);
+            hchk(hipMemcpy(rep_recs.p, prim.data(), sizeof(alvrl_gather_rec) * nb, hipMemcpyHostToDevice), "copy records");
+            std::vector<alvrl_gather_rec> r;
+            std::vector<uint32_t> cid, cstr;
+            std::vector<uint64_t> coff;
+            for (size_t d = 0; d < ch.recs.size(); d++) {
+                for (size_t j = 0; j < ch.recs[d].size(); j++) {
+                    const uint32_t i = ch.src[d][j];
+                    r.push_back(ch.recs[d][j]);
+                    cid.push_back(ids[i]); coff.push_back(boff[i]); cstr.push_back(bstr[i]);
+                }
+                lv_off.push_back((uint32_t)r.size());
+            }
+            const size_t n = r.size();
+            ch_recs.ensure(n); ch_ids.ensure(n); ch_off.ensure(n); ch_stride.ensure(n);
+            if (n) {
+                hchk(hipMemcpyAsync(ch_recs.p, r.data(), sizeof(alvrl_gather_rec) * n, hipMemcpyHostToDevice, stream), "copy chain records");
+                hchk(hipMemcpyAsync(ch_ids.p, cid.data(), sizeof(uint32_t) * n, hipMemcpyHostToDevice, stream), "copy chain ids");
+                hchk(hipMemcpyAsync(ch_off.p, coff.data(), sizeof(uint64_t) * n, hipMemcpyHostToDevice, stream), "copy chain offsets");
+                hchk(hipMemcpyAsync(ch_stride.p, cstr.data(), sizeof(uint32_t) * n, hipMemcpyHostToDevice, stream), "copy chain strides");
+                hchk(hipStreamSynchronize(stream), "sync");   // r, cid, ... are freed on return
+            }
         }
         hchk(hipMemsetAsync(nz_dev.p, 0, nv, stream), "clear mask");
         hipEvent_t e0, e1;
@@ -405,6 +514,10 @@ struct alvrl_integrator {
         hchk(hipEventRecord(e0, stream), "event");
         chk(alvrl_build_R_blocks(ctx, rep_recs.p, rep_ids.p, nb, Rt.p, rb_off.p, rb_stride.p, nz_dev.p, stream),
             "alvrl_build_R_blocks");
+        for (size_t d = 0; d + 1 < lv_off.size(); d++)
+            chk(alvrl_build_R_blocks(ctx, ch_recs.p + lv_off[d], ch_ids.p + lv_off[d], lv_off[d + 1] - lv_off[d], Rt.p,
+                                     ch_off.p + lv_off[d], ch_stride.p + lv_off[d], nz_dev.p, stream),
+                "alvrl_build_R_blocks (chain level)");
         hchk(hipEventRecord(e1, stream), "event");
         nz->assign(nv, 0);
         if (nv) hchk(hipMemcpyAsync(nz->data(), nz_dev.p, nv, hipMemcpyDeviceToHost, stream), "copy mask");
@@ -626,30 +739,59 @@ struct alvrl_integrator {
     void prepare_render(uint32_t rank, uint32_t world)
     {
         const uint32_t mode = clustered ? 2u : 1u;
-        if (cache_rank == rank && cache_world == world && cache_mode == mode) return;
+        // chains depend on the pass (their Russian roulette)
+        if (cache_rank == rank && cache_world == world && cache_mode == mode && (!chains || cache_pass == cur_pass))
+            return;
         const int W = scene.width, H = scene.height;
         uint32_t npix = 0;
         chk_host(alvrl_tile_pixels(W, H, rank, world, nullptr, 0, &npix));
         std::vector<uint32_t> pix(npix);
         chk_host(alvrl_tile_pixels(W, H, rank, world, pix.data(), npix, &npix));
         std::vector<alvrl_work_item> items;
-        if (clustered) {   // bucket by slice (stable), wave work items
-            std::vector<uint32_t> sl(pix.size());
-            for (size_t i = 0; i < pix.size(); i++) {
-                const uint32_t x = pix[i] % (uint32_t)W, y = pix[i] / (uint32_t)W;
+        // bucket a level's records by the slice of their pixel (stable; the
+        // camera ray's slice at every depth, :550-560) into wave work items
+        auto bucket = [&](std::vector<uint32_t>* order, const std::vector<uint32_t>& recpix, uint32_t base) {
+            std::vector<uint32_t> sl(recpix.size());
+            for (size_t i = 0; i < recpix.size(); i++) {
+                const uint32_t x = recpix[i] % (uint32_t)W, y = recpix[i] / (uint32_t)W;
                 sl[i] = pixel_to_slice[y + (uint32_t)H * x];   // m_slices[y + H*x] (:560)
             }
-            std::vector<uint32_t> perm(pix.size());
-            for (size_t i = 0; i < perm.size(); i++) perm[i] = (uint32_t)i;
-            std::stable_sort(perm.begin(), perm.end(), [&](uint32_t a, uint32_t b) { return sl[a] < sl[b]; });
-            std::vector<uint32_t> p2(pix.size()), s2(pix.size());
-            for (size_t i = 0; i < perm.size(); i++) { p2[i] = pix[perm[i]]; s2[i] = sl[perm[i]]; }
+            order->resize(recpix.size());
+            for (size_t i = 0; i < order->size(); i++) (*order)[i] = (uint32_t)i;
+            std::stable_sort(order->begin(), order->end(), [&](uint32_t a, uint32_t b) { return sl[a] < sl[b]; });
+            std::vector<uint32_t> s2(sl.size());
+            for (size_t i = 0; i < s2.size(); i++) s2[i] = sl[(*order)[i]];
+            std::vector<alvrl_work_item> it(s2.size() + 1);
+            const uint32_t n = alvrl_make_work_items(s2.data(), (uint32_t)s2.size(), it.data(), (uint32_t)it.size());
+            for (uint32_t k = 0; k < n; k++) { it[k].begin += base; items.push_back(it[k]); }
+        };
+        if (clustered) {
+            std::vector<uint32_t> order;
+            bucket(&order, pix, 0);
+            std::vector<uint32_t> p2(pix.size());
+            for (size_t i = 0; i < order.size(); i++) p2[i] = pix[order[i]];
             pix.swap(p2);
-            items.resize(pix.size() + 1);
-            const uint32_t n = alvrl_make_work_items(s2.data(), (uint32_t)s2.size(), items.data(), (uint32_t)items.size());
-            items.resize(n);
         }
         const bool scat = !(scene.medium.sigma_s[0] == 0 && scene.medium.sigma_s[1] == 0 && scene.medium.sigma_s[2] == 0);
+        const uint32_t nprim = (uint32_t)pix.size();
+        level_rec.assign({0u, nprim});
+        level_item.assign({0u, (uint32_t)items.size()});
+        std::vector<alvrl_gather_rec> extra;   // the chains' records, level by level
+        std::vector<alvrl_gather_rec> prim;
+        if (chains) {
+            Chains ch = expand_chains(pix, scat, false, &prim);
+            for (size_t d = 0; d < ch.recs.size(); d++) {
+                std::vector<uint32_t> recpix(ch.src[d].size());
+                for (size_t j = 0; j < recpix.size(); j++) recpix[j] = pix[ch.src[d][j]];
+                const uint32_t base = nprim + (uint32_t)extra.size();
+                std::vector<uint32_t> order(recpix.size());
+                for (size_t j = 0; j < order.size(); j++) order[j] = (uint32_t)j;
+                if (clustered) bucket(&order, recpix, base);
+                for (uint32_t j : order) { extra.push_back(ch.recs[d][j]); pix.push_back(recpix[j]); }
+                level_rec.push_back(nprim + (uint32_t)extra.size());
+                level_item.push_back((uint32_t)items.size());
+            }
+        }
         nrec = (uint32_t)pix.size();
         nitems = (uint32_t)items.size();
         rec_buf.ensure(nrec);
@@ -657,13 +799,21 @@ struct alvrl_integrator {
         out_buf.ensure((size_t)3 * nrec);
         hchk(hipMemcpyAsync(pix_buf.p, pix.data(), sizeof(uint32_t) * nrec, hipMemcpyHostToDevice, stream), "copy pixels");
         // the eye-ray first hits of the owned pixels, on the device
-        chk_host(alvrl_scene_records_gpu(&scene_desc, scat ? 1 : 0, pix_buf.p, nrec, rec_buf.p, stream));
+        if (chains) {
+            if (nprim)
+                hchk(hipMemcpyAsync(rec_buf.p, prim.data(), sizeof(alvrl_gather_rec) * nprim, hipMemcpyHostToDevice,
+                                    stream), "copy records");
+        } else
+            chk_host(alvrl_scene_records_gpu(&scene_desc, scat ? 1 : 0, pix_buf.p, nprim, rec_buf.p, stream));
+        if (!extra.empty())
+            hchk(hipMemcpyAsync(rec_buf.p + nprim, extra.data(), sizeof(alvrl_gather_rec) * extra.size(),
+                                hipMemcpyHostToDevice, stream), "copy chain records");
         if (nitems) {
             item_buf.ensure(nitems);
             hchk(hipMemcpyAsync(item_buf.p, items.data(), sizeof(alvrl_work_item) * nitems, hipMemcpyHostToDevice, stream), "copy items");
         }
         hchk(hipStreamSynchronize(stream), "sync");
-        cache_rank = rank; cache_world = world; cache_mode = mode;
+        cache_rank = rank; cache_world = world; cache_mode = mode; cache_pass = cur_pass;
     }
 
     void render(uint32_t rank, uint32_t world, float* d_fb, hipStream_t s)
@@ -676,17 +826,28 @@ struct alvrl_integrator {
         // wins over slicesFalseColor; convergenceFalseColor only rewrites the
         // result after a specular (delta-BSDF) chain (:514-521), which the
         // smoke box's diffuse walls never start, so it leaves the image as is
+        // With delta-BSDF chains every level's records are gathered in the same
+        // launch (their path weights applied in the kernels) and the levels
+        // are added into the frame in depth order, one launch each, so that
+        // no two additions to a pixel race.  slicesFalseColor stops at the
+        // first hit (:461-462); numVrlFalseColor keeps weight 1 down the
+        // chain (:502-503), which the false-colour kernel never applies.
+        uint32_t levels = (uint32_t)level_rec.size() - 1;
         if (numVrlFalseColor || slicesFalseColor) {
             if (!clustered && !numVrlFalseColor)
                 throw IntegError(ALVRL_ERR_INVALID, "requested slices false color image without clustering!");
             const int mode = numVrlFalseColor ? ALVRL_FALSE_COLOR_NUM_VRLS : ALVRL_FALSE_COLOR_SLICES;
+            if (!numVrlFalseColor) levels = 1;
             chk(alvrl_gather_false_color(ctx, mode, rec_buf.p, clustered ? item_buf.p : nullptr,
-                                         clustered ? nitems : nrec, out_buf.p, s), "alvrl_gather_false_color");
+                                         clustered ? level_item[levels] : level_rec[levels], out_buf.p, s),
+                "alvrl_gather_false_color");
         } else if (clustered)
             chk(alvrl_gather_clustered(ctx, rec_buf.p, pix_buf.p, item_buf.p, nitems, out_buf.p, s), "alvrl_gather_clustered");
         else
             chk(alvrl_gather_brute(ctx, rec_buf.p, pix_buf.p, nrec, out_buf.p, s), "alvrl_gather_brute");
-        chk(alvrl_accumulate_rgb(ctx, out_buf.p, pix_buf.p, nrec, d_fb, s), "alvrl_accumulate_rgb");
+        for (uint32_t d = 0; d < levels; d++)
+            chk(alvrl_accumulate_rgb(ctx, out_buf.p + (size_t)3 * level_rec[d], pix_buf.p + level_rec[d],
+                                     level_rec[d + 1] - level_rec[d], d_fb, s), "alvrl_accumulate_rgb");
     }
 };
 

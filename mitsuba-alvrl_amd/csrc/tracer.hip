@@ -27,6 +27,7 @@ namespace alvrl {
 namespace host {
 extern thread_local std::string g_host_err;
 SmokeBox to_box(const alvrl_scene_desc& s);   // host_capi.cpp
+const char* scene_problem(const alvrl_scene_desc& s);
 }
 }  // namespace alvrl
 
@@ -350,7 +351,12 @@ struct DevBvh {
     {
         const uint32_t nt = (uint32_t)(occ.size() / 9);
         if (nt == 0) return hipSuccess;
-        const alvrl::BvhHost b = alvrl::build_bvh(occ.data(), nt);
+        alvrl::BvhHost b;
+        try {
+            b = alvrl::build_bvh(occ.data(), nt);
+        } catch (const std::exception&) {
+            return hipErrorInvalidValue;   // deeper than the traversal stacks hold
+        }
         hipError_t e = nodes.alloc(b.nodes.size());
         if (e == hipSuccess) e = tris.alloc(b.tris.size());
         if (e == hipSuccess) e = ids.alloc(b.ids.size());
@@ -698,7 +704,10 @@ ALVRL_API int alvrl_volpath_render(const alvrl_scene_desc* s, const alvrl_volpat
     if (spp == 0) return terr(ALVRL_ERR_INVALID, "alvrl_volpath_render: spp must be > 0");
     if (s->medium.phase_type != 0)
         return terr(ALVRL_ERR_INVALID, "alvrl_volpath_render: only the isotropic phase function is supported");
+    if (const char* m = alvrl::host::scene_problem(*s)) return terr(ALVRL_ERR_INVALID, m);
     const alvrl::host::SmokeBox box = alvrl::host::to_box(*s);
+    if (box.has_delta())
+        return terr(ALVRL_ERR_INVALID, "alvrl_volpath_render: mirror / null occluders are not supported by the volpath reference");
     const uint64_t npix = (uint64_t)box.width * (uint64_t)box.height;
     if (!d_pixel_ids && n > npix) return terr(ALVRL_ERR_INVALID, "alvrl_volpath_render: n > W*H without pixel ids");
     if (n == 0) return ALVRL_OK;
@@ -727,7 +736,11 @@ ALVRL_API int alvrl_scene_records_gpu(const alvrl_scene_desc* s, int medium_scat
                                       uint32_t n, alvrl_gather_rec* d_out, void* stream)
 {
     if (!s || (!d_out && n)) return terr(ALVRL_ERR_INVALID, "alvrl_scene_records_gpu: null argument");
+    if (const char* m = alvrl::host::scene_problem(*s)) return terr(ALVRL_ERR_INVALID, m);
     const alvrl::host::SmokeBox box = alvrl::host::to_box(*s);
+    if (box.has_delta())
+        return terr(ALVRL_ERR_INVALID, "alvrl_scene_records_gpu: mirror / null occluders: the eye paths are formed "
+                                       "on the host (alvrl_scene_records, the integrator's chain records)");
     const uint64_t npix = (uint64_t)box.width * (uint64_t)box.height;
     if (!d_pixel_ids && n > npix) return terr(ALVRL_ERR_INVALID, "alvrl_scene_records_gpu: n > W*H without pixel ids");
     if (n == 0) return ALVRL_OK;
@@ -753,7 +766,10 @@ ALVRL_API int alvrl_trace_vrls_gpu(const alvrl_scene_desc* s, uint32_t seed, uin
 {
     if (!s || !n || !particles) return terr(ALVRL_ERR_INVALID, "alvrl_trace_vrls_gpu: null argument");
     // the scene as the host tracer resolves it (to_box + MediumParams::resolve)
+    if (const char* m = alvrl::host::scene_problem(*s)) return terr(ALVRL_ERR_INVALID, m);
     const alvrl::host::SmokeBox box = alvrl::host::to_box(*s);
+    if (box.has_delta())
+        return terr(ALVRL_ERR_INVALID, "alvrl_trace_vrls_gpu: mirror / null occluders are traced on the host (alvrl_trace_vrls)");
     TScene sc = make_tscene(box);
     DevBvh bvh;
     if (bvh.upload(box.occ) != hipSuccess) return terr(ALVRL_ERR_HIP, "alvrl_trace_vrls_gpu: BVH upload");

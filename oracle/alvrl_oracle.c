@@ -200,7 +200,7 @@ static int tri_intersect(const float *tri, v3 o, v3 d, float *u, float *v, float
  * (scene.cpp:619-679): the segment's ray has mint = Epsilon (1e-4) from a
  * surface, 0 from a medium point; any triangle hit in [mint, remaining]
  * blocks.  The box walls cannot (both points are inside). */
-static int segment_visible(const float *occ, uint32_t nocc, v3 p1, int p1_surface, v3 p2)
+static int segment_visible(const float *occ, const uint32_t *mat, uint32_t nocc, v3 p1, int p1_surface, v3 p2)
 {
     if (!nocc) return 1;
     v3 d = sub(p2, p1);
@@ -210,6 +210,7 @@ static int segment_visible(const float *occ, uint32_t nocc, v3 p1, int p1_surfac
     float mint = p1_surface ? 1e-4f : 0.0f;
     float maxt = remaining * 1.0f;
     for (uint32_t i = 0; i < nocc; i++) {
+        if (mat && mat[i] == ALVRL_O_MAT_NULL) continue;   /* ENull: passes (scene.cpp:636-637) */
         float u, v, t;
         if (tri_intersect(occ + 9 * (size_t)i, p1, d, &u, &v, &t) && !(t < mint || t > maxt)) return 0;
     }
@@ -224,7 +225,7 @@ static void shadow_transmittance(const alvrl_o_params *P, v3 p1, int p1_surface,
     float negLength = 0.0f - remaining;
     for (int i = 0; i < 3; i++)
         tr[i] = m->sigma_t[i] != 0 ? fastexp(m->sigma_t[i] * negLength) : 1.0f;
-    if (!segment_visible(P->occ, P->nocc, p1, p1_surface, p2)) tr[0] = tr[1] = tr[2] = 0.0f;
+    if (!segment_visible(P->occ, P->occ_mat, P->nocc, p1, p1_surface, p2)) tr[0] = tr[1] = tr[2] = 0.0f;
 }
 
 /* isotropic.cpp:76-78, hg.cpp:107-110 */
@@ -784,9 +785,11 @@ void alvrl_o_make_record(const alvrl_o_scene *s, int medium_scatters, int x, int
     v3 O = ld3(o), D = ld3(d), n, p;
     int tri;
     float t = first_hit(s, O, D, camera_mint(s, (float)x + 0.5f, (float)y + 0.5f), &n, &p, &tri);
-    const float *alb = tri >= 0 ? s->occ_albedo : s->albedo;
+    static const float zero3[3] = { 0.0f, 0.0f, 0.0f };
+    uint32_t mt = (tri >= 0 && s->occ_mat) ? s->occ_mat[tri] : ALVRL_O_MAT_DIFFUSE;
+    const float *alb = mt != ALVRL_O_MAT_DIFFUSE ? zero3 : (tri >= 0 ? s->occ_albedo : s->albedo);
     uint32_t flags = 0;
-    if (isfinite(t)) flags |= ALVRL_O_FLAG_HIT | ALVRL_O_FLAG_SMOOTH;
+    if (isfinite(t)) flags |= ALVRL_O_FLAG_HIT | (mt == ALVRL_O_MAT_DIFFUSE ? ALVRL_O_FLAG_SMOOTH : ALVRL_O_FLAG_DELTA);
     if (medium_scatters) flags |= ALVRL_O_FLAG_MEDIUM;
     rec[0] = O.x; rec[1] = O.y; rec[2] = O.z;
     rec[3] = D.x; rec[4] = D.y; rec[5] = D.z;
@@ -797,6 +800,116 @@ void alvrl_o_make_record(const alvrl_o_scene *s, int medium_scatters, int x, int
     rec[16] = rec[17] = rec[18] = 1.0f;   /* the camera ray: weight 1, depth 0 */
     uint32_t depth = 0;
     memcpy(&rec[19], &depth, 4);
+}
+
+static uint32_t mat_of(const alvrl_o_scene *s, int tri)
+{
+    return (tri >= 0 && s->occ_mat) ? s->occ_mat[tri] : ALVRL_O_MAT_DIFFUSE;
+}
+
+static void frame_of(v3 a, v3 *b, v3 *c);
+
+void alvrl_o_make_slice_record(const alvrl_o_scene *s, int x, int y, float *rec)
+{
+    float o[3], d[3];
+    alvrl_o_camera_ray(s, (float)x + 0.5f, (float)y + 0.5f, o, d);
+    v3 O = ld3(o), D = ld3(d), n, p;
+    int tri;
+    float t = first_hit(s, O, D, camera_mint(s, (float)x + 0.5f, (float)y + 0.5f), &n, &p, &tri);
+    uint32_t flags = 0;
+    v3 gp = p, gn = n;
+    if (isfinite(t)) {
+        flags = ALVRL_O_FLAG_HIT;
+        for (;;) {   /* Preprocessor.cpp:1157-1169: keep going through null surfaces */
+            gp = p; gn = n;
+            if (mat_of(s, tri) != ALVRL_O_MAT_NULL) break;
+            t = first_hit(s, O, D, t + 1e-4f, &n, &p, &tri);   /* Ray(ray, its.t + Epsilon, ray.maxt) */
+            if (!isfinite(t)) break;
+        }
+    }
+    for (int k = 0; k < ALVRL_O_REC_WORDS; k++) rec[k] = 0.0f;
+    rec[0] = O.x; rec[1] = O.y; rec[2] = O.z;
+    rec[3] = D.x; rec[4] = D.y; rec[5] = D.z;
+    rec[6] = gp.x; rec[7] = gp.y; rec[8] = gp.z;
+    rec[9] = gn.x; rec[10] = gn.y; rec[11] = gn.z;
+    memcpy(&rec[15], &flags, 4);
+    rec[16] = rec[17] = rec[18] = 1.0f;
+}
+
+uint32_t alvrl_o_make_chain(const alvrl_o_scene *s, const alvrl_o_medium *m, int medium_scatters, int x, int y,
+                            uint32_t seed, uint32_t pass, int spec_rr_depth, float init_throughput,
+                            float *recs, uint32_t cap)
+{
+    float o[3], d[3];
+    alvrl_o_camera_ray(s, (float)x + 0.5f, (float)y + 0.5f, o, d);   /* pixel centre (integrator.cpp:243-245) */
+    v3 O = ld3(o), D = ld3(d);
+    float mint = camera_mint(s, (float)x + 0.5f, (float)y + 0.5f);
+    uint32_t pixel = (uint32_t)y * (uint32_t)s->width + (uint32_t)x;
+    float weight[3] = { 1.0f, 1.0f, 1.0f };
+    float thr[3] = { init_throughput, init_throughput, init_throughput };   /* throughputWithEtaSq */
+    int depth = 1;                                                          /* rRec.depth of a sensor ray */
+    uint32_t nrec = 0;
+    for (uint32_t k = 0; k < 256 && nrec < cap; k++) {
+        v3 n, p;
+        int tri;
+        float t = first_hit(s, O, D, mint, &n, &p, &tri);
+        if (!isfinite(t)) break;                                            /* :414-419 */
+        uint32_t mt = mat_of(s, tri);
+        uint32_t flags = ALVRL_O_FLAG_HIT | (mt == ALVRL_O_MAT_DIFFUSE ? ALVRL_O_FLAG_SMOOTH : ALVRL_O_FLAG_DELTA) |
+                         (medium_scatters ? ALVRL_O_FLAG_MEDIUM : 0u);
+        const float *alb = tri >= 0 ? s->occ_albedo : s->albedo;
+        float *rec = recs + (size_t)nrec * ALVRL_O_REC_WORDS;
+        rec[0] = O.x; rec[1] = O.y; rec[2] = O.z;
+        rec[3] = D.x; rec[4] = D.y; rec[5] = D.z;
+        rec[6] = p.x; rec[7] = p.y; rec[8] = p.z;
+        rec[9] = n.x; rec[10] = n.y; rec[11] = n.z;
+        for (int i = 0; i < 3; i++) rec[12 + i] = mt == ALVRL_O_MAT_DIFFUSE ? alb[i] : 0.0f;
+        memcpy(&rec[15], &flags, 4);
+        for (int i = 0; i < 3; i++) rec[16 + i] = weight[i];
+        memcpy(&rec[19], &k, 4);
+        nrec++;
+        if (mt == ALVRL_O_MAT_DIFFUSE) break;                               /* no delta component (:449-450) */
+        /* rRec.medium->eval(Ray(ray, 0, its.t)) (:452-458) */
+        float tr[3];
+        for (int i = 0; i < 3; i++) tr[i] = fastexp(m->sigma_t[i] * (-t));
+        {
+            float mx = tr[0] > tr[1] ? tr[0] : tr[1];
+            mx = mx > tr[2] ? mx : tr[2];
+            if (mx < 1e-20f) tr[0] = tr[1] = tr[2] = 0;
+        }
+        if (tr[0] == 0 && tr[1] == 0 && tr[2] == 0) break;                  /* :459-460 */
+        v3 fs, ft;
+        frame_of(n, &fs, &ft);
+        v3 mwi = neg(D);
+        float cos_wi = dot(mwi, n);
+        float bw[3];
+        v3 wol;
+        if (mt == ALVRL_O_MAT_MIRROR) {                                     /* conductor.cpp:254-268 */
+            if (cos_wi <= 0) break;
+            wol = mk(-dot(mwi, fs), -dot(mwi, ft), cos_wi);
+            for (int i = 0; i < 3; i++) bw[i] = s->occ_spec[i];
+        } else {                                                            /* null.cpp:53-63 */
+            wol = mk(-dot(mwi, fs), -dot(mwi, ft), -cos_wi);
+            bw[0] = bw[1] = bw[2] = 1.0f;
+        }
+        /* Russian roulette (:477-492), eta = 1 */
+        float thr2[3];
+        for (int i = 0; i < 3; i++) thr2[i] = ((thr[i] * tr[i]) * bw[i]) * 1.0f;
+        float maxRR = depth >= spec_rr_depth ? 0.98f : 1.0f;
+        float mx = thr2[0] > thr2[1] ? thr2[0] : thr2[1];
+        mx = mx > thr2[2] ? mx : thr2[2];
+        float rrProb = maxRR < mx ? maxRR : mx;
+        if (rrProb <= 0 || (rrProb < 1 && draw(seed, pass, 7u, pixel, k, 0u, 0u) > rrProb)) break;
+        for (int i = 0; i < 3; i++) {
+            thr[i] = thr2[i] / rrProb;
+            weight[i] = ((weight[i] * tr[i]) * bw[i]) / rrProb;              /* :503-510 */
+        }
+        O = p;
+        D = add(add(scl(fs, wol.x), scl(ft, wol.y)), scl(n, wol.z));        /* its.toWorld(bRec.wo) */
+        mint = 1e-4f;
+        depth++;
+    }
+    return nrec;
 }
 
 void alvrl_o_make_records(const alvrl_o_scene *s, int medium_scatters, float *recs)
@@ -964,9 +1077,20 @@ static void trace_particle(const alvrl_o_scene *s, const alvrl_o_medium *m, seq_
             float bx = seq_next(smp), by = seq_next(smp);
             float bw[3] = { 0, 0, 0 };
             v3 wol = mk(0, 0, 0);
-            if (!(cos_wi <= 0)) {
-                wol = cosine_hemisphere(bx, by);
-                for (int i = 0; i < 3; i++) bw[i] = alb[i];
+            uint32_t mt = mat_of(s, tri);
+            if (mt == ALVRL_O_MAT_DIFFUSE) {          /* SmoothDiffuse::sample */
+                if (!(cos_wi <= 0)) {
+                    wol = cosine_hemisphere(bx, by);
+                    for (int i = 0; i < 3; i++) bw[i] = alb[i];
+                }
+            } else if (mt == ALVRL_O_MAT_MIRROR) {    /* SmoothConductor::sample (conductor.cpp:254-268) */
+                if (!(cos_wi <= 0)) {
+                    wol = mk(-dot(mwi, fs), -dot(mwi, ft), cos_wi);
+                    for (int i = 0; i < 3; i++) bw[i] = s->occ_spec[i];
+                }
+            } else {                                  /* Null::sample (null.cpp:53-63) */
+                wol = mk(-dot(mwi, fs), -dot(mwi, ft), -cos_wi);
+                bw[0] = bw[1] = bw[2] = 1.0f;
             }
             if (bw[0] == 0 && bw[1] == 0 && bw[2] == 0) { end_current(k, p); break; }
             v3 wo = add(add(scl(fs, wol.x), scl(ft, wol.y)), scl(n, wol.z));
@@ -1035,7 +1159,7 @@ static void vp_light_direct(const alvrl_o_scene *s, const alvrl_o_medium *m, v3 
     float negLength = 0.0f - remaining;
     float tr[3];
     for (int i = 0; i < 3; i++) tr[i] = m->sigma_t[i] != 0 ? fastexp(m->sigma_t[i] * negLength) : 1.0f;
-    if (!segment_visible(s->occ, s->nocc, ref, on_surface, L)) tr[0] = tr[1] = tr[2] = 0.0f;
+    if (!segment_visible(s->occ, s->occ_mat, s->nocc, ref, on_surface, L)) tr[0] = tr[1] = tr[2] = 0.0f;
     for (int i = 0; i < 3; i++) {
         val[i] = s->light_intensity[i] * (invDist * invDist);
         val[i] *= tr[i] * 1.0f;

@@ -83,6 +83,7 @@ typedef struct {
     int r_samples;           /* Rsamples (vrlIntegrator.cpp:194): samples per R entry, 0/1 = one */
     const float *occ;        /* occluder triangles (9 floats each) blocking U-V / surface-V, or NULL */
     uint32_t nocc;
+    const uint32_t *occ_mat; /* their ALVRL_O_MAT_* (NULL: all diffuse); null ones let the segment pass */
 } alvrl_o_params;
 
 /* Gather record ("eye segment"): 20 x 32-bit words.
@@ -132,7 +133,24 @@ typedef struct {
     const float *occ;        /* occluder triangles inside the box (9 floats: p0 p1 p2), or NULL */
     uint32_t nocc;
     float occ_albedo[3];     /* their one-sided diffuse reflectance */
+    const uint32_t *occ_mat; /* per triangle ALVRL_O_MAT_* (NULL: all diffuse) */
+    float occ_spec[3];       /* the mirrors' specular reflectance */
 } alvrl_o_scene;
+#define ALVRL_O_MAT_DIFFUSE 0u   /* SmoothDiffuse, one-sided (diffuse.cpp) */
+#define ALVRL_O_MAT_MIRROR 1u    /* SmoothConductor, material none (conductor.cpp:254-268) */
+#define ALVRL_O_MAT_NULL 2u      /* index-matched null BSDF (null.cpp:38-76) */
+/* LiInternal's eye path of pixel centre (x, y) through delta BSDFs
+ * (vrlIntegrator.cpp:386-524): one gather record per segment with the path
+ * weight of :503-510 and its depth; Russian roulette from init_throughput,
+ * maxRR 0.98 from rRec.depth spec_rr_depth on (:475-492), its uniform from
+ * stream (seed, pass, dom 7, pixel, segment).  Writes at most cap records;
+ * returns the count. */
+uint32_t alvrl_o_make_chain(const alvrl_o_scene *s, const alvrl_o_medium *m, int medium_scatters, int x, int y,
+                            uint32_t seed, uint32_t pass, int spec_rr_depth, float init_throughput,
+                            float *recs, uint32_t cap);
+/* buildSlices' gather point of pixel (x, y): the first hit continued through
+ * null surfaces (Preprocessor.cpp:1144-1170), as a record (flags: hit). */
+void alvrl_o_make_slice_record(const alvrl_o_scene *s, int x, int y, float *rec);
 /* Scene::rayIntersect over walls + occluders (t >= mint; walls win ties, then
  * the lowest triangle index): t (INFINITY: none), normal, its.p, triangle (-1
  * = wall). */

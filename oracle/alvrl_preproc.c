@@ -1253,7 +1253,7 @@ int alvrl_o_prep_build_slices(alvrl_o_prep *P, const alvrl_o_scene *s, uint32_t 
     for (int i = 0; i < W; i++) {
         for (int j = 0; j < H; j++) {
             float rec[ALVRL_O_REC_WORDS];
-            alvrl_o_make_record(s, 1, i, j, rec);
+            alvrl_o_make_slice_record(s, i, j, rec);   /* through null surfaces (:1157-1169) */
             uint32_t flags;
             memcpy(&flags, &rec[15], 4);
             uint32_t k = (uint32_t)i * H + j;

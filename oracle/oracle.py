@@ -36,7 +36,8 @@ class Medium(C.Structure):
 class Params(C.Structure):
     _fields_ = [("medium", Medium), ("vol_vol_samples", C.c_int), ("vol_surf_samples", C.c_int),
                 ("short_vrls", C.c_int), ("seed", C.c_uint32), ("pass_", C.c_uint32),
-                ("r_samples", C.c_int), ("occ", C.POINTER(C.c_float)), ("nocc", C.c_uint32)]
+                ("r_samples", C.c_int), ("occ", C.POINTER(C.c_float)), ("nocc", C.c_uint32),
+                ("occ_mat", C.POINTER(C.c_uint32))]
 
 
 class Scene(C.Structure):
@@ -44,13 +45,18 @@ class Scene(C.Structure):
                 ("fov_x_deg", C.c_float), ("width", C.c_int), ("height", C.c_int),
                 ("box_min", C.c_float * 3), ("box_max", C.c_float * 3), ("albedo", C.c_float * 3),
                 ("light_pos", C.c_float * 3), ("light_intensity", C.c_float * 3),
-                ("occ", C.POINTER(C.c_float)), ("nocc", C.c_uint32), ("occ_albedo", C.c_float * 3)]
+                ("occ", C.POINTER(C.c_float)), ("nocc", C.c_uint32), ("occ_albedo", C.c_float * 3),
+                ("occ_mat", C.POINTER(C.c_uint32)), ("occ_spec", C.c_float * 3)]
 
 
-def set_occluders(obj, tris, albedo=None):
+MAT_DIFFUSE, MAT_MIRROR, MAT_NULL = 0, 1, 2
+
+
+def set_occluders(obj, tris, albedo=None, material=None, specular=None):
     """Occluder triangles ((n, 9) float32) on a Scene (hit by eye rays and
-    particles, occ_albedo) or a Params (blocking the gather's connections).
-    The array is kept alive on the object."""
+    particles, occ_albedo) or a Params (blocking the gather's connections);
+    material: None (all diffuse) or one MAT_* per triangle; specular: the
+    mirrors' reflectance (Scene).  The arrays are kept alive on the object."""
     arr = np.ascontiguousarray(np.asarray(tris, np.float32).reshape(-1, 9))
     obj._occ_keep = arr
     obj.occ = arr.ctypes.data_as(C.POINTER(C.c_float)) if len(arr) else None
@@ -58,6 +64,13 @@ def set_occluders(obj, tris, albedo=None):
     if albedo is not None:
         for i in range(3):
             obj.occ_albedo[i] = float(albedo[i])
+    if material is not None:
+        mat = np.ascontiguousarray(np.broadcast_to(np.asarray(material, np.uint32), (len(arr),)))
+        obj._mat_keep = mat
+        obj.occ_mat = mat.ctypes.data_as(C.POINTER(C.c_uint32))
+    if specular is not None:
+        for i in range(3):
+            obj.occ_spec[i] = float(specular[i])
     return obj
 
 
@@ -106,6 +119,9 @@ class Oracle:
         L.alvrl_o_camera_ray.argtypes = [P(Scene), f32, f32, P(f32), P(f32)]
         L.alvrl_o_make_records.argtypes = [P(Scene), i32, P(f32)]
         L.alvrl_o_make_record.argtypes = [P(Scene), i32, i32, i32, P(f32)]
+        L.alvrl_o_make_slice_record.argtypes = [P(Scene), i32, i32, P(f32)]
+        L.alvrl_o_make_chain.argtypes = [P(Scene), P(Medium), i32, i32, i32, u32, u32, i32, f32, P(f32), u32]
+        L.alvrl_o_make_chain.restype = u32
         L.alvrl_o_trace_vrls.argtypes = [P(Scene), P(Medium), u32, u32, u32, i32, i32, i32,
                                          P(f32), u32, P(u64)]
         L.alvrl_o_trace_vrls.restype = u32
@@ -181,6 +197,28 @@ class Oracle:
     def record(self, scene: Scene, x: int, y: int, medium_scatters: bool = True) -> np.ndarray:
         out = np.zeros(REC_WORDS, np.float32)
         self.lib.alvrl_o_make_record(C.byref(scene), int(medium_scatters), x, y, _p(out))
+        return out
+
+    def chain(self, scene: Scene, medium: Medium, x: int, y: int, medium_scatters: bool = True,
+              seed=0xA1B2C3D4, pass_=0, spec_rr_depth=100, init_throughput=20.0, cap=256) -> np.ndarray:
+        """LiInternal's eye path of pixel (x, y): (k, REC_WORDS) records."""
+        out = np.zeros((cap, REC_WORDS), np.float32)
+        n = self.lib.alvrl_o_make_chain(C.byref(scene), C.byref(medium), int(medium_scatters), x, y, seed,
+                                        pass_, spec_rr_depth, init_throughput, _p(out), cap)
+        return out[:n].copy()
+
+    def chains(self, scene: Scene, medium: Medium, pixel_ids, **kw):
+        """Eye paths of row-major pixel ids: (records, pixel of each record)."""
+        recs, pix = [], []
+        for p in np.asarray(pixel_ids, np.uint32):
+            c = self.chain(scene, medium, int(p % scene.width), int(p // scene.width), **kw)
+            recs.append(c)
+            pix.append(np.full(len(c), p, np.uint32))
+        return np.concatenate(recs), np.concatenate(pix)
+
+    def slice_record(self, scene: Scene, x: int, y: int) -> np.ndarray:
+        out = np.zeros(REC_WORDS, np.float32)
+        self.lib.alvrl_o_make_slice_record(C.byref(scene), x, y, _p(out))
         return out
 
     def volpath(self, scene: Scene, medium: Medium, spp: int, seed=0xA1B2C3D4, pass_=0, pixel_ids=None,
