@@ -61,14 +61,25 @@ typedef struct {
 } alvrl_config;
 
 /* Homogeneous medium + phase function of the (single) medium the VRLs live in.
- * Replaces HomogeneousMedium(const Properties&) (src/medium/homogeneous.cpp:156-219),
- * 'balance' strategy, and IsotropicPhaseFunction / HGPhaseFunction eval. */
+ * Replaces HomogeneousMedium(const Properties&) (src/medium/homogeneous.cpp:156-227)
+ * with its distance-sampling "strategy" -- which sets the tracer's distances
+ * and pdfs (sampleDistance, :275-352) and the pdfFailure the gather divides
+ * by (eval, :354-396) -- and IsotropicPhaseFunction / HGPhaseFunction eval.
+ * A zero-filled tail (strategy, channel, sampling_density) is the default
+ * 'balance' strategy. */
+#define ALVRL_STRATEGY_BALANCE 0  /* a random channel's sigma_t per sample */
+#define ALVRL_STRATEGY_SINGLE 1   /* one channel's sigma_t (:188-214) */
+#define ALVRL_STRATEGY_MANUAL 2   /* "samplingDensity" (:221-223) */
+#define ALVRL_STRATEGY_MAXIMUM 3  /* MaxExpDist over sigma_t (maxexp.h:28-94); channels must differ */
 typedef struct {
     float sigma_s[3];
     float sigma_a[3];
     float sampling_weight;  /* "mediumSamplingWeight"; -1 = auto (max albedo, >= 0.5) */
     int phase_type;         /* 0 = isotropic (isotropic.cpp:76-78), 1 = HG (hg.cpp:107-110) */
     float phase_g;
+    int strategy;           /* ALVRL_STRATEGY_* */
+    int channel;            /* 'single': 1 + "channel" (0: the smallest sigma_t, :191-202) */
+    float sampling_density; /* 'manual': "samplingDensity" */
 } alvrl_medium_desc;
 
 /* One eye segment ("gather record"), 80 B.  What LiInternal knows at the point

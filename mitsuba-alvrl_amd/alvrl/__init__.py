@@ -49,7 +49,12 @@ class Config(C.Structure):
 
 class MediumDesc(C.Structure):
     _fields_ = [("sigma_s", C.c_float * 3), ("sigma_a", C.c_float * 3),
-                ("sampling_weight", C.c_float), ("phase_type", C.c_int), ("phase_g", C.c_float)]
+                ("sampling_weight", C.c_float), ("phase_type", C.c_int), ("phase_g", C.c_float),
+                ("strategy", C.c_int), ("channel", C.c_int), ("sampling_density", C.c_float)]
+
+
+# HomogeneousMedium "strategy" (alvrl_medium_desc.strategy)
+STRATEGIES = {"balance": 0, "single": 1, "manual": 2, "maximum": 3}
 
 
 class ClusterJob(C.Structure):
@@ -135,6 +140,14 @@ class Medium:
     sampling_weight: float = -1.0
     phase_type: int = 0
     phase_g: float = 0.0
+    strategy: str = "balance"      # "balance" | "single" | "manual" | "maximum"
+    channel: int = -1              # 'single': the channel (-1: the smallest sigma_t)
+    sampling_density: float = 0.0  # 'manual': samplingDensity
+
+    def desc(self) -> "MediumDesc":
+        return MediumDesc((C.c_float * 3)(*self.sigma_s), (C.c_float * 3)(*self.sigma_a),
+                          self.sampling_weight, self.phase_type, self.phase_g,
+                          STRATEGIES[self.strategy], self.channel + 1, self.sampling_density)
 
 
 class Context:
@@ -165,8 +178,7 @@ class Context:
 
     # ---- state ----
     def set_medium(self, m: Medium):
-        d = MediumDesc((C.c_float * 3)(*m.sigma_s), (C.c_float * 3)(*m.sigma_a),
-                       m.sampling_weight, m.phase_type, m.phase_g)
+        d = m.desc()
         _check(self.L.alvrl_set_medium(self.h, C.byref(d)))
 
     def set_pass(self, p: int):
@@ -668,8 +680,7 @@ def tile_pixels(width: int, height: int, rank: int = 0, world: int = 1) -> np.nd
 
 def read_vrl_file(path: str, medium: Medium = Medium()):
     L = _host()
-    md = MediumDesc((C.c_float * 3)(*medium.sigma_s), (C.c_float * 3)(*medium.sigma_a),
-                    medium.sampling_weight, medium.phase_type, medium.phase_g)
+    md = medium.desc()
     n = C.c_uint32(); pc = C.c_uint64()
     _hcheck(L.alvrl_read_vrl_file(path.encode(), C.byref(md), None, 0, C.byref(n), C.byref(pc)))
     soa = np.zeros((9, max(1, n.value)), np.float32)

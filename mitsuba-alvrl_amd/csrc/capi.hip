@@ -7,6 +7,7 @@
 // every LocalWorker, renderproc.cpp:52-86) only need their own streams.
 #include "../../include/alvrl.h"
 #include "vrl_device.hpp"
+#include "host/scene.hpp"
 
 #include <algorithm>
 #include <cmath>
@@ -20,6 +21,9 @@
 #include <vector>
 
 namespace alvrl {
+namespace host {
+MediumParams medium_of(const alvrl_medium_desc& d);   // host_capi.cpp
+}  // namespace host
 hipError_t launch_prepare_vrls(const float* soa, uint32_t n, VrlPrep* out, hipStream_t s);
 hipError_t launch_gather_brute(const Rec* recs, const uint32_t* ids, uint32_t nrec,
                                const VrlPrep* vp, uint32_t nvrl, const DevParams& P,
@@ -280,20 +284,22 @@ ALVRL_API void alvrl_ctx_destroy(alvrl_ctx* c)
 ALVRL_API int alvrl_set_medium(alvrl_ctx* c, const alvrl_medium_desc* m)
 {
     if (!c || !m) return fail(ALVRL_ERR_INVALID, "alvrl_set_medium: null argument");
-    float w = m->sampling_weight;
-    float st[3];
-    for (int i = 0; i < 3; i++) st[i] = m->sigma_s[i] + m->sigma_a[i];
-    if (w == -1) {   // homogeneous.cpp:168-184
-        for (int i = 0; i < 3; i++) {
-            float albedo = m->sigma_s[i] / st[i];
-            if (albedo > w && st[i] != 0) w = albedo;
-        }
-        if (w > 0) w = std::max(w, 0.5f);
-    }
     if (m->phase_type != 0 && m->phase_type != 1)
         return fail(ALVRL_ERR_INVALID, "alvrl_set_medium: phase_type must be 0 (isotropic) or 1 (hg)");
-    for (int i = 0; i < 3; i++) { c->P.sigma_s[i] = m->sigma_s[i]; c->P.sigma_t[i] = st[i]; }
-    c->P.w = w;
+    // HomogeneousMedium(props): sigma_t, the auto sampling weight
+    // (homogeneous.cpp:168-184) and the strategy's terms, as the host tracer has them
+    alvrl::host::MediumParams mp = alvrl::host::medium_of(*m);
+    if (const char* e = mp.problem()) return fail(ALVRL_ERR_INVALID, std::string("alvrl_set_medium: ") + e);
+    mp.resolve();
+    for (int i = 0; i < 3; i++) { c->P.sigma_s[i] = mp.sigma_s[i]; c->P.sigma_t[i] = mp.sigma_t[i]; }
+    c->P.w = mp.sampling_weight;
+    c->P.strategy = mp.strategy;
+    c->P.density = mp.density;
+    for (int i = 0; i < 3; i++) {
+        c->P.mx_sigma[i] = mp.mx_sigma[i]; c->P.mx_start[i] = mp.mx_start[i]; c->P.mx_lower[i] = mp.mx_lower[i];
+    }
+    for (int i = 0; i < 4; i++) c->P.mx_cdf[i] = mp.mx_cdf[i];
+    c->P.mx_inv_norm = mp.mx_inv_norm;
     c->P.phase_type = m->phase_type;
     c->P.g = m->phase_g;
     c->medium_set = true;

@@ -379,7 +379,7 @@ hipError_t launch_gather_brute(const Rec* recs, const uint32_t* ids, uint32_t nr
     const dim3 grid((nrec + 255) / 256), block(256);
     if (P.occ.ntri)   // occluders: shadow tests (generic sample counts only)
         hipLaunchKernelGGL((k_gather_brute<-1, -1, true>), grid, block, 0, s, recs, ids, nrec, vp, nvrl, P, normalization, out, counter);
-    else if (P.nvv == 2 && P.nvs == 2)
+    else if (P.nvv == 2 && P.nvs == 2 && P.strategy == 0)   // unrolled, 'balance' only
         hipLaunchKernelGGL((k_gather_brute<2, 2>), grid, block, 0, s, recs, ids, nrec, vp, nvrl, P,
                            normalization, out, counter);
     else
@@ -399,7 +399,7 @@ hipError_t launch_gather_clustered(const Rec* recs, const uint32_t* ids, const W
     const dim3 grid((nitems + 3) / 4), block(256);
     if (P.occ.ntri)   // occluders: shadow tests (generic sample counts only)
         hipLaunchKernelGGL((k_gather_clustered<-1, -1, true>), grid, block, 0, s, recs, ids, items, nitems, vp, slice_off, reps, weights, fb_reps, fb_w, n_fb, P, inv_pc, out, counter);
-    else if (P.nvv == 2 && P.nvs == 2)
+    else if (P.nvv == 2 && P.nvs == 2 && P.strategy == 0)   // unrolled, 'balance' only
         hipLaunchKernelGGL((k_gather_clustered<2, 2>), grid, block, 0, s, recs, ids, items, nitems,
                            vp, slice_off, reps, weights, fb_reps, fb_w, n_fb, P, inv_pc, out,
                            counter);
@@ -419,7 +419,7 @@ hipError_t launch_build_R(const Rec* recs, const uint32_t* ids, uint32_t nrows, 
     const dim3 grid((nrows + 63) / 64, (nvrl + chunk - 1) / chunk), block(256);
     if (P.occ.ntri)   // occluders: shadow tests (generic sample counts only)
         hipLaunchKernelGGL((k_build_R<-1, -1, true>), grid, block, 0, s, recs, ids, nrows, vp, nvrl, chunk, P, normalization, Rt, ld, row0, counter);
-    else if (P.nvv == 2 && P.nvs == 2)
+    else if (P.nvv == 2 && P.nvs == 2 && P.strategy == 0)   // unrolled, 'balance' only
         hipLaunchKernelGGL((k_build_R<2, 2>), grid, block, 0, s, recs, ids, nrows, vp, nvrl, chunk,
                            P, normalization, Rt, ld, row0, counter);
     else
@@ -438,7 +438,7 @@ hipError_t launch_build_R_blocks(const Rec* recs, const uint32_t* ids, uint32_t 
     const dim3 grid((nrows + 63) / 64, (nvrl + chunk - 1) / chunk), block(256);
     if (P.occ.ntri)   // occluders: shadow tests (generic sample counts only)
         hipLaunchKernelGGL((k_build_R_blocks<-1, -1, true>), grid, block, 0, s, recs, ids, nrows, vp, nvrl, chunk, P, normalization, Rt, roff, rstride, nonzero, counter);
-    else if (P.nvv == 2 && P.nvs == 2)
+    else if (P.nvv == 2 && P.nvs == 2 && P.strategy == 0)   // unrolled, 'balance' only
         hipLaunchKernelGGL((k_build_R_blocks<2, 2>), grid, block, 0, s, recs, ids, nrows, vp, nvrl, chunk,
                            P, normalization, Rt, roff, rstride, nonzero, counter);
     else

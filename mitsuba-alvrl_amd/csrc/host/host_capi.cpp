@@ -14,10 +14,24 @@ using namespace alvrl::host;
 namespace alvrl {
 namespace host {
 thread_local std::string g_host_err;
+// HomogeneousMedium(props) of a descriptor, unresolved (MediumParams::problem, resolve)
+MediumParams medium_of(const alvrl_medium_desc& d)
+{
+    MediumParams m;
+    for (int i = 0; i < 3; i++) { m.sigma_s[i] = d.sigma_s[i]; m.sigma_a[i] = d.sigma_a[i]; }
+    m.sampling_weight = d.sampling_weight;
+    m.phase_type = d.phase_type;
+    m.phase_g = d.phase_g;
+    m.strategy = d.strategy;
+    m.channel = d.channel;
+    m.density = d.sampling_density;
+    return m;
+}
 // what is wrong with a scene descriptor, or nullptr
 const char* scene_problem(const alvrl_scene_desc& s)
 {
     if (s.width <= 0 || s.height <= 0) return "alvrl_scene_desc: width and height must be > 0";
+    if (const char* m = medium_of(s.medium).problem()) return m;
     if (s.n_occluders && !s.occluders) return "alvrl_scene_desc: n_occluders > 0 without occluders";
     if (s.occluders && s.occluder_material)
         for (uint32_t i = 0; i < s.n_occluders; i++)
@@ -35,12 +49,9 @@ SmokeBox to_box(const alvrl_scene_desc& s)
     for (int i = 0; i < 3; i++) {
         b.box_min[i] = s.box_min[i]; b.box_max[i] = s.box_max[i];
         b.albedo[i] = s.albedo[i]; b.light_intensity[i] = s.light_intensity[i];
-        b.medium.sigma_s[i] = s.medium.sigma_s[i]; b.medium.sigma_a[i] = s.medium.sigma_a[i];
     }
     b.light_pos = v3(s.light_pos[0], s.light_pos[1], s.light_pos[2]);
-    b.medium.sampling_weight = s.medium.sampling_weight;
-    b.medium.phase_type = s.medium.phase_type;
-    b.medium.phase_g = s.medium.phase_g;
+    b.medium = medium_of(s.medium);
     b.medium.resolve();
     if (s.occluders && s.n_occluders) b.occ.assign(s.occluders, s.occluders + 9 * (size_t)s.n_occluders);
     for (int i = 0; i < 3; i++) b.occ_albedo[i] = s.occluder_albedo[i];

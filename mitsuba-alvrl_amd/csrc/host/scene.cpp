@@ -3,6 +3,7 @@
 // oracle's restatement, so records and VRL sets agree bit for bit with it.
 #include "scene.hpp"
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -40,6 +41,94 @@ void MediumParams::resolve()
         if (w > 0) w = w > 0.5f ? w : 0.5f;
     }
     sampling_weight = w;
+    density = strategy == 2 ? density : 0.0f;
+    if (strategy == 1) {   // homogeneous.cpp:188-204
+        int ch = channel - 1;
+        if (ch < 0) {
+            float smallest = INFINITY;
+            ch = 0;
+            for (int i = 0; i < 3; i++)
+                if (sigma_t[i] < smallest) { smallest = sigma_t[i]; ch = i; }
+        }
+        density = sigma_t[ch];
+    } else if (strategy == 3) {   // MaxExpDist(sigmaT), maxexp.h:30-57
+        float s[3] = {sigma_t[0], sigma_t[1], sigma_t[2]};
+        std::sort(s, s + 3, [](float a, float b) { return a > b; });
+        float cdf[4];
+        cdf[0] = 0;
+        for (int i = 0; i < 3; i++) {
+            const float lower = (i == 0) ? -1 : -std::pow(s[i] / s[i - 1], -s[i] / (s[i] - s[i - 1]));
+            const float upper = (i == 2) ? 0 : -std::pow(s[i + 1] / s[i], -s[i] / (s[i + 1] - s[i]));
+            cdf[i + 1] = cdf[i] + (upper - lower);
+            mx_start[i] = (i == 0) ? 0 : fastlog(s[i] / s[i - 1]) / (s[i] - s[i - 1]);
+            mx_lower[i] = lower;
+            mx_sigma[i] = s[i];
+        }
+        mx_norm = cdf[3];
+        mx_inv_norm = 1 / mx_norm;
+        for (int i = 0; i < 4; i++) mx_cdf[i] = cdf[i] * mx_inv_norm;
+    }
+}
+
+const char* MediumParams::problem() const
+{
+    if (strategy < 0 || strategy > 3) return "alvrl_medium_desc: unknown sampling strategy";
+    if (strategy == 1 && (channel < 0 || channel > 3)) return "alvrl_medium_desc: 'single' channel out of range";
+    if (strategy == 3) {
+        float s[3];
+        for (int i = 0; i < 3; i++) s[i] = sigma_s[i] + sigma_a[i];
+        if (s[0] == s[1] || s[1] == s[2] || s[0] == s[2])
+            return "alvrl_medium_desc: 'maximum' needs sigma_t to vary across channels (maxexp.h:37-38)";
+    }
+    return nullptr;
+}
+
+namespace {
+// std::max(0, lower_bound(a, a + n, x) - a - 1)
+int interval_of(const float* a, int n, float x)
+{
+    int k = 0;
+    while (k < n && a[k] < x) k++;
+    return k > 0 ? k - 1 : 0;
+}
+}  // namespace
+
+float MediumParams::maxexp_sample(float u, float* pdf) const
+{
+    // the index clamped to the last interval (u = 1 above a rounded m_cdf[n])
+    const int i = std::min(interval_of(mx_cdf, 4, u), 2);
+    const float t = -fastlog(fastexp(-mx_start[i] * mx_sigma[i]) - mx_norm * (u - mx_cdf[i])) / mx_sigma[i];
+    *pdf = mx_sigma[i] * fastexp(-mx_sigma[i] * t) * mx_inv_norm;
+    return t;
+}
+
+float MediumParams::maxexp_cdf(float t) const
+{
+    const int i = interval_of(mx_start, 3, t);
+    const float upper = -fastexp(-mx_sigma[i] * t);
+    return mx_cdf[i] + (upper - mx_lower[i]) * mx_inv_norm;
+}
+
+void MediumParams::pdfs(float sampled, float pdf_max, float* ps, float* pf) const
+{
+    const float w = sampling_weight;
+    float s = 0.0f, f = 0.0f;
+    if (strategy == 3) {
+        f = 1 - maxexp_cdf(sampled);
+        s = pdf_max;
+    } else if (strategy == 0) {
+        for (int i = 0; i < 3; i++) {
+            const float tmp = fastexp(-sigma_t[i] * sampled);
+            f += tmp;
+            s += sigma_t[i] * tmp;
+        }
+        f /= 3; s /= 3;
+    } else {
+        f = fastexp(-density * sampled);
+        s = density * f;
+    }
+    *ps = s * w;
+    *pf = w * f + (1 - w);
 }
 
 void SmokeBox::camera_ray(float px, float py, V3* o, V3* d, float* mint) const
@@ -294,6 +383,24 @@ struct Sink {   // vrlVector::put + the tracer's current VRL (vrlTracer.h:56-89,
     uint32_t size() const { return (uint32_t)s[0].size(); }
 };
 
+// sampleDistance's draws (homogeneous.cpp:277-296): the distance (INFINITY:
+// no medium interaction) and, for 'maximum', the pdf of the sample
+float sample_distance(const MediumParams& m, Stream& smp, float* pdf_max)
+{
+    float rnd = smp.next();
+    const float w = m.sampling_weight;
+    if (!(rnd < w)) return INFINITY;
+    rnd /= w;
+    if (m.strategy == 3) return m.maxexp_sample(1 - rnd, pdf_max);
+    float density = m.density;
+    if (m.strategy == 0) {   // a random channel each time
+        int ch = (int)(smp.next() * 3);
+        if (ch > 2) ch = 2;
+        density = m.sigma_t[ch];
+    }
+    return -fastlog(1 - rnd) / density;
+}
+
 void trace_particle(const SmokeBox& sc, Stream& smp, bool short_vrls, int max_depth, int rr_depth, Sink& k)
 {
     const MediumParams& m = sc.medium;
@@ -309,23 +416,15 @@ void trace_particle(const SmokeBox& sc, Stream& smp, bool short_vrls, int max_de
     int depth = 1;
     float thr[3] = {1.0f, 1.0f, 1.0f};
     const float eta = 1.0f;
-    const float w = m.sampling_weight;
     float mint = 1e-4f;   // Ray() default mint (Epsilon), then 0 after a medium and Epsilon after a surface
     while (!(thr[0] == 0 && thr[1] == 0 && thr[2] == 0) && (depth <= max_depth || max_depth < 0)) {
         V3 n, hp;
         int tri;
         const float its_t = sc.first_hit(o, dir, mint, &n, &hp, &tri);
         const bool its_valid = std::isfinite(its_t);
-        // HomogeneousMedium::sampleDistance (homogeneous.cpp:275-352), balance
-        float rnd = smp.next(), sampled;
-        if (rnd < w) {
-            rnd /= w;
-            int ch = (int)(smp.next() * 3);
-            if (ch > 2) ch = 2;
-            sampled = -fastlog(1 - rnd) / m.sigma_t[ch];
-        } else {
-            sampled = INFINITY;
-        }
+        // HomogeneousMedium::sampleDistance (homogeneous.cpp:275-352)
+        float pdf_max = 0.0f;
+        float sampled = sample_distance(m, smp, &pdf_max);
         const float distSurf = its_t - 0.0f;
         bool success = true;
         V3 mp = o;
@@ -336,17 +435,10 @@ void trace_particle(const SmokeBox& sc, Stream& smp, bool short_vrls, int max_de
             sampled = distSurf;
             success = false;
         }
-        float pf = 0, ps = 0;
-        for (int i = 0; i < 3; i++) {
-            const float tmp = fastexp(-m.sigma_t[i] * sampled);
-            pf += tmp;
-            ps += m.sigma_t[i] * tmp;
-        }
-        pf /= 3; ps /= 3;
+        float pf, ps;
+        m.pdfs(sampled, pdf_max, &ps, &pf);
         float mtr[3];
         for (int i = 0; i < 3; i++) mtr[i] = fastexp(m.sigma_t[i] * (-sampled));
-        ps = ps * w;
-        pf = w * pf + (1 - w);
         {
             float mx = mtr[0] > mtr[1] ? mtr[0] : mtr[1];
             mx = mx > mtr[2] ? mx : mtr[2];

@@ -12,7 +12,8 @@
 //                        part of Scene::evalTransmittance (scene.cpp:619-679);
 //                        without them every interior pair is mutually visible
 //   point light          src/emitters/point.cpp:81-106
-//   homogeneous fog      src/medium/homogeneous.cpp (balance strategy)
+//   homogeneous fog      src/medium/homogeneous.cpp (balance / single /
+//                        manual / maximum distance sampling)
 #pragma once
 
 #include <cstdint>
@@ -45,7 +46,20 @@ struct MediumParams {
     float sampling_weight = -1.0f;   // resolved by resolve()
     int phase_type = 0;              // 0 isotropic, 1 HG
     float phase_g = 0.0f;
-    void resolve();                  // sigma_t and the auto sampling weight (homogeneous.cpp:168-184)
+    int strategy = 0;                // ALVRL_STRATEGY_* (homogeneous.cpp:150-227)
+    int channel = 0;                 // 'single': 1 + channel (0: the smallest sigma_t)
+    float density = 0.0f;            // 'manual': samplingDensity; after resolve() m_samplingDensity
+    // MaxExpDist (maxexp.h:28-94) after resolve(): sigma_t sorted decreasingly,
+    // the normalised CDF at the interval starts, the starts, the lower terms
+    float mx_sigma[3] = {0, 0, 0}, mx_cdf[4] = {0, 0, 0, 0}, mx_start[3] = {0, 0, 0}, mx_lower[3] = {0, 0, 0};
+    float mx_norm = 0.0f, mx_inv_norm = 0.0f;
+    const char* problem() const;     // what resolve() cannot accept, or nullptr
+    void resolve();                  // sigma_t, the auto sampling weight (:168-184), the strategy's terms
+    // sampleDistance's pdfs at the distance used (:317-346), the sampling weight
+    // applied; pdf_max: MaxExpDist::sample's pdf ('maximum')
+    void pdfs(float sampled, float pdf_max, float* ps, float* pf) const;
+    float maxexp_sample(float u, float* pdf) const;   // maxexp.h:59-73
+    float maxexp_cdf(float t) const;                  // maxexp.h:83-94
 };
 
 struct SmokeBox {

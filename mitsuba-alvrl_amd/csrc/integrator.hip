@@ -1067,12 +1067,13 @@ ALVRL_API int alvrl_integrator_slice_job(alvrl_integrator* it, uint32_t s, float
     const uint32_t n = (uint32_t)rows.size();
     *nrows = n;
     *ninit = (uint32_t)it->job_init_off.size() - 1;
+    // R and locw hold cap_rows rows: refuse before writing anything
+    if ((R || locw) && cap_rows < n) return ierr(ALVRL_ERR_INVALID, "alvrl_integrator_slice_job: buffer too small");
     if (pixel_under) *pixel_under = it->prep->slice_undersampling()[s];
     if (init_vrls) std::copy(it->job_init.begin(), it->job_init.end(), init_vrls);
     if (init_off) std::copy(it->job_init_off.begin(), it->job_init_off.end(), init_off);
     if (locw) std::copy(it->job_locw[k].begin(), it->job_locw[k].end(), locw);
     if (!R) return ALVRL_OK;
-    if (cap_rows < n) return ierr(ALVRL_ERR_INVALID, "alvrl_integrator_slice_job: buffer too small");
     GUARD({
         hchk(hipSetDevice(it->device), "hipSetDevice");
         hchk(hipStreamSynchronize(it->stream), "sync");

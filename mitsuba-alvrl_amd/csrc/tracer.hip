@@ -15,6 +15,9 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -40,6 +43,8 @@ struct TScene {
     float light_pos[3], power[3];
     float box_min[3], box_max[3], albedo[3];
     float sigma_s[3], sigma_t[3], w;
+    int strategy;                 // the medium's sampling strategy (MediumParams)
+    float density, mx_sigma[3], mx_cdf[4], mx_start[3], mx_lower[3], mx_norm, mx_inv_norm;
     int sigma_s_zero;
     alvrl::bvh::View bv;          // occluders (ntri == 0: none)
     float occ_albedo[3];
@@ -59,6 +64,53 @@ __device__ __forceinline__ F3 cross(F3 a, F3 b)
 __device__ __forceinline__ float safe_sqrt(float v) { return sqrtf(v > 0.0f ? v : 0.0f); }
 __device__ __forceinline__ float fastexp(float v) { return (float)exp((double)v); }   // math.h:185-199
 __device__ __forceinline__ float fastlog(float v) { return (float)log((double)v); }
+
+// HomogeneousMedium::sampleDistance (homogeneous.cpp:275-352) as the host's
+// MediumParams / sample_distance: the same float operations, so the same
+// values.  'maximum' follows MaxExpDist (maxexp.h:59-94).
+__device__ __forceinline__ int interval_of(const float* a, int n, float x)
+{
+    int k = 0;
+    while (k < n && a[k] < x) k++;
+    return k > 0 ? k - 1 : 0;
+}
+
+__device__ __forceinline__ float maxexp_sample(const TScene& sc, float u, float* pdf)
+{
+    const int i = min(interval_of(sc.mx_cdf, 4, u), 2);
+    const float t = -fastlog(fastexp(-sc.mx_start[i] * sc.mx_sigma[i]) - sc.mx_norm * (u - sc.mx_cdf[i])) / sc.mx_sigma[i];
+    *pdf = sc.mx_sigma[i] * fastexp(-sc.mx_sigma[i] * t) * sc.mx_inv_norm;
+    return t;
+}
+
+__device__ __forceinline__ float maxexp_cdf(const TScene& sc, float t)
+{
+    const int i = interval_of(sc.mx_start, 3, t);
+    const float upper = -fastexp(-sc.mx_sigma[i] * t);
+    return sc.mx_cdf[i] + (upper - sc.mx_lower[i]) * sc.mx_inv_norm;
+}
+
+__device__ __forceinline__ void medium_pdfs(const TScene& sc, float sampled, float pdf_max, float* ps, float* pf)
+{
+    const float w = sc.w;
+    float s = 0.0f, f = 0.0f;
+    if (sc.strategy == 3) {
+        f = 1 - maxexp_cdf(sc, sampled);
+        s = pdf_max;
+    } else if (sc.strategy == 0) {
+        for (int i = 0; i < 3; i++) {
+            const float tmp = fastexp(-sc.sigma_t[i] * sampled);
+            f += tmp;
+            s += sc.sigma_t[i] * tmp;
+        }
+        f /= 3; s /= 3;
+    } else {
+        f = fastexp(-sc.density * sampled);
+        s = sc.density * f;
+    }
+    *ps = s * w;
+    *pf = w * f + (1 - w);
+}
 
 // Random123 Philox4x32-10 and Random::nextFloat (random.cpp:630-639), as the host
 struct Stream {
@@ -84,6 +136,25 @@ struct Stream {
         return __uint_as_float(u) - 1.0f;
     }
 };
+
+// sampleDistance's draws (homogeneous.cpp:277-296): the distance (INFINITY:
+// no medium interaction) and, for 'maximum', the pdf of the sample
+template <class S>
+__device__ __forceinline__ float sample_distance(const TScene& sc, S& smp, float* pdf_max)
+{
+    float rnd = smp.next();
+    const float w = sc.w;
+    if (!(rnd < w)) return INFINITY;
+    rnd /= w;
+    if (sc.strategy == 3) return maxexp_sample(sc, 1 - rnd, pdf_max);
+    float density = sc.density;
+    if (sc.strategy == 0) {   // a random channel each time
+        int ch = (int)(smp.next() * 3);
+        if (ch > 2) ch = 2;
+        density = sc.sigma_t[ch];
+    }
+    return -fastlog(1 - rnd) / density;
+}
 
 __device__ F3 uniform_sphere(float sx, float sy)   // warp.cpp:25-31
 {
@@ -202,7 +273,6 @@ __device__ void trace_particle(const TScene& sc, Stream& smp, bool short_vrls, i
     int depth = 1;
     float thr[3] = {1.0f, 1.0f, 1.0f};
     const float eta = 1.0f;
-    const float w = sc.w;
     float mint = 1e-4f;   // Ray() default mint (Epsilon), then 0 after a medium and Epsilon after a surface
     while (!(thr[0] == 0 && thr[1] == 0 && thr[2] == 0) && (depth <= max_depth || max_depth < 0)) {
         F3 n, hp;
@@ -210,15 +280,8 @@ __device__ void trace_particle(const TScene& sc, Stream& smp, bool short_vrls, i
         const float its_t = first_hit(sc, o, dir, mint, &n, &hp, &hit_occ);
         const bool its_valid = isfinite(its_t);
         // HomogeneousMedium::sampleDistance (homogeneous.cpp:275-352), balance
-        float rnd = smp.next(), sampled;
-        if (rnd < w) {
-            rnd /= w;
-            int ch = (int)(smp.next() * 3);
-            if (ch > 2) ch = 2;
-            sampled = -fastlog(1 - rnd) / sc.sigma_t[ch];
-        } else {
-            sampled = INFINITY;
-        }
+        float pdf_max = 0.0f;
+        float sampled = sample_distance(sc, smp, &pdf_max);
         const float distSurf = its_t - 0.0f;
         bool success = true;
         F3 mp = o;
@@ -229,17 +292,10 @@ __device__ void trace_particle(const TScene& sc, Stream& smp, bool short_vrls, i
             sampled = distSurf;
             success = false;
         }
-        float pf = 0, ps = 0;
-        for (int i = 0; i < 3; i++) {
-            const float tmp = fastexp(-sc.sigma_t[i] * sampled);
-            pf += tmp;
-            ps += sc.sigma_t[i] * tmp;
-        }
-        pf /= 3; ps /= 3;
+        float pf, ps;
+        medium_pdfs(sc, sampled, pdf_max, &ps, &pf);
         float mtr[3];
         for (int i = 0; i < 3; i++) mtr[i] = fastexp(sc.sigma_t[i] * (-sampled));
-        ps = ps * w;
-        pf = w * pf + (1 - w);
         {
             float mx = mtr[0] > mtr[1] ? mtr[0] : mtr[1];
             mx = mx > mtr[2] ? mx : mtr[2];
@@ -367,6 +423,29 @@ struct DevBvh {
         return e;
     }
 };
+
+// The last BVH built on each device, keyed by the occluder triangles: the
+// integrator's calls for one scene (records every render cache refresh and R
+// build, the tracer every pass) reuse it instead of rebuilding it each call.
+// The cache is never destroyed (its device memory lives until the process
+// exits; freeing it from a static destructor could run after the HIP runtime
+// is gone); a caller keeps its BVH alive by holding the shared pointer.
+std::shared_ptr<DevBvh> cached_bvh(const std::vector<float>& occ, hipError_t* err)
+{
+    static std::mutex mu;
+    static auto* cache = new std::map<int, std::pair<std::vector<float>, std::shared_ptr<DevBvh>>>();
+    int dev = 0;
+    *err = hipGetDevice(&dev);
+    if (*err != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> g(mu);
+    auto it = cache->find(dev);
+    if (it != cache->end() && it->second.first == occ) return it->second.second;
+    auto b = std::make_shared<DevBvh>();
+    *err = b->upload(occ);
+    if (*err != hipSuccess) return nullptr;
+    (*cache)[dev] = {occ, b};
+    return b;
+}
 
 // The camera of SmokeBox::camera_ray with its per-scene terms formed on the
 // host (the same float operations, so the same values).
@@ -497,21 +576,13 @@ __device__ void volpath_li(const TScene& sc, const VParams& vp, VStream& smp, F3
     float its_t = first_hit(sc, o, dir, mint, &n, &hp, &hit_occ);
     float thr[3] = {1.0f, 1.0f, 1.0f};
     const float eta = 1.0f;
-    const float w = sc.w;
     int depth = 1;
     bool indirect = true;   // rRec.type keeps EIndirect*Radiance (ERadiance / ERadianceNoEmission)
     while (depth <= vp.max_depth || vp.max_depth < 0) {
         if (vp.only_vrl && depth > 2 && !(first_ok && second_ok)) break;   // :144-145
         // HomogeneousMedium::sampleDistance over Ray(ray, 0, its.t)
-        float rnd = smp.next(), sampled;
-        if (rnd < w) {
-            rnd /= w;
-            int ch = (int)(smp.next() * 3);
-            if (ch > 2) ch = 2;
-            sampled = -fastlog(1 - rnd) / sc.sigma_t[ch];
-        } else {
-            sampled = INFINITY;
-        }
+        float pdf_max = 0.0f;
+        float sampled = sample_distance(sc, smp, &pdf_max);
         const float distSurf = its_t - 0.0f;
         bool success = true;
         F3 mp = o;
@@ -522,17 +593,10 @@ __device__ void volpath_li(const TScene& sc, const VParams& vp, VStream& smp, F3
             sampled = distSurf;
             success = false;
         }
-        float pf = 0, ps = 0;
-        for (int i = 0; i < 3; i++) {
-            const float tmp = fastexp(-sc.sigma_t[i] * sampled);
-            pf += tmp;
-            ps += sc.sigma_t[i] * tmp;
-        }
-        pf /= 3; ps /= 3;
+        float pf, ps;
+        medium_pdfs(sc, sampled, pdf_max, &ps, &pf);
         float mtr[3];
         for (int i = 0; i < 3; i++) mtr[i] = fastexp(sc.sigma_t[i] * (-sampled));
-        ps = ps * w;
-        pf = w * pf + (1 - w);
         {
             float mx = mtr[0] > mtr[1] ? mtr[0] : mtr[1];
             mx = mx > mtr[2] ? mx : mtr[2];
@@ -658,6 +722,15 @@ TScene make_tscene(const alvrl::host::SmokeBox& box)
         sc.occ_albedo[i] = box.occ_albedo[i];
     }
     sc.w = box.medium.sampling_weight;
+    sc.strategy = box.medium.strategy;
+    sc.density = box.medium.density;
+    for (int i = 0; i < 3; i++) {
+        sc.mx_sigma[i] = box.medium.mx_sigma[i]; sc.mx_start[i] = box.medium.mx_start[i];
+        sc.mx_lower[i] = box.medium.mx_lower[i];
+    }
+    for (int i = 0; i < 4; i++) sc.mx_cdf[i] = box.medium.mx_cdf[i];
+    sc.mx_norm = box.medium.mx_norm;
+    sc.mx_inv_norm = box.medium.mx_inv_norm;
     sc.sigma_s_zero = (sc.sigma_s[0] == 0 && sc.sigma_s[1] == 0 && sc.sigma_s[2] == 0) ? 1 : 0;
     sc.bv = alvrl::bvh::View{nullptr, nullptr, nullptr, 0u};
     return sc;
@@ -712,9 +785,10 @@ ALVRL_API int alvrl_volpath_render(const alvrl_scene_desc* s, const alvrl_volpat
     if (!d_pixel_ids && n > npix) return terr(ALVRL_ERR_INVALID, "alvrl_volpath_render: n > W*H without pixel ids");
     if (n == 0) return ALVRL_OK;
     TScene sc = make_tscene(box);
-    DevBvh bv;
-    if (bv.upload(box.occ) != hipSuccess) return terr(ALVRL_ERR_HIP, "alvrl_volpath_render: BVH upload");
-    sc.bv = bv.view;
+    hipError_t be = hipSuccess;
+    const std::shared_ptr<DevBvh> bv = cached_bvh(box.occ, &be);
+    if (!bv) return terr(ALVRL_ERR_HIP, "alvrl_volpath_render: BVH upload");
+    sc.bv = bv->view;
     const TCam c = make_tcam(box, 1);
     VParams vp;
     vp.max_depth = p->max_depth; vp.rr_depth = p->rr_depth; vp.only_vrl = p->only_vrl_paths ? 1 : 0;
@@ -745,15 +819,16 @@ ALVRL_API int alvrl_scene_records_gpu(const alvrl_scene_desc* s, int medium_scat
     if (!d_pixel_ids && n > npix) return terr(ALVRL_ERR_INVALID, "alvrl_scene_records_gpu: n > W*H without pixel ids");
     if (n == 0) return ALVRL_OK;
     TScene sc = make_tscene(box);
-    DevBvh bv;
-    if (bv.upload(box.occ) != hipSuccess) return terr(ALVRL_ERR_HIP, "alvrl_scene_records_gpu: BVH upload");
-    sc.bv = bv.view;
+    hipError_t be = hipSuccess;
+    const std::shared_ptr<DevBvh> bv = cached_bvh(box.occ, &be);
+    if (!bv) return terr(ALVRL_ERR_HIP, "alvrl_scene_records_gpu: BVH upload");
+    sc.bv = bv->view;
     const TCam c = make_tcam(box, medium_scatters && !sc.sigma_s_zero ? 1 : 0);
     hipStream_t st = (hipStream_t)stream;
     hipLaunchKernelGGL(k_eye_records, dim3((n + 255) / 256), dim3(256), 0, st, c, sc, d_pixel_ids, n,
                        reinterpret_cast<float*>(d_out));
     if (hipGetLastError() != hipSuccess) return terr(ALVRL_ERR_HIP, "alvrl_scene_records_gpu: launch");
-    // the BVH buffers are freed on return: wait for the kernel that reads them
+    // stream-ordered callers may replace the cached BVH after return: wait for the kernel
     if (hipStreamSynchronize(st) != hipSuccess) return terr(ALVRL_ERR_HIP, "alvrl_scene_records_gpu: sync");
     return ALVRL_OK;
 }
@@ -771,9 +846,10 @@ ALVRL_API int alvrl_trace_vrls_gpu(const alvrl_scene_desc* s, uint32_t seed, uin
     if (box.has_delta())
         return terr(ALVRL_ERR_INVALID, "alvrl_trace_vrls_gpu: mirror / null occluders are traced on the host (alvrl_trace_vrls)");
     TScene sc = make_tscene(box);
-    DevBvh bvh;
-    if (bvh.upload(box.occ) != hipSuccess) return terr(ALVRL_ERR_HIP, "alvrl_trace_vrls_gpu: BVH upload");
-    sc.bv = bvh.view;
+    hipError_t be = hipSuccess;
+    const std::shared_ptr<DevBvh> bvh = cached_bvh(box.occ, &be);
+    if (!bvh) return terr(ALVRL_ERR_HIP, "alvrl_trace_vrls_gpu: BVH upload");
+    sc.bv = bvh->view;
     const TArgs a{seed, pass, short_vrls, max_depth, rr_depth};
     *n = 0;
     if (target == 0) { *particles = 0; return ALVRL_OK; }

@@ -55,6 +55,11 @@ struct DevParams {
     uint32_t seed, pass;
     int rsamples;           // Rsamples (vrlIntegrator.cpp:194): samples per R entry (0 = 1)
     bvh::View occ;          // occluders blocking U-V and surface-V (ntri == 0: convex container)
+    // the medium's sampling strategy (homogeneous.cpp:150-227): 0 balance,
+    // 1 single / 2 manual (density), 3 maximum (MaxExpDist, maxexp.h:28-94)
+    int strategy;
+    float density;
+    float mx_sigma[3], mx_cdf[4], mx_start[3], mx_lower[3], mx_inv_norm;
 };
 
 // ---------------------------------------------------------------- RNG --
@@ -184,16 +189,34 @@ struct RecPre {
     bool medium, surf, unit;   // unit: weight (1, 1, 1)
 };
 
+// MaxExpDist::cdf (maxexp.h:83-94); the interval of t by lower_bound over
+// the three starts (the first is 0)
+__device__ __forceinline__ float maxexp_cdf(const DevParams& P, float d)
+{
+    const int i = (P.mx_start[1] < d) + (P.mx_start[2] < d);
+    const float upper = -__expf(-P.mx_sigma[i] * d);
+    return P.mx_cdf[i] + (upper - P.mx_lower[i]) * P.mx_inv_norm;
+}
+
+// ANY_STRATEGY: the generic-sample-count kernels serve every strategy; the
+// unrolled (2, 2) kernels are launched for 'balance' only and carry no branch.
+template <bool ANY_STRATEGY>
 __device__ __forceinline__ void medium_tr(const DevParams& P, float d, float tr[3], float* pf)
 {
-    // HomogeneousMedium::eval (homogeneous.cpp:354-396): the pdf exponentials
-    // and the transmittance exponentials are the same values.
+    // HomogeneousMedium::eval (homogeneous.cpp:354-396): with 'balance' the
+    // pdf exponentials and the transmittance exponentials are the same values.
     const float t0 = __expf(P.sigma_t[0] * (-d));
     const float t1 = __expf(P.sigma_t[1] * (-d));
     const float t2 = __expf(P.sigma_t[2] * (-d));
     float s = 0.0f;
-    s += t0; s += t1; s += t2;
-    s *= (1.0f / 3.0f);
+    if (!ANY_STRATEGY || P.strategy == 0) {   // wave-uniform
+        s += t0; s += t1; s += t2;
+        s *= (1.0f / 3.0f);
+    } else if (P.strategy == 3) {
+        s = 1 - maxexp_cdf(P, d);
+    } else {
+        s = __expf(-P.density * d);
+    }
     *pf = s * P.w + (1 - P.w);
     const bool z = fmax3(t0, t1, t2) < 1e-20f;
     tr[0] = z ? 0.0f : t0; tr[1] = z ? 0.0f : t1; tr[2] = z ? 0.0f : t2;
@@ -451,7 +474,7 @@ __device__ __forceinline__ void integrate_vrl(const DevParams& P, const RecPre& 
             if (tuv[0] != 0 || tuv[1] != 0 || tuv[2] != 0) {
                 float teu[3], tsv[3], pf;
                 medium_tr_only(P, fabsf(ke.dotPr + t), teu);
-                medium_tr(P, dSV, tsv, &pf);
+                medium_tr<(NVV < 0)>(P, dSV, tsv, &pf);
                 // 1 / samplingPDF / distanceSquared(U, V)
                 const float g = (ke.ab - ke.aa) * rcp(ke.Dis * pdfV);
                 const float rpf = P.short_vrls ? rcp(pf) : 1.0f;
@@ -514,7 +537,7 @@ __device__ __forceinline__ void integrate_vrl(const DevParams& P, const RecPre& 
                     tuv[0] = P.sigma_t[0] != 0 ? __expf(P.sigma_t[0] * (0.0f - dUV)) : 1.0f;
                     tuv[1] = P.sigma_t[1] != 0 ? __expf(P.sigma_t[1] * (0.0f - dUV)) : 1.0f;
                     tuv[2] = P.sigma_t[2] != 0 ? __expf(P.sigma_t[2] * (0.0f - dUV)) : 1.0f;
-                    medium_tr(P, fabsf(ks.dotPr + t), tsv, &pf);
+                    medium_tr<(NVV < 0)>(P, fabsf(ks.dotPr + t), tsv, &pf);
                     const float cos_wo = fmaf(t, sn, -dn) * rdUV;
                     const bool bz = (q.cos_wi <= 0 || cos_wo <= 0);
                     const float fcos = bz ? 0.0f : kInvPi * cos_wo;

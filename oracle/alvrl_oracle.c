@@ -156,18 +156,134 @@ void alvrl_o_medium_init(alvrl_o_medium *m, const float sigma_s[3], const float 
     m->sampling_weight = w;
     m->phase_type = phase_type;
     m->phase_g = g;
+    m->strategy = ALVRL_O_BALANCE;
+    m->density = 0.0f;
 }
 
-/* HomogeneousMedium::eval, 'balance' strategy (homogeneous.cpp:354-396).
- * Only the fields used by integrateVRL are produced. */
+int alvrl_o_medium_strategy(alvrl_o_medium *m, int strategy, int channel, float density)
+{
+    m->strategy = strategy;
+    m->density = 0.0f;
+    if (strategy == ALVRL_O_BALANCE) return 0;
+    if (strategy == ALVRL_O_SINGLE) {   /* homogeneous.cpp:188-204 */
+        if (channel < 0) {
+            float smallest = INFINITY;
+            channel = 0;
+            for (int i = 0; i < 3; i++)
+                if (m->sigma_t[i] < smallest) { smallest = m->sigma_t[i]; channel = i; }
+        }
+        if (channel > 2) return -1;
+        m->density = m->sigma_t[channel];
+        return 0;
+    }
+    if (strategy == ALVRL_O_MANUAL) { m->density = density; return 0; }   /* :221-223 */
+    if (strategy != ALVRL_O_MAXIMUM) return -1;
+    /* MaxExpDist(sigmaT) (maxexp.h:30-57) */
+    float s[3] = { m->sigma_t[0], m->sigma_t[1], m->sigma_t[2] };
+    for (int i = 0; i < 3; i++)          /* std::sort(.., std::greater<Float>()) */
+        for (int j = i + 1; j < 3; j++)
+            if (s[j] > s[i]) { float t = s[i]; s[i] = s[j]; s[j] = t; }
+    float cdf[4];
+    cdf[0] = 0;
+    for (int i = 0; i < 3; i++) {
+        if (i > 0 && s[i] == s[i - 1]) return -1;
+        float lower = (i == 0) ? -1 : -powf(s[i] / s[i - 1], -s[i] / (s[i] - s[i - 1]));
+        float upper = (i == 2) ? 0 : -powf(s[i + 1] / s[i], -s[i] / (s[i + 1] - s[i]));
+        cdf[i + 1] = cdf[i] + (upper - lower);
+        m->mx_start[i] = (i == 0) ? 0 : fastlog(s[i] / s[i - 1]) / (s[i] - s[i - 1]);
+        m->mx_lower[i] = lower;
+        m->mx_sigma[i] = s[i];
+    }
+    m->mx_norm = cdf[3];
+    m->mx_inv_norm = 1 / m->mx_norm;
+    for (int i = 0; i < 4; i++) m->mx_cdf[i] = cdf[i] * m->mx_inv_norm;
+    return 0;
+}
+
+/* std::max(0, lower_bound(a, a + n, x) - a - 1) */
+static int interval_of(const float *a, int n, float x)
+{
+    int k = 0;
+    while (k < n && a[k] < x) k++;
+    return k > 0 ? k - 1 : 0;
+}
+
+/* MaxExpDist::sample (maxexp.h:59-73).  The index is clamped to the last
+ * interval (the reference's SAssert is compiled out: u = 1 above a rounded
+ * m_cdf[n] would read past its arrays). */
+static float maxexp_sample(const alvrl_o_medium *m, float u, float *pdf)
+{
+    int i = interval_of(m->mx_cdf, 4, u);
+    if (i > 2) i = 2;
+    float t = -fastlog(fastexp(-m->mx_start[i] * m->mx_sigma[i]) - m->mx_norm * (u - m->mx_cdf[i])) / m->mx_sigma[i];
+    *pdf = m->mx_sigma[i] * fastexp(-m->mx_sigma[i] * t) * m->mx_inv_norm;
+    return t;
+}
+
+/* MaxExpDist::cdf (maxexp.h:83-94) */
+static float maxexp_cdf(const alvrl_o_medium *m, float t)
+{
+    int i = interval_of(m->mx_start, 3, t);
+    float upper = -fastexp(-m->mx_sigma[i] * t);
+    return m->mx_cdf[i] + (upper - m->mx_lower[i]) * m->mx_inv_norm;
+}
+
+/* HomogeneousMedium::sampleDistance's draws (homogeneous.cpp:277-296): the
+ * sampled distance (INFINITY: no medium interaction) and, for 'maximum',
+ * the pdf of the sample. */
+static float medium_sample_distance(const alvrl_o_medium *m, seq_sampler *smp, float *pdf_max)
+{
+    float rnd = seq_next(smp), w = m->sampling_weight;
+    if (!(rnd < w)) return INFINITY;   /* no medium interaction */
+    rnd /= w;
+    if (m->strategy == ALVRL_O_MAXIMUM) return maxexp_sample(m, 1 - rnd, pdf_max);
+    float density = m->density;
+    if (m->strategy == ALVRL_O_BALANCE) {   /* a random channel each time */
+        int ch = (int)(seq_next(smp) * 3);
+        if (ch > 2) ch = 2;
+        density = m->sigma_t[ch];
+    }
+    return -fastlog(1 - rnd) / density;
+}
+/* The pdfs of sampleDistance (:317-346) at the distance used: pdfSuccess and
+ * pdfFailure with the sampling weight applied. */
+static void medium_pdfs(const alvrl_o_medium *m, float sampled, float pdf_max, float *ps, float *pf)
+{
+    float w = m->sampling_weight, s = 0.0f, f = 0.0f;
+    if (m->strategy == ALVRL_O_MAXIMUM) {
+        f = 1 - maxexp_cdf(m, sampled);
+        s = pdf_max;
+    } else if (m->strategy == ALVRL_O_BALANCE) {
+        for (int i = 0; i < 3; i++) {
+            float tmp = fastexp(-m->sigma_t[i] * sampled);
+            f += tmp;
+            s += m->sigma_t[i] * tmp;
+        }
+        f /= 3; s /= 3;
+    } else {
+        f = fastexp(-m->density * sampled);
+        s = m->density * f;
+    }
+    *ps = s * w;
+    *pf = w * f + (1 - w);
+}
+
+/* HomogeneousMedium::eval (homogeneous.cpp:354-396).  Only the fields used
+ * by integrateVRL are produced. */
 static void medium_eval(const alvrl_o_medium *m, float distance, float tr[3], float *pdf_failure)
 {
     float pf = 0.0f;
-    for (int i = 0; i < 3; i++) {
-        float temp = fastexp(-m->sigma_t[i] * distance);
-        pf += temp;
+    if (m->strategy == ALVRL_O_BALANCE) {
+        for (int i = 0; i < 3; i++) {
+            float temp = fastexp(-m->sigma_t[i] * distance);
+            pf += temp;
+        }
+        pf /= 3;
+    } else if (m->strategy == ALVRL_O_MAXIMUM) {
+        pf = 1 - maxexp_cdf(m, distance);
+    } else {
+        pf = fastexp(-m->density * distance);
     }
-    pf /= 3;
     for (int i = 0; i < 3; i++) tr[i] = fastexp(m->sigma_t[i] * (-distance));
     *pdf_failure = pf * m->sampling_weight + (1 - m->sampling_weight);
     float mx = tr[0] > tr[1] ? tr[0] : tr[1];
@@ -1015,17 +1131,9 @@ static void trace_particle(const alvrl_o_scene *s, const alvrl_o_medium *m, seq_
         int tri;
         float its_t = first_hit(s, o, dir, mint, &n, &hp, &tri);
         int its_valid = isfinite(its_t);
-        /* HomogeneousMedium::sampleDistance (homogeneous.cpp:275-352), balance */
-        float rnd = seq_next(smp), sampled;
-        float w = m->sampling_weight;
-        if (rnd < w) {
-            rnd /= w;
-            int ch = (int)(seq_next(smp) * 3);
-            if (ch > 2) ch = 2;
-            sampled = -fastlog(1 - rnd) / m->sigma_t[ch];
-        } else {
-            sampled = INFINITY;
-        }
+        /* HomogeneousMedium::sampleDistance (homogeneous.cpp:275-352) */
+        float pdf_max = 0.0f;
+        float sampled = medium_sample_distance(m, smp, &pdf_max);
         float distSurf = its_t - 0.0f;
         int success = 1;
         v3 mp = o;
@@ -1037,17 +1145,10 @@ static void trace_particle(const alvrl_o_scene *s, const alvrl_o_medium *m, seq_
             sampled = distSurf;
             success = 0;
         }
-        float pf = 0, ps = 0;
-        for (int i = 0; i < 3; i++) {
-            float tmp = fastexp(-m->sigma_t[i] * sampled);
-            pf += tmp;
-            ps += m->sigma_t[i] * tmp;
-        }
-        pf /= 3; ps /= 3;
+        float pf, ps;
+        medium_pdfs(m, sampled, pdf_max, &ps, &pf);
         float mtr[3];
         for (int i = 0; i < 3; i++) mtr[i] = fastexp(m->sigma_t[i] * (-sampled));
-        ps = ps * w;
-        pf = w * pf + (1 - w);
         {
             float mx = mtr[0] > mtr[1] ? mtr[0] : mtr[1];
             mx = mx > mtr[2] ? mx : mtr[2];
@@ -1175,19 +1276,12 @@ static void vp_li(const alvrl_o_scene *s, const alvrl_o_medium *m, const alvrl_o
     int tri;
     float its_t = first_hit(s, o, dir, mint, &n, &hp, &tri);
     float thr[3] = { 1, 1, 1 };
-    float eta = 1.0f, w = m->sampling_weight;
+    float eta = 1.0f;
     int depth = 1;
     while (depth <= vp->max_depth || vp->max_depth < 0) {
         if (vp->only_vrl_paths && depth > 2 && !(first_ok && second_ok)) break;   /* :144-145 */
-        float rnd = seq_next(smp), sampled;
-        if (rnd < w) {
-            rnd /= w;
-            int ch = (int)(seq_next(smp) * 3);
-            if (ch > 2) ch = 2;
-            sampled = -fastlog(1 - rnd) / m->sigma_t[ch];
-        } else {
-            sampled = INFINITY;
-        }
+        float pdf_max = 0.0f;
+        float sampled = medium_sample_distance(m, smp, &pdf_max);
         float distSurf = its_t - 0.0f;
         int success = 1;
         v3 mp = o;
@@ -1198,17 +1292,10 @@ static void vp_li(const alvrl_o_scene *s, const alvrl_o_medium *m, const alvrl_o
             sampled = distSurf;
             success = 0;
         }
-        float pf = 0, ps = 0;
-        for (int i = 0; i < 3; i++) {
-            float tmp = fastexp(-m->sigma_t[i] * sampled);
-            pf += tmp;
-            ps += m->sigma_t[i] * tmp;
-        }
-        pf /= 3; ps /= 3;
+        float pf, ps;
+        medium_pdfs(m, sampled, pdf_max, &ps, &pf);
         float mtr[3];
         for (int i = 0; i < 3; i++) mtr[i] = fastexp(m->sigma_t[i] * (-sampled));
-        ps = ps * w;
-        pf = w * pf + (1 - w);
         {
             float mx = mtr[0] > mtr[1] ? mtr[0] : mtr[1];
             mx = mx > mtr[2] ? mx : mtr[2];

@@ -58,7 +58,13 @@ float alvrl_o_kulla(const float A[3], const float B[3], const float D[3], float 
 float alvrl_o_sample_v_to_distance(const float E[3], const float d[3], const float hitp[3],
                                    const float S[3], const float End[3], float uniform, float V[3]);
 
-/* Homogeneous medium with the 'balance' strategy (homogeneous.cpp:156-184). */
+/* Homogeneous medium (homogeneous.cpp:156-227) with its distance sampling
+ * strategy: ALVRL_O_BALANCE (default), _SINGLE (one channel's sigma_t),
+ * _MANUAL (samplingDensity), _MAXIMUM (MaxExpDist, maxexp.h:28-94). */
+#define ALVRL_O_BALANCE 0
+#define ALVRL_O_SINGLE 1
+#define ALVRL_O_MANUAL 2
+#define ALVRL_O_MAXIMUM 3
 typedef struct {
     float sigma_s[3];
     float sigma_a[3];
@@ -66,10 +72,20 @@ typedef struct {
     float sampling_weight;   /* m_mediumSamplingWeight after the auto rule */
     int   phase_type;        /* 0 = isotropic, 1 = Henyey-Greenstein */
     float phase_g;
+    int   strategy;
+    float density;           /* m_samplingDensity (single, manual) */
+    /* MaxExpDist: sigma_t sorted decreasingly, its normalised CDF at the
+     * interval starts, the interval starts, -pow(...) lower terms */
+    float mx_sigma[3], mx_cdf[4], mx_start[3], mx_lower[3], mx_norm, mx_inv_norm;
 } alvrl_o_medium;
 
 void alvrl_o_medium_init(alvrl_o_medium *m, const float sigma_s[3], const float sigma_a[3],
                          float sampling_weight /* -1 = auto */, int phase_type, float g);
+/* The strategy of an initialised medium: channel (single) = -1 for the
+ * smallest sigma_t (:191-202), density (manual).  0, or -1 if MaxExpDist
+ * needs distinct sigma_t ("Internal error: sigmaT must vary", maxexp.h:37-38)
+ * or the arguments are out of range. */
+int alvrl_o_medium_strategy(alvrl_o_medium *m, int strategy, int channel, float density);
 /* HomogeneousMedium::eval, 'balance' strategy: transmittance + pdfFailure */
 void alvrl_o_medium_eval(const alvrl_o_medium *m, float distance, float tr[3], float *pdf_failure);
 

@@ -30,7 +30,13 @@ def build(force: bool = False) -> None:
 
 class Medium(C.Structure):
     _fields_ = [("sigma_s", C.c_float * 3), ("sigma_a", C.c_float * 3), ("sigma_t", C.c_float * 3),
-                ("sampling_weight", C.c_float), ("phase_type", C.c_int), ("phase_g", C.c_float)]
+                ("sampling_weight", C.c_float), ("phase_type", C.c_int), ("phase_g", C.c_float),
+                ("strategy", C.c_int), ("density", C.c_float), ("mx_sigma", C.c_float * 3),
+                ("mx_cdf", C.c_float * 4), ("mx_start", C.c_float * 3), ("mx_lower", C.c_float * 3),
+                ("mx_norm", C.c_float), ("mx_inv_norm", C.c_float)]
+
+
+STRATEGIES = {"balance": 0, "single": 1, "manual": 2, "maximum": 3}
 
 
 class Params(C.Structure):
@@ -100,6 +106,7 @@ class Oracle:
         L.alvrl_o_u01.argtypes = [u32]; L.alvrl_o_u01.restype = f32
         L.alvrl_o_medium_init.argtypes = [P(Medium), P(f32), P(f32), f32, i32, f32]
         L.alvrl_o_medium_eval.argtypes = [P(Medium), f32, P(f32), P(f32)]
+        L.alvrl_o_medium_strategy.argtypes = [P(Medium), i32, i32, f32]
         L.alvrl_o_closest_points.argtypes = [P(f32)] * 6
         L.alvrl_o_closest_points.restype = f32
         L.alvrl_o_kulla.argtypes = [P(f32), P(f32), P(f32), f32, P(f32)]
@@ -179,10 +186,14 @@ class Oracle:
         return s
 
     def medium(self, sigma_s=(0.8, 0.6, 0.4), sigma_a=(0.05, 0.05, 0.05), weight=-1.0,
-               phase_type=0, g=0.0) -> Medium:
+               phase_type=0, g=0.0, strategy="balance", channel=-1, density=0.0) -> Medium:
+        """HomogeneousMedium: strategy 'balance' | 'single' (channel, -1 = the
+        smallest sigma_t) | 'manual' (samplingDensity) | 'maximum'."""
         m = Medium()
         ss = (C.c_float * 3)(*sigma_s); sa = (C.c_float * 3)(*sigma_a)
         self.lib.alvrl_o_medium_init(C.byref(m), ss, sa, weight, phase_type, g)
+        if self.lib.alvrl_o_medium_strategy(C.byref(m), STRATEGIES[strategy], channel, density) != 0:
+            raise ValueError(f"medium strategy {strategy!r} not possible for sigma_t {list(m.sigma_t)}")
         return m
 
     def params(self, medium: Medium, nvv=2, nvs=2, short_vrls=1, seed=0xA1B2C3D4, pass_=0,

@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol():
 def test_struct_layouts():
     import alvrl
     assert C.sizeof(alvrl.Config) == 20
-    assert C.sizeof(alvrl.MediumDesc) == 36
+    assert C.sizeof(alvrl.MediumDesc) == 48
     assert alvrl.REC_WORDS * 4 == 80
 
 
