@@ -52,7 +52,10 @@ def test_gather_brute_chains(oracle, gpu_ok):
     ctx.upload_vrls(vrls, pc)
     ctx.set_occluders(tris, mat)
     d_out = torch.zeros((len(recs), 3), dtype=torch.float32, device="cuda")
-    ctx.gather_brute(torch.from_numpy(recs).cuda(), d_out, torch.from_numpy(pix.view(np.int32)).cuda())
+    # the inputs stay referenced until the device is done: the context's
+    # stream is not torch's, so a freed block could be reused under the kernel
+    d_recs, d_pix = torch.from_numpy(recs).cuda(), torch.from_numpy(pix.view(np.int32)).cuda()
+    ctx.gather_brute(d_recs, d_out, d_pix)
     torch.cuda.synchronize()
     dev = d_out.cpu().numpy()
     _assert_close(dev, cpu, "brute chain records")
@@ -82,6 +85,7 @@ def test_rbuild_chain_rows(oracle, gpu_ok):
     nr, nv = len(ids), vrls.shape[1]
     d_Rt = torch.zeros((nv, nr, 2), dtype=torch.float32, device="cuda")
     d_nz = torch.zeros(nv, dtype=torch.uint8, device="cuda")
+    keep = []   # every level's inputs stay referenced until the launches are done
     for d in range(int(depth.max()) + 1):
         sel = np.nonzero(depth == d)[0]
         r = recs[sel].copy()
@@ -89,9 +93,10 @@ def test_rbuild_chain_rows(oracle, gpu_ok):
             r[:, 15] = (r[:, 15].view(np.uint32) | alvrl.REC_ACCUM).view(np.float32)
         off = row[sel].astype(np.uint64)
         stride = np.full(len(sel), nr, np.uint32)
-        ctx.build_R_blocks(torch.from_numpy(r).cuda(), d_Rt, torch.from_numpy(off.view(np.int64)).cuda(),
-                           torch.from_numpy(stride.view(np.int32)).cuda(), d_nz,
-                           torch.from_numpy(pix[sel].view(np.int32)).cuda())
+        keep.append((torch.from_numpy(r).cuda(), torch.from_numpy(off.view(np.int64)).cuda(),
+                     torch.from_numpy(stride.view(np.int32)).cuda(), torch.from_numpy(pix[sel].view(np.int32)).cuda()))
+        t_r, t_off, t_str, t_ids = keep[-1]
+        ctx.build_R_blocks(t_r, d_Rt, t_off, t_str, d_nz, t_ids)
     torch.cuda.synchronize()
     Rg = d_Rt.cpu().numpy().transpose(1, 0, 2)
     _assert_close_pairs(Rg[..., 0], Rc[..., 0], "R mean chains")

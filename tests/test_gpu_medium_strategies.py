@@ -35,7 +35,8 @@ def test_gather_strategies(oracle, gpu_ok, strategy, channel, density):
         ctx = _ctx(_medium(alvrl, strategy, channel, density), short_vrls=short)
         ctx.upload_vrls(vrls, pc)
         d_out = torch.zeros((len(recs), 3), dtype=torch.float32, device="cuda")
-        ctx.gather_brute(torch.from_numpy(recs).cuda(), d_out)
+        d_recs = torch.from_numpy(recs).cuda()   # referenced until the kernel is done
+        ctx.gather_brute(d_recs, d_out)
         torch.cuda.synchronize()
         _assert_close(d_out.cpu().numpy(), cpu, f"brute {strategy} short={short}")
         # the balance gather of the same records differs (the strategy is not ignored)
@@ -47,7 +48,8 @@ def test_gather_strategies(oracle, gpu_ok, strategy, channel, density):
         _, R, _ = oracle.gather_brute(P, recs[ids], vrls, pc, rec_ids=ids, want_R=True, domain=2)
         nr, nv = len(ids), vrls.shape[1]
         d_Rt = torch.zeros((nv, nr, 2), dtype=torch.float32, device="cuda")
-        ctx.build_R(torch.from_numpy(recs[ids]).cuda(), d_Rt, ld=nr, d_ids=torch.from_numpy(ids.view(np.int32)).cuda())
+        d_rr, d_ids = torch.from_numpy(recs[ids]).cuda(), torch.from_numpy(ids.view(np.int32)).cuda()
+        ctx.build_R(d_rr, d_Rt, ld=nr, d_ids=d_ids)
         torch.cuda.synchronize()
         Rg = d_Rt.cpu().numpy().transpose(1, 0, 2)
         _assert_close_pairs(Rg[..., 0], R[..., 0], f"R mean {strategy}")
