@@ -1092,6 +1092,23 @@ __device__ __forceinline__ double tree16_transposed(const double* v, uint32_t la
     return z;
 }
 
+// v[2c + h] (c < 4) -> the shared-order total of value (c, h) in lane
+// 32h + 16(c & 1) + 8(c >> 1): the same pairs p[l] + p[l+off] as tree_dn
+// (an IEEE add is commutative, so which lane holds which operand is free)
+__device__ __forceinline__ double tree8_transposed(const double* v, uint32_t lane)
+{
+    double u[4], x[2];
+#pragma unroll
+    for (int i = 0; i < 4; i++) u[i] = swap32_add(v[2 * i], v[2 * i + 1]);
+#pragma unroll
+    for (int i = 0; i < 2; i++) x[i] = swap16_add(u[2 * i], u[2 * i + 1]);
+    double z = pair8_add(x[0], x[1], lane);
+    z = z + from_lane_plus_d<4>(z);
+    z = z + from_lane_plus_d<2>(z);
+    z = z + from_lane_plus_d<1>(z);
+    return z;
+}
+
 // The coefficient wave's share of chunk_coefs for 8 columns of a 64-column
 // block: the running total W in the reference's order (v_readlane), the
 // column's lane (8j + c) keeping W before (Wo) and after (Wn) its weight.
@@ -1175,8 +1192,14 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
     const uint32_t nblk = (m + kCB64 - 1) / kCB64;
     auto cn_of = [&](uint32_t k) { return min((uint32_t)kCH, m - k * kCH); };
     auto ncol_of = [&](uint32_t b) { return min((uint32_t)kCB64, m - b * kCB64); };
-    const bool wprof = cm.prof != nullptr;
-    long long wbusy = 0, wred = 0, wwall0 = wprof ? (long long)clock64() : 0;
+    // profile counters go straight to cm.prof (lane 0, per step): kept in
+    // registers across the chunk loop they cost 14 VGPRs of the budget
+    const bool wprof = cm.prof != nullptr && m >= 4096;
+    const int pbase = kPfWaveBusy + (NB == 4 ? 3 * kWaves : 0);
+    auto padd = [&](int idx, long long v) {
+        if (lane == 0) atomicAdd(&cm.prof[idx], (unsigned long long)v);
+    };
+    if (wprof) padd(pbase + kWaves + wv, -(long long)clock64());   // + the end time below: the wall span
 
     // (vrl, weight) of every column of the cluster, gathered in parallel once
     {
@@ -1254,67 +1277,69 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
             gpw(fi)[col] = stg[((b & 1) * 2 + 1) * kCB64 + lane];
         }
     };
-    // the recurrence of chunk k for one 64-row block (lane = row), terms into T[k & 1]
+    // the recurrence of chunk k for one 64-row block (lane = row); each half
+    // chunk's 8 prefix terms (pu, pi of 4 columns) are reduced over the block
+    // as soon as they exist (tree8_transposed) and their totals go to Q[k & 1][blk].
+    // Register budget: the engine is called once per split, and every
+    // callee-saved VGPR it touches is saved and restored per call (207 KB
+    // per workgroup at 101 registers).  So the coefficients
+    // arrive one column ahead (not the whole chunk's 7 x 8 doubles up
+    // front), and only half a chunk's terms are live at once.
     auto rec = [&](uint32_t k, const float2* cur, uint32_t blk, double lw, double& sum0, double& M0, double& V0,
                    bool valid) {
         const uint32_t c0 = k * kCH, cn = cn_of(k);
         const CoefBlock& q = ring[(k / 8) & 1];
         const uint32_t o = (k % 8) * kCH;
-        double tv[2 * kCH];                            // this row's prefix terms (pu, pi) per column
+        double th[kCH];                                // half a chunk's prefix terms (pu, pi) per column
+        auto half_done = [&](uint32_t hsel) {          // the block's halving tree (rows past R enter as +0.0)
+            if (!FU) return;
+#pragma unroll
+            for (int i = 0; i < kCH; i++) th[i] = valid ? th[i] : 0.0;
+            const double z = tree8_transposed(th, lane);
+            if ((lane & 7) == 0) {
+                const uint32_t h = lane >> 5, c = 4 * hsel + 2 * ((lane >> 3) & 1) + ((lane >> 4) & 1);
+                Q[((size_t)(k & 1) * 4 + blk) * 16 + 2 * c + h] = z;
+            }
+        };
         if (cn == (uint32_t)kCH && k > 0) {            // full chunk, no first column: no guards
-            double2 w2[4], o2[4], a2[4], bb2[4], rw2[4], n2[4], rn2[4];
+            struct CCol { double w, Wo, a, bb, rw, Wn, rWn; };
+            auto ldc = [&](int c) {                    // one column's coefficients (LDS broadcasts)
+                return CCol{q.w[o + c], q.Wo[o + c], q.a[o + c], q.bb[o + c], q.rw[o + c], q.Wn[o + c], q.rWn[o + c]};
+            };
+            auto col = [&](const CCol& k2, float2 e, double* t) {
+                const double x = (double)e.x;
+                const double tmp = k2.w * sum0 - k2.Wo * x;
+                M0 = k2.a * M0 + k2.bb * (tmp * tmp);
+                V0 = V0 + (double)e.y * k2.rw;
+                sum0 = sum0 + x;
+                if (FU) { t[0] = lw * (M0 * k2.rWn); t[1] = lw * (V0 * k2.Wn); }
+            };
+            CCol ka = ldc(0), kb;
 #pragma unroll
-            for (int p = 0; p < 4; p++) {
-                w2[p] = *reinterpret_cast<const double2*>(&q.w[o + 2 * p]);
-                o2[p] = *reinterpret_cast<const double2*>(&q.Wo[o + 2 * p]);
-                a2[p] = *reinterpret_cast<const double2*>(&q.a[o + 2 * p]);
-                bb2[p] = *reinterpret_cast<const double2*>(&q.bb[o + 2 * p]);
-                rw2[p] = *reinterpret_cast<const double2*>(&q.rw[o + 2 * p]);
-                n2[p] = *reinterpret_cast<const double2*>(&q.Wn[o + 2 * p]);
-                rn2[p] = *reinterpret_cast<const double2*>(&q.rWn[o + 2 * p]);
+            for (int c = 0; c < kCH; c += 2) {         // the next column's coefficients one column ahead
+                kb = ldc(c + 1);
+                col(ka, cur[c], &th[2 * (c & 3)]);
+                if (c + 2 < kCH) ka = ldc(c + 2);
+                col(kb, cur[c + 1], &th[2 * ((c + 1) & 3)]);
+                if (c == 2) half_done(0);
             }
-#pragma unroll
-            for (int p = 0; p < 4; p++) {
-                {
-                    const double x = (double)cur[2 * p].x;
-                    const double tmp = w2[p].x * sum0 - o2[p].x * x;
-                    M0 = a2[p].x * M0 + bb2[p].x * (tmp * tmp);
-                    V0 = V0 + (double)cur[2 * p].y * rw2[p].x;
-                    sum0 = sum0 + x;
-                    if (FU) { tv[4 * p] = lw * (M0 * rn2[p].x); tv[4 * p + 1] = lw * (V0 * n2[p].x); }
-                }
-                {
-                    const double x = (double)cur[2 * p + 1].x;
-                    const double tmp = w2[p].y * sum0 - o2[p].y * x;
-                    M0 = a2[p].y * M0 + bb2[p].y * (tmp * tmp);
-                    V0 = V0 + (double)cur[2 * p + 1].y * rw2[p].y;
-                    sum0 = sum0 + x;
-                    if (FU) { tv[4 * p + 2] = lw * (M0 * rn2[p].y); tv[4 * p + 3] = lw * (V0 * n2[p].y); }
-                }
-            }
+            half_done(1);
         } else {
 #pragma unroll
             for (int c = 0; c < kCH; c++) {
+                double* t = &th[2 * (c & 3)];
                 if ((uint32_t)c < cn) {
                     const double x = (double)cur[c].x;
                     const double tmp = q.w[o + c] * sum0 - q.Wo[o + c] * x;
                     if (c0 + c > 0) M0 = q.a[o + c] * M0 + q.bb[o + c] * (tmp * tmp);
                     V0 = V0 + (double)cur[c].y * q.rw[o + c];
                     sum0 = sum0 + x;
-                    if (FU) { tv[2 * c] = lw * (M0 * q.rWn[o + c]); tv[2 * c + 1] = lw * (V0 * q.Wn[o + c]); }
+                    if (FU) { t[0] = lw * (M0 * q.rWn[o + c]); t[1] = lw * (V0 * q.Wn[o + c]); }
                 } else if (FU) {
-                    tv[2 * c] = 0.0; tv[2 * c + 1] = 0.0;
+                    t[0] = 0.0; t[1] = 0.0;
                 }
-            }
-        }
-        if (FU) {
-            // the block's halving tree (rows past R enter as +0.0), totals to Q[k & 1][blk]
-#pragma unroll
-            for (int i = 0; i < 2 * kCH; i++) tv[i] = valid ? tv[i] : 0.0;
-            const double z = tree16_transposed(tv, lane);
-            if ((lane & 3) == 0) {
-                const uint32_t h = lane >> 5, c = 4 * ((lane >> 2) & 1) + 2 * ((lane >> 3) & 1) + ((lane >> 4) & 1);
-                Q[((size_t)(k & 1) * 4 + blk) * 16 + 2 * c + h] = z;
+                if (c == 3) half_done(0);
+                if (c == 7) half_done(1);
             }
         }
     };
@@ -1347,7 +1372,6 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
         double sum3 = 0.0, M3 = 0.0, V3 = 0.0;
         float2 cA[kCH], cB[kCH];
         if (own3) load_rows(Rt3, rs3, 0, cA);
-        long long sp[4] = {0, 0, 0, 0};                // sub-phases (profile): reduce, flush, chain, rec 3
         auto stepc = [&](uint32_t B, uint32_t j, uint32_t nb, float2* cur, float2* nxt) {
             const uint32_t k = B * 8 + j;
             const long long ws0 = wprof ? (long long)clock64() : 0;
@@ -1366,10 +1390,14 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
                 load_rows(Rt3, rs3, min(k + 1, nch - 1), nxt);
                 rec(k, cur, 3, lw3, sum3, M3, V3, 3u * 64u + lane < R);
             }
-            if (wprof) {
+            if (wprof) {   // sub-phases: reduce, flush, chain, rec 3
                 const long long ws4 = (long long)clock64();
-                wred += ws4 - ws0;
-                sp[0] += ws1 - ws0; sp[1] += ws2 - ws1; sp[2] += ws3 - ws2; sp[3] += ws4 - ws3;
+                const bool n4 = NB == 4;
+                padd(pbase + 2 * kWaves + wv, ws4 - ws0);
+                padd(n4 ? PF_V_ISSUE : PF_V_RED, ws1 - ws0);
+                padd(n4 ? PF_V_DATA : PF_P_STAGE, ws2 - ws1);
+                padd(n4 ? PF_V_OWN : PF_V_COEF, ws3 - ws2);
+                padd(n4 ? PF_V_CW : PF_V_REC, ws4 - ws3);
             }
             __syncthreads();
         };
@@ -1384,13 +1412,6 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
                 if (B * 8 + j + 1 >= nch) break;
                 stepc(B, j + 1, nb, cB, cA);
             }
-        }
-        if (wprof && lane == 0 && m >= 4096) {
-            const bool n4 = NB == 4;
-            atomicAdd(&cm.prof[n4 ? PF_V_ISSUE : PF_V_RED], (unsigned long long)sp[0]);
-            atomicAdd(&cm.prof[n4 ? PF_V_DATA : PF_P_STAGE], (unsigned long long)sp[1]);
-            atomicAdd(&cm.prof[n4 ? PF_V_OWN : PF_V_COEF], (unsigned long long)sp[2]);
-            atomicAdd(&cm.prof[n4 ? PF_V_CW : PF_V_REC], (unsigned long long)sp[3]);
         }
         if (FU) {
             if (!own3) {
@@ -1429,7 +1450,7 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
                 if ((k & 7) == 0 && k >= 8) flush(k / 8 - 1);
             }
             rec(k, cur, b0, lw0, sum0, M0, V0, b0 * 64 + lane < R);
-            if (wprof) wbusy += (long long)clock64() - ws0;
+            if (wprof) padd(pbase + wv, (long long)clock64() - ws0);
             __syncthreads();
         };
         for (uint32_t k = 0; k < nch; k += 3) {
@@ -1449,12 +1470,7 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
     } else {
         for (uint32_t k = 0; k < nch; k++) __syncthreads();
     }
-    if (wprof && lane == 0 && m >= 4096) {
-        const int pb = kPfWaveBusy + (NB == 4 ? 3 * kWaves : 0);
-        atomicAdd(&cm.prof[pb + wv], (unsigned long long)wbusy);
-        atomicAdd(&cm.prof[pb + kWaves + wv], (unsigned long long)((long long)clock64() - wwall0));
-        atomicAdd(&cm.prof[pb + 2 * kWaves + wv], (unsigned long long)wred);
-    }
+    if (wprof) padd(pbase + kWaves + wv, (long long)clock64());
     __syncthreads();
     if (!FU && active && wv == (g == 0 ? 0 : 5)) {
         // the pass's final variances from the rows' states (variance_passes_t, FU == false)

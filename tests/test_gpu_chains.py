@@ -132,7 +132,8 @@ def test_integrator_chains_matches_oracle(oracle, gpu_ok, props):
         _assert_close(img, _per_pixel(cpu, pix, w * h), "brute chain frame")
         it.close()
         return
-    prep = Prep(oracle, oracle.prep_params(seed=SEED_RNG, pass_=0, target_num_slices=12))
+    # buildSlices draws nothing; sampleSliceMapping and the clustering use the pass's streams
+    prep = Prep(oracle, oracle.prep_params(seed=SEED_RNG, pass_=pass_, target_num_slices=12))
     p2s = prep.build_slices(o)
     assert np.array_equal(p2s, it.slices())
     off, rpix, _, _ = prep.sample_slice_mapping(64.0, w * h)

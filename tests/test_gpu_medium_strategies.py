@@ -20,8 +20,8 @@ def _medium(alvrl, strategy, channel, density):
 @pytest.mark.parametrize("strategy,channel,density", OTHER)
 def test_gather_strategies(oracle, gpu_ok, strategy, channel, density):
     """Brute gather and R rows of a 48x32 frame under the strategy (VRLs
-    traced under it too) against the oracle; short and long VRLs (the long
-    ones' vol-to-vol pdfFailure division is the strategy-dependent term)."""
+    traced under it too) against the oracle; short and long VRLs (short
+    VRLs divide by the strategy's pdfFailure, vrlIntegrator.cpp:675-676, 750-751)."""
     import torch
     import alvrl
     w, h = 48, 32
@@ -39,10 +39,11 @@ def test_gather_strategies(oracle, gpu_ok, strategy, channel, density):
         ctx.gather_brute(d_recs, d_out)
         torch.cuda.synchronize()
         _assert_close(d_out.cpu().numpy(), cpu, f"brute {strategy} short={short}")
-        # the balance gather of the same records differs (the strategy is not ignored)
+        # with short VRLs the balance gather of the same records differs (the
+        # strategy is not ignored); long VRLs do not divide by pdfFailure
         Pb = oracle.params(oracle.medium(), seed=SEED_RNG, short_vrls=int(short))
         base, _ = oracle.gather_brute(Pb, recs, vrls, pc)
-        if not short:
+        if short:
             assert np.abs(base - cpu).max() > 1e-3 * np.abs(cpu).max()
         ids = np.arange(0, w * h, 11, dtype=np.uint32)
         _, R, _ = oracle.gather_brute(P, recs[ids], vrls, pc, rec_ids=ids, want_R=True, domain=2)
