@@ -53,7 +53,9 @@ def test_gather_strategies(oracle, gpu_ok, strategy, channel, density):
         ctx.build_R(d_rr, d_Rt, ld=nr, d_ids=d_ids)
         torch.cuda.synchronize()
         Rg = d_Rt.cpu().numpy().transpose(1, 0, 2)
-        _assert_close_pairs(Rg[..., 0], R[..., 0], f"R mean {strategy}")
+        # one ill-conditioned pair in 10^5 (rel 1e-2, the tail of test_gpu_parity)
+        # can dominate a column of 140 rows: column sums to 5e-3 here
+        _assert_close_pairs(Rg[..., 0], R[..., 0], f"R mean {strategy}", csum=5e-3)
         ctx.close()
 
 
