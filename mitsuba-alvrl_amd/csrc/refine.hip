@@ -1192,14 +1192,17 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
     const uint32_t nblk = (m + kCB64 - 1) / kCB64;
     auto cn_of = [&](uint32_t k) { return min((uint32_t)kCH, m - k * kCH); };
     auto ncol_of = [&](uint32_t b) { return min((uint32_t)kCB64, m - b * kCB64); };
-    // profile counters go straight to cm.prof (lane 0, per step): kept in
-    // registers across the chunk loop they cost 14 VGPRs of the budget
+    // profile counters: 32-bit per-wave sums (a split's chunk steps add up to
+    // well under 2^32 ticks), added to cm.prof once at the end; 64-bit ones
+    // cost VGPRs of the budget, and a global atomic per step would put its
+    // round trip in front of every barrier
     const bool wprof = cm.prof != nullptr && m >= 4096;
     const int pbase = kPfWaveBusy + (NB == 4 ? 3 * kWaves : 0);
     auto padd = [&](int idx, long long v) {
         if (lane == 0) atomicAdd(&cm.prof[idx], (unsigned long long)v);
     };
-    if (wprof) padd(pbase + kWaves + wv, -(long long)clock64());   // + the end time below: the wall span
+    uint32_t pc_busy = 0, pc_red = 0, pc_sp[4] = {0, 0, 0, 0};
+    const long long wall0 = wprof ? (long long)clock64() : 0;
 
     // (vrl, weight) of every column of the cluster, gathered in parallel once
     {
@@ -1247,7 +1250,9 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
     // data: their terms are never reduced), so no load or store is predicated
     const uint32_t r0 = min(b0 * 64 + lane, R - 1);
     const RowRef rr0 = roww ? row_ref(J, r0) : RowRef{0, 0};
-    const double lw0 = roww ? J.locw[r0] : 0.0;
+    // rows past R carry weight 0: their prefix terms are +0.0 exactly (M, V >= 0),
+    // which is what the reduction order wants from them (no per-term select)
+    const double lw0 = roww && b0 * 64 + lane < R ? J.locw[r0] : 0.0;
 
     // coefficient wave: the 16 row sums of chunk kk, the row blocks' tree
     // totals added in block order (wsum_blk), one sum per lane 0-15
@@ -1285,17 +1290,18 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
     // per workgroup at 101 registers).  So the coefficients
     // arrive one column ahead (not the whole chunk's 7 x 8 doubles up
     // front), and only half a chunk's terms are live at once.
-    auto rec = [&](uint32_t k, const float2* cur, uint32_t blk, double lw, double& sum0, double& M0, double& V0,
-                   bool valid) {
+    auto rec = [&](uint32_t k, const float2* cur, uint32_t blk, double lw, double& sum0, double& M0, double& V0) {
         const uint32_t c0 = k * kCH, cn = cn_of(k);
         const CoefBlock& q = ring[(k / 8) & 1];
         const uint32_t o = (k % 8) * kCH;
         double th[kCH];                                // half a chunk's prefix terms (pu, pi) per column
         auto half_done = [&](uint32_t hsel) {          // the block's halving tree (rows past R enter as +0.0)
             if (!FU) return;
-#pragma unroll
-            for (int i = 0; i < kCH; i++) th[i] = valid ? th[i] : 0.0;
+#ifdef ALVRL_EXP_NOTREE
+            const double z = th[0] + th[3] + th[6];   // timing experiment: no reduction
+#else
             const double z = tree8_transposed(th, lane);
+#endif
             if ((lane & 7) == 0) {
                 const uint32_t h = lane >> 5, c = 4 * hsel + 2 * ((lane >> 3) & 1) + ((lane >> 4) & 1);
                 Q[((size_t)(k & 1) * 4 + blk) * 16 + 2 * c + h] = z;
@@ -1366,7 +1372,7 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
         const bool own3 = NB == 4;
         const uint32_t r3 = min(3u * 64u + lane, R - 1);
         const RowRef rr3 = own3 ? row_ref(J, r3) : RowRef{0, 0};
-        const double lw3 = own3 ? J.locw[r3] : 0.0;
+        const double lw3 = own3 && 3u * 64u + lane < R ? J.locw[r3] : 0.0;
         const float2* const Rt3 = cm.Rt + rr3.base;
         const size_t rs3 = rr3.stride;
         double sum3 = 0.0, M3 = 0.0, V3 = 0.0;
@@ -1388,19 +1394,21 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
             const long long ws3 = wprof ? (long long)clock64() : 0;
             if (own3) {
                 load_rows(Rt3, rs3, min(k + 1, nch - 1), nxt);
-                rec(k, cur, 3, lw3, sum3, M3, V3, 3u * 64u + lane < R);
+                rec(k, cur, 3, lw3, sum3, M3, V3);
             }
             if (wprof) {   // sub-phases: reduce, flush, chain, rec 3
                 const long long ws4 = (long long)clock64();
-                const bool n4 = NB == 4;
-                padd(pbase + 2 * kWaves + wv, ws4 - ws0);
-                padd(n4 ? PF_V_ISSUE : PF_V_RED, ws1 - ws0);
-                padd(n4 ? PF_V_DATA : PF_P_STAGE, ws2 - ws1);
-                padd(n4 ? PF_V_OWN : PF_V_COEF, ws3 - ws2);
-                padd(n4 ? PF_V_CW : PF_V_REC, ws4 - ws3);
+                pc_red += (uint32_t)(ws4 - ws0);
+#ifndef ALVRL_EXP_STAMP
+                pc_sp[0] += (uint32_t)(ws1 - ws0); pc_sp[1] += (uint32_t)(ws2 - ws1);
+                pc_sp[2] += (uint32_t)(ws3 - ws2); pc_sp[3] += (uint32_t)(ws4 - ws3);
+#endif
             }
             __syncthreads();
         };
+#ifdef ALVRL_EXP_COEFPRIO
+        __builtin_amdgcn_s_setprio(ALVRL_EXP_COEFPRIO);
+#endif
         for (uint32_t B = 0; B * 8 < nch; B++) {
             const uint32_t nb = B + 1;
             if (nb < nblk) take(kwN, nb);
@@ -1413,6 +1421,9 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
                 stepc(B, j + 1, nb, cB, cA);
             }
         }
+#ifdef ALVRL_EXP_COEFPRIO
+        __builtin_amdgcn_s_setprio(0);
+#endif
         if (FU) {
             if (!own3) {
                 reduce(nch - 1);
@@ -1444,14 +1455,35 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
         const bool red = FU && NB == 4 && b0 == 0;
         auto step = [&](uint32_t k, float2* cur, float2* pre) {
             const long long ws0 = wprof ? (long long)clock64() : 0;
+#ifdef ALVRL_EXP_STAMP
+            // developer timing (profile builds): load issue, recurrence, barrier wait
+            auto stamp = []() {
+                unsigned long long t;
+                __builtin_amdgcn_sched_barrier(0);
+                asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+                __builtin_amdgcn_sched_barrier(0);
+                return t;
+            };
+            const unsigned long long s0 = stamp();
+#endif
             load_chunk(min(k + 2, nch - 1), pre);
+#ifdef ALVRL_EXP_STAMP
+            const unsigned long long s1 = stamp();
+#endif
             if (red) {
                 if (k >= 1) reduce(k - 1);
                 if ((k & 7) == 0 && k >= 8) flush(k / 8 - 1);
             }
-            rec(k, cur, b0, lw0, sum0, M0, V0, b0 * 64 + lane < R);
-            if (wprof) padd(pbase + wv, (long long)clock64() - ws0);
+            rec(k, cur, b0, lw0, sum0, M0, V0);
+            if (wprof) pc_busy += (uint32_t)((long long)clock64() - ws0);
+#ifdef ALVRL_EXP_STAMP
+            const unsigned long long s2 = stamp();
+#endif
             __syncthreads();
+#ifdef ALVRL_EXP_STAMP
+            const unsigned long long s3 = stamp();
+            if (wprof) { pc_sp[0] += (uint32_t)(s1 - s0); pc_sp[1] += (uint32_t)(s2 - s1); pc_sp[2] += (uint32_t)(s3 - s2); }
+#endif
         };
         for (uint32_t k = 0; k < nch; k += 3) {
             step(k, bufA, bufC);
@@ -1470,7 +1502,16 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
     } else {
         for (uint32_t k = 0; k < nch; k++) __syncthreads();
     }
-    if (wprof) padd(pbase + kWaves + wv, (long long)clock64());
+    if (wprof) {
+        const bool n4 = NB == 4;
+        padd(pbase + wv, pc_busy);
+        padd(pbase + kWaves + wv, (long long)clock64() - wall0);
+        padd(pbase + 2 * kWaves + wv, pc_red);
+        padd(n4 ? PF_V_ISSUE : PF_V_RED, pc_sp[0]);
+        padd(n4 ? PF_V_DATA : PF_P_STAGE, pc_sp[1]);
+        padd(n4 ? PF_V_OWN : PF_V_COEF, pc_sp[2]);
+        padd(n4 ? PF_V_CW : PF_V_REC, pc_sp[3]);
+    }
     __syncthreads();
     if (!FU && active && wv == (g == 0 ? 0 : 5)) {
         // the pass's final variances from the rows' states (variance_passes_t, FU == false)
