@@ -152,6 +152,9 @@ struct Common {
                                    // leader computes the initial clusters' variances (ALVRL_EARLY_SPEC=0: off)
     int team_setup;                // a job's first helper takes half the column weights and the
                                    // unclustered variance off the leader (ALVRL_TEAM_SETUP=0: off)
+    int heap_lds;                  // the leader's heap in LDS between its splits (ALVRL_HEAP_LDS=0: off)
+    uint32_t* poptr;               // ALVRL_POP_TRACE=1: wall ticks at 7 points of each leader pop of one job
+    uint32_t poptr_job, poptr_cap; // the traced job (most rows), records available
 };
 __device__ __forceinline__ void trace(const Common& cm, uint32_t phase, uint32_t value)
 {
@@ -238,6 +241,8 @@ struct Ctl {
     float diffLen, nd;
     int go, do_snap, stop, refined;
     int tmode, side;
+    unsigned long long sw;   // the popped cluster's state word, fetched by pop_wave (team mode)
+    uint32_t* prec;        // this pop's trace record (ALVRL_POP_TRACE), or null
     int team_off;          // the job's team was retired after a timed-out wait (split_team)
     uint32_t yb, ye, j;
     unsigned long long t0;
@@ -251,6 +256,8 @@ struct Ctl {
     // heap writes since the last snapshot (lane 0)
     uint32_t hlog[kHeapLog];
     int hlog_n, hlog_full;
+    int hlds;              // the heap is in the LDS pool (team mode, between splits), else in J.heap
+    void* hpool;           // the LDS pool (generic address; accessed through typed LDS pointers only)
 };
 
 // ------------------------------------------------------------ helpers --
@@ -437,29 +444,54 @@ __device__ __forceinline__ bool cless(const CNode& a, const CNode& b)
 {
     return a.uvar + a.ivar < b.uvar + b.ivar;
 }
-// The heap lives in global memory and is worked by lane 0.  Typed global
-// accesses (not flat: a flat op makes the next LDS wait drain every load in
-// flight), and every write is logged so a snapshot copies only what changed.
+// The heap is worked by lane 0 (pops by wave 0).  It lives in J.heap, and in
+// team mode the leader keeps it in the LDS pool between splits (heap_move):
+// each pop's sift-down is a chain of dependent heap reads, and at N >= 4 GPUs
+// the leader's pops are the refinement's critical path.  Accesses are typed
+// LDS or typed global ones on a uniform branch (HeapRef), never flat: flat
+// accesses to LDS faulted on this platform (memory aperture violation).
+// Every write is logged so a snapshot copies only what changed.
 typedef uint32_t hnode_v __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) hnode_v* hnode_p;
+typedef __attribute__((address_space(3))) hnode_v* hnode_l;
 __device__ __forceinline__ hnode_p hnodes(CNode* p) { return (hnode_p)p; }
+struct HeapRef {
+    hnode_p g;
+    hnode_l l;
+    int lds;
+    __device__ __forceinline__ hnode_v ld(long i) const
+    {
+        if (lds) return l[i];
+        return g[i];
+    }
+    __device__ __forceinline__ void st(long i, hnode_v v) const
+    {
+        if (lds) l[i] = v;
+        else g[i] = v;
+    }
+};
 __device__ __forceinline__ CNode hld(hnode_p H, long i)
 {
     const hnode_v v = H[i];
     return CNode{__uint_as_float(v.x), __uint_as_float(v.y), v.z, v.w};
 }
-__device__ __forceinline__ void hst(hnode_p H, long i, const CNode& c)
+__device__ __forceinline__ CNode hld(const HeapRef& H, long i)
 {
-    H[i] = hnode_v{__float_as_uint(c.uvar), __float_as_uint(c.ivar), c.begin, c.end};
+    const hnode_v v = H.ld(i);
+    return CNode{__uint_as_float(v.x), __uint_as_float(v.y), v.z, v.w};
 }
+__device__ __forceinline__ void hst(const HeapRef& H, long i, const CNode& c)
+{
+    H.st(i, hnode_v{__float_as_uint(c.uvar), __float_as_uint(c.ivar), c.begin, c.end});
+}
+constexpr int kHeapLdsMax = (int)(kPoolBytes / sizeof(hnode_v));
 __device__ __forceinline__ void heap_log(Ctl& C, long i)
 {
     if (C.hlog_n < kHeapLog) C.hlog[C.hlog_n++] = (uint32_t)i;
     else C.hlog_full = 1;
 }
-__device__ void push_heap_(CNode* first_g, long hole, long top, CNode value, Ctl& C)
+__device__ void push_heap_(const HeapRef& first, long hole, long top, CNode value, Ctl& C)
 {
-    const hnode_p first = hnodes(first_g);
     long parent = (hole - 1) / 2;
     while (hole > top) {
         const CNode pn = hld(first, parent);
@@ -472,42 +504,29 @@ __device__ void push_heap_(CNode* first_g, long hole, long top, CNode value, Ctl
     hst(first, hole, value);
     heap_log(C, hole);
 }
-__device__ void adjust_heap(CNode* first_g, long hole, long len, CNode value, Ctl& C)
-{
-    const hnode_p first = hnodes(first_g);
-    const long top = hole;
-    long second = hole;
-    while (second < (len - 1) / 2) {
-        second = 2 * (second + 1);
-        const CNode r = hld(first, second), l = hld(first, second - 1);
-        const bool left = cless(r, l);
-        if (left) second--;
-        hst(first, hole, left ? l : r);
-        heap_log(C, hole);
-        hole = second;
-    }
-    if ((len & 1) == 0 && second == (len - 2) / 2) {
-        second = 2 * (second + 1);
-        hst(first, hole, hld(first, second - 1));
-        heap_log(C, hole);
-        hole = second - 1;
-    }
-    push_heap_(first_g, hole, top, value, C);
-}
 
+__device__ __forceinline__ HeapRef heap_of(const JobDev& J, const Ctl& C)
+{
+    return HeapRef{hnodes(J.heap), lp(reinterpret_cast<hnode_v*>(C.hpool)), C.hlds};
+}
 // lane-0-only Clustering::addCluster (:549-579)
-__device__ void add_cluster(const JobDev& J, Ctl& C, uint32_t begin, uint32_t end, float uvar, float ivar)
+// (a single's id is read from J.vrls, or with an agent-scope load from spec:
+// a commit's range copy into J.vrls may still be in flight)
+__device__ void add_cluster(const JobDev& J, Ctl& C, uint32_t begin, uint32_t end, float uvar, float ivar,
+                            const uint32_t* spec = nullptr)
 {
     if (end == begin) { C.err = 1; return; }
     if (end == begin + 1) {
-        gpw(J.singles)[C.singles_n++] = gp(J.vrls)[begin];
+        gpw(J.singles)[C.singles_n++] =
+            spec ? __hip_atomic_load(&gp(spec)[begin], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : gp(J.vrls)[begin];
         if (uvar != 0) C.err = 1;
         C.clIntVar += ivar;
     } else {
         CNode cn{uvar, ivar, begin, end};
-        hst(hnodes(J.heap), C.heap_n++, cn);
+        const HeapRef H = heap_of(J, C);
+        hst(H, C.heap_n++, cn);
         heap_log(C, C.heap_n - 1);
-        push_heap_(J.heap, C.heap_n - 1, 0, cn, C);
+        push_heap_(H, C.heap_n - 1, 0, cn, C);
         C.clUnderVar += uvar;
         C.clIntVar += ivar;
     }
@@ -521,12 +540,16 @@ __device__ void add_cluster(const JobDev& J, Ctl& C, uint32_t begin, uint32_t en
 // moved last element then climbs that path while the node above it is less
 // (__push_heap), which only needs the path's original values: lane i holds
 // path node i.  Final array = std::pop_heap's; the slots written are logged.
-__device__ CNode pop_wave(const JobDev& J, Ctl& C)
+// With state set (team mode), lane 0 also fetches the popped cluster's state
+// word while the sift-down runs (split_team's first look): C.sw.
+__device__ CNode pop_wave(const JobDev& J, Ctl& C, const unsigned long long* state = nullptr)
 {
     const int lane = (int)(threadIdx.x & 63);
-    const hnode_p H = hnodes(J.heap);
+    const HeapRef H = heap_of(J, C);
     const long n = __builtin_amdgcn_readfirstlane(C.heap_n);
     const CNode top = hld(H, 0);
+    unsigned long long sw = 0;
+    if (state && lane == 0) sw = __hip_atomic_load(&gp(state)[top.begin], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (n > 1) {
         const long len = n - 1;
         const CNode value = hld(H, len);
@@ -542,7 +565,7 @@ __device__ CNode pop_wave(const JobDev& J, Ctl& C)
             const long idx = ((h + 1) << k) - 1 + j;
             const bool ex = lane < 62 && idx < len;
             hnode_v v = {0u, 0u, 0u, 0u};
-            if (ex) v = H[idx];
+            if (ex) v = H.ld(idx);
             const float key = __uint_as_float(v.x) + __uint_as_float(v.y);
             const float skey = __shfl_xor(key, 1);
             const int sex = __shfl_xor((int)ex, 1);
@@ -574,7 +597,7 @@ __device__ CNode pop_wave(const JobDev& J, Ctl& C)
         hnode_v up;
         up.x = __shfl_down(pv.x, 1); up.y = __shfl_down(pv.y, 1);
         up.z = __shfl_down(pv.z, 1); up.w = __shfl_down(pv.w, 1);
-        if (lane < fin) H[pidx] = up;
+        if (lane < fin) H.st(pidx, up);
         if (lane == fin) hst(H, pidx, value);
         if (lane == 0) hst(H, len, top);
         const int base = C.hlog_n, w = fin + 2;
@@ -589,6 +612,7 @@ __device__ CNode pop_wave(const JobDev& J, Ctl& C)
         C.heap_n = (int)n - 1;
         C.clUnderVar -= top.uvar;
         C.clIntVar -= top.ivar;
+        if (state) C.sw = sw;
     }
     return top;
 }
@@ -616,16 +640,16 @@ __device__ float lower_bound(Ctl& C, uint32_t nvrl, float pu)
 __device__ void snapshot(const JobDev& J, Ctl& C)
 {
     const int nh = C.heap_n, ns = C.singles_n;
-    const hnode_p H = hnodes(J.heap);
+    const HeapRef H = heap_of(J, C);
     const hnode_p SH = hnodes(J.sh_heap);
     if (C.hlog_full) {
-        for (int i = threadIdx.x; i < nh; i += kThreads) SH[i] = H[i];
+        for (int i = threadIdx.x; i < nh; i += kThreads) SH[i] = H.ld(i);
         for (int i = threadIdx.x; i < ns; i += kThreads) gpw(J.sh_singles)[i] = gp(J.singles)[i];
     } else {
         const int nl = C.hlog_n;
         for (int t = threadIdx.x; t < nl; t += kThreads) {
             const uint32_t i = C.hlog[t];
-            if ((int)i < nh) SH[i] = H[i];
+            if ((int)i < nh) SH[i] = H.ld(i);
         }
         for (int i = C.sh_singles_n + threadIdx.x; i < ns; i += kThreads) gpw(J.sh_singles)[i] = gp(J.singles)[i];
     }
@@ -642,16 +666,16 @@ __device__ void restore(const JobDev& J, Ctl& C)
     // The singles below the snapshot's count never change (appends only), and
     // the heap differs from the snapshot only where the log says.
     const int nh = C.sh_heap_n, ns = C.sh_singles_n;
-    const hnode_p H = hnodes(J.heap);
+    const HeapRef H = heap_of(J, C);
     const hnode_p SH = hnodes(J.sh_heap);
     if (C.hlog_full) {
-        for (int i = threadIdx.x; i < nh; i += kThreads) H[i] = SH[i];
+        for (int i = threadIdx.x; i < nh; i += kThreads) H.st(i, SH[i]);
         for (int i = threadIdx.x; i < ns; i += kThreads) gpw(J.singles)[i] = gp(J.sh_singles)[i];
     } else {
         const int nl = C.hlog_n;
         for (int t = threadIdx.x; t < nl; t += kThreads) {
             const uint32_t i = C.hlog[t];
-            if ((int)i < nh) H[i] = SH[i];
+            if ((int)i < nh) H.st(i, SH[i]);
         }
     }
     __syncthreads();
@@ -660,6 +684,27 @@ __device__ void restore(const JobDev& J, Ctl& C)
         C.heap_n = nh; C.singles_n = ns;
         C.hlog_n = 0; C.hlog_full = 0;
     }
+    __syncthreads();
+}
+
+// Collective: move the heap into the LDS pool (to_lds, if it fits with room
+// for one more split's net growth) or back to J.heap.  The pool is the split
+// engines' scratch, so the heap goes back before any split by this workgroup
+// and before the representatives.  Content and order are unchanged.
+__device__ void heap_move(const JobDev& J, Ctl& C, bool to_lds)
+{
+    __syncthreads();
+    const int n = C.heap_n;
+    const bool cur = C.hlds != 0;
+    if (to_lds ? (cur || n + 2 > kHeapLdsMax) : !cur) return;   // uniform
+    const hnode_p G = hnodes(J.heap);
+    const hnode_l L = lp(reinterpret_cast<hnode_v*>(C.hpool));
+    for (int i = threadIdx.x; i < n; i += kThreads) {
+        if (to_lds) L[i] = G[i];
+        else G[i] = L[i];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) C.hlds = to_lds ? 1 : 0;
     __syncthreads();
 }
 
@@ -2111,7 +2156,16 @@ __device__ void split(const JobDev& J, const Common& cm, Ctl& C, uint32_t begin,
     __syncthreads();
     pf.mark(PF_PROJ);
     const unsigned long long* sorted = sort_keys(J, C, m, lds);
-    for (uint32_t i = tid; i < m; i += kThreads) vrlsW[begin + i] = (uint32_t)gp(sorted)[i];
+    // a speculative split's range and result are handed to the leader, which
+    // reads them with agent-scope loads and no acquire (MI355X_MICROARCH.md,
+    // valid forms: every store of the handed-off bytes sc1 and drained before
+    // the flag, every load of them sc1): agent-scope (sc1) stores here
+    if (commit) {
+        for (uint32_t i = tid; i < m; i += kThreads) vrlsW[begin + i] = (uint32_t)gp(sorted)[i];
+    } else {
+        for (uint32_t i = tid; i < m; i += kThreads)
+            __hip_atomic_store(&vrlsW[begin + i], (uint32_t)gp(sorted)[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     __syncthreads();
     pf.mark(PF_SORT);
     const long long hv0 = pf.p && tid == 0 ? (long long)clock64() : 0;
@@ -2155,7 +2209,11 @@ __device__ void split(const JobDev& J, const Common& cm, Ctl& C, uint32_t begin,
                 r.fsu = pref(0, idx - 1); r.fsi = pref(1, idx - 1);
                 r.feu = pref(2, m - 1 - idx); r.fei = pref(3, m - 1 - idx);
             }
-            *res = r;
+            auto* const rw = gpw(reinterpret_cast<uint32_t*>(res));   // sc1 stores, see the range above
+            const uint32_t* rv = reinterpret_cast<const uint32_t*>(&r);
+#pragma unroll
+            for (int k = 0; k < (int)(sizeof(SplitRes) / 4); k++)
+                __hip_atomic_store(&rw[k], rv[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else if (idx == 0xFFFFFFFFu) {
             Cs.err = 1;
         } else {
@@ -2238,6 +2296,11 @@ __device__ __forceinline__ void drain_vmem() { asm volatile("s_waitcnt vmcnt(0)"
 // team.state is read again), an idle helper gives up after spin_ticks
 // without a task.
 __device__ __forceinline__ unsigned long long wall() { return __builtin_amdgcn_s_memrealtime(); }
+// thread 0: trace point k of the current pop (ALVRL_POP_TRACE)
+__device__ __forceinline__ void pmark(const Ctl& C, int k)
+{
+    if (threadIdx.x == 0 && C.prec) gpw(C.prec)[k] = (uint32_t)wall();
+}
 constexpr unsigned long long kSpinTicks = 6000000000ull;   // default of Common::spin_ticks
 
 // Thread 0 of the leader: queue the multi-clusters near the top of the heap
@@ -2258,7 +2321,7 @@ __device__ void enqueue_candidates(const JobDev& J, const Common& cm, Ctl& C)
     unsigned long long spec = 0;
     CNode cn{0.0f, 0.0f, 0u, 0u};
     if ((int)lane < K) {
-        cn = hld(hnodes(J.heap), lane);
+        cn = hld(heap_of(J, C), lane);
         if (cn.end - cn.begin >= cm.spec_min) {
             const unsigned long long sv = ld_rlx(&T.state[cn.begin]);
             const bool mine = (uint32_t)(sv >> 3) == cn.end;
@@ -2321,6 +2384,28 @@ __device__ void copy_range(uint32_t* dst, const uint32_t* src, uint32_t b, uint3
         for (uint32_t k = 0; k < U; k++) {
             const uint32_t i = i0 + k * kThreads;
             v[k] = i < e ? sp[i] : 0u;
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < U; k++) {
+            const uint32_t i = i0 + k * kThreads;
+            if (i < e) d[i] = v[k];
+        }
+    }
+}
+
+// copy_range with agent-scope (sc1) loads: the leader's commit of a result a
+// helper stored with sc1 stores (split), read without an acquire
+__device__ void copy_range_sc1(uint32_t* dst, const uint32_t* src, uint32_t b, uint32_t e)
+{
+    const auto d = gpw(dst);
+    const auto sp = gp(src);
+    constexpr uint32_t U = 8;
+    for (uint32_t i0 = b + threadIdx.x; i0 < e; i0 += U * kThreads) {
+        uint32_t v[U];
+#pragma unroll
+        for (uint32_t k = 0; k < U; k++) {
+            const uint32_t i = i0 + k * kThreads;
+            v[k] = __hip_atomic_load(&sp[i < e ? i : b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
 #pragma unroll
         for (uint32_t k = 0; k < U; k++) {
@@ -2402,16 +2487,23 @@ __device__ void split_team(const JobDev& J, const Common& cm, Ctl& C, uint32_t b
                            unsigned long long* lds, Prof& pf, bool spec)
 {
     const Team& T = J.team;
-    if (!T.helpers || !spec || C.team_off) { split(J, cm, C, b, e, lds, pf); return; }
+    if (!T.helpers || !spec || C.team_off) { heap_move(J, C, false); split(J, cm, C, b, e, lds, pf); return; }
     const int tid = threadIdx.x;
+    if (C.hlds && C.heap_n + 2 > kHeapLdsMax) heap_move(J, C, false);   // uniform (after the caller's barrier)
+    bool parked = false;   // the heap went back to global memory for a split here
     if (tid < 64 && cm.enq_start) enqueue_candidates(J, cm, C);
     if (tid == 0) {
         trace(cm, 3, b);
         unsigned long long* st = &T.state[b];
         const unsigned long long key = (unsigned long long)e << 3;
-        unsigned long long sv = ld_rlx(st);
+        // the word pop_wave fetched: since then it can only have moved on
+        // (queued -> running -> done), which the CAS and the wait loop see
+        const unsigned long long sv = C.sw;
         int mode = 0;
-        if ((uint32_t)(sv >> 3) == e && (sv & 7) != kStNone && (sv & 7) != kStLeader) {
+        if ((uint32_t)(sv >> 3) == e && (sv & 7) == kStDone) {
+            mode = 1;   // finished already: commit (sc1 loads of the sc1-stored result, no acquire)
+            tcount(cm, TS_COMMIT);
+        } else if ((uint32_t)(sv >> 3) == e && (sv & 7) != kStNone && (sv & 7) != kStLeader) {
             if ((sv & 7) == kStQueued && cas_rlx(st, sv, key | kStLeader)) {
                 mode = 0;
                 tcount(cm, TS_STEAL);
@@ -2428,6 +2520,7 @@ __device__ void split_team(const JobDev& J, const Common& cm, Ctl& C, uint32_t b
     }
     __syncthreads();
     pf.mark(PF_T_STATE);
+    pmark(C, 2);
     while (true) {
         const int tm = C.tmode;
         __syncthreads();   // every thread has read tmode before thread 0 rewrites it
@@ -2436,9 +2529,7 @@ __device__ void split_team(const JobDev& J, const Common& cm, Ctl& C, uint32_t b
             const unsigned long long sv = ld_rlx(&T.state[b]);
             C.side = 0;
             if ((sv & 7) == kStDone && (uint32_t)(sv >> 3) == e) {
-                fence_acq();   // the CU's one acquire, complete before the loop's barriers
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                C.tmode = 1;
+                C.tmode = 1;   // the commit reads the result with sc1 loads: no acquire
                 tcount(cm, TS_COMMIT);
             } else if (wall() - C.t0 > cm.wait_ticks) {
                 // give up on the helper: it still owns team.spec[b, e),
@@ -2456,43 +2547,67 @@ __device__ void split_team(const JobDev& J, const Common& cm, Ctl& C, uint32_t b
         }
         __syncthreads();
         pf.mark(PF_T_WAIT);
-        if (C.side) spec_split(J, J_spec(J), cm, C, lds, C.yb, C.ye);
+        if (C.side) {
+            if (C.hlds) { heap_move(J, C, false); parked = true; }
+            spec_split(J, J_spec(J), cm, C, lds, C.yb, C.ye);
+        }
         __syncthreads();
         pf.mark(PF_T_SIDE);
     }
     const int mode = C.tmode;
+    pmark(C, 3);
+    if (tid == 0 && C.prec) gpw(C.prec)[7] = (uint32_t)mode | (min(e - b, 0xFFFFFFu) << 8);
     if (C.team_off) {   // set by thread 0 before the loop's last barrier
         stop_team(J, cm);
+        heap_move(J, C, false);
         split(J, cm, C, b, e, lds, pf);
         return;
     }
     if (mode == 0) {
+        if (C.hlds) { heap_move(J, C, false); parked = true; }
         split(J, cm, C, b, e, lds, pf);
-    } else if (mode == 1) {
-        copy_range(J.vrls, T.spec, b, e);
-        __syncthreads();
+    }
+    if (parked) heap_move(J, C, true);
+    if (mode == 1) {
+        // the result and the range were stored sc1 and drained before the done
+        // flag (split, spec_split): sc1 loads, no acquire, and no barrier:
+        // thread 0 pushes the children (a single's id from the spec range)
+        // while the range copy is in flight; wave 0 then queues (below), and
+        // the range's readers come after later barriers
+        SplitRes r;
         if (tid == 0) {
-            const SplitRes r = T.res[b];
+            const auto* rr = gp(reinterpret_cast<const uint32_t*>(&T.res[b]));
+            uint32_t* rv = reinterpret_cast<uint32_t*>(&r);
+#pragma unroll
+            for (int k = 0; k < (int)(sizeof(SplitRes) / 4); k++)
+                rv[k] = __hip_atomic_load(&rr[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        copy_range_sc1(J.vrls, T.spec, b, e);
+        if (tid == 0) {
             if (r.err || r.idx == 0xFFFFFFFFu) {
                 C.err = 1;
             } else {
                 const uint32_t m = e - b, s2 = b + r.idx;
-                add_cluster(J, C, b, s2, r.fsu, r.fsi);
-                add_cluster(J, C, s2, e, r.feu, r.fei);
+                add_cluster(J, C, b, s2, r.fsu, r.fsi, T.spec);
+                add_cluster(J, C, s2, e, r.feu, r.fei, T.spec);
                 // the children's input is this result, in team.spec
                 st_rlx(&T.state[b], ((unsigned long long)s2 << 3) | kStNone | kStSpecBit);
                 st_rlx(&T.state[s2], ((unsigned long long)e << 3) | kStNone | kStSpecBit);
                 (void)m;
             }
         }
-        __syncthreads();
         pf.mark(PF_T_COMMIT);
     }
+    pmark(C, 4);
     // an own split releases its vrls (every wave drained, barrier, one
     // write-back) before its children can be queued; a committed one's
     // children read team.spec
-    drain_vmem();
-    __syncthreads();
+    if (mode == 0) {
+        drain_vmem();
+        __syncthreads();
+    } else if (mode == 1 && tid < 64 && !C.hlds) {
+        drain_vmem();   // wave 0 queues from the global heap thread 0 just wrote
+    }
     if (tid < 64) {
         if (mode == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         enqueue_candidates(J, cm, C);
@@ -2500,6 +2615,7 @@ __device__ void split_team(const JobDev& J, const Common& cm, Ctl& C, uint32_t b
     if (tid == 0) trace(cm, 5, b);
     __syncthreads();
     pf.mark(PF_T_ENQ);
+    pmark(C, 5);
 }
 
 // Setup tasks of a job's first helper (Team::ctl words 4-9, zeroed per
@@ -2898,6 +3014,8 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
         C.heap_n = C.singles_n = C.sh_heap_n = C.sh_singles_n = 0;
         C.err = 0; C.refined = 1; C.team_off = 0;
         C.hlog_n = 0; C.hlog_full = 1;
+        C.prec = nullptr;
+        C.hlds = 0; C.hpool = pool;
     }
     __syncthreads();
     const bool tsu = cm.team_setup && cm.team > 1 && J.team.helpers != 0;
@@ -2970,12 +3088,13 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
         if (J.undersampling > 0) {
             // refineFixedDepth (:387-399)
             const uint32_t target = (uint32_t)(0.5 + (double)((float)N / J.undersampling));
+            if (J.team.helpers && cm.heap_lds) heap_move(J, C, true);
             while (true) {
                 if (tid < 64) {   // wave 0 decides (every lane reads C itself) and pops (pop_wave)
                     const bool go = (n_clusters(C) < target && C.heap_n > 0 && !C.err);
                     if (tid == 0) C.go = go;
                     if (go) {
-                        const CNode cn = pop_wave(J, C);
+                        const CNode cn = pop_wave(J, C, J.team.helpers && !C.team_off ? J.team.state : nullptr);
                         if (tid == 0) { C.b = cn.begin; C.e = cn.end; split_cols += cn.end - cn.begin; }
                     }
                 }
@@ -2983,6 +3102,7 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
                 if (!C.go) break;
                 split_team(J, cm, C, C.b, C.e, lds, pf, true);
             }
+            heap_move(J, C, false);
         } else {
             // refineAdaptively (:402-489)
             const float dc = J.depth_correction;
@@ -2999,18 +3119,26 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
                 __shared__ int nsplit, bestN;
                 if (tid == 0) { best = conv_const(C, N, J.pixel_under); nsplit = 0; bestN = 0; }
                 snapshot(J, C);
+                if (J.team.helpers && cm.heap_lds) heap_move(J, C, true);
+                uint32_t npop = 0;
                 while (true) {
+                    if (tid == 0) {
+                        C.prec = cm.poptr && blockIdx.x == cm.poptr_job && npop < cm.poptr_cap ? cm.poptr + 8 * npop : nullptr;
+                        npop++;
+                    }
+                    pmark(C, 0);
                     if (tid < 64) {   // wave 0 decides (every lane reads C itself) and pops (pop_wave)
                         const bool go = C.heap_n > 0 && !C.err;
                         if (tid == 0) C.go = go;
                         if (go) {
-                            const CNode cn = pop_wave(J, C);
+                            const CNode cn = pop_wave(J, C, J.team.helpers && !C.team_off ? J.team.state : nullptr);
                             if (tid == 0) { C.b = cn.begin; C.e = cn.end; split_cols += cn.end - cn.begin; }
                         }
                     }
                     __syncthreads();
                     if (!C.go) break;
                     pf.mark(PF_T_HEAP);
+                    pmark(C, 1);
                     split_team(J, cm, C, C.b, C.e, lds, pf, true);
                     if (tid == 0) {
                         nsplit++;
@@ -3027,9 +3155,12 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
                     pf.mark(PF_T_HEAP);
                     if (C.do_snap) snapshot(J, C);
                     pf.mark(PF_T_SNAP);
+                    pmark(C, 6);
                     if (C.stop) break;
                 }
+                if (tid == 0) C.prec = nullptr;
                 stop_team(J, cm);
+                heap_move(J, C, false);
                 restore(J, C);
                 if (dc != 1) {
                     const int corrected = (int)(0.5 + dc * bestN);
@@ -3453,6 +3584,8 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
         cm.team_setup = tsu ? std::atoi(tsu) : 1;
         const char* esp = std::getenv("ALVRL_EARLY_SPEC");
         cm.early_spec = esp ? std::atoi(esp) : 1;
+        const char* hl = std::getenv("ALVRL_HEAP_LDS");
+        cm.heap_lds = hl ? std::atoi(hl) : 1;
     }
     // ALVRL_ROAM_ORDER=1: roaming helpers scan the jobs with the most rows
     // first.  Measured slower (C4 refine 436 vs 420 ms: the roamers crowd the
@@ -3483,6 +3616,21 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
     const char* pe = std::getenv("ALVRL_REFINE_PROFILE");
     if (pe && pe[0] == '1' && hipMalloc(&cm.prof, kPfTotal * 8) == hipSuccess)
         (void)hipMemsetAsync(cm.prof, 0, kPfTotal * 8, s);
+    // ALVRL_POP_TRACE=1: the leader of the job with the most rows records the
+    // wall clock at 7 points of each pop (tools: the summary printed below)
+    cm.poptr = nullptr; cm.poptr_job = 0; cm.poptr_cap = 0;
+    {
+        const char* pt = std::getenv("ALVRL_POP_TRACE");
+        if (pt && pt[0] == '1') {
+            uint32_t jm = 0;
+            for (uint32_t j = 1; j < njobs; j++) if (jobs[j].nrows > jobs[jm].nrows) jm = j;
+            cm.poptr_job = jm; cm.poptr_cap = 32768;
+            if (hipMalloc(&cm.poptr, (size_t)cm.poptr_cap * 32) == hipSuccess)
+                (void)hipMemsetAsync(cm.poptr, 0, (size_t)cm.poptr_cap * 32, s);
+            else
+                cm.poptr = nullptr;
+        }
+    }
     hipEvent_t e0 = nullptr, e1 = nullptr;
     e = hipEventCreate(&e0);
     if (e == hipSuccess) e = hipEventCreate(&e1);
@@ -3585,6 +3733,65 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
             }
             hipFree(cm.jtime);
         }
+    }
+    if (cm.poptr) {
+        std::vector<uint32_t> pr((size_t)cm.poptr_cap * 8);
+        if (hipMemcpy(pr.data(), cm.poptr, pr.size() * 4, hipMemcpyDeviceToHost) == hipSuccess) {
+            // segments (100 MHz ticks -> us): pop, state, wait loop, commit or own split,
+            // release + queueing, convergence test + snapshot, back to the next pop
+            const char* nm[7] = {"pop", "state check", "wait loop", "commit/own split", "queueing", "conv+snapshot", "loop"};
+            std::vector<double> seg[7], segc[7];
+            uint32_t n = 0, nc = 0;
+            for (uint32_t p = 0; p < cm.poptr_cap; p++) {
+                const uint32_t* r = &pr[(size_t)p * 8];
+                if (r[0] == 0 || r[6] == 0) break;
+                const bool quick = (r[7] & 255u) == 1 && (r[3] - r[2]) < 500;   // committed, waited < 5 us
+                for (int k = 0; k < 7; k++) {
+                    const uint32_t a = r[k], b = k < 6 ? r[k + 1] : (p + 1 < cm.poptr_cap ? pr[(size_t)(p + 1) * 8] : 0u);
+                    if (k == 6 && b == 0) continue;
+                    seg[k].push_back((b - a) * 1e-2);
+                    if (quick) segc[k].push_back((b - a) * 1e-2);
+                }
+                n++; nc += quick;
+            }
+            auto stat = [](std::vector<double> v, double* mean, double* p50, double* p90) {
+                if (v.empty()) { *mean = *p50 = *p90 = 0; return; }
+                double t = 0; for (double x : v) t += x;
+                std::sort(v.begin(), v.end());
+                *mean = t / v.size(); *p50 = v[v.size() / 2]; *p90 = v[v.size() * 9 / 10];
+            };
+            std::fprintf(stderr, "[pop trace] job %u (%u rows): %u pops, %u committed without a wait; us per pop "
+                         "(all: mean p50 p90 | committed w/o wait: mean p50)\n", cm.poptr_job, jobs[cm.poptr_job].nrows, n, nc);
+            double tot = 0, totc = 0;
+            for (int k = 0; k < 7; k++) {
+                double m, a, b, mc, ac, bc;
+                stat(seg[k], &m, &a, &b); stat(segc[k], &mc, &ac, &bc);
+                tot += m * seg[k].size(); totc += mc;
+                std::fprintf(stderr, "  %-18s %8.2f %8.2f %8.2f | %8.2f %8.2f\n", nm[k], m, a, b, mc, ac);
+            }
+            std::fprintf(stderr, "  total %.1f ms over the pops; a committed pop without a wait %.2f us\n", tot * 1e-3, totc);
+            // waits (wait loop > 5 us) by log2 of the popped cluster's size, and when they happen
+            double wt[32] = {0}; uint32_t wn[32] = {0};
+            for (uint32_t p = 0; p < n; p++) {
+                const uint32_t* r = &pr[(size_t)p * 8];
+                const double w = (r[3] - r[2]) * 1e-2;
+                if (w < 5.0) continue;
+                const uint32_t m = r[7] >> 8;
+                const int lb = m ? 31 - __builtin_clz(m) : 0;
+                wt[lb] += w; wn[lb]++;
+            }
+            for (int lb = 0; lb < 32; lb++)
+                if (wn[lb]) std::fprintf(stderr, "  waits on clusters of %7u-%7u columns: %5u, %8.2f ms, %8.1f us each\n",
+                                         1u << lb, (2u << lb) - 1, wn[lb], wt[lb] * 1e-3, wt[lb] / wn[lb]);
+            const uint32_t t0 = pr[0];
+            for (int q = 1; q <= 4; q++) {   // pops done by each quarter of the traced time
+                const uint32_t lim = t0 + (uint32_t)((double)(pr[(size_t)(n - 1) * 8 + 6] - t0) * q / 4);
+                uint32_t c = 0;
+                while (c < n && pr[(size_t)c * 8 + 6] <= lim) c++;
+                std::fprintf(stderr, "  pops finished by %d/4 of the time: %u\n", q, c);
+            }
+        }
+        hipFree(cm.poptr);
     }
     if (cm.prof) {
         unsigned long long h[kPfTotal];
