@@ -25,6 +25,9 @@ Multi-GPU (--shard):
                     xGMI sums the N passes' framebuffers into rank 0 -- the
                     progressive accumulation (integrator.cpp:396-433) spread
                     over GPUs.  Per-GPU work is fixed: "scaling": "weak".
+With N > 1 and slices, the same run also times the passes decomposition
+(W + K more steps) and reports it as "alt_decomposition" beside the line
+(--no-alt skips it); "value" is always the slices measurement.
 """
 from __future__ import annotations
 
@@ -74,6 +77,8 @@ def parse():
     ap.add_argument("--shard", default="slices", choices=["passes", "slices"],
                     help="multi-GPU decomposition (see the module docstring)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-alt", action="store_true",
+                    help="N > 1 with --shard slices: skip the second, pass-parallel measurement")
     ap.add_argument("--cpu-row-stride", type=int, default=64,
                     help="CPU baseline sample: every n-th image row")
     ap.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "r02_pmc_traffic.json"),
@@ -90,6 +95,8 @@ def aggregate_over_ranks(elapsed, counts, world, device):
         return elapsed, [int(c) for c in counts]
     import torch
     import torch.distributed as dist
+    if dist.get_backend() == "gloo":
+        device = torch.device("cpu")
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     c = torch.tensor([float(x) for x in counts], dtype=torch.float64, device=device)
@@ -114,10 +121,17 @@ def main():
     if world < cfg0.get("min_world", 1) or (cfg0.get("shard") and args.shard != cfg0["shard"]):
         raise SystemExit(f"{args.config} needs --shard {cfg0.get('shard', args.shard)} on >= "
                          f"{cfg0.get('min_world', 1)} GPUs (R does not fit one GPU)")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # rehearsal of the N > 1 path on a one-GPU box (never for a measurement):
+    # ALVRL_BENCH_ONE_GPU=1 puts every rank on cuda:0 and uses gloo
+    rehearse = os.environ.get("ALVRL_BENCH_ONE_GPU") == "1"
+    gpu = 0 if rehearse else local
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     cfg = CONFIGS[args.config]
     W, H = cfg["w"], cfg["h"]
@@ -126,7 +140,7 @@ def main():
     # resident for every pass exactly like the reference's vrlFile mode.
     vrls, pc = alvrl.trace_vrls(scene, cfg["nvrl"], seed=SEED_VRL)
     props = cfg["props"] + (";" if cfg["props"] else "") + f"seed={SEED_RNG}"
-    it = alvrl.Integrator(props, device=local)
+    it = alvrl.Integrator(props, device=gpu)
     it.set_vrls(vrls, pc)
     it.preprocess(scene)
     clustered = "localRefinement=false" not in props
@@ -134,9 +148,9 @@ def main():
     stream = torch.cuda.current_stream(dev).cuda_stream
 
     by_slices = args.shard == "slices"
-    exchange = alvrl.Exchange(device=dev) if (world > 1 and by_slices) else None
+    exchange = alvrl.Exchange(device=None if rehearse else dev) if (world > 1 and by_slices) else None
 
-    def step(i):
+    def step(i, by_slices=by_slices):
         fb.zero_()
         if by_slices:   # one pass, LightSlice work and tiles sharded over ranks
             it.prepass(i, rank, world, exchange)
@@ -145,7 +159,12 @@ def main():
             it.prepass(i * world + rank)
             it.render(fb, 0, 1, stream=stream)
         if world > 1:
-            dist.reduce(fb, dst=0)   # the single RCCL framebuffer reduce per step
+            if rehearse:
+                h = fb.cpu()
+                dist.reduce(h, dst=0)
+                fb.copy_(h)
+            else:
+                dist.reduce(fb, dst=0)   # the single RCCL framebuffer reduce per step
 
     def barrier():
         torch.cuda.synchronize(dev)
@@ -179,6 +198,29 @@ def main():
         elapsed, [contrib, render_pairs, pre_pairs], world, dev)
 
     value = contrib / elapsed
+
+    # N > 1: the other decomposition too, on the same ranks and scene
+    # (reported beside the line, never as its value): whole progressive
+    # passes per GPU and one framebuffer reduce, which scales weakly
+    alt = None
+    if world > 1 and by_slices and not args.no_alt:
+        base = args.warmup + args.steps
+        for i in range(args.warmup):
+            step(base + i, by_slices=False)
+        barrier()
+        a0 = it.stats()
+        barrier()
+        ta = time.perf_counter()
+        for i in range(args.steps):
+            step(base + args.warmup + i, by_slices=False)
+        barrier()
+        a_el = time.perf_counter() - ta
+        a1 = it.stats()
+        a_c = (a1["contrib_preprocess"] - a0["contrib_preprocess"]) + (a1["contrib_render"] - a0["contrib_render"])
+        a_el, (a_c,) = aggregate_over_ranks(a_el, [a_c], world, dev)
+        alt = {"shard": "passes", "scaling": "weak", "value": a_c / a_el, "unit": "VRL contributions/s",
+               "ms_per_step": a_el / args.steps * 1e3, "steps": args.steps, "warmup": args.warmup,
+               "parallelism": f"{world} progressive passes per step, one per GPU, RCCL reduce of the framebuffer"}
     # Rooflines (this rank's launches, HIP events on the stream each kernel ran
     # on).  Algorithmic bytes per launch (DESIGN.md "Roofline"): the gathers
     # and the R build count BYTES_PER_PAIR per VRL contribution; the
@@ -275,6 +317,8 @@ def main():
             "rooflines": rooflines,
             "cpu_baseline": None,
         }
+        if alt is not None:
+            out["alt_decomposition"] = alt
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"], out["pixel_rmse_vs_cpu"] = cpu_baseline(args, cfg, scene, vrls, pc, fb, it,
                                                                        clustered)
