@@ -81,7 +81,7 @@ def parse():
                     help="N > 1 with --shard slices: skip the second, pass-parallel measurement")
     ap.add_argument("--cpu-row-stride", type=int, default=64,
                     help="CPU baseline sample: every n-th image row")
-    ap.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "r02_pmc_traffic.json"),
+    ap.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "r03", "pmc_traffic_r3h.json"),
                     help="per-launch HBM bytes of the dominant kernel from a rocprofv3 --pmc pass")
     ap.add_argument("--valu-json", default=os.path.join(REPO, "profiles", "r03", "pmc_valu_{cfg}.json"),
                     help="per-kernel VALU counters (tools/pmc_valu.sh + tools/pmc_valu.py)")
@@ -176,7 +176,7 @@ def main():
         step(i)
     barrier()
     s0 = it.stats()
-    kernel_ms, rbuild_ms, refine_ms, prepass_ms, refine_kms, refine_ent = [], [], [], [], [], []
+    kernel_ms, rbuild_ms, refine_ms, prepass_ms, refine_kms, refine_ent, refine_split = [], [], [], [], [], [], []
     barrier()
     t0 = time.perf_counter()
     for i in range(args.steps):
@@ -188,6 +188,7 @@ def main():
         prepass_ms.append(st["ms_prepass_wall"])
         refine_kms.append(st["ms_refine_kernel"])
         refine_ent.append(st["refine_entries"])
+        refine_split.append(st["refine_split_entries"])
     barrier()
     elapsed = time.perf_counter() - t0
     s1 = it.stats()
@@ -224,7 +225,12 @@ def main():
     # Rooflines (this rank's launches, HIP events on the stream each kernel ran
     # on).  Algorithmic bytes per launch (DESIGN.md "Roofline"): the gathers
     # and the R build count BYTES_PER_PAIR per VRL contribution; the
-    # refinement counts 8 B per R entry it must read (alvrl_last_refine_entries).
+    # refinement counts 8 B per R entry per pass over it: the
+    # three setup passes read the local matrix once each, and every split
+    # reads its cluster three times -- projections, forward and reverse
+    # calculateClusterVariance (alvrl_last_refine_entries + 2 x
+    # alvrl_last_refine_split_entries); "frac_one_pass" keeps the earlier
+    # rounds' count (each split's cluster once) for comparison.
     nst = max(args.steps, 1)
     kind = "clustered" if clustered else "brute"
     pmc = {}
@@ -273,9 +279,14 @@ def main():
                                "the gather is VALU/transcendental-bound (VRL records are broadcast from "
                                "SGPRs), see DESIGN.md")}
     if clustered:
-        rooflines["refine"] = roof("k_refine", "refine", 8.0 * float(np.mean(refine_ent)),
-                                   float(np.mean(refine_kms)),
-                                   "latency-bound f64 recurrences (speculative split teams), see DESIGN.md")
+        ent1 = float(np.mean(refine_ent))
+        ent3 = ent1 + 2.0 * float(np.mean(refine_split))
+        rooflines["refine"] = roof("k_refine", "refine", 8.0 * ent3, float(np.mean(refine_kms)),
+                                   "8 B per R entry per pass: 3 setup passes + 3 per split (projections, "
+                                   "forward and reverse variance); latency-bound f64 recurrences, see DESIGN.md")
+        rk = float(np.mean(refine_kms)) / 1e3
+        rooflines["refine"]["frac_one_pass"] = (8.0 * ent1 / rk / 1e9 / HBM_PEAK_GBS) if rk > 0 else None
+        rooflines["refine"]["bytes_one_pass"] = 8.0 * ent1
         rooflines["rbuild"] = roof("k_build_R_blocks", "rbuild",
                                    BYTES_PER_PAIR["rbuild"] * (s1["contrib_preprocess"] - s0["contrib_preprocess"]) / nst,
                                    float(np.mean(rbuild_ms)), "VALU-bound like the gather")
@@ -308,6 +319,7 @@ def main():
                           "rbuild_ms": float(np.mean(rbuild_ms)), "refine_ms": float(np.mean(refine_ms)),
                           "refine_kernel_ms": float(np.mean(refine_kms)),
                           "refine_entries": float(np.mean(refine_ent)),
+                          "refine_split_entries": float(np.mean(refine_split)),
                           "prepass_wall_ms": float(np.mean(prepass_ms)),
                           "slices": int(s1["slices"]), "rep_rows": int(s1["rep_rows"]),
                           "clusters_total": int(s1["clusters_total"]),

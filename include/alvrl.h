@@ -282,9 +282,14 @@ ALVRL_API int alvrl_last_refine_ms(alvrl_ctx *ctx, float *ms);
 /* R entries (float2, 8 B each) the last alvrl_refine had to read, summed over
  * its jobs: nrows * (3 * nvrl + the columns of every cluster it split) --
  * column weights, initial cluster variances and the unclustered variance read
- * the whole local matrix once, a split reads its cluster's columns once.  The
- * algorithmic bytes of the refinement's roofline. */
+ * the whole local matrix once, and each split's cluster is counted once. */
 ALVRL_API int alvrl_last_refine_entries(alvrl_ctx *ctx, uint64_t *entries);
+/* Of those, the splits' share: nrows * (the columns of every cluster split).
+ * A split reads them three times (Clustering::split, Preprocessor.cpp:590-684:
+ * the projections, then the forward and the reverse calculateClusterVariance
+ * pass), so the refinement's algorithmic bytes (one count per
+ * split pass) are 8 * (entries + 2 * split_entries). */
+ALVRL_API int alvrl_last_refine_split_entries(alvrl_ctx *ctx, uint64_t *entries);
 
 /* ---- framebuffer --------------------------------------------------- */
 /* ImageBlock::put of 1-spp box-filtered samples (imageblock.h:124-131):

@@ -224,6 +224,7 @@ typedef struct {
     double ms_refine_kernel;
     uint64_t refine_entries;
     uint64_t global_clusters;   /* clusters of the globalCluster refinement (0 if off) */
+    uint64_t refine_split_entries;   /* the splits' share of refine_entries (alvrl_last_refine_split_entries) */
 } alvrl_integrator_stats;
 ALVRL_API int alvrl_integrator_get_stats(alvrl_integrator *it, alvrl_integrator_stats *st);
 /* The device context the integrator drives (for low-level access). */

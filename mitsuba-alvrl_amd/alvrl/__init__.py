@@ -97,6 +97,7 @@ def lib() -> C.CDLL:
                                P(u32), P(f32), P(i32), vp]
     L.alvrl_last_refine_ms.argtypes = [vp, P(f32)]
     L.alvrl_last_refine_entries.argtypes = [vp, P(u64)]
+    L.alvrl_last_refine_split_entries.argtypes = [vp, P(u64)]
     L.alvrl_set_rsamples.argtypes = [vp, i32]
     L.alvrl_build_R_blocks.argtypes = [vp, vp, vp, u32, vp, vp, vp, vp, vp]
     L.alvrl_refine_members.argtypes = [vp, vp, u64, P(ClusterJob), P(u32), P(u32), u32, P(u32), P(u32),
@@ -299,6 +300,12 @@ class Context:
         _check(self.L.alvrl_last_refine_entries(self.h, C.byref(n)))
         return int(n.value)
 
+    def last_refine_split_entries(self) -> int:
+        """The splits' share of last_refine_entries (each split reads it three times)."""
+        n = C.c_uint64()
+        _check(self.L.alvrl_last_refine_split_entries(self.h, C.byref(n)))
+        return int(n.value)
+
     # ---- host-pointer conveniences ----
     def gather_brute_host(self, recs: np.ndarray, ids=None) -> np.ndarray:
         recs = _np(recs, np.float32)
@@ -366,7 +373,8 @@ class IntegratorStats(C.Structure):
                 ("ms_prepass_wall", C.c_double), ("slices_failed", C.c_uint32),
                 ("fallback_built", C.c_int), ("slices_local", C.c_uint64), ("rows_built", C.c_uint64),
                 ("ms_exchange", C.c_double), ("ms_refine_kernel", C.c_double),
-                ("refine_entries", C.c_uint64), ("global_clusters", C.c_uint64)]
+                ("refine_entries", C.c_uint64), ("global_clusters", C.c_uint64),
+                ("refine_split_entries", C.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

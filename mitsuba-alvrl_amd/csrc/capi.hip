@@ -141,7 +141,7 @@ struct alvrl_ctx {
     uint32_t cap_slices = 0, cap_rep = 0, cap_fb = 0;   // grow-only: a prepass re-sets them every pass
     bool clusters_set = false;
     float refine_ms = 0.0f;
-    unsigned long long refine_entries = 0;
+    unsigned long long refine_entries[2] = {0, 0};   // refine_jobs: all entries, the splits' share
     // occluder BVH (alvrl_set_occluders); P.occ views it
     BvhNode* d_bvh_nodes = nullptr;
     float* d_bvh_tris = nullptr;
@@ -582,7 +582,7 @@ ALVRL_API int alvrl_refine(alvrl_ctx* c, const float* d_Rt, uint64_t ld, uint32_
     std::lock_guard<std::mutex> g(c->mu);   // the context's refine scratch
     int rc = refine_jobs(pick(c, stream), d_Rt, ld, c->nvrl, c->P.seed, c->P.pass, njobs, hj.data(),
                          init_vrls, init_off, ninit, out_off, out_reps, out_weights, out_refined,
-                         &ms, &c->refine_entries, &err, &c->refine_arenas);
+                         &ms, c->refine_entries, &err, &c->refine_arenas);
     c->refine_ms = ms;
     if (rc) return fail(rc, err);
     return ALVRL_OK;
@@ -619,7 +619,7 @@ ALVRL_API int alvrl_refine_members(alvrl_ctx* c, const float* d_Rt, uint64_t ld,
     std::lock_guard<std::mutex> g(c->mu);   // the context's refine scratch
     int rc = refine_jobs(pick(c, stream), d_Rt, ld, c->nvrl, c->P.seed, c->P.pass, 1, &hj, init_vrls,
                          init_off, ninit, off.data(), reps.data(), w.data(), out_refined, &ms,
-                         &c->refine_entries, &err, &c->refine_arenas);
+                         c->refine_entries, &err, &c->refine_arenas);
     c->refine_ms = ms;
     if (rc) return fail(rc, err);
     (void)nv;
@@ -636,7 +636,14 @@ ALVRL_API int alvrl_last_refine_ms(alvrl_ctx* c, float* ms)
 ALVRL_API int alvrl_last_refine_entries(alvrl_ctx* c, uint64_t* entries)
 {
     if (!c || !entries) return fail(ALVRL_ERR_INVALID, "alvrl_last_refine_entries: null argument");
-    *entries = c->refine_entries;
+    *entries = c->refine_entries[0];
+    return ALVRL_OK;
+}
+
+ALVRL_API int alvrl_last_refine_split_entries(alvrl_ctx* c, uint64_t* entries)
+{
+    if (!c || !entries) return fail(ALVRL_ERR_INVALID, "alvrl_last_refine_split_entries: null argument");
+    *entries = c->refine_entries[1];
     return ALVRL_OK;
 }
 

@@ -279,6 +279,7 @@ struct alvrl_integrator {
         st.fallback_built = 0;
         st.ms_rbuild = st.ms_refine = st.ms_exchange = st.ms_refine_kernel = 0;
         st.refine_entries = 0;
+        st.refine_split_entries = 0;
         st.global_clusters = 0;
         st.slices_local = 0;
         st.rows_built = 0;
@@ -602,8 +603,11 @@ struct alvrl_integrator {
                 uint64_t ent = 0;
                 chk(alvrl_last_refine_ms(ctx, &kms), "alvrl_last_refine_ms");
                 chk(alvrl_last_refine_entries(ctx, &ent), "alvrl_last_refine_entries");
+                uint64_t sent = 0;
+                chk(alvrl_last_refine_split_entries(ctx, &sent), "alvrl_last_refine_split_entries");
                 st.ms_refine_kernel += kms;
                 st.refine_entries += ent;
+                st.refine_split_entries += sent;
             }
             if (!ok) throw IntegError(ALVRL_ERR_NUMERIC, "Couldn't refine global clustering!");
             std::copy(mem.begin(), mem.begin() + nnz, init.begin());
@@ -652,8 +656,11 @@ struct alvrl_integrator {
             uint64_t ent = 0;
             chk(alvrl_last_refine_ms(ctx, &kms), "alvrl_last_refine_ms");
             chk(alvrl_last_refine_entries(ctx, &ent), "alvrl_last_refine_entries");
+            uint64_t sent = 0;
+            chk(alvrl_last_refine_split_entries(ctx, &sent), "alvrl_last_refine_split_entries");
             st.ms_refine_kernel += kms;
             st.refine_entries += ent;
+            st.refine_split_entries += sent;
         }
         // every rank gets every slice's list
         SliceClusters m;
@@ -708,8 +715,11 @@ struct alvrl_integrator {
                 uint64_t ent = 0;
                 chk(alvrl_last_refine_ms(ctx, &kms), "alvrl_last_refine_ms");
                 chk(alvrl_last_refine_entries(ctx, &ent), "alvrl_last_refine_entries");
+                uint64_t sent = 0;
+                chk(alvrl_last_refine_split_entries(ctx, &sent), "alvrl_last_refine_split_entries");
                 st.ms_refine_kernel += kms;
                 st.refine_entries += ent;
+                st.refine_split_entries += sent;
             }
             if (!fref) throw IntegError(ALVRL_ERR_NUMERIC, "couldn't refine global clustering! (but all VRLs should be non-zero!)");
             fb_reps.assign(frep.begin(), frep.begin() + foff[1]);

@@ -130,7 +130,8 @@ struct Common {
     uint32_t ninit;
     uint32_t seed, pass;
     unsigned long long* prof;   // per-phase cycle totals (ALVRL_REFINE_PROFILE=1), or null
-    unsigned long long* entries;   // R entries the clustering has to read (roofline bytes / 8)
+    unsigned long long* entries;   // [0]: R entries read once per setup pass and split (roofline bytes / 8),
+                                   // [1]: of those, the splits' (each split reads them three times)
     uint32_t njobs;                // leaders = blocks [0, njobs); helpers follow, team by team
     uint32_t team;                 // workgroups per job (1 = no speculation)
     uint32_t spec_min;             // smallest cluster worth a speculative split
@@ -3241,7 +3242,10 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
         *J.out_err = C.err;
         // column weights, initial clusters and unclustered variance read every
         // entry once; a split reads its cluster's columns (at least) once
-        if (cm.entries) atomicAdd(cm.entries, (3ull * N + split_cols) * R);
+        if (cm.entries) {
+            atomicAdd(&cm.entries[0], (3ull * N + split_cols) * R);
+            atomicAdd(&cm.entries[1], split_cols * R);
+        }
     }
     if (cm.jtime && tid == 0) cm.jtime[3 * blockIdx.x + 2] = wall();
     if (cm.roam_on) {
@@ -3333,7 +3337,7 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
         ~Finally() { if (l) l->release(); }
     } fin{cache ? nullptr : &local};
     if (ms) *ms = 0.0f;
-    if (entries) *entries = 0;
+    if (entries) entries[0] = entries[1] = 0;
     out_off[0] = 0;
     if (njobs == 0) return 0;
     // the initial clusters partition the VRLs they list (every VRL for the
@@ -3395,7 +3399,7 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
     };
     size_t total = align_up(rows_total * 8) + align_up(rows_total * 4) + align_up(rows_total * 8) + align_up((size_t)nv * 4) +
                    align_up((size_t)(ninit + 1) * 4) + align_up((size_t)njobs * sizeof(JobDev)) +
-                   align_up((size_t)njobs * 12) + 2 * align_up((size_t)njobs * N * 4) + align_up(8);
+                   align_up((size_t)njobs * 12) + 2 * align_up((size_t)njobs * N * 4) + align_up(16);
     for (uint32_t j = 0; j < njobs; j++) { job_off[j] = total; total += job_bytes(jobs[j]); }
     hipError_t e = arena_get(&ar.arena, &ar.arena_cap, total, cache != nullptr);
     if (e != hipSuccess) { *err = std::string("alvrl_refine: hipMalloc: ") + hipGetErrorString(e); return 4; }
@@ -3640,7 +3644,7 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
     if (e == hipSuccess) e = hipMemcpyAsync(d_init, init_vrls, (size_t)nv * 4, hipMemcpyHostToDevice, s);
     if (e == hipSuccess) e = hipMemcpyAsync(d_init_off, init_off, (size_t)(ninit + 1) * 4, hipMemcpyHostToDevice, s);
     if (e == hipSuccess) e = hipMemcpyAsync(d_jobs, h_jobs.data(), njobs * sizeof(JobDev), hipMemcpyHostToDevice, s);
-    if (e == hipSuccess) e = hipMemsetAsync(d_entries, 0, 8, s);
+    if (e == hipSuccess) e = hipMemsetAsync(d_entries, 0, 16, s);
     if (e == hipSuccess && tarena) e = hipMemsetAsync(tarena, 0, tbytes, s);
     for (uint32_t j = 0; j < njobs && e == hipSuccess && G > 1; j++)
         e = hipMemcpyAsync(const_cast<SplitWs*>(h_jobs[j].team.ws), &h_ws[(size_t)j * (G - 1)],
@@ -3690,15 +3694,15 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
     }
     // gather results: packed on the device, three copies
     std::vector<uint32_t> meta(3 * (size_t)njobs);
-    unsigned long long h_entries = 0;
+    unsigned long long h_entries[2] = {0, 0};
     if (e == hipSuccess) {
         hipLaunchKernelGGL(k_pack_results, dim3(njobs), dim3(256), 0, s, d_jobs, njobs, nvrl, d_meta, d_preps, d_pw);
         e = hipGetLastError();
     }
     if (e == hipSuccess) e = hipMemcpyAsync(meta.data(), d_meta, (size_t)njobs * 12, hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipMemcpyAsync(&h_entries, d_entries, 8, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(h_entries, d_entries, 16, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
-    if (entries) *entries = h_entries;
+    if (entries) { entries[0] = h_entries[0]; entries[1] = h_entries[1]; }
     if (cm.tstat) {
         unsigned long long h[TS_N];
         if (hipMemcpy(h, cm.tstat, sizeof(h), hipMemcpyDeviceToHost) == hipSuccess) {

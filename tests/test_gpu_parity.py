@@ -318,6 +318,9 @@ def test_refine_bit_exact(oracle, gpu_ok, undersampling):
     ctx, d_Rt, Rt, jobs, init, init_off = _refine_case(oracle, 96, 96, 1200, [40, 23, 64, 70, 5],
                                                        undersampling, torch)
     off, reps, w, refined = ctx.refine(d_Rt, Rt.shape[1], jobs, init, init_off)
+    # roofline counters: 3 setup passes over every job's rows, and the splits' columns
+    ent, sent = ctx.last_refine_entries(), ctx.last_refine_split_entries()
+    assert ent - sent == 3 * Rt.shape[0] * sum(len(j["rows"]) for j in jobs) and sent > 0, (ent, sent)
     for s, j in enumerate(jobs):
         cr, cw, cref = oracle.cluster_refine(Rt, j["rows"], j["locw"], init, init_off,
                                              j["pixel_undersampling"], undersampling,
