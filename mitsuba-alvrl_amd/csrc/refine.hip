@@ -1402,6 +1402,10 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
 #ifdef ALVRL_EXP_NOLOAD
 #pragma unroll
         for (int c = 0; c < kCH; c++) dst[c] = make_float2((float)ids[(uint32_t)c < cn ? c : 0] * 1e-7f + (float)lane * 1e-9f, 0.25f);
+#elif defined(ALVRL_EXP_NOBAR)
+        // timing experiment without the chunk barriers: ids may be stale, keep them in range
+#pragma unroll
+        for (int c = 0; c < kCH; c++) dst[c] = ldg2(Rt, (size_t)min(ids[(uint32_t)c < cn ? c : 0], cm.nvrl - 1) * rstride);
 #else
 #pragma unroll
         for (int c = 0; c < kCH; c++) dst[c] = ldg2(Rt, (size_t)ids[(uint32_t)c < cn ? c : 0] * rstride);
@@ -1450,7 +1454,9 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
                 pc_sp[2] += (uint32_t)(ws3 - ws2); pc_sp[3] += (uint32_t)(ws4 - ws3);
 #endif
             }
+            #ifndef ALVRL_EXP_NOBAR
             __syncthreads();
+            #endif
         };
 #ifdef ALVRL_EXP_COEFPRIO
         __builtin_amdgcn_s_setprio(ALVRL_EXP_COEFPRIO);
@@ -1525,7 +1531,9 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
 #ifdef ALVRL_EXP_STAMP
             const unsigned long long s2 = stamp();
 #endif
+            #ifndef ALVRL_EXP_NOBAR
             __syncthreads();
+            #endif
 #ifdef ALVRL_EXP_STAMP
             const unsigned long long s3 = stamp();
             if (wprof) { pc_sp[0] += (uint32_t)(s1 - s0); pc_sp[1] += (uint32_t)(s2 - s1); pc_sp[2] += (uint32_t)(s3 - s2); }
@@ -1546,7 +1554,9 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
             gpw(st)[2 * R + b0 * 64 + lane] = V0;
         }
     } else {
+        #ifndef ALVRL_EXP_NOBAR
         for (uint32_t k = 0; k < nch; k++) __syncthreads();
+        #endif
     }
     if (wprof) {
         const bool n4 = NB == 4;

@@ -63,12 +63,14 @@ def main():
             torch.cuda.synchronize()
             if r:
                 ms.append(ctx.last_refine_ms())
-        assert ok.all() and (np.diff(off) == 2).all(), (off[:4], ok[:4])
         ent = ctx.last_refine_entries()
         rec = {"jobs": J, "kernel_ms": min(ms), "kernel_ms_all": ms, "entries": ent,
                "cycles_per_column_est": min(ms) * 1e-3 * 2.4e9 / N}
         out["runs"].append(rec)
         print(json.dumps(rec), flush=True)
+        # timing-only variants (tools/build_variant.sh with ALVRL_EXP_* macros) give no valid clusters
+        if os.environ.get("ALVRL_ENGINE_NOCHECK") != "1":
+            assert ok.all() and (np.diff(off) == 2).all(), (off[:4], ok[:4])
     print(json.dumps(out))
 
 
