@@ -1366,14 +1366,14 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
                 sum0 = sum0 + x;
                 if (FU) { t[0] = lw * (M0 * k2.rWn); t[1] = lw * (V0 * k2.Wn); }
             };
-            CCol ka = ldc(0), kb;
+            // coefficients two columns ahead (one ahead: 0.3-1 % slower, profiles/r03/engine/pf2/)
+            CCol k0 = ldc(0), k1 = ldc(1), k2 = k1;
 #pragma unroll
-            for (int c = 0; c < kCH; c += 2) {         // the next column's coefficients one column ahead
-                kb = ldc(c + 1);
-                col(ka, cur[c], &th[2 * (c & 3)]);
-                if (c + 2 < kCH) ka = ldc(c + 2);
-                col(kb, cur[c + 1], &th[2 * ((c + 1) & 3)]);
-                if (c == 2) half_done(0);
+            for (int c = 0; c < kCH; c++) {
+                if (c + 2 < kCH) k2 = ldc(c + 2);
+                col(k0, cur[c], &th[2 * (c & 3)]);
+                k0 = k1; k1 = k2;
+                if (c == 3) half_done(0);
             }
             half_done(1);
         } else {
