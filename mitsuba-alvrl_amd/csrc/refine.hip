@@ -61,6 +61,7 @@ struct SplitWs {                      // a workgroup's private split scratch
     unsigned long long* keys0;
     unsigned long long* keys1;
     float* fsu; float* fsi; float* feu; float* fei;
+    double* carry;                    // [2][N][2] row-group sums of the v3 engine (null: rows <= 256)
 };
 struct Team {
     uint32_t helpers;                 // workgroups besides the leader (0 = off)
@@ -105,6 +106,7 @@ struct JobDev {
     unsigned long long* keys0;
     unsigned long long* keys1;
     float* fsu; float* fsi; float* feu; float* fei;
+    double* carry;     // [2][N][2]: the v3 engine's block-ordered row sums between row groups (null: rows <= 256)
     double* st;        // 2 x 3 * nrows: sum, M, sumVars per variance direction
     double* bufM;      // 2 x kCH * (nrows | 1): per-row terms when they do not fit in LDS
     double* bufV;
@@ -244,6 +246,12 @@ struct Ctl {
     int tmode, side;
     unsigned long long sw;   // the popped cluster's state word, fetched by pop_wave (team mode)
     uint32_t* prec;        // this pop's trace record (ALVRL_POP_TRACE), or null
+    // the v3 variance engine over row groups of <= 256 rows (variance_passes):
+    // this call's first row, whether it is the first / last group, and the
+    // running block-ordered row sums carried between groups (2 passes x m x (u, i))
+    uint32_t g_row0;
+    int g_first, g_last;
+    double* g_carry;
     int team_off;          // the job's team was retired after a timed-out wait (split_team)
     uint32_t yb, ye, j;
     unsigned long long t0;
@@ -1209,12 +1217,20 @@ __device__ __forceinline__ void coef_block_finish(Ctl& C, double w, double Wo, d
 // FU == false: only the final variances of npass passes (no prefix terms, no
 // reduction per chunk): the rows' final states go to J.st and one wave per
 // pass forms the two sums, as variance_passes_t does.
-template <bool FU>
+template <bool FU, bool GRP = false>
 __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm, Ctl& C, const uint32_t* base,
                                                uint32_t m, int npass, float* fu0, float* fi0, float* fu1, float* fi1,
                                                unsigned char* pool)
 {
-    const uint32_t R = J.nrows;
+    // a group of <= 256 rows (row0 .. row0 + R) of the job's Rfull: the
+    // coefficients are the same for every group, the block-ordered row sums
+    // continue from the previous group's (C.g_carry), and the prefix results
+    // are written by the last group only
+    // (GRP = false: one group of all the rows, the constants fold away)
+    const uint32_t Rfull = J.nrows, row0 = GRP ? C.g_row0 : 0u;
+    const uint32_t R = GRP ? min(Rfull - row0, 256u) : Rfull;
+    const bool gfirst = GRP ? C.g_first != 0 : true, glast = GRP ? C.g_last != 0 : true;
+    double* const carry = GRP ? C.g_carry : nullptr;
     const uint32_t NB = (R + 63) / 64;                 // <= 4 (block 3 on the coefficient wave)
     const int tid = threadIdx.x, wv = tid >> 6;
     const uint32_t lane = (uint32_t)(tid & 63);
@@ -1295,10 +1311,10 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
     // every lane of a row wave runs the recurrence (rows past R on row R-1's
     // data: their terms are never reduced), so no load or store is predicated
     const uint32_t r0 = min(b0 * 64 + lane, R - 1);
-    const RowRef rr0 = roww ? row_ref(J, r0) : RowRef{0, 0};
+    const RowRef rr0 = roww ? row_ref(J, row0 + r0) : RowRef{0, 0};
     // rows past R carry weight 0: their prefix terms are +0.0 exactly (M, V >= 0),
     // which is what the reduction order wants from them (no per-term select)
-    const double lw0 = roww && b0 * 64 + lane < R ? J.locw[r0] : 0.0;
+    const double lw0 = roww && b0 * 64 + lane < R ? J.locw[row0 + r0] : 0.0;
 
     // coefficient wave: the 16 row sums of chunk kk, the row blocks' tree
     // totals added in block order (wsum_blk), one sum per lane 0-15
@@ -1306,12 +1322,17 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
         const uint32_t cn = cn_of(kk);
         const double* Qk = Q + (size_t)(kk & 1) * 4 * 16;
         const uint32_t sl = lane & 15, c = sl >> 1, h = sl & 1;
-        double acc = Qk[sl];
+        const uint32_t n = kk * kCH + c;
+        double* const cy = carry + ((size_t)g * m + min(n, m - 1)) * 2 + h;   // this pass's running sum
+        double acc = gfirst ? Qk[sl] : gp(cy)[0];
 #pragma unroll
-        for (uint32_t b = 1; b < 4; b++)
+        for (uint32_t b = gfirst ? 1 : 0; b < 4; b++)
             if (b < NB) acc = acc + Qk[b * 16 + sl];
+        if (!glast) {
+            if (lane < 16 && c < cn) gpw(cy)[0] = acc;
+            return;
+        }
         if (lane < 16 && c < cn) {
-            const uint32_t n = kk * kCH + c;
             const float f = h == 0 ? (n == 0 ? 0.0f : (float)acc) : (float)acc;
             stg[(((kk / 8) & 1) * 2 + h) * kCB64 + (kk % 8) * kCH + c] = f;
             if (n == m - 1) {
@@ -1323,7 +1344,7 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
 
     auto flush = [&](uint32_t b) {                     // block b's prefix results, one column per lane
         const uint32_t col = b * kCB64 + lane;
-        if (col < m) {                                 // global, not flat: a flat store would make
+        if (glast && col < m) {                                 // global, not flat: a flat store would make
             gpw(fu)[col] = stg[((b & 1) * 2 + 0) * kCB64 + lane];   // every LDS wait a vmcnt(0)
             gpw(fi)[col] = stg[((b & 1) * 2 + 1) * kCB64 + lane];
         }
@@ -1421,8 +1442,8 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
         // outer iteration: no register copy of a load in flight)
         const bool own3 = NB == 4;
         const uint32_t r3 = min(3u * 64u + lane, R - 1);
-        const RowRef rr3 = own3 ? row_ref(J, r3) : RowRef{0, 0};
-        const double lw3 = own3 && 3u * 64u + lane < R ? J.locw[r3] : 0.0;
+        const RowRef rr3 = own3 ? row_ref(J, row0 + r3) : RowRef{0, 0};
+        const double lw3 = own3 && 3u * 64u + lane < R ? J.locw[row0 + r3] : 0.0;
         const float2* const Rt3 = cm.Rt + rr3.base;
         const size_t rs3 = rr3.stride;
         double sum3 = 0.0, M3 = 0.0, V3 = 0.0;
@@ -1484,9 +1505,9 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
         } else {
             if (lane == 0) V.Wcur = W;
             if (own3 && 3u * 64u + lane < R) {
-                double* st = J.st + (size_t)g * 3 * R;
-                gpw(st)[R + 3u * 64u + lane] = M3;
-                gpw(st)[2 * R + 3u * 64u + lane] = V3;
+                double* st = J.st + (size_t)g * 3 * Rfull;
+                gpw(st)[Rfull + row0 + 3u * 64u + lane] = M3;
+                gpw(st)[2 * Rfull + row0 + 3u * 64u + lane] = V3;
             }
         }
     } else if (roww) {
@@ -1549,9 +1570,9 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
             flush((nch - 1) / 8);
         }
         if (!FU && b0 * 64 + lane < R) {
-            double* st = J.st + (size_t)g * 3 * R;
-            gpw(st)[R + b0 * 64 + lane] = M0;
-            gpw(st)[2 * R + b0 * 64 + lane] = V0;
+            double* st = J.st + (size_t)g * 3 * Rfull;
+            gpw(st)[Rfull + row0 + b0 * 64 + lane] = M0;
+            gpw(st)[2 * Rfull + row0 + b0 * 64 + lane] = V0;
         }
     } else {
         #ifndef ALVRL_EXP_NOBAR
@@ -1569,14 +1590,14 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
         padd(n4 ? PF_V_CW : PF_V_REC, pc_sp[3]);
     }
     __syncthreads();
-    if (!FU && active && wv == (g == 0 ? 0 : 5)) {
-        // the pass's final variances from the rows' states (variance_passes_t, FU == false)
-        const double* st = J.st + (size_t)g * 3 * R;
+    if (!FU && glast && active && wv == (g == 0 ? 0 : 5)) {
+        // the pass's final variances from every row's state (variance_passes_t, FU == false)
+        const double* st = J.st + (size_t)g * 3 * Rfull;
         const double Wt = V.Wcur, rW = 1.0 / Wt;
         double pu = 0.0, pi = 0.0;
-        for (uint32_t r = lane; r < R; r += 64) {
-            pu = pu + J.locw[r] * (gp(st)[R + r] * rW);
-            pi = pi + J.locw[r] * (gp(st)[2 * R + r] * Wt);
+        for (uint32_t r = lane; r < Rfull; r += 64) {
+            pu = pu + J.locw[r] * (gp(st)[Rfull + r] * rW);
+            pi = pi + J.locw[r] * (gp(st)[2 * Rfull + r] * Wt);
         }
         pu = tree_d(pu);
         pi = tree_d(pi);
@@ -1727,6 +1748,23 @@ __device__ void variance_passes(const JobDev& J, const Common& cm, Ctl& C, const
     const uint32_t NB = (J.nrows + 63) / 64;
     if (pf && (!pf->p || threadIdx.x != 0)) pf = nullptr;
     const bool lds = (size_t)2 * 2 * kCH * NB * 64 * sizeof(double2) <= kPoolBytes;
+    if (NB > 4 && cm.var_v3 && J.carry && (fu0 ? npass == 2 : true)) {
+        // more than 256 rows: the v3 engine once per group of <= 256 rows, the
+        // block-ordered row sums carried from group to group (wsum_blk's order
+        // over all the blocks), the prefix results written by the last group
+        const uint32_t G = (J.nrows + 255) / 256;
+        for (uint32_t gr = 0; gr < G; gr++) {
+            if (threadIdx.x == 0) {
+                C.g_row0 = gr * 256u; C.g_first = gr == 0; C.g_last = gr + 1 == G; C.g_carry = J.carry;
+            }
+            __syncthreads();
+            if (fu0) variance_split_v3<true, true>(J, cm, C, base, m, 2, fu0, fi0, fu1, fi1, pool);
+            else variance_split_v3<false, true>(J, cm, C, base, m, npass, nullptr, nullptr, nullptr, nullptr, pool);
+        }
+        if (threadIdx.x == 0) { C.g_row0 = 0; C.g_first = 1; C.g_last = 1; C.g_carry = nullptr; }
+        __syncthreads();
+        return;
+    }
     if (fu0 && npass == 2 && NB <= 4 && cm.var_v3) {
         variance_split_v3<true>(J, cm, C, base, m, 2, fu0, fi0, fu1, fi1, pool);
         return;
@@ -2717,7 +2755,7 @@ __device__ __noinline__ void helper_loop(const JobDev& J0, uint32_t hid, const C
     const SplitWs& w = T.ws[hid];
     J.vrls = T.spec;
     J.dir = w.dir; J.st = w.st; J.bufM = w.bufM; J.keys0 = w.keys0; J.keys1 = w.keys1;
-    J.fsu = w.fsu; J.fsi = w.fsi; J.feu = w.feu; J.fei = w.fei;
+    J.fsu = w.fsu; J.fsi = w.fsi; J.feu = w.feu; J.fei = w.fei; J.carry = w.carry;
     const int tid = threadIdx.x;
     if (tid == 0) C.err = 0;
     trace(cm, 10, 0);
@@ -2787,7 +2825,7 @@ __device__ __noinline__ void roam_loop(const JobDev* jobs, const SplitWs& w, uin
         JobDev Jw = J0;
         Jw.vrls = J0.team.spec;
         Jw.dir = w.dir; Jw.st = w.st; Jw.bufM = w.bufM; Jw.keys0 = w.keys0; Jw.keys1 = w.keys1;
-        Jw.fsu = w.fsu; Jw.fsi = w.fsi; Jw.feu = w.feu; Jw.fei = w.fei;
+        Jw.fsu = w.fsu; Jw.fsi = w.fsi; Jw.feu = w.feu; Jw.fei = w.fei; Jw.carry = w.carry;
         const unsigned long long t_busy = wall();
         spec_split(J0, Jw, cm, C, lds, C.b, C.e);
         if (tid == 0) { tcount(cm, TS_HDONE); tadd(cm, TS_RBUSY, wall() - t_busy); }
@@ -2998,6 +3036,8 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
     __shared__ Ctl C;
     __shared__ __attribute__((aligned(16))) unsigned char pool[kPoolBytes];
     unsigned long long* lds = reinterpret_cast<unsigned long long*>(pool);
+    if (threadIdx.x == 0) { C.g_row0 = 0; C.g_first = 1; C.g_last = 1; C.g_carry = nullptr; }   // one row group
+    __syncthreads();
     if (blockIdx.x >= cm.njobs * cm.team) {   // a roaming helper
         const uint32_t rid = blockIdx.x - cm.njobs * cm.team;
         roam_loop(jobs, cm.roam_ws[rid], rid * 37u, cm, C, lds);
@@ -3261,7 +3301,7 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
     if (cm.roam_on) {
         // this job is done: its leader helps the others with its own scratch
         __syncthreads();
-        const SplitWs w{J.dir, J.st, J.bufM, J.keys0, J.keys1, J.fsu, J.fsi, J.feu, J.fei};
+        const SplitWs w{J.dir, J.st, J.bufM, J.keys0, J.keys1, J.fsu, J.fsi, J.feu, J.fei, J.carry};
         roam_loop(jobs, w, blockIdx.x + 1, cm, C, lds);
     }
 }
@@ -3405,7 +3445,8 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
         return align_up(N * 4) * 2 + align_up(N * sizeof(CNode)) * 2 + align_up(N * 4) * 2 +
                align_up((size_t)R * 4) + align_up(N * 8) * 2 + align_up(N * 4) * 4 +
                align_up((size_t)6 * R * 8) + align_up((size_t)2 * 2 * kCH * ((R + 63) / 64) * 64 * 16) +
-               align_up(N * 4) * 2 + align_up(16) + (H.members ? align_up(N * 4) + align_up((N + 1) * 4) + align_up(4) : 0);
+               align_up(N * 4) * 2 + align_up(16) + (H.members ? align_up(N * 4) + align_up((N + 1) * 4) + align_up(4) : 0) +
+               (R > 256 ? align_up((size_t)4 * N * 8) : 0);
     };
     size_t total = align_up(rows_total * 8) + align_up(rows_total * 4) + align_up(rows_total * 8) + align_up((size_t)nv * 4) +
                    align_up((size_t)(ninit + 1) * 4) + align_up((size_t)njobs * sizeof(JobDev)) +
@@ -3471,6 +3512,8 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
         J.fsi = (float*)p; p += align_up(N * 4);
         J.feu = (float*)p; p += align_up(N * 4);
         J.fei = (float*)p; p += align_up(N * 4);
+        J.carry = nullptr;
+        if (Rw > 256) { J.carry = (double*)p; p += align_up((size_t)4 * N * 8); }
         J.st = (double*)p; p += align_up((size_t)6 * Rw * 8);
         J.bufM = (double*)p; p += align_up((size_t)2 * 2 * kCH * ((Rw + 63) / 64) * 64 * 16);   // T, 2 passes x 2 chunks
         J.bufV = nullptr;
@@ -3492,7 +3535,8 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
     if (team_on) {
         auto helper_bytes = [&](uint32_t R) {
             return align_up((size_t)R * 4) + align_up((size_t)6 * R * 8) +
-                   align_up((size_t)2 * 2 * kCH * ((R + 63) / 64) * 64 * 16) + 2 * align_up(N * 8) + 4 * align_up(N * 4);
+                   align_up((size_t)2 * 2 * kCH * ((R + 63) / 64) * 64 * 16) + 2 * align_up(N * 8) + 4 * align_up(N * 4) +
+                   (R > 256 ? align_up((size_t)4 * N * 8) : 0);
         };
         const size_t team_fixed = align_up(N * 4) + align_up(N * 8) + align_up(N * sizeof(SplitRes)) +
                                   align_up((size_t)kQueue * 8) + align_up(16) + align_up((size_t)(G - 1) * sizeof(SplitWs));
@@ -3532,6 +3576,8 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
                 w.fsi = (float*)q; q += align_up(N * 4);
                 w.feu = (float*)q; q += align_up(N * 4);
                 w.fei = (float*)q; q += align_up(N * 4);
+                w.carry = nullptr;
+                if (R > 256) { w.carry = (double*)q; q += align_up((size_t)4 * N * 8); }
             }
             to = (size_t)(q - tarena);
         }
@@ -3549,6 +3595,7 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
                 w.fsi = (float*)carve(N * 4);
                 w.feu = (float*)carve(N * 4);
                 w.fei = (float*)carve(N * 4);
+                w.carry = Rmax > 256 ? (double*)carve((size_t)4 * N * 8) : nullptr;
             }
         }
     }

@@ -26,6 +26,8 @@ import c5_share      # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--oracle", action="store_true")
+    ap.add_argument("--oracle-rows", type=int, default=0,
+                    help="compare the local slice whose row count is nearest this (default: the smallest)")
     ap.add_argument("--props", default="")
     ap.add_argument("--json", default="")
     ap.add_argument("--vrls", type=int, default=c5_share.C5_VRLS)
@@ -45,7 +47,8 @@ def main():
     if a.oracle:
         from oracle import Oracle
         o = Oracle()
-        k = int(np.argmin(info["rows_local"]))
+        rl = np.array(info["rows_local"])
+        k = int(np.argmin(np.abs(rl - a.oracle_rows))) if a.oracle_rows else int(np.argmin(rl))
         s = mine[k]
         t0 = time.time()
         job = it.slice_job(s)
