@@ -1623,9 +1623,10 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
 // Outputs stay in LDS: out[0..3][c] = fsu, fsi, feu, fei (prefix c of the
 // forward / reverse pass; the forward u of prefix 0 is 0).
 constexpr uint32_t kSmallMax = 256;
+constexpr uint32_t kSmallBlocks = 14;                 // row blocks: up to 896 rows (row waves take blk, blk + 4, ...)
 constexpr uint32_t kSmallCoefBytes = 2u * 7u * kSmallMax * 8u;
 constexpr uint32_t kSmallVrlBytes = 2u * kSmallMax * 4u;
-constexpr uint32_t kSmallQBytes = 2u * kSmallMax * 2u * 4u * 8u;
+constexpr uint32_t kSmallQBytes = 2u * kSmallMax * 2u * kSmallBlocks * 8u;
 constexpr uint32_t kSmallOutOff = kSmallCoefBytes + kSmallVrlBytes + kSmallQBytes;
 static_assert(kSmallOutOff + 4u * kSmallMax * 4u <= kPoolBytes, "small split engine exceeds the LDS pool");
 __device__ __forceinline__ const float* small_out(const unsigned char* pool) { return reinterpret_cast<const float*>(pool + kSmallOutOff); }
@@ -1676,9 +1677,11 @@ __device__ __noinline__ void variance_split_small(const JobDev& J, const Common&
         }
     }
     __syncthreads();
-    if (blk < NB) {
-        const bool valid = blk * 64 + lane < R;
-        const uint32_t r = min(blk * 64 + lane, R - 1);
+    // row wave blk runs row blocks blk, blk + 4, ... (more than 256 rows: one
+    // after the other, each from a zero state)
+    for (uint32_t bb = blk; bb < NB; bb += 4) {
+        const bool valid = bb * 64 + lane < R;
+        const uint32_t r = min(bb * 64 + lane, R - 1);
         const RowRef rr = row_ref(J, r);
         const double lw = J.locw[r];
         const float2* const Rt = cm.Rt + rr.base;
@@ -1711,7 +1714,7 @@ __device__ __noinline__ void variance_split_small(const JobDev& J, const Common&
             const double z = tree16_transposed(tv, lane);
             if ((lane & 3) == 0) {
                 const uint32_t h = lane >> 5, c = 4 * ((lane >> 2) & 1) + 2 * ((lane >> 3) & 1) + ((lane >> 4) & 1);
-                if (c0 + c < m) Q[(((size_t)g * kSmallMax + c0 + c) * 2 + h) * 4 + blk] = z;
+                if (c0 + c < m) Q[(((size_t)g * kSmallMax + c0 + c) * 2 + h) * kSmallBlocks + bb] = z;
             }
         };
         load(0, bufA);
@@ -1728,7 +1731,7 @@ __device__ __noinline__ void variance_split_small(const JobDev& J, const Common&
     VarGroup* const vgrp = C.vg;
     for (uint32_t t = (uint32_t)tid; t < 4 * m; t += kThreads) {
         const uint32_t gh = t / m, c = t - gh * m, gg = gh >> 1, h = gh & 1;
-        const auto* q = Q + (((size_t)gg * kSmallMax + c) * 2 + h) * 4;
+        const auto* q = Q + (((size_t)gg * kSmallMax + c) * 2 + h) * kSmallBlocks;
         double acc = q[0];
         for (uint32_t b = 1; b < NB; b++) acc = acc + q[b];
         const float f = (h == 0 && c == 0) ? 0.0f : (float)acc;
@@ -2218,7 +2221,7 @@ __device__ void split(const JobDev& J, const Common& cm, Ctl& C, uint32_t begin,
     __syncthreads();
     pf.mark(PF_SORT);
     const long long hv0 = pf.p && tid == 0 ? (long long)clock64() : 0;
-    const bool small = cm.var_small && m <= kSmallMax && R <= 256;
+    const bool small = cm.var_small && m <= kSmallMax && R <= 64u * kSmallBlocks;
     unsigned char* const pool = reinterpret_cast<unsigned char*>(lds);
     if (small)
         variance_split_small(J, cm, C, J.vrls + begin, m, pool);
