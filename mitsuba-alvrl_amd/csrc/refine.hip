@@ -245,6 +245,14 @@ struct Ctl {
     int go, do_snap, stop, refined;
     int tmode, side;
     unsigned long long sw;   // the popped cluster's state word, fetched by pop_wave (team mode)
+    // the heap top's state word as enqueue_candidates read it, kept when no
+    // helper can change it before the leader's next pop (pre_b: its begin, or ~0)
+    unsigned long long pre_sw;
+    uint32_t pre_b;
+    // the queue tail the leader has written slots up to; published to
+    // team.ctl[1] (publish_tail) at the next split_team or stop_team
+    uint32_t qtail;
+    int qpend;
     uint32_t* prec;        // this pop's trace record (ALVRL_POP_TRACE), or null
     // the v3 variance engine over row groups of <= 256 rows (variance_passes):
     // this call's first row, whether it is the first / last group, and the
@@ -551,14 +559,22 @@ __device__ void add_cluster(const JobDev& J, Ctl& C, uint32_t begin, uint32_t en
 // path node i.  Final array = std::pop_heap's; the slots written are logged.
 // With state set (team mode), lane 0 also fetches the popped cluster's state
 // word while the sift-down runs (split_team's first look): C.sw.
-__device__ CNode pop_wave(const JobDev& J, Ctl& C, const unsigned long long* state = nullptr)
+#ifdef ALVRL_PT_POP   // diagnostic: trace points 1-3 inside the pop, 4 after its barrier
+#define PT_POP(k) do { if ((threadIdx.x & 63) == 0 && C.prec) gpw(C.prec)[k] = (uint32_t)__builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define PT_POP(k) do { } while (0)
+#endif
+__device__ __noinline__ CNode pop_wave(const JobDev& J, Ctl& C, const unsigned long long* state = nullptr)
 {
     const int lane = (int)(threadIdx.x & 63);
     const HeapRef H = heap_of(J, C);
     const long n = __builtin_amdgcn_readfirstlane(C.heap_n);
     const CNode top = hld(H, 0);
     unsigned long long sw = 0;
-    if (state && lane == 0) sw = __hip_atomic_load(&gp(state)[top.begin], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    PT_POP(1);
+    if (state && lane == 0)
+        sw = C.pre_b == top.begin ? C.pre_sw
+                                  : __hip_atomic_load(&gp(state)[top.begin], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (n > 1) {
         const long len = n - 1;
         const CNode value = hld(H, len);
@@ -599,6 +615,7 @@ __device__ CNode pop_wave(const JobDev& J, Ctl& C, const unsigned long long* sta
                 if (kk == 5) h = ic;
             }
         }
+        PT_POP(2);
         // __push_heap from p_L: climbs while the node above is less
         const bool stay = lane >= 1 && lane <= L && !((__uint_as_float(pv.x) + __uint_as_float(pv.y)) < vkey);
         const unsigned long long nf = __ballot(stay);
@@ -622,7 +639,9 @@ __device__ CNode pop_wave(const JobDev& J, Ctl& C, const unsigned long long* sta
         C.clUnderVar -= top.uvar;
         C.clIntVar -= top.ivar;
         if (state) C.sw = sw;
+        C.pre_b = ~0u;
     }
+    PT_POP(3);
     return top;
 }
 
@@ -2367,15 +2386,16 @@ __device__ void enqueue_candidates(const JobDev& J, const Common& cm, Ctl& C)
     const Team& T = J.team;
     const uint32_t lane = threadIdx.x & 63;
     const int K = min(min(C.heap_n, (int)(cm.spec_width ? cm.spec_width : 2 * T.helpers + 2)), 64);
-    const uint32_t tail = T.ctl[1];
+    const uint32_t tail = C.qpend ? C.qtail : T.ctl[1];
     const uint32_t head = ld_rlx(&T.ctl[0]);
     bool elig = false;
-    unsigned long long spec = 0;
+    unsigned long long spec = 0, sv = 0;
     CNode cn{0.0f, 0.0f, 0u, 0u};
     if ((int)lane < K) {
         cn = hld(heap_of(J, C), lane);
-        if (cn.end - cn.begin >= cm.spec_min) {
-            const unsigned long long sv = ld_rlx(&T.state[cn.begin]);
+        const bool big = cn.end - cn.begin >= cm.spec_min;
+        if (big || lane == 0) sv = ld_rlx(&T.state[cn.begin]);   // lane 0: the next pop's word too
+        if (big) {
             const bool mine = (uint32_t)(sv >> 3) == cn.end;
             elig = !(mine && (sv & 7) != kStNone);
             spec = mine ? (sv & kStSpecBit) : 0ull;
@@ -2386,15 +2406,35 @@ __device__ void enqueue_candidates(const JobDev& J, const Common& cm, Ctl& C)
     const uint32_t room = used >= kQueue ? 0u : kQueue - used;
     const unsigned long long lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     const uint32_t rank = (uint32_t)__popcll(bal & lt);
-    if (elig && rank < room) {
+    const bool queued = elig && rank < room;
+    if (queued) {
         st_rlx(&T.state[cn.begin], ((unsigned long long)cn.end << 3) | kStQueued | spec);
         st_rlx(&T.queue[(tail + rank) % kQueue], ((unsigned long long)cn.begin << 32) | cn.end | (spec ? kQSpecBit : 0u));
         tcount(cm, TS_ENQ);
     }
     const uint32_t npush = min((uint32_t)__popcll(bal), room);
-    if (npush) {
-        drain_vmem();   // slots and states land before the tail that publishes them
-        if (lane == 0) st_rlx(&T.ctl[1], tail + npush);
+    if (lane == 0) {
+        // the heap top is the next pop (nothing reorders the heap before it):
+        // its word is final for the leader unless a helper may still take it
+        // (queued) or finish it (running)
+        const uint32_t st = (uint32_t)(sv & 7);
+        const bool live = queued || ((uint32_t)(sv >> 3) == cn.end && (st == kStQueued || st == kStRunning));
+        C.pre_b = (K > 0 && !live) ? cn.begin : ~0u;
+        C.pre_sw = sv;
+        // the slots are published with the next split_team's first look
+        // (publish_tail), by when these stores have landed
+        if (npush) { C.qtail = tail + npush; C.qpend = 1; }
+    }
+}
+
+// Thread 0 of the leader: publish the slots enqueue_candidates wrote (their
+// stores land before the tail that publishes them).
+__device__ __forceinline__ void publish_tail(const Team& T, Ctl& C)
+{
+    if (C.qpend) {
+        drain_vmem();
+        st_rlx(&T.ctl[1], C.qtail);
+        C.qpend = 0;
     }
 }
 
@@ -2407,7 +2447,7 @@ __device__ void enqueue_early(const JobDev& J, const Common& cm, uint32_t b, uin
 {
     const Team& T = J.team;
     if (e <= b || e - b < cm.spec_min) return;
-    const uint32_t tail = T.ctl[1];
+    const uint32_t tail = T.ctl[1];   // (the first enqueue: nothing pending)
     if (tail - ld_rlx(&T.ctl[0]) >= kQueue) return;
     st_rlx(&T.state[b], ((unsigned long long)e << 3) | kStQueued);
     st_rlx(&T.queue[tail % kQueue], ((unsigned long long)b << 32) | e);
@@ -2416,9 +2456,9 @@ __device__ void enqueue_early(const JobDev& J, const Common& cm, uint32_t b, uin
     st_rlx(&T.ctl[1], tail + 1);
 }
 
-__device__ void stop_team(const JobDev& J, const Common& cm)
+__device__ void stop_team(const JobDev& J, const Common& cm, Ctl& C)
 {
-    if (J.team.helpers && threadIdx.x == 0) st_rel(&J.team.ctl[2], 1u);
+    if (J.team.helpers && threadIdx.x == 0) { publish_tail(J.team, C); st_rel(&J.team.ctl[2], 1u); }
     trace(cm, 6, 0);
 }
 
@@ -2531,6 +2571,77 @@ __device__ void spec_split(const JobDev& J0, const JobDev& Jw, const Common& cm,
     __syncthreads();
 }
 
+// The commit of a finished speculative split of [b, e) (split_team's mode
+// 1).  The result and the range were stored sc1 and drained before the done
+// flag (split, spec_split): sc1 loads, no acquire, and no barrier: thread 0
+// pushes the children (a single's id from the spec range) while the range
+// copy is in flight; wave 0 then queues, and the range's readers come after
+// later barriers.
+__device__ __forceinline__ void commit_spec(const JobDev& J, Ctl& C, uint32_t b, uint32_t e)
+{
+    const Team& T = J.team;
+    const int tid = threadIdx.x;
+    SplitRes r;
+    if (tid == 0) {
+        const auto* rr = gp(reinterpret_cast<const uint32_t*>(&T.res[b]));
+        uint32_t* rv = reinterpret_cast<uint32_t*>(&r);
+#pragma unroll
+        for (int k = 0; k < (int)(sizeof(SplitRes) / 4); k++)
+            rv[k] = __hip_atomic_load(&rr[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    copy_range_sc1(J.vrls, T.spec, b, e);
+    if (tid == 0) {
+        if (r.err || r.idx == 0xFFFFFFFFu) {
+            C.err = 1;
+        } else {
+            const uint32_t m = e - b, s2 = b + r.idx;
+            add_cluster(J, C, b, s2, r.fsu, r.fsi, T.spec);
+            add_cluster(J, C, s2, e, r.feu, r.fei, T.spec);
+            // the children's input is this result, in team.spec
+            st_rlx(&T.state[b], ((unsigned long long)s2 << 3) | kStNone | kStSpecBit);
+            st_rlx(&T.state[s2], ((unsigned long long)e << 3) | kStNone | kStSpecBit);
+            (void)m;
+        }
+    }
+}
+
+// The leader's usual split (split_team at N >= 2, where the pops are the
+// critical path): the popped cluster's speculative split has finished (the
+// word pop_wave fetched says done), so the leader commits it and queues the
+// next candidates.  Out of line and without calls: it saves no callee-saved
+// registers on entry, which split_team (its splits' state lives across calls)
+// does on every pop.  commit_ready_ok is uniform (C after the pop's barrier).
+__device__ __forceinline__ bool commit_ready_ok(const JobDev& J, const Common& cm, const Ctl& C, uint32_t e)
+{
+    return J.team.helpers && !C.team_off && !cm.enq_start && !(C.hlds && C.heap_n + 2 > kHeapLdsMax) &&
+           (uint32_t)(C.sw >> 3) == e && (C.sw & 7) == kStDone;
+}
+__device__ __noinline__ void commit_ready(const JobDev& J, const Common& cm, Ctl& C, uint32_t b, uint32_t e)
+{
+    const int tid = threadIdx.x;
+    if (tid == 0) {
+        publish_tail(J.team, C);
+        trace(cm, 3, b);
+        tcount(cm, TS_COMMIT);
+        if (C.prec) gpw(C.prec)[7] = 1u | (min(e - b, 0xFFFFFFu) << 8);
+    }
+#ifndef ALVRL_PT_POP
+    pmark(C, 2);
+    pmark(C, 3);
+#endif
+    commit_spec(J, C, b, e);
+#ifndef ALVRL_PT_POP
+    pmark(C, 4);
+#endif
+    if (tid < 64) {
+        if (!C.hlds) drain_vmem();   // wave 0 queues from the global heap thread 0 just wrote
+        enqueue_candidates(J, cm, C);
+    }
+    if (tid == 0) trace(cm, 5, b);
+    __syncthreads();
+    pmark(C, 5);
+}
+
 // The leader's split of [b, e): claim a queued task, wait for a running one
 // and commit its result, or split here.  While a helper still runs [b, e)
 // the leader splits other queued clusters speculatively.  spec = false:
@@ -2545,6 +2656,7 @@ __device__ void split_team(const JobDev& J, const Common& cm, Ctl& C, uint32_t b
     bool parked = false;   // the heap went back to global memory for a split here
     if (tid < 64 && cm.enq_start) enqueue_candidates(J, cm, C);
     if (tid == 0) {
+        publish_tail(T, C);
         trace(cm, 3, b);
         unsigned long long* st = &T.state[b];
         const unsigned long long key = (unsigned long long)e << 3;
@@ -2572,7 +2684,9 @@ __device__ void split_team(const JobDev& J, const Common& cm, Ctl& C, uint32_t b
     }
     __syncthreads();
     pf.mark(PF_T_STATE);
+#ifndef ALVRL_PT_POP
     pmark(C, 2);
+#endif
     while (true) {
         const int tm = C.tmode;
         __syncthreads();   // every thread has read tmode before thread 0 rewrites it
@@ -2607,10 +2721,12 @@ __device__ void split_team(const JobDev& J, const Common& cm, Ctl& C, uint32_t b
         pf.mark(PF_T_SIDE);
     }
     const int mode = C.tmode;
+#ifndef ALVRL_PT_POP
     pmark(C, 3);
+#endif
     if (tid == 0 && C.prec) gpw(C.prec)[7] = (uint32_t)mode | (min(e - b, 0xFFFFFFu) << 8);
     if (C.team_off) {   // set by thread 0 before the loop's last barrier
-        stop_team(J, cm);
+        stop_team(J, cm, C);
         heap_move(J, C, false);
         split(J, cm, C, b, e, lds, pf);
         return;
@@ -2621,36 +2737,12 @@ __device__ void split_team(const JobDev& J, const Common& cm, Ctl& C, uint32_t b
     }
     if (parked) heap_move(J, C, true);
     if (mode == 1) {
-        // the result and the range were stored sc1 and drained before the done
-        // flag (split, spec_split): sc1 loads, no acquire, and no barrier:
-        // thread 0 pushes the children (a single's id from the spec range)
-        // while the range copy is in flight; wave 0 then queues (below), and
-        // the range's readers come after later barriers
-        SplitRes r;
-        if (tid == 0) {
-            const auto* rr = gp(reinterpret_cast<const uint32_t*>(&T.res[b]));
-            uint32_t* rv = reinterpret_cast<uint32_t*>(&r);
-#pragma unroll
-            for (int k = 0; k < (int)(sizeof(SplitRes) / 4); k++)
-                rv[k] = __hip_atomic_load(&rr[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        copy_range_sc1(J.vrls, T.spec, b, e);
-        if (tid == 0) {
-            if (r.err || r.idx == 0xFFFFFFFFu) {
-                C.err = 1;
-            } else {
-                const uint32_t m = e - b, s2 = b + r.idx;
-                add_cluster(J, C, b, s2, r.fsu, r.fsi, T.spec);
-                add_cluster(J, C, s2, e, r.feu, r.fei, T.spec);
-                // the children's input is this result, in team.spec
-                st_rlx(&T.state[b], ((unsigned long long)s2 << 3) | kStNone | kStSpecBit);
-                st_rlx(&T.state[s2], ((unsigned long long)e << 3) | kStNone | kStSpecBit);
-                (void)m;
-            }
-        }
+        commit_spec(J, C, b, e);
         pf.mark(PF_T_COMMIT);
     }
+#ifndef ALVRL_PT_POP
     pmark(C, 4);
+#endif
     // an own split releases its vrls (every wave drained, barrier, one
     // write-back) before its children can be queued; a committed one's
     // children read team.spec
@@ -3070,6 +3162,7 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
         C.hlog_n = 0; C.hlog_full = 1;
         C.prec = nullptr;
         C.hlds = 0; C.hpool = pool;
+        C.qpend = 0; C.pre_b = ~0u;
     }
     __syncthreads();
     const bool tsu = cm.team_setup && cm.team > 1 && J.team.helpers != 0;
@@ -3154,7 +3247,8 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
                 }
                 __syncthreads();
                 if (!C.go) break;
-                split_team(J, cm, C, C.b, C.e, lds, pf, true);
+                if (commit_ready_ok(J, cm, C, C.e)) commit_ready(J, cm, C, C.b, C.e);
+                else split_team(J, cm, C, C.b, C.e, lds, pf, true);
             }
             heap_move(J, C, false);
         } else {
@@ -3192,8 +3286,13 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
                     __syncthreads();
                     if (!C.go) break;
                     pf.mark(PF_T_HEAP);
+#ifdef ALVRL_PT_POP
+                    pmark(C, 4);
+#else
                     pmark(C, 1);
-                    split_team(J, cm, C, C.b, C.e, lds, pf, true);
+#endif
+                    if (commit_ready_ok(J, cm, C, C.e)) commit_ready(J, cm, C, C.b, C.e);
+                    else split_team(J, cm, C, C.b, C.e, lds, pf, true);
                     if (tid == 0) {
                         nsplit++;
                         const float curr = conv_const(C, N, J.pixel_under);
@@ -3213,7 +3312,7 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
                     if (C.stop) break;
                 }
                 if (tid == 0) C.prec = nullptr;
-                stop_team(J, cm);
+                stop_team(J, cm, C);
                 heap_move(J, C, false);
                 restore(J, C);
                 if (dc != 1) {
@@ -3235,7 +3334,7 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
             }
         }
     }
-    stop_team(J, cm);
+    stop_team(J, cm, C);
     if (cm.jtime && threadIdx.x == 0) cm.jtime[3 * blockIdx.x + 1] = wall();
     __syncthreads();
     pf.mark(PF_CTRL);
