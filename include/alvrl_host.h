@@ -85,6 +85,24 @@ ALVRL_API int alvrl_scene_records_gpu(const alvrl_scene_desc *s, int medium_scat
 ALVRL_API int alvrl_scene_chain(const alvrl_scene_desc *s, int medium_scatters, uint32_t seed, uint32_t pass,
                                 int spec_rr_depth, float init_throughput, int x, int y, alvrl_gather_rec *out,
                                 uint32_t cap, uint32_t *n);
+/* Multi-sample renders (renderBlock's sample loop, integrator.cpp:240-264):
+ * sensor sample j of spp is the pixel centre when spp == 1, else (x, y) +
+ * rRec.nextSample2D(), drawn from the counter stream (seed, pass, dom 8,
+ * pixel, j).  A record's depth word carries j in bits 16-31, and the gathers
+ * key their streams by it (bits 0-15 of the stream word), so sample 0 gives
+ * the single-sample records and contributions.  alvrl_scene_records_spp:
+ * n * spp records, sample major (record j * n + i = pixel_ids[i], sample j).
+ * alvrl_scene_chain_spp: alvrl_scene_chain's eye path from sensor sample j
+ * (record k's depth word k | (j << 16); its roulette draws from (pixel,
+ * k | (j << 16))).  spp <= 65535. */
+ALVRL_API int alvrl_scene_records_spp(const alvrl_scene_desc *s, int medium_scatters, uint32_t seed, uint32_t pass,
+                                      uint32_t spp, const uint32_t *pixel_ids, uint32_t n, alvrl_gather_rec *out);
+ALVRL_API int alvrl_scene_records_spp_gpu(const alvrl_scene_desc *s, int medium_scatters, uint32_t seed,
+                                          uint32_t pass, uint32_t spp, const uint32_t *d_pixel_ids, uint32_t n,
+                                          alvrl_gather_rec *d_out, void *stream);
+ALVRL_API int alvrl_scene_chain_spp(const alvrl_scene_desc *s, int medium_scatters, uint32_t seed, uint32_t pass,
+                                    int spec_rr_depth, float init_throughput, int x, int y, uint32_t sample,
+                                    uint32_t spp, alvrl_gather_rec *out, uint32_t cap, uint32_t *n);
 /* The slicing record of pixel (x, y) (buildSlices, Preprocessor.cpp:1140-1170):
  * the first hit that is not a null surface; HIT flag, position and normal. */
 ALVRL_API int alvrl_scene_slice_record(const alvrl_scene_desc *s, int x, int y, alvrl_gather_rec *out);

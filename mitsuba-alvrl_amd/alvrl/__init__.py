@@ -493,6 +493,9 @@ def _host():
     L.alvrl_trace_vrls.argtypes = [P(SceneDesc), u32, u32, u32, i32, i32, i32, vp, u32, P(u32), P(u64)]
     L.alvrl_trace_vrls_gpu.argtypes = [P(SceneDesc), u32, u32, u32, i32, i32, i32, vp, u32, P(u32), P(u64)]
     L.alvrl_scene_records_gpu.argtypes = [P(SceneDesc), i32, vp, u32, vp, vp]
+    L.alvrl_scene_records_spp.argtypes = [P(SceneDesc), i32, u32, u32, u32, vp, u32, vp]
+    L.alvrl_scene_records_spp_gpu.argtypes = [P(SceneDesc), i32, u32, u32, u32, vp, u32, vp, vp]
+    L.alvrl_scene_chain_spp.argtypes = [P(SceneDesc), i32, u32, u32, i32, f32, i32, i32, u32, u32, vp, u32, P(u32)]
     L.alvrl_volpath_default.argtypes = [P(VolpathParams)]; L.alvrl_volpath_default.restype = None
     L.alvrl_volpath_render.argtypes = [P(SceneDesc), P(VolpathParams), u32, u32, u32, vp, u32, vp, vp]
     L.alvrl_read_vrl_file.argtypes = [C.c_char_p, P(MediumDesc), vp, u32, P(u32), P(u64)]
@@ -601,6 +604,31 @@ def scene_chain(scene: SceneDesc, x: int, y: int, medium_scatters: bool = True, 
     return out[:n.value].copy()
 
 
+def scene_records_spp(scene: SceneDesc, spp: int, pixel_ids=None, medium_scatters: bool = True,
+                      seed: int = 0xA1B2C3D4, pass_: int = 0) -> np.ndarray:
+    """alvrl_scene_records_spp: the records of spp sensor samples per pixel,
+    sample major ((spp * n, REC_WORDS); record j * n + i = pixel i, sample j)."""
+    L = _host()
+    n = scene.width * scene.height if pixel_ids is None else len(pixel_ids)
+    out = np.zeros((spp * n, REC_WORDS), np.float32)
+    ids = None if pixel_ids is None else _np(pixel_ids, np.uint32)
+    _hcheck(L.alvrl_scene_records_spp(C.byref(scene), int(medium_scatters), seed, pass_, spp, _ptr(ids), n,
+                                      _ptr(out)))
+    return out
+
+
+def scene_chain_spp(scene: SceneDesc, x: int, y: int, sample: int, spp: int, medium_scatters: bool = True,
+                    seed: int = 0xA1B2C3D4, pass_: int = 0, spec_rr_depth: int = 100,
+                    init_throughput: float = 20.0) -> np.ndarray:
+    """alvrl_scene_chain_spp: the eye path of sensor sample `sample` of `spp`."""
+    L = _host()
+    out = np.zeros((256, REC_WORDS), np.float32)
+    n = C.c_uint32()
+    _hcheck(L.alvrl_scene_chain_spp(C.byref(scene), int(medium_scatters), seed, pass_, spec_rr_depth,
+                                    float(init_throughput), x, y, sample, spp, _ptr(out), 256, C.byref(n)))
+    return out[:n.value].copy()
+
+
 def scene_slice_record(scene: SceneDesc, x: int, y: int) -> np.ndarray:
     L = _host()
     out = np.zeros(REC_WORDS, np.float32)
@@ -631,6 +659,22 @@ def scene_records_gpu(scene: SceneDesc, pixel_ids=None, medium_scatters: bool = 
         stream = torch.cuda.current_stream(dev).cuda_stream
         _hcheck(L.alvrl_scene_records_gpu(C.byref(scene), int(medium_scatters),
                                           None if ids is None else ids.data_ptr(), n, out.data_ptr(), stream))
+    return out
+
+
+def scene_records_spp_gpu(scene: SceneDesc, spp: int, pixel_ids=None, medium_scatters: bool = True,
+                          seed: int = 0xA1B2C3D4, pass_: int = 0, device: int = 0):
+    """alvrl_scene_records_spp_gpu: scene_records_spp on the HIP device (a CUDA tensor)."""
+    import torch
+    L = _host()
+    dev = torch.device("cuda", device)
+    n = scene.width * scene.height if pixel_ids is None else len(pixel_ids)
+    out = torch.empty((spp * n, REC_WORDS), dtype=torch.float32, device=dev)
+    ids = None if pixel_ids is None else torch.as_tensor(np.asarray(pixel_ids, np.uint32).astype(np.int32)).to(dev)
+    with torch.cuda.device(dev):
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        _hcheck(L.alvrl_scene_records_spp_gpu(C.byref(scene), int(medium_scatters), seed, pass_, spp,
+                                              None if ids is None else ids.data_ptr(), n, out.data_ptr(), stream))
     return out
 
 

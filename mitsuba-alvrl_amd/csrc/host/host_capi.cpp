@@ -114,17 +114,47 @@ ALVRL_API int alvrl_scene_records(const alvrl_scene_desc* s, int medium_scatters
     return ALVRL_OK;
 }
 
+ALVRL_API int alvrl_scene_records_spp(const alvrl_scene_desc* s, int medium_scatters, uint32_t seed, uint32_t pass,
+                                      uint32_t spp, const uint32_t* ids, uint32_t n, alvrl_gather_rec* out)
+{
+    if (!s || (!out && n)) return herr(ALVRL_ERR_INVALID, "alvrl_scene_records_spp: null argument");
+    if (spp == 0 || (uint64_t)spp * n > 0xFFFFFFFFull || spp > 0xFFFFu)
+        return herr(ALVRL_ERR_INVALID, "alvrl_scene_records_spp: spp out of range");
+    if (const char* m = scene_problem(*s)) return herr(ALVRL_ERR_INVALID, m);
+    const SmokeBox b = to_box(*s);
+    const uint64_t npix = (uint64_t)b.width * (uint64_t)b.height;
+    if (!ids && n != npix) return herr(ALVRL_ERR_INVALID, "alvrl_scene_records_spp: n must be W*H without pixel ids");
+    const bool scat = medium_scatters && !(b.medium.sigma_s[0] == 0 && b.medium.sigma_s[1] == 0 && b.medium.sigma_s[2] == 0);
+    for (uint32_t j = 0; j < spp; j++)
+        for (uint32_t i = 0; i < n; i++) {
+            const uint32_t p = ids ? ids[i] : i;
+            if (p >= npix) return herr(ALVRL_ERR_INVALID, "alvrl_scene_records_spp: pixel id out of range");
+            b.make_record((int)(p % (uint32_t)b.width), (int)(p / (uint32_t)b.width), scat,
+                          reinterpret_cast<float*>(&out[(size_t)j * n + i]), seed, pass, j, spp);
+        }
+    return ALVRL_OK;
+}
+
 ALVRL_API int alvrl_scene_chain(const alvrl_scene_desc* s, int medium_scatters, uint32_t seed, uint32_t pass,
                                 int spec_rr_depth, float init_throughput, int x, int y, alvrl_gather_rec* out,
                                 uint32_t cap, uint32_t* n)
 {
+    return alvrl_scene_chain_spp(s, medium_scatters, seed, pass, spec_rr_depth, init_throughput, x, y, 0, 1, out,
+                                 cap, n);
+}
+
+ALVRL_API int alvrl_scene_chain_spp(const alvrl_scene_desc* s, int medium_scatters, uint32_t seed, uint32_t pass,
+                                    int spec_rr_depth, float init_throughput, int x, int y, uint32_t sample,
+                                    uint32_t spp, alvrl_gather_rec* out, uint32_t cap, uint32_t* n)
+{
+    if (spp == 0 || sample >= spp || spp > 0xFFFFu) return herr(ALVRL_ERR_INVALID, "alvrl_scene_chain: sample out of range");
     if (!s || !n || (!out && cap)) return herr(ALVRL_ERR_INVALID, "alvrl_scene_chain: null argument");
     if (const char* m = scene_problem(*s)) return herr(ALVRL_ERR_INVALID, m);
     const SmokeBox b = to_box(*s);
     if (x < 0 || y < 0 || x >= b.width || y >= b.height) return herr(ALVRL_ERR_INVALID, "alvrl_scene_chain: pixel out of range");
     const bool scat = medium_scatters && !(b.medium.sigma_s[0] == 0 && b.medium.sigma_s[1] == 0 && b.medium.sigma_s[2] == 0);
     std::vector<float> recs;
-    b.make_chain(x, y, scat, seed, pass, spec_rr_depth, init_throughput, &recs);
+    b.make_chain(x, y, scat, seed, pass, spec_rr_depth, init_throughput, &recs, sample, spp);
     const uint32_t k = (uint32_t)(recs.size() / kRecWords);
     *n = k;
     if (k > cap) return herr(ALVRL_ERR_INVALID, "alvrl_scene_chain: capacity too small");

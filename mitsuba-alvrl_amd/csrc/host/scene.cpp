@@ -18,6 +18,7 @@ namespace {
 constexpr double kPi = 3.14159265358979323846;
 constexpr uint32_t kDomTracer = 3u;
 constexpr uint32_t kDomEye = 7u;   // Russian roulette of the eye paths' specular chains
+constexpr uint32_t kDomPixel = 8u;   // sensor sample offsets of multi-sample renders
 
 inline float fastexp(float v) { return (float)std::exp((double)v); }   // math.h:185-199
 inline float fastlog(float v) { return (float)std::log((double)v); }
@@ -235,11 +236,13 @@ bool SmokeBox::visible(V3 p1, bool p1_surface, V3 p2, bool p2_surface) const
     return true;
 }
 
-void SmokeBox::make_record(int x, int y, bool medium_scatters, float rec[kRecWords]) const
+void SmokeBox::make_record(int x, int y, bool medium_scatters, float rec[kRecWords], uint32_t seed, uint32_t pass,
+                           uint32_t sample, uint32_t spp) const
 {
     V3 O, D, n, p;
-    float mint;
-    camera_ray((float)x + 0.5f, (float)y + 0.5f, &O, &D, &mint);   // renderBlock pixel centre, integrator.cpp:243-245
+    float mint, px, py;
+    pixel_sample(x, y, seed, pass, sample, spp, &px, &py);
+    camera_ray(px, py, &O, &D, &mint);   // renderBlock's sensor sample, integrator.cpp:240-247
     int tri;
     const float t = first_hit(O, D, mint, &n, &p, &tri);
     const uint32_t m = mat(tri);
@@ -255,7 +258,7 @@ void SmokeBox::make_record(int x, int y, bool medium_scatters, float rec[kRecWor
     rec[12] = a[0]; rec[13] = a[1]; rec[14] = a[2];
     std::memcpy(&rec[15], &flags, 4);
     rec[16] = rec[17] = rec[18] = 1.0f;   // the camera ray: path weight 1, depth 0
-    const uint32_t depth = 0;
+    const uint32_t depth = sample << 16;
     std::memcpy(&rec[19], &depth, 4);
 }
 
@@ -507,12 +510,26 @@ void trace_particle(const SmokeBox& sc, Stream& smp, bool short_vrls, int max_de
 
 }  // namespace
 
+void SmokeBox::pixel_sample(int x, int y, uint32_t seed, uint32_t pass, uint32_t sample, uint32_t spp, float* px,
+                            float* py) const
+{
+    if (spp <= 1) {
+        *px = (float)x + 0.5f;
+        *py = (float)y + 0.5f;
+        return;
+    }
+    Stream smp{seed, pass, kDomPixel, (uint32_t)y * (uint32_t)width + (uint32_t)x, sample, 0u};
+    *px = (float)x + smp.next();
+    *py = (float)y + smp.next();
+}
+
 void SmokeBox::make_chain(int x, int y, bool medium_scatters, uint32_t seed, uint32_t pass, int spec_rr_depth,
-                          float init_throughput, std::vector<float>* out) const
+                          float init_throughput, std::vector<float>* out, uint32_t sample, uint32_t spp) const
 {
     V3 O, D;
-    float mint;
-    camera_ray((float)x + 0.5f, (float)y + 0.5f, &O, &D, &mint);   // the pixel centre (integrator.cpp:243-245)
+    float mint, px, py;
+    pixel_sample(x, y, seed, pass, sample, spp, &px, &py);
+    camera_ray(px, py, &O, &D, &mint);   // the sensor sample (integrator.cpp:240-247)
     const uint32_t pixel = (uint32_t)y * (uint32_t)width + (uint32_t)x;
     float weight[3] = {1.0f, 1.0f, 1.0f};
     float thr[3] = {init_throughput, init_throughput, init_throughput};   // throughputWithEtaSq (:381)
@@ -535,7 +552,8 @@ void SmokeBox::make_chain(int x, int y, bool medium_scatters, uint32_t seed, uin
         for (int i = 0; i < 3; i++) rec[12 + i] = m == 0u ? a[i] : 0.0f;
         std::memcpy(&rec[15], &flags, 4);
         for (int i = 0; i < 3; i++) rec[16 + i] = weight[i];
-        std::memcpy(&rec[19], &k, 4);
+        const uint32_t kw = k | (sample << 16);
+        std::memcpy(&rec[19], &kw, 4);
         if (m == 0u) break;                                               // no delta component (:449-450)
         // transmittance of the segment, rRec.medium->eval(Ray(ray, 0, its.t)) (:452-458)
         float tr[3];
@@ -568,7 +586,7 @@ void SmokeBox::make_chain(int x, int y, bool medium_scatters, uint32_t seed, uin
         float mx = thr2[0] > thr2[1] ? thr2[0] : thr2[1];
         mx = mx > thr2[2] ? mx : thr2[2];
         const float rrProb = maxRR < mx ? maxRR : mx;
-        Stream smp{seed, pass, kDomEye, pixel, k, 0u};
+        Stream smp{seed, pass, kDomEye, pixel, k | (sample << 16), 0u};
         if (rrProb <= 0 || (rrProb < 1 && smp.next() > rrProb)) break;
         for (int i = 0; i < 3; i++) {
             thr[i] = thr2[i] / rrProb;

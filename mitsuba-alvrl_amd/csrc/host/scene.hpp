@@ -105,15 +105,25 @@ struct SmokeBox {
     // its depth; Russian roulette from initialSpecularThroughput, maxRR 0.98
     // past specularForcedRRdepth (:475-492), its uniform from the stream
     // (seed, pass, dom 7, pixel, depth).  Appends kRecWords floats per record.
+    // sample, spp: sensor sample j of spp (pixel_sample); record k's depth
+    // word is k | (j << 16) and its roulette draws from (pixel, k | (j << 16)).
     void make_chain(int x, int y, bool medium_scatters, uint32_t seed, uint32_t pass, int spec_rr_depth,
-                    float init_throughput, std::vector<float>* out) const;
+                    float init_throughput, std::vector<float>* out, uint32_t sample = 0, uint32_t spp = 1) const;
     // buildSlices' gather point of pixel (x, y) (Preprocessor.cpp:1144-1170):
     // the camera ray's first hit, continued through null surfaces; a record
     // with the hit flag, position and normal of that point.
     void make_slice_record(int x, int y, float rec[kRecWords]) const;
     uint32_t n_occ() const { return (uint32_t)(occ.size() / 9); }
-    // Gather record (alvrl_gather_rec layout) of pixel centre (x, y).
-    void make_record(int x, int y, bool medium_scatters, float rec[kRecWords]) const;
+    // The sensor sample of pixel (x, y), sample j of spp (renderBlock,
+    // integrator.cpp:240-247): the pixel centre for one sample per pixel,
+    // else (x, y) + rRec.nextSample2D(), here draws 0 and 1 of the stream
+    // (seed, pass, dom 8, pixel, j).
+    void pixel_sample(int x, int y, uint32_t seed, uint32_t pass, uint32_t sample, uint32_t spp, float* px,
+                      float* py) const;
+    // Gather record (alvrl_gather_rec layout) of pixel centre (x, y), or of
+    // its sensor sample j of spp; the depth word carries j in bits 16-31.
+    void make_record(int x, int y, bool medium_scatters, float rec[kRecWords], uint32_t seed = 0,
+                     uint32_t pass = 0, uint32_t sample = 0, uint32_t spp = 1) const;
     float scene_diagonal() const;   // distance(getAABB().min, getAABB().max)
 };
 

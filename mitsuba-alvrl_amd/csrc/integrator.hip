@@ -82,6 +82,12 @@ struct DevBuf {
 };
 }  // namespace
 
+__global__ void __launch_bounds__(256) k_scale_f32(float* __restrict__ v, uint32_t n, float f)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) v[i] *= f;
+}
+
 struct alvrl_integrator {
     // ---- properties (vrlIntegrator.cpp:128-208; integrator.cpp:272-277, 348-349)
     bool shortVrls = true;
@@ -90,6 +96,7 @@ struct alvrl_integrator {
     int specRRdepth = 100;
     float initialSpecularThroughput = 20;
     int volVolSamples = 2, volSurfSamples = 2;
+    int sampleCount = 1;      // the sampler's sampleCount: sensor samples per pixel and pass (integrator.cpp:240-264)
     bool globalCluster = false;
     float globalUndersampling = -1;
     bool localRefinement = true;
@@ -184,6 +191,10 @@ struct alvrl_integrator {
         else if (k == "initialSpecularThroughput") initialSpecularThroughput = f(v);
         else if (k == "volVolSamples") volVolSamples = i(v);
         else if (k == "volSurfSamples") volSurfSamples = i(v);
+        else if (k == "sampleCount") {
+            sampleCount = i(v);
+            if (sampleCount < 1 || sampleCount > 65535) throw IntegError(ALVRL_ERR_INVALID, "sampleCount must be in [1, 65535]");
+        }
         else if (k == "globalCluster") globalCluster = b(v);
         else if (k == "globalUndersampling") globalUndersampling = f(v);
         else if (k == "localRefinement") localRefinement = b(v);
@@ -377,7 +388,7 @@ struct alvrl_integrator {
         std::vector<std::vector<uint32_t>> src;
     };
     Chains expand_chains(const std::vector<uint32_t>& ids, bool scat, bool accum,
-                         std::vector<alvrl_gather_rec>* prim) const
+                         std::vector<alvrl_gather_rec>* prim, uint32_t sample = 0, uint32_t spp = 1) const
     {
         prim->resize(ids.size());
         const uint32_t n = (uint32_t)ids.size();
@@ -390,10 +401,11 @@ struct alvrl_integrator {
             Chains& c = part[t];
             const uint32_t b = (uint32_t)((uint64_t)n * t / nt), e = (uint32_t)((uint64_t)n * (t + 1) / nt);
             for (uint32_t i = b; i < e; i++) {
-                scene.make_record((int)(ids[i] % W), (int)(ids[i] / W), scat, reinterpret_cast<float*>(&(*prim)[i]));
+                scene.make_record((int)(ids[i] % W), (int)(ids[i] / W), scat, reinterpret_cast<float*>(&(*prim)[i]),
+                                  seed, cur_pass, sample, spp);
                 buf.clear();
                 scene.make_chain((int)(ids[i] % W), (int)(ids[i] / W), scat, seed, cur_pass, specRRdepth,
-                                 initialSpecularThroughput, &buf);
+                                 initialSpecularThroughput, &buf, sample, spp);
                 const size_t k = buf.size() / kRecWords;
                 for (size_t d = 1; d < k; d++) {
                     if (c.recs.size() < d) { c.recs.resize(d); c.src.resize(d); }
@@ -749,8 +761,10 @@ struct alvrl_integrator {
     void prepare_render(uint32_t rank, uint32_t world)
     {
         const uint32_t mode = clustered ? 2u : 1u;
-        // chains depend on the pass (their Russian roulette)
-        if (cache_rank == rank && cache_world == world && cache_mode == mode && (!chains || cache_pass == cur_pass))
+        // chains (their Russian roulette) and sensor samples depend on the pass
+        const uint32_t S = (uint32_t)sampleCount;
+        if (cache_rank == rank && cache_world == world && cache_mode == mode &&
+            ((!chains && S == 1) || cache_pass == cur_pass))
             return;
         const int W = scene.width, H = scene.height;
         uint32_t npix = 0;
@@ -784,22 +798,48 @@ struct alvrl_integrator {
         }
         const bool scat = !(scene.medium.sigma_s[0] == 0 && scene.medium.sigma_s[1] == 0 && scene.medium.sigma_s[2] == 0);
         const uint32_t nprim = (uint32_t)pix.size();
-        level_rec.assign({0u, nprim});
-        level_item.assign({0u, (uint32_t)items.size()});
+        if ((uint64_t)nprim * S > 0x7FFFFFFFull) throw IntegError(ALVRL_ERR_INVALID, "sampleCount too large for the frame");
+        // the sensor samples' primary records, sample major: block j holds
+        // sample j of every owned pixel (the pixel order and work items of
+        // block 0); each block is one accumulation level
+        level_rec.assign({0u});
+        level_item.assign({0u});
+        {
+            const size_t nit = items.size();
+            for (uint32_t j = 0; j < S; j++) {
+                if (j)
+                    for (size_t k = 0; k < nit; k++) {
+                        alvrl_work_item w = items[k];
+                        w.begin += j * nprim;
+                        items.push_back(w);
+                    }
+                level_rec.push_back((j + 1) * nprim);
+                level_item.push_back((uint32_t)items.size());
+            }
+            const std::vector<uint32_t> p0(pix);
+            pix.reserve((size_t)nprim * S);
+            for (uint32_t j = 1; j < S; j++) pix.insert(pix.end(), p0.begin(), p0.end());
+        }
         std::vector<alvrl_gather_rec> extra;   // the chains' records, level by level
         std::vector<alvrl_gather_rec> prim;
         if (chains) {
-            Chains ch = expand_chains(pix, scat, false, &prim);
-            for (size_t d = 0; d < ch.recs.size(); d++) {
-                std::vector<uint32_t> recpix(ch.src[d].size());
-                for (size_t j = 0; j < recpix.size(); j++) recpix[j] = pix[ch.src[d][j]];
-                const uint32_t base = nprim + (uint32_t)extra.size();
-                std::vector<uint32_t> order(recpix.size());
-                for (size_t j = 0; j < order.size(); j++) order[j] = (uint32_t)j;
-                if (clustered) bucket(&order, recpix, base);
-                for (uint32_t j : order) { extra.push_back(ch.recs[d][j]); pix.push_back(recpix[j]); }
-                level_rec.push_back(nprim + (uint32_t)extra.size());
-                level_item.push_back((uint32_t)items.size());
+            prim.resize((size_t)nprim * S);
+            const std::vector<uint32_t> ppix(pix.begin(), pix.begin() + nprim);
+            for (uint32_t j = 0; j < S; j++) {
+                std::vector<alvrl_gather_rec> pj;
+                Chains ch = expand_chains(ppix, scat, false, &pj, j, S);
+                std::copy(pj.begin(), pj.end(), prim.begin() + (size_t)j * nprim);
+                for (size_t d = 0; d < ch.recs.size(); d++) {
+                    std::vector<uint32_t> recpix(ch.src[d].size());
+                    for (size_t k = 0; k < recpix.size(); k++) recpix[k] = ppix[ch.src[d][k]];
+                    const uint32_t base = nprim * S + (uint32_t)extra.size();
+                    std::vector<uint32_t> order(recpix.size());
+                    for (size_t k = 0; k < order.size(); k++) order[k] = (uint32_t)k;
+                    if (clustered) bucket(&order, recpix, base);
+                    for (uint32_t k : order) { extra.push_back(ch.recs[d][k]); pix.push_back(recpix[k]); }
+                    level_rec.push_back(nprim * S + (uint32_t)extra.size());
+                    level_item.push_back((uint32_t)items.size());
+                }
             }
         }
         nrec = (uint32_t)pix.size();
@@ -808,15 +848,16 @@ struct alvrl_integrator {
         pix_buf.ensure(nrec);
         out_buf.ensure((size_t)3 * nrec);
         hchk(hipMemcpyAsync(pix_buf.p, pix.data(), sizeof(uint32_t) * nrec, hipMemcpyHostToDevice, stream), "copy pixels");
-        // the eye-ray first hits of the owned pixels, on the device
+        // the eye-ray first hits of the owned pixels' sensor samples, on the device
         if (chains) {
             if (nprim)
-                hchk(hipMemcpyAsync(rec_buf.p, prim.data(), sizeof(alvrl_gather_rec) * nprim, hipMemcpyHostToDevice,
-                                    stream), "copy records");
+                hchk(hipMemcpyAsync(rec_buf.p, prim.data(), sizeof(alvrl_gather_rec) * prim.size(),
+                                    hipMemcpyHostToDevice, stream), "copy records");
         } else
-            chk_host(alvrl_scene_records_gpu(&scene_desc, scat ? 1 : 0, pix_buf.p, nprim, rec_buf.p, stream));
+            chk_host(alvrl_scene_records_spp_gpu(&scene_desc, scat ? 1 : 0, seed, cur_pass, S, pix_buf.p, nprim,
+                                                 rec_buf.p, stream));
         if (!extra.empty())
-            hchk(hipMemcpyAsync(rec_buf.p + nprim, extra.data(), sizeof(alvrl_gather_rec) * extra.size(),
+            hchk(hipMemcpyAsync(rec_buf.p + (size_t)nprim * S, extra.data(), sizeof(alvrl_gather_rec) * extra.size(),
                                 hipMemcpyHostToDevice, stream), "copy chain records");
         if (nitems) {
             item_buf.ensure(nitems);
@@ -847,7 +888,7 @@ struct alvrl_integrator {
             if (!clustered && !numVrlFalseColor)
                 throw IntegError(ALVRL_ERR_INVALID, "requested slices false color image without clustering!");
             const int mode = numVrlFalseColor ? ALVRL_FALSE_COLOR_NUM_VRLS : ALVRL_FALSE_COLOR_SLICES;
-            if (!numVrlFalseColor) levels = 1;
+            if (!numVrlFalseColor) levels = (uint32_t)sampleCount;   // the primary blocks
             chk(alvrl_gather_false_color(ctx, mode, rec_buf.p, clustered ? item_buf.p : nullptr,
                                          clustered ? level_item[levels] : level_rec[levels], out_buf.p, s),
                 "alvrl_gather_false_color");
@@ -855,6 +896,14 @@ struct alvrl_integrator {
             chk(alvrl_gather_clustered(ctx, rec_buf.p, pix_buf.p, item_buf.p, nitems, out_buf.p, s), "alvrl_gather_clustered");
         else
             chk(alvrl_gather_brute(ctx, rec_buf.p, pix_buf.p, nrec, out_buf.p, s), "alvrl_gather_brute");
+        // ImageBlock::put of each sensor sample, normalised by the box
+        // filter's weight sum at develop time: the mean over the samples
+        if (sampleCount > 1 && level_rec[levels]) {
+            const uint32_t nv = 3u * level_rec[levels];
+            hipLaunchKernelGGL(k_scale_f32, dim3((nv + 255) / 256), dim3(256), 0, s, out_buf.p, nv,
+                               1.0f / (float)sampleCount);
+            hchk(hipGetLastError(), "k_scale_f32");
+        }
         for (uint32_t d = 0; d < levels; d++)
             chk(alvrl_accumulate_rgb(ctx, out_buf.p + (size_t)3 * level_rec[d], pix_buf.p + level_rec[d],
                                      level_rec[d + 1] - level_rec[d], d_fb, s), "alvrl_accumulate_rgb");

@@ -459,13 +459,41 @@ struct TCam {
 // Sensor::sampleRay at the pixel centre + Scene::rayIntersect (host
 // SmokeBox::make_record, bit for bit): the GPU eye-ray first hit of SURVEY
 // 8(f) row 1.  pix == nullptr: pixel i.
+// Sensor sample j of spp > 1 (SmokeBox::pixel_sample): draws 0 and 1 of the
+// counter stream (seed, pass, dom 8, pixel, j).
+constexpr uint32_t kDomPixel = 8u;
+__device__ __forceinline__ void pixel_jitter(uint32_t seed, uint32_t pass, uint32_t pixel, uint32_t j, float* u,
+                                             float* v)
+{
+    uint32_t c0 = pixel, c1 = j, c2 = 0u, c3 = kDomPixel << 24;
+    uint32_t k0 = seed, k1 = pass;
+    for (int r = 0; r < 10; r++) {
+        if (r > 0) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0, n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        c0 = n0; c1 = (uint32_t)p1; c2 = n2; c3 = (uint32_t)p0;
+    }
+    *u = __uint_as_float((c0 >> 9) | 0x3f800000u) - 1.0f;
+    *v = __uint_as_float((c1 >> 9) | 0x3f800000u) - 1.0f;
+}
+
+// spp records per pixel, sample major: record j * n + i is pixel pix[i],
+// sensor sample j (its depth word j << 16); spp == 1: pixel centres.
 __global__ void __launch_bounds__(256) k_eye_records(TCam c, TScene sc, const uint32_t* __restrict__ pix,
-                                                     uint32_t n, float* __restrict__ out)
+                                                     uint32_t n, uint32_t spp, uint32_t seed, uint32_t pass,
+                                                     float* __restrict__ out)
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t id = pix ? pix[i] : i;
-    const float px = (float)(id % c.width) + 0.5f, py = (float)(id / c.width) + 0.5f;
+    if (i >= n * spp) return;
+    const uint32_t j = i / n, ii = i - j * n;
+    const uint32_t id = pix ? pix[ii] : ii;
+    float px = (float)(id % c.width) + 0.5f, py = (float)(id / c.width) + 0.5f;
+    if (spp > 1) {
+        float u, v;
+        pixel_jitter(seed, pass, id, j, &u, &v);
+        px = (float)(id % c.width) + u;
+        py = (float)(id / c.width) + v;
+    }
     const float sx = px * c.inv_w, sy = py * c.inv_h;
     const float xc = (1.0f - 2.0f * sx) * c.tanh_;
     const float yc = ((1.0f - 2.0f * sy) / c.aspect) * c.tanh_;
@@ -489,7 +517,7 @@ __global__ void __launch_bounds__(256) k_eye_records(TCam c, TScene sc, const ui
     for (int k = 0; k < 15; k++) r[k] = v[k];
     r[15] = __uint_as_float(flags);
     r[16] = 1.0f; r[17] = 1.0f; r[18] = 1.0f;   // a camera ray: path weight 1, depth 0
-    r[19] = __uint_as_float(0u);
+    r[19] = __uint_as_float(j << 16);
 }
 
 // ----------------------------------------------------- volpath reference --
@@ -809,7 +837,18 @@ ALVRL_API int alvrl_volpath_render(const alvrl_scene_desc* s, const alvrl_volpat
 ALVRL_API int alvrl_scene_records_gpu(const alvrl_scene_desc* s, int medium_scatters, const uint32_t* d_pixel_ids,
                                       uint32_t n, alvrl_gather_rec* d_out, void* stream)
 {
+    return alvrl_scene_records_spp_gpu(s, medium_scatters, 0u, 0u, 1u, d_pixel_ids, n, d_out, stream);
+}
+
+// The sensor samples of alvrl_scene_records_spp (the host's, bit for bit):
+// n * spp device records, sample major.
+ALVRL_API int alvrl_scene_records_spp_gpu(const alvrl_scene_desc* s, int medium_scatters, uint32_t seed,
+                                          uint32_t pass, uint32_t spp, const uint32_t* d_pixel_ids, uint32_t n,
+                                          alvrl_gather_rec* d_out, void* stream)
+{
     if (!s || (!d_out && n)) return terr(ALVRL_ERR_INVALID, "alvrl_scene_records_gpu: null argument");
+    if (spp == 0 || spp > 0xFFFFu || (uint64_t)spp * n > 0xFFFFFFFFull)
+        return terr(ALVRL_ERR_INVALID, "alvrl_scene_records_spp_gpu: spp out of range");
     if (const char* m = alvrl::host::scene_problem(*s)) return terr(ALVRL_ERR_INVALID, m);
     const alvrl::host::SmokeBox box = alvrl::host::to_box(*s);
     if (box.has_delta())
@@ -825,8 +864,9 @@ ALVRL_API int alvrl_scene_records_gpu(const alvrl_scene_desc* s, int medium_scat
     sc.bv = bv->view;
     const TCam c = make_tcam(box, medium_scatters && !sc.sigma_s_zero ? 1 : 0);
     hipStream_t st = (hipStream_t)stream;
-    hipLaunchKernelGGL(k_eye_records, dim3((n + 255) / 256), dim3(256), 0, st, c, sc, d_pixel_ids, n,
-                       reinterpret_cast<float*>(d_out));
+    const uint32_t total = n * spp;
+    hipLaunchKernelGGL(k_eye_records, dim3((total + 255) / 256), dim3(256), 0, st, c, sc, d_pixel_ids, n, spp, seed,
+                       pass, reinterpret_cast<float*>(d_out));
     if (hipGetLastError() != hipSuccess) return terr(ALVRL_ERR_HIP, "alvrl_scene_records_gpu: launch");
     // stream-ordered callers may replace the cached BVH after return: wait for the kernel
     if (hipStreamSynchronize(st) != hipSuccess) return terr(ALVRL_ERR_HIP, "alvrl_scene_records_gpu: sync");

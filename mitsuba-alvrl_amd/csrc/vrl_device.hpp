@@ -172,7 +172,8 @@ struct Rec {
     float ox, oy, oz, dx, dy, dz, px, py, pz, nx, ny, nz, ar, ag, ab;
     uint32_t flags;
     float wr, wg, wb;   // path weight of the segment (LiInternal's 'weight', vrlIntegrator.cpp:503-510)
-    uint32_t depth;     // eye-path vertex of the segment's start (0: camera ray): keys its streams
+    uint32_t depth;     // bits 0-15: eye-path vertex of the segment's start (0: camera ray); bits 16-31:
+                        // the sensor sample (multi-sample renders); both key its streams
 };
 static_assert(sizeof(Rec) == 80, "Rec layout");
 constexpr uint32_t kRecAccum = 16u;   // ALVRL_REC_ACCUM: the R build adds to the row's entries
@@ -423,7 +424,8 @@ __device__ __forceinline__ void integrate_vrl(const DevParams& P, const RecPre& 
     float mean = 0.0f, M2 = 0.0f, mean_acc = 0.0f, var_acc = 0.0f;
     const uint32_t k0 = P.seed, k1 = P.pass;
     // stream word: domain, the segment's eye-path depth, the R sample index
-    const uint32_t c3 = (domain << 24) | ((q.depth & 0xFFu) << 16) | (rsub & 0xFFFFu);
+    // plus the record's sensor sample (its depth word's bits 16-31)
+    const uint32_t c3 = (domain << 24) | ((q.depth & 0xFFu) << 16) | ((rsub + (q.depth >> 16)) & 0xFFFFu);
 
     // draws 0..3: volVol samples 0,1 (V, U); draws 4..7: volSurf / further volVol
     U4 rb = philox4x32_10(rec_id, vrl_id, 0u, c3, k0, k1);

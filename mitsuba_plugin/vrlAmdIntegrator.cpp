@@ -122,7 +122,8 @@ public:
                 continue;
             oss << names[i] << "=" << props.getAsString(names[i]) << ";";
         }
-        check(alvrl_integrator_create(oss.str().c_str(), m_device, &m_it), "alvrl_integrator_create");
+        m_props = oss.str();
+        check(alvrl_integrator_create(m_props.c_str(), m_device, &m_it), "alvrl_integrator_create");
         checkHip(hipSetDevice(m_device), "hipSetDevice");
         checkHip(hipStreamCreateWithFlags(&m_stream, hipStreamNonBlocking), "hipStreamCreate");
     }
@@ -137,6 +138,18 @@ public:
             int sceneResID, int sensorResID, int samplerResID) {
         ProgressiveMonteCarloIntegrator::preprocess(scene, queue, job, sceneResID,
             sensorResID, samplerResID);
+        /* the sampler's sampleCount: sensor samples per pixel and pass
+           (renderBlock's sample loop, integrator.cpp:240-264); the frame
+           mode's integrator jitters them itself, so it is re-created with it */
+        const Sampler *smp = static_cast<Sampler *>(Scheduler::getInstance()->getResource(samplerResID, 0));
+        m_sampleCount = (int) smp->getSampleCount();
+        if (!m_recordsMode && m_sampleCount != 1) {
+            std::ostringstream oss;
+            oss << m_props << "sampleCount=" << m_sampleCount << ";";
+            alvrl_integrator_destroy(m_it);
+            m_it = NULL;
+            check(alvrl_integrator_create(oss.str().c_str(), m_device, &m_it), "alvrl_integrator_create");
+        }
         describe(scene);
         alvrl_scene_desc sd = m_desc;
         sd.occluders = m_tris.empty() ? NULL : &m_tris[0];
@@ -347,14 +360,22 @@ private:
         std::vector<alvrl_gather_rec> recs;
         std::vector<uint32_t> ids, slice, owner;
         const bool clustered = !m_p2s.empty();
+        std::vector<Point2> pos;   // each sensor sample's image position
         for (size_t i = 0; i < points.size() && !stop; ++i) {
-            const Point2i p = Point2i(points[i]) + Vector2i(off);
-            RayDifferential ray;
-            sensor->sampleRayDifferential(ray, Point2(p) + Vector2(0.5f), Point2(0.5f), 0.5f);
+          const Point2i p = Point2i(points[i]) + Vector2i(off);
+          const uint32_t pid = (uint32_t) p.y * (uint32_t) m_width + (uint32_t) p.x;
+          const uint32_t sl = clustered ? m_p2s[(size_t) p.y + (size_t) m_height * p.x] : 0u;   // m_slices[y + H*x]
+          sampler->generate(p);
+          for (size_t j = 0; j < sampler->getSampleCount(); ++j) {
             RadianceQueryRecord rRec(scene, sampler);
             rRec.newQuery(RadianceQueryRecord::ESensorRay, sensor->getMedium());
-            const uint32_t pid = (uint32_t) p.y * (uint32_t) m_width + (uint32_t) p.x;
-            const uint32_t sl = clustered ? m_p2s[(size_t) p.y + (size_t) m_height * p.x] : 0u;   // m_slices[y + H*x]
+            /* the pixel centre for one sample per pixel, else a sampler draw (integrator.cpp:240-247) */
+            const Point2 samplePos = Point2(p) + (sampler->getSampleCount() == 1 ? Vector2(0.5f)
+                                                                                : Vector2(rRec.nextSample2D()));
+            RayDifferential ray;
+            sensor->sampleRayDifferential(ray, samplePos, Point2(0.5f), 0.5f);
+            const uint32_t owner_id = (uint32_t) pos.size();
+            pos.push_back(samplePos);
             Spectrum weight(1.0f), throughput(m_initialSpecularThroughput);
             for (uint32_t depth = 0; depth < 256; ++depth) {
                 if (!rRec.rayIntersect(ray)) break;
@@ -372,11 +393,11 @@ private:
                 r.flags = ALVRL_REC_HIT | (smooth ? ALVRL_REC_SMOOTH : ALVRL_REC_DELTA) |
                     (rRec.medium && !rRec.medium->getSigmaS().isZero() ? ALVRL_REC_MEDIUM : 0u);
                 put3(r.weight, weight);
-                r.depth = depth;
+                r.depth = depth | ((uint32_t) j << 16);   /* the sample keys the gather's streams */
                 recs.push_back(r);
                 ids.push_back(pid);
                 slice.push_back(sl);
-                owner.push_back((uint32_t) i);
+                owner.push_back(owner_id);
                 if (!(type & BSDF::EDelta)) break;
                 /* the delta component, transmittance, roulette (:450-510) */
                 MediumSamplingRecord mRec;
@@ -401,6 +422,8 @@ private:
                     rRec2.medium = its.getTargetMedium(ray.d);
                 rRec = rRec2;
             }
+            sampler->advance();
+          }
         }
         const uint32_t n = (uint32_t) recs.size();
         std::vector<float> rgb((size_t) 3 * n);
@@ -412,20 +435,20 @@ private:
                 checkDevice(alvrl_gather_brute_host(ctx, &recs[0], &ids[0], n, &rgb[0]), ctx,
                     "alvrl_gather_brute_host");
         }
-        std::vector<Spectrum> L(points.size(), Spectrum(0.0f));
+        std::vector<Spectrum> L(pos.size(), Spectrum(0.0f));
         for (uint32_t k = 0; k < n; ++k) {
             Spectrum s;
             s.fromLinearRGB(rgb[3 * k], rgb[3 * k + 1], rgb[3 * k + 2]);
             L[owner[k]] += s;
         }
         Float alpha = 1.0f;
-        for (size_t i = 0; i < points.size() && !stop; ++i) {
-            const Point2i p = Point2i(points[i]) + Vector2i(off);
-            block->put(Point2(p) + Vector2(0.5f), L[i], alpha);
-        }
+        for (size_t i = 0; i < pos.size() && !stop; ++i)
+            block->put(pos[i], L[i], alpha);   /* each sample, as renderBlock (integrator.cpp:262) */
     }
 
     alvrl_integrator *m_it = NULL;
+    std::string m_props;   /* the integrator's properties (alvrl_integrator_create) */
+    int m_sampleCount = 1;
     hipStream_t m_stream = NULL;
     int m_device = 0;
     bool m_recordsMode = false;

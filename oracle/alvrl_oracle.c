@@ -497,7 +497,7 @@ static void integrate_vrl_w(const alvrl_o_params *P, const float *rec, uint32_t 
     uint32_t flags, depth;
     memcpy(&flags, &rec[15], 4);
     memcpy(&depth, &rec[19], 4);
-    rsub = ((depth & 0xFFu) << 16) | (rsub & 0xFFFFu);
+    rsub = ((depth & 0xFFu) << 16) | ((rsub + (depth >> 16)) & 0xFFFFu);
     const float wt[3] = { use_weight ? rec[16] : 1.0f, use_weight ? rec[17] : 1.0f, use_weight ? rec[18] : 1.0f };
     if (contrib) *contrib = 0;
     if (variance) *variance = 0;
@@ -894,13 +894,34 @@ float alvrl_o_first_hit(const alvrl_o_scene *s, const float o[3], const float d[
     return t;
 }
 
-void alvrl_o_make_record(const alvrl_o_scene *s, int medium_scatters, int x, int y, float *rec)
+/* The sensor sample of pixel (x, y), sample j of spp (renderBlock,
+ * integrator.cpp:240-247): the pixel centre when the sampler takes one
+ * sample, else offset + rRec.nextSample2D(), here draws 0 and 1 of the
+ * counter stream (seed, pass, dom 8, pixel, sample). */
+void alvrl_o_pixel_sample(uint32_t seed, uint32_t pass, int x, int y, int width, uint32_t sample, uint32_t spp,
+                          float *px, float *py)
 {
-    float o[3], d[3];
-    alvrl_o_camera_ray(s, (float)x + 0.5f, (float)y + 0.5f, o, d);
+    if (spp <= 1) {
+        *px = (float)x + 0.5f;
+        *py = (float)y + 0.5f;
+        return;
+    }
+    const uint32_t pixel = (uint32_t)y * (uint32_t)width + (uint32_t)x;
+    *px = (float)x + draw(seed, pass, ALVRL_O_DOM_PIXEL, pixel, sample, 0u, 0u);
+    *py = (float)y + draw(seed, pass, ALVRL_O_DOM_PIXEL, pixel, sample, 0u, 1u);
+}
+
+/* The record of sensor sample j of pixel (x, y); its depth word carries the
+ * sample index in bits 16-31 (the gather's streams are keyed by it). */
+void alvrl_o_make_record_s(const alvrl_o_scene *s, int medium_scatters, int x, int y, uint32_t seed, uint32_t pass,
+                           uint32_t sample, uint32_t spp, float *rec)
+{
+    float o[3], d[3], px, py;
+    alvrl_o_pixel_sample(seed, pass, x, y, s->width, sample, spp, &px, &py);
+    alvrl_o_camera_ray(s, px, py, o, d);
     v3 O = ld3(o), D = ld3(d), n, p;
     int tri;
-    float t = first_hit(s, O, D, camera_mint(s, (float)x + 0.5f, (float)y + 0.5f), &n, &p, &tri);
+    float t = first_hit(s, O, D, camera_mint(s, px, py), &n, &p, &tri);
     static const float zero3[3] = { 0.0f, 0.0f, 0.0f };
     uint32_t mt = (tri >= 0 && s->occ_mat) ? s->occ_mat[tri] : ALVRL_O_MAT_DIFFUSE;
     const float *alb = mt != ALVRL_O_MAT_DIFFUSE ? zero3 : (tri >= 0 ? s->occ_albedo : s->albedo);
@@ -914,8 +935,13 @@ void alvrl_o_make_record(const alvrl_o_scene *s, int medium_scatters, int x, int
     rec[12] = alb[0]; rec[13] = alb[1]; rec[14] = alb[2];
     memcpy(&rec[15], &flags, 4);
     rec[16] = rec[17] = rec[18] = 1.0f;   /* the camera ray: weight 1, depth 0 */
-    uint32_t depth = 0;
+    uint32_t depth = sample << 16;
     memcpy(&rec[19], &depth, 4);
+}
+
+void alvrl_o_make_record(const alvrl_o_scene *s, int medium_scatters, int x, int y, float *rec)
+{
+    alvrl_o_make_record_s(s, medium_scatters, x, y, 0u, 0u, 0u, 1u, rec);
 }
 
 static uint32_t mat_of(const alvrl_o_scene *s, int tri)
@@ -956,10 +982,22 @@ uint32_t alvrl_o_make_chain(const alvrl_o_scene *s, const alvrl_o_medium *m, int
                             uint32_t seed, uint32_t pass, int spec_rr_depth, float init_throughput,
                             float *recs, uint32_t cap)
 {
-    float o[3], d[3];
-    alvrl_o_camera_ray(s, (float)x + 0.5f, (float)y + 0.5f, o, d);   /* pixel centre (integrator.cpp:243-245) */
+    return alvrl_o_make_chain_s(s, m, medium_scatters, x, y, seed, pass, spec_rr_depth, init_throughput, 0u, 1u,
+                                recs, cap);
+}
+
+/* The eye path of sensor sample j of spp: record k's depth word is
+ * k | (j << 16), and the Russian roulette draws from the (pixel, k | (j << 16))
+ * stream (sample 0: the single-sample streams). */
+uint32_t alvrl_o_make_chain_s(const alvrl_o_scene *s, const alvrl_o_medium *m, int medium_scatters, int x, int y,
+                              uint32_t seed, uint32_t pass, int spec_rr_depth, float init_throughput,
+                              uint32_t sample, uint32_t spp, float *recs, uint32_t cap)
+{
+    float o[3], d[3], px, py;
+    alvrl_o_pixel_sample(seed, pass, x, y, s->width, sample, spp, &px, &py);
+    alvrl_o_camera_ray(s, px, py, o, d);   /* the sensor sample (integrator.cpp:240-247) */
     v3 O = ld3(o), D = ld3(d);
-    float mint = camera_mint(s, (float)x + 0.5f, (float)y + 0.5f);
+    float mint = camera_mint(s, px, py);
     uint32_t pixel = (uint32_t)y * (uint32_t)s->width + (uint32_t)x;
     float weight[3] = { 1.0f, 1.0f, 1.0f };
     float thr[3] = { init_throughput, init_throughput, init_throughput };   /* throughputWithEtaSq */
@@ -982,7 +1020,8 @@ uint32_t alvrl_o_make_chain(const alvrl_o_scene *s, const alvrl_o_medium *m, int
         for (int i = 0; i < 3; i++) rec[12 + i] = mt == ALVRL_O_MAT_DIFFUSE ? alb[i] : 0.0f;
         memcpy(&rec[15], &flags, 4);
         for (int i = 0; i < 3; i++) rec[16 + i] = weight[i];
-        memcpy(&rec[19], &k, 4);
+        const uint32_t kw = k | (sample << 16);
+        memcpy(&rec[19], &kw, 4);
         nrec++;
         if (mt == ALVRL_O_MAT_DIFFUSE) break;                               /* no delta component (:449-450) */
         /* rRec.medium->eval(Ray(ray, 0, its.t)) (:452-458) */
@@ -1015,7 +1054,7 @@ uint32_t alvrl_o_make_chain(const alvrl_o_scene *s, const alvrl_o_medium *m, int
         float mx = thr2[0] > thr2[1] ? thr2[0] : thr2[1];
         mx = mx > thr2[2] ? mx : thr2[2];
         float rrProb = maxRR < mx ? maxRR : mx;
-        if (rrProb <= 0 || (rrProb < 1 && draw(seed, pass, 7u, pixel, k, 0u, 0u) > rrProb)) break;
+        if (rrProb <= 0 || (rrProb < 1 && draw(seed, pass, 7u, pixel, k | (sample << 16), 0u, 0u) > rrProb)) break;
         for (int i = 0; i < 3; i++) {
             thr[i] = thr2[i] / rrProb;
             weight[i] = ((weight[i] * tr[i]) * bw[i]) / rrProb;              /* :503-510 */

@@ -45,6 +45,7 @@ extern "C" {
 #define ALVRL_O_DOM_GATHER  1u   /* render gather (getClusteredVrlContributions / getVRLContributions) */
 #define ALVRL_O_DOM_RBUILD  2u   /* R rows (Rbuilder::run) */
 #define ALVRL_O_DOM_TRACER  3u   /* vrlTracer particles */
+#define ALVRL_O_DOM_PIXEL   8u   /* sensor sample offsets of multi-sample renders (integrator.cpp:240-247) */
 #define ALVRL_O_DOM_REPS    4u   /* Slice::sampleRepresentativePixels */
 #define ALVRL_O_DOM_CLUSTER 5u   /* Clustering split / sampleRepresentatives */
 
@@ -164,6 +165,9 @@ typedef struct {
 uint32_t alvrl_o_make_chain(const alvrl_o_scene *s, const alvrl_o_medium *m, int medium_scatters, int x, int y,
                             uint32_t seed, uint32_t pass, int spec_rr_depth, float init_throughput,
                             float *recs, uint32_t cap);
+uint32_t alvrl_o_make_chain_s(const alvrl_o_scene *s, const alvrl_o_medium *m, int medium_scatters, int x, int y,
+                              uint32_t seed, uint32_t pass, int spec_rr_depth, float init_throughput,
+                              uint32_t sample, uint32_t spp, float *recs, uint32_t cap);
 /* buildSlices' gather point of pixel (x, y): the first hit continued through
  * null surfaces (Preprocessor.cpp:1144-1170), as a record (flags: hit). */
 void alvrl_o_make_slice_record(const alvrl_o_scene *s, int x, int y, float *rec);
@@ -180,6 +184,10 @@ void alvrl_o_camera_ray(const alvrl_o_scene *s, float px, float py, float o[3], 
 void alvrl_o_make_records(const alvrl_o_scene *s, int medium_scatters, float *recs);
 /* Record of a single pixel centre. */
 void alvrl_o_make_record(const alvrl_o_scene *s, int medium_scatters, int x, int y, float *rec);
+void alvrl_o_pixel_sample(uint32_t seed, uint32_t pass, int x, int y, int width, uint32_t sample, uint32_t spp,
+                          float *px, float *py);
+void alvrl_o_make_record_s(const alvrl_o_scene *s, int medium_scatters, int x, int y, uint32_t seed, uint32_t pass,
+                           uint32_t sample, uint32_t spp, float *rec);
 
 /* vrlTracer::randomWalk restatement.  Writes up to max_vrls VRLs (SoA with
  * capacity cap), returns # VRLs, *particles = particleCount. */

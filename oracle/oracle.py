@@ -129,6 +129,10 @@ class Oracle:
         L.alvrl_o_make_slice_record.argtypes = [P(Scene), i32, i32, P(f32)]
         L.alvrl_o_make_chain.argtypes = [P(Scene), P(Medium), i32, i32, i32, u32, u32, i32, f32, P(f32), u32]
         L.alvrl_o_make_chain.restype = u32
+        L.alvrl_o_make_record_s.argtypes = [P(Scene), i32, i32, i32, u32, u32, u32, u32, P(f32)]
+        L.alvrl_o_make_chain_s.argtypes = [P(Scene), P(Medium), i32, i32, i32, u32, u32, i32, f32, u32, u32,
+                                           P(f32), u32]
+        L.alvrl_o_make_chain_s.restype = u32
         L.alvrl_o_trace_vrls.argtypes = [P(Scene), P(Medium), u32, u32, u32, i32, i32, i32,
                                          P(f32), u32, P(u64)]
         L.alvrl_o_trace_vrls.restype = u32
@@ -216,6 +220,36 @@ class Oracle:
         out = np.zeros((cap, REC_WORDS), np.float32)
         n = self.lib.alvrl_o_make_chain(C.byref(scene), C.byref(medium), int(medium_scatters), x, y, seed,
                                         pass_, spec_rr_depth, init_throughput, _p(out), cap)
+        return out[:n].copy()
+
+    def record_s(self, scene: Scene, x: int, y: int, sample: int, spp: int, medium_scatters: bool = True,
+                 seed=0xA1B2C3D4, pass_=0) -> np.ndarray:
+        """Record of sensor sample `sample` of `spp` of pixel (x, y) (jittered
+        unless spp == 1; the depth word carries the sample in bits 16-31)."""
+        out = np.zeros(REC_WORDS, np.float32)
+        self.lib.alvrl_o_make_record_s(C.byref(scene), int(medium_scatters), x, y, seed, pass_, sample, spp, _p(out))
+        return out
+
+    def records_spp(self, scene: Scene, pixel_ids, spp: int, medium_scatters: bool = True, seed=0xA1B2C3D4,
+                    pass_=0):
+        """Records of every sensor sample of the row-major pixel ids, sample
+        major (record s * n + i: pixel_ids[i], sample s): (records, pixels)."""
+        ids = np.asarray(pixel_ids, np.uint32)
+        out = np.zeros((spp * len(ids), REC_WORDS), np.float32)
+        for sm in range(spp):
+            for i, p in enumerate(ids):
+                self.lib.alvrl_o_make_record_s(C.byref(scene), int(medium_scatters), int(p % scene.width),
+                                               int(p // scene.width), seed, pass_, sm, spp,
+                                               _p(out[sm * len(ids) + i]))
+        return out, np.tile(ids, spp)
+
+    def chain_s(self, scene: Scene, medium: Medium, x: int, y: int, sample: int, spp: int,
+                medium_scatters: bool = True, seed=0xA1B2C3D4, pass_=0, spec_rr_depth=100, init_throughput=20.0,
+                cap=256) -> np.ndarray:
+        """The eye path of sensor sample `sample` of `spp` of pixel (x, y)."""
+        out = np.zeros((cap, REC_WORDS), np.float32)
+        n = self.lib.alvrl_o_make_chain_s(C.byref(scene), C.byref(medium), int(medium_scatters), x, y, seed, pass_,
+                                          spec_rr_depth, init_throughput, sample, spp, _p(out), cap)
         return out[:n].copy()
 
     def chains(self, scene: Scene, medium: Medium, pixel_ids, **kw):
