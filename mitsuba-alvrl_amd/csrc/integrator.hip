@@ -795,6 +795,19 @@ struct alvrl_integrator {
             std::vector<uint32_t> p2(pix.size());
             for (size_t i = 0; i < order.size(); i++) p2[i] = pix[order[i]];
             pix.swap(p2);
+            // launch the waves of the longest representative lists first: the
+            // last waves to start are then the short ones (C4: 44.5 against
+            // 45.7 ms, tools/gather_tail.py); the lists are the pass's, the
+            // order a scheduling choice only (every wave's result is the same)
+            if (slice_off.size() > 1) {
+                auto len = [&](uint32_t sl) -> uint32_t {
+                    return sl == 0xFFFFFFFFu || sl + 1 >= slice_off.size() ? (uint32_t)fb_reps.size()
+                                                                          : slice_off[sl + 1] - slice_off[sl];
+                };
+                std::stable_sort(items.begin(), items.end(), [&](const alvrl_work_item& a, const alvrl_work_item& b) {
+                    return len(a.slice) > len(b.slice);
+                });
+            }
         }
         const bool scat = !(scene.medium.sigma_s[0] == 0 && scene.medium.sigma_s[1] == 0 && scene.medium.sigma_s[2] == 0);
         const uint32_t nprim = (uint32_t)pix.size();

@@ -1478,7 +1478,12 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
             if (FU && !own3 && j == 0 && B >= 1) flush(B - 1);
             const long long ws2 = wprof ? (long long)clock64() : 0;
             if (nb < nblk) {
+#ifdef ALVRL_EXP_NOCHAIN
+                // timing experiment (results invalid): no running weight total
+                cWo = 1.0 + (double)(nb * 64u + lane); cWn = cWo + 1.0;   // telescoping like the real totals
+#else
                 coef_chain8(W, cw_w, j, ncol_of(nb), cWo, cWn);
+#endif
                 if (j == 7 || k == nch - 1) coef_block_finish(C, cw_w, cWo, cWn, cw_v, ncol_of(nb), &ring[nb & 1]);
             }
             const long long ws3 = wprof ? (long long)clock64() : 0;
@@ -4003,7 +4008,11 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
             const uint32_t n = meta[3 * (size_t)j];
             const int refined = (int)meta[3 * (size_t)j + 1];
             const int jerr = (int)meta[3 * (size_t)j + 2];
+#ifndef ALVRL_EXP_NOCHAIN   // timing variants with invalid results do not report them
             if (jerr) { rc = 5; *err = "alvrl_refine: clustering invariant violated in job " + std::to_string(j); }
+#else
+            (void)jerr;
+#endif
             if (n > nvrl) { rc = 5; *err = "alvrl_refine: corrupt representative count"; break; }
             out_refined[j] = refined;
             off += n;
