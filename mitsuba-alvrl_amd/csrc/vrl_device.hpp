@@ -122,13 +122,14 @@ constexpr float kLog2eLo = 1.925963033500e-8f;          // log2(e) - (float)log2
 __device__ __forceinline__ float asinh_fast(float x)
 {
     const float ax = fabsf(x);
+    const bool big = ax > 4096.0f;
     const float s = sqrtf(fmaf(ax, ax, 1.0f));
     const float y = ax + fdiv(ax * ax, 1.0f + s);
     const float u = 1.0f + y;
-    const float l = __builtin_amdgcn_logf(u) * kLn2;
+    // one hardware log for both ranges: ln(u), or ln(|x|) + ln 2 = ln(2|x|)
+    const float l = __builtin_amdgcn_logf(big ? ax : u) * kLn2;
     const float small = (u == 1.0f) ? y : l * fdiv(y, u - 1.0f);
-    const float big = (__builtin_amdgcn_logf(ax) + 1.0f) * kLn2;
-    return copysignf(ax > 4096.0f ? big : small, x);
+    return copysignf(big ? l + kLn2 : small, x);
 }
 
 // ------------------------------------------------- circular functions --
@@ -280,7 +281,7 @@ __device__ __forceinline__ float luminance(float r, float g, float b)
 // (KullaSampling, vrlIntegrator.cpp:889-914).  I = A + dotPr * dir is the foot
 // of D on the segment's line, DI = D - I.  The reference's distance(A, I) and
 // distance(I, B) are |dotPr| and |lenAB - dotPr| (I, A, B are collinear).
-struct KullaFrame { F3 DI; float Dis, dotPr, aa, ab; };
+struct KullaFrame { F3 DI; float Dis, rDis, dotPr, aa, ab; };
 
 __device__ __forceinline__ KullaFrame kulla_frame(F3 A, F3 dir, float lenAB, F3 D)
 {
@@ -288,8 +289,11 @@ __device__ __forceinline__ KullaFrame kulla_frame(F3 A, F3 dir, float lenAB, F3 
     const F3 w = D - A;
     k.dotPr = dot(dir, w);
     k.DI = w - dir * k.dotPr;
-    k.Dis = len(k.DI);
-    const float rDis = rcp(k.Dis);
+    // |DI| and its reciprocal from one v_rsq_f32 (Dis = 0: rDis = inf, as rcp(0))
+    const float l2 = len2(k.DI);
+    const float rDis = __builtin_amdgcn_rsqf(l2);
+    k.Dis = l2 > 0.0f ? l2 * rDis : 0.0f;
+    k.rDis = rDis;
     const float dAI = fabsf(k.dotPr);
     float aa = atan_fast(dAI * rDis);
     float ab = atan_fast(fabsf(lenAB - k.dotPr) * rDis);
@@ -324,18 +328,18 @@ __device__ __forceinline__ void sinhcosh_fast(float x, float* sh, float* ch)
 }
 
 // Pair-constant part of sampleVtoDistance (:916-953) incl. getClosestPoints (:962-1032).
-struct NovakFrame { float sinT, rsinT, h, rh, A0, dA, rdenom, dVhS; bool parallel, zero; };
+struct NovakFrame { float sinT, rsinT, h, rh, A0, dA, rdenom, dVhS, ipdf; bool parallel, zero; };
 
 __device__ __forceinline__ NovakFrame novak_frame(const RecPre& q, const VrlPrep& v)
 {
     NovakFrame f;
-    const F3 S = f3(v.sx, v.sy, v.sz), End = f3(v.ex, v.ey, v.ez);
+    const F3 S = f3(v.sx, v.sy, v.sz);
     const float cosT = dot(q.dN, f3(v.dx, v.dy, v.dz));
     const float s2 = 1 - cosT * cosT;
     f.zero = v.len == 0.0f;                          // :920-924
     f.sinT = sqrtf(s2 > 0.0f ? s2 : 0.0f);
     f.parallel = f.sinT < kEpsilon;
-    f.h = f.rh = f.A0 = f.dA = f.rdenom = f.rsinT = f.dVhS = 0.0f;
+    f.h = f.rh = f.A0 = f.dA = f.rdenom = f.rsinT = f.dVhS = f.ipdf = 0.0f;
     if (!f.parallel && !f.zero) {
         // getClosestPoints(E, its.p, start, end)
         const F3 u = q.P - q.E;
@@ -365,11 +369,11 @@ __device__ __forceinline__ NovakFrame novak_frame(const RecPre& q, const VrlPrep
         }
         const float sc = fdiv(sN, sD), tc = fdiv(tN, tD);
         const F3 dP = (w + u * sc) - vv * tc;
-        const F3 Vh = S + vv * tc;
         f.h = len(dP);
-        f.dVhS = len(Vh - S);
+        // Vh = S + vv tc: distance(Vh, S) = |tc| len, distance(Vh, End) = |tc - 1| len
+        f.dVhS = fabsf(tc) * v.len;
         const float V0c = -1 * f.dVhS;
-        const float V1c = len(Vh - End);
+        const float V1c = fabsf(tc - 1.0f) * v.len;
         f.rh = rcp(f.h);
         const float A0 = asinh_fast((V0c * f.rh) * f.sinT);
         const float A1 = asinh_fast((V1c * f.rh) * f.sinT);
@@ -377,6 +381,8 @@ __device__ __forceinline__ NovakFrame novak_frame(const RecPre& q, const VrlPrep
         f.dA = A1 - A0;
         f.rsinT = rcp(f.sinT);
         f.rdenom = fdiv(f.sinT, f.dA);
+        // 1 / pdf = cosh(x) * h * dA / sinT (the sample's pdf without its cosh)
+        f.ipdf = (f.h * f.dA) * f.rsinT;
     }
     return f;
 }
@@ -449,19 +455,19 @@ __device__ __forceinline__ void integrate_vrl(const DevParams& P, const RecPre& 
         float lumv = 0.0f;
         const float u0 = draw(2 * sample), u1 = draw(2 * sample + 1);
         F3 V;
-        float pdfV, dSV;
+        float ipdfV, dSV;                           // 1 / samplingPDF of V
         if (nf.zero) {                              // sampleVtoDistance :920-924
-            V = S; pdfV = 1.0f; dSV = 0.0f;
+            V = S; ipdfV = 1.0f; dSV = 0.0f;
         } else if (nf.parallel) {                   // :929-933
             V = S + f3(v.vx, v.vy, v.vz) * u0;
-            pdfV = rcp(v.len);
+            ipdfV = v.len;
             dSV = u0 * v.len;
         } else {                                    // :935-952
             float sh, ch;
             sinhcosh_fast(nf.A0 + (u0 * nf.dA), &sh, &ch);
             const float newV = fmaf(nf.h * sh, nf.rsinT, nf.dVhS);
             V = S + SV * newV;
-            pdfV = (nf.rh * rcp(ch)) * nf.rdenom;
+            ipdfV = ch * nf.ipdf;                   // pdf = (1 / (h cosh)) sinT / dA
             dSV = fabsf(newV);
         }
         const KullaFrame ke = kulla_frame(q.E, q.dirAB, q.lenAB, V);
@@ -469,16 +475,22 @@ __device__ __forceinline__ void integrate_vrl(const DevParams& P, const RecPre& 
         const float l2 = fmaf(ke.Dis, ke.Dis, t * t);
         if (l2 != 0 && !(VIS && blocked(P, q.E + q.dirAB * (ke.dotPr + t), false, V))) {
             const float dUV = sqrtf(l2);
-            float tuv[3];
-            tuv[0] = P.sigma_t[0] != 0 ? __expf(P.sigma_t[0] * (0.0f - dUV)) : 1.0f;
-            tuv[1] = P.sigma_t[1] != 0 ? __expf(P.sigma_t[1] * (0.0f - dUV)) : 1.0f;
-            tuv[2] = P.sigma_t[2] != 0 ? __expf(P.sigma_t[2] * (0.0f - dUV)) : 1.0f;
-            if (tuv[0] != 0 || tuv[1] != 0 || tuv[2] != 0) {
-                float teu[3], tsv[3], pf;
-                medium_tr_only(P, fabsf(ke.dotPr + t), teu);
+            // T(U, V) T(E, U) in one exponential per channel, exp(-sigma_t (dUV + dEU));
+            // evalTransmittance(E, U)'s clamp (every channel below 1e-20) as
+            // min sigma_t * dEU > ln 1e20
+            const float dEU = fabsf(ke.dotPr + t);
+            const float smin = fminf(fminf(P.sigma_t[0], P.sigma_t[1]), P.sigma_t[2]);
+            const bool zeu = smin * dEU > 46.0517019f;
+            const float dUE = dUV + dEU;
+            float tue[3];
+            tue[0] = zeu ? 0.0f : __expf(P.sigma_t[0] * (0.0f - dUE));
+            tue[1] = zeu ? 0.0f : __expf(P.sigma_t[1] * (0.0f - dUE));
+            tue[2] = zeu ? 0.0f : __expf(P.sigma_t[2] * (0.0f - dUE));
+            if (tue[0] != 0 || tue[1] != 0 || tue[2] != 0) {
+                float tsv[3], pf;
                 medium_tr<(NVV < 0)>(P, dSV, tsv, &pf);
                 // 1 / samplingPDF / distanceSquared(U, V)
-                const float g = (ke.ab - ke.aa) * rcp(ke.Dis * pdfV);
+                const float g = ((ke.ab - ke.aa) * ke.rDis) * ipdfV;
                 const float rpf = P.short_vrls ? rcp(pf) : 1.0f;
                 float ph = kInvFourPi * kInvFourPi;
                 if (hg) {
@@ -487,9 +499,9 @@ __device__ __forceinline__ void integrate_vrl(const DevParams& P, const RecPre& 
                 }
                 const float gg = g * rpf * ph;
                 float c0 = v.pr * (ss0 * ss0), c1 = v.pg * (ss1 * ss1), c2 = v.pb * (ss2 * ss2);
-                c0 *= tsv[0] * tuv[0] * teu[0];
-                c1 *= tsv[1] * tuv[1] * teu[1];
-                c2 *= tsv[2] * tuv[2] * teu[2];
+                c0 *= tsv[0] * tue[0];
+                c1 *= tsv[1] * tue[1];
+                c2 *= tsv[2] * tue[2];
                 c0 *= gg; c1 *= gg; c2 *= gg;
                 if (WANT_STATS && !q.unit) { c0 *= q.w[0]; c1 *= q.w[1]; c2 *= q.w[2]; }
                 if (spec_valid(c0, c1, c2)) {
@@ -517,7 +529,7 @@ __device__ __forceinline__ void integrate_vrl(const DevParams& P, const RecPre& 
         float gs = 0.0f, sn = 0.0f, dn = 0.0f, base0 = 0.0f, base1 = 0.0f, base2 = 0.0f;
         if (q.surf) {
             ks = kulla_frame(S, SV, v.len, q.P);    // sampleV -> KullaSampling(S, End, Usurf)
-            gs = (ks.ab - ks.aa) * rcp(ks.Dis);     // 1 / samplingPDF / distanceSquared(U, V)
+            gs = (ks.ab - ks.aa) * ks.rDis;         // 1 / samplingPDF / distanceSquared(U, V)
             sn = dot(SV, q.n);                      // cos_wo = (t sn - dn) / dUV
             dn = dot(ks.DI, q.n);
             base0 = v.pr * ss0 * q.teus[0];
@@ -533,8 +545,8 @@ __device__ __forceinline__ void integrate_vrl(const DevParams& P, const RecPre& 
                 const float t = kulla_t(ks, u);
                 const float l2 = fmaf(ks.Dis, ks.Dis, t * t);
                 if (l2 != 0 && !(VIS && blocked(P, q.P, true, S + SV * (ks.dotPr + t)))) {
-                    const float dUV = sqrtf(l2);
-                    const float rdUV = rcp(dUV);
+                    const float rdUV = __builtin_amdgcn_rsqf(l2);   // l2 > 0 here
+                    const float dUV = l2 * rdUV;
                     float tuv[3], tsv[3], pf;
                     tuv[0] = P.sigma_t[0] != 0 ? __expf(P.sigma_t[0] * (0.0f - dUV)) : 1.0f;
                     tuv[1] = P.sigma_t[1] != 0 ? __expf(P.sigma_t[1] * (0.0f - dUV)) : 1.0f;
