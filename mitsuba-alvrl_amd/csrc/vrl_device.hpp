@@ -283,6 +283,31 @@ __device__ __forceinline__ float luminance(float r, float g, float b)
 // distance(I, B) are |dotPr| and |lenAB - dotPr| (I, A, B are collinear).
 struct KullaFrame { F3 DI; float Dis, rDis, dotPr, aa, ab; };
 
+// atan of two arguments with one reciprocal for both reduced ratios
+// (num / den of atan_fast; den is |x|, |x| + 1 or 1, so den1 * den2 only
+// overflows where both ratios are -1/|x| ~ 0, which then come out as 0)
+__device__ __forceinline__ void atan2_fast(float x1, float x2, float* r1, float* r2)
+{
+    const float a1 = fabsf(x1), a2 = fabsf(x2);
+    const bool hi1 = a1 > 2.414213562373095f, mid1 = a1 > 0.4142135623730950f;
+    const bool hi2 = a2 > 2.414213562373095f, mid2 = a2 > 0.4142135623730950f;
+    const float n1 = hi1 ? -1.0f : (mid1 ? a1 - 1.0f : a1), d1 = hi1 ? a1 : (mid1 ? a1 + 1.0f : 1.0f);
+    const float n2 = hi2 ? -1.0f : (mid2 ? a2 - 1.0f : a2), d2 = hi2 ? a2 : (mid2 ? a2 + 1.0f : 1.0f);
+    const float rr = rcp(d1 * d2);
+    const float t1 = (n1 * d2) * rr, t2 = (n2 * d1) * rr;
+    const float y1 = hi1 ? 1.57079632679489661923f : (mid1 ? 0.78539816339744830962f : 0.0f);
+    const float y2 = hi2 ? 1.57079632679489661923f : (mid2 ? 0.78539816339744830962f : 0.0f);
+    const float z1 = t1 * t1, z2 = t2 * t2;
+    float p1 = fmaf(z1, 8.05374449538e-2f, -1.38776856032e-1f);
+    float p2 = fmaf(z2, 8.05374449538e-2f, -1.38776856032e-1f);
+    p1 = fmaf(p1, z1, 1.99777106478e-1f);
+    p2 = fmaf(p2, z2, 1.99777106478e-1f);
+    p1 = fmaf(p1, z1, -3.33329491539e-1f);
+    p2 = fmaf(p2, z2, -3.33329491539e-1f);
+    *r1 = copysignf(y1 + fmaf(p1 * z1, t1, t1), x1);
+    *r2 = copysignf(y2 + fmaf(p2 * z2, t2, t2), x2);
+}
+
 __device__ __forceinline__ KullaFrame kulla_frame(F3 A, F3 dir, float lenAB, F3 D)
 {
     KullaFrame k;
@@ -295,8 +320,8 @@ __device__ __forceinline__ KullaFrame kulla_frame(F3 A, F3 dir, float lenAB, F3 
     k.Dis = l2 > 0.0f ? l2 * rDis : 0.0f;
     k.rDis = rDis;
     const float dAI = fabsf(k.dotPr);
-    float aa = atan_fast(dAI * rDis);
-    float ab = atan_fast(fabsf(lenAB - k.dotPr) * rDis);
+    float aa, ab;
+    atan2_fast(dAI * rDis, fabsf(lenAB - k.dotPr) * rDis, &aa, &ab);
     if (k.dotPr > 0) {
         aa = -aa;
         if (dAI > lenAB) ab = -ab;
@@ -337,7 +362,9 @@ __device__ __forceinline__ NovakFrame novak_frame(const RecPre& q, const VrlPrep
     const float cosT = dot(q.dN, f3(v.dx, v.dy, v.dz));
     const float s2 = 1 - cosT * cosT;
     f.zero = v.len == 0.0f;                          // :920-924
-    f.sinT = sqrtf(s2 > 0.0f ? s2 : 0.0f);
+    // sinT and 1 / sinT from one v_rsq_f32
+    const float rs2 = __builtin_amdgcn_rsqf(s2);
+    f.sinT = s2 > 0.0f ? s2 * rs2 : 0.0f;
     f.parallel = f.sinT < kEpsilon;
     f.h = f.rh = f.A0 = f.dA = f.rdenom = f.rsinT = f.dVhS = f.ipdf = 0.0f;
     if (!f.parallel && !f.zero) {
@@ -367,19 +394,22 @@ __device__ __forceinline__ NovakFrame novak_frame(const RecPre& q, const VrlPrep
             else if ((-d + b) > a) sN = sD;
             else { sN = (-d + b); sD = a; }
         }
-        const float sc = fdiv(sN, sD), tc = fdiv(tN, tD);
+        const float rst = rcp(sD * tD);              // |sD|, |tD| <= a c: no overflow
+        const float sc = (sN * tD) * rst, tc = (tN * sD) * rst;
         const F3 dP = (w + u * sc) - vv * tc;
-        f.h = len(dP);
+        const float h2 = len2(dP);
+        const float rh = __builtin_amdgcn_rsqf(h2);
+        f.h = h2 > 0.0f ? h2 * rh : 0.0f;
         // Vh = S + vv tc: distance(Vh, S) = |tc| len, distance(Vh, End) = |tc - 1| len
         f.dVhS = fabsf(tc) * v.len;
         const float V0c = -1 * f.dVhS;
         const float V1c = fabsf(tc - 1.0f) * v.len;
-        f.rh = rcp(f.h);
+        f.rh = rh;
         const float A0 = asinh_fast((V0c * f.rh) * f.sinT);
         const float A1 = asinh_fast((V1c * f.rh) * f.sinT);
         f.A0 = A0;
         f.dA = A1 - A0;
-        f.rsinT = rcp(f.sinT);
+        f.rsinT = rs2;
         f.rdenom = fdiv(f.sinT, f.dA);
         // 1 / pdf = cosh(x) * h * dA / sinT (the sample's pdf without its cosh)
         f.ipdf = (f.h * f.dA) * f.rsinT;
