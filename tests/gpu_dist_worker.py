@@ -29,6 +29,7 @@ CASES = [
     ("neighbours", "targetNumSlices=30;neighbourCount=3;neighbourWeight=0.5", 192, 128, 900, 1),
     ("fixed", "targetNumSlices=25;localUndersampling=20", 160, 160, 1200, 5),
     ("global", "targetNumSlices=20;globalCluster=true;globalUndersampling=8", 128, 128, 800, 0),
+    ("samples", "targetNumSlices=30;sampleCount=3", 160, 128, 900, 3),
 ]
 
 

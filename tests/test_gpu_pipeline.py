@@ -202,7 +202,9 @@ def test_sharded_prepass(gpu_ok, tmp_path):
     """The slice-sharded prepass (alvrl_integrator_prepass_dist):
     2 gloo ranks on the one GPU, see tests/gpu_dist_worker.py.  Cluster lists
     and the frame are identical to the one-GPU prepass bit for bit; without
-    neighbours every slice and R row is built exactly once over the ranks."""
+    neighbours every slice and R row is built exactly once over the ranks.
+    The 'samples' case renders three jittered sensor samples per pixel
+    (sampleCount) on each rank's tiles."""
     import json
     import os
     import socket
@@ -223,7 +225,7 @@ def test_sharded_prepass(gpu_ok, tmp_path):
     v = json.loads(out.read_text())
     print(v)
     assert v["world"] == 2
-    for name in ("adaptive", "neighbours", "fixed", "global"):
+    for name in ("adaptive", "neighbours", "fixed", "global", "samples"):
         c = v[name]
         assert c["clusters_identical_all_ranks"] and c["frame_bit_exact"], name
         assert c["slices_sum"] == c["slices"], name
