@@ -353,7 +353,7 @@ __device__ __forceinline__ void sinhcosh_fast(float x, float* sh, float* ch)
 }
 
 // Pair-constant part of sampleVtoDistance (:916-953) incl. getClosestPoints (:962-1032).
-struct NovakFrame { float sinT, rsinT, h, rh, A0, dA, rdenom, dVhS, ipdf; bool parallel, zero; };
+struct NovakFrame { float sinT, rsinT, h, rh, A0, dA, dVhS, ipdf; bool parallel, zero; };
 
 __device__ __forceinline__ NovakFrame novak_frame(const RecPre& q, const VrlPrep& v)
 {
@@ -366,7 +366,7 @@ __device__ __forceinline__ NovakFrame novak_frame(const RecPre& q, const VrlPrep
     const float rs2 = __builtin_amdgcn_rsqf(s2);
     f.sinT = s2 > 0.0f ? s2 * rs2 : 0.0f;
     f.parallel = f.sinT < kEpsilon;
-    f.h = f.rh = f.A0 = f.dA = f.rdenom = f.rsinT = f.dVhS = f.ipdf = 0.0f;
+    f.h = f.rh = f.A0 = f.dA = f.rsinT = f.dVhS = f.ipdf = 0.0f;
     if (!f.parallel && !f.zero) {
         // getClosestPoints(E, its.p, start, end)
         const F3 u = q.P - q.E;
@@ -410,7 +410,6 @@ __device__ __forceinline__ NovakFrame novak_frame(const RecPre& q, const VrlPrep
         f.A0 = A0;
         f.dA = A1 - A0;
         f.rsinT = rs2;
-        f.rdenom = fdiv(f.sinT, f.dA);
         // 1 / pdf = cosh(x) * h * dA / sinT (the sample's pdf without its cosh)
         f.ipdf = (f.h * f.dA) * f.rsinT;
     }
