@@ -56,6 +56,10 @@ typedef struct {
 #define ALVRL_MAT_DIFFUSE 0u
 #define ALVRL_MAT_MIRROR 1u
 #define ALVRL_MAT_NULL 2u
+/* smooth dielectric interface (dielectric.cpp): a delta BSDF with a reflection
+ * and a transmission component; blocks shadow segments like any non-null
+ * surface.  Host-cast scenes (alvrl_scene_ext) only. */
+#define ALVRL_MAT_DIELECTRIC 3u
 
 /* The benchmark scene of BASELINE.md ("homogeneous smoke box"). */
 ALVRL_API void alvrl_scene_default(alvrl_scene_desc *s, int width, int height);
@@ -225,6 +229,71 @@ ALVRL_API int alvrl_exchange_clusters(const alvrl_exchange *ex, uint32_t world, 
                                       const uint32_t *local_reps, const float *local_w,
                                       int *refined, uint32_t *slice_off, uint32_t *reps,
                                       float *weights, uint64_t cap, uint64_t *total);
+
+/* ---- host-cast scenes (the Mitsuba plugin's "records" mode) ------------
+ * For scenes the descriptor above cannot express -- area and other emitters,
+ * any shapes and BSDFs, a medium in any container -- the host application
+ * casts every ray with its own scene and traces the VRLs itself
+ * (vrlTracer.h:91-230 -> alvrl_integrator_set_vrls before each prepass); the
+ * library keeps the per-pair work: R, the clustering and the gathers.
+ *
+ *   preprocess  alvrl_integrator_preprocess_ext: buildSlices
+ *               (Preprocessor.cpp:1130-1193) over the host's gather point of
+ *               every pixel centre ray (null surfaces passed, :1157-1169);
+ *   prepass     alvrl_integrator_rep_pixels (sampleSliceMapping of the pass,
+ *               :1502-1525) -> the host casts each representative pixel's
+ *               eye path (sensor->sampleRay at the pixel centre, :327-328;
+ *               LiInternal's delta-BSDF chains, :445-511, one record per
+ *               segment with its path weight) -> alvrl_integrator_prepass_records
+ *               (R rows, buildClusters, cluster lists; slice-sharded with
+ *               world > 1 as alvrl_integrator_prepass_dist);
+ *   render      the host's eye records through alvrl_gather_clustered_host /
+ *               alvrl_gather_brute_host on alvrl_integrator_ctx (slice of a
+ *               pixel: alvrl_integrator_slices); alvrl_integrator_render is
+ *               refused (it casts the descriptor's camera rays). */
+typedef struct {
+    int width, height;
+    float scene_min[3], scene_max[3];   /* Scene::getAABB(): buildSlices' direction scale (:1137) */
+    alvrl_medium_desc medium;           /* the homogeneous medium the VRLs live in */
+    /* W*H records, row-major (y*W + x): the gather point of the ray through
+     * the pixel centre -- ALVRL_REC_HIT, p and the shading normal; no HIT
+     * flag for a ray that leaves the scene (the pixel gets no slice) */
+    const alvrl_gather_rec *slice_recs;
+    /* every triangle of the scene, 9 floats each, for the gathers' occluder
+     * test (Scene::evalTransmittance, scene.cpp:619-679); ALVRL_MAT_NULL
+     * triangles let a shadow segment pass (NULL material list: all block) */
+    const float *triangles;
+    uint32_t n_triangles;
+    const uint32_t *triangle_material;
+} alvrl_scene_ext;
+
+ALVRL_API int alvrl_integrator_preprocess_ext(alvrl_integrator *it, const alvrl_scene_ext *s);
+/* The representative pixels of pass 'pass' in R-row order (row-major pixel
+ * ids y*W + x): rows rep_off[s]..rep_off[s+1] of alvrl_integrator_reps are
+ * slice s's.  cap may be 0 with pixel_ids NULL to learn *n. */
+ALVRL_API int alvrl_integrator_rep_pixels(alvrl_integrator *it, uint32_t pass, uint32_t *pixel_ids, uint32_t cap,
+                                          uint32_t *n);
+/* The prepass of pass 'pass' over the host's records: recs[i] belongs to R
+ * row row_of_rec[i] (the index into alvrl_integrator_rep_pixels' list); a
+ * row's records are its eye path's segments in LiInternal's order and add
+ * into the row (getLiLuminanceVrlContributions, :527-539, 812-813); a row
+ * without records (its ray left the scene) is zero.  Each record's gathers
+ * draw from the counter streams of the row's pixel id.  world > 1: this rank
+ * builds and refines slices s % world == rank only (ex as in
+ * alvrl_integrator_prepass_dist; world == 1 may pass NULL). */
+ALVRL_API int alvrl_integrator_prepass_records(alvrl_integrator *it, uint32_t pass, const alvrl_gather_rec *recs,
+                                               const uint32_t *row_of_rec, uint32_t n, uint32_t rank,
+                                               uint32_t world, const alvrl_exchange *ex);
+/* The vrlClusterInfo resource in memory (bindUsedResources / wakeup,
+ * vrlIntegrator.cpp:371-384: a render worker receives m_vrls and m_ci
+ * instead of running the prepass): the pass's VRLs are set or traced as a
+ * prepass would, then these lists are installed.  Same arrays as
+ * alvrl_cluster_info_write; npix must be the scene's pixel count. */
+ALVRL_API int alvrl_integrator_set_cluster_info(alvrl_integrator *it, uint32_t pass, uint32_t npix,
+                                                const uint32_t *pixel_to_slice, uint32_t nslices,
+                                                const uint32_t *slice_off, const uint32_t *reps,
+                                                const float *weights, uint32_t n_fb, const uint32_t *fb_reps,
+                                                const float *fb_weights);
 
 /* Timing / statistics of the last prepass and render. */
 typedef struct {

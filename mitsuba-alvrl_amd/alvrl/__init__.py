@@ -23,11 +23,11 @@ LIB_PATH = os.environ.get("ALVRL_LIB") or os.path.join(PKG_DIR, "libalvrl.so")  
 
 REC_WORDS = 20
 REC_HIT, REC_SMOOTH, REC_MEDIUM, REC_DELTA, REC_ACCUM = 1, 2, 4, 8, 16   # alvrl_gather_rec.flags
-REC_HIT, REC_SMOOTH, REC_MEDIUM = 1, 2, 4
 UINT32_MAX = 0xFFFFFFFF
 
 ALVRL_OK = 0
-ERRORS = {1: "INVALID", 2: "STATE", 3: "HIP", 4: "NOMEM", 5: "NUMERIC"}
+ALVRL_ERR_INVALID, ALVRL_ERR_STATE, ALVRL_ERR_HIP, ALVRL_ERR_NOMEM, ALVRL_ERR_NUMERIC, ALVRL_ERR_COMM = 1, 2, 3, 4, 5, 6
+ERRORS = {1: "INVALID", 2: "STATE", 3: "HIP", 4: "NOMEM", 5: "NUMERIC", 6: "COMM"}
 
 
 class AlvrlError(RuntimeError):
@@ -166,7 +166,17 @@ class Context:
         self.nvrl = 0
         self.particle_count = 0
 
+    @classmethod
+    def borrow(cls, handle, device: int = 0) -> "Context":
+        """A non-owning view of a context another object owns (alvrl_integrator_ctx)."""
+        c = cls.__new__(cls)
+        c.L, c.h, c.device, c.nvrl, c.particle_count, c._borrowed = lib(), handle, device, 0, 0, True
+        return c
+
     def close(self):
+        if getattr(self, "_borrowed", False):
+            self.h = None
+            return
         if getattr(self, "h", None):
             self.L.alvrl_ctx_destroy(self.h)
             self.h = None
@@ -361,7 +371,14 @@ class SceneDesc(C.Structure):
                 ("occluder_specular", C.c_float * 3)]
 
 
-MAT_DIFFUSE, MAT_MIRROR, MAT_NULL = 0, 1, 2
+MAT_DIFFUSE, MAT_MIRROR, MAT_NULL, MAT_DIELECTRIC = 0, 1, 2, 3
+
+
+class SceneExt(C.Structure):
+    """alvrl_scene_ext: a host-cast scene (the Mitsuba plugin's records mode)."""
+    _fields_ = [("width", C.c_int), ("height", C.c_int), ("scene_min", C.c_float * 3),
+                ("scene_max", C.c_float * 3), ("medium", MediumDesc), ("slice_recs", C.c_void_p),
+                ("triangles", C.c_void_p), ("n_triangles", C.c_uint32), ("triangle_material", C.c_void_p)]
 
 
 class IntegratorStats(C.Structure):
@@ -533,6 +550,10 @@ def _host():
     L.alvrl_read_exr.argtypes = [C.c_char_p, vp, u64, P(i32), P(i32)]
     L.alvrl_image_rms.argtypes = [vp, vp, u64, C.c_double, C.c_double, i32, P(C.c_double)]
     L.alvrl_pass_file_name.argtypes = [C.c_char_p, u64, C.c_char_p, i32] + [C.c_double] * 6
+    L.alvrl_integrator_preprocess_ext.argtypes = [vp, P(SceneExt)]
+    L.alvrl_integrator_rep_pixels.argtypes = [vp, u32, vp, u32, P(u32)]
+    L.alvrl_integrator_prepass_records.argtypes = [vp, u32, vp, vp, u32, u32, u32, P(ExchangeDesc)]
+    L.alvrl_integrator_set_cluster_info.argtypes = [vp, u32, u32, vp, u32, vp, vp, vp, u32, vp, vp]
     _host_bound = True
     return L
 
@@ -861,6 +882,59 @@ class Integrator:
     def render(self, d_fb, rank: int = 0, world: int = 1, stream=None):
         _hcheck(self.L.alvrl_integrator_render(self.h, rank, world, _ptr(d_fb),
                                                C.c_void_p(stream) if stream else None))
+
+    def preprocess_ext(self, width: int, height: int, slice_recs: np.ndarray, scene_min, scene_max,
+                       medium: "Medium" = None, triangles=None, material=None):
+        """alvrl_integrator_preprocess_ext: buildSlices over the caller's gather
+        points (slice_recs: W*H records, row-major)."""
+        sr = _np(slice_recs, np.float32)
+        if sr.shape != (width * height, REC_WORDS):
+            raise ValueError("slice_recs must be (W*H, REC_WORDS)")
+        tri = None if triangles is None else _np(triangles, np.float32).reshape(-1, 9)
+        mat = None if material is None else _np(material, np.uint32)
+        e = SceneExt(width, height, (C.c_float * 3)(*scene_min), (C.c_float * 3)(*scene_max),
+                     (medium or Medium()).desc(), sr.ctypes.data, None if tri is None else tri.ctypes.data,
+                     0 if tri is None else tri.shape[0], None if mat is None else mat.ctypes.data)
+        self.scene = e
+        self._ext_keep = (sr, tri, mat)
+        _hcheck(self.L.alvrl_integrator_preprocess_ext(self.h, C.byref(e)))
+
+    def rep_pixels(self, pass_: int = 0) -> np.ndarray:
+        """sampleSliceMapping of the pass: representative pixels (row-major ids) in R-row order."""
+        n = C.c_uint32()
+        _hcheck(self.L.alvrl_integrator_rep_pixels(self.h, pass_, None, 0, C.byref(n)))
+        out = np.zeros(max(1, n.value), np.uint32)
+        _hcheck(self.L.alvrl_integrator_rep_pixels(self.h, pass_, _ptr(out), out.size, C.byref(n)))
+        return out[:n.value].copy()
+
+    def prepass_records(self, pass_: int, recs: np.ndarray, rows, rank: int = 0, world: int = 1,
+                        exchange: "Exchange" = None):
+        """The prepass over the caller's R-row records (recs[i] adds into row rows[i])."""
+        r = _np(recs, np.float32).reshape(-1, REC_WORDS)
+        rw = _np(rows, np.uint32)
+        if rw.size != r.shape[0]:
+            raise ValueError("one row per record")
+        if world > 1 and exchange is None:
+            raise ValueError("a sharded prepass needs an Exchange")
+        rc = self.L.alvrl_integrator_prepass_records(self.h, pass_, _ptr(r), _ptr(rw), r.shape[0], rank, world,
+                                                     C.byref(exchange.desc) if exchange is not None else None)
+        if rc != ALVRL_OK:
+            if exchange is not None:
+                exchange._check(rc)
+            _hcheck(rc)
+
+    def set_cluster_info(self, info: dict, pass_: int = 0):
+        """alvrl_integrator_set_cluster_info: install a vrlClusterInfo (dict as
+        read_cluster_info returns) for the pass."""
+        u = lambda k: _np(info.get(k, np.zeros(0)), np.uint32)
+        f = lambda k: _np(info.get(k, np.zeros(0)), np.float32)
+        sl, so, rp, w, fr, fw = u("slices"), u("slice_off"), u("reps"), f("weights"), u("fb_reps"), f("fb_weights")
+        _hcheck(self.L.alvrl_integrator_set_cluster_info(self.h, pass_, sl.size, _ptr(sl), so.size - 1, _ptr(so),
+                                                         _ptr(rp), _ptr(w), fr.size, _ptr(fr), _ptr(fw)))
+
+    def context(self) -> "Context":
+        """The device context this integrator drives (a non-owning view)."""
+        return Context.borrow(self.L.alvrl_integrator_ctx(self.h), self.device)
 
     def save_cluster_info(self, path: str):
         """The vrlClusterInfo of the last prepass, to a file (vrlIntegrator.cpp:66-101)."""

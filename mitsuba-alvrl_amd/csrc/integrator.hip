@@ -31,6 +31,7 @@ namespace alvrl {
 namespace host {
 extern thread_local std::string g_host_err;
 SmokeBox to_box(const alvrl_scene_desc& s);
+MediumParams medium_of(const alvrl_medium_desc& d);
 }  // namespace host
 }  // namespace alvrl
 
@@ -166,6 +167,14 @@ struct alvrl_integrator {
     DevBuf<float> out_buf;
     uint32_t nrec = 0, nitems = 0;
     alvrl_integrator_stats st{};
+    // host-cast scene (alvrl_integrator_preprocess_ext): no descriptor; the
+    // slicing records, the R rows' records and the VRLs come from the caller.
+    // ext_recs / ext_row / ext_n: the records of the running
+    // alvrl_integrator_prepass_records call
+    bool ext = false, ext_active = false;
+    const alvrl_gather_rec* ext_recs = nullptr;
+    const uint32_t* ext_row = nullptr;
+    uint32_t ext_n = 0;
 
     ~alvrl_integrator()
     {
@@ -233,6 +242,7 @@ struct alvrl_integrator {
 
     void preprocess(const alvrl_scene_desc& s)
     {
+        ext = false;
         scene = to_box(s);
         scene_desc = s;
         scene_desc.occluders = scene.occ.empty() ? nullptr : scene.occ.data();   // the owned copy
@@ -246,11 +256,7 @@ struct alvrl_integrator {
             throw IntegError(ALVRL_ERR_INVALID, "convergenceFalseColor is not supported with delta-BSDF occluders");
         chk(alvrl_set_occluders(ctx, scene_desc.occluders, scene_desc.n_occluders, scene_desc.occluder_material),
             "alvrl_set_occluders");
-        if (!vrlFile.empty()) {   // :243-252
-            std::string err;
-            if (!read_vrl_file(vrlFile.c_str(), scene.medium, &vrls, &err)) throw IntegError(ALVRL_ERR_INVALID, err);
-            vrls_from_file = true;
-        }
+        load_vrl_file();
         if (clustered) {          // :254-265
             PrepParams pp;
             pp.target_num_slices = (uint32_t)targetNumSlices;
@@ -279,8 +285,97 @@ struct alvrl_integrator {
         cache_rank = 0xFFFFFFFFu;
     }
 
+    void load_vrl_file()
+    {
+        if (!vrlFile.empty()) {   // :243-252
+            std::string err;
+            if (!read_vrl_file(vrlFile.c_str(), scene.medium, &vrls, &err)) throw IntegError(ALVRL_ERR_INVALID, err);
+            vrls_from_file = true;
+            uploaded_pass = 0xFFFFFFFFu;
+        }
+    }
+
+    // preprocess (:237-267) of a host-cast scene: the medium, the scene's
+    // triangles for the gathers' occluder test, buildSlices over the host's
+    // gather points (Preprocessor.cpp:1130-1193)
+    void preprocess_ext(const alvrl_scene_ext& e)
+    {
+        if (e.width <= 0 || e.height <= 0) throw IntegError(ALVRL_ERR_INVALID, "alvrl_scene_ext: width and height must be > 0");
+        if (!e.slice_recs) throw IntegError(ALVRL_ERR_INVALID, "alvrl_scene_ext: slice_recs is required");
+        if (e.n_triangles && !e.triangles) throw IntegError(ALVRL_ERR_INVALID, "alvrl_scene_ext: n_triangles > 0 without triangles");
+        MediumParams m = medium_of(e.medium);
+        if (const char* p = m.problem()) throw IntegError(ALVRL_ERR_INVALID, p);
+        m.resolve();
+        SmokeBox b;
+        b.width = e.width;
+        b.height = e.height;
+        for (int i = 0; i < 3; i++) { b.box_min[i] = e.scene_min[i]; b.box_max[i] = e.scene_max[i]; }
+        b.medium = m;
+        if (e.n_triangles) b.occ.assign(e.triangles, e.triangles + 9 * (size_t)e.n_triangles);
+        if (e.n_triangles && e.triangle_material) {
+            b.occ_mat.assign(e.triangle_material, e.triangle_material + e.n_triangles);
+            for (uint32_t x : b.occ_mat)
+                if (x > ALVRL_MAT_DIELECTRIC) throw IntegError(ALVRL_ERR_INVALID, "alvrl_scene_ext: unknown triangle material");
+        }
+        scene = b;
+        std::memset(&scene_desc, 0, sizeof(scene_desc));
+        ext = true;
+        have_scene = true;
+        chains = false;
+        alvrl_medium_desc md = e.medium;
+        chk(alvrl_set_medium(ctx, &md), "alvrl_set_medium");
+        chk(alvrl_set_occluders(ctx, scene.occ.empty() ? nullptr : scene.occ.data(), scene.n_occ(),
+                                scene.occ_mat.empty() ? nullptr : scene.occ_mat.data()), "alvrl_set_occluders");
+        load_vrl_file();
+        if (clustered) {
+            PrepParams pp;
+            pp.target_num_slices = (uint32_t)targetNumSlices;
+            pp.neighbour_count = (uint32_t)neighbourCount;
+            pp.neighbour_weight = neighbourWeight;
+            pp.slice_curvature_factor = sliceCurvatureFactor;
+            pp.seed = seed;
+            pp.pass = 0;
+            prep.reset(new Preprocessor(pp));
+            const double t0 = now_ms();
+            pixel_to_slice = prep->build_slices(scene, reinterpret_cast<const float*>(e.slice_recs));
+            st.ms_slices = now_ms() - t0;
+            st.slices = prep->num_slices();
+        }
+        cache_rank = 0xFFFFFFFFu;
+    }
+
+    // sampleSliceMapping of the pass (:293-296): representative pixels,
+    // row-major ids in R-row order
+    std::vector<uint32_t> rep_pixels(uint32_t pass)
+    {
+        if (!have_scene) throw IntegError(ALVRL_ERR_STATE, "rep_pixels before preprocess");
+        if (!clustered || !prep) throw IntegError(ALVRL_ERR_STATE, "no slices: the integrator does not cluster");
+        prep->set_pass(pass);
+        prep->sample_slice_mapping(targetPixelUndersampling);
+        const auto& rp = prep->rep_pix();
+        const uint32_t W = (uint32_t)scene.width, H = (uint32_t)scene.height;
+        std::vector<uint32_t> out(rp.size());
+        for (size_t i = 0; i < rp.size(); i++) out[i] = (rp[i] % H) * W + rp[i] / H;   // x*H + y -> y*W + x
+        return out;
+    }
+
+    void prepass_records(uint32_t pass, const alvrl_gather_rec* recs, const uint32_t* rows, uint32_t n,
+                         uint32_t rank, uint32_t world, const alvrl_exchange* ex)
+    {
+        if (!ext) throw IntegError(ALVRL_ERR_STATE, "alvrl_integrator_prepass_records needs a host-cast scene (alvrl_integrator_preprocess_ext)");
+        if (n && (!recs || !rows)) throw IntegError(ALVRL_ERR_INVALID, "alvrl_integrator_prepass_records: null records");
+        struct Done {
+            alvrl_integrator* it;
+            ~Done() { it->ext_active = false; it->ext_recs = nullptr; it->ext_row = nullptr; it->ext_n = 0; }
+        } done{this};
+        ext_recs = recs; ext_row = rows; ext_n = n; ext_active = true;
+        prepass(pass, rank, world, ex);
+    }
+
     void prepass(uint32_t pass, uint32_t rank = 0, uint32_t world = 1, const alvrl_exchange* ex = nullptr)
     {
+        if (ext && clustered && !ext_active)
+            throw IntegError(ALVRL_ERR_STATE, "host-cast scene: run the prepass with alvrl_integrator_prepass_records");
         if (world == 0 || rank >= world) throw IntegError(ALVRL_ERR_INVALID, "bad rank/world");
         if (world > 1 && (!ex || !ex->allgather)) throw IntegError(ALVRL_ERR_INVALID, "world > 1 needs an alvrl_exchange");
         if (!have_scene) throw IntegError(ALVRL_ERR_STATE, "prepass before preprocess");
@@ -301,6 +396,8 @@ struct alvrl_integrator {
     // the pass's VRLs on the device (:276-287): traced per pass unless preloaded
     void pass_vrls(uint32_t pass)
     {
+        if (ext && !vrls_from_file)
+            throw IntegError(ALVRL_ERR_STATE, "host-cast scene: set the pass's VRLs with alvrl_integrator_set_vrls first");
         chk(alvrl_set_pass(ctx, pass), "alvrl_set_pass");
         cur_pass = pass;
         // VRLs (:276-287): traced per pass unless preloaded from a file
@@ -360,6 +457,22 @@ struct alvrl_integrator {
         std::vector<float> w(nr), fw(nfb);
         chk_host(alvrl_cluster_info_get(ci, p2s.data(), so.data(), rp.data(), w.data(), nullptr, nullptr,
                                         fr.data(), fw.data()));
+        install_cluster_info(pass, p2s, so, rp, w, fr, fw);
+    }
+
+    // the vrlClusterInfo of a pass received instead of computed (wakeup, :378-384)
+    void install_cluster_info(uint32_t pass, std::vector<uint32_t>& p2s, std::vector<uint32_t>& so,
+                              std::vector<uint32_t>& rp, std::vector<float>& w, std::vector<uint32_t>& fr,
+                              std::vector<float>& fw)
+    {
+        if (!have_scene) throw IntegError(ALVRL_ERR_STATE, "cluster info before preprocess");
+        if (p2s.size() != (size_t)scene.width * (size_t)scene.height)
+            throw IntegError(ALVRL_ERR_INVALID, "cluster info: pixel count does not match the scene");
+        if (so.empty() || so[0] != 0 || so.back() != rp.size() || w.size() != rp.size() || fw.size() != fr.size())
+            throw IntegError(ALVRL_ERR_INVALID, "cluster info: inconsistent list sizes");
+        for (size_t s = 0; s + 1 < so.size(); s++)
+            if (so[s] > so[s + 1]) throw IntegError(ALVRL_ERR_INVALID, "cluster info: slice offsets decrease");
+        const uint32_t ns = (uint32_t)so.size() - 1;
         for (uint32_t s : p2s)
             if (s != 0xFFFFFFFFu && s >= ns) throw IntegError(ALVRL_ERR_INVALID, "cluster info: slice id out of range");
         pass_vrls(pass);
@@ -367,7 +480,8 @@ struct alvrl_integrator {
             if (v >= vrls.n) throw IntegError(ALVRL_ERR_INVALID, "cluster info: VRL id out of range");
         for (uint32_t v : fr)
             if (v >= vrls.n) throw IntegError(ALVRL_ERR_INVALID, "cluster info: VRL id out of range");
-        chk(alvrl_set_clusters(ctx, ns, so.data(), rp.data(), w.data(), fr.data(), fw.data(), nfb), "alvrl_set_clusters");
+        chk(alvrl_set_clusters(ctx, ns, so.data(), rp.data(), w.data(), fr.data(), fw.data(), (uint32_t)fr.size()),
+            "alvrl_set_clusters");
         pixel_to_slice.swap(p2s);
         slice_off.swap(so); reps.swap(rp); weights.swap(w); fb_reps.swap(fr); fb_w.swap(fw);
         clustered = true;
@@ -437,6 +551,36 @@ struct alvrl_integrator {
         return out;
     }
 
+    // The host's records of the built rows gl[i] (alvrl_integrator_prepass_records),
+    // in the form expand_chains gives: prim[i] = row i's first record (zero --
+    // no hit, no contribution -- if it has none), then level by level the
+    // further ones, flagged ALVRL_REC_ACCUM (getLiLuminanceVrlContributions
+    // adds a path's segments into the row, :812-813)
+    Chains host_rows(const std::vector<uint32_t>& gl, uint32_t rows, std::vector<alvrl_gather_rec>* prim) const
+    {
+        const uint32_t nb = (uint32_t)gl.size();
+        std::vector<uint32_t> bidx(rows, 0xFFFFFFFFu);
+        for (uint32_t i = 0; i < nb; i++) bidx[gl[i]] = i;
+        prim->assign(nb, alvrl_gather_rec{});
+        std::vector<uint32_t> cnt(nb, 0);
+        Chains ch;
+        for (uint32_t k = 0; k < ext_n; k++) {
+            const uint32_t g = ext_row[k];
+            if (g >= rows) throw IntegError(ALVRL_ERR_INVALID, "alvrl_integrator_prepass_records: row_of_rec out of range");
+            const uint32_t i = bidx[g];
+            if (i == 0xFFFFFFFFu) continue;   // a row of another rank's slice
+            alvrl_gather_rec r = ext_recs[k];
+            r.flags &= ~ALVRL_REC_ACCUM;
+            const uint32_t d = cnt[i]++;
+            if (d == 0) { (*prim)[i] = r; continue; }
+            if (ch.recs.size() < d) { ch.recs.resize(d); ch.src.resize(d); }
+            r.flags |= ALVRL_REC_ACCUM;
+            ch.recs[d - 1].push_back(r);
+            ch.src[d - 1].push_back(i);
+        }
+        return ch;
+    }
+
     // Building R (:302-333) for the rows of the slices flagged in 'need'.  R is
     // stored as one [vrl][row] block per slice (the reference's
     // R[slice][rep][vrl], transposed): a slice's local matrix is then one
@@ -460,7 +604,7 @@ struct alvrl_integrator {
         // records of the representative pixel centres (sensor->sampleRay at
         // the pixel centre, :327-328 / :1060-1061), formed on the device from
         // the row-major pixel ids (the RNG ids too)
-        std::vector<uint32_t> ids, bstr;
+        std::vector<uint32_t> ids, bstr, gl;
         std::vector<uint64_t> boff;
         uint64_t acc = 0;
         for (uint32_t s2 = 0; s2 < ns; s2++) {
@@ -471,6 +615,7 @@ struct alvrl_integrator {
                 row_stride[g] = n;
                 const uint32_t x = rpix[g] / (uint32_t)H, y = rpix[g] % (uint32_t)H;
                 ids.push_back(y * (uint32_t)W + x);
+                gl.push_back(g);
                 boff.push_back(row_base[g]);
                 bstr.push_back(n);
             }
@@ -486,7 +631,7 @@ struct alvrl_integrator {
         Rt.ensure((size_t)2 * nv * acc);
         if (nb) {
             hchk(hipMemcpyAsync(rep_ids.p, ids.data(), sizeof(uint32_t) * nb, hipMemcpyHostToDevice, stream), "copy rep ids");
-            if (!chains) chk_host(alvrl_scene_records_gpu(&scene_desc, scat ? 1 : 0, rep_ids.p, nb, rep_recs.p, stream));
+            if (!chains && !ext) chk_host(alvrl_scene_records_gpu(&scene_desc, scat ? 1 : 0, rep_ids.p, nb, rep_recs.p, stream));
             hchk(hipMemcpyAsync(rb_off.p, boff.data(), sizeof(uint64_t) * nb, hipMemcpyHostToDevice, stream), "copy row offsets");
             hchk(hipMemcpyAsync(rb_stride.p, bstr.data(), sizeof(uint32_t) * nb, hipMemcpyHostToDevice, stream), "copy row strides");
         }
@@ -496,9 +641,10 @@ struct alvrl_integrator {
         // records flagged ALVRL_REC_ACCUM (a row has at most one record per level)
         Chains ch;
         std::vector<uint32_t> lv_off{0};
-        if (chains && nb) {
+        if ((chains || ext) && nb) {
             std::vector<alvrl_gather_rec> prim;
-            ch = expand_chains(ids, scat, true, &prim);
+            if (ext) ch = host_rows(gl, rows, &prim);
+            else ch = expand_chains(ids, scat, true, &prim);
             hchk(hipMemcpy(rep_recs.p, prim.data(), sizeof(alvrl_gather_rec) * nb, hipMemcpyHostToDevice), "copy records");
             std::vector<alvrl_gather_rec> r;
             std::vector<uint32_t> cid, cstr;
@@ -883,6 +1029,9 @@ struct alvrl_integrator {
     void render(uint32_t rank, uint32_t world, float* d_fb, hipStream_t s)
     {
         if (!have_scene) throw IntegError(ALVRL_ERR_STATE, "render before preprocess");
+        if (ext)
+            throw IntegError(ALVRL_ERR_STATE, "host-cast scene: gather the host's eye records with "
+                                              "alvrl_gather_clustered_host / alvrl_gather_brute_host");
         if (world == 0 || rank >= world) throw IntegError(ALVRL_ERR_INVALID, "bad rank/world");
         prepare_render(rank, world);
         // the caller's stream waits for the records upload (done, synchronous above)
@@ -978,6 +1127,59 @@ ALVRL_API int alvrl_integrator_preprocess(alvrl_integrator* it, const alvrl_scen
 {
     if (!it || !s) return ierr(ALVRL_ERR_INVALID, "alvrl_integrator_preprocess: null argument");
     GUARD({ hchk(hipSetDevice(it->device), "hipSetDevice"); it->preprocess(*s); });
+    return ALVRL_OK;
+}
+
+ALVRL_API int alvrl_integrator_preprocess_ext(alvrl_integrator* it, const alvrl_scene_ext* s)
+{
+    if (!it || !s) return ierr(ALVRL_ERR_INVALID, "alvrl_integrator_preprocess_ext: null argument");
+    GUARD({ hchk(hipSetDevice(it->device), "hipSetDevice"); it->preprocess_ext(*s); });
+    return ALVRL_OK;
+}
+
+ALVRL_API int alvrl_integrator_rep_pixels(alvrl_integrator* it, uint32_t pass, uint32_t* pixel_ids, uint32_t cap,
+                                          uint32_t* n)
+{
+    if (!it || !n) return ierr(ALVRL_ERR_INVALID, "alvrl_integrator_rep_pixels: null argument");
+    GUARD({
+        const std::vector<uint32_t> p = it->rep_pixels(pass);
+        *n = (uint32_t)p.size();
+        if (pixel_ids) {
+            if (cap < p.size()) throw IntegError(ALVRL_ERR_INVALID, "alvrl_integrator_rep_pixels: buffer too small");
+            std::copy(p.begin(), p.end(), pixel_ids);
+        }
+    });
+    return ALVRL_OK;
+}
+
+ALVRL_API int alvrl_integrator_prepass_records(alvrl_integrator* it, uint32_t pass, const alvrl_gather_rec* recs,
+                                               const uint32_t* row_of_rec, uint32_t n, uint32_t rank,
+                                               uint32_t world, const alvrl_exchange* ex)
+{
+    if (!it) return ierr(ALVRL_ERR_INVALID, "alvrl_integrator_prepass_records: null argument");
+    GUARD({
+        hchk(hipSetDevice(it->device), "hipSetDevice");
+        it->prepass_records(pass, recs, row_of_rec, n, rank, world, ex);
+    });
+    return ALVRL_OK;
+}
+
+ALVRL_API int alvrl_integrator_set_cluster_info(alvrl_integrator* it, uint32_t pass, uint32_t npix,
+                                                const uint32_t* p2s, uint32_t nslices, const uint32_t* slice_off,
+                                                const uint32_t* reps, const float* weights, uint32_t n_fb,
+                                                const uint32_t* fb_reps, const float* fb_weights)
+{
+    if (!it || (npix && !p2s) || !slice_off || (n_fb && (!fb_reps || !fb_weights)))
+        return ierr(ALVRL_ERR_INVALID, "alvrl_integrator_set_cluster_info: null argument");
+    const uint32_t nr = slice_off[nslices];
+    if (nr && (!reps || !weights)) return ierr(ALVRL_ERR_INVALID, "alvrl_integrator_set_cluster_info: null lists");
+    GUARD({
+        hchk(hipSetDevice(it->device), "hipSetDevice");
+        std::vector<uint32_t> a(p2s, p2s + npix), so(slice_off, slice_off + nslices + 1), rp(reps, reps + nr),
+            fr(fb_reps, fb_reps + n_fb);
+        std::vector<float> w(weights, weights + nr), fw(fb_weights, fb_weights + n_fb);
+        it->install_cluster_info(pass, a, so, rp, w, fr, fw);
+    });
     return ALVRL_OK;
 }
 

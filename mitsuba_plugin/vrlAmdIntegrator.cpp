@@ -1,15 +1,16 @@
 /*
- * vrlAmdIntegrator.cpp -- the "vrl_amd" Mitsuba integrator plugin: the vrl
- * integrator (src/integrators/vrl/vrlIntegrator.cpp) with its hot path --
- * the per-pixel VRL gather, the reduced matrix R and the per-slice cluster
- * refinement -- on an MI355X through libalvrl.so (include/alvrl.h,
- * include/alvrl_host.h).
+ * vrlAmdIntegrator.cpp -- the vrl integrator (src/integrators/vrl/
+ * vrlIntegrator.cpp) for Mitsuba 0.x with its hot path -- the per-pixel VRL
+ * gather, the reduced matrix R and the per-slice cluster refinement -- on an
+ * MI355X through libalvrl.so (include/alvrl.h, include/alvrl_host.h).
  *
- * Build: compiled inside the mitsuba-ALVRL tree against its headers, like
- * the reference plugin (INTEGRATION.md "Build"); links libalvrl.so and the
- * HIP runtime.  This file is not compiled in this repository (no Mitsuba
- * headers or Boost here); tests/test_plugin_source.py checks that every
- * libalvrl entry point it calls is exported with the declared signature.
+ * Build: inside the mitsuba-ALVRL tree, next to the reference plugin's
+ * sources (it includes their vrlTracer.h), linked against libalvrl.so and the
+ * HIP runtime, and installed as plugins/vrl.so so that scene files keep
+ * type="vrl" (INTEGRATION.md "Build").  tests/test_plugin_source.py compiles
+ * it here against a mock of exactly the Mitsuba declarations it uses
+ * (tests/mitsuba_mock/), whose MTS_IMPLEMENT_CLASS_S expands to
+ * `new vrlAmdIntegrator(stream, manager)` as class.h:219-222 does.
  *
  * Two modes, chosen by the property "amdMode":
  *
@@ -20,21 +21,29 @@
  *                      library traces the VRLs, builds R, refines the
  *                      clusters and renders the whole frame on the GPU once
  *                      per pass; renderBlock copies its block out of that
- *                      frame.  Delta-BSDF chains are expanded by the library
- *                      (LiInternal's recursion, :445-511).
+ *                      frame.  Delta-BSDF chains are expanded by the library.
  *
- *   "records"          For scenes the descriptor cannot express: Mitsuba
- *                      itself casts the eye rays (and follows specular
- *                      chains) in renderBlock and hands the device one gather
- *                      record per eye segment (alvrl_gather_rec);
- *                      alvrl_gather_clustered_host / alvrl_gather_brute_host
- *                      return the radiance of each.  Worker threads call it
+ *   "records"          Any scene with one homogeneous medium: Mitsuba casts
+ *                      every ray itself and the library only does the
+ *                      per-pair work.  preprocess casts buildSlices' ray per
+ *                      pixel (Preprocessor.cpp:1130-1170); prepass traces the
+ *                      VRLs with the host's own vrlTracer (any emitter,
+ *                      vrlTracer.h:91-230), casts the representative pixels'
+ *                      eye paths for R (vrlIntegrator.cpp:322-330) and hands
+ *                      both to the library (alvrl_integrator_prepass_records),
+ *                      which builds R and clusters; renderBlock casts the
+ *                      eye paths -- LiInternal's recursion into every delta
+ *                      component (:445-511) -- and gathers them in one call
+ *                      per block (alvrl_gather_clustered_host).  Every
+ *                      triangle of the scene (Shape::createTriMesh) is the
+ *                      gathers' occluder set.  Worker threads call it
  *                      concurrently: the library gives every calling thread
  *                      its own HIP stream and scratch (alvrl.h "Threading").
- *                      The VRLs and the cluster lists still come from the
- *                      library's prepass over the descriptor's occluders,
- *                      so the scene's triangles are handed to it as
- *                      occluders for the gathers' visibility tests.
+ *
+ * Remote workers: the integrator serializes like the reference (:210-235)
+ * plus its library properties; the pass's VRLs and cluster lists travel as
+ * the "vrls" and "vrlClusterInfo" resources (:353-354, 371-384) and wakeup
+ * installs them (alvrl_integrator_set_vrls / _set_cluster_info).
  *
  * Properties: every property of the reference integrator, with its name and
  * default (vrlIntegrator.cpp:128-208), is parsed by the library
@@ -44,6 +53,7 @@
  * "channel", "samplingDensity" (homogeneous.cpp:156-227).
  */
 #include <mitsuba/core/plugin.h>
+#include <mitsuba/core/sched.h>
 #include <mitsuba/render/bsdf.h>
 #include <mitsuba/render/emitter.h>
 #include <mitsuba/render/medium.h>
@@ -54,13 +64,16 @@
 
 #include <hip/hip_runtime_api.h>
 
+#include <algorithm>
 #include <condition_variable>
+#include <cstring>
 #include <mutex>
 #include <sstream>
 #include <vector>
 
 #include "alvrl.h"
 #include "alvrl_host.h"
+#include "vrlTracer.h"   /* the host's VRL tracer (src/integrators/vrl/), records mode */
 
 MTS_NAMESPACE_BEGIN
 
@@ -69,15 +82,15 @@ namespace {
 /* ALVRL_ERR_* -> Log(EError), which throws like the reference's own errors */
 void check(int rc, const char *what) {
     if (rc != ALVRL_OK)
-        SLog(EError, "vrl_amd: %s: %s", what, alvrl_host_last_error());
+        SLog(EError, "vrl (amd): %s: %s", what, alvrl_host_last_error());
 }
 void checkDevice(int rc, alvrl_ctx *ctx, const char *what) {
     if (rc != ALVRL_OK)
-        SLog(EError, "vrl_amd: %s: %s", what, alvrl_last_error(ctx));
+        SLog(EError, "vrl (amd): %s: %s", what, alvrl_last_error(ctx));
 }
 void checkHip(hipError_t e, const char *what) {
     if (e != hipSuccess)
-        SLog(EError, "vrl_amd: %s: %s", what, hipGetErrorString(e));
+        SLog(EError, "vrl (amd): %s: %s", what, hipGetErrorString(e));
 }
 
 void put3(float *dst, const Spectrum &s) {
@@ -93,14 +106,103 @@ bool isMitsubaOnly(const std::string &k) {
         k == "channel" || k == "samplingDensity";
 }
 
+/* Longest eye path (records per sensor sample) the records mode follows */
+const size_t kMaxPathRecords = 256;
+
 } // namespace
+
+/* The pass's VRLs as a scheduler resource ("vrls", :353): nine float planes
+ * and the particle count. */
+class AmdVrlSet : public SerializableObject {
+public:
+    AmdVrlSet() : m_particles(0), m_pass(0) { }
+    AmdVrlSet(Stream *stream, InstanceManager *manager) {
+        m_pass = stream->readUInt();
+        m_particles = stream->readULong();
+        m_soa.resize((size_t) stream->readULong());
+        if (!m_soa.empty()) stream->readSingleArray(&m_soa[0], m_soa.size());
+    }
+    void serialize(Stream *stream, InstanceManager *manager) const {
+        stream->writeUInt(m_pass);
+        stream->writeULong(m_particles);
+        stream->writeULong(m_soa.size());
+        if (!m_soa.empty()) stream->writeSingleArray(&m_soa[0], m_soa.size());
+    }
+    uint32_t count() const { return (uint32_t) (m_soa.size() / 9); }
+    std::vector<float> m_soa;
+    uint64_t m_particles;
+    uint32_t m_pass;
+    MTS_DECLARE_CLASS()
+};
+
+/* The pass's cluster lists ("vrlClusterInfo", :354), in vrlClusterInfo's
+ * stream layout (:66-101: m_slices, per-slice ids, per-slice weights, global
+ * and fall-back lists), preceded by the pass number. */
+class AmdClusterInfo : public SerializableObject {
+public:
+    AmdClusterInfo() : m_pass(0) { }
+    AmdClusterInfo(Stream *stream, InstanceManager *manager) {
+        m_pass = stream->readUInt();
+        m_slices.resize((size_t) stream->readULong());
+        for (size_t i = 0; i < m_slices.size(); ++i) m_slices[i] = stream->readUInt();
+        const size_t ns = (size_t) stream->readULong();
+        m_off.assign(ns + 1, 0);
+        std::vector<std::vector<uint32_t> > ids(ns);
+        for (size_t s = 0; s < ns; ++s) {
+            ids[s].resize((size_t) stream->readULong());
+            for (size_t k = 0; k < ids[s].size(); ++k) ids[s][k] = stream->readUInt();
+            m_off[s + 1] = m_off[s] + (uint32_t) ids[s].size();
+        }
+        if ((size_t) stream->readULong() != ns) SLog(EError, "vrlClusterInfo: slice counts differ");
+        for (size_t s = 0; s < ns; ++s) {
+            if ((size_t) stream->readULong() != ids[s].size()) SLog(EError, "vrlClusterInfo: list sizes differ");
+            for (size_t k = 0; k < ids[s].size(); ++k) {
+                m_reps.push_back(ids[s][k]);
+                m_w.push_back(stream->readFloat());
+            }
+        }
+        for (size_t n = (size_t) stream->readULong(), i = 0; i < n; ++i) stream->readUInt();    /* global (unused, :163) */
+        for (size_t n = (size_t) stream->readULong(), i = 0; i < n; ++i) stream->readFloat();
+        m_fbReps.resize((size_t) stream->readULong());
+        for (size_t i = 0; i < m_fbReps.size(); ++i) m_fbReps[i] = stream->readUInt();
+        m_fbW.resize((size_t) stream->readULong());
+        for (size_t i = 0; i < m_fbW.size(); ++i) m_fbW[i] = (float) stream->readFloat();
+    }
+    void serialize(Stream *stream, InstanceManager *manager) const {
+        stream->writeUInt(m_pass);
+        stream->writeULong(m_slices.size());
+        for (size_t i = 0; i < m_slices.size(); ++i) stream->writeUInt(m_slices[i]);
+        const size_t ns = m_off.empty() ? 0 : m_off.size() - 1;
+        stream->writeULong(ns);
+        for (size_t s = 0; s < ns; ++s) {
+            stream->writeULong(m_off[s + 1] - m_off[s]);
+            for (uint32_t k = m_off[s]; k < m_off[s + 1]; ++k) stream->writeUInt(m_reps[k]);
+        }
+        stream->writeULong(ns);
+        for (size_t s = 0; s < ns; ++s) {
+            stream->writeULong(m_off[s + 1] - m_off[s]);
+            for (uint32_t k = m_off[s]; k < m_off[s + 1]; ++k) stream->writeFloat(m_w[k]);
+        }
+        stream->writeULong(0);
+        stream->writeULong(0);
+        stream->writeULong(m_fbReps.size());
+        for (size_t i = 0; i < m_fbReps.size(); ++i) stream->writeUInt(m_fbReps[i]);
+        stream->writeULong(m_fbW.size());
+        for (size_t i = 0; i < m_fbW.size(); ++i) stream->writeFloat(m_fbW[i]);
+    }
+    std::vector<uint32_t> m_slices, m_off, m_reps, m_fbReps;
+    std::vector<float> m_w, m_fbW;
+    uint32_t m_pass;
+    MTS_DECLARE_CLASS()
+};
 
 class vrlAmdIntegrator : public ProgressiveMonteCarloIntegrator {
 public:
     vrlAmdIntegrator(const Properties &props) : ProgressiveMonteCarloIntegrator(props) {
-        m_recordsMode = props.getString("amdMode", "frame") == "records";
-        if (!m_recordsMode && props.getString("amdMode", "frame") != "frame")
+        const std::string mode = props.getString("amdMode", "frame");
+        if (mode != "frame" && mode != "records")
             Log(EError, "amdMode must be \"frame\" or \"records\"");
+        m_recordsMode = mode == "records";
         m_device = props.getInteger("amdDevice", 0);
         m_samplingWeight = props.getFloat("mediumSamplingWeight", -1);
         std::string strategy = props.getString("strategy", "balance");
@@ -111,8 +213,18 @@ public:
         else Log(EError, "Specified an unknown sampling strategy");
         m_channel = props.getInteger("channel", -1) + 1;
         m_samplingDensity = props.getFloat("samplingDensity", 0.0f);
+        /* the reference's serialized fields (:212-218) and what records mode reads itself */
+        m_volVolSamples = props.getInteger("volVolSamples", 2);
+        m_volSurfSamples = props.getInteger("volSurfSamples", 2);
+        m_globalCluster = props.getBoolean("globalCluster", false);
+        m_localRefinement = props.getBoolean("localRefinement", true);
         m_specRRdepth = props.getInteger("specularForcedRRdepth", 100);
         m_initialSpecularThroughput = props.getFloat("initialSpecularThroughput", 20);
+        m_shortVrls = props.getBoolean("shortVrls", true);
+        m_vrlTargetNum = props.getInteger("vrlTargetNum", 500);
+        m_maxParticleDepth = props.getInteger("maxParticleDepth", -1);
+        m_rrDepth = props.getInteger("rrDepth", 5);
+        m_vrlFile = props.getString("vrlFile", "");
 
         std::vector<std::string> names;
         props.putPropertyNames(names);
@@ -123,60 +235,123 @@ public:
             oss << names[i] << "=" << props.getAsString(names[i]) << ";";
         }
         m_props = oss.str();
-        check(alvrl_integrator_create(m_props.c_str(), m_device, &m_it), "alvrl_integrator_create");
-        checkHip(hipSetDevice(m_device), "hipSetDevice");
-        checkHip(hipStreamCreateWithFlags(&m_stream, hipStreamNonBlocking), "hipStreamCreate");
+        create(1);
+    }
+
+    /* unserialization (vrlIntegrator.cpp:210-221): the reference's fields,
+     * then this plugin's own; the library integrator is re-created from them */
+    vrlAmdIntegrator(Stream *stream, InstanceManager *manager)
+        : ProgressiveMonteCarloIntegrator(stream, manager) {
+        m_volVolSamples = stream->readInt();
+        m_volSurfSamples = stream->readInt();
+        m_globalCluster = stream->readBool();
+        m_localRefinement = stream->readBool();
+        m_specRRdepth = stream->readInt();
+        m_initialSpecularThroughput = stream->readFloat();
+        m_shortVrls = stream->readBool();
+        m_props = stream->readString();
+        m_recordsMode = stream->readBool();
+        m_device = stream->readInt();
+        m_samplingWeight = (float) stream->readFloat();
+        m_strategy = stream->readInt();
+        m_channel = stream->readInt();
+        m_samplingDensity = (float) stream->readFloat();
+        m_sampleCount = stream->readInt();
+        m_vrlsID = m_ciID = 0;
+        create(m_sampleCount);
+    }
+
+    void serialize(Stream *stream, InstanceManager *manager) const {
+        ProgressiveMonteCarloIntegrator::serialize(stream, manager);
+        stream->writeInt(m_volVolSamples);
+        stream->writeInt(m_volSurfSamples);
+        stream->writeBool(m_globalCluster);
+        stream->writeBool(m_localRefinement);
+        stream->writeInt(m_specRRdepth);
+        stream->writeFloat(m_initialSpecularThroughput);
+        stream->writeBool(m_shortVrls);
+        stream->writeString(m_props);
+        stream->writeBool(m_recordsMode);
+        stream->writeInt(m_device);
+        stream->writeFloat(m_samplingWeight);
+        stream->writeInt(m_strategy);
+        stream->writeInt(m_channel);
+        stream->writeFloat(m_samplingDensity);
+        stream->writeInt(m_sampleCount);
     }
 
     ~vrlAmdIntegrator() {
         if (m_fb) hipFree(m_fb);
         if (m_stream) hipStreamDestroy(m_stream);
-        alvrl_integrator_destroy(m_it);
+        if (m_it) alvrl_integrator_destroy(m_it);
     }
 
     bool preprocess(const Scene *scene, RenderQueue *queue, const RenderJob *job,
             int sceneResID, int sensorResID, int samplerResID) {
-        ProgressiveMonteCarloIntegrator::preprocess(scene, queue, job, sceneResID,
-            sensorResID, samplerResID);
+        if (!ProgressiveMonteCarloIntegrator::preprocess(scene, queue, job, sceneResID,
+                sensorResID, samplerResID))
+            return false;
         /* the sampler's sampleCount: sensor samples per pixel and pass
            (renderBlock's sample loop, integrator.cpp:240-264); the frame
-           mode's integrator jitters them itself, so it is re-created with it */
+           mode's library integrator jitters them itself */
         const Sampler *smp = static_cast<Sampler *>(Scheduler::getInstance()->getResource(samplerResID, 0));
-        m_sampleCount = (int) smp->getSampleCount();
-        if (!m_recordsMode && m_sampleCount != 1) {
-            std::ostringstream oss;
-            oss << m_props << "sampleCount=" << m_sampleCount << ";";
-            alvrl_integrator_destroy(m_it);
-            m_it = NULL;
-            check(alvrl_integrator_create(oss.str().c_str(), m_device, &m_it), "alvrl_integrator_create");
-        }
-        describe(scene);
-        alvrl_scene_desc sd = m_desc;
-        sd.occluders = m_tris.empty() ? NULL : &m_tris[0];
-        sd.occluder_material = m_mats.empty() ? NULL : &m_mats[0];
-        check(alvrl_integrator_preprocess(m_it, &sd), "alvrl_integrator_preprocess");
-        const Vector2i size = scene->getSensor()->getFilm()->getCropSize();
-        m_width = size.x; m_height = size.y;
-        m_rgb.assign((size_t) 3 * m_width * m_height, 0.0f);
-        if (m_fb) hipFree(m_fb);
-        checkHip(hipMalloc(&m_fb, sizeof(float) * m_rgb.size()), "hipMalloc");
+        const size_t spp = smp->getSampleCount();
+        if (spp < 1 || spp > 65535)
+            Log(EError, "sampleCount must be in [1, 65535], got %d", (int) spp);
+        create((int) spp);
+        setUp(scene, true);
         return true;
     }
 
     /* vrlIntegrator::prepass (:270-356): VRLs, representatives, R, clusters */
-    bool prepass(const Scene *, Sampler *) {
-        check(alvrl_integrator_prepass(m_it, m_pass), "alvrl_integrator_prepass");
-        if (m_recordsMode) {   // the slice of every pixel, for the blocks' clustered gathers
-            m_p2s.clear();
-            if (alvrl_integrator_num_slices(m_it) > 0) {
-                m_p2s.resize((size_t) m_width * m_height);
-                check(alvrl_integrator_slices(m_it, &m_p2s[0], (uint32_t) m_p2s.size()), "alvrl_integrator_slices");
-            }
-        }
+    bool prepass(const Scene *scene, Sampler *sampler) {
+        if (m_recordsMode)
+            prepassRecords(scene, sampler);
+        else
+            check(alvrl_integrator_prepass(m_it, m_pass), "alvrl_integrator_prepass");
+        publishResources();
         std::lock_guard<std::mutex> g(m_frameLock);
         m_framePass = -1;   // the frame of the new pass is rendered on first use
         ++m_pass;
         return true;
+    }
+
+    /* the pass's VRLs and cluster info as scheduler resources (:353-354) */
+    void bindUsedResources(ParallelProcess *proc) const {
+        ProgressiveMonteCarloIntegrator::bindUsedResources(proc);
+        if (m_vrlsID) proc->bindResource("vrls", m_vrlsID);
+        if (m_ciID) proc->bindResource("vrlClusterInfo", m_ciID);
+    }
+
+    /* a render worker (renderproc.cpp:52-66): install the resources it
+     * received instead of running the prepass (:378-384) */
+    void wakeup(ConfigurableObject *parent, std::map<std::string, SerializableObject *> &params) {
+        ProgressiveMonteCarloIntegrator::wakeup(parent, params);
+        std::map<std::string, SerializableObject *>::iterator v = params.find("vrls");
+        std::map<std::string, SerializableObject *>::iterator c = params.find("vrlClusterInfo");
+        if (v == params.end())
+            return;
+        const Scene *scene = static_cast<const Scene *>(parent);
+        if (!m_ready && scene)
+            setUp(scene, false);
+        const AmdVrlSet *vs = static_cast<const AmdVrlSet *>(v->second);
+        check(alvrl_integrator_set_vrls(m_it, vs->count() ? &vs->m_soa[0] : NULL, vs->count(),
+                                        std::max<uint64_t>(vs->m_particles, 1)), "alvrl_integrator_set_vrls");
+        if (c != params.end()) {
+            const AmdClusterInfo *ci = static_cast<const AmdClusterInfo *>(c->second);
+            check(alvrl_integrator_set_cluster_info(m_it, ci->m_pass, (uint32_t) ci->m_slices.size(),
+                      ci->m_slices.empty() ? NULL : &ci->m_slices[0], (uint32_t) ci->m_off.size() - 1,
+                      &ci->m_off[0], ci->m_reps.empty() ? NULL : &ci->m_reps[0], ci->m_w.empty() ? NULL : &ci->m_w[0],
+                      (uint32_t) ci->m_fbReps.size(), ci->m_fbReps.empty() ? NULL : &ci->m_fbReps[0],
+                      ci->m_fbW.empty() ? NULL : &ci->m_fbW[0]), "alvrl_integrator_set_cluster_info");
+            m_p2s = ci->m_slices;
+            m_pass = (int) ci->m_pass;
+        } else {
+            check(alvrl_integrator_prepass(m_it, vs->m_pass), "alvrl_integrator_prepass");   /* brute force */
+            m_pass = (int) vs->m_pass;
+        }
+        std::lock_guard<std::mutex> g(m_frameLock);
+        m_framePass = -1;
     }
 
     void renderBlock(const Scene *scene, const Sensor *sensor, Sampler *sampler, ImageBlock *block,
@@ -199,7 +374,7 @@ public:
     }
 
     Spectrum Li(const RayDifferential &, RadianceQueryRecord &) const {
-        Log(EError, "vrl_amd renders whole blocks (renderBlock)");
+        Log(EError, "vrl (amd) renders whole blocks (renderBlock)");
         return Spectrum(0.0f);
     }
 
@@ -219,6 +394,75 @@ public:
     MTS_DECLARE_CLASS()
 
 private:
+    /* the library integrator for 'spp' sensor samples per pixel */
+    void create(int spp) {
+        if (m_it && spp == m_sampleCount)
+            return;
+        if (m_it) alvrl_integrator_destroy(m_it);
+        m_it = NULL;
+        m_sampleCount = spp;
+        std::ostringstream oss;
+        oss << m_props << "sampleCount=" << spp << ";";
+        check(alvrl_integrator_create(oss.str().c_str(), m_device, &m_it), "alvrl_integrator_create");
+        if (!m_stream) {
+            checkHip(hipSetDevice(m_device), "hipSetDevice");
+            checkHip(hipStreamCreateWithFlags(&m_stream, hipStreamNonBlocking), "hipStreamCreate");
+        }
+        m_ready = false;
+    }
+
+    /* the scene to the library: the descriptor (frame mode) or, in records
+     * mode, buildSlices' gather points (only on the master: 'slicing') */
+    void setUp(const Scene *scene, bool slicing) {
+        const Vector2i size = scene->getSensor()->getFilm()->getSize();
+        const Vector2i crop = scene->getSensor()->getFilm()->getCropSize();
+        if (size.x != crop.x || size.y != crop.y)
+            Log(EError, "vrl (amd): crop windows are not supported (m_slices covers the whole film)");
+        m_width = size.x; m_height = size.y;
+        if (m_recordsMode) {
+            describeExt(scene, slicing);
+        } else {
+            describe(scene);
+            alvrl_scene_desc sd = m_desc;
+            sd.occluders = m_tris.empty() ? NULL : &m_tris[0];
+            sd.occluder_material = m_mats.empty() ? NULL : &m_mats[0];
+            check(alvrl_integrator_preprocess(m_it, &sd), "alvrl_integrator_preprocess");
+        }
+        m_rgb.assign((size_t) 3 * m_width * m_height, 0.0f);
+        if (m_fb) hipFree(m_fb);
+        m_fb = NULL;
+        if (!m_recordsMode)
+            checkHip(hipMalloc(&m_fb, sizeof(float) * m_rgb.size()), "hipMalloc");
+        m_ready = true;
+    }
+
+    /* the one homogeneous medium, in the library's terms */
+    const Medium *describeMedium(const Scene *scene, alvrl_medium_desc *md) const {
+        const Medium *medium = scene->getSensor()->getMedium();
+        if (scene->getMedia().size() != 1)
+            Log(EError, "vrl (amd) needs exactly one (homogeneous) medium, the one the VRLs live in");
+        if (!medium) medium = scene->getMedia()[0].get();
+        if (medium->getClass()->getName() != "HomogeneousMedium")
+            Log(EError, "vrl (amd): the medium must be homogeneous");
+        const Spectrum ss = medium->getSigmaS(), sa = medium->getSigmaA();
+        for (int i = 0; i < 3; ++i) {
+            md->sigma_s[i] = (float) ss[i];
+            md->sigma_a[i] = (float) sa[i];
+        }
+        md->sampling_weight = m_samplingWeight;
+        md->strategy = m_strategy;
+        md->channel = m_channel;
+        md->sampling_density = m_samplingDensity;
+        const PhaseFunction *phase = medium->getPhaseFunction();
+        const std::string pn = phase->getClass()->getName();
+        if (pn != "HGPhaseFunction" && pn != "IsotropicPhaseFunction")
+            Log(EError, "vrl (amd): the phase function must be isotropic or hg");
+        const bool hg = pn == "HGPhaseFunction";
+        md->phase_type = hg ? 1 : 0;
+        md->phase_g = hg ? (float) phase->getMeanCosine() : 0.0f;
+        return medium;
+    }
+
     /* The scene in the library's terms (alvrl_scene_desc): the perspective
      * camera, the medium and its container box, the point light, and the
      * remaining triangles as occluders. */
@@ -227,7 +471,7 @@ private:
         const Sensor *sensor = scene->getSensor();
         const PerspectiveCamera *cam = dynamic_cast<const PerspectiveCamera *>(sensor);
         if (!cam)
-            Log(EError, "vrl_amd needs a perspective camera");
+            Log(EError, "vrl (amd) frame mode needs a perspective camera (amdMode=records takes any sensor)");
         const Transform toWorld = cam->getWorldTransform()->eval(0);
         const Point o = toWorld(Point(0.0f));
         const Point t = toWorld(Point(0.0f, 0.0f, 1.0f));
@@ -238,34 +482,20 @@ private:
             m_desc.cam_up[i] = (float) up[i];
         }
         m_desc.fov_x_deg = (float) cam->getXFov();
-        const Vector2i size = sensor->getFilm()->getCropSize();
-        m_desc.width = size.x; m_desc.height = size.y;
+        m_desc.width = m_width; m_desc.height = m_height;
 
         /* the medium and the shape that contains it */
-        const Medium *medium = sensor->getMedium();
-        if (!medium || scene->getMedia().size() != 1)
-            Log(EError, "vrl_amd needs the camera inside one homogeneous medium");
-        const Spectrum ss = medium->getSigmaS(), sa = medium->getSigmaA();
-        for (int i = 0; i < 3; ++i) {
-            m_desc.medium.sigma_s[i] = (float) ss[i];
-            m_desc.medium.sigma_a[i] = (float) sa[i];
-        }
-        m_desc.medium.sampling_weight = m_samplingWeight;
-        m_desc.medium.strategy = m_strategy;
-        m_desc.medium.channel = m_channel;
-        m_desc.medium.sampling_density = m_samplingDensity;
-        const PhaseFunction *phase = medium->getPhaseFunction();
-        const bool hg = phase->getClass()->getName() == "HGPhaseFunction";
-        m_desc.medium.phase_type = hg ? 1 : 0;
-        m_desc.medium.phase_g = hg ? (float) phase->getMeanCosine() : 0.0f;
+        if (!sensor->getMedium())
+            Log(EError, "vrl (amd) frame mode needs the camera inside the medium (amdMode=records does not)");
+        const Medium *medium = describeMedium(scene, &m_desc.medium);
 
         /* the point light: samplePosition returns its power, intensity * 4 pi (point.cpp:81-91) */
         const Emitter *light = NULL;
         for (size_t i = 0; i < scene->getEmitters().size(); ++i)
             if (scene->getEmitters()[i]->getType() & Emitter::EDeltaPosition)
                 light = scene->getEmitters()[i].get();
-        if (!light)
-            Log(EError, "vrl_amd needs a point light");
+        if (!light || scene->getEmitters().size() != 1)
+            Log(EError, "vrl (amd) frame mode needs one point light (amdMode=records takes any emitters)");
         PositionSamplingRecord pRec(0.0f);
         const Spectrum power = light->samplePosition(pRec, Point2(0.5f));
         put3(m_desc.light_intensity, power * (Float) (0.25f * INV_PI));
@@ -291,37 +521,199 @@ private:
             }
             const TriMesh *mesh = dynamic_cast<const TriMesh *>(sh);
             if (!mesh)
-                Log(EError, "vrl_amd: shape \"%s\" inside the medium is not a triangle mesh",
-                    sh->getName().c_str());
+                Log(EError, "vrl (amd): shape \"%s\" inside the medium is not a triangle mesh "
+                    "(amdMode=records takes any shape)", sh->getName().c_str());
             uint32_t mat = ALVRL_MAT_DIFFUSE;
             if (bsdf) {
                 const unsigned int type = bsdf->getType();
                 if (type & BSDF::ENull) {
                     mat = ALVRL_MAT_NULL;
-                } else if ((type & BSDF::EDeltaReflection) && !(type & BSDF::ESmooth)) {
+                } else if ((type & BSDF::EDeltaReflection) && !(type & BSDF::EDeltaTransmission) &&
+                           !(type & BSDF::ESmooth)) {
                     mat = ALVRL_MAT_MIRROR;
                     if (!haveSpec) put3(m_desc.occluder_specular, bsdf->getSpecularReflectance(its));
                     haveSpec = true;
+                } else if (type & BSDF::EDelta) {
+                    Log(EError, "vrl (amd) frame mode: BSDF of \"%s\" is neither diffuse, mirror nor null "
+                        "(amdMode=records follows every delta component)", sh->getName().c_str());
                 } else if (!haveOccAlbedo) {
                     put3(m_desc.occluder_albedo, bsdf->getDiffuseReflectance(its));
                     haveOccAlbedo = true;
                 }
             }
-            const Point *pos = mesh->getVertexPositions();
-            const Triangle *tri = mesh->getTriangles();
-            for (size_t f = 0; f < mesh->getTriangleCount(); ++f) {
-                for (int k = 0; k < 3; ++k) {
-                    const Point &p = pos[tri[f].idx[k]];
-                    m_tris.push_back((float) p.x);
-                    m_tris.push_back((float) p.y);
-                    m_tris.push_back((float) p.z);
-                }
-                m_mats.push_back(mat);
-            }
+            appendTriangles(mesh, mat);
         }
         if (!haveBox)
-            Log(EError, "vrl_amd needs a shape that contains the medium (its interior)");
+            Log(EError, "vrl (amd) needs a shape that contains the medium (its interior)");
         m_desc.n_occluders = (uint32_t) m_mats.size();
+    }
+
+    void appendTriangles(const TriMesh *mesh, uint32_t mat) {
+        const Point *pos = mesh->getVertexPositions();
+        const Triangle *tri = mesh->getTriangles();
+        for (size_t f = 0; f < mesh->getTriangleCount(); ++f) {
+            for (int k = 0; k < 3; ++k) {
+                const Point &p = pos[tri[f].idx[k]];
+                m_tris.push_back((float) p.x);
+                m_tris.push_back((float) p.y);
+                m_tris.push_back((float) p.z);
+            }
+            m_mats.push_back(mat);
+        }
+    }
+
+    /* records mode: the medium, every shape's triangles for the gathers'
+     * occluder test, and (on the master) buildSlices' gather point of every
+     * pixel (Preprocessor.cpp:1140-1170): the centre ray's first hit,
+     * continued past null surfaces */
+    void describeExt(const Scene *scene, bool slicing) {
+        alvrl_scene_ext e;
+        std::memset(&e, 0, sizeof(e));
+        e.width = m_width; e.height = m_height;
+        const AABB &aabb = scene->getAABB();
+        for (int i = 0; i < 3; ++i) { e.scene_min[i] = (float) aabb.min[i]; e.scene_max[i] = (float) aabb.max[i]; }
+        m_medium = describeMedium(scene, &e.medium);
+        m_tris.clear(); m_mats.clear();
+        const ref_vector<Shape> &shapes = scene->getShapes();
+        for (size_t s = 0; s < shapes.size(); ++s) {
+            Shape *sh = const_cast<Shape *>(shapes[s].get());
+            ref<TriMesh> mesh = sh->createTriMesh();
+            if (!mesh)
+                Log(EError, "vrl (amd): shape \"%s\" has no triangle mesh for the gathers' visibility",
+                    sh->getName().c_str());
+            const BSDF *bsdf = sh->getBSDF();
+            uint32_t mat = ALVRL_MAT_DIFFUSE;
+            if (bsdf && (bsdf->getType() & BSDF::ENull)) mat = ALVRL_MAT_NULL;
+            else if (bsdf && (bsdf->getType() & BSDF::EDeltaTransmission)) mat = ALVRL_MAT_DIELECTRIC;
+            else if (bsdf && (bsdf->getType() & BSDF::EDelta)) mat = ALVRL_MAT_MIRROR;
+            appendTriangles(mesh.get(), mat);
+        }
+        e.triangles = m_tris.empty() ? NULL : &m_tris[0];
+        e.n_triangles = (uint32_t) m_mats.size();
+        e.triangle_material = m_mats.empty() ? NULL : &m_mats[0];
+        std::vector<alvrl_gather_rec> sl;
+        if (slicing) {
+            sl.resize((size_t) m_width * m_height);
+            std::memset(&sl[0], 0, sizeof(alvrl_gather_rec) * sl.size());
+            const Sensor *sensor = scene->getSensor();
+            for (int x = 0; x < m_width; ++x) {
+                for (int y = 0; y < m_height; ++y) {
+                    Ray ray;
+                    Intersection its;
+                    sensor->sampleRay(ray, Point2(x + 0.5f, y + 0.5f), Point2(0.0f), 0.0f);
+                    if (!scene->rayIntersect(ray, its))
+                        continue;   /* no gather point: no slice */
+                    Point gp;
+                    Vector n;
+                    while (true) {
+                        gp = its.p;
+                        n = its.shFrame.n;
+                        if (!(its.getBSDF()->getType() & BSDF::ENull))
+                            break;
+                        ray = Ray(ray, its.t + Epsilon, ray.maxt);
+                        if (!scene->rayIntersect(ray, its))
+                            break;
+                    }
+                    alvrl_gather_rec &r = sl[(size_t) y * m_width + x];
+                    for (int k = 0; k < 3; ++k) { r.p[k] = (float) gp[k]; r.n[k] = (float) n[k]; }
+                    r.flags = ALVRL_REC_HIT;
+                }
+            }
+        }
+        e.slice_recs = sl.empty() ? NULL : &sl[0];
+        check(alvrl_integrator_preprocess_ext(m_it, &e), "alvrl_integrator_preprocess_ext");
+    }
+
+    /* records mode prepass: the host's VRLs, then R over the host's eye paths */
+    void prepassRecords(const Scene *scene, Sampler *sampler) {
+        if (m_vrlFile.empty()) {   /* vrl tracing (:276-280) */
+            ref<vrlTracer> tracer = new vrlTracer(sampler, m_maxParticleDepth, m_rrDepth);
+            ref<vrlVector> v = tracer->randomWalk(scene, m_vrlTargetNum, m_shortVrls);
+            const size_t n = v->size();
+            std::vector<float> soa(9 * n);
+            for (size_t i = 0; i < n; ++i) {
+                const VRL &l = (*v)[i];
+                Float r, g, b;
+                l.m_power.toLinearRGB(r, g, b);
+                const float f[9] = { (float) l.m_start.x, (float) l.m_start.y, (float) l.m_start.z,
+                                     (float) l.m_end.x, (float) l.m_end.y, (float) l.m_end.z,
+                                     (float) r, (float) g, (float) b };
+                for (int k = 0; k < 9; ++k) soa[(size_t) k * n + i] = f[k];
+            }
+            check(alvrl_integrator_set_vrls(m_it, n ? &soa[0] : NULL, (uint32_t) n,
+                                            std::max<uint64_t>(v->getParticleCount(), 1)), "alvrl_integrator_set_vrls");
+        }   /* else: the library read vrlFile in preprocess (:243-252) */
+        if (!m_globalCluster && !m_localRefinement) {
+            check(alvrl_integrator_prepass(m_it, m_pass), "alvrl_integrator_prepass");   /* brute force */
+            m_p2s.clear();
+            return;
+        }
+        uint32_t nrows = 0;
+        check(alvrl_integrator_rep_pixels(m_it, m_pass, NULL, 0, &nrows), "alvrl_integrator_rep_pixels");
+        std::vector<uint32_t> pix(nrows + 1);
+        check(alvrl_integrator_rep_pixels(m_it, m_pass, &pix[0], nrows + 1, &nrows), "alvrl_integrator_rep_pixels");
+        /* R rows (:322-330): the ray through the representative pixel's centre,
+           LiInternal's eye path (getLiLuminanceVrlContributions, :527-539) */
+        std::vector<alvrl_gather_rec> recs;
+        std::vector<uint32_t> rows;
+        const Sensor *sensor = scene->getSensor();
+        for (uint32_t i = 0; i < nrows; ++i) {
+            const Point2i p((int) (pix[i] % (uint32_t) m_width), (int) (pix[i] / (uint32_t) m_width));
+            sampler->generate(p);
+            RadianceQueryRecord rRec(scene, sampler);
+            rRec.newQuery(RadianceQueryRecord::ESensorRay, sensor->getMedium());
+            Ray ray0;
+            sensor->sampleRay(ray0, Point2(p) + Vector2(0.5f), Point2(0.0f), 0.0f);
+            const RayDifferential ray(ray0);
+            appendPath(ray, rRec, Spectrum(1.0f), Spectrum(m_initialSpecularThroughput), 0u, &recs);
+            rows.resize(recs.size(), i);
+            sampler->advance();
+        }
+        check(alvrl_integrator_prepass_records(m_it, m_pass, recs.empty() ? NULL : &recs[0],
+                                               rows.empty() ? NULL : &rows[0], (uint32_t) recs.size(), 0, 1, NULL),
+              "alvrl_integrator_prepass_records");
+        m_p2s.resize((size_t) m_width * m_height);
+        check(alvrl_integrator_slices(m_it, &m_p2s[0], (uint32_t) m_p2s.size()), "alvrl_integrator_slices");
+    }
+
+    /* the pass's VRLs and cluster lists for remote workers (:353-354) */
+    void publishResources() {
+        ref<Scheduler> sched = Scheduler::getInstance();
+        if (m_vrlsID) sched->unregisterResource(m_vrlsID);
+        if (m_ciID) sched->unregisterResource(m_ciID);
+        m_vrlsID = m_ciID = 0;
+        ref<AmdVrlSet> vs = new AmdVrlSet();
+        uint32_t n = 0;
+        uint64_t pc = 0;
+        check(alvrl_integrator_vrls(m_it, NULL, 0, &n, &pc), "alvrl_integrator_vrls");
+        vs->m_soa.resize((size_t) 9 * n);
+        if (n) check(alvrl_integrator_vrls(m_it, &vs->m_soa[0], n, &n, &pc), "alvrl_integrator_vrls");
+        vs->m_particles = pc;
+        vs->m_pass = (uint32_t) m_pass;
+        m_vrlsID = sched->registerResource(vs);
+        const uint32_t ns = alvrl_integrator_num_slices(m_it);
+        if (!ns)
+            return;
+        ref<AmdClusterInfo> ci = new AmdClusterInfo();
+        ci->m_pass = (uint32_t) m_pass;
+        ci->m_slices.resize((size_t) m_width * m_height);
+        check(alvrl_integrator_slices(m_it, &ci->m_slices[0], (uint32_t) ci->m_slices.size()), "alvrl_integrator_slices");
+        alvrl_integrator_stats st;
+        check(alvrl_integrator_get_stats(m_it, &st), "alvrl_integrator_get_stats");
+        ci->m_off.resize(ns + 1);
+        ci->m_reps.resize((size_t) st.clusters_total + 1);
+        ci->m_w.resize((size_t) st.clusters_total + 1);
+        ci->m_fbReps.resize((size_t) n + 1);
+        ci->m_fbW.resize((size_t) n + 1);
+        uint32_t nfb = 0;
+        check(alvrl_integrator_clusters(m_it, &ci->m_off[0], &ci->m_reps[0], &ci->m_w[0],
+                                        (uint32_t) ci->m_reps.size(), &ci->m_fbReps[0], &ci->m_fbW[0],
+                                        (uint32_t) ci->m_fbReps.size(), &nfb), "alvrl_integrator_clusters");
+        ci->m_reps.resize(ci->m_off[ns]);
+        ci->m_w.resize(ci->m_off[ns]);
+        ci->m_fbReps.resize(nfb);
+        ci->m_fbW.resize(nfb);
+        m_ciID = sched->registerResource(ci);
     }
 
     /* "frame" mode: one device render of the whole frame per pass, shared by
@@ -351,8 +743,84 @@ private:
         check(rc, "alvrl_integrator_render");
     }
 
-    /* "records" mode: LiInternal's eye path per pixel (:398-524), cast by
-     * Mitsuba; one record per segment with the recursion's weight */
+    /* LiInternal (vrlIntegrator.cpp:398-524) as gather records: the segment
+     * of 'ray' and, through a delta BSDF, each delta component's continuation
+     * (bRec.component = i, :467-511) with its own weight, throughput and
+     * roulette.  A record's depth word is its index in the pixel sample's
+     * path tree (record k of sample j: k | j << 16): it keys the gathers'
+     * streams, so branches at the same depth draw independently. */
+    void appendPath(const RayDifferential &ray, RadianceQueryRecord &rRec, const Spectrum &weight,
+            const Spectrum &throughputWithEtaSq, uint32_t sampleIndex, std::vector<alvrl_gather_rec> *recs) const {
+        appendPathAt(ray, rRec, weight, throughputWithEtaSq, sampleIndex, recs, recs->size());
+    }
+
+    void appendPathAt(const RayDifferential &ray, RadianceQueryRecord &rRec, const Spectrum &weight,
+            const Spectrum &throughputWithEtaSq, uint32_t sampleIndex, std::vector<alvrl_gather_rec> *recs,
+            size_t first) const {
+        if (recs->size() - first >= kMaxPathRecords)
+            return;
+        if (!rRec.rayIntersect(ray))
+            return;   /* :418-423: no contribution (an infinite eye ray's is dropped) */
+        const Intersection &its = rRec.its;
+        const BSDF *bsdf = its.getBSDF();
+        const unsigned int type = bsdf->getType();
+        alvrl_gather_rec r;
+        std::memset(&r, 0, sizeof(r));
+        for (int k = 0; k < 3; ++k) {
+            r.o[k] = (float) ray.o[k]; r.d[k] = (float) ray.d[k];
+            r.p[k] = (float) its.p[k]; r.n[k] = (float) its.shFrame.n[k];
+        }
+        const bool smooth = (type & BSDF::ESmooth) != 0;
+        if (smooth && !(type & BSDF::EDiffuseReflection))
+            warnOnce("a smooth non-diffuse BSDF's vol->surf term is evaluated as its diffuse reflectance");
+        put3(r.albedo, smooth ? bsdf->getDiffuseReflectance(its) : Spectrum(0.0f));
+        r.flags = ALVRL_REC_HIT | (smooth ? ALVRL_REC_SMOOTH : 0u) | ((type & BSDF::EDelta) ? ALVRL_REC_DELTA : 0u) |
+            (rRec.medium && !rRec.medium->getSigmaS().isZero() ? ALVRL_REC_MEDIUM : 0u);
+        put3(r.weight, weight);
+        r.depth = (uint32_t) (recs->size() - first) | (sampleIndex << 16);
+        recs->push_back(r);
+        if (!(type & BSDF::EDelta))
+            return;   /* no specular chains */
+        Spectrum transmittance(1.0f);
+        if (rRec.medium) {
+            MediumSamplingRecord mRec;
+            rRec.medium->eval(Ray(ray, 0, its.t), mRec);
+            transmittance = mRec.transmittance;
+        }
+        if (transmittance.isZero())
+            return;
+        RadianceQueryRecord rRec2;
+        for (int i = 0; i < bsdf->getComponentCount(); ++i) {
+            if (!(bsdf->getType(i) & BSDF::EDelta))
+                continue;
+            BSDFSamplingRecord bRec(rRec.its, rRec.sampler, ERadiance);
+            bRec.component = i;
+            const Spectrum bsdfWeight = bsdf->sample(bRec, Point2(0.5f));
+            if (bsdfWeight.isZero())
+                continue;
+            Spectrum thr2 = throughputWithEtaSq * transmittance * bsdfWeight * (bRec.eta * bRec.eta);
+            const Float maxRR = rRec.depth >= m_specRRdepth ? (Float) 0.98f : (Float) 1.0f;
+            const Float rrProb = std::min(maxRR, thr2.max());
+            if (rrProb <= 0 || (rrProb < 1 && rRec.nextSample1D() > rrProb))
+                continue;
+            thr2 /= rrProb;
+            rRec2.recursiveQuery(rRec);
+            const RayDifferential ray2(rRec.its.p, rRec.its.toWorld(bRec.wo), ray.time);
+            if (rRec.its.isMediumTransition())
+                rRec2.medium = rRec.its.getTargetMedium(ray2.d);
+            appendPathAt(ray2, rRec2, weight * transmittance * bsdfWeight / rrProb, thr2, sampleIndex, recs, first);
+        }
+    }
+
+    void warnOnce(const char *msg) const {
+        std::lock_guard<std::mutex> g(m_frameLock);
+        if (m_warned) return;
+        m_warned = true;
+        Log(EWarn, "vrl (amd): %s", msg);
+    }
+
+    /* "records" mode: every sensor sample's eye path cast by Mitsuba, the
+     * block's records gathered on the device in one call */
     void renderBlockRecords(const Scene *scene, const Sensor *sensor, Sampler *sampler, ImageBlock *block,
             const bool &stop, const std::vector< TPoint2<uint8_t> > &points) const {
         alvrl_ctx *ctx = alvrl_integrator_ctx(m_it);
@@ -362,71 +830,32 @@ private:
         const bool clustered = !m_p2s.empty();
         std::vector<Point2> pos;   // each sensor sample's image position
         for (size_t i = 0; i < points.size() && !stop; ++i) {
-          const Point2i p = Point2i(points[i]) + Vector2i(off);
-          const uint32_t pid = (uint32_t) p.y * (uint32_t) m_width + (uint32_t) p.x;
-          const uint32_t sl = clustered ? m_p2s[(size_t) p.y + (size_t) m_height * p.x] : 0u;   // m_slices[y + H*x]
-          sampler->generate(p);
-          for (size_t j = 0; j < sampler->getSampleCount(); ++j) {
-            RadianceQueryRecord rRec(scene, sampler);
-            rRec.newQuery(RadianceQueryRecord::ESensorRay, sensor->getMedium());
-            /* the pixel centre for one sample per pixel, else a sampler draw (integrator.cpp:240-247) */
-            const Point2 samplePos = Point2(p) + (sampler->getSampleCount() == 1 ? Vector2(0.5f)
-                                                                                : Vector2(rRec.nextSample2D()));
-            RayDifferential ray;
-            sensor->sampleRayDifferential(ray, samplePos, Point2(0.5f), 0.5f);
-            const uint32_t owner_id = (uint32_t) pos.size();
-            pos.push_back(samplePos);
-            Spectrum weight(1.0f), throughput(m_initialSpecularThroughput);
-            for (uint32_t depth = 0; depth < 256; ++depth) {
-                if (!rRec.rayIntersect(ray)) break;
-                const Intersection &its = rRec.its;
-                const BSDF *bsdf = its.getBSDF();
-                const unsigned int type = bsdf->getType();
-                alvrl_gather_rec r;
-                for (int k = 0; k < 3; ++k) {
-                    r.o[k] = (float) ray.o[k]; r.d[k] = (float) ray.d[k];
-                    r.p[k] = (float) its.p[k]; r.n[k] = (float) its.shFrame.n[k];
+            const Point2i p = Point2i(points[i]) + Vector2i(off);
+            const uint32_t pid = (uint32_t) p.y * (uint32_t) m_width + (uint32_t) p.x;
+            const uint32_t sl = clustered ? m_p2s[(size_t) p.y + (size_t) m_height * p.x] : 0u;   // m_slices[y + H*x]
+            sampler->generate(p);
+            for (size_t j = 0; j < sampler->getSampleCount(); ++j) {
+                RadianceQueryRecord rRec(scene, sampler);
+                rRec.newQuery(RadianceQueryRecord::ESensorRay, sensor->getMedium());
+                /* the pixel centre for one sample per pixel, else a sampler draw (integrator.cpp:240-247) */
+                const Point2 samplePos = Point2(p) + (sampler->getSampleCount() == 1 ? Vector2(0.5f)
+                                                                                    : Vector2(rRec.nextSample2D()));
+                RayDifferential ray;
+                sensor->sampleRayDifferential(ray, samplePos, Point2(0.5f), 0.5f);
+                const uint32_t ownerId = (uint32_t) pos.size();
+                pos.push_back(samplePos);
+                const size_t before = recs.size();
+                appendPath(ray, rRec, Spectrum(1.0f), Spectrum(m_initialSpecularThroughput), (uint32_t) j, &recs);
+                for (size_t k = before; k < recs.size(); ++k) {
+                    ids.push_back(pid);
+                    slice.push_back(sl);
+                    owner.push_back(ownerId);
                 }
-                const bool smooth = (type & BSDF::ESmooth) != 0;
-                Spectrum rho = smooth ? bsdf->getDiffuseReflectance(its) : Spectrum(0.0f);
-                put3(r.albedo, rho);
-                r.flags = ALVRL_REC_HIT | (smooth ? ALVRL_REC_SMOOTH : ALVRL_REC_DELTA) |
-                    (rRec.medium && !rRec.medium->getSigmaS().isZero() ? ALVRL_REC_MEDIUM : 0u);
-                put3(r.weight, weight);
-                r.depth = depth | ((uint32_t) j << 16);   /* the sample keys the gather's streams */
-                recs.push_back(r);
-                ids.push_back(pid);
-                slice.push_back(sl);
-                owner.push_back(owner_id);
-                if (!(type & BSDF::EDelta)) break;
-                /* the delta component, transmittance, roulette (:450-510) */
-                MediumSamplingRecord mRec;
-                Spectrum tr(1.0f);
-                if (rRec.medium) {
-                    rRec.medium->eval(Ray(ray, 0, its.t), mRec);
-                    tr = mRec.transmittance;
-                }
-                if (tr.isZero()) break;
-                BSDFSamplingRecord bRec(its, rRec.sampler, ERadiance);
-                const Spectrum bw = bsdf->sample(bRec, Point2(0.5f));
-                if (bw.isZero()) break;
-                const Spectrum thr2 = throughput * tr * bw * (bRec.eta * bRec.eta);
-                const Float rrProb = std::min((Float) (rRec.depth >= m_specRRdepth ? 0.98f : 1.0f), thr2.max());
-                if (rrProb <= 0 || (rrProb < 1 && rRec.nextSample1D() > rrProb)) break;
-                throughput = thr2 / rrProb;
-                weight = weight * tr * bw / rrProb;
-                RadianceQueryRecord rRec2;
-                rRec2.recursiveQuery(rRec);
-                ray = RayDifferential(its.p, its.toWorld(bRec.wo), ray.time);
-                if (its.isMediumTransition())
-                    rRec2.medium = its.getTargetMedium(ray.d);
-                rRec = rRec2;
+                sampler->advance();
             }
-            sampler->advance();
-          }
         }
         const uint32_t n = (uint32_t) recs.size();
-        std::vector<float> rgb((size_t) 3 * n);
+        std::vector<float> rgb((size_t) 3 * n + 3);
         if (n) {
             if (clustered)
                 checkDevice(alvrl_gather_clustered_host(ctx, &recs[0], &ids[0], &slice[0], n, &rgb[0]), ctx,
@@ -448,29 +877,39 @@ private:
 
     alvrl_integrator *m_it = NULL;
     std::string m_props;   /* the integrator's properties (alvrl_integrator_create) */
-    int m_sampleCount = 1;
+    int m_sampleCount = 0;
     hipStream_t m_stream = NULL;
     int m_device = 0;
     bool m_recordsMode = false;
     float m_samplingWeight = -1.0f, m_samplingDensity = 0.0f;
     int m_strategy = ALVRL_STRATEGY_BALANCE, m_channel = 0;
+    int m_volVolSamples = 2, m_volSurfSamples = 2;
+    bool m_globalCluster = false, m_localRefinement = true, m_shortVrls = true;
     int m_specRRdepth = 100;
     Float m_initialSpecularThroughput = 20;
+    int m_vrlTargetNum = 500, m_maxParticleDepth = -1, m_rrDepth = 5;
+    std::string m_vrlFile;
+    const Medium *m_medium = NULL;
     alvrl_scene_desc m_desc;
     std::vector<float> m_tris;
     std::vector<uint32_t> m_mats;
     std::vector<uint32_t> m_p2s;   // records mode: the pass's slice of every pixel (column-major)
     int m_width = 0, m_height = 0;
     float *m_fb = NULL;
+    bool m_ready = false;
+    int m_vrlsID = 0, m_ciID = 0;
     /* the current pass's frame (frame mode) */
     mutable std::vector<float> m_rgb;
     mutable std::mutex m_frameLock;
     mutable std::condition_variable m_frameReady;
     mutable bool m_rendering = false;
+    mutable bool m_warned = false;
     mutable int m_framePass = -1;
     int m_pass = 0;
 };
 
+MTS_IMPLEMENT_CLASS_S(AmdVrlSet, false, SerializableObject)
+MTS_IMPLEMENT_CLASS_S(AmdClusterInfo, false, SerializableObject)
 MTS_IMPLEMENT_CLASS_S(vrlAmdIntegrator, false, ProgressiveMonteCarloIntegrator)
 MTS_EXPORT_PLUGIN(vrlAmdIntegrator, "VRL integrator with Adaptive LightSlice on an MI355X (libalvrl)");
 MTS_NAMESPACE_END

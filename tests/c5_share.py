@@ -1,18 +1,31 @@
-"""Rank 0's share of BASELINE.json configs[4] (C5: 2048^2, 1M VRLs, adaptive
-LightSlice, 8 GPUs) on ONE GPU, through the real slice-sharded prepass
-(alvrl_integrator_prepass_dist): this rank builds R for, and
-refines, slices s % 8 == 0 only -- its 1/8 of C5's R, about 65 GB.
+"""BASELINE.json configs[4] (C5: 2048^2, 1M VRLs, adaptive LightSlice, 8 GPUs)
+on ONE GPU, rank by rank, through the real slice-sharded prepass
+(alvrl_integrator_prepass_dist).  Rank r builds R for, and
+refines, slices s % 8 == r -- its 1/8 of C5's R, about 61 GB -- so the eight
+shares run one after the other on one card, each freed before the next.
 
-The seven other ranks are stood in for by `StubExchange`, an in-process
-alvrl_exchange: the non-zero VRL mask gets zeros from them (OR-neutral), and
-the cluster all-gather gets, for every slice s % 8 != 0, a one-entry list
-(VRL 0, weight 1) in the wire format of csrc/host/exchange.cpp.  Rank 0's
-own slices go through the library's exchange code unchanged.
+The exchange (`SimExchange`, an in-process alvrl_exchange) plays the other
+seven ranks with the data they would really send:
 
-Used by tests/test_gpu_scale.py and tools/c5_share.py (timings)."""
+  phase 1  every rank builds its R rows; its non-zero VRL mask (the OR round of
+           Preprocessor::cluster, :843-855) is captured and the prepass is
+           stopped there (the callback fails -> ALVRL_ERR_COMM);
+  phase 2  every rank's prepass runs to the end with the TRUE OR of all eight
+           masks; the cluster all-gather hands it one-entry placeholder lists
+           for the other ranks' slices (they are not read: the rank's own
+           slices are taken from its result);
+  phase 3  the eight ranks' own slices are merged into one vrlClusterInfo (the
+           resource the reference ships to render workers, vrlIntegrator.cpp:
+           29-101), installed with alvrl_integrator_load_cluster_info, and the
+           2048^2 frame is rendered as the eight ranks' 64x64 tiles, summed
+           (the framebuffer reduce of vrlIntegrator's render over ranks).
+
+`run_share` keeps round 3's rank-0-only form for the timing tool.
+Used by tests/test_gpu_scale.py and tools/c5_share.py."""
 from __future__ import annotations
 
 import ctypes as C
+import os
 import struct
 import time
 
@@ -25,19 +38,28 @@ C5_VRLS = 1_000_000
 C5_WORLD = 8
 
 
-class StubExchange:
-    """alvrl_exchange for rank 0 of `world`, the other ranks simulated."""
+class SimExchange:
+    """alvrl_exchange for rank `rank` of `world`, the other ranks simulated.
 
-    def __init__(self, world: int, nslices: int, nvrl: int):
+    masks: None -> capture mode: the OR round records this rank's mask and
+    fails the call (the prepass stops before refining).  Otherwise a list of
+    `world` byte strings: the OR round receives them in rank order (this
+    rank's own bytes in its slot), so the library ORs the true masks.
+    "zero": the others send zero masks (round 3's rank-0 timing form)."""
+
+    def __init__(self, rank: int, world: int, nslices: int, masks=None):
         import alvrl
-        self.world, self.nslices, self.nvrl = world, nslices, nvrl
+        self.rank, self.world, self.nslices = rank, world, nslices
+        self.masks = masks
+        self.mask = None            # captured own mask (capture mode)
         self.error = None
         self.calls = []
-        self._pending = None        # per-rank messages after a count round
-        self.others = []
-        for r in range(1, world):
-            msg = b"".join(struct.pack("<IIIIf", s, 1, 1, 0, 1.0) for s in range(r, nslices, world))
-            self.others.append(msg)
+        self._pending = None        # a counts round was seen: the next call is the data round
+        self.others = {}
+        for r in range(world):
+            if r != rank:
+                self.others[r] = b"".join(struct.pack("<IIIIf", s, 1, 1, 0, 1.0)
+                                          for s in range(r, nslices, world))
 
         def allgather(user, send, nbytes, recv):
             try:
@@ -45,17 +67,26 @@ class StubExchange:
                 src = C.string_at(send, n) if n else b""
                 if self._pending is None and n == 8:             # allgather_counts
                     own = struct.unpack("<Q", src)[0]
-                    counts = [own] + [len(m) for m in self.others]
+                    counts = [own if r == rank else len(self.others[r]) for r in range(world)]
                     out = struct.pack(f"<{world}Q", *counts)
                     self._pending = True
                     self.calls.append(("counts", counts))
                 elif self._pending:                               # allgatherv data, padded to n
-                    out = src + b"".join(m.ljust(n, b"\0") for m in self.others)
+                    out = b"".join(src if r == rank else self.others[r].ljust(n, b"\0") for r in range(world))
                     self._pending = None
                     self.calls.append(("data", n))
                 else:                                             # or_reduce of the mask
-                    out = src + b"\0" * (n * (world - 1))
                     self.calls.append(("or", n))
+                    if self.masks is None:
+                        self.mask = src
+                        return 7                                  # stop the prepass here
+                    if isinstance(self.masks, str):               # "zero": OR-neutral others
+                        out = src + b"\0" * (n * (world - 1))
+                        C.memmove(recv, out, len(out))
+                        return 0
+                    if any(len(m) != n for m in self.masks):
+                        raise ValueError("mask sizes differ between ranks")
+                    out = b"".join(src if r == rank else self.masks[r] for r in range(world))
                 C.memmove(recv, out, len(out))
                 return 0
             except Exception as e:     # reported as ALVRL_ERR_COMM
@@ -72,20 +103,124 @@ class StubExchange:
                                    + (f" ({self.error!r})" if self.error else ""))
 
 
+def _props(nvrl: int, gpu_tracer: bool, props: str) -> str:
+    return (f"vrlTargetNum={nvrl};gpuTracer={'true' if gpu_tracer else 'false'};"
+            f"seed={SEED_RNG};vrlSeed={SEED_VRL}" + (";" + props if props else ""))
+
+
+def run_full(props: str = "", nvrl: int = C5_VRLS, width: int = C5_W, height: int = C5_H,
+             world: int = C5_WORLD, pass_: int = 0, check=None, workdir: str = "/tmp", log=print):
+    """C5's eight ranks on one GPU (phases 1-3 above).
+
+    check(rank, it, info, mine): called after rank `rank`'s full prepass while
+    its R is still resident (for oracle checks of its slices).
+    Returns (integrator with the merged cluster info installed, info dict);
+    the caller renders and closes it."""
+    import alvrl
+    scene = alvrl.scene_default(width, height)
+    P = _props(nvrl, True, props)
+    t_start = time.time()
+    # phase 1: the masks
+    masks, ns = [], None
+    for r in range(world):
+        it = alvrl.Integrator(P, device=0)
+        try:
+            it.preprocess(scene)
+            ns = it.num_slices()
+            ex = SimExchange(r, world, ns, masks=None)
+            try:
+                it.prepass(pass_, rank=r, world=world, exchange=ex)
+                raise AssertionError("capture exchange did not stop the prepass")
+            except alvrl.AlvrlError as e:
+                if ex.mask is None:
+                    raise
+                assert e.code == alvrl.ALVRL_ERR_COMM, e
+            masks.append(ex.mask)
+        finally:
+            it.close()
+    nz = np.zeros(len(masks[0]), np.uint8)
+    for m in masks:
+        nz |= np.frombuffer(m, np.uint8)
+    t1 = time.time()
+    log(f"C5 phase 1: {world} masks in {t1 - t_start:.1f} s, {int(nz.sum())} of {nz.size} VRLs non-zero "
+        f"(per rank {[int(np.frombuffer(m, np.uint8).sum()) for m in masks]})")
+    # phase 2: every rank's prepass with the true OR
+    per_rank, own = [], {}
+    p2s = vrls = None
+    for r in range(world):
+        it = alvrl.Integrator(P, device=0)
+        try:
+            it.preprocess(scene)
+            ex = SimExchange(r, world, ns, masks=masks)
+            t0 = time.time()
+            it.prepass(pass_, rank=r, world=world, exchange=ex)
+            dt = time.time() - t0
+            st = it.stats()
+            off, _ = it.reps()
+            mine = list(range(r, ns, world))
+            rows = np.diff(off)[mine]
+            cl = it.clusters()
+            for s in mine:
+                b, e = cl["slice_off"][s], cl["slice_off"][s + 1]
+                own[s] = (cl["reps"][b:e].copy(), cl["weights"][b:e].copy())
+            info = dict(rank=r, slices_local=int(st["slices_local"]), rows_local=[int(x) for x in rows],
+                        rows_built=int(st["rows_built"]), vrls=int(st["vrls"]),
+                        R_bytes=int(st["rows_built"]) * int(st["vrls"]) * 8, ms_rbuild=st["ms_rbuild"],
+                        ms_refine_kernel=st["ms_refine_kernel"], refine_entries=int(st["refine_entries"]),
+                        refine_split_entries=int(st["refine_split_entries"]),
+                        contrib_preprocess=int(st["contrib_preprocess"]), slices_failed=int(st["slices_failed"]),
+                        fallback_built=int(st["fallback_built"]), s_prepass=dt,
+                        clusters_local=[int(len(own[s][0])) for s in mine],
+                        exchange_calls=[c[0] for c in ex.calls])
+            per_rank.append(info)
+            log(f"C5 rank {r}: {len(mine)} slices, rows {rows.min()}..{rows.max()} (sum {rows.sum()}), "
+                f"R {info['R_bytes'] / 1e9:.1f} GB, R build {info['ms_rbuild']:.0f} ms, "
+                f"refine {info['ms_refine_kernel']:.0f} ms ({info['refine_entries'] / 1e9:.1f}e9 entries), "
+                f"prepass {dt:.1f} s")
+            if r == 0:
+                p2s = it.slices()
+                vrls = it.vrls()
+            if check is not None:
+                check(r, it, info, mine)
+        finally:
+            it.close()
+    t2 = time.time()
+    # phase 3: merge and install
+    slice_off = np.zeros(ns + 1, np.uint32)
+    for s in range(ns):
+        slice_off[s + 1] = slice_off[s] + len(own[s][0])
+    reps = np.concatenate([own[s][0] for s in range(ns)]).astype(np.uint32)
+    weights = np.concatenate([own[s][1] for s in range(ns)]).astype(np.float32)
+    path = os.path.join(workdir, f"c5_cluster_info_{os.getpid()}.bin")
+    alvrl.write_cluster_info(path, dict(slices=p2s, slice_off=slice_off, reps=reps, weights=weights))
+    it = alvrl.Integrator(P, device=0)
+    try:
+        it.preprocess(scene)
+        it.load_cluster_info(path, pass_)
+    except Exception:
+        it.close()
+        raise
+    finally:
+        os.unlink(path)
+    info = dict(slices=ns, per_rank=per_rank, p2s=p2s, vrls=vrls, slice_off=slice_off, reps=reps,
+                weights=weights, s_phase1=t1 - t_start, s_phase2=t2 - t1,
+                refine_ms_per_rank=[x["ms_refine_kernel"] for x in per_rank],
+                rbuild_ms_per_rank=[x["ms_rbuild"] for x in per_rank])
+    return it, info
+
+
 def run_share(props: str = "", nvrl: int = C5_VRLS, width: int = C5_W, height: int = C5_H,
               world: int = C5_WORLD, pass_: int = 0, gpu_tracer: bool = True, log=print):
-    """Rank 0's prepass of the C5 pass: returns (integrator, info dict)."""
+    """Rank 0's prepass of the C5 pass alone, the other ranks' masks zero (round
+    3's timing form): returns (integrator, info dict, rank 0's slices)."""
     import alvrl
     t0 = time.time()
     scene = alvrl.scene_default(width, height)
-    it = alvrl.Integrator(f"vrlTargetNum={nvrl};gpuTracer={'true' if gpu_tracer else 'false'};"
-                          f"seed={SEED_RNG};vrlSeed={SEED_VRL}" + (";" + props if props else ""), device=0)
+    it = alvrl.Integrator(_props(nvrl, gpu_tracer, props), device=0)
     it.preprocess(scene)
     t1 = time.time()
     ns = it.num_slices()
-    # the VRL count of the pass is known only after tracing; the mask stub
-    # only needs the byte count it is handed, so nvrl is informational
-    ex = StubExchange(world, ns, nvrl)
+    ex = SimExchange(0, world, ns, masks="zero")
     it.prepass(pass_, rank=0, world=world, exchange=ex)
     t2 = time.time()
     st = it.stats()

@@ -1,0 +1,2 @@
+/* mock: see mitsuba/mock.h */
+#include <mitsuba/mock.h>

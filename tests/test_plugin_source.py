@@ -24,3 +24,33 @@ def test_plugin_uses_declared_exports():
     types = set(re.findall(r"\b(alvrl_[a-z_]+)\b(?=\s*[\*&\s]\s*\w)", src)) - calls
     for t in types:
         assert re.search(r"\}\s*%s\s*;|typedef struct %s\b" % (t, t), headers), f"type {t} not declared"
+
+
+def test_plugin_compiles_against_mitsuba_declarations(tmp_path):
+    """The plugin compiles against a mock of exactly the Mitsuba declarations
+    it uses (tests/mitsuba_mock/: signatures as in the mitsuba-ALVRL headers,
+    MTS_IMPLEMENT_CLASS_S and MTS_EXPORT_PLUGIN as in class.h:219-226 and
+    cobject.h:99-107).  A missing unserialization constructor, an abstract
+    class, a call that does not match Mitsuba's API or an override that
+    hides a base virtual with another signature (-Werror=overloaded-virtual)
+    fails here.  The object must define the plugin entry points and the
+    unserializers of the integrator and its two resources."""
+    import shutil
+    import subprocess
+    gxx = shutil.which("g++")
+    hip = pathlib.Path("/opt/rocm/include/hip/hip_runtime_api.h")
+    if not gxx or not hip.exists():
+        import pytest
+        pytest.skip("needs g++ and the HIP headers")
+    mock = ROOT / "tests" / "mitsuba_mock"
+    obj = tmp_path / "vrl_plugin.o"
+    cmd = [gxx, "-std=c++11", "-c", "-fPIC", "-Wall", "-Wextra", "-Wno-unused-parameter", "-Werror",
+           "-Werror=overloaded-virtual", "-D__HIP_PLATFORM_AMD__", f"-I{mock / 'include'}", f"-I{mock / 'vrl'}",
+           f"-I{ROOT / 'include'}", "-I/opt/rocm/include", str(ROOT / "mitsuba_plugin" / "vrlAmdIntegrator.cpp"),
+           "-o", str(obj)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-4000:]
+    syms = subprocess.run(["nm", "-C", str(obj)], capture_output=True, text=True).stdout
+    for s in ("T CreateInstance", "T GetDescription", "__vrlAmdIntegrator_unSer", "__AmdVrlSet_unSer",
+              "__AmdClusterInfo_unSer"):
+        assert s in syms, s

@@ -5,6 +5,7 @@ oracle runs, so a long check is not taken for a hang).
 
   python tools/c5_share.py [--oracle] [--json out.json] [--props "..."]
   python tools/c5_share.py --res 1024 --vrls 100000 --world 8   # C4's rank-0 share at N = 8
+  python tools/c5_share.py --full [--res 256 --vrls 10000]        # every rank in turn + the tile render
 """
 import argparse
 import json
@@ -34,7 +35,10 @@ def main():
     ap.add_argument("--res", type=int, default=c5_share.C5_W, help="image width = height")
     ap.add_argument("--world", type=int, default=c5_share.C5_WORLD)
     ap.add_argument("--passes", type=int, default=1, help="prepasses run (timings of the last)")
+    ap.add_argument("--full", action="store_true", help="all ranks, true mask OR, merged lists, tile render")
     a = ap.parse_args()
+    if a.full:
+        return full(a)
     for p in range(a.passes):
         it, info, mine = c5_share.run_share(a.props, nvrl=a.vrls, width=a.res, height=a.res, world=a.world,
                                             pass_=p, log=lambda s: print(s, flush=True))
@@ -81,6 +85,35 @@ def main():
         with open(a.json, "w") as f:
             json.dump(info, f, indent=1)
     it.close()
+
+
+def full(a):
+    import torch
+    t0 = time.time()
+    it, info = c5_share.run_full(a.props, nvrl=a.vrls, width=a.res, height=a.res, world=a.world,
+                                 log=lambda s: print(s, flush=True))
+    W = H = a.res
+    total = torch.zeros(W * H * 3, dtype=torch.float32, device="cuda")
+    for r in range(a.world):
+        fb = torch.zeros_like(total)
+        it.render(fb, rank=r, world=a.world, stream=torch.cuda.current_stream().cuda_stream)
+        total += fb
+    one = torch.zeros_like(total)
+    it.render(one)
+    torch.cuda.synchronize()
+    same = bool(torch.equal(total, one))
+    st = it.stats()
+    out = {k: v for k, v in info.items() if k not in ("p2s", "vrls", "slice_off", "reps", "weights")}
+    out.update(tiles_equal_world1=same, render_kernel_ms=st["ms_render_kernel"], s_total=time.time() - t0,
+               clusters_total=int(info["slice_off"][-1]))
+    print(json.dumps(dict(refine_ms_per_rank=out["refine_ms_per_rank"], tiles_equal_world1=same,
+                          render_kernel_ms=out["render_kernel_ms"], s_total=out["s_total"])), flush=True)
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump(out, f, indent=1)
+    it.close()
+    if not same:
+        sys.exit(1)
 
 
 if __name__ == "__main__":
