@@ -49,16 +49,20 @@ typedef struct {
      *   NULL     index-matched interface (null.cpp:38-76): light passes through
      *            unchanged; transparent to Scene::evalTransmittance
      *            (scene.cpp:633-676), skipped by buildSlices (Preprocessor.cpp:
-     *            1157-1169), it cuts VRLs (vrlTracer.h:173-213). */
+     *            1157-1169), it cuts VRLs (vrlTracer.h:173-213);
+     *   DIELECTRIC  smooth dielectric interface with m_eta = occluder_eta
+     *            (dielectric.cpp, specular reflectance and transmittance 1): a
+     *            delta BSDF with two components, so LiInternal's chains branch
+     *            into reflection and transmission (bRec.component = i, :467-511);
+     *            particles reflect with probability F, else refract
+     *            (dielectric.cpp:335-364); blocks shadow segments. */
     const uint32_t *occluder_material;
     float occluder_specular[3];
+    float occluder_eta;   /* intIOR / extIOR of DIELECTRIC triangles (<= 0: bk7 / air, ior.h:43, 60) */
 } alvrl_scene_desc;
 #define ALVRL_MAT_DIFFUSE 0u
 #define ALVRL_MAT_MIRROR 1u
 #define ALVRL_MAT_NULL 2u
-/* smooth dielectric interface (dielectric.cpp): a delta BSDF with a reflection
- * and a transmission component; blocks shadow segments like any non-null
- * surface.  Host-cast scenes (alvrl_scene_ext) only. */
 #define ALVRL_MAT_DIELECTRIC 3u
 
 /* The benchmark scene of BASELINE.md ("homogeneous smoke box"). */

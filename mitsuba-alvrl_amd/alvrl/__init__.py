@@ -368,7 +368,7 @@ class SceneDesc(C.Structure):
                 ("light_pos", C.c_float * 3), ("light_intensity", C.c_float * 3),
                 ("medium", MediumDesc), ("occluders", C.POINTER(C.c_float)), ("n_occluders", C.c_uint32),
                 ("occluder_albedo", C.c_float * 3), ("occluder_material", C.POINTER(C.c_uint32)),
-                ("occluder_specular", C.c_float * 3)]
+                ("occluder_specular", C.c_float * 3), ("occluder_eta", C.c_float)]
 
 
 MAT_DIFFUSE, MAT_MIRROR, MAT_NULL, MAT_DIELECTRIC = 0, 1, 2, 3
@@ -570,11 +570,14 @@ def scene_default(width: int, height: int) -> SceneDesc:
 
 
 def scene_set_occluders(scene: SceneDesc, tris, albedo=(0.5, 0.5, 0.5), material=None,
-                        specular=(1.0, 1.0, 1.0)) -> SceneDesc:
+                        specular=(1.0, 1.0, 1.0), eta=None) -> SceneDesc:
     """Occluder triangles inside the box (alvrl_scene_desc.occluders): an
     (n, 9) float array of (p0, p1, p2), face normal cross(p1 - p0, p2 - p0);
     material: None (all diffuse) or one MAT_* per triangle; specular: the
-    mirrors' reflectance.  The arrays are kept alive on the descriptor."""
+    mirrors' reflectance; eta: the dielectrics' intIOR / extIOR (None: the
+    default bk7 / air).  The arrays are kept alive on the descriptor."""
+    if eta is not None:
+        scene.occluder_eta = float(eta)
     arr = np.ascontiguousarray(np.asarray(tris, np.float32).reshape(-1, 9))
     scene._occ_keep = arr
     scene.occluders = arr.ctypes.data_as(C.POINTER(C.c_float)) if len(arr) else None

@@ -35,7 +35,7 @@ const char* scene_problem(const alvrl_scene_desc& s)
     if (s.n_occluders && !s.occluders) return "alvrl_scene_desc: n_occluders > 0 without occluders";
     if (s.occluders && s.occluder_material)
         for (uint32_t i = 0; i < s.n_occluders; i++)
-            if (s.occluder_material[i] > ALVRL_MAT_NULL) return "alvrl_scene_desc: unknown occluder material";
+            if (s.occluder_material[i] > ALVRL_MAT_DIELECTRIC) return "alvrl_scene_desc: unknown occluder material";
     return nullptr;
 }
 SmokeBox to_box(const alvrl_scene_desc& s)
@@ -58,6 +58,7 @@ SmokeBox to_box(const alvrl_scene_desc& s)
     if (s.occluders && s.n_occluders && s.occluder_material)
         b.occ_mat.assign(s.occluder_material, s.occluder_material + s.n_occluders);
     for (int i = 0; i < 3; i++) b.occ_spec[i] = s.occluder_specular[i];
+    if (s.occluder_eta > 0) b.occ_eta = s.occluder_eta;
     return b;
 }
 }  // namespace host
@@ -94,6 +95,7 @@ ALVRL_API void alvrl_scene_default(alvrl_scene_desc* s, int width, int height)
     for (int i = 0; i < 3; i++) s->occluder_albedo[i] = b.occ_albedo[i];
     s->occluder_material = nullptr;
     for (int i = 0; i < 3; i++) s->occluder_specular[i] = b.occ_spec[i];
+    s->occluder_eta = b.occ_eta;
 }
 
 ALVRL_API int alvrl_scene_records(const alvrl_scene_desc* s, int medium_scatters, const uint32_t* ids,

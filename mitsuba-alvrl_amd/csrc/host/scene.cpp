@@ -169,6 +169,26 @@ float SmokeBox::box_hit(V3 o, V3 d, V3* n) const
     return best;
 }
 
+float fresnel_dielectric_ext(float cos_theta_i, float* cos_theta_t, float eta)
+{
+    if (eta == 1) {
+        *cos_theta_t = -cos_theta_i;
+        return 0.0f;
+    }
+    const float scale = (cos_theta_i > 0) ? 1 / eta : eta;
+    const float cos_t_sqr = 1 - (1 - cos_theta_i * cos_theta_i) * (scale * scale);
+    if (cos_t_sqr <= 0.0f) {   // total internal reflection
+        *cos_theta_t = 0.0f;
+        return 1.0f;
+    }
+    const float ci = std::fabs(cos_theta_i);
+    const float ct = std::sqrt(cos_t_sqr);
+    const float Rs = (ci - eta * ct) / (ci + eta * ct);
+    const float Rp = (eta * ci - ct) / (eta * ci + ct);
+    *cos_theta_t = (cos_theta_i > 0) ? -ct : ct;
+    return 0.5f * (Rs * Rs + Rp * Rp);
+}
+
 bool tri_intersect(const float* tri, V3 o, V3 d, float* u, float* v, float* t)
 {
     const V3 p0 = v3(tri[0], tri[1], tri[2]), p1 = v3(tri[3], tri[4], tri[5]), p2 = v3(tri[6], tri[7], tri[8]);
@@ -418,7 +438,7 @@ void trace_particle(const SmokeBox& sc, Stream& smp, bool short_vrls, int max_de
     for (int i = 0; i < 3; i++) k.power[i] = power[i];
     int depth = 1;
     float thr[3] = {1.0f, 1.0f, 1.0f};
-    const float eta = 1.0f;
+    float eta = 1.0f;
     float mint = 1e-4f;   // Ray() default mint (Epsilon), then 0 after a medium and Epsilon after a surface
     while (!(thr[0] == 0 && thr[1] == 0 && thr[2] == 0) && (depth <= max_depth || max_depth < 0)) {
         V3 n, hp;
@@ -480,6 +500,18 @@ void trace_particle(const SmokeBox& sc, Stream& smp, bool short_vrls, int max_de
                     wol = v3(-dot(mwi, fs), -dot(mwi, ft), cos_wi);   // reflect(wi)
                     for (int i = 0; i < 3; i++) bw[i] = sc.occ_spec[i];
                 }
+            } else if (mt == 3u) {   // SmoothDielectric::sample, both components, EImportance (dielectric.cpp:335-364)
+                float cos_t;
+                const float F = fresnel_dielectric_ext(cos_wi, &cos_t, sc.occ_eta);
+                if (bx <= F) {
+                    wol = v3(-dot(mwi, fs), -dot(mwi, ft), cos_wi);
+                } else {
+                    const float inv_eta = 1 / sc.occ_eta;
+                    const float scale = -(cos_t < 0 ? inv_eta : sc.occ_eta);   // refract(wi, cosThetaT)
+                    wol = v3(scale * dot(mwi, fs), scale * dot(mwi, ft), cos_t);
+                    eta *= cos_t < 0 ? sc.occ_eta : inv_eta;                   // bRec.eta
+                }
+                bw[0] = bw[1] = bw[2] = 1.0f;                                 // importance: factor 1
             } else {                 // Null::sample (null.cpp:53-63): wo = -wi
                 wol = v3(-dot(mwi, fs), -dot(mwi, ft), -cos_wi);
                 bw[0] = bw[1] = bw[2] = 1.0f;
@@ -531,71 +563,99 @@ void SmokeBox::make_chain(int x, int y, bool medium_scatters, uint32_t seed, uin
     pixel_sample(x, y, seed, pass, sample, spp, &px, &py);
     camera_ray(px, py, &O, &D, &mint);   // the sensor sample (integrator.cpp:240-247)
     const uint32_t pixel = (uint32_t)y * (uint32_t)width + (uint32_t)x;
-    float weight[3] = {1.0f, 1.0f, 1.0f};
-    float thr[3] = {init_throughput, init_throughput, init_throughput};   // throughputWithEtaSq (:381)
-    int depth = 1;                                                        // rRec.depth of the sensor ray
-    for (uint32_t k = 0; k < 256; k++) {
-        V3 n, p;
-        int tri;
-        const float t = first_hit(O, D, mint, &n, &p, &tri);
-        if (!std::isfinite(t)) break;                                     // :414-419
-        const uint32_t m = mat(tri);
-        uint32_t flags = 1u | (m == 0u ? 2u : 8u) | (medium_scatters ? 4u : 0u);
-        const float* a = tri >= 0 ? occ_albedo : albedo;
-        const size_t o = out->size();
-        out->resize(o + kRecWords);
-        float* rec = out->data() + o;
-        rec[0] = O.x; rec[1] = O.y; rec[2] = O.z;
-        rec[3] = D.x; rec[4] = D.y; rec[5] = D.z;
-        rec[6] = p.x; rec[7] = p.y; rec[8] = p.z;
-        rec[9] = n.x; rec[10] = n.y; rec[11] = n.z;
-        for (int i = 0; i < 3; i++) rec[12 + i] = m == 0u ? a[i] : 0.0f;
-        std::memcpy(&rec[15], &flags, 4);
-        for (int i = 0; i < 3; i++) rec[16 + i] = weight[i];
-        const uint32_t kw = k | (sample << 16);
-        std::memcpy(&rec[19], &kw, 4);
-        if (m == 0u) break;                                               // no delta component (:449-450)
-        // transmittance of the segment, rRec.medium->eval(Ray(ray, 0, its.t)) (:452-458)
-        float tr[3];
-        for (int i = 0; i < 3; i++) tr[i] = fastexp(medium.sigma_t[i] * (-t));
-        {
-            float mx = tr[0] > tr[1] ? tr[0] : tr[1];
-            mx = mx > tr[2] ? mx : tr[2];
-            if (mx < 1e-20f) tr[0] = tr[1] = tr[2] = 0;
-        }
-        if (tr[0] == 0 && tr[1] == 0 && tr[2] == 0) break;               // :459-460
-        // the delta component, bsdf->sample(bRec, Point2(0.5f)) (:470-475)
-        V3 fs, ft;
-        frame_of(n, &fs, &ft);
-        const V3 mwi = -D;
-        const float cos_wi = dot(mwi, n);
+    const float weight[3] = {1.0f, 1.0f, 1.0f};
+    const float thr[3] = {init_throughput, init_throughput, init_throughput};   // throughputWithEtaSq (:381)
+    uint32_t k = 0;
+    chain_node(O, D, mint, weight, thr, 1, pixel, sample, medium_scatters, seed, pass, spec_rr_depth, out, &k);
+}
+
+// One LiInternal call (:398-524): the record of the ray's hit, then each
+// delta component's continuation.  depth: rRec.depth (1 for the sensor ray).
+void SmokeBox::chain_node(V3 O, V3 D, float mint, const float weight[3], const float thr[3], int depth,
+                          uint32_t pixel, uint32_t sample, bool medium_scatters, uint32_t seed, uint32_t pass,
+                          int spec_rr_depth, std::vector<float>* out, uint32_t* k) const
+{
+    if (*k >= 256) return;
+    V3 n, p;
+    int tri;
+    const float t = first_hit(O, D, mint, &n, &p, &tri);
+    if (!std::isfinite(t)) return;                                        // :414-419
+    const uint32_t m = mat(tri);
+    const uint32_t flags = 1u | (m == 0u ? 2u : 8u) | (medium_scatters ? 4u : 0u);
+    const float* a = tri >= 0 ? occ_albedo : albedo;
+    const size_t o = out->size();
+    out->resize(o + kRecWords);
+    float* rec = out->data() + o;
+    rec[0] = O.x; rec[1] = O.y; rec[2] = O.z;
+    rec[3] = D.x; rec[4] = D.y; rec[5] = D.z;
+    rec[6] = p.x; rec[7] = p.y; rec[8] = p.z;
+    rec[9] = n.x; rec[10] = n.y; rec[11] = n.z;
+    for (int i = 0; i < 3; i++) rec[12 + i] = m == 0u ? a[i] : 0.0f;
+    std::memcpy(&rec[15], &flags, 4);
+    for (int i = 0; i < 3; i++) rec[16 + i] = weight[i];
+    const uint32_t kw = *k | (sample << 16);
+    std::memcpy(&rec[19], &kw, 4);
+    ++*k;
+    if (m == 0u) return;                                                  // no delta component (:447-448)
+    // transmittance of the segment, rRec.medium->eval(Ray(ray, 0, its.t)) (:450-460)
+    float tr[3];
+    for (int i = 0; i < 3; i++) tr[i] = fastexp(medium.sigma_t[i] * (-t));
+    {
+        float mx = tr[0] > tr[1] ? tr[0] : tr[1];
+        mx = mx > tr[2] ? mx : tr[2];
+        if (mx < 1e-20f) tr[0] = tr[1] = tr[2] = 0;
+    }
+    if (tr[0] == 0 && tr[1] == 0 && tr[2] == 0) return;
+    V3 fs, ft;
+    frame_of(n, &fs, &ft);
+    const V3 mwi = -D;
+    const float cos_wi = dot(mwi, n);
+    Stream smp{seed, pass, kDomEye, pixel, kw, 0u};
+    const int ncomp = m == 3u ? 2 : 1;
+    for (int c = 0; c < ncomp; c++) {   // the delta components (:467-511), bsdf->sample(bRec, Point2(0.5f))
         float bw[3];
+        float beta = 1.0f;              // bRec.eta
         V3 wol;
-        if (m == 1u) {   // conductor.cpp:254-268
-            if (cos_wi <= 0) break;
+        if (m == 1u) {                  // conductor.cpp:254-268
+            if (cos_wi <= 0) continue;
             wol = v3(-dot(mwi, fs), -dot(mwi, ft), cos_wi);
             for (int i = 0; i < 3; i++) bw[i] = occ_spec[i];
-        } else {         // null.cpp:53-63
+        } else if (m == 2u) {           // null.cpp:53-63
             wol = v3(-dot(mwi, fs), -dot(mwi, ft), -cos_wi);
             bw[0] = bw[1] = bw[2] = 1.0f;
+        } else {                        // dielectric.cpp:365-385, one component, ERadiance
+            float cos_t;
+            const float F = fresnel_dielectric_ext(cos_wi, &cos_t, occ_eta);
+            const float inv_eta = 1 / occ_eta;
+            if (c == 0) {
+                wol = v3(-dot(mwi, fs), -dot(mwi, ft), cos_wi);
+                bw[0] = bw[1] = bw[2] = F;
+            } else {
+                const float scale = -(cos_t < 0 ? inv_eta : occ_eta);
+                wol = v3(scale * dot(mwi, fs), scale * dot(mwi, ft), cos_t);
+                beta = cos_t < 0 ? occ_eta : inv_eta;
+                const float factor = cos_t < 0 ? inv_eta : occ_eta;
+                bw[0] = bw[1] = bw[2] = factor * factor * (1 - F);
+            }
+            if (bw[0] == 0) continue;
         }
-        // Russian roulette (:477-492): eta = 1 for both BSDFs
+        // Russian roulette (:480-492)
         float thr2[3];
-        for (int i = 0; i < 3; i++) thr2[i] = ((thr[i] * tr[i]) * bw[i]) * 1.0f;
+        for (int i = 0; i < 3; i++) thr2[i] = ((thr[i] * tr[i]) * bw[i]) * (beta * beta);
         const float maxRR = depth >= spec_rr_depth ? 0.98f : 1.0f;
         float mx = thr2[0] > thr2[1] ? thr2[0] : thr2[1];
         mx = mx > thr2[2] ? mx : thr2[2];
         const float rrProb = maxRR < mx ? maxRR : mx;
-        Stream smp{seed, pass, kDomEye, pixel, k | (sample << 16), 0u};
-        if (rrProb <= 0 || (rrProb < 1 && smp.next() > rrProb)) break;
+        if (rrProb <= 0 || (rrProb < 1 && smp.next() > rrProb)) continue;
+        float thr_c[3], w_c[3];
         for (int i = 0; i < 3; i++) {
-            thr[i] = thr2[i] / rrProb;
-            weight[i] = ((weight[i] * tr[i]) * bw[i]) / rrProb;             // weight * transmittance * bsdfWeight / rrProb (:503-510)
+            thr_c[i] = thr2[i] / rrProb;
+            w_c[i] = ((weight[i] * tr[i]) * bw[i]) / rrProb;                  // weight * transmittance * bsdfWeight / rrProb (:505)
         }
-        O = p;
-        D = (fs * wol.x + ft * wol.y) + n * wol.z;                            // its.toWorld(bRec.wo)
-        mint = 1e-4f;                                                         // RayDifferential(its.p, wo): mint = Epsilon
-        depth++;
+        const V3 D2 = (fs * wol.x + ft * wol.y) + n * wol.z;                 // its.toWorld(bRec.wo)
+        // RayDifferential(its.p, wo): mint = Epsilon
+        chain_node(p, D2, 1e-4f, w_c, thr_c, depth + 1, pixel, sample, medium_scatters, seed, pass, spec_rr_depth,
+                   out, k);
     }
 }
 

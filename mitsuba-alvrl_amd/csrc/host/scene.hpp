@@ -78,7 +78,9 @@ struct SmokeBox {
     float occ_albedo[3] = {0.5f, 0.5f, 0.5f};
     std::vector<uint32_t> occ_mat;    // per triangle ALVRL_MAT_* (empty: all diffuse)
     float occ_spec[3] = {1.0f, 1.0f, 1.0f};
-    // the BSDF of a hit: 0 diffuse (walls: tri < 0), 1 mirror, 2 null
+    // dielectric triangles: m_eta = intIOR / extIOR (dielectric.cpp:149-158; bk7 / air, ior.h:43, 60)
+    float occ_eta = 1.5046f / 1.000277f;
+    // the BSDF of a hit: 0 diffuse (walls: tri < 0), 1 mirror, 2 null, 3 dielectric
     uint32_t mat(int tri) const { return (tri < 0 || occ_mat.empty()) ? 0u : occ_mat[(size_t)tri]; }
     bool has_delta() const
     {
@@ -101,12 +103,16 @@ struct SmokeBox {
     bool visible(V3 p1, bool p1_surface, V3 p2, bool p2_surface) const;
     // The eye path of pixel centre (x, y) through delta BSDFs: LiInternal's
     // recursion (vrlIntegrator.cpp:386-524) as gather records, one per
-    // segment, each with the weight the recursion passes down (:503-510) and
-    // its depth; Russian roulette from initialSpecularThroughput, maxRR 0.98
-    // past specularForcedRRdepth (:475-492), its uniform from the stream
-    // (seed, pass, dom 7, pixel, depth).  Appends kRecWords floats per record.
-    // sample, spp: sensor sample j of spp (pixel_sample); record k's depth
-    // word is k | (j << 16) and its roulette draws from (pixel, k | (j << 16)).
+    // segment, each with the weight the recursion passes down (:503-510).
+    // A delta BSDF's every delta component is followed (bRec.component = i,
+    // :467-511): a dielectric branches into reflection and transmission, so
+    // the records form a tree, emitted depth first (component 0's subtree
+    // before component 1's).  Record k (pre-order index, = its depth on a
+    // path without branches) has depth word k | (j << 16) for sensor sample j
+    // of spp (pixel_sample); the Russian roulette of its components (from
+    // initialSpecularThroughput, maxRR 0.98 past specularForcedRRdepth,
+    // :475-492) draws in component order from the stream (seed, pass, dom 7,
+    // pixel, k | (j << 16)).  Appends kRecWords floats per record (<= 256).
     void make_chain(int x, int y, bool medium_scatters, uint32_t seed, uint32_t pass, int spec_rr_depth,
                     float init_throughput, std::vector<float>* out, uint32_t sample = 0, uint32_t spp = 1) const;
     // buildSlices' gather point of pixel (x, y) (Preprocessor.cpp:1144-1170):
@@ -125,7 +131,16 @@ struct SmokeBox {
     void make_record(int x, int y, bool medium_scatters, float rec[kRecWords], uint32_t seed = 0,
                      uint32_t pass = 0, uint32_t sample = 0, uint32_t spp = 1) const;
     float scene_diagonal() const;   // distance(getAABB().min, getAABB().max)
+
+private:
+    void chain_node(V3 O, V3 D, float mint, const float weight[3], const float thr[3], int depth, uint32_t pixel,
+                    uint32_t sample, bool medium_scatters, uint32_t seed, uint32_t pass, int spec_rr_depth,
+                    std::vector<float>* out, uint32_t* k) const;
 };
+
+// fresnelDielectricExt (src/libcore/util.cpp:651-681): unpolarized Fresnel
+// reflectance and the signed cosine of the transmitted direction.
+float fresnel_dielectric_ext(float cos_theta_i, float* cos_theta_t, float eta);
 
 // TriangleT::rayIntersect (triangle.h:109-145): t of the hit, or false.
 bool tri_intersect(const float* tri, V3 o, V3 d, float* u, float* v, float* t);

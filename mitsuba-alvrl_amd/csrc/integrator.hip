@@ -1069,6 +1069,17 @@ struct alvrl_integrator {
         for (uint32_t d = 0; d < levels; d++)
             chk(alvrl_accumulate_rgb(ctx, out_buf.p + (size_t)3 * level_rec[d], pix_buf.p + level_rec[d],
                                      level_rec[d + 1] - level_rec[d], d_fb, s), "alvrl_accumulate_rgb");
+        if (s != stream) {
+            // the launches above read rec_buf / pix_buf / out_buf on the
+            // caller's stream; the next prepare_render rewrites them on the
+            // integrator's own stream, which therefore waits for them
+            hipEvent_t ev = nullptr;
+            hchk(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
+            hipError_t e = hipEventRecord(ev, s);
+            if (e == hipSuccess) e = hipStreamWaitEvent(stream, ev, 0);
+            (void)hipEventDestroy(ev);
+            hchk(e, "order the integrator's stream after the render");
+        }
     }
 };
 

@@ -456,6 +456,24 @@ __device__ float det_std_normal_x(float sx, float sy)
     return (float)(det_cos(phi) * r);
 }
 
+// LDS-pool bounds checks (build with -DALVRL_LDS_CHECK, tools/build_variant.sh):
+// an index past the pool is counted in g_lds_viol, reported once with printf,
+// and the access is skipped (a typed ds_* access past the allocation would be
+// dropped or read 0 silently; a flat one faults).  alvrl_refine fails with
+// ALVRL_ERR_NUMERIC when any was seen.  Off in the product build.
+#ifdef ALVRL_LDS_CHECK
+__device__ unsigned int g_lds_viol;
+#define LDS_OK(cond, what, a, b)                                                                          \
+    ((cond) ? true                                                                                       \
+            : ((atomicAdd(&g_lds_viol, 1u) == 0u                                                         \
+                    ? (void)printf("ALVRL_LDS_CHECK %s: %ld %ld (block %d thread %d)\n", what, (long)(a),  \
+                                   (long)(b), (int)blockIdx.x, (int)threadIdx.x)                         \
+                    : (void)0),                                                                          \
+               false))
+#else
+#define LDS_OK(cond, what, a, b) true
+#endif
+
 // ------------------------------------------------------------- heap --
 __device__ __forceinline__ bool cless(const CNode& a, const CNode& b)
 {
@@ -469,6 +487,7 @@ __device__ __forceinline__ bool cless(const CNode& a, const CNode& b)
 // accesses to LDS faulted on this platform (memory aperture violation).
 // Every write is logged so a snapshot copies only what changed.
 typedef uint32_t hnode_v __attribute__((ext_vector_type(4)));
+constexpr int kHeapLdsMax = (int)(kPoolBytes / sizeof(hnode_v));
 typedef __attribute__((address_space(1))) hnode_v* hnode_p;
 typedef __attribute__((address_space(3))) hnode_v* hnode_l;
 __device__ __forceinline__ hnode_p hnodes(CNode* p) { return (hnode_p)p; }
@@ -478,13 +497,19 @@ struct HeapRef {
     int lds;
     __device__ __forceinline__ hnode_v ld(long i) const
     {
-        if (lds) return l[i];
+        if (lds) {
+            if (!LDS_OK(i >= 0 && i < kHeapLdsMax, "heap load", i, kHeapLdsMax)) return hnode_v{0u, 0u, 0u, 0u};
+            return l[i];
+        }
         return g[i];
     }
     __device__ __forceinline__ void st(long i, hnode_v v) const
     {
-        if (lds) l[i] = v;
-        else g[i] = v;
+        if (lds) {
+            if (LDS_OK(i >= 0 && i < kHeapLdsMax, "heap store", i, kHeapLdsMax)) l[i] = v;
+        } else {
+            g[i] = v;
+        }
     }
 };
 __device__ __forceinline__ CNode hld(hnode_p H, long i)
@@ -501,7 +526,6 @@ __device__ __forceinline__ void hst(const HeapRef& H, long i, const CNode& c)
 {
     H.st(i, hnode_v{__float_as_uint(c.uvar), __float_as_uint(c.ivar), c.begin, c.end});
 }
-constexpr int kHeapLdsMax = (int)(kPoolBytes / sizeof(hnode_v));
 __device__ __forceinline__ void heap_log(Ctl& C, long i)
 {
     if (C.hlog_n < kHeapLog) C.hlog[C.hlog_n++] = (uint32_t)i;
@@ -727,6 +751,7 @@ __device__ void heap_move(const JobDev& J, Ctl& C, bool to_lds)
     if (to_lds ? (cur || n + 2 > kHeapLdsMax) : !cur) return;   // uniform
     const hnode_p G = hnodes(J.heap);
     const hnode_l L = lp(reinterpret_cast<hnode_v*>(C.hpool));
+    if (!LDS_OK(n <= kHeapLdsMax, "heap_move", n, kHeapLdsMax)) return;
     for (int i = threadIdx.x; i < n; i += kThreads) {
         if (to_lds) L[i] = G[i];
         else G[i] = L[i];
@@ -1661,6 +1686,7 @@ __device__ __noinline__ void variance_split_small(const JobDev& J, const Common&
     const int tid = threadIdx.x, wv = tid >> 6;
     const uint32_t lane = (uint32_t)(tid & 63);
     const int g = wv >> 2;                              // 0: forward, 1: reverse
+    if (!LDS_OK(m <= kSmallMax && NB <= kSmallBlocks, "small split size", m, NB)) return;
     const uint32_t blk = (uint32_t)(wv & 3);
     auto* const coef = lp(reinterpret_cast<double*>(pool));                          // [g][7][kSmallMax]
     auto* const vr = lp(reinterpret_cast<uint32_t*>(pool + kSmallCoefBytes));        // [g][kSmallMax]
@@ -1834,6 +1860,7 @@ __device__ __forceinline__ void bitonic_lds(lds_u64* lds, const glb_u64* in, glb
     const int tid = threadIdx.x;
     uint32_t n2 = 1;
     while (n2 < n) n2 <<= 1;
+    if (!LDS_OK(n2 <= (uint32_t)kBitonicMax, "bitonic keys", n2, kBitonicMax)) return;
     for (uint32_t i = tid; i < n2; i += kThreads) lds[i] = i < n ? in[i] : ~0ull;
     __syncthreads();
     for (uint32_t k = 2; k <= n2; k <<= 1) {
@@ -3856,6 +3883,18 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
             std::this_thread::sleep_for(std::chrono::milliseconds(200));
         }
     }
+#ifdef ALVRL_LDS_CHECK
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    unsigned int viol = 0;
+    if (e == hipSuccess) e = hipMemcpyFromSymbol(&viol, HIP_SYMBOL(g_lds_viol), sizeof(viol));
+    if (e == hipSuccess && viol) {
+        const unsigned int zero = 0;
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_lds_viol), &zero, sizeof(zero));
+        std::fprintf(stderr, "[refine] ALVRL_LDS_CHECK: %u LDS-pool bounds violations\n", viol);
+        *err = "alvrl_refine: LDS-pool bounds violation (ALVRL_LDS_CHECK)";
+        return 1;
+    }
+#endif
     // gather results: packed on the device, three copies
     std::vector<uint32_t> meta(3 * (size_t)njobs);
     unsigned long long h_entries[2] = {0, 0};

@@ -68,8 +68,13 @@ struct U4 { uint32_t x, y, z, w; };
 __device__ __forceinline__ U4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                                             uint32_t k0, uint32_t k1)
 {
+#ifdef ALVRL_EXP_RNG_ROUNDS   // timing-only experiment: fewer rounds (results differ from the oracle)
+    constexpr int kRounds = ALVRL_EXP_RNG_ROUNDS;
+#else
+    constexpr int kRounds = 10;
+#endif
 #pragma unroll
-    for (int r = 0; r < 10; ++r) {
+    for (int r = 0; r < kRounds; ++r) {
         if (r > 0) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
         // one 32x32->64 product per multiplier (v_mad_u64_u32) instead of a
         // v_mul_hi_u32 + v_mul_lo_u32 pair

@@ -798,6 +798,28 @@ void alvrl_o_scene_default(alvrl_o_scene *s, int width, int height)
         s->light_intensity[i] = 10.0f;
     }
     s->light_pos[0] = 0; s->light_pos[1] = 0.8f; s->light_pos[2] = 0;
+    s->occ_eta = 1.5046f / 1.000277f;   /* bk7 / air (ior.h:43, 60) */
+}
+
+/* fresnelDielectricExt (src/libcore/util.cpp:651-681) */
+static float fresnel_dielectric_ext(float cos_theta_i, float *cos_theta_t, float eta)
+{
+    if (eta == 1) {
+        *cos_theta_t = -cos_theta_i;
+        return 0.0f;
+    }
+    float scale = (cos_theta_i > 0) ? 1 / eta : eta;
+    float cos_t_sqr = 1 - (1 - cos_theta_i * cos_theta_i) * (scale * scale);
+    if (cos_t_sqr <= 0.0f) {
+        *cos_theta_t = 0.0f;
+        return 1.0f;
+    }
+    float ci = fabsf(cos_theta_i);
+    float ct = sqrtf(cos_t_sqr);
+    float Rs = (ci - eta * ct) / (ci + eta * ct);
+    float Rp = (eta * ci - ct) / (eta * ci + ct);
+    *cos_theta_t = (cos_theta_i > 0) ? -ct : ct;
+    return 0.5f * (Rs * Rs + Rp * Rp);
 }
 
 /* Perspective pinhole with Mitsuba's conventions (perspective.cpp:126-155,
@@ -986,6 +1008,101 @@ uint32_t alvrl_o_make_chain(const alvrl_o_scene *s, const alvrl_o_medium *m, int
                                 recs, cap);
 }
 
+/* One LiInternal call (:398-524): the record of the ray's hit, then each
+ * delta component's continuation, depth first.  depth: rRec.depth. */
+typedef struct {
+    const alvrl_o_scene *s;
+    const alvrl_o_medium *m;
+    int medium_scatters, spec_rr_depth;
+    uint32_t seed, pass, pixel, sample, cap, nrec;
+    float *recs;
+} chain_ctx;
+
+static void chain_node(chain_ctx *cx, v3 O, v3 D, float mint, const float weight[3], const float thr[3], int depth)
+{
+    const alvrl_o_scene *s = cx->s;
+    if (cx->nrec >= cx->cap || cx->nrec >= 256) return;
+    v3 n, p;
+    int tri;
+    float t = first_hit(s, O, D, mint, &n, &p, &tri);
+    if (!isfinite(t)) return;                                               /* :414-419 */
+    uint32_t mt = mat_of(s, tri);
+    uint32_t flags = ALVRL_O_FLAG_HIT | (mt == ALVRL_O_MAT_DIFFUSE ? ALVRL_O_FLAG_SMOOTH : ALVRL_O_FLAG_DELTA) |
+                     (cx->medium_scatters ? ALVRL_O_FLAG_MEDIUM : 0u);
+    const float *alb = tri >= 0 ? s->occ_albedo : s->albedo;
+    float *rec = cx->recs + (size_t)cx->nrec * ALVRL_O_REC_WORDS;
+    rec[0] = O.x; rec[1] = O.y; rec[2] = O.z;
+    rec[3] = D.x; rec[4] = D.y; rec[5] = D.z;
+    rec[6] = p.x; rec[7] = p.y; rec[8] = p.z;
+    rec[9] = n.x; rec[10] = n.y; rec[11] = n.z;
+    for (int i = 0; i < 3; i++) rec[12 + i] = mt == ALVRL_O_MAT_DIFFUSE ? alb[i] : 0.0f;
+    memcpy(&rec[15], &flags, 4);
+    for (int i = 0; i < 3; i++) rec[16 + i] = weight[i];
+    const uint32_t kw = cx->nrec | (cx->sample << 16);
+    memcpy(&rec[19], &kw, 4);
+    cx->nrec++;
+    if (mt == ALVRL_O_MAT_DIFFUSE) return;                                  /* no delta component (:447-448) */
+    /* rRec.medium->eval(Ray(ray, 0, its.t)) (:450-460) */
+    float tr[3];
+    for (int i = 0; i < 3; i++) tr[i] = fastexp(cx->m->sigma_t[i] * (-t));
+    {
+        float mx = tr[0] > tr[1] ? tr[0] : tr[1];
+        mx = mx > tr[2] ? mx : tr[2];
+        if (mx < 1e-20f) tr[0] = tr[1] = tr[2] = 0;
+    }
+    if (tr[0] == 0 && tr[1] == 0 && tr[2] == 0) return;
+    v3 fs, ft;
+    frame_of(n, &fs, &ft);
+    v3 mwi = neg(D);
+    float cos_wi = dot(mwi, n);
+    seq_sampler smp;
+    seq_init(&smp, cx->seed, cx->pass, 7u, cx->pixel, kw, 0u);
+    int ncomp = mt == ALVRL_O_MAT_DIELECTRIC ? 2 : 1;
+    for (int c = 0; c < ncomp; c++) {                                       /* :467-511 */
+        float bw[3];
+        float beta = 1.0f;                                                  /* bRec.eta */
+        v3 wol;
+        if (mt == ALVRL_O_MAT_MIRROR) {                                     /* conductor.cpp:254-268 */
+            if (cos_wi <= 0) continue;
+            wol = mk(-dot(mwi, fs), -dot(mwi, ft), cos_wi);
+            for (int i = 0; i < 3; i++) bw[i] = s->occ_spec[i];
+        } else if (mt == ALVRL_O_MAT_NULL) {                                /* null.cpp:53-63 */
+            wol = mk(-dot(mwi, fs), -dot(mwi, ft), -cos_wi);
+            bw[0] = bw[1] = bw[2] = 1.0f;
+        } else {                                                            /* dielectric.cpp:365-385, ERadiance */
+            float cos_t;
+            float F = fresnel_dielectric_ext(cos_wi, &cos_t, s->occ_eta);
+            float inv_eta = 1 / s->occ_eta;
+            if (c == 0) {
+                wol = mk(-dot(mwi, fs), -dot(mwi, ft), cos_wi);
+                bw[0] = bw[1] = bw[2] = F;
+            } else {
+                float scale = -(cos_t < 0 ? inv_eta : s->occ_eta);
+                wol = mk(scale * dot(mwi, fs), scale * dot(mwi, ft), cos_t);
+                beta = cos_t < 0 ? s->occ_eta : inv_eta;
+                float factor = cos_t < 0 ? inv_eta : s->occ_eta;
+                bw[0] = bw[1] = bw[2] = factor * factor * (1 - F);
+            }
+            if (bw[0] == 0) continue;
+        }
+        /* Russian roulette (:480-492) */
+        float thr2[3];
+        for (int i = 0; i < 3; i++) thr2[i] = ((thr[i] * tr[i]) * bw[i]) * (beta * beta);
+        float maxRR = depth >= cx->spec_rr_depth ? 0.98f : 1.0f;
+        float mx = thr2[0] > thr2[1] ? thr2[0] : thr2[1];
+        mx = mx > thr2[2] ? mx : thr2[2];
+        float rrProb = maxRR < mx ? maxRR : mx;
+        if (rrProb <= 0 || (rrProb < 1 && seq_next(&smp) > rrProb)) continue;
+        float thr_c[3], w_c[3];
+        for (int i = 0; i < 3; i++) {
+            thr_c[i] = thr2[i] / rrProb;
+            w_c[i] = ((weight[i] * tr[i]) * bw[i]) / rrProb;                 /* :505 */
+        }
+        v3 D2 = add(add(scl(fs, wol.x), scl(ft, wol.y)), scl(n, wol.z));    /* its.toWorld(bRec.wo) */
+        chain_node(cx, p, D2, 1e-4f, w_c, thr_c, depth + 1);
+    }
+}
+
 /* The eye path of sensor sample j of spp: record k's depth word is
  * k | (j << 16), and the Russian roulette draws from the (pixel, k | (j << 16))
  * stream (sample 0: the single-sample streams). */
@@ -996,75 +1113,14 @@ uint32_t alvrl_o_make_chain_s(const alvrl_o_scene *s, const alvrl_o_medium *m, i
     float o[3], d[3], px, py;
     alvrl_o_pixel_sample(seed, pass, x, y, s->width, sample, spp, &px, &py);
     alvrl_o_camera_ray(s, px, py, o, d);   /* the sensor sample (integrator.cpp:240-247) */
-    v3 O = ld3(o), D = ld3(d);
-    float mint = camera_mint(s, px, py);
-    uint32_t pixel = (uint32_t)y * (uint32_t)s->width + (uint32_t)x;
+    chain_ctx cx;
+    cx.s = s; cx.m = m; cx.medium_scatters = medium_scatters; cx.spec_rr_depth = spec_rr_depth;
+    cx.seed = seed; cx.pass = pass; cx.pixel = (uint32_t)y * (uint32_t)s->width + (uint32_t)x;
+    cx.sample = sample; cx.cap = cap; cx.nrec = 0; cx.recs = recs;
     float weight[3] = { 1.0f, 1.0f, 1.0f };
     float thr[3] = { init_throughput, init_throughput, init_throughput };   /* throughputWithEtaSq */
-    int depth = 1;                                                          /* rRec.depth of a sensor ray */
-    uint32_t nrec = 0;
-    for (uint32_t k = 0; k < 256 && nrec < cap; k++) {
-        v3 n, p;
-        int tri;
-        float t = first_hit(s, O, D, mint, &n, &p, &tri);
-        if (!isfinite(t)) break;                                            /* :414-419 */
-        uint32_t mt = mat_of(s, tri);
-        uint32_t flags = ALVRL_O_FLAG_HIT | (mt == ALVRL_O_MAT_DIFFUSE ? ALVRL_O_FLAG_SMOOTH : ALVRL_O_FLAG_DELTA) |
-                         (medium_scatters ? ALVRL_O_FLAG_MEDIUM : 0u);
-        const float *alb = tri >= 0 ? s->occ_albedo : s->albedo;
-        float *rec = recs + (size_t)nrec * ALVRL_O_REC_WORDS;
-        rec[0] = O.x; rec[1] = O.y; rec[2] = O.z;
-        rec[3] = D.x; rec[4] = D.y; rec[5] = D.z;
-        rec[6] = p.x; rec[7] = p.y; rec[8] = p.z;
-        rec[9] = n.x; rec[10] = n.y; rec[11] = n.z;
-        for (int i = 0; i < 3; i++) rec[12 + i] = mt == ALVRL_O_MAT_DIFFUSE ? alb[i] : 0.0f;
-        memcpy(&rec[15], &flags, 4);
-        for (int i = 0; i < 3; i++) rec[16 + i] = weight[i];
-        const uint32_t kw = k | (sample << 16);
-        memcpy(&rec[19], &kw, 4);
-        nrec++;
-        if (mt == ALVRL_O_MAT_DIFFUSE) break;                               /* no delta component (:449-450) */
-        /* rRec.medium->eval(Ray(ray, 0, its.t)) (:452-458) */
-        float tr[3];
-        for (int i = 0; i < 3; i++) tr[i] = fastexp(m->sigma_t[i] * (-t));
-        {
-            float mx = tr[0] > tr[1] ? tr[0] : tr[1];
-            mx = mx > tr[2] ? mx : tr[2];
-            if (mx < 1e-20f) tr[0] = tr[1] = tr[2] = 0;
-        }
-        if (tr[0] == 0 && tr[1] == 0 && tr[2] == 0) break;                  /* :459-460 */
-        v3 fs, ft;
-        frame_of(n, &fs, &ft);
-        v3 mwi = neg(D);
-        float cos_wi = dot(mwi, n);
-        float bw[3];
-        v3 wol;
-        if (mt == ALVRL_O_MAT_MIRROR) {                                     /* conductor.cpp:254-268 */
-            if (cos_wi <= 0) break;
-            wol = mk(-dot(mwi, fs), -dot(mwi, ft), cos_wi);
-            for (int i = 0; i < 3; i++) bw[i] = s->occ_spec[i];
-        } else {                                                            /* null.cpp:53-63 */
-            wol = mk(-dot(mwi, fs), -dot(mwi, ft), -cos_wi);
-            bw[0] = bw[1] = bw[2] = 1.0f;
-        }
-        /* Russian roulette (:477-492), eta = 1 */
-        float thr2[3];
-        for (int i = 0; i < 3; i++) thr2[i] = ((thr[i] * tr[i]) * bw[i]) * 1.0f;
-        float maxRR = depth >= spec_rr_depth ? 0.98f : 1.0f;
-        float mx = thr2[0] > thr2[1] ? thr2[0] : thr2[1];
-        mx = mx > thr2[2] ? mx : thr2[2];
-        float rrProb = maxRR < mx ? maxRR : mx;
-        if (rrProb <= 0 || (rrProb < 1 && draw(seed, pass, 7u, pixel, k | (sample << 16), 0u, 0u) > rrProb)) break;
-        for (int i = 0; i < 3; i++) {
-            thr[i] = thr2[i] / rrProb;
-            weight[i] = ((weight[i] * tr[i]) * bw[i]) / rrProb;              /* :503-510 */
-        }
-        O = p;
-        D = add(add(scl(fs, wol.x), scl(ft, wol.y)), scl(n, wol.z));        /* its.toWorld(bRec.wo) */
-        mint = 1e-4f;
-        depth++;
-    }
-    return nrec;
+    chain_node(&cx, ld3(o), ld3(d), camera_mint(s, px, py), weight, thr, 1);   /* rRec.depth 1 */
+    return cx.nrec;
 }
 
 void alvrl_o_make_records(const alvrl_o_scene *s, int medium_scatters, float *recs)
@@ -1228,6 +1284,19 @@ static void trace_particle(const alvrl_o_scene *s, const alvrl_o_medium *m, seq_
                     wol = mk(-dot(mwi, fs), -dot(mwi, ft), cos_wi);
                     for (int i = 0; i < 3; i++) bw[i] = s->occ_spec[i];
                 }
+            } else if (mt == ALVRL_O_MAT_DIELECTRIC) {   /* SmoothDielectric::sample, both components,
+                                                           EImportance (dielectric.cpp:335-364) */
+                float cos_t;
+                float F = fresnel_dielectric_ext(cos_wi, &cos_t, s->occ_eta);
+                if (bx <= F) {
+                    wol = mk(-dot(mwi, fs), -dot(mwi, ft), cos_wi);
+                } else {
+                    float inv_eta = 1 / s->occ_eta;
+                    float scale = -(cos_t < 0 ? inv_eta : s->occ_eta);
+                    wol = mk(scale * dot(mwi, fs), scale * dot(mwi, ft), cos_t);
+                    eta *= cos_t < 0 ? s->occ_eta : inv_eta;
+                }
+                bw[0] = bw[1] = bw[2] = 1.0f;
             } else {                                  /* Null::sample (null.cpp:53-63) */
                 wol = mk(-dot(mwi, fs), -dot(mwi, ft), -cos_wi);
                 bw[0] = bw[1] = bw[2] = 1.0f;

@@ -152,16 +152,22 @@ typedef struct {
     float occ_albedo[3];     /* their one-sided diffuse reflectance */
     const uint32_t *occ_mat; /* per triangle ALVRL_O_MAT_* (NULL: all diffuse) */
     float occ_spec[3];       /* the mirrors' specular reflectance */
+    float occ_eta;           /* the dielectrics' intIOR / extIOR (dielectric.cpp:149-158) */
 } alvrl_o_scene;
 #define ALVRL_O_MAT_DIFFUSE 0u   /* SmoothDiffuse, one-sided (diffuse.cpp) */
 #define ALVRL_O_MAT_MIRROR 1u    /* SmoothConductor, material none (conductor.cpp:254-268) */
 #define ALVRL_O_MAT_NULL 2u      /* index-matched null BSDF (null.cpp:38-76) */
+#define ALVRL_O_MAT_DIELECTRIC 3u /* smooth dielectric, reflectance / transmittance 1 (dielectric.cpp) */
 /* LiInternal's eye path of pixel centre (x, y) through delta BSDFs
  * (vrlIntegrator.cpp:386-524): one gather record per segment with the path
- * weight of :503-510 and its depth; Russian roulette from init_throughput,
- * maxRR 0.98 from rRec.depth spec_rr_depth on (:475-492), its uniform from
- * stream (seed, pass, dom 7, pixel, segment).  Writes at most cap records;
- * returns the count. */
+ * weight of :503-510.  Every delta component is followed (bRec.component =
+ * i, :467-511), so a dielectric branches into reflection and transmission:
+ * the records form a tree, written depth first (component 0's subtree before
+ * component 1's), record k (pre-order) with depth word k.  The Russian
+ * roulette of record k's components (from init_throughput, maxRR 0.98 from
+ * rRec.depth spec_rr_depth on, :475-492) draws in component order from
+ * stream (seed, pass, dom 7, pixel, k).  Writes at most min(cap, 256)
+ * records; returns the count. */
 uint32_t alvrl_o_make_chain(const alvrl_o_scene *s, const alvrl_o_medium *m, int medium_scatters, int x, int y,
                             uint32_t seed, uint32_t pass, int spec_rr_depth, float init_throughput,
                             float *recs, uint32_t cap);

@@ -52,13 +52,13 @@ class Scene(C.Structure):
                 ("box_min", C.c_float * 3), ("box_max", C.c_float * 3), ("albedo", C.c_float * 3),
                 ("light_pos", C.c_float * 3), ("light_intensity", C.c_float * 3),
                 ("occ", C.POINTER(C.c_float)), ("nocc", C.c_uint32), ("occ_albedo", C.c_float * 3),
-                ("occ_mat", C.POINTER(C.c_uint32)), ("occ_spec", C.c_float * 3)]
+                ("occ_mat", C.POINTER(C.c_uint32)), ("occ_spec", C.c_float * 3), ("occ_eta", C.c_float)]
 
 
-MAT_DIFFUSE, MAT_MIRROR, MAT_NULL = 0, 1, 2
+MAT_DIFFUSE, MAT_MIRROR, MAT_NULL, MAT_DIELECTRIC = 0, 1, 2, 3
 
 
-def set_occluders(obj, tris, albedo=None, material=None, specular=None):
+def set_occluders(obj, tris, albedo=None, material=None, specular=None, eta=None):
     """Occluder triangles ((n, 9) float32) on a Scene (hit by eye rays and
     particles, occ_albedo) or a Params (blocking the gather's connections);
     material: None (all diffuse) or one MAT_* per triangle; specular: the
@@ -77,6 +77,8 @@ def set_occluders(obj, tris, albedo=None, material=None, specular=None):
     if specular is not None:
         for i in range(3):
             obj.occ_spec[i] = float(specular[i])
+    if eta is not None:
+        obj.occ_eta = float(eta)
     return obj
 
 
