@@ -328,6 +328,9 @@ def main():
             "roofline": rooflines[dominant],
             "rooflines": rooflines,
             "cpu_baseline": None,
+            # the prebuilt in-tree library this run loaded, and whether it was
+            # built from this tree's sources (alvrl_build_id vs the tree's hash)
+            "build_mode": dict(alvrl.build_info(), mode="prebuilt in-tree (make, hipcc --offload-arch=gfx950)"),
         }
         if alt is not None:
             out["alt_decomposition"] = alt

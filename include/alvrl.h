@@ -124,6 +124,11 @@ ALVRL_API void alvrl_ctx_destroy(alvrl_ctx *ctx);
 /* Last error of this context on the calling thread (ctx == NULL: global). */
 ALVRL_API const char *alvrl_last_error(const alvrl_ctx *ctx);
 ALVRL_API int alvrl_abi_version(void);
+/* "src <hash> ...": the first 16 hex digits of the SHA-1 of the library's
+ * sources (the .hip, .hpp, host .cpp/.hpp and include .h files, concatenated
+ * in path order, mitsuba-alvrl_amd/Makefile SRC_HASH) it was built from; the Python binding recomputes it from the tree
+ * (alvrl.build_info) so a prebuilt library is checked against its sources. */
+ALVRL_API const char *alvrl_build_id(void);
 
 /* ---- per-scene / per-pass state (set in preprocess/prepass; immutable
  *      while gathers run, vrlIntegrator.cpp:237-356) -------------------- */

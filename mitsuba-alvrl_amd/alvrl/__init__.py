@@ -113,6 +113,31 @@ def lib() -> C.CDLL:
     return L
 
 
+def build_info() -> dict:
+    """The loaded library's build id and whether its source hash matches the
+    sources in this tree (Makefile SRC_HASH): {"library", "build_id",
+    "src_hash_tree", "matches_tree"}."""
+    import glob
+    import hashlib
+    L = lib()
+    if hasattr(L, "alvrl_build_id"):
+        L.alvrl_build_id.restype = C.c_char_p
+        bid = L.alvrl_build_id().decode()
+    else:                                   # a developer variant built before the id existed
+        bid = "unknown"
+    os_ = os.path
+    rel = []
+    for pat in ("csrc/*.hip", "csrc/*.hpp", "csrc/host/*.cpp", "csrc/host/*.hpp", "../include/*.h"):
+        rel += [os_.relpath(p, PKG_DIR) for p in glob.glob(os_.join(PKG_DIR, pat))]
+    h = hashlib.sha1()
+    for r in sorted(rel):
+        with open(os_.join(PKG_DIR, r), "rb") as f:
+            h.update(f.read())
+    tree = h.hexdigest()[:16]
+    return {"library": os_.relpath(LIB_PATH, REPO), "build_id": bid, "src_hash_tree": tree,
+            "matches_tree": bid.split()[1] == tree if bid.startswith("src ") else False}
+
+
 def _check(rc: int):
     if rc != ALVRL_OK:
         raise AlvrlError(rc, lib().alvrl_last_error(None).decode())

@@ -219,6 +219,11 @@ extern "C" {
 
 ALVRL_API int alvrl_abi_version(void) { return ALVRL_ABI_VERSION; }
 
+#ifndef ALVRL_SRC_HASH
+#define ALVRL_SRC_HASH "unknown"
+#endif
+ALVRL_API const char* alvrl_build_id(void) { return "src " ALVRL_SRC_HASH " gfx950 hipcc -O3"; }
+
 ALVRL_API const char* alvrl_last_error(const alvrl_ctx*) { return g_err.c_str(); }
 
 ALVRL_API int alvrl_ctx_create(const alvrl_config* cfg, alvrl_ctx** out)

@@ -17,7 +17,8 @@
  *   "frame" (default)  The scene is described to the library once
  *                      (camera, film, the homogeneous medium's container
  *                      box and its diffuse walls, a point light, triangle
- *                      occluders with diffuse / mirror / null BSDFs).  The
+ *                      occluders with diffuse / mirror / dielectric / null
+ *                      BSDFs).  The
  *                      library traces the VRLs, builds R, refines the
  *                      clusters and renders the whole frame on the GPU once
  *                      per pass; renderBlock copies its block out of that
@@ -503,7 +504,7 @@ private:
 
         /* the container: the shape whose interior is the medium; its walls' diffuse reflectance */
         m_tris.clear(); m_mats.clear();
-        bool haveBox = false, haveOccAlbedo = false, haveSpec = false;
+        bool haveBox = false, haveOccAlbedo = false, haveSpec = false, haveEta = false;
         const ref_vector<Shape> &shapes = scene->getShapes();
         for (size_t s = 0; s < shapes.size(); ++s) {
             const Shape *sh = shapes[s].get();
@@ -533,9 +534,17 @@ private:
                     mat = ALVRL_MAT_MIRROR;
                     if (!haveSpec) put3(m_desc.occluder_specular, bsdf->getSpecularReflectance(its));
                     haveSpec = true;
+                } else if ((type & BSDF::EDeltaReflection) && (type & BSDF::EDeltaTransmission) &&
+                           !(type & BSDF::ESmooth)) {
+                    /* smooth dielectric (dielectric.cpp): both delta components */
+                    mat = ALVRL_MAT_DIELECTRIC;
+                    if (haveEta && (float) bsdf->getEta() != m_desc.occluder_eta)
+                        Log(EError, "vrl (amd) frame mode: dielectrics with different IORs (amdMode=records takes any)");
+                    m_desc.occluder_eta = (float) bsdf->getEta();
+                    haveEta = true;
                 } else if (type & BSDF::EDelta) {
-                    Log(EError, "vrl (amd) frame mode: BSDF of \"%s\" is neither diffuse, mirror nor null "
-                        "(amdMode=records follows every delta component)", sh->getName().c_str());
+                    Log(EError, "vrl (amd) frame mode: BSDF of \"%s\" is neither diffuse, mirror, dielectric nor "
+                        "null (amdMode=records follows every delta component)", sh->getName().c_str());
                 } else if (!haveOccAlbedo) {
                     put3(m_desc.occluder_albedo, bsdf->getDiffuseReflectance(its));
                     haveOccAlbedo = true;

@@ -347,6 +347,7 @@ public:
     virtual Spectrum sample(BSDFSamplingRecord &bRec, const Point2 &sample) const = 0;
     virtual Spectrum getDiffuseReflectance(const Intersection &its) const = 0;
     virtual Spectrum getSpecularReflectance(const Intersection &its) const;
+    virtual Float getEta() const;
 };
 
 struct PositionSamplingRecord {

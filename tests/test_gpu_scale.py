@@ -82,8 +82,8 @@ def test_c5_end_to_end(oracle, gpu_ok, tmp_path):
         total = torch.zeros(W * H * 3, dtype=torch.float32, device="cuda")
         for r in range(world):
             fb = torch.zeros(W * H * 3, dtype=torch.float32, device="cuda")
-            # on torch's stream: the add below must see the finished tiles
-            it.render(fb, rank=r, world=world, stream=torch.cuda.current_stream().cuda_stream)
+            it.render(fb, rank=r, world=world)
+            torch.cuda.synchronize()   # the render ran on the integrator's stream
             total += fb
             del fb
         torch.cuda.synchronize()

@@ -96,12 +96,27 @@ def full(a):
     total = torch.zeros(W * H * 3, dtype=torch.float32, device="cuda")
     for r in range(a.world):
         fb = torch.zeros_like(total)
-        it.render(fb, rank=r, world=a.world, stream=torch.cuda.current_stream().cuda_stream)
+        it.render(fb, rank=r, world=a.world)
+        torch.cuda.synchronize()   # the render ran on the integrator's stream
         total += fb
     one = torch.zeros_like(total)
     it.render(one)
     torch.cuda.synchronize()
     same = bool(torch.equal(total, one))
+    if not same:
+        two = torch.zeros_like(total)
+        it.render(two)
+        torch.cuda.synchronize()
+        d = (total - one).abs()
+        bad = (total != one).view(-1, 3).any(1)
+        print(f"tiles != world 1: {int(bad.sum())} of {bad.numel()} pixels differ, max |diff| {float(d.max()):.3e}, "
+              f"nan total {int(torch.isnan(total).sum())} one {int(torch.isnan(one).sum())}, "
+              f"world-1 repeat equal {bool(torch.equal(one, two))}, zero pixels total {int((total.view(-1, 3) == 0).all(1).sum())} "
+              f"one {int((one.view(-1, 3) == 0).all(1).sum())}", flush=True)
+        idx = torch.nonzero(bad).view(-1)[:8].tolist()
+        for i in idx:
+            print(f"  pixel {i} (x {i % W}, y {i // W}): tiles {total.view(-1, 3)[i].tolist()} one {one.view(-1, 3)[i].tolist()}",
+                  flush=True)
     st = it.stats()
     out = {k: v for k, v in info.items() if k not in ("p2s", "vrls", "slice_off", "reps", "weights")}
     out.update(tiles_equal_world1=same, render_kernel_ms=st["ms_render_kernel"], s_total=time.time() - t0,

@@ -6,7 +6,7 @@ log=$1; to=$2; cmd=$3
 for i in $(seq 1 30); do
   /usr/local/graft/bin/gpurun --timeout "$to" -- "$cmd" > "$log" 2>&1
   rc=$?
-  if grep -q "status=transient" "$log" && ! grep -q "charged=[1-9]" "$log"; then sleep 90; continue; fi
+  if [ $rc -eq 3 ] || { grep -q "status=transient" "$log" && ! grep -q "charged=[1-9]" "$log"; }; then sleep 90; continue; fi
   exit $rc
 done
 exit 3
