@@ -3163,7 +3163,10 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
     __shared__ Ctl C;
     __shared__ __attribute__((aligned(16))) unsigned char pool[kPoolBytes];
     unsigned long long* lds = reinterpret_cast<unsigned long long*>(pool);
-    if (threadIdx.x == 0) { C.g_row0 = 0; C.g_first = 1; C.g_last = 1; C.g_carry = nullptr; }   // one row group
+    if (threadIdx.x == 0) {   // one row group; no LDS heap, no trace record until a leader sets them
+        C.g_row0 = 0; C.g_first = 1; C.g_last = 1; C.g_carry = nullptr;
+        C.hlds = 0; C.hpool = pool; C.prec = nullptr;
+    }
     __syncthreads();
     if (blockIdx.x >= cm.njobs * cm.team) {   // a roaming helper
         const uint32_t rid = blockIdx.x - cm.njobs * cm.team;
