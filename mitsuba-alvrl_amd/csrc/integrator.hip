@@ -121,6 +121,10 @@ struct alvrl_integrator {
     int device = 0;
     alvrl_ctx* ctx = nullptr;
     hipStream_t stream = nullptr;
+    // the last render's gather, timed on the stream it ran on by the
+    // integrator's own events (get_stats may run on any thread)
+    hipEvent_t ev_r0 = nullptr, ev_r1 = nullptr;
+    bool render_timed = false;
     SmokeBox scene;
     alvrl_scene_desc scene_desc{};
     bool have_scene = false;
@@ -179,6 +183,8 @@ struct alvrl_integrator {
     ~alvrl_integrator()
     {
         if (ctx) alvrl_ctx_destroy(ctx);
+        if (ev_r0) hipEventDestroy(ev_r0);
+        if (ev_r1) hipEventDestroy(ev_r1);
         if (stream) hipStreamDestroy(stream);
     }
 
@@ -1054,10 +1060,17 @@ struct alvrl_integrator {
             chk(alvrl_gather_false_color(ctx, mode, rec_buf.p, clustered ? item_buf.p : nullptr,
                                          clustered ? level_item[levels] : level_rec[levels], out_buf.p, s),
                 "alvrl_gather_false_color");
-        } else if (clustered)
-            chk(alvrl_gather_clustered(ctx, rec_buf.p, pix_buf.p, item_buf.p, nitems, out_buf.p, s), "alvrl_gather_clustered");
-        else
-            chk(alvrl_gather_brute(ctx, rec_buf.p, pix_buf.p, nrec, out_buf.p, s), "alvrl_gather_brute");
+        } else {
+            render_timed = false;
+            hchk(hipEventRecord(ev_r0, s), "hipEventRecord");
+            if (clustered)
+                chk(alvrl_gather_clustered(ctx, rec_buf.p, pix_buf.p, item_buf.p, nitems, out_buf.p, s),
+                    "alvrl_gather_clustered");
+            else
+                chk(alvrl_gather_brute(ctx, rec_buf.p, pix_buf.p, nrec, out_buf.p, s), "alvrl_gather_brute");
+            hchk(hipEventRecord(ev_r1, s), "hipEventRecord");
+            render_timed = true;
+        }
         // ImageBlock::put of each sensor sample, normalised by the box
         // filter's weight sum at develop time: the mean over the samples
         if (sampleCount > 1 && level_rec[levels]) {
@@ -1127,6 +1140,8 @@ ALVRL_API int alvrl_integrator_create(const char* props, int device, alvrl_integ
         chk(alvrl_set_rsamples(it->ctx, it->Rsamples), "alvrl_set_rsamples");
         hchk(hipSetDevice(device), "hipSetDevice");
         hchk(hipStreamCreateWithFlags(&it->stream, hipStreamNonBlocking), "hipStreamCreate");
+        hchk(hipEventCreate(&it->ev_r0), "hipEventCreate");
+        hchk(hipEventCreate(&it->ev_r1), "hipEventCreate");
     });
     *out = it.release();
     return ALVRL_OK;
@@ -1256,7 +1271,9 @@ ALVRL_API int alvrl_integrator_get_stats(alvrl_integrator* it, alvrl_integrator_
         it->st.contrib_preprocess = pre;
         it->st.contrib_render = ren;
         float ms = 0;
-        if (alvrl_last_kernel_ms(it->ctx, &ms) == ALVRL_OK) it->st.ms_render_kernel = ms;
+        if (it->render_timed && hipEventSynchronize(it->ev_r1) == hipSuccess &&
+            hipEventElapsedTime(&ms, it->ev_r0, it->ev_r1) == hipSuccess)
+            it->st.ms_render_kernel = ms;
         *st = it->st;
     });
     return ALVRL_OK;

@@ -73,6 +73,41 @@ struct Team {
     const SplitWs* ws;                // [helpers]
 };
 enum : uint32_t { kStNone = 0, kStQueued = 1, kStRunning = 2, kStDone = 3, kStLeader = 4 };
+// Split parts.  A large split's two variance passes over a group of row
+// blocks are independent of every other (pass, group): each writes the 64-row
+// block totals of its per-column prefix terms, and the owner of the split
+// adds them in ascending block order afterwards (wsum_blk's order, so the
+// prefixes are those of the one-workgroup engine bit for bit).  The owner
+// publishes the parts on a slot of the part board; idle workgroups (helpers,
+// roamers, a leader waiting for a helper) claim them.  Nothing a claimer does
+// waits for anyone, so the owner's wait for its claimed parts ends.
+struct PartJob {
+    const unsigned long long* roff;   // the job's row layout (JobDev's)
+    const uint32_t* rstride;
+    unsigned long long off0;
+    uint32_t stride0;
+    int contig;
+    const double* locw;
+    uint32_t nrows;
+    uint32_t kind;                    // kPartVar: variance passes; kPartProj: projections
+    const unsigned long long* cw;     // kPartVar: the cluster's (weight << 32 | vrl), column order (the owner's keys1)
+    const uint32_t* ids;              // kPartProj: the cluster's columns, their split direction, the keys out
+    const float* dir;
+    unsigned long long* keys;
+    uint32_t m;                       // columns
+    uint32_t nblk, pblk, np;          // 64-row blocks, blocks per part (kPartVar), parts
+    uint32_t cpp;                     // kPartProj: columns per part
+};
+enum : uint32_t { kPartVar = 0, kPartProj = 1 };
+struct PartSlot {
+    unsigned long long word;          // generation << 32 | parts << 16 | parts claimed
+    uint32_t busy;                    // an owner holds the slot
+    uint32_t done;                    // parts finished (each after a release)
+    uint32_t err;                     // a part's engine error
+    uint32_t pad;
+    double* T;                        // [pass][u|i][block][column] block totals (fixed per slot)
+    PartJob pj;
+};
 // A cluster born from a committed speculative split has its vrls in team.spec
 // already (the parent's output, which the leader copied to vrls): bit 63 of
 // its state word and bit 31 of its queue entry's end say so, and its helper
@@ -158,6 +193,13 @@ struct Common {
     int heap_lds;                  // the leader's heap in LDS between its splits (ALVRL_HEAP_LDS=0: off)
     uint32_t* poptr;               // ALVRL_POP_TRACE=1: wall ticks at 7 points of each leader pop of one job
     uint32_t poptr_job, poptr_cap; // the traced job (most rows), records available
+    PartSlot* parts;               // the part board (null: splits are never divided)
+    uint32_t nslots;               // its slots
+    uint32_t part_min;             // smallest split (columns) divided into parts
+    uint32_t part_blk;             // 64-row blocks per part (<= 7)
+    uint32_t* part_open;           // slots with parts not yet claimed (a hint for idle workgroups)
+    uint32_t proj_min;             // smallest split whose projections are divided (0: never)
+    uint32_t proj_cpp;             // columns per projection part
 };
 __device__ __forceinline__ void trace(const Common& cm, uint32_t phase, uint32_t value)
 {
@@ -167,7 +209,8 @@ __device__ __forceinline__ void trace(const Common& cm, uint32_t phase, uint32_t
 }
 // team counters
 enum { TS_ENQ, TS_HSTART, TS_HDONE, TS_COMMIT, TS_STEAL, TS_WAIT_TMO, TS_OWN, TS_IDLE_EXIT, TS_LSIDE,
-       TS_HIDLE, TS_RIDLE, TS_HBUSY, TS_RBUSY, TS_ACQ, TS_REL, TS_N };   // *IDLE/*BUSY: wall ticks (100 MHz) summed
+       TS_HIDLE, TS_RIDLE, TS_HBUSY, TS_RBUSY, TS_ACQ, TS_REL, TS_PSPLIT, TS_PSOLO, TS_POWN, TS_POTHER,
+       TS_PWAIT, TS_N };   // *IDLE/*BUSY: wall ticks (100 MHz) summed
 __device__ __forceinline__ void tcount(const Common& cm, int k)
 {
     if (cm.tstat) atomicAdd(&cm.tstat[k], 1ull);
@@ -1659,6 +1702,174 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
     __syncthreads();
 }
 
+// One part of a divided split (PartJob): pass g (0 forward, 1 reverse) of
+// variance_split_v3 over the row blocks [gb0, gb0 + nb) of the job (nb <= 7),
+// with the whole workgroup on that pass: wave 0 forms the coefficients (the
+// running weight total in the pass's column order, as every group of the
+// one-workgroup engine does) and stores the row blocks' per-column totals to
+// T instead of adding them; waves 1..nb run one 64-row block's recurrence
+// each.  Per row and column the same IEEE operations in the same order as
+// variance_split_v3 (rec below is its full-chunk and guarded paths), so the
+// block totals are bit-identical to the ones that engine adds.
+constexpr uint32_t kPartMaxBlk = 7;
+__device__ __noinline__ void variance_part(const PartJob& pj, const Common& cm, Ctl& C, const double* Tout_c, uint32_t g,
+                                           uint32_t gb0, uint32_t nb, unsigned char* pool)
+{
+    double* const Tout = const_cast<double*>(Tout_c);
+    const uint32_t Rt_rows = pj.nrows, m = pj.m, nblk_t = pj.nblk;
+    const int tid = threadIdx.x, wv = tid >> 6;
+    const uint32_t lane = (uint32_t)(tid & 63);
+    const bool coefw = wv == 0;
+    const uint32_t b0 = (uint32_t)wv - 1u;                       // row waves 1..nb: local block b0
+    const bool roww = wv >= 1 && b0 < nb;
+    double* Q = reinterpret_cast<double*>(pool);                 // [k & 1][kPartMaxBlk][16]
+    CoefBlock* ring = reinterpret_cast<CoefBlock*>(pool + 2 * kPartMaxBlk * 16 * sizeof(double));
+    const auto cwp = gp(pj.cw);
+    const uint32_t nch = (m + kCH - 1) / kCH;
+    const uint32_t nblk = (m + kCB64 - 1) / kCB64;
+    auto cn_of = [&](uint32_t k) { return min((uint32_t)kCH, m - k * kCH); };
+    auto ncol_of = [&](uint32_t b) { return min((uint32_t)kCB64, m - b * kCB64); };
+    auto kw_of_blk = [&](uint32_t b) -> unsigned long long {
+        if (b >= nblk) return 0ull;
+        const uint32_t i = b * kCB64 + min(lane, ncol_of(b) - 1);
+        return cwp[g == 0 ? i : m - 1 - i];
+    };
+    double W = 0.0, cWo = 0.0, cWn = 0.0, cw_w = 1.0;
+    uint32_t cw_v = 0;
+    unsigned long long kwN = 0;
+    auto take = [&](unsigned long long kw, uint32_t b) {
+        cw_v = (uint32_t)kw;
+        cw_w = lane < ncol_of(b) ? (double)__uint_as_float((uint32_t)(kw >> 32)) : 1.0;
+        cWo = 0.0; cWn = 0.0;
+        if (lane < ncol_of(b)) ring[b & 1].vrl[lane] = cw_v;
+    };
+    if (coefw) {
+        take(kw_of_blk(0), 0);
+        for (uint32_t j = 0; j < 8; j++) coef_chain8(W, cw_w, j, ncol_of(0), cWo, cWn);
+        coef_block_finish(C, cw_w, cWo, cWn, cw_v, ncol_of(0), &ring[0]);
+        kwN = kw_of_blk(1);
+    }
+    __syncthreads();
+    // rows past the job's last take its data at weight 0 (variance_split_v3)
+    const uint32_t grow = (gb0 + (roww ? b0 : 0u)) * 64u + lane;
+    const uint32_t r0 = min(grow, Rt_rows - 1);
+    const RowRef rr0 = roww ? (pj.contig ? RowRef{(size_t)(pj.off0 + r0), (size_t)pj.stride0}
+                                         : RowRef{(size_t)gp(pj.roff)[r0], (size_t)gp(pj.rstride)[r0]})
+                            : RowRef{0, 0};
+    const double lw0 = roww && grow < Rt_rows ? gp(pj.locw)[r0] : 0.0;
+    // wave 0: the block totals of chunk kk to T[g][h][gb0 + b][n]
+    auto store_totals = [&](uint32_t kk) {
+        const uint32_t cn = cn_of(kk);
+        const double* Qk = Q + (size_t)(kk & 1) * kPartMaxBlk * 16;
+        const uint32_t sl = lane & 15, c = sl >> 1, h = sl & 1;
+        const uint32_t n = kk * kCH + c;
+        if (lane < 16 && c < cn) {
+            double* const t = Tout + ((size_t)(g * 2 + h) * nblk_t + gb0) * m + n;
+            for (uint32_t b = 0; b < nb; b++) gpw(t)[(size_t)b * m] = Qk[b * 16 + sl];
+        }
+    };
+    auto rec = [&](uint32_t k, const float2* cur, uint32_t blk, double lw, double& sum0, double& M0, double& V0) {
+        const uint32_t c0 = k * kCH, cn = cn_of(k);
+        const CoefBlock& q = ring[(k / 8) & 1];
+        const uint32_t o = (k % 8) * kCH;
+        double th[kCH];
+        auto half_done = [&](uint32_t hsel) {
+            const double z = tree8_transposed(th, lane);
+            if ((lane & 7) == 0) {
+                const uint32_t h = lane >> 5, c = 4 * hsel + 2 * ((lane >> 3) & 1) + ((lane >> 4) & 1);
+                Q[((size_t)(k & 1) * kPartMaxBlk + blk) * 16 + 2 * c + h] = z;
+            }
+        };
+        if (cn == (uint32_t)kCH && k > 0) {
+            struct CCol { double w, Wo, a, bb, rw, Wn, rWn; };
+            auto ldc = [&](int c) {
+                return CCol{q.w[o + c], q.Wo[o + c], q.a[o + c], q.bb[o + c], q.rw[o + c], q.Wn[o + c], q.rWn[o + c]};
+            };
+            auto col = [&](const CCol& k2, float2 e, double* t) {
+                const double x = (double)e.x;
+                const double tmp = k2.w * sum0 - k2.Wo * x;
+                M0 = k2.a * M0 + k2.bb * (tmp * tmp);
+                V0 = V0 + (double)e.y * k2.rw;
+                sum0 = sum0 + x;
+                t[0] = lw * (M0 * k2.rWn); t[1] = lw * (V0 * k2.Wn);
+            };
+            CCol k0 = ldc(0), k1 = ldc(1), k2 = k1;
+#pragma unroll
+            for (int c = 0; c < kCH; c++) {
+                if (c + 2 < kCH) k2 = ldc(c + 2);
+                col(k0, cur[c], &th[2 * (c & 3)]);
+                k0 = k1; k1 = k2;
+                if (c == 3) half_done(0);
+            }
+            half_done(1);
+        } else {
+#pragma unroll
+            for (int c = 0; c < kCH; c++) {
+                double* t = &th[2 * (c & 3)];
+                if ((uint32_t)c < cn) {
+                    const double x = (double)cur[c].x;
+                    const double tmp = q.w[o + c] * sum0 - q.Wo[o + c] * x;
+                    if (c0 + c > 0) M0 = q.a[o + c] * M0 + q.bb[o + c] * (tmp * tmp);
+                    V0 = V0 + (double)cur[c].y * q.rw[o + c];
+                    sum0 = sum0 + x;
+                    t[0] = lw * (M0 * q.rWn[o + c]); t[1] = lw * (V0 * q.Wn[o + c]);
+                } else {
+                    t[0] = 0.0; t[1] = 0.0;
+                }
+                if (c == 3) half_done(0);
+                if (c == 7) half_done(1);
+            }
+        }
+    };
+    if (coefw) {
+        // chunk k = 8B + j: store chunk k-1's block totals, form 8 columns of
+        // block B+1's coefficients (the divisions at j = 7)
+        for (uint32_t B = 0; B * 8 < nch; B++) {
+            const uint32_t nbk = B + 1;
+            if (nbk < nblk) take(kwN, nbk);
+            kwN = kw_of_blk(nbk + 1);
+#pragma unroll 1
+            for (uint32_t j = 0; j < 8; j++) {
+                const uint32_t k = B * 8 + j;
+                if (k >= nch) break;
+                if (k >= 1) store_totals(k - 1);
+                if (nbk < nblk) {
+                    coef_chain8(W, cw_w, j, ncol_of(nbk), cWo, cWn);
+                    if (j == 7 || k == nch - 1) coef_block_finish(C, cw_w, cWo, cWn, cw_v, ncol_of(nbk), &ring[nbk & 1]);
+                }
+                __syncthreads();
+            }
+        }
+        store_totals(nch - 1);
+    } else if (roww) {
+        double sum0 = 0.0, M0 = 0.0, V0 = 0.0;
+        float2 bufA[kCH], bufB[kCH], bufC[kCH];
+        const float2* const Rt = cm.Rt + rr0.base;
+        const size_t rstride = rr0.stride;
+        auto load_chunk = [&](uint32_t k, float2* dst) {
+            const uint32_t* ids = &ring[(k / 8) & 1].vrl[(k % 8) * kCH];
+            const uint32_t cn = cn_of(k);
+#pragma unroll
+            for (int c = 0; c < kCH; c++) dst[c] = ldg2(Rt, (size_t)ids[(uint32_t)c < cn ? c : 0] * rstride);
+        };
+        load_chunk(0, bufA);
+        load_chunk(min(1u, nch - 1), bufB);
+        auto step = [&](uint32_t k, float2* cur, float2* pre) {
+            load_chunk(min(k + 2, nch - 1), pre);
+            rec(k, cur, b0, lw0, sum0, M0, V0);
+            __syncthreads();
+        };
+        for (uint32_t k = 0; k < nch; k += 3) {
+            step(k, bufA, bufC);
+            if (k + 1 < nch) step(k + 1, bufB, bufA);
+            if (k + 2 < nch) step(k + 2, bufC, bufB);
+        }
+    } else {
+        for (uint32_t k = 0; k < nch; k++) __syncthreads();
+    }
+    __syncthreads();
+}
+
 // The two passes of a small split (m <= kSmallMax columns, R <= 256 rows) in
 // one step, without the chunk pipeline of variance_split_v3: waves 0-3 run
 // the forward pass over row blocks 0-3, waves 4-7 the reverse one.  Wave 0
@@ -1794,10 +2005,17 @@ __device__ __noinline__ void variance_split_small(const JobDev& J, const Common&
     __syncthreads();
 }
 
+__device__ __noinline__ bool split_parts(const JobDev& J, const Common& cm, Ctl& C, const uint32_t* base, uint32_t m,
+                            float* fu0, float* fi0, float* fu1, float* fi1, unsigned char* pool);
+__device__ bool proj_parts(const JobDev& J, const Common& cm, Ctl& C, uint32_t begin, uint32_t m, unsigned char* pool);
 __device__ void variance_passes(const JobDev& J, const Common& cm, Ctl& C, const uint32_t* base, uint32_t m,
                                 int npass, float* fu0, float* fi0, float* fu1, float* fi1, unsigned char* pool,
                                 Prof* pf = nullptr)
 {
+    // a large split in parts on idle workgroups (split_parts), when a slot is free
+    if (fu0 && npass == 2 && cm.parts && cm.var_v3 && cm.part_min && m >= cm.part_min &&
+        split_parts(J, cm, C, base, m, fu0, fi0, fu1, fi1, pool))
+        return;
     const uint32_t NB = (J.nrows + 63) / 64;
     if (pf && (!pf->p || threadIdx.x != 0)) pf = nullptr;
     const bool lds = (size_t)2 * 2 * kCH * NB * 64 * sizeof(double2) <= kPoolBytes;
@@ -2024,17 +2242,24 @@ __device__ __noinline__ unsigned long long* sort_keys(const JobDev& J, Ctl& C, u
 // batch, rows in the shared order (norm, then the normalised dot product with
 // the split direction).  For R <= 64*kRB the batch's entries stay in
 // registers for both sums and the next batch's loads are in flight while
-// the current one is reduced (ping-pong buffers, no copies).
-__device__ __noinline__ void split_projections(const JobDev& J, const Common& cm, uint32_t begin, uint32_t m)
+// the current one is reduced (ping-pong buffers, no copies).  Columns
+// [jb, je) of the cluster pj.ids[0..m): each column's key depends on that
+// column alone, so ranges can run on different workgroups (split parts).
+__device__ __forceinline__ RowRef row_ref(const PartJob& pj, uint32_t r)
 {
-    const uint32_t R = J.nrows;
+    return pj.contig ? RowRef{(size_t)(pj.off0 + r), (size_t)pj.stride0}
+                     : RowRef{(size_t)gp(pj.roff)[r], (size_t)gp(pj.rstride)[r]};
+}
+__device__ __noinline__ void proj_range(const PartJob& pj, const Common& cm, uint32_t jb, uint32_t je)
+{
+    const uint32_t R = pj.nrows;
     const int wave = threadIdx.x >> 6;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t stride = kWaves * kCB;
     const float2* const Rt = cm.Rt;                  // register copy (cm is behind a generic pointer)
-    auto* const k0 = gpw(J.keys0);
-    const auto* const vrls = gp(J.vrls);
-    const auto* const dir = gp(J.dir);
+    auto* const k0 = gpw(pj.keys);
+    const auto* const vrls = gp(pj.ids);
+    const auto* const dir = gp(pj.dir);
     if (R <= 64u * kRB) {
         float d[kRB];
         RowRef row[kRB];
@@ -2042,13 +2267,13 @@ __device__ __noinline__ void split_projections(const JobDev& J, const Common& cm
         for (int rb = 0; rb < kRB; rb++) {
             const uint32_t r = lane + 64u * rb;
             d[rb] = r < R ? dir[r] : 0.0f;
-            row[rb] = row_ref(J, r < R ? r : 0);
+            row[rb] = row_ref(pj, r < R ? r : 0);
         }
         uint32_t vA[kCB], vB[kCB];
         float xA[kRB][kCB], xB[kRB][kCB];
         auto load = [&](uint32_t j0, uint32_t* v, float (*x)[kCB]) {
 #pragma unroll
-            for (int q = 0; q < kCB; q++) v[q] = vrls[begin + min(j0 + (uint32_t)q, m - 1)];
+            for (int q = 0; q < kCB; q++) v[q] = vrls[min(j0 + (uint32_t)q, je - 1)];
 #pragma unroll
             for (int rb = 0; rb < kRB; rb++)
 #pragma unroll
@@ -2078,28 +2303,28 @@ __device__ __noinline__ void split_projections(const JobDev& J, const Common& cm
             if (lane == 0) {
 #pragma unroll
                 for (int q = 0; q < kCB; q++)
-                    if (j0 + q < m) k0[j0 + q] = proj_key(nc[q] != 0 ? pp[q] : 0.0f, v[q]);
+                    if (j0 + q < je) k0[j0 + q] = proj_key(nc[q] != 0 ? pp[q] : 0.0f, v[q]);
             }
         };
-        uint32_t j0 = (uint32_t)wave * kCB;
-        if (j0 < m) load(j0, vA, xA);
-        for (; j0 < m; j0 += 2 * stride) {
-            if (j0 + stride < m) load(j0 + stride, vB, xB);
+        uint32_t j0 = jb + (uint32_t)wave * kCB;
+        if (j0 < je) load(j0, vA, xA);
+        for (; j0 < je; j0 += 2 * stride) {
+            if (j0 + stride < je) load(j0 + stride, vB, xB);
             reduce(j0, vA, xA);
-            if (j0 + stride >= m) break;
-            if (j0 + 2 * stride < m) load(j0 + 2 * stride, vA, xA);
+            if (j0 + stride >= je) break;
+            if (j0 + 2 * stride < je) load(j0 + 2 * stride, vA, xA);
             reduce(j0 + stride, vB, xB);
         }
     } else {                                // tall local matrices: two passes from memory
-        for (uint32_t j0 = (uint32_t)wave * kCB; j0 < m; j0 += stride) {
+        for (uint32_t j0 = jb + (uint32_t)wave * kCB; j0 < je; j0 += stride) {
             uint32_t vr[kCB];
 #pragma unroll
-            for (int q = 0; q < kCB; q++) vr[q] = vrls[begin + min(j0 + (uint32_t)q, m - 1)];
+            for (int q = 0; q < kCB; q++) vr[q] = vrls[min(j0 + (uint32_t)q, je - 1)];
             float pn[kCB], pp[kCB];
 #pragma unroll
             for (int q = 0; q < kCB; q++) { pn[q] = 0.0f; pp[q] = 0.0f; }
             for (uint32_t r = lane; r < R; r += 64) {
-                const RowRef rw = row_ref(J, r);
+                const RowRef rw = row_ref(pj, r);
 #pragma unroll
                 for (int q = 0; q < kCB; q++) { const float a = fabsf(ldg2(Rt, rw.base + (size_t)vr[q] * rw.stride).x); pn[q] = pn[q] + a * a; }
             }
@@ -2107,7 +2332,7 @@ __device__ __noinline__ void split_projections(const JobDev& J, const Common& cm
 #pragma unroll
             for (int q = 0; q < kCB; q++) nc[q] = sqrtf(__shfl(tree_f(pn[q]), 0, 64));
             for (uint32_t r = lane; r < R; r += 64) {
-                const RowRef rw = row_ref(J, r);
+                const RowRef rw = row_ref(pj, r);
                 const float dd = dir[r];
 #pragma unroll
                 for (int q = 0; q < kCB; q++) pp[q] = pp[q] + dd * (ldg2(Rt, rw.base + (size_t)vr[q] * rw.stride).x / nc[q]);
@@ -2115,10 +2340,23 @@ __device__ __noinline__ void split_projections(const JobDev& J, const Common& cm
 #pragma unroll
             for (int q = 0; q < kCB; q++) {
                 const float pr = tree_f(pp[q]);
-                if (lane == 0 && j0 + q < m) k0[j0 + q] = proj_key(nc[q] != 0 ? pr : 0.0f, vr[q]);
+                if (lane == 0 && j0 + q < je) k0[j0 + q] = proj_key(nc[q] != 0 ? pr : 0.0f, vr[q]);
             }
         }
     }
+}
+__device__ __forceinline__ PartJob part_job(const JobDev& J)
+{
+    PartJob pj{};
+    pj.roff = J.roff; pj.rstride = J.rstride; pj.off0 = J.off0; pj.stride0 = J.stride0; pj.contig = J.contig;
+    pj.locw = J.locw; pj.nrows = J.nrows;
+    return pj;
+}
+__device__ void split_projections(const JobDev& J, const Common& cm, uint32_t begin, uint32_t m)
+{
+    PartJob pj = part_job(J);
+    pj.ids = J.vrls + begin; pj.dir = J.dir; pj.keys = J.keys0; pj.m = m;
+    proj_range(pj, cm, 0, m);
 }
 
 // ------------------------------------------------------------ split --
@@ -2255,7 +2493,9 @@ __device__ void split(const JobDev& J, const Common& cm, Ctl& C, uint32_t begin,
     }
     pf.mark(PF_DIR);
     hbp = pf.t - hb0;
-    split_projections(J, cm, begin, m);
+    if (!(cm.parts && cm.proj_min && m >= cm.proj_min &&
+          proj_parts(J, cm, C, begin, m, reinterpret_cast<unsigned char*>(lds))))
+        split_projections(J, cm, begin, m);
     __syncthreads();
     pf.mark(PF_PROJ);
     const unsigned long long* sorted = sort_keys(J, C, m, lds);
@@ -2560,6 +2800,205 @@ __device__ int try_claim(const Team& T, uint32_t* b, uint32_t* e, uint64_t max_c
     return cas_rlx(&T.state[*b], key | kStQueued, key | kStRunning) ? 1 : 2;   // spec_split acquires
 }
 
+// ------------------------------------------------------- split parts --
+// Thread 0: the next part of slot S (-1: every part is claimed).  The CAS
+// reads the generation word the owner stored after its release fence, and
+// the acquire fence after it makes the slot's fields (and the owner's cw)
+// visible to this CU.
+__device__ int part_claim_slot(const Common& cm, PartSlot* S)
+{
+    while (true) {
+        const unsigned long long w = ld_rlx(&S->word);
+        const uint32_t np = (uint32_t)(w >> 16) & 0xFFFFu, nx = (uint32_t)w & 0xFFFFu;
+        if (nx >= np) return -1;
+        if (cas_rlx(&S->word, w, w + 1ull)) {
+            if (nx + 1 == np) __hip_atomic_fetch_add(cm.part_open, 0xFFFFFFFFu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            fence_acq();
+            return (int)nx;
+        }
+    }
+}
+// Thread 0 of an idle workgroup: claim a part of any open slot.
+__device__ bool part_try(const Common& cm, uint32_t* slot, uint32_t* part)
+{
+    if (!cm.parts || ld_rlx(cm.part_open) == 0u) return false;
+    for (uint32_t s = 0; s < cm.nslots; s++) {
+        const int p = part_claim_slot(cm, &cm.parts[s]);
+        if (p >= 0) { *slot = s; *part = (uint32_t)p; return true; }
+    }
+    return false;
+}
+// Every thread: run part p of slot s and publish it (spec_split's producer
+// form: drained stores, barrier, one agent release, relaxed count).  C.err
+// is the caller's.
+__device__ __noinline__ void run_part(const Common& cm, Ctl& C, uint32_t s, uint32_t p, unsigned char* pool, bool own)
+{
+    PartSlot* const S = &cm.parts[s];
+    if (threadIdx.x == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // thread 0's acquire, complete
+    __syncthreads();
+    const PartJob pj = S->pj;   // once per part: flat loads are fine here
+    const double* const T = gp(&S->T)[0];
+    const int err_saved = C.err;
+    __syncthreads();
+    if (threadIdx.x == 0) C.err = 0;
+    __syncthreads();
+    if (pj.kind == kPartProj) {
+        const uint32_t jb = p * pj.cpp;
+        if (jb < pj.m) proj_range(pj, cm, jb, min(pj.m, jb + pj.cpp));
+    } else {
+        const uint32_t g = p & 1u, gb0 = (p >> 1) * pj.pblk;
+        if (LDS_OK(gb0 < pj.nblk && pj.pblk <= kPartMaxBlk, "part blocks", gb0, pj.nblk))
+            variance_part(pj, cm, C, T, g, gb0, min(pj.pblk, pj.nblk - gb0), pool);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (C.err) __hip_atomic_fetch_or(&S->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        C.err = err_saved;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_fetch_add(&S->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        tcount(cm, own ? TS_POWN : TS_POTHER);
+    }
+    __syncthreads();
+}
+// Every thread: a free slot of the board, or -1.
+__device__ int part_slot_take(const Common& cm, Ctl& C)
+{
+    if (threadIdx.x == 0) {
+        int got = -1;
+        uint32_t s = blockIdx.x % cm.nslots;   // owners spread over the slots
+        for (uint32_t i = 0; i < cm.nslots && got < 0; i++) {
+            if (ld_rlx(&cm.parts[s].busy) == 0u && cas_rlx(&cm.parts[s].busy, 0u, 1u)) got = (int)s;
+            if (++s == cm.nslots) s = 0;
+        }
+        C.go = got;
+        if (got < 0) tcount(cm, TS_PSOLO);
+    }
+    __syncthreads();
+    const int sl = C.go;
+    __syncthreads();
+    return sl;
+}
+// Every thread: publish pj's parts on slot sl (its inputs stored by this
+// workgroup before the call), run parts until none is left, then wait for
+// the claimed ones.  The claimed parts run on workgroups that wait for
+// nobody, so the wait ends; a 60 s guard fails the job (false) and keeps the
+// slot, which a late part may still write.
+__device__ bool part_run_all(const Common& cm, Ctl& C, uint32_t sl, const PartJob& pj, unsigned char* pool)
+{
+    PartSlot* const S = &cm.parts[sl];
+    const int tid = threadIdx.x;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+        S->pj = pj;
+        st_rlx(&S->done, 0u);
+        st_rlx(&S->err, 0u);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned long long w = ld_rlx(&S->word);
+        st_rlx(&S->word, (((w >> 32) + 1ull) << 32) | ((unsigned long long)pj.np << 16));
+        __hip_atomic_fetch_add(cm.part_open, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        tcount(cm, TS_PSPLIT);
+    }
+    __syncthreads();
+    while (true) {
+        if (tid == 0) C.go = part_claim_slot(cm, S);
+        __syncthreads();
+        const int p = C.go;
+        __syncthreads();
+        if (p < 0) break;
+        run_part(cm, C, sl, (uint32_t)p, pool, true);
+    }
+    if (tid == 0) {
+        const unsigned long long t0 = wall();
+        int ok = 1;
+        while (ld_rlx(&S->done) != pj.np) {
+            if (wall() - t0 > kSpinTicks) { ok = 0; break; }
+            __builtin_amdgcn_s_sleep(4);
+        }
+        tadd(cm, TS_PWAIT, wall() - t0);
+        fence_acq();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (!ok || ld_rlx(&S->err)) C.err = 1;
+        C.go = ok;
+    }
+    __syncthreads();
+    const bool ok = C.go != 0;
+    __syncthreads();
+    return ok;
+}
+__device__ void part_slot_free(const Common& cm, uint32_t sl)
+{
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(&cm.parts[sl].busy, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+// The owner's side of a divided split's variance passes (variance_passes,
+// both passes with prefixes): false when no slot is free (the caller runs the
+// one-workgroup engine).  The cluster's (weight, vrl) pairs are gathered once
+// for every part; afterwards the block totals are added in ascending block
+// order into the float prefixes (variance_split_v3's reduce, the last group's).
+__device__ __noinline__ bool split_parts(const JobDev& J, const Common& cm, Ctl& C, const uint32_t* base, uint32_t m,
+                            float* fu0, float* fi0, float* fu1, float* fi1, unsigned char* pool)
+{
+    const int tid = threadIdx.x;
+    const int sl = part_slot_take(cm, C);
+    if (sl < 0) return false;
+    unsigned long long* const cw = J.keys1;
+    {
+        constexpr int B = 8;
+        for (uint32_t i0 = (uint32_t)tid; i0 < m; i0 += B * kThreads) {
+            uint32_t v[B];
+#pragma unroll
+            for (int b = 0; b < B; b++) v[b] = gp(base)[min(i0 + (uint32_t)b * kThreads, m - 1)];
+            float wt[B];
+#pragma unroll
+            for (int b = 0; b < B; b++) wt[b] = gp(J.colw)[v[b]];
+#pragma unroll
+            for (int b = 0; b < B; b++)
+                if (i0 + (uint32_t)b * kThreads < m)
+                    gpw(cw)[i0 + (uint32_t)b * kThreads] = ((unsigned long long)__float_as_uint(wt[b]) << 32) | v[b];
+        }
+    }
+    const uint32_t nblk = (J.nrows + 63) / 64, pblk = min(max(cm.part_blk, 1u), kPartMaxBlk);
+    PartJob pj = part_job(J);
+    pj.kind = kPartVar; pj.cw = cw; pj.m = m; pj.nblk = nblk; pj.pblk = pblk;
+    pj.np = 2 * ((nblk + pblk - 1) / pblk);
+    if (!part_run_all(cm, C, (uint32_t)sl, pj, pool)) return true;
+    const double* const T = gp(&cm.parts[sl].T)[0];
+    for (uint32_t t = (uint32_t)tid; t < 4u * m; t += kThreads) {
+        const uint32_t gh = t / m, n = t - gh * m, g = gh >> 1, h = gh & 1;
+        const auto* q = gp(T + (size_t)gh * nblk * m + n);
+        double acc = q[0];
+        for (uint32_t b = 1; b < nblk; b++) acc = acc + q[(size_t)b * m];
+        const float f = (h == 0 && n == 0) ? 0.0f : (float)acc;
+        float* const out = g == 0 ? (h == 0 ? fu0 : fi0) : (h == 0 ? fu1 : fi1);
+        gpw(out)[n] = f;
+        if (n == m - 1) {
+            if (h == 0) C.vg[g].res_u = f; else C.vg[g].res_i = f;
+            if (!isfinite(f) || f < 0) C.err = 1;
+        }
+    }
+    part_slot_free(cm, (uint32_t)sl);
+    return true;
+}
+// The owner's side of a divided split's projections (split): column ranges
+// of the cluster on idle workgroups.  False when no slot is free.
+__device__ __noinline__ bool proj_parts(const JobDev& J, const Common& cm, Ctl& C, uint32_t begin, uint32_t m, unsigned char* pool)
+{
+    const int sl = part_slot_take(cm, C);
+    if (sl < 0) return false;
+    PartJob pj = part_job(J);
+    pj.kind = kPartProj; pj.ids = J.vrls + begin; pj.dir = J.dir; pj.keys = J.keys0; pj.m = m;
+    pj.cpp = max(cm.proj_cpp, 64u);
+    pj.np = min((m + pj.cpp - 1) / pj.cpp, 0xFFFFu);
+    pj.cpp = (m + pj.np - 1) / pj.np;
+    part_run_all(cm, C, (uint32_t)sl, pj, pool);
+    part_slot_free(cm, (uint32_t)sl);
+    return true;
+}
+
 // Split [b, e) speculatively with Jw's scratch (Jw.vrls = team.spec; e may
 // carry kQSpecBit: the input is there already) and
 // publish the result (MI355X_MICROARCH.md, valid producer form: every storing
@@ -2738,16 +3177,23 @@ __device__ void split_team(const JobDev& J, const Common& cm, Ctl& C, uint32_t b
                 tcount(cm, TS_WAIT_TMO);
             } else {
                 uint32_t yb = 0, ye = 0;
-                const int got = try_claim(T, &yb, &ye, (uint64_t)(e - b) * cm.side_k / 16);
-                if (got == 1) { C.side = 1; C.yb = yb; C.ye = ye; tcount(cm, TS_LSIDE); }
-                else if (got == 0) __builtin_amdgcn_s_sleep(8);
+                if (part_try(cm, &yb, &ye)) {   // a part of a divided split (perhaps the awaited one's)
+                    C.side = 2; C.yb = yb; C.ye = ye;
+                } else {
+                    const int got = try_claim(T, &yb, &ye, (uint64_t)(e - b) * cm.side_k / 16);
+                    if (got == 1) { C.side = 1; C.yb = yb; C.ye = ye; tcount(cm, TS_LSIDE); }
+                    else if (got == 0) __builtin_amdgcn_s_sleep(8);
+                }
             }
         }
         __syncthreads();
         pf.mark(PF_T_WAIT);
         if (C.side) {
             if (C.hlds) { heap_move(J, C, false); parked = true; }
-            spec_split(J, J_spec(J), cm, C, lds, C.yb, C.ye);
+            const uint32_t yb = C.yb, ye = C.ye;
+            __syncthreads();
+            if (C.side == 2) run_part(cm, C, yb, ye, reinterpret_cast<unsigned char*>(lds), false);
+            else spec_split(J, J_spec(J), cm, C, lds, yb, ye);
         }
         __syncthreads();
         pf.mark(PF_T_SIDE);
@@ -2894,6 +3340,7 @@ __device__ __noinline__ void helper_loop(const JobDev& J0, uint32_t hid, const C
             uint32_t b = 0, e = 0;
             while (true) {
                 if (ld_rlx(&T.ctl[2])) { got = -1; break; }
+                if (part_try(cm, &b, &e)) { got = 2; break; }   // a part of a divided split first
                 const int c = try_claim(T, &b, &e);
                 if (c == 1) { got = 1; tcount(cm, TS_HSTART); break; }
                 if (c == 2) continue;
@@ -2905,6 +3352,12 @@ __device__ __noinline__ void helper_loop(const JobDev& J0, uint32_t hid, const C
         }
         __syncthreads();
         if (C.go < 0) break;
+        if (C.go == 2) {
+            const uint32_t ps = C.b, pp = C.e;
+            __syncthreads();
+            run_part(cm, C, ps, pp, reinterpret_cast<unsigned char*>(lds), false);
+            continue;
+        }
         trace(cm, 11, C.b);
         const unsigned long long t_busy = wall();
         spec_split(J0, J, cm, C, lds, C.b, C.e);
@@ -2928,6 +3381,7 @@ __device__ __noinline__ void roam_loop(const JobDev* jobs, const SplitWs& w, uin
             int got = 0;
             uint32_t b = 0, e = 0, jj = j;
             while (true) {
+                if (part_try(cm, &b, &e)) { got = 2; break; }   // a part of a divided split first
                 uint32_t live = 0;
                 for (uint32_t k = 0; k < njobs && !got; k++) {
                     jj = cm.roam_order ? cm.roam_order[k] : (j + k < njobs ? j + k : j + k - njobs);
@@ -2939,7 +3393,7 @@ __device__ __noinline__ void roam_loop(const JobDev* jobs, const SplitWs& w, uin
                     if (c == 1) got = 1;
                 }
                 if (got) { tcount(cm, TS_HSTART); break; }
-                if (!live || wall() - t_idle > cm.spin_ticks) { got = -1; break; }
+                if ((!live && !(cm.parts && ld_rlx(cm.part_open))) || wall() - t_idle > cm.spin_ticks) { got = -1; break; }
                 __builtin_amdgcn_s_sleep(32);
             }
             tadd(cm, TS_RIDLE, wall() - t_idle);
@@ -2947,6 +3401,12 @@ __device__ __noinline__ void roam_loop(const JobDev* jobs, const SplitWs& w, uin
         }
         __syncthreads();
         if (C.go < 0) break;
+        if (C.go == 2) {
+            const uint32_t ps = C.b, pp = C.e;
+            __syncthreads();
+            run_part(cm, C, ps, pp, reinterpret_cast<unsigned char*>(lds), false);
+            continue;
+        }
         j = C.j;
         const JobDev& J0 = jobs[j];
         JobDev Jw = J0;
@@ -3668,7 +4128,8 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
         }
     }
     char* tarena = nullptr;
-    size_t tbytes = 0;
+    size_t tbytes = 0, board_off = 0, board_ctl = 0, slot_T = 0;
+    uint32_t nslots = 0, part_min = 0, part_blk = 4;
     if (team_on) {
         auto helper_bytes = [&](uint32_t R) {
             return align_up((size_t)R * 4) + align_up((size_t)6 * R * 8) +
@@ -3680,8 +4141,29 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
         for (uint32_t j = 0; j < njobs; j++) tbytes += team_fixed + (size_t)(G - 1) * helper_bytes(roam_on ? Rmax : jobs[j].nrows);
         tbytes += align_up((size_t)nroam * sizeof(SplitWs)) + (size_t)nroam * helper_bytes(Rmax);
         tbytes += align_up((size_t)njobs * 4);   // roam order
-        if (arena_get(&ar.tarena, &ar.tarena_cap, tbytes, cache != nullptr) != hipSuccess) {
-            (void)hipGetLastError(); G = 1; nroam = 0;
+        // the part board after everything else: slots, the open count, and
+        // each slot's block totals (4 x 64-row blocks x N doubles; only the
+        // control words are cleared per launch)
+        board_off = tbytes;
+        const char* pm = std::getenv("ALVRL_PART_MIN");
+        part_min = pm ? (uint32_t)std::max(0, std::atoi(pm)) : 4096u;
+        const char* pb = std::getenv("ALVRL_PART_BLK");
+        part_blk = pb ? (uint32_t)std::min(std::max(1, std::atoi(pb)), (int)kPartMaxBlk) : 4u;
+        if (part_min) {
+            const char* ps = std::getenv("ALVRL_PART_SLOTS");
+            const char* pmb = std::getenv("ALVRL_PART_MB");
+            slot_T = align_up((size_t)4 * ((Rmax + 63) / 64) * N * 8);
+            const size_t budget = (pmb ? (size_t)std::max(1, std::atoi(pmb)) : 8192u) << 20;
+            nslots = (uint32_t)std::min<size_t>(ps ? (size_t)std::max(0, std::atoi(ps)) : 64u, budget / slot_T);
+            nslots = std::min<uint32_t>(nslots, njobs * G + nroam);
+        }
+        board_ctl = nslots ? align_up((size_t)nslots * sizeof(PartSlot)) + align_up(4) : 0;
+        if (arena_get(&ar.tarena, &ar.tarena_cap, tbytes + board_ctl + nslots * slot_T, cache != nullptr) != hipSuccess) {
+            (void)hipGetLastError();
+            nslots = 0; board_ctl = 0;   // without the board
+            if (arena_get(&ar.tarena, &ar.tarena_cap, tbytes, cache != nullptr) != hipSuccess) {
+                (void)hipGetLastError(); G = 1; nroam = 0;
+            }
         }
         tarena = ar.tarena;
     }
@@ -3798,8 +4280,23 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
             for (uint32_t j = 0; j < njobs; j++) h_order[j] = j;
             std::stable_sort(h_order.begin(), h_order.end(),
                              [&](uint32_t a, uint32_t b) { return jobs[a].nrows > jobs[b].nrows; });
-            cm.roam_order = (const uint32_t*)(tarena + tbytes - align_up((size_t)njobs * 4));
+            cm.roam_order = (const uint32_t*)(tarena + board_off - align_up((size_t)njobs * 4));
         }
+    }
+    cm.parts = nullptr; cm.nslots = 0; cm.part_min = part_min; cm.part_blk = part_blk; cm.part_open = nullptr;
+    {
+        const char* pm = std::getenv("ALVRL_PROJ_MIN");
+        cm.proj_min = pm ? (uint32_t)std::max(0, std::atoi(pm)) : (part_min ? 16384u : 0u);
+        const char* pc = std::getenv("ALVRL_PROJ_CPP");
+        cm.proj_cpp = pc ? (uint32_t)std::max(64, std::atoi(pc)) : 16384u;
+    }
+    std::vector<PartSlot> h_slots;
+    if (tarena && nslots && part_min) {
+        cm.parts = (PartSlot*)(tarena + board_off);
+        cm.part_open = (uint32_t*)(tarena + board_off + align_up((size_t)nslots * sizeof(PartSlot)));
+        cm.nslots = nslots;
+        h_slots.assign(nslots, PartSlot{});
+        for (uint32_t k = 0; k < nslots; k++) h_slots[k].T = (double*)(tarena + board_off + board_ctl + k * slot_T);
     }
     cm.init_vrls = d_init; cm.init_off = d_init_off; cm.ninit = ninit;
     cm.seed = seed; cm.pass = pass;
@@ -3839,7 +4336,9 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
     if (e == hipSuccess) e = hipMemcpyAsync(d_init_off, init_off, (size_t)(ninit + 1) * 4, hipMemcpyHostToDevice, s);
     if (e == hipSuccess) e = hipMemcpyAsync(d_jobs, h_jobs.data(), njobs * sizeof(JobDev), hipMemcpyHostToDevice, s);
     if (e == hipSuccess) e = hipMemsetAsync(d_entries, 0, 16, s);
-    if (e == hipSuccess && tarena) e = hipMemsetAsync(tarena, 0, tbytes, s);
+    if (e == hipSuccess && tarena) e = hipMemsetAsync(tarena, 0, board_off + board_ctl, s);
+    if (e == hipSuccess && cm.parts)
+        e = hipMemcpyAsync(cm.parts, h_slots.data(), (size_t)nslots * sizeof(PartSlot), hipMemcpyHostToDevice, s);
     for (uint32_t j = 0; j < njobs && e == hipSuccess && G > 1; j++)
         e = hipMemcpyAsync(const_cast<SplitWs*>(h_jobs[j].team.ws), &h_ws[(size_t)j * (G - 1)],
                            (size_t)(G - 1) * sizeof(SplitWs), hipMemcpyHostToDevice, s);
@@ -3909,6 +4408,7 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
     if (e == hipSuccess) e = hipMemcpyAsync(h_entries, d_entries, 16, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (entries) { entries[0] = h_entries[0]; entries[1] = h_entries[1]; }
+    unsigned long long jt_start_traced = 0;   // the pop-traced job's start (wall ticks), with team stats
     if (cm.tstat) {
         unsigned long long h[TS_N];
         if (hipMemcpy(h, cm.tstat, sizeof(h), hipMemcpyDeviceToHost) == hipSuccess) {
@@ -3922,6 +4422,10 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
             std::fprintf(stderr, "[refine team] speculative splits' hand-offs, wall ms summed: acquire %.1f, release %.1f "
                          "(%.2f / %.2f us each)\n", h[TS_ACQ] * 1e-5, h[TS_REL] * 1e-5,
                          h[TS_HSTART] ? h[TS_ACQ] * 1e-2 / h[TS_HSTART] : 0.0, h[TS_HSTART] ? h[TS_REL] * 1e-2 / h[TS_HSTART] : 0.0);
+            std::fprintf(stderr, "[refine team] split parts: %u slots, min %u columns, %u blocks per part | divided "
+                         "splits %llu (no free slot %llu), parts by owner %llu, by others %llu, owner wait ms summed %.1f\n",
+                         cm.nslots, cm.part_min, cm.part_blk, h[TS_PSPLIT], h[TS_PSOLO], h[TS_POWN], h[TS_POTHER],
+                         h[TS_PWAIT] * 1e-5);
         }
         hipFree(cm.tstat);
         if (cm.jtime) {
@@ -3940,6 +4444,7 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
                 std::fprintf(stderr, "[refine team] job end ms: min %.1f p10 %.1f median %.1f p90 %.1f max %.1f "
                              "(job %u, %u rows, refine %.1f ms)\n", f2.front(), f2[njobs / 10], f2[njobs / 2],
                              f2[(njobs * 9) / 10], f2.back(), jmax, jobs[jmax].nrows, dur[jmax]);
+                if (cm.poptr) jt_start_traced = jt[3 * cm.poptr_job];
             }
             hipFree(cm.jtime);
         }
@@ -3980,6 +4485,9 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
                 std::fprintf(stderr, "  %-18s %8.2f %8.2f %8.2f | %8.2f %8.2f\n", nm[k], m, a, b, mc, ac);
             }
             std::fprintf(stderr, "  total %.1f ms over the pops; a committed pop without a wait %.2f us\n", tot * 1e-3, totc);
+            if (jt_start_traced && n)
+                std::fprintf(stderr, "  first pop %.1f ms after the job's start (column weights, initial clusters, "
+                             "unclustered variance)\n", (uint32_t)(pr[0] - (uint32_t)jt_start_traced) * 1e-5);
             // waits (wait loop > 5 us) by log2 of the popped cluster's size, and when they happen
             double wt[32] = {0}; uint32_t wn[32] = {0};
             for (uint32_t p = 0; p < n; p++) {

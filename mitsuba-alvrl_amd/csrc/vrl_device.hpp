@@ -463,16 +463,19 @@ __device__ __forceinline__ void integrate_vrl(const DevParams& P, const RecPre& 
     float tot0 = 0.0f, tot1 = 0.0f, tot2 = 0.0f;
     float mean = 0.0f, M2 = 0.0f, mean_acc = 0.0f, var_acc = 0.0f;
     const uint32_t k0 = P.seed, k1 = P.pass;
-    // stream word: domain, the segment's eye-path depth, the R sample index
-    // plus the record's sensor sample (its depth word's bits 16-31)
-    const uint32_t c3 = (domain << 24) | ((q.depth & 0xFFu) << 16) | ((rsub + (q.depth >> 16)) & 0xFFFFu);
+    // stream word: domain, the segment's eye-path depth and the record's
+    // sensor sample (its depth word's bits 16-31); the R sample index sits in
+    // bits 8-23 of the block counter (a pair's draws use blocks < 2^8), so no
+    // two (sensor sample, R sample) pairs of one record share a stream
+    const uint32_t c3 = (domain << 24) | ((q.depth & 0xFFu) << 16) | ((q.depth >> 16) & 0xFFFFu);
+    const uint32_t cr = (rsub & 0xFFFFu) << 8;
 
     // draws 0..3: volVol samples 0,1 (V, U); draws 4..7: volSurf / further volVol
-    U4 rb = philox4x32_10(rec_id, vrl_id, 0u, c3, k0, k1);
+    U4 rb = philox4x32_10(rec_id, vrl_id, cr, c3, k0, k1);
     uint32_t cur_blk = 0;
     auto draw = [&](int k) -> float {
         const uint32_t blk = (uint32_t)k >> 2;
-        if (blk != cur_blk) { rb = philox4x32_10(rec_id, vrl_id, blk, c3, k0, k1); cur_blk = blk; }
+        if (blk != cur_blk) { rb = philox4x32_10(rec_id, vrl_id, cr | blk, c3, k0, k1); cur_blk = blk; }
         const uint32_t s = k & 3;
         const uint32_t b = s == 0 ? rb.x : (s == 1 ? rb.y : (s == 2 ? rb.z : rb.w));
         return u01(b);

@@ -482,9 +482,11 @@ void alvrl_o_medium_eval(const alvrl_o_medium *m, float distance, float tr[3], f
 /* ===================================================================== */
 /*  integrateVRL, vrlIntegrator.cpp:603-785                                */
 /* ===================================================================== */
-/* 'rsub' is the low 16 bits of the stream word: the sample index of an R
- * entry with Rsamples > 1 (LiInternal's samples loop, vrlIntegrator.cpp:427-443);
- * bits 16-23 carry the record's eye-path depth.  use_weight: integrateVRL's
+/* 'rsub' is the sample index of an R entry with Rsamples > 1 (LiInternal's
+ * samples loop, vrlIntegrator.cpp:427-443), in bits 8-23 of the block counter
+ * (the draws' block index stays below 2^8); the stream word carries the
+ * record's eye-path depth in bits 16-23 and its sensor sample in bits 0-15,
+ * so R sample r of sensor sample j never meets another (j', r') stream.  use_weight: integrateVRL's
  * 'weight' argument (:605) is the record's path weight, the first factor of
  * every sample's contribution (:668, :743), as getVRLContributions passes it
  * (:808); getClusteredVrlContributions calls with the default 1 and
@@ -497,7 +499,8 @@ static void integrate_vrl_w(const alvrl_o_params *P, const float *rec, uint32_t 
     uint32_t flags, depth;
     memcpy(&flags, &rec[15], 4);
     memcpy(&depth, &rec[19], 4);
-    rsub = ((depth & 0xFFu) << 16) | ((rsub + (depth >> 16)) & 0xFFFFu);
+    const uint32_t sw = ((depth & 0xFFu) << 16) | ((depth >> 16) & 0xFFFFu);
+    const uint32_t koff = (rsub & 0xFFFFu) << 10;   /* + k: counter word (k >> 2) | rsub << 8 */
     const float wt[3] = { use_weight ? rec[16] : 1.0f, use_weight ? rec[17] : 1.0f, use_weight ? rec[18] : 1.0f };
     if (contrib) *contrib = 0;
     if (variance) *variance = 0;
@@ -521,8 +524,8 @@ static void integrate_vrl_w(const alvrl_o_params *P, const float *rec, uint32_t 
     float mean = 0, M2 = 0;
     for (int sample = 0; sample < nVV; sample++) {
         float lumv = 0.0f;
-        float u0 = draw(P->seed, P->pass, domain, rec_id, vrl_id, rsub, 2 * sample);
-        float u1 = draw(P->seed, P->pass, domain, rec_id, vrl_id, rsub, 2 * sample + 1);
+        float u0 = draw(P->seed, P->pass, domain, rec_id, vrl_id, sw, koff + 2 * sample);
+        float u1 = draw(P->seed, P->pass, domain, rec_id, vrl_id, sw, koff + 2 * sample + 1);
         v3 V, U;
         float pdf = sample_v_to_distance(E, dray, Usurf, S, End, &V, u0);
         pdf *= kulla(A, B, V, &U, u1);
@@ -582,7 +585,7 @@ static void integrate_vrl_w(const alvrl_o_params *P, const float *rec, uint32_t 
     for (int sample = 0; sample < nVS; sample++) {
         float lumv = 0.0f;
         if (do_surf) {
-            float u = draw(P->seed, P->pass, domain, rec_id, vrl_id, rsub, 2 * nVV + sample);
+            float u = draw(P->seed, P->pass, domain, rec_id, vrl_id, sw, koff + 2 * nVV + sample);
             v3 V;
             float pdf = kulla(S, End, U, &V, u);
             if (dist(U, V) != 0) {

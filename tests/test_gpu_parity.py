@@ -435,6 +435,41 @@ def test_refine_bit_exact_c5_rows(oracle, gpu_ok, undersampling):
         assert np.array_equal(gw.view(np.uint32), cw.view(np.uint32)), sizes[s]
 
 
+@pytest.mark.parametrize("blk,proj", [(1, 0), (3, 300), (4, 300)])
+def test_refine_bit_exact_split_parts(oracle, gpu_ok, monkeypatch, capfd, blk, proj):
+    """Every split of more than 256 columns divided into parts (split_parts:
+    one part per variance pass and group of `blk` row blocks, run by idle
+    workgroups, the block totals added in block order by the split's owner),
+    and with proj > 0 the projections of every split of >= proj columns in
+    64-column ranges (proj_parts): device == oracle, bit for bit, and some
+    parts ran on other workgroups."""
+    import re
+    torch = _torch()
+    monkeypatch.setenv("ALVRL_PART_MIN", "64")
+    monkeypatch.setenv("ALVRL_PART_BLK", str(blk))
+    monkeypatch.setenv("ALVRL_PROJ_MIN", str(proj))
+    monkeypatch.setenv("ALVRL_PROJ_CPP", "64")
+    monkeypatch.setenv("ALVRL_REFINE_TEAM_STATS", "1")
+    sizes = [40, 129, 214, 260, 455]
+    ctx, d_Rt, Rt, jobs, init, init_off = _refine_case(oracle, 64, 64, 1500, sizes, -1.0, torch)
+    capfd.readouterr()
+    off, reps, w, refined = ctx.refine(d_Rt, Rt.shape[1], jobs, init, init_off)
+    err = capfd.readouterr().err
+    m = re.search(r"divided splits (\d+) \(no free slot (\d+)\), parts by owner (\d+), by others (\d+)", err)
+    assert m, err
+    print(m.group(0))
+    assert int(m.group(1)) > 0 and int(m.group(3)) + int(m.group(4)) >= 2 * int(m.group(1))
+    for s, j in enumerate(jobs):
+        cr, cw, cref = oracle.cluster_refine(Rt, j["rows"], j["locw"], init, init_off,
+                                             j["pixel_undersampling"], -1.0,
+                                             stage_refine=j["stage_refine"],
+                                             stage_sample=j["stage_sample"], seed=SEED_RNG)
+        gr, gw = reps[off[s]:off[s + 1]], w[off[s]:off[s + 1]]
+        assert bool(refined[s]) == cref, sizes[s]
+        assert np.array_equal(gr, cr), sizes[s]
+        assert np.array_equal(gw.view(np.uint32), cw.view(np.uint32)), sizes[s]
+
+
 @pytest.mark.parametrize("depth_correction", [0.8, 1.3])
 def test_refine_depth_correction(oracle, gpu_ok, depth_correction):
     """refineAdaptively with depthCorrection != 1 (Preprocessor.cpp:456-469:

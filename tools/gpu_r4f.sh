@@ -1,0 +1,6 @@
+# Round-4 session f: projection parts -- refinement parity, C4 bench, C5 rank-0 share.
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_parity.py -k "refine" > gpurun_out/r4f_parity.log 2>&1 && \
+ALVRL_REFINE_TEAM_STATS=1 timeout -k 10 200 python -u bench.py --config C4 --steps 3 --warmup 1 --no-cpu-baseline --no-alt > gpurun_out/r4f_c4.json 2> gpurun_out/r4f_c4.err && \
+ALVRL_REFINE_PROFILE=1 ALVRL_REFINE_TEAM_STATS=1 timeout -k 10 300 python -u tools/c5_share.py > gpurun_out/r4f_c5.log 2>&1 && \
+ALVRL_PART_MB=40000 ALVRL_REFINE_TEAM_STATS=1 timeout -k 10 300 python -u tools/c5_share.py > gpurun_out/r4f_c5_s.log 2>&1
