@@ -96,15 +96,20 @@ struct PartJob {
     unsigned long long* keys;
     uint32_t m;                       // columns
     uint32_t nblk, pblk, np;          // 64-row blocks, blocks per part (kPartVar), parts
-    uint32_t cpp;                     // kPartProj: columns per part
+    uint32_t cpp;                     // kPartProj / kPartColw: columns per part
+    float* colw;                      // kPartColw: the column weights out
+    uint32_t c0;                      // kPartColw: the first column (parts cover [c0, m))
+    double* st;                       // kPartInit: the rows' final (sum, M, V) states out (the owner's J.st)
+    double* wsum;                     // kPartInit: the total column weight (the slot's)
 };
-enum : uint32_t { kPartVar = 0, kPartProj = 1 };
+enum : uint32_t { kPartVar = 0, kPartProj = 1, kPartColw = 2, kPartInit = 3 };
 struct PartSlot {
     unsigned long long word;          // generation << 32 | parts << 16 | parts claimed
     uint32_t busy;                    // an owner holds the slot
     uint32_t done;                    // parts finished (each after a release)
     uint32_t err;                     // a part's engine error
     uint32_t pad;
+    double wsum;                      // kPartInit: the pass's total column weight
     double* T;                        // [pass][u|i][block][column] block totals (fixed per slot)
     PartJob pj;
 };
@@ -198,6 +203,11 @@ struct Common {
     uint32_t part_min;             // smallest split (columns) divided into parts
     uint32_t part_blk;             // 64-row blocks per part (<= 7)
     uint32_t* part_open;           // slots with parts not yet claimed (a hint for idle workgroups)
+    uint32_t* idle;                // helpers and roamers waiting for work (parts are published only if some are)
+    uint32_t idle_min;             // ... at least this many (0: always)
+    uint32_t part_min_tall;        // the same for jobs of more than 256 rows
+    uint32_t nbig;                 // slots [0, nbig) hold splits of any size, the rest up to small_cap columns
+    uint32_t small_cap;
     uint32_t proj_min;             // smallest split whose projections are divided (0: never)
     uint32_t proj_cpp;             // columns per projection part
 };
@@ -1711,7 +1721,10 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
 // each.  Per row and column the same IEEE operations in the same order as
 // variance_split_v3 (rec below is its full-chunk and guarded paths), so the
 // block totals are bit-identical to the ones that engine adds.
+// FU = false (kPartInit): no prefix terms; the rows' final states go to
+// pj.st and wave 0 stores the total weight to pj.wsum (variance_split_v3<false>).
 constexpr uint32_t kPartMaxBlk = 7;
+template <bool FU>
 __device__ __noinline__ void variance_part(const PartJob& pj, const Common& cm, Ctl& C, const double* Tout_c, uint32_t g,
                                            uint32_t gb0, uint32_t nb, unsigned char* pool)
 {
@@ -1774,6 +1787,7 @@ __device__ __noinline__ void variance_part(const PartJob& pj, const Common& cm, 
         const uint32_t o = (k % 8) * kCH;
         double th[kCH];
         auto half_done = [&](uint32_t hsel) {
+            if (!FU) return;
             const double z = tree8_transposed(th, lane);
             if ((lane & 7) == 0) {
                 const uint32_t h = lane >> 5, c = 4 * hsel + 2 * ((lane >> 3) & 1) + ((lane >> 4) & 1);
@@ -1791,7 +1805,7 @@ __device__ __noinline__ void variance_part(const PartJob& pj, const Common& cm, 
                 M0 = k2.a * M0 + k2.bb * (tmp * tmp);
                 V0 = V0 + (double)e.y * k2.rw;
                 sum0 = sum0 + x;
-                t[0] = lw * (M0 * k2.rWn); t[1] = lw * (V0 * k2.Wn);
+                if (FU) { t[0] = lw * (M0 * k2.rWn); t[1] = lw * (V0 * k2.Wn); }
             };
             CCol k0 = ldc(0), k1 = ldc(1), k2 = k1;
 #pragma unroll
@@ -1812,8 +1826,8 @@ __device__ __noinline__ void variance_part(const PartJob& pj, const Common& cm, 
                     if (c0 + c > 0) M0 = q.a[o + c] * M0 + q.bb[o + c] * (tmp * tmp);
                     V0 = V0 + (double)cur[c].y * q.rw[o + c];
                     sum0 = sum0 + x;
-                    t[0] = lw * (M0 * q.rWn[o + c]); t[1] = lw * (V0 * q.Wn[o + c]);
-                } else {
+                    if (FU) { t[0] = lw * (M0 * q.rWn[o + c]); t[1] = lw * (V0 * q.Wn[o + c]); }
+                } else if (FU) {
                     t[0] = 0.0; t[1] = 0.0;
                 }
                 if (c == 3) half_done(0);
@@ -1832,7 +1846,7 @@ __device__ __noinline__ void variance_part(const PartJob& pj, const Common& cm, 
             for (uint32_t j = 0; j < 8; j++) {
                 const uint32_t k = B * 8 + j;
                 if (k >= nch) break;
-                if (k >= 1) store_totals(k - 1);
+                if (FU && k >= 1) store_totals(k - 1);
                 if (nbk < nblk) {
                     coef_chain8(W, cw_w, j, ncol_of(nbk), cWo, cWn);
                     if (j == 7 || k == nch - 1) coef_block_finish(C, cw_w, cWo, cWn, cw_v, ncol_of(nbk), &ring[nbk & 1]);
@@ -1840,7 +1854,8 @@ __device__ __noinline__ void variance_part(const PartJob& pj, const Common& cm, 
                 __syncthreads();
             }
         }
-        store_totals(nch - 1);
+        if (FU) store_totals(nch - 1);
+        else if (lane == 0 && gb0 == 0) gpw(pj.wsum)[0] = W;
     } else if (roww) {
         double sum0 = 0.0, M0 = 0.0, V0 = 0.0;
         float2 bufA[kCH], bufB[kCH], bufC[kCH];
@@ -1863,6 +1878,10 @@ __device__ __noinline__ void variance_part(const PartJob& pj, const Common& cm, 
             step(k, bufA, bufC);
             if (k + 1 < nch) step(k + 1, bufB, bufA);
             if (k + 2 < nch) step(k + 2, bufC, bufB);
+        }
+        if (!FU && grow < Rt_rows) {   // the row's final state (variance_split_v3<false>)
+            gpw(pj.st)[Rt_rows + grow] = M0;
+            gpw(pj.st)[2 * Rt_rows + grow] = V0;
         }
     } else {
         for (uint32_t k = 0; k < nch; k++) __syncthreads();
@@ -2008,13 +2027,19 @@ __device__ __noinline__ void variance_split_small(const JobDev& J, const Common&
 __device__ __noinline__ bool split_parts(const JobDev& J, const Common& cm, Ctl& C, const uint32_t* base, uint32_t m,
                             float* fu0, float* fi0, float* fu1, float* fi1, unsigned char* pool);
 __device__ bool proj_parts(const JobDev& J, const Common& cm, Ctl& C, uint32_t begin, uint32_t m, unsigned char* pool);
+__device__ bool init_parts(const JobDev& J, const Common& cm, Ctl& C, const uint32_t* base, uint32_t m, unsigned char* pool);
+__device__ bool colw_parts(const JobDev& J, const Common& cm, Ctl& C, uint32_t vb, uint32_t ve, unsigned char* pool);
 __device__ void variance_passes(const JobDev& J, const Common& cm, Ctl& C, const uint32_t* base, uint32_t m,
                                 int npass, float* fu0, float* fi0, float* fu1, float* fi1, unsigned char* pool,
                                 Prof* pf = nullptr)
 {
     // a large split in parts on idle workgroups (split_parts), when a slot is free
-    if (fu0 && npass == 2 && cm.parts && cm.var_v3 && cm.part_min && m >= cm.part_min &&
+    const uint32_t pmin = J.nrows > 256 ? cm.part_min_tall : cm.part_min;   // 0: never
+    if (fu0 && npass == 2 && cm.parts && cm.var_v3 && pmin && m >= pmin &&
         split_parts(J, cm, C, base, m, fu0, fi0, fu1, fi1, pool))
+        return;
+    if (!fu0 && npass == 1 && cm.parts && cm.var_v3 && cm.part_min_tall && m >= cm.part_min_tall && J.nrows > 256 &&
+        init_parts(J, cm, C, base, m, pool))
         return;
     const uint32_t NB = (J.nrows + 63) / 64;
     if (pf && (!pf->p || threadIdx.x != 0)) pf = nullptr;
@@ -2493,7 +2518,7 @@ __device__ void split(const JobDev& J, const Common& cm, Ctl& C, uint32_t begin,
     }
     pf.mark(PF_DIR);
     hbp = pf.t - hb0;
-    if (!(cm.parts && cm.proj_min && m >= cm.proj_min &&
+    if (!(cm.parts && cm.proj_min && m >= cm.proj_min && (R > 256 ? cm.part_min_tall : cm.part_min) &&
           proj_parts(J, cm, C, begin, m, reinterpret_cast<unsigned char*>(lds))))
         split_projections(J, cm, begin, m);
     __syncthreads();
@@ -2828,6 +2853,8 @@ __device__ bool part_try(const Common& cm, uint32_t* slot, uint32_t* part)
     }
     return false;
 }
+template <class JV>
+__device__ void colw_raw(const JV& J, const Common& cm, Ctl& C, uint32_t vb, uint32_t ve);
 // Every thread: run part p of slot s and publish it (spec_split's producer
 // form: drained stores, barrier, one agent release, relaxed count).  C.err
 // is the caller's.
@@ -2842,13 +2869,20 @@ __device__ __noinline__ void run_part(const Common& cm, Ctl& C, uint32_t s, uint
     __syncthreads();
     if (threadIdx.x == 0) C.err = 0;
     __syncthreads();
-    if (pj.kind == kPartProj) {
-        const uint32_t jb = p * pj.cpp;
-        if (jb < pj.m) proj_range(pj, cm, jb, min(pj.m, jb + pj.cpp));
+    if (pj.kind == kPartProj || pj.kind == kPartColw) {
+        const uint32_t jb = pj.c0 + p * pj.cpp;
+        if (jb < pj.m) {
+            if (pj.kind == kPartProj) proj_range(pj, cm, jb, min(pj.m, jb + pj.cpp));
+            else colw_raw(pj, cm, C, jb, min(pj.m, jb + pj.cpp));
+        }
+    } else if (pj.kind == kPartInit) {
+        const uint32_t gb0 = p * pj.pblk;
+        if (LDS_OK(gb0 < pj.nblk && pj.pblk <= kPartMaxBlk, "part blocks", gb0, pj.nblk))
+            variance_part<false>(pj, cm, C, nullptr, 0, gb0, min(pj.pblk, pj.nblk - gb0), pool);
     } else {
         const uint32_t g = p & 1u, gb0 = (p >> 1) * pj.pblk;
         if (LDS_OK(gb0 < pj.nblk && pj.pblk <= kPartMaxBlk, "part blocks", gb0, pj.nblk))
-            variance_part(pj, cm, C, T, g, gb0, min(pj.pblk, pj.nblk - gb0), pool);
+            variance_part<true>(pj, cm, C, T, g, gb0, min(pj.pblk, pj.nblk - gb0), pool);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -2862,16 +2896,26 @@ __device__ __noinline__ void run_part(const Common& cm, Ctl& C, uint32_t s, uint
     }
     __syncthreads();
 }
-// Every thread: a free slot of the board, or -1.
-__device__ int part_slot_take(const Common& cm, Ctl& C)
+// Every thread: a free slot of the board whose block-total buffer holds a
+// split of `cols` columns (0: none needed), or -1.  Slots [0, nbig) hold any
+// split, the others up to small_cap columns; small needs try those first.
+__device__ int part_slot_take(const Common& cm, Ctl& C, uint32_t cols)
 {
     if (threadIdx.x == 0) {
         int got = -1;
-        uint32_t s = blockIdx.x % cm.nslots;   // owners spread over the slots
-        for (uint32_t i = 0; i < cm.nslots && got < 0; i++) {
-            if (ld_rlx(&cm.parts[s].busy) == 0u && cas_rlx(&cm.parts[s].busy, 0u, 1u)) got = (int)s;
-            if (++s == cm.nslots) s = 0;
-        }
+        // nobody idle to take parts (a busy launch): the one-workgroup engines
+        const bool idle = cm.idle_min == 0 || ld_rlx(cm.idle) >= cm.idle_min;
+        auto scan = [&](uint32_t lo, uint32_t hi) {
+            if (hi <= lo) return;
+            const uint32_t n = hi - lo;
+            uint32_t s = lo + blockIdx.x % n;   // owners spread over the slots
+            for (uint32_t i = 0; i < n && got < 0; i++) {
+                if (ld_rlx(&cm.parts[s].busy) == 0u && cas_rlx(&cm.parts[s].busy, 0u, 1u)) got = (int)s;
+                if (++s == hi) s = lo;
+            }
+        };
+        if (idle && cols <= cm.small_cap) scan(cm.nbig, cm.nslots);
+        if (idle && got < 0) scan(0, cm.nbig);
         C.go = got;
         if (got < 0) tcount(cm, TS_PSOLO);
     }
@@ -2934,6 +2978,24 @@ __device__ void part_slot_free(const Common& cm, uint32_t sl)
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_store(&cm.parts[sl].busy, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
+// Every thread: the cluster's (weight << 32 | vrl) pairs in column order, for
+// every part of a divided variance pass (variance_split_v3's gather)
+__device__ void gather_cw(const JobDev& J, const uint32_t* base, uint32_t m, unsigned long long* cw)
+{
+    constexpr int B = 8;
+    for (uint32_t i0 = threadIdx.x; i0 < m; i0 += B * kThreads) {
+        uint32_t v[B];
+#pragma unroll
+        for (int b = 0; b < B; b++) v[b] = gp(base)[min(i0 + (uint32_t)b * kThreads, m - 1)];
+        float wt[B];
+#pragma unroll
+        for (int b = 0; b < B; b++) wt[b] = gp(J.colw)[v[b]];
+#pragma unroll
+        for (int b = 0; b < B; b++)
+            if (i0 + (uint32_t)b * kThreads < m)
+                gpw(cw)[i0 + (uint32_t)b * kThreads] = ((unsigned long long)__float_as_uint(wt[b]) << 32) | v[b];
+    }
+}
 // The owner's side of a divided split's variance passes (variance_passes,
 // both passes with prefixes): false when no slot is free (the caller runs the
 // one-workgroup engine).  The cluster's (weight, vrl) pairs are gathered once
@@ -2943,24 +3005,10 @@ __device__ __noinline__ bool split_parts(const JobDev& J, const Common& cm, Ctl&
                             float* fu0, float* fi0, float* fu1, float* fi1, unsigned char* pool)
 {
     const int tid = threadIdx.x;
-    const int sl = part_slot_take(cm, C);
+    const int sl = part_slot_take(cm, C, m);
     if (sl < 0) return false;
     unsigned long long* const cw = J.keys1;
-    {
-        constexpr int B = 8;
-        for (uint32_t i0 = (uint32_t)tid; i0 < m; i0 += B * kThreads) {
-            uint32_t v[B];
-#pragma unroll
-            for (int b = 0; b < B; b++) v[b] = gp(base)[min(i0 + (uint32_t)b * kThreads, m - 1)];
-            float wt[B];
-#pragma unroll
-            for (int b = 0; b < B; b++) wt[b] = gp(J.colw)[v[b]];
-#pragma unroll
-            for (int b = 0; b < B; b++)
-                if (i0 + (uint32_t)b * kThreads < m)
-                    gpw(cw)[i0 + (uint32_t)b * kThreads] = ((unsigned long long)__float_as_uint(wt[b]) << 32) | v[b];
-        }
-    }
+    gather_cw(J, base, m, cw);
     const uint32_t nblk = (J.nrows + 63) / 64, pblk = min(max(cm.part_blk, 1u), kPartMaxBlk);
     PartJob pj = part_job(J);
     pj.kind = kPartVar; pj.cw = cw; pj.m = m; pj.nblk = nblk; pj.pblk = pblk;
@@ -2987,7 +3035,7 @@ __device__ __noinline__ bool split_parts(const JobDev& J, const Common& cm, Ctl&
 // of the cluster on idle workgroups.  False when no slot is free.
 __device__ __noinline__ bool proj_parts(const JobDev& J, const Common& cm, Ctl& C, uint32_t begin, uint32_t m, unsigned char* pool)
 {
-    const int sl = part_slot_take(cm, C);
+    const int sl = part_slot_take(cm, C, 0u);
     if (sl < 0) return false;
     PartJob pj = part_job(J);
     pj.kind = kPartProj; pj.ids = J.vrls + begin; pj.dir = J.dir; pj.keys = J.keys0; pj.m = m;
@@ -2996,6 +3044,60 @@ __device__ __noinline__ bool proj_parts(const JobDev& J, const Common& cm, Ctl& 
     pj.cpp = (m + pj.np - 1) / pj.np;
     part_run_all(cm, C, (uint32_t)sl, pj, pool);
     part_slot_free(cm, (uint32_t)sl);
+    return true;
+}
+// The owner's side of divided column weights (calculateColumnWeigths over
+// columns [vb, ve), each column's sum its own): false when no slot is free.
+__device__ __noinline__ bool colw_parts(const JobDev& J, const Common& cm, Ctl& C, uint32_t vb, uint32_t ve,
+                                        unsigned char* pool)
+{
+    const int sl = part_slot_take(cm, C, 0u);
+    if (sl < 0) return false;
+    PartJob pj = part_job(J);
+    pj.kind = kPartColw; pj.colw = J.colw; pj.c0 = vb; pj.m = ve;
+    pj.cpp = max(cm.proj_cpp, 64u);
+    pj.np = min((ve - vb + pj.cpp - 1) / pj.cpp, 0xFFFFu);
+    pj.cpp = (ve - vb + pj.np - 1) / pj.np;
+    part_run_all(cm, C, (uint32_t)sl, pj, pool);
+    part_slot_free(cm, (uint32_t)sl);
+    return true;
+}
+// The owner's side of a divided cluster variance (variance_passes without
+// prefixes, one pass, more than 256 rows): each part writes its rows' final
+// states, then wave 0 forms the two sums over all rows as
+// variance_split_v3<false>'s last group does.  False when no slot is free.
+__device__ __noinline__ bool init_parts(const JobDev& J, const Common& cm, Ctl& C, const uint32_t* base, uint32_t m,
+                                        unsigned char* pool)
+{
+    const int sl = part_slot_take(cm, C, 0u);
+    if (sl < 0) return false;
+    gather_cw(J, base, m, J.keys1);
+    const uint32_t nblk = (J.nrows + 63) / 64, pblk = min(max(cm.part_blk, 1u), kPartMaxBlk);
+    PartJob pj = part_job(J);
+    pj.kind = kPartInit; pj.cw = J.keys1; pj.m = m; pj.nblk = nblk; pj.pblk = pblk;
+    pj.np = (nblk + pblk - 1) / pblk;
+    pj.st = J.st; pj.wsum = &cm.parts[sl].wsum;
+    if (part_run_all(cm, C, (uint32_t)sl, pj, pool) && threadIdx.x < 64) {
+        const uint32_t lane = threadIdx.x, Rfull = J.nrows;
+        const double* st = J.st;
+        const double Wt = gp(pj.wsum)[0], rW = 1.0 / Wt;
+        double pu = 0.0, pi = 0.0;
+        for (uint32_t r = lane; r < Rfull; r += 64) {
+            pu = pu + J.locw[r] * (gp(st)[Rfull + r] * rW);
+            pi = pi + J.locw[r] * (gp(st)[2 * Rfull + r] * Wt);
+        }
+        pu = tree_d(pu);
+        pi = tree_d(pi);
+        if (lane == 0) {
+            VarGroup& V = C.vg[0];
+            V.Wcur = Wt;
+            V.res_u = (float)pu; V.res_i = (float)pi;
+            if (!isfinite(V.res_u) || V.res_u < 0) C.err = 1;
+            if (!isfinite(V.res_i) || V.res_i < 0) C.err = 1;
+        }
+    }
+    part_slot_free(cm, (uint32_t)sl);
+    __syncthreads();
     return true;
 }
 
@@ -3290,7 +3392,6 @@ __device__ bool su_wait(const Team& T, uint32_t task, const Common& cm, Ctl& C)
     __syncthreads();
     return ok;
 }
-__device__ void colw_raw(const JobDev& J, const Common& cm, Ctl& C, uint32_t vb, uint32_t ve);
 __device__ void unclustered_variance(const JobDev& J, const Common& cm, Ctl& C, const uint32_t* vrls_in, uint32_t nv);
 // the helper's side (Jw: its own scratch, colw shared with the leader)
 __device__ void setup_tasks(const JobDev& J0, const JobDev& Jw, const Common& cm, Ctl& C, bool)
@@ -3338,6 +3439,7 @@ __device__ __noinline__ void helper_loop(const JobDev& J0, uint32_t hid, const C
             const unsigned long long t_idle = wall();
             int got = 0;
             uint32_t b = 0, e = 0;
+            if (cm.idle) __hip_atomic_fetch_add(cm.idle, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             while (true) {
                 if (ld_rlx(&T.ctl[2])) { got = -1; break; }
                 if (part_try(cm, &b, &e)) { got = 2; break; }   // a part of a divided split first
@@ -3347,6 +3449,7 @@ __device__ __noinline__ void helper_loop(const JobDev& J0, uint32_t hid, const C
                 if (wall() - t_idle > cm.spin_ticks) { got = -1; tcount(cm, TS_IDLE_EXIT); break; }
                 __builtin_amdgcn_s_sleep(32);
             }
+            if (cm.idle) __hip_atomic_fetch_add(cm.idle, 0xFFFFFFFFu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             tadd(cm, TS_HIDLE, wall() - t_idle);
             C.go = got; C.b = b; C.e = e;
         }
@@ -3380,6 +3483,7 @@ __device__ __noinline__ void roam_loop(const JobDev* jobs, const SplitWs& w, uin
             const unsigned long long t_idle = wall();
             int got = 0;
             uint32_t b = 0, e = 0, jj = j;
+            if (cm.idle) __hip_atomic_fetch_add(cm.idle, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             while (true) {
                 if (part_try(cm, &b, &e)) { got = 2; break; }   // a part of a divided split first
                 uint32_t live = 0;
@@ -3396,6 +3500,7 @@ __device__ __noinline__ void roam_loop(const JobDev* jobs, const SplitWs& w, uin
                 if ((!live && !(cm.parts && ld_rlx(cm.part_open))) || wall() - t_idle > cm.spin_ticks) { got = -1; break; }
                 __builtin_amdgcn_s_sleep(32);
             }
+            if (cm.idle) __hip_atomic_fetch_add(cm.idle, 0xFFFFFFFFu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             tadd(cm, TS_RIDLE, wall() - t_idle);
             C.go = got; C.b = b; C.e = e; C.j = jj;
         }
@@ -3424,7 +3529,9 @@ __device__ __noinline__ void roam_loop(const JobDev* jobs, const SplitWs& w, uin
 // (scratch reloads, each a vmcnt(0) wait).
 // calculateColumnWeigths' per-column weights of columns [vb, ve) (the part
 // a job's helper can take; colw_finish adds the average afterwards)
-__device__ __noinline__ void colw_raw(const JobDev& J, const Common& cm, Ctl& C, uint32_t vb, uint32_t ve)
+// (JV: the job, or a part's view of it -- rows, locality weights, colw)
+template <class JV>
+__device__ __noinline__ void colw_raw(const JV& J, const Common& cm, Ctl& C, uint32_t vb, uint32_t ve)
 {
     const int tid = threadIdx.x, wave = tid >> 6;
     const uint32_t lane = (uint32_t)(tid & 63);
@@ -3661,10 +3768,15 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
     }
     __syncthreads();
     const bool tsu = cm.team_setup && cm.team > 1 && J.team.helpers != 0;
-    if (tsu) {
+    // column ranges on idle workgroups (colw_parts) for wide jobs: the
+    // helper's half is claimed first so that nobody computes it twice
+    const bool cparts = cm.parts && cm.proj_min && N >= cm.proj_min && (R > 256 ? cm.part_min_tall : cm.part_min);
+    if (tsu && cparts && su_claim(J.team, kSuColw, C)) {
+        if (!colw_parts(J, cm, C, 0, N, pool)) colw_raw(J, cm, C, 0, N);
+    } else if (tsu) {
         // the first half here, the second on the job's helper unless it
         // has not claimed it yet
-        colw_raw(J, cm, C, 0, N / 2);
+        if (!(cparts && colw_parts(J, cm, C, 0, N / 2, pool))) colw_raw(J, cm, C, 0, N / 2);
         if (su_claim(J.team, kSuColw, C)) {
             colw_raw(J, cm, C, N / 2, N);
         } else if (!su_wait(J.team, kSuColw, cm, C)) {
@@ -3673,7 +3785,7 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
             C.err = 1;
         }
         __syncthreads();
-    } else {
+    } else if (!(cparts && colw_parts(J, cm, C, 0, N, pool))) {
         colw_raw(J, cm, C, 0, N);
     }
     colw_finish(J, cm, C);
@@ -4128,8 +4240,8 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
         }
     }
     char* tarena = nullptr;
-    size_t tbytes = 0, board_off = 0, board_ctl = 0, slot_T = 0;
-    uint32_t nslots = 0, part_min = 0, part_blk = 4;
+    size_t tbytes = 0, board_off = 0, board_ctl = 0, slot_T = 0, slot_Ts = 0, board_T = 0;
+    uint32_t nslots = 0, nbig = 0, nsmall = 0, small_cap = 0, part_min = 0, part_min_tall = 0, part_blk = 4;
     if (team_on) {
         auto helper_bytes = [&](uint32_t R) {
             return align_up((size_t)R * 4) + align_up((size_t)6 * R * 8) +
@@ -4145,22 +4257,41 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
         // each slot's block totals (4 x 64-row blocks x N doubles; only the
         // control words are cleared per launch)
         board_off = tbytes;
+        // jobs of <= 256 rows: divided splits only where workgroups idle --
+        // with about a third as many jobs as resident workgroups or more the
+        // launch is busy and the one-workgroup engines do more per CU
+        // (C4 at N = 1: 305 against 312-320 ms with parts)
         const char* pm = std::getenv("ALVRL_PART_MIN");
-        part_min = pm ? (uint32_t)std::max(0, std::atoi(pm)) : 4096u;
+        part_min = pm ? (uint32_t)std::max(0, std::atoi(pm)) : (njobs * 3u > njobs * G + nroam ? 0u : 4096u);
+        const char* pt = std::getenv("ALVRL_PART_MIN_TALL");
+        part_min_tall = pt ? (uint32_t)std::max(0, std::atoi(pt)) : (pm ? std::min(part_min, 257u) : 257u);
         const char* pb = std::getenv("ALVRL_PART_BLK");
         part_blk = pb ? (uint32_t)std::min(std::max(1, std::atoi(pb)), (int)kPartMaxBlk) : 4u;
-        if (part_min) {
+        if (part_min || (part_min_tall && Rmax > 256)) {
+            // big slots (any split, up to N columns) within ALVRL_PART_MB (default
+            // 16 GB, at most a quarter of the free memory), small ones (up to
+            // ALVRL_PART_SMALL columns) for the many mid-size splits of tall jobs
             const char* ps = std::getenv("ALVRL_PART_SLOTS");
             const char* pmb = std::getenv("ALVRL_PART_MB");
-            slot_T = align_up((size_t)4 * ((Rmax + 63) / 64) * N * 8);
-            const size_t budget = (pmb ? (size_t)std::max(1, std::atoi(pmb)) : 8192u) << 20;
-            nslots = (uint32_t)std::min<size_t>(ps ? (size_t)std::max(0, std::atoi(ps)) : 64u, budget / slot_T);
-            nslots = std::min<uint32_t>(nslots, njobs * G + nroam);
+            const char* psc = std::getenv("ALVRL_PART_SMALL");
+            const size_t nbk = (Rmax + 63) / 64;
+            slot_T = align_up((size_t)4 * nbk * N * 8);
+            small_cap = std::min<uint32_t>(psc ? (uint32_t)std::max(0, std::atoi(psc)) : 16384u, (uint32_t)N);
+            slot_Ts = align_up((size_t)4 * nbk * std::max<uint32_t>(small_cap, 1u) * 8);
+            size_t budget = (pmb ? (size_t)std::max(1, std::atoi(pmb)) : 16384u) << 20;
+            size_t fr = 0, tot = 0;
+            if (!pmb && hipMemGetInfo(&fr, &tot) == hipSuccess) budget = std::min(budget, fr / 4);
+            const uint32_t wgs = njobs * G + nroam;
+            nbig = (uint32_t)std::min<size_t>(ps ? (size_t)std::max(0, std::atoi(ps)) : 64u, budget / slot_T);
+            nbig = std::min<uint32_t>(nbig, wgs);
+            nsmall = small_cap < N ? std::min<uint32_t>(wgs, (uint32_t)std::min<size_t>(256u, (budget / 8) / slot_Ts)) : 0u;
+            nslots = nbig + nsmall;
         }
-        board_ctl = nslots ? align_up((size_t)nslots * sizeof(PartSlot)) + align_up(4) : 0;
-        if (arena_get(&ar.tarena, &ar.tarena_cap, tbytes + board_ctl + nslots * slot_T, cache != nullptr) != hipSuccess) {
+        board_ctl = nslots ? align_up((size_t)nslots * sizeof(PartSlot)) + align_up(8) : 0;
+        board_T = nbig * slot_T + nsmall * slot_Ts;
+        if (arena_get(&ar.tarena, &ar.tarena_cap, tbytes + board_ctl + board_T, cache != nullptr) != hipSuccess) {
             (void)hipGetLastError();
-            nslots = 0; board_ctl = 0;   // without the board
+            nslots = nbig = nsmall = 0; board_ctl = board_T = 0;   // without the board
             if (arena_get(&ar.tarena, &ar.tarena_cap, tbytes, cache != nullptr) != hipSuccess) {
                 (void)hipGetLastError(); G = 1; nroam = 0;
             }
@@ -4284,19 +4415,28 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
         }
     }
     cm.parts = nullptr; cm.nslots = 0; cm.part_min = part_min; cm.part_blk = part_blk; cm.part_open = nullptr;
+    cm.nbig = 0; cm.small_cap = 0; cm.idle = nullptr;
+    {
+        const char* im = std::getenv("ALVRL_PART_IDLE");
+        cm.idle_min = im ? (uint32_t)std::max(0, std::atoi(im)) : 1u;
+    }
+    cm.part_min_tall = part_min_tall;
     {
         const char* pm = std::getenv("ALVRL_PROJ_MIN");
-        cm.proj_min = pm ? (uint32_t)std::max(0, std::atoi(pm)) : (part_min ? 16384u : 0u);
+        cm.proj_min = pm ? (uint32_t)std::max(0, std::atoi(pm)) : 16384u;
         const char* pc = std::getenv("ALVRL_PROJ_CPP");
         cm.proj_cpp = pc ? (uint32_t)std::max(64, std::atoi(pc)) : 16384u;
     }
     std::vector<PartSlot> h_slots;
-    if (tarena && nslots && part_min) {
+    if (tarena && nslots) {
         cm.parts = (PartSlot*)(tarena + board_off);
         cm.part_open = (uint32_t*)(tarena + board_off + align_up((size_t)nslots * sizeof(PartSlot)));
-        cm.nslots = nslots;
+        cm.idle = cm.part_open + 1;
+        cm.nslots = nslots; cm.nbig = nbig; cm.small_cap = small_cap;
         h_slots.assign(nslots, PartSlot{});
-        for (uint32_t k = 0; k < nslots; k++) h_slots[k].T = (double*)(tarena + board_off + board_ctl + k * slot_T);
+        for (uint32_t k = 0; k < nslots; k++)
+            h_slots[k].T = (double*)(tarena + board_off + board_ctl +
+                                     (k < nbig ? k * slot_T : nbig * slot_T + (k - nbig) * slot_Ts));
     }
     cm.init_vrls = d_init; cm.init_off = d_init_off; cm.ninit = ninit;
     cm.seed = seed; cm.pass = pass;
@@ -4422,9 +4562,11 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
             std::fprintf(stderr, "[refine team] speculative splits' hand-offs, wall ms summed: acquire %.1f, release %.1f "
                          "(%.2f / %.2f us each)\n", h[TS_ACQ] * 1e-5, h[TS_REL] * 1e-5,
                          h[TS_HSTART] ? h[TS_ACQ] * 1e-2 / h[TS_HSTART] : 0.0, h[TS_HSTART] ? h[TS_REL] * 1e-2 / h[TS_HSTART] : 0.0);
-            std::fprintf(stderr, "[refine team] split parts: %u slots, min %u columns, %u blocks per part | divided "
+            std::fprintf(stderr, "[refine team] split parts: %u slots (%u for any split, %u up to %u columns), min %u / %u "
+                         "(> 256 rows) columns, %u blocks per part | divided "
                          "splits %llu (no free slot %llu), parts by owner %llu, by others %llu, owner wait ms summed %.1f\n",
-                         cm.nslots, cm.part_min, cm.part_blk, h[TS_PSPLIT], h[TS_PSOLO], h[TS_POWN], h[TS_POTHER],
+                         cm.nslots, cm.nbig, cm.nslots - cm.nbig, cm.small_cap, cm.part_min, cm.part_min_tall, cm.part_blk,
+                         h[TS_PSPLIT], h[TS_PSOLO], h[TS_POWN], h[TS_POTHER],
                          h[TS_PWAIT] * 1e-5);
         }
         hipFree(cm.tstat);

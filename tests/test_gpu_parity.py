@@ -440,12 +440,15 @@ def test_refine_bit_exact_split_parts(oracle, gpu_ok, monkeypatch, capfd, blk, p
     """Every split of more than 256 columns divided into parts (split_parts:
     one part per variance pass and group of `blk` row blocks, run by idle
     workgroups, the block totals added in block order by the split's owner),
-    and with proj > 0 the projections of every split of >= proj columns in
-    64-column ranges (proj_parts): device == oracle, bit for bit, and some
-    parts ran on other workgroups."""
+    the initial clusters' variances of the jobs above 256 rows by row groups
+    (init_parts), and with proj > 0 the projections of every split of >= proj
+    columns and the column weights in 64-column ranges (proj_parts,
+    colw_parts): device == oracle, bit for bit, and some parts ran on other
+    workgroups."""
     import re
     torch = _torch()
     monkeypatch.setenv("ALVRL_PART_MIN", "64")
+    monkeypatch.setenv("ALVRL_PART_IDLE", "0")
     monkeypatch.setenv("ALVRL_PART_BLK", str(blk))
     monkeypatch.setenv("ALVRL_PROJ_MIN", str(proj))
     monkeypatch.setenv("ALVRL_PROJ_CPP", "64")
