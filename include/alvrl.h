@@ -158,9 +158,14 @@ ALVRL_API uint32_t alvrl_num_vrls(const alvrl_ctx *ctx);
 /* Replaces m_ci->m_selectedVrls / m_clusterWeight / m_fallBackVrls /
  * m_fallBackWeight (vrlClusterInfo, :17-115; written by buildClusters at :341-346).
  * CSR on the host: slice s uses reps[slice_off[s] .. slice_off[s+1]).  The
- * device lists are overwritten in place: the call first waits for every
- * launch on the device (hipDeviceSynchronize), so a gather still reading the
- * previous lists on any stream -- the caller's included -- finishes first. */
+ * device lists are overwritten in place.  The call takes the context's state
+ * lock exclusively (the gathers and R builds hold it shared from their checks
+ * to their enqueue, so none is enqueued during the update) and then waits for
+ * the whole device (hipDeviceSynchronize): a gather still reading the
+ * previous lists on any stream -- the caller's included -- finishes first.
+ * That wait also waits for unrelated work on other streams of the device
+ * (e.g. a collective in flight); call it between passes, as the prepass does.
+ * alvrl_upload_vrls and alvrl_set_occluders behave the same way. */
 ALVRL_API int alvrl_set_clusters(alvrl_ctx *ctx, uint32_t nslices, const uint32_t *slice_off,
                                  const uint32_t *reps, const float *weights,
                                  const uint32_t *fb_reps, const float *fb_weights, uint32_t n_fb);

@@ -15,6 +15,7 @@
 #include <cstring>
 #include <memory>
 #include <mutex>
+#include <shared_mutex>
 #include <string>
 #include <thread>
 #include <unordered_map>
@@ -148,6 +149,11 @@ struct alvrl_ctx {
     uint32_t* d_bvh_ids = nullptr;
     RefineArenas refine_arenas;   // alvrl_refine's device scratch, reused across passes
     std::mutex mu;
+    // launches that read the context's device state (VRLs, cluster lists,
+    // occluders) hold it shared from their checks to their enqueue; calls
+    // that overwrite that state hold it exclusively and then wait for the
+    // device, so no launch is enqueued between that wait and the overwrite
+    std::shared_mutex state_mu;
     std::mutex slots_mu;
     std::unordered_map<std::thread::id, std::unique_ptr<ThreadSlot>> slots;
 };
@@ -167,6 +173,12 @@ static ThreadSlot* slot_of(alvrl_ctx* c, hipError_t* e)
     return p.get();
 }
 
+#define STATE_SHARED(c)                                                                         \
+    std::shared_lock<std::shared_mutex> state_;                                                 \
+    if (c) state_ = std::shared_lock<std::shared_mutex>((c)->state_mu)
+#define STATE_EXCLUSIVE(c)                                                                      \
+    std::unique_lock<std::shared_mutex> state_;                                                 \
+    if (c) state_ = std::unique_lock<std::shared_mutex>((c)->state_mu)
 #define SLOT(c, t)                                                                              \
     ThreadSlot* t = nullptr;                                                                    \
     do {                                                                                        \
@@ -313,6 +325,7 @@ ALVRL_API int alvrl_set_medium(alvrl_ctx* c, const alvrl_medium_desc* m)
 
 ALVRL_API int alvrl_set_occluders(alvrl_ctx* c, const float* tris, uint32_t ntri, const uint32_t* material)
 {
+    STATE_EXCLUSIVE(c);
     if (!c || (!tris && ntri)) return fail(ALVRL_ERR_INVALID, "alvrl_set_occluders: null argument");
     HIPCHK(hipSetDevice(c->cfg.device));
     HIPCHK(hipDeviceSynchronize());   // no gather on any stream still reads the old BVH
@@ -347,6 +360,7 @@ ALVRL_API uint32_t alvrl_num_vrls(const alvrl_ctx* c) { return c ? c->nvrl : 0; 
 
 ALVRL_API int alvrl_upload_vrls(alvrl_ctx* c, const float* soa, uint32_t n, uint64_t pc, int on_dev)
 {
+    STATE_EXCLUSIVE(c);
     if (!c || (!soa && n)) return fail(ALVRL_ERR_INVALID, "alvrl_upload_vrls: null argument");
     if (n > 0 && pc == 0) return fail(ALVRL_ERR_INVALID, "alvrl_upload_vrls: particle_count must be > 0");
     HIPCHK(hipSetDevice(c->cfg.device));
@@ -376,6 +390,7 @@ ALVRL_API int alvrl_set_clusters(alvrl_ctx* c, uint32_t nslices, const uint32_t*
                                  const uint32_t* reps, const float* weights,
                                  const uint32_t* fb_reps, const float* fb_w, uint32_t n_fb)
 {
+    STATE_EXCLUSIVE(c);
     if (!c || (!slice_off && nslices)) return fail(ALVRL_ERR_INVALID, "alvrl_set_clusters: null argument");
     HIPCHK(hipSetDevice(c->cfg.device));
     // the lists' device buffers are reused: every gather or false-colour
@@ -435,6 +450,7 @@ static int check_ready(alvrl_ctx* c, const char* fn)
 ALVRL_API int alvrl_gather_brute(alvrl_ctx* c, const alvrl_gather_rec* d_recs, const uint32_t* d_ids,
                                  uint32_t nrec, float* d_out, void* stream)
 {
+    STATE_SHARED(c);
     int rc = check_ready(c, "alvrl_gather_brute");
     if (rc) return rc;
     if (nrec && (!d_recs || !d_out)) return fail(ALVRL_ERR_INVALID, "alvrl_gather_brute: null buffer");
@@ -455,6 +471,7 @@ ALVRL_API int alvrl_gather_clustered(alvrl_ctx* c, const alvrl_gather_rec* d_rec
                                      const alvrl_work_item* d_items, uint32_t nitems, float* d_out,
                                      void* stream)
 {
+    STATE_SHARED(c);
     int rc = check_ready(c, "alvrl_gather_clustered");
     if (rc) return rc;
     if (!c->clusters_set) return fail(ALVRL_ERR_STATE, "alvrl_gather_clustered: alvrl_set_clusters not called");
@@ -477,6 +494,7 @@ ALVRL_API int alvrl_gather_false_color(alvrl_ctx* c, int mode, const alvrl_gathe
                                        const alvrl_work_item* d_items, uint32_t n, float* d_out_rgb,
                                        void* stream)
 {
+    STATE_SHARED(c);
     int rc = check_ready(c, "alvrl_gather_false_color");
     if (rc) return rc;
     if (mode != ALVRL_FALSE_COLOR_NUM_VRLS && mode != ALVRL_FALSE_COLOR_SLICES)
@@ -509,6 +527,7 @@ ALVRL_API uint32_t alvrl_make_work_items(const uint32_t* sl, uint32_t nrec, alvr
 ALVRL_API int alvrl_build_R(alvrl_ctx* c, const alvrl_gather_rec* d_recs, const uint32_t* d_ids,
                             uint32_t nrows, float* d_Rt, uint64_t ld, uint64_t row0, void* stream)
 {
+    STATE_SHARED(c);
     int rc = check_ready(c, "alvrl_build_R");
     if (rc) return rc;
     if (nrows && (!d_recs || !d_Rt)) return fail(ALVRL_ERR_INVALID, "alvrl_build_R: null buffer");
@@ -538,6 +557,7 @@ ALVRL_API int alvrl_build_R_blocks(alvrl_ctx* c, const alvrl_gather_rec* d_recs,
                                    uint32_t nrows, float* d_Rt, const uint64_t* d_row_off,
                                    const uint32_t* d_row_stride, uint8_t* d_nonzero, void* stream)
 {
+    STATE_SHARED(c);
     int rc = check_ready(c, "alvrl_build_R_blocks");
     if (rc) return rc;
     if (nrows && (!d_recs || !d_Rt || !d_row_off || !d_row_stride))
@@ -730,6 +750,7 @@ static size_t carve(size_t* at, size_t bytes)
 ALVRL_API int alvrl_gather_brute_host(alvrl_ctx* c, const alvrl_gather_rec* recs, const uint32_t* ids,
                                       uint32_t nrec, float* out)
 {
+    STATE_SHARED(c);
     int rc = check_ready(c, "alvrl_gather_brute_host");
     if (rc) return rc;
     if (nrec == 0) return ALVRL_OK;
@@ -766,6 +787,7 @@ ALVRL_API int alvrl_gather_clustered_host(alvrl_ctx* c, const alvrl_gather_rec* 
                                           const uint32_t* ids, const uint32_t* slice_of_rec,
                                           uint32_t nrec, float* out)
 {
+    STATE_SHARED(c);
     int rc = check_ready(c, "alvrl_gather_clustered_host");
     if (rc) return rc;
     if (!c->clusters_set) return fail(ALVRL_ERR_STATE, "alvrl_gather_clustered_host: alvrl_set_clusters not called");

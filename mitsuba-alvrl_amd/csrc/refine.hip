@@ -201,7 +201,8 @@ struct Common {
     PartSlot* parts;               // the part board (null: splits are never divided)
     uint32_t nslots;               // its slots
     uint32_t part_min;             // smallest split (columns) divided into parts
-    uint32_t part_blk;             // 64-row blocks per part (<= 7)
+    uint32_t part_blk;             // 64-row blocks per part (<= 7), jobs of more than 256 rows
+    uint32_t part_blk_short;       // ... and of <= 256 rows
     uint32_t* part_open;           // slots with parts not yet claimed (a hint for idle workgroups)
     uint32_t* idle;                // helpers and roamers waiting for work (parts are published only if some are)
     uint32_t idle_min;             // ... at least this many (0: always)
@@ -2038,7 +2039,7 @@ __device__ void variance_passes(const JobDev& J, const Common& cm, Ctl& C, const
     if (fu0 && npass == 2 && cm.parts && cm.var_v3 && pmin && m >= pmin &&
         split_parts(J, cm, C, base, m, fu0, fi0, fu1, fi1, pool))
         return;
-    if (!fu0 && npass == 1 && cm.parts && cm.var_v3 && cm.part_min_tall && m >= cm.part_min_tall && J.nrows > 256 &&
+    if (!fu0 && npass == 1 && cm.parts && cm.var_v3 && pmin && m >= pmin &&
         init_parts(J, cm, C, base, m, pool))
         return;
     const uint32_t NB = (J.nrows + 63) / 64;
@@ -3009,7 +3010,8 @@ __device__ __noinline__ bool split_parts(const JobDev& J, const Common& cm, Ctl&
     if (sl < 0) return false;
     unsigned long long* const cw = J.keys1;
     gather_cw(J, base, m, cw);
-    const uint32_t nblk = (J.nrows + 63) / 64, pblk = min(max(cm.part_blk, 1u), kPartMaxBlk);
+    const uint32_t nblk = (J.nrows + 63) / 64,
+                   pblk = min(max(J.nrows > 256 ? cm.part_blk : cm.part_blk_short, 1u), kPartMaxBlk);
     PartJob pj = part_job(J);
     pj.kind = kPartVar; pj.cw = cw; pj.m = m; pj.nblk = nblk; pj.pblk = pblk;
     pj.np = 2 * ((nblk + pblk - 1) / pblk);
@@ -3072,7 +3074,8 @@ __device__ __noinline__ bool init_parts(const JobDev& J, const Common& cm, Ctl& 
     const int sl = part_slot_take(cm, C, 0u);
     if (sl < 0) return false;
     gather_cw(J, base, m, J.keys1);
-    const uint32_t nblk = (J.nrows + 63) / 64, pblk = min(max(cm.part_blk, 1u), kPartMaxBlk);
+    const uint32_t nblk = (J.nrows + 63) / 64,
+                   pblk = min(max(J.nrows > 256 ? cm.part_blk : cm.part_blk_short, 1u), kPartMaxBlk);
     PartJob pj = part_job(J);
     pj.kind = kPartInit; pj.cw = J.keys1; pj.m = m; pj.nblk = nblk; pj.pblk = pblk;
     pj.np = (nblk + pblk - 1) / pblk;
@@ -4416,6 +4419,10 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
     }
     cm.parts = nullptr; cm.nslots = 0; cm.part_min = part_min; cm.part_blk = part_blk; cm.part_open = nullptr;
     cm.nbig = 0; cm.small_cap = 0; cm.idle = nullptr;
+    {
+        const char* pbs = std::getenv("ALVRL_PART_BLK_SHORT");
+        cm.part_blk_short = pbs ? (uint32_t)std::min(std::max(1, std::atoi(pbs)), (int)kPartMaxBlk) : 2u;
+    }
     {
         const char* im = std::getenv("ALVRL_PART_IDLE");
         cm.idle_min = im ? (uint32_t)std::max(0, std::atoi(im)) : 1u;

@@ -450,6 +450,7 @@ def test_refine_bit_exact_split_parts(oracle, gpu_ok, monkeypatch, capfd, blk, p
     monkeypatch.setenv("ALVRL_PART_MIN", "64")
     monkeypatch.setenv("ALVRL_PART_IDLE", "0")
     monkeypatch.setenv("ALVRL_PART_BLK", str(blk))
+    monkeypatch.setenv("ALVRL_PART_BLK_SHORT", str(blk))
     monkeypatch.setenv("ALVRL_PROJ_MIN", str(proj))
     monkeypatch.setenv("ALVRL_PROJ_CPP", "64")
     monkeypatch.setenv("ALVRL_REFINE_TEAM_STATS", "1")
