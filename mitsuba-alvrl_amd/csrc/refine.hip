@@ -206,6 +206,7 @@ struct Common {
     uint32_t* part_open;           // slots with parts not yet claimed (a hint for idle workgroups)
     uint32_t* idle;                // helpers and roamers waiting for work (parts are published only if some are)
     uint32_t idle_min;             // ... at least this many (0: always)
+    uint32_t idle_min_short;       // ... for jobs of <= 256 rows
     uint32_t part_min_tall;        // the same for jobs of more than 256 rows
     uint32_t nbig;                 // slots [0, nbig) hold splits of any size, the rest up to small_cap columns
     uint32_t small_cap;
@@ -2900,12 +2901,13 @@ __device__ __noinline__ void run_part(const Common& cm, Ctl& C, uint32_t s, uint
 // Every thread: a free slot of the board whose block-total buffer holds a
 // split of `cols` columns (0: none needed), or -1.  Slots [0, nbig) hold any
 // split, the others up to small_cap columns; small needs try those first.
-__device__ int part_slot_take(const Common& cm, Ctl& C, uint32_t cols)
+__device__ int part_slot_take(const Common& cm, Ctl& C, uint32_t cols, uint32_t rows)
 {
     if (threadIdx.x == 0) {
         int got = -1;
-        // nobody idle to take parts (a busy launch): the one-workgroup engines
-        const bool idle = cm.idle_min == 0 || ld_rlx(cm.idle) >= cm.idle_min;
+        // too few workgroups idle to take parts: the one-workgroup engines
+        const uint32_t imin = rows > 256 ? cm.idle_min : cm.idle_min_short;
+        const bool idle = imin == 0 || ld_rlx(cm.idle) >= imin;
         auto scan = [&](uint32_t lo, uint32_t hi) {
             if (hi <= lo) return;
             const uint32_t n = hi - lo;
@@ -3006,7 +3008,7 @@ __device__ __noinline__ bool split_parts(const JobDev& J, const Common& cm, Ctl&
                             float* fu0, float* fi0, float* fu1, float* fi1, unsigned char* pool)
 {
     const int tid = threadIdx.x;
-    const int sl = part_slot_take(cm, C, m);
+    const int sl = part_slot_take(cm, C, m, J.nrows);
     if (sl < 0) return false;
     unsigned long long* const cw = J.keys1;
     gather_cw(J, base, m, cw);
@@ -3037,7 +3039,7 @@ __device__ __noinline__ bool split_parts(const JobDev& J, const Common& cm, Ctl&
 // of the cluster on idle workgroups.  False when no slot is free.
 __device__ __noinline__ bool proj_parts(const JobDev& J, const Common& cm, Ctl& C, uint32_t begin, uint32_t m, unsigned char* pool)
 {
-    const int sl = part_slot_take(cm, C, 0u);
+    const int sl = part_slot_take(cm, C, 0u, J.nrows);
     if (sl < 0) return false;
     PartJob pj = part_job(J);
     pj.kind = kPartProj; pj.ids = J.vrls + begin; pj.dir = J.dir; pj.keys = J.keys0; pj.m = m;
@@ -3053,7 +3055,7 @@ __device__ __noinline__ bool proj_parts(const JobDev& J, const Common& cm, Ctl& 
 __device__ __noinline__ bool colw_parts(const JobDev& J, const Common& cm, Ctl& C, uint32_t vb, uint32_t ve,
                                         unsigned char* pool)
 {
-    const int sl = part_slot_take(cm, C, 0u);
+    const int sl = part_slot_take(cm, C, 0u, J.nrows);
     if (sl < 0) return false;
     PartJob pj = part_job(J);
     pj.kind = kPartColw; pj.colw = J.colw; pj.c0 = vb; pj.m = ve;
@@ -3071,7 +3073,7 @@ __device__ __noinline__ bool colw_parts(const JobDev& J, const Common& cm, Ctl& 
 __device__ __noinline__ bool init_parts(const JobDev& J, const Common& cm, Ctl& C, const uint32_t* base, uint32_t m,
                                         unsigned char* pool)
 {
-    const int sl = part_slot_take(cm, C, 0u);
+    const int sl = part_slot_take(cm, C, 0u, J.nrows);
     if (sl < 0) return false;
     gather_cw(J, base, m, J.keys1);
     const uint32_t nblk = (J.nrows + 63) / 64,
@@ -4245,6 +4247,7 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
     char* tarena = nullptr;
     size_t tbytes = 0, board_off = 0, board_ctl = 0, slot_T = 0, slot_Ts = 0, board_T = 0;
     uint32_t nslots = 0, nbig = 0, nsmall = 0, small_cap = 0, part_min = 0, part_min_tall = 0, part_blk = 4;
+    bool busy_launch = false;
     if (team_on) {
         auto helper_bytes = [&](uint32_t R) {
             return align_up((size_t)R * 4) + align_up((size_t)6 * R * 8) +
@@ -4260,12 +4263,10 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
         // each slot's block totals (4 x 64-row blocks x N doubles; only the
         // control words are cleared per launch)
         board_off = tbytes;
-        // jobs of <= 256 rows: divided splits only where workgroups idle --
-        // with about a third as many jobs as resident workgroups or more the
-        // launch is busy and the one-workgroup engines do more per CU
-        // (C4 at N = 1: 305 against 312-320 ms with parts)
+        // (a busy launch gates the short jobs' parts on many idle workgroups, below)
         const char* pm = std::getenv("ALVRL_PART_MIN");
-        part_min = pm ? (uint32_t)std::max(0, std::atoi(pm)) : (njobs * 3u > njobs * G + nroam ? 0u : 4096u);
+        part_min = pm ? (uint32_t)std::max(0, std::atoi(pm)) : 4096u;
+        busy_launch = njobs * 3u > njobs * G + nroam;
         const char* pt = std::getenv("ALVRL_PART_MIN_TALL");
         part_min_tall = pt ? (uint32_t)std::max(0, std::atoi(pt)) : (pm ? std::min(part_min, 257u) : 257u);
         const char* pb = std::getenv("ALVRL_PART_BLK");
@@ -4426,6 +4427,12 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
     {
         const char* im = std::getenv("ALVRL_PART_IDLE");
         cm.idle_min = im ? (uint32_t)std::max(0, std::atoi(im)) : 1u;
+        // jobs of <= 256 rows in a busy launch (about a third as many jobs as
+        // resident workgroups or more): divided only when many workgroups
+        // idle, as in the launch's tail -- the one-workgroup engines do more
+        // per CU (C4 at N = 1: 305 against 312-320 ms with parts throughout)
+        const char* ims = std::getenv("ALVRL_PART_IDLE_SHORT");
+        cm.idle_min_short = ims ? (uint32_t)std::max(0, std::atoi(ims)) : (busy_launch ? 16u : cm.idle_min);
     }
     cm.part_min_tall = part_min_tall;
     {

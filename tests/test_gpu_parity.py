@@ -449,6 +449,7 @@ def test_refine_bit_exact_split_parts(oracle, gpu_ok, monkeypatch, capfd, blk, p
     torch = _torch()
     monkeypatch.setenv("ALVRL_PART_MIN", "64")
     monkeypatch.setenv("ALVRL_PART_IDLE", "0")
+    monkeypatch.setenv("ALVRL_PART_IDLE_SHORT", "0")
     monkeypatch.setenv("ALVRL_PART_BLK", str(blk))
     monkeypatch.setenv("ALVRL_PART_BLK_SHORT", str(blk))
     monkeypatch.setenv("ALVRL_PROJ_MIN", str(proj))
