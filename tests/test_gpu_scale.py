@@ -29,6 +29,7 @@ from test_gpu_parity import _assert_close
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.timeout(900)
 def test_c5_end_to_end(oracle, gpu_ok, tmp_path):
     import torch
     import alvrl
