@@ -12,6 +12,20 @@
 // kernels are VALU/transcendental-bound; HBM traffic per pair is << 1 B.
 #include "vrl_device.hpp"
 
+// Resident blocks of 256 per CU the render gathers are compiled for: 4
+// (128 VGPRs, four waves per SIMD; a few bytes spilled).  With the two
+// samples side by side the compiler's own choice is 139 VGPRs, three waves:
+// C2 5.09e10 against 5.18e10 contributions/s at four (profiles/r04/gather_ab.txt).
+// Developer A/B: -DALVRL_GATHER_MINB=n, 0 = the compiler's choice.
+#ifndef ALVRL_GATHER_MINB
+#define ALVRL_GATHER_MINB 4
+#endif
+#if ALVRL_GATHER_MINB > 0
+#define ALVRL_GATHER_BOUNDS __launch_bounds__(256, ALVRL_GATHER_MINB)
+#else
+#define ALVRL_GATHER_BOUNDS __launch_bounds__(256)
+#endif
+
 namespace alvrl {
 
 __global__ void __launch_bounds__(256) k_prepare_vrls(const float* __restrict__ soa, uint32_t n,
@@ -62,7 +76,7 @@ __device__ __forceinline__ void count_pairs(unsigned long long* counter, bool la
 }
 
 template <int NVV, int NVS, bool VIS = false>
-__global__ void __launch_bounds__(256) k_gather_brute(const Rec* __restrict__ recs,
+__global__ void ALVRL_GATHER_BOUNDS k_gather_brute(const Rec* __restrict__ recs,
                                                       const uint32_t* __restrict__ ids, uint32_t nrec,
                                                       const VrlPrep* __restrict__ vp, uint32_t nvrl,
                                                       DevParams P, float normalization,
@@ -101,7 +115,7 @@ __device__ __forceinline__ void gather_item(const Rec* __restrict__ recs, const 
                                             float* __restrict__ out, unsigned long long* counter);
 
 template <int NVV, int NVS, bool VIS = false>
-__global__ void __launch_bounds__(256) k_gather_clustered(
+__global__ void ALVRL_GATHER_BOUNDS k_gather_clustered(
     const Rec* __restrict__ recs, const uint32_t* __restrict__ ids,
     const WorkItem* __restrict__ items, uint32_t nitems, const VrlPrep* __restrict__ vp,
     const uint32_t* __restrict__ slice_off, const uint32_t* __restrict__ reps,

@@ -357,6 +357,116 @@ __device__ __forceinline__ void sinhcosh_fast(float x, float* sh, float* ch)
     *ch = small ? pc : 0.5f * (e + re);
 }
 
+// ------------------------------------------------ two samples at once --
+// The unrolled (2, 2) kernels evaluate a pair's two volVol samples, and its
+// two volSurf samples, side by side: per-sample arithmetic on float pairs
+// (v_pk_fma/mul/add_f32, two lanes' worth of FP32 per instruction), the
+// transcendentals and selects per element.  Every value is formed by the
+// same operations as the one-sample code above.
+typedef float v2f __attribute__((ext_vector_type(2)));
+struct V3 { v2f x, y, z; };
+__device__ __forceinline__ v2f v2(float a) { return v2f{a, a}; }
+__device__ __forceinline__ v2f vfma(v2f a, v2f b, v2f c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ v2f vabs(v2f a) { return __builtin_elementwise_abs(a); }
+__device__ __forceinline__ v2f vcopysign(v2f a, v2f b) { return __builtin_elementwise_copysign(a, b); }
+__device__ __forceinline__ v2f vsel(bool c0, bool c1, v2f a, v2f b) { return v2f{c0 ? a.x : b.x, c1 ? a.y : b.y}; }
+__device__ __forceinline__ v2f vrcp(v2f a) { return v2f{rcp(a.x), rcp(a.y)}; }
+
+__device__ __forceinline__ void sinhcosh2(v2f x, v2f* sh, v2f* ch)
+{
+    const v2f ax = vabs(x);
+    const v2f x2 = ax * ax;
+    const v2f ps = vfma(ax * x2, vfma(x2, vfma(x2, v2(1.0f / 5040.0f), v2(1.0f / 120.0f)), v2(1.0f / 6.0f)), ax);
+    const v2f pc = vfma(x2, vfma(x2, vfma(x2, v2(1.0f / 720.0f), v2(1.0f / 24.0f)), v2(0.5f)), v2(1.0f));
+    const v2f ph = ax * kLog2e;
+    const v2f pl = vfma(ax, v2(kLog2e), -ph) + ax * kLog2eLo;
+    const v2f e = v2f{__builtin_amdgcn_exp2f(ph.x), __builtin_amdgcn_exp2f(ph.y)} * vfma(pl, v2(kLn2), v2(1.0f));
+    const v2f re = vrcp(e);
+    const bool s0 = ax.x < 0.25f, s1 = ax.y < 0.25f;
+    *sh = vcopysign(vsel(s0, s1, ps, 0.5f * (e - re)), x);
+    *ch = vsel(s0, s1, pc, 0.5f * (e + re));
+}
+
+__device__ __forceinline__ v2f tan2(v2f x)     // tan_fast per element
+{
+    const v2f xs = x * 0.63661977236758134308f;
+    const v2f j = v2f{rintf(xs.x), rintf(xs.y)};
+    v2f r = vfma(j, v2(-1.5703125f), x);
+    r = vfma(j, v2(-4.837512969970703125e-4f), r);
+    r = vfma(j, v2(-7.54978995489188216e-8f), r);
+    const v2f z = r * r;
+    v2f p = vfma(z, v2(9.38540185543e-3f), v2(3.11992232697e-3f));
+    p = vfma(p, z, v2(2.44301354525e-2f));
+    p = vfma(p, z, v2(5.34112807005e-2f));
+    p = vfma(p, z, v2(1.33387994085e-1f));
+    p = vfma(p, z, v2(3.33331568548e-1f));
+    const v2f t = vfma(p * z, r, r);
+    return vsel(j.x != 0.0f, j.y != 0.0f, -vrcp(t), t);
+}
+
+// atan2_fast for each element's pair (x1, x2)
+__device__ __forceinline__ void atan2_2(v2f x1, v2f x2, v2f* r1, v2f* r2)
+{
+    const v2f a1 = vabs(x1), a2 = vabs(x2);
+    const bool h10 = a1.x > 2.414213562373095f, h11 = a1.y > 2.414213562373095f;
+    const bool m10 = a1.x > 0.4142135623730950f, m11 = a1.y > 0.4142135623730950f;
+    const bool h20 = a2.x > 2.414213562373095f, h21 = a2.y > 2.414213562373095f;
+    const bool m20 = a2.x > 0.4142135623730950f, m21 = a2.y > 0.4142135623730950f;
+    const v2f n1 = vsel(h10, h11, v2(-1.0f), vsel(m10, m11, a1 - 1.0f, a1));
+    const v2f d1 = vsel(h10, h11, a1, vsel(m10, m11, a1 + 1.0f, v2(1.0f)));
+    const v2f n2 = vsel(h20, h21, v2(-1.0f), vsel(m20, m21, a2 - 1.0f, a2));
+    const v2f d2 = vsel(h20, h21, a2, vsel(m20, m21, a2 + 1.0f, v2(1.0f)));
+    const v2f rr = vrcp(d1 * d2);
+    const v2f t1 = (n1 * d2) * rr, t2 = (n2 * d1) * rr;
+    const v2f y1 = vsel(h10, h11, v2(1.57079632679489661923f), vsel(m10, m11, v2(0.78539816339744830962f), v2(0.0f)));
+    const v2f y2 = vsel(h20, h21, v2(1.57079632679489661923f), vsel(m20, m21, v2(0.78539816339744830962f), v2(0.0f)));
+    const v2f z1 = t1 * t1, z2 = t2 * t2;
+    v2f p1 = vfma(z1, v2(8.05374449538e-2f), v2(-1.38776856032e-1f));
+    v2f p2 = vfma(z2, v2(8.05374449538e-2f), v2(-1.38776856032e-1f));
+    p1 = vfma(p1, z1, v2(1.99777106478e-1f));
+    p2 = vfma(p2, z2, v2(1.99777106478e-1f));
+    p1 = vfma(p1, z1, v2(-3.33329491539e-1f));
+    p2 = vfma(p2, z2, v2(-3.33329491539e-1f));
+    *r1 = vcopysign(y1 + vfma(p1 * z1, t1, t1), x1);
+    *r2 = vcopysign(y2 + vfma(p2 * z2, t2, t2), x2);
+}
+
+struct KullaFrame2 { V3 DI; v2f Dis, rDis, dotPr, aa, ab; };
+__device__ __forceinline__ KullaFrame2 kulla_frame2(F3 A, F3 dir, float lenAB, const V3& D)
+{
+    KullaFrame2 k;
+    const V3 w{D.x - A.x, D.y - A.y, D.z - A.z};
+    k.dotPr = dir.x * w.x + dir.y * w.y + dir.z * w.z;
+    k.DI = V3{w.x - dir.x * k.dotPr, w.y - dir.y * k.dotPr, w.z - dir.z * k.dotPr};
+    const v2f l2 = k.DI.x * k.DI.x + k.DI.y * k.DI.y + k.DI.z * k.DI.z;
+    const v2f rDis = v2f{__builtin_amdgcn_rsqf(l2.x), __builtin_amdgcn_rsqf(l2.y)};
+    k.Dis = vsel(l2.x > 0.0f, l2.y > 0.0f, l2 * rDis, v2(0.0f));
+    k.rDis = rDis;
+    const v2f dAI = vabs(k.dotPr);
+    v2f aa, ab;
+    atan2_2(dAI * rDis, vabs(lenAB - k.dotPr) * rDis, &aa, &ab);
+    const bool p0 = k.dotPr.x > 0, p1 = k.dotPr.y > 0;
+    k.aa = vsel(p0, p1, -aa, aa);
+    k.ab = vsel(p0 && dAI.x > lenAB, p1 && dAI.y > lenAB, -ab, ab);
+    return k;
+}
+
+// medium_tr<false> ('balance') per element
+__device__ __forceinline__ void medium_tr2(const DevParams& P, v2f d, v2f tr[3], v2f* pf)
+{
+    const v2f nd = -d;
+    const v2f e0 = P.sigma_t[0] * nd, e1 = P.sigma_t[1] * nd, e2 = P.sigma_t[2] * nd;
+    const v2f t0 = v2f{__expf(e0.x), __expf(e0.y)};
+    const v2f t1 = v2f{__expf(e1.x), __expf(e1.y)};
+    const v2f t2 = v2f{__expf(e2.x), __expf(e2.y)};
+    v2f s = v2(0.0f);
+    s += t0; s += t1; s += t2;
+    s *= (1.0f / 3.0f);
+    *pf = s * P.w + (1 - P.w);
+    const bool z0 = fmax3(t0.x, t1.x, t2.x) < 1e-20f, z1 = fmax3(t0.y, t1.y, t2.y) < 1e-20f;
+    tr[0] = vsel(z0, z1, v2(0.0f), t0); tr[1] = vsel(z0, z1, v2(0.0f), t1); tr[2] = vsel(z0, z1, v2(0.0f), t2);
+}
+
 // Pair-constant part of sampleVtoDistance (:916-953) incl. getClosestPoints (:962-1032).
 struct NovakFrame { float sinT, rsinT, h, rh, A0, dA, dVhS, ipdf; bool parallel, zero; };
 
@@ -486,6 +596,76 @@ __device__ __forceinline__ void integrate_vrl(const DevParams& P, const RecPre& 
     const float ss0 = P.sigma_s[0], ss1 = P.sigma_s[1], ss2 = P.sigma_s[2];
 
     // ---------------- volume -> volume (:647-703) ----------------
+    if constexpr (NVV == 2 && !VIS && !WANT_STATS) {
+        // both samples side by side (see "two samples at once")
+        const v2f u0 = v2f{draw(0), draw(2)}, u1 = v2f{draw(1), draw(3)};
+        V3 V;
+        v2f ipdfV, dSV;
+        if (nf.zero) {
+            V = V3{v2(S.x), v2(S.y), v2(S.z)}; ipdfV = v2(1.0f); dSV = v2(0.0f);
+        } else if (nf.parallel) {
+            V = V3{S.x + v.vx * u0, S.y + v.vy * u0, S.z + v.vz * u0};
+            ipdfV = v2(v.len);
+            dSV = u0 * v.len;
+        } else {
+            v2f sh, ch;
+            sinhcosh2(nf.A0 + (u0 * nf.dA), &sh, &ch);
+            const v2f newV = vfma(nf.h * sh, v2(nf.rsinT), v2(nf.dVhS));
+            V = V3{S.x + SV.x * newV, S.y + SV.y * newV, S.z + SV.z * newV};
+            ipdfV = ch * nf.ipdf;
+            dSV = vabs(newV);
+        }
+        const KullaFrame2 ke = kulla_frame2(q.E, q.dirAB, q.lenAB, V);
+        const v2f t = ke.Dis * tan2(((1.0f - u1) * ke.aa) + (u1 * ke.ab));
+        const v2f l2 = vfma(ke.Dis, ke.Dis, t * t);
+        const v2f dUV = v2f{sqrtf(l2.x), sqrtf(l2.y)};
+        const v2f dEU = vabs(ke.dotPr + t);
+        const float smin = fminf(fminf(P.sigma_t[0], P.sigma_t[1]), P.sigma_t[2]);
+        const v2f sd = smin * dEU;
+        const bool zeu0 = sd.x > 46.0517019f, zeu1 = sd.y > 46.0517019f;
+        const v2f ndUE = 0.0f - (dUV + dEU);
+        v2f tue[3];
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            const v2f e = P.sigma_t[c] * ndUE;
+            tue[c] = vsel(zeu0, zeu1, v2(0.0f), v2f{__expf(e.x), __expf(e.y)});
+        }
+        v2f tsv[3], pf;
+        medium_tr2(P, dSV, tsv, &pf);
+        const v2f g = ((ke.ab - ke.aa) * ke.rDis) * ipdfV;
+        const v2f rpf = P.short_vrls ? vrcp(pf) : v2(1.0f);
+        v2f ph = v2(kInvFourPi * kInvFourPi);
+        if (hg) {
+#pragma unroll
+            for (int k = 0; k < 2; k++) {
+                const float tk = t[k], rd = rcp(dUV[k]);
+                const F3 VU = (q.dirAB * tk - f3(ke.DI.x[k], ke.DI.y[k], ke.DI.z[k])) * rd;
+                ph[k] = phase(P, neg(VU), neg(q.d)) * phase(P, neg(SV), VU);
+            }
+        }
+        const v2f gg = g * rpf * ph;
+        v2f c0 = v2(v.pr * (ss0 * ss0)), c1 = v2(v.pg * (ss1 * ss1)), c2 = v2(v.pb * (ss2 * ss2));
+        c0 *= tsv[0] * tue[0];
+        c1 *= tsv[1] * tue[1];
+        c2 *= tsv[2] * tue[2];
+        c0 *= gg; c1 *= gg; c2 *= gg;
+        if (WANT_STATS && !q.unit) { c0 *= q.w[0]; c1 *= q.w[1]; c2 *= q.w[2]; }
+#pragma unroll
+        for (int sample = 0; sample < 2; ++sample) {
+            float lumv = 0.0f;
+            const bool live = l2[sample] != 0 && (tue[0][sample] != 0 || tue[1][sample] != 0 || tue[2][sample] != 0);
+            if (live && spec_valid(c0[sample], c1[sample], c2[sample])) {
+                const float rn = 1.0f / (float)nVV;
+                tot0 += c0[sample] * rn; tot1 += c1[sample] * rn; tot2 += c2[sample] * rn;
+                lumv = luminance(c0[sample], c1[sample], c2[sample]);
+            }
+            if (WANT_STATS) {
+                const float delta = lumv - mean;
+                mean += delta / (sample + 1);
+                M2 += delta * (lumv - mean);
+            }
+        }
+    } else {
 #pragma unroll
     for (int sample = 0; sample < (NVV >= 0 ? NVV : 64); ++sample) {
         if (NVV < 0 && sample >= nVV) break;
@@ -554,6 +734,7 @@ __device__ __forceinline__ void integrate_vrl(const DevParams& P, const RecPre& 
             M2 += delta * (lumv - mean);
         }
     }
+    }
     if (WANT_STATS && nVV > 0) {
         mean_acc += mean;
         var_acc += M2 / ((nVV - 1) * nVV);
@@ -573,6 +754,57 @@ __device__ __forceinline__ void integrate_vrl(const DevParams& P, const RecPre& 
             base1 = v.pg * ss1 * q.teus[1];
             base2 = v.pb * ss2 * q.teus[2];
         }
+        if constexpr (NVS == 2 && !VIS && !WANT_STATS) {
+            // both samples side by side (see "two samples at once")
+            v2f c0 = v2(0.0f), c1 = v2(0.0f), c2 = v2(0.0f);
+            bool live0 = false, live1 = false;
+            if (q.surf) {
+                const v2f u = v2f{draw(2 * nVV), draw(2 * nVV + 1)};
+                const v2f t = ks.Dis * tan2(((1.0f - u) * ks.aa) + (u * ks.ab));
+                const v2f l2 = vfma(v2(ks.Dis), v2(ks.Dis), t * t);
+                live0 = l2.x != 0; live1 = l2.y != 0;
+                const v2f rdUV = v2f{__builtin_amdgcn_rsqf(l2.x), __builtin_amdgcn_rsqf(l2.y)};
+                const v2f dUV = l2 * rdUV;
+                const v2f ndUV = 0.0f - dUV;
+                v2f tuv[3], tsv[3], pf;
+#pragma unroll
+                for (int c = 0; c < 3; c++) {
+                    const v2f e = P.sigma_t[c] * ndUV;
+                    tuv[c] = P.sigma_t[c] != 0 ? v2f{__expf(e.x), __expf(e.y)} : v2(1.0f);
+                }
+                medium_tr2(P, vabs(ks.dotPr + t), tsv, &pf);
+                const v2f cos_wo = vfma(t, v2(sn), v2(-dn)) * rdUV;
+                const bool bz0 = q.cos_wi <= 0 || cos_wo.x <= 0, bz1 = q.cos_wi <= 0 || cos_wo.y <= 0;
+                const v2f fcos = vsel(bz0, bz1, v2(0.0f), kInvPi * cos_wo);
+                v2f phV = v2(kInvFourPi);
+                if (hg) {
+#pragma unroll
+                    for (int k = 0; k < 2; k++) phV[k] = phase(P, neg(SV), (ks.DI - SV * t[k]) * rdUV[k]);
+                }
+                const v2f rpf = P.short_vrls ? vrcp(pf) : v2(1.0f);
+                const v2f gg = gs * rpf * phV * fcos;
+                c0 = v2(base0 * q.alb[0]); c1 = v2(base1 * q.alb[1]); c2 = v2(base2 * q.alb[2]);
+                c0 *= tsv[0] * tuv[0];
+                c1 *= tsv[1] * tuv[1];
+                c2 *= tsv[2] * tuv[2];
+                c0 *= gg; c1 *= gg; c2 *= gg;
+                if (WANT_STATS && !q.unit) { c0 *= q.w[0]; c1 *= q.w[1]; c2 *= q.w[2]; }
+            }
+#pragma unroll
+            for (int sample = 0; sample < 2; ++sample) {
+                float lumv = 0.0f;
+                if ((sample == 0 ? live0 : live1) && spec_valid(c0[sample], c1[sample], c2[sample])) {
+                    const float rn = 1.0f / (float)nVS;
+                    tot0 += c0[sample] * rn; tot1 += c1[sample] * rn; tot2 += c2[sample] * rn;
+                    lumv = luminance(c0[sample], c1[sample], c2[sample]);
+                }
+                if (WANT_STATS) {
+                    const float delta = lumv - mean;
+                    mean += delta / (sample + 1);
+                    M2 += delta * (lumv - mean);
+                }
+            }
+        } else {
 #pragma unroll
         for (int sample = 0; sample < (NVS >= 0 ? NVS : 64); ++sample) {
             if (NVS < 0 && sample >= nVS) break;
@@ -614,6 +846,7 @@ __device__ __forceinline__ void integrate_vrl(const DevParams& P, const RecPre& 
                 mean += delta / (sample + 1);
                 M2 += delta * (lumv - mean);
             }
+        }
         }
         if (WANT_STATS) {
             mean_acc += mean;
