@@ -26,6 +26,10 @@
 #define ALVRL_GATHER_BOUNDS __launch_bounds__(256)
 #endif
 
+#ifndef ALVRL_RB_MINB
+#define ALVRL_RB_MINB 3   // the R build: three waves per SIMD
+#endif
+
 namespace alvrl {
 
 __global__ void __launch_bounds__(256) k_prepare_vrls(const float* __restrict__ soa, uint32_t n,
@@ -226,7 +230,7 @@ hipError_t launch_false_color(const Rec* recs, const WorkItem* items, uint32_t n
 // R build: lane = representative row, the block's 4 waves interleave over a
 // VRL chunk.  Writes Rt[v][row0 + r] = (mean * norm, var * norm * norm).
 template <int NVV, int NVS, bool VIS = false>
-__global__ void __launch_bounds__(256, 3) k_build_R(const Rec* __restrict__ recs,
+__global__ void __launch_bounds__(256, ALVRL_RB_MINB) k_build_R(const Rec* __restrict__ recs,
                                                  const uint32_t* __restrict__ ids, uint32_t nrows,
                                                  const VrlPrep* __restrict__ vp, uint32_t nvrl,
                                                  uint32_t chunk, DevParams P, float normalization,
@@ -282,7 +286,7 @@ template <int NVV, int NVS, bool VIS = false>
 // Three waves per SIMD (<= 168 VGPRs): the R build's one long FP32 chain per
 // pair hides more latency than at two (179 VGPRs, 45.2 -> 40.3 ms at C4);
 // four (128 VGPRs) spill and lose (49.3 ms)
-__global__ void __launch_bounds__(256, 3) k_build_R_blocks(const Rec* __restrict__ recs,
+__global__ void __launch_bounds__(256, ALVRL_RB_MINB) k_build_R_blocks(const Rec* __restrict__ recs,
                                                         const uint32_t* __restrict__ ids, uint32_t nrows,
                                                         const VrlPrep* __restrict__ vp, uint32_t nvrl,
                                                         uint32_t chunk, DevParams P, float normalization,

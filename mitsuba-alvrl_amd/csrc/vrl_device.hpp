@@ -363,6 +363,11 @@ __device__ __forceinline__ void sinhcosh_fast(float x, float* sh, float* ch)
 // (v_pk_fma/mul/add_f32, two lanes' worth of FP32 per instruction), the
 // transcendentals and selects per element.  Every value is formed by the
 // same operations as the one-sample code above.
+// (the R build's gathers keep the one-sample code unless ALVRL_RB_PACKED:
+// their Welford statistics leave fewer registers for the pairs)
+#ifndef ALVRL_RB_PACKED
+#define ALVRL_RB_PACKED 0
+#endif
 typedef float v2f __attribute__((ext_vector_type(2)));
 struct V3 { v2f x, y, z; };
 __device__ __forceinline__ v2f v2(float a) { return v2f{a, a}; }
@@ -596,7 +601,7 @@ __device__ __forceinline__ void integrate_vrl(const DevParams& P, const RecPre& 
     const float ss0 = P.sigma_s[0], ss1 = P.sigma_s[1], ss2 = P.sigma_s[2];
 
     // ---------------- volume -> volume (:647-703) ----------------
-    if constexpr (NVV == 2 && !VIS && !WANT_STATS) {
+    if constexpr (NVV == 2 && !VIS && (!WANT_STATS || ALVRL_RB_PACKED)) {
         // both samples side by side (see "two samples at once")
         const v2f u0 = v2f{draw(0), draw(2)}, u1 = v2f{draw(1), draw(3)};
         V3 V;
@@ -754,7 +759,7 @@ __device__ __forceinline__ void integrate_vrl(const DevParams& P, const RecPre& 
             base1 = v.pg * ss1 * q.teus[1];
             base2 = v.pb * ss2 * q.teus[2];
         }
-        if constexpr (NVS == 2 && !VIS && !WANT_STATS) {
+        if constexpr (NVS == 2 && !VIS && (!WANT_STATS || ALVRL_RB_PACKED)) {
             // both samples side by side (see "two samples at once")
             v2f c0 = v2(0.0f), c1 = v2(0.0f), c2 = v2(0.0f);
             bool live0 = false, live1 = false;
