@@ -121,6 +121,13 @@ struct PartSlot {
 constexpr unsigned long long kStSpecBit = 1ull << 63;
 constexpr uint32_t kQSpecBit = 1u << 31;
 constexpr uint32_t kQueue = 1024;
+// The leader's heap nodes carry two flags in the top bits of `end`: queued by
+// this leader (a helper may be on it: its state word decides), and its vrls
+// already in team.spec (a committed speculative split's child).  Queueing
+// needs no state-word loads; every other reader strips them (kEndMask).
+constexpr uint32_t kEndQ = 1u << 31;
+constexpr uint32_t kEndS = 1u << 30;
+constexpr uint32_t kEndMask = kEndS - 1u;
 
 struct JobDev {
     // entry (vrl v, local row r) of R is Rt[roff[r] + v * rstride[r]] (float2
@@ -306,8 +313,10 @@ struct Ctl {
     uint32_t pre_b;
     // the queue tail the leader has written slots up to; published to
     // team.ctl[1] (publish_tail) at the next split_team or stop_team
-    uint32_t qtail;
+    uint32_t qtail;        // the queue tail (always current; published at publish_tail)
     int qpend;
+    uint32_t qhead;        // a queue head seen earlier (<= the real one: a room bound)
+    uint32_t early_b;      // the cluster enqueue_early queued (its heap node is flagged), or ~0
     uint32_t* prec;        // this pop's trace record (ALVRL_POP_TRACE), or null
     // the v3 variance engine over row groups of <= 256 rows (variance_passes):
     // this call's first row, whether it is the first / last group, and the
@@ -609,7 +618,7 @@ __device__ __forceinline__ HeapRef heap_of(const JobDev& J, const Ctl& C)
 // (a single's id is read from J.vrls, or with an agent-scope load from spec:
 // a commit's range copy into J.vrls may still be in flight)
 __device__ void add_cluster(const JobDev& J, Ctl& C, uint32_t begin, uint32_t end, float uvar, float ivar,
-                            const uint32_t* spec = nullptr)
+                            const uint32_t* spec = nullptr, uint32_t flags = 0u)
 {
     if (end == begin) { C.err = 1; return; }
     if (end == begin + 1) {
@@ -618,7 +627,7 @@ __device__ void add_cluster(const JobDev& J, Ctl& C, uint32_t begin, uint32_t en
         if (uvar != 0) C.err = 1;
         C.clIntVar += ivar;
     } else {
-        CNode cn{uvar, ivar, begin, end};
+        CNode cn{uvar, ivar, begin, end | flags | (spec ? kEndS : 0u)};
         const HeapRef H = heap_of(J, C);
         hst(H, C.heap_n++, cn);
         heap_log(C, C.heap_n - 1);
@@ -651,9 +660,9 @@ __device__ __noinline__ CNode pop_wave(const JobDev& J, Ctl& C, const unsigned l
     const CNode top = hld(H, 0);
     unsigned long long sw = 0;
     PT_POP(1);
-    if (state && lane == 0)
-        sw = C.pre_b == top.begin ? C.pre_sw
-                                  : __hip_atomic_load(&gp(state)[top.begin], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // a node this leader never queued: no helper is on it (kStNone)
+    if (state && lane == 0 && (top.end & kEndQ))
+        sw = __hip_atomic_load(&gp(state)[top.begin], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (n > 1) {
         const long len = n - 1;
         const CNode value = hld(H, len);
@@ -721,7 +730,7 @@ __device__ __noinline__ CNode pop_wave(const JobDev& J, Ctl& C, const unsigned l
         C.pre_b = ~0u;
     }
     PT_POP(3);
-    return top;
+    return CNode{top.uvar, top.ivar, top.begin, top.end & kEndMask};
 }
 
 __device__ __forceinline__ uint32_t n_clusters(const Ctl& C) { return (uint32_t)(C.singles_n + C.heap_n); }
@@ -2265,13 +2274,13 @@ __device__ __noinline__ unsigned long long* sort_keys(const JobDev& J, Ctl& C, u
     return J.keys0;
 }
 
-// Projections of split() (:625-640): one wave per column, kCB columns per
-// batch, rows in the shared order (norm, then the normalised dot product with
-// the split direction).  For R <= 64*kRB the batch's entries stay in
-// registers for both sums and the next batch's loads are in flight while
-// the current one is reduced (ping-pong buffers, no copies).  Columns
-// [jb, je) of the cluster pj.ids[0..m): each column's key depends on that
-// column alone, so ranges can run on different workgroups (split parts).
+// The projections of a range of a divided split's columns (proj_parts):
+// split_projections' arithmetic over columns [jb, je) of pj.ids[0..m), each
+// column's key depends on that column alone.  (split() keeps its own
+// JobDev-based split_projections below: routing every split through this
+// function cost 10 ms of the C4 refinement -- 309 against 300 ms, same box,
+// profiles/r04/parts/r4u_summary.txt -- from the code it changed around the
+// calls, not from the projections themselves.)
 __device__ __forceinline__ RowRef row_ref(const PartJob& pj, uint32_t r)
 {
     return pj.contig ? RowRef{(size_t)(pj.off0 + r), (size_t)pj.stride0}
@@ -2379,12 +2388,107 @@ __device__ __forceinline__ PartJob part_job(const JobDev& J)
     pj.locw = J.locw; pj.nrows = J.nrows;
     return pj;
 }
-__device__ void split_projections(const JobDev& J, const Common& cm, uint32_t begin, uint32_t m)
+// Projections of split() (:625-640): one wave per column, kCB columns per
+// batch, rows in the shared order (norm, then the normalised dot product with
+// the split direction).  For R <= 64*kRB the batch's entries stay in
+// registers for both sums and the next batch's loads are in flight while
+// the current one is reduced (ping-pong buffers, no copies).
+__device__ __noinline__ void split_projections(const JobDev& J, const Common& cm, uint32_t begin, uint32_t m)
 {
-    PartJob pj = part_job(J);
-    pj.ids = J.vrls + begin; pj.dir = J.dir; pj.keys = J.keys0; pj.m = m;
-    proj_range(pj, cm, 0, m);
+    const uint32_t R = J.nrows;
+    const int wave = threadIdx.x >> 6;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t stride = kWaves * kCB;
+    const float2* const Rt = cm.Rt;                  // register copy (cm is behind a generic pointer)
+    auto* const k0 = gpw(J.keys0);
+    const auto* const vrls = gp(J.vrls);
+    const auto* const dir = gp(J.dir);
+    if (R <= 64u * kRB) {
+        float d[kRB];
+        RowRef row[kRB];
+#pragma unroll
+        for (int rb = 0; rb < kRB; rb++) {
+            const uint32_t r = lane + 64u * rb;
+            d[rb] = r < R ? dir[r] : 0.0f;
+            row[rb] = row_ref(J, r < R ? r : 0);
+        }
+        uint32_t vA[kCB], vB[kCB];
+        float xA[kRB][kCB], xB[kRB][kCB];
+        auto load = [&](uint32_t j0, uint32_t* v, float (*x)[kCB]) {
+#pragma unroll
+            for (int q = 0; q < kCB; q++) v[q] = vrls[begin + min(j0 + (uint32_t)q, m - 1)];
+#pragma unroll
+            for (int rb = 0; rb < kRB; rb++)
+#pragma unroll
+                for (int q = 0; q < kCB; q++) x[rb][q] = ldg2(Rt, row[rb].base + (size_t)v[q] * row[rb].stride).x;
+        };
+        auto reduce = [&](uint32_t j0, const uint32_t* v, float (*x)[kCB]) {
+            float pn[kCB], pp[kCB];
+#pragma unroll
+            for (int q = 0; q < kCB; q++) { pn[q] = 0.0f; pp[q] = 0.0f; }
+#pragma unroll
+            for (int rb = 0; rb < kRB; rb++)
+                if (lane + 64u * rb < R) {
+#pragma unroll
+                    for (int q = 0; q < kCB; q++) { const float a = fabsf(x[rb][q]); pn[q] = pn[q] + a * a; }
+                }
+            tree_fn<kCB>(pn);
+            float nc[kCB];
+#pragma unroll
+            for (int q = 0; q < kCB; q++) nc[q] = sqrtf(__shfl(pn[q], 0, 64));
+#pragma unroll
+            for (int rb = 0; rb < kRB; rb++)
+                if (lane + 64u * rb < R) {
+#pragma unroll
+                    for (int q = 0; q < kCB; q++) pp[q] = pp[q] + d[rb] * (x[rb][q] / nc[q]);
+                }
+            tree_fn<kCB>(pp);
+            if (lane == 0) {
+#pragma unroll
+                for (int q = 0; q < kCB; q++)
+                    if (j0 + q < m) k0[j0 + q] = proj_key(nc[q] != 0 ? pp[q] : 0.0f, v[q]);
+            }
+        };
+        uint32_t j0 = (uint32_t)wave * kCB;
+        if (j0 < m) load(j0, vA, xA);
+        for (; j0 < m; j0 += 2 * stride) {
+            if (j0 + stride < m) load(j0 + stride, vB, xB);
+            reduce(j0, vA, xA);
+            if (j0 + stride >= m) break;
+            if (j0 + 2 * stride < m) load(j0 + 2 * stride, vA, xA);
+            reduce(j0 + stride, vB, xB);
+        }
+    } else {                                // tall local matrices: two passes from memory
+        for (uint32_t j0 = (uint32_t)wave * kCB; j0 < m; j0 += stride) {
+            uint32_t vr[kCB];
+#pragma unroll
+            for (int q = 0; q < kCB; q++) vr[q] = vrls[begin + min(j0 + (uint32_t)q, m - 1)];
+            float pn[kCB], pp[kCB];
+#pragma unroll
+            for (int q = 0; q < kCB; q++) { pn[q] = 0.0f; pp[q] = 0.0f; }
+            for (uint32_t r = lane; r < R; r += 64) {
+                const RowRef rw = row_ref(J, r);
+#pragma unroll
+                for (int q = 0; q < kCB; q++) { const float a = fabsf(ldg2(Rt, rw.base + (size_t)vr[q] * rw.stride).x); pn[q] = pn[q] + a * a; }
+            }
+            float nc[kCB];
+#pragma unroll
+            for (int q = 0; q < kCB; q++) nc[q] = sqrtf(__shfl(tree_f(pn[q]), 0, 64));
+            for (uint32_t r = lane; r < R; r += 64) {
+                const RowRef rw = row_ref(J, r);
+                const float dd = dir[r];
+#pragma unroll
+                for (int q = 0; q < kCB; q++) pp[q] = pp[q] + dd * (ldg2(Rt, rw.base + (size_t)vr[q] * rw.stride).x / nc[q]);
+            }
+#pragma unroll
+            for (int q = 0; q < kCB; q++) {
+                const float pr = tree_f(pp[q]);
+                if (lane == 0 && j0 + q < m) k0[j0 + q] = proj_key(nc[q] != 0 ? pr : 0.0f, vr[q]);
+            }
+        }
+    }
 }
+
 
 // ------------------------------------------------------------ split --
 // Clustering::split (:590-684), collective.
@@ -2685,41 +2789,38 @@ __device__ void enqueue_candidates(const JobDev& J, const Common& cm, Ctl& C)
     const Team& T = J.team;
     const uint32_t lane = threadIdx.x & 63;
     const int K = min(min(C.heap_n, (int)(cm.spec_width ? cm.spec_width : 2 * T.helpers + 2)), 64);
-    const uint32_t tail = C.qpend ? C.qtail : T.ctl[1];
-    const uint32_t head = ld_rlx(&T.ctl[0]);
+    const HeapRef H = heap_of(J, C);
+    const uint32_t tail = C.qtail;
     bool elig = false;
-    unsigned long long spec = 0, sv = 0;
+    uint32_t flags = 0u;
     CNode cn{0.0f, 0.0f, 0u, 0u};
     if ((int)lane < K) {
-        cn = hld(heap_of(J, C), lane);
-        const bool big = cn.end - cn.begin >= cm.spec_min;
-        if (big || lane == 0) sv = ld_rlx(&T.state[cn.begin]);   // lane 0: the next pop's word too
-        if (big) {
-            const bool mine = (uint32_t)(sv >> 3) == cn.end;
-            elig = !(mine && (sv & 7) != kStNone);
-            spec = mine ? (sv & kStSpecBit) : 0ull;
-        }
+        cn = hld(H, lane);
+        flags = cn.end & ~kEndMask;
+        cn.end &= kEndMask;
+        elig = cn.end - cn.begin >= cm.spec_min && !(flags & kEndQ);   // not queued by this leader yet
     }
     const unsigned long long bal = __ballot(elig);
+    const uint32_t want = (uint32_t)__popcll(bal);
+    // room from the head seen last (helpers only advance it); reloaded when short
+    uint32_t head = C.qhead;
+    if (want && tail - head + want > kQueue) head = ld_rlx(&T.ctl[0]);
     const uint32_t used = tail - head;
     const uint32_t room = used >= kQueue ? 0u : kQueue - used;
     const unsigned long long lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     const uint32_t rank = (uint32_t)__popcll(bal & lt);
     const bool queued = elig && rank < room;
     if (queued) {
-        st_rlx(&T.state[cn.begin], ((unsigned long long)cn.end << 3) | kStQueued | spec);
+        const bool spec = (flags & kEndS) != 0;
+        st_rlx(&T.state[cn.begin], ((unsigned long long)cn.end << 3) | kStQueued | (spec ? kStSpecBit : 0ull));
         st_rlx(&T.queue[(tail + rank) % kQueue], ((unsigned long long)cn.begin << 32) | cn.end | (spec ? kQSpecBit : 0u));
+        hst(H, lane, CNode{cn.uvar, cn.ivar, cn.begin, cn.end | flags | kEndQ});   // (a flag: not logged)
         tcount(cm, TS_ENQ);
     }
-    const uint32_t npush = min((uint32_t)__popcll(bal), room);
+    const uint32_t npush = min(want, room);
     if (lane == 0) {
-        // the heap top is the next pop (nothing reorders the heap before it):
-        // its word is final for the leader unless a helper may still take it
-        // (queued) or finish it (running)
-        const uint32_t st = (uint32_t)(sv & 7);
-        const bool live = queued || ((uint32_t)(sv >> 3) == cn.end && (st == kStQueued || st == kStRunning));
-        C.pre_b = (K > 0 && !live) ? cn.begin : ~0u;
-        C.pre_sw = sv;
+        C.qhead = head;
+        C.pre_b = ~0u;
         // the slots are published with the next split_team's first look
         // (publish_tail), by when these stores have landed
         if (npush) { C.qtail = tail + npush; C.qpend = 1; }
@@ -2742,17 +2843,19 @@ __device__ __forceinline__ void publish_tail(const Team& T, Ctl& C)
 // the initial clusters' variances).  Its vrls and the column weights were
 // released by the caller.  Popped later, the cluster is stolen back, waited
 // for or committed exactly like a cluster enqueue_candidates queued.
-__device__ void enqueue_early(const JobDev& J, const Common& cm, uint32_t b, uint32_t e)
+__device__ void enqueue_early(const JobDev& J, const Common& cm, Ctl& C, uint32_t b, uint32_t e)
 {
     const Team& T = J.team;
     if (e <= b || e - b < cm.spec_min) return;
-    const uint32_t tail = T.ctl[1];   // (the first enqueue: nothing pending)
+    const uint32_t tail = C.qtail;   // (the first enqueue: nothing pending)
     if (tail - ld_rlx(&T.ctl[0]) >= kQueue) return;
     st_rlx(&T.state[b], ((unsigned long long)e << 3) | kStQueued);
     st_rlx(&T.queue[tail % kQueue], ((unsigned long long)b << 32) | e);
     tcount(cm, TS_ENQ);
     drain_vmem();   // slot and state land before the tail that publishes them
     st_rlx(&T.ctl[1], tail + 1);
+    C.qtail = tail + 1;
+    C.early_b = b;   // its heap node is flagged queued when the leader adds it
 }
 
 __device__ void stop_team(const JobDev& J, const Common& cm, Ctl& C)
@@ -3770,6 +3873,7 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
         C.prec = nullptr;
         C.hlds = 0; C.hpool = pool;
         C.qpend = 0; C.pre_b = ~0u;
+        C.qtail = 0; C.qhead = 0; C.early_b = ~0u;
     }
     __syncthreads();
     const bool tsu = cm.team_setup && cm.team > 1 && J.team.helpers != 0;
@@ -3804,7 +3908,7 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
         __syncthreads();
         if (tid == 0) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            enqueue_early(J, cm, cm.init_off[0], cm.init_off[1]);
+            enqueue_early(J, cm, C, cm.init_off[0], cm.init_off[1]);
         }
         __syncthreads();
     }
@@ -3815,11 +3919,11 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
         const uint32_t b1 = two ? cm.init_off[i + 1] : 0, e1 = two ? cm.init_off[i + 2] : 0;
         if (b0 == e0 || (two && b1 == e1)) { if (tid == 0) C.err = 1; __syncthreads(); continue; }
         variance_passes(J, cm, C, J.vrls + b0, e0 - b0, 1, nullptr, nullptr, nullptr, nullptr, pool);
-        if (tid == 0) add_cluster(J, C, b0, e0, C.vg[0].res_u, C.vg[0].res_i);
+        if (tid == 0) add_cluster(J, C, b0, e0, C.vg[0].res_u, C.vg[0].res_i, nullptr, b0 == C.early_b ? kEndQ : 0u);
         __syncthreads();
         if (two) {
             variance_passes(J, cm, C, J.vrls + b1, e1 - b1, 1, nullptr, nullptr, nullptr, nullptr, pool);
-            if (tid == 0) add_cluster(J, C, b1, e1, C.vg[0].res_u, C.vg[0].res_i);
+            if (tid == 0) add_cluster(J, C, b1, e1, C.vg[0].res_u, C.vg[0].res_i, nullptr, b1 == C.early_b ? kEndQ : 0u);
             __syncthreads();
         }
     }
@@ -3950,6 +4054,9 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
     if (cm.jtime && threadIdx.x == 0) cm.jtime[3 * blockIdx.x + 1] = wall();
     __syncthreads();
     pf.mark(PF_CTRL);
+    // the heap nodes' queue flags off (their ends are the clusters')
+    for (int k = tid; k < C.heap_n; k += kThreads) gpw(&J.heap[k].end)[0] = J.heap[k].end & kEndMask;
+    __syncthreads();
     // sampleRepresentatives (:354-378)
     // singletons first (std::list push_front order), then one weighted pick
     // per multi-cluster in heap order; every cluster has its own stream, so
