@@ -210,6 +210,7 @@ struct Common {
     uint32_t part_min;             // smallest split (columns) divided into parts
     uint32_t part_blk;             // 64-row blocks per part (<= 7), jobs of more than 256 rows
     uint32_t part_blk_short;       // ... and of <= 256 rows
+    uint32_t part_blk_init;        // ... for an initial cluster's variance (init_parts)
     uint32_t* part_open;           // slots with parts not yet claimed (a hint for idle workgroups)
     uint32_t* idle;                // helpers and roamers waiting for work (parts are published only if some are)
     uint32_t idle_min;             // ... at least this many (0: always)
@@ -3179,8 +3180,10 @@ __device__ __noinline__ bool init_parts(const JobDev& J, const Common& cm, Ctl& 
     const int sl = part_slot_take(cm, C, 0u, J.nrows);
     if (sl < 0) return false;
     gather_cw(J, base, m, J.keys1);
+    // tall jobs: one row block per part (ALVRL_PART_BLK_INIT) -- the setup is
+    // every job's critical path and idle workgroups abound then
     const uint32_t nblk = (J.nrows + 63) / 64,
-                   pblk = min(max(J.nrows > 256 ? cm.part_blk : cm.part_blk_short, 1u), kPartMaxBlk);
+                   pblk = min(max(J.nrows > 256 ? cm.part_blk_init : cm.part_blk_short, 1u), kPartMaxBlk);
     PartJob pj = part_job(J);
     pj.kind = kPartInit; pj.cw = J.keys1; pj.m = m; pj.nblk = nblk; pj.pblk = pblk;
     pj.np = (nblk + pblk - 1) / pblk;
@@ -3506,7 +3509,10 @@ __device__ void setup_tasks(const JobDev& J0, const JobDev& Jw, const Common& cm
 {
     const Team& T = J0.team;
     const uint32_t N = cm.nvrl;
-    if (su_claim(T, kSuColw, C)) {
+    // where the leader divides a tall job's column weights (colw_parts) it takes them
+    // all: a helper's half on one workgroup would be the setup's critical path
+    const bool cparts = cm.parts && cm.proj_min && N >= cm.proj_min && J0.nrows > 256 && cm.part_min_tall;
+    if (!cparts && su_claim(T, kSuColw, C)) {
         if (threadIdx.x == 0) C.err = 0;
         __syncthreads();
         colw_raw(Jw, cm, C, N / 2, N);
@@ -3880,7 +3886,7 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
     // column ranges on idle workgroups (colw_parts) for wide jobs: the
     // helper's half is claimed first so that nobody computes it twice
     const bool cparts = cm.parts && cm.proj_min && N >= cm.proj_min && (R > 256 ? cm.part_min_tall : cm.part_min);
-    if (tsu && cparts && su_claim(J.team, kSuColw, C)) {
+    if (tsu && cparts && R > 256 && su_claim(J.team, kSuColw, C)) {
         if (!colw_parts(J, cm, C, 0, N, pool)) colw_raw(J, cm, C, 0, N);
     } else if (tsu) {
         // the first half here, the second on the job's helper unless it
@@ -4530,6 +4536,8 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
     {
         const char* pbs = std::getenv("ALVRL_PART_BLK_SHORT");
         cm.part_blk_short = pbs ? (uint32_t)std::min(std::max(1, std::atoi(pbs)), (int)kPartMaxBlk) : 2u;
+        const char* pbi = std::getenv("ALVRL_PART_BLK_INIT");
+        cm.part_blk_init = pbi ? (uint32_t)std::min(std::max(1, std::atoi(pbi)), (int)kPartMaxBlk) : 1u;
     }
     {
         const char* im = std::getenv("ALVRL_PART_IDLE");
