@@ -220,8 +220,28 @@ struct Common {
     uint32_t small_cap;
     uint32_t proj_min;             // smallest split whose projections are divided (0: never)
     uint32_t proj_cpp;             // columns per projection part
+    // the jobs as seen with another workgroup's split scratch: views[w * njobs + j] is job j with
+    // vrls = team.spec and the scratch of workgroup w (roamers, then helpers, then leaders; k_views)
+    const __attribute__((address_space(4))) JobDev* views;
 };
-__device__ __forceinline__ void trace(const Common& cm, uint32_t phase, uint32_t value)
+// The jobs, their views and Common live in device memory the kernel never
+// writes, reached through the constant address space: uniform field reads are
+// scalar loads (s_load, the scalar cache), not per-lane vector loads of a
+// private copy, whose waits (vmcnt) also waited out every store in flight.
+// A function's reference parameters arrive in VGPRs; uni() moves the address
+// to SGPRs so that the compiler knows it is uniform.
+#define ALVRL_AS4 __attribute__((address_space(4)))
+using CJ = const ALVRL_AS4 JobDev;
+using CC = const ALVRL_AS4 Common;
+using CT = const ALVRL_AS4 Team;
+template <class T>
+__device__ __forceinline__ const T& uni(const T& r)
+{
+    const uint64_t p = (uint64_t)&r;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)p), hi = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
+    return *reinterpret_cast<const T*>(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ void trace(CC& cm, uint32_t phase, uint32_t value)
 {
     if (cm.trace && threadIdx.x == 0 && blockIdx.x < 256)
         __hip_atomic_store(&cm.trace[blockIdx.x], ((unsigned long long)phase << 32) | value, __ATOMIC_RELAXED,
@@ -231,11 +251,11 @@ __device__ __forceinline__ void trace(const Common& cm, uint32_t phase, uint32_t
 enum { TS_ENQ, TS_HSTART, TS_HDONE, TS_COMMIT, TS_STEAL, TS_WAIT_TMO, TS_OWN, TS_IDLE_EXIT, TS_LSIDE,
        TS_HIDLE, TS_RIDLE, TS_HBUSY, TS_RBUSY, TS_ACQ, TS_REL, TS_PSPLIT, TS_PSOLO, TS_POWN, TS_POTHER,
        TS_PWAIT, TS_N };   // *IDLE/*BUSY: wall ticks (100 MHz) summed
-__device__ __forceinline__ void tcount(const Common& cm, int k)
+__device__ __forceinline__ void tcount(CC& cm, int k)
 {
     if (cm.tstat) atomicAdd(&cm.tstat[k], 1ull);
 }
-__device__ __forceinline__ void tadd(const Common& cm, int k, unsigned long long v)
+__device__ __forceinline__ void tadd(CC& cm, int k, unsigned long long v)
 {
     if (cm.tstat) atomicAdd(&cm.tstat[k], v);
 }
@@ -374,11 +394,11 @@ __device__ __forceinline__ float2 ldg2(const float2* base, size_t i)
 }
 
 struct RowRef { size_t base, stride; };
-__device__ __forceinline__ RowRef row_ref(const JobDev& J, uint32_t r)
+__device__ __forceinline__ RowRef row_ref(CJ& J, uint32_t r)
 {
     return J.contig ? RowRef{(size_t)(J.off0 + r), (size_t)J.stride0} : RowRef{(size_t)J.roff[r], (size_t)J.rstride[r]};
 }
-__device__ __forceinline__ float Rmean(const Common& cm, RowRef rr, uint32_t v)
+__device__ __forceinline__ float Rmean(CC& cm, RowRef rr, uint32_t v)
 {
     return ldg2(cm.Rt, rr.base + (size_t)v * rr.stride).x;
 }
@@ -611,16 +631,17 @@ __device__ void push_heap_(const HeapRef& first, long hole, long top, CNode valu
     heap_log(C, hole);
 }
 
-__device__ __forceinline__ HeapRef heap_of(const JobDev& J, const Ctl& C)
+__device__ __forceinline__ HeapRef heap_of(CJ& J, const Ctl& C)
 {
     return HeapRef{hnodes(J.heap), lp(reinterpret_cast<hnode_v*>(C.hpool)), C.hlds};
 }
 // lane-0-only Clustering::addCluster (:549-579)
 // (a single's id is read from J.vrls, or with an agent-scope load from spec:
 // a commit's range copy into J.vrls may still be in flight)
-__device__ void add_cluster(const JobDev& J, Ctl& C, uint32_t begin, uint32_t end, float uvar, float ivar,
+__device__ void add_cluster(CJ& J_in, Ctl& C, uint32_t begin, uint32_t end, float uvar, float ivar,
                             const uint32_t* spec = nullptr, uint32_t flags = 0u)
 {
+    CJ& J = uni(J_in);
     if (end == begin) { C.err = 1; return; }
     if (end == begin + 1) {
         gpw(J.singles)[C.singles_n++] =
@@ -653,8 +674,9 @@ __device__ void add_cluster(const JobDev& J, Ctl& C, uint32_t begin, uint32_t en
 #else
 #define PT_POP(k) do { } while (0)
 #endif
-__device__ __noinline__ CNode pop_wave(const JobDev& J, Ctl& C, const unsigned long long* state = nullptr)
+__device__ __noinline__ CNode pop_wave(CJ& J_in, Ctl& C, const unsigned long long* state = nullptr)
 {
+    CJ& J = uni(J_in);
     const int lane = (int)(threadIdx.x & 63);
     const HeapRef H = heap_of(J, C);
     const long n = __builtin_amdgcn_readfirstlane(C.heap_n);
@@ -754,8 +776,9 @@ __device__ float lower_bound(Ctl& C, uint32_t nvrl, float pu)
 // Between two snapshots the singles only grow and the heap changes where the
 // log says; a snapshot copies those (or everything after a restore or a log
 // overflow).  The snapshot's content is the same as a full copy.
-__device__ void snapshot(const JobDev& J, Ctl& C)
+__device__ void snapshot(CJ& J_in, Ctl& C)
 {
+    CJ& J = uni(J_in);
     const int nh = C.heap_n, ns = C.singles_n;
     const HeapRef H = heap_of(J, C);
     const hnode_p SH = hnodes(J.sh_heap);
@@ -778,8 +801,9 @@ __device__ void snapshot(const JobDev& J, Ctl& C)
     }
     __syncthreads();
 }
-__device__ void restore(const JobDev& J, Ctl& C)
+__device__ void restore(CJ& J_in, Ctl& C)
 {
+    CJ& J = uni(J_in);
     // The singles below the snapshot's count never change (appends only), and
     // the heap differs from the snapshot only where the log says.
     const int nh = C.sh_heap_n, ns = C.sh_singles_n;
@@ -808,8 +832,9 @@ __device__ void restore(const JobDev& J, Ctl& C)
 // for one more split's net growth) or back to J.heap.  The pool is the split
 // engines' scratch, so the heap goes back before any split by this workgroup
 // and before the representatives.  Content and order are unchanged.
-__device__ void heap_move(const JobDev& J, Ctl& C, bool to_lds)
+__device__ void heap_move(CJ& J_in, Ctl& C, bool to_lds)
 {
+    CJ& J = uni(J_in);
     __syncthreads();
     const int n = C.heap_n;
     const bool cur = C.hlds != 0;
@@ -926,10 +951,12 @@ __device__ __forceinline__ void chunk_coefs(VarGroup& V, Ctl& C, unsigned long l
 // No global store and no dependent global load sits on the row waves'
 // critical path.  With FU == false only the final variances are formed.
 template <bool TLDS, bool FU>
-__device__ __noinline__ void variance_passes_t(const JobDev& J, const Common& cm, Ctl& C, const uint32_t* base,
+__device__ __noinline__ void variance_passes_t(CJ& J_in, CC& cm_in, Ctl& C, const uint32_t* base,
                                                uint32_t m, int npass, float* fu0, float* fi0, float* fu1, float* fi1,
                                                unsigned char* pool, Prof* pf)
 {
+    CJ& J = uni(J_in);
+    CC& cm = uni(cm_in);
     const uint32_t R = J.nrows;
     const uint32_t NB = (R + 63) / 64;
     const int tid = threadIdx.x;
@@ -1327,10 +1354,12 @@ __device__ __forceinline__ void coef_block_finish(Ctl& C, double w, double Wo, d
 // reduction per chunk): the rows' final states go to J.st and one wave per
 // pass forms the two sums, as variance_passes_t does.
 template <bool FU, bool GRP = false>
-__device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm, Ctl& C, const uint32_t* base,
+__device__ __noinline__ void variance_split_v3(CJ& J_in, CC& cm_in, Ctl& C, const uint32_t* base,
                                                uint32_t m, int npass, float* fu0, float* fi0, float* fu1, float* fi1,
                                                unsigned char* pool)
 {
+    CJ& J = uni(J_in);
+    CC& cm = uni(cm_in);
     // a group of <= 256 rows (row0 .. row0 + R) of the job's Rfull: the
     // coefficients are the same for every group, the block-ordered row sums
     // continue from the previous group's (C.g_carry), and the prefix results
@@ -1737,9 +1766,10 @@ __device__ __noinline__ void variance_split_v3(const JobDev& J, const Common& cm
 // pj.st and wave 0 stores the total weight to pj.wsum (variance_split_v3<false>).
 constexpr uint32_t kPartMaxBlk = 7;
 template <bool FU>
-__device__ __noinline__ void variance_part(const PartJob& pj, const Common& cm, Ctl& C, const double* Tout_c, uint32_t g,
+__device__ __noinline__ void variance_part(const PartJob& pj, CC& cm_in, Ctl& C, const double* Tout_c, uint32_t g,
                                            uint32_t gb0, uint32_t nb, unsigned char* pool)
 {
+    CC& cm = uni(cm_in);
     double* const Tout = const_cast<double*>(Tout_c);
     const uint32_t Rt_rows = pj.nrows, m = pj.m, nblk_t = pj.nblk;
     const int tid = threadIdx.x, wv = tid >> 6;
@@ -1921,9 +1951,11 @@ constexpr uint32_t kSmallQBytes = 2u * kSmallMax * 2u * kSmallBlocks * 8u;
 constexpr uint32_t kSmallOutOff = kSmallCoefBytes + kSmallVrlBytes + kSmallQBytes;
 static_assert(kSmallOutOff + 4u * kSmallMax * 4u <= kPoolBytes, "small split engine exceeds the LDS pool");
 __device__ __forceinline__ const float* small_out(const unsigned char* pool) { return reinterpret_cast<const float*>(pool + kSmallOutOff); }
-__device__ __noinline__ void variance_split_small(const JobDev& J, const Common& cm, Ctl& C, const uint32_t* base,
+__device__ __noinline__ void variance_split_small(CJ& J_in, CC& cm_in, Ctl& C, const uint32_t* base,
                                                   uint32_t m, unsigned char* pool)
 {
+    CJ& J = uni(J_in);
+    CC& cm = uni(cm_in);
     const uint32_t R = J.nrows, NB = (R + 63) / 64;
     const int tid = threadIdx.x, wv = tid >> 6;
     const uint32_t lane = (uint32_t)(tid & 63);
@@ -2036,15 +2068,17 @@ __device__ __noinline__ void variance_split_small(const JobDev& J, const Common&
     __syncthreads();
 }
 
-__device__ __noinline__ bool split_parts(const JobDev& J, const Common& cm, Ctl& C, const uint32_t* base, uint32_t m,
+__device__ __noinline__ bool split_parts(CJ& J, CC& cm, Ctl& C, const uint32_t* base, uint32_t m,
                             float* fu0, float* fi0, float* fu1, float* fi1, unsigned char* pool);
-__device__ bool proj_parts(const JobDev& J, const Common& cm, Ctl& C, uint32_t begin, uint32_t m, unsigned char* pool);
-__device__ bool init_parts(const JobDev& J, const Common& cm, Ctl& C, const uint32_t* base, uint32_t m, unsigned char* pool);
-__device__ bool colw_parts(const JobDev& J, const Common& cm, Ctl& C, uint32_t vb, uint32_t ve, unsigned char* pool);
-__device__ void variance_passes(const JobDev& J, const Common& cm, Ctl& C, const uint32_t* base, uint32_t m,
+__device__ bool proj_parts(CJ& J, CC& cm, Ctl& C, uint32_t begin, uint32_t m, unsigned char* pool);
+__device__ bool init_parts(CJ& J, CC& cm, Ctl& C, const uint32_t* base, uint32_t m, unsigned char* pool);
+__device__ bool colw_parts(CJ& J, CC& cm, Ctl& C, uint32_t vb, uint32_t ve, unsigned char* pool);
+__device__ void variance_passes(CJ& J_in, CC& cm_in, Ctl& C, const uint32_t* base, uint32_t m,
                                 int npass, float* fu0, float* fi0, float* fu1, float* fi1, unsigned char* pool,
                                 Prof* pf = nullptr)
 {
+    CJ& J = uni(J_in);
+    CC& cm = uni(cm_in);
     // a large split in parts on idle workgroups (split_parts), when a slot is free
     const uint32_t pmin = J.nrows > 256 ? cm.part_min_tall : cm.part_min;   // 0: never
     if (fu0 && npass == 2 && cm.parts && cm.var_v3 && pmin && m >= pmin &&
@@ -2207,8 +2241,9 @@ __device__ __forceinline__ float key_proj(uint32_t u)
 {
     return __uint_as_float((u & 0x80000000u) ? (u & 0x7FFFFFFFu) : ~u);
 }
-__device__ __noinline__ unsigned long long* sort_keys(const JobDev& J, Ctl& C, uint32_t m, unsigned long long* lds_g)
+__device__ __noinline__ unsigned long long* sort_keys(CJ& J_in, Ctl& C, uint32_t m, unsigned long long* lds_g)
 {
+    CJ& J = uni(J_in);
     const int tid = threadIdx.x;
     auto* const k0 = gpw(J.keys0);
     auto* const k1 = gpw(J.keys1);
@@ -2287,8 +2322,9 @@ __device__ __forceinline__ RowRef row_ref(const PartJob& pj, uint32_t r)
     return pj.contig ? RowRef{(size_t)(pj.off0 + r), (size_t)pj.stride0}
                      : RowRef{(size_t)gp(pj.roff)[r], (size_t)gp(pj.rstride)[r]};
 }
-__device__ __noinline__ void proj_range(const PartJob& pj, const Common& cm, uint32_t jb, uint32_t je)
+__device__ __noinline__ void proj_range(const PartJob& pj, CC& cm_in, uint32_t jb, uint32_t je)
 {
+    CC& cm = uni(cm_in);
     const uint32_t R = pj.nrows;
     const int wave = threadIdx.x >> 6;
     const uint32_t lane = threadIdx.x & 63;
@@ -2382,7 +2418,7 @@ __device__ __noinline__ void proj_range(const PartJob& pj, const Common& cm, uin
         }
     }
 }
-__device__ __forceinline__ PartJob part_job(const JobDev& J)
+__device__ __forceinline__ PartJob part_job(CJ& J)
 {
     PartJob pj{};
     pj.roff = J.roff; pj.rstride = J.rstride; pj.off0 = J.off0; pj.stride0 = J.stride0; pj.contig = J.contig;
@@ -2394,8 +2430,10 @@ __device__ __forceinline__ PartJob part_job(const JobDev& J)
 // the split direction).  For R <= 64*kRB the batch's entries stay in
 // registers for both sums and the next batch's loads are in flight while
 // the current one is reduced (ping-pong buffers, no copies).
-__device__ __noinline__ void split_projections(const JobDev& J, const Common& cm, uint32_t begin, uint32_t m)
+__device__ __noinline__ void split_projections(CJ& J_in, CC& cm_in, uint32_t begin, uint32_t m)
 {
+    CJ& J = uni(J_in);
+    CC& cm = uni(cm_in);
     const uint32_t R = J.nrows;
     const int wave = threadIdx.x >> 6;
     const uint32_t lane = threadIdx.x & 63;
@@ -2495,9 +2533,11 @@ __device__ __noinline__ void split_projections(const JobDev& J, const Common& cm
 // Clustering::split (:590-684), collective.
 // commit: push the two children (the leader); otherwise write the result to
 // *res (a helper working on J with its own scratch and vrls = team.spec)
-__device__ void split(const JobDev& J, const Common& cm, Ctl& C, uint32_t begin, uint32_t end,
+__device__ void split(CJ& J_in, CC& cm_in, Ctl& C, uint32_t begin, uint32_t end,
                       unsigned long long* lds, Prof& pf, bool commit = true, SplitRes* res = nullptr)
 {
+    CJ& J = uni(J_in);
+    CC& cm = uni(cm_in);
     pf.mark(PF_CTRL);
     pf.count(PF_NSPLIT, 1);
     pf.count(PF_SPLITCOLS, end - begin);
@@ -2785,9 +2825,11 @@ constexpr unsigned long long kSpinTicks = 6000000000ull;   // default of Common:
 // dependent chain on lane 0); the first 'room' eligible entries in heap order
 // are queued, as the sequential loop would.  The vrls of every cluster in the
 // heap were released when its parent's split ended (split_team).
-__device__ void enqueue_candidates(const JobDev& J, const Common& cm, Ctl& C)
+__device__ void enqueue_candidates(CJ& J_in, CC& cm_in, Ctl& C)
 {
-    const Team& T = J.team;
+    CJ& J = uni(J_in);
+    CC& cm = uni(cm_in);
+    CT& T = J.team;
     const uint32_t lane = threadIdx.x & 63;
     const int K = min(min(C.heap_n, (int)(cm.spec_width ? cm.spec_width : 2 * T.helpers + 2)), 64);
     const HeapRef H = heap_of(J, C);
@@ -2830,7 +2872,7 @@ __device__ void enqueue_candidates(const JobDev& J, const Common& cm, Ctl& C)
 
 // Thread 0 of the leader: publish the slots enqueue_candidates wrote (their
 // stores land before the tail that publishes them).
-__device__ __forceinline__ void publish_tail(const Team& T, Ctl& C)
+__device__ __forceinline__ void publish_tail(CT& T, Ctl& C)
 {
     if (C.qpend) {
         drain_vmem();
@@ -2844,9 +2886,11 @@ __device__ __forceinline__ void publish_tail(const Team& T, Ctl& C)
 // the initial clusters' variances).  Its vrls and the column weights were
 // released by the caller.  Popped later, the cluster is stolen back, waited
 // for or committed exactly like a cluster enqueue_candidates queued.
-__device__ void enqueue_early(const JobDev& J, const Common& cm, Ctl& C, uint32_t b, uint32_t e)
+__device__ void enqueue_early(CJ& J_in, CC& cm_in, Ctl& C, uint32_t b, uint32_t e)
 {
-    const Team& T = J.team;
+    CJ& J = uni(J_in);
+    CC& cm = uni(cm_in);
+    CT& T = J.team;
     if (e <= b || e - b < cm.spec_min) return;
     const uint32_t tail = C.qtail;   // (the first enqueue: nothing pending)
     if (tail - ld_rlx(&T.ctl[0]) >= kQueue) return;
@@ -2859,8 +2903,10 @@ __device__ void enqueue_early(const JobDev& J, const Common& cm, Ctl& C, uint32_
     C.early_b = b;   // its heap node is flagged queued when the leader adds it
 }
 
-__device__ void stop_team(const JobDev& J, const Common& cm, Ctl& C)
+__device__ void stop_team(CJ& J_in, CC& cm_in, Ctl& C)
 {
+    CJ& J = uni(J_in);
+    CC& cm = uni(cm_in);
     if (J.team.helpers && threadIdx.x == 0) { publish_tail(J.team, C); st_rel(&J.team.ctl[2], 1u); }
     trace(cm, 6, 0);
 }
@@ -2910,17 +2956,17 @@ __device__ void copy_range_sc1(uint32_t* dst, const uint32_t* src, uint32_t b, u
     }
 }
 
-__device__ __forceinline__ JobDev J_spec(const JobDev& J)
-{
-    JobDev Jw = J;
-    Jw.vrls = J.team.spec;
-    return Jw;
-}
+// Workgroup w's view of job j (Common::views): roamers 0.., then the helpers
+// of job 0, 1, ..., then the leaders
+__device__ __forceinline__ uint32_t wid_helper(CC& cm, uint32_t j, uint32_t hid) { return cm.nroam + j * (cm.team - 1) + hid; }
+__device__ __forceinline__ uint32_t wid_leader(CC& cm, uint32_t j) { return cm.nroam + cm.njobs * (cm.team - 1) + j; }
+__device__ __forceinline__ CJ& view_of(CC& cm, uint32_t w, uint32_t j) { return uni(cm.views[(size_t)w * cm.njobs + j]); }
 
 // Thread 0: take the oldest queued task.  1 = claimed (*b, *e), 0 = queue
 // empty, 2 = lost a race (try again).
-__device__ int try_claim(const Team& T, uint32_t* b, uint32_t* e, uint64_t max_cols = ~0ull)
+__device__ int try_claim(CT& T_in, uint32_t* b, uint32_t* e, uint64_t max_cols = ~0ull)
 {
+    CT& T = uni(T_in);
     const uint32_t h = ld_rlx(&T.ctl[0]), t = ld_rlx(&T.ctl[1]);
     if (h >= t) return 0;
     const unsigned long long task = ld_rlx(&T.queue[h % kQueue]);
@@ -2936,8 +2982,9 @@ __device__ int try_claim(const Team& T, uint32_t* b, uint32_t* e, uint64_t max_c
 // reads the generation word the owner stored after its release fence, and
 // the acquire fence after it makes the slot's fields (and the owner's cw)
 // visible to this CU.
-__device__ int part_claim_slot(const Common& cm, PartSlot* S)
+__device__ int part_claim_slot(CC& cm_in, PartSlot* S)
 {
+    CC& cm = uni(cm_in);
     while (true) {
         const unsigned long long w = ld_rlx(&S->word);
         const uint32_t np = (uint32_t)(w >> 16) & 0xFFFFu, nx = (uint32_t)w & 0xFFFFu;
@@ -2950,8 +2997,9 @@ __device__ int part_claim_slot(const Common& cm, PartSlot* S)
     }
 }
 // Thread 0 of an idle workgroup: claim a part of any open slot.
-__device__ bool part_try(const Common& cm, uint32_t* slot, uint32_t* part)
+__device__ bool part_try(CC& cm_in, uint32_t* slot, uint32_t* part)
 {
+    CC& cm = uni(cm_in);
     if (!cm.parts || ld_rlx(cm.part_open) == 0u) return false;
     for (uint32_t s = 0; s < cm.nslots; s++) {
         const int p = part_claim_slot(cm, &cm.parts[s]);
@@ -2960,12 +3008,13 @@ __device__ bool part_try(const Common& cm, uint32_t* slot, uint32_t* part)
     return false;
 }
 template <class JV>
-__device__ void colw_raw(const JV& J, const Common& cm, Ctl& C, uint32_t vb, uint32_t ve);
+__device__ void colw_raw(const JV& J, CC& cm, Ctl& C, uint32_t vb, uint32_t ve);
 // Every thread: run part p of slot s and publish it (spec_split's producer
 // form: drained stores, barrier, one agent release, relaxed count).  C.err
 // is the caller's.
-__device__ __noinline__ void run_part(const Common& cm, Ctl& C, uint32_t s, uint32_t p, unsigned char* pool, bool own)
+__device__ __noinline__ void run_part(CC& cm_in, Ctl& C, uint32_t s, uint32_t p, unsigned char* pool, bool own)
 {
+    CC& cm = uni(cm_in);
     PartSlot* const S = &cm.parts[s];
     if (threadIdx.x == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // thread 0's acquire, complete
     __syncthreads();
@@ -3005,8 +3054,9 @@ __device__ __noinline__ void run_part(const Common& cm, Ctl& C, uint32_t s, uint
 // Every thread: a free slot of the board whose block-total buffer holds a
 // split of `cols` columns (0: none needed), or -1.  Slots [0, nbig) hold any
 // split, the others up to small_cap columns; small needs try those first.
-__device__ int part_slot_take(const Common& cm, Ctl& C, uint32_t cols, uint32_t rows)
+__device__ int part_slot_take(CC& cm_in, Ctl& C, uint32_t cols, uint32_t rows)
 {
+    CC& cm = uni(cm_in);
     if (threadIdx.x == 0) {
         int got = -1;
         // too few workgroups idle to take parts: the one-workgroup engines
@@ -3036,8 +3086,9 @@ __device__ int part_slot_take(const Common& cm, Ctl& C, uint32_t cols, uint32_t 
 // the claimed ones.  The claimed parts run on workgroups that wait for
 // nobody, so the wait ends; a 60 s guard fails the job (false) and keeps the
 // slot, which a late part may still write.
-__device__ bool part_run_all(const Common& cm, Ctl& C, uint32_t sl, const PartJob& pj, unsigned char* pool)
+__device__ bool part_run_all(CC& cm_in, Ctl& C, uint32_t sl, const PartJob& pj, unsigned char* pool)
 {
+    CC& cm = uni(cm_in);
     PartSlot* const S = &cm.parts[sl];
     const int tid = threadIdx.x;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -3080,15 +3131,17 @@ __device__ bool part_run_all(const Common& cm, Ctl& C, uint32_t sl, const PartJo
     __syncthreads();
     return ok;
 }
-__device__ void part_slot_free(const Common& cm, uint32_t sl)
+__device__ void part_slot_free(CC& cm_in, uint32_t sl)
 {
+    CC& cm = uni(cm_in);
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_store(&cm.parts[sl].busy, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 // Every thread: the cluster's (weight << 32 | vrl) pairs in column order, for
 // every part of a divided variance pass (variance_split_v3's gather)
-__device__ void gather_cw(const JobDev& J, const uint32_t* base, uint32_t m, unsigned long long* cw)
+__device__ void gather_cw(CJ& J_in, const uint32_t* base, uint32_t m, unsigned long long* cw)
 {
+    CJ& J = uni(J_in);
     constexpr int B = 8;
     for (uint32_t i0 = threadIdx.x; i0 < m; i0 += B * kThreads) {
         uint32_t v[B];
@@ -3108,9 +3161,11 @@ __device__ void gather_cw(const JobDev& J, const uint32_t* base, uint32_t m, uns
 // one-workgroup engine).  The cluster's (weight, vrl) pairs are gathered once
 // for every part; afterwards the block totals are added in ascending block
 // order into the float prefixes (variance_split_v3's reduce, the last group's).
-__device__ __noinline__ bool split_parts(const JobDev& J, const Common& cm, Ctl& C, const uint32_t* base, uint32_t m,
+__device__ __noinline__ bool split_parts(CJ& J_in, CC& cm_in, Ctl& C, const uint32_t* base, uint32_t m,
                             float* fu0, float* fi0, float* fu1, float* fi1, unsigned char* pool)
 {
+    CJ& J = uni(J_in);
+    CC& cm = uni(cm_in);
     const int tid = threadIdx.x;
     const int sl = part_slot_take(cm, C, m, J.nrows);
     if (sl < 0) return false;
@@ -3141,8 +3196,10 @@ __device__ __noinline__ bool split_parts(const JobDev& J, const Common& cm, Ctl&
 }
 // The owner's side of a divided split's projections (split): column ranges
 // of the cluster on idle workgroups.  False when no slot is free.
-__device__ __noinline__ bool proj_parts(const JobDev& J, const Common& cm, Ctl& C, uint32_t begin, uint32_t m, unsigned char* pool)
+__device__ __noinline__ bool proj_parts(CJ& J_in, CC& cm_in, Ctl& C, uint32_t begin, uint32_t m, unsigned char* pool)
 {
+    CJ& J = uni(J_in);
+    CC& cm = uni(cm_in);
     const int sl = part_slot_take(cm, C, 0u, J.nrows);
     if (sl < 0) return false;
     PartJob pj = part_job(J);
@@ -3156,9 +3213,11 @@ __device__ __noinline__ bool proj_parts(const JobDev& J, const Common& cm, Ctl& 
 }
 // The owner's side of divided column weights (calculateColumnWeigths over
 // columns [vb, ve), each column's sum its own): false when no slot is free.
-__device__ __noinline__ bool colw_parts(const JobDev& J, const Common& cm, Ctl& C, uint32_t vb, uint32_t ve,
+__device__ __noinline__ bool colw_parts(CJ& J_in, CC& cm_in, Ctl& C, uint32_t vb, uint32_t ve,
                                         unsigned char* pool)
 {
+    CJ& J = uni(J_in);
+    CC& cm = uni(cm_in);
     const int sl = part_slot_take(cm, C, 0u, J.nrows);
     if (sl < 0) return false;
     PartJob pj = part_job(J);
@@ -3174,9 +3233,11 @@ __device__ __noinline__ bool colw_parts(const JobDev& J, const Common& cm, Ctl& 
 // prefixes, one pass, more than 256 rows): each part writes its rows' final
 // states, then wave 0 forms the two sums over all rows as
 // variance_split_v3<false>'s last group does.  False when no slot is free.
-__device__ __noinline__ bool init_parts(const JobDev& J, const Common& cm, Ctl& C, const uint32_t* base, uint32_t m,
+__device__ __noinline__ bool init_parts(CJ& J_in, CC& cm_in, Ctl& C, const uint32_t* base, uint32_t m,
                                         unsigned char* pool)
 {
+    CJ& J = uni(J_in);
+    CC& cm = uni(cm_in);
     const int sl = part_slot_take(cm, C, 0u, J.nrows);
     if (sl < 0) return false;
     gather_cw(J, base, m, J.keys1);
@@ -3217,10 +3278,13 @@ __device__ __noinline__ bool init_parts(const JobDev& J, const Common& cm, Ctl& 
 // publish the result (MI355X_MICROARCH.md, valid producer form: every storing
 // wave drains, barrier, lane 0 releases at agent scope and drains the
 // write-back, then the relaxed agent flag store).  C.err is the caller's.
-__device__ void spec_split(const JobDev& J0, const JobDev& Jw, const Common& cm, Ctl& C,
+__device__ void spec_split(CJ& J0_in, CJ& Jw_in, CC& cm_in, Ctl& C,
                            unsigned long long* lds, uint32_t b, uint32_t e)
 {
-    const Team& T = J0.team;
+    CJ& J0 = uni(J0_in);
+    CJ& Jw = uni(Jw_in);
+    CC& cm = uni(cm_in);
+    CT& T = J0.team;
     const int tid = threadIdx.x;
     const bool in_spec = (e & kQSpecBit) != 0;
     e &= ~kQSpecBit;
@@ -3261,9 +3325,9 @@ __device__ void spec_split(const JobDev& J0, const JobDev& Jw, const Common& cm,
 // pushes the children (a single's id from the spec range) while the range
 // copy is in flight; wave 0 then queues, and the range's readers come after
 // later barriers.
-__device__ __forceinline__ void commit_spec(const JobDev& J, Ctl& C, uint32_t b, uint32_t e)
+__device__ __forceinline__ void commit_spec(CJ& J, Ctl& C, uint32_t b, uint32_t e)
 {
-    const Team& T = J.team;
+    CT& T = J.team;
     const int tid = threadIdx.x;
     SplitRes r;
     if (tid == 0) {
@@ -3295,13 +3359,15 @@ __device__ __forceinline__ void commit_spec(const JobDev& J, Ctl& C, uint32_t b,
 // next candidates.  Out of line and without calls: it saves no callee-saved
 // registers on entry, which split_team (its splits' state lives across calls)
 // does on every pop.  commit_ready_ok is uniform (C after the pop's barrier).
-__device__ __forceinline__ bool commit_ready_ok(const JobDev& J, const Common& cm, const Ctl& C, uint32_t e)
+__device__ __forceinline__ bool commit_ready_ok(CJ& J, CC& cm, const Ctl& C, uint32_t e)
 {
     return J.team.helpers && !C.team_off && !cm.enq_start && !(C.hlds && C.heap_n + 2 > kHeapLdsMax) &&
            (uint32_t)(C.sw >> 3) == e && (C.sw & 7) == kStDone;
 }
-__device__ __noinline__ void commit_ready(const JobDev& J, const Common& cm, Ctl& C, uint32_t b, uint32_t e)
+__device__ __noinline__ void commit_ready(CJ& J_in, CC& cm_in, Ctl& C, uint32_t b, uint32_t e)
 {
+    CJ& J = uni(J_in);
+    CC& cm = uni(cm_in);
     const int tid = threadIdx.x;
     if (tid == 0) {
         publish_tail(J.team, C);
@@ -3330,10 +3396,12 @@ __device__ __noinline__ void commit_ready(const JobDev& J, const Common& cm, Ctl
 // and commit its result, or split here.  While a helper still runs [b, e)
 // the leader splits other queued clusters speculatively.  spec = false:
 // plain split.
-__device__ void split_team(const JobDev& J, const Common& cm, Ctl& C, uint32_t b, uint32_t e,
+__device__ void split_team(CJ& J_in, CC& cm_in, Ctl& C, uint32_t b, uint32_t e,
                            unsigned long long* lds, Prof& pf, bool spec)
 {
-    const Team& T = J.team;
+    CJ& J = uni(J_in);
+    CC& cm = uni(cm_in);
+    CT& T = J.team;
     if (!T.helpers || !spec || C.team_off) { heap_move(J, C, false); split(J, cm, C, b, e, lds, pf); return; }
     const int tid = threadIdx.x;
     if (C.hlds && C.heap_n + 2 > kHeapLdsMax) heap_move(J, C, false);   // uniform (after the caller's barrier)
@@ -3406,7 +3474,7 @@ __device__ void split_team(const JobDev& J, const Common& cm, Ctl& C, uint32_t b
             const uint32_t yb = C.yb, ye = C.ye;
             __syncthreads();
             if (C.side == 2) run_part(cm, C, yb, ye, reinterpret_cast<unsigned char*>(lds), false);
-            else spec_split(J, J_spec(J), cm, C, lds, yb, ye);
+            else spec_split(J, view_of(cm, wid_leader(cm, blockIdx.x), blockIdx.x), cm, C, lds, yb, ye);   // (leaders only)
         }
         __syncthreads();
         pf.mark(PF_T_SIDE);
@@ -3462,16 +3530,18 @@ __device__ void split_team(const JobDev& J, const Common& cm, Ctl& C, uint32_t b
 // nothing depends on the helper being resident.  Results are those of the
 // leader alone: the same per-column and per-row arithmetic in the same order.
 enum : uint32_t { kSuColw = 4, kSuUncl = 5, kSuIntVar = 6, kSuTrVar = 7, kSuUnclErr = 8, kSuColwErr = 9 };
-__device__ bool su_claim(const Team& T, uint32_t task, Ctl& C)
+__device__ bool su_claim(CT& T_in, uint32_t task, Ctl& C)
 {
+    CT& T = uni(T_in);
     if (threadIdx.x == 0) C.go = cas_rlx(&T.ctl[task], 0u, 1u) ? 1 : 0;
     __syncthreads();
     const bool got = C.go != 0;
     __syncthreads();
     return got;
 }
-__device__ void su_publish(const Team& T, uint32_t task)
+__device__ void su_publish(CT& T_in, uint32_t task)
 {
+    CT& T = uni(T_in);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -3485,8 +3555,10 @@ __device__ void su_publish(const Team& T, uint32_t task)
 // and depends on nobody, so the wait ends; it is not bounded by the wait
 // knobs (the helper writes colw, which the leader must not finish under it),
 // only by a 60 s guard (false: the job fails)
-__device__ bool su_wait(const Team& T, uint32_t task, const Common& cm, Ctl& C)
+__device__ bool su_wait(CT& T_in, uint32_t task, CC& cm_in, Ctl& C)
 {
+    CT& T = uni(T_in);
+    CC& cm = uni(cm_in);
     if (threadIdx.x == 0) {
         const unsigned long long t0 = wall();
         int ok = 1;
@@ -3503,11 +3575,14 @@ __device__ bool su_wait(const Team& T, uint32_t task, const Common& cm, Ctl& C)
     __syncthreads();
     return ok;
 }
-__device__ void unclustered_variance(const JobDev& J, const Common& cm, Ctl& C, const uint32_t* vrls_in, uint32_t nv);
+__device__ void unclustered_variance(CJ& J, CC& cm, Ctl& C, const uint32_t* vrls_in, uint32_t nv);
 // the helper's side (Jw: its own scratch, colw shared with the leader)
-__device__ void setup_tasks(const JobDev& J0, const JobDev& Jw, const Common& cm, Ctl& C, bool)
+__device__ void setup_tasks(CJ& J0_in, CJ& Jw_in, CC& cm_in, Ctl& C, bool)
 {
-    const Team& T = J0.team;
+    CJ& J0 = uni(J0_in);
+    CJ& Jw = uni(Jw_in);
+    CC& cm = uni(cm_in);
+    CT& T = J0.team;
     const uint32_t N = cm.nvrl;
     // where the leader divides a tall job's column weights (colw_parts) it takes them
     // all: a helper's half on one workgroup would be the setup's critical path
@@ -3535,15 +3610,13 @@ __device__ void setup_tasks(const JobDev& J0, const JobDev& Jw, const Common& cm
 }
 
 // A helper workgroup: split queued clusters of job J until the leader stops.
-__device__ __noinline__ void helper_loop(const JobDev& J0, uint32_t hid, const Common& cm, Ctl& C,
+__device__ __noinline__ void helper_loop(CJ& J0_in, uint32_t j, uint32_t hid, CC& cm_in, Ctl& C,
                                          unsigned long long* lds)
 {
-    const Team& T = J0.team;
-    JobDev J = J0;
-    const SplitWs& w = T.ws[hid];
-    J.vrls = T.spec;
-    J.dir = w.dir; J.st = w.st; J.bufM = w.bufM; J.keys0 = w.keys0; J.keys1 = w.keys1;
-    J.fsu = w.fsu; J.fsi = w.fsi; J.feu = w.feu; J.fei = w.fei; J.carry = w.carry;
+    CJ& J0 = uni(J0_in);
+    CC& cm = uni(cm_in);
+    CT& T = J0.team;
+    CJ& J = view_of(cm, wid_helper(cm, j, hid), j);   // vrls = team.spec, this helper's scratch
     const int tid = threadIdx.x;
     if (tid == 0) C.err = 0;
     trace(cm, 10, 0);
@@ -3585,9 +3658,10 @@ __device__ __noinline__ void helper_loop(const JobDev& J0, uint32_t hid, const C
 
 // A roaming helper: takes queued clusters from any job's queue (starting
 // from the job it last served), splits them with its own scratch.
-__device__ __noinline__ void roam_loop(const JobDev* jobs, const SplitWs& w, uint32_t start, const Common& cm,
+__device__ __noinline__ void roam_loop(const ALVRL_AS4 JobDev* jobs, uint32_t wid, uint32_t start, CC& cm_in,
                                        Ctl& C, unsigned long long* lds)
 {
+    CC& cm = uni(cm_in);
     const uint32_t njobs = cm.njobs;
     const int tid = threadIdx.x;
     uint32_t j = start % njobs;
@@ -3603,7 +3677,7 @@ __device__ __noinline__ void roam_loop(const JobDev* jobs, const SplitWs& w, uin
                 uint32_t live = 0;
                 for (uint32_t k = 0; k < njobs && !got; k++) {
                     jj = cm.roam_order ? cm.roam_order[k] : (j + k < njobs ? j + k : j + k - njobs);
-                    const Team& T = jobs[jj].team;
+                    CT& T = jobs[jj].team;
                     if (ld_rlx(&T.ctl[2])) continue;
                     live++;
                     int c;
@@ -3627,11 +3701,8 @@ __device__ __noinline__ void roam_loop(const JobDev* jobs, const SplitWs& w, uin
             continue;
         }
         j = C.j;
-        const JobDev& J0 = jobs[j];
-        JobDev Jw = J0;
-        Jw.vrls = J0.team.spec;
-        Jw.dir = w.dir; Jw.st = w.st; Jw.bufM = w.bufM; Jw.keys0 = w.keys0; Jw.keys1 = w.keys1;
-        Jw.fsu = w.fsu; Jw.fsi = w.fsi; Jw.feu = w.feu; Jw.fei = w.fei; Jw.carry = w.carry;
+        CJ& J0 = uni(jobs[j]);
+        CJ& Jw = view_of(cm, wid, j);   // vrls = team.spec, this workgroup's scratch
         const unsigned long long t_busy = wall();
         spec_split(J0, Jw, cm, C, lds, C.b, C.e);
         if (tid == 0) { tcount(cm, TS_HDONE); tadd(cm, TS_RBUSY, wall() - t_busy); }
@@ -3645,8 +3716,10 @@ __device__ __noinline__ void roam_loop(const JobDev* jobs, const SplitWs& w, uin
 // a job's helper can take; colw_finish adds the average afterwards)
 // (JV: the job, or a part's view of it -- rows, locality weights, colw)
 template <class JV>
-__device__ __noinline__ void colw_raw(const JV& J, const Common& cm, Ctl& C, uint32_t vb, uint32_t ve)
+__device__ __noinline__ void colw_raw(const JV& J_in, CC& cm_in, Ctl& C, uint32_t vb, uint32_t ve)
 {
+    const JV& J = uni(J_in);
+    CC& cm = uni(cm_in);
     const int tid = threadIdx.x, wave = tid >> 6;
     const uint32_t lane = (uint32_t)(tid & 63);
     const uint32_t R = J.nrows;
@@ -3733,8 +3806,10 @@ __device__ __noinline__ void colw_raw(const JV& J, const Common& cm, Ctl& C, uin
 
 // the average of all column weights (running float sum in index order) and
 // its 1 % added to every weight (:1002-1007)
-__device__ __noinline__ void colw_finish(const JobDev& J, const Common& cm, Ctl& C)
+__device__ __noinline__ void colw_finish(CJ& J_in, CC& cm_in, Ctl& C)
 {
+    CJ& J = uni(J_in);
+    CC& cm = uni(cm_in);
     const int tid = threadIdx.x, wave = tid >> 6;
     const uint32_t lane = (uint32_t)(tid & 63);
     const uint32_t N = cm.nvrl;
@@ -3765,9 +3840,11 @@ __device__ __noinline__ void colw_finish(const JobDev& J, const Common& cm, Ctl&
 }
 
 // calculateUnclusteredVariance (:1022-1048), out of line for the same reason
-__device__ __noinline__ void unclustered_variance(const JobDev& J, const Common& cm, Ctl& C, const uint32_t* vrls_in,
+__device__ __noinline__ void unclustered_variance(CJ& J_in, CC& cm_in, Ctl& C, const uint32_t* vrls_in,
                                                   uint32_t nv)
 {
+    CJ& J = uni(J_in);
+    CC& cm = uni(cm_in);
     const int tid = threadIdx.x, wave = tid >> 6;
     const uint32_t lane = (uint32_t)(tid & 63);
     const uint32_t R = J.nrows;
@@ -3839,8 +3916,10 @@ __device__ __noinline__ void unclustered_variance(const JobDev& J, const Common&
 }
 
 // ---------------------------------------------------------- kernel --
-__global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ jobs, Common cm)
+__global__ void __launch_bounds__(kThreads) k_refine(const ALVRL_AS4 JobDev* __restrict__ jobs,
+                                                     const ALVRL_AS4 Common* __restrict__ cmp)
 {
+    CC& cm = *cmp;
     __shared__ Ctl C;
     __shared__ __attribute__((aligned(16))) unsigned char pool[kPoolBytes];
     unsigned long long* lds = reinterpret_cast<unsigned long long*>(pool);
@@ -3851,19 +3930,19 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
     __syncthreads();
     if (blockIdx.x >= cm.njobs * cm.team) {   // a roaming helper
         const uint32_t rid = blockIdx.x - cm.njobs * cm.team;
-        roam_loop(jobs, cm.roam_ws[rid], rid * 37u, cm, C, lds);
+        roam_loop(jobs, rid, rid * 37u, cm, C, lds);
         trace(cm, 14, 0);
         return;
     }
     if (blockIdx.x >= cm.njobs) {   // a helper of job (blockIdx.x - njobs) / (team - 1)
         const uint32_t h = blockIdx.x - cm.njobs, per = cm.team - 1;
-        helper_loop(jobs[h / per], h % per, cm, C, lds);
+        helper_loop(jobs[h / per], h / per, h % per, cm, C, lds);
         // its job is done: help the others until every job is
-        if (cm.roam_on) roam_loop(jobs, jobs[h / per].team.ws[h % per], h / per + 1, cm, C, lds);
+        if (cm.roam_on) roam_loop(jobs, wid_helper(cm, h / per, h % per), h / per + 1, cm, C, lds);
         trace(cm, 13, 0);
         return;
     }
-    const JobDev J = jobs[blockIdx.x];
+    CJ& J = jobs[blockIdx.x];
     trace(cm, 1, 0);
     if (cm.jtime && threadIdx.x == 0) cm.jtime[3 * blockIdx.x] = wall();
     const int tid = threadIdx.x, wave = tid >> 6;
@@ -4128,13 +4207,39 @@ __global__ void __launch_bounds__(kThreads) k_refine(const JobDev* __restrict__ 
     if (cm.roam_on) {
         // this job is done: its leader helps the others with its own scratch
         __syncthreads();
-        const SplitWs w{J.dir, J.st, J.bufM, J.keys0, J.keys1, J.fsu, J.fsi, J.feu, J.fei, J.carry};
-        roam_loop(jobs, w, blockIdx.x + 1, cm, C, lds);
+        roam_loop(jobs, wid_leader(cm, blockIdx.x), blockIdx.x + 1, cm, C, lds);
     }
 }
 
 // Packs the jobs' representative lists back to back (job order) so the host
 // fetches every result with three copies: meta[3j..3j+2] = (n, refined, err).
+// Common::views: job j with vrls = team.spec and workgroup w's split scratch
+// (a roamer's, a helper's or a leader's own), one view per thread
+__global__ void __launch_bounds__(256) k_views(const JobDev* __restrict__ jobs, const Common* __restrict__ cmp,
+                                               JobDev* __restrict__ views)
+{
+    const Common& cm = *cmp;
+    const uint32_t nj = cm.njobs, G = cm.team, nh = nj * (G - 1);
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (cm.nroam + nh + nj) * nj) return;
+    const uint32_t w = i / nj, j = i % nj;
+    JobDev v = jobs[j];
+    v.vrls = jobs[j].team.spec;
+    SplitWs ws;
+    if (w < cm.nroam) {
+        ws = cm.roam_ws[w];
+    } else if (w < cm.nroam + nh) {
+        const uint32_t h = w - cm.nroam;
+        ws = jobs[h / (G - 1)].team.ws[h % (G - 1)];
+    } else {
+        const JobDev& o = jobs[w - cm.nroam - nh];
+        ws = SplitWs{o.dir, o.st, o.bufM, o.keys0, o.keys1, o.fsu, o.fsi, o.feu, o.fei, o.carry};
+    }
+    v.dir = ws.dir; v.st = ws.st; v.bufM = ws.bufM; v.keys0 = ws.keys0; v.keys1 = ws.keys1;
+    v.fsu = ws.fsu; v.fsi = ws.fsi; v.feu = ws.feu; v.fei = ws.fei; v.carry = ws.carry;
+    views[i] = v;
+}
+
 __global__ void __launch_bounds__(256) k_pack_results(const JobDev* __restrict__ jobs, uint32_t njobs,
                                                       uint32_t nvrl, uint32_t* __restrict__ meta,
                                                       uint32_t* __restrict__ reps, float* __restrict__ w)
@@ -4186,8 +4291,9 @@ void RefineArenas::release()
 {
     if (arena) (void)hipFree(arena);
     if (tarena) (void)hipFree(tarena);
-    arena = tarena = nullptr;
-    arena_cap = tarena_cap = 0;
+    if (varena) (void)hipFree(varena);
+    arena = tarena = varena = nullptr;
+    arena_cap = tarena_cap = varena_cap = 0;
 }
 static hipError_t arena_get(char** buf, size_t* cap, size_t bytes, bool cached)
 {
@@ -4595,6 +4701,15 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
                 cm.poptr = nullptr;
         }
     }
+    // the kernel's Common and, with helpers or roamers, every workgroup's view
+    // of every job (k_views), in device memory read through the constant
+    // address space
+    const size_t nviews = team_on && tarena ? (size_t)(nroam + njobs * G) * njobs : 0;
+    e = arena_get(&ar.varena, &ar.varena_cap, align_up(sizeof(Common)) + nviews * sizeof(JobDev), cache != nullptr);
+    if (e != hipSuccess) { *err = std::string("alvrl_refine: hipMalloc: ") + hipGetErrorString(e); return 4; }
+    Common* const d_cm = reinterpret_cast<Common*>(ar.varena);
+    JobDev* const d_views = nviews ? reinterpret_cast<JobDev*>(ar.varena + align_up(sizeof(Common))) : nullptr;
+    cm.views = (const ALVRL_AS4 JobDev*)(uintptr_t)d_views;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     e = hipEventCreate(&e0);
     if (e == hipSuccess) e = hipEventCreate(&e1);
@@ -4615,13 +4730,20 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
         e = hipMemcpyAsync(d_rws, h_rws.data(), (size_t)nroam * sizeof(SplitWs), hipMemcpyHostToDevice, s);
     if (e == hipSuccess && cm.roam_order)
         e = hipMemcpyAsync(const_cast<uint32_t*>(cm.roam_order), h_order.data(), (size_t)njobs * 4, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(d_cm, &cm, sizeof(Common), hipMemcpyHostToDevice, s);
+    if (e == hipSuccess && nviews) {
+        hipLaunchKernelGGL(k_views, dim3((uint32_t)((nviews + 255) / 256)), dim3(256), 0, s, d_jobs, d_cm, d_views);
+        e = hipGetLastError();
+    }
+    const auto* const a_jobs = (const ALVRL_AS4 JobDev*)(uintptr_t)d_jobs;
+    const auto* const a_cm = (const ALVRL_AS4 Common*)(uintptr_t)d_cm;
     if (e == hipSuccess) e = hipEventRecord(e0, s);
     if (e == hipSuccess && team_on && tarena) {
         // sized to the resident capacity, but correct without co-residency:
         // no workgroup ever waits for one that has not started (a leader waits
         // only on a cluster a running helper has claimed, helpers only poll),
         // so a late helper finds its job stopped and leaves
-        hipLaunchKernelGGL(k_refine, dim3(njobs * G + nroam), dim3(kThreads), 0, s, d_jobs, cm);
+        hipLaunchKernelGGL(k_refine, dim3(njobs * G + nroam), dim3(kThreads), 0, s, a_jobs, a_cm);
         e = hipGetLastError();
     } else if (e == hipSuccess) {
         // ALVRL_REFINE_BATCH=n (developer knob): launch the jobs n at a time,
@@ -4629,7 +4751,7 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
         const char* bs = bs_env;
         const uint32_t batch = bs ? (uint32_t)std::max(1, std::atoi(bs)) : njobs;
         for (uint32_t j0 = 0; j0 < njobs && e == hipSuccess; j0 += batch) {
-            hipLaunchKernelGGL(k_refine, dim3(std::min(batch, njobs - j0)), dim3(kThreads), 0, s, d_jobs + j0, cm);
+            hipLaunchKernelGGL(k_refine, dim3(std::min(batch, njobs - j0)), dim3(kThreads), 0, s, a_jobs + j0, a_cm);
             e = hipGetLastError();
         }
     }

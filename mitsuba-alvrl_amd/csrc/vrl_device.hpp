@@ -866,7 +866,8 @@ __device__ __forceinline__ void integrate_vrl(const DevParams& P, const RecPre& 
 struct RefineArenas {
     char* arena = nullptr;
     char* tarena = nullptr;
-    size_t arena_cap = 0, tarena_cap = 0;
+    char* varena = nullptr;           // the kernel's Common and the jobs' views (k_views)
+    size_t arena_cap = 0, tarena_cap = 0, varena_cap = 0;
     void release();
 };
 
