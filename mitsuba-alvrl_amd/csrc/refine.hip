@@ -280,10 +280,12 @@ static const char* kPfNames[PF_N] = {"column weights", "initial clusters", "uncl
                                      "ctrl: side splits", "ctrl: commit", "ctrl: snapshot", "ctrl: state check",
                                      "#splits", "#split columns"};
 constexpr int kPfSmall = 2;   // split-phase table of small splits: m < 64, 64 <= m < 256
+// (in LDS: a reference to a private Prof made every mark a per-lane flat load
+// of p, whose wait also waited out the stores in flight)
 struct Prof {
     unsigned long long* p;
     long long t;
-    int sm = -1;                 // small-split class of the split in progress (-1: none)
+    int sm;                      // small-split class of the split in progress (-1: none)
     __device__ void mark(int id);
     __device__ void count(int id, unsigned long long v) { if (p && threadIdx.x == 0) atomicAdd(&p[id], v); }
 };
@@ -3018,10 +3020,14 @@ __device__ __noinline__ void run_part(CC& cm_in, Ctl& C, uint32_t s, uint32_t p,
     PartSlot* const S = &cm.parts[s];
     if (threadIdx.x == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // thread 0's acquire, complete
     __syncthreads();
-    const PartJob pj = S->pj;   // once per part: flat loads are fine here
+    // the part's view in LDS: its readers' field loads are LDS reads, not
+    // per-lane flat loads whose waits include every store in flight
+    __shared__ PartJob pjs;
+    if (threadIdx.x == 0) pjs = S->pj;
     const double* const T = gp(&S->T)[0];
     const int err_saved = C.err;
     __syncthreads();
+    const PartJob& pj = pjs;
     if (threadIdx.x == 0) C.err = 0;
     __syncthreads();
     if (pj.kind == kPartProj || pj.kind == kPartColw) {
@@ -3301,9 +3307,9 @@ __device__ void spec_split(CJ& J0_in, CJ& Jw_in, CC& cm_in, Ctl& C,
     __syncthreads();
     const int err_saved = C.err;
     __syncthreads();
-    if (tid == 0) C.err = 0;
+    __shared__ Prof off;
+    if (tid == 0) { C.err = 0; off.p = nullptr; off.t = 0; off.sm = -1; }
     __syncthreads();
-    Prof off{nullptr, 0};
     split(Jw, cm, C, b, e, lds, off, false, &T.res[b]);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -3948,9 +3954,10 @@ __global__ void __launch_bounds__(kThreads) k_refine(const ALVRL_AS4 JobDev* __r
     const int tid = threadIdx.x, wave = tid >> 6;
     const uint32_t N = cm.nvrl, R = J.nrows;
     const uint32_t nv = cm.init_off[cm.ninit];
-    Prof pf{cm.prof, (long long)clock64()};
+    __shared__ Prof pf;
     unsigned long long split_cols = 0;   // thread 0: columns of the clusters split
     if (tid == 0) {
+        pf.p = cm.prof; pf.t = (long long)clock64(); pf.sm = -1;
         C.tracingVar = C.unclIntVar = C.clUnderVar = C.clIntVar = 0.0f;
         C.heap_n = C.singles_n = C.sh_heap_n = C.sh_singles_n = 0;
         C.err = 0; C.refined = 1; C.team_off = 0;
