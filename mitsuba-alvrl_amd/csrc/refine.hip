@@ -231,16 +231,28 @@ struct Common {
 // A function's reference parameters arrive in VGPRs; uni() moves the address
 // to SGPRs so that the compiler knows it is uniform.
 #define ALVRL_AS4 __attribute__((address_space(4)))
+// the leader's pop and quick commit: out of line by default (ALVRL_POP_INLINE=1
+// inlines them into k_refine, which drops the wait for every memory operation
+// in flight that a call's entry carries)
+#ifdef ALVRL_POP_INLINE
+#define ALVRL_POP_INL __forceinline__
+#else
+#define ALVRL_POP_INL __noinline__
+#endif
 using CJ = const ALVRL_AS4 JobDev;
 using CC = const ALVRL_AS4 Common;
 using CT = const ALVRL_AS4 Team;
 template <class T>
-__device__ __forceinline__ const T& uni(const T& r)
+__device__ __forceinline__ const ALVRL_AS4 T& uni(const ALVRL_AS4 T& r)
 {
     const uint64_t p = (uint64_t)&r;
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)p), hi = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
-    return *reinterpret_cast<const T*>(((uint64_t)hi << 32) | lo);
+    return *reinterpret_cast<const ALVRL_AS4 T*>(((uint64_t)hi << 32) | lo);
 }
+// any other reference (a part's view in LDS) as it is: an integer round trip
+// would turn it into a generic pointer
+template <class T>
+__device__ __forceinline__ const T& uni(const T& r) { return r; }
 __device__ __forceinline__ void trace(CC& cm, uint32_t phase, uint32_t value)
 {
     if (cm.trace && threadIdx.x == 0 && blockIdx.x < 256)
@@ -463,13 +475,18 @@ __device__ __forceinline__ float ws_block_wave(float x, uint32_t lane, float* to
     const float base = r == 0 ? 0.0f : (r == 1 ? b1 : (r == 2 ? b2 : b3));
     return base + x;
 }
-__device__ __noinline__ uint32_t weighted_sample_wave(const float* wv, const float* colw, const uint32_t* ids,
-                                                      uint32_t m, Smp& smp, int* err, uint32_t zero_at,
-                                                      float* prob, bool wv_lds = false)
+// The stream state comes by value and its new draw count goes back with the
+// pick (a reference to the caller's private Smp made every draw a per-lane
+// flat load and store); the caller resumes the stream at WsPick::k.
+struct WsPick { uint32_t idx, k; int err; float prob; };
+__device__ __noinline__ WsPick weighted_sample_wave(const float* wv, const float* colw, const uint32_t* ids,
+                                                    uint32_t m, Smp smp, uint32_t zero_at, bool want_prob,
+                                                    bool wv_lds = false)
 {
     const uint32_t lane = threadIdx.x & 63;
-    if (m == 0) { *err = 1; return 0; }
-    if (m == 1) { if (prob) *prob = 1.0f; return 0; }
+    WsPick r{0u, smp.k, 0, 1.0f};
+    if (m == 0) { r.err = 1; return r; }
+    if (m == 1) return r;
     auto ld = [&](uint32_t i) -> float {
         const uint32_t c = min(i, m - 1);
         const float x = wv ? (wv_lds ? lp(wv)[c] : gp(wv)[c]) : gp(colw)[gp(ids)[c]];
@@ -490,9 +507,9 @@ __device__ __noinline__ uint32_t weighted_sample_wave(const float* wv, const flo
         int tries = 0;
         do {
             idx = (uint32_t)((float)0u + smp.next() * (float)m);
-            if (++tries > 1000) { *err = 1; idx = 0; break; }
+            if (++tries > 1000) { r.err = 1; idx = 0; break; }
         } while (idx >= m);
-        if (prob) *prob = (float)(1.0 / (double)m);
+        if (want_prob) r.prob = (float)(1.0 / (double)m);
     } else {
         const float alpha = smp.next() * weightSum;
         float S = 0.0f;
@@ -506,12 +523,14 @@ __device__ __noinline__ uint32_t weighted_sample_wave(const float* wv, const flo
             S = S + tot;
             cur = nxt;
         }
-        if (prob) {
+        if (want_prob) {
             const float wi = idx == zero_at ? 0.0f : (wv ? (wv_lds ? lp(wv)[idx] : gp(wv)[idx]) : gp(colw)[gp(ids)[idx]]);
-            *prob = wi / weightSum;
+            r.prob = wi / weightSum;
         }
     }
-    return idx;
+    r.idx = idx;
+    r.k = smp.k;
+    return r;
 }
 
 // deterministic Box-Muller x (oracle alvrl_o_det_std_normal_x)
@@ -598,38 +617,66 @@ struct HeapRef {
             g[i] = v;
         }
     }
+    // the placement known at compile time (L == lds): an LDS heap's accesses
+    // then wait on LDS counters only, not on the memory loads in flight
+    template <bool L>
+    __device__ __forceinline__ hnode_v ldt(long i) const
+    {
+        if (L) {
+            if (!LDS_OK(i >= 0 && i < kHeapLdsMax, "heap load", i, kHeapLdsMax)) return hnode_v{0u, 0u, 0u, 0u};
+            return l[i];
+        }
+        return g[i];
+    }
+    template <bool L>
+    __device__ __forceinline__ void stt(long i, hnode_v v) const
+    {
+        if (L) {
+            if (LDS_OK(i >= 0 && i < kHeapLdsMax, "heap store", i, kHeapLdsMax)) l[i] = v;
+        } else {
+            g[i] = v;
+        }
+    }
 };
 __device__ __forceinline__ CNode hld(hnode_p H, long i)
 {
     const hnode_v v = H[i];
     return CNode{__uint_as_float(v.x), __uint_as_float(v.y), v.z, v.w};
 }
+// PL: the heap's placement, -1 = H.lds at run time, 0 = global, 1 = LDS
+template <int PL = -1>
 __device__ __forceinline__ CNode hld(const HeapRef& H, long i)
 {
-    const hnode_v v = H.ld(i);
+    hnode_v v;
+    if constexpr (PL < 0) v = H.ld(i);
+    else v = H.template ldt<PL == 1>(i);
     return CNode{__uint_as_float(v.x), __uint_as_float(v.y), v.z, v.w};
 }
+template <int PL = -1>
 __device__ __forceinline__ void hst(const HeapRef& H, long i, const CNode& c)
 {
-    H.st(i, hnode_v{__float_as_uint(c.uvar), __float_as_uint(c.ivar), c.begin, c.end});
+    const hnode_v v{__float_as_uint(c.uvar), __float_as_uint(c.ivar), c.begin, c.end};
+    if constexpr (PL < 0) H.st(i, v);
+    else H.template stt<PL == 1>(i, v);
 }
 __device__ __forceinline__ void heap_log(Ctl& C, long i)
 {
     if (C.hlog_n < kHeapLog) C.hlog[C.hlog_n++] = (uint32_t)i;
     else C.hlog_full = 1;
 }
+template <int PL = -1>
 __device__ void push_heap_(const HeapRef& first, long hole, long top, CNode value, Ctl& C)
 {
     long parent = (hole - 1) / 2;
     while (hole > top) {
-        const CNode pn = hld(first, parent);
+        const CNode pn = hld<PL>(first, parent);
         if (!cless(pn, value)) break;
-        hst(first, hole, pn);
+        hst<PL>(first, hole, pn);
         heap_log(C, hole);
         hole = parent;
         parent = (hole - 1) / 2;
     }
-    hst(first, hole, value);
+    hst<PL>(first, hole, value);
     heap_log(C, hole);
 }
 
@@ -640,6 +687,7 @@ __device__ __forceinline__ HeapRef heap_of(CJ& J, const Ctl& C)
 // lane-0-only Clustering::addCluster (:549-579)
 // (a single's id is read from J.vrls, or with an agent-scope load from spec:
 // a commit's range copy into J.vrls may still be in flight)
+template <int PL = -1>
 __device__ void add_cluster(CJ& J_in, Ctl& C, uint32_t begin, uint32_t end, float uvar, float ivar,
                             const uint32_t* spec = nullptr, uint32_t flags = 0u)
 {
@@ -653,9 +701,9 @@ __device__ void add_cluster(CJ& J_in, Ctl& C, uint32_t begin, uint32_t end, floa
     } else {
         CNode cn{uvar, ivar, begin, end | flags | (spec ? kEndS : 0u)};
         const HeapRef H = heap_of(J, C);
-        hst(H, C.heap_n++, cn);
+        hst<PL>(H, C.heap_n++, cn);
         heap_log(C, C.heap_n - 1);
-        push_heap_(H, C.heap_n - 1, 0, cn, C);
+        push_heap_<PL>(H, C.heap_n - 1, 0, cn, C);
         C.clUnderVar += uvar;
         C.clIntVar += ivar;
     }
@@ -676,11 +724,18 @@ __device__ void add_cluster(CJ& J_in, Ctl& C, uint32_t begin, uint32_t end, floa
 #else
 #define PT_POP(k) do { } while (0)
 #endif
-__device__ __noinline__ CNode pop_wave(CJ& J_in, Ctl& C, const unsigned long long* state = nullptr)
+template <bool LH>
+__device__ __forceinline__ CNode pop_wave_t(CJ& J, Ctl& C, const unsigned long long* state)
 {
-    CJ& J = uni(J_in);
     const int lane = (int)(threadIdx.x & 63);
     const HeapRef H = heap_of(J, C);
+    auto hld = [&](const HeapRef& Hr, long i) {
+        const hnode_v v = Hr.ldt<LH>(i);
+        return CNode{__uint_as_float(v.x), __uint_as_float(v.y), v.z, v.w};
+    };
+    auto hst = [&](const HeapRef& Hr, long i, const CNode& c) {
+        Hr.stt<LH>(i, hnode_v{__float_as_uint(c.uvar), __float_as_uint(c.ivar), c.begin, c.end});
+    };
     const long n = __builtin_amdgcn_readfirstlane(C.heap_n);
     const CNode top = hld(H, 0);
     unsigned long long sw = 0;
@@ -703,7 +758,7 @@ __device__ __noinline__ CNode pop_wave(CJ& J_in, Ctl& C, const unsigned long lon
             const long idx = ((h + 1) << k) - 1 + j;
             const bool ex = lane < 62 && idx < len;
             hnode_v v = {0u, 0u, 0u, 0u};
-            if (ex) v = H.ld(idx);
+            if (ex) v = H.ldt<LH>(idx);
             const float key = __uint_as_float(v.x) + __uint_as_float(v.y);
             const float skey = __shfl_xor(key, 1);
             const int sex = __shfl_xor((int)ex, 1);
@@ -736,7 +791,7 @@ __device__ __noinline__ CNode pop_wave(CJ& J_in, Ctl& C, const unsigned long lon
         hnode_v up;
         up.x = __shfl_down(pv.x, 1); up.y = __shfl_down(pv.y, 1);
         up.z = __shfl_down(pv.z, 1); up.w = __shfl_down(pv.w, 1);
-        if (lane < fin) H.st(pidx, up);
+        if (lane < fin) H.stt<LH>(pidx, up);
         if (lane == fin) hst(H, pidx, value);
         if (lane == 0) hst(H, len, top);
         const int base = C.hlog_n, w = fin + 2;
@@ -756,6 +811,11 @@ __device__ __noinline__ CNode pop_wave(CJ& J_in, Ctl& C, const unsigned long lon
     }
     PT_POP(3);
     return CNode{top.uvar, top.ivar, top.begin, top.end & kEndMask};
+}
+__device__ ALVRL_POP_INL CNode pop_wave(CJ& J_in, Ctl& C, const unsigned long long* state = nullptr)
+{
+    CJ& J = uni(J_in);
+    return C.hlds ? pop_wave_t<true>(J, C, state) : pop_wave_t<false>(J, C, state);
 }
 
 __device__ __forceinline__ uint32_t n_clusters(const Ctl& C) { return (uint32_t)(C.singles_n + C.heap_n); }
@@ -2599,12 +2659,13 @@ __device__ void split(CJ& J_in, CC& cm_in, Ctl& C, uint32_t begin, uint32_t end,
     if (wave == 0) {
         Smp smp;
         smp.init(seed, pass, begin, end, stage);
-        int e = 0;
-        const uint32_t i1 = weighted_sample_wave(wv, nullptr, nullptr, m, smp, &e, 0xFFFFFFFFu, nullptr, wv_lds);
-        const uint32_t i2 = weighted_sample_wave(wv, nullptr, nullptr, m, smp, &e, i1, nullptr, wv_lds);   // colw[vrl1] = 0
+        const WsPick p1 = weighted_sample_wave(wv, nullptr, nullptr, m, smp, 0xFFFFFFFFu, false, wv_lds);
+        smp.k = p1.k; smp.blk = 0xFFFFFFFFu;   // the same stream from draw p1.k
+        const WsPick p2 = weighted_sample_wave(wv, nullptr, nullptr, m, smp, p1.idx, false, wv_lds);   // colw[vrl1] = 0
+        const uint32_t i1 = p1.idx, i2 = p2.idx;
         if (lane == 0) {
-            if (e) Cs.err = 1;
-            Cs.vrl1 = vrlsR[begin + i1]; Cs.vrl2 = vrlsR[begin + i2]; Cs.draw_k = smp.k;
+            if (p1.err | p2.err) Cs.err = 1;
+            Cs.vrl1 = vrlsR[begin + i1]; Cs.vrl2 = vrlsR[begin + i2]; Cs.draw_k = p2.k;
         }
     }
     __syncthreads();
@@ -2827,6 +2888,7 @@ constexpr unsigned long long kSpinTicks = 6000000000ull;   // default of Common:
 // dependent chain on lane 0); the first 'room' eligible entries in heap order
 // are queued, as the sequential loop would.  The vrls of every cluster in the
 // heap were released when its parent's split ended (split_team).
+template <int PL = -1>
 __device__ void enqueue_candidates(CJ& J_in, CC& cm_in, Ctl& C)
 {
     CJ& J = uni(J_in);
@@ -2840,7 +2902,7 @@ __device__ void enqueue_candidates(CJ& J_in, CC& cm_in, Ctl& C)
     uint32_t flags = 0u;
     CNode cn{0.0f, 0.0f, 0u, 0u};
     if ((int)lane < K) {
-        cn = hld(H, lane);
+        cn = hld<PL>(H, lane);
         flags = cn.end & ~kEndMask;
         cn.end &= kEndMask;
         elig = cn.end - cn.begin >= cm.spec_min && !(flags & kEndQ);   // not queued by this leader yet
@@ -2859,7 +2921,7 @@ __device__ void enqueue_candidates(CJ& J_in, CC& cm_in, Ctl& C)
         const bool spec = (flags & kEndS) != 0;
         st_rlx(&T.state[cn.begin], ((unsigned long long)cn.end << 3) | kStQueued | (spec ? kStSpecBit : 0ull));
         st_rlx(&T.queue[(tail + rank) % kQueue], ((unsigned long long)cn.begin << 32) | cn.end | (spec ? kQSpecBit : 0u));
-        hst(H, lane, CNode{cn.uvar, cn.ivar, cn.begin, cn.end | flags | kEndQ});   // (a flag: not logged)
+        hst<PL>(H, lane, CNode{cn.uvar, cn.ivar, cn.begin, cn.end | flags | kEndQ});   // (a flag: not logged)
         tcount(cm, TS_ENQ);
     }
     const uint32_t npush = min(want, room);
@@ -3023,7 +3085,9 @@ __device__ __noinline__ void run_part(CC& cm_in, Ctl& C, uint32_t s, uint32_t p,
     // the part's view in LDS: its readers' field loads are LDS reads, not
     // per-lane flat loads whose waits include every store in flight
     __shared__ PartJob pjs;
-    if (threadIdx.x == 0) pjs = S->pj;
+    static_assert(sizeof(PartJob) % 4 == 0 && sizeof(PartJob) / 4 <= 64, "PartJob copy");
+    if (threadIdx.x < sizeof(PartJob) / 4)   // one dword per lane, typed global loads
+        reinterpret_cast<uint32_t*>(&pjs)[threadIdx.x] = gp(reinterpret_cast<const uint32_t*>(&S->pj))[threadIdx.x];
     const double* const T = gp(&S->T)[0];
     const int err_saved = C.err;
     __syncthreads();
@@ -3331,6 +3395,7 @@ __device__ void spec_split(CJ& J0_in, CJ& Jw_in, CC& cm_in, Ctl& C,
 // pushes the children (a single's id from the spec range) while the range
 // copy is in flight; wave 0 then queues, and the range's readers come after
 // later barriers.
+template <int PL = -1>
 __device__ __forceinline__ void commit_spec(CJ& J, Ctl& C, uint32_t b, uint32_t e)
 {
     CT& T = J.team;
@@ -3349,8 +3414,8 @@ __device__ __forceinline__ void commit_spec(CJ& J, Ctl& C, uint32_t b, uint32_t 
             C.err = 1;
         } else {
             const uint32_t m = e - b, s2 = b + r.idx;
-            add_cluster(J, C, b, s2, r.fsu, r.fsi, T.spec);
-            add_cluster(J, C, s2, e, r.feu, r.fei, T.spec);
+            add_cluster<PL>(J, C, b, s2, r.fsu, r.fsi, T.spec);
+            add_cluster<PL>(J, C, s2, e, r.feu, r.fei, T.spec);
             // the children's input is this result, in team.spec
             st_rlx(&T.state[b], ((unsigned long long)s2 << 3) | kStNone | kStSpecBit);
             st_rlx(&T.state[s2], ((unsigned long long)e << 3) | kStNone | kStSpecBit);
@@ -3370,10 +3435,11 @@ __device__ __forceinline__ bool commit_ready_ok(CJ& J, CC& cm, const Ctl& C, uin
     return J.team.helpers && !C.team_off && !cm.enq_start && !(C.hlds && C.heap_n + 2 > kHeapLdsMax) &&
            (uint32_t)(C.sw >> 3) == e && (C.sw & 7) == kStDone;
 }
-__device__ __noinline__ void commit_ready(CJ& J_in, CC& cm_in, Ctl& C, uint32_t b, uint32_t e)
+// (PL: the heap's placement, so that an LDS heap's pushes and queueing do
+// not wait for the range copy's stores)
+template <int PL>
+__device__ __forceinline__ void commit_ready_t(CJ& J, CC& cm, Ctl& C, uint32_t b, uint32_t e)
 {
-    CJ& J = uni(J_in);
-    CC& cm = uni(cm_in);
     const int tid = threadIdx.x;
     if (tid == 0) {
         publish_tail(J.team, C);
@@ -3385,17 +3451,24 @@ __device__ __noinline__ void commit_ready(CJ& J_in, CC& cm_in, Ctl& C, uint32_t 
     pmark(C, 2);
     pmark(C, 3);
 #endif
-    commit_spec(J, C, b, e);
+    commit_spec<PL>(J, C, b, e);
 #ifndef ALVRL_PT_POP
     pmark(C, 4);
 #endif
     if (tid < 64) {
-        if (!C.hlds) drain_vmem();   // wave 0 queues from the global heap thread 0 just wrote
-        enqueue_candidates(J, cm, C);
+        if (PL == 0) drain_vmem();   // wave 0 queues from the global heap thread 0 just wrote
+        enqueue_candidates<PL>(J, cm, C);
     }
     if (tid == 0) trace(cm, 5, b);
     __syncthreads();
     pmark(C, 5);
+}
+__device__ ALVRL_POP_INL void commit_ready(CJ& J_in, CC& cm_in, Ctl& C, uint32_t b, uint32_t e)
+{
+    CJ& J = uni(J_in);
+    CC& cm = uni(cm_in);
+    if (C.hlds) commit_ready_t<1>(J, cm, C, b, e);
+    else commit_ready_t<0>(J, cm, C, b, e);
 }
 
 // The leader's split of [b, e): claim a queued task, wait for a running one
@@ -3745,39 +3818,46 @@ __device__ __noinline__ void colw_raw(const JV& J_in, CC& cm_in, Ctl& C, uint32_
             rr[b] = row_ref(J, min(r, R - 1));
             lw[b] = r < R ? gp(J.locw)[r] : 0.0;
         }
-        for (uint32_t v0 = vb + (uint32_t)wave * Q; v0 < ve; v0 += kWaves * Q) {
-            float2 x[4][Q];
+        // the row-block count as a template constant: every load of a group
+        // is issued back to back, with no branch between them (a branch per
+        // load made the compiler wait for each before issuing the next)
+        auto run = [&](auto nbc) {
+            constexpr int NB = decltype(nbc)::value;
+            for (uint32_t v0 = vb + (uint32_t)wave * Q; v0 < ve; v0 += kWaves * Q) {
+                float2 x[NB][Q];
 #pragma unroll
-            for (int b = 0; b < 4; b++)
+                for (int b = 0; b < NB; b++)
 #pragma unroll
-                for (int q = 0; q < Q; q++)
-                    x[b][q] = (uint32_t)b < NBr ? ldg2(Rt, rr[b].base + (size_t)min(v0 + (uint32_t)q, ve - 1) * rr[b].stride)
-                                                : make_float2(0.0f, 0.0f);
-            double v[Q];
+                    for (int q = 0; q < Q; q++)
+                        x[b][q] = ldg2(Rt, rr[b].base + (size_t)min(v0 + (uint32_t)q, ve - 1) * rr[b].stride);
+                double v[Q];
 #pragma unroll
-            for (int q = 0; q < Q; q++) {
-                double p = 0.0;
+                for (int q = 0; q < Q; q++) {
+                    double p = 0.0;
 #pragma unroll
-                for (int b = 0; b < 4; b++) {
-                    if ((uint32_t)b < NBr) {                   // wave-uniform
+                    for (int b = 0; b < NB; b++) {
                         const double mean = (double)x[b][q].x, var = (double)x[b][q].y;
                         const double xx = mean * mean + var;
                         const double pn = p + lw[b] * xx;
                         p = (uint32_t)b * 64 + lane < R ? pn : p;   // a select, not a branch
                     }
+                    v[q] = p;
                 }
-                v[q] = p;
-            }
-            const double t = tree16_transposed(v, lane);
-            if ((lane & 3) == 0) {
-                const uint32_t j = ((lane >> 5) & 1) | (((lane >> 4) & 1) << 1) | (((lane >> 3) & 1) << 2) | (((lane >> 2) & 1) << 3);
-                if (v0 + j < ve) {
-                    const float cw = (float)sqrt(t > 0.0 ? t : 0.0);
-                    colw[v0 + j] = cw;
-                    if (!isfinite(cw)) C.err = 1;
+                const double t = tree16_transposed(v, lane);
+                if ((lane & 3) == 0) {
+                    const uint32_t j = ((lane >> 5) & 1) | (((lane >> 4) & 1) << 1) | (((lane >> 3) & 1) << 2) | (((lane >> 2) & 1) << 3);
+                    if (v0 + j < ve) {
+                        const float cw = (float)sqrt(t > 0.0 ? t : 0.0);
+                        colw[v0 + j] = cw;
+                        if (!isfinite(cw)) C.err = 1;
+                    }
                 }
             }
-        }
+        };
+        if (NBr <= 1) run(std::integral_constant<int, 1>{});
+        else if (NBr == 2) run(std::integral_constant<int, 2>{});
+        else if (NBr == 3) run(std::integral_constant<int, 3>{});
+        else run(std::integral_constant<int, 4>{});
     } else {
         for (uint32_t v0 = vb + (uint32_t)wave * kCB; v0 < ve; v0 += kWaves * kCB) {
             double p[kCB];
@@ -4165,14 +4245,12 @@ __global__ void __launch_bounds__(kThreads) k_refine(const ALVRL_AS4 JobDev* __r
             const CNode cn = J.heap[k];
             Smp smp;
             smp.init(cm.seed, cm.pass, cn.begin, cn.end, J.stage_sample);
-            float prob = 1.0f;
-            int e = 0;
-            const uint32_t j = weighted_sample_wave(nullptr, J.colw, J.vrls + cn.begin, cn.end - cn.begin, smp,
-                                                    &e, 0xFFFFFFFFu, &prob);
+            const WsPick pk = weighted_sample_wave(nullptr, J.colw, J.vrls + cn.begin, cn.end - cn.begin, smp,
+                                                   0xFFFFFFFFu, true);
             if ((threadIdx.x & 63) == 0) {
-                if (e) atomicOr(&C.err, 1);
-                J.out_reps[ns + k] = J.vrls[cn.begin + j];
-                J.out_w[ns + k] = 1.0f / prob;
+                if (pk.err) atomicOr(&C.err, 1);
+                J.out_reps[ns + k] = J.vrls[cn.begin + pk.idx];
+                J.out_w[ns + k] = 1.0f / pk.prob;
             }
         }
     }
