@@ -81,7 +81,7 @@ def parse():
                     help="N > 1 with --shard slices: skip the second, pass-parallel measurement")
     ap.add_argument("--cpu-row-stride", type=int, default=64,
                     help="CPU baseline sample: every n-th image row")
-    ap.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "r04", "pmc_traffic_r4g.json"),
+    ap.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "r04", "pmc_traffic_r4h.json"),
                     help="per-launch HBM bytes of the dominant kernel from a rocprofv3 --pmc pass")
     ap.add_argument("--valu-json", default=os.path.join(REPO, "profiles", "r04", "pmc_valu_{cfg}.json"),
                     help="per-kernel VALU counters (tools/pmc_valu.sh + tools/pmc_valu.py)")

@@ -234,6 +234,18 @@ struct Common {
 // the leader's pop and quick commit: out of line by default (ALVRL_POP_INLINE=1
 // inlines them into k_refine, which drops the wait for every memory operation
 // in flight that a call's entry carries)
+// developer A/B: the split phases' helpers inlined into split() (no call-entry waits)
+#ifdef ALVRL_INL_PROJ
+#define ALVRL_PROJ_INL __forceinline__
+#else
+#define ALVRL_PROJ_INL __noinline__
+#endif
+// the weighted picks are inlined (C4 refinement -2 ms, profiles/r04/inl/); ALVRL_WS_OUTLINE: a call
+#ifdef ALVRL_WS_OUTLINE
+#define ALVRL_WS_INL __noinline__
+#else
+#define ALVRL_WS_INL __forceinline__
+#endif
 #ifdef ALVRL_POP_INLINE
 #define ALVRL_POP_INL __forceinline__
 #else
@@ -479,7 +491,7 @@ __device__ __forceinline__ float ws_block_wave(float x, uint32_t lane, float* to
 // pick (a reference to the caller's private Smp made every draw a per-lane
 // flat load and store); the caller resumes the stream at WsPick::k.
 struct WsPick { uint32_t idx, k; int err; float prob; };
-__device__ __noinline__ WsPick weighted_sample_wave(const float* wv, const float* colw, const uint32_t* ids,
+__device__ ALVRL_WS_INL WsPick weighted_sample_wave(const float* wv, const float* colw, const uint32_t* ids,
                                                     uint32_t m, Smp smp, uint32_t zero_at, bool want_prob,
                                                     bool wv_lds = false)
 {
@@ -2303,7 +2315,7 @@ __device__ __forceinline__ float key_proj(uint32_t u)
 {
     return __uint_as_float((u & 0x80000000u) ? (u & 0x7FFFFFFFu) : ~u);
 }
-__device__ __noinline__ unsigned long long* sort_keys(CJ& J_in, Ctl& C, uint32_t m, unsigned long long* lds_g)
+__device__ ALVRL_PROJ_INL unsigned long long* sort_keys(CJ& J_in, Ctl& C, uint32_t m, unsigned long long* lds_g)
 {
     CJ& J = uni(J_in);
     const int tid = threadIdx.x;
@@ -2492,7 +2504,7 @@ __device__ __forceinline__ PartJob part_job(CJ& J)
 // the split direction).  For R <= 64*kRB the batch's entries stay in
 // registers for both sums and the next batch's loads are in flight while
 // the current one is reduced (ping-pong buffers, no copies).
-__device__ __noinline__ void split_projections(CJ& J_in, CC& cm_in, uint32_t begin, uint32_t m)
+__device__ ALVRL_PROJ_INL void split_projections(CJ& J_in, CC& cm_in, uint32_t begin, uint32_t m)
 {
     CJ& J = uni(J_in);
     CC& cm = uni(cm_in);
