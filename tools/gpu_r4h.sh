@@ -8,7 +8,4 @@ ALVRL_POP_TRACE=1 ALVRL_REFINE_TEAM_STATS=1 timeout -k 10 200 python -u tools/c5
 ALVRL_REFINE_TEAM_STATS=1 timeout -k 10 200 python -u tools/c5_share.py --res 1024 --vrls 100000 --world 8 > gpurun_out/r4h_w8.log 2>&1 && \
 ALVRL_REFINE_PROFILE=1 ALVRL_REFINE_TEAM_STATS=1 timeout -k 10 200 python -u bench.py --config C4 --steps 2 --warmup 1 --no-cpu-baseline --no-alt > gpurun_out/r4h_prof_c4.json 2> gpurun_out/r4h_prof_c4.err
 rc=$?
-# part_min for short jobs (env knob): 2048 and 1024 columns at rank 0 of 8
-[ $rc -eq 0 ] && ALVRL_PART_MIN=2048 ALVRL_REFINE_TEAM_STATS=1 timeout -k 10 200 python -u tools/c5_share.py --res 1024 --vrls 100000 --world 8 > gpurun_out/r4h_w8_pm2048.log 2>&1 && \
-ALVRL_PART_MIN=1024 ALVRL_REFINE_TEAM_STATS=1 timeout -k 10 200 python -u tools/c5_share.py --res 1024 --vrls 100000 --world 8 > gpurun_out/r4h_w8_pm1024.log 2>&1
-echo "== r4h exit=$rc $?"
+echo "== r4h exit=$rc"
