@@ -241,6 +241,21 @@ ALVRL_API int alvrl_build_R_blocks(alvrl_ctx *ctx, const alvrl_gather_rec *d_rec
                                    const uint64_t *d_row_off, const uint32_t *d_row_stride,
                                    uint8_t *d_nonzero, void *stream);
 
+/* The R build in the CPU restatement's arithmetic (no replaced reference
+ * function: a mode of alvrl_build_R / alvrl_build_R_blocks).  on != 0: both
+ * evaluate integrateVRL (vrlIntegrator.cpp:603-785) statement for statement
+ * as oracle/alvrl_oracle.c does, with IEEE division / sqrt, no contraction and
+ * the deterministic transcendentals of csrc/detmath.h, so every R entry is the
+ * oracle's bit for bit and the clustering downstream reproduces the oracle's
+ * own pipeline.  Slower than the default fast build.
+ * Integrator property "strictRbuild". */
+ALVRL_API int alvrl_set_strict_rbuild(alvrl_ctx *ctx, int on);
+
+/* csrc/detmath.h on the current device, elementwise over n floats (device
+ * pointers; fn 0 exp, 1 log, 2 atan, 3 tan, 4 asinh, 5 sinh): the host =
+ * device check of the definitions the strict paths share with the oracle. */
+ALVRL_API int alvrl_detmath_eval(int fn, const float *d_in, float *d_out, uint32_t n, void *stream);
+
 /* ---- hot path (b) part 2: cluster refinement ------------------------- */
 /* One Clustering (Preprocessor.cpp:287-720): ctor (column weights, initial
  * clusters, unclustered variances, :301-341), optional refine() (:380-489),

@@ -261,7 +261,10 @@ typedef struct {
     alvrl_medium_desc medium;           /* the homogeneous medium the VRLs live in */
     /* W*H records, row-major (y*W + x): the gather point of the ray through
      * the pixel centre -- ALVRL_REC_HIT, p and the shading normal; no HIT
-     * flag for a ray that leaves the scene (the pixel gets no slice) */
+     * flag for a ray that leaves the scene (the pixel gets no slice).
+     * NULL: no slicing -- a render worker that receives its slices and
+     * cluster lists through alvrl_integrator_set_cluster_info (wakeup,
+     * vrlIntegrator.cpp:378-384); such an integrator cannot run a prepass. */
     const alvrl_gather_rec *slice_recs;
     /* every triangle of the scene, 9 floats each, for the gathers' occluder
      * test (Scene::evalTransmittance, scene.cpp:619-679); ALVRL_MAT_NULL

@@ -109,6 +109,8 @@ def lib() -> C.CDLL:
     L.alvrl_last_kernel_ms.argtypes = [vp, P(f32)]
     L.alvrl_nonzero_columns.argtypes = [vp, vp, u64, u32, vp, vp]
     L.alvrl_accumulate_rgb.argtypes = [vp, vp, vp, u32, vp, vp]
+    L.alvrl_set_strict_rbuild.argtypes = [vp, i32]
+    L.alvrl_detmath_eval.argtypes = [i32, vp, vp, u32, vp]
     _lib = L
     return L
 
@@ -127,7 +129,7 @@ def build_info() -> dict:
         bid = "unknown"
     os_ = os.path
     rel = []
-    for pat in ("csrc/*.hip", "csrc/*.hpp", "csrc/host/*.cpp", "csrc/host/*.hpp", "../include/*.h"):
+    for pat in ("csrc/*.hip", "csrc/*.hpp", "csrc/*.h", "csrc/host/*.cpp", "csrc/host/*.hpp", "../include/*.h"):
         rel += [os_.relpath(p, PKG_DIR) for p in glob.glob(os_.join(PKG_DIR, pat))]
     h = hashlib.sha1()
     for r in sorted(rel):
@@ -136,6 +138,16 @@ def build_info() -> dict:
     tree = h.hexdigest()[:16]
     return {"library": os_.relpath(LIB_PATH, REPO), "build_id": bid, "src_hash_tree": tree,
             "matches_tree": bid.split()[1] == tree if bid.startswith("src ") else False}
+
+
+DETMATH_FNS = ("exp", "log", "atan", "tan", "asinh", "sinh")
+
+
+def detmath_eval(fn: str, d_in, d_out, stream=None):
+    """csrc/detmath.h's float function `fn` on the device, elementwise over
+    float32 CUDA tensors (alvrl_detmath_eval)."""
+    _check(lib().alvrl_detmath_eval(DETMATH_FNS.index(fn), _ptr(d_in), _ptr(d_out), int(d_in.numel()),
+                                    C.c_void_p(stream) if stream else None))
 
 
 def _check(rc: int):
@@ -274,6 +286,11 @@ class Context:
 
     def set_rsamples(self, n: int):
         _check(self.L.alvrl_set_rsamples(self.h, n))
+
+    def set_strict_rbuild(self, on: bool = True):
+        """The R build in the oracle's arithmetic (alvrl_set_strict_rbuild): R
+        entries equal the CPU restatement's bit for bit."""
+        _check(self.L.alvrl_set_strict_rbuild(self.h, int(bool(on))))
 
     def build_R_blocks(self, d_recs, d_Rt, d_row_off, d_row_stride, d_nonzero=None, d_ids=None,
                        stream=None):

@@ -44,6 +44,11 @@ hipError_t launch_build_R_blocks(const Rec* recs, const uint32_t* ids, uint32_t 
                                  uint32_t nvrl, const DevParams& P, float normalization, float2* Rt,
                                  const uint64_t* roff, const uint32_t* rstride, uint8_t* nonzero,
                                  unsigned long long* counter, hipStream_t s);
+hipError_t launch_build_R_strict(const Rec* recs, const uint32_t* ids, uint32_t nrows, const float* soa,
+                                 uint32_t nvrl, const DevParams& P, float normalization, float2* Rt, uint64_t ld,
+                                 uint64_t row0, const uint64_t* roff, const uint32_t* rstride, uint8_t* nonzero,
+                                 unsigned long long* counter, hipStream_t s);
+hipError_t launch_detmath(int fn, const float* in, float* out, uint32_t n, hipStream_t s);
 hipError_t launch_false_color(const Rec* recs, const WorkItem* items, uint32_t n, int mode,
                               const uint32_t* slice_off, uint32_t n_fb, uint32_t nvrl, float* out,
                               unsigned long long* counter, hipStream_t s);
@@ -141,6 +146,7 @@ struct alvrl_ctx {
     float* d_fb_w = nullptr;
     uint32_t cap_slices = 0, cap_rep = 0, cap_fb = 0;   // grow-only: a prepass re-sets them every pass
     bool clusters_set = false;
+    bool strict_rb = false;   // alvrl_set_strict_rbuild: the R build in the oracle's arithmetic
     float refine_ms = 0.0f;
     unsigned long long refine_entries[2] = {0, 0};   // refine_jobs: all entries, the splits' share
     // occluder BVH (alvrl_set_occluders); P.occ views it
@@ -537,8 +543,13 @@ ALVRL_API int alvrl_build_R(alvrl_ctx* c, const alvrl_gather_rec* d_recs, const 
     const float norm = (float)(1.0 / (double)c->particle_count);
     SLOT(c, ts);
     HIPCHK(hipEventRecord(ts->ev0, s));
-    HIPCHK(launch_build_R(reinterpret_cast<const Rec*>(d_recs), d_ids, nrows, c->d_vrl, c->nvrl, c->P,
-                          norm, reinterpret_cast<float2*>(d_Rt), ld, row0, c->d_counter + 0, s));
+    if (c->strict_rb)
+        HIPCHK(launch_build_R_strict(reinterpret_cast<const Rec*>(d_recs), d_ids, nrows, c->d_soa, c->nvrl, c->P,
+                                     norm, reinterpret_cast<float2*>(d_Rt), ld, row0, nullptr, nullptr, nullptr,
+                                     c->d_counter + 0, s));
+    else
+        HIPCHK(launch_build_R(reinterpret_cast<const Rec*>(d_recs), d_ids, nrows, c->d_vrl, c->nvrl, c->P,
+                              norm, reinterpret_cast<float2*>(d_Rt), ld, row0, c->d_counter + 0, s));
     HIPCHK(hipEventRecord(ts->ev1, s));
     ts->timed = true;
     return ALVRL_OK;
@@ -550,6 +561,22 @@ ALVRL_API int alvrl_set_rsamples(alvrl_ctx* c, int rsamples)
     if (rsamples < 1 || rsamples > 0xFFFF) return fail(ALVRL_ERR_INVALID, "Rsamples must be in [1, 2^16)");
     std::lock_guard<std::mutex> g(c->mu);
     c->P.rsamples = rsamples;
+    return ALVRL_OK;
+}
+
+ALVRL_API int alvrl_set_strict_rbuild(alvrl_ctx* c, int on)
+{
+    if (!c) return fail(ALVRL_ERR_INVALID, "alvrl_set_strict_rbuild: null ctx");
+    std::lock_guard<std::mutex> g(c->mu);
+    c->strict_rb = on != 0;
+    return ALVRL_OK;
+}
+
+ALVRL_API int alvrl_detmath_eval(int fn, const float* d_in, float* d_out, uint32_t n, void* stream)
+{
+    if (fn < 0 || fn > 5) return fail(ALVRL_ERR_INVALID, "alvrl_detmath_eval: fn must be in [0, 5]");
+    if (n && (!d_in || !d_out)) return fail(ALVRL_ERR_INVALID, "alvrl_detmath_eval: null buffer");
+    HIPCHK(launch_detmath(fn, d_in, d_out, n, (hipStream_t)stream));
     return ALVRL_OK;
 }
 
@@ -567,9 +594,14 @@ ALVRL_API int alvrl_build_R_blocks(alvrl_ctx* c, const alvrl_gather_rec* d_recs,
     const float norm = (float)(1.0 / (double)c->particle_count);
     SLOT(c, ts);
     HIPCHK(hipEventRecord(ts->ev0, s));
-    HIPCHK(launch_build_R_blocks(reinterpret_cast<const Rec*>(d_recs), d_ids, nrows, c->d_vrl, c->nvrl, c->P,
-                                 norm, reinterpret_cast<float2*>(d_Rt), d_row_off, d_row_stride, d_nonzero,
-                                 c->d_counter + 0, s));
+    if (c->strict_rb)
+        HIPCHK(launch_build_R_strict(reinterpret_cast<const Rec*>(d_recs), d_ids, nrows, c->d_soa, c->nvrl, c->P,
+                                     norm, reinterpret_cast<float2*>(d_Rt), 0, 0, d_row_off, d_row_stride,
+                                     d_nonzero, c->d_counter + 0, s));
+    else
+        HIPCHK(launch_build_R_blocks(reinterpret_cast<const Rec*>(d_recs), d_ids, nrows, c->d_vrl, c->nvrl, c->P,
+                                     norm, reinterpret_cast<float2*>(d_Rt), d_row_off, d_row_stride, d_nonzero,
+                                     c->d_counter + 0, s));
     HIPCHK(hipEventRecord(ts->ev1, s));
     ts->timed = true;
     return ALVRL_OK;

@@ -11,6 +11,8 @@
 #include <sstream>
 #include <string>
 
+#include "detmath.h"
+
 namespace alvrl {
 namespace host {
 
@@ -20,8 +22,10 @@ constexpr uint32_t kDomTracer = 3u;
 constexpr uint32_t kDomEye = 7u;   // Russian roulette of the eye paths' specular chains
 constexpr uint32_t kDomPixel = 8u;   // sensor sample offsets of multi-sample renders
 
-inline float fastexp(float v) { return (float)std::exp((double)v); }   // math.h:185-199
-inline float fastlog(float v) { return (float)std::log((double)v); }
+// math::fastexp / fastlog (math.h:185-199) with the deterministic definitions
+// the oracle and tracer.hip share (detmath.h, DESIGN.md section 8 deviation 3)
+inline float fastexp(float v) { return dm_expf(v); }
+inline float fastlog(float v) { return dm_logf(v); }
 inline float safe_sqrt(float v) { return std::sqrt(v > 0.0f ? v : 0.0f); }
 }  // namespace
 

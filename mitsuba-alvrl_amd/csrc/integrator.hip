@@ -117,6 +117,7 @@ struct alvrl_integrator {
     int rrDepth = 5, maxDepth = -1;
     uint32_t seed = 0xA1B2C3D4u, vrlSeed = 0x5EED0001u;
     bool gpuTracer = false;   // trace the pass's VRLs on the device (csrc/tracer.hip)
+    bool strictRbuild = false;   // the R build in the oracle's arithmetic (alvrl_set_strict_rbuild)
     // ---- state
     int device = 0;
     alvrl_ctx* ctx = nullptr;
@@ -200,6 +201,7 @@ struct alvrl_integrator {
         if (k == "nc") throw IntegError(ALVRL_ERR_INVALID, "Neighbourcount is now called 'neighbourCount' instead of 'nc'!");
         else if (k == "shortVrls") shortVrls = b(v);
         else if (k == "gpuTracer") gpuTracer = b(v);
+        else if (k == "strictRbuild") strictRbuild = b(v);
         else if (k == "vrlTargetNum") vrlTargetNum = i(v);
         else if (k == "maxParticleDepth") maxParticleDepth = i(v);
         else if (k == "specularForcedRRdepth") specRRdepth = i(v);
@@ -307,7 +309,6 @@ struct alvrl_integrator {
     void preprocess_ext(const alvrl_scene_ext& e)
     {
         if (e.width <= 0 || e.height <= 0) throw IntegError(ALVRL_ERR_INVALID, "alvrl_scene_ext: width and height must be > 0");
-        if (!e.slice_recs) throw IntegError(ALVRL_ERR_INVALID, "alvrl_scene_ext: slice_recs is required");
         if (e.n_triangles && !e.triangles) throw IntegError(ALVRL_ERR_INVALID, "alvrl_scene_ext: n_triangles > 0 without triangles");
         MediumParams m = medium_of(e.medium);
         if (const char* p = m.problem()) throw IntegError(ALVRL_ERR_INVALID, p);
@@ -333,7 +334,13 @@ struct alvrl_integrator {
         chk(alvrl_set_occluders(ctx, scene.occ.empty() ? nullptr : scene.occ.data(), scene.n_occ(),
                                 scene.occ_mat.empty() ? nullptr : scene.occ_mat.data()), "alvrl_set_occluders");
         load_vrl_file();
-        if (clustered) {
+        prep.reset();
+        pixel_to_slice.clear();
+        st.slices = 0;
+        // no gather points: a render worker whose slices and cluster lists
+        // arrive through alvrl_integrator_set_cluster_info (the reference's
+        // wakeup, vrlIntegrator.cpp:378-384) and that never runs a prepass
+        if (clustered && e.slice_recs) {
             PrepParams pp;
             pp.target_num_slices = (uint32_t)targetNumSlices;
             pp.neighbour_count = (uint32_t)neighbourCount;
@@ -1052,6 +1059,7 @@ struct alvrl_integrator {
         // first hit (:461-462); numVrlFalseColor keeps weight 1 down the
         // chain (:502-503), which the false-colour kernel never applies.
         uint32_t levels = (uint32_t)level_rec.size() - 1;
+        render_timed = false;   // get_stats' ms_render_kernel: the gather of this render only
         if (numVrlFalseColor || slicesFalseColor) {
             if (!clustered && !numVrlFalseColor)
                 throw IntegError(ALVRL_ERR_INVALID, "requested slices false color image without clustering!");
@@ -1061,7 +1069,6 @@ struct alvrl_integrator {
                                          clustered ? level_item[levels] : level_rec[levels], out_buf.p, s),
                 "alvrl_gather_false_color");
         } else {
-            render_timed = false;
             hchk(hipEventRecord(ev_r0, s), "hipEventRecord");
             if (clustered)
                 chk(alvrl_gather_clustered(ctx, rec_buf.p, pix_buf.p, item_buf.p, nitems, out_buf.p, s),
@@ -1138,6 +1145,7 @@ ALVRL_API int alvrl_integrator_create(const char* props, int device, alvrl_integ
         alvrl_config cfg{device, it->volVolSamples, it->volSurfSamples, it->shortVrls ? 1 : 0, it->seed};
         chk(alvrl_ctx_create(&cfg, &it->ctx), "alvrl_ctx_create");
         chk(alvrl_set_rsamples(it->ctx, it->Rsamples), "alvrl_set_rsamples");
+        chk(alvrl_set_strict_rbuild(it->ctx, it->strictRbuild ? 1 : 0), "alvrl_set_strict_rbuild");
         hchk(hipSetDevice(device), "hipSetDevice");
         hchk(hipStreamCreateWithFlags(&it->stream, hipStreamNonBlocking), "hipStreamCreate");
         hchk(hipEventCreate(&it->ev_r0), "hipEventCreate");

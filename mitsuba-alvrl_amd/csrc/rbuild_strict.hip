@@ -1,0 +1,498 @@
+// rbuild_strict.hip -- the R build in the oracle's arithmetic (integrator
+// property strictRbuild, alvrl_set_strict_rbuild).
+//
+// getLiLuminanceVrlContributions (vrlIntegrator.cpp:527-539) through
+// integrateVRL's mean / variance outputs (:603-785) and its samplers
+// (:831-1032), HomogeneousMedium::eval (homogeneous.cpp:354-396) and the
+// shadow term of Scene::evalTransmittance (scene.cpp:619-679), evaluated
+// statement for statement in the order of the CPU restatement
+// (oracle/alvrl_oracle.c integrate_vrl_w): IEEE float division and sqrt, no
+// contraction (this file is built with -ffp-contract=off and without the
+// gathers' approximate division), and the transcendentals of detmath.h, which
+// the oracle shares.  Its R entries are the oracle's bit for bit, so the
+// discrete clustering decisions downstream (already bit-exact given the same R,
+// refine.hip) follow the oracle's own pipeline (tests/test_gpu_strict.py).
+//
+// The fast build (gather.hip k_build_R_blocks) keeps the reduced forms and the
+// hardware transcendentals and matches the oracle on the error distribution
+// stated in tests/test_gpu_parity.py; its clusters may then differ from the
+// oracle's where R rounds differently.
+//
+// Values the oracle recomputes but that are identical by construction (the
+// row's eye segment and vol->surf transmittance, a pair's closest points and
+// asinh bounds, the pdf and transmittance exponentials of one distance) are
+// evaluated once: the same operations on the same operands give the same bits.
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+
+#include "detmath.h"
+#include "vrl_device.hpp"
+
+namespace alvrl {
+namespace strict {
+
+struct V3 { float x, y, z; };
+__device__ __forceinline__ V3 mk(float x, float y, float z) { return V3{x, y, z}; }
+__device__ __forceinline__ V3 sub(V3 a, V3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ V3 add(V3 a, V3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ V3 scl(V3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
+__device__ __forceinline__ V3 neg(V3 a) { return mk(-a.x, -a.y, -a.z); }
+__device__ __forceinline__ float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ float len2(V3 a) { return a.x * a.x + a.y * a.y + a.z * a.z; }
+__device__ __forceinline__ float len(V3 a) { return sqrtf(len2(a)); }
+__device__ __forceinline__ float dist(V3 a, V3 b) { return len(sub(a, b)); }
+__device__ __forceinline__ float dist2(V3 a, V3 b) { return len2(sub(a, b)); }
+// normalize(v) = v * (1 / |v|) (operator/ multiplies by the reciprocal)
+__device__ __forceinline__ V3 nrm(V3 a) { const float r = 1.0f / len(a); return scl(a, r); }
+
+constexpr float kEps = 1e-4f;
+constexpr uint32_t kFlagHit = 1u, kFlagSmooth = 2u, kFlagMedium = 4u;
+
+// Random-access draw k of the counter stream (dom, a, b, c), one Philox
+// block of four cached (oracle draw()).
+struct Draws {
+    uint32_t a, b, c, seed, pass, blk;
+    U4 buf;
+    __device__ __forceinline__ float at(uint32_t k)
+    {
+        const uint32_t bk = k >> 2;
+        if (bk != blk) {
+            buf = philox4x32_10(a, b, bk, (kDomRbuild << 24) | (c & 0xFFFFFFu), seed, pass);
+            blk = bk;
+        }
+        const uint32_t j = k & 3u;
+        return u01(j == 0 ? buf.x : j == 1 ? buf.y : j == 2 ? buf.z : buf.w);
+    }
+};
+
+// MaxExpDist::cdf (maxexp.h:83-94)
+__device__ __forceinline__ float mxexp_cdf(const DevParams& P, float t)
+{
+    int k = 0;
+    while (k < 3 && P.mx_start[k] < t) k++;
+    const int i = k > 0 ? k - 1 : 0;
+    const float upper = -dm_expf(-P.mx_sigma[i] * t);
+    return P.mx_cdf[i] + (upper - P.mx_lower[i]) * P.mx_inv_norm;
+}
+
+// HomogeneousMedium::eval (homogeneous.cpp:354-396): transmittance and the
+// pdfFailure of the sampling strategy
+__device__ __forceinline__ void medium_eval(const DevParams& P, float distance, float tr[3], float* pdf_failure)
+{
+    const float e0 = dm_expf(P.sigma_t[0] * (-distance));
+    const float e1 = dm_expf(P.sigma_t[1] * (-distance));
+    const float e2 = dm_expf(P.sigma_t[2] * (-distance));
+    float pf = 0.0f;
+    if (P.strategy == 0) {
+        pf += e0; pf += e1; pf += e2;
+        pf /= 3;
+    } else if (P.strategy == 3) {
+        pf = 1 - mxexp_cdf(P, distance);
+    } else {
+        pf = dm_expf(-P.density * distance);
+    }
+    tr[0] = e0; tr[1] = e1; tr[2] = e2;
+    *pdf_failure = pf * P.w + (1 - P.w);
+    float mx = tr[0] > tr[1] ? tr[0] : tr[1];
+    mx = mx > tr[2] ? mx : tr[2];
+    if (mx < 1e-20f) tr[0] = tr[1] = tr[2] = 0.0f;
+}
+
+// Scene::evalTransmittance(p1, p1OnSurface, p2): exp(-sigma_t |p2 - p1|) per
+// channel, zero when an occluder (not a null surface) lies on the segment
+__device__ __forceinline__ void shadow_transmittance(const DevParams& P, V3 p1, bool p1_surface, V3 p2, float tr[3])
+{
+    const V3 d = sub(p2, p1);
+    const float remaining = len(d);
+    const float negLength = 0.0f - remaining;
+    for (int i = 0; i < 3; i++) tr[i] = P.sigma_t[i] != 0 ? dm_expf(P.sigma_t[i] * negLength) : 1.0f;
+    if (P.occ.ntri == 0 || !(remaining > 0)) return;
+    const V3 dn = scl(d, 1.0f / remaining);
+    const float mint = p1_surface ? 1e-4f : 0.0f;
+    const float maxt = remaining * 1.0f;
+    if (bvh::occluded(P.occ, bvh::mk(p1.x, p1.y, p1.z), bvh::mk(dn.x, dn.y, dn.z), mint, maxt))
+        tr[0] = tr[1] = tr[2] = 0.0f;
+}
+
+// isotropic.cpp:76-78, hg.cpp:107-110
+__device__ __forceinline__ float phase_eval(const DevParams& P, V3 wi, V3 wo)
+{
+    if (P.phase_type == 0) return kInvFourPi;
+    const float g = P.g;
+    const float temp = 1.0f + g * g + 2.0f * g * dot(wi, wo);
+    return kInvFourPi * (1 - g * g) / (temp * sqrtf(temp));
+}
+
+// getClosestPoints (vrlIntegrator.cpp:962-1032); returns |dP| and the closest
+// point on the second segment
+__device__ __forceinline__ float closest_points(V3 S1P0, V3 S1P1, V3 S2P0, V3 S2P1, V3* S2h)
+{
+    const V3 u = sub(S1P1, S1P0), v = sub(S2P1, S2P0), w = sub(S1P0, S2P0);
+    const float a = dot(u, u), b = dot(u, v), c = dot(v, v), d = dot(u, w), e = dot(v, w);
+    const float D = a * c - b * b;
+    float sN, sD = D, tN, tD = D;
+    if (D < kEps * len2(u) * len2(v)) {
+        sN = 0.0f; sD = 1.0f; tN = e; tD = c;
+    } else {
+        sN = (b * e - c * d);
+        tN = (a * e - b * d);
+        if (sN < 0.0f) { sN = 0.0f; tN = e; tD = c; }
+        else if (sN > sD) { sN = sD; tN = e + b; tD = c; }
+    }
+    if (tN < 0.0f) {
+        tN = 0.0f;
+        if (-d < 0.0f) sN = 0.0f;
+        else if (-d > a) sN = sD;
+        else { sN = -d; sD = a; }
+    } else if (tN > tD) {
+        tN = tD;
+        if ((-d + b) < 0.0f) sN = 0;
+        else if ((-d + b) > a) sN = sD;
+        else { sN = (-d + b); sD = a; }
+    }
+    const float sc = sN / sD;
+    const float tc = tN / tD;
+    const V3 dP = sub(add(w, scl(u, sc)), scl(v, tc));
+    *S2h = add(S2P0, scl(sub(S2P1, S2P0), tc));
+    return len(dP);
+}
+
+// KullaSampling (vrlIntegrator.cpp:889-914) split into the part fixed by the
+// segment A->B and the point D, and the per-uniform sample
+struct Kulla { V3 dir, I; float Dis, aa, ab; };
+
+__device__ __forceinline__ Kulla kulla_frame(V3 A, V3 B, V3 dir, V3 D)
+{
+    Kulla k;
+    k.dir = dir;
+    const float dotPr = dot(dir, sub(D, A));
+    k.I = add(A, scl(dir, dotPr));
+    k.Dis = dist(D, k.I);
+    float angle_a = dm_atanf(dist(A, k.I) / k.Dis);
+    float angle_b = dm_atanf(dist(k.I, B) / k.Dis);
+    if (dotPr > 0) {
+        angle_a *= -1;
+        if (dist(A, k.I) > dist(A, B)) angle_b *= -1;
+    }
+    k.aa = angle_a; k.ab = angle_b;
+    return k;
+}
+
+__device__ __forceinline__ float kulla_sample(const Kulla& k, float uniform, V3* result)
+{
+    const float t = k.Dis * dm_tanf(((1.0f - uniform) * k.aa) + (uniform * k.ab));
+    const float pdf = k.Dis / ((k.ab - k.aa) * (k.Dis * k.Dis + t * t));
+    *result = add(k.I, scl(k.dir, t));
+    return pdf;
+}
+
+// sampleVtoDistance (vrlIntegrator.cpp:916-953), the uniform-free part
+struct Novak {
+    int mode;           // 0: zero-length VRL, 1: parallel (uniform on the VRL), 2: Novak
+    float invlen;       // 1 / distance(End, S) (mode 1)
+    float h, sinTheta, A0, A1, denom, dVhS;
+    V3 dirSE;           // normalize(End - S)
+};
+
+__device__ __forceinline__ Novak novak_frame(V3 E, V3 d, V3 hitp, V3 S, V3 End)
+{
+    Novak n;
+    n.mode = 0;
+    if (dist(S, End) == 0) return n;
+    const float cosTheta = dot(nrm(d), nrm(sub(End, S)));
+    const float st2 = 1 - cosTheta * cosTheta;
+    n.sinTheta = sqrtf(st2 > 0.0f ? st2 : 0.0f);
+    if (n.sinTheta < kEps) {
+        n.mode = 1;
+        n.invlen = 1 / dist(End, S);
+        return n;
+    }
+    n.mode = 2;
+    V3 Vh;
+    n.h = closest_points(E, hitp, S, End, &Vh);
+    const float V0c = -1 * dist(Vh, S);
+    const float V1c = dist(Vh, End);
+    n.A0 = dm_asinhf((V0c / n.h) * n.sinTheta);
+    n.A1 = dm_asinhf((V1c / n.h) * n.sinTheta);
+    n.denom = (n.A1 - n.A0) / n.sinTheta;
+    n.dVhS = dist(Vh, S);
+    n.dirSE = nrm(sub(End, S));
+    return n;
+}
+
+__device__ __forceinline__ float novak_sample(const Novak& n, V3 S, V3 End, float uniform, V3* V)
+{
+    if (n.mode == 0) { *V = S; return 1; }
+    if (n.mode == 1) { *V = add(S, scl(sub(End, S), uniform)); return n.invlen; }
+    float newV = n.h * dm_sinhf(n.A0 + (uniform * (n.A1 - n.A0)));
+    newV = newV / n.sinTheta;
+    const float result = 1.0f / sqrtf(n.h * n.h + newV * newV * n.sinTheta * n.sinTheta);
+    newV += n.dVhS;
+    *V = add(S, scl(n.dirSE, newV));
+    return result / n.denom;
+}
+
+// the row's eye segment: everything integrateVRL derives without the VRL
+struct Row {
+    V3 E, d, U, n, A, B, dirAB;
+    float alb[3], wt[3], teus[3], cos_wi;
+    uint32_t flags, rid, sw;
+    bool surf;
+};
+
+__device__ __forceinline__ Row make_row(const DevParams& P, const Rec& r, uint32_t rid)
+{
+    Row w;
+    w.E = mk(r.ox, r.oy, r.oz); w.d = mk(r.dx, r.dy, r.dz);
+    w.U = mk(r.px, r.py, r.pz); w.n = mk(r.nx, r.ny, r.nz);
+    w.alb[0] = r.ar; w.alb[1] = r.ag; w.alb[2] = r.ab;
+    w.wt[0] = r.wr; w.wt[1] = r.wg; w.wt[2] = r.wb;      // use_weight: the record's path weight
+    w.flags = r.flags;
+    w.rid = rid;
+    w.sw = ((r.depth & 0xFFu) << 16) | ((r.depth >> 16) & 0xFFFFu);
+    const float edist = dist(w.U, w.E);                  // sampleUVKulla :865-871
+    w.A = w.E;
+    w.B = add(w.E, scl(w.d, edist));
+    w.dirAB = nrm(sub(w.B, w.A));
+    w.teus[0] = w.teus[1] = w.teus[2] = 0.0f;
+    if ((r.flags & kFlagHit) && dist(w.U, w.E) != 0) {
+        float pfd;
+        medium_eval(P, dist(w.U, w.E), w.teus, &pfd);
+    }
+    w.surf = (w.teus[0] != 0 || w.teus[1] != 0 || w.teus[2] != 0) && (r.flags & kFlagSmooth);
+    w.cos_wi = dot(neg(w.d), w.n);
+    return w;
+}
+
+__device__ __forceinline__ float lum(const float c[3]) { return c[0] * 0.212671f + c[1] * 0.715160f + c[2] * 0.072169f; }
+__device__ __forceinline__ bool valid(const float c[3])
+{
+    for (int i = 0; i < 3; i++)
+        if (!isfinite(c[i]) || c[i] < 0.0f) return false;
+    return true;
+}
+
+// integrate_vrl_w's contribution (mean) and variance outputs for one pair
+__device__ void integrate_R(const DevParams& P, const Row& w, const float* __restrict__ soa, uint32_t nvrl,
+                            uint32_t v, uint32_t rsub, float* contrib, float* variance)
+{
+    *contrib = 0; *variance = 0;
+    if (!(w.flags & kFlagMedium)) return;
+    const V3 S = mk(soa[0 * (size_t)nvrl + v], soa[1 * (size_t)nvrl + v], soa[2 * (size_t)nvrl + v]);
+    const V3 End = mk(soa[3 * (size_t)nvrl + v], soa[4 * (size_t)nvrl + v], soa[5 * (size_t)nvrl + v]);
+    const float power[3] = {soa[6 * (size_t)nvrl + v], soa[7 * (size_t)nvrl + v], soa[8 * (size_t)nvrl + v]};
+    const V3 SV = nrm(sub(End, S));
+    const V3 EU = w.d;
+    const int nVV = P.nvv, nVS = P.nvs;
+    const uint32_t koff = (rsub & 0xFFFFu) << 10;
+    Draws dr{w.rid, v, w.sw, P.seed, P.pass, 0xFFFFFFFFu, U4{0u, 0u, 0u, 0u}};
+
+    // ---- volume to volume (:647-703) ----
+    const Novak nv = novak_frame(w.E, w.d, w.U, S, End);
+    float mean = 0, M2 = 0;
+    for (int sample = 0; sample < nVV; sample++) {
+        float lumv = 0.0f;
+        const float u0 = dr.at(koff + 2 * sample);
+        const float u1 = dr.at(koff + 2 * sample + 1);
+        V3 V, U;
+        float pdf = novak_sample(nv, S, End, u0, &V);
+        pdf *= kulla_sample(kulla_frame(w.A, w.B, w.dirAB, V), u1, &U);
+        if (dist(U, V) != 0) {
+            const V3 VU = nrm(sub(U, V));
+            float tuv[3], teu[3], tsv[3], pf_eu, pf_sv;
+            shadow_transmittance(P, U, false, V, tuv);
+            if (!(tuv[0] == 0 && tuv[1] == 0 && tuv[2] == 0)) {
+                medium_eval(P, dist(w.E, U), teu, &pf_eu);
+                medium_eval(P, dist(S, V), tsv, &pf_sv);
+                const float rpdf = 1.0f / pdf;
+                const float rd2 = 1 / dist2(U, V);
+                const float phU = phase_eval(P, neg(VU), neg(EU));
+                const float phV = phase_eval(P, neg(SV), VU);
+                const float rpf = 1.0f / pf_sv;
+                float c[3];
+                for (int i = 0; i < 3; i++) {
+                    c[i] = w.wt[i];
+                    c[i] *= power[i];
+                    c[i] *= (P.sigma_s[i] * P.sigma_s[i]) * rpdf;
+                    c[i] *= rd2;
+                    c[i] *= tsv[i];
+                    c[i] *= tuv[i];
+                    c[i] *= teu[i];
+                    if (P.short_vrls) c[i] *= rpf;
+                    c[i] *= phU;
+                    c[i] *= phV;
+                }
+                if (valid(c)) lumv = lum(c);
+            }
+        }
+        const float delta = lumv - mean;                 // :693-699
+        mean += delta / (sample + 1);
+        M2 += delta * (lumv - mean);
+    }
+    if (nVV > 0) { *contrib += mean; *variance += M2 / ((nVV - 1) * nVV); }
+
+    // ---- volume to surface (:706-782) ----
+    mean = 0; M2 = 0;
+    if (w.surf && nVS > 0) {
+        const Kulla ks = kulla_frame(S, End, nrm(sub(End, S)), w.U);
+        for (int sample = 0; sample < nVS; sample++) {
+            float lumv = 0.0f;
+            const float u = dr.at(koff + 2 * nVV + sample);
+            V3 V;
+            const float pdf = kulla_sample(ks, u, &V);
+            if (dist(w.U, V) != 0) {
+                const V3 VU = nrm(sub(w.U, V));
+                float tuv[3], tsv[3], pf_sv;
+                shadow_transmittance(P, w.U, true, V, tuv);
+                medium_eval(P, dist(S, V), tsv, &pf_sv);
+                // SmoothDiffuse::eval (diffuse.cpp:110-118)
+                const float cos_wo = dot(neg(VU), w.n);
+                float f[3] = {0, 0, 0};
+                if (!(w.cos_wi <= 0 || cos_wo <= 0))
+                    for (int i = 0; i < 3; i++) f[i] = w.alb[i] * (kInvPi * cos_wo);
+                const float phV = phase_eval(P, neg(SV), VU);
+                const float rpdf = 1.0f / pdf;
+                const float rd2 = 1 / dist2(w.U, V);
+                const float rpf = 1.0f / pf_sv;
+                float c[3];
+                for (int i = 0; i < 3; i++) {
+                    c[i] = w.wt[i];
+                    c[i] *= power[i];
+                    c[i] *= P.sigma_s[i] * rpdf;
+                    c[i] *= rd2;
+                    c[i] *= tsv[i];
+                    c[i] *= tuv[i];
+                    c[i] *= w.teus[i];
+                    if (P.short_vrls) c[i] *= rpf;
+                    c[i] *= phV;
+                    c[i] *= f[i];
+                }
+                if (valid(c)) lumv = lum(c);
+            }
+            const float delta = lumv - mean;
+            mean += delta / (sample + 1);
+            M2 += delta * (lumv - mean);
+        }
+    } else {
+        // no surface sample contributes: the Welford recurrence over zeros
+        // leaves mean = M2 = 0
+    }
+    if (nVS > 0) { *contrib += mean; *variance += M2 / ((nVS - 1) * nVS); }
+}
+
+__device__ __forceinline__ Rec load_rec(const Rec* __restrict__ recs, uint32_t r)
+{
+    const float4* p = reinterpret_cast<const float4*>(recs + r);
+    const float4 a = p[0], b = p[1], c = p[2], d = p[3], e = p[4];
+    Rec x;
+    x.ox = a.x; x.oy = a.y; x.oz = a.z; x.dx = a.w;
+    x.dy = b.x; x.dz = b.y; x.px = b.z; x.py = b.w;
+    x.pz = c.x; x.nx = c.y; x.ny = c.z; x.nz = c.w;
+    x.ar = d.x; x.ag = d.y; x.ab = d.z; x.flags = __float_as_uint(d.w);
+    x.wr = e.x; x.wg = e.y; x.wb = e.z; x.depth = __float_as_uint(e.w);
+    return x;
+}
+
+// One R entry: the sum over Rsamples of (contribution, variance) scaled by
+// the normalization as brute_worker / Rbuilder write it (:812-813).
+__device__ __forceinline__ float2 entry(const DevParams& P, const Row& w, const float* __restrict__ soa,
+                                       uint32_t nvrl, uint32_t v, float normalization)
+{
+    const int nsamp = P.rsamples > 1 ? P.rsamples : 1;
+    float m = 0.0f, s = 0.0f;
+    for (int si = 0; si < nsamp; si++) {
+        float contribution, variance;
+        integrate_R(P, w, soa, nvrl, v, (uint32_t)si, &contribution, &variance);
+        m += contribution * normalization;
+        s += variance * normalization * normalization;
+    }
+    return make_float2(m, s);
+}
+
+// lane = row, the block's four waves interleave over a 256-VRL chunk, as
+// gather.hip's k_build_R / k_build_R_blocks (same outputs, same counters).
+// roff == nullptr: dense Rt[v * ld + row0 + r].
+__global__ void __launch_bounds__(256) k_build_R_strict(const Rec* __restrict__ recs,
+                                                        const uint32_t* __restrict__ ids, uint32_t nrows,
+                                                        const float* __restrict__ soa, uint32_t nvrl,
+                                                        uint32_t chunk, DevParams P, float normalization,
+                                                        float2* __restrict__ Rt, uint64_t ld, uint64_t row0,
+                                                        const uint64_t* __restrict__ roff,
+                                                        const uint32_t* __restrict__ rstride,
+                                                        uint8_t* __restrict__ nonzero,
+                                                        unsigned long long* counter)
+{
+    const uint32_t r = blockIdx.x * 64 + (threadIdx.x & 63);
+    const uint32_t wave = threadIdx.x >> 6;
+    const bool active = r < nrows;
+    Rec rec;
+    if (active) rec = load_rec(recs, r);
+    else { rec = Rec{}; rec.flags = 0u; }
+    const uint32_t rid = active ? (ids ? ids[r] : r) : 0u;
+    const Row w = make_row(P, rec, rid);
+    const bool medium = active && (rec.flags & kFlagMedium);
+    const uint64_t base = !active ? 0 : roff ? roff[r] : row0 + r;
+    const uint64_t stride = !active ? 0 : roff ? rstride[r] : ld;
+    const uint32_t v0 = blockIdx.y * chunk;
+    const uint32_t v1 = min(nvrl, v0 + chunk);
+    const int nsamp = P.rsamples > 1 ? P.rsamples : 1;
+    uint32_t done = 0;
+    for (uint32_t v = v0 + wave; v < v1; v += 4) {
+        float2 e = make_float2(0.0f, 0.0f);
+        if (medium) e = entry(P, w, soa, nvrl, v, normalization);
+        if (active) {
+            float2* p = &Rt[base + (uint64_t)v * stride];
+            if (rec.flags & kRecAccum) { const float2 o = *p; *p = make_float2(o.x + e.x, o.y + e.y); }
+            else *p = e;
+        }
+        if (nonzero && __ballot(active && e.x != 0.0f) && (threadIdx.x & 63) == 0) nonzero[v] = 1;
+        ++done;
+    }
+    const unsigned long long m = __ballot(medium);
+    if ((threadIdx.x & 63) == 0 && m) atomicAdd(counter, (unsigned long long)__popcll(m) * done * (uint32_t)nsamp);
+}
+
+// detmath.h on the device, elementwise (alvrl_detmath_eval): the host = device
+// check of the shared definitions
+__global__ void __launch_bounds__(256) k_detmath(int fn, const float* __restrict__ in, float* __restrict__ out,
+                                                 uint32_t n)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float x = in[i];
+    float y;
+    switch (fn) {
+    case 0: y = dm_expf(x); break;
+    case 1: y = dm_logf(x); break;
+    case 2: y = dm_atanf(x); break;
+    case 3: y = dm_tanf(x); break;
+    case 4: y = dm_asinhf(x); break;
+    default: y = dm_sinhf(x); break;
+    }
+    out[i] = y;
+}
+
+}  // namespace strict
+
+hipError_t launch_build_R_strict(const Rec* recs, const uint32_t* ids, uint32_t nrows, const float* soa,
+                                 uint32_t nvrl, const DevParams& P, float normalization, float2* Rt, uint64_t ld,
+                                 uint64_t row0, const uint64_t* roff, const uint32_t* rstride, uint8_t* nonzero,
+                                 unsigned long long* counter, hipStream_t s)
+{
+    if (nrows == 0 || nvrl == 0) return hipSuccess;
+    const uint32_t chunk = 256;
+    const dim3 grid((nrows + 63) / 64, (nvrl + chunk - 1) / chunk), block(256);
+    hipLaunchKernelGGL(strict::k_build_R_strict, grid, block, 0, s, recs, ids, nrows, soa, nvrl, chunk, P,
+                       normalization, Rt, ld, row0, roff, rstride, nonzero, counter);
+    return hipGetLastError();
+}
+
+hipError_t launch_detmath(int fn, const float* in, float* out, uint32_t n, hipStream_t s)
+{
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(strict::k_detmath, dim3((n + 255) / 256), dim3(256), 0, s, fn, in, out, n);
+    return hipGetLastError();
+}
+
+}  // namespace alvrl

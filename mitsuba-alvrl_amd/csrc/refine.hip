@@ -3289,8 +3289,9 @@ __device__ __noinline__ bool proj_parts(CJ& J_in, CC& cm_in, Ctl& C, uint32_t be
     pj.cpp = max(cm.proj_cpp, 64u);
     pj.np = min((m + pj.cpp - 1) / pj.cpp, 0xFFFFu);
     pj.cpp = (m + pj.np - 1) / pj.np;
-    part_run_all(cm, C, (uint32_t)sl, pj, pool);
-    part_slot_free(cm, (uint32_t)sl);
+    // a timed-out slot stays busy: a late part may still write into it
+    // (part_run_all; C.err is set and the job fails)
+    if (part_run_all(cm, C, (uint32_t)sl, pj, pool)) part_slot_free(cm, (uint32_t)sl);
     return true;
 }
 // The owner's side of divided column weights (calculateColumnWeigths over
@@ -3307,8 +3308,7 @@ __device__ __noinline__ bool colw_parts(CJ& J_in, CC& cm_in, Ctl& C, uint32_t vb
     pj.cpp = max(cm.proj_cpp, 64u);
     pj.np = min((ve - vb + pj.cpp - 1) / pj.cpp, 0xFFFFu);
     pj.cpp = (ve - vb + pj.np - 1) / pj.np;
-    part_run_all(cm, C, (uint32_t)sl, pj, pool);
-    part_slot_free(cm, (uint32_t)sl);
+    if (part_run_all(cm, C, (uint32_t)sl, pj, pool)) part_slot_free(cm, (uint32_t)sl);   // as proj_parts
     return true;
 }
 // The owner's side of a divided cluster variance (variance_passes without
@@ -3331,7 +3331,8 @@ __device__ __noinline__ bool init_parts(CJ& J_in, CC& cm_in, Ctl& C, const uint3
     pj.kind = kPartInit; pj.cw = J.keys1; pj.m = m; pj.nblk = nblk; pj.pblk = pblk;
     pj.np = (nblk + pblk - 1) / pblk;
     pj.st = J.st; pj.wsum = &cm.parts[sl].wsum;
-    if (part_run_all(cm, C, (uint32_t)sl, pj, pool) && threadIdx.x < 64) {
+    const bool done = part_run_all(cm, C, (uint32_t)sl, pj, pool);
+    if (done && threadIdx.x < 64) {
         const uint32_t lane = threadIdx.x, Rfull = J.nrows;
         const double* st = J.st;
         const double Wt = gp(pj.wsum)[0], rW = 1.0 / Wt;
@@ -3350,7 +3351,7 @@ __device__ __noinline__ bool init_parts(CJ& J_in, CC& cm_in, Ctl& C, const uint3
             if (!isfinite(V.res_i) || V.res_i < 0) C.err = 1;
         }
     }
-    part_slot_free(cm, (uint32_t)sl);
+    if (done) part_slot_free(cm, (uint32_t)sl);   // as proj_parts
     __syncthreads();
     return true;
 }

@@ -25,6 +25,7 @@
 #include "bvh_device.hpp"
 #include "host/bvh.hpp"
 #include "host/scene.hpp"
+#include "detmath.h"
 
 namespace alvrl {
 namespace host {
@@ -62,8 +63,9 @@ __device__ __forceinline__ F3 cross(F3 a, F3 b)
     return f3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
 }
 __device__ __forceinline__ float safe_sqrt(float v) { return sqrtf(v > 0.0f ? v : 0.0f); }
-__device__ __forceinline__ float fastexp(float v) { return (float)exp((double)v); }   // math.h:185-199
-__device__ __forceinline__ float fastlog(float v) { return (float)log((double)v); }
+// math::fastexp / fastlog (math.h:185-199): detmath.h, bit for bit the host's and the oracle's
+__device__ __forceinline__ float fastexp(float v) { return dm_expf(v); }
+__device__ __forceinline__ float fastlog(float v) { return dm_logf(v); }
 
 // HomogeneousMedium::sampleDistance (homogeneous.cpp:275-352) as the host's
 // MediumParams / sample_distance: the same float operations, so the same

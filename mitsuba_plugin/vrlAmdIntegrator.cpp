@@ -325,12 +325,21 @@ public:
     }
 
     /* a render worker (renderproc.cpp:52-66): install the resources it
-     * received instead of running the prepass (:378-384) */
+     * received instead of running the prepass (:378-384).  Every local worker
+     * of the master process calls this on the master's own instance
+     * (Scheduler::getResource hands local workers the registered object), so
+     * the objects this instance published itself are skipped: its prepass
+     * already holds them, and installing them would pin its VRLs (set_vrls
+     * is the vrlFile mode) and race the workers already in renderBlock.  A
+     * remote process installs each received pass once, under a lock. */
     void wakeup(ConfigurableObject *parent, std::map<std::string, SerializableObject *> &params) {
         ProgressiveMonteCarloIntegrator::wakeup(parent, params);
         std::map<std::string, SerializableObject *>::iterator v = params.find("vrls");
         std::map<std::string, SerializableObject *>::iterator c = params.find("vrlClusterInfo");
         if (v == params.end())
+            return;
+        std::lock_guard<std::mutex> install(m_wakeLock);
+        if (v->second == m_pubVrls || v->second == m_installedVrls)
             return;
         const Scene *scene = static_cast<const Scene *>(parent);
         if (!m_ready && scene)
@@ -351,6 +360,7 @@ public:
             check(alvrl_integrator_prepass(m_it, vs->m_pass), "alvrl_integrator_prepass");   /* brute force */
             m_pass = (int) vs->m_pass;
         }
+        m_installedVrls = v->second;
         std::lock_guard<std::mutex> g(m_frameLock);
         m_framePass = -1;
     }
@@ -700,6 +710,7 @@ private:
         vs->m_particles = pc;
         vs->m_pass = (uint32_t) m_pass;
         m_vrlsID = sched->registerResource(vs);
+        m_pubVrls = vs.get();
         const uint32_t ns = alvrl_integrator_num_slices(m_it);
         if (!ns)
             return;
@@ -907,6 +918,10 @@ private:
     float *m_fb = NULL;
     bool m_ready = false;
     int m_vrlsID = 0, m_ciID = 0;
+    /* wakeup: the VRL resource this instance published (the master) and the
+     * last one it installed (a render worker) */
+    const SerializableObject *m_pubVrls = NULL, *m_installedVrls = NULL;
+    std::mutex m_wakeLock;
     /* the current pass's frame (frame mode) */
     mutable std::vector<float> m_rgb;
     mutable std::mutex m_frameLock;

@@ -13,6 +13,8 @@
 #include <string.h>
 #include <pthread.h>
 
+#include "detmath.h"
+
 /* include/mitsuba/core/constants.h:27-33 (SINGLE_PRECISION) */
 #define EPSILON       1e-4f
 #define INV_FOURPI    0.07957747154594766788f
@@ -116,9 +118,30 @@ static inline v3 cross(v3 a, v3 b)
 }
 static inline v3 ld3(const float *p) { return mk(p[0], p[1], p[2]); }
 
-/* math::fastexp on Linux/x86_64 (include/mitsuba/core/math.h:175-199) */
+/* math::fastexp / fastlog on Linux/x86_64 (include/mitsuba/core/math.h:175-199)
+ * and the float atan / tan / asinh / sinh of the samplers (vrlIntegrator.cpp:
+ * 889-957).  The parity checker evaluates them with the deterministic
+ * definitions of detmath.h (double, rounded once to float: the correctly
+ * rounded value outside a few ulps of double around float rounding
+ * boundaries, tests/test_detmath.py), which the strict device kernels share,
+ * so that the strict R build and the tracer reproduce it bit for bit
+ * (deviation 3).  The timed CPU baseline
+ * (liboracle_fast.so, -DALVRL_O_LIBM) calls libm as the reference does. */
+#ifdef ALVRL_O_LIBM
 static inline float fastexp(float v) { return (float)exp((double)v); }
 static inline float fastlog(float v) { return (float)log((double)v); }
+#define m_atanf atanf
+#define m_tanf tanf
+#define m_asinhf asinhf
+#define m_sinhf sinhf
+#else
+static inline float fastexp(float v) { return dm_expf(v); }
+static inline float fastlog(float v) { return dm_logf(v); }
+#define m_atanf dm_atanf
+#define m_tanf dm_tanf
+#define m_asinhf dm_asinhf
+#define m_sinhf dm_sinhf
+#endif
 static inline float safe_sqrt(float v) { return sqrtf(v > 0.0f ? v : 0.0f); }
 
 /* Spectrum::isValid, include/mitsuba/core/spectrum.h:467-472 */
@@ -405,19 +428,19 @@ static float kulla(v3 A, v3 B, v3 D, v3 *result, float uniform)
     float dotPr = dot(dir, sub(D, A));
     v3 I = add(A, scl(dir, dotPr));
     float Dis = dist(D, I);
-    float angle_a = atanf(dist(A, I) / Dis);
-    float angle_b = atanf(dist(I, B) / Dis);
+    float angle_a = m_atanf(dist(A, I) / Dis);
+    float angle_b = m_atanf(dist(I, B) / Dis);
     if (dotPr > 0) {
         angle_a *= -1;
         if (dist(A, I) > dist(A, B)) angle_b *= -1;
     }
-    float t = Dis * tanf(((1.0f - uniform) * angle_a) + (uniform * angle_b));
+    float t = Dis * m_tanf(((1.0f - uniform) * angle_a) + (uniform * angle_b));
     float pdf = Dis / ((angle_b - angle_a) * (Dis * Dis + t * t));
     *result = add(I, scl(dir, t));
     return pdf;
 }
 
-static inline float Afun(float x, float h, float sinTheta) { return asinhf((x / h) * sinTheta); }
+static inline float Afun(float x, float h, float sinTheta) { return m_asinhf((x / h) * sinTheta); }
 
 /* sampleVtoDistance, vrlIntegrator.cpp:916-953 (Novak et al. 2012) */
 static float sample_v_to_distance(v3 E, v3 d, v3 hitp, v3 S, v3 End, v3 *V, float uniform)
@@ -433,7 +456,7 @@ static float sample_v_to_distance(v3 E, v3 d, v3 hitp, v3 S, v3 End, v3 *V, floa
     float h = closest_points(E, hitp, S, End, &Uh, &Vh);
     float V0c = -1 * dist(Vh, S);
     float V1c = dist(Vh, End);
-    float newV = h * sinhf(Afun(V0c, h, sinTheta)
+    float newV = h * m_sinhf(Afun(V0c, h, sinTheta)
                            + (uniform * (Afun(V1c, h, sinTheta) - Afun(V0c, h, sinTheta))));
     newV = newV / sinTheta;
     float result = 1.0f / sqrtf(h * h + newV * newV * sinTheta * sinTheta);
@@ -472,6 +495,24 @@ float alvrl_o_sample_v_to_distance(const float E[3], const float d[3], const flo
     float pdf = sample_v_to_distance(v3p(E), v3p(d), v3p(hitp), v3p(S), v3p(End), &r, uniform);
     v3s(r, V);
     return pdf;
+}
+
+/* detmath.h's float functions over an array (fn: 0 exp, 1 log, 2 atan,
+ * 3 tan, 4 asinh, 5 sinh): tests/test_detmath.py */
+void alvrl_o_detmath(int fn, const float *in, float *out, uint32_t n)
+{
+    for (uint32_t i = 0; i < n; i++) {
+        float x = in[i], y;
+        switch (fn) {
+        case 0: y = dm_expf(x); break;
+        case 1: y = dm_logf(x); break;
+        case 2: y = dm_atanf(x); break;
+        case 3: y = dm_tanf(x); break;
+        case 4: y = dm_asinhf(x); break;
+        default: y = dm_sinhf(x); break;
+        }
+        out[i] = y;
+    }
 }
 
 void alvrl_o_medium_eval(const alvrl_o_medium *m, float distance, float tr[3], float *pdf_failure)

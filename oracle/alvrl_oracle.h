@@ -89,6 +89,8 @@ void alvrl_o_medium_init(alvrl_o_medium *m, const float sigma_s[3], const float 
 int alvrl_o_medium_strategy(alvrl_o_medium *m, int strategy, int channel, float density);
 /* HomogeneousMedium::eval, 'balance' strategy: transmittance + pdfFailure */
 void alvrl_o_medium_eval(const alvrl_o_medium *m, float distance, float tr[3], float *pdf_failure);
+/* detmath.h (0 exp, 1 log, 2 atan, 3 tan, 4 asinh, 5 sinh), elementwise */
+void alvrl_o_detmath(int fn, const float *in, float *out, uint32_t n);
 
 typedef struct {
     alvrl_o_medium medium;

@@ -100,7 +100,9 @@ class Oracle:
 
     def __init__(self, fast: bool = False):
         build()
-        self.lib = C.CDLL(os.path.join(HERE, "liboracle_fast.so" if fast else "liboracle.so"))
+        # ALVRL_ORACLE_LIB: the sanitizer build of the checker (tools/sanitize_cpu.sh)
+        path = os.environ.get("ALVRL_ORACLE_LIB") if not fast else None
+        self.lib = C.CDLL(path or os.path.join(HERE, "liboracle_fast.so" if fast else "liboracle.so"))
         L = self.lib
         u32, f32, i32, u64 = C.c_uint32, C.c_float, C.c_int, C.c_uint64
         P = C.POINTER
@@ -108,6 +110,7 @@ class Oracle:
         L.alvrl_o_u01.argtypes = [u32]; L.alvrl_o_u01.restype = f32
         L.alvrl_o_medium_init.argtypes = [P(Medium), P(f32), P(f32), f32, i32, f32]
         L.alvrl_o_medium_eval.argtypes = [P(Medium), f32, P(f32), P(f32)]
+        L.alvrl_o_detmath.argtypes = [i32, P(f32), P(f32), u32]
         L.alvrl_o_medium_strategy.argtypes = [P(Medium), i32, i32, f32]
         L.alvrl_o_closest_points.argtypes = [P(f32)] * 6
         L.alvrl_o_closest_points.restype = f32
@@ -179,6 +182,15 @@ class Oracle:
         r = f3()
         pdf = self.lib.alvrl_o_sample_v_to_distance(f3(*E), f3(*d), f3(*hitp), f3(*S), f3(*End), u, r)
         return pdf, list(r)
+
+    DETMATH_FNS = ("exp", "log", "atan", "tan", "asinh", "sinh")
+
+    def detmath(self, fn: str, x):
+        """detmath.h's float function `fn` elementwise (float32 in and out)."""
+        x = np.ascontiguousarray(x, np.float32)
+        out = np.empty_like(x)
+        self.lib.alvrl_o_detmath(self.DETMATH_FNS.index(fn), _p(x), _p(out), x.size)
+        return out
 
     def medium_eval(self, medium: Medium, distance: float):
         tr = (C.c_float * 3)(); pf = C.c_float()

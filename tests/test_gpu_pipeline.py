@@ -147,13 +147,16 @@ def test_tile_sharding_covers_frame(gpu_ok):
 
 def test_golden_c1_small_device(oracle, gpu_ok):
     """The committed fixtures (tests/golden/c1_small.npz, vrls_c1.txt) against
-    the device: brute frame and R rows within test_gpu_parity's tolerance;
-    the integrator pipeline (host slicing + device R + device refinement) gives
-    the fixture's slice map and representatives bit for bit, and its clustered
-    frame matches the fixture's."""
+    the device.  Fast paths: brute frame and R rows within test_gpu_parity's
+    tolerance.  Strict R build (strictRbuild): the fixture's R rows bit for
+    bit, and the integrator pipeline (host slicing + strict device R + device
+    refinement) gives the fixture's slice map, representatives and cluster
+    lists bit for bit -- the oracle's own clustering of its own R -- and its
+    clustered frame matches the fixture's on the gather tolerance."""
     import os
     import torch
     import alvrl
+    from test_gpu_strict import _assert_bits
     gdir = os.path.join(os.path.dirname(__file__), "golden")
     g = np.load(os.path.join(gdir, "c1_small.npz"))
     w, h = 48, 32
@@ -166,14 +169,18 @@ def test_golden_c1_small_device(oracle, gpu_ok):
     d_out = torch.zeros((w * h, 3), dtype=torch.float32, device="cuda")
     ctx.gather_brute(torch.from_numpy(recs).cuda(), d_out)
     rows = g["R_rows"]
+    d_rows, d_ids = torch.from_numpy(recs[rows]).cuda(), torch.from_numpy(rows.view(np.int32)).cuda()
     d_Rt = torch.zeros((vrls.shape[1], len(rows), 2), dtype=torch.float32, device="cuda")
-    ctx.build_R(torch.from_numpy(recs[rows]).cuda(), d_Rt, ld=len(rows),
-                d_ids=torch.from_numpy(rows.view(np.int32)).cuda())
+    ctx.build_R(d_rows, d_Rt, ld=len(rows), d_ids=d_ids)
+    d_Rs = torch.zeros_like(d_Rt)
+    ctx.set_strict_rbuild(True)
+    ctx.build_R(d_rows, d_Rs, ld=len(rows), d_ids=d_ids)
     torch.cuda.synchronize()
     _assert_close(d_out.cpu().numpy(), g["brute"], "golden brute")
     _assert_close_pairs(d_Rt.cpu().numpy()[..., 0].T, g["R"][..., 0], "golden R mean")
+    _assert_bits(d_Rs.cpu().numpy().transpose(1, 0, 2), g["R"], "golden R, strict build")
 
-    it = alvrl.Integrator(f"targetNumSlices=12;seed={SEED_RNG}", device=0)
+    it = alvrl.Integrator(f"targetNumSlices=12;strictRbuild=true;seed={SEED_RNG}", device=0)
     it.set_vrls(vrls, pc)
     it.preprocess(alvrl.scene_default(w, h))
     it.prepass(0)
@@ -184,18 +191,12 @@ def test_golden_c1_small_device(oracle, gpu_ok):
     off, pix = it.reps()
     assert np.array_equal(off, g["rep_off"]) and np.array_equal(pix, g["rep_pix"])
     cl = it.clusters()
-    same = (np.array_equal(cl["slice_off"], g["cl_slice_off"]) and np.array_equal(cl["reps"], g["cl_reps"])
-            and np.array_equal(cl["weights"].view(np.uint32), g["cl_weights"].view(np.uint32)))
-    print(f"golden clusters identical: {same} ({len(cl['reps'])} vs {len(g['cl_reps'])} representatives)")
-    if same:
-        _assert_close(fb.view(-1, 3).cpu().numpy(), g["clustered"], "golden clustered")
-    else:
-        # device R differs from the fixture's by float rounding; the clustering
-        # on it is then checked against the oracle's clustering of the same R
-        # (bit-exact, test_c1_pipeline_adaptive), and here statistically
-        img = fb.view(-1, 3).cpu().numpy()
-        rel = abs(img.mean() - g["clustered"].mean()) / g["clustered"].mean()
-        assert rel < 2e-2, rel
+    assert np.array_equal(cl["slice_off"], g["cl_slice_off"]) and np.array_equal(cl["reps"], g["cl_reps"])
+    assert np.array_equal(cl["weights"].view(np.uint32), g["cl_weights"].view(np.uint32))
+    if it.stats()["fallback_built"]:   # built lazily (deviation 4)
+        assert np.array_equal(cl["fb_reps"], g["cl_fb_reps"])
+        assert np.array_equal(cl["fb_weights"].view(np.uint32), g["cl_fb_weights"].view(np.uint32))
+    _assert_close(fb.view(-1, 3).cpu().numpy(), g["clustered"], "golden clustered")
 
 
 def test_sharded_prepass(gpu_ok, tmp_path):
