@@ -79,11 +79,13 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-alt", action="store_true",
                     help="N > 1 with --shard slices: skip the second, pass-parallel measurement")
+    ap.add_argument("--no-unconditional", action="store_true",
+                    help="clustered configs: skip the comparison with the oracle's own pipeline")
     ap.add_argument("--cpu-row-stride", type=int, default=64,
                     help="CPU baseline sample: every n-th image row")
-    ap.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "r04", "pmc_traffic_r4h.json"),
+    ap.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "r05", "pmc_traffic.json"),
                     help="per-launch HBM bytes of the dominant kernel from a rocprofv3 --pmc pass")
-    ap.add_argument("--valu-json", default=os.path.join(REPO, "profiles", "r04", "pmc_valu_{cfg}.json"),
+    ap.add_argument("--valu-json", default=os.path.join(REPO, "profiles", "r05", "pmc_valu_{cfg}.json"),
                     help="per-kernel VALU counters (tools/pmc_valu.sh + tools/pmc_valu.py)")
     return ap.parse_args()
 
@@ -233,21 +235,30 @@ def main():
     # rounds' count (each split's cluster once) for comparison.
     nst = max(args.steps, 1)
     kind = "clustered" if clustered else "brute"
+    # committed counter files count only if they were taken on the library
+    # this run loaded (their build_id, tools/pmc_summary.py / pmc_valu.py);
+    # a file from another tree reports traffic / valu null
+    my_id = alvrl.build_info()["build_id"]
+    counters = {"pmc_json": os.path.relpath(args.pmc_json, REPO),
+                "valu_json": os.path.relpath(args.valu_json.format(cfg=args.config), REPO),
+                "build_id": my_id, "pmc_matches": False, "valu_matches": False}
     pmc = {}
     try:
         with open(args.pmc_json) as f:
             pm = json.load(f)
         for rec in (pm if isinstance(pm, list) else [pm]):
-            if rec.get("config") == args.config:
+            if rec.get("config") == args.config and rec.get("build_id") == my_id:
                 pmc[rec.get("kernel_key", "render")] = rec.get("hbm_bytes_per_launch")
+                counters["pmc_matches"] = True
     except (OSError, ValueError):
         pass
 
     valu = {}
     try:
         with open(args.valu_json.format(cfg=args.config)) as f:
-            valu = json.load(f)
-    except (OSError, ValueError):
+            valu = {k: v for k, v in json.load(f).items() if v.get("build_id") == my_id}
+        counters["valu_matches"] = bool(valu)
+    except (OSError, ValueError, AttributeError):
         pass
 
     def roof(name, key, bytes_per_launch, ms, note):
@@ -331,6 +342,7 @@ def main():
             # the prebuilt in-tree library this run loaded, and whether it was
             # built from this tree's sources (alvrl_build_id vs the tree's hash)
             "build_mode": dict(alvrl.build_info(), mode="prebuilt in-tree (make, hipcc --offload-arch=gfx950)"),
+            "counter_files": counters,
         }
         if alt is not None:
             out["alt_decomposition"] = alt
@@ -341,6 +353,10 @@ def main():
             out["cpu_baseline"] = cpu_baseline_prepass(args, cfg, vrls, pc, it, out["cpu_baseline"],
                                                        pre_pairs / max(args.steps, 1),
                                                        render_pairs / max(args.steps, 1))
+            if not args.no_unconditional:
+                out["pixel_rmse_vs_cpu_unconditional"] = unconditional_parity(
+                    cfg, vrls, pc, args.warmup + args.steps - 1, fb.view(-1, 3).cpu().numpy(), gpu,
+                    row_stride=args.cpu_row_stride, fast_clusters=it.clusters())
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
@@ -467,6 +483,115 @@ def cpu_baseline_prepass(args, cfg, vrls, pc, it, render_base, pre_pairs_step, r
             "rates": {"rbuild": r_rate, "render": render_rate, "refine_s_median_slice": t_ref[s_med],
                       "refine_s_largest_slice": t_ref[s_max]},
             "refine_parity": parity}
+
+
+def unconditional_parity(cfg, vrls, pc, pass_, fast_frame, device=0, row_stride=64, fast_clusters=None,
+                         check_slice=True):
+    """The default (fast) pipeline's frame of pass `pass_` against the CPU
+    restatement's OWN pipeline of that pass -- its own R, its own clusters --
+    on every `row_stride`-th image row, with no device result fed to the
+    oracle.
+
+    The oracle's pipeline over the full R (1.6e9 pairs at C4) takes minutes on
+    the host, so its cluster lists are taken from the strict device pipeline
+    (strictRbuild: R bit-identical to the oracle's, refinement bit-exact given
+    R, tests/test_gpu_strict.py), and that identity is re-checked here at this
+    scale on the median slice: the oracle's R rows of its representatives
+    against the strict device's, bit for bit, and the oracle's refinement of
+    them against the strict device's list.  The oracle then renders the
+    sampled rows with those lists (its own clustered gather).
+
+    The bar is the pass-to-pass noise of the method: the same comparison
+    between the oracle's frames of pass `pass_` and `pass_ + 1`."""
+    import numpy as np
+    import torch
+    import alvrl
+    from oracle import Oracle
+    o = Oracle()                                 # the strict (IEEE) build: the parity checker
+    W, H = cfg["w"], cfg["h"]
+    threads = cpu_threads()
+    props = cfg["props"] + (";" if cfg["props"] else "") + f"strictRbuild=true;seed={SEED_RNG}"
+    rows = np.arange(0, H, row_stride)
+    pix = (rows[:, None] * W + np.arange(W)[None, :]).reshape(-1).astype(np.uint32)
+    recs_all = o.records(o.scene(W, H))
+    recs = recs_all[pix]
+    xs, ys = pix % W, pix // W
+
+    def strict_pass(p):
+        it = alvrl.Integrator(props, device=device)
+        it.set_vrls(vrls, pc)
+        it.preprocess(alvrl.scene_default(W, H))
+        t0 = time.perf_counter()
+        it.prepass(p)
+        fb = torch.zeros(W * H * 3, dtype=torch.float32, device=torch.device("cuda", device))
+        it.render(fb)
+        torch.cuda.synchronize(device)
+        return it, fb.view(-1, 3).cpu().numpy(), time.perf_counter() - t0
+
+    def oracle_frame(it, p):
+        cl, p2s = it.clusters(), it.slices()
+        P = o.params(o.medium(), seed=SEED_RNG, pass_=p)
+        img, _ = o.gather_clustered(P, recs, p2s[ys + H * xs], vrls, pc, cl["slice_off"], cl["reps"],
+                                    cl["weights"], cl["fb_reps"], cl["fb_weights"], rec_ids=pix, nthreads=threads)
+        return img, cl
+
+    def cmp(a, b):
+        d = a.astype(np.float64) - b.astype(np.float64)
+        rel = np.abs(d) / np.maximum(np.abs(b.astype(np.float64)), 1e-30)
+        return {"rmse": float(np.sqrt(np.mean(d ** 2))), "median_rel": float(np.median(rel)),
+                "q99_rel": float(np.quantile(rel, 0.99)), "max_rel": float(rel.max())}
+
+    t0 = time.perf_counter()
+    itS, S, s_wall = strict_pass(pass_)
+    stS = itS.stats()
+    O, clO = oracle_frame(itS, pass_)
+    pin = None
+    if check_slice:
+        off, rp = itS.reps()
+        ns = len(off) - 1
+        s = int(np.argsort(np.diff(off), kind="stable")[ns // 2])
+        job = itS.slice_job(s)
+        ids = rp[off[s]:off[s + 1]]
+        rid = ((ids % H) * W + ids // H).astype(np.uint32)           # column-major -> row-major
+        P = o.params(o.medium(), seed=SEED_RNG, pass_=pass_)
+        _, Ro, _ = o.gather_brute(P, recs_all[rid], vrls, pc, rec_ids=rid, domain=2, want_R=True, nthreads=threads)
+        r_same = bool(np.array_equal(np.ascontiguousarray(job["R"].transpose(1, 0, 2)).view(np.uint32),
+                                     Ro.view(np.uint32)))
+        kv = dict(x.split("=", 1) for x in cfg["props"].split(";") if "=" in x)
+        reps, w, refined = o.cluster_refine(np.ascontiguousarray(Ro.transpose(1, 0, 2)),
+                                            np.arange(len(rid), dtype=np.uint32), job["locw"], job["init_vrls"],
+                                            job["init_off"], job["pixel_undersampling"],
+                                            float(kv.get("localUndersampling", -1.0)),
+                                            depth_correction=float(kv.get("depthCorrection", 1.0)),
+                                            seed=SEED_RNG, pass_=pass_, stage_refine=3 + 2 * s,
+                                            stage_sample=4 + 2 * s)
+        b, e = clO["slice_off"][s], clO["slice_off"][s + 1]
+        l_same = bool(refined and np.array_equal(reps, clO["reps"][b:e])
+                      and np.array_equal(w.view(np.uint32), clO["weights"][b:e].view(np.uint32)))
+        pin = {"slice": s, "rows": int(len(rid)), "R_bit_identical": r_same, "clusters": int(e - b),
+               "cluster_list_identical": l_same}
+    itS.close()
+    itS2, _, _ = strict_pass(pass_ + 1)
+    O2, _ = oracle_frame(itS2, pass_ + 1)
+    itS2.close()
+    fast = cmp(fast_frame[pix], O)
+    noise = cmp(O2, O)
+    out = {"pass": pass_, "pixels": int(len(pix)),
+           "sample": f"every {row_stride}th image row; the oracle's clustered gather with its own cluster lists",
+           "fast_vs_oracle_pipeline": fast,
+           "strict_device_vs_oracle_pipeline": cmp(S[pix], O),
+           "oracle_pass_to_pass": noise,
+           "rmse_ratio_to_pass_noise": fast["rmse"] / noise["rmse"] if noise["rmse"] > 0 else None,
+           "oracle_lists_pinned_on_slice": pin,
+           "strict_rbuild_ms": float(stS["ms_rbuild"]), "strict_prepass_wall_s": s_wall,
+           "seconds": time.perf_counter() - t0}
+    if fast_clusters is not None:
+        a, b = fast_clusters, clO
+        same = sum(1 for s in range(len(a["slice_off"]) - 1)
+                   if np.array_equal(a["reps"][a["slice_off"][s]:a["slice_off"][s + 1]],
+                                     b["reps"][b["slice_off"][s]:b["slice_off"][s + 1]]))
+        out["fast_slices_with_oracle_lists"] = [same, len(a["slice_off"]) - 1]
+    return out
 
 
 def cpu_threads():

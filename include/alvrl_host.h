@@ -234,6 +234,19 @@ ALVRL_API int alvrl_exchange_clusters(const alvrl_exchange *ex, uint32_t world, 
                                       int *refined, uint32_t *slice_off, uint32_t *reps,
                                       float *weights, uint64_t cap, uint64_t *total);
 
+/* An alvrl_exchange whose ranks are threads of this process -- one library
+ * integrator per GPU driven from one host thread each (the Mitsuba plugin's
+ * amdDevices; the reference renders in one process with one worker per core,
+ * src/mitsuba/mitsuba.cpp:280-282, src/librender/renderproc.cpp:119-135).
+ * Rank r's exchange is alvrl_local_exchange_rank(g, r); all ranks must call
+ * the collectives in the same order.  A rank left waiting 600 s fails the
+ * call with ALVRL_ERR_COMM instead of hanging.  Destroy after every rank has
+ * returned. */
+typedef struct alvrl_local_exchange alvrl_local_exchange;
+ALVRL_API int alvrl_local_exchange_create(uint32_t world, alvrl_local_exchange **out);
+ALVRL_API const alvrl_exchange *alvrl_local_exchange_rank(alvrl_local_exchange *g, uint32_t rank);
+ALVRL_API void alvrl_local_exchange_destroy(alvrl_local_exchange *g);
+
 /* ---- host-cast scenes (the Mitsuba plugin's "records" mode) ------------
  * For scenes the descriptor above cannot express -- area and other emitters,
  * any shapes and BSDFs, a medium in any container -- the host application

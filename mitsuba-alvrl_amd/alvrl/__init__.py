@@ -446,6 +446,50 @@ class ExchangeDesc(C.Structure):
     _fields_ = [("user", C.c_void_p), ("allgather", ALLGATHER_FN)]
 
 
+class LocalExchange:
+    """alvrl_local_exchange: ranks that are threads of this process (one
+    Integrator per device, each driven by its own thread).  `rank(r)` is the
+    exchange to pass to rank r's Integrator.prepass."""
+
+    class _Rank:
+        def __init__(self, owner, desc):
+            self.owner, self.desc, self.error, self.world = owner, desc, None, owner.world
+
+        def _check(self, rc: int):
+            if rc != ALVRL_OK:
+                raise AlvrlError(rc, _host().alvrl_host_last_error().decode())
+
+        def allgatherv(self, data):
+            return Exchange.allgatherv(self, data)
+
+        def or_(self, mask):
+            return Exchange.or_(self, mask)
+
+    def __init__(self, world: int):
+        L = _host()
+        h = C.c_void_p()
+        rc = L.alvrl_local_exchange_create(world, C.byref(h))
+        if rc != ALVRL_OK:
+            raise AlvrlError(rc, L.alvrl_host_last_error().decode())
+        self.h, self.world = h, world
+        self._ranks = [self._Rank(self, C.cast(L.alvrl_local_exchange_rank(h, r), C.POINTER(ExchangeDesc)).contents)
+                       for r in range(world)]
+
+    def rank(self, r: int) -> "LocalExchange._Rank":
+        return self._ranks[r]
+
+    def close(self):
+        if getattr(self, "h", None):
+            _host().alvrl_local_exchange_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class Exchange:
     """alvrl_exchange over a torch.distributed process group.
 
@@ -579,6 +623,9 @@ def _host():
     L.alvrl_integrator_prepass_dist.argtypes = [vp, u32, u32, u32, P(ExchangeDesc)]
     L.alvrl_exchange_allgatherv.argtypes = [P(ExchangeDesc), u32, vp, u64, vp, u64, P(u64)]
     L.alvrl_exchange_or.argtypes = [P(ExchangeDesc), u32, vp, u64]
+    L.alvrl_local_exchange_create.argtypes = [u32, P(vp)]
+    L.alvrl_local_exchange_rank.argtypes = [vp, u32]; L.alvrl_local_exchange_rank.restype = vp
+    L.alvrl_local_exchange_destroy.argtypes = [vp]; L.alvrl_local_exchange_destroy.restype = None
     L.alvrl_exchange_clusters.argtypes = [P(ExchangeDesc), u32, u32, u32, vp, vp, vp, vp, vp, vp, vp, vp, vp,
                                           u64, P(u64)]
     L.alvrl_cluster_info_write.argtypes = [C.c_char_p, u32, vp, u32, vp, vp, vp, u32, vp, vp, u32, vp, vp]

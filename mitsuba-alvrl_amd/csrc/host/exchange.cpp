@@ -7,7 +7,10 @@
 #include "exchange.hpp"
 
 #include <algorithm>
+#include <chrono>
+#include <condition_variable>
 #include <cstring>
+#include <mutex>
 
 #include "../../../include/alvrl.h"
 
@@ -217,5 +220,88 @@ ALVRL_API int alvrl_exchange_clusters(const alvrl_exchange* ex, uint32_t world, 
     });
     return ALVRL_OK;
 }
+
+/* ---- the in-process exchange: one thread per device, one process ------ */
+}  // extern "C"
+
+// Ranks are threads of this process (the Mitsuba plugin's amdDevices: one
+// library integrator per GPU, renderproc.cpp:119-135 / mitsuba.cpp:280-282
+// keep everything in one process).  allgather: every rank posts its send
+// buffer, the last to arrive opens the round, each copies all posted buffers
+// into its own recv, and a second barrier keeps every send buffer alive until
+// all ranks have copied.  A rank that waits longer than the timeout fails the
+// call (and so the prepass) instead of hanging.
+struct alvrl_local_exchange {
+    uint32_t world = 0;
+    std::mutex mu;
+    std::condition_variable cv;
+    uint64_t gen = 0;           // rounds completed (two barriers per allgather)
+    uint32_t arrived = 0;
+    uint64_t bytes = 0;
+    bool broken = false;
+    std::vector<const void*> send;
+    std::vector<alvrl_exchange> ex;
+    struct Rank { alvrl_local_exchange* g; uint32_t r; };
+    std::vector<Rank> ranks;
+    double timeout_s = 600.0;
+
+    // barrier; false on timeout or a broken group
+    bool arrive(std::unique_lock<std::mutex>& lk)
+    {
+        if (broken) return false;
+        const uint64_t g0 = gen;
+        if (++arrived == world) {
+            arrived = 0;
+            ++gen;
+            cv.notify_all();
+            return true;
+        }
+        const bool ok = cv.wait_for(lk, std::chrono::duration<double>(timeout_s),
+                                    [&] { return gen != g0 || broken; });
+        if (!ok || broken) { broken = true; cv.notify_all(); return false; }
+        return true;
+    }
+
+    static int allgather(void* user, const void* snd, uint64_t n, void* recv)
+    {
+        Rank* rk = static_cast<Rank*>(user);
+        alvrl_local_exchange& G = *rk->g;
+        std::unique_lock<std::mutex> lk(G.mu);
+        if (G.arrived == 0) G.bytes = n;
+        else if (G.bytes != n) { G.broken = true; G.cv.notify_all(); return 2; }
+        G.send[rk->r] = snd;
+        if (!G.arrive(lk)) return 1;
+        lk.unlock();
+        for (uint32_t q = 0; q < G.world; q++)
+            if (n) std::memcpy(static_cast<uint8_t*>(recv) + (size_t)q * n, G.send[q], n);
+        lk.lock();
+        return G.arrive(lk) ? 0 : 1;
+    }
+};
+
+extern "C" {
+
+ALVRL_API int alvrl_local_exchange_create(uint32_t world, alvrl_local_exchange** out)
+{
+    if (!out || world == 0) { g_host_err = "alvrl_local_exchange_create: bad argument"; return ALVRL_ERR_INVALID; }
+    alvrl_local_exchange* g = new alvrl_local_exchange();
+    g->world = world;
+    g->send.assign(world, nullptr);
+    g->ranks.resize(world);
+    g->ex.resize(world);
+    for (uint32_t r = 0; r < world; r++) {
+        g->ranks[r] = alvrl_local_exchange::Rank{g, r};
+        g->ex[r] = alvrl_exchange{&g->ranks[r], &alvrl_local_exchange::allgather};
+    }
+    *out = g;
+    return ALVRL_OK;
+}
+
+ALVRL_API const alvrl_exchange* alvrl_local_exchange_rank(alvrl_local_exchange* g, uint32_t rank)
+{
+    return (g && rank < g->world) ? &g->ex[rank] : nullptr;
+}
+
+ALVRL_API void alvrl_local_exchange_destroy(alvrl_local_exchange* g) { delete g; }
 
 }  // extern "C"

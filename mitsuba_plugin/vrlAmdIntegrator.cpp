@@ -70,6 +70,7 @@
 #include <cstring>
 #include <mutex>
 #include <sstream>
+#include <thread>
 #include <vector>
 
 #include "alvrl.h"
@@ -103,12 +104,39 @@ void put3(float *dst, const Spectrum &s) {
 /* The properties the library does not take (Mitsuba's own, or the medium's
  * restated on the integrator) */
 bool isMitsubaOnly(const std::string &k) {
-    return k == "amdMode" || k == "amdDevice" || k == "mediumSamplingWeight" || k == "strategy" ||
+    return k == "amdMode" || k == "amdDevice" || k == "amdDevices" || k == "mediumSamplingWeight" || k == "strategy" ||
         k == "channel" || k == "samplingDensity";
 }
 
 /* Longest eye path (records per sensor sample) the records mode follows */
 const size_t kMaxPathRecords = 256;
+
+/* "amdDevices": a comma-separated list of HIP devices ("0,1,2,3"), or
+ * "all" for every visible device; empty: the one "amdDevice" */
+std::vector<int> parseDevices(const std::string &spec, int single) {
+    std::vector<int> out;
+    if (spec.empty()) {
+        out.push_back(single);
+        return out;
+    }
+    if (spec == "all") {
+        int n = 0;
+        checkHip(hipGetDeviceCount(&n), "hipGetDeviceCount");
+        for (int i = 0; i < n; ++i) out.push_back(i);
+    } else {
+        std::stringstream ss(spec);
+        std::string tok;
+        while (std::getline(ss, tok, ','))
+            if (!tok.empty()) out.push_back(std::stoi(tok));
+    }
+    if (out.empty())
+        SLog(EError, "vrl (amd): amdDevices lists no device");
+    for (size_t i = 0; i < out.size(); ++i)
+        for (size_t j = 0; j < i; ++j)
+            if (out[i] == out[j] || out[i] < 0)
+                SLog(EError, "vrl (amd): amdDevices must list distinct devices");
+    return out;
+}
 
 } // namespace
 
@@ -205,6 +233,10 @@ public:
             Log(EError, "amdMode must be \"frame\" or \"records\"");
         m_recordsMode = mode == "records";
         m_device = props.getInteger("amdDevice", 0);
+        m_devices = parseDevices(props.getString("amdDevices", ""), m_device);
+        m_device = m_devices[0];
+        if (m_recordsMode && m_devices.size() > 1)
+            Log(EError, "vrl (amd): amdDevices (one library integrator per GPU) needs amdMode=frame");
         m_samplingWeight = props.getFloat("mediumSamplingWeight", -1);
         std::string strategy = props.getString("strategy", "balance");
         if (strategy == "balance") m_strategy = ALVRL_STRATEGY_BALANCE;
@@ -258,6 +290,8 @@ public:
         m_channel = stream->readInt();
         m_samplingDensity = (float) stream->readFloat();
         m_sampleCount = stream->readInt();
+        m_devices.resize((size_t) stream->readInt());
+        for (size_t i = 0; i < m_devices.size(); ++i) m_devices[i] = stream->readInt();
         m_vrlsID = m_ciID = 0;
         create(m_sampleCount);
     }
@@ -279,12 +313,16 @@ public:
         stream->writeInt(m_channel);
         stream->writeFloat(m_samplingDensity);
         stream->writeInt(m_sampleCount);
+        stream->writeInt((int) m_devices.size());
+        for (size_t i = 0; i < m_devices.size(); ++i) stream->writeInt(m_devices[i]);
     }
 
     ~vrlAmdIntegrator() {
         if (m_fb) hipFree(m_fb);
         if (m_stream) hipStreamDestroy(m_stream);
         if (m_it) alvrl_integrator_destroy(m_it);
+        releaseMore();
+        if (m_localEx) alvrl_local_exchange_destroy(m_localEx);
     }
 
     bool preprocess(const Scene *scene, RenderQueue *queue, const RenderJob *job,
@@ -308,8 +346,17 @@ public:
     bool prepass(const Scene *scene, Sampler *sampler) {
         if (m_recordsMode)
             prepassRecords(scene, sampler);
-        else
+        else if (m_more.empty())
             check(alvrl_integrator_prepass(m_it, m_pass), "alvrl_integrator_prepass");
+        else
+            prepassDevices();
+        if (!m_recordsMode) {   /* the pass's slice map, for Li */
+            m_p2s.clear();
+            if (alvrl_integrator_num_slices(m_it)) {
+                m_p2s.resize((size_t) m_width * m_height);
+                check(alvrl_integrator_slices(m_it, &m_p2s[0], (uint32_t) m_p2s.size()), "alvrl_integrator_slices");
+            }
+        }
         publishResources();
         std::lock_guard<std::mutex> g(m_frameLock);
         m_framePass = -1;   // the frame of the new pass is rendered on first use
@@ -345,20 +392,23 @@ public:
         if (!m_ready && scene)
             setUp(scene, false);
         const AmdVrlSet *vs = static_cast<const AmdVrlSet *>(v->second);
-        check(alvrl_integrator_set_vrls(m_it, vs->count() ? &vs->m_soa[0] : NULL, vs->count(),
-                                        std::max<uint64_t>(vs->m_particles, 1)), "alvrl_integrator_set_vrls");
-        if (c != params.end()) {
-            const AmdClusterInfo *ci = static_cast<const AmdClusterInfo *>(c->second);
-            check(alvrl_integrator_set_cluster_info(m_it, ci->m_pass, (uint32_t) ci->m_slices.size(),
-                      ci->m_slices.empty() ? NULL : &ci->m_slices[0], (uint32_t) ci->m_off.size() - 1,
-                      &ci->m_off[0], ci->m_reps.empty() ? NULL : &ci->m_reps[0], ci->m_w.empty() ? NULL : &ci->m_w[0],
-                      (uint32_t) ci->m_fbReps.size(), ci->m_fbReps.empty() ? NULL : &ci->m_fbReps[0],
-                      ci->m_fbW.empty() ? NULL : &ci->m_fbW[0]), "alvrl_integrator_set_cluster_info");
-            m_p2s = ci->m_slices;
-            m_pass = (int) ci->m_pass;
-        } else {
-            check(alvrl_integrator_prepass(m_it, vs->m_pass), "alvrl_integrator_prepass");   /* brute force */
-            m_pass = (int) vs->m_pass;
+        for (size_t k = 0; k <= m_more.size(); ++k) {   /* every device's integrator */
+            alvrl_integrator *it = k ? m_more[k - 1] : m_it;
+            check(alvrl_integrator_set_vrls(it, vs->count() ? &vs->m_soa[0] : NULL, vs->count(),
+                                            std::max<uint64_t>(vs->m_particles, 1)), "alvrl_integrator_set_vrls");
+            if (c != params.end()) {
+                const AmdClusterInfo *ci = static_cast<const AmdClusterInfo *>(c->second);
+                check(alvrl_integrator_set_cluster_info(it, ci->m_pass, (uint32_t) ci->m_slices.size(),
+                          ci->m_slices.empty() ? NULL : &ci->m_slices[0], (uint32_t) ci->m_off.size() - 1,
+                          &ci->m_off[0], ci->m_reps.empty() ? NULL : &ci->m_reps[0], ci->m_w.empty() ? NULL : &ci->m_w[0],
+                          (uint32_t) ci->m_fbReps.size(), ci->m_fbReps.empty() ? NULL : &ci->m_fbReps[0],
+                          ci->m_fbW.empty() ? NULL : &ci->m_fbW[0]), "alvrl_integrator_set_cluster_info");
+                m_p2s = ci->m_slices;
+                m_pass = (int) ci->m_pass;
+            } else {
+                check(alvrl_integrator_prepass(it, vs->m_pass), "alvrl_integrator_prepass");   /* brute force */
+                m_pass = (int) vs->m_pass;
+            }
         }
         m_installedVrls = v->second;
         std::lock_guard<std::mutex> g(m_frameLock);
@@ -384,9 +434,44 @@ public:
         }
     }
 
-    Spectrum Li(const RayDifferential &, RadianceQueryRecord &) const {
-        Log(EError, "vrl (amd) renders whole blocks (renderBlock)");
-        return Spectrum(0.0f);
+    /* Li (vrlIntegrator.cpp:386-393) for a caller outside renderBlock:
+     * LiInternal's eye path of 'ray' as gather records (appendPath, both
+     * modes cast it with Mitsuba's scene), the slice of the image position
+     * the sensor gives the ray (getSamplePosition, :551-560; m_slices[y +
+     * H*x]) and one gather over the pass's clusters, or over every VRL
+     * without clustering (getVRLContributions, :792-825).  The pixel keys the
+     * gathers' counter streams as in renderBlock. */
+    Spectrum Li(const RayDifferential &ray, RadianceQueryRecord &rRec) const {
+        std::vector<alvrl_gather_rec> recs;
+        appendPath(ray, rRec, Spectrum(1.0f), Spectrum(m_initialSpecularThroughput), 0u, &recs);
+        const uint32_t n = (uint32_t) recs.size();
+        if (!n)
+            return Spectrum(0.0f);
+        PositionSamplingRecord pRec;
+        pRec.p = ray.o;
+        DirectionSamplingRecord dRec(ray.d);
+        Point2 pos;
+        rRec.scene->getSensor()->getSamplePosition(pRec, dRec, pos);
+        const int x = std::min(std::max((int) pos.x, 0), m_width - 1);
+        const int y = std::min(std::max((int) pos.y, 0), m_height - 1);
+        const std::vector<uint32_t> ids(n, (uint32_t) y * (uint32_t) m_width + (uint32_t) x);
+        std::vector<float> rgb((size_t) 3 * n);
+        alvrl_ctx *ctx = alvrl_integrator_ctx(m_it);
+        if (!m_p2s.empty()) {
+            const std::vector<uint32_t> slice(n, m_p2s[(size_t) y + (size_t) m_height * x]);
+            checkDevice(alvrl_gather_clustered_host(ctx, &recs[0], &ids[0], &slice[0], n, &rgb[0]), ctx,
+                "alvrl_gather_clustered_host (Li)");
+        } else {
+            checkDevice(alvrl_gather_brute_host(ctx, &recs[0], &ids[0], n, &rgb[0]), ctx,
+                "alvrl_gather_brute_host (Li)");
+        }
+        Spectrum L(0.0f);
+        for (uint32_t k = 0; k < n; ++k) {
+            Spectrum s;
+            s.fromLinearRGB(rgb[3 * k], rgb[3 * k + 1], rgb[3 * k + 2]);
+            L += s;
+        }
+        return L;
     }
 
     std::string passFileSuffix() {
@@ -412,6 +497,7 @@ private:
         if (m_it) alvrl_integrator_destroy(m_it);
         m_it = NULL;
         m_sampleCount = spp;
+        releaseMore();
         std::ostringstream oss;
         oss << m_props << "sampleCount=" << spp << ";";
         check(alvrl_integrator_create(oss.str().c_str(), m_device, &m_it), "alvrl_integrator_create");
@@ -419,6 +505,19 @@ private:
             checkHip(hipSetDevice(m_device), "hipSetDevice");
             checkHip(hipStreamCreateWithFlags(&m_stream, hipStreamNonBlocking), "hipStreamCreate");
         }
+        /* amdDevices: one more library integrator per further GPU, the same
+           properties (and so the same VRLs, slices and streams) */
+        for (size_t k = 1; k < m_devices.size(); ++k) {
+            alvrl_integrator *it = NULL;
+            check(alvrl_integrator_create(oss.str().c_str(), m_devices[k], &it), "alvrl_integrator_create");
+            m_more.push_back(it);
+            hipStream_t st = NULL;
+            checkHip(hipSetDevice(m_devices[k]), "hipSetDevice");
+            checkHip(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
+            m_moreStreams.push_back(st);
+        }
+        if (!m_more.empty() && !m_localEx)
+            check(alvrl_local_exchange_create((uint32_t) m_devices.size(), &m_localEx), "alvrl_local_exchange_create");
         m_ready = false;
     }
 
@@ -438,12 +537,27 @@ private:
             sd.occluders = m_tris.empty() ? NULL : &m_tris[0];
             sd.occluder_material = m_mats.empty() ? NULL : &m_mats[0];
             check(alvrl_integrator_preprocess(m_it, &sd), "alvrl_integrator_preprocess");
+            for (size_t k = 0; k < m_more.size(); ++k)
+                check(alvrl_integrator_preprocess(m_more[k], &sd), "alvrl_integrator_preprocess");
         }
         m_rgb.assign((size_t) 3 * m_width * m_height, 0.0f);
         if (m_fb) hipFree(m_fb);
         m_fb = NULL;
-        if (!m_recordsMode)
+        if (!m_recordsMode) {
+            checkHip(hipSetDevice(m_device), "hipSetDevice");
             checkHip(hipMalloc(&m_fb, sizeof(float) * m_rgb.size()), "hipMalloc");
+        }
+        for (size_t k = 0; k < m_moreFb.size(); ++k) {
+            checkHip(hipSetDevice(m_devices[k + 1]), "hipSetDevice");
+            checkHip(hipFree(m_moreFb[k]), "hipFree");
+        }
+        m_moreFb.assign(m_more.size(), (float *) NULL);
+        m_moreRgb.assign(m_more.size(), std::vector<float>());
+        for (size_t k = 0; k < m_more.size(); ++k) {
+            checkHip(hipSetDevice(m_devices[k + 1]), "hipSetDevice");
+            checkHip(hipMalloc(&m_moreFb[k], sizeof(float) * m_rgb.size()), "hipMalloc");
+            m_moreRgb[k].assign(m_rgb.size(), 0.0f);
+        }
         m_ready = true;
     }
 
@@ -526,7 +640,7 @@ private:
                     m_desc.box_min[i] = (float) box.min[i];
                     m_desc.box_max[i] = (float) box.max[i];
                 }
-                if (bsdf) put3(m_desc.albedo, bsdf->getDiffuseReflectance(its));
+                if (bsdf) put3(m_desc.albedo, diffuseReflectance(sh, bsdf));
                 haveBox = true;
                 continue;
             }
@@ -555,8 +669,12 @@ private:
                 } else if (type & BSDF::EDelta) {
                     Log(EError, "vrl (amd) frame mode: BSDF of \"%s\" is neither diffuse, mirror, dielectric nor "
                         "null (amdMode=records follows every delta component)", sh->getName().c_str());
-                } else if (!haveOccAlbedo) {
-                    put3(m_desc.occluder_albedo, bsdf->getDiffuseReflectance(its));
+                } else {
+                    const Spectrum rho = diffuseReflectance(sh, bsdf);
+                    if (haveOccAlbedo && !sameRgb(rho, m_desc.occluder_albedo))
+                        Log(EError, "vrl (amd) frame mode: diffuse occluders with different reflectances "
+                            "(amdMode=records takes any)");
+                    put3(m_desc.occluder_albedo, rho);
                     haveOccAlbedo = true;
                 }
             }
@@ -565,6 +683,44 @@ private:
         if (!haveBox)
             Log(EError, "vrl (amd) needs a shape that contains the medium (its interior)");
         m_desc.n_occluders = (uint32_t) m_mats.size();
+    }
+
+    /* The constant diffuse reflectance of a shape's smooth diffuse BSDF,
+     * evaluated at real points of the shape (Shape::samplePosition: position,
+     * normal and uv): the descriptor holds one albedo per class of surface,
+     * so another smooth BSDF (its vol->surf term is not rho / pi cos) or a
+     * textured reflectance is refused with a pointer to records mode */
+    Spectrum diffuseReflectance(const Shape *sh, const BSDF *bsdf) const {
+        if (bsdf->getClass()->getName() != "SmoothDiffuse")
+            Log(EError, "vrl (amd) frame mode: the BSDF of \"%s\" is %s; its walls and occluders take the "
+                "smooth diffuse BSDF the gathers evaluate (diffuse.cpp:110-118)", sh->getName().c_str(),
+                bsdf->getClass()->getName().c_str());
+        const Point2 at[3] = { Point2(0.25f, 0.25f), Point2(0.5f, 0.75f), Point2(0.875f, 0.125f) };
+        Spectrum first(0.0f);
+        for (int k = 0; k < 3; ++k) {
+            PositionSamplingRecord pRec(0.0f);
+            sh->samplePosition(pRec, at[k]);
+            Intersection its;
+            its.t = 0.0f;
+            its.p = pRec.p;
+            its.uv = pRec.uv;
+            its.shape = sh;
+            its.geoFrame.n = pRec.n;
+            its.shFrame.n = pRec.n;
+            const Spectrum rho = bsdf->getDiffuseReflectance(its);
+            if (k == 0)
+                first = rho;
+            else if (rho != first)
+                Log(EError, "vrl (amd) frame mode: \"%s\" has a textured reflectance (amdMode=records "
+                    "evaluates it per gather point)", sh->getName().c_str());
+        }
+        return first;
+    }
+
+    static bool sameRgb(const Spectrum &s, const float *rgb) {
+        float v[3];
+        put3(v, s);
+        return v[0] == rgb[0] && v[1] == rgb[1] && v[2] == rgb[2];
     }
 
     void appendTriangles(const TriMesh *mesh, uint32_t mat) {
@@ -748,12 +904,32 @@ private:
         m_rendering = true;
         g.unlock();
         int rc = ALVRL_OK;
-        hipError_t e = hipSetDevice(m_device);
-        if (e == hipSuccess) e = hipMemsetAsync(m_fb, 0, sizeof(float) * m_rgb.size(), m_stream);
-        if (e == hipSuccess) rc = alvrl_integrator_render(m_it, 0, 1, m_fb, m_stream);
-        if (e == hipSuccess && rc == ALVRL_OK)
-            e = hipMemcpyAsync(&m_rgb[0], m_fb, sizeof(float) * m_rgb.size(), hipMemcpyDeviceToHost, m_stream);
-        if (e == hipSuccess && rc == ALVRL_OK) e = hipStreamSynchronize(m_stream);
+        hipError_t e = hipSuccess;
+        if (m_more.empty()) {
+            e = renderTiles(m_it, m_device, 0, 1, m_fb, m_stream, &m_rgb[0], m_rgb.size(), &rc);
+        } else {
+            /* every GPU renders its 64x64 tiles (alvrl_integrator_render with
+               rank k of N) on its own host thread; the tiles partition the
+               frame, so the framebuffer reduce is the sum of the N frames */
+            const uint32_t n = (uint32_t) m_devices.size();
+            std::vector<int> rcs(n, ALVRL_OK);
+            std::vector<hipError_t> es(n, hipSuccess);
+            std::vector<std::thread> th;
+            for (uint32_t k = 0; k < n; ++k)
+                th.push_back(std::thread([&, k]() {
+                    es[k] = renderTiles(k ? m_more[k - 1] : m_it, m_devices[k], k, n, k ? m_moreFb[k - 1] : m_fb,
+                                        k ? m_moreStreams[k - 1] : m_stream, k ? &m_moreRgb[k - 1][0] : &m_rgb[0],
+                                        m_rgb.size(), &rcs[k]);
+                }));
+            for (size_t k = 0; k < th.size(); ++k) th[k].join();
+            for (uint32_t k = 0; k < n; ++k) {
+                if (e == hipSuccess) e = es[k];
+                if (rc == ALVRL_OK) rc = rcs[k];
+            }
+            if (e == hipSuccess && rc == ALVRL_OK)
+                for (size_t k = 0; k < m_moreRgb.size(); ++k)
+                    for (size_t i = 0; i < m_rgb.size(); ++i) m_rgb[i] += m_moreRgb[k][i];
+        }
         g.lock();
         m_rendering = false;
         if (e == hipSuccess && rc == ALVRL_OK) m_framePass = m_pass;
@@ -761,6 +937,49 @@ private:
         g.unlock();
         checkHip(e, "frame render");
         check(rc, "alvrl_integrator_render");
+    }
+
+    /* one device's share of the frame: zero, render rank k's tiles, copy back */
+    static hipError_t renderTiles(alvrl_integrator *it, int device, uint32_t rank, uint32_t world, float *fb,
+            hipStream_t st, float *host, size_t n, int *rc) {
+        *rc = ALVRL_OK;
+        hipError_t e = hipSetDevice(device);
+        if (e == hipSuccess) e = hipMemsetAsync(fb, 0, sizeof(float) * n, st);
+        if (e == hipSuccess) *rc = alvrl_integrator_render(it, rank, world, fb, st);
+        if (e == hipSuccess && *rc == ALVRL_OK)
+            e = hipMemcpyAsync(host, fb, sizeof(float) * n, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess && *rc == ALVRL_OK) e = hipStreamSynchronize(st);
+        return e;
+    }
+
+    /* amdDevices: the slice-sharded prepass (alvrl_integrator_prepass_dist)
+     * with one host thread per GPU and the in-process exchange: rank k
+     * builds R for and refines the slices s % N == k, the non-zero mask is
+     * OR-ed and the cluster lists all-gathered, so every integrator ends the
+     * pass with every slice's list */
+    void prepassDevices() {
+        const uint32_t n = (uint32_t) m_devices.size();
+        std::vector<int> rcs(n, ALVRL_OK);
+        std::vector<std::thread> th;
+        for (uint32_t k = 0; k < n; ++k)
+            th.push_back(std::thread([&, k]() {
+                if (hipSetDevice(m_devices[k]) != hipSuccess) { rcs[k] = ALVRL_ERR_HIP; return; }
+                rcs[k] = alvrl_integrator_prepass_dist(k ? m_more[k - 1] : m_it, (uint32_t) m_pass, k, n,
+                                                       alvrl_local_exchange_rank(m_localEx, k));
+            }));
+        for (size_t k = 0; k < th.size(); ++k) th[k].join();
+        for (uint32_t k = 0; k < n; ++k)
+            check(rcs[k], "alvrl_integrator_prepass_dist (amdDevices)");
+    }
+
+    void releaseMore() {
+        for (size_t k = 0; k < m_more.size(); ++k) {
+            (void) hipSetDevice(m_devices[k + 1]);
+            if (k < m_moreFb.size() && m_moreFb[k]) (void) hipFree(m_moreFb[k]);
+            if (k < m_moreStreams.size() && m_moreStreams[k]) (void) hipStreamDestroy(m_moreStreams[k]);
+            alvrl_integrator_destroy(m_more[k]);
+        }
+        m_more.clear(); m_moreFb.clear(); m_moreStreams.clear(); m_moreRgb.clear();
     }
 
     /* LiInternal (vrlIntegrator.cpp:398-524) as gather records: the segment
@@ -791,8 +1010,12 @@ private:
             r.p[k] = (float) its.p[k]; r.n[k] = (float) its.shFrame.n[k];
         }
         const bool smooth = (type & BSDF::ESmooth) != 0;
-        if (smooth && !(type & BSDF::EDiffuseReflection))
-            warnOnce("a smooth non-diffuse BSDF's vol->surf term is evaluated as its diffuse reflectance");
+        /* the gathers' vol->surf term is SmoothDiffuse::eval; any
+           other smooth BSDF (plastic, rough or glossy ones) is refused rather
+           than approximated by its diffuse reflectance */
+        if (smooth && bsdf->getClass()->getName() != "SmoothDiffuse")
+            Log(EError, "vrl (amd): a smooth %s BSDF is not supported (the library's vol->surf term is the "
+                "smooth diffuse BSDF, diffuse.cpp:110-118)", bsdf->getClass()->getName().c_str());
         put3(r.albedo, smooth ? bsdf->getDiffuseReflectance(its) : Spectrum(0.0f));
         r.flags = ALVRL_REC_HIT | (smooth ? ALVRL_REC_SMOOTH : 0u) | ((type & BSDF::EDelta) ? ALVRL_REC_DELTA : 0u) |
             (rRec.medium && !rRec.medium->getSigmaS().isZero() ? ALVRL_REC_MEDIUM : 0u);
@@ -830,13 +1053,6 @@ private:
                 rRec2.medium = rRec.its.getTargetMedium(ray2.d);
             appendPathAt(ray2, rRec2, weight * transmittance * bsdfWeight / rrProb, thr2, sampleIndex, recs, first);
         }
-    }
-
-    void warnOnce(const char *msg) const {
-        std::lock_guard<std::mutex> g(m_frameLock);
-        if (m_warned) return;
-        m_warned = true;
-        Log(EWarn, "vrl (amd): %s", msg);
     }
 
     /* "records" mode: every sensor sample's eye path cast by Mitsuba, the
@@ -913,11 +1129,19 @@ private:
     alvrl_scene_desc m_desc;
     std::vector<float> m_tris;
     std::vector<uint32_t> m_mats;
-    std::vector<uint32_t> m_p2s;   // records mode: the pass's slice of every pixel (column-major)
+    std::vector<uint32_t> m_p2s;   // the pass's slice of every pixel (column-major); empty: brute force
     int m_width = 0, m_height = 0;
     float *m_fb = NULL;
     bool m_ready = false;
     int m_vrlsID = 0, m_ciID = 0;
+    /* amdDevices: m_devices[0] drives m_it / m_fb / m_stream; the others have
+     * their own library integrator, framebuffer, stream and host frame */
+    std::vector<int> m_devices;
+    std::vector<alvrl_integrator *> m_more;
+    std::vector<float *> m_moreFb;
+    std::vector<hipStream_t> m_moreStreams;
+    mutable std::vector<std::vector<float> > m_moreRgb;
+    alvrl_local_exchange *m_localEx = NULL;
     /* wakeup: the VRL resource this instance published (the master) and the
      * last one it installed (a render worker) */
     const SerializableObject *m_pubVrls = NULL, *m_installedVrls = NULL;
@@ -927,7 +1151,6 @@ private:
     mutable std::mutex m_frameLock;
     mutable std::condition_variable m_frameReady;
     mutable bool m_rendering = false;
-    mutable bool m_warned = false;
     mutable int m_framePass = -1;
     int m_pass = 0;
 };

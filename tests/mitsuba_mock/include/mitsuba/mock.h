@@ -249,6 +249,8 @@ public:
     Spectrum operator/(Float f) const;
     Spectrum &operator/=(Float f);
     Spectrum &operator+=(const Spectrum &s);
+    bool operator==(const Spectrum &s) const;
+    bool operator!=(const Spectrum &s) const;
     bool isZero() const;
     Float max() const;
     void toLinearRGB(Float &r, Float &g, Float &b) const;
@@ -350,12 +352,26 @@ public:
     virtual Float getEta() const;
 };
 
+/* render/common.h:56-69 */
+enum EMeasure { EInvalidMeasure = 0, ESolidAngle = 1, ELength = 2, EArea = 3, EDiscrete = 4 };
+
 struct PositionSamplingRecord {
     Point p;
     Normal n;
+    Point2 uv;
     Float pdf;
     const Object *object;
+    PositionSamplingRecord();
     PositionSamplingRecord(Float time);
+};
+
+/* render/common.h:164-218 */
+struct DirectionSamplingRecord {
+    Vector d;
+    Float pdf;
+    EMeasure measure;
+    DirectionSamplingRecord();
+    DirectionSamplingRecord(const Vector &d, EMeasure measure = ESolidAngle);
 };
 
 class Emitter : public ConfigurableObject {
@@ -369,6 +385,8 @@ public:
 class Shape : public ConfigurableObject {
 public:
     virtual AABB getAABB() const = 0;
+    /* render/shape.h:361-362 */
+    virtual void samplePosition(PositionSamplingRecord &pRec, const Point2 &sample) const;
     virtual ref<TriMesh> createTriMesh();
     const BSDF *getBSDF() const;
     const Medium *getInteriorMedium() const;
@@ -401,6 +419,9 @@ public:
                                Float timeSample) const = 0;
     virtual Spectrum sampleRayDifferential(RayDifferential &ray, const Point2 &samplePosition,
                                            const Point2 &apertureSample, Float timeSample) const;
+    /* render/sensor.h:265-266 */
+    virtual bool getSamplePosition(const PositionSamplingRecord &pRec, const DirectionSamplingRecord &dRec,
+                                   Point2 &position) const;
     const Film *getFilm() const;
     const Medium *getMedium() const;
     const AnimatedTransform *getWorldTransform() const;

@@ -28,7 +28,10 @@ NSIMD = 1024
 
 
 def main():
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from pmc_summary import build_id_of_run
     cfg, root, dst = sys.argv[1], sys.argv[2], sys.argv[3]
+    bid = build_id_of_run(os.path.join(root, f"pmc_{cfg}_VALU.log"))
     pairs = json.load(open(sys.argv[4])) if len(sys.argv) > 4 else {}
     rows = {}
     for fn in glob.glob(os.path.join(root, f"pmc_{cfg}_VALU", "**", "*counter_collection.csv"), recursive=True):
@@ -46,7 +49,7 @@ def main():
     for (key, _), d in rows.items():
         ns = d.get("ns")
         cyc = d["GRBM_GUI_ACTIVE"] / 8.0
-        rec = {"kernel": d["kernel"], "config": cfg, "ms": ns / 1e6 if ns else None,
+        rec = {"kernel": d["kernel"], "config": cfg, "build_id": bid, "ms": ns / 1e6 if ns else None,
                "clock_ghz": cyc / ns if ns else None,
                "valu_insts": d["SQ_INSTS_VALU"], "valu_trans_f32": d.get("SQ_INSTS_VALU_TRANS_F32"),
                "salu_insts": d.get("SQ_INSTS_SALU"), "lds_insts": d.get("SQ_INSTS_LDS"),
