@@ -79,6 +79,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-alt", action="store_true",
                     help="N > 1 with --shard slices: skip the second, pass-parallel measurement")
+    ap.add_argument("--no-records-mode", action="store_true",
+                    help="clustered configs: skip timing the host-cast (records mode) pipeline")
     ap.add_argument("--no-unconditional", action="store_true",
                     help="clustered configs: skip the comparison with the oracle's own pipeline")
     ap.add_argument("--cpu-row-stride", type=int, default=64,
@@ -353,6 +355,8 @@ def main():
             out["cpu_baseline"] = cpu_baseline_prepass(args, cfg, vrls, pc, it, out["cpu_baseline"],
                                                        pre_pairs / max(args.steps, 1),
                                                        render_pairs / max(args.steps, 1))
+            if not args.no_records_mode:
+                out["records_mode"] = records_mode(cfg, vrls, pc, args.warmup + args.steps + 10, gpu)
             if not args.no_unconditional:
                 out["pixel_rmse_vs_cpu_unconditional"] = unconditional_parity(
                     cfg, vrls, pc, args.warmup + args.steps - 1, fb.view(-1, 3).cpu().numpy(), gpu,
@@ -592,6 +596,65 @@ def unconditional_parity(cfg, vrls, pc, pass_, fast_frame, device=0, row_stride=
                                      b["reps"][b["slice_off"][s]:b["slice_off"][s + 1]]))
         out["fast_slices_with_oracle_lists"] = [same, len(a["slice_off"]) - 1]
     return out
+
+
+def records_mode(cfg, vrls, pc, pass0, device=0, steps=2, block=32, threads=16):
+    """The host-cast ABI the Mitsuba plugin's records mode drives
+    (include/alvrl_host.h "host-cast scenes"), timed per pass:
+    the host hands the representative pixels' eye records to
+    alvrl_integrator_prepass_records (R, clusters) and renders the frame in
+    32x32 blocks from `threads` host threads, one alvrl_gather_clustered_host
+    call per block with host-memory records and results (renderBlock,
+    renderproc.cpp:52-86) -- every record crosses PCIe.  The host here plays
+    Mitsuba with the library's own scene (the smoke box has no null surfaces,
+    so buildSlices' gather point of a pixel is its eye record's hit)."""
+    import numpy as np
+    import alvrl
+    from concurrent.futures import ThreadPoolExecutor
+    W, H = cfg["w"], cfg["h"]
+    s = alvrl.scene_default(W, H)
+    recs = alvrl.scene_records(s)                        # the host's rays, cast once
+    props = cfg["props"] + (";" if cfg["props"] else "") + f"seed={SEED_RNG}"
+    it = alvrl.Integrator(props, device=device)
+    it.set_vrls(vrls, pc)
+    it.preprocess_ext(W, H, recs, list(s.box_min), list(s.box_max), alvrl.Medium())
+    ctx = it.context()
+    p2s = it.slices()
+    allpix = np.arange(W * H, dtype=np.uint32)
+    sl_all = p2s[(allpix % W) * H + allpix // W]
+    blocks = []
+    for by in range(0, H, block):
+        for bx in range(0, W, block):
+            ids = (np.arange(by, min(by + block, H))[:, None] * W + np.arange(bx, min(bx + block, W))[None, :])
+            ids = ids.ravel().astype(np.uint32)
+            blocks.append((np.ascontiguousarray(recs[ids]), np.ascontiguousarray(sl_all[ids]), ids))
+    frame = np.zeros((W * H, 3), np.float32)
+
+    def render_block(b):
+        r, sl, ids = b
+        frame[ids] = ctx.gather_clustered_host(r, sl, ids=ids)
+
+    def one_pass(p):
+        pix = it.rep_pixels(p)
+        it.prepass_records(p, recs[pix], np.arange(len(pix), dtype=np.uint32))
+        t = time.perf_counter()
+        with ThreadPoolExecutor(threads) as ex:
+            list(ex.map(render_block, blocks))
+        return time.perf_counter() - t
+
+    one_pass(pass0)                                      # warm-up
+    s0 = it.stats()
+    t0 = time.perf_counter()
+    render_s = sum(one_pass(pass0 + 1 + i) for i in range(steps))
+    dt = time.perf_counter() - t0
+    s1 = it.stats()
+    pairs = (s1["contrib_preprocess"] - s0["contrib_preprocess"]) + (s1["contrib_render"] - s0["contrib_render"])
+    it.close()
+    return {"value": pairs / dt, "unit": "VRL contributions/s", "steps": steps, "ms_per_step": dt / steps * 1e3,
+            "render_ms_per_step": render_s / steps * 1e3, "blocks": len(blocks), "block": block,
+            "host_threads": threads,
+            "note": "host-pointer ABI (records and results cross PCIe), renderBlock-sized calls from "
+                    "concurrent host threads; not the metric's value"}
 
 
 def cpu_threads():

@@ -59,6 +59,18 @@ typedef struct {
     const uint32_t *occluder_material;
     float occluder_specular[3];
     float occluder_eta;   /* intIOR / extIOR of DIELECTRIC triangles (<= 0: bk7 / air, ior.h:43, 60) */
+    /* Optional area emitter (src/emitters/area.cpp on a triangle mesh),
+     * replacing the point light when n_emitter_tris > 0: 9 floats per
+     * triangle (p0, p1, p2), emitting radiance emitter_radiance on the side of
+     * normalize(cross(p1 - p0, p2 - p0)).  Particles start at a point drawn
+     * uniformly by area (TriMesh::samplePosition, trimesh.cpp:388-423;
+     * Triangle::sample, triangle.cpp:24-59) with power radiance * pi * area
+     * (area.cpp:198) and a cosine-weighted direction (area.cpp:115-123).  The
+     * emitter is no surface of its own: list its triangles among the
+     * occluders too for eye rays and shadow tests to see it. */
+    const float *emitter_tris;
+    uint32_t n_emitter_tris;
+    float emitter_radiance[3];
 } alvrl_scene_desc;
 #define ALVRL_MAT_DIFFUSE 0u
 #define ALVRL_MAT_MIRROR 1u

@@ -410,7 +410,9 @@ class SceneDesc(C.Structure):
                 ("light_pos", C.c_float * 3), ("light_intensity", C.c_float * 3),
                 ("medium", MediumDesc), ("occluders", C.POINTER(C.c_float)), ("n_occluders", C.c_uint32),
                 ("occluder_albedo", C.c_float * 3), ("occluder_material", C.POINTER(C.c_uint32)),
-                ("occluder_specular", C.c_float * 3), ("occluder_eta", C.c_float)]
+                ("occluder_specular", C.c_float * 3), ("occluder_eta", C.c_float),
+                ("emitter_tris", C.POINTER(C.c_float)), ("n_emitter_tris", C.c_uint32),
+                ("emitter_radiance", C.c_float * 3)]
 
 
 MAT_DIFFUSE, MAT_MIRROR, MAT_NULL, MAT_DIELECTRIC = 0, 1, 2, 3
@@ -656,6 +658,19 @@ def scene_default(width: int, height: int) -> SceneDesc:
     s = SceneDesc()
     _host().alvrl_scene_default(C.byref(s), width, height)
     return s
+
+
+def scene_set_area_emitter(scene: SceneDesc, tris, radiance) -> SceneDesc:
+    """An area emitter replacing the point light (alvrl_scene_desc.emitter_tris):
+    (n, 9) triangles emitting `radiance` on the side of cross(p1 - p0, p2 - p0).
+    The array is kept alive on the descriptor."""
+    arr = np.ascontiguousarray(np.asarray(tris, np.float32).reshape(-1, 9))
+    scene._emit_keep = arr
+    scene.emitter_tris = arr.ctypes.data_as(C.POINTER(C.c_float)) if len(arr) else None
+    scene.n_emitter_tris = len(arr)
+    for i in range(3):
+        scene.emitter_radiance[i] = float(radiance[i])
+    return scene
 
 
 def scene_set_occluders(scene: SceneDesc, tris, albedo=(0.5, 0.5, 0.5), material=None,

@@ -3,6 +3,7 @@
 // live in integrator.hip (they drive the device).
 #include "alvrl_host.h"
 
+#include <cmath>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -36,6 +37,18 @@ const char* scene_problem(const alvrl_scene_desc& s)
     if (s.occluders && s.occluder_material)
         for (uint32_t i = 0; i < s.n_occluders; i++)
             if (s.occluder_material[i] > ALVRL_MAT_DIELECTRIC) return "alvrl_scene_desc: unknown occluder material";
+    if (s.n_emitter_tris && !s.emitter_tris) return "alvrl_scene_desc: n_emitter_tris > 0 without emitter_tris";
+    if (s.n_emitter_tris) {
+        for (size_t i = 0; i < 9 * (size_t)s.n_emitter_tris; i++)
+            if (!std::isfinite(s.emitter_tris[i])) return "alvrl_scene_desc: non-finite emitter vertex";
+        for (int i = 0; i < 3; i++)
+            if (!std::isfinite(s.emitter_radiance[i]) || s.emitter_radiance[i] < 0)
+                return "alvrl_scene_desc: emitter radiance must be finite and >= 0";
+        SmokeBox b;
+        b.emit.assign(s.emitter_tris, s.emitter_tris + 9 * (size_t)s.n_emitter_tris);
+        b.prepare_emitter();
+        if (!(b.emit_area > 0)) return "alvrl_scene_desc: the emitter triangles have no area";
+    }
     return nullptr;
 }
 SmokeBox to_box(const alvrl_scene_desc& s)
@@ -59,6 +72,11 @@ SmokeBox to_box(const alvrl_scene_desc& s)
         b.occ_mat.assign(s.occluder_material, s.occluder_material + s.n_occluders);
     for (int i = 0; i < 3; i++) b.occ_spec[i] = s.occluder_specular[i];
     if (s.occluder_eta > 0) b.occ_eta = s.occluder_eta;
+    if (s.emitter_tris && s.n_emitter_tris) {
+        b.emit.assign(s.emitter_tris, s.emitter_tris + 9 * (size_t)s.n_emitter_tris);
+        for (int i = 0; i < 3; i++) b.emit_radiance[i] = s.emitter_radiance[i];
+        b.prepare_emitter();
+    }
     return b;
 }
 }  // namespace host

@@ -431,13 +431,18 @@ float sample_distance(const MediumParams& m, Stream& smp, float* pdf_max)
 void trace_particle(const SmokeBox& sc, Stream& smp, bool short_vrls, int max_depth, int rr_depth, Sink& k)
 {
     const MediumParams& m = sc.medium;
-    (void)smp.next(); (void)smp.next();   // sampleEmitterPosition (scene.cpp:958-974)
+    const float sx = smp.next(), sy = smp.next();   // sampleEmitterPosition (scene.cpp:958-974)
     float power[3];
-    for (int i = 0; i < 3; i++) power[i] = sc.light_intensity[i] * (float)(4 * kPi);
-    const float dx = smp.next(), dy = smp.next();   // sampleDirection (point.cpp:99-106)
-    V3 dir = uniform_sphere(dx, dy);
+    const float dx = smp.next(), dy = smp.next();   // sampleDirection (point.cpp:99-106, area.cpp:115-123)
+    V3 dir, o;
+    if (sc.area_light()) {
+        sc.sample_area_emission(sx, sy, dx, dy, &o, &dir, power);
+    } else {
+        for (int i = 0; i < 3; i++) power[i] = sc.light_intensity[i] * (float)(4 * kPi);
+        dir = uniform_sphere(dx, dy);
+        o = sc.light_pos;
+    }
     if (power[0] == 0 && power[1] == 0 && power[2] == 0) return;
-    V3 o = sc.light_pos;
     k.start = o;
     for (int i = 0; i < 3; i++) k.power[i] = power[i];
     int depth = 1;
@@ -545,6 +550,57 @@ void trace_particle(const SmokeBox& sc, Stream& smp, bool short_vrls, int max_de
 }
 
 }  // namespace
+
+// TriMesh::prepareSamplingTable (trimesh.cpp:388-403): Triangle::surfaceArea
+// (triangle.cpp: 0.5 |cross(p1 - p0, p2 - p0)|) appended to a
+// DiscreteDistribution (running float sum), normalized (pmf.h:101-114)
+void SmokeBox::prepare_emitter()
+{
+    const size_t n = emit.size() / 9;
+    emit_cdf.assign(1, 0.0f);
+    for (size_t i = 0; i < n; i++) {
+        const float* t = &emit[9 * i];
+        const V3 p0 = v3(t[0], t[1], t[2]), p1 = v3(t[3], t[4], t[5]), p2 = v3(t[6], t[7], t[8]);
+        const float a = 0.5f * length(cross(p1 - p0, p2 - p0));
+        emit_cdf.push_back(emit_cdf.back() + a);
+    }
+    emit_area = emit_cdf.back();
+    if (emit_area > 0) {
+        const float norm = 1.0f / emit_area;
+        for (size_t i = 1; i < emit_cdf.size(); i++) emit_cdf[i] *= norm;
+        emit_cdf.back() = 1.0f;
+    }
+}
+
+void SmokeBox::sample_area_emission(float sx, float sy, float dx, float dy, V3* o, V3* d, float power[3]) const
+{
+    // Scene::sampleEmitterPosition: one emitter, so m_emitterPDF.sampleReuse
+    // leaves sample.x as it is and the pdf is 1 (pmf.h:124-169)
+    // TriMesh::samplePosition: the triangle by m_areaDistr.sampleReuse(sample.y)
+    const size_t n = emit_cdf.size() - 1;
+    size_t lb = (size_t)(std::lower_bound(emit_cdf.begin(), emit_cdf.end(), sy) - emit_cdf.begin());
+    size_t idx = std::min(n - 1, (size_t)std::max((ptrdiff_t)0, (ptrdiff_t)lb - 1));
+    // a zero-area triangle is skipped (the reference's loop would read past the table
+    // if the last one had zero area)
+    while (idx + 1 < n && emit_cdf[idx + 1] - emit_cdf[idx] == 0) ++idx;
+    const float y = (sy - emit_cdf[idx]) / (emit_cdf[idx + 1] - emit_cdf[idx]);
+    // Triangle::sample with warp::squareToUniformTriangle (warp.cpp:76-79)
+    const float a = safe_sqrt(1.0f - sx);
+    const float bx = 1 - a, by = a * y;
+    const float* t = &emit[9 * idx];
+    const V3 p0 = v3(t[0], t[1], t[2]), p1 = v3(t[3], t[4], t[5]), p2 = v3(t[6], t[7], t[8]);
+    const V3 sideA = p1 - p0, sideB = p2 - p0;
+    *o = (p0 + sideA * bx) + sideB * by;
+    const V3 nn = normalize(cross(sideA, sideB));
+    // AreaEmitter::samplePosition returns m_power = m_radiance * M_PI * area
+    // (area.cpp:94-98, 198); sampleDirection: a cosine-weighted direction in
+    // Frame(pRec.n), weight 1 (area.cpp:115-123)
+    for (int i = 0; i < 3; i++) power[i] = (emit_radiance[i] * (float)kPi) * emit_area;
+    const V3 l = cosine_hemisphere(dx, dy);
+    V3 fs, ft;
+    frame_of(nn, &fs, &ft);
+    *d = (fs * l.x + ft * l.y) + nn * l.z;
+}
 
 void SmokeBox::pixel_sample(int x, int y, uint32_t seed, uint32_t pass, uint32_t sample, uint32_t spp, float* px,
                             float* py) const

@@ -80,6 +80,19 @@ struct SmokeBox {
     float occ_spec[3] = {1.0f, 1.0f, 1.0f};
     // dielectric triangles: m_eta = intIOR / extIOR (dielectric.cpp:149-158; bk7 / air, ior.h:43, 60)
     float occ_eta = 1.5046f / 1.000277f;
+    // area emitter (alvrl_scene_desc::emitter_tris): triangles, radiance, and
+    // TriMesh's sampling table (prepare_emitter): the normalized area CDF of
+    // DiscreteDistribution (pmf.h:101-114) and the surface area
+    std::vector<float> emit;
+    float emit_radiance[3] = {0.0f, 0.0f, 0.0f};
+    std::vector<float> emit_cdf;
+    float emit_area = 0.0f;
+    bool area_light() const { return !emit.empty(); }
+    void prepare_emitter();
+    // Scene::sampleEmitterPosition + Emitter::sampleDirection of the area
+    // emitter for the tracer's draws (sx, sy) and (dx, dy): origin, direction
+    // and power (vrlTracer.h:109-120)
+    void sample_area_emission(float sx, float sy, float dx, float dy, V3* o, V3* d, float power[3]) const;
     // the BSDF of a hit: 0 diffuse (walls: tri < 0), 1 mirror, 2 null, 3 dielectric
     uint32_t mat(int tri) const { return (tri < 0 || occ_mat.empty()) ? 0u : occ_mat[(size_t)tri]; }
     bool has_delta() const

@@ -259,6 +259,8 @@ struct alvrl_integrator {
         alvrl_medium_desc md = s.medium;
         chk(alvrl_set_medium(ctx, &md), "alvrl_set_medium");
         scene_desc.occluder_material = scene.occ_mat.empty() ? nullptr : scene.occ_mat.data();
+        scene_desc.emitter_tris = scene.emit.empty() ? nullptr : scene.emit.data();   // the owned copy
+        scene_desc.n_emitter_tris = (uint32_t)(scene.emit.size() / 9);
         chains = scene.has_delta();
         if (chains && convergenceFalseColor)
             throw IntegError(ALVRL_ERR_INVALID, "convergenceFalseColor is not supported with delta-BSDF occluders");

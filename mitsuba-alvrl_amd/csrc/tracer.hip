@@ -49,6 +49,12 @@ struct TScene {
     int sigma_s_zero;
     alvrl::bvh::View bv;          // occluders (ntri == 0: none)
     float occ_albedo[3];
+    // area emitter (SmokeBox::emit; nemit == 0: the point light): triangles,
+    // the normalized area CDF (nemit + 1 entries), radiance and surface area
+    const float* emit;
+    const float* emit_cdf;
+    uint32_t nemit;
+    float emit_radiance[3], emit_area;
 };
 
 struct F3 { float x, y, z; };
@@ -263,15 +269,50 @@ struct Sink {
     }
 };
 
+// SmokeBox::sample_area_emission (host/scene.cpp), the same operations:
+// Scene::sampleEmitterPosition with one emitter, TriMesh::samplePosition,
+// Triangle::sample, AreaEmitter::sampleDirection (area.cpp:94-123)
+__device__ F3 area_emission(const TScene& sc, float sx, float sy, float dx, float dy, F3* dir, float power[3])
+{
+    const uint32_t n = sc.nemit;
+    uint32_t lb = 0;
+    while (lb <= n && sc.emit_cdf[lb] < sy) lb++;   // std::lower_bound
+    uint32_t idx = lb > 0 ? lb - 1 : 0;
+    if (idx > n - 1) idx = n - 1;
+    while (idx + 1 < n && sc.emit_cdf[idx + 1] - sc.emit_cdf[idx] == 0) ++idx;
+    const float y = (sy - sc.emit_cdf[idx]) / (sc.emit_cdf[idx + 1] - sc.emit_cdf[idx]);
+    const float a = safe_sqrt(1.0f - sx);
+    const float bx = 1 - a, by = a * y;
+    const float* t = sc.emit + 9 * (size_t)idx;
+    const F3 p0 = f3(t[0], t[1], t[2]);
+    const F3 sideA = sub(f3(t[3], t[4], t[5]), p0), sideB = sub(f3(t[6], t[7], t[8]), p0);
+    const F3 o = add(add(p0, mul(sideA, bx)), mul(sideB, by));
+    const F3 c = cross(sideA, sideB);
+    const F3 nn = mul(c, 1.0f / len(c));
+    for (int i = 0; i < 3; i++) power[i] = (sc.emit_radiance[i] * (float)kPi) * sc.emit_area;
+    const F3 l = cosine_hemisphere(dx, dy);
+    F3 fs, ft;
+    frame_of(nn, &fs, &ft);
+    *dir = add(add(mul(fs, l.x), mul(ft, l.y)), mul(nn, l.z));
+    return o;
+}
+
 __device__ void trace_particle(const TScene& sc, Stream& smp, bool short_vrls, int max_depth, int rr_depth, Sink& k)
 {
-    (void)smp.next(); (void)smp.next();   // sampleEmitterPosition (scene.cpp:958-974)
-    const float dx = smp.next(), dy = smp.next();   // sampleDirection (point.cpp:99-106)
-    F3 dir = uniform_sphere(dx, dy);
-    if (sc.power[0] == 0 && sc.power[1] == 0 && sc.power[2] == 0) return;
-    F3 o = f3(sc.light_pos[0], sc.light_pos[1], sc.light_pos[2]);
+    const float sx = smp.next(), sy = smp.next();   // sampleEmitterPosition (scene.cpp:958-974)
+    const float dx = smp.next(), dy = smp.next();   // sampleDirection (point.cpp:99-106, area.cpp:115-123)
+    float power[3];
+    F3 dir, o;
+    if (sc.nemit) {
+        o = area_emission(sc, sx, sy, dx, dy, &dir, power);
+    } else {
+        dir = uniform_sphere(dx, dy);
+        o = f3(sc.light_pos[0], sc.light_pos[1], sc.light_pos[2]);
+        for (int i = 0; i < 3; i++) power[i] = sc.power[i];
+    }
+    if (power[0] == 0 && power[1] == 0 && power[2] == 0) return;
     k.start = o;
-    for (int i = 0; i < 3; i++) k.power[i] = sc.power[i];
+    for (int i = 0; i < 3; i++) k.power[i] = power[i];
     int depth = 1;
     float thr[3] = {1.0f, 1.0f, 1.0f};
     const float eta = 1.0f;
@@ -311,7 +352,7 @@ __device__ void trace_particle(const TScene& sc, Stream& smp, bool short_vrls, i
             const F3 endPoint = short_vrls ? mp : hp;
             k.end_current(endPoint);
             k.start = mp;
-            for (int i = 0; i < 3; i++) k.power[i] = thr[i] * sc.power[i];
+            for (int i = 0; i < 3; i++) k.power[i] = thr[i] * power[i];
             o = mp; dir = wo; mint = 0.0f;
         } else if (its_valid) {   // vrlTracer.h:173-213
             const float rpf = 1.0f / pf;
@@ -336,7 +377,7 @@ __device__ void trace_particle(const TScene& sc, Stream& smp, bool short_vrls, i
             for (int i = 0; i < 3; i++) thr[i] *= bw[i];
             k.end_current(p);
             k.start = p;
-            for (int i = 0; i < 3; i++) k.power[i] = thr[i] * sc.power[i];
+            for (int i = 0; i < 3; i++) k.power[i] = thr[i] * power[i];
             o = p; dir = wo; mint = 1e-4f;
         } else {
             break;
@@ -763,6 +804,11 @@ TScene make_tscene(const alvrl::host::SmokeBox& box)
     sc.mx_inv_norm = box.medium.mx_inv_norm;
     sc.sigma_s_zero = (sc.sigma_s[0] == 0 && sc.sigma_s[1] == 0 && sc.sigma_s[2] == 0) ? 1 : 0;
     sc.bv = alvrl::bvh::View{nullptr, nullptr, nullptr, 0u};
+    sc.emit = nullptr;
+    sc.emit_cdf = nullptr;
+    sc.nemit = (uint32_t)(box.emit.size() / 9);
+    for (int i = 0; i < 3; i++) sc.emit_radiance[i] = box.emit_radiance[i];
+    sc.emit_area = box.emit_area;
     return sc;
 }
 
@@ -811,6 +857,8 @@ ALVRL_API int alvrl_volpath_render(const alvrl_scene_desc* s, const alvrl_volpat
     const alvrl::host::SmokeBox box = alvrl::host::to_box(*s);
     if (box.has_delta())
         return terr(ALVRL_ERR_INVALID, "alvrl_volpath_render: mirror / null occluders are not supported by the volpath reference");
+    if (box.area_light())
+        return terr(ALVRL_ERR_INVALID, "alvrl_volpath_render: the volpath reference samples the point light only");
     const uint64_t npix = (uint64_t)box.width * (uint64_t)box.height;
     if (!d_pixel_ids && n > npix) return terr(ALVRL_ERR_INVALID, "alvrl_volpath_render: n > W*H without pixel ids");
     if (n == 0) return ALVRL_OK;
@@ -896,8 +944,20 @@ ALVRL_API int alvrl_trace_vrls_gpu(const alvrl_scene_desc* s, uint32_t seed, uin
     *n = 0;
     if (target == 0) { *particles = 0; return ALVRL_OK; }
     if (sc.sigma_s_zero) { *particles = 1000001; return ALVRL_OK; }   // the host loop's bound
-    if (sc.power[0] == 0 && sc.power[1] == 0 && sc.power[2] == 0)
+    const float* pw = sc.nemit ? sc.emit_radiance : sc.power;
+    if (pw[0] == 0 && pw[1] == 0 && pw[2] == 0)
         return terr(ALVRL_ERR_INVALID, "alvrl_trace_vrls_gpu: the light emits nothing (the VRL target is unreachable)");
+    // the area emitter's triangles and sampling table on the device
+    DMem<float> d_emit, d_cdf;
+    if (sc.nemit) {
+        if (d_emit.alloc(box.emit.size()) != hipSuccess || d_cdf.alloc(box.emit_cdf.size()) != hipSuccess)
+            return terr(ALVRL_ERR_NOMEM, "alvrl_trace_vrls_gpu: device memory");
+        if (hipMemcpy(d_emit.p, box.emit.data(), box.emit.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy(d_cdf.p, box.emit_cdf.data(), box.emit_cdf.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+            return terr(ALVRL_ERR_HIP, "alvrl_trace_vrls_gpu: copy");
+        sc.emit = d_emit.p;
+        sc.emit_cdf = d_cdf.p;
+    }
     // count pass, batch by batch, until the running total reaches the target
     const uint32_t P = std::min<uint32_t>(1u << 20, std::max<uint32_t>(4096u, target));
     DMem<uint32_t> d_cnt;

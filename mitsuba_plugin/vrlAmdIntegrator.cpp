@@ -614,17 +614,31 @@ private:
             Log(EError, "vrl (amd) frame mode needs the camera inside the medium (amdMode=records does not)");
         const Medium *medium = describeMedium(scene, &m_desc.medium);
 
-        /* the point light: samplePosition returns its power, intensity * 4 pi (point.cpp:81-91) */
-        const Emitter *light = NULL;
-        for (size_t i = 0; i < scene->getEmitters().size(); ++i)
-            if (scene->getEmitters()[i]->getType() & Emitter::EDeltaPosition)
-                light = scene->getEmitters()[i].get();
-        if (!light || scene->getEmitters().size() != 1)
-            Log(EError, "vrl (amd) frame mode needs one point light (amdMode=records takes any emitters)");
+        /* the one emitter: a point light (samplePosition returns its power,
+           intensity * 4 pi, point.cpp:81-91) or an area emitter on a triangle
+           mesh (alvrl_scene_desc::emitter_tris; its radiance from
+           evalPosition = radiance * pi, area.cpp:100-102) */
+        if (scene->getEmitters().size() != 1)
+            Log(EError, "vrl (amd) frame mode needs exactly one emitter (amdMode=records takes any emitters)");
+        const Emitter *light = scene->getEmitters()[0].get();
         PositionSamplingRecord pRec(0.0f);
         const Spectrum power = light->samplePosition(pRec, Point2(0.5f));
-        put3(m_desc.light_intensity, power * (Float) (0.25f * INV_PI));
-        for (int i = 0; i < 3; ++i) m_desc.light_pos[i] = (float) pRec.p[i];
+        m_emit.clear();
+        if (light->getType() & Emitter::EDeltaPosition) {
+            put3(m_desc.light_intensity, power * (Float) (0.25f * INV_PI));
+            for (int i = 0; i < 3; ++i) m_desc.light_pos[i] = (float) pRec.p[i];
+        } else if (light->getType() & Emitter::EOnSurface) {
+            const TriMesh *lmesh = NULL;
+            for (size_t s = 0; s < scene->getShapes().size(); ++s)
+                if (scene->getShapes()[s]->isEmitter() && scene->getShapes()[s]->getEmitter() == light)
+                    lmesh = dynamic_cast<const TriMesh *>(scene->getShapes()[s].get());
+            if (!lmesh)
+                Log(EError, "vrl (amd) frame mode: the area emitter must sit on a triangle mesh");
+            appendTriangles(lmesh, &m_emit);
+            put3(m_desc.emitter_radiance, light->evalPosition(pRec) * (Float) INV_PI);
+        } else {
+            Log(EError, "vrl (amd) frame mode needs a point light or an area emitter (amdMode=records takes any)");
+        }
 
         /* the container: the shape whose interior is the medium; its walls' diffuse reflectance */
         m_tris.clear(); m_mats.clear();
@@ -640,8 +654,22 @@ private:
                     m_desc.box_min[i] = (float) box.min[i];
                     m_desc.box_max[i] = (float) box.max[i];
                 }
-                if (bsdf) put3(m_desc.albedo, diffuseReflectance(sh, bsdf));
+                if (bsdf) put3(m_desc.albedo, diffuseReflectance(sh, bsdf, true));
                 haveBox = true;
+                /* a container that is not the box itself (a rotated or curved
+                   mesh) bounds the medium with its own triangles; on the box's
+                   faces they tie with its walls, which win */
+                if (const TriMesh *cm = dynamic_cast<const TriMesh *>(sh)) {
+                    if (!onBoxFaces(cm, box)) {
+                        const Spectrum rho = diffuseReflectance(sh, bsdf, false);
+                        if (haveOccAlbedo && !sameRgb(rho, m_desc.occluder_albedo))
+                            Log(EError, "vrl (amd) frame mode: a mesh container and diffuse occluders with "
+                                "different reflectances (amdMode=records takes any)");
+                        put3(m_desc.occluder_albedo, rho);
+                        haveOccAlbedo = true;
+                        appendTriangles(cm, ALVRL_MAT_DIFFUSE);
+                    }
+                }
                 continue;
             }
             const TriMesh *mesh = dynamic_cast<const TriMesh *>(sh);
@@ -683,6 +711,8 @@ private:
         if (!haveBox)
             Log(EError, "vrl (amd) needs a shape that contains the medium (its interior)");
         m_desc.n_occluders = (uint32_t) m_mats.size();
+        m_desc.emitter_tris = m_emit.empty() ? NULL : &m_emit[0];
+        m_desc.n_emitter_tris = (uint32_t) (m_emit.size() / 9);
     }
 
     /* The constant diffuse reflectance of a shape's smooth diffuse BSDF,
@@ -690,8 +720,11 @@ private:
      * normal and uv): the descriptor holds one albedo per class of surface,
      * so another smooth BSDF (its vol->surf term is not rho / pi cos) or a
      * textured reflectance is refused with a pointer to records mode */
-    Spectrum diffuseReflectance(const Shape *sh, const BSDF *bsdf) const {
-        if (bsdf->getClass()->getName() != "SmoothDiffuse")
+    Spectrum diffuseReflectance(const Shape *sh, const BSDF *bsdf, bool container = false) const {
+        /* the box's walls face the medium whatever the mesh's winding, so a
+           two-sided diffuse container is the same surface */
+        const std::string cls = bsdf->getClass()->getName();
+        if (cls != "SmoothDiffuse" && !(container && cls == "TwoSidedBRDF"))
             Log(EError, "vrl (amd) frame mode: the BSDF of \"%s\" is %s; its walls and occluders take the "
                 "smooth diffuse BSDF the gathers evaluate (diffuse.cpp:110-118)", sh->getName().c_str(),
                 bsdf->getClass()->getName().c_str());
@@ -724,17 +757,37 @@ private:
     }
 
     void appendTriangles(const TriMesh *mesh, uint32_t mat) {
+        appendTriangles(mesh, &m_tris);
+        m_mats.resize(m_tris.size() / 9, mat);
+    }
+
+    static void appendTriangles(const TriMesh *mesh, std::vector<float> *out) {
+        const Point *pos = mesh->getVertexPositions();
+        const Triangle *tri = mesh->getTriangles();
+        for (size_t f = 0; f < mesh->getTriangleCount(); ++f)
+            for (int k = 0; k < 3; ++k) {
+                const Point &p = pos[tri[f].idx[k]];
+                out->push_back((float) p.x);
+                out->push_back((float) p.y);
+                out->push_back((float) p.z);
+            }
+    }
+
+    /* every vertex on a face of the box: the mesh is the box itself */
+    static bool onBoxFaces(const TriMesh *mesh, const AABB &box) {
         const Point *pos = mesh->getVertexPositions();
         const Triangle *tri = mesh->getTriangles();
         for (size_t f = 0; f < mesh->getTriangleCount(); ++f) {
-            for (int k = 0; k < 3; ++k) {
-                const Point &p = pos[tri[f].idx[k]];
-                m_tris.push_back((float) p.x);
-                m_tris.push_back((float) p.y);
-                m_tris.push_back((float) p.z);
-            }
-            m_mats.push_back(mat);
+            bool face = false;   /* all three vertices on one common face */
+            for (int a = 0; a < 3 && !face; ++a)
+                for (int side = 0; side < 2 && !face; ++side) {
+                    const Float c = side ? box.max[a] : box.min[a];
+                    face = pos[tri[f].idx[0]][a] == c && pos[tri[f].idx[1]][a] == c && pos[tri[f].idx[2]][a] == c;
+                }
+            if (!face)
+                return false;
         }
+        return true;
     }
 
     /* records mode: the medium, every shape's triangles for the gathers'
@@ -1129,6 +1182,7 @@ private:
     alvrl_scene_desc m_desc;
     std::vector<float> m_tris;
     std::vector<uint32_t> m_mats;
+    std::vector<float> m_emit;   /* frame mode: the area emitter's triangles */
     std::vector<uint32_t> m_p2s;   // the pass's slice of every pixel (column-major); empty: brute force
     int m_width = 0, m_height = 0;
     float *m_fb = NULL;

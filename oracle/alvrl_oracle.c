@@ -1245,19 +1245,79 @@ static void end_current(vrl_sink *k, v3 p)
     vrl_put(k, p);
 }
 
-static void trace_particle(const alvrl_o_scene *s, const alvrl_o_medium *m, seq_sampler *smp,
-                           int short_vrls, int max_depth, int rr_depth, vrl_sink *k)
+/* The area emitter's sampling table: TriMesh::prepareSamplingTable
+ * (trimesh.cpp:388-403) appends Triangle::surfaceArea (0.5 |sideA x sideB|)
+ * to a DiscreteDistribution (a running float sum) and normalizes it
+ * (pmf.h:101-114: cdf[i] *= 1 / sum for i >= 1, the last entry 1). */
+typedef struct { float *cdf; uint32_t n; float area; } area_table;
+
+static void area_table_init(area_table *t, const float *tris, uint32_t n)
+{
+    t->n = n;
+    t->cdf = (float *)calloc((size_t)n + 1, sizeof(float));
+    t->cdf[0] = 0.0f;
+    for (uint32_t i = 0; i < n; i++) {
+        const float *q = tris + 9 * (size_t)i;
+        v3 sideA = sub(ld3(q + 3), ld3(q)), sideB = sub(ld3(q + 6), ld3(q));
+        t->cdf[i + 1] = t->cdf[i] + 0.5f * len(cross(sideA, sideB));
+    }
+    t->area = t->cdf[n];
+    if (t->area > 0) {
+        float norm = 1.0f / t->area;
+        for (uint32_t i = 1; i <= n; i++) t->cdf[i] *= norm;
+        t->cdf[n] = 1.0f;
+    }
+}
+
+/* Scene::sampleEmitterPosition (scene.cpp:958-974; one emitter: sample.x is
+ * kept and the pdf is 1) -> AreaEmitter::samplePosition (area.cpp:94-98) ->
+ * TriMesh::samplePosition (trimesh.cpp:412-423: the triangle by
+ * m_areaDistr.sampleReuse(sample.y), pmf.h:124-169) -> Triangle::sample with
+ * squareToUniformTriangle (triangle.cpp:24-59, warp.cpp:76-79); power =
+ * m_power = radiance * pi * area (area.cpp:198); then sampleDirection: a
+ * cosine-weighted direction in Frame(n), weight 1 (area.cpp:115-123). */
+static v3 area_emission(const alvrl_o_scene *s, const area_table *t, float sx, float sy, float dx, float dy,
+                        v3 *dir, float power[3])
+{
+    uint32_t lb = 0;
+    while (lb <= t->n && t->cdf[lb] < sy) lb++;            /* std::lower_bound */
+    int64_t idx = (int64_t)lb - 1;
+    if (idx < 0) idx = 0;
+    if (idx > (int64_t)t->n - 1) idx = (int64_t)t->n - 1;
+    /* a zero-area triangle is skipped (past the last one the reference would read outside the table) */
+    while (idx + 1 < (int64_t)t->n && t->cdf[idx + 1] - t->cdf[idx] == 0) idx++;
+    float y = (sy - t->cdf[idx]) / (t->cdf[idx + 1] - t->cdf[idx]);
+    float a = safe_sqrt(1.0f - sx);
+    float bx = 1 - a, by = a * y;
+    const float *q = s->emit + 9 * (size_t)idx;
+    v3 p0 = ld3(q), sideA = sub(ld3(q + 3), p0), sideB = sub(ld3(q + 6), p0);
+    v3 p = add(add(p0, scl(sideA, bx)), scl(sideB, by));
+    v3 nn = nrm(cross(sideA, sideB));
+    for (int i = 0; i < 3; i++) power[i] = (s->emit_radiance[i] * (float)M_PI) * t->area;
+    v3 l = cosine_hemisphere(dx, dy), fs, ft;
+    frame_of(nn, &fs, &ft);
+    *dir = add(add(scl(fs, l.x), scl(ft, l.y)), scl(nn, l.z));
+    return p;
+}
+
+static void trace_particle(const alvrl_o_scene *s, const alvrl_o_medium *m, const area_table *at,
+                           seq_sampler *smp, int short_vrls, int max_depth, int rr_depth, vrl_sink *k)
 {
     /* sampleEmitterPosition (scene.cpp:958-974) + PointEmitter::samplePosition (point.cpp:81-89) */
-    (void)seq_next(smp); (void)seq_next(smp);
+    float sx = seq_next(smp), sy = seq_next(smp);
     float power[3];
-    for (int i = 0; i < 3; i++) power[i] = s->light_intensity[i] * (float)(4 * M_PI);
     /* PointEmitter::sampleDirection (point.cpp:99-106) */
     float dx = seq_next(smp), dy = seq_next(smp);
-    v3 dir = uniform_sphere(dx, dy);
+    v3 dir, o;
+    if (at) {
+        o = area_emission(s, at, sx, sy, dx, dy, &dir, power);
+    } else {
+        for (int i = 0; i < 3; i++) power[i] = s->light_intensity[i] * (float)(4 * M_PI);
+        dir = uniform_sphere(dx, dy);
+        o = ld3(s->light_pos);
+    }
     if (power[0] == 0 && power[1] == 0 && power[2] == 0) return;
     /* handleEmission: m_vrls->nextParticle() is counted by the caller */
-    v3 o = ld3(s->light_pos);
     k->start = o;
     for (int i = 0; i < 3; i++) k->power[i] = power[i];
 
@@ -1377,14 +1437,18 @@ uint32_t alvrl_o_trace_vrls(const alvrl_o_scene *s, const alvrl_o_medium *m, uin
     memset(&k, 0, sizeof(k));
     k.soa = vrl_soa; k.cap = cap; k.n = 0;
     k.sigma_s_zero = (m->sigma_s[0] == 0 && m->sigma_s[1] == 0 && m->sigma_s[2] == 0);
+    area_table at;
+    memset(&at, 0, sizeof(at));
+    if (s->emit && s->nemit) area_table_init(&at, s->emit, s->nemit);
     uint64_t p = 0;
     while (k.n < target && k.n < cap) {
         seq_sampler smp;
         seq_init(&smp, seed, pass, ALVRL_O_DOM_TRACER, (uint32_t)p, (uint32_t)(p >> 32), 0);
-        p++;   /* handleEmission -> nextParticle() (the point light always emits) */
-        trace_particle(s, m, &smp, short_vrls, max_depth, rr_depth, &k);
+        p++;   /* handleEmission -> nextParticle() (the light always emits) */
+        trace_particle(s, m, at.cdf ? &at : NULL, &smp, short_vrls, max_depth, rr_depth, &k);
         if (k.sigma_s_zero && p > 1000000) break;
     }
+    free(at.cdf);
     if (particles) *particles = p;
     return k.n;
 }

@@ -155,6 +155,12 @@ typedef struct {
     const uint32_t *occ_mat; /* per triangle ALVRL_O_MAT_* (NULL: all diffuse) */
     float occ_spec[3];       /* the mirrors' specular reflectance */
     float occ_eta;           /* the dielectrics' intIOR / extIOR (dielectric.cpp:149-158) */
+    /* area emitter replacing the point light when nemit > 0 (area.cpp on a
+     * triangle mesh): triangles (9 floats), radiance on the side of
+     * cross(p1 - p0, p2 - p0) */
+    const float *emit;
+    uint32_t nemit;
+    float emit_radiance[3];
 } alvrl_o_scene;
 #define ALVRL_O_MAT_DIFFUSE 0u   /* SmoothDiffuse, one-sided (diffuse.cpp) */
 #define ALVRL_O_MAT_MIRROR 1u    /* SmoothConductor, material none (conductor.cpp:254-268) */

@@ -52,10 +52,23 @@ class Scene(C.Structure):
                 ("box_min", C.c_float * 3), ("box_max", C.c_float * 3), ("albedo", C.c_float * 3),
                 ("light_pos", C.c_float * 3), ("light_intensity", C.c_float * 3),
                 ("occ", C.POINTER(C.c_float)), ("nocc", C.c_uint32), ("occ_albedo", C.c_float * 3),
-                ("occ_mat", C.POINTER(C.c_uint32)), ("occ_spec", C.c_float * 3), ("occ_eta", C.c_float)]
+                ("occ_mat", C.POINTER(C.c_uint32)), ("occ_spec", C.c_float * 3), ("occ_eta", C.c_float),
+                ("emit", C.POINTER(C.c_float)), ("nemit", C.c_uint32), ("emit_radiance", C.c_float * 3)]
 
 
 MAT_DIFFUSE, MAT_MIRROR, MAT_NULL, MAT_DIELECTRIC = 0, 1, 2, 3
+
+
+def set_area_emitter(scene, tris, radiance):
+    """An area emitter replacing the point light ((n, 9) float32 triangles,
+    radiance on the side of cross(p1 - p0, p2 - p0)); kept alive on the Scene."""
+    arr = np.ascontiguousarray(np.asarray(tris, np.float32).reshape(-1, 9))
+    scene._emit_keep = arr
+    scene.emit = arr.ctypes.data_as(C.POINTER(C.c_float)) if len(arr) else None
+    scene.nemit = len(arr)
+    for i in range(3):
+        scene.emit_radiance[i] = float(radiance[i])
+    return scene
 
 
 def set_occluders(obj, tris, albedo=None, material=None, specular=None, eta=None):

@@ -380,6 +380,8 @@ public:
     unsigned int getType() const;
     virtual Spectrum samplePosition(PositionSamplingRecord &pRec, const Point2 &sample,
                                     const Point2 *extra = NULL) const = 0;
+    /* render/emitter.h: the spatial part of the emitted radiance */
+    virtual Spectrum evalPosition(const PositionSamplingRecord &pRec) const;
 };
 
 class Shape : public ConfigurableObject {
@@ -389,6 +391,9 @@ public:
     virtual void samplePosition(PositionSamplingRecord &pRec, const Point2 &sample) const;
     virtual ref<TriMesh> createTriMesh();
     const BSDF *getBSDF() const;
+    /* render/shape.h: the attached area emitter */
+    bool isEmitter() const;
+    const Emitter *getEmitter() const;
     const Medium *getInteriorMedium() const;
     const Medium *getExteriorMedium() const;
     virtual std::string getName() const;
