@@ -598,16 +598,18 @@ def unconditional_parity(cfg, vrls, pc, pass_, fast_frame, device=0, row_stride=
     return out
 
 
-def records_mode(cfg, vrls, pc, pass0, device=0, steps=2, block=32, threads=16):
+def records_mode(cfg, vrls, pc, pass0, device=0, steps=2, blocks=(128, 32), threads=16):
     """The host-cast ABI the Mitsuba plugin's records mode drives
     (include/alvrl_host.h "host-cast scenes"), timed per pass:
     the host hands the representative pixels' eye records to
     alvrl_integrator_prepass_records (R, clusters) and renders the frame in
-    32x32 blocks from `threads` host threads, one alvrl_gather_clustered_host
+    image blocks from `threads` host threads, one alvrl_gather_clustered_host
     call per block with host-memory records and results (renderBlock,
-    renderproc.cpp:52-86) -- every record crosses PCIe.  The host here plays
-    Mitsuba with the library's own scene (the smoke box has no null surfaces,
-    so buildSlices' gather point of a pixel is its eye record's hit)."""
+    renderproc.cpp:52-86) -- every record crosses PCIe.  Block sizes: 128
+    (`mitsuba -b 128`, the largest mitsuba.cpp:233-237 accepts) and the
+    default 32.  The host here plays Mitsuba with the library's own scene (the
+    smoke box has no null surfaces, so buildSlices' gather point of a pixel is
+    its eye record's hit)."""
     import numpy as np
     import alvrl
     from concurrent.futures import ThreadPoolExecutor
@@ -622,39 +624,51 @@ def records_mode(cfg, vrls, pc, pass0, device=0, steps=2, block=32, threads=16):
     p2s = it.slices()
     allpix = np.arange(W * H, dtype=np.uint32)
     sl_all = p2s[(allpix % W) * H + allpix // W]
-    blocks = []
-    for by in range(0, H, block):
-        for bx in range(0, W, block):
-            ids = (np.arange(by, min(by + block, H))[:, None] * W + np.arange(bx, min(bx + block, W))[None, :])
-            ids = ids.ravel().astype(np.uint32)
-            blocks.append((np.ascontiguousarray(recs[ids]), np.ascontiguousarray(sl_all[ids]), ids))
     frame = np.zeros((W * H, 3), np.float32)
+    out = {"unit": "VRL contributions/s", "steps": steps, "host_threads": threads,
+           "note": "host-pointer ABI (records and results cross PCIe), renderBlock-sized calls from "
+                   "concurrent host threads; not the metric's value", "by_block": {}}
+    p = pass0
+    for block in blocks:
+        bl = []
+        for by in range(0, H, block):
+            for bx in range(0, W, block):
+                ids = (np.arange(by, min(by + block, H))[:, None] * W + np.arange(bx, min(bx + block, W))[None, :])
+                ids = ids.ravel().astype(np.uint32)
+                bl.append((np.ascontiguousarray(recs[ids]), np.ascontiguousarray(sl_all[ids]), ids))
 
-    def render_block(b):
-        r, sl, ids = b
-        frame[ids] = ctx.gather_clustered_host(r, sl, ids=ids)
+        def render_block(b):
+            r, sl, ids = b
+            frame[ids] = ctx.gather_clustered_host(r, sl, ids=ids)
 
-    def one_pass(p):
-        pix = it.rep_pixels(p)
-        it.prepass_records(p, recs[pix], np.arange(len(pix), dtype=np.uint32))
-        t = time.perf_counter()
-        with ThreadPoolExecutor(threads) as ex:
-            list(ex.map(render_block, blocks))
-        return time.perf_counter() - t
+        def one_pass(q):
+            pix = it.rep_pixels(q)
+            it.prepass_records(q, recs[pix], np.arange(len(pix), dtype=np.uint32))
+            t = time.perf_counter()
+            with ThreadPoolExecutor(threads) as ex:
+                list(ex.map(render_block, bl))
+            return time.perf_counter() - t
 
-    one_pass(pass0)                                      # warm-up
-    s0 = it.stats()
-    t0 = time.perf_counter()
-    render_s = sum(one_pass(pass0 + 1 + i) for i in range(steps))
-    dt = time.perf_counter() - t0
-    s1 = it.stats()
-    pairs = (s1["contrib_preprocess"] - s0["contrib_preprocess"]) + (s1["contrib_render"] - s0["contrib_render"])
+        one_pass(p)                                      # warm-up
+        p += 1
+        s0 = it.stats()
+        hb0 = ctx.host_batch_stats()["clustered"]
+        t0 = time.perf_counter()
+        render_s = 0.0
+        for _ in range(steps):
+            render_s += one_pass(p)
+            p += 1
+        dt = time.perf_counter() - t0
+        s1 = it.stats()
+        pairs = (s1["contrib_preprocess"] - s0["contrib_preprocess"]) + (s1["contrib_render"] - s0["contrib_render"])
+        hb1 = ctx.host_batch_stats()["clustered"]
+        out["by_block"][str(block)] = {"value": pairs / dt, "ms_per_step": dt / steps * 1e3,
+                                       "render_ms_per_step": render_s / steps * 1e3, "blocks": len(bl),
+                                       "launches_per_step": (hb1[0] - hb0[0]) / steps}
     it.close()
-    return {"value": pairs / dt, "unit": "VRL contributions/s", "steps": steps, "ms_per_step": dt / steps * 1e3,
-            "render_ms_per_step": render_s / steps * 1e3, "blocks": len(blocks), "block": block,
-            "host_threads": threads,
-            "note": "host-pointer ABI (records and results cross PCIe), renderBlock-sized calls from "
-                    "concurrent host threads; not the metric's value"}
+    best = out["by_block"][str(blocks[0])]
+    out.update(value=best["value"], ms_per_step=best["ms_per_step"], block=blocks[0])
+    return out
 
 
 def cpu_threads():

@@ -330,12 +330,20 @@ ALVRL_API int alvrl_reset_stats(alvrl_ctx *ctx);
 
 /* ---- host-pointer conveniences for the Mitsuba shim's renderBlock ----- */
 /* Same as alvrl_gather_brute / alvrl_gather_clustered with host arrays;
- * slice_of_rec may be unsorted (UINT32_MAX = fall-back).  Blocking. */
+ * slice_of_rec may be unsorted (UINT32_MAX = fall-back).  Blocking.
+ * Calls from several threads are merged: one caller stages every request
+ * queued so far in pinned memory and runs them as one launch (a record's
+ * result is the same bits in any batch); rec_ids NULL keys a record's streams
+ * by its index in its own call.  alvrl_last_kernel_ms of a thread whose
+ * request another thread launched is not updated. */
 ALVRL_API int alvrl_gather_brute_host(alvrl_ctx *ctx, const alvrl_gather_rec *recs,
                                       const uint32_t *rec_ids, uint32_t nrec, float *out_rgb);
 ALVRL_API int alvrl_gather_clustered_host(alvrl_ctx *ctx, const alvrl_gather_rec *recs,
                                           const uint32_t *rec_ids, const uint32_t *slice_of_rec,
                                           uint32_t nrec, float *out_rgb);
+/* Diagnostic: launches of the host-pointer gathers and the requests they
+ * carried, [0] brute, [1] clustered, since the context was created. */
+ALVRL_API int alvrl_host_batch_stats(alvrl_ctx *ctx, uint64_t batches[2], uint64_t requests[2]);
 
 /* ---- timing of the last kernel launched on the context (HIP events) --- */
 /* Milliseconds between the begin/end events recorded around the most recent

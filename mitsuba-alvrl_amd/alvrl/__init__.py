@@ -110,6 +110,7 @@ def lib() -> C.CDLL:
     L.alvrl_nonzero_columns.argtypes = [vp, vp, u64, u32, vp, vp]
     L.alvrl_accumulate_rgb.argtypes = [vp, vp, vp, u32, vp, vp]
     L.alvrl_set_strict_rbuild.argtypes = [vp, i32]
+    L.alvrl_host_batch_stats.argtypes = [vp, P(u64), P(u64)]
     L.alvrl_detmath_eval.argtypes = [i32, vp, vp, u32, vp]
     _lib = L
     return L
@@ -286,6 +287,13 @@ class Context:
 
     def set_rsamples(self, n: int):
         _check(self.L.alvrl_set_rsamples(self.h, n))
+
+    def host_batch_stats(self) -> dict:
+        """Launches of the host-pointer gathers and the requests they carried
+        (concurrent calls are merged, alvrl_host_batch_stats)."""
+        b = (C.c_uint64 * 2)(); r = (C.c_uint64 * 2)()
+        _check(self.L.alvrl_host_batch_stats(self.h, b, r))
+        return {"brute": (int(b[0]), int(r[0])), "clustered": (int(b[1]), int(r[1]))}
 
     def set_strict_rbuild(self, on: bool = True):
         """The R build in the oracle's arithmetic (alvrl_set_strict_rbuild): R

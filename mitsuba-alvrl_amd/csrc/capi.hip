@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <condition_variable>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -127,6 +128,31 @@ struct ThreadSlot {
     }
 };
 
+// Host-pointer gathers (alvrl_gather_*_host) called concurrently are merged:
+// the first caller leads one launch over every request queued by then and
+// hands the lead to a waiting caller, so renderBlock-sized calls from many
+// worker threads (renderproc.cpp:52-86) fill the device instead of queueing
+// small launches behind the process's few hardware queues.
+struct HostReq {
+    const alvrl_gather_rec* recs;
+    const uint32_t* ids;      // nullptr: the record's index in its own call
+    const uint32_t* sl;       // clustered: slice per record
+    uint32_t n;
+    float* out;
+    int rc = ALVRL_OK;
+    std::string err;
+    bool done = false;
+};
+struct HostBatcher {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::vector<HostReq*> pending[2];   // [0] brute, [1] clustered
+    bool leading[2] = {false, false};
+    char* pin[2] = {nullptr, nullptr};  // the leader's pinned staging, per kind
+    size_t pin_cap[2] = {0, 0};
+    unsigned long long batches[2] = {0, 0}, requests[2] = {0, 0};
+};
+
 struct alvrl_ctx {
     alvrl_config cfg;
     DevParams P;
@@ -162,6 +188,7 @@ struct alvrl_ctx {
     std::shared_mutex state_mu;
     std::mutex slots_mu;
     std::unordered_map<std::thread::id, std::unique_ptr<ThreadSlot>> slots;
+    HostBatcher hb;
 };
 
 // the calling thread's slot (created on first use)
@@ -299,6 +326,8 @@ ALVRL_API void alvrl_ctx_destroy(alvrl_ctx* c)
     free_clusters(c);
     free_occluders(c);
     c->refine_arenas.release();
+    for (int k = 0; k < 2; k++)
+        if (c->hb.pin[k]) (void)hipHostFree(c->hb.pin[k]);
     c->slots.clear();
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
@@ -779,6 +808,137 @@ static size_t carve(size_t* at, size_t bytes)
     return o;
 }
 
+// One launch over a batch of host-pointer requests (kind 0 brute, 1
+// clustered): records staged in pinned memory, for the clustered gather
+// bucketed by slice (stable) into wave work items, results scattered back.
+// A record's result depends on its own record, stream id and list only, so a
+// batch gives every request the bits it would get alone.
+static int run_host_batch(alvrl_ctx* c, int kind, const std::vector<HostReq*>& batch, std::string* err)
+{
+    size_t n = 0;
+    for (const HostReq* r : batch) n += r->n;
+    if (n > 0xFFFFFFFFull) { *err = "host gather batch: more than 2^32 records"; return ALVRL_ERR_INVALID; }
+    const uint32_t nrec = (uint32_t)n;
+    HostBatcher& B = c->hb;
+    size_t at = 0;
+    const size_t h_r = carve(&at, sizeof(alvrl_gather_rec) * nrec);
+    const size_t h_i = carve(&at, sizeof(uint32_t) * nrec);
+    const size_t h_t = carve(&at, kind ? sizeof(alvrl_work_item) * nrec : 0);
+    const size_t h_o = carve(&at, sizeof(float) * 3 * nrec);
+    if (at > B.pin_cap[kind]) {
+        if (B.pin[kind]) (void)hipHostFree(B.pin[kind]);
+        B.pin[kind] = nullptr;
+        B.pin_cap[kind] = 0;
+        const size_t want = at + at / 2;
+        if (hipHostMalloc(&B.pin[kind], want, hipHostMallocDefault) != hipSuccess) {
+            *err = "host gather: pinned staging";
+            return ALVRL_ERR_NOMEM;
+        }
+        B.pin_cap[kind] = want;
+    }
+    auto* r2 = reinterpret_cast<alvrl_gather_rec*>(B.pin[kind] + h_r);
+    auto* id2 = reinterpret_cast<uint32_t*>(B.pin[kind] + h_i);
+    auto* items = reinterpret_cast<alvrl_work_item*>(B.pin[kind] + h_t);
+    auto* o2 = reinterpret_cast<float*>(B.pin[kind] + h_o);
+    // (request, index) of every staged record
+    std::vector<std::pair<uint32_t, uint32_t>> src(nrec);
+    {
+        uint32_t g = 0;
+        for (uint32_t q = 0; q < (uint32_t)batch.size(); q++)
+            for (uint32_t i = 0; i < batch[q]->n; i++) src[g++] = {q, i};
+    }
+    if (kind) {
+        std::stable_sort(src.begin(), src.end(), [&](const std::pair<uint32_t, uint32_t>& a,
+                                                     const std::pair<uint32_t, uint32_t>& b) {
+            return batch[a.first]->sl[a.second] < batch[b.first]->sl[b.second];
+        });
+    }
+    std::vector<uint32_t> sl2(kind ? nrec : 0);
+    for (uint32_t g = 0; g < nrec; g++) {
+        const HostReq* q = batch[src[g].first];
+        const uint32_t i = src[g].second;
+        r2[g] = q->recs[i];
+        id2[g] = q->ids ? q->ids[i] : i;
+        if (kind) sl2[g] = q->sl[i];
+    }
+    const uint32_t nit = kind ? alvrl_make_work_items(sl2.data(), nrec, items, nrec) : 0;
+    hipError_t e = hipSetDevice(c->cfg.device);
+    ThreadSlot* ts = e == hipSuccess ? slot_of(c, &e) : nullptr;
+    if (!ts) { *err = std::string("per-thread stream: ") + hipGetErrorString(e); return ALVRL_ERR_HIP; }
+    at = 0;
+    const size_t o_r = carve(&at, sizeof(alvrl_gather_rec) * nrec);
+    const size_t o_i = carve(&at, sizeof(uint32_t) * nrec);
+    const size_t o_o = carve(&at, sizeof(float) * 3 * nrec);
+    const size_t o_t = carve(&at, sizeof(alvrl_work_item) * nit);
+    e = ts->need(at);
+    hipStream_t s = ts->stream;
+    auto* dr = reinterpret_cast<alvrl_gather_rec*>(ts->scratch + o_r);
+    auto* di = reinterpret_cast<uint32_t*>(ts->scratch + o_i);
+    auto* dout = reinterpret_cast<float*>(ts->scratch + o_o);
+    auto* dit = reinterpret_cast<alvrl_work_item*>(ts->scratch + o_t);
+    if (e == hipSuccess) e = hipMemcpyAsync(dr, r2, sizeof(alvrl_gather_rec) * nrec, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(di, id2, sizeof(uint32_t) * nrec, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess && kind)
+        e = hipMemcpyAsync(dit, items, sizeof(alvrl_work_item) * nit, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipEventRecord(ts->ev0, s);
+    if (e == hipSuccess) {
+        if (kind) {
+            const float inv_pc = 1.0f / (float)c->particle_count;   // Li /= getParticleCount() (:590)
+            e = launch_gather_clustered(reinterpret_cast<const Rec*>(dr), di, reinterpret_cast<const WorkItem*>(dit),
+                                        nit, c->d_vrl, c->d_slice_off, c->d_reps, c->d_weights, c->d_fb_reps,
+                                        c->d_fb_w, c->n_fb, c->P, inv_pc, dout, c->d_counter + 1, s);
+        } else {
+            const float norm = (float)(1.0 / (double)c->particle_count);   // :805
+            e = launch_gather_brute(reinterpret_cast<const Rec*>(dr), di, nrec, c->d_vrl, c->nvrl, c->P, norm, dout,
+                                    c->d_counter + 1, s);
+        }
+    }
+    if (e == hipSuccess) e = hipEventRecord(ts->ev1, s);
+    if (e == hipSuccess) ts->timed = true;
+    if (e == hipSuccess) e = hipMemcpyAsync(o2, dout, sizeof(float) * 3 * nrec, hipMemcpyDeviceToHost, s);
+    const hipError_t e2 = hipStreamSynchronize(s);
+    if (e == hipSuccess) e = e2;
+    if (e != hipSuccess) {
+        *err = std::string(kind ? "alvrl_gather_clustered_host: " : "alvrl_gather_brute_host: ") + hipGetErrorString(e);
+        return ALVRL_ERR_HIP;
+    }
+    for (uint32_t g = 0; g < nrec; g++) {
+        float* o = batch[src[g].first]->out + 3 * (size_t)src[g].second;
+        o[0] = o2[3 * (size_t)g]; o[1] = o2[3 * (size_t)g + 1]; o[2] = o2[3 * (size_t)g + 2];
+    }
+    B.batches[kind]++;
+    B.requests[kind] += batch.size();
+    return ALVRL_OK;
+}
+
+// Queue the request; the caller that finds no leader leads one batch (every
+// request queued by then, its own included) and, with its own result in
+// hand, hands the lead on to a waiting caller.
+static int host_gather(alvrl_ctx* c, int kind, HostReq* req)
+{
+    HostBatcher& B = c->hb;
+    std::unique_lock<std::mutex> lk(B.mu);
+    B.pending[kind].push_back(req);
+    while (!req->done) {
+        if (B.leading[kind]) {
+            B.cv.wait(lk, [&] { return req->done || !B.leading[kind]; });
+            continue;
+        }
+        B.leading[kind] = true;
+        std::vector<HostReq*> batch;
+        batch.swap(B.pending[kind]);
+        lk.unlock();
+        std::string err;
+        const int rc = run_host_batch(c, kind, batch, &err);
+        lk.lock();
+        for (HostReq* r : batch) { r->rc = rc; r->err = err; r->done = true; }
+        B.leading[kind] = false;
+        B.cv.notify_all();
+    }
+    if (req->rc != ALVRL_OK) return fail(req->rc, req->err);
+    return ALVRL_OK;
+}
+
 ALVRL_API int alvrl_gather_brute_host(alvrl_ctx* c, const alvrl_gather_rec* recs, const uint32_t* ids,
                                       uint32_t nrec, float* out)
 {
@@ -787,32 +947,8 @@ ALVRL_API int alvrl_gather_brute_host(alvrl_ctx* c, const alvrl_gather_rec* recs
     if (rc) return rc;
     if (nrec == 0) return ALVRL_OK;
     if (!recs || !out) return fail(ALVRL_ERR_INVALID, "alvrl_gather_brute_host: null buffer");
-    HIPCHK(hipSetDevice(c->cfg.device));
-    SLOT(c, ts);
-    size_t at = 0;
-    const size_t o_r = carve(&at, sizeof(alvrl_gather_rec) * nrec);
-    const size_t o_i = carve(&at, ids ? sizeof(uint32_t) * nrec : 0);
-    const size_t o_o = carve(&at, sizeof(float) * 3 * nrec);
-    HIPCHK(ts->need(at));
-    hipStream_t s = ts->stream;
-    auto* dr = reinterpret_cast<alvrl_gather_rec*>(ts->scratch + o_r);
-    uint32_t* di = ids ? reinterpret_cast<uint32_t*>(ts->scratch + o_i) : nullptr;
-    float* dout = reinterpret_cast<float*>(ts->scratch + o_o);
-    hipError_t e = hipMemcpyAsync(dr, recs, sizeof(alvrl_gather_rec) * nrec, hipMemcpyHostToDevice, s);
-    if (e == hipSuccess && ids) e = hipMemcpyAsync(di, ids, sizeof(uint32_t) * nrec, hipMemcpyHostToDevice, s);
-    if (e == hipSuccess) e = hipEventRecord(ts->ev0, s);
-    if (e == hipSuccess) {
-        const float norm = (float)(1.0 / (double)c->particle_count);
-        e = launch_gather_brute(reinterpret_cast<const Rec*>(dr), di, nrec, c->d_vrl, c->nvrl, c->P,
-                                norm, dout, c->d_counter + 1, s);
-    }
-    if (e == hipSuccess) e = hipEventRecord(ts->ev1, s);
-    if (e == hipSuccess) ts->timed = true;
-    if (e == hipSuccess) e = hipMemcpyAsync(out, dout, sizeof(float) * 3 * nrec, hipMemcpyDeviceToHost, s);
-    hipError_t e2 = hipStreamSynchronize(s);
-    if (e == hipSuccess) e = e2;
-    if (e != hipSuccess) return fail(ALVRL_ERR_HIP, std::string("alvrl_gather_brute_host: ") + hipGetErrorString(e));
-    return ALVRL_OK;
+    HostReq req{recs, ids, nullptr, nrec, out};
+    return host_gather(c, 0, &req);
 }
 
 ALVRL_API int alvrl_gather_clustered_host(alvrl_ctx* c, const alvrl_gather_rec* recs,
@@ -828,54 +964,17 @@ ALVRL_API int alvrl_gather_clustered_host(alvrl_ctx* c, const alvrl_gather_rec* 
     for (uint32_t i = 0; i < nrec; i++)
         if (slice_of_rec[i] != 0xFFFFFFFFu && slice_of_rec[i] >= c->nslices)
             return fail(ALVRL_ERR_INVALID, "alvrl_gather_clustered_host: slice out of range");
-    // bucket records by slice (stable), build wave work items
-    std::vector<uint32_t> perm(nrec);
-    for (uint32_t i = 0; i < nrec; i++) perm[i] = i;
-    std::stable_sort(perm.begin(), perm.end(), [&](uint32_t a, uint32_t b) {
-        return slice_of_rec[a] < slice_of_rec[b];
-    });
-    std::vector<alvrl_gather_rec> r2(nrec);
-    std::vector<uint32_t> id2(nrec), sl2(nrec);
-    for (uint32_t i = 0; i < nrec; i++) {
-        r2[i] = recs[perm[i]];
-        id2[i] = ids ? ids[perm[i]] : perm[i];
-        sl2[i] = slice_of_rec[perm[i]];
-    }
-    std::vector<alvrl_work_item> items(nrec);
-    const uint32_t nit = alvrl_make_work_items(sl2.data(), nrec, items.data(), nrec);
-    HIPCHK(hipSetDevice(c->cfg.device));
-    SLOT(c, ts);
-    size_t at = 0;
-    const size_t o_r = carve(&at, sizeof(alvrl_gather_rec) * nrec);
-    const size_t o_i = carve(&at, sizeof(uint32_t) * nrec);
-    const size_t o_o = carve(&at, sizeof(float) * 3 * nrec);
-    const size_t o_t = carve(&at, sizeof(alvrl_work_item) * nit);
-    HIPCHK(ts->need(at));
-    hipStream_t s = ts->stream;
-    auto* dr = reinterpret_cast<alvrl_gather_rec*>(ts->scratch + o_r);
-    auto* di = reinterpret_cast<uint32_t*>(ts->scratch + o_i);
-    auto* dout = reinterpret_cast<float*>(ts->scratch + o_o);
-    auto* dit = reinterpret_cast<alvrl_work_item*>(ts->scratch + o_t);
-    hipError_t e = hipMemcpyAsync(dr, r2.data(), sizeof(alvrl_gather_rec) * nrec, hipMemcpyHostToDevice, s);
-    if (e == hipSuccess) e = hipMemcpyAsync(di, id2.data(), sizeof(uint32_t) * nrec, hipMemcpyHostToDevice, s);
-    if (e == hipSuccess) e = hipMemcpyAsync(dit, items.data(), sizeof(alvrl_work_item) * nit, hipMemcpyHostToDevice, s);
-    std::vector<float> o2(3 * (size_t)nrec);
-    if (e == hipSuccess) e = hipEventRecord(ts->ev0, s);
-    if (e == hipSuccess) {
-        const float inv_pc = 1.0f / (float)c->particle_count;
-        e = launch_gather_clustered(reinterpret_cast<const Rec*>(dr), di,
-                                    reinterpret_cast<const WorkItem*>(dit), nit, c->d_vrl,
-                                    c->d_slice_off, c->d_reps, c->d_weights, c->d_fb_reps, c->d_fb_w,
-                                    c->n_fb, c->P, inv_pc, dout, c->d_counter + 1, s);
-    }
-    if (e == hipSuccess) e = hipEventRecord(ts->ev1, s);
-    if (e == hipSuccess) ts->timed = true;
-    if (e == hipSuccess) e = hipMemcpyAsync(o2.data(), dout, sizeof(float) * 3 * nrec, hipMemcpyDeviceToHost, s);
-    hipError_t e2 = hipStreamSynchronize(s);
-    if (e == hipSuccess) e = e2;
-    if (e != hipSuccess) return fail(ALVRL_ERR_HIP, std::string("alvrl_gather_clustered_host: ") + hipGetErrorString(e));
-    for (uint32_t i = 0; i < nrec; i++)
-        for (int ch = 0; ch < 3; ch++) out[3 * (size_t)perm[i] + ch] = o2[3 * (size_t)i + ch];
+    HostReq req{recs, ids, slice_of_rec, nrec, out};
+    return host_gather(c, 1, &req);
+}
+
+/* diagnostic: host-pointer gather launches and the requests they carried */
+ALVRL_API int alvrl_host_batch_stats(alvrl_ctx* c, uint64_t* batches, uint64_t* requests)
+{
+    if (!c || !batches || !requests) return fail(ALVRL_ERR_INVALID, "alvrl_host_batch_stats: null argument");
+    std::lock_guard<std::mutex> g(c->hb.mu);
+    batches[0] = c->hb.batches[0]; batches[1] = c->hb.batches[1];
+    requests[0] = c->hb.requests[0]; requests[1] = c->hb.requests[1];
     return ALVRL_OK;
 }
 

@@ -9,7 +9,9 @@ thread gets its own stream and device scratch (csrc/capi.hip ThreadSlot).
   * 8 host threads render a frame block by block through
     alvrl_gather_clustered_host / alvrl_gather_brute_host; the assembled frame
     equals the one-call frame bit for bit (every pixel's sum depends only on
-    its record, id and slice list);
+    its record, id and slice list), and the concurrent calls were merged into
+    fewer launches (the library's host-gather batching), also for calls
+    without record ids;
   * alvrl_set_clusters right after a gather launched on a caller's stream:
     the gather still sees the lists it was launched with (set_clusters waits
     for it, alvrl.h).
@@ -81,6 +83,24 @@ def test_concurrent_block_gathers(gpu_ok, mode):
         t_blocks = time.perf_counter() - t0
         assert np.array_equal(frame.view(np.uint32), whole.view(np.uint32)), rep
     assert whole.any()
+    # concurrent calls were merged into fewer launches (csrc/capi.hip host_gather)
+    nb, nr = ctx.host_batch_stats()[mode]
+    assert nr == 1 + 2 * len(blocks) and nb < nr, (nb, nr)
+    print(f"{mode}: {nr} requests in {nb} launches")
+    # without ids a record's streams are keyed by its index in its own call,
+    # also when its call is merged with others
+    sub = [b[:300] for b in blocks[:24]]
+
+    def gather_noid(ids):
+        if mode == "clustered":
+            return ctx.gather_clustered_host(recs[ids], sl[ids])
+        return ctx.gather_brute_host(recs[ids])
+
+    alone = [gather_noid(ids) for ids in sub]
+    with ThreadPoolExecutor(max_workers=8) as ex:
+        merged = list(ex.map(gather_noid, sub))
+    for a, m in zip(alone, merged):
+        assert np.array_equal(a.view(np.uint32), m.view(np.uint32))
     print(f"{mode}: {len(blocks)} blocks of 32x32 on 8 threads {t_blocks * 1e3:.1f} ms, "
           f"one call {t_whole * 1e3:.1f} ms")
 
