@@ -8,6 +8,6 @@ name=$1; shift
 mkdir -p variants
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -Wno-unused-value \
   -I../include -ffp-contract=off "$@" -c csrc/refine.hip -o /tmp/refine_$name.o
-objs=$(ls build/*.o | grep -v '/refine.o$')
+objs=$(ls build/*.o | grep -v '/refine.o$' | grep -v '/asan_')
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o variants/libalvrl_$name.so /tmp/refine_$name.o $objs -lpthread
 echo "variants/libalvrl_$name.so"

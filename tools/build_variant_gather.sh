@@ -9,6 +9,6 @@ name=$1; shift
 mkdir -p variants
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -Wno-unused-value \
   -I../include -fno-hip-fp32-correctly-rounded-divide-sqrt -fgpu-flush-denormals-to-zero "$@" -c csrc/gather.hip -o /tmp/gather_$name.o
-objs=$(ls build/*.o | grep -v '/gather.o$')
+objs=$(ls build/*.o | grep -v '/gather.o$' | grep -v '/asan_')
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o variants/libalvrl_$name.so /tmp/gather_$name.o $objs -lpthread
 echo "variants/libalvrl_$name.so"
