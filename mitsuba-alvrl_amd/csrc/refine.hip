@@ -32,6 +32,7 @@
 #include <thread>
 #include <cstdlib>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 namespace alvrl {
@@ -195,6 +196,8 @@ struct Common {
     uint32_t nroam;                // roaming helpers (after the teams): serve every job's queue
     int var_v3;                    // split variances on variance_split_v3 (ALVRL_VAR_V3=0: the older engine)
     int var_small;                 // splits of <= kSmallMax columns on variance_split_small (ALVRL_VAR_SMALL=0: off)
+    int split_fused;               // small splits on split_fused: 2 (default) float2 and means-only staging,
+                                   // 1 float2 staging only, 0 off (ALVRL_SPLIT_FUSED)
     int roam_on;                   // finished leaders and helpers roam too (scratch sized for Rmax)
     const SplitWs* roam_ws;        // [nroam] their scratch, sized for the largest job
     const uint32_t* roam_order;    // null: roam from the last job served; else scan jobs in this order
@@ -349,6 +352,7 @@ struct Ctl {
     int heap_n, sh_heap_n, singles_n, sh_singles_n;
     int err;
     uint32_t b, e, vrl1, vrl2, draw_k;
+    uint32_t fi1, fi2;       // split_fused: the two centres' positions in the cluster
     int degenerate;
     float diffLen, nd;
     int go, do_snap, stop, refined;
@@ -2030,6 +2034,7 @@ __device__ __noinline__ void variance_split_small(CJ& J_in, CC& cm_in, Ctl& C, c
 {
     CJ& J = uni(J_in);
     CC& cm = uni(cm_in);
+    m = (uint32_t)__builtin_amdgcn_readfirstlane((int)m);   // uniform: scalar loop and guard branches
     const uint32_t R = J.nrows, NB = (R + 63) / 64;
     const int tid = threadIdx.x, wv = tid >> 6;
     const uint32_t lane = (uint32_t)(tid & 63);
@@ -2115,13 +2120,19 @@ __device__ __noinline__ void variance_split_small(CJ& J_in, CC& cm_in, Ctl& C, c
                 if (c0 + c < m) Q[(((size_t)g * kSmallMax + c0 + c) * 2 + h) * kSmallBlocks + bb] = z;
             }
         };
-        load(0, bufA);
-        for (uint32_t c0 = 0; c0 < m; c0 += 2 * kCH) {
-            if (c0 + kCH < m) load(c0 + kCH, bufB);
-            chunk(c0, bufA);
-            if (c0 + kCH >= m) break;
-            if (c0 + 2 * kCH < m) load(c0 + 2 * kCH, bufA);
-            chunk(c0 + kCH, bufB);
+        // three chunks' entries issued together (clamped: past the end the
+        // last chunk again), then the three chunks.  Loads issued under a
+        // branch, or in flight across the loop's back edge, make the compiler
+        // wait for every load in flight (it cannot match them across paths)
+        const uint32_t nch = (m + kCH - 1) / kCH;
+        float2 bufC[kCH];
+        for (uint32_t k = 0; k < nch; k += 3) {
+            load(k * kCH, bufA);
+            load(min(k + 1, nch - 1) * kCH, bufB);
+            load(min(k + 2, nch - 1) * kCH, bufC);
+            chunk(k * kCH, bufA);
+            if (k + 1 < nch) chunk((k + 1) * kCH, bufB);
+            if (k + 2 < nch) chunk((k + 2) * kCH, bufC);
         }
     }
     __syncthreads();
@@ -2603,6 +2614,486 @@ __device__ ALVRL_PROJ_INL void split_projections(CJ& J_in, CC& cm_in, uint32_t b
 }
 
 
+// The end of a split (:664-684): the argmin over the split position of the
+// four prefix variances pref(k, i) (fsu, fsi of the forward pass, feu, fei of
+// the reverse one), then the two children pushed (commit) or the result
+// written to *res for the leader (sc1 stores, see split()'s range copy).
+template <class Pref>
+__device__ __forceinline__ void split_finish(CJ& J, Ctl& C, uint32_t begin, uint32_t end, bool commit,
+                                             SplitRes* res, Pref pref)
+{
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const uint32_t m = end - begin;
+    auto& Cs = *lp(&C);
+    float bv = INFINITY;
+    uint32_t bi = 0xFFFFFFFFu;
+    for (uint32_t i = 1 + tid; i < m; i += kThreads) {
+        const float v = pref(0, i - 1) + pref(1, i - 1) + pref(2, m - 1 - i) + pref(3, m - 1 - i);
+        if (v < bv) { bv = v; bi = i; }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const float ov = __shfl_down(bv, off, 64);
+        const uint32_t oi = __shfl_down(bi, off, 64);
+        if (lane < off && (ov < bv || (ov == bv && oi < bi))) { bv = ov; bi = oi; }
+    }
+    if (lane == 0) { Cs.best_v[wave] = bv; Cs.best_i[wave] = bi; }
+    __syncthreads();
+    if (tid == 0) {
+        float v = INFINITY;
+        uint32_t idx = 0xFFFFFFFFu;
+        for (int w = 0; w < kWaves; w++)
+            if (Cs.best_v[w] < v || (Cs.best_v[w] == v && Cs.best_i[w] < idx)) { v = Cs.best_v[w]; idx = Cs.best_i[w]; }
+        if (!commit) {
+            SplitRes r{idx, Cs.err | (idx == 0xFFFFFFFFu ? 1 : 0), 0.0f, 0.0f, 0.0f, 0.0f};
+            if (idx != 0xFFFFFFFFu) {
+                r.fsu = pref(0, idx - 1); r.fsi = pref(1, idx - 1);
+                r.feu = pref(2, m - 1 - idx); r.fei = pref(3, m - 1 - idx);
+            }
+            auto* const rw = gpw(reinterpret_cast<uint32_t*>(res));   // sc1 stores, see split()'s range copy
+            const uint32_t* rv = reinterpret_cast<const uint32_t*>(&r);
+#pragma unroll
+            for (int k = 0; k < (int)(sizeof(SplitRes) / 4); k++)
+                __hip_atomic_store(&rw[k], rv[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else if (idx == 0xFFFFFFFFu) {
+            Cs.err = 1;
+        } else {
+            const uint32_t s = begin + idx;
+            add_cluster(J, C, begin, s, pref(0, idx - 1), pref(1, idx - 1));
+            add_cluster(J, C, s, end, pref(2, m - 1 - idx), pref(3, m - 1 - idx));
+        }
+    }
+    __syncthreads();
+}
+
+// ------------------------------------------------------- fused split --
+// A small split whose cluster fits the LDS pool: split() with
+// variance_split_small in one function, every phase from LDS.  One pass over
+// HBM stages the cluster's m x R entries (float2, [cluster position][row]),
+// ids and weights, while wave 0 draws the two centres.  The centres' norms,
+// the direction, the projections, the sort (a rank count over the unique
+// keys: any correct sort gives std::sort's order), both variance passes and
+// the argmin then run without a call or another global round trip; the
+// sorted ids and the result are the only stores.  split() reads the entries
+// three times from HBM, with about ten dependent round trips and four calls
+// per split: the ~50k-cycle floor of a split of a few columns.
+// Every value is formed by the same IEEE operations in the same order as
+// split() with variance_split_small, so the results are bit-identical.
+constexpr uint32_t kFusedMaxRows = 256;
+#ifndef ALVRL_FUSED_KB
+#define ALVRL_FUSED_KB 16   // staging loads in flight per thread
+#endif
+// LDS bytes.  XO = false: coefficients 112m, block totals 128m, then the
+// entries, 8mR (float2).  XO = true (a cluster whose float2 entries do not
+// fit): the entries' means only, 4mR, in the space the coefficients and block
+// totals take once the projections are done; the variance passes stream the
+// entries from global memory (L2-warm: this workgroup just read them).  Then
+// keys 8m, row bases 8R, prefix variances 16m, weights / ids / sorted
+// positions / sorted ids 4m each, direction and row strides 4R each.
+template <bool XO>
+__host__ __device__ constexpr uint32_t fused_base(uint32_t m, uint32_t R)
+{
+    return XO ? (((4u * m * R > 240u * m ? 4u * m * R : 240u * m) + 7u) & ~7u) : 240u * m + 8u * m * R;
+}
+template <bool XO>
+__host__ __device__ constexpr uint32_t fused_bytes(uint32_t m, uint32_t R)
+{
+    return fused_base<XO>(m, R) + 40u * m + 16u * R;
+}
+template <bool XO>
+__device__ __forceinline__ bool fused_fits(uint32_t m, uint32_t R)
+{
+    return m <= kSmallMax && R <= kFusedMaxRows && fused_bytes<XO>(m, R) <= kPoolBytes;
+}
+__device__ __forceinline__ float readlane0_f(float x)
+{
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 0));
+}
+template <bool XO>
+__device__ __noinline__ void split_fused(CJ& J_in, CC& cm_in, Ctl& C, uint32_t begin, uint32_t end,
+                                         unsigned long long* lds, Prof& pf, bool commit, SplitRes* res)
+{
+    CJ& J = uni(J_in);
+    CC& cm = uni(cm_in);
+    // uniform in SGPRs: the loops and guards on m branch on scalars
+    begin = (uint32_t)__builtin_amdgcn_readfirstlane((int)begin);
+    end = (uint32_t)__builtin_amdgcn_readfirstlane((int)end);
+    const int tid = threadIdx.x, wave = tid >> 6;
+    // the phase profile through typed LDS and global accesses: a flat one
+    // (Prof::mark's) makes every later wait of the function a wait for all
+    // loads in flight
+    auto* const pfs = lp(&pf);
+    auto* const pfp = gpw(pfs->p);
+    auto padd = [&](int id, unsigned long long v) {
+        __hip_atomic_fetch_add(&pfp[id], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    auto pmark = [&](int id) {
+        if (pfp && tid == 0) {
+            const long long now = clock64();
+            padd(id, (unsigned long long)(now - pfs->t));
+            if (pfs->sm >= 0 && id >= PF_WSAMP && id <= PF_ARGMIN)
+                padd(kPfSmallAt + pfs->sm * kPfSmallPh + (id - PF_WSAMP), (unsigned long long)(now - pfs->t));
+            pfs->t = now;
+        }
+    };
+    pmark(PF_CTRL);
+    if (pfp && tid == 0) {
+        padd(PF_NSPLIT, 1);
+        padd(PF_SPLITCOLS, end - begin);
+        pfs->sm = end - begin < 64 ? 0 : end - begin < 256 ? 1 : -1;
+    }
+    const long long hb0 = pfs->t;
+    long long hbv = 0, hbp = 0;
+    const uint32_t lane = (uint32_t)(tid & 63);
+    const uint32_t m = end - begin, R = J.nrows, NB = (R + 63) / 64;
+    auto& Cs = *lp(&C);
+    if (!LDS_OK(fused_fits<XO>(m, R), "fused split size", m, R)) return;
+    // register copies of the job's fields (see split())
+    const auto* const vrlsR = gp(J.vrls);
+    auto* const vrlsW = gpw(J.vrls);
+    const auto* const colwR = gp(J.colw);
+    const uint32_t stage = J.stage_refine;
+    const uint32_t seed = cm.seed, pass = cm.pass;
+    const float2* const Rt = cm.Rt;
+    const int contig = J.contig;
+    const unsigned long long off0 = J.off0;
+    const uint32_t stride0 = J.stride0;
+    unsigned char* const pool = reinterpret_cast<unsigned char*>(lds);
+    const uint32_t oE = XO ? 0u : 240u * m, oK = fused_base<XO>(m, R), o4 = oK + 8u * m + 8u * R;
+    auto* const coef = lp(reinterpret_cast<double*>(pool));                                // [g][7][m]
+    auto* const Q = lp(reinterpret_cast<double*>(pool + 112u * m));                        // [g][c][h][block]
+    auto* const Eu = lp(reinterpret_cast<unsigned long long*>(pool + oE));                 // [m][R] (float2 bits; !XO)
+    auto* const Ex = lp(reinterpret_cast<float*>(pool + oE));                              // the means
+    auto xat = [&](uint32_t i) -> float { return Ex[XO ? i : 2u * i]; };                  // mean of element i = c * R + r
+    auto* const keys = lp(reinterpret_cast<unsigned long long*>(pool + oK));               // [m]
+    auto* const rbase = lp(reinterpret_cast<unsigned long long*>(pool + oK + 8u * m));     // [R]
+    auto* const out = lp(reinterpret_cast<float*>(pool + o4));                             // [4][m]
+    float* const wv = reinterpret_cast<float*>(pool + o4 + 16u * m);                       // [m]
+    auto* const ids = lp(reinterpret_cast<uint32_t*>(pool + o4 + 20u * m));                // [m]
+    auto* const spos = lp(reinterpret_cast<uint32_t*>(pool + o4 + 24u * m));               // [m]: sorted -> cluster position
+    auto* const svrl = lp(reinterpret_cast<uint32_t*>(pool + o4 + 28u * m));               // [m]: sorted ids
+    auto* const dir = lp(reinterpret_cast<float*>(pool + o4 + 32u * m));                   // [R]
+    auto* const rstr = lp(reinterpret_cast<uint32_t*>(pool + o4 + 32u * m + 4u * R));      // [R]
+    // this thread's variance row (wave = pass * 4 + row block), its weight in flight from here
+    const int g = wave >> 2;
+    const uint32_t blk = (uint32_t)(wave & 3);
+    const uint32_t vrow = min(blk * 64u + lane, R - 1);
+    const double lw = gp(J.locw)[vrow];
+
+    // ids and weights (:597-602); the row layout of a non-contiguous job
+    if (tid < (int)m) {
+        const uint32_t v = vrlsR[begin + (uint32_t)tid];
+        ids[tid] = v;
+        lp(wv)[tid] = colwR[v];
+    } else if (!contig && tid >= 256 && (uint32_t)tid - 256u < R) {
+        const uint32_t r = (uint32_t)tid - 256u;
+        rbase[r] = gp(J.roff)[r];
+        rstr[r] = gp(J.rstride)[r];
+    }
+    __syncthreads();
+    if (wave == 0) {
+        // the two centres (:597-602), as split()
+        Smp smp;
+        smp.init(seed, pass, begin, end, stage);
+        const WsPick p1 = weighted_sample_wave(wv, nullptr, nullptr, m, smp, 0xFFFFFFFFu, false, true);
+        smp.k = p1.k; smp.blk = 0xFFFFFFFFu;   // the same stream from draw p1.k
+        const WsPick p2 = weighted_sample_wave(wv, nullptr, nullptr, m, smp, p1.idx, false, true);
+        if (lane == 0) {
+            if (p1.err | p2.err) Cs.err = 1;
+            Cs.fi1 = p1.idx; Cs.fi2 = p2.idx;
+            Cs.vrl1 = ids[p1.idx]; Cs.vrl2 = ids[p2.idx]; Cs.draw_k = p2.k;
+        }
+    } else {
+        // the entries on waves 1-7, kCB columns per wave and batch, lanes
+        // over the rows (split_projections' loads).  No guards: rows past R
+        // load and store row R - 1 again, columns past m column m - 1 (the
+        // same values to the same places), so that every load of a batch is
+        // in flight together -- a load under a per-lane branch makes the
+        // compiler wait for every load in flight where the branch rejoins
+        const auto* const R64 = gp(reinterpret_cast<const unsigned long long*>(Rt));
+        size_t rbs[kRB], rss[kRB];
+        uint32_t rcl[kRB];
+#pragma unroll
+        for (int rb = 0; rb < kRB; rb++) {
+            rcl[rb] = min(lane + 64u * rb, R - 1);
+            rbs[rb] = contig ? (size_t)(off0 + rcl[rb]) : (size_t)rbase[rcl[rb]];
+            rss[rb] = contig ? (size_t)stride0 : (size_t)rstr[rcl[rb]];
+        }
+        for (uint32_t j0 = (uint32_t)(wave - 1) * kCB; j0 < m; j0 += (kWaves - 1) * kCB) {
+            uint32_t jc[kCB], v[kCB];
+#pragma unroll
+            for (int q = 0; q < kCB; q++) { jc[q] = min(j0 + (uint32_t)q, m - 1); v[q] = ids[jc[q]]; }
+            unsigned long long x[kRB][kCB];
+#pragma unroll
+            for (int rb = 0; rb < kRB; rb++)
+#pragma unroll
+                for (int q = 0; q < kCB; q++) x[rb][q] = R64[rbs[rb] + (size_t)v[q] * rss[rb]];
+#pragma unroll
+            for (int rb = 0; rb < kRB; rb++)
+#pragma unroll
+                for (int q = 0; q < kCB; q++) {
+                    const uint32_t i = jc[q] * R + rcl[rb];
+                    if (XO) Ex[i] = __uint_as_float((uint32_t)x[rb][q]);
+                    else Eu[i] = x[rb][q];
+                }
+        }
+    }
+    __syncthreads();
+    pmark(PF_WSAMP);
+    // |c1|, |c2|, |c2 - c1| (:607-616) and the direction (:617-624), wave 0
+    if (wave == 0) {
+        const uint32_t i1 = Cs.fi1, i2 = Cs.fi2;
+        float p1 = 0.0f, p2 = 0.0f, pd = 0.0f;
+        for (uint32_t r = lane; r < R; r += 64) {
+            const float a = xat(i1 * R + r), b = xat(i2 * R + r);
+            const float d = b - a;
+            const float ua = fabsf(a), ub = fabsf(b), ud = fabsf(d);
+            p1 = p1 + ua * ua; p2 = p2 + ub * ub; pd = pd + ud * ud;
+        }
+        p1 = tree_f(p1); p2 = tree_f(p2); pd = tree_f(pd);
+        const float n1 = sqrtf(readlane0_f(p1)), n2 = sqrtf(readlane0_f(p2)), dl = sqrtf(readlane0_f(pd));
+        const bool degen = !(n1 != 0 && n2 != 0 && dl != 0);
+        if (lane == 0) {
+            Cs.nrm3[0] = n1; Cs.nrm3[1] = n2; Cs.nrm3[2] = dl;
+            Cs.diffLen = dl; Cs.degenerate = degen;
+        }
+        if (!degen)
+            for (uint32_t r = lane; r < R; r += 64) dir[r] = (xat(i2 * R + r) - xat(i1 * R + r)) / dl;
+    }
+    __syncthreads();
+    if (Cs.degenerate) {
+        // a random direction (:618-621), as split()
+        uint32_t k = Cs.draw_k;
+        while (true) {
+            for (uint32_t r = tid; r < R; r += kThreads) {
+                const float sx = draw_at(seed, pass, begin, end, stage, k + 2 * r);
+                const float sy = draw_at(seed, pass, begin, end, stage, k + 2 * r + 1);
+                dir[r] = det_std_normal_x(sx, sy);
+            }
+            __syncthreads();
+            if (wave == 0) {
+                float p = 0.0f;
+                for (uint32_t r = lane; r < R; r += 64) { const float u = fabsf(dir[r]); p = p + u * u; }
+                p = tree_f(p);
+                if (lane == 0) Cs.nd = sqrtf(p);
+            }
+            __syncthreads();
+            if (Cs.nd != 0) break;
+            k += 2 * R;
+            if (k > Cs.draw_k + 64u * 2u * R) {   // hang guard, as split()
+                if (tid == 0) Cs.err = 1;
+                __syncthreads();
+                break;
+            }
+        }
+        const float nd = Cs.nd != 0 ? Cs.nd : 1.0f;
+        for (uint32_t r = tid; r < R; r += kThreads) dir[r] = dir[r] / nd;
+        __syncthreads();
+    }
+    pmark(PF_DIR);
+    hbp = pfs->t - hb0;
+    // projections (:625-640): split_projections' arithmetic, kCB columns per wave
+    {
+        float d[kRB];
+#pragma unroll
+        for (int rb = 0; rb < kRB; rb++) {
+            const uint32_t r = lane + 64u * rb;
+            d[rb] = r < R ? dir[r] : 0.0f;
+        }
+        for (uint32_t j0 = (uint32_t)wave * kCB; j0 < m; j0 += kWaves * kCB) {
+            uint32_t v[kCB];
+            float x[kRB][kCB];
+#pragma unroll
+            for (int q = 0; q < kCB; q++) {
+                const uint32_t jc = min(j0 + (uint32_t)q, m - 1);
+                v[q] = ids[jc];
+#pragma unroll
+                for (int rb = 0; rb < kRB; rb++) {
+                    const uint32_t r = lane + 64u * rb;
+                    x[rb][q] = 64u * rb < R ? xat(jc * R + (r < R ? r : 0u)) : 0.0f;
+                }
+            }
+            float pn[kCB], pp[kCB];
+#pragma unroll
+            for (int q = 0; q < kCB; q++) { pn[q] = 0.0f; pp[q] = 0.0f; }
+#pragma unroll
+            for (int rb = 0; rb < kRB; rb++)
+                if (lane + 64u * rb < R) {
+#pragma unroll
+                    for (int q = 0; q < kCB; q++) { const float a = fabsf(x[rb][q]); pn[q] = pn[q] + a * a; }
+                }
+            tree_fn<kCB>(pn);
+            float nc[kCB];
+#pragma unroll
+            for (int q = 0; q < kCB; q++) nc[q] = sqrtf(__shfl(pn[q], 0, 64));
+#pragma unroll
+            for (int rb = 0; rb < kRB; rb++)
+                if (lane + 64u * rb < R) {
+#pragma unroll
+                    for (int q = 0; q < kCB; q++) pp[q] = pp[q] + d[rb] * (x[rb][q] / nc[q]);
+                }
+            tree_fn<kCB>(pp);
+            if (lane == 0) {
+#pragma unroll
+                for (int q = 0; q < kCB; q++)
+                    if (j0 + q < m) keys[j0 + q] = proj_key(nc[q] != 0 ? pp[q] : 0.0f, v[q]);
+            }
+        }
+    }
+    __syncthreads();
+    pmark(PF_PROJ);
+    // the sort (:641-648): each key's rank among the m unique keys; the
+    // sorted ids to vrls (a speculative split's with sc1 stores, as split())
+    if (tid < (int)m) {
+        const unsigned long long k = keys[tid];
+        uint32_t rank = 0;
+#pragma unroll 4
+        for (uint32_t j = 0; j < m; j++) rank += keys[j] < k ? 1u : 0u;
+        spos[rank] = (uint32_t)tid;
+        const uint32_t v = ids[tid];
+        svrl[rank] = v;
+        if (commit) vrlsW[begin + rank] = v;
+        else __hip_atomic_store(&vrlsW[begin + rank], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    pmark(PF_SORT);
+    const long long hv0 = pfp && tid == 0 ? (long long)clock64() : 0;
+    // variance_split_small from LDS: waves 0 / 4 form the forward / reverse
+    // pass's coefficients (chunk_coefs, :1075-1085)
+    if (blk == 0) {
+        auto* const cg = coef + (size_t)g * 7 * m;
+        double W = 0.0;
+        for (uint32_t c0 = 0; c0 < m; c0 += 64) {
+            const uint32_t c = c0 + lane;
+            const bool has = c < m;
+            const uint32_t i = has ? c : m - 1;
+            const double w = (double)lp(wv)[spos[g == 0 ? i : m - 1 - i]];
+            const uint32_t n = min(64u, m - c0);
+            double Wo = 0.0, Wn = 0.0;
+            for (uint32_t k = 0; k < n; k++) {
+                const double wk = readlane_d(w, k);
+                const bool me = lane == k;
+                Wo = me ? W : Wo;
+                W = W + wk;
+                Wn = me ? W : Wn;
+            }
+            if (has) {
+                if (!isfinite(w) || w <= 0) Cs.err = 1;
+                const double rw = 1.0 / w;
+                cg[c] = w;
+                cg[m + c] = Wo;
+                cg[2 * m + c] = (Wn * Wn) / (Wo * Wo);
+                cg[3 * m + c] = (rw + 1.0 / Wo);
+                cg[4 * m + c] = rw;
+                cg[5 * m + c] = Wn;
+                cg[6 * m + c] = 1.0 / Wn;
+            }
+        }
+    }
+    __syncthreads();
+    // the rows' recurrence (:1086-1106), wave = pass * 4 + row block, and each
+    // column's two prefix terms reduced over the block (tree16_transposed)
+    if (blk < NB) {
+        const bool valid = blk * 64u + lane < R;
+        const auto* const cg = coef + (size_t)g * 7 * m;
+        double sum = 0.0, M = 0.0, V = 0.0;
+        const size_t rb0 = contig ? (size_t)(off0 + vrow) : (size_t)rbase[vrow];
+        const size_t rs0 = contig ? (size_t)stride0 : (size_t)rstr[vrow];
+        auto ld = [&](uint32_t c0, float2* e) {   // XO: from global memory, two chunks ahead
+#pragma unroll
+            for (int q = 0; q < kCH; q++) {
+                const uint32_t c = min(c0 + (uint32_t)q, m - 1), cp = g == 0 ? c : m - 1 - c;
+                if (XO) {
+                    e[q] = ldg2(Rt, rb0 + (size_t)svrl[cp] * rs0);
+                } else {
+                    const unsigned long long u = Eu[spos[cp] * R + vrow];
+                    e[q] = make_float2(__uint_as_float((uint32_t)u), __uint_as_float((uint32_t)(u >> 32)));
+                }
+            }
+        };
+        auto chunk = [&](uint32_t c0, const float2* cur) {
+            double tv[2 * kCH];
+            if (c0 > 0 && c0 + kCH <= m) {             // a full chunk past column 0: no guards
+#pragma unroll
+                for (int q = 0; q < kCH; q++) {
+                    const uint32_t c = c0 + (uint32_t)q;
+                    const double x = (double)cur[q].x;
+                    const double tmp = cg[c] * sum - cg[m + c] * x;
+                    M = cg[2 * m + c] * M + cg[3 * m + c] * (tmp * tmp);
+                    V = V + (double)cur[q].y * cg[4 * m + c];
+                    sum = sum + x;
+                    tv[2 * q] = lw * (M * cg[6 * m + c]);
+                    tv[2 * q + 1] = lw * (V * cg[5 * m + c]);
+                }
+            } else {
+#pragma unroll
+                for (int q = 0; q < kCH; q++) {
+                    const uint32_t c = c0 + (uint32_t)q;
+                    if (c < m) {
+                        const double x = (double)cur[q].x;
+                        const double tmp = cg[c] * sum - cg[m + c] * x;
+                        if (c > 0) M = cg[2 * m + c] * M + cg[3 * m + c] * (tmp * tmp);
+                        V = V + (double)cur[q].y * cg[4 * m + c];
+                        sum = sum + x;
+                        tv[2 * q] = lw * (M * cg[6 * m + c]);
+                        tv[2 * q + 1] = lw * (V * cg[5 * m + c]);
+                    } else {
+                        tv[2 * q] = 0.0; tv[2 * q + 1] = 0.0;
+                    }
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < 2 * kCH; i++) tv[i] = valid ? tv[i] : 0.0;
+            const double z = tree16_transposed(tv, lane);
+            if ((lane & 3) == 0) {
+                const uint32_t h = lane >> 5, c = 4 * ((lane >> 2) & 1) + 2 * ((lane >> 3) & 1) + ((lane >> 4) & 1);
+                if (c0 + c < m) Q[(((size_t)g * m + c0 + c) * 2 + h) * 4 + blk] = z;
+            }
+        };
+        // three chunks' entries issued together (clamped: past the end the
+        // last chunk again), then the three chunks: nothing is in flight
+        // across the loop's back edge, where the compiler would wait for
+        // every load (it cannot match loads in flight from two paths)
+        const uint32_t nch = (m + kCH - 1) / kCH;
+        float2 bufA[kCH], bufB[kCH], bufC[kCH];
+        for (uint32_t k = 0; k < nch; k += 3) {
+            ld(k * kCH, bufA);
+            ld(min(k + 1, nch - 1) * kCH, bufB);
+            ld(min(k + 2, nch - 1) * kCH, bufC);
+            chunk(k * kCH, bufA);
+            if (k + 1 < nch) chunk((k + 1) * kCH, bufB);
+            if (k + 2 < nch) chunk((k + 2) * kCH, bufC);
+        }
+    }
+    __syncthreads();
+    // block totals in ascending block order (wsum_blk), as floats
+    for (uint32_t t = (uint32_t)tid; t < 4 * m; t += kThreads) {
+        const uint32_t gh = t / m, c = t - gh * m, gg = gh >> 1, h = gh & 1;
+        const auto* q = Q + (((size_t)gg * m + c) * 2 + h) * 4;
+        double acc = q[0];
+        for (uint32_t b = 1; b < NB; b++) acc = acc + q[b];
+        const float f = (h == 0 && c == 0) ? 0.0f : (float)acc;
+        out[gh * m + c] = f;
+        if (c == m - 1) {
+            if (h == 0) Cs.vg[gg].res_u = f; else Cs.vg[gg].res_i = f;
+            if (!isfinite(f) || f < 0) Cs.err = 1;
+        }
+    }
+    __syncthreads();
+    if (pfp && tid == 0) hbv = (long long)clock64() - hv0;
+    pmark(PF_CVF);
+    split_finish(J, C, begin, end, commit, res, [&](int k, uint32_t i) -> float { return out[(uint32_t)k * m + i]; });
+    pmark(PF_ARGMIN);
+    if (pfp && tid == 0) {
+        pfs->sm = -1;
+        const int b = pf_bucket(m);
+        padd(PF_N + 4 * b, 1ull);
+        padd(PF_N + 4 * b + 1, (unsigned long long)(pfs->t - hb0));
+        padd(PF_N + 4 * b + 2, (unsigned long long)hbv);
+        padd(PF_N + 4 * b + 3, (unsigned long long)hbp);
+    }
+}
+
 // ------------------------------------------------------------ split --
 // Clustering::split (:590-684), collective.
 // commit: push the two children (the leader); otherwise write the result to
@@ -2612,6 +3103,16 @@ __device__ void split(CJ& J_in, CC& cm_in, Ctl& C, uint32_t begin, uint32_t end,
 {
     CJ& J = uni(J_in);
     CC& cm = uni(cm_in);
+    if (cm.split_fused && cm.var_small) {
+        if (fused_fits<false>(end - begin, J.nrows)) {
+            split_fused<false>(J, cm, C, begin, end, lds, pf, commit, res);
+            return;
+        }
+        if (cm.split_fused > 1 && fused_fits<true>(end - begin, J.nrows)) {
+            split_fused<true>(J, cm, C, begin, end, lds, pf, commit, res);
+            return;
+        }
+    }
     pf.mark(PF_CTRL);
     pf.count(PF_NSPLIT, 1);
     pf.count(PF_SPLITCOLS, end - begin);
@@ -2773,46 +3274,8 @@ __device__ void split(CJ& J_in, CC& cm_in, Ctl& C, uint32_t begin, uint32_t end,
         if (small) return so[k * kSmallMax + i];
         return k == 0 ? fsuR[i] : k == 1 ? fsiR[i] : k == 2 ? feuR[i] : feiR[i];
     };
-    // argmin over split position (:664-675)
-    float bv = INFINITY;
-    uint32_t bi = 0xFFFFFFFFu;
-    for (uint32_t i = 1 + tid; i < m; i += kThreads) {
-        const float v = pref(0, i - 1) + pref(1, i - 1) + pref(2, m - 1 - i) + pref(3, m - 1 - i);
-        if (v < bv) { bv = v; bi = i; }
-    }
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        const float ov = __shfl_down(bv, off, 64);
-        const uint32_t oi = __shfl_down(bi, off, 64);
-        if (lane < off && (ov < bv || (ov == bv && oi < bi))) { bv = ov; bi = oi; }
-    }
-    if (lane == 0) { Cs.best_v[wave] = bv; Cs.best_i[wave] = bi; }
-    __syncthreads();
-    if (tid == 0) {
-        float v = INFINITY;
-        uint32_t idx = 0xFFFFFFFFu;
-        for (int w = 0; w < kWaves; w++)
-            if (Cs.best_v[w] < v || (Cs.best_v[w] == v && Cs.best_i[w] < idx)) { v = Cs.best_v[w]; idx = Cs.best_i[w]; }
-        if (!commit) {
-            SplitRes r{idx, Cs.err | (idx == 0xFFFFFFFFu ? 1 : 0), 0.0f, 0.0f, 0.0f, 0.0f};
-            if (idx != 0xFFFFFFFFu) {
-                r.fsu = pref(0, idx - 1); r.fsi = pref(1, idx - 1);
-                r.feu = pref(2, m - 1 - idx); r.fei = pref(3, m - 1 - idx);
-            }
-            auto* const rw = gpw(reinterpret_cast<uint32_t*>(res));   // sc1 stores, see the range above
-            const uint32_t* rv = reinterpret_cast<const uint32_t*>(&r);
-#pragma unroll
-            for (int k = 0; k < (int)(sizeof(SplitRes) / 4); k++)
-                __hip_atomic_store(&rw[k], rv[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else if (idx == 0xFFFFFFFFu) {
-            Cs.err = 1;
-        } else {
-            const uint32_t s = begin + idx;
-            add_cluster(J, C, begin, s, pref(0, idx - 1), pref(1, idx - 1));
-            add_cluster(J, C, s, end, pref(2, m - 1 - idx), pref(3, m - 1 - idx));
-        }
-    }
-    __syncthreads();
+    // argmin over split position (:664-675), the children or the result
+    split_finish(J, C, begin, end, commit, res, pref);
     pf.mark(PF_ARGMIN);
     pf.sm = -1;
     if (pf.p && tid == 0) {
@@ -4780,6 +5243,8 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
         cm.var_v3 = !(vv && vv[0] == '0');
         const char* vs = std::getenv("ALVRL_VAR_SMALL");
         cm.var_small = !(vs && vs[0] == '0');
+        const char* sf = std::getenv("ALVRL_SPLIT_FUSED");
+        cm.split_fused = sf ? std::min(std::max(std::atoi(sf), 0), 2) : 2;
     }
     const char* pe = std::getenv("ALVRL_REFINE_PROFILE");
     if (pe && pe[0] == '1' && hipMalloc(&cm.prof, kPfTotal * 8) == hipSuccess)
