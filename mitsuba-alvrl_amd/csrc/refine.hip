@@ -2519,6 +2519,8 @@ __device__ ALVRL_PROJ_INL void split_projections(CJ& J_in, CC& cm_in, uint32_t b
 {
     CJ& J = uni(J_in);
     CC& cm = uni(cm_in);
+    begin = (uint32_t)__builtin_amdgcn_readfirstlane((int)begin);   // uniform: scalar loop exits
+    m = (uint32_t)__builtin_amdgcn_readfirstlane((int)m);
     const uint32_t R = J.nrows;
     const int wave = threadIdx.x >> 6;
     const uint32_t lane = threadIdx.x & 63;
@@ -2536,11 +2538,15 @@ __device__ ALVRL_PROJ_INL void split_projections(CJ& J_in, CC& cm_in, uint32_t b
             d[rb] = r < R ? dir[r] : 0.0f;
             row[rb] = row_ref(J, r < R ? r : 0);
         }
-        uint32_t vA[kCB], vB[kCB];
-        float xA[kRB][kCB], xB[kRB][kCB];
-        auto load = [&](uint32_t j0, uint32_t* v, float (*x)[kCB]) {
+        // a batch's ids are loaded two steps ahead and its entries one step
+        // ahead, every load issued (clamped to the wave's last batch): the ids
+        // an entry load needs are then older than the entries in flight, and
+        // no wait drains the queue (vmcnt counts in issue order)
+        auto ldid = [&](uint32_t j0, uint32_t* v) {
 #pragma unroll
             for (int q = 0; q < kCB; q++) v[q] = vrls[begin + min(j0 + (uint32_t)q, m - 1)];
+        };
+        auto ldx = [&](const uint32_t* v, float (*x)[kCB]) {
 #pragma unroll
             for (int rb = 0; rb < kRB; rb++)
 #pragma unroll
@@ -2574,13 +2580,30 @@ __device__ ALVRL_PROJ_INL void split_projections(CJ& J_in, CC& cm_in, uint32_t b
             }
         };
         uint32_t j0 = (uint32_t)wave * kCB;
-        if (j0 < m) load(j0, vA, xA);
-        for (; j0 < m; j0 += 2 * stride) {
-            if (j0 + stride < m) load(j0 + stride, vB, xB);
-            reduce(j0, vA, xA);
-            if (j0 + stride >= m) break;
-            if (j0 + 2 * stride < m) load(j0 + 2 * stride, vA, xA);
-            reduce(j0 + stride, vB, xB);
+        if (j0 < m) {
+            const uint32_t jl = j0 + ((m - 1 - j0) / stride) * stride;   // the wave's last batch
+            auto cl = [&](uint32_t j) { return min(j, jl); };
+            uint32_t kA[kCB], kB[kCB], vN[kCB];
+            float xA[kRB][kCB], xB[kRB][kCB];
+            ldid(j0, vN);
+#pragma unroll
+            for (int q = 0; q < kCB; q++) kA[q] = vN[q];
+            ldid(cl(j0 + stride), vN);
+            ldx(kA, xA);
+            for (;; j0 += 2 * stride) {
+#pragma unroll
+                for (int q = 0; q < kCB; q++) kB[q] = vN[q];
+                ldid(cl(j0 + 2 * stride), vN);
+                ldx(kB, xB);
+                reduce(j0, kA, xA);
+                if (j0 + stride >= m) break;
+#pragma unroll
+                for (int q = 0; q < kCB; q++) kA[q] = vN[q];
+                ldid(cl(j0 + 3 * stride), vN);
+                ldx(kA, xA);
+                reduce(j0 + stride, kB, xB);
+                if (j0 + 2 * stride >= m) break;
+            }
         }
     } else {                                // tall local matrices: two passes from memory
         for (uint32_t j0 = (uint32_t)wave * kCB; j0 < m; j0 += stride) {
