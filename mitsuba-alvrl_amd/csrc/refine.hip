@@ -274,17 +274,26 @@ __device__ __forceinline__ void trace(CC& cm, uint32_t phase, uint32_t value)
         __hip_atomic_store(&cm.trace[blockIdx.x], ((unsigned long long)phase << 32) | value, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
 }
+// A counter add through a typed global pointer: HIP's atomicAdd on a plain
+// pointer is a flat atomic, and one flat operation anywhere in a function makes
+// the compiler's later waits there wait for every memory operation in flight
+// (a flat op may complete out of order with respect to either counter)
+__device__ __forceinline__ void gadd(unsigned long long* p, unsigned long long v)
+{
+    __hip_atomic_fetch_add((__attribute__((address_space(1))) unsigned long long*)p, v, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
 // team counters
 enum { TS_ENQ, TS_HSTART, TS_HDONE, TS_COMMIT, TS_STEAL, TS_WAIT_TMO, TS_OWN, TS_IDLE_EXIT, TS_LSIDE,
        TS_HIDLE, TS_RIDLE, TS_HBUSY, TS_RBUSY, TS_ACQ, TS_REL, TS_PSPLIT, TS_PSOLO, TS_POWN, TS_POTHER,
        TS_PWAIT, TS_N };   // *IDLE/*BUSY: wall ticks (100 MHz) summed
 __device__ __forceinline__ void tcount(CC& cm, int k)
 {
-    if (cm.tstat) atomicAdd(&cm.tstat[k], 1ull);
+    if (cm.tstat) gadd(&cm.tstat[k], 1ull);
 }
 __device__ __forceinline__ void tadd(CC& cm, int k, unsigned long long v)
 {
-    if (cm.tstat) atomicAdd(&cm.tstat[k], v);
+    if (cm.tstat) gadd(&cm.tstat[k], v);
 }
 
 // Phase timer of lane 0 (s_memtime deltas summed over jobs).
@@ -314,7 +323,7 @@ struct Prof {
     long long t;
     int sm;                      // small-split class of the split in progress (-1: none)
     __device__ void mark(int id);
-    __device__ void count(int id, unsigned long long v) { if (p && threadIdx.x == 0) atomicAdd(&p[id], v); }
+    __device__ void count(int id, unsigned long long v) { if (p && threadIdx.x == 0) gadd(&p[id], v); }
 };
 // split-size histogram after the phase totals: per log2(columns) bucket
 // (count, split cycles, variance cycles, cycles before the projections)
@@ -327,9 +336,9 @@ __device__ void Prof::mark(int id)
 {
     if (p && threadIdx.x == 0) {
         const long long now = clock64();
-        atomicAdd(&p[id], (unsigned long long)(now - t));
+        gadd(&p[id], (unsigned long long)(now - t));
         if (sm >= 0 && id >= PF_WSAMP && id <= PF_ARGMIN)
-            atomicAdd(&p[kPfSmallAt + sm * kPfSmallPh + (id - PF_WSAMP)], (unsigned long long)(now - t));
+            gadd(&p[kPfSmallAt + sm * kPfSmallPh + (id - PF_WSAMP)], (unsigned long long)(now - t));
         t = now;
     }
 }
@@ -1239,9 +1248,9 @@ __device__ __noinline__ void variance_passes_t(CJ& J_in, CC& cm_in, Ctl& C, cons
     }
     if (FU && (nch & 1)) reduce(nch - 1, 1);
     if (wprof && lane == 0 && m >= 4096) {
-        atomicAdd(&cm.prof[kPfWaveBusy + tid / 64], (unsigned long long)wbusy);
-        atomicAdd(&cm.prof[kPfWaveBusy + kWaves + tid / 64], (unsigned long long)((long long)clock64() - wwall0));
-        atomicAdd(&cm.prof[kPfWaveBusy + 2 * kWaves + tid / 64], (unsigned long long)wred);
+        gadd(&cm.prof[kPfWaveBusy + tid / 64], (unsigned long long)wbusy);
+        gadd(&cm.prof[kPfWaveBusy + kWaves + tid / 64], (unsigned long long)((long long)clock64() - wwall0));
+        gadd(&cm.prof[kPfWaveBusy + 2 * kWaves + tid / 64], (unsigned long long)wred);
     }
     // the last pair's sums, the final variances
     if (FU && active && w == 3 && nch > 0 && lane < 2u * kCH) {
@@ -1477,7 +1486,7 @@ __device__ __noinline__ void variance_split_v3(CJ& J_in, CC& cm_in, Ctl& C, cons
     const bool wprof = cm.prof != nullptr && m >= 4096;
     const int pbase = kPfWaveBusy + (NB == 4 ? 3 * kWaves : 0);
     auto padd = [&](int idx, long long v) {
-        if (lane == 0) atomicAdd(&cm.prof[idx], (unsigned long long)v);
+        if (lane == 0) gadd(&cm.prof[idx], (unsigned long long)v);
     };
     uint32_t pc_busy = 0, pc_red = 0, pc_sp[4] = {0, 0, 0, 0};
     const long long wall0 = wprof ? (long long)clock64() : 0;
@@ -3303,10 +3312,10 @@ __device__ void split(CJ& J_in, CC& cm_in, Ctl& C, uint32_t begin, uint32_t end,
     pf.sm = -1;
     if (pf.p && tid == 0) {
         const int b = pf_bucket(m);
-        atomicAdd(&pf.p[PF_N + 4 * b], 1ull);
-        atomicAdd(&pf.p[PF_N + 4 * b + 1], (unsigned long long)(pf.t - hb0));
-        atomicAdd(&pf.p[PF_N + 4 * b + 2], (unsigned long long)hbv);
-        atomicAdd(&pf.p[PF_N + 4 * b + 3], (unsigned long long)hbp);
+        gadd(&pf.p[PF_N + 4 * b], 1ull);
+        gadd(&pf.p[PF_N + 4 * b + 1], (unsigned long long)(pf.t - hb0));
+        gadd(&pf.p[PF_N + 4 * b + 2], (unsigned long long)hbv);
+        gadd(&pf.p[PF_N + 4 * b + 3], (unsigned long long)hbp);
     }
 }
 
@@ -4783,8 +4792,8 @@ __global__ void __launch_bounds__(kThreads) k_refine(const ALVRL_AS4 JobDev* __r
         // column weights, initial clusters and unclustered variance read every
         // entry once; a split reads its cluster's columns (at least) once
         if (cm.entries) {
-            atomicAdd(&cm.entries[0], (3ull * N + split_cols) * R);
-            atomicAdd(&cm.entries[1], split_cols * R);
+            gadd(&cm.entries[0], (3ull * N + split_cols) * R);
+            gadd(&cm.entries[1], split_cols * R);
         }
     }
     if (cm.jtime && tid == 0) cm.jtime[3 * blockIdx.x + 2] = wall();
