@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--jobs", type=int, nargs="+", default=[1, 256])
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--tag", default="")
+    ap.add_argument("--shuffle", action="store_true",
+                    help="the root cluster's columns in a random order (not memory order)")
     a = ap.parse_args()
     os.environ.setdefault("ALVRL_REFINE_TEAM", "1")
     import torch
@@ -49,8 +51,11 @@ def main():
     rows = np.arange(R, dtype=np.uint32)
     locw = np.full(R, 1.0 / R, np.float64)
     init_vrls = np.arange(N, dtype=np.uint32)
+    if a.shuffle:
+        init_vrls = np.random.default_rng(7).permutation(N).astype(np.uint32)
     init_off = np.array([0, N], np.uint32)
-    out = {"rows": R, "vrls": N, "lib": os.environ.get("ALVRL_LIB", "default"), "tag": a.tag, "runs": []}
+    out = {"rows": R, "vrls": N, "lib": os.environ.get("ALVRL_LIB", "default"), "tag": a.tag,
+           "shuffle": a.shuffle, "runs": []}
     for J in a.jobs:
         jobs = [dict(rows=rows, locw=locw, pixel_undersampling=1.0 / 64.0, undersampling=N / 2.0,
                      depth_correction=1.0, do_refine=True, stage_refine=3 + 2 * j, stage_sample=4 + 2 * j)
