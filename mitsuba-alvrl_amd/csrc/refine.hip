@@ -2712,6 +2712,9 @@ __device__ __forceinline__ void split_finish(CJ& J, Ctl& C, uint32_t begin, uint
 // Every value is formed by the same IEEE operations in the same order as
 // split() with variance_split_small, so the results are bit-identical.
 constexpr uint32_t kFusedMaxRows = 256;
+#ifndef ALVRL_FUSED_KB
+#define ALVRL_FUSED_KB 16   // staging loads in flight per thread
+#endif
 // LDS bytes.  XO = false: coefficients 112m, block totals 128m, then the
 // entries, 8mR (float2).  XO = true (a cluster whose float2 entries do not
 // fit): the entries' means only, 4mR, in the space the coefficients and block
