@@ -322,7 +322,7 @@ TEAM_ENV_KEYS = ("ALVRL_REFINE_TEAM", "ALVRL_REFINE_ROAM", "ALVRL_SPEC_WIDTH", "
                  "ALVRL_REFINE_SPIN_MS", "ALVRL_ENQ_START", "ALVRL_LEADER_SIDE",
                  "ALVRL_LEADER_WAIT_TICKS", "ALVRL_REFINE_TEAM_STATS", "ALVRL_ROAM_ORDER",
                  "ALVRL_TEAM_SETUP", "ALVRL_EARLY_SPEC", "ALVRL_VAR_SMALL", "ALVRL_REFINE_NROAM",
-                 "ALVRL_FINISHED_ROAM")
+                 "ALVRL_FINISHED_ROAM", "ALVRL_SPLIT_FUSED")
 
 
 def test_team_mode_settings(gpu_ok):
@@ -360,7 +360,8 @@ def test_team_mode_settings(gpu_ok):
                 dict(ALVRL_LEADER_WAIT_TICKS=0), dict(ALVRL_TEAM_SETUP=0),
                 dict(ALVRL_TEAM_SETUP=1, ALVRL_REFINE_ROAM=0), dict(ALVRL_EARLY_SPEC=0),
                 dict(ALVRL_EARLY_SPEC=1, ALVRL_REFINE_ROAM=0, ALVRL_LEADER_WAIT_TICKS=0), dict(ALVRL_VAR_SMALL=0),
-                dict(ALVRL_REFINE_NROAM=3, ALVRL_FINISHED_ROAM=0), {}]
+                dict(ALVRL_REFINE_NROAM=3, ALVRL_FINISHED_ROAM=0), dict(ALVRL_SPLIT_FUSED=0),
+                dict(ALVRL_SPLIT_FUSED=1), {}]
     try:
         for props in ("targetNumSlices=40", "targetNumSlices=30;localUndersampling=10",
                       "targetNumSlices=25;depthCorrection=0.8"):
