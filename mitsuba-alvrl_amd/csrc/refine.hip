@@ -5177,7 +5177,10 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
     }
     {
         const char* sw = std::getenv("ALVRL_SPEC_WIDTH");
-        cm.spec_width = sw ? (uint32_t)std::max(1, std::atoi(sw)) : 32u;   // C4 refine sweeps (tools/env_sweep.sh), min 2: width 24 401 ms; 32 398 (no queueing after the pop)
+        // C4 refine sweeps: round 1 (tools/env_sweep.sh, min 2) width 24 401 ms, 32 398; round 5,
+        // after the fused small split (tools/env_sweep2.sh, three runs each) 32 260.4, 40 258.6,
+        // 48 257.6, 56 257.1, 64 258.5 ms (at most 64: one wave examines the heap's top)
+        cm.spec_width = sw ? (uint32_t)std::max(1, std::atoi(sw)) : 56u;
     }
     {
         const char* sp = std::getenv("ALVRL_REFINE_SPIN_MS");
