@@ -2419,6 +2419,8 @@ __device__ __forceinline__ RowRef row_ref(const PartJob& pj, uint32_t r)
 __device__ __noinline__ void proj_range(const PartJob& pj, CC& cm_in, uint32_t jb, uint32_t je)
 {
     CC& cm = uni(cm_in);
+    jb = (uint32_t)__builtin_amdgcn_readfirstlane((int)jb);   // uniform: scalar loop exits
+    je = (uint32_t)__builtin_amdgcn_readfirstlane((int)je);
     const uint32_t R = pj.nrows;
     const int wave = threadIdx.x >> 6;
     const uint32_t lane = threadIdx.x & 63;
@@ -2436,11 +2438,13 @@ __device__ __noinline__ void proj_range(const PartJob& pj, CC& cm_in, uint32_t j
             d[rb] = r < R ? dir[r] : 0.0f;
             row[rb] = row_ref(pj, r < R ? r : 0);
         }
-        uint32_t vA[kCB], vB[kCB];
-        float xA[kRB][kCB], xB[kRB][kCB];
-        auto load = [&](uint32_t j0, uint32_t* v, float (*x)[kCB]) {
+        // ids two steps ahead, entries one step ahead, every load issued (see
+        // split_projections)
+        auto ldid = [&](uint32_t j0, uint32_t* v) {
 #pragma unroll
             for (int q = 0; q < kCB; q++) v[q] = vrls[min(j0 + (uint32_t)q, je - 1)];
+        };
+        auto ldx = [&](const uint32_t* v, float (*x)[kCB]) {
 #pragma unroll
             for (int rb = 0; rb < kRB; rb++)
 #pragma unroll
@@ -2474,13 +2478,30 @@ __device__ __noinline__ void proj_range(const PartJob& pj, CC& cm_in, uint32_t j
             }
         };
         uint32_t j0 = jb + (uint32_t)wave * kCB;
-        if (j0 < je) load(j0, vA, xA);
-        for (; j0 < je; j0 += 2 * stride) {
-            if (j0 + stride < je) load(j0 + stride, vB, xB);
-            reduce(j0, vA, xA);
-            if (j0 + stride >= je) break;
-            if (j0 + 2 * stride < je) load(j0 + 2 * stride, vA, xA);
-            reduce(j0 + stride, vB, xB);
+        if (j0 < je) {
+            const uint32_t jl = j0 + ((je - 1 - j0) / stride) * stride;   // the wave's last batch
+            auto cl = [&](uint32_t j) { return min(j, jl); };
+            uint32_t kA[kCB], kB[kCB], vN[kCB];
+            float xA[kRB][kCB], xB[kRB][kCB];
+            ldid(j0, vN);
+#pragma unroll
+            for (int q = 0; q < kCB; q++) kA[q] = vN[q];
+            ldid(cl(j0 + stride), vN);
+            ldx(kA, xA);
+            for (;; j0 += 2 * stride) {
+#pragma unroll
+                for (int q = 0; q < kCB; q++) kB[q] = vN[q];
+                ldid(cl(j0 + 2 * stride), vN);
+                ldx(kB, xB);
+                reduce(j0, kA, xA);
+                if (j0 + stride >= je) break;
+#pragma unroll
+                for (int q = 0; q < kCB; q++) kA[q] = vN[q];
+                ldid(cl(j0 + 3 * stride), vN);
+                ldx(kA, xA);
+                reduce(j0 + stride, kB, xB);
+                if (j0 + 2 * stride >= je) break;
+            }
         }
     } else {                                // tall local matrices: two passes from memory
         for (uint32_t j0 = jb + (uint32_t)wave * kCB; j0 < je; j0 += stride) {
