@@ -122,6 +122,7 @@ struct PartSlot {
 constexpr unsigned long long kStSpecBit = 1ull << 63;
 constexpr uint32_t kQSpecBit = 1u << 31;
 constexpr uint32_t kQueue = 1024;
+constexpr int kSpecWidthMax = 256;      // heap entries a leader examines per enqueue (ALVRL_SPEC_WIDTH)
 // The leader's heap nodes carry two flags in the top bits of `end`: queued by
 // this leader (a helper may be on it: its state word decides), and its vrls
 // already in team.spec (a committed speculative split's child).  Queueing
@@ -3412,7 +3413,7 @@ constexpr unsigned long long kSpinTicks = 6000000000ull;   // default of Common:
 // Thread 0 of the leader: queue the multi-clusters near the top of the heap
 // that are not queued yet.
 // The leader's queueing of the clusters near the top of the heap, on wave 0:
-// lane k examines heap entry k (one round trip for all of them instead of a
+// lane k examines heap entries k, k + 64 (one round trip per 64 instead of a
 // dependent chain on lane 0); the first 'room' eligible entries in heap order
 // are queued, as the sequential loop would.  The vrls of every cluster in the
 // heap were released when its parent's split ended (split_team).
@@ -3423,36 +3424,44 @@ __device__ void enqueue_candidates(CJ& J_in, CC& cm_in, Ctl& C)
     CC& cm = uni(cm_in);
     CT& T = J.team;
     const uint32_t lane = threadIdx.x & 63;
-    const int K = min(min(C.heap_n, (int)(cm.spec_width ? cm.spec_width : 2 * T.helpers + 2)), 64);
+    // the heap's first Kt entries, 64 per round (lane = entry), in heap order
+    const int Kt = min(min(C.heap_n, (int)(cm.spec_width ? cm.spec_width : 2 * T.helpers + 2)), kSpecWidthMax);
     const HeapRef H = heap_of(J, C);
     const uint32_t tail = C.qtail;
-    bool elig = false;
-    uint32_t flags = 0u;
-    CNode cn{0.0f, 0.0f, 0u, 0u};
-    if ((int)lane < K) {
-        cn = hld<PL>(H, lane);
-        flags = cn.end & ~kEndMask;
-        cn.end &= kEndMask;
-        elig = cn.end - cn.begin >= cm.spec_min && !(flags & kEndQ);   // not queued by this leader yet
+    uint32_t head = C.qhead, npush = 0, room = 0;
+    for (int base = 0; base < Kt; base += 64) {
+        const int K = min(Kt - base, 64);
+        bool elig = false;
+        uint32_t flags = 0u;
+        CNode cn{0.0f, 0.0f, 0u, 0u};
+        if ((int)lane < K) {
+            cn = hld<PL>(H, base + (int)lane);
+            flags = cn.end & ~kEndMask;
+            cn.end &= kEndMask;
+            elig = cn.end - cn.begin >= cm.spec_min && !(flags & kEndQ);   // not queued by this leader yet
+        }
+        const unsigned long long bal = __ballot(elig);
+        const uint32_t want = (uint32_t)__popcll(bal);
+        if (base == 0) {
+            // room from the head seen last (helpers only advance it); reloaded when short
+            if (want && tail - head + want > kQueue) head = ld_rlx(&T.ctl[0]);
+            const uint32_t used = tail - head;
+            room = used >= kQueue ? 0u : kQueue - used;
+        }
+        const unsigned long long lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+        const uint32_t rank = (uint32_t)__popcll(bal & lt);
+        const bool queued = elig && rank < room;
+        if (queued) {
+            const bool spec = (flags & kEndS) != 0;
+            st_rlx(&T.state[cn.begin], ((unsigned long long)cn.end << 3) | kStQueued | (spec ? kStSpecBit : 0ull));
+            st_rlx(&T.queue[(tail + npush + rank) % kQueue], ((unsigned long long)cn.begin << 32) | cn.end | (spec ? kQSpecBit : 0u));
+            hst<PL>(H, base + (int)lane, CNode{cn.uvar, cn.ivar, cn.begin, cn.end | flags | kEndQ});   // (a flag: not logged)
+            tcount(cm, TS_ENQ);
+        }
+        const uint32_t n = min(want, room);
+        npush += n;
+        room -= n;
     }
-    const unsigned long long bal = __ballot(elig);
-    const uint32_t want = (uint32_t)__popcll(bal);
-    // room from the head seen last (helpers only advance it); reloaded when short
-    uint32_t head = C.qhead;
-    if (want && tail - head + want > kQueue) head = ld_rlx(&T.ctl[0]);
-    const uint32_t used = tail - head;
-    const uint32_t room = used >= kQueue ? 0u : kQueue - used;
-    const unsigned long long lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    const uint32_t rank = (uint32_t)__popcll(bal & lt);
-    const bool queued = elig && rank < room;
-    if (queued) {
-        const bool spec = (flags & kEndS) != 0;
-        st_rlx(&T.state[cn.begin], ((unsigned long long)cn.end << 3) | kStQueued | (spec ? kStSpecBit : 0ull));
-        st_rlx(&T.queue[(tail + rank) % kQueue], ((unsigned long long)cn.begin << 32) | cn.end | (spec ? kQSpecBit : 0u));
-        hst<PL>(H, lane, CNode{cn.uvar, cn.ivar, cn.begin, cn.end | flags | kEndQ});   // (a flag: not logged)
-        tcount(cm, TS_ENQ);
-    }
-    const uint32_t npush = min(want, room);
     if (lane == 0) {
         C.qhead = head;
         C.pre_b = ~0u;
@@ -5199,9 +5208,10 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
     {
         const char* sw = std::getenv("ALVRL_SPEC_WIDTH");
         // C4 refine sweeps: round 1 (tools/env_sweep.sh, min 2) width 24 401 ms, 32 398; round 5,
-        // after the fused small split (tools/env_sweep2.sh, three runs each) 32 260.4, 40 258.6,
-        // 48 257.6, 56 257.1, 64 258.5 ms (at most 64: one wave examines the heap's top)
-        cm.spec_width = sw ? (uint32_t)std::max(1, std::atoi(sw)) : 56u;
+        // after the fused small split (tools/env_sweep2.sh, tools/w8_width.sh, profiles/r05/sweep/):
+        // N = 1 (a busy launch) 32 260.4, 56 257.1, 128 258.1-258.4, 192 259.9-260.8, 256 262.3-262.8
+        // ms; C4 rank 0 of 8 32 127-133, 56 115-122, 128 106-109, 192 104-107 ms
+        cm.spec_width = sw ? (uint32_t)std::max(1, std::atoi(sw)) : (busy_launch ? 128u : 192u);
     }
     {
         const char* sp = std::getenv("ALVRL_REFINE_SPIN_MS");
