@@ -786,8 +786,10 @@ __device__ __forceinline__ CNode pop_wave_t(CJ& J, Ctl& C, const unsigned long l
             hnode_v v = {0u, 0u, 0u, 0u};
             if (ex) v = H.ldt<LH>(idx);
             const float key = __uint_as_float(v.x) + __uint_as_float(v.y);
-            const float skey = __shfl_xor(key, 1);
-            const int sex = __shfl_xor((int)ex, 1);
+            // the sibling's key and existence: a DPP quad permutation [1,0,3,2]
+            // (siblings are lanes 2i, 2i + 1), not an LDS round trip
+            const float skey = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(key), 0xB1, 0xF, 0xF, false));
+            const int sex = __builtin_amdgcn_mov_dpp((int)ex, 0xB1, 0xF, 0xF, false);
             // left (even j): taken unless the right exists and !(right < left)
             const bool chosen = (j & 1) ? (ex && !(key < skey)) : (ex && (!sex || skey < key));
             const unsigned long long mask = __ballot(chosen);
@@ -799,16 +801,23 @@ __device__ __forceinline__ CNode pop_wave_t(CJ& J, Ctl& C, const unsigned long l
                 const int c = (two & 1ull) ? lc : lc + 1;
                 jp = 2 * jp + (c - lc);
                 const long ic = ((h + 1) << kk) - 1 + jp;
-                hnode_v vc;
-                vc.x = __builtin_amdgcn_readlane(v.x, c);
-                vc.y = __builtin_amdgcn_readlane(v.y, c);
-                vc.z = __builtin_amdgcn_readlane(v.z, c);
-                vc.w = __builtin_amdgcn_readlane(v.w, c);
                 L++;
-                if (lane == L) { pidx = ic; pv = vc; }
+                if constexpr (LH) {
+                    // an LDS heap: the path's values are read back below
+                    if (lane == L) pidx = ic;
+                } else {
+                    hnode_v vc;
+                    vc.x = __builtin_amdgcn_readlane(v.x, c);
+                    vc.y = __builtin_amdgcn_readlane(v.y, c);
+                    vc.z = __builtin_amdgcn_readlane(v.z, c);
+                    vc.w = __builtin_amdgcn_readlane(v.w, c);
+                    if (lane == L) { pidx = ic; pv = vc; }
+                }
                 if (kk == 5) h = ic;
             }
         }
+        // (nothing is written during the search: lane i reads path node i)
+        if (LH && lane >= 1 && lane <= L) pv = H.ldt<LH>(pidx);
         PT_POP(2);
         // __push_heap from p_L: climbs while the node above is less
         const bool stay = lane >= 1 && lane <= L && !((__uint_as_float(pv.x) + __uint_as_float(pv.y)) < vkey);
