@@ -12,7 +12,7 @@ rc=$?
 tail -2 gpurun_out/ab_pytest.log
 [ $rc -eq 0 ] || exit $rc
 C="python tools/c5_share.py --res 1024 --vrls 100000 --world 8 --passes 2"
-for i in 1 2 3; do
+for i in ${AB_RUNS:-1 2 3}; do
   ALVRL_LIB=$PWD/mitsuba-alvrl_amd/variants/libalvrl_$V.so timeout -k 10 300 $C > gpurun_out/w8_${V}_$i.log 2>&1 || exit 1
   timeout -k 10 300 $C > gpurun_out/w8_tree_$i.log 2>&1 || exit 1
   echo "$V $i: $(grep -o 'refine [0-9]* ms' gpurun_out/w8_${V}_$i.log | tr '\n' ' ')  tree $i: $(grep -o 'refine [0-9]* ms' gpurun_out/w8_tree_$i.log | tr '\n' ' ')"
