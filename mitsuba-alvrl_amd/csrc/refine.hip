@@ -54,7 +54,9 @@ struct CNode { float uvar, ivar; uint32_t begin, end; };
 // leader into range-indexed side buffers; the leader, which runs the
 // reference's control flow unchanged, commits a finished result when it pops
 // that cluster (or claims a queued one, or splits an unqueued one itself).
-struct SplitRes { uint32_t idx; int err; float fsu, fsi, feu, fei; };
+// v_first / v_last: the ids at the first and last sorted positions, so that a
+// commit pushes a single child without reading its id back from team.spec
+struct SplitRes { uint32_t idx; int err; float fsu, fsi, feu, fei; uint32_t v_first, v_last; };
 struct SplitWs {                      // a workgroup's private split scratch
     float* dir;
     double* st;
@@ -715,13 +717,14 @@ __device__ __forceinline__ HeapRef heap_of(CJ& J, const Ctl& C)
 // a commit's range copy into J.vrls may still be in flight)
 template <int PL = -1>
 __device__ void add_cluster(CJ& J_in, Ctl& C, uint32_t begin, uint32_t end, float uvar, float ivar,
-                            const uint32_t* spec = nullptr, uint32_t flags = 0u)
+                            const uint32_t* spec = nullptr, uint32_t flags = 0u, uint32_t single_id = ~0u)
 {
     CJ& J = uni(J_in);
     if (end == begin) { C.err = 1; return; }
     if (end == begin + 1) {
         gpw(J.singles)[C.singles_n++] =
-            spec ? __hip_atomic_load(&gp(spec)[begin], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : gp(J.vrls)[begin];
+            single_id != ~0u ? single_id
+            : spec ? __hip_atomic_load(&gp(spec)[begin], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : gp(J.vrls)[begin];
         if (uvar != 0) C.err = 1;
         C.clIntVar += ivar;
     } else {
@@ -2683,7 +2686,7 @@ __device__ ALVRL_PROJ_INL void split_projections(CJ& J_in, CC& cm_in, uint32_t b
 // written to *res for the leader (sc1 stores, see split()'s range copy).
 template <class Pref>
 __device__ __forceinline__ void split_finish(CJ& J, Ctl& C, uint32_t begin, uint32_t end, bool commit,
-                                             SplitRes* res, Pref pref)
+                                             SplitRes* res, Pref pref, uint32_t v_first = 0u, uint32_t v_last = 0u)
 {
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const uint32_t m = end - begin;
@@ -2708,7 +2711,7 @@ __device__ __forceinline__ void split_finish(CJ& J, Ctl& C, uint32_t begin, uint
         for (int w = 0; w < kWaves; w++)
             if (Cs.best_v[w] < v || (Cs.best_v[w] == v && Cs.best_i[w] < idx)) { v = Cs.best_v[w]; idx = Cs.best_i[w]; }
         if (!commit) {
-            SplitRes r{idx, Cs.err | (idx == 0xFFFFFFFFu ? 1 : 0), 0.0f, 0.0f, 0.0f, 0.0f};
+            SplitRes r{idx, Cs.err | (idx == 0xFFFFFFFFu ? 1 : 0), 0.0f, 0.0f, 0.0f, 0.0f, v_first, v_last};
             if (idx != 0xFFFFFFFFu) {
                 r.fsu = pref(0, idx - 1); r.fsi = pref(1, idx - 1);
                 r.feu = pref(2, m - 1 - idx); r.fei = pref(3, m - 1 - idx);
@@ -3145,7 +3148,8 @@ __device__ __noinline__ void split_fused(CJ& J_in, CC& cm_in, Ctl& C, uint32_t b
     __syncthreads();
     if (pfp && tid == 0) hbv = (long long)clock64() - hv0;
     pmark(PF_CVF);
-    split_finish(J, C, begin, end, commit, res, [&](int k, uint32_t i) -> float { return out[(uint32_t)k * m + i]; });
+    split_finish(J, C, begin, end, commit, res, [&](int k, uint32_t i) -> float { return out[(uint32_t)k * m + i]; },
+                 svrl[0], svrl[m - 1]);
     pmark(PF_ARGMIN);
     if (pfp && tid == 0) {
         pfs->sm = -1;
@@ -3338,7 +3342,9 @@ __device__ void split(CJ& J_in, CC& cm_in, Ctl& C, uint32_t begin, uint32_t end,
         return k == 0 ? fsuR[i] : k == 1 ? fsiR[i] : k == 2 ? feuR[i] : feiR[i];
     };
     // argmin over split position (:664-675), the children or the result
-    split_finish(J, C, begin, end, commit, res, pref);
+    uint32_t v_first = 0u, v_last = 0u;
+    if (!commit && tid == 0) { v_first = (uint32_t)gp(sorted)[0]; v_last = (uint32_t)gp(sorted)[m - 1]; }
+    split_finish(J, C, begin, end, commit, res, pref, v_first, v_last);
     pf.mark(PF_ARGMIN);
     pf.sm = -1;
     if (pf.p && tid == 0) {
@@ -3961,8 +3967,8 @@ __device__ __forceinline__ void commit_spec(CJ& J, Ctl& C, uint32_t b, uint32_t 
             C.err = 1;
         } else {
             const uint32_t m = e - b, s2 = b + r.idx;
-            add_cluster<PL>(J, C, b, s2, r.fsu, r.fsi, T.spec);
-            add_cluster<PL>(J, C, s2, e, r.feu, r.fei, T.spec);
+            add_cluster<PL>(J, C, b, s2, r.fsu, r.fsi, T.spec, 0u, r.v_first);   // a single's id: the result's
+            add_cluster<PL>(J, C, s2, e, r.feu, r.fei, T.spec, 0u, r.v_last);
             // the children's input is this result, in team.spec
             st_rlx(&T.state[b], ((unsigned long long)s2 << 3) | kStNone | kStSpecBit);
             st_rlx(&T.state[s2], ((unsigned long long)e << 3) | kStNone | kStSpecBit);
