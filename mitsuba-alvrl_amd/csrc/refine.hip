@@ -192,6 +192,7 @@ struct Common {
     int enq_start;                 // also queue candidates right after the pop (before the split)
     unsigned long long spin_ticks; // bound of an idle helper's wait for a task (100 MHz ticks)
     unsigned long long wait_ticks; // bound of a leader's wait for a running helper (100 MHz ticks)
+    uint32_t sort_radix_min;       // clusters of at least this many columns: radix8_sort
     unsigned long long* tstat;     // team counters (ALVRL_REFINE_TEAM_STATS=1), or null
     unsigned long long* jtime;     // with tstat: per job, wall ticks at start / end of refine / end
     unsigned long long* trace;     // host-mapped per-block (phase << 32 | value), ALVRL_REFINE_TRACE=1
@@ -2334,6 +2335,141 @@ __device__ glb_u64* radix_sort(Ctl& C, glb_u64* src, glb_u64* dst, uint32_t n)
     return src;
 }
 
+// LSD radix sort of n unique keys, digits of <= 8 bits over the bit ranges
+// that vary (the low and the high word separately: a projection key's
+// vrl id and its orderable float each span a run of bits).  Each wave owns a
+// contiguous 1/8 of the array and keeps its own count per digit, so a pass
+// has no barrier inside it: a key's place is its digit's offset for the
+// wave (the scan of counts in (digit, wave) order) plus its rank among the
+// batch's lanes with the same digit (ballots per digit bit), which keeps the
+// sort stable.  The scatter also counts the next pass's digits per owner of
+// the destination.  LDS: counts[2][256][8], offsets[256][8] (24 KB of the
+// pool).  Keys in a; b is scratch of n keys; returns the array holding the
+// sorted keys.
+__device__ __noinline__ glb_u64* radix8_sort(Ctl& C_in, glb_u64* a, glb_u64* b, uint32_t n, unsigned char* pool)
+{
+    const int tid = threadIdx.x, wave = tid >> 6;
+    const uint32_t lane = (uint32_t)(tid & 63);
+    auto& C = *lp(&C_in);
+    auto* const cnt = lp(reinterpret_cast<uint32_t*>(pool));   // [2][256 * 8]
+    auto* const off = cnt + 2 * 2048;                           // [256 * 8]
+    auto* const wsum = off + 2048;                              // [8]
+    n = (uint32_t)__builtin_amdgcn_readfirstlane((int)n);
+    // the bits that vary
+    if (tid == 0) { C.lo_or = 0; C.hi_or = 0; C.lo_and = 0xFFFFFFFFu; C.hi_and = 0xFFFFFFFFu; }
+    __syncthreads();
+    {
+        uint32_t lo_o = 0, hi_o = 0, lo_a = 0xFFFFFFFFu, hi_a = 0xFFFFFFFFu;
+        for (uint32_t i = (uint32_t)tid; i < n; i += kThreads) {
+            const unsigned long long k = a[i];
+            lo_o |= (uint32_t)k; hi_o |= (uint32_t)(k >> 32);
+            lo_a &= (uint32_t)k; hi_a &= (uint32_t)(k >> 32);
+        }
+        __hip_atomic_fetch_or(&C.lo_or, lo_o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_or(&C.hi_or, hi_o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_and(&C.lo_and, lo_a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_and(&C.hi_and, hi_a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    for (uint32_t i = (uint32_t)tid; i < 2048; i += kThreads) cnt[i] = 0;
+    __syncthreads();
+    const uint32_t vlo = C.lo_or ^ C.lo_and, vhi = C.hi_or ^ C.hi_and;
+    // digit windows: nl over the low word's varying run, nh over the high word's
+    const uint32_t l0 = vlo ? (uint32_t)__builtin_ctz(vlo) : 0u, l1 = vlo ? 32u - (uint32_t)__builtin_clz(vlo) : 0u;
+    const uint32_t h0 = vhi ? (uint32_t)__builtin_ctz(vhi) : 0u, h1 = vhi ? 32u - (uint32_t)__builtin_clz(vhi) : 0u;
+    const uint32_t nl = (l1 - l0 + 7) / 8, nh = (h1 - h0 + 7) / 8;
+    const uint32_t wl = nl ? (l1 - l0 + nl - 1) / nl : 0u, wh = nh ? (h1 - h0 + nh - 1) / nh : 0u;
+    const uint32_t P = nl + nh;
+    auto win = [&](uint32_t p, uint32_t& sh, uint32_t& w) {
+        if (p < nl) { sh = l0 + p * wl; w = min(wl, l1 - sh); }
+        else { sh = 32u + h0 + (p - nl) * wh; w = min(wh, 32u + h1 - sh); }
+    };
+    // each wave's segment: S keys (a multiple of 64), the last ones shorter
+    const uint32_t S = ((n + 8u * 64u - 1) / (8u * 64u)) * 64u;
+    const float rS = 1.0f / (float)S;
+    auto seg_of = [&](uint32_t o) {
+        uint32_t g = min(7u, (uint32_t)((float)o * rS));
+        if (g * S > o) g--;
+        else if (g < 7u && (g + 1) * S <= o) g++;
+        return g;
+    };
+    const uint32_t sb = min(n, (uint32_t)wave * S), se = min(n, sb + S);
+    if (P > 0) {   // the first pass's counts
+        uint32_t sh, w;
+        win(0, sh, w);
+        const uint32_t mask = (1u << w) - 1u;
+        for (uint32_t i = sb + lane; i < se; i += 64) {
+            const uint32_t d = (uint32_t)(a[i] >> sh) & mask;
+            __hip_atomic_fetch_add(&cnt[d * 8 + (uint32_t)wave], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    }
+    __syncthreads();
+    glb_u64* src = a;
+    glb_u64* dst = b;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    for (uint32_t p = 0; p < P; p++) {
+        uint32_t sh, w, sh2 = 0, w2 = 1;
+        win(p, sh, w);
+        const bool more = p + 1 < P;
+        if (more) win(p + 1, sh2, w2);
+        const uint32_t mask = (1u << w) - 1u, mask2 = (1u << w2) - 1u;
+        auto* const cc = cnt + (p & 1) * 2048;
+        auto* const cn = cnt + ((p + 1) & 1) * 2048;
+        // exclusive scan of the counts in (digit, wave) order: 4 per thread
+        {
+            const uint32_t i0 = (uint32_t)tid * 4;
+            const uint32_t c0 = cc[i0], c1 = cc[i0 + 1], c2 = cc[i0 + 2], c3 = cc[i0 + 3];
+            const uint32_t t = c0 + c1 + c2 + c3;
+            uint32_t x = t;   // inclusive scan over the wave
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
+                if (lane >= (uint32_t)d) x += y;
+            }
+            if (lane == 63) wsum[wave] = x;
+            __syncthreads();
+            uint32_t base = 0;
+            for (int v = 0; v < wave; v++) base += wsum[v];
+            const uint32_t e0 = base + x - t;
+            off[i0] = e0; off[i0 + 1] = e0 + c0; off[i0 + 2] = e0 + c0 + c1; off[i0 + 3] = e0 + c0 + c1 + c2;
+            cn[i0] = 0; cn[i0 + 1] = 0; cn[i0 + 2] = 0; cn[i0 + 3] = 0;   // the next pass's counts
+        }
+        __syncthreads();
+        // the scatter, 8 batches of 64 keys in flight per wave
+        for (uint32_t base = sb; base < se; base += 512) {
+            unsigned long long k[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) k[j] = src[min(base + (uint32_t)j * 64 + lane, se - 1)];
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const uint32_t i = base + (uint32_t)j * 64;
+                if (i >= se) break;
+                const bool valid = i + lane < se;
+                const uint32_t d = (uint32_t)(k[j] >> sh) & mask;
+                unsigned long long mm = __ballot(valid);
+                for (uint32_t bt = 0; bt < w; bt++) {
+                    const bool one = (d >> bt) & 1u;
+                    const unsigned long long bl = __ballot(one);
+                    mm &= one ? bl : ~bl;
+                }
+                const uint32_t rank = (uint32_t)__popcll(mm & lt);
+                const uint32_t ob = off[d * 8 + (uint32_t)wave];
+                const uint32_t o = ob + rank;
+                if (valid) {
+                    dst[o] = k[j];
+                    if ((mm >> lane) == 1ull) off[d * 8 + (uint32_t)wave] = ob + (uint32_t)__popcll(mm);
+                    if (more) {
+                        const uint32_t d2 = (uint32_t)(k[j] >> sh2) & mask2;
+                        __hip_atomic_fetch_add(&cn[d2 * 8 + seg_of(o)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        glb_u64* const t = src; src = dst; dst = t;
+    }
+    return src;
+}
+
 // The projection sort of split() (:641-648): sorts keys0[0..m) in place
 // (keys are unique, so every correct sort gives the same order).  Up to
 // kBitonicMax keys: one bitonic sort in LDS.  Larger clusters: a bucket pass
@@ -2348,12 +2484,21 @@ __device__ __forceinline__ float key_proj(uint32_t u)
 {
     return __uint_as_float((u & 0x80000000u) ? (u & 0x7FFFFFFFu) : ~u);
 }
-__device__ ALVRL_PROJ_INL unsigned long long* sort_keys(CJ& J_in, Ctl& C, uint32_t m, unsigned long long* lds_g)
+__device__ ALVRL_PROJ_INL unsigned long long* sort_keys(CJ& J_in, Ctl& C, uint32_t m, unsigned long long* lds_g,
+                                                     uint32_t radix_min)
 {
     CJ& J = uni(J_in);
     const int tid = threadIdx.x;
     auto* const k0 = gpw(J.keys0);
     auto* const k1 = gpw(J.keys1);
+    if (m >= radix_min) {   // the result in keys0: a later phase writes keys1
+        const glb_u64* r = radix8_sort(C, k0, k1, m, reinterpret_cast<unsigned char*>(lds_g));
+        if (r != k0) {
+            for (uint32_t i = tid; i < m; i += kThreads) k0[i] = r[i];
+            __syncthreads();
+        }
+        return J.keys0;
+    }
     if (m <= (uint32_t)kBitonicMax) {
         bitonic_lds(lp(lds_g), k0, k0, m);
         return J.keys0;
@@ -3313,7 +3458,7 @@ __device__ void split(CJ& J_in, CC& cm_in, Ctl& C, uint32_t begin, uint32_t end,
         split_projections(J, cm, begin, m);
     __syncthreads();
     pf.mark(PF_PROJ);
-    const unsigned long long* sorted = sort_keys(J, C, m, lds);
+    const unsigned long long* sorted = sort_keys(J, C, m, lds, cm.sort_radix_min);
     // a speculative split's range and result are handed to the leader, which
     // reads them with agent-scope loads and no acquire (MI355X_MICROARCH.md,
     // valid forms: every store of the handed-off bytes sc1 and drained before
@@ -5235,6 +5380,10 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
         // wait for a running helper; by default the same as an idle helper's
         const char* wt = std::getenv("ALVRL_LEADER_WAIT_TICKS");
         cm.wait_ticks = wt ? std::strtoull(wt, nullptr, 10) : cm.spin_ticks;
+        // ALVRL_SORT_RADIX_MIN (developer knob, 0: never): the split sort's radix threshold
+        const char* rm = std::getenv("ALVRL_SORT_RADIX_MIN");
+        const long rmv = rm ? std::atol(rm) : 16385L;
+        cm.sort_radix_min = rmv <= 0 ? 0xFFFFFFFFu : (uint32_t)std::min<long>(std::max<long>(rmv, 2L), 0x7FFFFFFFL);
     }
     cm.tstat = nullptr;
     cm.trace = nullptr;
