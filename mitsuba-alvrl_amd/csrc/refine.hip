@@ -193,6 +193,7 @@ struct Common {
     unsigned long long spin_ticks; // bound of an idle helper's wait for a task (100 MHz ticks)
     unsigned long long wait_ticks; // bound of a leader's wait for a running helper (100 MHz ticks)
     uint32_t sort_radix_min;       // clusters of at least this many columns: radix8_sort
+    uint32_t ws_wg_min;            // clusters of at least this many columns: weighted_sample_wg
     unsigned long long* tstat;     // team counters (ALVRL_REFINE_TEAM_STATS=1), or null
     unsigned long long* jtime;     // with tstat: per job, wall ticks at start / end of refine / end
     unsigned long long* trace;     // host-mapped per-block (phase << 32 | value), ALVRL_REFINE_TRACE=1
@@ -212,6 +213,9 @@ struct Common {
     int heap_lds;                  // the leader's heap in LDS between its splits (ALVRL_HEAP_LDS=0: off)
     uint32_t* poptr;               // ALVRL_POP_TRACE=1: wall ticks at 7 points of each leader pop of one job
     uint32_t poptr_job, poptr_cap; // the traced job (most rows), records available
+    unsigned long long* evlog;     // developer event log (a -DALVRL_EVLOG build, ALVRL_EVLOG=file): 3 words per event
+    uint32_t* evlog_n;             // events written
+    uint32_t evlog_cap;
     PartSlot* parts;               // the part board (null: splits are never divided)
     uint32_t nslots;               // its slots
     uint32_t part_min;             // smallest split (columns) divided into parts
@@ -287,6 +291,22 @@ __device__ __forceinline__ void gadd(unsigned long long* p, unsigned long long v
     __hip_atomic_fetch_add((__attribute__((address_space(1))) unsigned long long*)p, v, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
 }
+// Developer event log (tools/evlog.py reads it): compiled in only with
+// -DALVRL_EVLOG; thread 0 of a workgroup appends (wall ticks, tag | block,
+// a | b).  Timestamps without printf's host round trips.
+#ifdef ALVRL_EVLOG
+#define EVLOG(cm, tag, a, b) do { if ((cm).evlog && threadIdx.x == 0) {                                        \
+        const uint32_t ei_ = __hip_atomic_fetch_add((__attribute__((address_space(1))) uint32_t*)(cm).evlog_n, \
+                                                    1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);           \
+        if (ei_ < (cm).evlog_cap) {                                                                          \
+            auto* e_ = (__attribute__((address_space(1))) unsigned long long*)((cm).evlog + 3ull * ei_);      \
+            e_[0] = __builtin_amdgcn_s_memrealtime();                                                        \
+            e_[1] = ((unsigned long long)(tag) << 32) | blockIdx.x;                                          \
+            e_[2] = ((unsigned long long)(uint32_t)(a) << 32) | (uint32_t)(b);                               \
+        } } } while (0)
+#else
+#define EVLOG(cm, tag, a, b) ((void)0)
+#endif
 // team counters
 enum { TS_ENQ, TS_HSTART, TS_HDONE, TS_COMMIT, TS_STEAL, TS_WAIT_TMO, TS_OWN, TS_IDLE_EXIT, TS_LSIDE,
        TS_HIDLE, TS_RIDLE, TS_HBUSY, TS_RBUSY, TS_ACQ, TS_REL, TS_PSPLIT, TS_PSOLO, TS_POWN, TS_POTHER,
@@ -559,6 +579,97 @@ __device__ ALVRL_WS_INL WsPick weighted_sample_wave(const float* wv, const float
     }
     r.idx = idx;
     r.k = smp.k;
+    return r;
+}
+
+// weighted_sample_wave's pick, bit for bit, with the whole workgroup: every
+// wave forms the block totals of its blocks (the same DPP tree), 8 blocks'
+// weights in flight per lane, into tot[] (LDS, nb floats); lane 0 then runs
+// the two sequential float chains: weightSum = sum of the totals in block
+// order, and the search S_b = S_{b-1} + tot_{b-1} for the first block with
+// S_b + tot_b >= alpha.  That test is the wave's per-lane test of that block:
+// the prefixes P[l] grow with l (non-negative weights, monotone rounding),
+// a lane past m or at zero_at adds +0.0, and the block's last prefix is its
+// total (b3 + t3 either way), so some lane of block b reaches alpha exactly
+// when S_b + tot_b does.  Wave 0 then scans that block alone.  Every thread
+// returns the pick; the caller resumes the stream at WsPick::k.
+__device__ __noinline__ WsPick weighted_sample_wg(const float* wv, bool wv_lds, uint32_t m, Smp smp, uint32_t zero_at,
+                                                  float* tot_in)
+{
+    const int tid = threadIdx.x;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t lane = (uint32_t)(tid & 63);
+    auto* const tot = lp(tot_in);
+    __shared__ uint32_t res[3];
+    m = (uint32_t)__builtin_amdgcn_readfirstlane((int)m);
+    wv_lds = __builtin_amdgcn_readfirstlane((int)wv_lds) != 0;
+    WsPick r{0u, smp.k, 0, 1.0f};
+    if (m <= 1) { r.err = m == 0; return r; }
+    auto ld = [&](uint32_t i) -> float {
+        const uint32_t c = min(i, m - 1);
+        const float x = wv_lds ? lp(wv)[c] : gp(wv)[c];
+        return (i >= m || i == zero_at) ? 0.0f : x;
+    };
+    const uint32_t nb = (m + 63) / 64;
+    constexpr uint32_t B = 8;
+    for (uint32_t b0 = wave; b0 < nb; b0 += B * kWaves) {
+        float x[B];
+#pragma unroll
+        for (uint32_t j = 0; j < B; j++) x[j] = ld(min(b0 + j * kWaves, nb - 1) * 64 + lane);
+#pragma unroll
+        for (uint32_t j = 0; j < B; j++) {
+            float t;
+            (void)ws_block_wave(x[j], lane, &t);
+            if (lane == 0 && b0 + j * kWaves < nb) tot[b0 + j * kWaves] = t;
+        }
+    }
+    __syncthreads();
+    if (wave == 0) {
+        // the chains take 64 totals per LDS read, one v_readlane each
+        auto rl = [](float v, int j) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j)); };
+        float weightSum = 0.0f;
+        for (uint32_t g0 = 0; g0 < nb; g0 += 64) {
+            const float v = tot[min(g0 + lane, nb - 1)];
+            if (g0 + 64 <= nb) {
+#pragma unroll
+                for (int j = 0; j < 64; j++) weightSum = weightSum + rl(v, j);
+            } else {
+                for (uint32_t j = 0; j < nb - g0; j++) weightSum = weightSum + rl(v, (int)j);
+            }
+        }
+        uint32_t idx = 0;
+        int err = 0;
+        if (weightSum <= 0) {
+            int tries = 0;
+            do {
+                idx = (uint32_t)((float)0u + smp.next() * (float)m);
+                if (++tries > 1000) { err = 1; idx = 0; break; }
+            } while (idx >= m);
+        } else {
+            const float alpha = smp.next() * weightSum;
+            float S = 0.0f;
+            uint32_t bh = nb;
+            for (uint32_t g0 = 0; g0 < nb && bh == nb; g0 += 64) {
+                const float v = tot[min(g0 + lane, nb - 1)];
+                const uint32_t n = min(64u, nb - g0);
+                for (uint32_t j = 0; j < n; j++) {
+                    const float t = rl(v, (int)j);
+                    if (S + t >= alpha) { bh = g0 + j; break; }
+                    S = S + t;
+                }
+            }
+            if (bh < nb) {
+                float t;
+                const float P = ws_block_wave(ld(bh * 64 + lane), lane, &t);
+                const unsigned long long hit = __ballot(bh * 64 + lane < m && S + P >= alpha);
+                if (hit) idx = bh * 64 + (uint32_t)__ffsll((long long)hit) - 1;
+            }
+        }
+        if (lane == 0) { res[0] = idx; res[1] = smp.k; res[2] = (uint32_t)err; }
+    }
+    __syncthreads();
+    r.idx = res[0]; r.k = res[1]; r.err = (int)res[2];
+    __syncthreads();
     return r;
 }
 
@@ -2343,27 +2454,35 @@ __device__ glb_u64* radix_sort(Ctl& C, glb_u64* src, glb_u64* dst, uint32_t n)
 // wave (the scan of counts in (digit, wave) order) plus its rank among the
 // batch's lanes with the same digit (ballots per digit bit), which keeps the
 // sort stable.  The scatter also counts the next pass's digits per owner of
-// the destination.  LDS: counts[2][256][8], offsets[256][8] (24 KB of the
-// pool).  Keys in a; b is scratch of n keys; returns the array holding the
-// sorted keys.
+// the destination.  Every loop keeps 8 (the scatter 16) loads per lane in
+// flight.  LDS: counts[2][256][8], offsets[256][8] (24 KB of
+// the pool).  Keys in a; b is scratch of n keys; returns the array holding
+// the sorted keys.
 __device__ __noinline__ glb_u64* radix8_sort(Ctl& C_in, glb_u64* a, glb_u64* b, uint32_t n, unsigned char* pool)
 {
-    const int tid = threadIdx.x, wave = tid >> 6;
+    const int tid = threadIdx.x;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t lane = (uint32_t)(tid & 63);
     auto& C = *lp(&C_in);
     auto* const cnt = lp(reinterpret_cast<uint32_t*>(pool));   // [2][256 * 8]
     auto* const off = cnt + 2 * 2048;                           // [256 * 8]
     auto* const wsum = off + 2048;                              // [8]
     n = (uint32_t)__builtin_amdgcn_readfirstlane((int)n);
+    constexpr uint32_t B = 8;
     // the bits that vary
     if (tid == 0) { C.lo_or = 0; C.hi_or = 0; C.lo_and = 0xFFFFFFFFu; C.hi_and = 0xFFFFFFFFu; }
     __syncthreads();
     {
         uint32_t lo_o = 0, hi_o = 0, lo_a = 0xFFFFFFFFu, hi_a = 0xFFFFFFFFu;
-        for (uint32_t i = (uint32_t)tid; i < n; i += kThreads) {
-            const unsigned long long k = a[i];
-            lo_o |= (uint32_t)k; hi_o |= (uint32_t)(k >> 32);
-            lo_a &= (uint32_t)k; hi_a &= (uint32_t)(k >> 32);
+        for (uint32_t i0 = 0; i0 < n; i0 += B * kThreads) {
+            unsigned long long k[B];
+#pragma unroll
+            for (uint32_t j = 0; j < B; j++) k[j] = a[min(i0 + j * kThreads + (uint32_t)tid, n - 1)];   // a repeat is harmless
+#pragma unroll
+            for (uint32_t j = 0; j < B; j++) {
+                lo_o |= (uint32_t)k[j]; hi_o |= (uint32_t)(k[j] >> 32);
+                lo_a &= (uint32_t)k[j]; hi_a &= (uint32_t)(k[j] >> 32);
+            }
         }
         __hip_atomic_fetch_or(&C.lo_or, lo_o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         __hip_atomic_fetch_or(&C.hi_or, hi_o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -2372,7 +2491,8 @@ __device__ __noinline__ glb_u64* radix8_sort(Ctl& C_in, glb_u64* a, glb_u64* b, 
     }
     for (uint32_t i = (uint32_t)tid; i < 2048; i += kThreads) cnt[i] = 0;
     __syncthreads();
-    const uint32_t vlo = C.lo_or ^ C.lo_and, vhi = C.hi_or ^ C.hi_and;
+    const uint32_t vlo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(C.lo_or ^ C.lo_and));
+    const uint32_t vhi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(C.hi_or ^ C.hi_and));
     // digit windows: nl over the low word's varying run, nh over the high word's
     const uint32_t l0 = vlo ? (uint32_t)__builtin_ctz(vlo) : 0u, l1 = vlo ? 32u - (uint32_t)__builtin_clz(vlo) : 0u;
     const uint32_t h0 = vhi ? (uint32_t)__builtin_ctz(vhi) : 0u, h1 = vhi ? 32u - (uint32_t)__builtin_clz(vhi) : 0u;
@@ -2386,20 +2506,26 @@ __device__ __noinline__ glb_u64* radix8_sort(Ctl& C_in, glb_u64* a, glb_u64* b, 
     // each wave's segment: S keys (a multiple of 64), the last ones shorter
     const uint32_t S = ((n + 8u * 64u - 1) / (8u * 64u)) * 64u;
     const float rS = 1.0f / (float)S;
-    auto seg_of = [&](uint32_t o) {
+    auto seg_of = [&](uint32_t o) {   // o / S without a division
         uint32_t g = min(7u, (uint32_t)((float)o * rS));
-        if (g * S > o) g--;
-        else if (g < 7u && (g + 1) * S <= o) g++;
+        g = g * S > o ? g - 1u : g;
+        g = g < 7u && (g + 1u) * S <= o ? g + 1u : g;
         return g;
     };
-    const uint32_t sb = min(n, (uint32_t)wave * S), se = min(n, sb + S);
-    if (P > 0) {   // the first pass's counts
+    const uint32_t sb = min(n, wave * S), se = min(n, sb + S);
+    if (P > 0 && sb < se) {   // the first pass's counts
         uint32_t sh, w;
         win(0, sh, w);
         const uint32_t mask = (1u << w) - 1u;
-        for (uint32_t i = sb + lane; i < se; i += 64) {
-            const uint32_t d = (uint32_t)(a[i] >> sh) & mask;
-            __hip_atomic_fetch_add(&cnt[d * 8 + (uint32_t)wave], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        for (uint32_t i0 = sb; i0 < se; i0 += B * 64) {
+            unsigned long long k[B];
+#pragma unroll
+            for (uint32_t j = 0; j < B; j++) k[j] = a[min(i0 + j * 64 + lane, se - 1)];
+#pragma unroll
+            for (uint32_t j = 0; j < B; j++)
+                if (i0 + j * 64 + lane < se)
+                    __hip_atomic_fetch_add(&cnt[((uint32_t)(k[j] >> sh) & mask) * 8 + wave], 1u, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP);
         }
     }
     __syncthreads();
@@ -2428,41 +2554,56 @@ __device__ __noinline__ glb_u64* radix8_sort(Ctl& C_in, glb_u64* a, glb_u64* b, 
             if (lane == 63) wsum[wave] = x;
             __syncthreads();
             uint32_t base = 0;
-            for (int v = 0; v < wave; v++) base += wsum[v];
+            for (uint32_t v = 0; v < wave; v++) base += wsum[v];
             const uint32_t e0 = base + x - t;
             off[i0] = e0; off[i0 + 1] = e0 + c0; off[i0 + 2] = e0 + c0 + c1; off[i0 + 3] = e0 + c0 + c1 + c2;
             cn[i0] = 0; cn[i0 + 1] = 0; cn[i0 + 2] = 0; cn[i0 + 3] = 0;   // the next pass's counts
         }
         __syncthreads();
-        // the scatter, 8 batches of 64 keys in flight per wave
-        for (uint32_t base = sb; base < se; base += 512) {
-            unsigned long long k[8];
+        // the scatter: 8 batches of 64 keys per step, the next step's loaded
+        // before this one's are placed
+        auto ld = [&](uint32_t base, unsigned long long* k) {
 #pragma unroll
-            for (int j = 0; j < 8; j++) k[j] = src[min(base + (uint32_t)j * 64 + lane, se - 1)];
+            for (uint32_t j = 0; j < B; j++) k[j] = src[min(base + j * 64 + lane, se - 1)];
+        };
+        auto place = [&](uint32_t base, const unsigned long long* k) {
 #pragma unroll
-            for (int j = 0; j < 8; j++) {
-                const uint32_t i = base + (uint32_t)j * 64;
+            for (uint32_t j = 0; j < B; j++) {
+                const uint32_t i = base + j * 64;
                 if (i >= se) break;
                 const bool valid = i + lane < se;
                 const uint32_t d = (uint32_t)(k[j] >> sh) & mask;
                 unsigned long long mm = __ballot(valid);
-                for (uint32_t bt = 0; bt < w; bt++) {
-                    const bool one = (d >> bt) & 1u;
-                    const unsigned long long bl = __ballot(one);
-                    mm &= one ? bl : ~bl;
+#pragma unroll
+                for (uint32_t bt = 0; bt < 8; bt++) {
+                    if (bt < w) {
+                        const bool one = (d >> bt) & 1u;
+                        const unsigned long long bl = __ballot(one);
+                        mm &= one ? bl : ~bl;
+                    }
                 }
                 const uint32_t rank = (uint32_t)__popcll(mm & lt);
-                const uint32_t ob = off[d * 8 + (uint32_t)wave];
+                const uint32_t ob = off[d * 8 + wave];
                 const uint32_t o = ob + rank;
                 if (valid) {
                     dst[o] = k[j];
-                    if ((mm >> lane) == 1ull) off[d * 8 + (uint32_t)wave] = ob + (uint32_t)__popcll(mm);
+                    if ((mm >> lane) == 1ull) off[d * 8 + wave] = ob + (uint32_t)__popcll(mm);
                     if (more) {
                         const uint32_t d2 = (uint32_t)(k[j] >> sh2) & mask2;
                         __hip_atomic_fetch_add(&cn[d2 * 8 + seg_of(o)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     }
                 }
             }
+        };
+        // (two sets loaded at the top of each step and placed within it: a
+        // load in flight across the loop's back edge costs a full drain)
+        constexpr uint32_t ST = B * 64;
+        for (uint32_t base = sb; base < se; base += 2 * ST) {
+            unsigned long long kA[B], kB[B];
+            ld(base, kA);
+            ld(base + ST, kB);
+            place(base, kA);
+            place(base + ST, kB);
         }
         __syncthreads();
         glb_u64* const t = src; src = dst; dst = t;
@@ -3334,6 +3475,7 @@ __device__ void split(CJ& J_in, CC& cm_in, Ctl& C, uint32_t begin, uint32_t end,
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const uint32_t m = end - begin;
     const uint32_t R = J.nrows;
+    if (m >= 4096) EVLOG(cm, 10, m, begin);
     // register copies of the job's fields and of cm: both sit behind generic
     // pointers, so every field read after a barrier would be a flat reload,
     // and a flat op makes the next LDS wait wait for all loads in flight
@@ -3381,7 +3523,21 @@ __device__ void split(CJ& J_in, CC& cm_in, Ctl& C, uint32_t begin, uint32_t end,
         }
     }
     __syncthreads();
-    if (wave == 0) {
+    // large clusters: the block totals on every wave (weighted_sample_wg),
+    // their LDS array after the weights
+    const uint32_t tot_off = wv_lds ? ((m * 4u + 15u) & ~15u) : 0u;
+    if (m >= cm.ws_wg_min && tot_off + (m + 63) / 64 * 4u <= kPoolBytes) {
+        float* const totp = reinterpret_cast<float*>(reinterpret_cast<unsigned char*>(lds) + tot_off);
+        Smp smp;
+        smp.init(seed, pass, begin, end, stage);
+        const WsPick p1 = weighted_sample_wg(wv, wv_lds, m, smp, 0xFFFFFFFFu, totp);
+        smp.k = p1.k; smp.blk = 0xFFFFFFFFu;   // the same stream from draw p1.k
+        const WsPick p2 = weighted_sample_wg(wv, wv_lds, m, smp, p1.idx, totp);   // colw[vrl1] = 0
+        if (tid == 0) {
+            if (p1.err | p2.err) Cs.err = 1;
+            Cs.vrl1 = vrlsR[begin + p1.idx]; Cs.vrl2 = vrlsR[begin + p2.idx]; Cs.draw_k = p2.k;
+        }
+    } else if (wave == 0) {
         Smp smp;
         smp.init(seed, pass, begin, end, stage);
         const WsPick p1 = weighted_sample_wave(wv, nullptr, nullptr, m, smp, 0xFFFFFFFFu, false, wv_lds);
@@ -3395,6 +3551,7 @@ __device__ void split(CJ& J_in, CC& cm_in, Ctl& C, uint32_t begin, uint32_t end,
     }
     __syncthreads();
     pf.mark(PF_WSAMP);
+    if (m >= 4096) EVLOG(cm, 11, m, begin);
     const uint32_t vrl1 = Cs.vrl1, vrl2 = Cs.vrl2;
     // |c1|, |c2|, |c2 - c1| (:607-616), rows in the shared order
     if (wave == 0) {
@@ -3452,12 +3609,14 @@ __device__ void split(CJ& J_in, CC& cm_in, Ctl& C, uint32_t begin, uint32_t end,
         __syncthreads();
     }
     pf.mark(PF_DIR);
+    if (m >= 4096) EVLOG(cm, 12, m, begin);
     hbp = pf.t - hb0;
     if (!(cm.parts && cm.proj_min && m >= cm.proj_min && (R > 256 ? cm.part_min_tall : cm.part_min) &&
           proj_parts(J, cm, C, begin, m, reinterpret_cast<unsigned char*>(lds))))
         split_projections(J, cm, begin, m);
     __syncthreads();
     pf.mark(PF_PROJ);
+    if (m >= 4096) EVLOG(cm, 13, m, begin);
     const unsigned long long* sorted = sort_keys(J, C, m, lds, cm.sort_radix_min);
     // a speculative split's range and result are handed to the leader, which
     // reads them with agent-scope loads and no acquire (MI355X_MICROARCH.md,
@@ -3471,6 +3630,7 @@ __device__ void split(CJ& J_in, CC& cm_in, Ctl& C, uint32_t begin, uint32_t end,
     }
     __syncthreads();
     pf.mark(PF_SORT);
+    if (m >= 4096) EVLOG(cm, 14, m, begin);
     const long long hv0 = pf.p && tid == 0 ? (long long)clock64() : 0;
     const bool small = cm.var_small && m <= kSmallMax && R <= 64u * kSmallBlocks;
     unsigned char* const pool = reinterpret_cast<unsigned char*>(lds);
@@ -3480,6 +3640,7 @@ __device__ void split(CJ& J_in, CC& cm_in, Ctl& C, uint32_t begin, uint32_t end,
         variance_passes(J, cm, C, J.vrls + begin, m, 2, J.fsu, J.fsi, J.feu, J.fei, pool, &pf);
     if (pf.p && tid == 0) hbv = (long long)clock64() - hv0;
     pf.mark(PF_CVF);
+    if (m >= 4096) EVLOG(cm, 15, m, begin);
     // the prefix variances: fsu/fsi of the forward pass, feu/fei of the reverse
     const auto* const so = lp(small_out(pool));
     auto pref = [&](int k, uint32_t i) -> float {
@@ -3491,6 +3652,7 @@ __device__ void split(CJ& J_in, CC& cm_in, Ctl& C, uint32_t begin, uint32_t end,
     if (!commit && tid == 0) { v_first = (uint32_t)gp(sorted)[0]; v_last = (uint32_t)gp(sorted)[m - 1]; }
     split_finish(J, C, begin, end, commit, res, pref, v_first, v_last);
     pf.mark(PF_ARGMIN);
+    if (m >= 4096) EVLOG(cm, 16, m, begin);
     pf.sm = -1;
     if (pf.p && tid == 0) {
         const int b = pf_bucket(m);
@@ -3790,6 +3952,7 @@ __device__ __noinline__ void run_part(CC& cm_in, Ctl& C, uint32_t s, uint32_t p,
     __syncthreads();
     const PartJob& pj = pjs;
     if (threadIdx.x == 0) C.err = 0;
+    EVLOG(cm, 30, pj.kind, p);
     __syncthreads();
     if (pj.kind == kPartProj || pj.kind == kPartColw) {
         const uint32_t jb = pj.c0 + p * pj.cpp;
@@ -3808,6 +3971,7 @@ __device__ __noinline__ void run_part(CC& cm_in, Ctl& C, uint32_t s, uint32_t p,
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    EVLOG(cm, 31, pj.kind, pj.m);
     if (threadIdx.x == 0) {
         if (C.err) __hip_atomic_fetch_or(&S->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         C.err = err_saved;
@@ -3938,12 +4102,14 @@ __device__ __noinline__ bool split_parts(CJ& J_in, CC& cm_in, Ctl& C, const uint
     if (sl < 0) return false;
     unsigned long long* const cw = J.keys1;
     gather_cw(J, base, m, cw);
+    EVLOG(cm, 20, m, J.nrows);
     const uint32_t nblk = (J.nrows + 63) / 64,
                    pblk = min(max(J.nrows > 256 ? cm.part_blk : cm.part_blk_short, 1u), kPartMaxBlk);
     PartJob pj = part_job(J);
     pj.kind = kPartVar; pj.cw = cw; pj.m = m; pj.nblk = nblk; pj.pblk = pblk;
     pj.np = 2 * ((nblk + pblk - 1) / pblk);
     if (!part_run_all(cm, C, (uint32_t)sl, pj, pool)) return true;
+    EVLOG(cm, 21, m, pj.np);
     const double* const T = gp(&cm.parts[sl].T)[0];
     for (uint32_t t = (uint32_t)tid; t < 4u * m; t += kThreads) {
         const uint32_t gh = t / m, n = t - gh * m, g = gh >> 1, h = gh & 1;
@@ -3958,6 +4124,7 @@ __device__ __noinline__ bool split_parts(CJ& J_in, CC& cm_in, Ctl& C, const uint
             if (!isfinite(f) || f < 0) C.err = 1;
         }
     }
+    EVLOG(cm, 22, m, 0);
     part_slot_free(cm, (uint32_t)sl);
     return true;
 }
@@ -4728,6 +4895,7 @@ __global__ void __launch_bounds__(kThreads) k_refine(const ALVRL_AS4 JobDev* __r
     }
     CJ& J = jobs[blockIdx.x];
     trace(cm, 1, 0);
+    EVLOG(cm, 1, J.nrows, 0);
     if (cm.jtime && threadIdx.x == 0) cm.jtime[3 * blockIdx.x] = wall();
     const int tid = threadIdx.x, wave = tid >> 6;
     const uint32_t N = cm.nvrl, R = J.nrows;
@@ -4769,6 +4937,7 @@ __global__ void __launch_bounds__(kThreads) k_refine(const ALVRL_AS4 JobDev* __r
     }
     colw_finish(J, cm, C);
     pf.mark(PF_COLW);
+    EVLOG(cm, 2, J.nrows, 0);
     for (uint32_t i = tid; i < nv; i += kThreads) J.vrls[i] = cm.init_vrls[i];
     __syncthreads();
     if (cm.early_spec && cm.team > 1 && J.team.helpers != 0 && J.do_refine && cm.ninit > 0 && !C.err) {
@@ -4798,6 +4967,7 @@ __global__ void __launch_bounds__(kThreads) k_refine(const ALVRL_AS4 JobDev* __r
         }
     }
     pf.mark(PF_INIT);
+    EVLOG(cm, 3, J.nrows, 0);
     if (tsu && !su_claim(J.team, kSuUncl, C)) {
         const bool ok = su_wait(J.team, kSuUncl, cm, C);
         if (tid == 0) {
@@ -4810,6 +4980,7 @@ __global__ void __launch_bounds__(kThreads) k_refine(const ALVRL_AS4 JobDev* __r
         unclustered_variance(J, cm, C, cm.init_vrls, nv);
     }
     pf.mark(PF_UNCL);
+    EVLOG(cm, 4, J.nrows, 0);
     // release the initial clusters' vrls to the helpers (see split_team)
     drain_vmem();
     __syncthreads();
@@ -4921,6 +5092,7 @@ __global__ void __launch_bounds__(kThreads) k_refine(const ALVRL_AS4 JobDev* __r
         }
     }
     stop_team(J, cm, C);
+    EVLOG(cm, 5, J.nrows, 0);
     if (cm.jtime && threadIdx.x == 0) cm.jtime[3 * blockIdx.x + 1] = wall();
     __syncthreads();
     pf.mark(PF_CTRL);
@@ -5380,10 +5552,15 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
         // wait for a running helper; by default the same as an idle helper's
         const char* wt = std::getenv("ALVRL_LEADER_WAIT_TICKS");
         cm.wait_ticks = wt ? std::strtoull(wt, nullptr, 10) : cm.spin_ticks;
-        // ALVRL_SORT_RADIX_MIN (developer knob, 0: never): the split sort's radix threshold
+        // ALVRL_SORT_RADIX_MIN (developer knob, 0: never): the split sort's radix threshold.
+        // C4 refine (profiles/r05/sort/): 16,385 243.7 ms, 4,096 241.8, 1,024 240.0; bitonic only 258
         const char* rm = std::getenv("ALVRL_SORT_RADIX_MIN");
-        const long rmv = rm ? std::atol(rm) : 16385L;
+        const long rmv = rm ? std::atol(rm) : 1024L;
         cm.sort_radix_min = rmv <= 0 ? 0xFFFFFFFFu : (uint32_t)std::min<long>(std::max<long>(rmv, 2L), 0x7FFFFFFFL);
+        // ALVRL_WS_WG_MIN (developer knob, 0: never): the split's weighted picks on every wave
+        const char* wm = std::getenv("ALVRL_WS_WG_MIN");
+        const long wmv = wm ? std::atol(wm) : 4096L;
+        cm.ws_wg_min = wmv <= 0 ? 0xFFFFFFFFu : (uint32_t)std::min<long>(std::max<long>(wmv, 2L), 0x7FFFFFFFL);
     }
     cm.tstat = nullptr;
     cm.trace = nullptr;
@@ -5482,6 +5659,18 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
     // ALVRL_POP_TRACE=1: the leader of the job with the most rows records the
     // wall clock at 7 points of each pop (tools: the summary printed below)
     cm.poptr = nullptr; cm.poptr_job = 0; cm.poptr_cap = 0;
+    // ALVRL_EVLOG=file: the developer event log of a -DALVRL_EVLOG build, written to file
+    cm.evlog = nullptr; cm.evlog_n = nullptr; cm.evlog_cap = 0;
+    const char* evf = std::getenv("ALVRL_EVLOG");
+    if (evf && evf[0]) {
+        cm.evlog_cap = 1u << 20;
+        if (hipMalloc(&cm.evlog, (size_t)cm.evlog_cap * 24 + 256) == hipSuccess) {
+            cm.evlog_n = reinterpret_cast<uint32_t*>(reinterpret_cast<unsigned char*>(cm.evlog) + (size_t)cm.evlog_cap * 24);
+            (void)hipMemsetAsync(cm.evlog_n, 0, 4, s);
+        } else {
+            cm.evlog = nullptr; cm.evlog_cap = 0;
+        }
+    }
     {
         const char* pt = std::getenv("ALVRL_POP_TRACE");
         if (pt && pt[0] == '1') {
@@ -5634,6 +5823,23 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
             }
             hipFree(cm.jtime);
         }
+    }
+    if (cm.evlog) {
+        uint32_t n = 0;
+        if (hipMemcpy(&n, cm.evlog_n, 4, hipMemcpyDeviceToHost) == hipSuccess) {
+            n = std::min(n, cm.evlog_cap);
+            std::vector<unsigned long long> ev((size_t)n * 3);
+            FILE* f = n && hipMemcpy(ev.data(), cm.evlog, ev.size() * 8, hipMemcpyDeviceToHost) == hipSuccess
+                          ? std::fopen(evf, "a") : nullptr;
+            if (f) {
+                std::fprintf(f, "# launch: %u jobs, %u events\n", njobs, n);
+                for (uint32_t i = 0; i < n; i++)
+                    std::fprintf(f, "%llu %u %u %u %u\n", ev[3 * i], (uint32_t)(ev[3 * i + 1] >> 32), (uint32_t)ev[3 * i + 1],
+                                 (uint32_t)(ev[3 * i + 2] >> 32), (uint32_t)ev[3 * i + 2]);
+                std::fclose(f);
+            }
+        }
+        hipFree(cm.evlog);
     }
     if (cm.poptr) {
         std::vector<uint32_t> pr((size_t)cm.poptr_cap * 8);

@@ -10,7 +10,7 @@ mkdir -p gpurun_out
 P="python -u -m pytest -x -v --timeout 300 --timeout-method thread"
 timeout -k 10 600 $P tests/test_gpu_sort.py > gpurun_out/sort_pytest1.log 2>&1 || { tail -30 gpurun_out/sort_pytest1.log; exit 1; }
 tail -2 gpurun_out/sort_pytest1.log
-ALVRL_SORT_RADIX_MIN=2 timeout -k 10 900 $P tests/test_gpu_parity.py tests/test_gpu_pipeline.py > gpurun_out/sort_pytest2.log 2>&1 || { tail -30 gpurun_out/sort_pytest2.log; exit 1; }
+ALVRL_SORT_RADIX_MIN=2 ALVRL_WS_WG_MIN=2 timeout -k 10 900 $P tests/test_gpu_parity.py tests/test_gpu_pipeline.py > gpurun_out/sort_pytest2.log 2>&1 || { tail -30 gpurun_out/sort_pytest2.log; exit 1; }
 tail -2 gpurun_out/sort_pytest2.log
 C="python tools/c5_share.py --res 1024 --vrls 100000 --world 8 --passes 2"
 for i in 1 2; do
