@@ -194,6 +194,8 @@ struct Common {
     unsigned long long wait_ticks; // bound of a leader's wait for a running helper (100 MHz ticks)
     uint32_t sort_radix_min;       // clusters of at least this many columns: radix8_sort
     uint32_t ws_wg_min;            // clusters of at least this many columns: weighted_sample_wg
+    int colw_all;                  // the leader divides all of a <= 256-row job's column weights (no
+                                   // helper half): launches that are not busy (ALVRL_COLW_ALL)
     unsigned long long* tstat;     // team counters (ALVRL_REFINE_TEAM_STATS=1), or null
     unsigned long long* jtime;     // with tstat: per job, wall ticks at start / end of refine / end
     unsigned long long* trace;     // host-mapped per-block (phase << 32 | value), ALVRL_REFINE_TRACE=1
@@ -2101,11 +2103,15 @@ __device__ __noinline__ void variance_part(const PartJob& pj, CC& cm_in, Ctl& C,
                 const uint32_t k = B * 8 + j;
                 if (k >= nch) break;
                 if (FU && k >= 1) store_totals(k - 1);
+#ifndef ALVRL_EXPP_NOCOEF
                 if (nbk < nblk) {
                     coef_chain8(W, cw_w, j, ncol_of(nbk), cWo, cWn);
                     if (j == 7 || k == nch - 1) coef_block_finish(C, cw_w, cWo, cWn, cw_v, ncol_of(nbk), &ring[nbk & 1]);
                 }
+#endif
+#ifndef ALVRL_EXPP_NOBAR
                 __syncthreads();
+#endif
             }
         }
         if (FU) store_totals(nch - 1);
@@ -2118,15 +2124,25 @@ __device__ __noinline__ void variance_part(const PartJob& pj, CC& cm_in, Ctl& C,
         auto load_chunk = [&](uint32_t k, float2* dst) {
             const uint32_t* ids = &ring[(k / 8) & 1].vrl[(k % 8) * kCH];
             const uint32_t cn = cn_of(k);
+#ifdef ALVRL_EXPP_NOLOAD
+#pragma unroll
+            for (int c = 0; c < kCH; c++) dst[c] = make_float2((float)ids[(uint32_t)c < cn ? c : 0] * 1e-7f + (float)lane * 1e-9f, 0.25f);
+#elif defined(ALVRL_EXPP_NOBAR)
+#pragma unroll
+            for (int c = 0; c < kCH; c++) dst[c] = ldg2(Rt, (size_t)min(ids[(uint32_t)c < cn ? c : 0], cm.nvrl - 1) * rstride);
+#else
 #pragma unroll
             for (int c = 0; c < kCH; c++) dst[c] = ldg2(Rt, (size_t)ids[(uint32_t)c < cn ? c : 0] * rstride);
+#endif
         };
         load_chunk(0, bufA);
         load_chunk(min(1u, nch - 1), bufB);
         auto step = [&](uint32_t k, float2* cur, float2* pre) {
             load_chunk(min(k + 2, nch - 1), pre);
             rec(k, cur, b0, lw0, sum0, M0, V0);
+#ifndef ALVRL_EXPP_NOBAR
             __syncthreads();
+#endif
         };
         for (uint32_t k = 0; k < nch; k += 3) {
             step(k, bufA, bufC);
@@ -2138,7 +2154,9 @@ __device__ __noinline__ void variance_part(const PartJob& pj, CC& cm_in, Ctl& C,
             gpw(pj.st)[2 * Rt_rows + grow] = V0;
         }
     } else {
+#ifndef ALVRL_EXPP_NOBAR
         for (uint32_t k = 0; k < nch; k++) __syncthreads();
+#endif
     }
     __syncthreads();
 }
@@ -4530,11 +4548,14 @@ __device__ void setup_tasks(CJ& J0_in, CJ& Jw_in, CC& cm_in, Ctl& C, bool)
     const uint32_t N = cm.nvrl;
     // where the leader divides a tall job's column weights (colw_parts) it takes them
     // all: a helper's half on one workgroup would be the setup's critical path
-    const bool cparts = cm.parts && cm.proj_min && N >= cm.proj_min && J0.nrows > 256 && cm.part_min_tall;
+    const bool cparts = cm.parts && cm.proj_min && N >= cm.proj_min &&
+                        (J0.nrows > 256 ? cm.part_min_tall : (cm.colw_all ? cm.part_min : 0u));
     if (!cparts && su_claim(T, kSuColw, C)) {
         if (threadIdx.x == 0) C.err = 0;
         __syncthreads();
+        EVLOG(cm, 6, N / 2, N);
         colw_raw(Jw, cm, C, N / 2, N);
+        EVLOG(cm, 7, N / 2, N);
         if (threadIdx.x == 0) st_rlx(&T.ctl[kSuColwErr], (uint32_t)C.err);
         su_publish(T, kSuColw);
     }
@@ -4766,15 +4787,28 @@ __device__ __noinline__ void colw_finish(CJ& J_in, CC& cm_in, Ctl& C)
     const uint32_t N = cm.nvrl;
     if (wave == 0) {
         // the running float sum in index order (one add after the other, as
-        // the reference's loop), 64 weights per load, broadcast by v_readlane
+        // the reference's loop), 64 weights per load, broadcast by v_readlane;
+        // 16 loads per lane issued at the top of each step and used within it
+        // (a load in flight across the loop's back edge costs a full drain)
         const auto* cwp = gp(J.colw);
         float acc = 0.0f;
-        float x = lane < N ? cwp[lane] : 0.0f;
-        for (uint32_t b = 0; b < N; b += 64) {
-            const float nx = b + 64 + lane < N ? cwp[b + 64 + lane] : 0.0f;
-            const uint32_t cnt = min(64u, N - b);
-            for (uint32_t c = 0; c < cnt; c++) acc += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), c));
-            x = nx;
+        constexpr uint32_t K = 16;
+        const uint32_t Nu = (uint32_t)__builtin_amdgcn_readfirstlane((int)N);
+        for (uint32_t b0 = 0; b0 < Nu; b0 += K * 64) {
+            float x[K];
+#pragma unroll
+            for (uint32_t k = 0; k < K; k++) x[k] = cwp[min(b0 + k * 64 + lane, Nu - 1)];
+#pragma unroll
+            for (uint32_t k = 0; k < K; k++) {
+                const uint32_t b = b0 + k * 64;
+                if (b >= Nu) break;
+                if (b + 64 <= Nu) {
+#pragma unroll
+                    for (int c = 0; c < 64; c++) acc += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x[k]), c));
+                } else {
+                    for (uint32_t c = 0; c < Nu - b; c++) acc += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x[k]), c));
+                }
+            }
         }
         if (lane == 0) {
             float avg = acc / N;
@@ -4918,7 +4952,7 @@ __global__ void __launch_bounds__(kThreads) k_refine(const ALVRL_AS4 JobDev* __r
     // column ranges on idle workgroups (colw_parts) for wide jobs: the
     // helper's half is claimed first so that nobody computes it twice
     const bool cparts = cm.parts && cm.proj_min && N >= cm.proj_min && (R > 256 ? cm.part_min_tall : cm.part_min);
-    if (tsu && cparts && R > 256 && su_claim(J.team, kSuColw, C)) {
+    if (tsu && cparts && (R > 256 || cm.colw_all) && su_claim(J.team, kSuColw, C)) {
         if (!colw_parts(J, cm, C, 0, N, pool)) colw_raw(J, cm, C, 0, N);
     } else if (tsu) {
         // the first half here, the second on the job's helper unless it
@@ -5622,6 +5656,8 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
         // per CU (C4 at N = 1: 305 against 312-320 ms with parts throughout)
         const char* ims = std::getenv("ALVRL_PART_IDLE_SHORT");
         cm.idle_min_short = ims ? (uint32_t)std::max(0, std::atoi(ims)) : (busy_launch ? 16u : cm.idle_min);
+        const char* ca = std::getenv("ALVRL_COLW_ALL");
+        cm.colw_all = ca ? (ca[0] == '1') : !busy_launch;
     }
     cm.part_min_tall = part_min_tall;
     {
