@@ -194,6 +194,7 @@ struct Common {
     unsigned long long wait_ticks; // bound of a leader's wait for a running helper (100 MHz ticks)
     uint32_t sort_radix_min;       // clusters of at least this many columns: radix8_sort
     uint32_t ws_wg_min;            // clusters of at least this many columns: weighted_sample_wg
+    int part_red;                  // variance parts of <= 3 row blocks: trees on reducer waves (ALVRL_PART_RED)
     int colw_all;                  // the leader divides all of a <= 256-row job's column weights (no
                                    // helper half): launches that are not busy (ALVRL_COLW_ALL)
     unsigned long long* tstat;     // team counters (ALVRL_REFINE_TEAM_STATS=1), or null
@@ -1978,7 +1979,16 @@ __device__ __noinline__ void variance_split_v3(CJ& J_in, CC& cm_in, Ctl& C, cons
 // block totals are bit-identical to the ones that engine adds.
 // FU = false (kPartInit): no prefix terms; the rows' final states go to
 // pj.st and wave 0 stores the total weight to pj.wsum (variance_split_v3<false>).
+// With nb <= 3 (FU) the halving trees leave the row waves: a row wave stores
+// its half chunks' terms to LDS, and reducer wave nb + 1 + b runs block b's
+// tree (the same tree8_transposed on the same values) one chunk later, so the
+// coefficient wave stores chunk k - 2's totals at chunk k.  A part runs one
+// wave per SIMD, where the trees' latency was the row wave's (var parts of a
+// 100k-column split: 10.6 ms, against 7.2 ms for the tree-less init parts).
 constexpr uint32_t kPartMaxBlk = 7;
+constexpr uint32_t kPartRedMax = 3;   // row blocks whose trees run on reducer waves
+static_assert(2 * kPartMaxBlk * 16 * sizeof(double) + 2 * sizeof(CoefBlock) + 2 * kPartRedMax * 2 * 8 * 64 * sizeof(double) <=
+                  kPoolBytes, "variance part: pool");
 template <bool FU>
 __device__ __noinline__ void variance_part(const PartJob& pj, CC& cm_in, Ctl& C, const double* Tout_c, uint32_t g,
                                            uint32_t gb0, uint32_t nb, unsigned char* pool)
@@ -1991,8 +2001,16 @@ __device__ __noinline__ void variance_part(const PartJob& pj, CC& cm_in, Ctl& C,
     const bool coefw = wv == 0;
     const uint32_t b0 = (uint32_t)wv - 1u;                       // row waves 1..nb: local block b0
     const bool roww = wv >= 1 && b0 < nb;
+    const bool red = FU && cm.part_red && nb <= kPartRedMax;     // trees on reducer waves nb+1..2nb
+    const uint32_t rb = (uint32_t)wv - 1u - nb;                  // a reducer's block
+    const bool redw = red && wv >= 1 + (int)nb && rb < nb;
     double* Q = reinterpret_cast<double*>(pool);                 // [k & 1][kPartMaxBlk][16]
     CoefBlock* ring = reinterpret_cast<CoefBlock*>(pool + 2 * kPartMaxBlk * 16 * sizeof(double));
+    // the row waves' terms for the reducers: [k & 1][block][half][8][lane]
+    auto* const TH = lp(reinterpret_cast<double*>(pool + 2 * kPartMaxBlk * 16 * sizeof(double) + 2 * sizeof(CoefBlock)));
+    auto th_at = [&](uint32_t k, uint32_t blk, uint32_t hsel, uint32_t i) {
+        return ((((k & 1u) * kPartRedMax + blk) * 2u + hsel) * 8u + i) * 64u + lane;
+    };
     const auto cwp = gp(pj.cw);
     const uint32_t nch = (m + kCH - 1) / kCH;
     const uint32_t nblk = (m + kCB64 - 1) / kCB64;
@@ -2044,6 +2062,11 @@ __device__ __noinline__ void variance_part(const PartJob& pj, CC& cm_in, Ctl& C,
         double th[kCH];
         auto half_done = [&](uint32_t hsel) {
             if (!FU) return;
+            if (red) {
+#pragma unroll
+                for (uint32_t i = 0; i < 8; i++) TH[th_at(k, blk, hsel, i)] = th[i];
+                return;
+            }
             const double z = tree8_transposed(th, lane);
             if ((lane & 7) == 0) {
                 const uint32_t h = lane >> 5, c = 4 * hsel + 2 * ((lane >> 3) & 1) + ((lane >> 4) & 1);
@@ -2102,7 +2125,8 @@ __device__ __noinline__ void variance_part(const PartJob& pj, CC& cm_in, Ctl& C,
             for (uint32_t j = 0; j < 8; j++) {
                 const uint32_t k = B * 8 + j;
                 if (k >= nch) break;
-                if (FU && k >= 1) store_totals(k - 1);
+                if (FU && !red && k >= 1) store_totals(k - 1);
+                if (red && k >= 2) store_totals(k - 2);
 #ifndef ALVRL_EXPP_NOCOEF
                 if (nbk < nblk) {
                     coef_chain8(W, cw_w, j, ncol_of(nbk), cWo, cWn);
@@ -2113,6 +2137,10 @@ __device__ __noinline__ void variance_part(const PartJob& pj, CC& cm_in, Ctl& C,
                 __syncthreads();
 #endif
             }
+        }
+        if (red) {   // the reducers' last chunk
+            if (nch >= 2) store_totals(nch - 2);
+            __syncthreads();
         }
         if (FU) store_totals(nch - 1);
         else if (lane == 0 && gb0 == 0) gpw(pj.wsum)[0] = W;
@@ -2149,13 +2177,37 @@ __device__ __noinline__ void variance_part(const PartJob& pj, CC& cm_in, Ctl& C,
             if (k + 1 < nch) step(k + 1, bufB, bufA);
             if (k + 2 < nch) step(k + 2, bufC, bufB);
         }
+        if (red) __syncthreads();
         if (!FU && grow < Rt_rows) {   // the row's final state (variance_split_v3<false>)
             gpw(pj.st)[Rt_rows + grow] = M0;
             gpw(pj.st)[2 * Rt_rows + grow] = V0;
         }
+    } else if (redw) {
+        // chunk k - 1's trees for block rb (half_done's tree and Q slots)
+        auto reduce = [&](uint32_t k) {
+#pragma unroll
+            for (uint32_t hsel = 0; hsel < 2; hsel++) {
+                double th[kCH];
+#pragma unroll
+                for (uint32_t i = 0; i < 8; i++) th[i] = TH[th_at(k, rb, hsel, i)];
+                const double z = tree8_transposed(th, lane);
+                if ((lane & 7) == 0) {
+                    const uint32_t h = lane >> 5, c = 4 * hsel + 2 * ((lane >> 3) & 1) + ((lane >> 4) & 1);
+                    Q[((size_t)(k & 1) * kPartMaxBlk + rb) * 16 + 2 * c + h] = z;
+                }
+            }
+        };
+        for (uint32_t k = 0; k < nch; k++) {
+            if (k >= 1) reduce(k - 1);
+#ifndef ALVRL_EXPP_NOBAR
+            __syncthreads();
+#endif
+        }
+        reduce(nch - 1);
+        __syncthreads();
     } else {
 #ifndef ALVRL_EXPP_NOBAR
-        for (uint32_t k = 0; k < nch; k++) __syncthreads();
+        for (uint32_t k = 0; k < nch + (red ? 1u : 0u); k++) __syncthreads();
 #endif
     }
     __syncthreads();
@@ -4129,17 +4181,45 @@ __device__ __noinline__ bool split_parts(CJ& J_in, CC& cm_in, Ctl& C, const uint
     if (!part_run_all(cm, C, (uint32_t)sl, pj, pool)) return true;
     EVLOG(cm, 21, m, pj.np);
     const double* const T = gp(&cm.parts[sl].T)[0];
-    for (uint32_t t = (uint32_t)tid; t < 4u * m; t += kThreads) {
+    // the block totals added in block order; up to 4 blocks, 8 sums per
+    // thread with all their loads issued before the adds (one round trip)
+    auto finish = [&](uint32_t t, double acc) {
         const uint32_t gh = t / m, n = t - gh * m, g = gh >> 1, h = gh & 1;
-        const auto* q = gp(T + (size_t)gh * nblk * m + n);
-        double acc = q[0];
-        for (uint32_t b = 1; b < nblk; b++) acc = acc + q[(size_t)b * m];
         const float f = (h == 0 && n == 0) ? 0.0f : (float)acc;
         float* const out = g == 0 ? (h == 0 ? fu0 : fi0) : (h == 0 ? fu1 : fi1);
         gpw(out)[n] = f;
         if (n == m - 1) {
             if (h == 0) C.vg[g].res_u = f; else C.vg[g].res_i = f;
             if (!isfinite(f) || f < 0) C.err = 1;
+        }
+    };
+    const uint32_t tot = 4u * m;
+    if (nblk <= 4) {
+        constexpr uint32_t U = 8;
+        for (uint32_t t0 = (uint32_t)tid; t0 < tot; t0 += U * kThreads) {
+            double x[4][U];
+#pragma unroll
+            for (uint32_t u = 0; u < U; u++) {
+                const uint32_t t = min(t0 + u * kThreads, tot - 1), gh = t / m, n = t - gh * m;
+                const auto* q = gp(T + (size_t)gh * nblk * m + n);
+#pragma unroll
+                for (uint32_t b = 0; b < 4; b++) x[b][u] = q[(size_t)min(b, nblk - 1) * m];
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < U; u++) {
+                double acc = x[0][u];
+#pragma unroll
+                for (uint32_t b = 1; b < 4; b++) acc = b < nblk ? acc + x[b][u] : acc;
+                if (t0 + u * kThreads < tot) finish(t0 + u * kThreads, acc);
+            }
+        }
+    } else {
+        for (uint32_t t = (uint32_t)tid; t < tot; t += kThreads) {
+            const uint32_t gh = t / m, n = t - gh * m;
+            const auto* q = gp(T + (size_t)gh * nblk * m + n);
+            double acc = q[0];
+            for (uint32_t b = 1; b < nblk; b++) acc = acc + q[(size_t)b * m];
+            finish(t, acc);
         }
     }
     EVLOG(cm, 22, m, 0);
@@ -5656,6 +5736,8 @@ int refine_jobs(hipStream_t s, const float* d_Rt, uint64_t ld, uint32_t nvrl, ui
         // per CU (C4 at N = 1: 305 against 312-320 ms with parts throughout)
         const char* ims = std::getenv("ALVRL_PART_IDLE_SHORT");
         cm.idle_min_short = ims ? (uint32_t)std::max(0, std::atoi(ims)) : (busy_launch ? 16u : cm.idle_min);
+        const char* pr = std::getenv("ALVRL_PART_RED");
+        cm.part_red = !(pr && pr[0] == '0');
         const char* ca = std::getenv("ALVRL_COLW_ALL");
         cm.colw_all = ca ? (ca[0] == '1') : !busy_launch;
     }
