@@ -260,6 +260,20 @@ struct Common {
 #else
 #define ALVRL_WS_INL __forceinline__
 #endif
+// the fused small split inlined into split(): one call boundary (and its
+// callee-saved register stores and reloads) less per small split, C4 refinement
+// 235.8 -> 232.9 ms (profiles/r05/inl/); ALVRL_FUSED_OUTLINE: a call
+#ifdef ALVRL_FUSED_OUTLINE
+#define ALVRL_FUSED_INL __noinline__
+#else
+#define ALVRL_FUSED_INL __forceinline__
+#endif
+// developer A/B: split() inlined into its callers (ALVRL_SPLIT_INLINE)
+#ifdef ALVRL_SPLIT_INLINE
+#define ALVRL_SPLIT_INL __forceinline__
+#else
+#define ALVRL_SPLIT_INL
+#endif
 #ifdef ALVRL_POP_INLINE
 #define ALVRL_POP_INL __forceinline__
 #else
@@ -3132,7 +3146,7 @@ __device__ __forceinline__ float readlane0_f(float x)
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 0));
 }
 template <bool XO>
-__device__ __noinline__ void split_fused(CJ& J_in, CC& cm_in, Ctl& C, uint32_t begin, uint32_t end,
+__device__ ALVRL_FUSED_INL void split_fused(CJ& J_in, CC& cm_in, Ctl& C, uint32_t begin, uint32_t end,
                                          unsigned long long* lds, Prof& pf, bool commit, SplitRes* res)
 {
     CJ& J = uni(J_in);
@@ -3521,7 +3535,7 @@ __device__ __noinline__ void split_fused(CJ& J_in, CC& cm_in, Ctl& C, uint32_t b
 // Clustering::split (:590-684), collective.
 // commit: push the two children (the leader); otherwise write the result to
 // *res (a helper working on J with its own scratch and vrls = team.spec)
-__device__ void split(CJ& J_in, CC& cm_in, Ctl& C, uint32_t begin, uint32_t end,
+__device__ ALVRL_SPLIT_INL void split(CJ& J_in, CC& cm_in, Ctl& C, uint32_t begin, uint32_t end,
                       unsigned long long* lds, Prof& pf, bool commit = true, SplitRes* res = nullptr)
 {
     CJ& J = uni(J_in);
