@@ -268,6 +268,13 @@ struct Common {
 #else
 #define ALVRL_FUSED_INL __forceinline__
 #endif
+// the profile marks inline: split() called them out of line (C4 refinement
+// 233.3-234.8 against 234.8-235.1 ms, profiles/r05/inl/); ALVRL_MARK_OUTLINE: calls
+#ifdef ALVRL_MARK_OUTLINE
+#define ALVRL_MARK_INL
+#else
+#define ALVRL_MARK_INL __forceinline__
+#endif
 // developer A/B: split() inlined into its callers (ALVRL_SPLIT_INLINE)
 #ifdef ALVRL_SPLIT_INLINE
 #define ALVRL_SPLIT_INL __forceinline__
@@ -363,7 +370,7 @@ struct Prof {
     unsigned long long* p;
     long long t;
     int sm;                      // small-split class of the split in progress (-1: none)
-    __device__ void mark(int id);
+    __device__ ALVRL_MARK_INL void mark(int id);
     __device__ void count(int id, unsigned long long v) { if (p && threadIdx.x == 0) gadd(&p[id], v); }
 };
 // split-size histogram after the phase totals: per log2(columns) bucket
@@ -373,7 +380,7 @@ constexpr int kPfWaveBusy = PF_N + 4 * kPfBuckets;   // per-wave busy cycles in 
 constexpr int kPfSmallAt = kPfWaveBusy + 6 * kWaves;   // [NB < 4 | NB == 4][busy, wall, reduce][wave]
 constexpr int kPfSmallPh = PF_ARGMIN - PF_WSAMP + 1;
 constexpr int kPfTotal = kPfSmallAt + kPfSmall * kPfSmallPh;
-__device__ void Prof::mark(int id)
+__device__ ALVRL_MARK_INL void Prof::mark(int id)
 {
     if (p && threadIdx.x == 0) {
         const long long now = clock64();
