@@ -260,10 +260,17 @@ struct Common {
 #else
 #define ALVRL_WS_INL __forceinline__
 #endif
-// the fused small split inlined into split(): one call boundary (and its
-// callee-saved register stores and reloads) less per small split, C4 refinement
-// 235.8 -> 232.9 ms (profiles/r05/inl/); ALVRL_FUSED_OUTLINE: a call
-#ifdef ALVRL_FUSED_OUTLINE
+// Small splits and their call frames (profiles/r05/inl/): split() is an inline
+// dispatcher that calls split_fused (2-17 callee-saved VGPR stores) or
+// split_big (41) directly, so a small split no longer enters the large path's
+// frame: C4 refinement 232.2 against 230.0 ms (four interleaved pairs), after
+// split_fused inlined into a one-function split() had taken 235.8 to 232.9 ms.
+// ALVRL_SPLIT_NODISPATCH: the one-function split() (split_fused inlined unless
+// ALVRL_FUSED_OUTLINE)
+#ifndef ALVRL_SPLIT_NODISPATCH
+#define ALVRL_SPLIT_DISPATCH
+#endif
+#if defined(ALVRL_FUSED_OUTLINE) || defined(ALVRL_SPLIT_DISPATCH)
 #define ALVRL_FUSED_INL __noinline__
 #else
 #define ALVRL_FUSED_INL __forceinline__
@@ -3542,6 +3549,14 @@ __device__ ALVRL_FUSED_INL void split_fused(CJ& J_in, CC& cm_in, Ctl& C, uint32_
 // Clustering::split (:590-684), collective.
 // commit: push the two children (the leader); otherwise write the result to
 // *res (a helper working on J with its own scratch and vrls = team.spec)
+#ifdef ALVRL_SPLIT_DISPATCH
+// (split() below is the inline dispatcher; ALVRL_SPLIT_NODISPATCH: this body is split())
+__device__ __noinline__ void split_big(CJ& J_in, CC& cm_in, Ctl& C, uint32_t begin, uint32_t end,
+                                       unsigned long long* lds, Prof& pf, bool commit, SplitRes* res)
+{
+    CJ& J = uni(J_in);
+    CC& cm = uni(cm_in);
+#else
 __device__ ALVRL_SPLIT_INL void split(CJ& J_in, CC& cm_in, Ctl& C, uint32_t begin, uint32_t end,
                       unsigned long long* lds, Prof& pf, bool commit = true, SplitRes* res = nullptr)
 {
@@ -3557,6 +3572,7 @@ __device__ ALVRL_SPLIT_INL void split(CJ& J_in, CC& cm_in, Ctl& C, uint32_t begi
             return;
         }
     }
+#endif
     pf.mark(PF_CTRL);
     pf.count(PF_NSPLIT, 1);
     pf.count(PF_SPLITCOLS, end - begin);
@@ -3753,6 +3769,25 @@ __device__ ALVRL_SPLIT_INL void split(CJ& J_in, CC& cm_in, Ctl& C, uint32_t begi
         gadd(&pf.p[PF_N + 4 * b + 3], (unsigned long long)hbp);
     }
 }
+#ifdef ALVRL_SPLIT_DISPATCH
+__device__ __forceinline__ void split(CJ& J_in, CC& cm_in, Ctl& C, uint32_t begin, uint32_t end,
+                                      unsigned long long* lds, Prof& pf, bool commit = true, SplitRes* res = nullptr)
+{
+    CJ& J = uni(J_in);
+    CC& cm = uni(cm_in);
+    if (cm.split_fused && cm.var_small) {
+        if (fused_fits<false>(end - begin, J.nrows)) {
+            split_fused<false>(J, cm, C, begin, end, lds, pf, commit, res);
+            return;
+        }
+        if (cm.split_fused > 1 && fused_fits<true>(end - begin, J.nrows)) {
+            split_fused<true>(J, cm, C, begin, end, lds, pf, commit, res);
+            return;
+        }
+    }
+    split_big(J, cm, C, begin, end, lds, pf, commit, res);
+}
+#endif
 
 // ------------------------------------------------------- team mode --
 __device__ __forceinline__ unsigned long long ld_acq(unsigned long long* p)
