@@ -253,8 +253,18 @@ ALVRL_API int alvrl_set_strict_rbuild(alvrl_ctx *ctx, int on);
 
 /* csrc/detmath.h on the current device, elementwise over n floats (device
  * pointers; fn 0 exp, 1 log, 2 atan, 3 tan, 4 asinh, 5 sinh): the host =
- * device check of the definitions the strict paths share with the oracle. */
+ * device check of the definitions the strict paths share with the oracle.
+ * fn + 8 (8, 10-13) evaluates the strict kernels' fast form
+ * (csrc/detmath_fast.h) instead. */
 ALVRL_API int alvrl_detmath_eval(int fn, const float *d_in, float *d_out, uint32_t n, void *stream);
+
+/* The fast form against detmath.h for every float bit pattern in [begin, end)
+ * (end <= 2^32), on the current device, synchronous: *mismatches = the number
+ * of inputs whose results differ in any bit, first[0 .. min(nfirst, 16)) =
+ * some of them (0xFFFFFFFF past the last).  fn 0 exp, 2 atan, 3 tan,
+ * 4 asinh, 5 sinh. */
+ALVRL_API int alvrl_detmath_exhaustive(int fn, uint64_t begin, uint64_t end, uint64_t *mismatches,
+                                       uint32_t *first, uint32_t nfirst);
 
 /* ---- hot path (b) part 2: cluster refinement ------------------------- */
 /* One Clustering (Preprocessor.cpp:287-720): ctor (column weights, initial

@@ -112,6 +112,7 @@ def lib() -> C.CDLL:
     L.alvrl_set_strict_rbuild.argtypes = [vp, i32]
     L.alvrl_host_batch_stats.argtypes = [vp, P(u64), P(u64)]
     L.alvrl_detmath_eval.argtypes = [i32, vp, vp, u32, vp]
+    L.alvrl_detmath_exhaustive.argtypes = [i32, u64, u64, P(u64), P(u32), u32]
     _lib = L
     return L
 
@@ -149,6 +150,23 @@ def detmath_eval(fn: str, d_in, d_out, stream=None):
     float32 CUDA tensors (alvrl_detmath_eval)."""
     _check(lib().alvrl_detmath_eval(DETMATH_FNS.index(fn), _ptr(d_in), _ptr(d_out), int(d_in.numel()),
                                     C.c_void_p(stream) if stream else None))
+
+
+def detmath_fast_eval(fn: str, d_in, d_out, stream=None):
+    """The strict kernels' fast form of detmath.h's `fn` (csrc/detmath_fast.h,
+    fn in exp/atan/tan/asinh/sinh) on the device, elementwise."""
+    _check(lib().alvrl_detmath_eval(8 + DETMATH_FNS.index(fn), _ptr(d_in), _ptr(d_out), int(d_in.numel()),
+                                    C.c_void_p(stream) if stream else None))
+
+
+def detmath_exhaustive(fn: str, begin: int = 0, end: int = 1 << 32):
+    """detmath_fast.h against detmath.h on every float bit pattern in
+    [begin, end) (alvrl_detmath_exhaustive): (number of inputs whose results
+    differ, some of those inputs as uint32 bit patterns)."""
+    mism = C.c_uint64(0)
+    first = (C.c_uint32 * 16)()
+    _check(lib().alvrl_detmath_exhaustive(DETMATH_FNS.index(fn), int(begin), int(end), C.byref(mism), first, 16))
+    return int(mism.value), [int(x) for x in first if x != 0xFFFFFFFF]
 
 
 def _check(rc: int):

@@ -45,11 +45,15 @@ hipError_t launch_build_R_blocks(const Rec* recs, const uint32_t* ids, uint32_t 
                                  uint32_t nvrl, const DevParams& P, float normalization, float2* Rt,
                                  const uint64_t* roff, const uint32_t* rstride, uint8_t* nonzero,
                                  unsigned long long* counter, hipStream_t s);
-hipError_t launch_build_R_strict(const Rec* recs, const uint32_t* ids, uint32_t nrows, const float* soa,
+hipError_t launch_build_R_strict(const Rec* recs, const uint32_t* ids, uint32_t nrows, const void* svrl,
                                  uint32_t nvrl, const DevParams& P, float normalization, float2* Rt, uint64_t ld,
                                  uint64_t row0, const uint64_t* roff, const uint32_t* rstride, uint8_t* nonzero,
                                  unsigned long long* counter, hipStream_t s);
 hipError_t launch_detmath(int fn, const float* in, float* out, uint32_t n, hipStream_t s);
+hipError_t launch_detmath_exhaustive(int fn, uint64_t begin, uint64_t end, unsigned long long* out,
+                                     uint32_t* first, hipStream_t s);
+size_t strict_vrl_bytes();
+hipError_t launch_prepare_strict(const float* soa, uint32_t n, void* out, hipStream_t s);
 hipError_t launch_false_color(const Rec* recs, const WorkItem* items, uint32_t n, int mode,
                               const uint32_t* slice_off, uint32_t n_fb, uint32_t nvrl, float* out,
                               unsigned long long* counter, hipStream_t s);
@@ -160,6 +164,7 @@ struct alvrl_ctx {
     hipStream_t stream = nullptr;
     float* d_soa = nullptr;
     VrlPrep* d_vrl = nullptr;
+    void* d_svrl = nullptr;   // the strict R build's per-VRL values (rbuild_strict.hip StrictVrl)
     uint32_t nvrl = 0, cap_vrl = 0;
     uint64_t particle_count = 0;
     unsigned long long* d_counter = nullptr;   // [0] preprocess, [1] render
@@ -322,7 +327,7 @@ ALVRL_API void alvrl_ctx_destroy(alvrl_ctx* c)
     if (!c) return;
     hipSetDevice(c->cfg.device);
     if (c->stream) hipStreamSynchronize(c->stream);
-    hipFree(c->d_soa); hipFree(c->d_vrl); hipFree(c->d_counter);
+    hipFree(c->d_soa); hipFree(c->d_vrl); hipFree(c->d_svrl); hipFree(c->d_counter);
     free_clusters(c);
     free_occluders(c);
     c->refine_arenas.release();
@@ -403,10 +408,11 @@ ALVRL_API int alvrl_upload_vrls(alvrl_ctx* c, const float* soa, uint32_t n, uint
     // caller's included) may still read the previous pass's
     HIPCHK(hipDeviceSynchronize());
     if (n > c->cap_vrl) {
-        hipFree(c->d_soa); hipFree(c->d_vrl);
-        c->d_soa = nullptr; c->d_vrl = nullptr; c->cap_vrl = 0;
+        hipFree(c->d_soa); hipFree(c->d_vrl); hipFree(c->d_svrl);
+        c->d_soa = nullptr; c->d_vrl = nullptr; c->d_svrl = nullptr; c->cap_vrl = 0;
         HIPCHK(hipMalloc(&c->d_soa, sizeof(float) * 9 * (size_t)n));
         HIPCHK(hipMalloc(&c->d_vrl, sizeof(VrlPrep) * (size_t)n));
+        HIPCHK(hipMalloc(&c->d_svrl, strict_vrl_bytes() * (size_t)n));
         c->cap_vrl = n;
     }
     if (n) {
@@ -414,6 +420,7 @@ ALVRL_API int alvrl_upload_vrls(alvrl_ctx* c, const float* soa, uint32_t n, uint
         HIPCHK(hipMemcpyAsync(c->d_soa, soa, sizeof(float) * 9 * (size_t)n,
                               on_dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, c->stream));
         HIPCHK(launch_prepare_vrls(c->d_soa, n, c->d_vrl, c->stream));
+        HIPCHK(launch_prepare_strict(c->d_soa, n, c->d_svrl, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
     }
     c->nvrl = n;
@@ -573,7 +580,7 @@ ALVRL_API int alvrl_build_R(alvrl_ctx* c, const alvrl_gather_rec* d_recs, const 
     SLOT(c, ts);
     HIPCHK(hipEventRecord(ts->ev0, s));
     if (c->strict_rb)
-        HIPCHK(launch_build_R_strict(reinterpret_cast<const Rec*>(d_recs), d_ids, nrows, c->d_soa, c->nvrl, c->P,
+        HIPCHK(launch_build_R_strict(reinterpret_cast<const Rec*>(d_recs), d_ids, nrows, c->d_svrl, c->nvrl, c->P,
                                      norm, reinterpret_cast<float2*>(d_Rt), ld, row0, nullptr, nullptr, nullptr,
                                      c->d_counter + 0, s));
     else
@@ -603,9 +610,37 @@ ALVRL_API int alvrl_set_strict_rbuild(alvrl_ctx* c, int on)
 
 ALVRL_API int alvrl_detmath_eval(int fn, const float* d_in, float* d_out, uint32_t n, void* stream)
 {
-    if (fn < 0 || fn > 5) return fail(ALVRL_ERR_INVALID, "alvrl_detmath_eval: fn must be in [0, 5]");
+    if (fn < 0 || fn > 13 || (fn > 5 && fn < 8) || fn == 9)
+        return fail(ALVRL_ERR_INVALID, "alvrl_detmath_eval: fn must be in [0, 5] or 8, 10-13");
     if (n && (!d_in || !d_out)) return fail(ALVRL_ERR_INVALID, "alvrl_detmath_eval: null buffer");
     HIPCHK(launch_detmath(fn, d_in, d_out, n, (hipStream_t)stream));
+    return ALVRL_OK;
+}
+
+ALVRL_API int alvrl_detmath_exhaustive(int fn, uint64_t begin, uint64_t end, uint64_t* mismatches,
+                                       uint32_t* first, uint32_t nfirst)
+{
+    if (fn != 0 && (fn < 2 || fn > 5))
+        return fail(ALVRL_ERR_INVALID, "alvrl_detmath_exhaustive: fn must be 0 or in [2, 5]");
+    if (end > (1ull << 32) || begin > end) return fail(ALVRL_ERR_INVALID, "alvrl_detmath_exhaustive: bad range");
+    if (!mismatches) return fail(ALVRL_ERR_INVALID, "alvrl_detmath_exhaustive: null output");
+    unsigned long long* d_out = nullptr;
+    uint32_t* d_first = nullptr;
+    HIPCHK(hipMalloc(&d_out, 2 * sizeof(unsigned long long)));
+    hipError_t e = hipMalloc(&d_first, 16 * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMemset(d_out, 0, 2 * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMemset(d_first, 0xFF, 16 * sizeof(uint32_t));
+    if (e == hipSuccess) e = launch_detmath_exhaustive(fn, begin, end, d_out, d_first, nullptr);
+    unsigned long long h[2] = {0, 0};
+    uint32_t hf[16];
+    if (e == hipSuccess) e = hipMemcpy(h, d_out, sizeof(h), hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(hf, d_first, sizeof(hf), hipMemcpyDeviceToHost);
+    hipFree(d_out);
+    hipFree(d_first);
+    HIPCHK(e);
+    *mismatches = h[0];
+    if (first)
+        for (uint32_t i = 0; i < nfirst && i < 16; i++) first[i] = hf[i];
     return ALVRL_OK;
 }
 
@@ -624,7 +659,7 @@ ALVRL_API int alvrl_build_R_blocks(alvrl_ctx* c, const alvrl_gather_rec* d_recs,
     SLOT(c, ts);
     HIPCHK(hipEventRecord(ts->ev0, s));
     if (c->strict_rb)
-        HIPCHK(launch_build_R_strict(reinterpret_cast<const Rec*>(d_recs), d_ids, nrows, c->d_soa, c->nvrl, c->P,
+        HIPCHK(launch_build_R_strict(reinterpret_cast<const Rec*>(d_recs), d_ids, nrows, c->d_svrl, c->nvrl, c->P,
                                      norm, reinterpret_cast<float2*>(d_Rt), 0, 0, d_row_off, d_row_stride,
                                      d_nonzero, c->d_counter + 0, s));
     else

@@ -1,5 +1,5 @@
 // rbuild_strict.hip -- the R build in the oracle's arithmetic (integrator
-// property strictRbuild, alvrl_set_strict_rbuild).
+// property strictRbuild, alvrl_set_strict_rbuild; the default pipeline).
 //
 // getLiLuminanceVrlContributions (vrlIntegrator.cpp:527-539) through
 // integrateVRL's mean / variance outputs (:603-785) and its samplers
@@ -9,24 +9,27 @@
 // (oracle/alvrl_oracle.c integrate_vrl_w): IEEE float division and sqrt, no
 // contraction (this file is built with -ffp-contract=off and without the
 // gathers' approximate division), and the transcendentals of detmath.h, which
-// the oracle shares.  Its R entries are the oracle's bit for bit, so the
-// discrete clustering decisions downstream (already bit-exact given the same R,
-// refine.hip) follow the oracle's own pipeline (tests/test_gpu_strict.py).
+// the oracle shares -- evaluated here through detmath_fast.h, which returns
+// detmath.h's float for every one of the 2^32 inputs (checked exhaustively
+// on the device, k_detmath_exhaustive).  Its R entries are the oracle's bit for
+// bit, so the discrete clustering decisions downstream (bit-exact given the
+// same R, refine.hip) follow the oracle's own pipeline (tests/test_gpu_strict.py).
 //
-// The fast build (gather.hip k_build_R_blocks) keeps the reduced forms and the
-// hardware transcendentals and matches the oracle on the error distribution
-// stated in tests/test_gpu_parity.py; its clusters may then differ from the
-// oracle's where R rounds differently.
-//
-// Values the oracle recomputes but that are identical by construction (the
-// row's eye segment and vol->surf transmittance, a pair's closest points and
-// asinh bounds, the pdf and transmittance exponentials of one distance) are
-// evaluated once: the same operations on the same operands give the same bits.
+// Execution model (as gather.hip's k_build_R_blocks): lane = representative
+// row, the VRL is wave-uniform and its prepared record (StrictVrl: the
+// VRL-only values the restatement derives, computed by the same operations
+// once per VRL) is read with scalar loads; the row's own values are hoisted
+// out of the VRL loop.  Values the oracle recomputes but that are identical by
+// construction (the row's eye segment and vol->surf transmittance, a pair's
+// closest points and asinh bounds, |U - V| for the shadow ray, the pdf and
+// transmittance exponentials of one distance) are evaluated once: the same
+// operations on the same operands give the same bits.
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
 
 #include "detmath.h"
+#include "detmath_fast.h"
 #include "vrl_device.hpp"
 
 namespace alvrl {
@@ -49,8 +52,56 @@ __device__ __forceinline__ V3 nrm(V3 a) { const float r = 1.0f / len(a); return 
 constexpr float kEps = 1e-4f;
 constexpr uint32_t kFlagHit = 1u, kFlagSmooth = 2u, kFlagMedium = 4u;
 
-// Random-access draw k of the counter stream (dom, a, b, c), one Philox
-// block of four cached (oracle draw()).
+// The transcendentals of one evaluation: FAST = detmath_fast.h's flag-raising
+// forms (a lane whose flag is set re-evaluates its R entry with FAST = false),
+// otherwise detmath.h itself.
+template <bool FAST>
+struct Tx {
+    static __device__ __forceinline__ float exp(float x, bool& s) { return FAST ? fx_expf_r(x, s) : dm_expf(x); }
+    static __device__ __forceinline__ float atan(float x, bool& s) { return FAST ? fx_atanf_r(x, s) : dm_atanf(x); }
+    static __device__ __forceinline__ float tan(float x, bool& s) { return FAST ? fx_tanf_r(x, s) : dm_tanf(x); }
+    static __device__ __forceinline__ float asinh(float x, bool& s) { return FAST ? fx_asinhf_r(x, s) : dm_asinhf(x); }
+    static __device__ __forceinline__ float sinh(float x, bool& s) { return FAST ? fx_sinhf_r(x, s) : dm_sinhf(x); }
+};
+
+// The VRL-only values of integrate_vrl_w, by the restatement's own operations
+// (k_prepare_strict).  128 B: two s_load_dwordx16.
+struct __attribute__((aligned(16))) StrictVrl {
+    float sx, sy, sz, ex, ey, ez;   // m_start, m_end
+    float pr, pg, pb;               // m_power
+    float dx, dy, dz;               // normalize(End - S) (SV, Novak's dirSE, the vol->surf Kulla direction)
+    float vx, vy, vz;               // End - S (closest points' v)
+    float c;                        // dot(v, v) = len2(v)
+    float dSE;                      // distance(S, End)
+    float invlen;                   // 1 / distance(End, S)
+    float pad[13];
+};
+static_assert(sizeof(StrictVrl) == 128, "StrictVrl layout");
+
+__global__ void __launch_bounds__(256) k_prepare_strict(const float* __restrict__ soa, uint32_t n,
+                                                        StrictVrl* __restrict__ out)
+{
+    const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= n) return;
+    const V3 S = mk(soa[0 * (size_t)n + v], soa[1 * (size_t)n + v], soa[2 * (size_t)n + v]);
+    const V3 End = mk(soa[3 * (size_t)n + v], soa[4 * (size_t)n + v], soa[5 * (size_t)n + v]);
+    StrictVrl o;
+    o.sx = S.x; o.sy = S.y; o.sz = S.z; o.ex = End.x; o.ey = End.y; o.ez = End.z;
+    o.pr = soa[6 * (size_t)n + v]; o.pg = soa[7 * (size_t)n + v]; o.pb = soa[8 * (size_t)n + v];
+    const V3 sv = nrm(sub(End, S));
+    o.dx = sv.x; o.dy = sv.y; o.dz = sv.z;
+    const V3 vv = sub(End, S);
+    o.vx = vv.x; o.vy = vv.y; o.vz = vv.z;
+    o.c = dot(vv, vv);
+    o.dSE = dist(S, End);
+    o.invlen = 1 / dist(End, S);
+    for (int i = 0; i < 13; i++) o.pad[i] = 0.0f;
+    out[v] = o;
+}
+
+// Draw k of the counter stream (dom, a, b, c): one Philox block of four per
+// four draws (oracle draw()).  With a compile-time sample count and
+// Rsamples = 1 every k is a constant and the block cache folds away.
 struct Draws {
     uint32_t a, b, c, seed, pass, blk;
     U4 buf;
@@ -67,30 +118,33 @@ struct Draws {
 };
 
 // MaxExpDist::cdf (maxexp.h:83-94)
-__device__ __forceinline__ float mxexp_cdf(const DevParams& P, float t)
+template <bool FAST>
+__device__ __forceinline__ float mxexp_cdf(const DevParams& P, float t, bool& slow)
 {
     int k = 0;
     while (k < 3 && P.mx_start[k] < t) k++;
     const int i = k > 0 ? k - 1 : 0;
-    const float upper = -dm_expf(-P.mx_sigma[i] * t);
+    const float upper = -Tx<FAST>::exp(-P.mx_sigma[i] * t, slow);
     return P.mx_cdf[i] + (upper - P.mx_lower[i]) * P.mx_inv_norm;
 }
 
 // HomogeneousMedium::eval (homogeneous.cpp:354-396): transmittance and the
 // pdfFailure of the sampling strategy
-__device__ __forceinline__ void medium_eval(const DevParams& P, float distance, float tr[3], float* pdf_failure)
+template <bool FAST>
+__device__ __forceinline__ void medium_eval(const DevParams& P, float distance, float tr[3], float* pdf_failure,
+                                            bool& slow)
 {
-    const float e0 = dm_expf(P.sigma_t[0] * (-distance));
-    const float e1 = dm_expf(P.sigma_t[1] * (-distance));
-    const float e2 = dm_expf(P.sigma_t[2] * (-distance));
+    const float e0 = Tx<FAST>::exp(P.sigma_t[0] * (-distance), slow);
+    const float e1 = Tx<FAST>::exp(P.sigma_t[1] * (-distance), slow);
+    const float e2 = Tx<FAST>::exp(P.sigma_t[2] * (-distance), slow);
     float pf = 0.0f;
     if (P.strategy == 0) {
         pf += e0; pf += e1; pf += e2;
         pf /= 3;
     } else if (P.strategy == 3) {
-        pf = 1 - mxexp_cdf(P, distance);
+        pf = 1 - mxexp_cdf<FAST>(P, distance, slow);
     } else {
-        pf = dm_expf(-P.density * distance);
+        pf = Tx<FAST>::exp(-P.density * distance, slow);
     }
     tr[0] = e0; tr[1] = e1; tr[2] = e2;
     *pdf_failure = pf * P.w + (1 - P.w);
@@ -100,14 +154,18 @@ __device__ __forceinline__ void medium_eval(const DevParams& P, float distance, 
 }
 
 // Scene::evalTransmittance(p1, p1OnSurface, p2): exp(-sigma_t |p2 - p1|) per
-// channel, zero when an occluder (not a null surface) lies on the segment
-__device__ __forceinline__ void shadow_transmittance(const DevParams& P, V3 p1, bool p1_surface, V3 p2, float tr[3])
+// channel, zero when an occluder (not a null surface) lies on the segment.
+// `remaining` = |p2 - p1|, which the caller has as distance(p1, p2) (the
+// squares of negated components are the same floats).
+template <bool FAST, bool OCC>
+__device__ __forceinline__ void shadow_transmittance(const DevParams& P, V3 p1, bool p1_surface, V3 p2,
+                                                     float remaining, float tr[3], bool& slow)
 {
-    const V3 d = sub(p2, p1);
-    const float remaining = len(d);
     const float negLength = 0.0f - remaining;
-    for (int i = 0; i < 3; i++) tr[i] = P.sigma_t[i] != 0 ? dm_expf(P.sigma_t[i] * negLength) : 1.0f;
+    for (int i = 0; i < 3; i++) tr[i] = P.sigma_t[i] != 0 ? Tx<FAST>::exp(P.sigma_t[i] * negLength, slow) : 1.0f;
+    if (!OCC) return;
     if (P.occ.ntri == 0 || !(remaining > 0)) return;
+    const V3 d = sub(p2, p1);
     const V3 dn = scl(d, 1.0f / remaining);
     const float mint = p1_surface ? 1e-4f : 0.0f;
     const float maxt = remaining * 1.0f;
@@ -124,15 +182,25 @@ __device__ __forceinline__ float phase_eval(const DevParams& P, V3 wi, V3 wo)
     return kInvFourPi * (1 - g * g) / (temp * sqrtf(temp));
 }
 
-// getClosestPoints (vrlIntegrator.cpp:962-1032); returns |dP| and the closest
-// point on the second segment
-__device__ __forceinline__ float closest_points(V3 S1P0, V3 S1P1, V3 S2P0, V3 S2P1, V3* S2h)
+// the row's eye segment: everything integrateVRL derives without the VRL
+struct Row {
+    V3 E, d, U, n, B, dirAB, nd, u;
+    float alb[3], wt[3], teus[3], cos_wi;
+    float dAB;              // distance(A, B) (Kulla on the eye segment, A = E)
+    float a_uu, eps_luu;    // closest points: dot(u, u), kEps * len2(u)
+    uint32_t flags, rid, sw;
+    bool surf;
+};
+
+// getClosestPoints (vrlIntegrator.cpp:962-1032) for S1 = the eye segment E ->
+// hit, S2 = the VRL; returns |dP| and the closest point on the VRL
+__device__ __forceinline__ float closest_points(const Row& w, V3 S, const V3& vv, float c, V3* S2h)
 {
-    const V3 u = sub(S1P1, S1P0), v = sub(S2P1, S2P0), w = sub(S1P0, S2P0);
-    const float a = dot(u, u), b = dot(u, v), c = dot(v, v), d = dot(u, w), e = dot(v, w);
+    const V3 u = w.u, v = vv, wv = sub(w.E, S);
+    const float a = w.a_uu, b = dot(u, v), d = dot(u, wv), e = dot(v, wv);
     const float D = a * c - b * b;
     float sN, sD = D, tN, tD = D;
-    if (D < kEps * len2(u) * len2(v)) {
+    if (D < w.eps_luu * c) {
         sN = 0.0f; sD = 1.0f; tN = e; tD = c;
     } else {
         sN = (b * e - c * d);
@@ -153,8 +221,8 @@ __device__ __forceinline__ float closest_points(V3 S1P0, V3 S1P1, V3 S2P0, V3 S2
     }
     const float sc = sN / sD;
     const float tc = tN / tD;
-    const V3 dP = sub(add(w, scl(u, sc)), scl(v, tc));
-    *S2h = add(S2P0, scl(sub(S2P1, S2P0), tc));
+    const V3 dP = sub(add(wv, scl(u, sc)), scl(v, tc));
+    *S2h = add(S, scl(v, tc));
     return len(dP);
 }
 
@@ -162,26 +230,29 @@ __device__ __forceinline__ float closest_points(V3 S1P0, V3 S1P1, V3 S2P0, V3 S2
 // segment A->B and the point D, and the per-uniform sample
 struct Kulla { V3 dir, I; float Dis, aa, ab; };
 
-__device__ __forceinline__ Kulla kulla_frame(V3 A, V3 B, V3 dir, V3 D)
+template <bool FAST>
+__device__ __forceinline__ Kulla kulla_frame(V3 A, V3 B, V3 dir, float dAB, V3 D, bool& slow)
 {
     Kulla k;
     k.dir = dir;
     const float dotPr = dot(dir, sub(D, A));
     k.I = add(A, scl(dir, dotPr));
     k.Dis = dist(D, k.I);
-    float angle_a = dm_atanf(dist(A, k.I) / k.Dis);
-    float angle_b = dm_atanf(dist(k.I, B) / k.Dis);
+    const float dAI = dist(A, k.I);
+    float angle_a = Tx<FAST>::atan(dAI / k.Dis, slow);
+    float angle_b = Tx<FAST>::atan(dist(k.I, B) / k.Dis, slow);
     if (dotPr > 0) {
         angle_a *= -1;
-        if (dist(A, k.I) > dist(A, B)) angle_b *= -1;
+        if (dAI > dAB) angle_b *= -1;
     }
     k.aa = angle_a; k.ab = angle_b;
     return k;
 }
 
-__device__ __forceinline__ float kulla_sample(const Kulla& k, float uniform, V3* result)
+template <bool FAST>
+__device__ __forceinline__ float kulla_sample(const Kulla& k, float uniform, V3* result, bool& slow)
 {
-    const float t = k.Dis * dm_tanf(((1.0f - uniform) * k.aa) + (uniform * k.ab));
+    const float t = k.Dis * Tx<FAST>::tan(((1.0f - uniform) * k.aa) + (uniform * k.ab), slow);
     const float pdf = k.Dis / ((k.ab - k.aa) * (k.Dis * k.Dis + t * t));
     *result = add(k.I, scl(k.dir, t));
     return pdf;
@@ -190,56 +261,48 @@ __device__ __forceinline__ float kulla_sample(const Kulla& k, float uniform, V3*
 // sampleVtoDistance (vrlIntegrator.cpp:916-953), the uniform-free part
 struct Novak {
     int mode;           // 0: zero-length VRL, 1: parallel (uniform on the VRL), 2: Novak
-    float invlen;       // 1 / distance(End, S) (mode 1)
     float h, sinTheta, A0, A1, denom, dVhS;
-    V3 dirSE;           // normalize(End - S)
 };
 
-__device__ __forceinline__ Novak novak_frame(V3 E, V3 d, V3 hitp, V3 S, V3 End)
+template <bool FAST>
+__device__ __forceinline__ Novak novak_frame(const Row& w, V3 S, V3 End, V3 SE, const V3& vv, float c, float dSE,
+                                             bool& slow)
 {
     Novak n;
     n.mode = 0;
-    if (dist(S, End) == 0) return n;
-    const float cosTheta = dot(nrm(d), nrm(sub(End, S)));
+    if (dSE == 0) return n;
+    const float cosTheta = dot(w.nd, SE);
     const float st2 = 1 - cosTheta * cosTheta;
     n.sinTheta = sqrtf(st2 > 0.0f ? st2 : 0.0f);
     if (n.sinTheta < kEps) {
         n.mode = 1;
-        n.invlen = 1 / dist(End, S);
         return n;
     }
     n.mode = 2;
     V3 Vh;
-    n.h = closest_points(E, hitp, S, End, &Vh);
-    const float V0c = -1 * dist(Vh, S);
-    const float V1c = dist(Vh, End);
-    n.A0 = dm_asinhf((V0c / n.h) * n.sinTheta);
-    n.A1 = dm_asinhf((V1c / n.h) * n.sinTheta);
-    n.denom = (n.A1 - n.A0) / n.sinTheta;
+    n.h = closest_points(w, S, vv, c, &Vh);
     n.dVhS = dist(Vh, S);
-    n.dirSE = nrm(sub(End, S));
+    const float V0c = -1 * n.dVhS;
+    const float V1c = dist(Vh, End);
+    n.A0 = Tx<FAST>::asinh((V0c / n.h) * n.sinTheta, slow);
+    n.A1 = Tx<FAST>::asinh((V1c / n.h) * n.sinTheta, slow);
+    n.denom = (n.A1 - n.A0) / n.sinTheta;
     return n;
 }
 
-__device__ __forceinline__ float novak_sample(const Novak& n, V3 S, V3 End, float uniform, V3* V)
+template <bool FAST>
+__device__ __forceinline__ float novak_sample(const Novak& n, V3 S, V3 End, V3 SE, float invlen, float uniform,
+                                              V3* V, bool& slow)
 {
     if (n.mode == 0) { *V = S; return 1; }
-    if (n.mode == 1) { *V = add(S, scl(sub(End, S), uniform)); return n.invlen; }
-    float newV = n.h * dm_sinhf(n.A0 + (uniform * (n.A1 - n.A0)));
+    if (n.mode == 1) { *V = add(S, scl(sub(End, S), uniform)); return invlen; }
+    float newV = n.h * Tx<FAST>::sinh(n.A0 + (uniform * (n.A1 - n.A0)), slow);
     newV = newV / n.sinTheta;
     const float result = 1.0f / sqrtf(n.h * n.h + newV * newV * n.sinTheta * n.sinTheta);
     newV += n.dVhS;
-    *V = add(S, scl(n.dirSE, newV));
+    *V = add(S, scl(SE, newV));
     return result / n.denom;
 }
-
-// the row's eye segment: everything integrateVRL derives without the VRL
-struct Row {
-    V3 E, d, U, n, A, B, dirAB;
-    float alb[3], wt[3], teus[3], cos_wi;
-    uint32_t flags, rid, sw;
-    bool surf;
-};
 
 __device__ __forceinline__ Row make_row(const DevParams& P, const Rec& r, uint32_t rid)
 {
@@ -252,16 +315,21 @@ __device__ __forceinline__ Row make_row(const DevParams& P, const Rec& r, uint32
     w.rid = rid;
     w.sw = ((r.depth & 0xFFu) << 16) | ((r.depth >> 16) & 0xFFFFu);
     const float edist = dist(w.U, w.E);                  // sampleUVKulla :865-871
-    w.A = w.E;
     w.B = add(w.E, scl(w.d, edist));
-    w.dirAB = nrm(sub(w.B, w.A));
+    w.dirAB = nrm(sub(w.B, w.E));
+    w.dAB = dist(w.E, w.B);
     w.teus[0] = w.teus[1] = w.teus[2] = 0.0f;
-    if ((r.flags & kFlagHit) && dist(w.U, w.E) != 0) {
+    if ((r.flags & kFlagHit) && edist != 0) {
         float pfd;
-        medium_eval(P, dist(w.U, w.E), w.teus, &pfd);
+        bool slow = false;
+        medium_eval<false>(P, edist, w.teus, &pfd, slow);
     }
     w.surf = (w.teus[0] != 0 || w.teus[1] != 0 || w.teus[2] != 0) && (r.flags & kFlagSmooth);
     w.cos_wi = dot(neg(w.d), w.n);
+    w.nd = nrm(w.d);
+    w.u = sub(w.U, w.E);                                 // closest points: u = S1P1 - S1P0
+    w.a_uu = dot(w.u, w.u);
+    w.eps_luu = kEps * len2(w.u);
     return w;
 }
 
@@ -273,38 +341,45 @@ __device__ __forceinline__ bool valid(const float c[3])
     return true;
 }
 
-// integrate_vrl_w's contribution (mean) and variance outputs for one pair
-__device__ void integrate_R(const DevParams& P, const Row& w, const float* __restrict__ soa, uint32_t nvrl,
-                            uint32_t v, uint32_t rsub, float* contrib, float* variance)
+// integrate_vrl_w's contribution (mean) and variance outputs for one pair.
+// NVV / NVS < 0: the sample counts come from P at run time.
+template <int NVV, int NVS, bool OCC, bool FAST>
+__device__ __forceinline__ void integrate_R(const DevParams& P, const Row& w, const StrictVrl& L, uint32_t v,
+                                            uint32_t koff, float* contrib, float* variance, bool& slow)
 {
     *contrib = 0; *variance = 0;
     if (!(w.flags & kFlagMedium)) return;
-    const V3 S = mk(soa[0 * (size_t)nvrl + v], soa[1 * (size_t)nvrl + v], soa[2 * (size_t)nvrl + v]);
-    const V3 End = mk(soa[3 * (size_t)nvrl + v], soa[4 * (size_t)nvrl + v], soa[5 * (size_t)nvrl + v]);
-    const float power[3] = {soa[6 * (size_t)nvrl + v], soa[7 * (size_t)nvrl + v], soa[8 * (size_t)nvrl + v]};
-    const V3 SV = nrm(sub(End, S));
+    const V3 S = mk(L.sx, L.sy, L.sz);
+    const V3 End = mk(L.ex, L.ey, L.ez);
+    const float power[3] = {L.pr, L.pg, L.pb};
+    const V3 SV = mk(L.dx, L.dy, L.dz);
+    const V3 vv = mk(L.vx, L.vy, L.vz);
     const V3 EU = w.d;
-    const int nVV = P.nvv, nVS = P.nvs;
-    const uint32_t koff = (rsub & 0xFFFFu) << 10;
-    Draws dr{w.rid, v, w.sw, P.seed, P.pass, 0xFFFFFFFFu, U4{0u, 0u, 0u, 0u}};
+    const int nVV = NVV >= 0 ? NVV : P.nvv, nVS = NVS >= 0 ? NVS : P.nvs;
+    // the Philox key schedule is re-derived per VRL (scalar adds) instead of
+    // being hoisted out of the VRL loop into twenty SGPRs that spill
+    uint32_t seed = P.seed, pass = P.pass;
+    asm volatile("" : "+s"(seed), "+s"(pass));
+    Draws dr{w.rid, v, w.sw, seed, pass, 0xFFFFFFFFu, U4{0u, 0u, 0u, 0u}};
 
     // ---- volume to volume (:647-703) ----
-    const Novak nv = novak_frame(w.E, w.d, w.U, S, End);
+    const Novak nv = novak_frame<FAST>(w, S, End, SV, vv, L.c, L.dSE, slow);
     float mean = 0, M2 = 0;
     for (int sample = 0; sample < nVV; sample++) {
         float lumv = 0.0f;
         const float u0 = dr.at(koff + 2 * sample);
         const float u1 = dr.at(koff + 2 * sample + 1);
         V3 V, U;
-        float pdf = novak_sample(nv, S, End, u0, &V);
-        pdf *= kulla_sample(kulla_frame(w.A, w.B, w.dirAB, V), u1, &U);
-        if (dist(U, V) != 0) {
+        float pdf = novak_sample<FAST>(nv, S, End, SV, L.invlen, u0, &V, slow);
+        pdf *= kulla_sample<FAST>(kulla_frame<FAST>(w.E, w.B, w.dirAB, w.dAB, V, slow), u1, &U, slow);
+        const float dUV = dist(U, V);
+        if (dUV != 0) {
             const V3 VU = nrm(sub(U, V));
             float tuv[3], teu[3], tsv[3], pf_eu, pf_sv;
-            shadow_transmittance(P, U, false, V, tuv);
+            shadow_transmittance<FAST, OCC>(P, U, false, V, dUV, tuv, slow);
             if (!(tuv[0] == 0 && tuv[1] == 0 && tuv[2] == 0)) {
-                medium_eval(P, dist(w.E, U), teu, &pf_eu);
-                medium_eval(P, dist(S, V), tsv, &pf_sv);
+                medium_eval<FAST>(P, dist(w.E, U), teu, &pf_eu, slow);
+                medium_eval<FAST>(P, dist(S, V), tsv, &pf_sv, slow);
                 const float rpdf = 1.0f / pdf;
                 const float rd2 = 1 / dist2(U, V);
                 const float phU = phase_eval(P, neg(VU), neg(EU));
@@ -335,17 +410,18 @@ __device__ void integrate_R(const DevParams& P, const Row& w, const float* __res
     // ---- volume to surface (:706-782) ----
     mean = 0; M2 = 0;
     if (w.surf && nVS > 0) {
-        const Kulla ks = kulla_frame(S, End, nrm(sub(End, S)), w.U);
+        const Kulla ks = kulla_frame<FAST>(S, End, SV, L.dSE, w.U, slow);
         for (int sample = 0; sample < nVS; sample++) {
             float lumv = 0.0f;
             const float u = dr.at(koff + 2 * nVV + sample);
             V3 V;
-            const float pdf = kulla_sample(ks, u, &V);
-            if (dist(w.U, V) != 0) {
+            const float pdf = kulla_sample<FAST>(ks, u, &V, slow);
+            const float dUV = dist(w.U, V);
+            if (dUV != 0) {
                 const V3 VU = nrm(sub(w.U, V));
                 float tuv[3], tsv[3], pf_sv;
-                shadow_transmittance(P, w.U, true, V, tuv);
-                medium_eval(P, dist(S, V), tsv, &pf_sv);
+                shadow_transmittance<FAST, OCC>(P, w.U, true, V, dUV, tuv, slow);
+                medium_eval<FAST>(P, dist(S, V), tsv, &pf_sv, slow);
                 // SmoothDiffuse::eval (diffuse.cpp:110-118)
                 const float cos_wo = dot(neg(VU), w.n);
                 float f[3] = {0, 0, 0};
@@ -396,14 +472,17 @@ __device__ __forceinline__ Rec load_rec(const Rec* __restrict__ recs, uint32_t r
 
 // One R entry: the sum over Rsamples of (contribution, variance) scaled by
 // the normalization as brute_worker / Rbuilder write it (:812-813).
-__device__ __forceinline__ float2 entry(const DevParams& P, const Row& w, const float* __restrict__ soa,
-                                       uint32_t nvrl, uint32_t v, float normalization)
+// RS1: Rsamples = 1 (one sample, draw offset 0).
+template <int NVV, int NVS, bool OCC, bool RS1, bool FAST>
+__device__ __forceinline__ float2 entry(const DevParams& P, const Row& w, const StrictVrl& L, uint32_t v,
+                                       float normalization, bool& slow)
 {
-    const int nsamp = P.rsamples > 1 ? P.rsamples : 1;
+    const int nsamp = RS1 ? 1 : (P.rsamples > 1 ? P.rsamples : 1);
     float m = 0.0f, s = 0.0f;
     for (int si = 0; si < nsamp; si++) {
         float contribution, variance;
-        integrate_R(P, w, soa, nvrl, v, (uint32_t)si, &contribution, &variance);
+        integrate_R<NVV, NVS, OCC, FAST>(P, w, L, v, RS1 ? 0u : ((uint32_t)si & 0xFFFFu) << 10, &contribution,
+                                         &variance, slow);
         m += contribution * normalization;
         s += variance * normalization * normalization;
     }
@@ -413,9 +492,10 @@ __device__ __forceinline__ float2 entry(const DevParams& P, const Row& w, const 
 // lane = row, the block's four waves interleave over a 256-VRL chunk, as
 // gather.hip's k_build_R / k_build_R_blocks (same outputs, same counters).
 // roff == nullptr: dense Rt[v * ld + row0 + r].
+template <int NVV, int NVS, bool OCC, bool RS1>
 __global__ void __launch_bounds__(256) k_build_R_strict(const Rec* __restrict__ recs,
                                                         const uint32_t* __restrict__ ids, uint32_t nrows,
-                                                        const float* __restrict__ soa, uint32_t nvrl,
+                                                        const StrictVrl* __restrict__ sv, uint32_t nvrl,
                                                         uint32_t chunk, DevParams P, float normalization,
                                                         float2* __restrict__ Rt, uint64_t ld, uint64_t row0,
                                                         const uint64_t* __restrict__ roff,
@@ -424,7 +504,7 @@ __global__ void __launch_bounds__(256) k_build_R_strict(const Rec* __restrict__ 
                                                         unsigned long long* counter)
 {
     const uint32_t r = blockIdx.x * 64 + (threadIdx.x & 63);
-    const uint32_t wave = threadIdx.x >> 6;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const bool active = r < nrows;
     Rec rec;
     if (active) rec = load_rec(recs, r);
@@ -436,11 +516,19 @@ __global__ void __launch_bounds__(256) k_build_R_strict(const Rec* __restrict__ 
     const uint64_t stride = !active ? 0 : roff ? rstride[r] : ld;
     const uint32_t v0 = blockIdx.y * chunk;
     const uint32_t v1 = min(nvrl, v0 + chunk);
-    const int nsamp = P.rsamples > 1 ? P.rsamples : 1;
+    const int nsamp = RS1 ? 1 : (P.rsamples > 1 ? P.rsamples : 1);
     uint32_t done = 0;
     for (uint32_t v = v0 + wave; v < v1; v += 4) {
         float2 e = make_float2(0.0f, 0.0f);
-        if (medium) e = entry(P, w, soa, nvrl, v, normalization);
+        if (medium) {
+            const StrictVrl L = sv[v];
+            bool slow = false;
+            e = entry<NVV, NVS, OCC, RS1, true>(P, w, L, v, normalization, slow);
+            // a lane whose fast transcendentals could round differently from
+            // detmath.h's (about one entry in 2^12 for a wave) recomputes the
+            // entry with detmath.h itself
+            if (slow) e = entry<NVV, NVS, OCC, RS1, false>(P, w, L, v, normalization, slow);
+        }
         if (active) {
             float2* p = &Rt[base + (uint64_t)v * stride];
             if (rec.flags & kRecAccum) { const float2 o = *p; *p = make_float2(o.x + e.x, o.y + e.y); }
@@ -454,7 +542,7 @@ __global__ void __launch_bounds__(256) k_build_R_strict(const Rec* __restrict__ 
 }
 
 // detmath.h on the device, elementwise (alvrl_detmath_eval): the host = device
-// check of the shared definitions
+// check of the shared definitions; fn + 8: the detmath_fast.h evaluation
 __global__ void __launch_bounds__(256) k_detmath(int fn, const float* __restrict__ in, float* __restrict__ out,
                                                  uint32_t n)
 {
@@ -468,14 +556,76 @@ __global__ void __launch_bounds__(256) k_detmath(int fn, const float* __restrict
     case 2: y = dm_atanf(x); break;
     case 3: y = dm_tanf(x); break;
     case 4: y = dm_asinhf(x); break;
-    default: y = dm_sinhf(x); break;
+    case 5: y = dm_sinhf(x); break;
+    case 8: y = fx_expf(x); break;
+    case 10: y = fx_atanf(x); break;
+    case 11: y = fx_tanf(x); break;
+    case 12: y = fx_asinhf(x); break;
+    default: y = fx_sinhf(x); break;
     }
     out[i] = y;
 }
 
+// Every float bit pattern in [begin, end): fx_*f(x) against dm_*f(x), bit for
+// bit.  out[0] counts mismatches, first[0..15] keeps some mismatching inputs.
+template <int FN>
+__device__ __forceinline__ void fx_dm(float x, float* f, float* d)
+{
+    if (FN == 0) { *f = fx_expf(x); *d = dm_expf(x); }
+    else if (FN == 2) { *f = fx_atanf(x); *d = dm_atanf(x); }
+    else if (FN == 3) { *f = fx_tanf(x); *d = dm_tanf(x); }
+    else if (FN == 4) { *f = fx_asinhf(x); *d = dm_asinhf(x); }
+    else { *f = fx_sinhf(x); *d = dm_sinhf(x); }
+}
+
+template <int FN>
+__global__ void __launch_bounds__(256) k_detmath_exhaustive(uint64_t begin, uint64_t end,
+                                                            unsigned long long* __restrict__ out,
+                                                            uint32_t* __restrict__ first)
+{
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint32_t bad = 0;
+    for (uint64_t b = begin + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < end; b += stride) {
+        const float x = __uint_as_float((uint32_t)b);
+        float f, d;
+        fx_dm<FN>(x, &f, &d);
+        if (__float_as_uint(f) != __float_as_uint(d)) {
+            ++bad;
+            const unsigned long long k = atomicAdd(out + 1, 1ull);
+            if (k < 16) first[k] = (uint32_t)b;
+        }
+    }
+    if (bad) atomicAdd(out, (unsigned long long)bad);
+}
+
 }  // namespace strict
 
-hipError_t launch_build_R_strict(const Rec* recs, const uint32_t* ids, uint32_t nrows, const float* soa,
+size_t strict_vrl_bytes() { return sizeof(strict::StrictVrl); }
+
+hipError_t launch_prepare_strict(const float* soa, uint32_t n, void* out, hipStream_t s)
+{
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(strict::k_prepare_strict, dim3((n + 255) / 256), dim3(256), 0, s, soa, n,
+                       reinterpret_cast<strict::StrictVrl*>(out));
+    return hipGetLastError();
+}
+
+template <int NVV, int NVS, bool OCC>
+static void launch_rs(bool rs1, dim3 grid, dim3 block, hipStream_t s, const Rec* recs, const uint32_t* ids,
+                      uint32_t nrows, const strict::StrictVrl* sv, uint32_t nvrl, uint32_t chunk,
+                      const DevParams& P, float normalization, float2* Rt, uint64_t ld, uint64_t row0,
+                      const uint64_t* roff, const uint32_t* rstride, uint8_t* nonzero,
+                      unsigned long long* counter)
+{
+    if (rs1)
+        hipLaunchKernelGGL((strict::k_build_R_strict<NVV, NVS, OCC, true>), grid, block, 0, s, recs, ids, nrows,
+                           sv, nvrl, chunk, P, normalization, Rt, ld, row0, roff, rstride, nonzero, counter);
+    else
+        hipLaunchKernelGGL((strict::k_build_R_strict<NVV, NVS, OCC, false>), grid, block, 0, s, recs, ids, nrows,
+                           sv, nvrl, chunk, P, normalization, Rt, ld, row0, roff, rstride, nonzero, counter);
+}
+
+hipError_t launch_build_R_strict(const Rec* recs, const uint32_t* ids, uint32_t nrows, const void* svrl,
                                  uint32_t nvrl, const DevParams& P, float normalization, float2* Rt, uint64_t ld,
                                  uint64_t row0, const uint64_t* roff, const uint32_t* rstride, uint8_t* nonzero,
                                  unsigned long long* counter, hipStream_t s)
@@ -483,8 +633,17 @@ hipError_t launch_build_R_strict(const Rec* recs, const uint32_t* ids, uint32_t 
     if (nrows == 0 || nvrl == 0) return hipSuccess;
     const uint32_t chunk = 256;
     const dim3 grid((nrows + 63) / 64, (nvrl + chunk - 1) / chunk), block(256);
-    hipLaunchKernelGGL(strict::k_build_R_strict, grid, block, 0, s, recs, ids, nrows, soa, nvrl, chunk, P,
-                       normalization, Rt, ld, row0, roff, rstride, nonzero, counter);
+    const auto* sv = reinterpret_cast<const strict::StrictVrl*>(svrl);
+    const bool rs1 = P.rsamples <= 1;
+    if (P.occ.ntri)
+        launch_rs<-1, -1, true>(rs1, grid, block, s, recs, ids, nrows, sv, nvrl, chunk, P, normalization, Rt, ld,
+                                row0, roff, rstride, nonzero, counter);
+    else if (P.nvv == 2 && P.nvs == 2)
+        launch_rs<2, 2, false>(rs1, grid, block, s, recs, ids, nrows, sv, nvrl, chunk, P, normalization, Rt, ld,
+                               row0, roff, rstride, nonzero, counter);
+    else
+        launch_rs<-1, -1, false>(rs1, grid, block, s, recs, ids, nrows, sv, nvrl, chunk, P, normalization, Rt,
+                                 ld, row0, roff, rstride, nonzero, counter);
     return hipGetLastError();
 }
 
@@ -492,6 +651,22 @@ hipError_t launch_detmath(int fn, const float* in, float* out, uint32_t n, hipSt
 {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(strict::k_detmath, dim3((n + 255) / 256), dim3(256), 0, s, fn, in, out, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_detmath_exhaustive(int fn, uint64_t begin, uint64_t end, unsigned long long* out,
+                                     uint32_t* first, hipStream_t s)
+{
+    if (end <= begin) return hipSuccess;
+    const dim3 grid(8192), block(256);
+    switch (fn) {
+    case 0: hipLaunchKernelGGL(strict::k_detmath_exhaustive<0>, grid, block, 0, s, begin, end, out, first); break;
+    case 2: hipLaunchKernelGGL(strict::k_detmath_exhaustive<2>, grid, block, 0, s, begin, end, out, first); break;
+    case 3: hipLaunchKernelGGL(strict::k_detmath_exhaustive<3>, grid, block, 0, s, begin, end, out, first); break;
+    case 4: hipLaunchKernelGGL(strict::k_detmath_exhaustive<4>, grid, block, 0, s, begin, end, out, first); break;
+    case 5: hipLaunchKernelGGL(strict::k_detmath_exhaustive<5>, grid, block, 0, s, begin, end, out, first); break;
+    default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 

@@ -65,6 +65,19 @@ def test_detmath_device_matches_host(oracle, gpu_ok):
         assert same.all(), (fn, x[~same][:4], dev[~same][:4], host[~same][:4])
 
 
+@pytest.mark.parametrize("fn", ["exp", "atan", "tan", "asinh", "sinh"])
+def test_detmath_fast_exhaustive(fn, gpu_ok):
+    """csrc/detmath_fast.h (the strict R build's transcendentals: a short f64
+    evaluation and Ziv's rounding test, detmath.h when the rounding is in
+    doubt) returns detmath.h's float for EVERY one of the 2^32 float inputs."""
+    import time
+    import alvrl
+    t0 = time.perf_counter()
+    bad, first = alvrl.detmath_exhaustive(fn)
+    print(f"[{fn}] 2^32 inputs in {time.perf_counter() - t0:.1f} s, {bad} differ")
+    assert bad == 0, (fn, bad, [hex(b) for b in first])
+
+
 def _strict_R(oracle, w, h, nvrl, step, medium=("balance", -1, 0.0), phase=(0, 0.0), short=True,
               nvv=2, nvs=2, rsamples=1, tris=None):
     import torch
