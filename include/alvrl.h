@@ -262,9 +262,17 @@ ALVRL_API int alvrl_detmath_eval(int fn, const float *d_in, float *d_out, uint32
  * (end <= 2^32), on the current device, synchronous: *mismatches = the number
  * of inputs whose results differ in any bit, first[0 .. min(nfirst, 16)) =
  * some of them (0xFFFFFFFF past the last).  fn 0 exp, 2 atan, 3 tan,
- * 4 asinh, 5 sinh. */
+ * 4 asinh, 5 sinh, 6 sqrt (the fast square root against IEEE sqrtf). */
 ALVRL_API int alvrl_detmath_exhaustive(int fn, uint64_t begin, uint64_t end, uint64_t *mismatches,
                                        uint32_t *first, uint32_t nfirst);
+
+/* The strict kernels' fast division (csrc/detmath_fast.h fx_divf) against
+ * IEEE a / b on n pseudo-random operand pairs (half uniform over all bit
+ * patterns, half log-uniform in [2^-44, 2^44]), on the current device,
+ * synchronous: *mismatches = pairs whose quotients differ in any bit,
+ * first[0 .. min(nfirst, 16)) = (a, b) bit patterns of some of them. */
+ALVRL_API int alvrl_detmath_div_check(uint64_t n, uint64_t seed, uint64_t *mismatches, uint32_t *first,
+                                      uint32_t nfirst);
 
 /* ---- hot path (b) part 2: cluster refinement ------------------------- */
 /* One Clustering (Preprocessor.cpp:287-720): ctor (column weights, initial

@@ -113,6 +113,7 @@ def lib() -> C.CDLL:
     L.alvrl_host_batch_stats.argtypes = [vp, P(u64), P(u64)]
     L.alvrl_detmath_eval.argtypes = [i32, vp, vp, u32, vp]
     L.alvrl_detmath_exhaustive.argtypes = [i32, u64, u64, P(u64), P(u32), u32]
+    L.alvrl_detmath_div_check.argtypes = [u64, u64, P(u64), P(u32), u32]
     _lib = L
     return L
 
@@ -165,8 +166,18 @@ def detmath_exhaustive(fn: str, begin: int = 0, end: int = 1 << 32):
     differ, some of those inputs as uint32 bit patterns)."""
     mism = C.c_uint64(0)
     first = (C.c_uint32 * 16)()
-    _check(lib().alvrl_detmath_exhaustive(DETMATH_FNS.index(fn), int(begin), int(end), C.byref(mism), first, 16))
+    _check(lib().alvrl_detmath_exhaustive(6 if fn == "sqrt" else DETMATH_FNS.index(fn), int(begin), int(end), C.byref(mism), first, 16))
     return int(mism.value), [int(x) for x in first if x != 0xFFFFFFFF]
+
+
+def detmath_div_check(n: int, seed: int = 1):
+    """The strict kernels' fast division against IEEE division on n random
+    operand pairs (alvrl_detmath_div_check): (mismatches, [(a_bits, b_bits)])."""
+    mism = C.c_uint64(0)
+    first = (C.c_uint32 * 16)()
+    _check(lib().alvrl_detmath_div_check(int(n), int(seed), C.byref(mism), first, 16))
+    pairs = [(int(first[2 * k]), int(first[2 * k + 1])) for k in range(8) if first[2 * k] != 0xFFFFFFFF]
+    return int(mism.value), pairs
 
 
 def _check(rc: int):

@@ -53,6 +53,7 @@ hipError_t launch_detmath(int fn, const float* in, float* out, uint32_t n, hipSt
 hipError_t launch_detmath_exhaustive(int fn, uint64_t begin, uint64_t end, unsigned long long* out,
                                      uint32_t* first, hipStream_t s);
 size_t strict_vrl_bytes();
+hipError_t launch_div_check(uint64_t n, uint64_t seed, unsigned long long* out, uint32_t* first, hipStream_t s);
 hipError_t launch_prepare_strict(const float* soa, uint32_t n, void* out, hipStream_t s);
 hipError_t launch_false_color(const Rec* recs, const WorkItem* items, uint32_t n, int mode,
                               const uint32_t* slice_off, uint32_t n_fb, uint32_t nvrl, float* out,
@@ -617,11 +618,35 @@ ALVRL_API int alvrl_detmath_eval(int fn, const float* d_in, float* d_out, uint32
     return ALVRL_OK;
 }
 
+ALVRL_API int alvrl_detmath_div_check(uint64_t n, uint64_t seed, uint64_t* mismatches, uint32_t* first,
+                                      uint32_t nfirst)
+{
+    if (!mismatches) return fail(ALVRL_ERR_INVALID, "alvrl_detmath_div_check: null output");
+    unsigned long long* d_out = nullptr;
+    uint32_t* d_first = nullptr;
+    HIPCHK(hipMalloc(&d_out, 2 * sizeof(unsigned long long)));
+    hipError_t e = hipMalloc(&d_first, 16 * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMemset(d_out, 0, 2 * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMemset(d_first, 0xFF, 16 * sizeof(uint32_t));
+    if (e == hipSuccess) e = launch_div_check(n, seed, d_out, d_first, nullptr);
+    unsigned long long h[2] = {0, 0};
+    uint32_t hf[16];
+    if (e == hipSuccess) e = hipMemcpy(h, d_out, sizeof(h), hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(hf, d_first, sizeof(hf), hipMemcpyDeviceToHost);
+    hipFree(d_out);
+    hipFree(d_first);
+    HIPCHK(e);
+    *mismatches = h[0];
+    if (first)
+        for (uint32_t i = 0; i < nfirst && i < 16; i++) first[i] = hf[i];
+    return ALVRL_OK;
+}
+
 ALVRL_API int alvrl_detmath_exhaustive(int fn, uint64_t begin, uint64_t end, uint64_t* mismatches,
                                        uint32_t* first, uint32_t nfirst)
 {
-    if (fn != 0 && (fn < 2 || fn > 5))
-        return fail(ALVRL_ERR_INVALID, "alvrl_detmath_exhaustive: fn must be 0 or in [2, 5]");
+    if (fn != 0 && (fn < 2 || fn > 6))
+        return fail(ALVRL_ERR_INVALID, "alvrl_detmath_exhaustive: fn must be 0 or in [2, 6]");
     if (end > (1ull << 32) || begin > end) return fail(ALVRL_ERR_INVALID, "alvrl_detmath_exhaustive: bad range");
     if (!mismatches) return fail(ALVRL_ERR_INVALID, "alvrl_detmath_exhaustive: null output");
     unsigned long long* d_out = nullptr;

@@ -28,9 +28,15 @@
 
 #include <stdint.h>
 
+#include <mutex>
+
 #include "detmath.h"
 #include "detmath_fast.h"
 #include "vrl_device.hpp"
+
+#ifndef ALVRL_STRICT_MINB
+#define ALVRL_STRICT_MINB 4   // 4 waves/SIMD (<= 128 VGPRs): 127 -> 117 ms at C4 against 3
+#endif
 
 namespace alvrl {
 namespace strict {
@@ -62,7 +68,18 @@ struct Tx {
     static __device__ __forceinline__ float tan(float x, bool& s) { return FAST ? fx_tanf_r(x, s) : dm_tanf(x); }
     static __device__ __forceinline__ float asinh(float x, bool& s) { return FAST ? fx_asinhf_r(x, s) : dm_asinhf(x); }
     static __device__ __forceinline__ float sinh(float x, bool& s) { return FAST ? fx_sinhf_r(x, s) : dm_sinhf(x); }
+    // IEEE sqrt and division: their cores without the scaling (flag outside
+    // the range where the scaling is the identity), or the compiler's expansion
+    static __device__ __forceinline__ float sqrt(float x, bool& s) { return FAST ? fx_sqrtf_r(x, s) : sqrtf(x); }
+    static __device__ __forceinline__ float div(float a, float b, bool& s) { return FAST ? fx_divf_r(a, b, s) : a / b; }
 };
+template <bool FAST> __device__ __forceinline__ float lenT(V3 a, bool& s) { return Tx<FAST>::sqrt(len2(a), s); }
+template <bool FAST> __device__ __forceinline__ float distT(V3 a, V3 b, bool& s) { return lenT<FAST>(sub(a, b), s); }
+template <bool FAST> __device__ __forceinline__ V3 nrmT(V3 a, bool& s)
+{
+    const float r = Tx<FAST>::div(1.0f, lenT<FAST>(a, s), s);
+    return scl(a, r);
+}
 
 // The VRL-only values of integrate_vrl_w, by the restatement's own operations
 // (k_prepare_strict).  128 B: two s_load_dwordx16.
@@ -140,7 +157,7 @@ __device__ __forceinline__ void medium_eval(const DevParams& P, float distance, 
     float pf = 0.0f;
     if (P.strategy == 0) {
         pf += e0; pf += e1; pf += e2;
-        pf /= 3;
+        pf = Tx<FAST>::div(pf, 3.0f, slow);
     } else if (P.strategy == 3) {
         pf = 1 - mxexp_cdf<FAST>(P, distance, slow);
     } else {
@@ -166,7 +183,7 @@ __device__ __forceinline__ void shadow_transmittance(const DevParams& P, V3 p1, 
     if (!OCC) return;
     if (P.occ.ntri == 0 || !(remaining > 0)) return;
     const V3 d = sub(p2, p1);
-    const V3 dn = scl(d, 1.0f / remaining);
+    const V3 dn = scl(d, Tx<FAST>::div(1.0f, remaining, slow));
     const float mint = p1_surface ? 1e-4f : 0.0f;
     const float maxt = remaining * 1.0f;
     if (bvh::occluded(P.occ, bvh::mk(p1.x, p1.y, p1.z), bvh::mk(dn.x, dn.y, dn.z), mint, maxt))
@@ -174,12 +191,13 @@ __device__ __forceinline__ void shadow_transmittance(const DevParams& P, V3 p1, 
 }
 
 // isotropic.cpp:76-78, hg.cpp:107-110
-__device__ __forceinline__ float phase_eval(const DevParams& P, V3 wi, V3 wo)
+template <bool FAST>
+__device__ __forceinline__ float phase_eval(const DevParams& P, V3 wi, V3 wo, bool& slow)
 {
     if (P.phase_type == 0) return kInvFourPi;
     const float g = P.g;
     const float temp = 1.0f + g * g + 2.0f * g * dot(wi, wo);
-    return kInvFourPi * (1 - g * g) / (temp * sqrtf(temp));
+    return Tx<FAST>::div(kInvFourPi * (1 - g * g), temp * Tx<FAST>::sqrt(temp, slow), slow);
 }
 
 // the row's eye segment: everything integrateVRL derives without the VRL
@@ -194,7 +212,8 @@ struct Row {
 
 // getClosestPoints (vrlIntegrator.cpp:962-1032) for S1 = the eye segment E ->
 // hit, S2 = the VRL; returns |dP| and the closest point on the VRL
-__device__ __forceinline__ float closest_points(const Row& w, V3 S, const V3& vv, float c, V3* S2h)
+template <bool FAST>
+__device__ __forceinline__ float closest_points(const Row& w, V3 S, const V3& vv, float c, V3* S2h, bool& slow)
 {
     const V3 u = w.u, v = vv, wv = sub(w.E, S);
     const float a = w.a_uu, b = dot(u, v), d = dot(u, wv), e = dot(v, wv);
@@ -219,11 +238,11 @@ __device__ __forceinline__ float closest_points(const Row& w, V3 S, const V3& vv
         else if ((-d + b) > a) sN = sD;
         else { sN = (-d + b); sD = a; }
     }
-    const float sc = sN / sD;
-    const float tc = tN / tD;
+    const float sc = Tx<FAST>::div(sN, sD, slow);
+    const float tc = Tx<FAST>::div(tN, tD, slow);
     const V3 dP = sub(add(wv, scl(u, sc)), scl(v, tc));
     *S2h = add(S, scl(v, tc));
-    return len(dP);
+    return lenT<FAST>(dP, slow);
 }
 
 // KullaSampling (vrlIntegrator.cpp:889-914) split into the part fixed by the
@@ -237,10 +256,10 @@ __device__ __forceinline__ Kulla kulla_frame(V3 A, V3 B, V3 dir, float dAB, V3 D
     k.dir = dir;
     const float dotPr = dot(dir, sub(D, A));
     k.I = add(A, scl(dir, dotPr));
-    k.Dis = dist(D, k.I);
-    const float dAI = dist(A, k.I);
-    float angle_a = Tx<FAST>::atan(dAI / k.Dis, slow);
-    float angle_b = Tx<FAST>::atan(dist(k.I, B) / k.Dis, slow);
+    k.Dis = distT<FAST>(D, k.I, slow);
+    const float dAI = distT<FAST>(A, k.I, slow);
+    float angle_a = Tx<FAST>::atan(Tx<FAST>::div(dAI, k.Dis, slow), slow);
+    float angle_b = Tx<FAST>::atan(Tx<FAST>::div(distT<FAST>(k.I, B, slow), k.Dis, slow), slow);
     if (dotPr > 0) {
         angle_a *= -1;
         if (dAI > dAB) angle_b *= -1;
@@ -253,7 +272,7 @@ template <bool FAST>
 __device__ __forceinline__ float kulla_sample(const Kulla& k, float uniform, V3* result, bool& slow)
 {
     const float t = k.Dis * Tx<FAST>::tan(((1.0f - uniform) * k.aa) + (uniform * k.ab), slow);
-    const float pdf = k.Dis / ((k.ab - k.aa) * (k.Dis * k.Dis + t * t));
+    const float pdf = Tx<FAST>::div(k.Dis, (k.ab - k.aa) * (k.Dis * k.Dis + t * t), slow);
     *result = add(k.I, scl(k.dir, t));
     return pdf;
 }
@@ -273,20 +292,20 @@ __device__ __forceinline__ Novak novak_frame(const Row& w, V3 S, V3 End, V3 SE, 
     if (dSE == 0) return n;
     const float cosTheta = dot(w.nd, SE);
     const float st2 = 1 - cosTheta * cosTheta;
-    n.sinTheta = sqrtf(st2 > 0.0f ? st2 : 0.0f);
+    n.sinTheta = Tx<FAST>::sqrt(st2 > 0.0f ? st2 : 0.0f, slow);
     if (n.sinTheta < kEps) {
         n.mode = 1;
         return n;
     }
     n.mode = 2;
     V3 Vh;
-    n.h = closest_points(w, S, vv, c, &Vh);
-    n.dVhS = dist(Vh, S);
+    n.h = closest_points<FAST>(w, S, vv, c, &Vh, slow);
+    n.dVhS = distT<FAST>(Vh, S, slow);
     const float V0c = -1 * n.dVhS;
-    const float V1c = dist(Vh, End);
-    n.A0 = Tx<FAST>::asinh((V0c / n.h) * n.sinTheta, slow);
-    n.A1 = Tx<FAST>::asinh((V1c / n.h) * n.sinTheta, slow);
-    n.denom = (n.A1 - n.A0) / n.sinTheta;
+    const float V1c = distT<FAST>(Vh, End, slow);
+    n.A0 = Tx<FAST>::asinh(Tx<FAST>::div(V0c, n.h, slow) * n.sinTheta, slow);
+    n.A1 = Tx<FAST>::asinh(Tx<FAST>::div(V1c, n.h, slow) * n.sinTheta, slow);
+    n.denom = Tx<FAST>::div(n.A1 - n.A0, n.sinTheta, slow);
     return n;
 }
 
@@ -297,11 +316,11 @@ __device__ __forceinline__ float novak_sample(const Novak& n, V3 S, V3 End, V3 S
     if (n.mode == 0) { *V = S; return 1; }
     if (n.mode == 1) { *V = add(S, scl(sub(End, S), uniform)); return invlen; }
     float newV = n.h * Tx<FAST>::sinh(n.A0 + (uniform * (n.A1 - n.A0)), slow);
-    newV = newV / n.sinTheta;
-    const float result = 1.0f / sqrtf(n.h * n.h + newV * newV * n.sinTheta * n.sinTheta);
+    newV = Tx<FAST>::div(newV, n.sinTheta, slow);
+    const float result = Tx<FAST>::div(1.0f, Tx<FAST>::sqrt(n.h * n.h + newV * newV * n.sinTheta * n.sinTheta, slow), slow);
     newV += n.dVhS;
     *V = add(S, scl(SE, newV));
-    return result / n.denom;
+    return Tx<FAST>::div(result, n.denom, slow);
 }
 
 __device__ __forceinline__ Row make_row(const DevParams& P, const Rec& r, uint32_t rid)
@@ -372,19 +391,19 @@ __device__ __forceinline__ void integrate_R(const DevParams& P, const Row& w, co
         V3 V, U;
         float pdf = novak_sample<FAST>(nv, S, End, SV, L.invlen, u0, &V, slow);
         pdf *= kulla_sample<FAST>(kulla_frame<FAST>(w.E, w.B, w.dirAB, w.dAB, V, slow), u1, &U, slow);
-        const float dUV = dist(U, V);
+        const float dUV = distT<FAST>(U, V, slow);
         if (dUV != 0) {
-            const V3 VU = nrm(sub(U, V));
+            const V3 VU = nrmT<FAST>(sub(U, V), slow);
             float tuv[3], teu[3], tsv[3], pf_eu, pf_sv;
             shadow_transmittance<FAST, OCC>(P, U, false, V, dUV, tuv, slow);
             if (!(tuv[0] == 0 && tuv[1] == 0 && tuv[2] == 0)) {
-                medium_eval<FAST>(P, dist(w.E, U), teu, &pf_eu, slow);
-                medium_eval<FAST>(P, dist(S, V), tsv, &pf_sv, slow);
-                const float rpdf = 1.0f / pdf;
-                const float rd2 = 1 / dist2(U, V);
-                const float phU = phase_eval(P, neg(VU), neg(EU));
-                const float phV = phase_eval(P, neg(SV), VU);
-                const float rpf = 1.0f / pf_sv;
+                medium_eval<FAST>(P, distT<FAST>(w.E, U, slow), teu, &pf_eu, slow);
+                medium_eval<FAST>(P, distT<FAST>(S, V, slow), tsv, &pf_sv, slow);
+                const float rpdf = Tx<FAST>::div(1.0f, pdf, slow);
+                const float rd2 = Tx<FAST>::div(1.0f, dist2(U, V), slow);
+                const float phU = phase_eval<FAST>(P, neg(VU), neg(EU), slow);
+                const float phV = phase_eval<FAST>(P, neg(SV), VU, slow);
+                const float rpf = Tx<FAST>::div(1.0f, pf_sv, slow);
                 float c[3];
                 for (int i = 0; i < 3; i++) {
                     c[i] = w.wt[i];
@@ -416,21 +435,21 @@ __device__ __forceinline__ void integrate_R(const DevParams& P, const Row& w, co
             const float u = dr.at(koff + 2 * nVV + sample);
             V3 V;
             const float pdf = kulla_sample<FAST>(ks, u, &V, slow);
-            const float dUV = dist(w.U, V);
+            const float dUV = distT<FAST>(w.U, V, slow);
             if (dUV != 0) {
-                const V3 VU = nrm(sub(w.U, V));
+                const V3 VU = nrmT<FAST>(sub(w.U, V), slow);
                 float tuv[3], tsv[3], pf_sv;
                 shadow_transmittance<FAST, OCC>(P, w.U, true, V, dUV, tuv, slow);
-                medium_eval<FAST>(P, dist(S, V), tsv, &pf_sv, slow);
+                medium_eval<FAST>(P, distT<FAST>(S, V, slow), tsv, &pf_sv, slow);
                 // SmoothDiffuse::eval (diffuse.cpp:110-118)
                 const float cos_wo = dot(neg(VU), w.n);
                 float f[3] = {0, 0, 0};
                 if (!(w.cos_wi <= 0 || cos_wo <= 0))
                     for (int i = 0; i < 3; i++) f[i] = w.alb[i] * (kInvPi * cos_wo);
-                const float phV = phase_eval(P, neg(SV), VU);
-                const float rpdf = 1.0f / pdf;
-                const float rd2 = 1 / dist2(w.U, V);
-                const float rpf = 1.0f / pf_sv;
+                const float phV = phase_eval<FAST>(P, neg(SV), VU, slow);
+                const float rpdf = Tx<FAST>::div(1.0f, pdf, slow);
+                const float rd2 = Tx<FAST>::div(1.0f, dist2(w.U, V), slow);
+                const float rpf = Tx<FAST>::div(1.0f, pf_sv, slow);
                 float c[3];
                 for (int i = 0; i < 3; i++) {
                     c[i] = w.wt[i];
@@ -489,11 +508,32 @@ __device__ __forceinline__ float2 entry(const DevParams& P, const Row& w, const 
     return make_float2(m, s);
 }
 
+// The queue of entries the fast evaluation could not settle: (launch row,
+// VRL) pairs, re-evaluated with detmath.h by k_build_R_strict_fixup.  Keeping
+// that evaluation out of the main kernel keeps its code (and instruction cache
+// footprint) to the fast form alone.
+struct FixQueue {
+    uint2* items;
+    unsigned long long* count;
+    uint32_t cap;
+};
+
+__device__ __forceinline__ void store_entry(float2* __restrict__ Rt, uint64_t idx, bool accum, float2 e)
+{
+    float2* p = &Rt[idx];
+    if (accum) { const float2 o = *p; *p = make_float2(o.x + e.x, o.y + e.y); }
+    else *p = e;
+}
+
 // lane = row, the block's four waves interleave over a 256-VRL chunk, as
 // gather.hip's k_build_R / k_build_R_blocks (same outputs, same counters).
-// roff == nullptr: dense Rt[v * ld + row0 + r].
+// roff == nullptr: dense Rt[v * ld + row0 + r].  A lane whose fast
+// transcendentals, division or square root could round differently from the
+// oracle's (one entry in ~5,000; about one wave iteration in 80) queues the
+// entry instead of storing it.  store = 0: only the queue is written (the
+// re-run after a queue overflow, which must not add accumulating rows twice).
 template <int NVV, int NVS, bool OCC, bool RS1>
-__global__ void __launch_bounds__(256) k_build_R_strict(const Rec* __restrict__ recs,
+__global__ void __launch_bounds__(256, ALVRL_STRICT_MINB) k_build_R_strict(const Rec* __restrict__ recs,
                                                         const uint32_t* __restrict__ ids, uint32_t nrows,
                                                         const StrictVrl* __restrict__ sv, uint32_t nvrl,
                                                         uint32_t chunk, DevParams P, float normalization,
@@ -501,7 +541,7 @@ __global__ void __launch_bounds__(256) k_build_R_strict(const Rec* __restrict__ 
                                                         const uint64_t* __restrict__ roff,
                                                         const uint32_t* __restrict__ rstride,
                                                         uint8_t* __restrict__ nonzero,
-                                                        unsigned long long* counter)
+                                                        unsigned long long* counter, FixQueue fq, int store)
 {
     const uint32_t r = blockIdx.x * 64 + (threadIdx.x & 63);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -520,25 +560,52 @@ __global__ void __launch_bounds__(256) k_build_R_strict(const Rec* __restrict__ 
     uint32_t done = 0;
     for (uint32_t v = v0 + wave; v < v1; v += 4) {
         float2 e = make_float2(0.0f, 0.0f);
+        bool slow = false;
         if (medium) {
             const StrictVrl L = sv[v];
-            bool slow = false;
             e = entry<NVV, NVS, OCC, RS1, true>(P, w, L, v, normalization, slow);
-            // a lane whose fast transcendentals could round differently from
-            // detmath.h's (about one entry in 2^12 for a wave) recomputes the
-            // entry with detmath.h itself
-            if (slow) e = entry<NVV, NVS, OCC, RS1, false>(P, w, L, v, normalization, slow);
         }
-        if (active) {
-            float2* p = &Rt[base + (uint64_t)v * stride];
-            if (rec.flags & kRecAccum) { const float2 o = *p; *p = make_float2(o.x + e.x, o.y + e.y); }
-            else *p = e;
+        if (store && active && !slow) store_entry(Rt, base + (uint64_t)v * stride, rec.flags & kRecAccum, e);
+        const unsigned long long sb = __ballot(slow);
+        if (sb) {   // wave-aggregated append
+            unsigned long long at = 0;
+            if ((threadIdx.x & 63) == 0) at = atomicAdd(fq.count, (unsigned long long)__popcll(sb));
+            at = __shfl(at, 0);
+            const uint32_t lane = threadIdx.x & 63;
+            const unsigned long long k = at + __popcll(sb & ((1ull << lane) - 1ull));
+            if (slow && k < fq.cap) fq.items[k] = make_uint2(r, v);
         }
-        if (nonzero && __ballot(active && e.x != 0.0f) && (threadIdx.x & 63) == 0) nonzero[v] = 1;
+        if (store && nonzero && __ballot(active && !slow && e.x != 0.0f) && (threadIdx.x & 63) == 0) nonzero[v] = 1;
         ++done;
     }
     const unsigned long long m = __ballot(medium);
-    if ((threadIdx.x & 63) == 0 && m) atomicAdd(counter, (unsigned long long)__popcll(m) * done * (uint32_t)nsamp);
+    if (store && (threadIdx.x & 63) == 0 && m) atomicAdd(counter, (unsigned long long)__popcll(m) * done * (uint32_t)nsamp);
+}
+
+// The queued entries with detmath.h, one lane each (same row set-up, same
+// entry, same store and mask as the main kernel)
+template <int NVV, int NVS, bool OCC, bool RS1>
+__global__ void __launch_bounds__(256) k_build_R_strict_fixup(const Rec* __restrict__ recs,
+                                                              const uint32_t* __restrict__ ids,
+                                                              const StrictVrl* __restrict__ sv, DevParams P,
+                                                              float normalization, float2* __restrict__ Rt,
+                                                              uint64_t ld, uint64_t row0,
+                                                              const uint64_t* __restrict__ roff,
+                                                              const uint32_t* __restrict__ rstride,
+                                                              uint8_t* __restrict__ nonzero,
+                                                              const uint2* __restrict__ items, uint32_t n)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t r = items[i].x, v = items[i].y;
+    const Rec rec = load_rec(recs, r);
+    const Row w = make_row(P, rec, ids ? ids[r] : r);
+    bool slow = false;
+    const float2 e = entry<NVV, NVS, OCC, RS1, false>(P, w, sv[v], v, normalization, slow);
+    const uint64_t base = roff ? roff[r] : row0 + r;
+    const uint64_t stride = roff ? rstride[r] : ld;
+    store_entry(Rt, base + (uint64_t)v * stride, rec.flags & kRecAccum, e);
+    if (nonzero && e.x != 0.0f) nonzero[v] = 1;
 }
 
 // detmath.h on the device, elementwise (alvrl_detmath_eval): the host = device
@@ -575,6 +642,7 @@ __device__ __forceinline__ void fx_dm(float x, float* f, float* d)
     else if (FN == 2) { *f = fx_atanf(x); *d = dm_atanf(x); }
     else if (FN == 3) { *f = fx_tanf(x); *d = dm_tanf(x); }
     else if (FN == 4) { *f = fx_asinhf(x); *d = dm_asinhf(x); }
+    else if (FN == 6) { *f = fx_sqrtf(x); *d = sqrtf(x); }
     else { *f = fx_sinhf(x); *d = dm_sinhf(x); }
 }
 
@@ -598,7 +666,48 @@ __global__ void __launch_bounds__(256) k_detmath_exhaustive(uint64_t begin, uint
     if (bad) atomicAdd(out, (unsigned long long)bad);
 }
 
+// fx_divf(a, b) against IEEE a / b, bit for bit, on n pseudo-random operand
+// pairs: even draws are uniform over all 2^32 bit patterns (every exponent,
+// zeros, subnormals, infinities, NaNs), odd draws log-uniform magnitudes in
+// [2^-44, 2^44] (the fast range and its edges) with random signs.
+__device__ __forceinline__ uint64_t mix64(uint64_t z)
+{
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__global__ void __launch_bounds__(256) k_div_check(uint64_t n, uint64_t seed, unsigned long long* __restrict__ out,
+                                                   uint32_t* __restrict__ first)
+{
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint32_t bad = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint64_t h = mix64(seed ^ (i * 0xD1B54A32D192ED03ull));
+        uint32_t ba = (uint32_t)h, bb = (uint32_t)(h >> 32);
+        if (i & 1) {   // sign | exponent in [127 - 44, 127 + 44] | mantissa
+            ba = (ba & 0x807FFFFFu) | ((83u + ((ba >> 23) & 0xFFu) % 89u) << 23);
+            bb = (bb & 0x807FFFFFu) | ((83u + ((bb >> 23) & 0xFFu) % 89u) << 23);
+        }
+        const float a = __uint_as_float(ba), b = __uint_as_float(bb);
+        const float f = fx_divf(a, b), d = a / b;
+        if (__float_as_uint(f) != __float_as_uint(d)) {
+            ++bad;
+            const unsigned long long k = atomicAdd(out + 1, 1ull);
+            if (k < 8) { first[2 * k] = ba; first[2 * k + 1] = bb; }
+        }
+    }
+    if (bad) atomicAdd(out, (unsigned long long)bad);
+}
+
 }  // namespace strict
+
+hipError_t launch_div_check(uint64_t n, uint64_t seed, unsigned long long* out, uint32_t* first, hipStream_t s)
+{
+    hipLaunchKernelGGL(strict::k_div_check, dim3(8192), dim3(256), 0, s, n, seed, out, first);
+    return hipGetLastError();
+}
 
 size_t strict_vrl_bytes() { return sizeof(strict::StrictVrl); }
 
@@ -610,19 +719,84 @@ hipError_t launch_prepare_strict(const float* soa, uint32_t n, void* out, hipStr
     return hipGetLastError();
 }
 
+// the fix-up queue of the strict R build, per device (grown on demand)
+static std::mutex g_fix_mu;
+struct FixBuf {
+    uint2* items = nullptr;
+    unsigned long long* count = nullptr;
+    unsigned long long* h_count = nullptr;
+    uint32_t cap = 0;
+};
+static FixBuf g_fix[64];
+
+template <int NVV, int NVS, bool OCC, bool RS1>
+static hipError_t run_strict(dim3 grid, dim3 block, hipStream_t s, const Rec* recs, const uint32_t* ids,
+                             uint32_t nrows, const strict::StrictVrl* sv, uint32_t nvrl, uint32_t chunk,
+                             const DevParams& P, float normalization, float2* Rt, uint64_t ld, uint64_t row0,
+                             const uint64_t* roff, const uint32_t* rstride, uint8_t* nonzero,
+                             unsigned long long* counter)
+{
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+    // one queue per device; launches of several host threads on one device
+    // serialise here (the queue is read back before the next launch uses it)
+    std::lock_guard<std::mutex> g(g_fix_mu);
+    FixBuf& fb = g_fix[dev];
+    if (!fb.count) {
+        if ((e = hipMalloc(&fb.count, sizeof(unsigned long long))) != hipSuccess) return e;
+        if ((e = hipHostMalloc(&fb.h_count, sizeof(unsigned long long))) != hipSuccess) return e;
+    }
+    if (fb.cap == 0) {
+        const uint32_t want = 1u << 20;
+        if ((e = hipMalloc(&fb.items, sizeof(uint2) * want)) != hipSuccess) return e;
+        fb.cap = want;
+    }
+    for (int attempt = 0; attempt < 2; attempt++) {
+        if ((e = hipMemsetAsync(fb.count, 0, sizeof(unsigned long long), s)) != hipSuccess) return e;
+        const strict::FixQueue fq{fb.items, fb.count, fb.cap};
+        hipLaunchKernelGGL((strict::k_build_R_strict<NVV, NVS, OCC, RS1>), grid, block, 0, s, recs, ids, nrows, sv,
+                           nvrl, chunk, P, normalization, Rt, ld, row0, roff, rstride, nonzero, counter, fq,
+                           attempt == 0 ? 1 : 0);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        if ((e = hipMemcpyAsync(fb.h_count, fb.count, sizeof(unsigned long long), hipMemcpyDeviceToHost, s)) !=
+            hipSuccess)
+            return e;
+        if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+        const unsigned long long n = *fb.h_count;
+        if (n <= fb.cap) {
+            if (n)
+                hipLaunchKernelGGL((strict::k_build_R_strict_fixup<NVV, NVS, OCC, RS1>),
+                                   dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, recs, ids, sv, P,
+                                   normalization, Rt, ld, row0, roff, rstride, nonzero, fb.items, (uint32_t)n);
+            return hipGetLastError();
+        }
+        // the queue overflowed (its first cap entries were kept, every other
+        // entry is stored): grow it and run again to list the queued entries
+        // only -- no stores, no counts -- then re-evaluate them
+        if (attempt == 1 || n > 0xFFFFFFFFull) return hipErrorOutOfMemory;
+        hipFree(fb.items);
+        fb.items = nullptr;
+        fb.cap = 0;
+        if ((e = hipMalloc(&fb.items, sizeof(uint2) * n)) != hipSuccess) return e;
+        fb.cap = (uint32_t)n;
+    }
+    return hipErrorUnknown;
+}
+
 template <int NVV, int NVS, bool OCC>
-static void launch_rs(bool rs1, dim3 grid, dim3 block, hipStream_t s, const Rec* recs, const uint32_t* ids,
-                      uint32_t nrows, const strict::StrictVrl* sv, uint32_t nvrl, uint32_t chunk,
-                      const DevParams& P, float normalization, float2* Rt, uint64_t ld, uint64_t row0,
-                      const uint64_t* roff, const uint32_t* rstride, uint8_t* nonzero,
-                      unsigned long long* counter)
+static hipError_t launch_rs(bool rs1, dim3 grid, dim3 block, hipStream_t s, const Rec* recs, const uint32_t* ids,
+                            uint32_t nrows, const strict::StrictVrl* sv, uint32_t nvrl, uint32_t chunk,
+                            const DevParams& P, float normalization, float2* Rt, uint64_t ld, uint64_t row0,
+                            const uint64_t* roff, const uint32_t* rstride, uint8_t* nonzero,
+                            unsigned long long* counter)
 {
     if (rs1)
-        hipLaunchKernelGGL((strict::k_build_R_strict<NVV, NVS, OCC, true>), grid, block, 0, s, recs, ids, nrows,
-                           sv, nvrl, chunk, P, normalization, Rt, ld, row0, roff, rstride, nonzero, counter);
-    else
-        hipLaunchKernelGGL((strict::k_build_R_strict<NVV, NVS, OCC, false>), grid, block, 0, s, recs, ids, nrows,
-                           sv, nvrl, chunk, P, normalization, Rt, ld, row0, roff, rstride, nonzero, counter);
+        return run_strict<NVV, NVS, OCC, true>(grid, block, s, recs, ids, nrows, sv, nvrl, chunk, P,
+                                               normalization, Rt, ld, row0, roff, rstride, nonzero, counter);
+    return run_strict<NVV, NVS, OCC, false>(grid, block, s, recs, ids, nrows, sv, nvrl, chunk, P, normalization,
+                                            Rt, ld, row0, roff, rstride, nonzero, counter);
 }
 
 hipError_t launch_build_R_strict(const Rec* recs, const uint32_t* ids, uint32_t nrows, const void* svrl,
@@ -636,15 +810,13 @@ hipError_t launch_build_R_strict(const Rec* recs, const uint32_t* ids, uint32_t 
     const auto* sv = reinterpret_cast<const strict::StrictVrl*>(svrl);
     const bool rs1 = P.rsamples <= 1;
     if (P.occ.ntri)
-        launch_rs<-1, -1, true>(rs1, grid, block, s, recs, ids, nrows, sv, nvrl, chunk, P, normalization, Rt, ld,
-                                row0, roff, rstride, nonzero, counter);
-    else if (P.nvv == 2 && P.nvs == 2)
-        launch_rs<2, 2, false>(rs1, grid, block, s, recs, ids, nrows, sv, nvrl, chunk, P, normalization, Rt, ld,
-                               row0, roff, rstride, nonzero, counter);
-    else
-        launch_rs<-1, -1, false>(rs1, grid, block, s, recs, ids, nrows, sv, nvrl, chunk, P, normalization, Rt,
-                                 ld, row0, roff, rstride, nonzero, counter);
-    return hipGetLastError();
+        return launch_rs<-1, -1, true>(rs1, grid, block, s, recs, ids, nrows, sv, nvrl, chunk, P, normalization, Rt,
+                                       ld, row0, roff, rstride, nonzero, counter);
+    if (P.nvv == 2 && P.nvs == 2)
+        return launch_rs<2, 2, false>(rs1, grid, block, s, recs, ids, nrows, sv, nvrl, chunk, P, normalization, Rt,
+                                      ld, row0, roff, rstride, nonzero, counter);
+    return launch_rs<-1, -1, false>(rs1, grid, block, s, recs, ids, nrows, sv, nvrl, chunk, P, normalization, Rt,
+                                    ld, row0, roff, rstride, nonzero, counter);
 }
 
 hipError_t launch_detmath(int fn, const float* in, float* out, uint32_t n, hipStream_t s)
@@ -665,6 +837,7 @@ hipError_t launch_detmath_exhaustive(int fn, uint64_t begin, uint64_t end, unsig
     case 3: hipLaunchKernelGGL(strict::k_detmath_exhaustive<3>, grid, block, 0, s, begin, end, out, first); break;
     case 4: hipLaunchKernelGGL(strict::k_detmath_exhaustive<4>, grid, block, 0, s, begin, end, out, first); break;
     case 5: hipLaunchKernelGGL(strict::k_detmath_exhaustive<5>, grid, block, 0, s, begin, end, out, first); break;
+    case 6: hipLaunchKernelGGL(strict::k_detmath_exhaustive<6>, grid, block, 0, s, begin, end, out, first); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -386,7 +386,13 @@ public:
         if (v == params.end())
             return;
         std::lock_guard<std::mutex> install(m_wakeLock);
-        if (v->second == m_pubVrls || v->second == m_installedVrls)
+        if (v->second == m_pubVrls)
+            return;
+        /* a pass is identified by its number, not by the object's address (a
+           later pass's set can be allocated where the freed previous one was) */
+        const int64_t passKey = (int64_t) static_cast<const AmdVrlSet *>(v->second)->m_pass
+            + (c != params.end() ? ((int64_t) static_cast<const AmdClusterInfo *>(c->second)->m_pass + 1) << 32 : 0);
+        if (passKey == m_installedPass)
             return;
         const Scene *scene = static_cast<const Scene *>(parent);
         if (!m_ready && scene)
@@ -410,7 +416,7 @@ public:
                 m_pass = (int) vs->m_pass;
             }
         }
-        m_installedVrls = v->second;
+        m_installedPass = passKey;
         std::lock_guard<std::mutex> g(m_frameLock);
         m_framePass = -1;
     }
@@ -443,7 +449,11 @@ public:
      * gathers' counter streams as in renderBlock. */
     Spectrum Li(const RayDifferential &ray, RadianceQueryRecord &rRec) const {
         std::vector<alvrl_gather_rec> recs;
-        appendPath(ray, rRec, Spectrum(1.0f), Spectrum(m_initialSpecularThroughput), 0u, &recs);
+        /* the sampler's sample index keys this call's counter streams (depth
+           word, sampleIndex << 16), so repeated calls for one pixel draw
+           fresh uniforms as the reference's rRec.sampler does */
+        const uint32_t sampleIndex = rRec.sampler ? (uint32_t) (rRec.sampler->getSampleIndex() & 0xFFFFu) : 0u;
+        appendPath(ray, rRec, Spectrum(1.0f), Spectrum(m_initialSpecularThroughput), sampleIndex, &recs);
         const uint32_t n = (uint32_t) recs.size();
         if (!n)
             return Spectrum(0.0f);
@@ -634,7 +644,7 @@ private:
                     lmesh = dynamic_cast<const TriMesh *>(scene->getShapes()[s].get());
             if (!lmesh)
                 Log(EError, "vrl (amd) frame mode: the area emitter must sit on a triangle mesh");
-            appendTriangles(lmesh, &m_emit);
+            appendEmitterTriangles(lmesh, &m_emit);
             put3(m_desc.emitter_radiance, light->evalPosition(pRec) * (Float) INV_PI);
         } else {
             Log(EError, "vrl (amd) frame mode needs a point light or an area emitter (amdMode=records takes any)");
@@ -771,6 +781,41 @@ private:
                 out->push_back((float) p.y);
                 out->push_back((float) p.z);
             }
+    }
+
+    /* An area emitter's triangles for the library, which emits on the side of
+     * cross(p1 - p0, p2 - p0).  Mitsuba emits on the side of the shading
+     * normal Triangle::sample interpolates from the vertex normals
+     * (triangle.cpp:34-42), and flipNormals negates those normals without
+     * touching the winding (trimesh.cpp:623-627, 660-664; the winding is
+     * swapped only without normals, :615-620): a triangle whose vertex
+     * normals point against its winding normal is handed over with p0 and p1
+     * swapped.  Normals that are not one direction per triangle (a curved
+     * light) have no equivalent here and are refused. */
+    static void appendEmitterTriangles(const TriMesh *mesh, std::vector<float> *out) {
+        const Point *pos = mesh->getVertexPositions();
+        const Triangle *tri = mesh->getTriangles();
+        const Normal *nrm = mesh->hasVertexNormals() ? mesh->getVertexNormals() : NULL;
+        for (size_t f = 0; f < mesh->getTriangleCount(); ++f) {
+            int order[3] = {0, 1, 2};
+            if (nrm) {
+                const Point &p0 = pos[tri[f].idx[0]], &p1 = pos[tri[f].idx[1]], &p2 = pos[tri[f].idx[2]];
+                const Vector g = cross(p1 - p0, p2 - p0);
+                const Vector n0(nrm[tri[f].idx[0]]), n1(nrm[tri[f].idx[1]]), n2(nrm[tri[f].idx[2]]);
+                const Float tol = 1e-4f;
+                if (dot(n0, n1) < 1 - tol || dot(n0, n2) < 1 - tol)
+                    Log(EError, "vrl (amd) frame mode: area emitter \"%s\" has smooth vertex normals (a curved "
+                        "light); use faceNormals=true or amdMode=records", mesh->getName().c_str());
+                if (dot(n0 + n1 + n2, g) < 0)
+                    std::swap(order[0], order[1]);
+            }
+            for (int k = 0; k < 3; ++k) {
+                const Point &p = pos[tri[f].idx[order[k]]];
+                out->push_back((float) p.x);
+                out->push_back((float) p.y);
+                out->push_back((float) p.z);
+            }
+        }
     }
 
     /* every vertex on a face of the box: the mesh is the box itself */
@@ -1198,7 +1243,8 @@ private:
     alvrl_local_exchange *m_localEx = NULL;
     /* wakeup: the VRL resource this instance published (the master) and the
      * last one it installed (a render worker) */
-    const SerializableObject *m_pubVrls = NULL, *m_installedVrls = NULL;
+    const SerializableObject *m_pubVrls = NULL;
+    int64_t m_installedPass = -1;   /* the pass (VRL set, cluster info) wakeup installed last */
     std::mutex m_wakeLock;
     /* the current pass's frame (frame mode) */
     mutable std::vector<float> m_rgb;

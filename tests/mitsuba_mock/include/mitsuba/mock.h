@@ -194,8 +194,11 @@ struct Vector {
     Vector(Float x, Float y, Float z);
     Float operator[](int i) const;
     Vector operator-() const;
+    Vector operator+(const Vector &v) const;
 };
 struct Normal : public Vector { };
+Vector cross(const Vector &a, const Vector &b);
+Float dot(const Vector &a, const Vector &b);
 struct Point {
     Float x, y, z;
     Point();
@@ -203,6 +206,7 @@ struct Point {
     Point(Float x, Float y, Float z);
     Float operator[](int i) const;
     Point operator+(const Vector &v) const;
+    Vector operator-(const Point &p) const;
 };
 struct Frame {
     Vector s, t;
@@ -290,6 +294,7 @@ public:
     virtual Float next1D() = 0;
     virtual Point2 next2D() = 0;
     size_t getSampleCount() const;
+    size_t getSampleIndex() const;
 };
 
 struct MediumSamplingRecord {
@@ -408,6 +413,8 @@ public:
     AABB getAABB() const;
     ref<TriMesh> createTriMesh();
     const Point *getVertexPositions() const;
+    const Normal *getVertexNormals() const;
+    bool hasVertexNormals() const;
     const Triangle *getTriangles() const;
     size_t getTriangleCount() const;
 };

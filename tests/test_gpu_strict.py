@@ -65,17 +65,32 @@ def test_detmath_device_matches_host(oracle, gpu_ok):
         assert same.all(), (fn, x[~same][:4], dev[~same][:4], host[~same][:4])
 
 
-@pytest.mark.parametrize("fn", ["exp", "atan", "tan", "asinh", "sinh"])
+@pytest.mark.parametrize("fn", ["exp", "atan", "tan", "asinh", "sinh", "sqrt"])
 def test_detmath_fast_exhaustive(fn, gpu_ok):
     """csrc/detmath_fast.h (the strict R build's transcendentals: a short f64
     evaluation and Ziv's rounding test, detmath.h when the rounding is in
-    doubt) returns detmath.h's float for EVERY one of the 2^32 float inputs."""
+    doubt; its square root: v_sqrt_f32 and the one-ulp correction, IEEE sqrtf
+    outside the range where that is exact) returns detmath.h's float -- IEEE
+    sqrtf's for sqrt -- for EVERY one of the 2^32 float inputs."""
     import time
     import alvrl
     t0 = time.perf_counter()
     bad, first = alvrl.detmath_exhaustive(fn)
     print(f"[{fn}] 2^32 inputs in {time.perf_counter() - t0:.1f} s, {bad} differ")
     assert bad == 0, (fn, bad, [hex(b) for b in first])
+
+
+def test_fast_division_matches_ieee(gpu_ok):
+    """The strict kernels' division (the IEEE expansion's core without its
+    scaling, IEEE division outside [2^-40, 2^40]) equals IEEE a / b bit for
+    bit on 2^34 random operand pairs: half over all bit patterns, half
+    log-uniform around the fast range's edges."""
+    import time
+    import alvrl
+    t0 = time.perf_counter()
+    bad, first = alvrl.detmath_div_check(1 << 34, seed=20261018)
+    print(f"2^34 pairs in {time.perf_counter() - t0:.1f} s, {bad} differ")
+    assert bad == 0, [(hex(a), hex(b)) for a, b in first]
 
 
 def _strict_R(oracle, w, h, nvrl, step, medium=("balance", -1, 0.0), phase=(0, 0.0), short=True,

@@ -45,7 +45,8 @@ def main():
             rb.append(st["ms_rbuild"])
             rf.append(st["ms_refine"])
             print(json.dumps({"mode": m, "pass": p, "rbuild_ms": rb[-1], "refine_ms": rf[-1],
-                              "wall_ms": wall[-1]}), flush=True)
+                              "wall_ms": wall[-1], "contrib_preprocess": st["contrib_preprocess"],
+                              "contrib_render": st["contrib_render"]}), flush=True)
         print(json.dumps({"mode": m, "config": a.config, "rbuild_ms_mean": sum(rb) / len(rb),
                           "refine_ms_mean": sum(rf) / len(rf), "prepass_wall_ms_mean": sum(wall) / len(wall),
                           "build_id": alvrl.build_info()["build_id"]}), flush=True)
