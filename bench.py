@@ -359,8 +359,15 @@ def main():
                 out["records_mode"] = records_mode(cfg, vrls, pc, args.warmup + args.steps + 10, gpu)
             if not args.no_unconditional:
                 out["pixel_rmse_vs_cpu_unconditional"] = unconditional_parity(
-                    cfg, vrls, pc, args.warmup + args.steps - 1, fb.view(-1, 3).cpu().numpy(), gpu,
-                    row_stride=args.cpu_row_stride, fast_clusters=it.clusters())
+                    cfg, vrls, pc, args.warmup + args.steps - 1, fb.view(-1, 3).cpu().numpy(), it, gpu,
+                    row_stride=args.cpu_row_stride)
+                u = out["pixel_rmse_vs_cpu_unconditional"]
+                d = u["default_vs_oracle_pipeline"]
+                # the headline's per-pixel RMSE vs the CPU reference: the
+                # oracle's own pipeline (no device result fed to it)
+                out["pixel_rmse_vs_cpu"]["unconditional"] = dict(d, within_gather_tolerance=bool(
+                    d["median_rel"] <= 1e-6 and d["q99_rel"] <= 1e-4 and d["max_rel"] <= 5e-2),
+                    all_pins_identical=u["all_pins_identical"])
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
@@ -489,24 +496,30 @@ def cpu_baseline_prepass(args, cfg, vrls, pc, it, render_base, pre_pairs_step, r
             "refine_parity": parity}
 
 
-def unconditional_parity(cfg, vrls, pc, pass_, fast_frame, device=0, row_stride=64, fast_clusters=None,
-                         check_slice=True):
-    """The default (fast) pipeline's frame of pass `pass_` against the CPU
-    restatement's OWN pipeline of that pass -- its own R, its own clusters --
-    on every `row_stride`-th image row, with no device result fed to the
-    oracle.
+def unconditional_parity(cfg, vrls, pc, pass_, frame, it, device=0, row_stride=64, pin_slices=True,
+                         fast_reference=True):
+    """The benchmarked (default, strict R) pipeline's frame of pass `pass_`
+    against the CPU restatement's OWN pipeline of that pass, on every
+    `row_stride`-th image row.  `it` is the integrator
+    that rendered `frame` and still holds that pass.
 
     The oracle's pipeline over the full R (1.6e9 pairs at C4) takes minutes on
-    the host, so its cluster lists are taken from the strict device pipeline
-    (strictRbuild: R bit-identical to the oracle's, refinement bit-exact given
-    R, tests/test_gpu_strict.py), and that identity is re-checked here at this
-    scale on the median slice: the oracle's R rows of its representatives
-    against the strict device's, bit for bit, and the oracle's refinement of
-    them against the strict device's list.  The oracle then renders the
-    sampled rows with those lists (its own clustered gather).
+    the host, so it is re-derived here on three slices -- the median-size, the
+    largest and the one with the most clusters: the oracle's own R rows of the
+    slice's representatives (oracle.gather_brute) against the device's, bit for
+    bit, and the oracle's refinement of those rows (oracle.cluster_refine)
+    against the device's list.  The device's pipeline computes every slice
+    with the same kernels (R bit-identical to the oracle's for every strategy
+    and scene in tests/test_gpu_strict.py, refinement bit-exact given R), so
+    its lists are the oracle's own; the oracle then renders the sampled rows
+    with them (its own clustered gather), and the device frame must meet the
+    gather tolerance of tests/test_gpu_parity.py against it.
 
-    The bar is the pass-to-pass noise of the method: the same comparison
-    between the oracle's frames of pass `pass_` and `pass_ + 1`."""
+    fast_reference: the fast R build (strictRbuild=false, the gathers' maths)
+    through the same pass, for the record: its cluster lists differ from the
+    oracle's (float rounding flips discrete decisions), so it is held to the
+    method's noise -- the RMSE between the oracle's frames of pass `pass_` and
+    `pass_ + 1` -- not to the float tolerance."""
     import numpy as np
     import torch
     import alvrl
@@ -514,26 +527,26 @@ def unconditional_parity(cfg, vrls, pc, pass_, fast_frame, device=0, row_stride=
     o = Oracle()                                 # the strict (IEEE) build: the parity checker
     W, H = cfg["w"], cfg["h"]
     threads = cpu_threads()
-    props = cfg["props"] + (";" if cfg["props"] else "") + f"strictRbuild=true;seed={SEED_RNG}"
+    base_props = cfg["props"] + (";" if cfg["props"] else "") + f"seed={SEED_RNG}"
     rows = np.arange(0, H, row_stride)
     pix = (rows[:, None] * W + np.arange(W)[None, :]).reshape(-1).astype(np.uint32)
     recs_all = o.records(o.scene(W, H))
     recs = recs_all[pix]
     xs, ys = pix % W, pix // W
+    kv = dict(x.split("=", 1) for x in cfg["props"].split(";") if "=" in x)
 
-    def strict_pass(p):
-        it = alvrl.Integrator(props, device=device)
-        it.set_vrls(vrls, pc)
-        it.preprocess(alvrl.scene_default(W, H))
-        t0 = time.perf_counter()
-        it.prepass(p)
+    def device_pass(p, strict):
+        it2 = alvrl.Integrator(base_props + f";strictRbuild={'true' if strict else 'false'}", device=device)
+        it2.set_vrls(vrls, pc)
+        it2.preprocess(alvrl.scene_default(W, H))
+        it2.prepass(p)
         fb = torch.zeros(W * H * 3, dtype=torch.float32, device=torch.device("cuda", device))
-        it.render(fb)
+        it2.render(fb)
         torch.cuda.synchronize(device)
-        return it, fb.view(-1, 3).cpu().numpy(), time.perf_counter() - t0
+        return it2, fb.view(-1, 3).cpu().numpy()
 
-    def oracle_frame(it, p):
-        cl, p2s = it.clusters(), it.slices()
+    def oracle_frame(itx, p):
+        cl, p2s = itx.clusters(), itx.slices()
         P = o.params(o.medium(), seed=SEED_RNG, pass_=p)
         img, _ = o.gather_clustered(P, recs, p2s[ys + H * xs], vrls, pc, cl["slice_off"], cl["reps"],
                                     cl["weights"], cl["fb_reps"], cl["fb_weights"], rec_ids=pix, nthreads=threads)
@@ -546,55 +559,68 @@ def unconditional_parity(cfg, vrls, pc, pass_, fast_frame, device=0, row_stride=
                 "q99_rel": float(np.quantile(rel, 0.99)), "max_rel": float(rel.max())}
 
     t0 = time.perf_counter()
-    itS, S, s_wall = strict_pass(pass_)
-    stS = itS.stats()
-    O, clO = oracle_frame(itS, pass_)
-    pin = None
-    if check_slice:
-        off, rp = itS.reps()
+    O, clO = oracle_frame(it, pass_)
+    pins = []
+    if pin_slices:
+        off, rp = it.reps()
         ns = len(off) - 1
-        s = int(np.argsort(np.diff(off), kind="stable")[ns // 2])
-        job = itS.slice_job(s)
-        ids = rp[off[s]:off[s + 1]]
-        rid = ((ids % H) * W + ids // H).astype(np.uint32)           # column-major -> row-major
+        nrows = np.diff(off)
+        ncl = np.diff(clO["slice_off"])
+        picks = {"median": int(np.argsort(nrows, kind="stable")[ns // 2]), "largest": int(np.argmax(nrows)),
+                 "most_clusters": int(np.argmax(ncl))}
         P = o.params(o.medium(), seed=SEED_RNG, pass_=pass_)
-        _, Ro, _ = o.gather_brute(P, recs_all[rid], vrls, pc, rec_ids=rid, domain=2, want_R=True, nthreads=threads)
-        r_same = bool(np.array_equal(np.ascontiguousarray(job["R"].transpose(1, 0, 2)).view(np.uint32),
-                                     Ro.view(np.uint32)))
-        kv = dict(x.split("=", 1) for x in cfg["props"].split(";") if "=" in x)
-        reps, w, refined = o.cluster_refine(np.ascontiguousarray(Ro.transpose(1, 0, 2)),
-                                            np.arange(len(rid), dtype=np.uint32), job["locw"], job["init_vrls"],
-                                            job["init_off"], job["pixel_undersampling"],
-                                            float(kv.get("localUndersampling", -1.0)),
-                                            depth_correction=float(kv.get("depthCorrection", 1.0)),
-                                            seed=SEED_RNG, pass_=pass_, stage_refine=3 + 2 * s,
-                                            stage_sample=4 + 2 * s)
-        b, e = clO["slice_off"][s], clO["slice_off"][s + 1]
-        l_same = bool(refined and np.array_equal(reps, clO["reps"][b:e])
-                      and np.array_equal(w.view(np.uint32), clO["weights"][b:e].view(np.uint32)))
-        pin = {"slice": s, "rows": int(len(rid)), "R_bit_identical": r_same, "clusters": int(e - b),
-               "cluster_list_identical": l_same}
-    itS.close()
-    itS2, _, _ = strict_pass(pass_ + 1)
-    O2, _ = oracle_frame(itS2, pass_ + 1)
-    itS2.close()
-    fast = cmp(fast_frame[pix], O)
+        for why, s in picks.items():
+            job = it.slice_job(s)
+            ids = rp[off[s]:off[s + 1]]
+            rid = ((ids % H) * W + ids // H).astype(np.uint32)           # column-major -> row-major
+            tr = time.perf_counter()
+            _, Ro, _ = o.gather_brute(P, recs_all[rid], vrls, pc, rec_ids=rid, domain=2, want_R=True,
+                                      nthreads=threads)
+            tr = time.perf_counter() - tr
+            r_same = bool(np.array_equal(np.ascontiguousarray(job["R"].transpose(1, 0, 2)).view(np.uint32),
+                                         Ro.view(np.uint32)))
+            tc = time.perf_counter()
+            reps, w, refined = o.cluster_refine(np.ascontiguousarray(Ro.transpose(1, 0, 2)),
+                                                np.arange(len(rid), dtype=np.uint32), job["locw"],
+                                                job["init_vrls"], job["init_off"], job["pixel_undersampling"],
+                                                float(kv.get("localUndersampling", -1.0)),
+                                                depth_correction=float(kv.get("depthCorrection", 1.0)),
+                                                seed=SEED_RNG, pass_=pass_, stage_refine=3 + 2 * s,
+                                                stage_sample=4 + 2 * s)
+            tc = time.perf_counter() - tc
+            b, e = clO["slice_off"][s], clO["slice_off"][s + 1]
+            l_same = bool(refined and np.array_equal(reps, clO["reps"][b:e])
+                          and np.array_equal(w.view(np.uint32), clO["weights"][b:e].view(np.uint32)))
+            pins.append({"slice": s, "pick": why, "rows": int(len(rid)), "R_bit_identical": r_same,
+                         "clusters": int(e - b), "cluster_list_identical": l_same,
+                         "oracle_R_s": tr, "oracle_refine_s": tc})
+    it2, _ = device_pass(pass_ + 1, True)
+    O2, _ = oracle_frame(it2, pass_ + 1)
+    it2.close()
     noise = cmp(O2, O)
+    dev = cmp(frame[pix], O)
     out = {"pass": pass_, "pixels": int(len(pix)),
            "sample": f"every {row_stride}th image row; the oracle's clustered gather with its own cluster lists",
-           "fast_vs_oracle_pipeline": fast,
-           "strict_device_vs_oracle_pipeline": cmp(S[pix], O),
+           "default_vs_oracle_pipeline": dev,
            "oracle_pass_to_pass": noise,
-           "rmse_ratio_to_pass_noise": fast["rmse"] / noise["rmse"] if noise["rmse"] > 0 else None,
-           "oracle_lists_pinned_on_slice": pin,
-           "strict_rbuild_ms": float(stS["ms_rbuild"]), "strict_prepass_wall_s": s_wall,
-           "seconds": time.perf_counter() - t0}
-    if fast_clusters is not None:
-        a, b = fast_clusters, clO
+           "oracle_pipeline_pinned_on_slices": pins,
+           "all_pins_identical": bool(pins) and all(q["R_bit_identical"] and q["cluster_list_identical"]
+                                                   for q in pins)}
+    if fast_reference:
+        itF, F = device_pass(pass_, False)
+        stF = itF.stats()
+        a, b = itF.clusters(), clO
         same = sum(1 for s in range(len(a["slice_off"]) - 1)
                    if np.array_equal(a["reps"][a["slice_off"][s]:a["slice_off"][s + 1]],
                                      b["reps"][b["slice_off"][s]:b["slice_off"][s + 1]]))
-        out["fast_slices_with_oracle_lists"] = [same, len(a["slice_off"]) - 1]
+        itF.close()
+        fast = cmp(F[pix], O)
+        out["fast_rbuild_reference"] = {
+            "note": "strictRbuild=false (not the default): held to the method's pass-to-pass noise",
+            "vs_oracle_pipeline": fast, "rmse_ratio_to_pass_noise": fast["rmse"] / noise["rmse"] if noise["rmse"] > 0
+            else None, "slices_with_oracle_lists": [same, len(a["slice_off"]) - 1],
+            "rbuild_ms": float(stF["ms_rbuild"])}
+    out["seconds"] = time.perf_counter() - t0
     return out
 
 

@@ -247,8 +247,10 @@ ALVRL_API int alvrl_build_R_blocks(alvrl_ctx *ctx, const alvrl_gather_rec *d_rec
  * as oracle/alvrl_oracle.c does, with IEEE division / sqrt, no contraction and
  * the deterministic transcendentals of csrc/detmath.h, so every R entry is the
  * oracle's bit for bit and the clustering downstream reproduces the oracle's
- * own pipeline.  Slower than the default fast build.
- * Integrator property "strictRbuild". */
+ * own pipeline.  Slower than the fast build.  A bare
+ * context starts with the fast build; the integrator pipeline
+ * (alvrl_integrator_create) turns this on unless its property "strictRbuild"
+ * is false. */
 ALVRL_API int alvrl_set_strict_rbuild(alvrl_ctx *ctx, int on);
 
 /* csrc/detmath.h on the current device, elementwise over n floats (device

@@ -262,9 +262,12 @@ ALVRL_API void alvrl_local_exchange_destroy(alvrl_local_exchange *g);
 /* ---- host-cast scenes (the Mitsuba plugin's "records" mode) ------------
  * For scenes the descriptor above cannot express -- area and other emitters,
  * any shapes and BSDFs, a medium in any container -- the host application
- * casts every ray with its own scene and traces the VRLs itself
- * (vrlTracer.h:91-230 -> alvrl_integrator_set_vrls before each prepass); the
- * library keeps the per-pair work: R, the clustering and the gathers.
+ * casts every eye ray with its own scene; the library keeps the per-pair work
+ * (R, the clustering and the gathers) and the VRLs: it traces them per pass
+ * itself over a descriptor of the scene's light transport (`tracer` below:
+ * vrlTracer.h:91-230 restated, on the device with the integrator property
+ * gpuTracer), or they come from vrlFile, or the host sets them with
+ * alvrl_integrator_set_vrls before each prepass.
  *
  *   preprocess  alvrl_integrator_preprocess_ext: buildSlices
  *               (Preprocessor.cpp:1130-1193) over the host's gather point of
@@ -297,6 +300,15 @@ typedef struct {
     const float *triangles;
     uint32_t n_triangles;
     const uint32_t *triangle_material;
+    /* The VRL tracer's scene (NULL: the VRLs come from vrlFile or
+     * alvrl_integrator_set_vrls): its medium container (box_min / box_max,
+     * albedo), occluders with materials, the point light or area emitter
+     * (camera fields unused).  Copied by alvrl_integrator_preprocess_ext; each
+     * prepass then traces the pass's VRLs over it (seed vrlSeed, the pass,
+     * vrlTargetNum, shortVrls, maxParticleDepth, rrDepth), on the device with
+     * gpuTracer=true, exactly as alvrl_integrator_prepass does for a
+     * descriptor scene. */
+    const alvrl_scene_desc *tracer;
 } alvrl_scene_ext;
 
 ALVRL_API int alvrl_integrator_preprocess_ext(alvrl_integrator *it, const alvrl_scene_ext *s);
@@ -344,6 +356,9 @@ typedef struct {
     uint64_t refine_entries;
     uint64_t global_clusters;   /* clusters of the globalCluster refinement (0 if off) */
     uint64_t refine_split_entries;   /* the splits' share of refine_entries (alvrl_last_refine_split_entries) */
+    /* host wall time of the last prepass's device allocations (R and its row
+     * tables grown with hipMalloc; zero once they are large enough) */
+    double ms_alloc;
 } alvrl_integrator_stats;
 ALVRL_API int alvrl_integrator_get_stats(alvrl_integrator *it, alvrl_integrator_stats *st);
 /* The device context the integrator drives (for low-level access). */

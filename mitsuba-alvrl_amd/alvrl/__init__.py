@@ -459,7 +459,8 @@ class SceneExt(C.Structure):
     """alvrl_scene_ext: a host-cast scene (the Mitsuba plugin's records mode)."""
     _fields_ = [("width", C.c_int), ("height", C.c_int), ("scene_min", C.c_float * 3),
                 ("scene_max", C.c_float * 3), ("medium", MediumDesc), ("slice_recs", C.c_void_p),
-                ("triangles", C.c_void_p), ("n_triangles", C.c_uint32), ("triangle_material", C.c_void_p)]
+                ("triangles", C.c_void_p), ("n_triangles", C.c_uint32), ("triangle_material", C.c_void_p),
+                ("tracer", C.POINTER(SceneDesc))]
 
 
 class IntegratorStats(C.Structure):
@@ -472,7 +473,7 @@ class IntegratorStats(C.Structure):
                 ("fallback_built", C.c_int), ("slices_local", C.c_uint64), ("rows_built", C.c_uint64),
                 ("ms_exchange", C.c_double), ("ms_refine_kernel", C.c_double),
                 ("refine_entries", C.c_uint64), ("global_clusters", C.c_uint64),
-                ("refine_split_entries", C.c_uint64)]
+                ("refine_split_entries", C.c_uint64), ("ms_alloc", C.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -1028,9 +1029,11 @@ class Integrator:
                                                C.c_void_p(stream) if stream else None))
 
     def preprocess_ext(self, width: int, height: int, slice_recs: np.ndarray, scene_min, scene_max,
-                       medium: "Medium" = None, triangles=None, material=None):
+                       medium: "Medium" = None, triangles=None, material=None, tracer: "SceneDesc" = None):
         """alvrl_integrator_preprocess_ext: buildSlices over the caller's gather
-        points (slice_recs: W*H records, row-major)."""
+        points (slice_recs: W*H records, row-major).  tracer: the VRL tracer's
+        scene (a SceneDesc; its arrays must stay alive for this call): each
+        prepass then traces the pass's VRLs over it (no set_vrls needed)."""
         sr = _np(slice_recs, np.float32)
         if sr.shape != (width * height, REC_WORDS):
             raise ValueError("slice_recs must be (W*H, REC_WORDS)")
@@ -1038,7 +1041,8 @@ class Integrator:
         mat = None if material is None else _np(material, np.uint32)
         e = SceneExt(width, height, (C.c_float * 3)(*scene_min), (C.c_float * 3)(*scene_max),
                      (medium or Medium()).desc(), sr.ctypes.data, None if tri is None else tri.ctypes.data,
-                     0 if tri is None else tri.shape[0], None if mat is None else mat.ctypes.data)
+                     0 if tri is None else tri.shape[0], None if mat is None else mat.ctypes.data,
+                     None if tracer is None else C.pointer(tracer))
         self.scene = e
         self._ext_keep = (sr, tri, mat)
         _hcheck(self.L.alvrl_integrator_preprocess_ext(self.h, C.byref(e)))

@@ -45,11 +45,14 @@
 #define FX_FN static __device__ __forceinline__
 
 // Half-width of the ambiguous band around the float halfway point, in units
-// of the double's last place: 2^10 ulp of double is at least 2^-43 relative,
-// 4x the largest fast-path error bound (the fits' 2^-45.1 plus evaluation
-// rounding) and well above detmath.h's own error (~2 ulp).
+// of the double's last place: 2^13 ulp of double is at least 2^-40 relative,
+// 16x the largest fast-path error bound (2^-44: the exp table's fit and
+// reduction, the other fits' <= 2^-43.5, plus evaluation rounding) and well
+// above detmath.h's own error (~2 ulp).  A lane lands in the band once in
+// 2^15 calls (~44 calls per R entry: 0.13 % of the entries go to the fix-up
+// queue, whose re-evaluation costs well under 1 % of the build).
 #ifndef ALVRL_FX_BAND
-#define ALVRL_FX_BAND (1u << 10)
+#define ALVRL_FX_BAND (1u << 13)
 #endif
 constexpr uint32_t kFxBand = ALVRL_FX_BAND;
 
@@ -75,15 +78,19 @@ FX_FN double fx_kd(double c, double dep)
     return c;
 }
 
-// 1 / d with two Newton steps on v_rcp_f64 (relative error ~2^-52, not
-// correctly rounded; d normal and finite)
+// 1 / d with Newton steps on v_rcp_f64 (d normal and finite; not correctly
+// rounded).  One step (ALVRL_FX_RCP_STEPS) squares v_rcp_f64's relative error.
+#ifndef ALVRL_FX_RCP_STEPS
+#define ALVRL_FX_RCP_STEPS 1
+#endif
 FX_FN double fx_rcp(double d)
 {
     double r = __builtin_amdgcn_rcp(d);
-    double e = fx_fma(-d, r, 1.0);
-    r = fx_fma(r, e, r);
-    e = fx_fma(-d, r, 1.0);
-    return fx_fma(r, e, r);
+    for (int i = 0; i < ALVRL_FX_RCP_STEPS; i++) {
+        const double e = fx_fma(-d, r, 1.0);
+        r = fx_fma(r, e, r);
+    }
+    return r;
 }
 
 // sqrt(s) for s >= 1 (finite): v_rsq_f64 refined by Goldschmidt steps
@@ -101,24 +108,99 @@ FX_FN double fx_sqrt(double s)
     return fx_fma(d, h, g);
 }
 
-// exp(x), |x| <= 87.5: x = k ln2 + r, |r| <= ln2/2, degree-9 fit (2^-45.6)
+// 2^(j/256), j = 0..255 (Python's float pow, within 1 ulp: 2^-52 relative),
+// the table of fx_exp_core.  Each kernel that evaluates fx_expf / fx_sinhf
+// copies it to LDS first (fx_tables_init, all threads of the block).
+__device__ __constant__ const double kFxExp2Tab[256] = {
+    0x1.0000000000000p+0, 0x1.00b1afa5abcbfp+0, 0x1.0163da9fb3335p+0, 0x1.02168143b0281p+0,
+    0x1.02c9a3e778061p+0, 0x1.037d42e11bbccp+0, 0x1.04315e86e7f85p+0, 0x1.04e5f72f654b1p+0,
+    0x1.059b0d3158574p+0, 0x1.0650a0e3c1f89p+0, 0x1.0706b29ddf6dep+0, 0x1.07bd42b72a836p+0,
+    0x1.0874518759bc8p+0, 0x1.092bdf66607e0p+0, 0x1.09e3ecac6f383p+0, 0x1.0a9c79b1f3919p+0,
+    0x1.0b5586cf9890fp+0, 0x1.0c0f145e46c85p+0, 0x1.0cc922b7247f7p+0, 0x1.0d83b23395decp+0,
+    0x1.0e3ec32d3d1a2p+0, 0x1.0efa55fdfa9c5p+0, 0x1.0fb66affed31bp+0, 0x1.1073028d7233ep+0,
+    0x1.11301d0125b51p+0, 0x1.11edbab5e2ab6p+0, 0x1.12abdc06c31ccp+0, 0x1.136a814f204abp+0,
+    0x1.1429aaea92de0p+0, 0x1.14e95934f312ep+0, 0x1.15a98c8a58e51p+0, 0x1.166a45471c3c2p+0,
+    0x1.172b83c7d517bp+0, 0x1.17ed48695bbc0p+0, 0x1.18af9388c8deap+0, 0x1.1972658375d2fp+0,
+    0x1.1a35beb6fcb75p+0, 0x1.1af99f8138a1cp+0, 0x1.1bbe084045cd4p+0, 0x1.1c82f95281c6bp+0,
+    0x1.1d4873168b9aap+0, 0x1.1e0e75eb44027p+0, 0x1.1ed5022fcd91dp+0, 0x1.1f9c18438ce4dp+0,
+    0x1.2063b88628cd6p+0, 0x1.212be3578a819p+0, 0x1.21f49917ddc96p+0, 0x1.22bdda27912d1p+0,
+    0x1.2387a6e756238p+0, 0x1.2451ffb82140ap+0, 0x1.251ce4fb2a63fp+0, 0x1.25e85711ece75p+0,
+    0x1.26b4565e27cddp+0, 0x1.2780e341ddf29p+0, 0x1.284dfe1f56381p+0, 0x1.291ba7591bb70p+0,
+    0x1.29e9df51fdee1p+0, 0x1.2ab8a66d10f13p+0, 0x1.2b87fd0dad990p+0, 0x1.2c57e39771b2fp+0,
+    0x1.2d285a6e4030bp+0, 0x1.2df961f641589p+0, 0x1.2ecafa93e2f56p+0, 0x1.2f9d24abd886bp+0,
+    0x1.306fe0a31b715p+0, 0x1.31432edeeb2fdp+0, 0x1.32170fc4cd831p+0, 0x1.32eb83ba8ea32p+0,
+    0x1.33c08b26416ffp+0, 0x1.3496266e3fa2dp+0, 0x1.356c55f929ff1p+0, 0x1.36431a2de883bp+0,
+    0x1.371a7373aa9cbp+0, 0x1.37f26231e754ap+0, 0x1.38cae6d05d866p+0, 0x1.39a401b7140efp+0,
+    0x1.3a7db34e59ff7p+0, 0x1.3b57fbfec6cf4p+0, 0x1.3c32dc313a8e5p+0, 0x1.3d0e544ede173p+0,
+    0x1.3dea64c123422p+0, 0x1.3ec70df1c5175p+0, 0x1.3fa4504ac801cp+0, 0x1.40822c367a024p+0,
+    0x1.4160a21f72e2ap+0, 0x1.423fb2709468ap+0, 0x1.431f5d950a897p+0, 0x1.43ffa3f84b9d4p+0,
+    0x1.44e086061892dp+0, 0x1.45c2042a7d232p+0, 0x1.46a41ed1d0057p+0, 0x1.4786d668b3237p+0,
+    0x1.486a2b5c13cd0p+0, 0x1.494e1e192aed2p+0, 0x1.4a32af0d7d3dep+0, 0x1.4b17dea6db7d7p+0,
+    0x1.4bfdad5362a27p+0, 0x1.4ce41b817c114p+0, 0x1.4dcb299fddd0dp+0, 0x1.4eb2d81d8abffp+0,
+    0x1.4f9b2769d2ca7p+0, 0x1.508417f4531eep+0, 0x1.516daa2cf6642p+0, 0x1.5257de83f4eefp+0,
+    0x1.5342b569d4f82p+0, 0x1.542e2f4f6ad27p+0, 0x1.551a4ca5d920fp+0, 0x1.56070dde910d2p+0,
+    0x1.56f4736b527dap+0, 0x1.57e27dbe2c4cfp+0, 0x1.58d12d497c7fdp+0, 0x1.59c0827ff07ccp+0,
+    0x1.5ab07dd485429p+0, 0x1.5ba11fba87a03p+0, 0x1.5c9268a5946b7p+0, 0x1.5d84590998b93p+0,
+    0x1.5e76f15ad2148p+0, 0x1.5f6a320dceb71p+0, 0x1.605e1b976dc09p+0, 0x1.6152ae6cdf6f4p+0,
+    0x1.6247eb03a5585p+0, 0x1.633dd1d1929fdp+0, 0x1.6434634ccc320p+0, 0x1.652b9febc8fb7p+0,
+    0x1.6623882552225p+0, 0x1.671c1c70833f6p+0, 0x1.68155d44ca973p+0, 0x1.690f4b19e9538p+0,
+    0x1.6a09e667f3bcdp+0, 0x1.6b052fa75173ep+0, 0x1.6c012750bdabfp+0, 0x1.6cfdcddd47645p+0,
+    0x1.6dfb23c651a2fp+0, 0x1.6ef9298593ae5p+0, 0x1.6ff7df9519484p+0, 0x1.70f7466f42e87p+0,
+    0x1.71f75e8ec5f74p+0, 0x1.72f8286ead08ap+0, 0x1.73f9a48a58174p+0, 0x1.74fbd35d7cbfdp+0,
+    0x1.75feb564267c9p+0, 0x1.77024b1ab6e09p+0, 0x1.780694fde5d3fp+0, 0x1.790b938ac1cf6p+0,
+    0x1.7a11473eb0187p+0, 0x1.7b17b0976cfdbp+0, 0x1.7c1ed0130c132p+0, 0x1.7d26a62ff86f0p+0,
+    0x1.7e2f336cf4e62p+0, 0x1.7f3878491c491p+0, 0x1.80427543e1a12p+0, 0x1.814d2add106d9p+0,
+    0x1.82589994cce13p+0, 0x1.8364c1eb941f7p+0, 0x1.8471a4623c7adp+0, 0x1.857f4179f5b21p+0,
+    0x1.868d99b4492edp+0, 0x1.879cad931a436p+0, 0x1.88ac7d98a6699p+0, 0x1.89bd0a478580fp+0,
+    0x1.8ace5422aa0dbp+0, 0x1.8be05bad61778p+0, 0x1.8cf3216b5448cp+0, 0x1.8e06a5e0866d9p+0,
+    0x1.8f1ae99157736p+0, 0x1.902fed0282c8ap+0, 0x1.9145b0b91ffc6p+0, 0x1.925c353aa2fe2p+0,
+    0x1.93737b0cdc5e5p+0, 0x1.948b82b5f98e5p+0, 0x1.95a44cbc8520fp+0, 0x1.96bdd9a7670b3p+0,
+    0x1.97d829fde4e50p+0, 0x1.98f33e47a22a2p+0, 0x1.9a0f170ca07bap+0, 0x1.9b2bb4d53fe0dp+0,
+    0x1.9c49182a3f090p+0, 0x1.9d674194bb8d5p+0, 0x1.9e86319e32323p+0, 0x1.9fa5e8d07f29ep+0,
+    0x1.a0c667b5de565p+0, 0x1.a1e7aed8eb8bbp+0, 0x1.a309bec4a2d33p+0, 0x1.a42c980460ad8p+0,
+    0x1.a5503b23e255dp+0, 0x1.a674a8af46052p+0, 0x1.a799e1330b358p+0, 0x1.a8bfe53c12e59p+0,
+    0x1.a9e6b5579fdbfp+0, 0x1.ab0e521356ebap+0, 0x1.ac36bbfd3f37ap+0, 0x1.ad5ff3a3c2774p+0,
+    0x1.ae89f995ad3adp+0, 0x1.afb4ce622f2ffp+0, 0x1.b0e07298db666p+0, 0x1.b20ce6c9a8952p+0,
+    0x1.b33a2b84f15fbp+0, 0x1.b468415b749b1p+0, 0x1.b59728de5593ap+0, 0x1.b6c6e29f1c52ap+0,
+    0x1.b7f76f2fb5e47p+0, 0x1.b928cf22749e4p+0, 0x1.ba5b030a1064ap+0, 0x1.bb8e0b79a6f1fp+0,
+    0x1.bcc1e904bc1d2p+0, 0x1.bdf69c3f3a207p+0, 0x1.bf2c25bd71e09p+0, 0x1.c06286141b33dp+0,
+    0x1.c199bdd85529cp+0, 0x1.c2d1cd9fa652cp+0, 0x1.c40ab5fffd07ap+0, 0x1.c544778fafb22p+0,
+    0x1.c67f12e57d14bp+0, 0x1.c7ba88988c933p+0, 0x1.c8f6d9406e7b5p+0, 0x1.ca3405751c4dbp+0,
+    0x1.cb720dcef9069p+0, 0x1.ccb0f2e6d1675p+0, 0x1.cdf0b555dc3fap+0, 0x1.cf3155b5bab74p+0,
+    0x1.d072d4a07897cp+0, 0x1.d1b532b08c968p+0, 0x1.d2f87080d89f2p+0, 0x1.d43c8eacaa1d6p+0,
+    0x1.d5818dcfba487p+0, 0x1.d6c76e862e6d3p+0, 0x1.d80e316c98398p+0, 0x1.d955d71ff6075p+0,
+    0x1.da9e603db3285p+0, 0x1.dbe7cd63a8315p+0, 0x1.dd321f301b460p+0, 0x1.de7d5641c0658p+0,
+    0x1.dfc97337b9b5fp+0, 0x1.e11676b197d17p+0, 0x1.e264614f5a129p+0, 0x1.e3b333b16ee12p+0,
+    0x1.e502ee78b3ff6p+0, 0x1.e653924676d76p+0, 0x1.e7a51fbc74c83p+0, 0x1.e8f7977cdb740p+0,
+    0x1.ea4afa2a490dap+0, 0x1.eb9f4867cca6ep+0, 0x1.ecf482d8e67f1p+0, 0x1.ee4aaa2188510p+0,
+    0x1.efa1bee615a27p+0, 0x1.f0f9c1cb6412ap+0, 0x1.f252b376bba97p+0, 0x1.f3ac948dd7274p+0,
+    0x1.f50765b6e4540p+0, 0x1.f6632798844f8p+0, 0x1.f7bfdad9cbe14p+0, 0x1.f91d802243c89p+0,
+    0x1.fa7c1819e90d8p+0, 0x1.fbdba3692d514p+0, 0x1.fd3c22b8f71f1p+0, 0x1.fe9d96b2a23d9p+0,
+};
+__shared__ double fx_exp2_lds[256];
+
+// Every thread of the block calls this before its first fx_expf / fx_sinhf
+FX_FN void fx_tables_init()
+{
+    for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) fx_exp2_lds[i] = kFxExp2Tab[i];
+    __syncthreads();
+}
+
+// exp(x), |x| <= 87.5: x = (256 k + j) ln2/256 + r, |r| <= ln2/512:
+// 2^k 2^(j/256) (1 + r q(r)), q a degree-2 fit of expm1(r)/r (2^-44.7
+// relative on exp), one-constant reduction (error <= 32,300 x 2^-61.4 ln2/256
+// absolute on r: 2^-46.4), the table entry (2^-52): within 2^-44 overall
 FX_FN double fx_exp_core(double x)
 {
-    const double t = fx_fma(x, DM_LOG2E, 0x1.8p52);      // k in the low word (round to nearest)
+    const double t = fx_fma(x, 0x1.71547652b82fep+8, 0x1.8p52);   // 256/ln2; n in the low word
     const double kd = t - 0x1.8p52;
-    const int k = (int)(uint32_t)__double_as_longlong(t);
-    double r = fx_fma(kd, -DM_LN2, x);
-    r = fx_fma(kd, -0x1.abc9e3b39803fp-56, r);     // ln2 - DM_LN2
-    double p = fx_fma(r, 0x1.72e1082a74e98p-19, 0x1.a17df15fe496fp-16);
-    p = fx_fma(p, r, fx_kd(0x1.a01994c7f6f2cp-13, p));
-    p = fx_fma(p, r, fx_kd(0x1.6c162bb7680d6p-10, p));
-    p = fx_fma(p, r, fx_kd(0x1.11111123bf2a8p-7, p));
-    p = fx_fma(p, r, fx_kd(0x1.55555588b87a9p-5, p));
-    p = fx_fma(p, r, fx_kd(0x1.5555555550d87p-3, p));
-    p = fx_fma(p, r, fx_kd(0x1.ffffffffe74efp-2, p));
-    p = fx_fma(p, r, fx_kd(0x1.0000000000006p+0, p));
-    p = fx_fma(p, r, fx_kd(0x1.000000000003dp+0, p));
-    return __builtin_amdgcn_ldexp(p, k);
+    const int n = (int)(uint32_t)__double_as_longlong(t);
+    const double r = fx_fma(kd, -0x1.62e42fefa39efp-9, x);         // ln2/256
+    const double r2 = r * r;
+    const double q = fx_fma(r, 0x1.555556deebd69p-3, 0x1.000001ebfc21fp-1);
+    const double p = fx_fma(r2, q, r);
+    const double T = fx_exp2_lds[n & 255];
+    return __builtin_amdgcn_ldexp(fx_fma(T, p, T), n >> 8);
 }
 
 // The _r forms return the fast float and set `slow` when it may differ from
@@ -161,7 +243,7 @@ FX_FN float fx_atanf_r(float x, bool& slow)
 }
 
 // tan(x), |x| <= 2^16: x = k pi/2 + r, |r| <= pi/4 (+), sin r / cos r
-// (degree-5 / 6 fits in r^2: 2^-47.6, 2^-52.7), one division
+// (degree-5 fits in r^2: 2^-47.6, 2^-43.5), one division
 FX_FN float fx_tanf_r(float x, bool& slow)
 {
     const double xd = (double)x;
@@ -177,12 +259,11 @@ FX_FN float fx_tanf_r(float x, bool& slow)
     s = fx_fma(s, z, fx_kd(-0x1.5555555550efdp-3, s));
     s = fx_fma(s, z, fx_kd(0x1.fffffffffffd9p-1, s));
     const double sn = r * s;
-    double c = fx_fma(z, 0x1.1b8af4e3db6c4p-29, -0x1.27df4008bd308p-22);
-    c = fx_fma(c, z, fx_kd(0x1.a019f7fd83c78p-16, c));
-    c = fx_fma(c, z, fx_kd(-0x1.6c16c163c5a2dp-10, c));
-    c = fx_fma(c, z, fx_kd(0x1.555555554e7ebp-5, c));
-    c = fx_fma(c, z, fx_kd(-0x1.fffffffffff79p-2, c));
-    c = fx_fma(c, z, 1.0);
+    double c = fx_fma(z, -0x1.23c5c0cad2c16p-22, 0x1.a00e9682df8e9p-16);
+    c = fx_fma(c, z, fx_kd(-0x1.6c16b2d3e066cp-10, c));
+    c = fx_fma(c, z, fx_kd(0x1.5555554476398p-5, c));
+    c = fx_fma(c, z, fx_kd(-0x1.ffffffffe3762p-2, c));
+    c = fx_fma(c, z, fx_kd(0x1.ffffffffffe0bp-1, c));
     const bool odd = k & 1u;
     const double num = odd ? -c : sn;
     const double den = odd ? sn : c;
@@ -228,7 +309,7 @@ FX_FN float fx_asinhf_r(float x, bool& slow)
     return zero ? 0.0f : (float)y;
 }
 
-// sinh(x): |x| < 1: x P(x^2) (degree-6 fit of sinh(a)/a, 2^-52.2);
+// sinh(x): |x| < 1: x P(x^2) (degree-5 fit of sinh(a)/a, 2^-43.5);
 // 1 <= |x| <= 87: (e - 1/e) / 2 with the exp above
 FX_FN float fx_sinhf_r(float x, bool& slow)
 {
@@ -236,12 +317,11 @@ FX_FN float fx_sinhf_r(float x, bool& slow)
     double r;
     if (a < 1.0) {
         const double z = a * a;
-        double p = fx_fma(z, 0x1.6712f2e298972p-33, 0x1.ae53fbcbba646p-26);
-        p = fx_fma(p, z, fx_kd(0x1.71de50a983cefp-19, p));
-        p = fx_fma(p, z, fx_kd(0x1.a01a0180d218ap-13, p));
-        p = fx_fma(p, z, fx_kd(0x1.1111111125edbp-7, p));
-        p = fx_fma(p, z, fx_kd(0x1.5555555555407p-3, p));
-        p = fx_fma(p, z, 1.0);
+        double p = fx_fma(z, 0x1.b6be36e12230dp-26, 0x1.71cb623ab9f8ap-19);
+        p = fx_fma(p, z, fx_kd(0x1.a01a28c329346p-13, p));
+        p = fx_fma(p, z, fx_kd(0x1.111110ec59911p-7, p));
+        p = fx_fma(p, z, fx_kd(0x1.5555555587b48p-3, p));
+        p = fx_fma(p, z, fx_kd(0x1.ffffffffffd34p-1, p));
         r = a * p;
     } else {
         const double e = fx_exp_core(a);

@@ -32,6 +32,7 @@ namespace host {
 extern thread_local std::string g_host_err;
 SmokeBox to_box(const alvrl_scene_desc& s);
 MediumParams medium_of(const alvrl_medium_desc& d);
+const char* scene_problem(const alvrl_scene_desc& s);
 }  // namespace host
 }  // namespace alvrl
 
@@ -117,7 +118,7 @@ struct alvrl_integrator {
     int rrDepth = 5, maxDepth = -1;
     uint32_t seed = 0xA1B2C3D4u, vrlSeed = 0x5EED0001u;
     bool gpuTracer = false;   // trace the pass's VRLs on the device (csrc/tracer.hip)
-    bool strictRbuild = false;   // the R build in the oracle's arithmetic (alvrl_set_strict_rbuild)
+    bool strictRbuild = true;    // the R build in the oracle's arithmetic (alvrl_set_strict_rbuild); false: the gathers' fast maths
     // ---- state
     int device = 0;
     alvrl_ctx* ctx = nullptr;
@@ -129,6 +130,10 @@ struct alvrl_integrator {
     SmokeBox scene;
     alvrl_scene_desc scene_desc{};
     bool have_scene = false;
+    // host-cast scene: the VRL tracer's scene (alvrl_scene_ext::tracer), owned copy
+    bool have_tracer = false;
+    SmokeBox tracer_box;
+    alvrl_scene_desc tracer_desc{};
     std::unique_ptr<Preprocessor> prep;
     std::vector<uint32_t> pixel_to_slice;   // y + H*x
     VrlSet vrls;
@@ -251,6 +256,7 @@ struct alvrl_integrator {
     void preprocess(const alvrl_scene_desc& s)
     {
         ext = false;
+        have_tracer = false;
         scene = to_box(s);
         scene_desc = s;
         scene_desc.occluders = scene.occ.empty() ? nullptr : scene.occ.data();   // the owned copy
@@ -326,6 +332,18 @@ struct alvrl_integrator {
             for (uint32_t x : b.occ_mat)
                 if (x > ALVRL_MAT_DIELECTRIC) throw IntegError(ALVRL_ERR_INVALID, "alvrl_scene_ext: unknown triangle material");
         }
+        have_tracer = false;
+        if (e.tracer) {   // the VRL tracer's view of the scene, traced every pass
+            if (const char* p = scene_problem(*e.tracer)) throw IntegError(ALVRL_ERR_INVALID, std::string("alvrl_scene_ext::tracer: ") + p);
+            tracer_box = to_box(*e.tracer);
+            tracer_desc = *e.tracer;
+            tracer_desc.occluders = tracer_box.occ.empty() ? nullptr : tracer_box.occ.data();
+            tracer_desc.n_occluders = tracer_box.n_occ();
+            tracer_desc.occluder_material = tracer_box.occ_mat.empty() ? nullptr : tracer_box.occ_mat.data();
+            tracer_desc.emitter_tris = tracer_box.emit.empty() ? nullptr : tracer_box.emit.data();
+            tracer_desc.n_emitter_tris = (uint32_t)(tracer_box.emit.size() / 9);
+            have_tracer = true;
+        }
         scene = b;
         std::memset(&scene_desc, 0, sizeof(scene_desc));
         ext = true;
@@ -398,7 +416,7 @@ struct alvrl_integrator {
         pass_vrls(pass);
         st.slices_failed = 0;
         st.fallback_built = 0;
-        st.ms_rbuild = st.ms_refine = st.ms_exchange = st.ms_refine_kernel = 0;
+        st.ms_rbuild = st.ms_refine = st.ms_exchange = st.ms_refine_kernel = st.ms_alloc = 0;
         st.refine_entries = 0;
         st.refine_split_entries = 0;
         st.global_clusters = 0;
@@ -411,27 +429,31 @@ struct alvrl_integrator {
     // the pass's VRLs on the device (:276-287): traced per pass unless preloaded
     void pass_vrls(uint32_t pass)
     {
-        if (ext && !vrls_from_file)
-            throw IntegError(ALVRL_ERR_STATE, "host-cast scene: set the pass's VRLs with alvrl_integrator_set_vrls first");
+        if (ext && !vrls_from_file && !have_tracer)
+            throw IntegError(ALVRL_ERR_STATE, "host-cast scene without a tracer scene: set the pass's VRLs with "
+                             "alvrl_integrator_set_vrls first");
         chk(alvrl_set_pass(ctx, pass), "alvrl_set_pass");
         cur_pass = pass;
-        // VRLs (:276-287): traced per pass unless preloaded from a file
+        // VRLs (:276-287): traced per pass unless preloaded from a file, over
+        // the descriptor scene or a host-cast scene's tracer scene
         if (!vrls_from_file) {
             const double t0 = now_ms();
+            const alvrl_scene_desc& td = ext ? tracer_desc : scene_desc;
+            const SmokeBox& tb = ext ? tracer_box : scene;
             if (gpuTracer) {
                 const uint32_t target = (uint32_t)std::max(vrlTargetNum, 0);
                 uint32_t n = 0;
                 uint64_t pc = 0;
-                chk_host(alvrl_trace_vrls_gpu(&scene_desc, vrlSeed, pass, target, shortVrls ? 1 : 0, maxParticleDepth,
+                chk_host(alvrl_trace_vrls_gpu(&td, vrlSeed, pass, target, shortVrls ? 1 : 0, maxParticleDepth,
                                               rrDepth, nullptr, 0, &n, &pc));
                 vrls.n = n;
                 vrls.particle_count = pc;
                 vrls.soa.assign(9 * (size_t)n, 0.0f);
                 if (n)
-                    chk_host(alvrl_trace_vrls_gpu(&scene_desc, vrlSeed, pass, target, shortVrls ? 1 : 0,
+                    chk_host(alvrl_trace_vrls_gpu(&td, vrlSeed, pass, target, shortVrls ? 1 : 0,
                                                   maxParticleDepth, rrDepth, vrls.soa.data(), n, &n, &pc));
             } else {
-                vrls = trace_vrls(scene, vrlSeed, pass, (uint32_t)std::max(vrlTargetNum, 0), shortVrls,
+                vrls = trace_vrls(tb, vrlSeed, pass, (uint32_t)std::max(vrlTargetNum, 0), shortVrls,
                                   maxParticleDepth, rrDepth);
             }
             st.ms_trace = now_ms() - t0;
@@ -638,12 +660,14 @@ struct alvrl_integrator {
         }
         const uint32_t nb = (uint32_t)ids.size();
         rows_built = nb;
+        const double ta = now_ms();
         rep_recs.ensure(nb);
         rep_ids.ensure(nb);
         rb_off.ensure(nb);
         rb_stride.ensure(nb);
         nz_dev.ensure(nv);
         Rt.ensure((size_t)2 * nv * acc);
+        st.ms_alloc += now_ms() - ta;
         if (nb) {
             hchk(hipMemcpyAsync(rep_ids.p, ids.data(), sizeof(uint32_t) * nb, hipMemcpyHostToDevice, stream), "copy rep ids");
             if (!chains && !ext) chk_host(alvrl_scene_records_gpu(&scene_desc, scat ? 1 : 0, rep_ids.p, nb, rep_recs.p, stream));

@@ -28,6 +28,7 @@
 
 #include <stdint.h>
 
+#include <algorithm>
 #include <mutex>
 
 #include "detmath.h"
@@ -63,15 +64,28 @@ constexpr uint32_t kFlagHit = 1u, kFlagSmooth = 2u, kFlagMedium = 4u;
 // otherwise detmath.h itself.
 template <bool FAST>
 struct Tx {
+#ifdef ALVRL_STRICT_STUB_TX   // developer timing variant: results invalid
+    static __device__ __forceinline__ float exp(float x, bool& s) { return __expf(x); }
+    static __device__ __forceinline__ float atan(float x, bool& s) { return x * 0.7f; }
+    static __device__ __forceinline__ float tan(float x, bool& s) { return x * 1.3f; }
+    static __device__ __forceinline__ float asinh(float x, bool& s) { return x * 0.9f; }
+    static __device__ __forceinline__ float sinh(float x, bool& s) { return x * 1.1f; }
+#else
     static __device__ __forceinline__ float exp(float x, bool& s) { return FAST ? fx_expf_r(x, s) : dm_expf(x); }
     static __device__ __forceinline__ float atan(float x, bool& s) { return FAST ? fx_atanf_r(x, s) : dm_atanf(x); }
     static __device__ __forceinline__ float tan(float x, bool& s) { return FAST ? fx_tanf_r(x, s) : dm_tanf(x); }
     static __device__ __forceinline__ float asinh(float x, bool& s) { return FAST ? fx_asinhf_r(x, s) : dm_asinhf(x); }
     static __device__ __forceinline__ float sinh(float x, bool& s) { return FAST ? fx_sinhf_r(x, s) : dm_sinhf(x); }
+#endif
+#ifdef ALVRL_STRICT_STUB_DIV   // developer timing variant: results invalid
+    static __device__ __forceinline__ float sqrt(float x, bool& s) { return __builtin_amdgcn_sqrtf(x); }
+    static __device__ __forceinline__ float div(float a, float b, bool& s) { return a * __builtin_amdgcn_rcpf(b); }
+#else
     // IEEE sqrt and division: their cores without the scaling (flag outside
     // the range where the scaling is the identity), or the compiler's expansion
     static __device__ __forceinline__ float sqrt(float x, bool& s) { return FAST ? fx_sqrtf_r(x, s) : sqrtf(x); }
     static __device__ __forceinline__ float div(float a, float b, bool& s) { return FAST ? fx_divf_r(a, b, s) : a / b; }
+#endif
 };
 template <bool FAST> __device__ __forceinline__ float lenT(V3 a, bool& s) { return Tx<FAST>::sqrt(len2(a), s); }
 template <bool FAST> __device__ __forceinline__ float distT(V3 a, V3 b, bool& s) { return lenT<FAST>(sub(a, b), s); }
@@ -543,6 +557,7 @@ __global__ void __launch_bounds__(256, ALVRL_STRICT_MINB) k_build_R_strict(const
                                                         uint8_t* __restrict__ nonzero,
                                                         unsigned long long* counter, FixQueue fq, int store)
 {
+    fx_tables_init();
     const uint32_t r = blockIdx.x * 64 + (threadIdx.x & 63);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const bool active = r < nrows;
@@ -613,6 +628,7 @@ __global__ void __launch_bounds__(256) k_build_R_strict_fixup(const Rec* __restr
 __global__ void __launch_bounds__(256) k_detmath(int fn, const float* __restrict__ in, float* __restrict__ out,
                                                  uint32_t n)
 {
+    fx_tables_init();
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const float x = in[i];
@@ -651,6 +667,7 @@ __global__ void __launch_bounds__(256) k_detmath_exhaustive(uint64_t begin, uint
                                                             unsigned long long* __restrict__ out,
                                                             uint32_t* __restrict__ first)
 {
+    fx_tables_init();
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     uint32_t bad = 0;
     for (uint64_t b = begin + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < end; b += stride) {
@@ -749,7 +766,10 @@ static hipError_t run_strict(dim3 grid, dim3 block, hipStream_t s, const Rec* re
         if ((e = hipHostMalloc(&fb.h_count, sizeof(unsigned long long))) != hipSuccess) return e;
     }
     if (fb.cap == 0) {
-        const uint32_t want = 1u << 20;
+        // ~0.13 % of the entries are queued (detmath_fast.h's band): room for
+        // 0.4 % of this launch's pairs, at least 2^20
+        const uint64_t pairs = (uint64_t)grid.x * 64u * nvrl;
+        const uint32_t want = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(1u << 20, pairs / 256u), 1u << 30);
         if ((e = hipMalloc(&fb.items, sizeof(uint2) * want)) != hipSuccess) return e;
         fb.cap = want;
     }

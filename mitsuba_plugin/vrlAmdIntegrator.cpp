@@ -4,9 +4,8 @@
  * gather, the reduced matrix R and the per-slice cluster refinement -- on an
  * MI355X through libalvrl.so (include/alvrl.h, include/alvrl_host.h).
  *
- * Build: inside the mitsuba-ALVRL tree, next to the reference plugin's
- * sources (it includes their vrlTracer.h), linked against libalvrl.so and the
- * HIP runtime, and installed as plugins/vrl.so so that scene files keep
+ * Build: inside the mitsuba-ALVRL tree (src/integrators/vrl/), linked
+ * against libalvrl.so and the HIP runtime, and installed as plugins/vrl.so so that scene files keep
  * type="vrl" (INTEGRATION.md "Build").  tests/test_plugin_source.py compiles
  * it here against a mock of exactly the Mitsuba declarations it uses
  * (tests/mitsuba_mock/), whose MTS_IMPLEMENT_CLASS_S expands to
@@ -24,15 +23,19 @@
  *                      per pass; renderBlock copies its block out of that
  *                      frame.  Delta-BSDF chains are expanded by the library.
  *
- *   "records"          Any scene with one homogeneous medium: Mitsuba casts
- *                      every ray itself and the library only does the
- *                      per-pair work.  preprocess casts buildSlices' ray per
- *                      pixel (Preprocessor.cpp:1130-1170); prepass traces the
- *                      VRLs with the host's own vrlTracer (any emitter,
- *                      vrlTracer.h:91-230), casts the representative pixels'
- *                      eye paths for R (vrlIntegrator.cpp:322-330) and hands
- *                      both to the library (alvrl_integrator_prepass_records),
- *                      which builds R and clusters; renderBlock casts the
+ *   "records"          Mitsuba casts every eye ray itself and the library
+ *                      does the per-pair work.  preprocess casts buildSlices'
+ *                      ray per pixel (Preprocessor.cpp:1130-1170); prepass
+ *                      casts the representative pixels' eye paths for R
+ *                      (vrlIntegrator.cpp:322-330) and hands them to the
+ *                      library (alvrl_integrator_prepass_records), which traces
+ *                      the pass's VRLs itself (vrlTracer.h:91-230 restated,
+ *                      on the GPU with gpuTracer=true) over the scene's
+ *                      description -- the medium's container, the triangles
+ *                      of every other shape and their BSDF classes, a point
+ *                      light or an area emitter on a triangle mesh -- or
+ *                      reads vrlFile, in which case any emitter and shape is
+ *                      taken; it builds R and clusters; renderBlock casts the
  *                      eye paths -- LiInternal's recursion into every delta
  *                      component (:445-511) -- and gathers them in one call
  *                      per block (alvrl_gather_clustered_host).  Every
@@ -75,7 +78,6 @@
 
 #include "alvrl.h"
 #include "alvrl_host.h"
-#include "vrlTracer.h"   /* the host's VRL tracer (src/integrators/vrl/), records mode */
 
 MTS_NAMESPACE_BEGIN
 
@@ -254,9 +256,6 @@ public:
         m_specRRdepth = props.getInteger("specularForcedRRdepth", 100);
         m_initialSpecularThroughput = props.getFloat("initialSpecularThroughput", 20);
         m_shortVrls = props.getBoolean("shortVrls", true);
-        m_vrlTargetNum = props.getInteger("vrlTargetNum", 500);
-        m_maxParticleDepth = props.getInteger("maxParticleDepth", -1);
-        m_rrDepth = props.getInteger("rrDepth", 5);
         m_vrlFile = props.getString("vrlFile", "");
 
         std::vector<std::string> names;
@@ -598,9 +597,8 @@ private:
         return medium;
     }
 
-    /* The scene in the library's terms (alvrl_scene_desc): the perspective
-     * camera, the medium and its container box, the point light, and the
-     * remaining triangles as occluders. */
+    /* The scene in the library's terms (alvrl_scene_desc), frame mode: the
+     * perspective camera, then the light transport (describeTransport) */
     void describe(const Scene *scene) {
         alvrl_scene_default(&m_desc, 1, 1);
         const Sensor *sensor = scene->getSensor();
@@ -618,40 +616,53 @@ private:
         }
         m_desc.fov_x_deg = (float) cam->getXFov();
         m_desc.width = m_width; m_desc.height = m_height;
-
-        /* the medium and the shape that contains it */
         if (!sensor->getMedium())
             Log(EError, "vrl (amd) frame mode needs the camera inside the medium (amdMode=records does not)");
-        const Medium *medium = describeMedium(scene, &m_desc.medium);
+        describeTransport(scene, false, &m_desc, &m_tris, &m_mats, &m_emit);
+    }
+
+    /* The light transport the library's VRL tracer (and, in frame mode, its
+     * eye rays) sees: the medium and the shape that contains it, the one
+     * emitter -- a point light or an area emitter on a triangle mesh -- and
+     * every other shape's triangles with its BSDF class.  Frame mode renders
+     * from it; records mode traces the pass's VRLs over it
+     * (alvrl_scene_ext::tracer) and refuses a scene it cannot express unless
+     * a vrlFile supplies the VRLs. */
+    void describeTransport(const Scene *scene, bool records, alvrl_scene_desc *d, std::vector<float> *tris,
+            std::vector<uint32_t> *mats, std::vector<float> *emit) {
+        const char *alt = records ? "records mode traces the VRLs over the scene's description; "
+                                    "a vrlFile takes any scene" : "amdMode=records takes any";
+        const char *mode = records ? "records" : "frame";
+        const Medium *medium = describeMedium(scene, &d->medium);
 
         /* the one emitter: a point light (samplePosition returns its power,
            intensity * 4 pi, point.cpp:81-91) or an area emitter on a triangle
            mesh (alvrl_scene_desc::emitter_tris; its radiance from
            evalPosition = radiance * pi, area.cpp:100-102) */
         if (scene->getEmitters().size() != 1)
-            Log(EError, "vrl (amd) frame mode needs exactly one emitter (amdMode=records takes any emitters)");
+            Log(EError, "vrl (amd) %s mode needs exactly one emitter (%s)", mode, alt);
         const Emitter *light = scene->getEmitters()[0].get();
         PositionSamplingRecord pRec(0.0f);
         const Spectrum power = light->samplePosition(pRec, Point2(0.5f));
-        m_emit.clear();
+        emit->clear();
         if (light->getType() & Emitter::EDeltaPosition) {
-            put3(m_desc.light_intensity, power * (Float) (0.25f * INV_PI));
-            for (int i = 0; i < 3; ++i) m_desc.light_pos[i] = (float) pRec.p[i];
+            put3(d->light_intensity, power * (Float) (0.25f * INV_PI));
+            for (int i = 0; i < 3; ++i) d->light_pos[i] = (float) pRec.p[i];
         } else if (light->getType() & Emitter::EOnSurface) {
             const TriMesh *lmesh = NULL;
             for (size_t s = 0; s < scene->getShapes().size(); ++s)
                 if (scene->getShapes()[s]->isEmitter() && scene->getShapes()[s]->getEmitter() == light)
                     lmesh = dynamic_cast<const TriMesh *>(scene->getShapes()[s].get());
             if (!lmesh)
-                Log(EError, "vrl (amd) frame mode: the area emitter must sit on a triangle mesh");
-            appendEmitterTriangles(lmesh, &m_emit);
-            put3(m_desc.emitter_radiance, light->evalPosition(pRec) * (Float) INV_PI);
+                Log(EError, "vrl (amd) %s mode: the area emitter must sit on a triangle mesh (%s)", mode, alt);
+            appendEmitterTriangles(lmesh, emit);
+            put3(d->emitter_radiance, light->evalPosition(pRec) * (Float) INV_PI);
         } else {
-            Log(EError, "vrl (amd) frame mode needs a point light or an area emitter (amdMode=records takes any)");
+            Log(EError, "vrl (amd) %s mode needs a point light or an area emitter (%s)", mode, alt);
         }
 
         /* the container: the shape whose interior is the medium; its walls' diffuse reflectance */
-        m_tris.clear(); m_mats.clear();
+        tris->clear(); mats->clear();
         bool haveBox = false, haveOccAlbedo = false, haveSpec = false, haveEta = false;
         const ref_vector<Shape> &shapes = scene->getShapes();
         for (size_t s = 0; s < shapes.size(); ++s) {
@@ -661,31 +672,31 @@ private:
             if (sh->getInteriorMedium() == medium && !haveBox) {
                 const AABB box = sh->getAABB();
                 for (int i = 0; i < 3; ++i) {
-                    m_desc.box_min[i] = (float) box.min[i];
-                    m_desc.box_max[i] = (float) box.max[i];
+                    d->box_min[i] = (float) box.min[i];
+                    d->box_max[i] = (float) box.max[i];
                 }
-                if (bsdf) put3(m_desc.albedo, diffuseReflectance(sh, bsdf, true));
+                if (bsdf) put3(d->albedo, diffuseReflectance(sh, bsdf, mode, alt, true));
                 haveBox = true;
                 /* a container that is not the box itself (a rotated or curved
                    mesh) bounds the medium with its own triangles; on the box's
                    faces they tie with its walls, which win */
                 if (const TriMesh *cm = dynamic_cast<const TriMesh *>(sh)) {
                     if (!onBoxFaces(cm, box)) {
-                        const Spectrum rho = diffuseReflectance(sh, bsdf, false);
-                        if (haveOccAlbedo && !sameRgb(rho, m_desc.occluder_albedo))
-                            Log(EError, "vrl (amd) frame mode: a mesh container and diffuse occluders with "
-                                "different reflectances (amdMode=records takes any)");
-                        put3(m_desc.occluder_albedo, rho);
+                        const Spectrum rho = diffuseReflectance(sh, bsdf, mode, alt, false);
+                        if (haveOccAlbedo && !sameRgb(rho, d->occluder_albedo))
+                            Log(EError, "vrl (amd) %s mode: a mesh container and diffuse occluders with "
+                                "different reflectances (%s)", mode, alt);
+                        put3(d->occluder_albedo, rho);
                         haveOccAlbedo = true;
-                        appendTriangles(cm, ALVRL_MAT_DIFFUSE);
+                        appendTriangles(cm, ALVRL_MAT_DIFFUSE, tris, mats);
                     }
                 }
                 continue;
             }
             const TriMesh *mesh = dynamic_cast<const TriMesh *>(sh);
             if (!mesh)
-                Log(EError, "vrl (amd): shape \"%s\" inside the medium is not a triangle mesh "
-                    "(amdMode=records takes any shape)", sh->getName().c_str());
+                Log(EError, "vrl (amd) %s mode: shape \"%s\" inside the medium is not a triangle mesh (%s)",
+                    mode, sh->getName().c_str(), alt);
             uint32_t mat = ALVRL_MAT_DIFFUSE;
             if (bsdf) {
                 const unsigned int type = bsdf->getType();
@@ -694,35 +705,43 @@ private:
                 } else if ((type & BSDF::EDeltaReflection) && !(type & BSDF::EDeltaTransmission) &&
                            !(type & BSDF::ESmooth)) {
                     mat = ALVRL_MAT_MIRROR;
-                    if (!haveSpec) put3(m_desc.occluder_specular, bsdf->getSpecularReflectance(its));
+                    if (!haveSpec) put3(d->occluder_specular, bsdf->getSpecularReflectance(its));
                     haveSpec = true;
                 } else if ((type & BSDF::EDeltaReflection) && (type & BSDF::EDeltaTransmission) &&
                            !(type & BSDF::ESmooth)) {
                     /* smooth dielectric (dielectric.cpp): both delta components */
                     mat = ALVRL_MAT_DIELECTRIC;
-                    if (haveEta && (float) bsdf->getEta() != m_desc.occluder_eta)
-                        Log(EError, "vrl (amd) frame mode: dielectrics with different IORs (amdMode=records takes any)");
-                    m_desc.occluder_eta = (float) bsdf->getEta();
+                    if (haveEta && (float) bsdf->getEta() != d->occluder_eta)
+                        Log(EError, "vrl (amd) %s mode: dielectrics with different IORs (%s)", mode, alt);
+                    d->occluder_eta = (float) bsdf->getEta();
                     haveEta = true;
                 } else if (type & BSDF::EDelta) {
-                    Log(EError, "vrl (amd) frame mode: BSDF of \"%s\" is neither diffuse, mirror, dielectric nor "
-                        "null (amdMode=records follows every delta component)", sh->getName().c_str());
+                    Log(EError, "vrl (amd) %s mode: BSDF of \"%s\" is neither diffuse, mirror, dielectric nor "
+                        "null (%s)", mode, sh->getName().c_str(), alt);
                 } else {
-                    const Spectrum rho = diffuseReflectance(sh, bsdf);
-                    if (haveOccAlbedo && !sameRgb(rho, m_desc.occluder_albedo))
-                        Log(EError, "vrl (amd) frame mode: diffuse occluders with different reflectances "
-                            "(amdMode=records takes any)");
-                    put3(m_desc.occluder_albedo, rho);
+                    const Spectrum rho = diffuseReflectance(sh, bsdf, mode, alt);
+                    if (haveOccAlbedo && !sameRgb(rho, d->occluder_albedo))
+                        Log(EError, "vrl (amd) %s mode: diffuse occluders with different reflectances (%s)",
+                            mode, alt);
+                    put3(d->occluder_albedo, rho);
                     haveOccAlbedo = true;
                 }
             }
-            appendTriangles(mesh, mat);
+            appendTriangles(mesh, mat, tris, mats);
         }
         if (!haveBox)
             Log(EError, "vrl (amd) needs a shape that contains the medium (its interior)");
-        m_desc.n_occluders = (uint32_t) m_mats.size();
-        m_desc.emitter_tris = m_emit.empty() ? NULL : &m_emit[0];
-        m_desc.n_emitter_tris = (uint32_t) (m_emit.size() / 9);
+        bindDesc(d, *tris, *mats, *emit);
+    }
+
+    /* point a descriptor at the arrays that hold its triangles */
+    static void bindDesc(alvrl_scene_desc *d, const std::vector<float> &tris, const std::vector<uint32_t> &mats,
+            const std::vector<float> &emit) {
+        d->occluders = tris.empty() ? NULL : &tris[0];
+        d->occluder_material = mats.empty() ? NULL : &mats[0];
+        d->n_occluders = (uint32_t) mats.size();
+        d->emitter_tris = emit.empty() ? NULL : &emit[0];
+        d->n_emitter_tris = (uint32_t) (emit.size() / 9);
     }
 
     /* The constant diffuse reflectance of a shape's smooth diffuse BSDF,
@@ -730,14 +749,15 @@ private:
      * normal and uv): the descriptor holds one albedo per class of surface,
      * so another smooth BSDF (its vol->surf term is not rho / pi cos) or a
      * textured reflectance is refused with a pointer to records mode */
-    Spectrum diffuseReflectance(const Shape *sh, const BSDF *bsdf, bool container = false) const {
+    Spectrum diffuseReflectance(const Shape *sh, const BSDF *bsdf, const char *mode, const char *alt,
+            bool container = false) const {
         /* the box's walls face the medium whatever the mesh's winding, so a
            two-sided diffuse container is the same surface */
         const std::string cls = bsdf->getClass()->getName();
         if (cls != "SmoothDiffuse" && !(container && cls == "TwoSidedBRDF"))
-            Log(EError, "vrl (amd) frame mode: the BSDF of \"%s\" is %s; its walls and occluders take the "
-                "smooth diffuse BSDF the gathers evaluate (diffuse.cpp:110-118)", sh->getName().c_str(),
-                bsdf->getClass()->getName().c_str());
+            Log(EError, "vrl (amd) %s mode: the BSDF of \"%s\" is %s; its walls and occluders take the "
+                "smooth diffuse BSDF the gathers evaluate (diffuse.cpp:110-118; %s)", mode, sh->getName().c_str(),
+                bsdf->getClass()->getName().c_str(), alt);
         const Point2 at[3] = { Point2(0.25f, 0.25f), Point2(0.5f, 0.75f), Point2(0.875f, 0.125f) };
         Spectrum first(0.0f);
         for (int k = 0; k < 3; ++k) {
@@ -754,8 +774,8 @@ private:
             if (k == 0)
                 first = rho;
             else if (rho != first)
-                Log(EError, "vrl (amd) frame mode: \"%s\" has a textured reflectance (amdMode=records "
-                    "evaluates it per gather point)", sh->getName().c_str());
+                Log(EError, "vrl (amd) %s mode: \"%s\" has a textured reflectance (%s)", mode,
+                    sh->getName().c_str(), alt);
         }
         return first;
     }
@@ -766,9 +786,10 @@ private:
         return v[0] == rgb[0] && v[1] == rgb[1] && v[2] == rgb[2];
     }
 
-    void appendTriangles(const TriMesh *mesh, uint32_t mat) {
-        appendTriangles(mesh, &m_tris);
-        m_mats.resize(m_tris.size() / 9, mat);
+    static void appendTriangles(const TriMesh *mesh, uint32_t mat, std::vector<float> *tris,
+            std::vector<uint32_t> *mats) {
+        appendTriangles(mesh, tris);
+        mats->resize(tris->size() / 9, mat);
     }
 
     static void appendTriangles(const TriMesh *mesh, std::vector<float> *out) {
@@ -859,7 +880,7 @@ private:
             if (bsdf && (bsdf->getType() & BSDF::ENull)) mat = ALVRL_MAT_NULL;
             else if (bsdf && (bsdf->getType() & BSDF::EDeltaTransmission)) mat = ALVRL_MAT_DIELECTRIC;
             else if (bsdf && (bsdf->getType() & BSDF::EDelta)) mat = ALVRL_MAT_MIRROR;
-            appendTriangles(mesh.get(), mat);
+            appendTriangles(mesh.get(), mat, &m_tris, &m_mats);
         }
         e.triangles = m_tris.empty() ? NULL : &m_tris[0];
         e.n_triangles = (uint32_t) m_mats.size();
@@ -894,28 +915,21 @@ private:
             }
         }
         e.slice_recs = sl.empty() ? NULL : &sl[0];
+        /* the VRL tracer's view of the scene (vrlTracer.h:91-230 runs in the
+           library, every pass): needed unless a vrlFile supplies the VRLs */
+        if (m_vrlFile.empty()) {
+            alvrl_scene_default(&m_tdesc, 1, 1);
+            describeTransport(scene, true, &m_tdesc, &m_ttris, &m_tmats, &m_temit);
+            e.tracer = &m_tdesc;
+        }
         check(alvrl_integrator_preprocess_ext(m_it, &e), "alvrl_integrator_preprocess_ext");
     }
 
-    /* records mode prepass: the host's VRLs, then R over the host's eye paths */
+    /* records mode prepass: the library traces the pass's VRLs over the
+     * scene's description (alvrl_scene_ext::tracer, vrl tracing :276-280) or
+     * has read vrlFile in preprocess (:243-252); then R over the host's eye
+     * paths */
     void prepassRecords(const Scene *scene, Sampler *sampler) {
-        if (m_vrlFile.empty()) {   /* vrl tracing (:276-280) */
-            ref<vrlTracer> tracer = new vrlTracer(sampler, m_maxParticleDepth, m_rrDepth);
-            ref<vrlVector> v = tracer->randomWalk(scene, m_vrlTargetNum, m_shortVrls);
-            const size_t n = v->size();
-            std::vector<float> soa(9 * n);
-            for (size_t i = 0; i < n; ++i) {
-                const VRL &l = (*v)[i];
-                Float r, g, b;
-                l.m_power.toLinearRGB(r, g, b);
-                const float f[9] = { (float) l.m_start.x, (float) l.m_start.y, (float) l.m_start.z,
-                                     (float) l.m_end.x, (float) l.m_end.y, (float) l.m_end.z,
-                                     (float) r, (float) g, (float) b };
-                for (int k = 0; k < 9; ++k) soa[(size_t) k * n + i] = f[k];
-            }
-            check(alvrl_integrator_set_vrls(m_it, n ? &soa[0] : NULL, (uint32_t) n,
-                                            std::max<uint64_t>(v->getParticleCount(), 1)), "alvrl_integrator_set_vrls");
-        }   /* else: the library read vrlFile in preprocess (:243-252) */
         if (!m_globalCluster && !m_localRefinement) {
             check(alvrl_integrator_prepass(m_it, m_pass), "alvrl_integrator_prepass");   /* brute force */
             m_p2s.clear();
@@ -1221,13 +1235,16 @@ private:
     bool m_globalCluster = false, m_localRefinement = true, m_shortVrls = true;
     int m_specRRdepth = 100;
     Float m_initialSpecularThroughput = 20;
-    int m_vrlTargetNum = 500, m_maxParticleDepth = -1, m_rrDepth = 5;
     std::string m_vrlFile;
     const Medium *m_medium = NULL;
-    alvrl_scene_desc m_desc;
-    std::vector<float> m_tris;
-    std::vector<uint32_t> m_mats;
-    std::vector<float> m_emit;   /* frame mode: the area emitter's triangles */
+    /* frame mode: the scene (m_desc over m_tris / m_mats / m_emit); records
+     * mode: m_tris / m_mats are every shape's triangles (the gathers'
+     * occluder set) and m_tdesc over m_ttris / m_tmats / m_temit the VRL
+     * tracer's view of the scene */
+    alvrl_scene_desc m_desc, m_tdesc;
+    std::vector<float> m_tris, m_ttris;
+    std::vector<uint32_t> m_mats, m_tmats;
+    std::vector<float> m_emit, m_temit;   /* the area emitter's triangles */
     std::vector<uint32_t> m_p2s;   // the pass's slice of every pixel (column-major); empty: brute force
     int m_width = 0, m_height = 0;
     float *m_fb = NULL;

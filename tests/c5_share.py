@@ -154,6 +154,15 @@ def run_full(props: str = "", nvrl: int = C5_VRLS, width: int = C5_W, height: in
             ex = SimExchange(r, world, ns, masks=masks)
             t0 = time.time()
             it.prepass(pass_, rank=r, world=world, exchange=ex)
+            dt_first = time.time() - t0
+            st_first = it.stats()
+            # the same pass again: the steady state of a rank that keeps its
+            # integrator across passes (R and the refinement's arenas already
+            # allocated, as in the bench); the first pass of a fresh
+            # integrator also pays their hipMalloc
+            ex = SimExchange(r, world, ns, masks=masks)
+            t0 = time.time()
+            it.prepass(pass_, rank=r, world=world, exchange=ex)
             dt = time.time() - t0
             st = it.stats()
             off, _ = it.reps()
@@ -169,14 +178,19 @@ def run_full(props: str = "", nvrl: int = C5_VRLS, width: int = C5_W, height: in
                         ms_refine_kernel=st["ms_refine_kernel"], refine_entries=int(st["refine_entries"]),
                         refine_split_entries=int(st["refine_split_entries"]),
                         contrib_preprocess=int(st["contrib_preprocess"]), slices_failed=int(st["slices_failed"]),
-                        fallback_built=int(st["fallback_built"]), s_prepass=dt,
+                        fallback_built=int(st["fallback_built"]), s_prepass=dt, s_prepass_first=dt_first,
+                        ms_refine_wall_first=st_first["ms_refine"],
+                        ms_alloc=st["ms_alloc"], ms_trace=st["ms_trace"], ms_refine_wall=st["ms_refine"],
+                        ms_exchange=st["ms_exchange"], ms_prepass_wall=st["ms_prepass_wall"],
                         clusters_local=[int(len(own[s][0])) for s in mine],
                         exchange_calls=[c[0] for c in ex.calls])
             per_rank.append(info)
             log(f"C5 rank {r}: {len(mine)} slices, rows {rows.min()}..{rows.max()} (sum {rows.sum()}), "
                 f"R {info['R_bytes'] / 1e9:.1f} GB, R build {info['ms_rbuild']:.0f} ms, "
                 f"refine {info['ms_refine_kernel']:.0f} ms ({info['refine_entries'] / 1e9:.1f}e9 entries), "
-                f"prepass {dt:.1f} s")
+                f"prepass {dt:.1f} s (first pass {dt_first:.1f} s, refine wall {st_first['ms_refine']:.0f} ms; "
+                f"steady: alloc {info['ms_alloc']:.0f} ms, trace {info['ms_trace']:.0f} ms, "
+                f"refine wall {info['ms_refine_wall']:.0f} ms, exchange {info['ms_exchange']:.0f} ms)")
             if r == 0:
                 p2s = it.slices()
                 vrls = it.vrls()

@@ -41,23 +41,39 @@ def test_area_gpu_tracer(alvrl, oracle, gpu_ok, target, short):
         assert rpc == dpc and np.array_equal(ref.view(np.uint32), dev.view(np.uint32))
 
 
-def test_area_scene_records_mode_vs_oracle(alvrl, oracle, gpu_ok):
+@pytest.mark.parametrize("vrl_source", ["set_vrls", "library_gpu_tracer"])
+def test_area_scene_records_mode_vs_oracle(alvrl, oracle, gpu_ok, vrl_source):
+    """vrl_source "library_gpu_tracer" is the Mitsuba plugin's records mode:
+    the scene's transport descriptor goes in as alvrl_scene_ext::tracer and
+    the prepass traces the pass's VRLs on the device (gpuTracer=true); they
+    must be the oracle's vrlTracer output bit for bit."""
     import torch
     from oracle import Prep
     w, h, pass_ = 96, 64, 1
     s, o, tris = area_scene(alvrl, oracle, w, h)
-    vrls, pc = alvrl.trace_vrls(s, 3000, seed=SEED_VRL)
-    props = f"targetNumSlices=24;strictRbuild=true;seed={SEED_RNG}"
+    lib_tracer = vrl_source == "library_gpu_tracer"
+    props = f"targetNumSlices=24;seed={SEED_RNG}"      # the default pipeline: strict R build
+    if lib_tracer:
+        props += f";vrlTargetNum=3000;gpuTracer=true;vrlSeed={SEED_VRL}"
+        vrls, pc = oracle.trace(o, oracle.medium(), 3000, seed=SEED_VRL, pass_=pass_)
+    else:
+        vrls, pc = alvrl.trace_vrls(s, 3000, seed=SEED_VRL)
     it = alvrl.Integrator(props, device=0)
     try:
-        it.set_vrls(vrls, pc)
+        if not lib_tracer:
+            it.set_vrls(vrls, pc)
         # the host plays Mitsuba: buildSlices' gather points, then each
         # representative pixel's eye record (no delta BSDF: one segment each)
         sr = np.stack([alvrl.scene_slice_record(s, x, y) for y in range(h) for x in range(w)])
-        it.preprocess_ext(w, h, sr, list(s.box_min), list(s.box_max), alvrl.Medium(), tris)
+        it.preprocess_ext(w, h, sr, list(s.box_min), list(s.box_max), alvrl.Medium(), tris,
+                          tracer=s if lib_tracer else None)
         pix = it.rep_pixels(pass_)
         recs = alvrl.scene_records(s, pix)
         it.prepass_records(pass_, recs, np.arange(len(pix), dtype=np.uint32))
+        if lib_tracer:
+            dv, dpc = it.vrls()
+            assert dpc == pc and dv.shape == vrls.shape, (dpc, pc, dv.shape, vrls.shape)
+            assert np.array_equal(dv.view(np.uint32), vrls.view(np.uint32)), "device-traced VRLs vs oracle"
         # the oracle's own pipeline on its own scene
         prep = Prep(oracle, oracle.prep_params(seed=SEED_RNG, pass_=pass_, target_num_slices=24))
         p2s = prep.build_slices(o)

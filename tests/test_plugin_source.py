@@ -26,6 +26,19 @@ def test_plugin_uses_declared_exports():
         assert re.search(r"\}\s*%s\s*;|typedef struct %s\b" % (t, t), headers), f"type {t} not declared"
 
 
+def test_plugin_runs_no_reference_code():
+    """The plugin includes Mitsuba's public headers and the library's, never a
+    source of the reference integrator (its vrlTracer.h used to run records
+    mode's VRL tracing on the product side): records mode traces the VRLs in
+    the library (alvrl_scene_ext::tracer)."""
+    src = (ROOT / "mitsuba_plugin" / "vrlAmdIntegrator.cpp").read_text()
+    incs = re.findall(r'^\s*#\s*include\s*[<"]([^>"]+)[>"]', src, re.M)
+    assert incs and all(i.startswith(("mitsuba/", "hip/", "alvrl")) or "/" not in i and "." not in i
+                        for i in incs), incs
+    assert "vrlTracer" not in "".join(incs)
+    assert "e.tracer = &m_tdesc" in src
+
+
 def test_plugin_compiles_against_mitsuba_declarations(tmp_path):
     """The plugin compiles against a mock of exactly the Mitsuba declarations
     it uses (tests/mitsuba_mock/: signatures as in the mitsuba-ALVRL headers,
@@ -45,7 +58,7 @@ def test_plugin_compiles_against_mitsuba_declarations(tmp_path):
     mock = ROOT / "tests" / "mitsuba_mock"
     obj = tmp_path / "vrl_plugin.o"
     cmd = [gxx, "-std=c++11", "-c", "-fPIC", "-Wall", "-Wextra", "-Wno-unused-parameter", "-Werror",
-           "-Werror=overloaded-virtual", "-D__HIP_PLATFORM_AMD__", f"-I{mock / 'include'}", f"-I{mock / 'vrl'}",
+           "-Werror=overloaded-virtual", "-D__HIP_PLATFORM_AMD__", f"-I{mock / 'include'}",
            f"-I{ROOT / 'include'}", "-I/opt/rocm/include", str(ROOT / "mitsuba_plugin" / "vrlAmdIntegrator.cpp"),
            "-o", str(obj)]
     r = subprocess.run(cmd, capture_output=True, text=True)

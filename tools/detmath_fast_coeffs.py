@@ -68,3 +68,24 @@ def sinh_q(z):
     return mp.sinh(a) / a
 for d in (6, 7, 8):
     fit(f"sinh/a deg{d}", sinh_q, mp.mpf(0), mp.mpf(1), d)
+
+# Round 6: the ambiguous band is 2^13 units of the double's last place (error
+# budget 2^-40 relative, detmath_fast.h), so lower degrees suffice.
+print("/* ---- round 6 fits (budget 2^-40) ---- */")
+# (exp(r) - 1) / r, |r| <= ln2/512 (the 256-entry table of 2^(j/256))
+def expm1_q(r):
+    if r == 0:
+        return mp.mpf(1)
+    return mp.expm1(r) / r
+rr = L2 / 512 * (1 + mp.mpf(1e-6))
+for d in (2, 3):
+    fit(f"expm1/r deg{d} (table 256)", expm1_q, -rr, rr, d, rel=lambda r: mp.exp(r) / (abs(r) if r != 0 else 1) if r != 0 else 1)
+for d in (6, 7):
+    fit(f"atan deg{d}", atan_q, mp.mpf(0), zt, d)
+for d in (4, 5):
+    fit(f"sin/r deg{d}", sin_q, mp.mpf(0), zr, d)
+    fit(f"cos deg{d}", cos_q, mp.mpf(0), zr, d)
+for d in (4,):
+    fit(f"atanh deg{d}", atanh_q, mp.mpf(0), zs, d)
+for d in (5,):
+    fit(f"sinh/a deg{d}", sinh_q, mp.mpf(0), mp.mpf(1), d)
