@@ -259,6 +259,23 @@ ALVRL_API int alvrl_local_exchange_create(uint32_t world, alvrl_local_exchange *
 ALVRL_API const alvrl_exchange *alvrl_local_exchange_rank(alvrl_local_exchange *g, uint32_t rank);
 ALVRL_API void alvrl_local_exchange_destroy(alvrl_local_exchange *g);
 
+/* The same in-process ranks over RCCL: one communicator per device
+ * (ncclCommInitAll over devices[0..world), which must be distinct), so the
+ * prepass's collective moves device to device over xGMI -- rank r's
+ * alvrl_exchange stages its bytes on devices[r] and runs ncclAllGather -- and
+ * the frame's tiles are summed on the devices: alvrl_device_exchange_reduce_frame
+ * is one ncclReduce (sum, in place) of every rank's n-float framebuffer into
+ * rank 0's on 'stream' (NULL: the rank's own), which a single D2H copy then
+ * hands to the host (north_star's "single RCCL gather of the framebuffer").
+ * Every rank calls it, each from its own thread.  The multi-GPU form of
+ * Mitsuba's one-process rendering (renderproc.cpp:142-160). */
+typedef struct alvrl_device_exchange alvrl_device_exchange;
+ALVRL_API int alvrl_device_exchange_create(const int *devices, uint32_t world, alvrl_device_exchange **out);
+ALVRL_API const alvrl_exchange *alvrl_device_exchange_rank(alvrl_device_exchange *g, uint32_t rank);
+ALVRL_API int alvrl_device_exchange_reduce_frame(alvrl_device_exchange *g, uint32_t rank, float *d_fb, uint64_t n,
+                                                 void *stream);
+ALVRL_API void alvrl_device_exchange_destroy(alvrl_device_exchange *g);
+
 /* ---- host-cast scenes (the Mitsuba plugin's "records" mode) ------------
  * For scenes the descriptor above cannot express -- area and other emitters,
  * any shapes and BSDFs, a medium in any container -- the host application

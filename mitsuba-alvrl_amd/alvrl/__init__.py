@@ -530,6 +530,33 @@ class LocalExchange:
             pass
 
 
+class DeviceExchange(LocalExchange):
+    """alvrl_device_exchange: ranks that are the GPUs of this process over
+    RCCL (one communicator per device, ncclCommInitAll; distinct devices).
+    `rank(r)` is rank r's exchange; `reduce_frame(r, d_fb)` sums every rank's
+    framebuffer into rank 0's (one ncclReduce, each rank calls it)."""
+
+    def __init__(self, devices):
+        L = _host()
+        h = C.c_void_p()
+        devs = np.asarray(list(devices), np.int32)
+        rc = L.alvrl_device_exchange_create(_ptr(devs), len(devs), C.byref(h))
+        if rc != ALVRL_OK:
+            raise AlvrlError(rc, L.alvrl_host_last_error().decode())
+        self.h, self.world, self.devices = h, len(devs), [int(d) for d in devs]
+        self._ranks = [self._Rank(self, C.cast(L.alvrl_device_exchange_rank(h, r), C.POINTER(ExchangeDesc)).contents)
+                       for r in range(self.world)]
+
+    def reduce_frame(self, rank: int, d_fb, stream=None):
+        _hcheck(_host().alvrl_device_exchange_reduce_frame(self.h, rank, _ptr(d_fb), d_fb.numel(),
+                                                           C.c_void_p(stream) if stream else None))
+
+    def close(self):
+        if getattr(self, "h", None):
+            _host().alvrl_device_exchange_destroy(self.h)
+            self.h = None
+
+
 class Exchange:
     """alvrl_exchange over a torch.distributed process group.
 
@@ -666,6 +693,10 @@ def _host():
     L.alvrl_local_exchange_create.argtypes = [u32, P(vp)]
     L.alvrl_local_exchange_rank.argtypes = [vp, u32]; L.alvrl_local_exchange_rank.restype = vp
     L.alvrl_local_exchange_destroy.argtypes = [vp]; L.alvrl_local_exchange_destroy.restype = None
+    L.alvrl_device_exchange_create.argtypes = [vp, u32, P(vp)]
+    L.alvrl_device_exchange_rank.argtypes = [vp, u32]; L.alvrl_device_exchange_rank.restype = vp
+    L.alvrl_device_exchange_reduce_frame.argtypes = [vp, u32, vp, u64, vp]
+    L.alvrl_device_exchange_destroy.argtypes = [vp]; L.alvrl_device_exchange_destroy.restype = None
     L.alvrl_exchange_clusters.argtypes = [P(ExchangeDesc), u32, u32, u32, vp, vp, vp, vp, vp, vp, vp, vp, vp,
                                           u64, P(u64)]
     L.alvrl_cluster_info_write.argtypes = [C.c_char_p, u32, vp, u32, vp, vp, vp, u32, vp, vp, u32, vp, vp]

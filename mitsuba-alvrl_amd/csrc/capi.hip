@@ -38,6 +38,14 @@ hipError_t launch_gather_clustered(const Rec* recs, const uint32_t* ids, const W
                                    const uint32_t* fb_reps, const float* fb_w, uint32_t n_fb,
                                    const DevParams& P, float inv_pc, float* out,
                                    unsigned long long* counter, hipStream_t s);
+struct SplitUnit { uint32_t item, first; };
+hipError_t launch_gather_clustered_split(const Rec* recs, const uint32_t* ids, const WorkItem* items,
+                                         uint32_t nitems, const SplitUnit* units, uint32_t nunits, uint32_t chunk,
+                                         const uint64_t* base, float* cbuf, const VrlPrep* vp,
+                                         const uint32_t* slice_off, const uint32_t* reps, const float* weights,
+                                         const uint32_t* fb_reps, const float* fb_w, uint32_t n_fb,
+                                         const DevParams& P, float inv_pc, float* out,
+                                         unsigned long long* counter, hipStream_t s);
 hipError_t launch_build_R(const Rec* recs, const uint32_t* ids, uint32_t nrows, const VrlPrep* vp,
                           uint32_t nvrl, const DevParams& P, float normalization, float2* Rt,
                           uint64_t ld, uint64_t row0, unsigned long long* counter, hipStream_t s);
@@ -148,7 +156,22 @@ struct HostReq {
     std::string err;
     bool done = false;
 };
+// Work items below which a host batch takes the split gather (2,048 waves:
+// half the chip's wave slots at two waves per SIMD); ALVRL_HOST_SPLIT=0 turns
+// it off (developer A/B), =1 forces it for every batch.
+constexpr uint32_t kSplitItems = 2048;
+static bool split_enabled()
+{
+    const char* e = std::getenv("ALVRL_HOST_SPLIT");
+    return !e || std::atoi(e) != 0;
+}
+static bool split_forced()
+{
+    const char* e = std::getenv("ALVRL_HOST_SPLIT");
+    return e && std::atoi(e) == 1;
+}
 struct HostBatcher {
+    unsigned long long split_batches = 0;   // batches that took the split gather
     std::mutex mu;
     std::condition_variable cv;
     std::vector<HostReq*> pending[2];   // [0] brute, [1] clustered
@@ -171,6 +194,7 @@ struct alvrl_ctx {
     unsigned long long* d_counter = nullptr;   // [0] preprocess, [1] render
     // clusters
     uint32_t nslices = 0, n_fb = 0;
+    std::vector<uint32_t> h_slice_off;   // the lists' sizes on the host (the host gathers' split form)
     uint32_t* d_slice_off = nullptr;
     uint32_t* d_reps = nullptr;
     float* d_weights = nullptr;
@@ -477,6 +501,7 @@ ALVRL_API int alvrl_set_clusters(alvrl_ctx* c, uint32_t nslices, const uint32_t*
     HIPCHK(hipStreamSynchronize(c->stream));   // the host buffers are the caller's
     c->nslices = nslices;
     c->n_fb = n_fb;
+    c->h_slice_off.assign(slice_off, slice_off + (nslices ? nslices + 1 : 0));
     c->clusters_set = true;
     return ALVRL_OK;
 }
@@ -922,6 +947,31 @@ static int run_host_batch(alvrl_ctx* c, int kind, const std::vector<HostReq*>& b
         if (kind) sl2[g] = q->sl[i];
     }
     const uint32_t nit = kind ? alvrl_make_work_items(sl2.data(), nrec, items, nrec) : 0;
+    // a batch too small to fill the chip takes the split form: one wave per
+    // chunk of a work item's representative list (gather.hip, same bits)
+    std::vector<SplitUnit> units;
+    std::vector<uint64_t> base;
+    uint64_t cfloats = 0;
+    uint32_t chunk = 0;
+    if (kind && (nit < kSplitItems || split_forced()) && split_enabled()) {
+        base.resize(nit);
+        uint64_t pairs = 0;
+        for (uint32_t j = 0; j < nit; j++) {
+            const uint32_t sj = items[j].slice;
+            const uint32_t k = sj == 0xFFFFFFFFu ? c->n_fb : c->h_slice_off[sj + 1] - c->h_slice_off[sj];
+            base[j] = cfloats;
+            cfloats += (uint64_t)k * 3 * 64;
+            pairs += k;
+        }
+        // about 8 waves per SIMD slot of the chip, chunks of 16..256 pairs
+        chunk = (uint32_t)std::min<uint64_t>(256, std::max<uint64_t>(16, pairs / 8192 + 1));
+        for (uint32_t j = 0; j < nit; j++) {
+            const uint32_t sj = items[j].slice;
+            const uint32_t k = sj == 0xFFFFFFFFu ? c->n_fb : c->h_slice_off[sj + 1] - c->h_slice_off[sj];
+            for (uint32_t f = 0; f < k; f += chunk) units.push_back({j, f});
+        }
+    }
+    const bool split = !base.empty();
     hipError_t e = hipSetDevice(c->cfg.device);
     ThreadSlot* ts = e == hipSuccess ? slot_of(c, &e) : nullptr;
     if (!ts) { *err = std::string("per-thread stream: ") + hipGetErrorString(e); return ALVRL_ERR_HIP; }
@@ -930,19 +980,37 @@ static int run_host_batch(alvrl_ctx* c, int kind, const std::vector<HostReq*>& b
     const size_t o_i = carve(&at, sizeof(uint32_t) * nrec);
     const size_t o_o = carve(&at, sizeof(float) * 3 * nrec);
     const size_t o_t = carve(&at, sizeof(alvrl_work_item) * nit);
+    const size_t o_u = carve(&at, sizeof(SplitUnit) * units.size());
+    const size_t o_b = carve(&at, sizeof(uint64_t) * base.size());
+    const size_t o_c = carve(&at, sizeof(float) * cfloats);
     e = ts->need(at);
     hipStream_t s = ts->stream;
     auto* dr = reinterpret_cast<alvrl_gather_rec*>(ts->scratch + o_r);
     auto* di = reinterpret_cast<uint32_t*>(ts->scratch + o_i);
     auto* dout = reinterpret_cast<float*>(ts->scratch + o_o);
     auto* dit = reinterpret_cast<alvrl_work_item*>(ts->scratch + o_t);
+    auto* du = reinterpret_cast<SplitUnit*>(ts->scratch + o_u);
+    auto* db = reinterpret_cast<uint64_t*>(ts->scratch + o_b);
+    auto* dcb = reinterpret_cast<float*>(ts->scratch + o_c);
     if (e == hipSuccess) e = hipMemcpyAsync(dr, r2, sizeof(alvrl_gather_rec) * nrec, hipMemcpyHostToDevice, s);
     if (e == hipSuccess) e = hipMemcpyAsync(di, id2, sizeof(uint32_t) * nrec, hipMemcpyHostToDevice, s);
     if (e == hipSuccess && kind)
         e = hipMemcpyAsync(dit, items, sizeof(alvrl_work_item) * nit, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess && split && !units.empty())
+        e = hipMemcpyAsync(du, units.data(), sizeof(SplitUnit) * units.size(), hipMemcpyHostToDevice, s);
+    if (e == hipSuccess && split)
+        e = hipMemcpyAsync(db, base.data(), sizeof(uint64_t) * base.size(), hipMemcpyHostToDevice, s);
     if (e == hipSuccess) e = hipEventRecord(ts->ev0, s);
     if (e == hipSuccess) {
-        if (kind) {
+        if (kind && split) {
+            const float inv_pc = 1.0f / (float)c->particle_count;   // Li /= getParticleCount() (:590)
+            e = launch_gather_clustered_split(reinterpret_cast<const Rec*>(dr), di,
+                                              reinterpret_cast<const WorkItem*>(dit), nit, du,
+                                              (uint32_t)units.size(), chunk, db, dcb, c->d_vrl, c->d_slice_off,
+                                              c->d_reps, c->d_weights, c->d_fb_reps, c->d_fb_w, c->n_fb, c->P,
+                                              inv_pc, dout, c->d_counter + 1, s);
+            B.split_batches++;
+        } else if (kind) {
             const float inv_pc = 1.0f / (float)c->particle_count;   // Li /= getParticleCount() (:590)
             e = launch_gather_clustered(reinterpret_cast<const Rec*>(dr), di, reinterpret_cast<const WorkItem*>(dit),
                                         nit, c->d_vrl, c->d_slice_off, c->d_reps, c->d_weights, c->d_fb_reps,

@@ -112,6 +112,21 @@ __global__ void ALVRL_GATHER_BOUNDS k_gather_brute(const Rec* __restrict__ recs,
 
 struct WorkItem { uint32_t slice, begin, count, pad; };
 
+// One pair's colour for the clustered gathers.  The one-wave-per-item kernel
+// and the split form of small host batches (k_gather_split_pairs) inline it
+// into different loops; this file is built with -ffp-contract=on (a*b+c fused
+// only within one source expression, Makefile GATHERFLAGS), so its roundings
+// do not depend on the surrounding code and a record's result does not
+// depend on which form its batch took (tests/test_gpu_boundary.py).
+template <int NVV, int NVS, bool VIS>
+__device__ __forceinline__ float3 pair_colour(const DevParams& P, const RecPre& q, const VrlPrep& V, uint32_t rid,
+                                           uint32_t v)
+{
+    float c[3], m, s;
+    integrate_vrl<NVV, NVS, false, VIS>(P, q, V, rid, v, kDomGather, P.nvv, P.nvs, c, &m, &s);
+    return make_float3(c[0], c[1], c[2]);
+}
+
 template <int NVV, int NVS, bool VIS>
 __device__ __forceinline__ void gather_item(const Rec* __restrict__ recs, const uint32_t* __restrict__ ids,
                                             const WorkItem& it, const uint32_t* lr, const float* lw, uint32_t k,
@@ -158,12 +173,94 @@ __device__ __forceinline__ void gather_item(const Rec* __restrict__ recs, const 
             const uint32_t v = lr[i];
             const float w = lw[i];
             const VrlPrep V = vp[v];
-            float c[3], m, s;
-            integrate_vrl<NVV, NVS, false, VIS>(P, q, V, rid, v, kDomGather, P.nvv, P.nvs, c, &m, &s);
+            const float3 c = pair_colour<NVV, NVS, VIS>(P, q, V, rid, v);
             // Li += weights->at(i) * integrateVRL(...)  (:587-589)
-            L0 += c[0] * w; L1 += c[1] * w; L2 += c[2] * w;
+            L0 += c.x * w; L1 += c.y * w; L2 += c.z * w;
         }
         // Li /= particleCount (:590); return Li * weight (:598)
+        L0 *= inv_pc; L1 *= inv_pc; L2 *= inv_pc;
+        if (!q.unit) { L0 *= q.w[0]; L1 *= q.w[1]; L2 *= q.w[2]; }
+    }
+    count_pairs(counter, active && q.medium, k);
+    if (active) {
+        out[3 * (size_t)r + 0] = L0; out[3 * (size_t)r + 1] = L1; out[3 * (size_t)r + 2] = L2;
+    }
+}
+
+// Small launches (the plugin's records mode: renderBlock-sized host calls,
+// a few hundred work items) leave most of the 4,096 wave slots of the chip
+// idle while each item's wave walks its whole representative list.  The split
+// form gives every chunk of a list its own wave: k_gather_split_pairs stores
+// each pair's integrateVRL colour (the same inlined code as gather_item), and
+// k_gather_split_sum adds them in list order with gather_item's own
+// accumulation expression, so a record gets the same bits either way
+// (tests/test_gpu_boundary.py).  Pair colours: item j's block at
+// cbuf[base[j] ...], entry (i * 3 + channel) * 64 + lane.
+struct SplitUnit { uint32_t item, first; };
+
+template <int NVV, int NVS, bool VIS>
+__global__ void ALVRL_GATHER_BOUNDS k_gather_split_pairs(
+    const Rec* __restrict__ recs, const uint32_t* __restrict__ ids, const WorkItem* __restrict__ items,
+    const SplitUnit* __restrict__ units, uint32_t nunits, uint32_t chunk, const VrlPrep* __restrict__ vp,
+    const uint32_t* __restrict__ slice_off, const uint32_t* __restrict__ reps, const uint32_t* __restrict__ fb_reps,
+    uint32_t n_fb, DevParams P, const uint64_t* __restrict__ base, float* __restrict__ cbuf)
+{
+    const uint32_t unit = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+    if (unit >= nunits) return;
+    const SplitUnit u = units[unit];
+    const WorkItem it = items[u.item];
+    const uint32_t* lr;
+    uint32_t k;
+    if (it.slice == 0xFFFFFFFFu) { lr = fb_reps; k = n_fb; }
+    else { const uint32_t b = slice_off[it.slice]; lr = reps + b; k = slice_off[it.slice + 1] - b; }
+    const uint32_t lane = threadIdx.x & 63;
+    const bool active = lane < it.count;
+    const uint32_t r = it.begin + lane;
+    const Rec rec = load_rec(recs, r, active);
+    const RecPre q = prepare_record(rec, P);
+    const uint32_t rid = active ? (ids ? ids[r] : r) : 0u;
+    float* __restrict__ cb = cbuf + base[u.item] + lane;
+    const uint32_t end = min(k, u.first + chunk);
+    if (q.medium) {
+        for (uint32_t i = u.first; i < end; ++i) {
+            const uint32_t v = lr[i];
+            const VrlPrep V = vp[v];
+            const float3 c = pair_colour<NVV, NVS, VIS>(P, q, V, rid, v);
+            cb[(size_t)(3 * i + 0) * 64] = c.x;
+            cb[(size_t)(3 * i + 1) * 64] = c.y;
+            cb[(size_t)(3 * i + 2) * 64] = c.z;
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) k_gather_split_sum(
+    const Rec* __restrict__ recs, const WorkItem* __restrict__ items, uint32_t nitems,
+    const uint32_t* __restrict__ slice_off, const float* __restrict__ weights, const float* __restrict__ fb_w,
+    uint32_t n_fb, DevParams P, float inv_pc, const uint64_t* __restrict__ base, const float* __restrict__ cbuf,
+    float* __restrict__ out, unsigned long long* counter)
+{
+    const uint32_t item = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+    if (item >= nitems) return;
+    const WorkItem it = items[item];
+    const float* lw;
+    uint32_t k;
+    if (it.slice == 0xFFFFFFFFu) { lw = fb_w; k = n_fb; }
+    else { const uint32_t b = slice_off[it.slice]; lw = weights + b; k = slice_off[it.slice + 1] - b; }
+    const uint32_t lane = threadIdx.x & 63;
+    const bool active = lane < it.count;
+    const uint32_t r = it.begin + lane;
+    const Rec rec = load_rec(recs, r, active);
+    const RecPre q = prepare_record(rec, P);
+    const float* __restrict__ cb = cbuf + base[item] + lane;
+    float L0 = 0.0f, L1 = 0.0f, L2 = 0.0f;
+    if (q.medium) {
+        for (uint32_t i = 0; i < k; ++i) {
+            const float w = lw[i];
+            const float c0 = cb[(size_t)(3 * i + 0) * 64], c1 = cb[(size_t)(3 * i + 1) * 64],
+                        c2 = cb[(size_t)(3 * i + 2) * 64];
+            // as gather_item: Li += weights->at(i) * integrateVRL(...)  (:587-589)
+            L0 += c0 * w; L1 += c1 * w; L2 += c2 * w;
+        }
         L0 *= inv_pc; L1 *= inv_pc; L2 *= inv_pc;
         if (!q.unit) { L0 *= q.w[0]; L1 *= q.w[1]; L2 *= q.w[2]; }
     }
@@ -428,6 +525,34 @@ hipError_t launch_gather_clustered(const Rec* recs, const uint32_t* ids, const W
         hipLaunchKernelGGL((k_gather_clustered<-1, -1>), grid, block, 0, s, recs, ids, items,
                            nitems, vp, slice_off, reps, weights, fb_reps, fb_w, n_fb, P, inv_pc,
                            out, counter);
+    return hipGetLastError();
+}
+
+hipError_t launch_gather_clustered_split(const Rec* recs, const uint32_t* ids, const WorkItem* items,
+                                         uint32_t nitems, const SplitUnit* units, uint32_t nunits, uint32_t chunk,
+                                         const uint64_t* base, float* cbuf, const VrlPrep* vp,
+                                         const uint32_t* slice_off, const uint32_t* reps, const float* weights,
+                                         const uint32_t* fb_reps, const float* fb_w, uint32_t n_fb,
+                                         const DevParams& P, float inv_pc, float* out,
+                                         unsigned long long* counter, hipStream_t s)
+{
+    if (nitems == 0) return hipSuccess;
+    if (nunits) {
+        const dim3 grid((nunits + 3) / 4), block(256);
+        if (P.occ.ntri)
+            hipLaunchKernelGGL((k_gather_split_pairs<-1, -1, true>), grid, block, 0, s, recs, ids, items, units, nunits,
+                               chunk, vp, slice_off, reps, fb_reps, n_fb, P, base, cbuf);
+        else if (P.nvv == 2 && P.nvs == 2 && P.strategy == 0)
+            hipLaunchKernelGGL((k_gather_split_pairs<2, 2, false>), grid, block, 0, s, recs, ids, items, units, nunits,
+                               chunk, vp, slice_off, reps, fb_reps, n_fb, P, base, cbuf);
+        else
+            hipLaunchKernelGGL((k_gather_split_pairs<-1, -1, false>), grid, block, 0, s, recs, ids, items, units,
+                               nunits, chunk, vp, slice_off, reps, fb_reps, n_fb, P, base, cbuf);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(k_gather_split_sum, dim3((nitems + 3) / 4), dim3(256), 0, s, recs, items, nitems, slice_off,
+                       weights, fb_w, n_fb, P, inv_pc, base, cbuf, out, counter);
     return hipGetLastError();
 }
 

@@ -117,7 +117,10 @@ struct alvrl_integrator {
     bool dumpPasses = false;
     int rrDepth = 5, maxDepth = -1;
     uint32_t seed = 0xA1B2C3D4u, vrlSeed = 0x5EED0001u;
-    bool gpuTracer = false;   // trace the pass's VRLs on the device (csrc/tracer.hip)
+    // trace the pass's VRLs on the device (csrc/tracer.hip, bit-identical to
+    // the host tracer) wherever the scene fits it -- no mirror / null /
+    // dielectric triangles, whose particles the host traces; false: always the host
+    bool gpuTracer = true;
     bool strictRbuild = true;    // the R build in the oracle's arithmetic (alvrl_set_strict_rbuild); false: the gathers' fast maths
     // ---- state
     int device = 0;
@@ -440,7 +443,7 @@ struct alvrl_integrator {
             const double t0 = now_ms();
             const alvrl_scene_desc& td = ext ? tracer_desc : scene_desc;
             const SmokeBox& tb = ext ? tracer_box : scene;
-            if (gpuTracer) {
+            if (gpuTracer && !tb.has_delta()) {
                 const uint32_t target = (uint32_t)std::max(vrlTargetNum, 0);
                 uint32_t n = 0;
                 uint64_t pc = 0;

@@ -54,7 +54,7 @@ def test_area_scene_records_mode_vs_oracle(alvrl, oracle, gpu_ok, vrl_source):
     lib_tracer = vrl_source == "library_gpu_tracer"
     props = f"targetNumSlices=24;seed={SEED_RNG}"      # the default pipeline: strict R build
     if lib_tracer:
-        props += f";vrlTargetNum=3000;gpuTracer=true;vrlSeed={SEED_VRL}"
+        props += f";vrlTargetNum=3000;vrlSeed={SEED_VRL}"      # gpuTracer: the default
         vrls, pc = oracle.trace(o, oracle.medium(), 3000, seed=SEED_VRL, pass_=pass_)
     else:
         vrls, pc = alvrl.trace_vrls(s, 3000, seed=SEED_VRL)

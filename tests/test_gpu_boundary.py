@@ -137,3 +137,50 @@ def test_set_clusters_waits_for_running_gather(gpu_ok):
     ctx.gather_clustered(d_recs, d_items, len(items), after, d_ids=d_ids)
     torch.cuda.synchronize()
     assert not torch.equal(after, ref)
+
+
+@pytest.mark.parametrize("samples", [2, 3])
+def test_split_gather_same_bits(gpu_ok, samples, monkeypatch):
+    """Host batches too small to fill the chip (renderBlock-sized calls) take
+    the split gather (csrc/gather.hip k_gather_split_pairs / _sum: a wave per
+    chunk of a representative list, the pairs added in list order afterwards).
+    Its frame equals the one-wave-per-item kernel's (the device-pointer
+    alvrl_gather_clustered) bit for bit: forced on, forced off, and in 32x32
+    blocks from 8 threads; samples = 3 takes the generic (not unrolled) form."""
+    import torch
+    import alvrl
+    w, h = 320, 256
+    ctx, recs, sl, cl = _setup(w, h, 3000, "targetNumSlices=40")
+    if samples != 2:
+        scene = alvrl.scene_default(w, h)
+        vrls, pc = alvrl.trace_vrls(scene, 3000, seed=SEED_VRL)
+        ctx = alvrl.Context(device=0, vol_vol_samples=samples, vol_surf_samples=samples, seed=SEED_RNG)
+        ctx.set_medium(alvrl.Medium())
+        ctx.upload_vrls(vrls, pc)
+        ctx.set_clusters(cl["slice_off"], cl["reps"], cl["weights"], cl["fb_reps"], cl["fb_weights"])
+    pid = np.arange(w * h, dtype=np.uint32)
+    order = np.argsort(sl, kind="stable").astype(np.uint32)
+    items = alvrl.Context.make_work_items(sl[order])
+    ref = torch.zeros((w * h, 3), dtype=torch.float32, device="cuda")
+    ctx.gather_clustered(torch.from_numpy(recs[order]).cuda(), torch.from_numpy(items.view(np.int32)).cuda(),
+                         len(items), ref, d_ids=torch.from_numpy(order.view(np.int32)).cuda())
+    torch.cuda.synchronize()
+    # the device-pointer gather writes record order[i]'s result at row i
+    ref_px = np.zeros((w * h, 3), np.float32)
+    ref_px[order] = ref.cpu().numpy()
+    assert ref_px.any()
+    for mode in ("0", "1"):
+        monkeypatch.setenv("ALVRL_HOST_SPLIT", mode)
+        whole = ctx.gather_clustered_host(recs, sl, ids=pid)
+        same = whole.view(np.uint32) == ref_px.view(np.uint32)
+        rel = np.abs(whole.astype(np.float64) - ref_px) / np.maximum(np.abs(ref_px), 1e-30)
+        print(f"ALVRL_HOST_SPLIT={mode}: {same.mean():.6f} of the values equal, max rel {rel.max():.3e}")
+        assert same.all(), f"ALVRL_HOST_SPLIT={mode}"
+    monkeypatch.delenv("ALVRL_HOST_SPLIT")
+    frame = np.zeros((w * h, 3), np.float32)
+    blocks = _blocks(w, h)
+    with ThreadPoolExecutor(max_workers=8) as ex:
+        for ids, out in zip(blocks, ex.map(lambda ids: ctx.gather_clustered_host(recs[ids], sl[ids], ids=ids),
+                                           blocks)):
+            frame[ids] = out
+    assert np.array_equal(frame.view(np.uint32), ref_px.view(np.uint32)), "32x32 blocks"

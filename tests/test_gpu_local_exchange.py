@@ -69,3 +69,72 @@ def test_local_exchange_integrators(gpu_ok, world, props):
     for it in its:
         it.close()
     g.close()
+
+
+def test_device_exchange_rccl(gpu_ok):
+    """alvrl_device_exchange (the plugin's amdDevices over RCCL): a repeated
+    device is refused; on every visible device (one on the test box) the
+    exchange's all-gather, OR and cluster merge give what the host exchange
+    gives, the framebuffer reduce is the sum, and the sharded prepass through
+    it equals the one-GPU prepass."""
+    import torch
+    import alvrl
+    with pytest.raises(alvrl.AlvrlError):
+        alvrl.DeviceExchange([0, 0])
+    n = torch.cuda.device_count()
+    devs = list(range(n))
+    g = alvrl.DeviceExchange(devs)
+    try:
+        out = [None] * n
+        errs = []
+
+        def run(r):
+            try:
+                torch.cuda.set_device(devs[r])
+                rk = g.rank(r)
+                data = np.arange(5 + r, dtype=np.uint8) * (r + 1)
+                parts = rk.allgatherv(data)
+                mask = np.zeros(64, np.uint8)
+                mask[r::n + 1] = 1
+                ored = rk.or_(mask)
+                fb = torch.full((1000,), float(r + 1), device=f"cuda:{devs[r]}")
+                g.reduce_frame(r, fb)
+                torch.cuda.synchronize(devs[r])
+                out[r] = (parts, ored, fb.cpu().numpy())
+            except Exception as e:   # reported below
+                errs.append((r, e))
+
+        th = [threading.Thread(target=run, args=(r,)) for r in range(n)]
+        [t.start() for t in th]
+        [t.join(120) for t in th]
+        assert not errs, errs
+        for r in range(n):
+            parts, ored, fb = out[r]
+            assert [p.tolist() for p in parts] == [(np.arange(5 + q, dtype=np.uint8) * (q + 1)).tolist()
+                                                   for q in range(n)]
+            ref = np.zeros(64, np.uint8)
+            for q in range(n):
+                ref[q::n + 1] = 1
+            assert np.array_equal(ored, ref)
+        assert np.all(out[0][2] == sum(range(1, n + 1)))   # rank 0 holds the sum
+        if n == 1:
+            # the sharded prepass over it (world 1) equals the plain prepass
+            w, h = 128, 96
+            scene = alvrl.scene_default(w, h)
+            vrls, pc = alvrl.trace_vrls(scene, 1500, seed=SEED_VRL)
+            res = []
+            for sharded in (False, True):
+                it = alvrl.Integrator(f"targetNumSlices=16;seed={SEED_RNG}", device=0)
+                it.set_vrls(vrls, pc)
+                it.preprocess(scene)
+                if sharded:
+                    import ctypes as C
+                    assert it.L.alvrl_integrator_prepass_dist(it.h, 3, 0, 1, C.byref(g.rank(0).desc)) == 0
+                else:
+                    it.prepass(3)
+                res.append(it.clusters())
+                it.close()
+            for k in res[0]:
+                assert np.array_equal(res[0][k].view(np.uint32), res[1][k].view(np.uint32)), k
+    finally:
+        g.close()
