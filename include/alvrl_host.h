@@ -258,6 +258,11 @@ typedef struct alvrl_local_exchange alvrl_local_exchange;
 ALVRL_API int alvrl_local_exchange_create(uint32_t world, alvrl_local_exchange **out);
 ALVRL_API const alvrl_exchange *alvrl_local_exchange_rank(alvrl_local_exchange *g, uint32_t rank);
 ALVRL_API void alvrl_local_exchange_destroy(alvrl_local_exchange *g);
+/* Mark the group broken: every rank waiting in a collective, or arriving at
+ * one later, fails it with ALVRL_ERR_COMM at once.  A rank whose prepass
+ * failed before its collective calls this so its peers do not wait for the
+ * timeout; the group is not reused afterwards. */
+ALVRL_API void alvrl_local_exchange_abort(alvrl_local_exchange *g);
 
 /* The same in-process ranks over RCCL: one communicator per device
  * (ncclCommInitAll over devices[0..world), which must be distinct), so the
@@ -275,6 +280,10 @@ ALVRL_API const alvrl_exchange *alvrl_device_exchange_rank(alvrl_device_exchange
 ALVRL_API int alvrl_device_exchange_reduce_frame(alvrl_device_exchange *g, uint32_t rank, float *d_fb, uint64_t n,
                                                  void *stream);
 ALVRL_API void alvrl_device_exchange_destroy(alvrl_device_exchange *g);
+/* ncclCommAbort on every rank's communicator: collectives in flight or
+ * started later fail instead of waiting for a rank that will not join; the
+ * group is not reused afterwards (destroy it). */
+ALVRL_API void alvrl_device_exchange_abort(alvrl_device_exchange *g);
 
 /* ---- host-cast scenes (the Mitsuba plugin's "records" mode) ------------
  * For scenes the descriptor above cannot express -- area and other emitters,

@@ -41,7 +41,6 @@ struct alvrl_device_exchange {
         uint8_t* d_send = nullptr;   // grow-only staging of allgather
         uint8_t* d_recv = nullptr;
         uint64_t cap_send = 0, cap_recv = 0;
-        int err = 0;
     };
     uint32_t world = 0;
     std::vector<Rank> ranks;
@@ -64,6 +63,7 @@ struct alvrl_device_exchange {
         Rank* rk = static_cast<Rank*>(user);
         const alvrl_device_exchange& G = *rk->g;
         if (bytes == 0) return 0;   // every rank skips (the byte count is common)
+        if (!rk->comm) return 2;    // aborted group
         if (hipSetDevice(rk->device) != hipSuccess) return 1;
         if (grow(&rk->d_send, &rk->cap_send, bytes) || grow(&rk->d_recv, &rk->cap_recv, bytes * G.world)) return 1;
         if (hipMemcpyAsync(rk->d_send, send, bytes, hipMemcpyHostToDevice, rk->stream) != hipSuccess) return 1;
@@ -146,6 +146,7 @@ ALVRL_API int alvrl_device_exchange_reduce_frame(alvrl_device_exchange* g, uint3
     auto& rk = g->ranks[rank];
     if (hipSetDevice(rk.device) != hipSuccess) { g_host_err = "alvrl_device_exchange_reduce_frame: hipSetDevice"; return ALVRL_ERR_HIP; }
     if (n == 0) return ALVRL_OK;
+    if (!rk.comm) { g_host_err = "alvrl_device_exchange_reduce_frame: the group was aborted"; return ALVRL_ERR_COMM; }
     const ncclResult_t nr = ncclReduce(d_fb, d_fb, n, ncclFloat, ncclSum, 0, rk.comm,
                                        stream ? static_cast<hipStream_t>(stream) : rk.stream);
     if (nr != ncclSuccess) {
@@ -156,5 +157,15 @@ ALVRL_API int alvrl_device_exchange_reduce_frame(alvrl_device_exchange* g, uint3
 }
 
 ALVRL_API void alvrl_device_exchange_destroy(alvrl_device_exchange* g) { delete g; }
+
+ALVRL_API void alvrl_device_exchange_abort(alvrl_device_exchange* g)
+{
+    if (!g) return;
+    for (auto& r : g->ranks)
+        if (r.comm) {
+            (void)ncclCommAbort(r.comm);   // also frees the communicator
+            r.comm = nullptr;
+        }
+}
 
 }  // extern "C"

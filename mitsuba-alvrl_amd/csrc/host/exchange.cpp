@@ -304,4 +304,12 @@ ALVRL_API const alvrl_exchange* alvrl_local_exchange_rank(alvrl_local_exchange* 
 
 ALVRL_API void alvrl_local_exchange_destroy(alvrl_local_exchange* g) { delete g; }
 
+ALVRL_API void alvrl_local_exchange_abort(alvrl_local_exchange* g)
+{
+    if (!g) return;
+    std::lock_guard<std::mutex> lk(g->mu);
+    g->broken = true;
+    g->cv.notify_all();
+}
+
 }  // extern "C"

@@ -106,7 +106,8 @@ void put3(float *dst, const Spectrum &s) {
 /* The properties the library does not take (Mitsuba's own, or the medium's
  * restated on the integrator) */
 bool isMitsubaOnly(const std::string &k) {
-    return k == "amdMode" || k == "amdDevice" || k == "amdDevices" || k == "mediumSamplingWeight" || k == "strategy" ||
+    return k == "amdMode" || k == "amdDevice" || k == "amdDevices" || k == "amdRehearseDevices" ||
+        k == "mediumSamplingWeight" || k == "strategy" ||
         k == "channel" || k == "samplingDensity";
 }
 
@@ -114,8 +115,10 @@ bool isMitsubaOnly(const std::string &k) {
 const size_t kMaxPathRecords = 256;
 
 /* "amdDevices": a comma-separated list of HIP devices ("0,1,2,3"), or
- * "all" for every visible device; empty: the one "amdDevice" */
-std::vector<int> parseDevices(const std::string &spec, int single) {
+ * "all" for every visible device; empty: the one "amdDevice".  A device may
+ * repeat only with the test property amdRehearseDevices=true (several
+ * integrators on one GPU, exchanging through host memory) */
+std::vector<int> parseDevices(const std::string &spec, int single, bool rehearse) {
     std::vector<int> out;
     if (spec.empty()) {
         out.push_back(single);
@@ -135,7 +138,7 @@ std::vector<int> parseDevices(const std::string &spec, int single) {
         SLog(EError, "vrl (amd): amdDevices lists no device");
     for (size_t i = 0; i < out.size(); ++i)
         for (size_t j = 0; j < i; ++j)
-            if (out[i] == out[j] || out[i] < 0)
+            if ((out[i] == out[j] && !rehearse) || out[i] < 0)
                 SLog(EError, "vrl (amd): amdDevices must list distinct devices");
     return out;
 }
@@ -235,7 +238,8 @@ public:
             Log(EError, "amdMode must be \"frame\" or \"records\"");
         m_recordsMode = mode == "records";
         m_device = props.getInteger("amdDevice", 0);
-        m_devices = parseDevices(props.getString("amdDevices", ""), m_device);
+        m_rehearse = props.getBoolean("amdRehearseDevices", false);
+        m_devices = parseDevices(props.getString("amdDevices", ""), m_device, m_rehearse);
         m_device = m_devices[0];
         if (m_recordsMode && m_devices.size() > 1)
             Log(EError, "vrl (amd): amdDevices (one library integrator per GPU) needs amdMode=frame");
@@ -291,6 +295,7 @@ public:
         m_sampleCount = stream->readInt();
         m_devices.resize((size_t) stream->readInt());
         for (size_t i = 0; i < m_devices.size(); ++i) m_devices[i] = stream->readInt();
+        m_rehearse = stream->readBool();
         m_vrlsID = m_ciID = 0;
         create(m_sampleCount);
     }
@@ -314,6 +319,7 @@ public:
         stream->writeInt(m_sampleCount);
         stream->writeInt((int) m_devices.size());
         for (size_t i = 0; i < m_devices.size(); ++i) stream->writeInt(m_devices[i]);
+        stream->writeBool(m_rehearse);
     }
 
     ~vrlAmdIntegrator() {
@@ -322,6 +328,7 @@ public:
         if (m_it) alvrl_integrator_destroy(m_it);
         releaseMore();
         if (m_localEx) alvrl_local_exchange_destroy(m_localEx);
+        if (m_devEx) alvrl_device_exchange_destroy(m_devEx);
     }
 
     bool preprocess(const Scene *scene, RenderQueue *queue, const RenderJob *job,
@@ -525,8 +532,7 @@ private:
             checkHip(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
             m_moreStreams.push_back(st);
         }
-        if (!m_more.empty() && !m_localEx)
-            check(alvrl_local_exchange_create((uint32_t) m_devices.size(), &m_localEx), "alvrl_local_exchange_create");
+        ensureExchange();
         m_ready = false;
     }
 
@@ -1022,23 +1028,39 @@ private:
         } else {
             /* every GPU renders its 64x64 tiles (alvrl_integrator_render with
                rank k of N) on its own host thread; the tiles partition the
-               frame, so the framebuffer reduce is the sum of the N frames */
+               frame, so the framebuffer reduce is the sum of the N frames:
+               one ncclReduce into device 0's framebuffer and one copy to the
+               host, or, rehearsing on one GPU, N copies summed on the host */
             const uint32_t n = (uint32_t) m_devices.size();
             std::vector<int> rcs(n, ALVRL_OK);
             std::vector<hipError_t> es(n, hipSuccess);
             std::vector<std::thread> th;
             for (uint32_t k = 0; k < n; ++k)
                 th.push_back(std::thread([&, k]() {
-                    es[k] = renderTiles(k ? m_more[k - 1] : m_it, m_devices[k], k, n, k ? m_moreFb[k - 1] : m_fb,
-                                        k ? m_moreStreams[k - 1] : m_stream, k ? &m_moreRgb[k - 1][0] : &m_rgb[0],
-                                        m_rgb.size(), &rcs[k]);
+                    float *fb = k ? m_moreFb[k - 1] : m_fb;
+                    hipStream_t st = k ? m_moreStreams[k - 1] : m_stream;
+                    if (m_devEx) {
+                        es[k] = renderTiles(k ? m_more[k - 1] : m_it, m_devices[k], k, n, fb, st, NULL, m_rgb.size(),
+                                            &rcs[k]);
+                        /* every rank joins the reduce, even after a failure of
+                           its own, so that no peer is left waiting in it */
+                        const int rr = alvrl_device_exchange_reduce_frame(m_devEx, k, fb, m_rgb.size(), st);
+                        if (rcs[k] == ALVRL_OK) rcs[k] = rr;
+                        if (es[k] == hipSuccess && rcs[k] == ALVRL_OK && k == 0)
+                            es[k] = hipMemcpyAsync(&m_rgb[0], fb, sizeof(float) * m_rgb.size(),
+                                                   hipMemcpyDeviceToHost, st);
+                        if (es[k] == hipSuccess) es[k] = hipStreamSynchronize(st);
+                    } else {
+                        es[k] = renderTiles(k ? m_more[k - 1] : m_it, m_devices[k], k, n, fb, st,
+                                            k ? &m_moreRgb[k - 1][0] : &m_rgb[0], m_rgb.size(), &rcs[k]);
+                    }
                 }));
             for (size_t k = 0; k < th.size(); ++k) th[k].join();
             for (uint32_t k = 0; k < n; ++k) {
                 if (e == hipSuccess) e = es[k];
                 if (rc == ALVRL_OK) rc = rcs[k];
             }
-            if (e == hipSuccess && rc == ALVRL_OK)
+            if (e == hipSuccess && rc == ALVRL_OK && !m_devEx)
                 for (size_t k = 0; k < m_moreRgb.size(); ++k)
                     for (size_t i = 0; i < m_rgb.size(); ++i) m_rgb[i] += m_moreRgb[k][i];
         }
@@ -1051,14 +1073,15 @@ private:
         check(rc, "alvrl_integrator_render");
     }
 
-    /* one device's share of the frame: zero, render rank k's tiles, copy back */
+    /* one device's share of the frame: zero, render rank k's tiles, copy back
+       (host == NULL: leave it on the device) */
     static hipError_t renderTiles(alvrl_integrator *it, int device, uint32_t rank, uint32_t world, float *fb,
             hipStream_t st, float *host, size_t n, int *rc) {
         *rc = ALVRL_OK;
         hipError_t e = hipSetDevice(device);
         if (e == hipSuccess) e = hipMemsetAsync(fb, 0, sizeof(float) * n, st);
         if (e == hipSuccess) *rc = alvrl_integrator_render(it, rank, world, fb, st);
-        if (e == hipSuccess && *rc == ALVRL_OK)
+        if (e == hipSuccess && *rc == ALVRL_OK && host)
             e = hipMemcpyAsync(host, fb, sizeof(float) * n, hipMemcpyDeviceToHost, st);
         if (e == hipSuccess && *rc == ALVRL_OK) e = hipStreamSynchronize(st);
         return e;
@@ -1070,18 +1093,47 @@ private:
      * OR-ed and the cluster lists all-gathered, so every integrator ends the
      * pass with every slice's list */
     void prepassDevices() {
+        ensureExchange();
         const uint32_t n = (uint32_t) m_devices.size();
         std::vector<int> rcs(n, ALVRL_OK);
         std::vector<std::thread> th;
         for (uint32_t k = 0; k < n; ++k)
             th.push_back(std::thread([&, k]() {
-                if (hipSetDevice(m_devices[k]) != hipSuccess) { rcs[k] = ALVRL_ERR_HIP; return; }
-                rcs[k] = alvrl_integrator_prepass_dist(k ? m_more[k - 1] : m_it, (uint32_t) m_pass, k, n,
-                                                       alvrl_local_exchange_rank(m_localEx, k));
+                if (hipSetDevice(m_devices[k]) != hipSuccess) rcs[k] = ALVRL_ERR_HIP;
+                else
+                    rcs[k] = alvrl_integrator_prepass_dist(k ? m_more[k - 1] : m_it, (uint32_t) m_pass, k, n,
+                                                           m_devEx ? alvrl_device_exchange_rank(m_devEx, k)
+                                                                   : alvrl_local_exchange_rank(m_localEx, k));
+                /* a rank that fails wakes the others at once instead of
+                   leaving them in the collective it will not join */
+                if (rcs[k] != ALVRL_OK) {
+                    if (m_devEx) alvrl_device_exchange_abort(m_devEx);
+                    else alvrl_local_exchange_abort(m_localEx);
+                }
             }));
         for (size_t k = 0; k < th.size(); ++k) th[k].join();
+        bool failed = false;
+        for (uint32_t k = 0; k < n; ++k) failed |= rcs[k] != ALVRL_OK;
+        if (failed) {   /* an aborted group is not reused: the next pass makes a new one */
+            if (m_devEx) alvrl_device_exchange_destroy(m_devEx);
+            if (m_localEx) alvrl_local_exchange_destroy(m_localEx);
+            m_devEx = NULL;
+            m_localEx = NULL;
+        }
         for (uint32_t k = 0; k < n; ++k)
             check(rcs[k], "alvrl_integrator_prepass_dist (amdDevices)");
+    }
+
+    /* the ranks' collective: RCCL over xGMI between distinct devices, host
+       memory for a one-GPU rehearsal (amdRehearseDevices) */
+    void ensureExchange() {
+        if (m_more.empty() || m_localEx || m_devEx)
+            return;
+        if (m_rehearse)
+            check(alvrl_local_exchange_create((uint32_t) m_devices.size(), &m_localEx), "alvrl_local_exchange_create");
+        else
+            check(alvrl_device_exchange_create(&m_devices[0], (uint32_t) m_devices.size(), &m_devEx),
+                  "alvrl_device_exchange_create");
     }
 
     void releaseMore() {
@@ -1257,7 +1309,9 @@ private:
     std::vector<float *> m_moreFb;
     std::vector<hipStream_t> m_moreStreams;
     mutable std::vector<std::vector<float> > m_moreRgb;
-    alvrl_local_exchange *m_localEx = NULL;
+    alvrl_local_exchange *m_localEx = NULL;   /* amdRehearseDevices: ranks exchange through host memory */
+    alvrl_device_exchange *m_devEx = NULL;     /* distinct devices: RCCL (mask, lists, frame reduce) */
+    bool m_rehearse = false;
     /* wakeup: the VRL resource this instance published (the master) and the
      * last one it installed (a render worker) */
     const SerializableObject *m_pubVrls = NULL;

@@ -177,7 +177,7 @@ def run_full(props: str = "", nvrl: int = C5_VRLS, width: int = C5_W, height: in
                         R_bytes=int(st["rows_built"]) * int(st["vrls"]) * 8, ms_rbuild=st["ms_rbuild"],
                         ms_refine_kernel=st["ms_refine_kernel"], refine_entries=int(st["refine_entries"]),
                         refine_split_entries=int(st["refine_split_entries"]),
-                        contrib_preprocess=int(st["contrib_preprocess"]), slices_failed=int(st["slices_failed"]),
+                        contrib_preprocess=int(st["contrib_preprocess"] - st_first["contrib_preprocess"]), slices_failed=int(st["slices_failed"]),
                         fallback_built=int(st["fallback_built"]), s_prepass=dt, s_prepass_first=dt_first,
                         ms_refine_wall_first=st_first["ms_refine"],
                         ms_alloc=st["ms_alloc"], ms_trace=st["ms_trace"], ms_refine_wall=st["ms_refine"],

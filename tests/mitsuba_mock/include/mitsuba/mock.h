@@ -1,8 +1,12 @@
 /*
  * mock.h -- the Mitsuba 0.x declarations that mitsuba_plugin/vrlAmdIntegrator.cpp
- * uses, restated as declarations only (no bodies: the plugin is compiled with
- * -c, never linked or run here).  Test infrastructure for
- * tests/test_plugin_source.py; it is not Mitsuba.  Signatures follow the
+ * uses, restated (test infrastructure, not Mitsuba).  tests/test_plugin_source.py
+ * compiles the plugin against them; tests/mitsuba_mock/src/mock_impl.cpp
+ * implements just enough of them -- a smoke-box scene, properties, the
+ * scheduler's resources, image blocks -- for tests/test_gpu_plugin_run.py to
+ * load the plugin and run it: preprocess, prepass, renderBlock.  The "mock
+ * state" members below hold that implementation's data; they are no part of
+ * the interface the plugin sees (it never names them).  Signatures follow the
  * mitsuba-ALVRL headers (include/mitsuba/core/{object,class,cobject,sched,
  * stream,properties}.h, render/{integrator,scene,sensor,film,bsdf,medium,
  * phase,emitter,shape,trimesh,imageblock,records}.h) so that a call or an
@@ -50,20 +54,29 @@ public:
     virtual std::string toString() const;
 protected:
     virtual ~Object();
+public:   /* mock state */
+    mutable int m_refCount;
 };
 
 template <typename T> class ref {
 public:
-    ref();
-    ref(T *ptr);
-    ref(const ref &r);
-    ~ref();
-    ref &operator=(const ref &r);
-    ref &operator=(T *ptr);
-    T *operator->() const;
-    T &operator*() const;
-    operator T *() const;
-    T *get() const;
+    ref() : m_ptr(NULL) { }
+    ref(T *ptr) : m_ptr(ptr) { if (m_ptr) ((const Object *) m_ptr)->incRef(); }
+    ref(const ref &r) : m_ptr(r.m_ptr) { if (m_ptr) ((const Object *) m_ptr)->incRef(); }
+    ~ref() { if (m_ptr) ((const Object *) m_ptr)->decRef(); }
+    ref &operator=(const ref &r) { return *this = r.m_ptr; }
+    ref &operator=(T *ptr) {
+        if (ptr) ((const Object *) ptr)->incRef();
+        if (m_ptr) ((const Object *) m_ptr)->decRef();
+        m_ptr = ptr;
+        return *this;
+    }
+    T *operator->() const { return m_ptr; }
+    T &operator*() const { return *m_ptr; }
+    operator T *() const { return m_ptr; }
+    T *get() const { return m_ptr; }
+private:
+    T *m_ptr;
 };
 template <typename T> class ref_vector : public std::vector< ref<T> > { };
 
@@ -72,6 +85,8 @@ public:
     Class(const std::string &name, bool abstract, const std::string &superClassName, void *instPtr = NULL,
           void *unSerPtr = NULL);
     const std::string &getName() const;
+public:   /* mock state */
+    std::string m_name;
 };
 
 #define MTS_DECLARE_CLASS() \
@@ -140,6 +155,7 @@ public:
 protected:
     ConfigurableObject(const Properties &props);
     ConfigurableObject(Stream *stream, InstanceManager *manager);
+    ConfigurableObject();   /* mock: the objects mock_impl.cpp builds directly */
 };
 
 class Properties {
@@ -150,6 +166,8 @@ public:
     std::string getString(const std::string &name, const std::string &defVal) const;
     std::string getAsString(const std::string &name) const;
     void putPropertyNames(std::vector<std::string> &results) const;
+public:   /* mock state */
+    std::map<std::string, std::string> m_values;
 };
 
 class ParallelProcess : public Object {
@@ -163,6 +181,9 @@ public:
     int registerResource(SerializableObject *resource);
     bool unregisterResource(int id);
     SerializableObject *getResource(int id, int coreIndex = -1);
+public:   /* mock state */
+    std::map<int, ref<SerializableObject> > m_res;
+    int m_next;
 };
 
 /* ---- geometry ---- */
@@ -218,10 +239,14 @@ struct AABB {
 struct Transform {
     Point operator()(const Point &p) const;
     Vector operator()(const Vector &v) const;
+    /* mock state: an affine map, evaluated in double */
+    double m[3][4];
 };
 class AnimatedTransform : public Object {
 public:
     Transform eval(Float t) const;
+public:   /* mock state */
+    Transform m_t;
 };
 
 struct Ray {
@@ -259,6 +284,8 @@ public:
     Float max() const;
     void toLinearRGB(Float &r, Float &g, Float &b) const;
     void fromLinearRGB(Float r, Float g, Float b);
+public:   /* mock state */
+    Float s[3];
 };
 
 /* ---- render ---- */
@@ -295,6 +322,8 @@ public:
     virtual Point2 next2D() = 0;
     size_t getSampleCount() const;
     size_t getSampleIndex() const;
+public:   /* mock state */
+    size_t m_sampleCount, m_sampleIndex;
 };
 
 struct MediumSamplingRecord {
@@ -316,6 +345,9 @@ public:
     const PhaseFunction *getPhaseFunction() const;
     const Spectrum &getSigmaA() const;
     const Spectrum &getSigmaS() const;
+public:   /* mock state */
+    Spectrum m_sigmaA, m_sigmaS;
+    ref<PhaseFunction> m_phase;
 };
 
 struct BSDFSamplingRecord {
@@ -355,6 +387,8 @@ public:
     virtual Spectrum getDiffuseReflectance(const Intersection &its) const = 0;
     virtual Spectrum getSpecularReflectance(const Intersection &its) const;
     virtual Float getEta() const;
+public:   /* mock state */
+    unsigned int m_type;
 };
 
 /* render/common.h:56-69 */
@@ -387,6 +421,8 @@ public:
                                     const Point2 *extra = NULL) const = 0;
     /* render/emitter.h: the spatial part of the emitted radiance */
     virtual Spectrum evalPosition(const PositionSamplingRecord &pRec) const;
+public:   /* mock state */
+    unsigned int m_type;
 };
 
 class Shape : public ConfigurableObject {
@@ -402,6 +438,11 @@ public:
     const Medium *getInteriorMedium() const;
     const Medium *getExteriorMedium() const;
     virtual std::string getName() const;
+public:   /* mock state */
+    ref<BSDF> m_bsdf;
+    ref<Emitter> m_emitter;
+    const Medium *m_interior, *m_exterior;
+    std::string m_name;
 };
 
 struct Triangle {
@@ -417,12 +458,18 @@ public:
     bool hasVertexNormals() const;
     const Triangle *getTriangles() const;
     size_t getTriangleCount() const;
+public:   /* mock state */
+    std::vector<Point> m_pos;
+    std::vector<Normal> m_nrm;
+    std::vector<Triangle> m_tri;
 };
 
 class Film : public ConfigurableObject {
 public:
     const Vector2i &getSize() const;
     const Vector2i &getCropSize() const;
+public:   /* mock state */
+    Vector2i m_size;
 };
 
 class Sensor : public ConfigurableObject {
@@ -437,11 +484,17 @@ public:
     const Film *getFilm() const;
     const Medium *getMedium() const;
     const AnimatedTransform *getWorldTransform() const;
+public:   /* mock state */
+    ref<Film> m_film;
+    const Medium *m_medium;
+    ref<AnimatedTransform> m_toWorld;
 };
 
 class PerspectiveCamera : public Sensor {
 public:
     Float getXFov() const;
+public:   /* mock state */
+    Float m_xfov;
 };
 
 class Scene : public ConfigurableObject {
@@ -452,6 +505,12 @@ public:
     const ref_vector<Medium> &getMedia() const;
     const ref_vector<Emitter> &getEmitters() const;
     const ref_vector<Shape> &getShapes() const;
+public:   /* mock state */
+    AABB m_aabb;
+    ref<Sensor> m_sensor;
+    ref_vector<Medium> m_media;
+    ref_vector<Emitter> m_emitters;
+    ref_vector<Shape> m_shapes;
 };
 
 class ImageBlock : public Object {
@@ -459,6 +518,11 @@ public:
     void clear();
     const Point2i &getOffset() const;
     bool put(const Point2 &pos, const Spectrum &spec, Float alpha);
+public:   /* mock state: puts land in an RGB frame of width m_frameWidth */
+    Point2i m_offset;
+    Vector2i m_size;
+    float *m_frame;
+    int m_frameWidth;
 };
 
 struct RadianceQueryRecord {
