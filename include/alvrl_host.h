@@ -214,8 +214,11 @@ typedef struct {
 } alvrl_exchange;
 
 /* vrlIntegrator::prepass with the LightSlice work sharded by slice: rank r
- * builds R for, and refines, the slices s with s % world == r (plus the rows
- * of their neighbour slices when neighbourCount > 0), the non-zero VRL mask
+ * builds R for, and refines, its share of the slices (plus the rows of their
+ * neighbour slices when neighbourCount > 0): by default the longest-
+ * processing-time assignment on the slices' local-matrix rows (every rank
+ * derives the same one; alvrl_integrator_local_slices lists this rank's),
+ * s % world == r with the property sliceSharding=roundrobin; the non-zero VRL mask
  * of Preprocessor::cluster (:843-855) is OR-reduced over ranks, and the
  * per-slice cluster lists are all-gathered so every rank can render any
  * tile.  Results are identical to alvrl_integrator_prepass on one GPU.  The
@@ -393,6 +396,9 @@ ALVRL_API alvrl_ctx *alvrl_integrator_ctx(alvrl_integrator *it);
  * y + H*x, vrlIntegrator.cpp:560), representative rows, cluster CSR. */
 ALVRL_API int alvrl_integrator_slices(alvrl_integrator *it, uint32_t *pixel_to_slice, uint32_t n);
 ALVRL_API uint32_t alvrl_integrator_num_slices(alvrl_integrator *it);
+/* The slices the last prepass refined on this integrator, ascending (all of
+ * them at world 1).  out may be NULL to learn *n. */
+ALVRL_API int alvrl_integrator_local_slices(alvrl_integrator *it, uint32_t *out, uint32_t cap, uint32_t *n);
 ALVRL_API int alvrl_integrator_reps(alvrl_integrator *it, uint32_t *rep_off, uint32_t *rep_pix,
                                     uint32_t cap);
 ALVRL_API int alvrl_integrator_clusters(alvrl_integrator *it, uint32_t *slice_off, uint32_t *reps,

@@ -693,6 +693,7 @@ def _host():
     L.alvrl_local_exchange_create.argtypes = [u32, P(vp)]
     L.alvrl_local_exchange_rank.argtypes = [vp, u32]; L.alvrl_local_exchange_rank.restype = vp
     L.alvrl_local_exchange_destroy.argtypes = [vp]; L.alvrl_local_exchange_destroy.restype = None
+    L.alvrl_integrator_local_slices.argtypes = [vp, vp, u32, P(u32)]
     L.alvrl_device_exchange_create.argtypes = [vp, u32, P(vp)]
     L.alvrl_device_exchange_rank.argtypes = [vp, u32]; L.alvrl_device_exchange_rank.restype = vp
     L.alvrl_device_exchange_reduce_frame.argtypes = [vp, u32, vp, u64, vp]
@@ -1128,6 +1129,14 @@ class Integrator:
         st = IntegratorStats()
         _hcheck(self.L.alvrl_integrator_get_stats(self.h, C.byref(st)))
         return st.as_dict()
+
+    def local_slices(self) -> np.ndarray:
+        """The slices the last prepass refined here (alvrl_integrator_local_slices)."""
+        n = C.c_uint32()
+        _hcheck(self.L.alvrl_integrator_local_slices(self.h, None, 0, C.byref(n)))
+        out = np.zeros(max(1, n.value), np.uint32)
+        _hcheck(self.L.alvrl_integrator_local_slices(self.h, _ptr(out), n.value, C.byref(n)))
+        return out[:n.value].copy()
 
     def num_slices(self) -> int:
         return int(self.L.alvrl_integrator_num_slices(self.h))

@@ -121,7 +121,10 @@ struct alvrl_integrator {
     // the host tracer) wherever the scene fits it -- no mirror / null /
     // dielectric triangles, whose particles the host traces; false: always the host
     bool gpuTracer = true;
-    bool strictRbuild = true;    // the R build in the oracle's arithmetic (alvrl_set_strict_rbuild); false: the gathers' fast maths
+    bool strictRbuild = true;
+    // slices to ranks with world > 1: "cost" (longest processing time first on
+    // each slice's local rows, the default) or "roundrobin" (s % world)
+    bool sliceRoundRobin = false;    // the R build in the oracle's arithmetic (alvrl_set_strict_rbuild); false: the gathers' fast maths
     // ---- state
     int device = 0;
     alvrl_ctx* ctx = nullptr;
@@ -141,6 +144,7 @@ struct alvrl_integrator {
     std::vector<uint32_t> pixel_to_slice;   // y + H*x
     VrlSet vrls;
     bool vrls_from_file = false;
+    std::vector<uint32_t> local_slices;     // the slices the last prepass refined here (alvrl_integrator_local_slices)
     uint32_t uploaded_pass = 0xFFFFFFFFu;
     bool clustered = false;
     // R
@@ -210,6 +214,10 @@ struct alvrl_integrator {
         else if (k == "shortVrls") shortVrls = b(v);
         else if (k == "gpuTracer") gpuTracer = b(v);
         else if (k == "strictRbuild") strictRbuild = b(v);
+        else if (k == "sliceSharding") {
+            if (v != "cost" && v != "roundrobin") throw IntegError(ALVRL_ERR_INVALID, "sliceSharding must be cost or roundrobin");
+            sliceRoundRobin = v == "roundrobin";
+        }
         else if (k == "vrlTargetNum") vrlTargetNum = i(v);
         else if (k == "maxParticleDepth") maxParticleDepth = i(v);
         else if (k == "specularForcedRRdepth") specRRdepth = i(v);
@@ -729,8 +737,39 @@ struct alvrl_integrator {
         hipEventDestroy(e0); hipEventDestroy(e1);
     }
 
-    // buildClusters (:293-346).  With world > 1 the slices are dealt round
-    // robin (s % world == rank): this rank builds R for its slices and their
+    // The slices of rank `rank` of `world`: longest processing time first over
+    // each slice's local-matrix rows (the refinement's and the R build's cost
+    // both grow with them; every slice has every column) -- slices by cost,
+    // largest first (ties: lower index), each to the least-loaded rank (ties:
+    // lower rank) -- or s % world with sliceSharding=roundrobin.  Every rank
+    // derives the same assignment from the pass's slice mapping.
+    std::vector<uint32_t> slices_of_rank(uint32_t rank, uint32_t world,
+                                         const std::vector<std::vector<uint32_t>>& all_rows) const
+    {
+        const uint32_t ns = (uint32_t)all_rows.size();
+        std::vector<uint32_t> mine;
+        if (world <= 1 || sliceRoundRobin) {
+            for (uint32_t s = rank; s < ns; s += world) mine.push_back(s);
+            return mine;
+        }
+        std::vector<uint32_t> order(ns);
+        for (uint32_t s = 0; s < ns; s++) order[s] = s;
+        std::stable_sort(order.begin(), order.end(),
+                         [&](uint32_t a, uint32_t b) { return all_rows[a].size() > all_rows[b].size(); });
+        std::vector<uint64_t> load(world, 0);
+        for (uint32_t s : order) {
+            uint32_t best = 0;
+            for (uint32_t r = 1; r < world; r++)
+                if (load[r] < load[best]) best = r;
+            load[best] += all_rows[s].size();
+            if (best == rank) mine.push_back(s);
+        }
+        std::sort(mine.begin(), mine.end());
+        return mine;
+    }
+
+    // buildClusters (:293-346).  With world > 1 the slices are sharded over
+    // the ranks (slices_of_rank): this rank builds R for its slices and their
     // neighbours' rows, refines its slices, and the exchange makes the mask
     // and the cluster lists global.
     void build_clusters(uint32_t pass_id, uint32_t rank, uint32_t world, const alvrl_exchange* ex)
@@ -743,15 +782,22 @@ struct alvrl_integrator {
         const uint32_t ns = prep->num_slices();
         const uint32_t rows = roff[ns];
         st.rep_rows = rows;
-        // local matrices of this rank's slices (getLocalMatrix, :779-827)
+        // local matrices (getLocalMatrix, :779-827): every slice's with world > 1
+        // (the assignment's costs), this rank's slices' otherwise
+        std::vector<std::vector<uint32_t>> all_rows(world > 1 ? ns : 0);
+        std::vector<std::vector<double>> all_w(world > 1 ? ns : 0);
+        for (uint32_t s = 0; s < (world > 1 ? ns : 0); s++) prep->local_matrix(s, &all_rows[s], &all_w[s]);
         std::vector<uint32_t> mine;
-        for (uint32_t s = rank; s < ns; s += world) mine.push_back(s);
+        if (world > 1) mine = slices_of_rank(rank, world, all_rows);
+        else for (uint32_t s = 0; s < ns; s++) mine.push_back(s);
+        local_slices = mine;
         const uint32_t nm = (uint32_t)mine.size();
         std::vector<std::vector<uint32_t>> lrows(nm);
         std::vector<std::vector<double>> lw(nm);
         std::vector<char> need(ns, 0);
         for (uint32_t k = 0; k < nm; k++) {
-            prep->local_matrix(mine[k], &lrows[k], &lw[k]);
+            if (world > 1) { lrows[k].swap(all_rows[mine[k]]); lw[k].swap(all_w[mine[k]]); }
+            else prep->local_matrix(mine[k], &lrows[k], &lw[k]);
             need[mine[k]] = 1;
             for (uint32_t g : lrows[k])
                 need[(uint32_t)(std::upper_bound(roff.begin(), roff.end(), g) - roff.begin()) - 1] = 1;
@@ -1329,6 +1375,15 @@ ALVRL_API int alvrl_integrator_load_cluster_info(alvrl_integrator* it, const cha
 {
     if (!it || !path) return ierr(ALVRL_ERR_INVALID, "alvrl_integrator_load_cluster_info: null argument");
     GUARD({ hchk(hipSetDevice(it->device), "hipSetDevice"); it->load_cluster_info(path, pass); });
+    return ALVRL_OK;
+}
+
+ALVRL_API int alvrl_integrator_local_slices(alvrl_integrator* it, uint32_t* out, uint32_t cap, uint32_t* n)
+{
+    if (!it || !n) return ierr(ALVRL_ERR_INVALID, "alvrl_integrator_local_slices: null argument");
+    *n = (uint32_t)it->local_slices.size();
+    if (out && cap < *n) return ierr(ALVRL_ERR_INVALID, "alvrl_integrator_local_slices: cap too small");
+    if (out) std::copy(it->local_slices.begin(), it->local_slices.end(), out);
     return ALVRL_OK;
 }
 

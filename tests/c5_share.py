@@ -47,7 +47,7 @@ class SimExchange:
     rank's own bytes in its slot), so the library ORs the true masks.
     "zero": the others send zero masks (round 3's rank-0 timing form)."""
 
-    def __init__(self, rank: int, world: int, nslices: int, masks=None):
+    def __init__(self, rank: int, world: int, nslices: int, masks=None, owners=None):
         import alvrl
         self.rank, self.world, self.nslices = rank, world, nslices
         self.masks = masks
@@ -56,10 +56,11 @@ class SimExchange:
         self.calls = []
         self._pending = None        # a counts round was seen: the next call is the data round
         self.others = {}
+        # the other ranks' slices (owners[r]; default s % world)
         for r in range(world):
             if r != rank:
-                self.others[r] = b"".join(struct.pack("<IIIIf", s, 1, 1, 0, 1.0)
-                                          for s in range(r, nslices, world))
+                mine = owners[r] if owners is not None else range(r, nslices, world)
+                self.others[r] = b"".join(struct.pack("<IIIIf", s, 1, 1, 0, 1.0) for s in mine)
 
         def allgather(user, send, nbytes, recv):
             try:
@@ -103,6 +104,21 @@ class SimExchange:
                                    + (f" ({self.error!r})" if self.error else ""))
 
 
+def lpt_owners(rows, world: int):
+    """The integrator's default slice assignment (integrator.hip
+    slices_of_rank) for slices whose local matrix is their own rows
+    (neighbourCount = 0): slices by row count, largest first (ties: lower
+    index), each to the least-loaded rank (ties: lower rank)."""
+    order = sorted(range(len(rows)), key=lambda s: (-int(rows[s]), s))
+    load = [0] * world
+    owners = [[] for _ in range(world)]
+    for s in order:
+        r = min(range(world), key=lambda q: (load[q], q))
+        load[r] += int(rows[s])
+        owners[r].append(s)
+    return [sorted(o) for o in owners]
+
+
 def _props(nvrl: int, gpu_tracer: bool, props: str) -> str:
     return (f"vrlTargetNum={nvrl};gpuTracer={'true' if gpu_tracer else 'false'};"
             f"seed={SEED_RNG};vrlSeed={SEED_VRL}" + (";" + props if props else ""))
@@ -120,14 +136,18 @@ def run_full(props: str = "", nvrl: int = C5_VRLS, width: int = C5_W, height: in
     scene = alvrl.scene_default(width, height)
     P = _props(nvrl, True, props)
     t_start = time.time()
-    # phase 1: the masks
-    masks, ns = [], None
+    # phase 1: the masks (and the slice assignment every rank derives)
+    masks, ns, phase1_owners = [], None, None
     for r in range(world):
         it = alvrl.Integrator(P, device=0)
         try:
             it.preprocess(scene)
             ns = it.num_slices()
-            ex = SimExchange(r, world, ns, masks=None)
+            if phase1_owners is None:
+                it.rep_pixels(pass_)
+                off, _ = it.reps()
+                phase1_owners = lpt_owners(np.diff(off), world)
+            ex = SimExchange(r, world, ns, masks=None, owners=phase1_owners)
             try:
                 it.prepass(pass_, rank=r, world=world, exchange=ex)
                 raise AssertionError("capture exchange did not stop the prepass")
@@ -141,6 +161,7 @@ def run_full(props: str = "", nvrl: int = C5_VRLS, width: int = C5_W, height: in
     nz = np.zeros(len(masks[0]), np.uint8)
     for m in masks:
         nz |= np.frombuffer(m, np.uint8)
+    owners = phase1_owners
     t1 = time.time()
     log(f"C5 phase 1: {world} masks in {t1 - t_start:.1f} s, {int(nz.sum())} of {nz.size} VRLs non-zero "
         f"(per rank {[int(np.frombuffer(m, np.uint8).sum()) for m in masks]})")
@@ -151,22 +172,23 @@ def run_full(props: str = "", nvrl: int = C5_VRLS, width: int = C5_W, height: in
         it = alvrl.Integrator(P, device=0)
         try:
             it.preprocess(scene)
-            ex = SimExchange(r, world, ns, masks=masks)
+            ex = SimExchange(r, world, ns, masks=masks, owners=owners)
             t0 = time.time()
             it.prepass(pass_, rank=r, world=world, exchange=ex)
             dt_first = time.time() - t0
+            assert [int(x) for x in it.local_slices()] == owners[r], "the integrator's slice assignment" 
             st_first = it.stats()
             # the same pass again: the steady state of a rank that keeps its
             # integrator across passes (R and the refinement's arenas already
             # allocated, as in the bench); the first pass of a fresh
             # integrator also pays their hipMalloc
-            ex = SimExchange(r, world, ns, masks=masks)
+            ex = SimExchange(r, world, ns, masks=masks, owners=owners)
             t0 = time.time()
             it.prepass(pass_, rank=r, world=world, exchange=ex)
             dt = time.time() - t0
             st = it.stats()
             off, _ = it.reps()
-            mine = list(range(r, ns, world))
+            mine = owners[r]
             rows = np.diff(off)[mine]
             cl = it.clusters()
             for s in mine:
@@ -234,12 +256,17 @@ def run_share(props: str = "", nvrl: int = C5_VRLS, width: int = C5_W, height: i
     it.preprocess(scene)
     t1 = time.time()
     ns = it.num_slices()
-    ex = SimExchange(0, world, ns, masks="zero")
+    it.rep_pixels(pass_)
+    off, _ = it.reps()
+    owners = lpt_owners(np.diff(off), world)
+    t1 = time.time()
+    ex = SimExchange(0, world, ns, masks="zero", owners=owners)
     it.prepass(pass_, rank=0, world=world, exchange=ex)
     t2 = time.time()
     st = it.stats()
     off, _ = it.reps()
-    mine = list(range(0, ns, world))
+    mine = owners[0]
+    assert [int(x) for x in it.local_slices()] == mine, "the integrator's slice assignment"
     rows = np.diff(off)[mine]
     info = dict(slices=ns, slices_local=st["slices_local"], vrls=st["vrls"], particles=st["particles"],
                 rep_rows=st["rep_rows"], rows_built=st["rows_built"], rows_local=[int(x) for x in rows],

@@ -7,8 +7,10 @@ tiles plus the framebuffer sum (tests/c5_share.py, phases 1-3).
 
 Checks against the oracle (oracle/alvrl_preproc.c, alvrl_oracle.c):
   * refinement (Preprocessor.cpp:254-283: Clustering ctor, refineAdaptively,
-    sampleRepresentatives) of rank 0's smallest slice and of rank 3's smallest
-    slice of more than 256 rows (the v3 engine over row groups) on the
+    sampleRepresentatives) of rank 0's smallest slice and of the smallest
+    slice of more than 256 rows of the first rank that holds one (the v3
+    engine over row groups; slices go to ranks by their cost, the
+    integrator's default sliceSharding) on the
     device's own jobs (alvrl_integrator_slice_job): representatives and
     weights bit for bit;
   * the frame: every 64th image row against the oracle's clustered gather
@@ -36,6 +38,7 @@ def test_c5_end_to_end(oracle, gpu_ok, tmp_path):
     import c5_share
     W, H, world = c5_share.C5_W, c5_share.C5_H, c5_share.C5_WORLD
     checked = []
+    checked_big = []
 
     def check(rank, it, info, mine):
         assert info["slices_local"] == len(mine) and info["slices_failed"] == 0
@@ -49,10 +52,10 @@ def test_c5_end_to_end(oracle, gpu_ok, tmp_path):
         picks = []
         if rank == 0:
             picks.append(mine[int(np.argmin(rows[mine]))])
-        if rank == 3:
-            big = [s for s in mine if rows[s] > 256]
-            assert big
+        big = [s for s in mine if rows[s] > 256]
+        if big and not checked_big:           # the first rank holding a slice of > 256 rows (row groups)
             picks.append(min(big, key=lambda s: rows[s]))
+            checked_big.append(rank)
         if not picks:
             return
         cl = it.clusters()
@@ -75,7 +78,7 @@ def test_c5_end_to_end(oracle, gpu_ok, tmp_path):
 
     it, info = c5_share.run_full(check=check, workdir=str(tmp_path))
     try:
-        assert [c["rank"] for c in checked] == [0, 3]
+        assert checked[0]["rank"] == 0 and len(checked) >= 2 and any(c["rows"] > 256 for c in checked), checked
         ns = info["slices"]
         assert len(info["slice_off"]) == ns + 1 and (np.diff(info["slice_off"]) > 0).all()
         # phase 3: the eight ranks' tiles and the framebuffer reduce
