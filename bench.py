@@ -85,9 +85,9 @@ def parse():
                     help="clustered configs: skip the comparison with the oracle's own pipeline")
     ap.add_argument("--cpu-row-stride", type=int, default=64,
                     help="CPU baseline sample: every n-th image row")
-    ap.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "r05", "pmc_traffic.json"),
+    ap.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "r06", "pmc_traffic.json"),
                     help="per-launch HBM bytes of the dominant kernel from a rocprofv3 --pmc pass")
-    ap.add_argument("--valu-json", default=os.path.join(REPO, "profiles", "r05", "pmc_valu_{cfg}.json"),
+    ap.add_argument("--valu-json", default=os.path.join(REPO, "profiles", "r06", "pmc_valu_{cfg}.json"),
                     help="per-kernel VALU counters (tools/pmc_valu.sh + tools/pmc_valu.py)")
     return ap.parse_args()
 
@@ -300,9 +300,13 @@ def main():
         rk = float(np.mean(refine_kms)) / 1e3
         rooflines["refine"]["frac_one_pass"] = (8.0 * ent1 / rk / 1e9 / HBM_PEAK_GBS) if rk > 0 else None
         rooflines["refine"]["bytes_one_pass"] = 8.0 * ent1
-        rooflines["rbuild"] = roof("k_build_R_blocks", "rbuild",
+        strict = "strictRbuild=false" not in props          # the integrator's default R build
+        rooflines["rbuild"] = roof("k_build_R_strict" if strict else "k_build_R_blocks", "rbuild",
                                    BYTES_PER_PAIR["rbuild"] * (s1["contrib_preprocess"] - s0["contrib_preprocess"]) / nst,
-                                   float(np.mean(rbuild_ms)), "VALU-bound like the gather")
+                                   float(np.mean(rbuild_ms)),
+                                   "VALU-bound: integrateVRL in the oracle's arithmetic (f64 transcendentals with a "
+                                   "Ziv rounding test, IEEE division and sqrt), bit-identical to the oracle's R"
+                                   if strict else "VALU-bound like the gather")
     dominant = max(rooflines, key=lambda k: rooflines[k]["launch_ms"])
 
     out = None

@@ -17,7 +17,7 @@ import os
 import sys
 
 KEYS = {"k_refine": "refine", "k_gather_clustered": "render", "k_gather_brute": "render",
-        "k_build_R_blocks": "rbuild"}
+        "k_build_R_blocks": "rbuild", "k_build_R_strict": "rbuild"}
 
 
 def per_kernel(d, counter):
