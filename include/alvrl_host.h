@@ -71,6 +71,12 @@ typedef struct {
     const float *emitter_tris;
     uint32_t n_emitter_tris;
     float emitter_radiance[3];
+    /* Optional per-occluder diffuse reflectance, 3 floats per triangle in
+     * [0, 1] (NULL: occluder_albedo for every DIFFUSE triangle): each
+     * shape's own SmoothDiffuse -- e.g. an area emitter's mesh, to which
+     * Mitsuba gives an all-absorbing one (shape.cpp:49-56).  Read like
+     * occluders. */
+    const float *occluder_albedos;
 } alvrl_scene_desc;
 #define ALVRL_MAT_DIFFUSE 0u
 #define ALVRL_MAT_MIRROR 1u

@@ -449,7 +449,7 @@ class SceneDesc(C.Structure):
                 ("occluder_albedo", C.c_float * 3), ("occluder_material", C.POINTER(C.c_uint32)),
                 ("occluder_specular", C.c_float * 3), ("occluder_eta", C.c_float),
                 ("emitter_tris", C.POINTER(C.c_float)), ("n_emitter_tris", C.c_uint32),
-                ("emitter_radiance", C.c_float * 3)]
+                ("emitter_radiance", C.c_float * 3), ("occluder_albedos", C.POINTER(C.c_float))]
 
 
 MAT_DIFFUSE, MAT_MIRROR, MAT_NULL, MAT_DIELECTRIC = 0, 1, 2, 3
@@ -744,12 +744,14 @@ def scene_set_area_emitter(scene: SceneDesc, tris, radiance) -> SceneDesc:
 
 
 def scene_set_occluders(scene: SceneDesc, tris, albedo=(0.5, 0.5, 0.5), material=None,
-                        specular=(1.0, 1.0, 1.0), eta=None) -> SceneDesc:
+                        specular=(1.0, 1.0, 1.0), eta=None, albedos=None) -> SceneDesc:
     """Occluder triangles inside the box (alvrl_scene_desc.occluders): an
     (n, 9) float array of (p0, p1, p2), face normal cross(p1 - p0, p2 - p0);
     material: None (all diffuse) or one MAT_* per triangle; specular: the
     mirrors' reflectance; eta: the dielectrics' intIOR / extIOR (None: the
-    default bk7 / air).  The arrays are kept alive on the descriptor."""
+    default bk7 / air); albedos: (n, 3) per-triangle diffuse reflectances
+    (occluder_albedos, replacing albedo).  The arrays are kept alive on the
+    descriptor."""
     if eta is not None:
         scene.occluder_eta = float(eta)
     arr = np.ascontiguousarray(np.asarray(tris, np.float32).reshape(-1, 9))
@@ -765,6 +767,12 @@ def scene_set_occluders(scene: SceneDesc, tris, albedo=(0.5, 0.5, 0.5), material
         mat = np.ascontiguousarray(np.broadcast_to(np.asarray(material, np.uint32), (len(arr),)))
         scene._mat_keep = mat
         scene.occluder_material = mat.ctypes.data_as(C.POINTER(C.c_uint32))
+    if albedos is None:
+        scene.occluder_albedos = None
+    else:
+        alb = np.ascontiguousarray(np.asarray(albedos, np.float32).reshape(len(arr), 3))
+        scene._alb_keep = alb
+        scene.occluder_albedos = alb.ctypes.data_as(C.POINTER(C.c_float))
     return scene
 
 

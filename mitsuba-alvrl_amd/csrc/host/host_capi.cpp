@@ -38,6 +38,10 @@ const char* scene_problem(const alvrl_scene_desc& s)
         for (uint32_t i = 0; i < s.n_occluders; i++)
             if (s.occluder_material[i] > ALVRL_MAT_DIELECTRIC) return "alvrl_scene_desc: unknown occluder material";
     if (s.n_emitter_tris && !s.emitter_tris) return "alvrl_scene_desc: n_emitter_tris > 0 without emitter_tris";
+    if (s.occluders && s.occluder_albedos)
+        for (size_t i = 0; i < 3 * (size_t)s.n_occluders; i++)
+            if (!(s.occluder_albedos[i] >= 0.0f && s.occluder_albedos[i] <= 1.0f))
+                return "alvrl_scene_desc: occluder_albedos must lie in [0, 1]";
     if (s.n_emitter_tris) {
         for (size_t i = 0; i < 9 * (size_t)s.n_emitter_tris; i++)
             if (!std::isfinite(s.emitter_tris[i])) return "alvrl_scene_desc: non-finite emitter vertex";
@@ -68,6 +72,8 @@ SmokeBox to_box(const alvrl_scene_desc& s)
     b.medium.resolve();
     if (s.occluders && s.n_occluders) b.occ.assign(s.occluders, s.occluders + 9 * (size_t)s.n_occluders);
     for (int i = 0; i < 3; i++) b.occ_albedo[i] = s.occluder_albedo[i];
+    if (s.occluders && s.n_occluders && s.occluder_albedos)
+        b.occ_alb.assign(s.occluder_albedos, s.occluder_albedos + 3 * (size_t)s.n_occluders);
     if (s.occluders && s.n_occluders && s.occluder_material)
         b.occ_mat.assign(s.occluder_material, s.occluder_material + s.n_occluders);
     for (int i = 0; i < 3; i++) b.occ_spec[i] = s.occluder_specular[i];

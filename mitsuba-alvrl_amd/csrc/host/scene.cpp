@@ -274,7 +274,7 @@ void SmokeBox::make_record(int x, int y, bool medium_scatters, float rec[kRecWor
     if (std::isfinite(t)) flags |= 1u | (m == 0u ? 2u : 8u);   // ESmooth (diffuse) or EDelta
     if (medium_scatters) flags |= 4u;
     static const float kZero[3] = {0.0f, 0.0f, 0.0f};
-    const float* a = m != 0u ? kZero : (tri >= 0 ? occ_albedo : albedo);
+    const float* a = m != 0u ? kZero : (tri >= 0 ? occ_albedo_of(tri) : albedo);
     rec[0] = O.x; rec[1] = O.y; rec[2] = O.z;
     rec[3] = D.x; rec[4] = D.y; rec[5] = D.z;
     rec[6] = p.x; rec[7] = p.y; rec[8] = p.z;
@@ -490,7 +490,7 @@ void trace_particle(const SmokeBox& sc, Stream& smp, bool short_vrls, int max_de
             const float rpf = 1.0f / pf;
             for (int i = 0; i < 3; i++) thr[i] *= mtr[i] * rpf;
             const V3 p = hp;
-            const float* alb = tri >= 0 ? sc.occ_albedo : sc.albedo;
+            const float* alb = tri >= 0 ? sc.occ_albedo_of(tri) : sc.albedo;
             V3 fs, ft;
             frame_of(n, &fs, &ft);
             const V3 mwi = -dir;
@@ -642,7 +642,7 @@ void SmokeBox::chain_node(V3 O, V3 D, float mint, const float weight[3], const f
     if (!std::isfinite(t)) return;                                        // :414-419
     const uint32_t m = mat(tri);
     const uint32_t flags = 1u | (m == 0u ? 2u : 8u) | (medium_scatters ? 4u : 0u);
-    const float* a = tri >= 0 ? occ_albedo : albedo;
+    const float* a = tri >= 0 ? occ_albedo_of(tri) : albedo;
     const size_t o = out->size();
     out->resize(o + kRecWords);
     float* rec = out->data() + o;

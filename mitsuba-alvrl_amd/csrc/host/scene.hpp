@@ -76,6 +76,8 @@ struct SmokeBox {
     MediumParams medium;
     std::vector<float> occ;           // occluder triangles, 9 floats each (p0, p1, p2)
     float occ_albedo[3] = {0.5f, 0.5f, 0.5f};
+    std::vector<float> occ_alb;       // per triangle reflectance, 3 floats each (empty: occ_albedo for all)
+    const float* occ_albedo_of(int tri) const { return occ_alb.empty() ? occ_albedo : &occ_alb[3 * (size_t)tri]; }
     std::vector<uint32_t> occ_mat;    // per triangle ALVRL_MAT_* (empty: all diffuse)
     float occ_spec[3] = {1.0f, 1.0f, 1.0f};
     // dielectric triangles: m_eta = intIOR / extIOR (dielectric.cpp:149-158; bk7 / air, ior.h:43, 60)

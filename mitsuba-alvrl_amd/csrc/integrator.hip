@@ -276,6 +276,7 @@ struct alvrl_integrator {
         alvrl_medium_desc md = s.medium;
         chk(alvrl_set_medium(ctx, &md), "alvrl_set_medium");
         scene_desc.occluder_material = scene.occ_mat.empty() ? nullptr : scene.occ_mat.data();
+        scene_desc.occluder_albedos = scene.occ_alb.empty() ? nullptr : scene.occ_alb.data();
         scene_desc.emitter_tris = scene.emit.empty() ? nullptr : scene.emit.data();   // the owned copy
         scene_desc.n_emitter_tris = (uint32_t)(scene.emit.size() / 9);
         chains = scene.has_delta();
@@ -351,6 +352,7 @@ struct alvrl_integrator {
             tracer_desc.occluders = tracer_box.occ.empty() ? nullptr : tracer_box.occ.data();
             tracer_desc.n_occluders = tracer_box.n_occ();
             tracer_desc.occluder_material = tracer_box.occ_mat.empty() ? nullptr : tracer_box.occ_mat.data();
+            tracer_desc.occluder_albedos = tracer_box.occ_alb.empty() ? nullptr : tracer_box.occ_alb.data();
             tracer_desc.emitter_tris = tracer_box.emit.empty() ? nullptr : tracer_box.emit.data();
             tracer_desc.n_emitter_tris = (uint32_t)(tracer_box.emit.size() / 9);
             have_tracer = true;

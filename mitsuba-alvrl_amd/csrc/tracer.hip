@@ -49,6 +49,7 @@ struct TScene {
     int sigma_s_zero;
     alvrl::bvh::View bv;          // occluders (ntri == 0: none)
     float occ_albedo[3];
+    const float* occ_alb;         // per-triangle reflectance (3 floats, by triangle index), or nullptr
     // area emitter (SmokeBox::emit; nemit == 0: the point light): triangles,
     // the normalized area CDF (nemit + 1 entries), radiance and surface area
     const float* emit;
@@ -217,14 +218,15 @@ __device__ float box_hit(const TScene& sc, F3 o, F3 d, F3* n)   // first wall hi
 
 // Scene::rayIntersect over the walls and the occluders (host SmokeBox::first_hit):
 // t, normal, its.p (ray(t) on a wall, barycentric on a triangle), occluder or not
-__device__ float first_hit(const TScene& sc, F3 o, F3 d, float mint, F3* n, F3* p, bool* occ)
+// *tri: the occluder's index (-1: a wall)
+__device__ float first_hit(const TScene& sc, F3 o, F3 d, float mint, F3* n, F3* p, int* tri)
 {
     float best = box_hit(sc, o, d, n);
     int id = -1, slot = -1;
     float bu = 0.0f, bv = 0.0f;
     alvrl::bvh::closest(sc.bv, alvrl::bvh::mk(o.x, o.y, o.z), alvrl::bvh::mk(d.x, d.y, d.z), mint, &best, &id, &slot,
                         &bu, &bv);
-    *occ = id >= 0;
+    *tri = id;
     if (id < 0) {
         *p = add(o, mul(d, best));
         return best;
@@ -238,6 +240,12 @@ __device__ float first_hit(const TScene& sc, F3 o, F3 d, float mint, F3* n, F3* 
     if (!(fn.x == 0 && fn.y == 0 && fn.z == 0)) fn = mul(fn, 1.0f / l);
     *n = fn;
     return best;
+}
+
+// the diffuse reflectance of what first_hit hit: the occluder's own or the shared one, or the walls'
+__device__ __forceinline__ const float* albedo_of(const TScene& sc, int tri)
+{
+    return tri < 0 ? sc.albedo : sc.occ_alb ? sc.occ_alb + 3 * (size_t)tri : sc.occ_albedo;
 }
 
 // vrlVector::put + the current VRL (vrlTracer.h:56-89, VRL.h:148-158); counts,
@@ -319,8 +327,8 @@ __device__ void trace_particle(const TScene& sc, Stream& smp, bool short_vrls, i
     float mint = 1e-4f;   // Ray() default mint (Epsilon), then 0 after a medium and Epsilon after a surface
     while (!(thr[0] == 0 && thr[1] == 0 && thr[2] == 0) && (depth <= max_depth || max_depth < 0)) {
         F3 n, hp;
-        bool hit_occ;
-        const float its_t = first_hit(sc, o, dir, mint, &n, &hp, &hit_occ);
+        int hit_tri;
+        const float its_t = first_hit(sc, o, dir, mint, &n, &hp, &hit_tri);
         const bool its_valid = isfinite(its_t);
         // HomogeneousMedium::sampleDistance (homogeneous.cpp:275-352), balance
         float pdf_max = 0.0f;
@@ -358,7 +366,7 @@ __device__ void trace_particle(const TScene& sc, Stream& smp, bool short_vrls, i
             const float rpf = 1.0f / pf;
             for (int i = 0; i < 3; i++) thr[i] *= mtr[i] * rpf;
             const F3 p = hp;
-            const float* alb = hit_occ ? sc.occ_albedo : sc.albedo;
+            const float* alb = albedo_of(sc, hit_tri);
             F3 fs, ft;
             frame_of(n, &fs, &ft);
             const F3 mwi = f3(-dir.x, -dir.y, -dir.z);
@@ -548,12 +556,12 @@ __global__ void __launch_bounds__(256) k_eye_records(TCam c, TScene sc, const ui
                     c.left[1] * dc.x + c.nup[1] * dc.y + c.fwd[1] * dc.z,
                     c.left[2] * dc.x + c.nup[2] * dc.y + c.fwd[2] * dc.z);
     F3 nn, p;
-    bool occ;
-    const float t = first_hit(sc, O, D, mint, &nn, &p, &occ);
+    int tri;
+    const float t = first_hit(sc, O, D, mint, &nn, &p, &tri);
     uint32_t flags = 0;
     if (isfinite(t)) flags |= 1u | 2u;
     if (c.scat) flags |= 4u;
-    const float* a = occ ? sc.occ_albedo : sc.albedo;
+    const float* a = albedo_of(sc, tri);
     float* r = out + 20 * (size_t)i;   // alvrl_gather_rec: 20 words
     const float v[15] = {O.x, O.y, O.z, D.x, D.y, D.z, p.x, p.y, p.z, nn.x, nn.y, nn.z, a[0], a[1], a[2]};
 #pragma unroll
@@ -643,8 +651,8 @@ __device__ void volpath_li(const TScene& sc, const VParams& vp, VStream& smp, F3
     Li[0] = Li[1] = Li[2] = 0.0f;
     bool first_ok = false, second_ok = false, prev_diffuse = false, prev_volume = false;
     F3 n, hp;
-    bool hit_occ;
-    float its_t = first_hit(sc, o, dir, mint, &n, &hp, &hit_occ);
+    int hit_tri;
+    float its_t = first_hit(sc, o, dir, mint, &n, &hp, &hit_tri);
     float thr[3] = {1.0f, 1.0f, 1.0f};
     const float eta = 1.0f;
     int depth = 1;
@@ -698,7 +706,7 @@ __device__ void volpath_li(const TScene& sc, const VParams& vp, VStream& smp, F3
             const float px_ = smp.next(), py_ = smp.next();
             const F3 wo = uniform_sphere(px_, py_);
             o = mp; dir = wo;
-            its_t = first_hit(sc, o, dir, 0.0f, &n, &hp, &hit_occ);
+            its_t = first_hit(sc, o, dir, 0.0f, &n, &hp, &hit_tri);
             if (!indirect) break;
             prev_volume = true;
             prev_diffuse = false;
@@ -707,7 +715,7 @@ __device__ void volpath_li(const TScene& sc, const VParams& vp, VStream& smp, F3
             for (int i = 0; i < 3; i++) thr[i] *= mtr[i] * rpf;
             if (!isfinite(its_t)) break;
             if (depth >= vp.max_depth && vp.max_depth != -1) break;
-            const float* alb = hit_occ ? sc.occ_albedo : sc.albedo;
+            const float* alb = albedo_of(sc, hit_tri);
             const F3 p = hp;
             const float cos_wi = dot(f3(-dir.x, -dir.y, -dir.z), n);
             if (!vp.only_vrl || (first_ok && second_ok)) {   // :319-350 (ESmooth diffuse)
@@ -735,7 +743,7 @@ __device__ void volpath_li(const TScene& sc, const VParams& vp, VStream& smp, F3
             prev_diffuse = true;
             for (int i = 0; i < 3; i++) thr[i] *= alb[i];
             o = p; dir = wo;
-            its_t = first_hit(sc, o, dir, 1e-4f, &n, &hp, &hit_occ);
+            its_t = first_hit(sc, o, dir, 1e-4f, &n, &hp, &hit_tri);
             if (!indirect) break;
         }
         if (depth++ >= vp.rr_depth) {   // :437-446
@@ -792,6 +800,7 @@ TScene make_tscene(const alvrl::host::SmokeBox& box)
         sc.sigma_t[i] = box.medium.sigma_t[i];
         sc.occ_albedo[i] = box.occ_albedo[i];
     }
+    sc.occ_alb = nullptr;   // set by the caller that uploads box.occ_alb (upload_albedos)
     sc.w = box.medium.sampling_weight;
     sc.strategy = box.medium.strategy;
     sc.density = box.medium.density;
@@ -845,6 +854,16 @@ ALVRL_API void alvrl_volpath_default(alvrl_volpath_params* p)
     p->vrl_vol_to_surf = 1;
 }
 
+// the occluders' own reflectances on the device (SmokeBox::occ_alb), for TScene::occ_alb
+static bool upload_albedos(const alvrl::host::SmokeBox& box, DMem<float>& d, TScene& sc)
+{
+    if (box.occ_alb.empty()) return true;
+    if (d.alloc(box.occ_alb.size()) != hipSuccess) return false;
+    if (hipMemcpy(d.p, box.occ_alb.data(), box.occ_alb.size() * 4, hipMemcpyHostToDevice) != hipSuccess) return false;
+    sc.occ_alb = d.p;
+    return true;
+}
+
 ALVRL_API int alvrl_volpath_render(const alvrl_scene_desc* s, const alvrl_volpath_params* p, uint32_t seed,
                                    uint32_t pass, uint32_t spp, const uint32_t* d_pixel_ids, uint32_t n,
                                    float* d_out_rgb, void* stream)
@@ -867,6 +886,8 @@ ALVRL_API int alvrl_volpath_render(const alvrl_scene_desc* s, const alvrl_volpat
     const std::shared_ptr<DevBvh> bv = cached_bvh(box.occ, &be);
     if (!bv) return terr(ALVRL_ERR_HIP, "alvrl_volpath_render: BVH upload");
     sc.bv = bv->view;
+    DMem<float> d_alb;
+    if (!upload_albedos(box, d_alb, sc)) return terr(ALVRL_ERR_HIP, "alvrl_volpath_render: albedo upload");
     const TCam c = make_tcam(box, 1);
     VParams vp;
     vp.max_depth = p->max_depth; vp.rr_depth = p->rr_depth; vp.only_vrl = p->only_vrl_paths ? 1 : 0;
@@ -912,6 +933,8 @@ ALVRL_API int alvrl_scene_records_spp_gpu(const alvrl_scene_desc* s, int medium_
     const std::shared_ptr<DevBvh> bv = cached_bvh(box.occ, &be);
     if (!bv) return terr(ALVRL_ERR_HIP, "alvrl_scene_records_gpu: BVH upload");
     sc.bv = bv->view;
+    DMem<float> d_alb;
+    if (!upload_albedos(box, d_alb, sc)) return terr(ALVRL_ERR_HIP, "alvrl_scene_records_gpu: albedo upload");
     const TCam c = make_tcam(box, medium_scatters && !sc.sigma_s_zero ? 1 : 0);
     hipStream_t st = (hipStream_t)stream;
     const uint32_t total = n * spp;
@@ -940,6 +963,8 @@ ALVRL_API int alvrl_trace_vrls_gpu(const alvrl_scene_desc* s, uint32_t seed, uin
     const std::shared_ptr<DevBvh> bvh = cached_bvh(box.occ, &be);
     if (!bvh) return terr(ALVRL_ERR_HIP, "alvrl_trace_vrls_gpu: BVH upload");
     sc.bv = bvh->view;
+    DMem<float> d_alb;
+    if (!upload_albedos(box, d_alb, sc)) return terr(ALVRL_ERR_HIP, "alvrl_trace_vrls_gpu: albedo upload");
     const TArgs a{seed, pass, short_vrls, max_depth, rr_depth};
     *n = 0;
     if (target == 0) { *particles = 0; return ALVRL_OK; }

@@ -549,8 +549,7 @@ private:
         } else {
             describe(scene);
             alvrl_scene_desc sd = m_desc;
-            sd.occluders = m_tris.empty() ? NULL : &m_tris[0];
-            sd.occluder_material = m_mats.empty() ? NULL : &m_mats[0];
+            bindDesc(&sd, m_tris, m_mats, m_emit, m_albs);
             check(alvrl_integrator_preprocess(m_it, &sd), "alvrl_integrator_preprocess");
             for (size_t k = 0; k < m_more.size(); ++k)
                 check(alvrl_integrator_preprocess(m_more[k], &sd), "alvrl_integrator_preprocess");
@@ -624,7 +623,7 @@ private:
         m_desc.width = m_width; m_desc.height = m_height;
         if (!sensor->getMedium())
             Log(EError, "vrl (amd) frame mode needs the camera inside the medium (amdMode=records does not)");
-        describeTransport(scene, false, &m_desc, &m_tris, &m_mats, &m_emit);
+        describeTransport(scene, false, &m_desc, &m_tris, &m_mats, &m_emit, &m_albs);
     }
 
     /* The light transport the library's VRL tracer (and, in frame mode, its
@@ -635,7 +634,7 @@ private:
      * (alvrl_scene_ext::tracer) and refuses a scene it cannot express unless
      * a vrlFile supplies the VRLs. */
     void describeTransport(const Scene *scene, bool records, alvrl_scene_desc *d, std::vector<float> *tris,
-            std::vector<uint32_t> *mats, std::vector<float> *emit) {
+            std::vector<uint32_t> *mats, std::vector<float> *emit, std::vector<float> *albs) {
         const char *alt = records ? "records mode traces the VRLs over the scene's description; "
                                     "a vrlFile takes any scene" : "amdMode=records takes any";
         const char *mode = records ? "records" : "frame";
@@ -667,9 +666,12 @@ private:
             Log(EError, "vrl (amd) %s mode needs a point light or an area emitter (%s)", mode, alt);
         }
 
-        /* the container: the shape whose interior is the medium; its walls' diffuse reflectance */
-        tris->clear(); mats->clear();
-        bool haveBox = false, haveOccAlbedo = false, haveSpec = false, haveEta = false;
+        /* the container: the shape whose interior is the medium; its walls' diffuse reflectance.
+           Every other shape's triangles carry their own diffuse reflectance
+           (occluder_albedos): an emitter's mesh, to which Mitsuba gives an
+           all-absorbing SmoothDiffuse (shape.cpp:49-56), absorbs */
+        tris->clear(); mats->clear(); albs->clear();
+        bool haveBox = false, haveSpec = false, haveEta = false;
         const ref_vector<Shape> &shapes = scene->getShapes();
         for (size_t s = 0; s < shapes.size(); ++s) {
             const Shape *sh = shapes[s].get();
@@ -689,12 +691,8 @@ private:
                 if (const TriMesh *cm = dynamic_cast<const TriMesh *>(sh)) {
                     if (!onBoxFaces(cm, box)) {
                         const Spectrum rho = diffuseReflectance(sh, bsdf, mode, alt, false);
-                        if (haveOccAlbedo && !sameRgb(rho, d->occluder_albedo))
-                            Log(EError, "vrl (amd) %s mode: a mesh container and diffuse occluders with "
-                                "different reflectances (%s)", mode, alt);
-                        put3(d->occluder_albedo, rho);
-                        haveOccAlbedo = true;
                         appendTriangles(cm, ALVRL_MAT_DIFFUSE, tris, mats);
+                        appendAlbedo(rho, mats->size(), albs);
                     }
                 }
                 continue;
@@ -704,6 +702,7 @@ private:
                 Log(EError, "vrl (amd) %s mode: shape \"%s\" inside the medium is not a triangle mesh (%s)",
                     mode, sh->getName().c_str(), alt);
             uint32_t mat = ALVRL_MAT_DIFFUSE;
+            Spectrum rho(0.0f);   /* the diffuse reflectance (delta and null BSDFs: unused) */
             if (bsdf) {
                 const unsigned int type = bsdf->getType();
                 if (type & BSDF::ENull) {
@@ -725,27 +724,32 @@ private:
                     Log(EError, "vrl (amd) %s mode: BSDF of \"%s\" is neither diffuse, mirror, dielectric nor "
                         "null (%s)", mode, sh->getName().c_str(), alt);
                 } else {
-                    const Spectrum rho = diffuseReflectance(sh, bsdf, mode, alt);
-                    if (haveOccAlbedo && !sameRgb(rho, d->occluder_albedo))
-                        Log(EError, "vrl (amd) %s mode: diffuse occluders with different reflectances (%s)",
-                            mode, alt);
-                    put3(d->occluder_albedo, rho);
-                    haveOccAlbedo = true;
+                    rho = diffuseReflectance(sh, bsdf, mode, alt);
                 }
             }
             appendTriangles(mesh, mat, tris, mats);
+            appendAlbedo(rho, mats->size(), albs);
         }
         if (!haveBox)
             Log(EError, "vrl (amd) needs a shape that contains the medium (its interior)");
-        bindDesc(d, *tris, *mats, *emit);
+        bindDesc(d, *tris, *mats, *emit, *albs);
+    }
+
+    /* the reflectance of the triangles appended last, up to n triangles in all */
+    static void appendAlbedo(const Spectrum &rho, size_t n, std::vector<float> *albs) {
+        float c[3];
+        put3(c, rho);
+        while (albs->size() < 3 * n)
+            albs->insert(albs->end(), c, c + 3);
     }
 
     /* point a descriptor at the arrays that hold its triangles */
     static void bindDesc(alvrl_scene_desc *d, const std::vector<float> &tris, const std::vector<uint32_t> &mats,
-            const std::vector<float> &emit) {
+            const std::vector<float> &emit, const std::vector<float> &albs) {
         d->occluders = tris.empty() ? NULL : &tris[0];
         d->occluder_material = mats.empty() ? NULL : &mats[0];
         d->n_occluders = (uint32_t) mats.size();
+        d->occluder_albedos = albs.empty() ? NULL : &albs[0];
         d->emitter_tris = emit.empty() ? NULL : &emit[0];
         d->n_emitter_tris = (uint32_t) (emit.size() / 9);
     }
@@ -784,12 +788,6 @@ private:
                     sh->getName().c_str(), alt);
         }
         return first;
-    }
-
-    static bool sameRgb(const Spectrum &s, const float *rgb) {
-        float v[3];
-        put3(v, s);
-        return v[0] == rgb[0] && v[1] == rgb[1] && v[2] == rgb[2];
     }
 
     static void appendTriangles(const TriMesh *mesh, uint32_t mat, std::vector<float> *tris,
@@ -925,7 +923,7 @@ private:
            library, every pass): needed unless a vrlFile supplies the VRLs */
         if (m_vrlFile.empty()) {
             alvrl_scene_default(&m_tdesc, 1, 1);
-            describeTransport(scene, true, &m_tdesc, &m_ttris, &m_tmats, &m_temit);
+            describeTransport(scene, true, &m_tdesc, &m_ttris, &m_tmats, &m_temit, &m_talbs);
             e.tracer = &m_tdesc;
         }
         check(alvrl_integrator_preprocess_ext(m_it, &e), "alvrl_integrator_preprocess_ext");
@@ -1297,6 +1295,7 @@ private:
     std::vector<float> m_tris, m_ttris;
     std::vector<uint32_t> m_mats, m_tmats;
     std::vector<float> m_emit, m_temit;   /* the area emitter's triangles */
+    std::vector<float> m_albs, m_talbs;   /* each triangle's diffuse reflectance */
     std::vector<uint32_t> m_p2s;   // the pass's slice of every pixel (column-major); empty: brute force
     int m_width = 0, m_height = 0;
     float *m_fb = NULL;

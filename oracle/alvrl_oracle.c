@@ -977,6 +977,13 @@ void alvrl_o_pixel_sample(uint32_t seed, uint32_t pass, int x, int y, int width,
     *py = (float)y + draw(seed, pass, ALVRL_O_DOM_PIXEL, pixel, sample, 0u, 1u);
 }
 
+/* The diffuse reflectance of occluder tri: its own (occ_albedos) or the
+ * shared occ_albedo */
+static const float *occ_alb(const alvrl_o_scene *s, int tri)
+{
+    return s->occ_albedos ? s->occ_albedos + 3 * (size_t)tri : s->occ_albedo;
+}
+
 /* The record of sensor sample j of pixel (x, y); its depth word carries the
  * sample index in bits 16-31 (the gather's streams are keyed by it). */
 void alvrl_o_make_record_s(const alvrl_o_scene *s, int medium_scatters, int x, int y, uint32_t seed, uint32_t pass,
@@ -990,7 +997,7 @@ void alvrl_o_make_record_s(const alvrl_o_scene *s, int medium_scatters, int x, i
     float t = first_hit(s, O, D, camera_mint(s, px, py), &n, &p, &tri);
     static const float zero3[3] = { 0.0f, 0.0f, 0.0f };
     uint32_t mt = (tri >= 0 && s->occ_mat) ? s->occ_mat[tri] : ALVRL_O_MAT_DIFFUSE;
-    const float *alb = mt != ALVRL_O_MAT_DIFFUSE ? zero3 : (tri >= 0 ? s->occ_albedo : s->albedo);
+    const float *alb = mt != ALVRL_O_MAT_DIFFUSE ? zero3 : (tri >= 0 ? occ_alb(s, tri) : s->albedo);
     uint32_t flags = 0;
     if (isfinite(t)) flags |= ALVRL_O_FLAG_HIT | (mt == ALVRL_O_MAT_DIFFUSE ? ALVRL_O_FLAG_SMOOTH : ALVRL_O_FLAG_DELTA);
     if (medium_scatters) flags |= ALVRL_O_FLAG_MEDIUM;
@@ -1073,7 +1080,7 @@ static void chain_node(chain_ctx *cx, v3 O, v3 D, float mint, const float weight
     uint32_t mt = mat_of(s, tri);
     uint32_t flags = ALVRL_O_FLAG_HIT | (mt == ALVRL_O_MAT_DIFFUSE ? ALVRL_O_FLAG_SMOOTH : ALVRL_O_FLAG_DELTA) |
                      (cx->medium_scatters ? ALVRL_O_FLAG_MEDIUM : 0u);
-    const float *alb = tri >= 0 ? s->occ_albedo : s->albedo;
+    const float *alb = tri >= 0 ? occ_alb(s, tri) : s->albedo;
     float *rec = cx->recs + (size_t)cx->nrec * ALVRL_O_REC_WORDS;
     rec[0] = O.x; rec[1] = O.y; rec[2] = O.z;
     rec[3] = D.x; rec[4] = D.y; rec[5] = D.z;
@@ -1369,7 +1376,7 @@ static void trace_particle(const alvrl_o_scene *s, const alvrl_o_medium *m, cons
             float rpf = 1.0f / pf;
             for (int i = 0; i < 3; i++) thr[i] *= mtr[i] * rpf;
             v3 p = hp;
-            const float *alb = tri >= 0 ? s->occ_albedo : s->albedo;
+            const float *alb = tri >= 0 ? occ_alb(s, tri) : s->albedo;
             v3 fs, ft;
             frame_of(n, &fs, &ft);
             v3 mwi = neg(dir);
@@ -1546,7 +1553,7 @@ static void vp_li(const alvrl_o_scene *s, const alvrl_o_medium *m, const alvrl_o
             for (int i = 0; i < 3; i++) thr[i] *= mtr[i] * rpf;
             if (!isfinite(its_t)) break;
             if (depth >= vp->max_depth && vp->max_depth != -1) break;
-            const float *alb = tri >= 0 ? s->occ_albedo : s->albedo;
+            const float *alb = tri >= 0 ? occ_alb(s, tri) : s->albedo;
             v3 p = hp;
             float cos_wi = dot(neg(dir), n);
             if (!vp->only_vrl_paths || (first_ok && second_ok)) {   /* :319-350 */

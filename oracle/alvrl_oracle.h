@@ -161,6 +161,10 @@ typedef struct {
     const float *emit;
     uint32_t nemit;
     float emit_radiance[3];
+    /* per-occluder diffuse reflectance, 3 floats each (NULL: occ_albedo for
+     * all): every shape's own smooth diffuse BSDF -- e.g. an emitter's mesh,
+     * which Mitsuba gives an all-absorbing one (shape.cpp:49-56) */
+    const float *occ_albedos;
 } alvrl_o_scene;
 #define ALVRL_O_MAT_DIFFUSE 0u   /* SmoothDiffuse, one-sided (diffuse.cpp) */
 #define ALVRL_O_MAT_MIRROR 1u    /* SmoothConductor, material none (conductor.cpp:254-268) */

@@ -53,7 +53,8 @@ class Scene(C.Structure):
                 ("light_pos", C.c_float * 3), ("light_intensity", C.c_float * 3),
                 ("occ", C.POINTER(C.c_float)), ("nocc", C.c_uint32), ("occ_albedo", C.c_float * 3),
                 ("occ_mat", C.POINTER(C.c_uint32)), ("occ_spec", C.c_float * 3), ("occ_eta", C.c_float),
-                ("emit", C.POINTER(C.c_float)), ("nemit", C.c_uint32), ("emit_radiance", C.c_float * 3)]
+                ("emit", C.POINTER(C.c_float)), ("nemit", C.c_uint32), ("emit_radiance", C.c_float * 3),
+                ("occ_albedos", C.POINTER(C.c_float))]
 
 
 MAT_DIFFUSE, MAT_MIRROR, MAT_NULL, MAT_DIELECTRIC = 0, 1, 2, 3
@@ -71,11 +72,12 @@ def set_area_emitter(scene, tris, radiance):
     return scene
 
 
-def set_occluders(obj, tris, albedo=None, material=None, specular=None, eta=None):
+def set_occluders(obj, tris, albedo=None, material=None, specular=None, eta=None, albedos=None):
     """Occluder triangles ((n, 9) float32) on a Scene (hit by eye rays and
     particles, occ_albedo) or a Params (blocking the gather's connections);
     material: None (all diffuse) or one MAT_* per triangle; specular: the
-    mirrors' reflectance (Scene).  The arrays are kept alive on the object."""
+    mirrors' reflectance (Scene); albedos: (n, 3) per-triangle reflectances
+    (Scene; replaces occ_albedo).  The arrays are kept alive on the object."""
     arr = np.ascontiguousarray(np.asarray(tris, np.float32).reshape(-1, 9))
     obj._occ_keep = arr
     obj.occ = arr.ctypes.data_as(C.POINTER(C.c_float)) if len(arr) else None
@@ -83,6 +85,10 @@ def set_occluders(obj, tris, albedo=None, material=None, specular=None, eta=None
     if albedo is not None:
         for i in range(3):
             obj.occ_albedo[i] = float(albedo[i])
+    if albedos is not None:
+        alb = np.ascontiguousarray(np.asarray(albedos, np.float32).reshape(len(arr), 3))
+        obj._alb_keep = alb
+        obj.occ_albedos = alb.ctypes.data_as(C.POINTER(C.c_float))
     if material is not None:
         mat = np.ascontiguousarray(np.broadcast_to(np.asarray(material, np.uint32), (len(arr),)))
         obj._mat_keep = mat

@@ -86,6 +86,27 @@ def test_gpu_tracer_occluders(gpu_ok):
         assert np.array_equal(dev.view(np.uint32), host.view(np.uint32)), (target, short)
 
 
+def test_gpu_occluder_albedos(gpu_ok):
+    """Per-triangle reflectances (alvrl_scene_desc.occluder_albedos) on the
+    device: the eye-record kernel and the GPU tracer equal the host (and so
+    the oracle, test_occluders.py) bit for bit, with the BVH's triangle order
+    mapped back to each triangle's own reflectance."""
+    import alvrl
+    from test_occluders import per_triangle_albedos
+    tris = scene_mesh(alvrl, big=True)
+    alb = per_triangle_albedos(len(tris))
+    alb[30:] = np.random.default_rng(5).uniform(0.0, 1.0, (len(tris) - 30, 3)).astype(np.float32)
+    s = alvrl.scene_set_occluders(alvrl.scene_default(256, 192), tris, ALB, albedos=alb)
+    host = alvrl.scene_records(s)
+    dev = alvrl.scene_records_gpu(s).cpu().numpy()
+    assert np.array_equal(dev.view(np.uint32), host.view(np.uint32))
+    s16 = alvrl.scene_set_occluders(alvrl.scene_default(16, 16), tris, ALB, albedos=alb)
+    for target, short in ((20000, True), (6000, False)):
+        d, pcd = alvrl.trace_vrls_gpu(s16, target, seed=SEED_VRL, short_vrls=short)
+        h, pch = alvrl.trace_vrls(s16, target, seed=SEED_VRL, short_vrls=short)
+        assert pcd == pch and np.array_equal(d.view(np.uint32), h.view(np.uint32)), (target, short)
+
+
 def test_gather_brute_occluders(oracle, gpu_ok):
     """Brute gather with shadow tests vs the oracle's (evalTransmittance with
     the occluders), 64x48 records x 2000 VRLs traced in the occluded scene;

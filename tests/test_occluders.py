@@ -70,3 +70,37 @@ def test_occluder_tracer_matches_oracle(alvrl, oracle):
         assert on_box.sum() > 0
         plain, _ = alvrl.trace_vrls(alvrl.scene_default(16, 16), target, seed=0x5EED0001, short_vrls=short)
         assert plain.shape != mine.shape or not np.array_equal(plain, mine)
+
+
+def per_triangle_albedos(n):
+    """Each occluder its own reflectance: the first box black (an emitter's
+    all-absorbing mesh, shape.cpp:49-56), the plate and the last triangle
+    coloured."""
+    alb = np.zeros((n, 3), np.float32)
+    alb[12:24] = (0.2, 0.6, 0.3)
+    alb[24:] = (0.9, 0.1, 0.5)
+    return alb
+
+
+def test_occluder_albedos_match_oracle(alvrl, oracle):
+    """alvrl_scene_desc.occluder_albedos (per-triangle reflectances): the
+    records and the tracer equal the oracle's bit for bit, a black occluder
+    ends the particles that reach it, and the records carry each triangle's
+    own reflectance."""
+    tris = occluder_mesh(alvrl)
+    alb = per_triangle_albedos(len(tris))
+    s = alvrl.scene_set_occluders(alvrl.scene_default(96, 64), tris, ALB, albedos=alb)
+    o = set_occluders(oracle.scene(96, 64), tris, ALB, albedos=alb)
+    mine = alvrl.scene_records(s)
+    ref = oracle.records(o)
+    assert np.array_equal(mine.view(np.uint32), ref.view(np.uint32))
+    for a in (alb[0], alb[12], alb[24]):
+        assert np.all(mine[:, 12:15] == a, axis=1).sum() > 50
+    s16 = alvrl.scene_set_occluders(alvrl.scene_default(16, 16), tris, ALB, albedos=alb)
+    o16 = set_occluders(oracle.scene(16, 16), tris, ALB, albedos=alb)
+    v, pc = alvrl.trace_vrls(s16, 900, seed=0x5EED0001)
+    rv, rpc = oracle.trace(o16, oracle.medium(), 900, seed=0x5EED0001)
+    assert pc == rpc and np.array_equal(v.view(np.uint32), rv.view(np.uint32))
+    shared, _ = alvrl.trace_vrls(alvrl.scene_set_occluders(alvrl.scene_default(16, 16), tris, ALB), 900,
+                                 seed=0x5EED0001)
+    assert shared.shape != v.shape or not np.array_equal(shared, v)
