@@ -264,7 +264,8 @@ ALVRL_API int alvrl_detmath_eval(int fn, const float *d_in, float *d_out, uint32
  * (end <= 2^32), on the current device, synchronous: *mismatches = the number
  * of inputs whose results differ in any bit, first[0 .. min(nfirst, 16)) =
  * some of them (0xFFFFFFFF past the last).  fn 0 exp, 2 atan, 3 tan,
- * 4 asinh, 5 sinh, 6 sqrt (the fast square root against IEEE sqrtf). */
+ * 4 asinh, 5 sinh, 6 sqrt (the fast square root against IEEE sqrtf), 7 rcp
+ * (the fast reciprocal against IEEE 1.0f / x). */
 ALVRL_API int alvrl_detmath_exhaustive(int fn, uint64_t begin, uint64_t end, uint64_t *mismatches,
                                        uint32_t *first, uint32_t nfirst);
 

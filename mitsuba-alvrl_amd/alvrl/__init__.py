@@ -166,7 +166,7 @@ def detmath_exhaustive(fn: str, begin: int = 0, end: int = 1 << 32):
     differ, some of those inputs as uint32 bit patterns)."""
     mism = C.c_uint64(0)
     first = (C.c_uint32 * 16)()
-    _check(lib().alvrl_detmath_exhaustive(6 if fn == "sqrt" else DETMATH_FNS.index(fn), int(begin), int(end), C.byref(mism), first, 16))
+    _check(lib().alvrl_detmath_exhaustive({"sqrt": 6, "rcp": 7}[fn] if fn in ("sqrt", "rcp") else DETMATH_FNS.index(fn), int(begin), int(end), C.byref(mism), first, 16))
     return int(mism.value), [int(x) for x in first if x != 0xFFFFFFFF]
 
 

@@ -670,8 +670,8 @@ ALVRL_API int alvrl_detmath_div_check(uint64_t n, uint64_t seed, uint64_t* misma
 ALVRL_API int alvrl_detmath_exhaustive(int fn, uint64_t begin, uint64_t end, uint64_t* mismatches,
                                        uint32_t* first, uint32_t nfirst)
 {
-    if (fn != 0 && (fn < 2 || fn > 6))
-        return fail(ALVRL_ERR_INVALID, "alvrl_detmath_exhaustive: fn must be 0 or in [2, 6]");
+    if (fn != 0 && (fn < 2 || fn > 7))
+        return fail(ALVRL_ERR_INVALID, "alvrl_detmath_exhaustive: fn must be 0 or in [2, 7]");
     if (end > (1ull << 32) || begin > end) return fail(ALVRL_ERR_INVALID, "alvrl_detmath_exhaustive: bad range");
     if (!mismatches) return fail(ALVRL_ERR_INVALID, "alvrl_detmath_exhaustive: null output");
     unsigned long long* d_out = nullptr;

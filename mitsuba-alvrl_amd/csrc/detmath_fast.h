@@ -373,6 +373,30 @@ FX_FN float fx_sqrtf_r(float x, bool& slow)
     return r;
 }
 
+// 1 / b in IEEE single precision, correctly rounded: v_rcp_f32 and two
+// residual corrections y += y * (1 - b y) (Markstein), for |b| in
+// [2^-40, 2^40] (flag otherwise).  Checked against IEEE 1.0f / b on every
+// float (alvrl_detmath_exhaustive fn 7).
+FX_FN float fx_rcpf_r(float b, bool& slow)
+{
+    float y = __builtin_amdgcn_rcpf(b);
+    float e = __builtin_fmaf(-b, y, 1.0f);
+    y = __builtin_fmaf(e, y, y);
+    e = __builtin_fmaf(-b, y, 1.0f);
+    y = __builtin_fmaf(e, y, y);
+    const uint32_t eb = __float_as_uint(b) & 0x7FFFFFFFu;
+    slow |= (eb - 0x2B800000u) > (0x53800000u - 0x2B800000u);
+    return y;
+}
+
+FX_FN float fx_rcpf(float b)
+{
+    bool slow = false;
+    float y = fx_rcpf_r(b, slow);
+    if (slow) y = 1.0f / b;
+    return y;
+}
+
 FX_FN float fx_divf(float a, float b)
 {
     bool slow = false;

@@ -80,18 +80,20 @@ struct Tx {
 #ifdef ALVRL_STRICT_STUB_DIV   // developer timing variant: results invalid
     static __device__ __forceinline__ float sqrt(float x, bool& s) { return __builtin_amdgcn_sqrtf(x); }
     static __device__ __forceinline__ float div(float a, float b, bool& s) { return a * __builtin_amdgcn_rcpf(b); }
+    static __device__ __forceinline__ float rcp(float b, bool& s) { return __builtin_amdgcn_rcpf(b); }
 #else
     // IEEE sqrt and division: their cores without the scaling (flag outside
     // the range where the scaling is the identity), or the compiler's expansion
     static __device__ __forceinline__ float sqrt(float x, bool& s) { return FAST ? fx_sqrtf_r(x, s) : sqrtf(x); }
     static __device__ __forceinline__ float div(float a, float b, bool& s) { return FAST ? fx_divf_r(a, b, s) : a / b; }
+    static __device__ __forceinline__ float rcp(float b, bool& s) { return FAST ? fx_rcpf_r(b, s) : 1.0f / b; }
 #endif
 };
 template <bool FAST> __device__ __forceinline__ float lenT(V3 a, bool& s) { return Tx<FAST>::sqrt(len2(a), s); }
 template <bool FAST> __device__ __forceinline__ float distT(V3 a, V3 b, bool& s) { return lenT<FAST>(sub(a, b), s); }
 template <bool FAST> __device__ __forceinline__ V3 nrmT(V3 a, bool& s)
 {
-    const float r = Tx<FAST>::div(1.0f, lenT<FAST>(a, s), s);
+    const float r = Tx<FAST>::rcp(lenT<FAST>(a, s), s);
     return scl(a, r);
 }
 
@@ -197,7 +199,7 @@ __device__ __forceinline__ void shadow_transmittance(const DevParams& P, V3 p1, 
     if (!OCC) return;
     if (P.occ.ntri == 0 || !(remaining > 0)) return;
     const V3 d = sub(p2, p1);
-    const V3 dn = scl(d, Tx<FAST>::div(1.0f, remaining, slow));
+    const V3 dn = scl(d, Tx<FAST>::rcp(remaining, slow));
     const float mint = p1_surface ? 1e-4f : 0.0f;
     const float maxt = remaining * 1.0f;
     if (bvh::occluded(P.occ, bvh::mk(p1.x, p1.y, p1.z), bvh::mk(dn.x, dn.y, dn.z), mint, maxt))
@@ -331,7 +333,7 @@ __device__ __forceinline__ float novak_sample(const Novak& n, V3 S, V3 End, V3 S
     if (n.mode == 1) { *V = add(S, scl(sub(End, S), uniform)); return invlen; }
     float newV = n.h * Tx<FAST>::sinh(n.A0 + (uniform * (n.A1 - n.A0)), slow);
     newV = Tx<FAST>::div(newV, n.sinTheta, slow);
-    const float result = Tx<FAST>::div(1.0f, Tx<FAST>::sqrt(n.h * n.h + newV * newV * n.sinTheta * n.sinTheta, slow), slow);
+    const float result = Tx<FAST>::rcp(Tx<FAST>::sqrt(n.h * n.h + newV * newV * n.sinTheta * n.sinTheta, slow), slow);
     newV += n.dVhS;
     *V = add(S, scl(SE, newV));
     return Tx<FAST>::div(result, n.denom, slow);
@@ -413,11 +415,11 @@ __device__ __forceinline__ void integrate_R(const DevParams& P, const Row& w, co
             if (!(tuv[0] == 0 && tuv[1] == 0 && tuv[2] == 0)) {
                 medium_eval<FAST>(P, distT<FAST>(w.E, U, slow), teu, &pf_eu, slow);
                 medium_eval<FAST>(P, distT<FAST>(S, V, slow), tsv, &pf_sv, slow);
-                const float rpdf = Tx<FAST>::div(1.0f, pdf, slow);
-                const float rd2 = Tx<FAST>::div(1.0f, dist2(U, V), slow);
+                const float rpdf = Tx<FAST>::rcp(pdf, slow);
+                const float rd2 = Tx<FAST>::rcp(dist2(U, V), slow);
                 const float phU = phase_eval<FAST>(P, neg(VU), neg(EU), slow);
                 const float phV = phase_eval<FAST>(P, neg(SV), VU, slow);
-                const float rpf = Tx<FAST>::div(1.0f, pf_sv, slow);
+                const float rpf = Tx<FAST>::rcp(pf_sv, slow);
                 float c[3];
                 for (int i = 0; i < 3; i++) {
                     c[i] = w.wt[i];
@@ -461,9 +463,9 @@ __device__ __forceinline__ void integrate_R(const DevParams& P, const Row& w, co
                 if (!(w.cos_wi <= 0 || cos_wo <= 0))
                     for (int i = 0; i < 3; i++) f[i] = w.alb[i] * (kInvPi * cos_wo);
                 const float phV = phase_eval<FAST>(P, neg(SV), VU, slow);
-                const float rpdf = Tx<FAST>::div(1.0f, pdf, slow);
-                const float rd2 = Tx<FAST>::div(1.0f, dist2(w.U, V), slow);
-                const float rpf = Tx<FAST>::div(1.0f, pf_sv, slow);
+                const float rpdf = Tx<FAST>::rcp(pdf, slow);
+                const float rd2 = Tx<FAST>::rcp(dist2(w.U, V), slow);
+                const float rpf = Tx<FAST>::rcp(pf_sv, slow);
                 float c[3];
                 for (int i = 0; i < 3; i++) {
                     c[i] = w.wt[i];
@@ -659,6 +661,7 @@ __device__ __forceinline__ void fx_dm(float x, float* f, float* d)
     else if (FN == 3) { *f = fx_tanf(x); *d = dm_tanf(x); }
     else if (FN == 4) { *f = fx_asinhf(x); *d = dm_asinhf(x); }
     else if (FN == 6) { *f = fx_sqrtf(x); *d = sqrtf(x); }
+    else if (FN == 7) { *f = fx_rcpf(x); *d = 1.0f / x; }
     else { *f = fx_sinhf(x); *d = dm_sinhf(x); }
 }
 
@@ -858,6 +861,7 @@ hipError_t launch_detmath_exhaustive(int fn, uint64_t begin, uint64_t end, unsig
     case 4: hipLaunchKernelGGL(strict::k_detmath_exhaustive<4>, grid, block, 0, s, begin, end, out, first); break;
     case 5: hipLaunchKernelGGL(strict::k_detmath_exhaustive<5>, grid, block, 0, s, begin, end, out, first); break;
     case 6: hipLaunchKernelGGL(strict::k_detmath_exhaustive<6>, grid, block, 0, s, begin, end, out, first); break;
+    case 7: hipLaunchKernelGGL(strict::k_detmath_exhaustive<7>, grid, block, 0, s, begin, end, out, first); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -65,13 +65,14 @@ def test_detmath_device_matches_host(oracle, gpu_ok):
         assert same.all(), (fn, x[~same][:4], dev[~same][:4], host[~same][:4])
 
 
-@pytest.mark.parametrize("fn", ["exp", "atan", "tan", "asinh", "sinh", "sqrt"])
+@pytest.mark.parametrize("fn", ["exp", "atan", "tan", "asinh", "sinh", "sqrt", "rcp"])
 def test_detmath_fast_exhaustive(fn, gpu_ok):
     """csrc/detmath_fast.h (the strict R build's transcendentals: a short f64
     evaluation and Ziv's rounding test, detmath.h when the rounding is in
-    doubt; its square root: v_sqrt_f32 and the one-ulp correction, IEEE sqrtf
-    outside the range where that is exact) returns detmath.h's float -- IEEE
-    sqrtf's for sqrt -- for EVERY one of the 2^32 float inputs."""
+    doubt; its square root: v_sqrt_f32 and the one-ulp correction; its reciprocal:
+    v_rcp_f32 and two Markstein corrections; IEEE sqrtf / 1.0f / x outside the
+    ranges where those are exact) returns detmath.h's float -- IEEE sqrtf's
+    and 1.0f / x's for sqrt and rcp -- for EVERY one of the 2^32 float inputs."""
     import time
     import alvrl
     t0 = time.perf_counter()
