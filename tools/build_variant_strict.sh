@@ -9,5 +9,5 @@ mkdir -p variants
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -Wno-unused-value \
   -I../include -Icsrc -ffp-contract=off -mllvm -disable-machine-licm "$@" -c csrc/rbuild_strict.hip -o /tmp/rbs_$name.o
 objs=$(ls build/*.o | grep -v '/rbuild_strict.o$' | grep -v '/asan_')
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o variants/libalvrl_$name.so /tmp/rbs_$name.o $objs -lpthread
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o variants/libalvrl_$name.so /tmp/rbs_$name.o $objs -lpthread -L/opt/rocm/lib -Wl,-rpath,/opt/rocm/lib -lrccl
 echo "variants/libalvrl_$name.so"
