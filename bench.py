@@ -239,7 +239,9 @@ def main():
     kind = "clustered" if clustered else "brute"
     # committed counter files count only if they were taken on the library
     # this run loaded (their build_id, tools/pmc_summary.py / pmc_valu.py);
-    # a file from another tree reports traffic / valu null
+    # a file from another tree reports traffic / valu null.  The traffic
+    # records are one GPU's launches (tools/pmc_traffic.sh runs N = 1): a rank
+    # of N > 1 launches over its share, so its traffic is reported null
     my_id = alvrl.build_info()["build_id"]
     counters = {"pmc_json": os.path.relpath(args.pmc_json, REPO),
                 "valu_json": os.path.relpath(args.valu_json.format(cfg=args.config), REPO),
@@ -249,7 +251,7 @@ def main():
         with open(args.pmc_json) as f:
             pm = json.load(f)
         for rec in (pm if isinstance(pm, list) else [pm]):
-            if rec.get("config") == args.config and rec.get("build_id") == my_id:
+            if rec.get("config") == args.config and rec.get("build_id") == my_id and world == 1:
                 pmc[rec.get("kernel_key", "render")] = rec.get("hbm_bytes_per_launch")
                 counters["pmc_matches"] = True
     except (OSError, ValueError):
