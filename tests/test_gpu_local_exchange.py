@@ -16,6 +16,7 @@ pytestmark = pytest.mark.gpu
 
 @pytest.mark.parametrize("world,props", [(2, "targetNumSlices=40"),
                                          (3, "targetNumSlices=30;neighbourCount=2;neighbourWeight=0.5"),
+                                         (3, "targetNumSlices=30;sliceSharding=roundrobin"),
                                          (2, "localRefinement=false;globalCluster=false")])
 def test_local_exchange_integrators(gpu_ok, world, props):
     import torch
@@ -64,8 +65,14 @@ def test_local_exchange_integrators(gpu_ok, world, props):
             cl = its[r].clusters()
             for k in ref_cl:
                 assert np.array_equal(cl[k].view(np.uint32), ref_cl[k].view(np.uint32)), (r, k)
-        # every slice refined once over the integrators
+        # every slice refined once over the integrators: the ranks' shares
+        # (longest processing time first by default, s mod N with
+        # sliceSharding=roundrobin) partition the slices
         assert sum(it.stats()["slices_local"] for it in its) == ref_st["slices"]
+        shares = [list(it.local_slices()) for it in its]
+        assert sorted(s_ for sh in shares for s_ in sh) == list(range(ref_st["slices"])), shares
+        if "roundrobin" in props:
+            assert all(s_ % world == r for r, sh in enumerate(shares) for s_ in sh), shares
     for it in its:
         it.close()
     g.close()

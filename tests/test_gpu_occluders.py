@@ -192,3 +192,55 @@ def test_integrator_occluders_matches_oracle(oracle, gpu_ok):
     assert np.array_equal(ocl["weights"].view(np.uint32), icl["weights"].view(np.uint32))
     assert np.isfinite(fb.cpu().numpy()).all()
     it.close()
+
+
+def test_default_pipeline_occluder_albedos_vs_oracle_pipeline(oracle, gpu_ok):
+    """The default pipeline (strict R build) over an occluded scene whose
+    triangles each carry their own reflectance, against the oracle's own
+    pipeline on the same scene: VRLs traced by the GPU tracer equal the
+    oracle's, then slices, representatives, R of the representative records
+    (shadow tests through the BVH, each record's own reflectance in vol->surf)
+    and the cluster lists, bit for bit; the frame within the gather tolerance."""
+    import torch
+    import alvrl
+    from oracle import Prep
+    from test_gpu_strict import _assert_bits
+    from test_occluders import per_triangle_albedos
+    w, h = 64, 48
+    tris = scene_mesh(alvrl, big=True)
+    alb = per_triangle_albedos(len(tris))
+    alb[30:] = np.random.default_rng(7).uniform(0.05, 0.95, (len(tris) - 30, 3)).astype(np.float32)
+    s = alvrl.scene_set_occluders(alvrl.scene_default(w, h), tris, ALB, albedos=alb)
+    o = set_occluders(oracle.scene(w, h), tris, ALB, albedos=alb)
+    m = oracle.medium()
+    vrls, pc = oracle.trace(o, m, 1500, seed=SEED_VRL)
+    gv, gpc = alvrl.trace_vrls_gpu(s, 1500, seed=SEED_VRL)
+    assert gpc == pc and np.array_equal(gv.view(np.uint32), vrls.view(np.uint32)), "GPU tracer vs oracle"
+    it = alvrl.Integrator(f"targetNumSlices=12;seed={SEED_RNG}", device=0)
+    it.set_vrls(vrls, pc)
+    it.preprocess(s)
+    it.prepass(0)
+    fb = torch.zeros(w * h * 3, dtype=torch.float32, device="cuda")
+    it.render(fb)
+    torch.cuda.synchronize()
+    prep = Prep(oracle, oracle.prep_params(seed=SEED_RNG, pass_=0, target_num_slices=12))
+    p2s = prep.build_slices(o)
+    assert np.array_equal(p2s, it.slices()), "slices"
+    off, pix, _, _ = prep.sample_slice_mapping(64.0, w * h)
+    ioff, ipix = it.reps()
+    assert np.array_equal(off, ioff) and np.array_equal(pix, ipix), "representatives"
+    rep_ids = ((pix % h) * w + pix // h).astype(np.uint32)
+    recs = oracle.records(o)
+    P = set_occluders(oracle.params(m, seed=SEED_RNG, pass_=0), tris)
+    _, R, _ = oracle.gather_brute(P, recs[rep_ids], vrls, pc, rec_ids=rep_ids, domain=2, want_R=True)
+    _assert_bits(it.R().transpose(1, 0, 2), R, "occluded R with per-triangle reflectances (strict)")
+    ocl, icl = prep.build_clusters(np.ascontiguousarray(R.transpose(1, 0, 2))), it.clusters()
+    for k in ("slice_off", "reps", "weights"):
+        a, b = ocl[k], icl[k]
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), k
+    pid = np.arange(w * h, dtype=np.uint32)
+    sl = p2s[(pid % w) * h + pid // w]
+    img, _ = oracle.gather_clustered(P, recs, sl, vrls, pc, ocl["slice_off"], ocl["reps"], ocl["weights"],
+                                     ocl["fb_reps"], ocl["fb_weights"], rec_ids=pid)
+    _assert_close(fb.view(h * w, 3).cpu().numpy(), img, "occluded frame, per-triangle reflectances")
+    it.close()
