@@ -46,8 +46,8 @@
 
 // Half-width of the ambiguous band around the float halfway point, in units
 // of the double's last place: 2^13 ulp of double is at least 2^-40 relative,
-// 16x the largest fast-path error bound (2^-44: the exp table's fit and
-// reduction, the other fits' <= 2^-43.5, plus evaluation rounding) and well
+// 5x the largest fast-path error bound (2^-42.5: exp's Taylor q, reduction
+// and table; the other fits' <= 2^-43.5, plus evaluation rounding) and well
 // above detmath.h's own error (~2 ulp).  A lane lands in the band once in
 // 2^15 calls (~44 calls per R entry: 0.13 % of the entries go to the fix-up
 // queue, whose re-evaluation costs well under 1 % of the build).
@@ -61,6 +61,59 @@ FX_FN bool fx_near_half(double y)
 {
     const uint32_t lo = (uint32_t)__double_as_longlong(y) & 0x1FFFFFFFu;
     return (lo - (0x10000000u - kFxBand)) < 2u * kFxBand;
+}
+
+// The flags of one unit of work (the strict R build: one R entry) as running
+// extremes instead of a boolean per operation.  A flag per operation costs a
+// compare and a lane-mask OR each (and, at every divergent join, a mask
+// merged into a VGPR): with ~120 checked operations per entry the flags were
+// 18 % of the build (profiles/r06/ab/strict_flags_r6b.txt).  Here each checked
+// operand adds one or two integer operations to a running minimum / maximum,
+// and the flag is read once per entry (fx_range_slow).  Every predicate below
+// flags at least what the per-operation form flags (the boolean sink of the
+// same functions), so the exhaustive checks of that form carry over:
+//
+//   q_*: the operands of fx_divf / fx_rcpf in the doubled frame w = 2 (bits &
+//        0x7FFFFFFF) - 2 (the shift drops the sign; +-0 wraps to 0xFFFFFFFE):
+//        a divisor must satisfy w in [2 (L - 1), 2 (H - 1)], L = bits(2^-40),
+//        H = bits(2^40) -- so a zero, tiny, huge or non-finite one is flagged;
+//        a numerator enters the minimum as w (zero passes, as in fx_divf_r) and
+//        the maximum as 2 (bits & 0x7FFFFFFF) (zero passes; |a| = 2^40 itself
+//        is flagged, which fx_divf_r does not: conservative);
+//   s_*: fx_sqrtf's argument bits (sign included) in the maximum, bits - 1 in
+//        the minimum: +0 passes, every negative value (-0 included, which
+//        fx_sqrtf_r lets through: conservative) and every value outside
+//        [2^-100, 2^100] is flagged;
+//   h_mn: the rounding test of the transcendentals, min over calls of
+//        8 (lo29 - (2^28 - band)) mod 2^32, flagged below 8 (2 band) --
+//        exactly fx_near_half's predicate;
+//   slow: the transcendentals' argument ranges, as in their boolean form.
+struct FxRange {
+    uint32_t q_mx, q_mn, s_mx, s_mn, h_mn;
+    bool slow;
+};
+constexpr uint32_t kFxQLo = 2u * (0x2B800000u - 1u), kFxQHi = 2u * (0x53800000u - 1u);
+constexpr uint32_t kFxSLo = 0x0D800000u - 1u, kFxSHi = 0x71800000u;
+FX_FN FxRange fx_range_init() { return FxRange{0u, 0xFFFFFFFFu, 0u, 0xFFFFFFFFu, 0xFFFFFFFFu, false}; }
+FX_FN bool fx_range_slow(const FxRange& g)
+{
+    return g.slow || g.q_mn < kFxQLo || g.q_mx > kFxQHi || g.s_mn < kFxSLo || g.s_mx > kFxSHi ||
+           g.h_mn < ((2u * kFxBand) << 3);
+}
+FX_FN uint32_t fx_umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
+FX_FN uint32_t fx_umax(uint32_t a, uint32_t b) { return a > b ? a : b; }
+
+// The two sinks of the fast functions' checks: a boolean (per operation) or
+// the running extremes.  rng = the argument lies outside the function's fast
+// range; y = the fast double whose float rounding must be unambiguous.
+FX_FN void fx_sink_tx(bool& s, bool rng, double y) { s |= rng || fx_near_half(y); }
+FX_FN void fx_sink_tx(FxRange& g, bool rng, double y)
+{
+    g.slow |= rng;
+    // the 29 dropped bits moved to the top of a word (one v_lshl_add_u32):
+    // 8 (lo29 - (2^28 - band)) mod 2^32
+    const uint32_t t = ((uint32_t)__double_as_longlong(y) << 3) - ((0x10000000u - kFxBand) << 3);
+    g.h_mn = fx_umin(g.h_mn, t);
 }
 
 FX_FN double fx_fma(double a, double b, double c) { return __builtin_fma(a, b, c); }
@@ -187,9 +240,10 @@ FX_FN void fx_tables_init()
 }
 
 // exp(x), |x| <= 87.5: x = (256 k + j) ln2/256 + r, |r| <= ln2/512:
-// 2^k 2^(j/256) (1 + r q(r)), q a degree-2 fit of expm1(r)/r (2^-44.7
-// relative on exp), one-constant reduction (error <= 32,300 x 2^-61.4 ln2/256
-// absolute on r: 2^-46.4), the table entry (2^-52): within 2^-44 overall
+// 2^k 2^(j/256) (1 + r + r^2 q(r)), q = 1/2 + r/6 (2^-42.7 relative on exp),
+// one-constant reduction (error <= 32,300 x 2^-61.4 ln2/256 absolute on r:
+// 2^-46.4), the table entry (2^-52): within 2^-42.5 overall, 5x inside the
+// rounding test's band (2^-40)
 FX_FN double fx_exp_core(double x)
 {
     const double t = fx_fma(x, 0x1.71547652b82fep+8, 0x1.8p52);   // 256/ln2; n in the low word
@@ -197,7 +251,10 @@ FX_FN double fx_exp_core(double x)
     const int n = (int)(uint32_t)__double_as_longlong(t);
     const double r = fx_fma(kd, -0x1.62e42fefa39efp-9, x);         // ln2/256
     const double r2 = r * r;
-    const double q = fx_fma(r, 0x1.555556deebd69p-3, 0x1.000001ebfc21fp-1);
+    // q = 1/2 + r/6 (Taylor; 2^-42.7 relative on exp over |r| <= ln2/512,
+    // tools/detmath_fast_coeffs.py): 1/2 is an inline operand of v_fma_f64
+    // and 1/6 an SGPR pair, so no constant is moved into VGPRs per call
+    const double q = fx_fma(r, fx_kd(0x1.5555555555555p-3, r), 0.5);
     const double p = fx_fma(r2, q, r);
     const double T = fx_exp2_lds[n & 255];
     return __builtin_amdgcn_ldexp(fx_fma(T, p, T), n >> 8);
@@ -205,17 +262,19 @@ FX_FN double fx_exp_core(double x)
 
 // The _r forms return the fast float and set `slow` when it may differ from
 // detmath's; the plain forms fall back lane by lane.
-FX_FN float fx_expf_r(float x, bool& slow)
+template <class FL>
+FX_FN float fx_expf_r(float x, FL& slow)
 {
     const double y = fx_exp_core((double)x);
     // |x| <= 87: the result is a normal float (exp(-87) > 2^-126)
-    slow |= !(__builtin_fabsf(x) <= 87.0f) || fx_near_half(y);
+    fx_sink_tx(slow, !(__builtin_fabsf(x) <= 87.0f), y);
     return (float)y;
 }
 
 // atan(x): |x| reduced to |t| <= tan(pi/8) with one division
 // (t = x, (x - 1)/(x + 1) or -1/x), degree-8 fit of atan(t)/t in t^2 (2^-45.1)
-FX_FN float fx_atanf_r(float x, bool& slow)
+template <class FL>
+FX_FN float fx_atanf_r(float x, FL& slow)
 {
     const double a = __builtin_fabs((double)x);
     const bool hi = a > 0x1.3504f333f9de6p+1;            // tan(3 pi/8)
@@ -238,13 +297,14 @@ FX_FN float fx_atanf_r(float x, bool& slow)
     // 2^-60 <= |x| <= 2^60: normal float results, no tiny-argument edge;
     // atan(+-0) = +0 as in detmath
     const bool zero = x == 0.0f;
-    slow |= !zero && (!(a >= 0x1p-60 && a <= 0x1p60) || fx_near_half(y));
+    fx_sink_tx(slow, !zero && !(a >= 0x1p-60 && a <= 0x1p60), zero ? 0.0 : y);
     return zero ? 0.0f : (float)y;
 }
 
 // tan(x), |x| <= 2^16: x = k pi/2 + r, |r| <= pi/4 (+), sin r / cos r
 // (degree-5 fits in r^2: 2^-47.6, 2^-43.5), one division
-FX_FN float fx_tanf_r(float x, bool& slow)
+template <class FL>
+FX_FN float fx_tanf_r(float x, FL& slow)
 {
     const double xd = (double)x;
     const double tk = fx_fma(xd, DM_TWOOPI, 0x1.8p52);
@@ -270,7 +330,7 @@ FX_FN float fx_tanf_r(float x, bool& slow)
     const double y = num * fx_rcp(den);
     // 2^-30 <= |x| <= 2^16, and |r| >= 2^-40 so the quotient stays in range
     const float ax = __builtin_fabsf(x);
-    slow |= !(ax >= 0x1p-30f && ax <= 0x1p16f) || !(__builtin_fabs(r) >= 0x1p-40) || fx_near_half(y);
+    fx_sink_tx(slow, !(ax >= 0x1p-30f && ax <= 0x1p16f) || !(__builtin_fabs(r) >= 0x1p-40), y);
     return (float)y;
 }
 
@@ -281,7 +341,8 @@ FX_FN float fx_tanf_r(float x, bool& slow)
 //     (2^-52 absolute) stays below 2^-46 relative for a >= 2^-6;
 //   a < 2^-6: a (1 - z/6 + 3z^2/40 - 5z^3/112), z = a^2 <= 2^-12 (series
 //     remainder 35 z^4 / 1152 < 2^-53)
-FX_FN float fx_asinhf_r(float x, bool& slow)
+template <class FL>
+FX_FN float fx_asinhf_r(float x, FL& slow)
 {
     const double a = __builtin_fabs((double)x);
     const double w = a + fx_sqrt(fx_fma(a, a, 1.0));
@@ -305,13 +366,14 @@ FX_FN float fx_asinhf_r(float x, bool& slow)
     const double r = a < 0x1p-6 ? a * q : rl;
     const double y = x < 0.0f ? -r : r;
     const bool zero = x == 0.0f;                             // asinh(+-0) = +0 (detmath)
-    slow |= !zero && (!(a >= 0x1p-60 && a <= 0x1p20) || fx_near_half(y));
+    fx_sink_tx(slow, !zero && !(a >= 0x1p-60 && a <= 0x1p20), zero ? 0.0 : y);
     return zero ? 0.0f : (float)y;
 }
 
 // sinh(x): |x| < 1: x P(x^2) (degree-5 fit of sinh(a)/a, 2^-43.5);
 // 1 <= |x| <= 87: (e - 1/e) / 2 with the exp above
-FX_FN float fx_sinhf_r(float x, bool& slow)
+template <class FL>
+FX_FN float fx_sinhf_r(float x, FL& slow)
 {
     const double a = __builtin_fabs((double)x);
     double r;
@@ -328,7 +390,7 @@ FX_FN float fx_sinhf_r(float x, bool& slow)
         r = fx_fma(0.5, e, -0.5 * fx_rcp(e));
     }
     const double y = x < 0.0f ? -r : r;
-    slow |= !(a >= 0x1p-20 && a <= 87.0) || fx_near_half(y);
+    fx_sink_tx(slow, !(a >= 0x1p-20 && a <= 87.0), y);
     return (float)y;
 }
 
@@ -389,36 +451,82 @@ FX_FN float fx_rcpf_r(float b, bool& slow)
     return y;
 }
 
+// The same cores with the checks folded into the running extremes (FxRange)
+FX_FN float fx_divf_r(float a, float b, FxRange& g)
+{
+    float y = __builtin_amdgcn_rcpf(b);
+    const float e = __builtin_fmaf(-b, y, 1.0f);
+    y = __builtin_fmaf(e, y, y);
+    const float q0 = a * y;
+    float r = __builtin_fmaf(-b, q0, a);
+    float q = __builtin_fmaf(r, y, q0);
+    r = __builtin_fmaf(-b, q, a);
+    q = __builtin_fmaf(r, y, q);
+    const uint32_t ba = __float_as_uint(a), bb = __float_as_uint(b);
+    const uint32_t wb = (bb << 1) - 2u, wa = (ba << 1) - 2u;
+    g.q_mx = fx_umax(fx_umax(g.q_mx, wb), ba << 1);
+    g.q_mn = fx_umin(fx_umin(g.q_mn, wb), wa);
+    return (ba << 1) == 0u ? q0 : q;
+}
+
+FX_FN float fx_sqrtf_r(float x, FxRange& g)
+{
+    const float y = __builtin_amdgcn_sqrtf(x);
+    const float ym = __uint_as_float(__float_as_uint(y) - 1u);
+    const float yp = __uint_as_float(__float_as_uint(y) + 1u);
+    float r = __builtin_fmaf(-ym, y, x) <= 0.0f ? ym : y;
+    r = __builtin_fmaf(-yp, y, x) > 0.0f ? yp : r;
+    const uint32_t bx = __float_as_uint(x);
+    g.s_mx = fx_umax(g.s_mx, bx);
+    g.s_mn = fx_umin(g.s_mn, bx - 1u);
+    return r;
+}
+
+FX_FN float fx_rcpf_r(float b, FxRange& g)
+{
+    float y = __builtin_amdgcn_rcpf(b);
+    float e = __builtin_fmaf(-b, y, 1.0f);
+    y = __builtin_fmaf(e, y, y);
+    e = __builtin_fmaf(-b, y, 1.0f);
+    y = __builtin_fmaf(e, y, y);
+    const uint32_t wb = (__float_as_uint(b) << 1) - 2u;
+    g.q_mx = fx_umax(g.q_mx, wb);
+    g.q_mn = fx_umin(g.q_mn, wb);
+    return y;
+}
+
 FX_FN float fx_rcpf(float b)
 {
-    bool slow = false;
-    float y = fx_rcpf_r(b, slow);
-    if (slow) y = 1.0f / b;
+    FxRange g = fx_range_init();
+    float y = fx_rcpf_r(b, g);
+    if (fx_range_slow(g)) y = 1.0f / b;
     return y;
 }
 
 FX_FN float fx_divf(float a, float b)
 {
-    bool slow = false;
-    float q = fx_divf_r(a, b, slow);
-    if (slow) q = a / b;
+    FxRange g = fx_range_init();
+    float q = fx_divf_r(a, b, g);
+    if (fx_range_slow(g)) q = a / b;
     return q;
 }
 
 FX_FN float fx_sqrtf(float x)
 {
-    bool slow = false;
-    float y = fx_sqrtf_r(x, slow);
-    if (slow) y = sqrtf(x);
+    FxRange g = fx_range_init();
+    float y = fx_sqrtf_r(x, g);
+    if (fx_range_slow(g)) y = sqrtf(x);
     return y;
 }
 
+// (through the running extremes: the exhaustive checks of k_detmath_exhaustive
+// and k_div_check cover the form the strict R build uses)
 #define FX_PLAIN(name)                                      \
     FX_FN float fx_##name##f(float x)                       \
     {                                                       \
-        bool slow = false;                                  \
-        float y = fx_##name##f_r(x, slow);                  \
-        if (slow) y = dm_##name##f(x);                      \
+        FxRange g = fx_range_init();                        \
+        float y = fx_##name##f_r(x, g);                     \
+        if (fx_range_slow(g)) y = dm_##name##f(x);          \
         return y;                                           \
     }
 FX_PLAIN(exp)

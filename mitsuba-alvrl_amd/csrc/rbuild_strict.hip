@@ -62,36 +62,45 @@ constexpr uint32_t kFlagHit = 1u, kFlagSmooth = 2u, kFlagMedium = 4u;
 // The transcendentals of one evaluation: FAST = detmath_fast.h's flag-raising
 // forms (a lane whose flag is set re-evaluates its R entry with FAST = false),
 // otherwise detmath.h itself.
+// ALVRL_STRICT_STUB_FLAGS (developer timing variant, results invalid): the
+// fast forms' range / rounding flags are computed into a dead local
+#ifdef ALVRL_STRICT_STUB_FLAGS
+#define TX_FLAG(s) d_
+#define TXD FxRange d_ = fx_range_init(); (void)d_;
+#else
+#define TX_FLAG(s) (s)
+#define TXD
+#endif
 template <bool FAST>
 struct Tx {
 #ifdef ALVRL_STRICT_STUB_TX   // developer timing variant: results invalid
-    static __device__ __forceinline__ float exp(float x, bool& s) { return __expf(x); }
-    static __device__ __forceinline__ float atan(float x, bool& s) { return x * 0.7f; }
-    static __device__ __forceinline__ float tan(float x, bool& s) { return x * 1.3f; }
-    static __device__ __forceinline__ float asinh(float x, bool& s) { return x * 0.9f; }
-    static __device__ __forceinline__ float sinh(float x, bool& s) { return x * 1.1f; }
+    static __device__ __forceinline__ float exp(float x, FxRange& s) { return __expf(x); }
+    static __device__ __forceinline__ float atan(float x, FxRange& s) { return x * 0.7f; }
+    static __device__ __forceinline__ float tan(float x, FxRange& s) { return x * 1.3f; }
+    static __device__ __forceinline__ float asinh(float x, FxRange& s) { return x * 0.9f; }
+    static __device__ __forceinline__ float sinh(float x, FxRange& s) { return x * 1.1f; }
 #else
-    static __device__ __forceinline__ float exp(float x, bool& s) { return FAST ? fx_expf_r(x, s) : dm_expf(x); }
-    static __device__ __forceinline__ float atan(float x, bool& s) { return FAST ? fx_atanf_r(x, s) : dm_atanf(x); }
-    static __device__ __forceinline__ float tan(float x, bool& s) { return FAST ? fx_tanf_r(x, s) : dm_tanf(x); }
-    static __device__ __forceinline__ float asinh(float x, bool& s) { return FAST ? fx_asinhf_r(x, s) : dm_asinhf(x); }
-    static __device__ __forceinline__ float sinh(float x, bool& s) { return FAST ? fx_sinhf_r(x, s) : dm_sinhf(x); }
+    static __device__ __forceinline__ float exp(float x, FxRange& s) { TXD return FAST ? fx_expf_r(x, TX_FLAG(s)) : dm_expf(x); }
+    static __device__ __forceinline__ float atan(float x, FxRange& s) { TXD return FAST ? fx_atanf_r(x, TX_FLAG(s)) : dm_atanf(x); }
+    static __device__ __forceinline__ float tan(float x, FxRange& s) { TXD return FAST ? fx_tanf_r(x, TX_FLAG(s)) : dm_tanf(x); }
+    static __device__ __forceinline__ float asinh(float x, FxRange& s) { TXD return FAST ? fx_asinhf_r(x, TX_FLAG(s)) : dm_asinhf(x); }
+    static __device__ __forceinline__ float sinh(float x, FxRange& s) { TXD return FAST ? fx_sinhf_r(x, TX_FLAG(s)) : dm_sinhf(x); }
 #endif
 #ifdef ALVRL_STRICT_STUB_DIV   // developer timing variant: results invalid
-    static __device__ __forceinline__ float sqrt(float x, bool& s) { return __builtin_amdgcn_sqrtf(x); }
-    static __device__ __forceinline__ float div(float a, float b, bool& s) { return a * __builtin_amdgcn_rcpf(b); }
-    static __device__ __forceinline__ float rcp(float b, bool& s) { return __builtin_amdgcn_rcpf(b); }
+    static __device__ __forceinline__ float sqrt(float x, FxRange& s) { return __builtin_amdgcn_sqrtf(x); }
+    static __device__ __forceinline__ float div(float a, float b, FxRange& s) { return a * __builtin_amdgcn_rcpf(b); }
+    static __device__ __forceinline__ float rcp(float b, FxRange& s) { return __builtin_amdgcn_rcpf(b); }
 #else
     // IEEE sqrt and division: their cores without the scaling (flag outside
     // the range where the scaling is the identity), or the compiler's expansion
-    static __device__ __forceinline__ float sqrt(float x, bool& s) { return FAST ? fx_sqrtf_r(x, s) : sqrtf(x); }
-    static __device__ __forceinline__ float div(float a, float b, bool& s) { return FAST ? fx_divf_r(a, b, s) : a / b; }
-    static __device__ __forceinline__ float rcp(float b, bool& s) { return FAST ? fx_rcpf_r(b, s) : 1.0f / b; }
+    static __device__ __forceinline__ float sqrt(float x, FxRange& s) { TXD return FAST ? fx_sqrtf_r(x, TX_FLAG(s)) : sqrtf(x); }
+    static __device__ __forceinline__ float div(float a, float b, FxRange& s) { TXD return FAST ? fx_divf_r(a, b, TX_FLAG(s)) : a / b; }
+    static __device__ __forceinline__ float rcp(float b, FxRange& s) { TXD return FAST ? fx_rcpf_r(b, TX_FLAG(s)) : 1.0f / b; }
 #endif
 };
-template <bool FAST> __device__ __forceinline__ float lenT(V3 a, bool& s) { return Tx<FAST>::sqrt(len2(a), s); }
-template <bool FAST> __device__ __forceinline__ float distT(V3 a, V3 b, bool& s) { return lenT<FAST>(sub(a, b), s); }
-template <bool FAST> __device__ __forceinline__ V3 nrmT(V3 a, bool& s)
+template <bool FAST> __device__ __forceinline__ float lenT(V3 a, FxRange& s) { return Tx<FAST>::sqrt(len2(a), s); }
+template <bool FAST> __device__ __forceinline__ float distT(V3 a, V3 b, FxRange& s) { return lenT<FAST>(sub(a, b), s); }
+template <bool FAST> __device__ __forceinline__ V3 nrmT(V3 a, FxRange& s)
 {
     const float r = Tx<FAST>::rcp(lenT<FAST>(a, s), s);
     return scl(a, r);
@@ -152,7 +161,7 @@ struct Draws {
 
 // MaxExpDist::cdf (maxexp.h:83-94)
 template <bool FAST>
-__device__ __forceinline__ float mxexp_cdf(const DevParams& P, float t, bool& slow)
+__device__ __forceinline__ float mxexp_cdf(const DevParams& P, float t, FxRange& slow)
 {
     int k = 0;
     while (k < 3 && P.mx_start[k] < t) k++;
@@ -165,7 +174,7 @@ __device__ __forceinline__ float mxexp_cdf(const DevParams& P, float t, bool& sl
 // pdfFailure of the sampling strategy
 template <bool FAST>
 __device__ __forceinline__ void medium_eval(const DevParams& P, float distance, float tr[3], float* pdf_failure,
-                                            bool& slow)
+                                            FxRange& slow)
 {
     const float e0 = Tx<FAST>::exp(P.sigma_t[0] * (-distance), slow);
     const float e1 = Tx<FAST>::exp(P.sigma_t[1] * (-distance), slow);
@@ -192,7 +201,7 @@ __device__ __forceinline__ void medium_eval(const DevParams& P, float distance, 
 // squares of negated components are the same floats).
 template <bool FAST, bool OCC>
 __device__ __forceinline__ void shadow_transmittance(const DevParams& P, V3 p1, bool p1_surface, V3 p2,
-                                                     float remaining, float tr[3], bool& slow)
+                                                     float remaining, float tr[3], FxRange& slow)
 {
     const float negLength = 0.0f - remaining;
     for (int i = 0; i < 3; i++) tr[i] = P.sigma_t[i] != 0 ? Tx<FAST>::exp(P.sigma_t[i] * negLength, slow) : 1.0f;
@@ -208,7 +217,7 @@ __device__ __forceinline__ void shadow_transmittance(const DevParams& P, V3 p1, 
 
 // isotropic.cpp:76-78, hg.cpp:107-110
 template <bool FAST>
-__device__ __forceinline__ float phase_eval(const DevParams& P, V3 wi, V3 wo, bool& slow)
+__device__ __forceinline__ float phase_eval(const DevParams& P, V3 wi, V3 wo, FxRange& slow)
 {
     if (P.phase_type == 0) return kInvFourPi;
     const float g = P.g;
@@ -229,7 +238,7 @@ struct Row {
 // getClosestPoints (vrlIntegrator.cpp:962-1032) for S1 = the eye segment E ->
 // hit, S2 = the VRL; returns |dP| and the closest point on the VRL
 template <bool FAST>
-__device__ __forceinline__ float closest_points(const Row& w, V3 S, const V3& vv, float c, V3* S2h, bool& slow)
+__device__ __forceinline__ float closest_points(const Row& w, V3 S, const V3& vv, float c, V3* S2h, FxRange& slow)
 {
     const V3 u = w.u, v = vv, wv = sub(w.E, S);
     const float a = w.a_uu, b = dot(u, v), d = dot(u, wv), e = dot(v, wv);
@@ -266,7 +275,7 @@ __device__ __forceinline__ float closest_points(const Row& w, V3 S, const V3& vv
 struct Kulla { V3 dir, I; float Dis, aa, ab; };
 
 template <bool FAST>
-__device__ __forceinline__ Kulla kulla_frame(V3 A, V3 B, V3 dir, float dAB, V3 D, bool& slow)
+__device__ __forceinline__ Kulla kulla_frame(V3 A, V3 B, V3 dir, float dAB, V3 D, FxRange& slow)
 {
     Kulla k;
     k.dir = dir;
@@ -285,7 +294,7 @@ __device__ __forceinline__ Kulla kulla_frame(V3 A, V3 B, V3 dir, float dAB, V3 D
 }
 
 template <bool FAST>
-__device__ __forceinline__ float kulla_sample(const Kulla& k, float uniform, V3* result, bool& slow)
+__device__ __forceinline__ float kulla_sample(const Kulla& k, float uniform, V3* result, FxRange& slow)
 {
     const float t = k.Dis * Tx<FAST>::tan(((1.0f - uniform) * k.aa) + (uniform * k.ab), slow);
     const float pdf = Tx<FAST>::div(k.Dis, (k.ab - k.aa) * (k.Dis * k.Dis + t * t), slow);
@@ -301,7 +310,7 @@ struct Novak {
 
 template <bool FAST>
 __device__ __forceinline__ Novak novak_frame(const Row& w, V3 S, V3 End, V3 SE, const V3& vv, float c, float dSE,
-                                             bool& slow)
+                                             FxRange& slow)
 {
     Novak n;
     n.mode = 0;
@@ -327,7 +336,7 @@ __device__ __forceinline__ Novak novak_frame(const Row& w, V3 S, V3 End, V3 SE, 
 
 template <bool FAST>
 __device__ __forceinline__ float novak_sample(const Novak& n, V3 S, V3 End, V3 SE, float invlen, float uniform,
-                                              V3* V, bool& slow)
+                                              V3* V, FxRange& slow)
 {
     if (n.mode == 0) { *V = S; return 1; }
     if (n.mode == 1) { *V = add(S, scl(sub(End, S), uniform)); return invlen; }
@@ -356,8 +365,8 @@ __device__ __forceinline__ Row make_row(const DevParams& P, const Rec& r, uint32
     w.teus[0] = w.teus[1] = w.teus[2] = 0.0f;
     if ((r.flags & kFlagHit) && edist != 0) {
         float pfd;
-        bool slow = false;
-        medium_eval<false>(P, edist, w.teus, &pfd, slow);
+        FxRange unused = fx_range_init();
+        medium_eval<false>(P, edist, w.teus, &pfd, unused);
     }
     w.surf = (w.teus[0] != 0 || w.teus[1] != 0 || w.teus[2] != 0) && (r.flags & kFlagSmooth);
     w.cos_wi = dot(neg(w.d), w.n);
@@ -380,7 +389,7 @@ __device__ __forceinline__ bool valid(const float c[3])
 // NVV / NVS < 0: the sample counts come from P at run time.
 template <int NVV, int NVS, bool OCC, bool FAST>
 __device__ __forceinline__ void integrate_R(const DevParams& P, const Row& w, const StrictVrl& L, uint32_t v,
-                                            uint32_t koff, float* contrib, float* variance, bool& slow)
+                                            uint32_t koff, float* contrib, float* variance, FxRange& slow)
 {
     *contrib = 0; *variance = 0;
     if (!(w.flags & kFlagMedium)) return;
@@ -510,7 +519,7 @@ __device__ __forceinline__ Rec load_rec(const Rec* __restrict__ recs, uint32_t r
 // RS1: Rsamples = 1 (one sample, draw offset 0).
 template <int NVV, int NVS, bool OCC, bool RS1, bool FAST>
 __device__ __forceinline__ float2 entry(const DevParams& P, const Row& w, const StrictVrl& L, uint32_t v,
-                                       float normalization, bool& slow)
+                                       float normalization, FxRange& slow)
 {
     const int nsamp = RS1 ? 1 : (P.rsamples > 1 ? P.rsamples : 1);
     float m = 0.0f, s = 0.0f;
@@ -580,7 +589,9 @@ __global__ void __launch_bounds__(256, ALVRL_STRICT_MINB) k_build_R_strict(const
         bool slow = false;
         if (medium) {
             const StrictVrl L = sv[v];
-            e = entry<NVV, NVS, OCC, RS1, true>(P, w, L, v, normalization, slow);
+            FxRange g = fx_range_init();
+            e = entry<NVV, NVS, OCC, RS1, true>(P, w, L, v, normalization, g);
+            slow = fx_range_slow(g);
         }
         if (store && active && !slow) store_entry(Rt, base + (uint64_t)v * stride, rec.flags & kRecAccum, e);
         const unsigned long long sb = __ballot(slow);
@@ -617,8 +628,8 @@ __global__ void __launch_bounds__(256) k_build_R_strict_fixup(const Rec* __restr
     const uint32_t r = items[i].x, v = items[i].y;
     const Rec rec = load_rec(recs, r);
     const Row w = make_row(P, rec, ids ? ids[r] : r);
-    bool slow = false;
-    const float2 e = entry<NVV, NVS, OCC, RS1, false>(P, w, sv[v], v, normalization, slow);
+    FxRange unused = fx_range_init();
+    const float2 e = entry<NVV, NVS, OCC, RS1, false>(P, w, sv[v], v, normalization, unused);
     const uint64_t base = roff ? roff[r] : row0 + r;
     const uint64_t stride = roff ? rstride[r] : ld;
     store_entry(Rt, base + (uint64_t)v * stride, rec.flags & kRecAccum, e);
