@@ -82,7 +82,11 @@ __device__ __forceinline__ U4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c
         const unsigned long long p1 = (unsigned long long)0xCD9E8D57u * c2;
         const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
         const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
-        const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        // each three-way XOR as one gfx950 v_bitop3_b32 (truth table 0x96 =
+        // A ^ B ^ C; the round key is its SGPR operand) instead of two v_xor_b32:
+        // two instructions fewer per round, ~5 % of the gather's VALU stream
+        const uint32_t n0 = __builtin_amdgcn_bitop3_b32(hi1, c1, k0, 0x96);
+        const uint32_t n2 = __builtin_amdgcn_bitop3_b32(hi0, c3, k1, 0x96);
         c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
     }
     return U4{c0, c1, c2, c3};
