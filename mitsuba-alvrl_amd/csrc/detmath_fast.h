@@ -107,9 +107,16 @@ FX_FN uint32_t fx_umax(uint32_t a, uint32_t b) { return a > b ? a : b; }
 // the running extremes.  rng = the argument lies outside the function's fast
 // range; y = the fast double whose float rounding must be unambiguous.
 FX_FN void fx_sink_tx(bool& s, bool rng, double y) { s |= rng || fx_near_half(y); }
+// (ALVRL_STUB_TXRANGE / _NEARHALF / _QS: developer timing variants that drop
+// one class of checks; results invalid for the fix-up decision)
 FX_FN void fx_sink_tx(FxRange& g, bool rng, double y)
 {
+#ifndef ALVRL_STUB_TXRANGE
     g.slow |= rng;
+#endif
+#ifdef ALVRL_STUB_NEARHALF
+    return;
+#endif
     // the 29 dropped bits moved to the top of a word (one v_lshl_add_u32):
     // 8 (lo29 - (2^28 - band)) mod 2^32
     const uint32_t t = ((uint32_t)__double_as_longlong(y) << 3) - ((0x10000000u - kFxBand) << 3);
@@ -462,11 +469,13 @@ FX_FN float fx_divf_r(float a, float b, FxRange& g)
     float q = __builtin_fmaf(r, y, q0);
     r = __builtin_fmaf(-b, q, a);
     q = __builtin_fmaf(r, y, q);
+#ifndef ALVRL_STUB_QS
     const uint32_t ba = __float_as_uint(a), bb = __float_as_uint(b);
     const uint32_t wb = (bb << 1) - 2u, wa = (ba << 1) - 2u;
     g.q_mx = fx_umax(fx_umax(g.q_mx, wb), ba << 1);
     g.q_mn = fx_umin(fx_umin(g.q_mn, wb), wa);
-    return (ba << 1) == 0u ? q0 : q;
+#endif
+    return (__float_as_uint(a) << 1) == 0u ? q0 : q;
 }
 
 FX_FN float fx_sqrtf_r(float x, FxRange& g)
@@ -476,9 +485,11 @@ FX_FN float fx_sqrtf_r(float x, FxRange& g)
     const float yp = __uint_as_float(__float_as_uint(y) + 1u);
     float r = __builtin_fmaf(-ym, y, x) <= 0.0f ? ym : y;
     r = __builtin_fmaf(-yp, y, x) > 0.0f ? yp : r;
+#ifndef ALVRL_STUB_QS
     const uint32_t bx = __float_as_uint(x);
     g.s_mx = fx_umax(g.s_mx, bx);
     g.s_mn = fx_umin(g.s_mn, bx - 1u);
+#endif
     return r;
 }
 
@@ -489,9 +500,11 @@ FX_FN float fx_rcpf_r(float b, FxRange& g)
     y = __builtin_fmaf(e, y, y);
     e = __builtin_fmaf(-b, y, 1.0f);
     y = __builtin_fmaf(e, y, y);
+#ifndef ALVRL_STUB_QS
     const uint32_t wb = (__float_as_uint(b) << 1) - 2u;
     g.q_mx = fx_umax(g.q_mx, wb);
     g.q_mn = fx_umin(g.q_mn, wb);
+#endif
     return y;
 }
 

@@ -62,6 +62,14 @@ constexpr uint32_t kFlagHit = 1u, kFlagSmooth = 2u, kFlagMedium = 4u;
 // The transcendentals of one evaluation: FAST = detmath_fast.h's flag-raising
 // forms (a lane whose flag is set re-evaluates its R entry with FAST = false),
 // otherwise detmath.h itself.
+// Division: the compiler's IEEE expansion (v_div_scale x2, v_rcp, five fmas,
+// v_div_fmas, v_div_fixup: 11 VALU, exact for every operand, nothing to check)
+// costs less than detmath_fast.h's unscaled core with its zero select and
+// range checks (10 + 5): R build alone 90.0 -> 89.3 ms.  ALVRL_STRICT_FASTDIV=1:
+// the core (developer A/B).
+#ifndef ALVRL_STRICT_FASTDIV
+#define ALVRL_STRICT_FASTDIV 0
+#endif
 // ALVRL_STRICT_STUB_FLAGS (developer timing variant, results invalid): the
 // fast forms' range / rounding flags are computed into a dead local
 #ifdef ALVRL_STRICT_STUB_FLAGS
@@ -91,10 +99,10 @@ struct Tx {
     static __device__ __forceinline__ float div(float a, float b, FxRange& s) { return a * __builtin_amdgcn_rcpf(b); }
     static __device__ __forceinline__ float rcp(float b, FxRange& s) { return __builtin_amdgcn_rcpf(b); }
 #else
-    // IEEE sqrt and division: their cores without the scaling (flag outside
+    // IEEE sqrt and reciprocal: their cores without the scaling (flag outside
     // the range where the scaling is the identity), or the compiler's expansion
     static __device__ __forceinline__ float sqrt(float x, FxRange& s) { TXD return FAST ? fx_sqrtf_r(x, TX_FLAG(s)) : sqrtf(x); }
-    static __device__ __forceinline__ float div(float a, float b, FxRange& s) { TXD return FAST ? fx_divf_r(a, b, TX_FLAG(s)) : a / b; }
+    static __device__ __forceinline__ float div(float a, float b, FxRange& s) { return ALVRL_STRICT_FASTDIV && FAST ? fx_divf_r(a, b, s) : a / b; }
     static __device__ __forceinline__ float rcp(float b, FxRange& s) { TXD return FAST ? fx_rcpf_r(b, TX_FLAG(s)) : 1.0f / b; }
 #endif
 };
